@@ -1,0 +1,219 @@
+#!/usr/bin/env python3
+"""Benchmark of the guided-bridge imputation hot path on MI355X.
+
+One "step" = one MCMC iteration over the whole per-GPU BlockEnsemble:
+  draw_proposal_path!(be)            (pCN + guided Euler–Maruyama + Girsanov weight, device RNG)
+  accept_reject_proposal_path!(be,i) (per-block MH test, selector swaps, histories)
+  fetch_ll(be) + accepted count      (deterministic reduction; RCCL all-gather over ranks)
+i.e. the caller loop of /root/reference/docs/src/tutorials/biblock/smoothing.md:40-44 at
+BlockEnsemble level (src/block_ensemble.jl:50,63-67,140).  Throughput unit: bridge-segment
+Euler steps (one grid increment of one segment) per second, whole job.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c5]
+Multi-GPU: launched by torch.distributed.run, one rank per GPU, weak scaling (each rank owns
+a full per-GPU ensemble, blocks keyed by global id; no data-path collective besides fetch_ll).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+WORKLOADS = {
+    "c2": ("C2: 2D OU guided bridge, 1024 blocks x 500 Euler steps per GPU, fp64", "f64"),
+    "c3": ("C3/C4: FitzHugh-Nagumo guided bridge, 65536 blocks x 1000 Euler steps per GPU, fp64", "f64"),
+    "c5": ("C5: Lorenz-63 guided bridge, 32768 blocks x 2000 Euler steps per GPU, fp32", "f32"),
+}
+
+
+def build_workload(name, rank):
+    from diffusionmcmctools_amd import workloads as W
+    if name == "c2":
+        return W.c2_ou2d(block_offset=rank)
+    if name == "c3":
+        return W.c3_fhn(block_offset=rank)
+    if name == "c5":
+        return W.c5_lorenz(block_offset=rank)
+    raise SystemExit(f"unknown config {name}")
+
+
+def algorithmic_bytes_per_step(w):
+    """s·(2m [read W, write W°] + d [write X°] + d [read F] + h [read H]),
+    h = d(d+1)/2 for per-block guiding tables, 0 when H is shared; shared grid ignored."""
+    s = 8 if w.precision == 0 else 4
+    h = 0 if w.H_shared else w.d * (w.d + 1) // 2
+    return s * (2 * w.m + 2 * w.d + h)
+
+
+def cpu_baseline(w, ens, lay, budget_s=12.0):
+    """The oracle's OpenMP restatement (oracle/dmt_oracle.c) timed on this host on a bounded
+    sample: whole MCMC iterations (draw + MH accept) of the same per-GPU workload."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as orc
+    from diffusionmcmctools_amd import _lib as L
+    nthreads = max(1, min(16, os.cpu_count() or 1))
+    B = w.nblocks
+    npts = w.n_points[0][0]
+    X = ens.download_paths(L.U, 0)
+    Wp = ens.download_paths(L.U, 1)
+    ens.loglikhd(lay, L.U, 0, B)
+    ll = ens.get_block_state(lay, L.BLK_LL, 0, B)
+    rho = np.full(B, w.rho)
+    prec = w.precision
+    rng = np.random.default_rng(0)
+    res = {}
+    for nt in sorted({1, nthreads}):
+        it = 0
+        acc_n = 0
+        Xa, Wa, lla = X.copy(), Wp.copy(), ll.copy()
+        t0 = time.perf_counter()
+        while True:
+            it += 1
+            Xo, Wo, llp, _ = orc.draw_terminal_blocks(
+                w.model.kind, w.d, w.m, npts, w.laws, w.t, w.H, w.F, Xa, Wa, rho, Z=None,
+                seed=1234, it=it, salt=0, prec=prec, nthreads=nt, t_shared=True,
+                H_shared=w.H_shared)
+            E = rng.exponential(1.0, B)
+            acc = E > -(llp - lla)
+            sel = np.repeat(acc, npts)
+            Xa = np.where(sel[:, None], Xo, Xa)
+            Wa = np.where(sel[:, None], Wo, Wa)
+            lla = np.where(acc, llp, lla)
+            acc_n += int(acc.sum())
+            el = time.perf_counter() - t0
+            if (el > budget_s / 2 and it >= 2) or it >= 10000:
+                break
+        res[nt] = (w.steps_per_iter * it / el, it, acc_n / (B * it))
+    v, its, ar = res[nthreads]
+    v1 = res[1][0]
+    return {"value": v, "unit": "steps/s", "cores": nthreads, "kind": "port",
+            "sample": f"{its} full MCMC iterations (draw + MH accept) of the same per-GPU workload "
+                      f"({B} blocks x {npts - 1} steps), device-equivalent Philox/Box-Muller normals",
+            "value_1thread": v1, "accept_rate": ar}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        dist.init_process_group("gloo")  # control plane only; the data path is RCCL in libdmt
+
+    import diffusionmcmctools_amd as dmt
+    from diffusionmcmctools_amd import _lib as L
+    from diffusionmcmctools_amd import workloads as W
+
+    w = build_workload(args.config, rank)
+    w.meta["hist_len"] = args.warmup + args.steps
+    ens = dmt.Ensemble(w.model.kind, w.d, w.m, w.n_points, precision=w.precision,
+                       seed=0xD1FF + 7919 * rank, device=local_rank, grid_shared=w.grid_shared)
+    lay = W.fill(ens, w, init_Z=False)
+    B = w.nblocks
+    if world > 1:
+        uid = [dmt.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        ens.comm_init(world, rank, uid[0])
+    ens.loglikhd(lay, L.U, 0, B)
+
+    def step(i):
+        ens.draw_proposal(lay, 0, B, iter=i)
+        ens.accept_reject(lay, 0, B, i)
+        return ens.fetch_ll(lay, 0, B, i)
+
+    def barrier():
+        ens.sync()
+        if dist is not None:
+            dist.barrier()
+
+    for i in range(1, args.warmup + 1):
+        step(i)
+    barrier()
+    ens.set_timing(True)
+    barrier()
+    t0 = time.perf_counter()
+    n_acc = 0
+    for i in range(args.warmup + 1, args.warmup + args.steps + 1):
+        _, _, na = step(i)
+        n_acc += na
+    barrier()
+    el = time.perf_counter() - t0
+    k_ms, k_n = ens.get_timing(L.K_DRAW)
+    a_ms, a_n = ens.get_timing(L.K_ACCEPT)
+    ens.set_timing(False)
+    if dist is not None:
+        import torch
+        t = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+
+    steps_total = w.steps_per_iter * args.steps * world
+    value = steps_total / el
+    k_avg_s = (k_ms / max(k_n, 1)) * 1e-3
+    bytes_launch = algorithmic_bytes_per_step(w) * w.steps_per_iter
+    achieved = bytes_launch / k_avg_s / 1e9 if k_avg_s > 0 else 0.0
+    accept_rate = n_acc / (B * world * args.steps)  # n_acc is already global (fetch_ll over ranks)
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(w, ens, lay, budget_s=args.cpu_budget)
+        desc, dtype = WORKLOADS[args.config]
+        line = {
+            "metric": "bridge-segment Euler steps/sec/GPU; accept-rate vs CPU ref",
+            "value": value,
+            "unit": "steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": el / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": dtype,
+            "data": "synthetic (seeded, SURVEY.md §8(d) configs; no reference checkpoints/datasets)",
+            "config": {"workload": desc, "blocks_per_gpu": B,
+                       "euler_steps_per_block": w.steps_per_iter // B, "rho": w.rho,
+                       "parallelism": f"blockensemble-shard x{world}",
+                       "rng": "device Philox4x32-10 + Box-Muller (perf mode)"},
+            "per_gpu": value / world,
+            "accept_rate": accept_rate,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS,
+                         "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS, "traffic": None,
+                         "kernel": "k_block (draw_proposal)", "kernel_avg_us": k_avg_s * 1e6,
+                         "algorithmic_bytes_per_launch": bytes_launch,
+                         "bytes_per_step": algorithmic_bytes_per_step(w)},
+            "accept_kernel_avg_us": (a_ms / max(a_n, 1)) * 1e3,
+            "cpu_baseline": cpu,
+        }
+        if cpu is not None:
+            line["accept_rate_cpu"] = cpu["accept_rate"]
+        print(json.dumps(line))
+    ens.close()
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

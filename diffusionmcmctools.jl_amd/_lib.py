@@ -1,0 +1,150 @@
+"""ctypes binding of libdmt.so (include/dmt.h).
+
+The product path has no CPU fallback: if the HIP library is missing, importing this
+module raises; if no GPU is present, ``dmt_create`` fails with DMT_ERR_HIP.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libdmt.so")
+INCLUDE_H = os.path.join(os.path.dirname(HERE), "include", "dmt.h")
+
+# ---- constants (mirror include/dmt.h) ----
+OK, ERR_INVALID, ERR_HIP, ERR_OOM, ERR_STATE, ERR_COMM = 0, 1, 2, 3, 4, 5
+MODEL_OU, MODEL_FHN, MODEL_LORENZ = 0, 1, 2
+F64, F32 = 0, 1
+U, UPROP = 0, 1
+LAW_PP, LAW_PPB = 0, 1
+SWAP_XX, SWAP_WW, SWAP_PP, SWAP_LL = 1, 2, 4, 8
+BLK_LL, BLK_LLPROP, BLK_LL_HIST, BLK_LLPROP_HIST, BLK_ACC_HIST = 0, 1, 2, 3, 4
+K_DRAW, K_ACCEPT, K_PATHLL, K_RECOMPUTE, K_REDUCE = 0, 1, 2, 3, 4
+LAW_STRIDE = 64
+LAW_THETA, LAW_SIGMA, LAW_A, LAW_BT, LAW_BETA, LAW_DA, LAW_C0, LAW_TRACE = 0, 16, 25, 31, 40, 43, 49, 50
+
+# exported symbols (checked against include/dmt.h by tests/test_abi.py)
+SYMBOLS = [
+    "dmt_create", "dmt_destroy", "dmt_upload_grid", "dmt_upload_law", "dmt_set_paths",
+    "dmt_download_paths", "dmt_draw_unit", "dmt_create_layout", "dmt_layout_size",
+    "dmt_draw_proposal", "dmt_accept_reject", "dmt_loglikhd", "dmt_recompute_path", "dmt_swap",
+    "dmt_save_ll", "dmt_set_accepted", "dmt_get_block_state", "dmt_set_block_state",
+    "dmt_fetch_ll", "dmt_guiding_linear", "dmt_comm_unique_id", "dmt_comm_init", "dmt_sync",
+    "dmt_set_timing", "dmt_get_timing", "dmt_memory_bytes", "dmt_debug_philox",
+    "dmt_debug_normals", "dmt_last_error", "dmt_version",
+]
+
+
+class DMTError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"libdmt error {code}: {msg}")
+        self.code = code
+
+
+class dmt_model(C.Structure):
+    _fields_ = [("model", C.c_int32), ("precision", C.c_int32), ("d", C.c_int32), ("m", C.c_int32)]
+
+
+class dmt_structure(C.Structure):
+    _fields_ = [("n_recordings", C.c_int64), ("n_segments", C.POINTER(C.c_int32)),
+                ("n_points", C.POINTER(C.c_int32))]
+
+
+class dmt_config(C.Structure):
+    _fields_ = [("seed", C.c_uint64), ("device", C.c_int32), ("grid_shared", C.c_int32)]
+
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        f"{LIB_PATH} is missing: build it with __graft_entry__.build() "
+        "(make -C diffusionmcmctools.jl_amd/csrc). There is no CPU fallback.")
+
+lib = C.CDLL(LIB_PATH)
+
+_P = C.c_void_p
+_pd = C.POINTER(C.c_double)
+_pu8 = C.POINTER(C.c_uint8)
+_pi32 = C.POINTER(C.c_int32)
+_pi64 = C.POINTER(C.c_int64)
+_pu32 = C.POINTER(C.c_uint32)
+_i32, _i64, _u32, _u64 = C.c_int32, C.c_int64, C.c_uint32, C.c_uint64
+
+_SIGS = {
+    "dmt_create": [C.POINTER(_P), C.POINTER(dmt_model), C.POINTER(dmt_structure), C.POINTER(dmt_config)],
+    "dmt_destroy": [_P],
+    "dmt_upload_grid": [_P, _pd],
+    "dmt_upload_law": [_P, _i32, _i32, _pd, _i32, _pd, _pd],
+    "dmt_set_paths": [_P, _i32, _pd, _pd],
+    "dmt_download_paths": [_P, _i32, _i32, _pd],
+    "dmt_draw_unit": [_P, _i32, _i64, _i64, _pd, _i64, _u32, _pd, _pu8],
+    "dmt_create_layout": [_P, _pi32, _pi32, _pi32, _pu8, _pd, _i64, _pi32],
+    "dmt_layout_size": [_P, _i32, _pi64],
+    "dmt_draw_proposal": [_P, _i32, _i64, _i64, _pd, _i64, _u32, _pu8],
+    "dmt_accept_reject": [_P, _i32, _i64, _i64, _pd, _i64, _u32, _pu8],
+    "dmt_loglikhd": [_P, _i32, _i32, _i64, _i64],
+    "dmt_recompute_path": [_P, _i32, _i64, _i64, _i32, _pu8],
+    "dmt_swap": [_P, _i32, _i32, _i64, _i64],
+    "dmt_save_ll": [_P, _i32, _i64, _i64, _i64],
+    "dmt_set_accepted": [_P, _i32, _i64, _i64, _i64, _pu8],
+    "dmt_get_block_state": [_P, _i32, _i32, _i64, _i64, _P],
+    "dmt_set_block_state": [_P, _i32, _i32, _i64, _i64, _P],
+    "dmt_fetch_ll": [_P, _i32, _i64, _i64, _i64, _pd, _pd, _pi64],
+    "dmt_guiding_linear": [_i32, _pd, _pd, _pd, _i32, _pd, _pd, _pd, C.c_double, _pd, _pd, _pd],
+    "dmt_comm_unique_id": [_pu8],
+    "dmt_comm_init": [_P, _i32, _i32, _pu8],
+    "dmt_sync": [_P],
+    "dmt_set_timing": [_P, _i32],
+    "dmt_get_timing": [_P, _i32, _pd, _pi64],
+    "dmt_memory_bytes": [_P, _pi64],
+    "dmt_debug_philox": [_i32, _u64, _pu32, _i64, _pu32],
+    "dmt_debug_normals": [_i32, _u64, _pu32, _i64, _pd],
+}
+for _name, _args in _SIGS.items():
+    _f = getattr(lib, _name)
+    _f.argtypes = _args
+    _f.restype = C.c_int32
+lib.dmt_last_error.restype = C.c_char_p
+lib.dmt_last_error.argtypes = []
+lib.dmt_version.restype = C.c_char_p
+lib.dmt_version.argtypes = []
+
+
+def check(status: int) -> None:
+    if status != OK:
+        raise DMTError(status, lib.dmt_last_error().decode(errors="replace"))
+
+
+def call(name: str, *args) -> None:
+    check(getattr(lib, name)(*args))
+
+
+# ---- array helpers ----
+def f64p(a):
+    if a is None:
+        return None
+    assert a.dtype == np.float64 and a.flags.c_contiguous, "need a C-contiguous float64 array"
+    return a.ctypes.data_as(_pd)
+
+
+def u8p(a):
+    if a is None:
+        return None
+    assert a.dtype == np.uint8 and a.flags.c_contiguous
+    return a.ctypes.data_as(_pu8)
+
+
+def i32p(a):
+    assert a.dtype == np.int32 and a.flags.c_contiguous
+    return a.ctypes.data_as(_pi32)
+
+
+def u32p(a):
+    assert a.dtype == np.uint32 and a.flags.c_contiguous
+    return a.ctypes.data_as(_pu32)
+
+
+def version() -> str:
+    return lib.dmt_version().decode()

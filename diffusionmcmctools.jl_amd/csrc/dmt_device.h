@@ -1,0 +1,279 @@
+// dmt_device.h — device building blocks of the guided-bridge engine (gfx950).
+//
+// Every arithmetic routine here follows the CANONICAL ARITHMETIC written in
+// DESIGN.md §3 operation by operation (explicit fma, -ffp-contract=off), so a
+// path computed on the MI355X is bit-identical to the CPU restatement.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/dmt.h"
+#include "dmt_internal.h"
+
+namespace dmt {
+
+__host__ __device__ constexpr int packed_idx(int d, int a, int b) {
+  return (a > b) ? packed_idx(d, b, a) : a * d - (a * (a - 1)) / 2 + (b - a);
+}
+
+__device__ __forceinline__ double dfma(double a, double b, double c) { return __builtin_fma(a, b, c); }
+__device__ __forceinline__ float dfma(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+
+// ---------------------------------------------------------------- models
+// Drifts of the DiffusionDefinition models.
+template <class T, int D_, int M_>
+struct OU {
+  static constexpr int D = D_, M = M_, NTH = 12;
+  // theta: Theta (d×d row-major) at 0, mu at 9
+  __device__ __forceinline__ static void drift(const T* th, const T* x, T* b) {
+    T y[D];
+#pragma unroll
+    for (int q = 0; q < D; ++q) y[q] = x[q] - th[9 + q];
+#pragma unroll
+    for (int a = 0; a < D; ++a) {
+      T acc = (-th[a * D + 0]) * y[0];
+#pragma unroll
+      for (int q = 1; q < D; ++q) acc = dfma(-th[a * D + q], y[q], acc);
+      b[a] = acc;
+    }
+  }
+};
+
+template <class T>
+struct FHN {
+  static constexpr int D = 2, M = 1, NTH = 4;
+  // theta: 1/eps, s, gamma, beta
+  __device__ __forceinline__ static void drift(const T* th, const T* x, T* b) {
+    T y = x[0], v = x[1];
+    T y3 = (y * y) * y;
+    T t0 = ((y - y3) - v) + th[1];
+    b[0] = t0 * th[0];
+    b[1] = dfma(th[2], y, th[3] - v);
+  }
+};
+
+template <class T>
+struct Lorenz {
+  static constexpr int D = 3, M = 3, NTH = 3;
+  // theta: s, r, beta
+  __device__ __forceinline__ static void drift(const T* th, const T* x, T* b) {
+    b[0] = th[0] * (x[1] - x[0]);
+    b[1] = dfma(x[0], th[1] - x[2], -x[1]);
+    b[2] = dfma(x[0], x[1], -(th[2] * x[2]));
+  }
+};
+
+// ---------------------------------------------------------------- law record in registers
+template <class Mdl, class T>
+struct Law {
+  static constexpr int D = Mdl::D, M = Mdl::M, HP = D * (D + 1) / 2;
+  T th[Mdl::NTH];
+  T sg[D * M];
+  T a[HP];
+  T Bt[D * D];
+  T beta[D];
+  T da[HP];
+  bool trace;
+  __device__ __forceinline__ void load(const double* L) {
+#pragma unroll
+    for (int i = 0; i < Mdl::NTH; ++i) th[i] = (T)L[DMT_LAW_THETA + i];
+#pragma unroll
+    for (int p = 0; p < D; ++p)
+#pragma unroll
+      for (int k = 0; k < M; ++k) sg[p * M + k] = (T)L[DMT_LAW_SIGMA + p * M + k];
+#pragma unroll
+    for (int i = 0; i < HP; ++i) a[i] = (T)L[DMT_LAW_A + i];
+#pragma unroll
+    for (int i = 0; i < D * D; ++i) Bt[i] = (T)L[DMT_LAW_BT + i];
+#pragma unroll
+    for (int i = 0; i < D; ++i) beta[i] = (T)L[DMT_LAW_BETA + i];
+#pragma unroll
+    for (int i = 0; i < HP; ++i) da[i] = (T)L[DMT_LAW_DA + i];
+    trace = L[DMT_LAW_TRACE] != 0.0;
+  }
+};
+
+// G(t_i, x_i) of the Girsanov weight; returns G, writes r = F - Hx and the drift b.
+template <class Mdl, class T>
+__device__ __forceinline__ T g_at(const Law<Mdl, T>& L, const T* H, const T* F, const T* x, T* r,
+                                  T* b) {
+  constexpr int D = Mdl::D;
+#pragma unroll
+  for (int p = 0; p < D; ++p) {
+    T acc = F[p];
+#pragma unroll
+    for (int q = 0; q < D; ++q) acc = dfma(-H[packed_idx(D, p, q)], x[q], acc);
+    r[p] = acc;
+  }
+  Mdl::drift(L.th, x, b);
+  T db[D];
+#pragma unroll
+  for (int p = 0; p < D; ++p) {
+    T bt = L.beta[p];
+#pragma unroll
+    for (int q = 0; q < D; ++q) bt = dfma(L.Bt[p * D + q], x[q], bt);
+    db[p] = b[p] - bt;
+  }
+  T G = db[0] * r[0];
+#pragma unroll
+  for (int p = 1; p < D; ++p) G = dfma(db[p], r[p], G);
+  if (L.trace) {
+    T tr = (T)0;
+#pragma unroll
+    for (int p = 0; p < D; ++p)
+#pragma unroll
+      for (int q = 0; q < D; ++q) {
+        T tmp = dfma(-r[p], r[q], H[packed_idx(D, p, q)]);
+        T w = L.da[packed_idx(D, p, q)];
+        tr = (p == 0 && q == 0) ? (w * tmp) : dfma(w, tmp, tr);
+      }
+    G = dfma((T)-0.5, tr, G);
+  }
+  return G;
+}
+
+// One guided Euler–Maruyama step (left point), canonical order.
+template <class Mdl, class T>
+__device__ __forceinline__ void euler_step(const Law<Mdl, T>& L, const T* r, const T* b, T dt,
+                                           const T* dW, T* x) {
+  constexpr int D = Mdl::D, M = Mdl::M;
+  T xn[D];
+#pragma unroll
+  for (int p = 0; p < D; ++p) {
+    T ar = L.a[packed_idx(D, p, 0)] * r[0];
+#pragma unroll
+    for (int q = 1; q < D; ++q) ar = dfma(L.a[packed_idx(D, p, q)], r[q], ar);
+    T bg = b[p] + ar;
+    T v = dfma(bg, dt, x[p]);
+#pragma unroll
+    for (int k = 0; k < M; ++k) v = dfma(L.sg[p * M + k], dW[k], v);
+    xn[p] = v;
+  }
+#pragma unroll
+  for (int p = 0; p < D; ++p) x[p] = xn[p];
+}
+
+// loglikhd_obs = -c0 - 1/2 x'H x + F'x
+template <int D, class T>
+__device__ __forceinline__ T obs_term(const T* H0, const T* F0, const T* x, T c0) {
+  T Hx[D];
+#pragma unroll
+  for (int p = 0; p < D; ++p) {
+    T acc = H0[packed_idx(D, p, 0)] * x[0];
+#pragma unroll
+    for (int q = 1; q < D; ++q) acc = dfma(H0[packed_idx(D, p, q)], x[q], acc);
+    Hx[p] = acc;
+  }
+  T quad = x[0] * Hx[0];
+#pragma unroll
+  for (int p = 1; p < D; ++p) quad = dfma(x[p], Hx[p], quad);
+  T lin = F0[0] * x[0];
+#pragma unroll
+  for (int p = 1; p < D; ++p) lin = dfma(F0[p], x[p], lin);
+  T tmp = dfma((T)-0.5, quad, lin);
+  return tmp - c0;
+}
+
+// ---------------------------------------------------------------- chunked pairwise sum
+// Streaming form of the adjacent-pair tree over chunks of 64 steps.
+template <class T>
+struct PSum {
+  T s[7];
+  int n;
+  T acc;
+  __device__ __forceinline__ void init() { n = 0; acc = (T)0; }
+  __device__ __forceinline__ void add(T v) {
+    int lvl = 0;
+    bool go = true;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {  // binary counter: merge while the low bits of n are 1
+      if (go && ((n >> j) & 1)) { v = s[j] + v; lvl = j + 1; }
+      else go = false;
+    }
+    // lvl is at most 6; write via a switch to keep s[] in registers
+    switch (lvl) {
+      case 0: s[0] = v; break; case 1: s[1] = v; break; case 2: s[2] = v; break;
+      case 3: s[3] = v; break; case 4: s[4] = v; break; case 5: s[5] = v; break;
+      default: s[6] = v; break;
+    }
+    if (++n == 64) { acc = acc + (s[6] + (T)0); n = 0; }
+  }
+  __device__ __forceinline__ T finish() {
+    if (n > 0) {
+      bool have = false; T r = (T)0;
+#pragma unroll
+      for (int lvl = 0; lvl < 6; ++lvl)
+        if ((n >> lvl) & 1) { r = have ? (s[lvl] + r) : s[lvl]; have = true; }
+      acc = acc + (r + (T)0);
+      n = 0;
+    }
+    return acc;
+  }
+};
+
+// ---------------------------------------------------------------- Philox4x32-10 + normals
+struct U4 { uint32_t x, y, z, w; };
+
+__device__ __forceinline__ U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
+    uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+    U4 n = {hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    c = n;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+
+__device__ __forceinline__ void normal_pair(U4 o, double& z0, double& z1) {
+  uint64_t k1 = ((uint64_t)(o.x >> 5) << 26) | (o.y >> 6);
+  uint64_t k2 = ((uint64_t)(o.z >> 5) << 26) | (o.w >> 6);
+  double u1 = (double)(k1 + 1) * 0x1p-53;
+  double u2 = (double)k2 * 0x1p-53;
+  double rad = sqrt(-2.0 * log(u1));
+  double s, c;
+  sincospi(2.0 * u2, &s, &c);
+  z0 = rad * c;
+  z1 = rad * s;
+}
+__device__ __forceinline__ void normal_pair(U4 o, float& z0, float& z1) {
+  float u1 = (float)((o.x >> 8) + 1u) * 0x1p-24f;
+  float u2 = (float)(o.z >> 8) * 0x1p-24f;
+  float rad = sqrtf(-2.0f * logf(u1));
+  float s, c;
+  sincospif(2.0f * u2, &s, &c);
+  z0 = rad * c;
+  z1 = rad * s;
+}
+
+__device__ __forceinline__ double exp1_draw(uint64_t seed, uint32_t blk, uint32_t iter,
+                                            uint32_t salt) {
+  U4 o = philox4x32_10(U4{blk, 0xFFFFFFFFu, iter, (salt << 1) | 1u}, (uint32_t)seed,
+                       (uint32_t)(seed >> 32));
+  uint64_t k1 = ((uint64_t)(o.x >> 5) << 26) | (o.y >> 6);
+  double u = (double)(k1 + 1) * 0x1p-53;
+  return -log(u);
+}
+
+// Normal stream of one segment: normal n = step*M + k uses pair n>>1 of Philox block
+// counter (n>>1, segment, iter, salt<<1).
+template <class T>
+struct NormalStream {
+  uint32_t k0, k1, seg, iter, c3;
+  T cached;
+  __device__ __forceinline__ void init(uint64_t seed, uint32_t g, uint32_t it, uint32_t salt) {
+    k0 = (uint32_t)seed; k1 = (uint32_t)(seed >> 32); seg = g; iter = it; c3 = salt << 1;
+  }
+  __device__ __forceinline__ T get(uint32_t n) {
+    if (n & 1u) return cached;
+    U4 o = philox4x32_10(U4{n >> 1, seg, iter, c3}, k0, k1);
+    T z0, z1;
+    normal_pair(o, z0, z1);
+    cached = z1;
+    return z0;
+  }
+};
+
+}  // namespace dmt

@@ -1,0 +1,112 @@
+// dmt_internal.h — structures shared by the host runtime and the kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dmt {
+
+constexpr int kLanes = 64;  // one recording per lane of a wave64 ("recording tile")
+// spare point rows at the end of every tile (and of shared tables): the software
+// prefetch reads up to 2*kChunk points past a segment end without bounds checks
+constexpr int kPadPoints = 16;
+
+// Kernel modes of the per-block recursion kernel.
+enum Mode : int {
+  MODE_PCN = 0,        // draw_proposal_path!: pCN-mixed W°, proposal written to u°
+  MODE_RECOMPUTE = 1,  // recompute_path!(b°, b.WW): given W, law u°.PP
+  MODE_FRESH = 2,      // draw_proposal_path!(u::SamplingUnit): fresh W (ρ = 0), in place
+};
+
+// Arguments of the block kernels.  Device-path arrays are "recording-tile planes":
+// element (recording r, point q of r, component c) of an array with C components lives at
+//   ((tile_qoff[r/64] + q) * C + c) * 64 + r%64
+// so the 64 lanes of a wave (64 recordings of one tile, same block index) touch 64
+// consecutive elements per component: every load/store is a coalesced 512 B (fp64) access.
+template <class T>
+struct BlockArgs {
+  int64_t R;
+  const int64_t* tile_qoff;  // [ntiles + 1]
+  const int32_t* seg_q;      // [G] first point of the segment within its recording
+  const int32_t* seg_np;     // [G] points of the segment
+  const int64_t* st_off;     // [G] first step of the segment in reference (Z) order
+  const uint8_t* selX;       // [G] physical buffer holding u.XX[g]; u° holds the other
+  const uint8_t* selW;
+  const uint8_t* selPP;
+  const uint8_t* selPPB;
+  T* X[2];
+  T* W[2];
+  const T* t;
+  int t_shared;
+  const T* H[2][2];  // [slot][kind]
+  int H_shared[2][2];
+  const T* F[2][2];
+  const double* law[2][2];
+  // layout
+  const int64_t* blk_off;  // [R + 1]
+  const int32_t* gfirst;   // [nblocks] global segment ids
+  const int32_t* glast;
+  const uint8_t* term;
+  const double* rho;
+  const double* srho;
+  int32_t MB;     // max blocks per recording in the layout
+  int64_t tile0, tile1;
+  int64_t b0, b1;
+  // unit selection (xor-ed with the selectors)
+  int law_flip, xs_flip, xd_flip, ws_flip, wd_flip;
+  const double* Z;  // parity mode normals, reference step order, or nullptr
+  uint64_t seed;
+  uint32_t iter, salt;
+  double* ll_out;     // [nblocks]
+  uint8_t* success;   // [nblocks] or nullptr
+};
+
+struct AcceptArgs {
+  int64_t b0, b1, nblocks;
+  const int32_t* gfirst;
+  const int32_t* glast;
+  uint8_t* selX;
+  uint8_t* selW;
+  double* ll;
+  double* llp;
+  double* ll_hist;
+  double* llp_hist;
+  uint8_t* acc_hist;
+  int64_t hist_len;
+  int64_t mcmciter;  // 1-based
+  const double* E;   // [b1-b0] or nullptr
+  uint64_t seed;
+  uint32_t salt;
+  uint8_t* acc_out;  // [b1-b0] or nullptr
+};
+
+// Model/precision dispatch keys.
+struct ModelKey {
+  int model, precision, d, m;
+};
+
+// launchers (dmt_kernels.hip)
+hipError_t launch_block_kernel(const ModelKey& k, int mode, const void* args, int64_t nwaves,
+                               hipStream_t s);
+hipError_t launch_pathll_kernel(const ModelKey& k, const void* args, int64_t nwaves, hipStream_t s);
+hipError_t launch_accept(const AcceptArgs& a, hipStream_t s);
+hipError_t launch_to_planes(int precision, const double* src, void* dst0, void* dst1,
+                            const uint8_t* sel, int flip, int C, int64_t P, const int64_t* pt_off,
+                            int64_t G, const int32_t* seg_rec, const int32_t* seg_q,
+                            const int64_t* tile_qoff, hipStream_t s);
+hipError_t launch_from_planes(int precision, double* dst, const void* src0, const void* src1,
+                              const uint8_t* sel, int flip, int C, int64_t P,
+                              const int64_t* pt_off, int64_t G, const int32_t* seg_rec,
+                              const int32_t* seg_q, const int64_t* tile_qoff, hipStream_t s);
+hipError_t launch_cast(int precision, const double* src, void* dst, int64_t n, hipStream_t s);
+hipError_t launch_block_sum(const double* ll, const double* llp, const uint8_t* acc, int64_t n,
+                            double* out3, hipStream_t s);
+hipError_t launch_flip(uint8_t* sel0, uint8_t* sel1, uint8_t* sel2, uint8_t* sel3,
+                       const int32_t* gfirst, const int32_t* glast, const uint8_t* term,
+                       int32_t swap_ppb_nonterm_only, int64_t b0, int64_t b1, hipStream_t s);
+hipError_t launch_swap_ll(double* ll, double* llp, int64_t b0, int64_t b1, hipStream_t s);
+hipError_t launch_save_ll(const double* ll, const double* llp, double* llh, double* llph,
+                          int64_t nblocks, int64_t it0, int64_t b0, int64_t b1, hipStream_t s);
+hipError_t launch_debug_philox(uint64_t seed, const uint32_t* ctr, int64_t n, uint32_t* out,
+                               double* normals, hipStream_t s);
+
+}  // namespace dmt

@@ -1,0 +1,616 @@
+// dmt_kernels.hip — gfx950 kernels of the guided-bridge imputation hot path.
+//
+// k_block  : pCN mix + guided Euler–Maruyama + Girsanov log-weight for whole blocks
+//            (replaces GP.rand!(…, ρ, Val(:ll), …) at src/biblock.jl:94-106, GP.solve_and_ll!
+//            at src/block.jl:165-167,180 and rand! at src/sampling_unit.jl:119).
+// k_pathll : Girsanov log-weight of a stored path (GP.loglikhd, src/block.jl:138-152).
+// k_accept : per-block Metropolis–Hastings decision, selector flips, histories
+//            (src/biblock.jl:121-127, broadcast src/block_collection.jl:60-64).
+// k_block_sum : deterministic tree reduction for fetch_ll / fetch_ll°
+//            (src/block_collection.jl:144,156, src/block_ensemble.jl:140,152).
+//
+// Mapping: one LANE per (recording, block): the 64 lanes of a wave run 64 independent
+// Euler recursions in lock-step over a recording tile whose paths are stored
+// lane-interleaved ("planes", dmt_internal.h), so every per-step load/store is one
+// coalesced 512 B access per component.  Inputs of the next K steps are prefetched into
+// registers while the current K steps are integrated (software pipeline, prefetch
+// distance K), which is what hides HBM latency at one wave per SIMD.
+#include <math.h>
+
+#include "dmt_device.h"
+#include "dmt_internal.h"
+
+namespace dmt {
+
+template <class Mdl, class T, int MODE, int K>
+__device__ __forceinline__ bool run_segment(const Law<Mdl, T>& L, const T* __restrict__ tpl,
+                                            const int t_sh, const T* __restrict__ Ht,
+                                            const int H_sh, const T* __restrict__ Ft,
+                                            const T* __restrict__ Ws, T* __restrict__ Wd,
+                                            T* __restrict__ Xd, const double* __restrict__ Zg,
+                                            NormalStream<T>& ns, const int64_t tq, const int64_t q0,
+                                            const int np, const int lane, const T rho,
+                                            const T srho, T* x, T& sl) {
+  constexpr int D = Mdl::D, M = Mdl::M, HP = D * (D + 1) / 2;
+  // Per-segment base pointers: point i, component c of an array with C components sits at
+  // base + (i*C + c)*64.  Tiles carry kPadPoints spare rows, so the prefetch of the chunk
+  // after the last one never leaves the allocation (its values are not used).
+  const int64_t row = tq + q0;
+  const T* tb = t_sh ? tpl + q0 : tpl + row * kLanes + lane;
+  const int tst = t_sh ? 1 : kLanes;
+  const T* Hb = H_sh ? Ht + q0 * HP : Ht + row * HP * kLanes + lane;
+  const int hst = H_sh ? 1 : kLanes;
+  const T* Fb = Ft + row * D * kLanes + lane;
+  const T* Wsb = Ws + row * M * kLanes + lane;
+  T* Wdb = Wd + row * M * kLanes + lane;
+  T* Xdb = Xd + row * D * kLanes + lane;
+
+  const int nst = np - 1;
+  T wprev[M], wf[M];
+  T tcur = tb[0];
+#pragma unroll
+  for (int p = 0; p < D; ++p) Xdb[p * kLanes] = x[p];
+#pragma unroll
+  for (int k = 0; k < M; ++k) {
+    wf[k] = (T)0;
+    T w0 = (MODE == MODE_FRESH) ? (T)0 : Wsb[k * kLanes];
+    T wo = (MODE == MODE_RECOMPUTE) ? w0 : dfma(rho, w0, srho * wf[k]);
+    if (MODE != MODE_RECOMPUTE) Wdb[k * kLanes] = wo;
+    wprev[k] = wo;
+  }
+  PSum<T> ps;
+  ps.init();
+
+  T bt[K], bH[K][HP], bF[K][D], bW[K][M];
+  auto load_chunk = [&](int c0, T* vt, T (*vH)[HP], T (*vF)[D], T (*vW)[M]) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const int64_t i = c0 + j;
+      vt[j] = tb[(i + 1) * tst];
+#pragma unroll
+      for (int c = 0; c < HP; ++c) vH[j][c] = Hb[(i * HP + c) * hst];
+#pragma unroll
+      for (int c = 0; c < D; ++c) vF[j][c] = Fb[(i * D + c) * kLanes];
+      if (MODE != MODE_FRESH) {
+#pragma unroll
+        for (int k = 0; k < M; ++k) vW[j][k] = Wsb[((i + 1) * M + k) * kLanes];
+      }
+    }
+  };
+  if (nst > 0) load_chunk(0, bt, bH, bF, bW);
+  for (int c0 = 0; c0 < nst; c0 += K) {
+    T nt[K], nH[K][HP], nF[K][D], nW[K][M];
+    load_chunk(c0 + K, nt, nH, nF, nW);  // prefetch (padded rows keep it in bounds)
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const int i = c0 + j;
+      if (i < nst) {
+        const T dt = bt[j] - tcur;
+        T dW[M];
+        if (MODE == MODE_RECOMPUTE) {
+#pragma unroll
+          for (int k = 0; k < M; ++k) {
+            T wn = bW[j][k];
+            dW[k] = wn - wprev[k];
+            wprev[k] = wn;
+          }
+        } else {
+          const T sdt = sqrt(dt);
+#pragma unroll
+          for (int k = 0; k < M; ++k) {
+            const uint32_t n = (uint32_t)(i * M + k);
+            T z = Zg ? (T)Zg[(int64_t)i * M + k] : ns.get(n);
+            wf[k] = dfma(sdt, z, wf[k]);
+            T w = (MODE == MODE_FRESH) ? (T)0 : bW[j][k];
+            T wn = dfma(rho, w, srho * wf[k]);
+            Wdb[((int64_t)(i + 1) * M + k) * kLanes] = wn;
+            dW[k] = wn - wprev[k];
+            wprev[k] = wn;
+          }
+        }
+        T r[D], b[D];
+        const T G = g_at<Mdl, T>(L, bH[j], bF[j], x, r, b);
+        ps.add(G * dt);
+        euler_step<Mdl, T>(L, r, b, dt, dW, x);
+#pragma unroll
+        for (int p = 0; p < D; ++p) Xdb[((int64_t)(i + 1) * D + p) * kLanes] = x[p];
+        tcur = bt[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      bt[j] = nt[j];
+#pragma unroll
+      for (int c = 0; c < HP; ++c) bH[j][c] = nH[j][c];
+#pragma unroll
+      for (int c = 0; c < D; ++c) bF[j][c] = nF[j][c];
+#pragma unroll
+      for (int k = 0; k < M; ++k) bW[j][k] = nW[j][k];
+    }
+  }
+  sl = ps.finish();
+  bool ok = isfinite(sl);
+#pragma unroll
+  for (int p = 0; p < D; ++p) ok = ok && isfinite(x[p]);
+  return ok;
+}
+
+// Common prologue: map (wave, lane) → (tile, block index, recording, flat block id).
+template <class T>
+__device__ __forceinline__ bool map_block(const BlockArgs<T>& a, int64_t& tile, int64_t& blk) {
+  const int lane = threadIdx.x;
+  const int64_t wave = blockIdx.x;
+  tile = a.tile0 + wave / a.MB;
+  const int b = (int)(wave % a.MB);
+  if (tile >= a.tile1) return false;
+  const int64_t r = tile * kLanes + lane;
+  if (r >= a.R) return false;
+  blk = a.blk_off[r] + b;
+  if (blk >= a.blk_off[r + 1] || blk < a.b0 || blk >= a.b1) return false;
+  return true;
+}
+
+template <class Mdl, class T, int MODE, int K>
+__global__ __launch_bounds__(64) void k_block(const BlockArgs<T> a) {
+  constexpr int D = Mdl::D, M = Mdl::M, HP = D * (D + 1) / 2;
+  int64_t tile, blk;
+  if (!map_block(a, tile, blk)) return;
+  const int lane = threadIdx.x;
+  const int64_t tq = a.tile_qoff[tile];
+  auto idx = [&](int64_t q, int c, int C) -> int64_t { return ((tq + q) * C + c) * kLanes + lane; };
+  const int g0 = a.gfirst[blk], g1 = a.glast[blk];
+  const bool term = a.term[blk] != 0;
+
+  T x[D];
+  {
+    const T* Xs = a.X[a.selX[g0] ^ a.xs_flip];
+    const int64_t q = a.seg_q[g0];
+#pragma unroll
+    for (int p = 0; p < D; ++p) x[p] = Xs[idx(q, p, D)];
+  }
+  T ll;
+  {
+    const int ls = a.selPP[g0] ^ a.law_flip;
+    const double* Lr = a.law[ls][0] + (int64_t)g0 * DMT_LAW_STRIDE;
+    const T* Ht = a.H[ls][0];
+    const T* Ft = a.F[ls][0];
+    const int64_t q = a.seg_q[g0];
+    T H0[HP], F0[D];
+#pragma unroll
+    for (int c = 0; c < HP; ++c) H0[c] = a.H_shared[ls][0] ? Ht[q * HP + c] : Ht[idx(q, c, HP)];
+#pragma unroll
+    for (int c = 0; c < D; ++c) F0[c] = Ft[idx(q, c, D)];
+    ll = obs_term<D, T>(H0, F0, x, (T)Lr[DMT_LAW_C0]);
+  }
+  bool ok = true;
+  const T rho = (MODE == MODE_FRESH) ? (T)0 : (T)a.rho[blk];
+  const T srho = (MODE == MODE_FRESH) ? (T)1 : (T)a.srho[blk];
+  for (int g = g0; g <= g1; ++g) {
+    const int kind = (!term && g == g1) ? 1 : 0;
+    const int ls = (kind ? a.selPPB[g] : a.selPP[g]) ^ a.law_flip;
+    Law<Mdl, T> L;
+    L.load(a.law[ls][kind] + (int64_t)g * DMT_LAW_STRIDE);
+    NormalStream<T> ns;
+    ns.init(a.seed, (uint32_t)g, a.iter, a.salt);
+    const double* Zg = a.Z ? a.Z + a.st_off[g] * M : nullptr;
+    T* Xd = a.X[a.selX[g] ^ a.xd_flip];
+    const T* Ws = a.W[a.selW[g] ^ a.ws_flip];
+    T* Wd = a.W[a.selW[g] ^ a.wd_flip];
+    T sl;
+    const bool sok = run_segment<Mdl, T, MODE, K>(
+        L, a.t, a.t_shared, a.H[ls][kind], a.H_shared[ls][kind], a.F[ls][kind], Ws, Wd, Xd, Zg,
+        ns, tq, a.seg_q[g], a.seg_np[g], lane, rho, srho, x, sl);
+    if (!sok) { ok = false; break; }
+    ll = ll + sl;
+  }
+  a.ll_out[blk] = ok ? (double)ll : -INFINITY;
+  if (a.success) a.success[blk] = ok ? 1 : 0;
+}
+
+// Girsanov log-weight of a stored path (loglikhd!), same summation order as k_block.
+template <class Mdl, class T, int K>
+__global__ __launch_bounds__(64) void k_pathll(const BlockArgs<T> a) {
+  constexpr int D = Mdl::D, HP = D * (D + 1) / 2;
+  int64_t tile, blk;
+  if (!map_block(a, tile, blk)) return;
+  const int lane = threadIdx.x;
+  const int64_t tq = a.tile_qoff[tile];
+  auto idx = [&](int64_t q, int c, int C) -> int64_t { return ((tq + q) * C + c) * kLanes + lane; };
+  auto tload = [&](int64_t q) -> T { return a.t_shared ? a.t[q] : a.t[idx(q, 0, 1)]; };
+  const int g0 = a.gfirst[blk], g1 = a.glast[blk];
+  const bool term = a.term[blk] != 0;
+  T ll;
+  {
+    const int ls = a.selPP[g0] ^ a.law_flip;
+    const double* Lr = a.law[ls][0] + (int64_t)g0 * DMT_LAW_STRIDE;
+    const T* Xs = a.X[a.selX[g0] ^ a.xs_flip];
+    const int64_t q = a.seg_q[g0];
+    T H0[HP], F0[D], x0[D];
+#pragma unroll
+    for (int c = 0; c < HP; ++c)
+      H0[c] = a.H_shared[ls][0] ? a.H[ls][0][q * HP + c] : a.H[ls][0][idx(q, c, HP)];
+#pragma unroll
+    for (int c = 0; c < D; ++c) F0[c] = a.F[ls][0][idx(q, c, D)];
+#pragma unroll
+    for (int c = 0; c < D; ++c) x0[c] = Xs[idx(q, c, D)];
+    ll = obs_term<D, T>(H0, F0, x0, (T)Lr[DMT_LAW_C0]);
+  }
+  for (int g = g0; g <= g1; ++g) {
+    const int kind = (!term && g == g1) ? 1 : 0;
+    const int ls = (kind ? a.selPPB[g] : a.selPP[g]) ^ a.law_flip;
+    Law<Mdl, T> L;
+    L.load(a.law[ls][kind] + (int64_t)g * DMT_LAW_STRIDE);
+    const T* __restrict__ Ht = a.H[ls][kind];
+    const T* __restrict__ Ft = a.F[ls][kind];
+    const int Hsh = a.H_shared[ls][kind];
+    const T* __restrict__ Xs = a.X[a.selX[g] ^ a.xs_flip];
+    const int64_t q0 = a.seg_q[g];
+    const int nst = a.seg_np[g] - 1;
+    PSum<T> ps;
+    ps.init();
+    T tcur = tload(q0);
+    for (int c0 = 0; c0 < nst; c0 += K) {
+      T vt[K], vH[K][HP], vF[K][D], vX[K][D];
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        int i = c0 + j;
+        i = i < nst ? i : nst - 1;
+        const int64_t q = q0 + i;
+        vt[j] = tload(q + 1);
+#pragma unroll
+        for (int c = 0; c < HP; ++c) vH[j][c] = Hsh ? Ht[q * HP + c] : Ht[idx(q, c, HP)];
+#pragma unroll
+        for (int c = 0; c < D; ++c) { vF[j][c] = Ft[idx(q, c, D)]; vX[j][c] = Xs[idx(q, c, D)]; }
+      }
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        if (c0 + j < nst) {
+          const T dt = vt[j] - tcur;
+          T r[D], b[D];
+          const T G = g_at<Mdl, T>(L, vH[j], vF[j], vX[j], r, b);
+          ps.add(G * dt);
+          tcur = vt[j];
+        }
+      }
+    }
+    ll = ll + ps.finish();
+  }
+  a.ll_out[blk] = (double)ll;
+}
+
+// ---------------------------------------------------------------- accept / reject
+__global__ __launch_bounds__(256) void k_accept(const AcceptArgs a) {
+  const int64_t blk = a.b0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (blk >= a.b1) return;
+  const double E = a.E ? a.E[blk - a.b0]
+                       : exp1_draw(a.seed, (uint32_t)blk, (uint32_t)a.mcmciter, a.salt);
+  const double ll = a.ll[blk], llp = a.llp[blk];
+  const bool acc = E > -(llp - ll);
+  if (acc) {
+    for (int g = a.gfirst[blk]; g <= a.glast[blk]; ++g) {
+      a.selX[g] ^= 1;
+      a.selW[g] ^= 1;
+    }
+  }
+  if (a.hist_len > 0) {
+    const int64_t o = (a.mcmciter - 1) * a.nblocks + blk;
+    a.acc_hist[o] = acc ? 1 : 0;
+    a.ll_hist[o] = ll;
+    a.llp_hist[o] = llp;
+  }
+  if (acc) {
+    a.ll[blk] = llp;
+    a.llp[blk] = ll;
+  }
+  if (a.acc_out) a.acc_out[blk - a.b0] = acc ? 1 : 0;
+}
+
+// ---------------------------------------------------------------- small utility kernels
+__global__ void k_flip(uint8_t* sel, const int32_t* gfirst, const int32_t* glast,
+                       const uint8_t* term, int only_nonterm, int64_t b0, int64_t b1) {
+  const int64_t blk = b0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (blk >= b1) return;
+  if (only_nonterm && term[blk]) return;
+  for (int g = gfirst[blk]; g <= glast[blk]; ++g) sel[g] ^= 1;
+}
+
+__global__ void k_swap_ll(double* ll, double* llp, int64_t b0, int64_t b1) {
+  const int64_t blk = b0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (blk >= b1) return;
+  double v = ll[blk];
+  ll[blk] = llp[blk];
+  llp[blk] = v;
+}
+
+__global__ void k_save_ll(const double* ll, const double* llp, double* llh, double* llph,
+                          int64_t nblocks, int64_t it0, int64_t b0, int64_t b1) {
+  const int64_t blk = b0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (blk >= b1) return;
+  llh[it0 * nblocks + blk] = ll[blk];
+  llph[it0 * nblocks + blk] = llp[blk];
+}
+
+__device__ __forceinline__ int64_t find_seg(const int64_t* pt_off, int64_t G, int64_t p) {
+  int64_t lo = 0, hi = G;  // largest g with pt_off[g] <= p
+  while (hi - lo > 1) {
+    int64_t mid = (lo + hi) >> 1;
+    if (pt_off[mid] <= p) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+template <class T>
+__global__ void k_to_planes(const double* __restrict__ src, T* dst0, T* dst1,
+                            const uint8_t* __restrict__ sel, int flip, int C, int64_t P,
+                            const int64_t* __restrict__ pt_off, int64_t G,
+                            const int32_t* __restrict__ seg_rec, const int32_t* __restrict__ seg_q,
+                            const int64_t* __restrict__ tile_qoff) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= P * C) return;
+  const int64_t p = e / C;
+  const int c = (int)(e % C);
+  const int64_t g = find_seg(pt_off, G, p);
+  const int64_t r = seg_rec[g];
+  const int64_t q = seg_q[g] + (p - pt_off[g]);
+  const int64_t o = ((tile_qoff[r >> 6] + q) * C + c) * kLanes + (r & 63);
+  const int slot = sel ? ((sel[g] ^ flip) & 1) : 0;
+  (slot ? dst1 : dst0)[o] = (T)src[e];
+}
+
+template <class T>
+__global__ void k_from_planes(double* __restrict__ dst, const T* src0, const T* src1,
+                              const uint8_t* __restrict__ sel, int flip, int C, int64_t P,
+                              const int64_t* __restrict__ pt_off, int64_t G,
+                              const int32_t* __restrict__ seg_rec,
+                              const int32_t* __restrict__ seg_q,
+                              const int64_t* __restrict__ tile_qoff) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= P * C) return;
+  const int64_t p = e / C;
+  const int c = (int)(e % C);
+  const int64_t g = find_seg(pt_off, G, p);
+  const int64_t r = seg_rec[g];
+  const int64_t q = seg_q[g] + (p - pt_off[g]);
+  const int64_t o = ((tile_qoff[r >> 6] + q) * C + c) * kLanes + (r & 63);
+  const int slot = sel ? ((sel[g] ^ flip) & 1) : 0;
+  dst[e] = (double)(slot ? src1 : src0)[o];
+}
+
+template <class T>
+__global__ void k_cast(const double* __restrict__ src, T* __restrict__ dst, int64_t n) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < n) dst[e] = (T)src[e];
+}
+
+// Deterministic sum over n leaves: the complete adjacent-pair binary tree over the
+// leaves padded with zeros to a power of two, one workgroup of 1024.
+__global__ __launch_bounds__(1024) void k_block_sum(const double* __restrict__ ll,
+                                                    const double* __restrict__ llp,
+                                                    const uint8_t* __restrict__ acc, int64_t n,
+                                                    double* __restrict__ out3) {
+  __shared__ double s0[1024], s1[1024];
+  __shared__ long long sc[1024];
+  const int tid = threadIdx.x;
+  int64_t n2 = 1;
+  while (n2 < n) n2 <<= 1;
+  const int64_t per = n2 > 1024 ? n2 / 1024 : 1;  // leaves per thread (power of two)
+  const int nthr = (int)(n2 > 1024 ? 1024 : n2);
+  double a = 0.0, b = 0.0;
+  long long c = 0;
+  if (tid < nthr) {
+    PSum<double> pa, pb;  // stack pairwise over exactly `per` leaves (zeros padded)
+    pa.init(); pb.init();
+    int64_t base = (int64_t)tid * per;
+    double ra = 0.0, rb = 0.0;
+    if (per == 1) {
+      ra = base < n ? ll[base] : 0.0;
+      rb = base < n ? llp[base] : 0.0;
+      if (acc && base < n) c = acc[base];
+    } else {
+      // `per` is a power of two >= 2: adjacent-pair tree over the run by a binary counter
+      double sa[48], sb[48];
+      for (int64_t j = 0; j < per; ++j) {
+        const int64_t i = base + j;
+        double va = i < n ? ll[i] : 0.0;
+        double vb = i < n ? llp[i] : 0.0;
+        if (acc && i < n) c += acc[i];
+        int lvl = 0;
+        for (int64_t k = j; k & 1; k >>= 1, ++lvl) { va = sa[lvl] + va; vb = sb[lvl] + vb; }
+        sa[lvl] = va;
+        sb[lvl] = vb;
+      }
+      int top = 0;
+      while (((int64_t)1 << top) < per) ++top;
+      ra = sa[top];
+      rb = sb[top];
+    }
+    a = ra; b = rb;
+  }
+  s0[tid] = a; s1[tid] = b; sc[tid] = c;
+  __syncthreads();
+  for (int w = 1024; w > 1; w >>= 1) {
+    if (tid < w / 2) {
+      s0[tid] = s0[2 * tid] + s0[2 * tid + 1];
+      s1[tid] = s1[2 * tid] + s1[2 * tid + 1];
+      sc[tid] = sc[2 * tid] + sc[2 * tid + 1];
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    out3[0] = s0[0] + 0.0;
+    out3[1] = s1[0] + 0.0;
+    out3[2] = (double)sc[0];
+  }
+}
+
+__global__ void k_debug_philox(uint64_t seed, const uint32_t* ctr, int64_t n, uint32_t* out,
+                               double* normals) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  U4 c{ctr[4 * i], ctr[4 * i + 1], ctr[4 * i + 2], ctr[4 * i + 3]};
+  U4 o = philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  out[4 * i] = o.x; out[4 * i + 1] = o.y; out[4 * i + 2] = o.z; out[4 * i + 3] = o.w;
+  double z0, z1;
+  normal_pair(o, z0, z1);
+  normals[2 * i] = z0;
+  normals[2 * i + 1] = z1;
+}
+
+// ---------------------------------------------------------------- launchers
+static inline unsigned nblk(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
+
+constexpr int kChunk = 4;
+
+template <class Mdl, class T>
+static hipError_t launch_block_t(int mode, const void* args, int64_t nwaves, hipStream_t s) {
+  const BlockArgs<T>& a = *static_cast<const BlockArgs<T>*>(args);
+  if (nwaves <= 0) return hipSuccess;
+  dim3 grid((unsigned)nwaves), block(64);
+  switch (mode) {
+    case MODE_PCN: k_block<Mdl, T, MODE_PCN, kChunk><<<grid, block, 0, s>>>(a); break;
+    case MODE_RECOMPUTE: k_block<Mdl, T, MODE_RECOMPUTE, kChunk><<<grid, block, 0, s>>>(a); break;
+    case MODE_FRESH: k_block<Mdl, T, MODE_FRESH, kChunk><<<grid, block, 0, s>>>(a); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+template <class Mdl, class T>
+static hipError_t launch_pathll_t(const void* args, int64_t nwaves, hipStream_t s) {
+  const BlockArgs<T>& a = *static_cast<const BlockArgs<T>*>(args);
+  if (nwaves <= 0) return hipSuccess;
+  k_pathll<Mdl, T, kChunk><<<dim3((unsigned)nwaves), dim3(64), 0, s>>>(a);
+  return hipGetLastError();
+}
+
+#define DMT_DISPATCH(KEY, CALL)                                                        \
+  do {                                                                                 \
+    if ((KEY).precision == DMT_F64) {                                                  \
+      using T = double;                                                                \
+      if ((KEY).model == DMT_MODEL_OU) {                                               \
+        if ((KEY).d == 1 && (KEY).m == 1) { using Mdl = OU<T, 1, 1>; return CALL; }    \
+        if ((KEY).d == 2 && (KEY).m == 2) { using Mdl = OU<T, 2, 2>; return CALL; }    \
+        if ((KEY).d == 2 && (KEY).m == 1) { using Mdl = OU<T, 2, 1>; return CALL; }    \
+        if ((KEY).d == 3 && (KEY).m == 3) { using Mdl = OU<T, 3, 3>; return CALL; }    \
+      } else if ((KEY).model == DMT_MODEL_FHN) {                                       \
+        using Mdl = FHN<T>; return CALL;                                               \
+      } else if ((KEY).model == DMT_MODEL_LORENZ) {                                    \
+        using Mdl = Lorenz<T>; return CALL;                                            \
+      }                                                                                \
+    } else {                                                                           \
+      using T = float;                                                                 \
+      if ((KEY).model == DMT_MODEL_OU) {                                               \
+        if ((KEY).d == 1 && (KEY).m == 1) { using Mdl = OU<T, 1, 1>; return CALL; }    \
+        if ((KEY).d == 2 && (KEY).m == 2) { using Mdl = OU<T, 2, 2>; return CALL; }    \
+        if ((KEY).d == 2 && (KEY).m == 1) { using Mdl = OU<T, 2, 1>; return CALL; }    \
+        if ((KEY).d == 3 && (KEY).m == 3) { using Mdl = OU<T, 3, 3>; return CALL; }    \
+      } else if ((KEY).model == DMT_MODEL_FHN) {                                       \
+        using Mdl = FHN<T>; return CALL;                                               \
+      } else if ((KEY).model == DMT_MODEL_LORENZ) {                                    \
+        using Mdl = Lorenz<T>; return CALL;                                            \
+      }                                                                                \
+    }                                                                                  \
+    return hipErrorInvalidValue;                                                       \
+  } while (0)
+
+hipError_t launch_block_kernel(const ModelKey& k, int mode, const void* args, int64_t nwaves,
+                               hipStream_t s) {
+  DMT_DISPATCH(k, (launch_block_t<Mdl, T>(mode, args, nwaves, s)));
+}
+
+hipError_t launch_pathll_kernel(const ModelKey& k, const void* args, int64_t nwaves,
+                                hipStream_t s) {
+  DMT_DISPATCH(k, (launch_pathll_t<Mdl, T>(args, nwaves, s)));
+}
+
+hipError_t launch_accept(const AcceptArgs& a, hipStream_t s) {
+  const int64_t n = a.b1 - a.b0;
+  if (n <= 0) return hipSuccess;
+  k_accept<<<nblk(n, 256), 256, 0, s>>>(a);
+  return hipGetLastError();
+}
+
+hipError_t launch_to_planes(int precision, const double* src, void* dst0, void* dst1,
+                            const uint8_t* sel, int flip, int C, int64_t P, const int64_t* pt_off,
+                            int64_t G, const int32_t* seg_rec, const int32_t* seg_q,
+                            const int64_t* tile_qoff, hipStream_t s) {
+  const int64_t n = P * C;
+  if (n <= 0) return hipSuccess;
+  if (precision == DMT_F64)
+    k_to_planes<double><<<nblk(n, 256), 256, 0, s>>>(src, (double*)dst0, (double*)dst1, sel, flip,
+                                                      C, P, pt_off, G, seg_rec, seg_q, tile_qoff);
+  else
+    k_to_planes<float><<<nblk(n, 256), 256, 0, s>>>(src, (float*)dst0, (float*)dst1, sel, flip, C,
+                                                     P, pt_off, G, seg_rec, seg_q, tile_qoff);
+  return hipGetLastError();
+}
+
+hipError_t launch_from_planes(int precision, double* dst, const void* src0, const void* src1,
+                              const uint8_t* sel, int flip, int C, int64_t P,
+                              const int64_t* pt_off, int64_t G, const int32_t* seg_rec,
+                              const int32_t* seg_q, const int64_t* tile_qoff, hipStream_t s) {
+  const int64_t n = P * C;
+  if (n <= 0) return hipSuccess;
+  if (precision == DMT_F64)
+    k_from_planes<double><<<nblk(n, 256), 256, 0, s>>>(dst, (const double*)src0,
+                                                        (const double*)src1, sel, flip, C, P,
+                                                        pt_off, G, seg_rec, seg_q, tile_qoff);
+  else
+    k_from_planes<float><<<nblk(n, 256), 256, 0, s>>>(dst, (const float*)src0, (const float*)src1,
+                                                       sel, flip, C, P, pt_off, G, seg_rec, seg_q,
+                                                       tile_qoff);
+  return hipGetLastError();
+}
+
+hipError_t launch_cast(int precision, const double* src, void* dst, int64_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  if (precision == DMT_F64)
+    k_cast<double><<<nblk(n, 256), 256, 0, s>>>(src, (double*)dst, n);
+  else
+    k_cast<float><<<nblk(n, 256), 256, 0, s>>>(src, (float*)dst, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_block_sum(const double* ll, const double* llp, const uint8_t* acc, int64_t n,
+                            double* out3, hipStream_t s) {
+  k_block_sum<<<1, 1024, 0, s>>>(ll, llp, acc, n, out3);
+  return hipGetLastError();
+}
+
+hipError_t launch_flip(uint8_t* sel0, uint8_t* sel1, uint8_t* sel2, uint8_t* sel3,
+                       const int32_t* gfirst, const int32_t* glast, const uint8_t* term,
+                       int32_t swap_ppb_nonterm_only, int64_t b0, int64_t b1, hipStream_t s) {
+  const int64_t n = b1 - b0;
+  if (n <= 0) return hipSuccess;
+  uint8_t* sels[4] = {sel0, sel1, sel2, sel3};
+  for (int i = 0; i < 4; ++i) {
+    if (!sels[i]) continue;
+    const int only_nonterm = (i == 3) ? swap_ppb_nonterm_only : 0;
+    k_flip<<<nblk(n, 256), 256, 0, s>>>(sels[i], gfirst, glast, term, only_nonterm, b0, b1);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_swap_ll(double* ll, double* llp, int64_t b0, int64_t b1, hipStream_t s) {
+  const int64_t n = b1 - b0;
+  if (n <= 0) return hipSuccess;
+  k_swap_ll<<<nblk(n, 256), 256, 0, s>>>(ll, llp, b0, b1);
+  return hipGetLastError();
+}
+
+hipError_t launch_save_ll(const double* ll, const double* llp, double* llh, double* llph,
+                          int64_t nblocks, int64_t it0, int64_t b0, int64_t b1, hipStream_t s) {
+  const int64_t n = b1 - b0;
+  if (n <= 0) return hipSuccess;
+  k_save_ll<<<nblk(n, 256), 256, 0, s>>>(ll, llp, llh, llph, nblocks, it0, b0, b1);
+  return hipGetLastError();
+}
+
+hipError_t launch_debug_philox(uint64_t seed, const uint32_t* ctr, int64_t n, uint32_t* out,
+                               double* normals, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  k_debug_philox<<<nblk(n, 256), 256, 0, s>>>(seed, ctr, n, out, normals);
+  return hipGetLastError();
+}
+
+}  // namespace dmt

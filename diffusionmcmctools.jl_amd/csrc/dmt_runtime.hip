@@ -1,0 +1,1265 @@
+// dmt_runtime.hip — host side of libdmt: the C-ABI of include/dmt.h.
+//
+// The handle owns every device buffer of a SamplingEnsemble (u and u°) and of its block
+// layouts.  Swaps are selector flips (one byte per segment per container kind), never
+// copies: the reference swaps container *pointers* element by element
+// (src/biblock.jl:148-199), and views from different block layouts alias the same
+// SamplingPair vectors (src/block.jl:66-72), so selectors live per segment.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/dmt.h"
+#include "dmt_internal.h"
+
+using namespace dmt;
+
+namespace {
+
+thread_local std::string g_err;
+
+dmt_status fail(dmt_status code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_OK(expr)                                                                      \
+  do {                                                                                    \
+    hipError_t _e = (expr);                                                               \
+    if (_e != hipSuccess)                                                                 \
+      return fail(DMT_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));        \
+  } while (0)
+
+template <class T>
+hipError_t dalloc(T** p, int64_t n) {
+  *p = nullptr;
+  if (n <= 0) n = 1;
+  return hipMalloc((void**)p, (size_t)n * sizeof(T));
+}
+
+struct Layout {
+  int64_t nblocks = 0;
+  int32_t MB = 0;
+  int64_t hist_len = 0;
+  std::vector<int64_t> blk_off;  // [R + 1]
+  std::vector<int32_t> gfirst, glast;
+  std::vector<uint8_t> term;
+  int64_t* d_blk_off = nullptr;
+  int32_t* d_gfirst = nullptr;
+  int32_t* d_glast = nullptr;
+  uint8_t* d_term = nullptr;
+  double* d_rho = nullptr;
+  double* d_srho = nullptr;
+  double* d_ll = nullptr;
+  double* d_llp = nullptr;
+  double* d_llh = nullptr;
+  double* d_llph = nullptr;
+  uint8_t* d_acch = nullptr;
+  uint8_t* d_success = nullptr;
+  uint8_t* d_acc = nullptr;
+  void release() {
+    void* ps[] = {d_blk_off, d_gfirst, d_glast, d_term, d_rho, d_srho, d_ll,
+                  d_llp,     d_llh,    d_llph,  d_acch, d_success, d_acc};
+    for (void* p : ps)
+      if (p) (void)hipFree(p);
+  }
+};
+
+}  // namespace
+
+struct dmt_ens {
+  ModelKey key{};
+  int d = 0, m = 0, hp = 0;
+  size_t esz = 8;
+  int device = 0;
+  uint64_t seed = 0;
+  int grid_shared = 0;
+  hipStream_t stream = nullptr;
+  // structure
+  int64_t R = 0, G = 0, P = 0, S = 0, ntiles = 0, Ptile = 0, Q0 = 0;
+  std::vector<int64_t> rec_seg0;  // [R + 1]
+  std::vector<int32_t> seg_rec, seg_q, seg_np;
+  std::vector<int64_t> pt_off, st_off, tile_qoff;
+  int64_t* d_pt_off = nullptr;
+  int64_t* d_st_off = nullptr;
+  int64_t* d_tile_qoff = nullptr;
+  int32_t* d_seg_rec = nullptr;
+  int32_t* d_seg_q = nullptr;
+  int32_t* d_seg_np = nullptr;
+  uint8_t* d_sel[4] = {nullptr, nullptr, nullptr, nullptr};  // X, W, PP, PPB
+  std::vector<uint8_t> h_selPP, h_selPPB;                     // host mirrors (laws swap only by dmt_swap)
+  void* d_X[2] = {nullptr, nullptr};
+  void* d_W[2] = {nullptr, nullptr};
+  void* d_t = nullptr;
+  bool have_t = false;
+  void* d_H[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};  // [slot][kind]
+  int H_shared[2] = {0, 0};                                     // per kind
+  void* d_F[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+  double* d_law[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+  bool have_law[2][2] = {{false, false}, {false, false}};  // [unit][kind] uploaded at least once
+  // staging
+  double* d_stage = nullptr;
+  int64_t stage_n = 0;
+  double* d_Z = nullptr;
+  int64_t Z_n = 0;
+  double* d_red = nullptr;  // [3] reduction output, [3 * nranks] gather
+  double* d_gather = nullptr;
+  std::vector<std::unique_ptr<Layout>> layouts;  // layouts[0] = internal "unit" layout
+  // timing
+  bool timing = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> pending[DMT_K_COUNT];
+  double t_ms[DMT_K_COUNT] = {0, 0, 0, 0, 0};
+  int64_t t_cnt[DMT_K_COUNT] = {0, 0, 0, 0, 0};
+  std::vector<hipEvent_t> free_events;
+  // comm
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0;
+  int64_t bytes = 0;
+};
+
+namespace {
+
+template <class T>
+dmt_status ens_alloc(dmt_ens* h, T** p, int64_t n) {
+  hipError_t e = dalloc(p, n);
+  if (e != hipSuccess)
+    return fail(DMT_ERR_OOM, std::string("hipMalloc of ") + std::to_string(n * sizeof(T)) +
+                                 " bytes failed: " + hipGetErrorString(e));
+  h->bytes += std::max<int64_t>(n, 1) * (int64_t)sizeof(T);
+  return DMT_OK;
+}
+dmt_status ens_alloc_bytes(dmt_ens* h, void** p, int64_t nbytes) {
+  return ens_alloc(h, (uint8_t**)p, nbytes);
+}
+
+#define DMT_TRY(expr)            \
+  do {                           \
+    dmt_status _s = (expr);      \
+    if (_s != DMT_OK) return _s; \
+  } while (0)
+
+hipEvent_t get_event(dmt_ens* h) {
+  if (!h->free_events.empty()) {
+    hipEvent_t e = h->free_events.back();
+    h->free_events.pop_back();
+    return e;
+  }
+  hipEvent_t e;
+  (void)hipEventCreate(&e);
+  return e;
+}
+
+void drain_timing(dmt_ens* h) {
+  for (int k = 0; k < DMT_K_COUNT; ++k) {
+    for (auto& pr : h->pending[k]) {
+      float ms = 0.f;
+      if (hipEventSynchronize(pr.second) == hipSuccess &&
+          hipEventElapsedTime(&ms, pr.first, pr.second) == hipSuccess) {
+        h->t_ms[k] += ms;
+        h->t_cnt[k] += 1;
+      }
+      h->free_events.push_back(pr.first);
+      h->free_events.push_back(pr.second);
+    }
+    h->pending[k].clear();
+  }
+}
+
+struct TimedScope {
+  dmt_ens* h;
+  int k;
+  hipEvent_t e0 = nullptr;
+  TimedScope(dmt_ens* h_, int k_) : h(h_), k(k_) {
+    if (h->timing) {
+      e0 = get_event(h);
+      (void)hipEventRecord(e0, h->stream);
+    }
+  }
+  ~TimedScope() {
+    if (h->timing) {
+      hipEvent_t e1 = get_event(h);
+      (void)hipEventRecord(e1, h->stream);
+      h->pending[k].push_back({e0, e1});
+      if (h->pending[k].size() > 512) drain_timing(h);
+    }
+  }
+};
+
+dmt_status ensure_stage(dmt_ens* h, int64_t n) {
+  if (n <= h->stage_n) return DMT_OK;
+  if (h->d_stage) {
+    (void)hipFree(h->d_stage);
+    h->bytes -= h->stage_n * 8;
+  }
+  h->d_stage = nullptr;
+  h->stage_n = 0;
+  DMT_TRY(ens_alloc(h, &h->d_stage, n));
+  h->stage_n = n;
+  return DMT_OK;
+}
+
+dmt_status ensure_Z(dmt_ens* h, int64_t n) {
+  if (n <= h->Z_n) return DMT_OK;
+  if (h->d_Z) {
+    (void)hipFree(h->d_Z);
+    h->bytes -= h->Z_n * 8;
+  }
+  h->d_Z = nullptr;
+  h->Z_n = 0;
+  DMT_TRY(ens_alloc(h, &h->d_Z, n));
+  h->Z_n = n;
+  return DMT_OK;
+}
+
+int64_t plane_elems(const dmt_ens* h, int C) { return h->Ptile * C * kLanes; }
+
+dmt_status check_h(dmt_ens* h) {
+  if (!h) return fail(DMT_ERR_INVALID, "null handle");
+  if (hipSetDevice(h->device) != hipSuccess) return fail(DMT_ERR_HIP, "hipSetDevice failed");
+  return DMT_OK;
+}
+
+dmt_status get_layout(dmt_ens* h, int32_t id, Layout** L) {
+  if (id < 0 || id >= (int32_t)h->layouts.size() || !h->layouts[id])
+    return fail(DMT_ERR_INVALID, "bad layout id " + std::to_string(id));
+  *L = h->layouts[id].get();
+  return DMT_OK;
+}
+
+dmt_status check_range(const Layout* L, int64_t b0, int64_t b1) {
+  if (b0 < 0 || b1 > L->nblocks || b0 > b1)
+    return fail(DMT_ERR_INVALID, "block range [" + std::to_string(b0) + "," + std::to_string(b1) +
+                                     ") outside layout of " + std::to_string(L->nblocks) + " blocks");
+  return DMT_OK;
+}
+
+// recording of a flat block id (largest r with blk_off[r] <= blk)
+int64_t rec_of_block(const Layout* L, int64_t blk) {
+  auto it = std::upper_bound(L->blk_off.begin(), L->blk_off.end(), blk);
+  return (int64_t)(it - L->blk_off.begin()) - 1;
+}
+
+dmt_status law_ready(dmt_ens* h, int unit_needed_flip, const Layout* L, int64_t b0, int64_t b1) {
+  // the PP law is always needed; PPB only for non-terminal blocks
+  bool need_ppb = false;
+  for (int64_t b = b0; b < b1 && !need_ppb; ++b) need_ppb = !L->term[b];
+  if (!h->have_t) return fail(DMT_ERR_STATE, "time grid not uploaded (dmt_upload_grid)");
+  if (!h->d_law[0][0] || !h->d_law[1][0] || !h->d_H[0][0] || !h->d_F[0][0])
+    return fail(DMT_ERR_STATE, "PP law not uploaded (dmt_upload_law)");
+  if (need_ppb && (!h->d_law[0][1] || !h->d_H[0][1] || !h->d_F[0][1]))
+    return fail(DMT_ERR_STATE, "PPb (blocking) law not uploaded but a non-terminal block is used");
+  (void)unit_needed_flip;
+  return DMT_OK;
+}
+
+template <class T>
+void fill_common(dmt_ens* h, const Layout* L, BlockArgs<T>& a) {
+  a.R = h->R;
+  a.tile_qoff = h->d_tile_qoff;
+  a.seg_q = h->d_seg_q;
+  a.seg_np = h->d_seg_np;
+  a.st_off = h->d_st_off;
+  a.selX = h->d_sel[0];
+  a.selW = h->d_sel[1];
+  a.selPP = h->d_sel[2];
+  a.selPPB = h->d_sel[3];
+  for (int s = 0; s < 2; ++s) {
+    a.X[s] = (T*)h->d_X[s];
+    a.W[s] = (T*)h->d_W[s];
+    for (int k = 0; k < 2; ++k) {
+      a.H[s][k] = (const T*)h->d_H[s][k];
+      a.H_shared[s][k] = h->H_shared[k];
+      a.F[s][k] = (const T*)h->d_F[s][k];
+      a.law[s][k] = h->d_law[s][k];
+    }
+  }
+  a.t = (const T*)h->d_t;
+  a.t_shared = h->grid_shared;
+  a.blk_off = L->d_blk_off;
+  a.gfirst = L->d_gfirst;
+  a.glast = L->d_glast;
+  a.term = L->d_term;
+  a.rho = L->d_rho;
+  a.srho = L->d_srho;
+  a.MB = L->MB;
+  a.seed = h->seed;
+  a.Z = nullptr;
+  a.success = nullptr;
+}
+
+dmt_status run_block_kernel(dmt_ens* h, const Layout* L, int mode, int kind_timer, int64_t b0,
+                            int64_t b1, int law_flip, int xs, int xd, int ws, int wd,
+                            const double* dZ, int64_t iter, uint32_t salt, double* ll_out,
+                            uint8_t* success, bool pathll) {
+  if (b1 <= b0) return DMT_OK;
+  const int64_t r0 = rec_of_block(L, b0), r1 = rec_of_block(L, b1 - 1);
+  const int64_t tile0 = r0 / kLanes, tile1 = r1 / kLanes + 1;
+  const int64_t nwaves = (tile1 - tile0) * (int64_t)L->MB;
+  TimedScope ts(h, kind_timer);
+  hipError_t e;
+  auto fill = [&](auto& a) {
+    fill_common(h, L, a);
+    a.tile0 = tile0;
+    a.tile1 = tile1;
+    a.b0 = b0;
+    a.b1 = b1;
+    a.law_flip = law_flip;
+    a.xs_flip = xs;
+    a.xd_flip = xd;
+    a.ws_flip = ws;
+    a.wd_flip = wd;
+    a.Z = dZ;
+    a.iter = (uint32_t)iter;
+    a.salt = salt;
+    a.ll_out = ll_out;
+    a.success = success;
+  };
+  if (h->key.precision == DMT_F64) {
+    BlockArgs<double> a{};
+    fill(a);
+    e = pathll ? launch_pathll_kernel(h->key, &a, nwaves, h->stream)
+               : launch_block_kernel(h->key, mode, &a, nwaves, h->stream);
+  } else {
+    BlockArgs<float> a{};
+    fill(a);
+    e = pathll ? launch_pathll_kernel(h->key, &a, nwaves, h->stream)
+               : launch_block_kernel(h->key, mode, &a, nwaves, h->stream);
+  }
+  if (e != hipSuccess) return fail(DMT_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(e));
+  return DMT_OK;
+}
+
+dmt_status upload_Z(dmt_ens* h, const double* Z, const double** dZ) {
+  *dZ = nullptr;
+  if (!Z) return DMT_OK;
+  const int64_t n = h->S * h->m;
+  DMT_TRY(ensure_Z(h, n));
+  HIP_OK(hipMemcpyAsync(h->d_Z, Z, (size_t)n * 8, hipMemcpyHostToDevice, h->stream));
+  *dZ = h->d_Z;
+  return DMT_OK;
+}
+
+dmt_status build_layout(dmt_ens* h, const int32_t* n_blocks, const int32_t* seg_first,
+                        const int32_t* seg_last, const uint8_t* last, const double* rho,
+                        int64_t hist_len, int32_t* id) {
+  auto L = std::make_unique<Layout>();
+  L->blk_off.assign(h->R + 1, 0);
+  for (int64_t r = 0; r < h->R; ++r) {
+    if (n_blocks[r] < 0) return fail(DMT_ERR_INVALID, "negative block count");
+    L->blk_off[r + 1] = L->blk_off[r] + n_blocks[r];
+    L->MB = std::max<int32_t>(L->MB, n_blocks[r]);
+  }
+  L->nblocks = L->blk_off[h->R];
+  L->hist_len = hist_len < 0 ? 0 : hist_len;
+  L->gfirst.resize(L->nblocks);
+  L->glast.resize(L->nblocks);
+  L->term.resize(L->nblocks);
+  std::vector<double> srho(L->nblocks), rr(L->nblocks);
+  for (int64_t r = 0; r < h->R; ++r) {
+    const int64_t nseg = h->rec_seg0[r + 1] - h->rec_seg0[r];
+    for (int64_t b = L->blk_off[r]; b < L->blk_off[r + 1]; ++b) {
+      if (seg_first[b] < 0 || seg_last[b] >= nseg || seg_first[b] > seg_last[b])
+        return fail(DMT_ERR_INVALID, "block " + std::to_string(b) + " has an invalid segment range");
+      if (!last[b] && seg_first[b] == seg_last[b])
+        return fail(DMT_ERR_INVALID, "non-terminal block " + std::to_string(b) +
+                                         " needs >= 2 segments (reference indexes PP[1], src/block.jl:66,178)");
+      L->gfirst[b] = (int32_t)(h->rec_seg0[r] + seg_first[b]);
+      L->glast[b] = (int32_t)(h->rec_seg0[r] + seg_last[b]);
+      L->term[b] = last[b] ? 1 : 0;
+      rr[b] = rho[b];
+      if (!(rho[b] >= 0.0 && rho[b] <= 1.0)) return fail(DMT_ERR_INVALID, "rho outside [0,1]");
+      srho[b] = std::sqrt(1.0 - rho[b] * rho[b]);
+    }
+  }
+  const int64_t nb = L->nblocks;
+  DMT_TRY(ens_alloc(h, &L->d_blk_off, h->R + 1));
+  DMT_TRY(ens_alloc(h, &L->d_gfirst, nb));
+  DMT_TRY(ens_alloc(h, &L->d_glast, nb));
+  DMT_TRY(ens_alloc(h, &L->d_term, nb));
+  DMT_TRY(ens_alloc(h, &L->d_rho, nb));
+  DMT_TRY(ens_alloc(h, &L->d_srho, nb));
+  DMT_TRY(ens_alloc(h, &L->d_ll, nb));
+  DMT_TRY(ens_alloc(h, &L->d_llp, nb));
+  DMT_TRY(ens_alloc(h, &L->d_success, nb));
+  DMT_TRY(ens_alloc(h, &L->d_acc, nb));
+  if (L->hist_len > 0) {
+    DMT_TRY(ens_alloc(h, &L->d_llh, L->hist_len * nb));
+    DMT_TRY(ens_alloc(h, &L->d_llph, L->hist_len * nb));
+    DMT_TRY(ens_alloc(h, &L->d_acch, L->hist_len * nb));
+    HIP_OK(hipMemsetAsync(L->d_llh, 0, (size_t)(L->hist_len * nb) * 8, h->stream));
+    HIP_OK(hipMemsetAsync(L->d_llph, 0, (size_t)(L->hist_len * nb) * 8, h->stream));
+    HIP_OK(hipMemsetAsync(L->d_acch, 0, (size_t)(L->hist_len * nb), h->stream));
+  }
+  HIP_OK(hipMemcpy(L->d_blk_off, L->blk_off.data(), (h->R + 1) * 8, hipMemcpyHostToDevice));
+  if (nb > 0) {
+    HIP_OK(hipMemcpy(L->d_gfirst, L->gfirst.data(), nb * 4, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(L->d_glast, L->glast.data(), nb * 4, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(L->d_term, L->term.data(), nb, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(L->d_rho, rr.data(), nb * 8, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(L->d_srho, srho.data(), nb * 8, hipMemcpyHostToDevice));
+    std::vector<double> ninf(nb, -INFINITY);  // ll = -Inf initially (src/block.jl:75)
+    HIP_OK(hipMemcpy(L->d_ll, ninf.data(), nb * 8, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(L->d_llp, ninf.data(), nb * 8, hipMemcpyHostToDevice));
+  }
+  h->layouts.push_back(std::move(L));
+  *id = (int32_t)h->layouts.size() - 1;
+  return DMT_OK;
+}
+
+inline int dmt_packed(int d, int a, int b) {
+  if (a > b) std::swap(a, b);
+  return a * d - (a * (a - 1)) / 2 + (b - a);
+}
+
+bool supported(const dmt_model* m) {
+  if (m->precision != DMT_F64 && m->precision != DMT_F32) return false;
+  switch (m->model) {
+    case DMT_MODEL_OU:
+      return (m->d == 1 && m->m == 1) || (m->d == 2 && m->m == 2) || (m->d == 2 && m->m == 1) ||
+             (m->d == 3 && m->m == 3);
+    case DMT_MODEL_FHN: return m->d == 2 && m->m == 1;
+    case DMT_MODEL_LORENZ: return m->d == 3 && m->m == 3;
+  }
+  return false;
+}
+
+// ------------------------------------------------------------ backward filter (host)
+// Small dense helpers, row-major d×d with d ≤ 3.
+struct Mat {
+  int n;
+  double a[9];
+  double& operator()(int i, int j) { return a[i * n + j]; }
+  double operator()(int i, int j) const { return a[i * n + j]; }
+};
+Mat mzero(int n) { Mat m; m.n = n; std::memset(m.a, 0, sizeof m.a); return m; }
+Mat meye(int n) { Mat m = mzero(n); for (int i = 0; i < n; ++i) m(i, i) = 1; return m; }
+Mat mmul(const Mat& A, const Mat& B) {
+  Mat C = mzero(A.n);
+  for (int i = 0; i < A.n; ++i)
+    for (int j = 0; j < A.n; ++j) {
+      double s = 0;
+      for (int k = 0; k < A.n; ++k) s += A(i, k) * B(k, j);
+      C(i, j) = s;
+    }
+  return C;
+}
+Mat mT(const Mat& A) { Mat C = mzero(A.n); for (int i = 0; i < A.n; ++i) for (int j = 0; j < A.n; ++j) C(i, j) = A(j, i); return C; }
+Mat madd(const Mat& A, const Mat& B, double s = 1.0) { Mat C = A; for (int i = 0; i < A.n * A.n; ++i) C.a[i] += s * B.a[i]; return C; }
+void mvec(const Mat& A, const double* x, double* y) {
+  for (int i = 0; i < A.n; ++i) { double s = 0; for (int k = 0; k < A.n; ++k) s += A(i, k) * x[k]; y[i] = s; }
+}
+double mnorm(const Mat& A) { double s = 0; for (int i = 0; i < A.n * A.n; ++i) s = std::max(s, std::fabs(A.a[i])); return s * A.n; }
+// inverse and log|det| by Gauss-Jordan with partial pivoting
+bool minv(const Mat& A, Mat& Inv, double& logabsdet) {
+  int n = A.n;
+  double w[3][6];
+  for (int i = 0; i < n; ++i) for (int j = 0; j < n; ++j) { w[i][j] = A(i, j); w[i][n + j] = (i == j); }
+  logabsdet = 0;
+  for (int c = 0; c < n; ++c) {
+    int p = c;
+    for (int i = c + 1; i < n; ++i) if (std::fabs(w[i][c]) > std::fabs(w[p][c])) p = i;
+    if (w[p][c] == 0.0) return false;
+    if (p != c) for (int j = 0; j < 2 * n; ++j) std::swap(w[p][j], w[c][j]);
+    double piv = w[c][c];
+    logabsdet += std::log(std::fabs(piv));
+    for (int j = 0; j < 2 * n; ++j) w[c][j] /= piv;
+    for (int i = 0; i < n; ++i) if (i != c) {
+      double f = w[i][c];
+      if (f != 0.0) for (int j = 0; j < 2 * n; ++j) w[i][j] -= f * w[c][j];
+    }
+  }
+  Inv = mzero(n);
+  for (int i = 0; i < n; ++i) for (int j = 0; j < n; ++j) Inv(i, j) = w[i][n + j];
+  return true;
+}
+
+// Exact transition of dX = (BX + beta)dt + sigma dW over a step h:
+// X_{t+h} = Phi X_t + mu + N(0, K).  Series with scaling-and-squaring.
+void transition(const Mat& B, const double* beta, const Mat& At, double h, Mat& Phi, double* mu, Mat& K) {
+  const int n = B.n;
+  int sq = 0;
+  double hs = h;
+  while (mnorm(B) * hs > 0.25 && sq < 40) { hs *= 0.5; ++sq; }
+  Mat A = B;
+  for (int i = 0; i < n * n; ++i) A.a[i] *= hs;
+  // Phi = sum A^k/k!, mu = hs sum A^k/(k+1)! beta, K = sum hs^{k+1}/(k+1)! L^k(At)
+  Phi = meye(n);
+  Mat term = meye(n);
+  Mat S1 = meye(n);  // sum A^k/(k+1)!
+  Mat Lk = At;       // L^k(At) * hs^k / k!   (L(X) = BX + XB^T)
+  K = mzero(n);
+  for (int i = 0; i < n * n; ++i) K.a[i] = hs * Lk.a[i];
+  for (int k = 1; k <= 30; ++k) {
+    term = mmul(term, A);
+    for (int i = 0; i < n * n; ++i) term.a[i] /= k;
+    Phi = madd(Phi, term);
+    Mat t2 = term;
+    for (int i = 0; i < n * n; ++i) t2.a[i] /= (k + 1);
+    S1 = madd(S1, t2);
+    Mat nl = madd(mmul(B, Lk), mmul(Lk, mT(B)));
+    for (int i = 0; i < n * n; ++i) nl.a[i] *= hs / k;
+    Lk = nl;
+    for (int i = 0; i < n * n; ++i) K.a[i] += hs * Lk.a[i] / (k + 1);
+    if (mnorm(term) < 1e-18 && mnorm(Lk) * hs < 1e-18 * (1.0 + mnorm(K))) break;
+  }
+  double sb[3];
+  mvec(S1, beta, sb);
+  for (int i = 0; i < n; ++i) mu[i] = hs * sb[i];
+  for (int s = 0; s < sq; ++s) {  // compose two half steps
+    double m2[3];
+    mvec(Phi, mu, m2);
+    for (int i = 0; i < n; ++i) mu[i] = m2[i] + mu[i];
+    K = madd(mmul(mmul(Phi, K), mT(Phi)), K);
+    Phi = mmul(Phi, Phi);
+  }
+  for (int i = 0; i < n; ++i) for (int j = i + 1; j < n; ++j) { double v = 0.5 * (K(i, j) + K(j, i)); K(i, j) = v; K(j, i) = v; }
+}
+
+}  // namespace
+
+// =====================================================================================
+extern "C" {
+
+const char* dmt_last_error(void) { return g_err.c_str(); }
+const char* dmt_version(void) { return "dmt-mi355x 0.1.0 (gfx950)"; }
+
+dmt_status dmt_create(dmt_ens** out, const dmt_model* model, const dmt_structure* st,
+                      const dmt_config* cfg) {
+  if (!out || !model || !st || !cfg) return fail(DMT_ERR_INVALID, "null argument");
+  *out = nullptr;
+  if (!supported(model)) return fail(DMT_ERR_INVALID, "unsupported model/dimension/precision combination");
+  if (st->n_recordings <= 0 || !st->n_segments || !st->n_points)
+    return fail(DMT_ERR_INVALID, "empty structure");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+    return fail(DMT_ERR_HIP, "no HIP device available: libdmt has no CPU fallback");
+  if (cfg->device < 0 || cfg->device >= ndev) return fail(DMT_ERR_INVALID, "bad device ordinal");
+  HIP_OK(hipSetDevice(cfg->device));
+  auto h = std::make_unique<dmt_ens>();
+  h->key = ModelKey{model->model, model->precision, model->d, model->m};
+  h->d = model->d;
+  h->m = model->m;
+  h->hp = model->d * (model->d + 1) / 2;
+  h->esz = model->precision == DMT_F64 ? 8 : 4;
+  h->device = cfg->device;
+  h->seed = cfg->seed;
+  h->grid_shared = cfg->grid_shared ? 1 : 0;
+  h->R = st->n_recordings;
+  h->rec_seg0.assign(h->R + 1, 0);
+  for (int64_t r = 0; r < h->R; ++r) {
+    if (st->n_segments[r] <= 0) return fail(DMT_ERR_INVALID, "recording without segments");
+    h->rec_seg0[r + 1] = h->rec_seg0[r] + st->n_segments[r];
+  }
+  h->G = h->rec_seg0[h->R];
+  if (h->G > INT32_MAX) return fail(DMT_ERR_INVALID, "too many segments");
+  h->seg_rec.resize(h->G);
+  h->seg_q.resize(h->G);
+  h->seg_np.resize(h->G);
+  h->pt_off.resize(h->G);
+  h->st_off.resize(h->G);
+  std::vector<int64_t> recQ(h->R);
+  int64_t P = 0, S = 0;
+  for (int64_t r = 0; r < h->R; ++r) {
+    int64_t q = 0;
+    for (int64_t g = h->rec_seg0[r]; g < h->rec_seg0[r + 1]; ++g) {
+      const int32_t np = st->n_points[g];
+      if (np < 2) return fail(DMT_ERR_INVALID, "segment with fewer than 2 grid points");
+      h->seg_rec[g] = (int32_t)r;
+      h->seg_q[g] = (int32_t)q;
+      h->seg_np[g] = np;
+      h->pt_off[g] = P;
+      h->st_off[g] = S;
+      q += np;
+      P += np;
+      S += np - 1;
+    }
+    recQ[r] = q;
+  }
+  h->P = P;
+  h->S = S;
+  h->Q0 = recQ[0];
+  if (h->grid_shared) {
+    for (int64_t r = 1; r < h->R; ++r) {
+      if (h->rec_seg0[r + 1] - h->rec_seg0[r] != h->rec_seg0[1] - h->rec_seg0[0])
+        return fail(DMT_ERR_INVALID, "grid_shared requires identical segment structure");
+      for (int64_t k = 0; k < h->rec_seg0[1]; ++k)
+        if (h->seg_np[h->rec_seg0[r] + k] != h->seg_np[k])
+          return fail(DMT_ERR_INVALID, "grid_shared requires identical segment structure");
+    }
+  }
+  h->ntiles = (h->R + kLanes - 1) / kLanes;
+  h->tile_qoff.assign(h->ntiles + 1, 0);
+  for (int64_t t = 0; t < h->ntiles; ++t) {
+    int64_t mx = 0;
+    for (int64_t r = t * kLanes; r < std::min<int64_t>(h->R, (t + 1) * kLanes); ++r) mx = std::max(mx, recQ[r]);
+    h->tile_qoff[t + 1] = h->tile_qoff[t] + mx + kPadPoints;
+  }
+  h->Ptile = h->tile_qoff[h->ntiles];
+  HIP_OK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+  dmt_ens* hp = h.get();
+  DMT_TRY(ens_alloc(hp, &hp->d_pt_off, hp->G));
+  DMT_TRY(ens_alloc(hp, &hp->d_st_off, hp->G));
+  DMT_TRY(ens_alloc(hp, &hp->d_tile_qoff, hp->ntiles + 1));
+  DMT_TRY(ens_alloc(hp, &hp->d_seg_rec, hp->G));
+  DMT_TRY(ens_alloc(hp, &hp->d_seg_q, hp->G));
+  DMT_TRY(ens_alloc(hp, &hp->d_seg_np, hp->G));
+  HIP_OK(hipMemcpy(hp->d_pt_off, hp->pt_off.data(), hp->G * 8, hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(hp->d_st_off, hp->st_off.data(), hp->G * 8, hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(hp->d_tile_qoff, hp->tile_qoff.data(), (hp->ntiles + 1) * 8, hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(hp->d_seg_rec, hp->seg_rec.data(), hp->G * 4, hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(hp->d_seg_q, hp->seg_q.data(), hp->G * 4, hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(hp->d_seg_np, hp->seg_np.data(), hp->G * 4, hipMemcpyHostToDevice));
+  for (int i = 0; i < 4; ++i) {
+    DMT_TRY(ens_alloc(hp, &hp->d_sel[i], hp->G));
+    HIP_OK(hipMemset(hp->d_sel[i], 0, hp->G));
+  }
+  hp->h_selPP.assign(hp->G, 0);
+  hp->h_selPPB.assign(hp->G, 0);
+  for (int s = 0; s < 2; ++s) {
+    DMT_TRY(ens_alloc_bytes(hp, &hp->d_X[s], plane_elems(hp, hp->d) * hp->esz));
+    DMT_TRY(ens_alloc_bytes(hp, &hp->d_W[s], plane_elems(hp, hp->m) * hp->esz));
+    HIP_OK(hipMemset(hp->d_X[s], 0, plane_elems(hp, hp->d) * hp->esz));
+    HIP_OK(hipMemset(hp->d_W[s], 0, plane_elems(hp, hp->m) * hp->esz));
+  }
+  DMT_TRY(ens_alloc(hp, &hp->d_red, 3));
+  // internal layout 0: one terminal block per recording over all its segments, ρ = 0
+  // (the view draw_proposal_path!(u::SamplingUnit) acts on, src/sampling_unit.jl:118-120)
+  {
+    std::vector<int32_t> nb(hp->R, 1), sf(hp->R, 0), sl(hp->R);
+    std::vector<uint8_t> lt(hp->R, 1);
+    std::vector<double> rz(hp->R, 0.0);
+    for (int64_t r = 0; r < hp->R; ++r) sl[r] = (int32_t)(hp->rec_seg0[r + 1] - hp->rec_seg0[r] - 1);
+    int32_t id;
+    DMT_TRY(build_layout(hp, nb.data(), sf.data(), sl.data(), lt.data(), rz.data(), 0, &id));
+  }
+  HIP_OK(hipStreamSynchronize(hp->stream));
+  *out = h.release();
+  return DMT_OK;
+}
+
+dmt_status dmt_destroy(dmt_ens* h) {
+  if (!h) return DMT_OK;
+  (void)hipSetDevice(h->device);
+  (void)hipStreamSynchronize(h->stream);
+  drain_timing(h);
+  for (auto e : h->free_events) (void)hipEventDestroy(e);
+  for (auto& L : h->layouts)
+    if (L) L->release();
+  void* ps[] = {h->d_pt_off, h->d_st_off, h->d_tile_qoff, h->d_seg_rec, h->d_seg_q, h->d_seg_np,
+                h->d_sel[0], h->d_sel[1], h->d_sel[2], h->d_sel[3], h->d_X[0], h->d_X[1],
+                h->d_W[0], h->d_W[1], h->d_t, h->d_stage, h->d_Z, h->d_red, h->d_gather};
+  for (void* p : ps)
+    if (p) (void)hipFree(p);
+  for (int s = 0; s < 2; ++s)
+    for (int k = 0; k < 2; ++k) {
+      if (h->d_H[s][k] && !(s == 1 && h->d_H[1][k] == h->d_H[0][k])) (void)hipFree(h->d_H[s][k]);
+      if (h->d_F[s][k]) (void)hipFree(h->d_F[s][k]);
+      if (h->d_law[s][k]) (void)hipFree(h->d_law[s][k]);
+    }
+  if (h->comm) (void)ncclCommDestroy(h->comm);
+  (void)hipStreamDestroy(h->stream);
+  delete h;
+  return DMT_OK;
+}
+
+dmt_status dmt_upload_grid(dmt_ens* h, const double* t) {
+  DMT_TRY(check_h(h));
+  if (!t) return fail(DMT_ERR_INVALID, "null grid");
+  if (h->grid_shared) {
+    if (!h->d_t) {
+      DMT_TRY(ens_alloc_bytes(h, &h->d_t, (h->Q0 + kPadPoints) * h->esz));
+      HIP_OK(hipMemsetAsync(h->d_t, 0, (h->Q0 + kPadPoints) * h->esz, h->stream));
+    }
+    DMT_TRY(ensure_stage(h, h->Q0));
+    HIP_OK(hipMemcpyAsync(h->d_stage, t, h->Q0 * 8, hipMemcpyHostToDevice, h->stream));
+    HIP_OK(launch_cast(h->key.precision, h->d_stage, h->d_t, h->Q0, h->stream));
+  } else {
+    if (!h->d_t) {
+      DMT_TRY(ens_alloc_bytes(h, &h->d_t, plane_elems(h, 1) * h->esz));
+      HIP_OK(hipMemsetAsync(h->d_t, 0, plane_elems(h, 1) * h->esz, h->stream));
+    }
+    DMT_TRY(ensure_stage(h, h->P));
+    HIP_OK(hipMemcpyAsync(h->d_stage, t, h->P * 8, hipMemcpyHostToDevice, h->stream));
+    HIP_OK(launch_to_planes(h->key.precision, h->d_stage, h->d_t, h->d_t, nullptr, 0, 1, h->P,
+                            h->d_pt_off, h->G, h->d_seg_rec, h->d_seg_q, h->d_tile_qoff, h->stream));
+  }
+  HIP_OK(hipStreamSynchronize(h->stream));
+  h->have_t = true;
+  return DMT_OK;
+}
+
+}  // extern "C"
+
+namespace {
+__global__ void k_scatter_rows(const double* src, double* dst0, double* dst1, const uint8_t* sel,
+                               int flip, int64_t G, int stride) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= G * stride) return;
+  const int64_t g = e / stride;
+  ((sel[g] ^ flip) & 1 ? dst1 : dst0)[e] = src[e];
+}
+}  // namespace
+
+extern "C" {
+
+dmt_status dmt_upload_law(dmt_ens* h, int32_t unit, int32_t kind, const double* H,
+                          int32_t H_shared, const double* F, const double* laws) {
+  DMT_TRY(check_h(h));
+  if ((unit != DMT_U && unit != DMT_UPROP) || (kind != DMT_LAW_PP && kind != DMT_LAW_PPB))
+    return fail(DMT_ERR_INVALID, "bad unit/kind");
+  uint8_t* sel = h->d_sel[2 + kind];
+  const std::vector<uint8_t>& hsel = kind == 0 ? h->h_selPP : h->h_selPPB;
+  const int esz = (int)h->esz;
+  // The very first upload of a law kind also fills the other unit: u° = deepcopy(u)
+  // (src/sampling_pair.jl:51).  Later uploads touch only the named unit, as
+  // recompute_guiding_term!(bb.b) leaves bb.b°'s laws alone (src/block.jl:102-110).
+  const bool seeded = h->have_law[0][kind] || h->have_law[1][kind];
+  if (H) {
+    if (H_shared) {
+      // a shared table serves every segment of the unit: the unit's laws must sit in one
+      // physical slot for all segments (selectors uniform)
+      for (int64_t g = 1; g < h->G; ++g)
+        if (hsel[g] != hsel[0])
+          return fail(DMT_ERR_STATE, "shared H upload needs uniform PP selectors (laws swapped on a subset)");
+      if (h->d_H[0][kind] && !h->H_shared[kind])
+        return fail(DMT_ERR_STATE, "cannot switch an uploaded per-segment H table to shared");
+      const int slot = hsel[0] ^ unit;
+      for (int s = 0; s < 2; ++s)
+        if (!h->d_H[s][kind]) {
+          DMT_TRY(ens_alloc_bytes(h, &h->d_H[s][kind], (h->Q0 + kPadPoints) * h->hp * esz));
+          HIP_OK(hipMemsetAsync(h->d_H[s][kind], 0, (h->Q0 + kPadPoints) * h->hp * esz, h->stream));
+        }
+      h->H_shared[kind] = 1;
+      DMT_TRY(ensure_stage(h, h->Q0 * h->hp));
+      HIP_OK(hipMemcpyAsync(h->d_stage, H, h->Q0 * h->hp * 8, hipMemcpyHostToDevice, h->stream));
+      HIP_OK(launch_cast(h->key.precision, h->d_stage, h->d_H[slot][kind], h->Q0 * h->hp, h->stream));
+      if (!seeded) {  // first upload of this kind also seeds the other unit
+        HIP_OK(launch_cast(h->key.precision, h->d_stage, h->d_H[slot ^ 1][kind], h->Q0 * h->hp, h->stream));
+      }
+    } else {
+      if (h->d_H[0][kind] && h->H_shared[kind])
+        return fail(DMT_ERR_STATE, "cannot switch an uploaded shared H table to per-segment");
+      for (int s = 0; s < 2; ++s)
+        if (!h->d_H[s][kind]) {
+          DMT_TRY(ens_alloc_bytes(h, &h->d_H[s][kind], plane_elems(h, h->hp) * esz));
+          HIP_OK(hipMemsetAsync(h->d_H[s][kind], 0, plane_elems(h, h->hp) * esz, h->stream));
+        }
+      h->H_shared[kind] = 0;
+      DMT_TRY(ensure_stage(h, h->P * h->hp));
+      HIP_OK(hipMemcpyAsync(h->d_stage, H, h->P * h->hp * 8, hipMemcpyHostToDevice, h->stream));
+      for (int pass = 0; pass < (seeded ? 1 : 2); ++pass)
+        HIP_OK(launch_to_planes(h->key.precision, h->d_stage, h->d_H[0][kind], h->d_H[1][kind], sel,
+                                unit ^ pass, h->hp, h->P, h->d_pt_off, h->G, h->d_seg_rec, h->d_seg_q,
+                                h->d_tile_qoff, h->stream));
+    }
+  }
+  if (F) {
+    for (int s = 0; s < 2; ++s)
+      if (!h->d_F[s][kind]) {
+        DMT_TRY(ens_alloc_bytes(h, &h->d_F[s][kind], plane_elems(h, h->d) * esz));
+        HIP_OK(hipMemsetAsync(h->d_F[s][kind], 0, plane_elems(h, h->d) * esz, h->stream));
+      }
+    DMT_TRY(ensure_stage(h, h->P * h->d));
+    HIP_OK(hipMemcpyAsync(h->d_stage, F, h->P * h->d * 8, hipMemcpyHostToDevice, h->stream));
+    for (int pass = 0; pass < (seeded ? 1 : 2); ++pass)
+      HIP_OK(launch_to_planes(h->key.precision, h->d_stage, h->d_F[0][kind], h->d_F[1][kind], sel,
+                              unit ^ pass, h->d, h->P, h->d_pt_off, h->G, h->d_seg_rec, h->d_seg_q,
+                              h->d_tile_qoff, h->stream));
+  }
+  if (laws) {
+    for (int s = 0; s < 2; ++s)
+      if (!h->d_law[s][kind]) {
+        DMT_TRY(ens_alloc(h, &h->d_law[s][kind], h->G * DMT_LAW_STRIDE));
+        HIP_OK(hipMemsetAsync(h->d_law[s][kind], 0, h->G * DMT_LAW_STRIDE * 8, h->stream));
+      }
+    DMT_TRY(ensure_stage(h, h->G * DMT_LAW_STRIDE));
+    HIP_OK(hipMemcpyAsync(h->d_stage, laws, h->G * DMT_LAW_STRIDE * 8, hipMemcpyHostToDevice, h->stream));
+    const int64_t n = h->G * DMT_LAW_STRIDE;
+    for (int pass = 0; pass < (seeded ? 1 : 2); ++pass) {
+      k_scatter_rows<<<(unsigned)((n + 255) / 256), 256, 0, h->stream>>>(
+          h->d_stage, h->d_law[0][kind], h->d_law[1][kind], sel, unit ^ pass, h->G, DMT_LAW_STRIDE);
+      HIP_OK(hipGetLastError());
+    }
+  }
+  HIP_OK(hipStreamSynchronize(h->stream));
+  if (H || F || laws) h->have_law[unit][kind] = true;
+  return DMT_OK;
+}
+
+dmt_status dmt_set_paths(dmt_ens* h, int32_t unit, const double* X, const double* W) {
+  DMT_TRY(check_h(h));
+  if (unit != DMT_U && unit != DMT_UPROP) return fail(DMT_ERR_INVALID, "bad unit");
+  const double* src[2] = {X, W};
+  const int C[2] = {h->d, h->m};
+  for (int w = 0; w < 2; ++w) {
+    if (!src[w]) continue;
+    DMT_TRY(ensure_stage(h, h->P * C[w]));
+    HIP_OK(hipMemcpyAsync(h->d_stage, src[w], h->P * C[w] * 8, hipMemcpyHostToDevice, h->stream));
+    void** dst = w == 0 ? h->d_X : h->d_W;
+    HIP_OK(launch_to_planes(h->key.precision, h->d_stage, dst[0], dst[1], h->d_sel[w], unit, C[w],
+                            h->P, h->d_pt_off, h->G, h->d_seg_rec, h->d_seg_q, h->d_tile_qoff,
+                            h->stream));
+  }
+  HIP_OK(hipStreamSynchronize(h->stream));
+  return DMT_OK;
+}
+
+dmt_status dmt_download_paths(dmt_ens* h, int32_t unit, int32_t what, double* out) {
+  DMT_TRY(check_h(h));
+  if ((unit != DMT_U && unit != DMT_UPROP) || (what != 0 && what != 1) || !out)
+    return fail(DMT_ERR_INVALID, "bad unit/what/out");
+  const int C = what == 0 ? h->d : h->m;
+  DMT_TRY(ensure_stage(h, h->P * C));
+  void** src = what == 0 ? h->d_X : h->d_W;
+  HIP_OK(launch_from_planes(h->key.precision, h->d_stage, src[0], src[1], h->d_sel[what], unit, C,
+                            h->P, h->d_pt_off, h->G, h->d_seg_rec, h->d_seg_q, h->d_tile_qoff,
+                            h->stream));
+  HIP_OK(hipMemcpyAsync(out, h->d_stage, h->P * C * 8, hipMemcpyDeviceToHost, h->stream));
+  HIP_OK(hipStreamSynchronize(h->stream));
+  return DMT_OK;
+}
+
+dmt_status dmt_create_layout(dmt_ens* h, const int32_t* n_blocks, const int32_t* seg_first,
+                             const int32_t* seg_last, const uint8_t* last, const double* rho,
+                             int64_t hist_len, int32_t* layout_id) {
+  DMT_TRY(check_h(h));
+  if (!n_blocks || !seg_first || !seg_last || !last || !rho || !layout_id)
+    return fail(DMT_ERR_INVALID, "null argument");
+  DMT_TRY(build_layout(h, n_blocks, seg_first, seg_last, last, rho, hist_len, layout_id));
+  HIP_OK(hipStreamSynchronize(h->stream));
+  return DMT_OK;
+}
+
+dmt_status dmt_layout_size(dmt_ens* h, int32_t layout, int64_t* n) {
+  DMT_TRY(check_h(h));
+  Layout* L;
+  DMT_TRY(get_layout(h, layout, &L));
+  *n = L->nblocks;
+  return DMT_OK;
+}
+
+dmt_status dmt_draw_unit(dmt_ens* h, int32_t unit, int64_t r0, int64_t r1, const double* Z,
+                         int64_t iter, uint32_t salt, double* ll_out, uint8_t* success_out) {
+  DMT_TRY(check_h(h));
+  if (unit != DMT_U && unit != DMT_UPROP) return fail(DMT_ERR_INVALID, "bad unit");
+  Layout* L;
+  DMT_TRY(get_layout(h, 0, &L));
+  DMT_TRY(check_range(L, r0, r1));
+  DMT_TRY(law_ready(h, unit, L, r0, r1));
+  const double* dZ;
+  DMT_TRY(upload_Z(h, Z, &dZ));
+  DMT_TRY(run_block_kernel(h, L, MODE_FRESH, DMT_K_DRAW, r0, r1, unit, unit, unit, unit, unit, dZ,
+                           iter, salt, L->d_llp, L->d_success, false));
+  if (ll_out) HIP_OK(hipMemcpyAsync(ll_out, L->d_llp + r0, (r1 - r0) * 8, hipMemcpyDeviceToHost, h->stream));
+  if (success_out) HIP_OK(hipMemcpyAsync(success_out, L->d_success + r0, r1 - r0, hipMemcpyDeviceToHost, h->stream));
+  HIP_OK(hipStreamSynchronize(h->stream));
+  return DMT_OK;
+}
+
+dmt_status dmt_draw_proposal(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, const double* Z,
+                             int64_t iter, uint32_t salt, uint8_t* success_out) {
+  DMT_TRY(check_h(h));
+  Layout* L;
+  DMT_TRY(get_layout(h, layout, &L));
+  DMT_TRY(check_range(L, b0, b1));
+  DMT_TRY(law_ready(h, 0, L, b0, b1));
+  const double* dZ;
+  DMT_TRY(upload_Z(h, Z, &dZ));
+  // law: accepted u.PP (flip 0); start from u.XX; write u°.XX/u°.WW; read u.WW
+  DMT_TRY(run_block_kernel(h, L, MODE_PCN, DMT_K_DRAW, b0, b1, 0, 0, 1, 0, 1, dZ, iter, salt,
+                           L->d_llp, success_out ? L->d_success : nullptr, false));
+  if (success_out) {
+    HIP_OK(hipMemcpyAsync(success_out, L->d_success + b0, b1 - b0, hipMemcpyDeviceToHost, h->stream));
+    HIP_OK(hipStreamSynchronize(h->stream));
+  } else if (Z) {
+    HIP_OK(hipStreamSynchronize(h->stream));  // host Z buffer must stay valid until copied
+  }
+  return DMT_OK;
+}
+
+dmt_status dmt_accept_reject(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, const double* E,
+                             int64_t mcmciter, uint32_t salt, uint8_t* acc_out) {
+  DMT_TRY(check_h(h));
+  Layout* L;
+  DMT_TRY(get_layout(h, layout, &L));
+  DMT_TRY(check_range(L, b0, b1));
+  if (L->hist_len > 0 && (mcmciter < 1 || mcmciter > L->hist_len))
+    return fail(DMT_ERR_INVALID, "mcmciter outside 1:ll_hist_len");
+  const double* dE = nullptr;
+  if (E) {
+    DMT_TRY(ensure_Z(h, std::max<int64_t>(b1 - b0, 1)));
+    HIP_OK(hipMemcpyAsync(h->d_Z, E, (b1 - b0) * 8, hipMemcpyHostToDevice, h->stream));
+    dE = h->d_Z;
+  }
+  AcceptArgs a{};
+  a.b0 = b0;
+  a.b1 = b1;
+  a.nblocks = L->nblocks;
+  a.gfirst = L->d_gfirst;
+  a.glast = L->d_glast;
+  a.selX = h->d_sel[0];
+  a.selW = h->d_sel[1];
+  a.ll = L->d_ll;
+  a.llp = L->d_llp;
+  a.ll_hist = L->d_llh;
+  a.llp_hist = L->d_llph;
+  a.acc_hist = L->d_acch;
+  a.hist_len = L->hist_len;
+  a.mcmciter = mcmciter;
+  a.E = dE;
+  a.seed = h->seed;
+  a.salt = salt;
+  a.acc_out = acc_out ? L->d_acc : nullptr;
+  {
+    TimedScope ts(h, DMT_K_ACCEPT);
+    HIP_OK(launch_accept(a, h->stream));
+  }
+  if (acc_out) {
+    HIP_OK(hipMemcpyAsync(acc_out, L->d_acc, b1 - b0, hipMemcpyDeviceToHost, h->stream));
+    HIP_OK(hipStreamSynchronize(h->stream));
+  } else if (E) {
+    HIP_OK(hipStreamSynchronize(h->stream));
+  }
+  return DMT_OK;
+}
+
+dmt_status dmt_loglikhd(dmt_ens* h, int32_t layout, int32_t unit, int64_t b0, int64_t b1) {
+  DMT_TRY(check_h(h));
+  if (unit != DMT_U && unit != DMT_UPROP) return fail(DMT_ERR_INVALID, "bad unit");
+  Layout* L;
+  DMT_TRY(get_layout(h, layout, &L));
+  DMT_TRY(check_range(L, b0, b1));
+  DMT_TRY(law_ready(h, unit, L, b0, b1));
+  DMT_TRY(run_block_kernel(h, L, 0, DMT_K_PATHLL, b0, b1, unit, unit, unit, unit, unit, nullptr, 0,
+                           0, unit == DMT_U ? L->d_ll : L->d_llp, nullptr, true));
+  return DMT_OK;
+}
+
+dmt_status dmt_recompute_path(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int32_t skip,
+                              uint8_t* success_out) {
+  DMT_TRY(check_h(h));
+  if (skip != 0)
+    return fail(DMT_ERR_INVALID, "skip != 0 is not supported (its upstream semantics are not pinned; "
+                                 "every reference call passes skip=0)");
+  Layout* L;
+  DMT_TRY(get_layout(h, layout, &L));
+  DMT_TRY(check_range(L, b0, b1));
+  DMT_TRY(law_ready(h, 1, L, b0, b1));
+  // law u°.PP (flip 1); start from u°.XX; write u°.XX; read u.WW (the accepted W)
+  DMT_TRY(run_block_kernel(h, L, MODE_RECOMPUTE, DMT_K_RECOMPUTE, b0, b1, 1, 1, 1, 0, 0, nullptr, 0,
+                           0, L->d_llp, success_out ? L->d_success : nullptr, false));
+  if (success_out) {
+    HIP_OK(hipMemcpyAsync(success_out, L->d_success + b0, b1 - b0, hipMemcpyDeviceToHost, h->stream));
+    HIP_OK(hipStreamSynchronize(h->stream));
+  }
+  return DMT_OK;
+}
+
+dmt_status dmt_swap(dmt_ens* h, int32_t layout, int32_t what, int64_t b0, int64_t b1) {
+  DMT_TRY(check_h(h));
+  Layout* L;
+  DMT_TRY(get_layout(h, layout, &L));
+  DMT_TRY(check_range(L, b0, b1));
+  if (what & ~(DMT_SWAP_XX | DMT_SWAP_WW | DMT_SWAP_PP | DMT_SWAP_LL))
+    return fail(DMT_ERR_INVALID, "bad swap mask");
+  uint8_t* s0 = (what & DMT_SWAP_XX) ? h->d_sel[0] : nullptr;
+  uint8_t* s1 = (what & DMT_SWAP_WW) ? h->d_sel[1] : nullptr;
+  uint8_t* s2 = (what & DMT_SWAP_PP) ? h->d_sel[2] : nullptr;
+  uint8_t* s3 = (what & DMT_SWAP_PP) ? h->d_sel[3] : nullptr;
+  // swap_PP!: BiBlock{true} swaps PP only; BiBlock{false} also P_last, P_excl, Pb_excl
+  // (src/biblock.jl:180-199) — i.e. PPb of all its segments.
+  HIP_OK(launch_flip(s0, s1, s2, s3, L->d_gfirst, L->d_glast, L->d_term, 1, b0, b1, h->stream));
+  if (what & DMT_SWAP_PP) {
+    for (int64_t b = b0; b < b1; ++b)
+      for (int32_t g = L->gfirst[b]; g <= L->glast[b]; ++g) {
+        h->h_selPP[g] ^= 1;
+        if (!L->term[b]) h->h_selPPB[g] ^= 1;
+      }
+  }
+  if (what & DMT_SWAP_LL) HIP_OK(launch_swap_ll(L->d_ll, L->d_llp, b0, b1, h->stream));
+  return DMT_OK;
+}
+
+dmt_status dmt_save_ll(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int64_t mcmciter) {
+  DMT_TRY(check_h(h));
+  Layout* L;
+  DMT_TRY(get_layout(h, layout, &L));
+  DMT_TRY(check_range(L, b0, b1));
+  if (mcmciter < 1 || mcmciter > L->hist_len) return fail(DMT_ERR_INVALID, "mcmciter outside 1:ll_hist_len");
+  HIP_OK(launch_save_ll(L->d_ll, L->d_llp, L->d_llh, L->d_llph, L->nblocks, mcmciter - 1, b0, b1, h->stream));
+  return DMT_OK;
+}
+
+dmt_status dmt_set_accepted(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int64_t mcmciter,
+                            const uint8_t* v) {
+  DMT_TRY(check_h(h));
+  Layout* L;
+  DMT_TRY(get_layout(h, layout, &L));
+  DMT_TRY(check_range(L, b0, b1));
+  if (mcmciter < 1 || mcmciter > L->hist_len) return fail(DMT_ERR_INVALID, "mcmciter outside 1:ll_hist_len");
+  if (!v) return fail(DMT_ERR_INVALID, "null values");
+  HIP_OK(hipMemcpyAsync(L->d_acch + (mcmciter - 1) * L->nblocks + b0, v, b1 - b0, hipMemcpyHostToDevice, h->stream));
+  HIP_OK(hipStreamSynchronize(h->stream));
+  return DMT_OK;
+}
+
+static dmt_status block_state_ptr(Layout* L, int32_t what, void** p, size_t* esz, bool* hist) {
+  *hist = false;
+  switch (what) {
+    case DMT_BLK_LL: *p = L->d_ll; *esz = 8; return DMT_OK;
+    case DMT_BLK_LLPROP: *p = L->d_llp; *esz = 8; return DMT_OK;
+    case DMT_BLK_LL_HIST: *p = L->d_llh; *esz = 8; *hist = true; break;
+    case DMT_BLK_LLPROP_HIST: *p = L->d_llph; *esz = 8; *hist = true; break;
+    case DMT_BLK_ACC_HIST: *p = L->d_acch; *esz = 1; *hist = true; break;
+    default: return fail(DMT_ERR_INVALID, "bad block-state selector");
+  }
+  if (L->hist_len <= 0) return fail(DMT_ERR_STATE, "layout has no histories (ll_hist_len = 0)");
+  return DMT_OK;
+}
+
+dmt_status dmt_get_block_state(dmt_ens* h, int32_t layout, int32_t what, int64_t b0, int64_t b1,
+                               void* out) {
+  DMT_TRY(check_h(h));
+  Layout* L;
+  DMT_TRY(get_layout(h, layout, &L));
+  DMT_TRY(check_range(L, b0, b1));
+  void* p; size_t esz; bool hist;
+  DMT_TRY(block_state_ptr(L, what, &p, &esz, &hist));
+  if (b1 > b0) {
+    if (!hist) {
+      HIP_OK(hipMemcpyAsync(out, (char*)p + b0 * esz, (b1 - b0) * esz, hipMemcpyDeviceToHost, h->stream));
+    } else {
+      HIP_OK(hipMemcpy2DAsync(out, (b1 - b0) * esz, (char*)p + b0 * esz, L->nblocks * esz, (b1 - b0) * esz,
+                              L->hist_len, hipMemcpyDeviceToHost, h->stream));
+    }
+  }
+  HIP_OK(hipStreamSynchronize(h->stream));
+  return DMT_OK;
+}
+
+dmt_status dmt_set_block_state(dmt_ens* h, int32_t layout, int32_t what, int64_t b0, int64_t b1,
+                               const void* in) {
+  DMT_TRY(check_h(h));
+  Layout* L;
+  DMT_TRY(get_layout(h, layout, &L));
+  DMT_TRY(check_range(L, b0, b1));
+  void* p; size_t esz; bool hist;
+  DMT_TRY(block_state_ptr(L, what, &p, &esz, &hist));
+  if (b1 > b0) {
+    if (!hist) {
+      HIP_OK(hipMemcpyAsync((char*)p + b0 * esz, in, (b1 - b0) * esz, hipMemcpyHostToDevice, h->stream));
+    } else {
+      HIP_OK(hipMemcpy2DAsync((char*)p + b0 * esz, L->nblocks * esz, in, (b1 - b0) * esz, (b1 - b0) * esz,
+                              L->hist_len, hipMemcpyHostToDevice, h->stream));
+    }
+  }
+  HIP_OK(hipStreamSynchronize(h->stream));
+  return DMT_OK;
+}
+
+dmt_status dmt_fetch_ll(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int64_t mcmciter,
+                        double* ll, double* ll_prop, int64_t* n_acc) {
+  DMT_TRY(check_h(h));
+  Layout* L;
+  DMT_TRY(get_layout(h, layout, &L));
+  DMT_TRY(check_range(L, b0, b1));
+  const uint8_t* acc = nullptr;
+  if (mcmciter > 0) {
+    if (mcmciter > L->hist_len) return fail(DMT_ERR_INVALID, "mcmciter outside 1:ll_hist_len");
+    acc = L->d_acch + (mcmciter - 1) * L->nblocks + b0;
+  }
+  {
+    TimedScope ts(h, DMT_K_REDUCE);
+    HIP_OK(launch_block_sum(L->d_ll + b0, L->d_llp + b0, acc, b1 - b0, h->d_red, h->stream));
+  }
+  double v[3];
+  if (h->comm && h->nranks > 1) {
+    if (!h->d_gather) DMT_TRY(ens_alloc(h, &h->d_gather, 3 * h->nranks));
+    if (ncclAllGather(h->d_red, h->d_gather, 3, ncclDouble, h->comm, h->stream) != ncclSuccess)
+      return fail(DMT_ERR_COMM, "ncclAllGather failed");
+    std::vector<double> all(3 * h->nranks);
+    HIP_OK(hipMemcpyAsync(all.data(), h->d_gather, 3 * h->nranks * 8, hipMemcpyDeviceToHost, h->stream));
+    HIP_OK(hipStreamSynchronize(h->stream));
+    // fixed rank-order adjacent-pair tree, ranks padded to a power of two
+    int n2 = 1;
+    while (n2 < h->nranks) n2 <<= 1;
+    for (int c = 0; c < 3; ++c) {
+      std::vector<double> lv(n2, 0.0);
+      for (int r = 0; r < h->nranks; ++r) lv[r] = all[3 * r + c];
+      for (int w = n2; w > 1; w >>= 1)
+        for (int j = 0; j < w / 2; ++j) lv[j] = lv[2 * j] + lv[2 * j + 1];
+      v[c] = lv[0] + 0.0;
+    }
+  } else {
+    HIP_OK(hipMemcpyAsync(v, h->d_red, 24, hipMemcpyDeviceToHost, h->stream));
+    HIP_OK(hipStreamSynchronize(h->stream));
+  }
+  if (ll) *ll = v[0];
+  if (ll_prop) *ll_prop = v[1];
+  if (n_acc) *n_acc = (int64_t)v[2];
+  return DMT_OK;
+}
+
+dmt_status dmt_guiding_linear(int32_t d, const double* Bt, const double* beta, const double* at,
+                              int32_t npts, const double* t, const double* HT, const double* FT,
+                              double cT, double* H, double* F, double* c) {
+  if (d < 1 || d > 3 || npts < 1 || !Bt || !beta || !at || !t || !HT || !FT || !H || !F || !c)
+    return fail(DMT_ERR_INVALID, "bad arguments to dmt_guiding_linear");
+  const int hp = d * (d + 1) / 2;
+  Mat B = mzero(d), A = mzero(d), Hc = mzero(d);
+  for (int i = 0; i < d * d; ++i) B.a[i] = Bt[i];
+  for (int i = 0; i < d; ++i)
+    for (int j = 0; j < d; ++j) {
+      A(i, j) = at[dmt_packed(d, i, j)];
+      Hc(i, j) = HT[dmt_packed(d, i, j)];
+    }
+  double Fc[3] = {0, 0, 0};
+  for (int i = 0; i < d; ++i) Fc[i] = FT[i];
+  double cc = cT;
+  auto store = [&](int i) {
+    for (int p = 0; p < d; ++p)
+      for (int q = p; q < d; ++q) H[(int64_t)i * hp + dmt_packed(d, p, q)] = Hc(p, q);
+    for (int p = 0; p < d; ++p) F[(int64_t)i * d + p] = Fc[p];
+    c[i] = cc;
+  };
+  store(npts - 1);
+  for (int i = npts - 2; i >= 0; --i) {
+    const double hstep = t[i + 1] - t[i];
+    if (!(hstep > 0)) return fail(DMT_ERR_INVALID, "time grid must be strictly increasing");
+    Mat Phi, K;
+    double mu[3];
+    transition(B, beta, A, hstep, Phi, mu, K);
+    // Gaussian integral over X_{t+h} ~ N(Phi x + mu, K) of exp(-c - x'Hx/2 + F'x)
+    Mat IHK = madd(meye(d), mmul(Hc, K));
+    Mat S;
+    double lad;
+    if (!minv(IHK, S, lad)) return fail(DMT_ERR_INVALID, "singular I + HK in backward filter");
+    Mat Hh = mmul(S, Hc);
+    for (int p = 0; p < d; ++p)
+      for (int q = p + 1; q < d; ++q) { double v = 0.5 * (Hh(p, q) + Hh(q, p)); Hh(p, q) = v; Hh(q, p) = v; }
+    double Fh[3], KF[3];
+    mvec(S, Fc, Fh);
+    mvec(K, Fc, KF);
+    double fkf = 0;
+    for (int p = 0; p < d; ++p) fkf += Fh[p] * KF[p];
+    double ch = cc + 0.5 * lad - 0.5 * fkf;
+    // shift by m = Phi x + mu
+    double Hmu[3];
+    mvec(Hh, mu, Hmu);
+    double g[3];
+    for (int p = 0; p < d; ++p) g[p] = Fh[p] - Hmu[p];
+    Mat PhT = mT(Phi);
+    double Fn[3];
+    mvec(PhT, g, Fn);
+    Mat Hn = mmul(mmul(PhT, Hh), Phi);
+    for (int p = 0; p < d; ++p)
+      for (int q = p + 1; q < d; ++q) { double v = 0.5 * (Hn(p, q) + Hn(q, p)); Hn(p, q) = v; Hn(q, p) = v; }
+    double fmu = 0, muHmu = 0;
+    for (int p = 0; p < d; ++p) { fmu += Fh[p] * mu[p]; muHmu += mu[p] * Hmu[p]; }
+    cc = ch - fmu + 0.5 * muHmu;
+    Hc = Hn;
+    for (int p = 0; p < d; ++p) Fc[p] = Fn[p];
+    store(i);
+  }
+  return DMT_OK;
+}
+
+dmt_status dmt_comm_unique_id(uint8_t* id_out) {
+  if (!id_out) return fail(DMT_ERR_INVALID, "null id");
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return fail(DMT_ERR_COMM, "ncclGetUniqueId failed");
+  static_assert(sizeof(ncclUniqueId) == 128, "unexpected ncclUniqueId size");
+  std::memcpy(id_out, &id, 128);
+  return DMT_OK;
+}
+
+dmt_status dmt_comm_init(dmt_ens* h, int32_t nranks, int32_t rank, const uint8_t* id) {
+  DMT_TRY(check_h(h));
+  if (nranks < 1 || rank < 0 || rank >= nranks || !id) return fail(DMT_ERR_INVALID, "bad comm args");
+  if (h->comm) {
+    (void)ncclCommDestroy(h->comm);
+    h->comm = nullptr;
+  }
+  h->nranks = nranks;
+  h->rank = rank;
+  if (nranks == 1) return DMT_OK;
+  ncclUniqueId uid;
+  std::memcpy(&uid, id, 128);
+  if (ncclCommInitRank(&h->comm, nranks, uid, rank) != ncclSuccess)
+    return fail(DMT_ERR_COMM, "ncclCommInitRank failed");
+  return DMT_OK;
+}
+
+dmt_status dmt_sync(dmt_ens* h) {
+  DMT_TRY(check_h(h));
+  HIP_OK(hipStreamSynchronize(h->stream));
+  return DMT_OK;
+}
+
+dmt_status dmt_set_timing(dmt_ens* h, int32_t on) {
+  DMT_TRY(check_h(h));
+  HIP_OK(hipStreamSynchronize(h->stream));
+  drain_timing(h);
+  for (int k = 0; k < DMT_K_COUNT; ++k) { h->t_ms[k] = 0; h->t_cnt[k] = 0; }
+  h->timing = on != 0;
+  return DMT_OK;
+}
+
+dmt_status dmt_get_timing(dmt_ens* h, int32_t kernel, double* ms, int64_t* count) {
+  DMT_TRY(check_h(h));
+  if (kernel < 0 || kernel >= DMT_K_COUNT) return fail(DMT_ERR_INVALID, "bad kernel id");
+  HIP_OK(hipStreamSynchronize(h->stream));
+  drain_timing(h);
+  if (ms) *ms = h->t_ms[kernel];
+  if (count) *count = h->t_cnt[kernel];
+  return DMT_OK;
+}
+
+dmt_status dmt_memory_bytes(dmt_ens* h, int64_t* bytes) {
+  if (!h || !bytes) return fail(DMT_ERR_INVALID, "null argument");
+  *bytes = h->bytes;
+  return DMT_OK;
+}
+
+dmt_status dmt_debug_philox(int32_t device, uint64_t seed, const uint32_t* ctr, int64_t n,
+                            uint32_t* out) {
+  if (!ctr || !out || n < 0) return fail(DMT_ERR_INVALID, "bad args");
+  HIP_OK(hipSetDevice(device));
+  uint32_t *dc, *dout;
+  double* dn;
+  HIP_OK(dalloc(&dc, 4 * n));
+  HIP_OK(dalloc(&dout, 4 * n));
+  HIP_OK(dalloc(&dn, 2 * n));
+  HIP_OK(hipMemcpy(dc, ctr, n * 16, hipMemcpyHostToDevice));
+  HIP_OK(launch_debug_philox(seed, dc, n, dout, dn, nullptr));
+  HIP_OK(hipMemcpy(out, dout, n * 16, hipMemcpyDeviceToHost));
+  (void)hipFree(dc); (void)hipFree(dout); (void)hipFree(dn);
+  return DMT_OK;
+}
+
+dmt_status dmt_debug_normals(int32_t device, uint64_t seed, const uint32_t* ctr, int64_t n,
+                             double* out) {
+  if (!ctr || !out || n < 0) return fail(DMT_ERR_INVALID, "bad args");
+  HIP_OK(hipSetDevice(device));
+  uint32_t *dc, *dout;
+  double* dn;
+  HIP_OK(dalloc(&dc, 4 * n));
+  HIP_OK(dalloc(&dout, 4 * n));
+  HIP_OK(dalloc(&dn, 2 * n));
+  HIP_OK(hipMemcpy(dc, ctr, n * 16, hipMemcpyHostToDevice));
+  HIP_OK(launch_debug_philox(seed, dc, n, dout, dn, nullptr));
+  HIP_OK(hipMemcpy(out, dn, n * 16, hipMemcpyDeviceToHost));
+  (void)hipFree(dc); (void)hipFree(dout); (void)hipFree(dn);
+  return DMT_OK;
+}
+
+}  // extern "C"

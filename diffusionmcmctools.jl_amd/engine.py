@@ -1,0 +1,249 @@
+"""Thin object wrapper of one libdmt ensemble handle (reference-layout host arrays).
+
+Host arrays follow the reference's in-memory layout (include/dmt.h): a segment's path is
+``double[npts][d]`` (Julia ``Vector{SVector{d,Float64}}``) and segments are concatenated
+recording-major.  Every call goes straight to the HIP library.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib as L
+
+
+class Ensemble:
+    """Device containers of a SamplingEnsemble (u and u°) plus its block layouts."""
+
+    def __init__(self, model: int, d: int, m: int, n_points, precision: int = L.F64,
+                 seed: int = 0, device: int = 0, grid_shared: bool = False):
+        # n_points: list (per recording) of lists (per segment) of grid-point counts
+        self.model, self.d, self.m, self.precision = int(model), int(d), int(m), int(precision)
+        self.hp = self.d * (self.d + 1) // 2
+        self.nseg = np.array([len(r) for r in n_points], dtype=np.int32)
+        self.npts = np.array([int(n) for r in n_points for n in r], dtype=np.int32)
+        self.R = len(self.nseg)
+        self.G = len(self.npts)
+        self.rec_seg0 = np.concatenate([[0], np.cumsum(self.nseg)]).astype(np.int64)
+        self.pt_off = np.concatenate([[0], np.cumsum(self.npts)[:-1]]).astype(np.int64)
+        self.st_off = (self.pt_off - np.arange(self.G)).astype(np.int64)
+        self.P = int(self.npts.sum())
+        self.S = self.P - self.G
+        self.grid_shared = bool(grid_shared)
+        self.Q0 = int(self.npts[: self.nseg[0]].sum())
+        self._h = C.c_void_p()
+        mdl = L.dmt_model(self.model, self.precision, self.d, self.m)
+        st = L.dmt_structure(self.R, L.i32p(self.nseg), L.i32p(self.npts))
+        cfg = L.dmt_config(int(seed) & (2**64 - 1), int(device), 1 if grid_shared else 0)
+        L.call("dmt_create", C.byref(self._h), C.byref(mdl), C.byref(st), C.byref(cfg))
+
+    # ---------------------------------------------------------------- lifetime
+    def close(self):
+        if self._h:
+            L.lib.dmt_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    # ---------------------------------------------------------------- uploads
+    def upload_grid(self, t):
+        t = np.ascontiguousarray(t, dtype=np.float64)
+        want = self.Q0 if self.grid_shared else self.P
+        if t.size != want:
+            raise ValueError(f"grid needs {want} values, got {t.size}")
+        L.call("dmt_upload_grid", self._h, L.f64p(t))
+
+    def upload_law(self, unit, kind, H=None, F=None, laws=None, H_shared=False):
+        H = None if H is None else np.ascontiguousarray(H, dtype=np.float64)
+        F = None if F is None else np.ascontiguousarray(F, dtype=np.float64)
+        laws = None if laws is None else np.ascontiguousarray(laws, dtype=np.float64)
+        if H is not None:
+            want = (self.Q0 if H_shared else self.P) * self.hp
+            if H.size != want:
+                raise ValueError(f"H needs {want} values, got {H.size}")
+        if F is not None and F.size != self.P * self.d:
+            raise ValueError("F has the wrong size")
+        if laws is not None and laws.size != self.G * L.LAW_STRIDE:
+            raise ValueError("laws has the wrong size")
+        L.call("dmt_upload_law", self._h, unit, kind, L.f64p(H), 1 if H_shared else 0,
+               L.f64p(F), L.f64p(laws))
+
+    def set_paths(self, unit, X=None, W=None):
+        X = None if X is None else np.ascontiguousarray(X, dtype=np.float64)
+        W = None if W is None else np.ascontiguousarray(W, dtype=np.float64)
+        if X is not None and X.size != self.P * self.d:
+            raise ValueError("X has the wrong size")
+        if W is not None and W.size != self.P * self.m:
+            raise ValueError("W has the wrong size")
+        L.call("dmt_set_paths", self._h, unit, L.f64p(X), L.f64p(W))
+
+    def download_paths(self, unit, what):
+        C_ = self.d if what == 0 else self.m
+        out = np.empty((self.P, C_), dtype=np.float64)
+        L.call("dmt_download_paths", self._h, unit, what, L.f64p(out))
+        return out
+
+    def XX(self, unit=L.U):
+        return self.download_paths(unit, 0)
+
+    def WW(self, unit=L.U):
+        return self.download_paths(unit, 1)
+
+    # ---------------------------------------------------------------- hot path
+    def _Z(self, Z):
+        if Z is None:
+            return None
+        Z = np.ascontiguousarray(Z, dtype=np.float64)
+        if Z.size != self.S * self.m:
+            raise ValueError(f"Z needs {self.S * self.m} values (steps × m), got {Z.size}")
+        return Z
+
+    def draw_unit(self, unit, r0=0, r1=None, Z=None, iter=0, salt=0):
+        r1 = self.R if r1 is None else r1
+        ll = np.empty(r1 - r0, dtype=np.float64)
+        ok = np.empty(r1 - r0, dtype=np.uint8)
+        Z = self._Z(Z)
+        L.call("dmt_draw_unit", self._h, unit, r0, r1, L.f64p(Z), int(iter), int(salt),
+               L.f64p(ll), L.u8p(ok))
+        return ll, ok.astype(bool)
+
+    def create_layout(self, n_blocks, seg_first, seg_last, last, rho, hist_len=0):
+        nb = np.ascontiguousarray(n_blocks, dtype=np.int32)
+        sf = np.ascontiguousarray(seg_first, dtype=np.int32)
+        sl = np.ascontiguousarray(seg_last, dtype=np.int32)
+        lt = np.ascontiguousarray(last, dtype=np.uint8)
+        rh = np.ascontiguousarray(rho, dtype=np.float64)
+        lid = C.c_int32()
+        L.call("dmt_create_layout", self._h, L.i32p(nb), L.i32p(sf), L.i32p(sl), L.u8p(lt),
+               L.f64p(rh), int(hist_len), C.byref(lid))
+        return lid.value
+
+    def layout_size(self, layout):
+        n = C.c_int64()
+        L.call("dmt_layout_size", self._h, layout, C.byref(n))
+        return n.value
+
+    def draw_proposal(self, layout, b0, b1, Z=None, iter=0, salt=0, want_success=False):
+        ok = np.empty(b1 - b0, dtype=np.uint8) if want_success else None
+        Z = self._Z(Z)
+        L.call("dmt_draw_proposal", self._h, layout, b0, b1, L.f64p(Z), int(iter), int(salt),
+               L.u8p(ok))
+        return None if ok is None else ok.astype(bool)
+
+    def accept_reject(self, layout, b0, b1, mcmciter, E=None, salt=0, want_acc=False):
+        acc = np.empty(b1 - b0, dtype=np.uint8) if want_acc else None
+        if E is not None:
+            E = np.ascontiguousarray(E, dtype=np.float64)
+            if E.size != b1 - b0:
+                raise ValueError("E needs one value per block")
+        L.call("dmt_accept_reject", self._h, layout, b0, b1, L.f64p(E), int(mcmciter), int(salt),
+               L.u8p(acc))
+        return None if acc is None else acc.astype(bool)
+
+    def loglikhd(self, layout, unit, b0, b1):
+        L.call("dmt_loglikhd", self._h, layout, unit, b0, b1)
+
+    def recompute_path(self, layout, b0, b1, skip=0, want_success=False):
+        ok = np.empty(b1 - b0, dtype=np.uint8) if want_success else None
+        L.call("dmt_recompute_path", self._h, layout, b0, b1, int(skip), L.u8p(ok))
+        return None if ok is None else ok.astype(bool)
+
+    def swap(self, layout, what, b0, b1):
+        L.call("dmt_swap", self._h, layout, int(what), b0, b1)
+
+    def save_ll(self, layout, b0, b1, mcmciter):
+        L.call("dmt_save_ll", self._h, layout, b0, b1, int(mcmciter))
+
+    def set_accepted(self, layout, b0, b1, mcmciter, v):
+        v = np.ascontiguousarray(np.broadcast_to(np.asarray(v, dtype=np.uint8), (b1 - b0,)))
+        L.call("dmt_set_accepted", self._h, layout, b0, b1, int(mcmciter), L.u8p(v))
+
+    def get_block_state(self, layout, what, b0, b1, hist_len=None):
+        if what in (L.BLK_LL, L.BLK_LLPROP):
+            out = np.empty(b1 - b0, dtype=np.float64)
+        else:
+            if hist_len is None:
+                raise ValueError("hist_len needed for histories")
+            dt = np.uint8 if what == L.BLK_ACC_HIST else np.float64
+            out = np.empty((hist_len, b1 - b0), dtype=dt)
+        L.call("dmt_get_block_state", self._h, layout, what, b0, b1, out.ctypes.data_as(C.c_void_p))
+        return out
+
+    def set_block_state(self, layout, what, b0, b1, values):
+        dt = np.uint8 if what == L.BLK_ACC_HIST else np.float64
+        v = np.ascontiguousarray(values, dtype=dt)
+        L.call("dmt_set_block_state", self._h, layout, what, b0, b1, v.ctypes.data_as(C.c_void_p))
+
+    def fetch_ll(self, layout, b0, b1, mcmciter=0):
+        a, b, n = C.c_double(), C.c_double(), C.c_int64()
+        L.call("dmt_fetch_ll", self._h, layout, b0, b1, int(mcmciter), C.byref(a), C.byref(b),
+               C.byref(n))
+        return a.value, b.value, n.value
+
+    # ---------------------------------------------------------------- misc
+    def sync(self):
+        L.call("dmt_sync", self._h)
+
+    def set_timing(self, on=True):
+        L.call("dmt_set_timing", self._h, 1 if on else 0)
+
+    def get_timing(self, kernel):
+        ms, n = C.c_double(), C.c_int64()
+        L.call("dmt_get_timing", self._h, kernel, C.byref(ms), C.byref(n))
+        return ms.value, n.value
+
+    def memory_bytes(self):
+        n = C.c_int64()
+        L.call("dmt_memory_bytes", self._h, C.byref(n))
+        return n.value
+
+    def comm_init(self, nranks, rank, uid: bytes):
+        buf = (C.c_uint8 * 128).from_buffer_copy(uid)
+        L.call("dmt_comm_init", self._h, int(nranks), int(rank), buf)
+
+
+def comm_unique_id() -> bytes:
+    buf = (C.c_uint8 * 128)()
+    L.call("dmt_comm_unique_id", buf)
+    return bytes(buf)
+
+
+def guiding_linear(Bt, beta, at_packed, t, HT_packed, FT, cT):
+    """Exact discrete backward filter on one segment (host; dmt_guiding_linear)."""
+    d = len(beta)
+    hp = d * (d + 1) // 2
+    t = np.ascontiguousarray(t, dtype=np.float64)
+    n = t.size
+    H = np.empty((n, hp))
+    F = np.empty((n, d))
+    c = np.empty(n)
+    L.call("dmt_guiding_linear", d, L.f64p(np.ascontiguousarray(Bt, dtype=np.float64).ravel()),
+           L.f64p(np.ascontiguousarray(beta, dtype=np.float64)),
+           L.f64p(np.ascontiguousarray(at_packed, dtype=np.float64)), n, L.f64p(t),
+           L.f64p(np.ascontiguousarray(HT_packed, dtype=np.float64)),
+           L.f64p(np.ascontiguousarray(FT, dtype=np.float64)), float(cT), L.f64p(H), L.f64p(F),
+           L.f64p(c))
+    return H, F, c
+
+
+def debug_philox(seed, ctr, device=0):
+    ctr = np.ascontiguousarray(ctr, dtype=np.uint32).reshape(-1, 4)
+    out = np.empty_like(ctr)
+    L.call("dmt_debug_philox", device, int(seed), L.u32p(ctr), ctr.shape[0], L.u32p(out))
+    return out
+
+
+def debug_normals(seed, ctr, device=0):
+    ctr = np.ascontiguousarray(ctr, dtype=np.uint32).reshape(-1, 4)
+    out = np.empty((ctr.shape[0], 2), dtype=np.float64)
+    L.call("dmt_debug_normals", device, int(seed), L.u32p(ctr), ctr.shape[0], L.f64p(out))
+    return out

@@ -1,0 +1,276 @@
+"""Models, auxiliary laws, observations, time grids and guiding-term set-up (host side).
+
+These replace the set-up the reference delegates to its upstream packages
+(DiffusionDefinition `@load_diffusion`, ObservationSchemes recordings/time grids,
+GuidedProposals `build_guid_prop`; call sites /root/reference/src/sampling_unit.jl:55-74).
+They only build the *inputs* of the device hot path: law records (include/dmt.h) and the
+guiding-term tables H, F, c.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib as L
+from .engine import guiding_linear
+
+
+def packed(M):
+    """Row-major upper-triangular packing of a symmetric d×d matrix (00,01,..,11,..)."""
+    M = np.asarray(M, dtype=np.float64)
+    d = M.shape[0]
+    return np.array([M[a, b] for a in range(d) for b in range(a, d)])
+
+
+def unpacked(p, d):
+    M = np.zeros((d, d))
+    k = 0
+    for a in range(d):
+        for b in range(a, d):
+            M[a, b] = M[b, a] = p[k]
+            k += 1
+    return M
+
+
+# ------------------------------------------------------------------ models
+@dataclass
+class LinearAux:
+    """Auxiliary law dX = (Bt X + beta) dt + sigma_t dW (GuidedProposals' linear P̃)."""
+    Bt: np.ndarray
+    beta: np.ndarray
+    sigma_t: np.ndarray  # d×m
+
+    @property
+    def at(self):
+        s = np.asarray(self.sigma_t, dtype=np.float64)
+        return s @ s.T
+
+
+class Model:
+    kind: int
+    d: int
+    m: int
+
+    def theta_vec(self) -> np.ndarray:
+        raise NotImplementedError
+
+    def sigma(self) -> np.ndarray:
+        raise NotImplementedError
+
+    def drift(self, x):
+        raise NotImplementedError
+
+    def law_record(self, aux: LinearAux, c0: float = 0.0) -> np.ndarray:
+        rec = np.zeros(L.LAW_STRIDE)
+        th = self.theta_vec()
+        rec[L.LAW_THETA:L.LAW_THETA + len(th)] = th
+        sg = np.asarray(self.sigma(), dtype=np.float64).reshape(self.d, self.m)
+        rec[L.LAW_SIGMA:L.LAW_SIGMA + self.d * self.m] = sg.ravel()
+        a = sg @ sg.T
+        hp = self.d * (self.d + 1) // 2
+        rec[L.LAW_A:L.LAW_A + hp] = packed(a)
+        rec[L.LAW_BT:L.LAW_BT + self.d * self.d] = np.asarray(aux.Bt, dtype=np.float64).ravel()
+        rec[L.LAW_BETA:L.LAW_BETA + self.d] = np.asarray(aux.beta, dtype=np.float64)
+        da = a - aux.at
+        rec[L.LAW_DA:L.LAW_DA + hp] = packed(da)
+        rec[L.LAW_C0] = c0
+        rec[L.LAW_TRACE] = 1.0 if np.any(da != 0.0) else 0.0
+        return rec
+
+    def simulate(self, t, x0, rng, substeps=1):
+        """Plain Euler–Maruyama forward simulation on grid t (data generation)."""
+        t = np.asarray(t, dtype=np.float64)
+        x = np.array(x0, dtype=np.float64)
+        out = np.empty((t.size, self.d))
+        out[0] = x
+        sg = self.sigma()
+        for i in range(t.size - 1):
+            h = (t[i + 1] - t[i]) / substeps
+            for _ in range(substeps):
+                x = x + self.drift(x) * h + sg @ rng.standard_normal(self.m) * math.sqrt(h)
+            out[i + 1] = x
+        return out
+
+
+class OU(Model):
+    """dX = -Theta (X - mu) dt + sigma dW (DiffusionDefinition OU-type model)."""
+
+    kind = L.MODEL_OU
+
+    def __init__(self, Theta, mu, sigma):
+        self.Theta = np.atleast_2d(np.asarray(Theta, dtype=np.float64))
+        self.mu = np.atleast_1d(np.asarray(mu, dtype=np.float64))
+        self.sg = np.atleast_2d(np.asarray(sigma, dtype=np.float64))
+        self.d = self.Theta.shape[0]
+        self.m = self.sg.shape[1]
+
+    def theta_vec(self):
+        v = np.zeros(12)
+        v[: self.d * self.d] = self.Theta.ravel()
+        v[9:9 + self.d] = self.mu
+        return v
+
+    def sigma(self):
+        return self.sg
+
+    def drift(self, x):
+        return -self.Theta @ (np.asarray(x) - self.mu)
+
+    def aux(self, Theta_t=None, mu_t=None, sigma_t=None):
+        """OU auxiliary law (Theta_t, mu_t): Bt = -Theta_t, beta = Theta_t mu_t."""
+        Th = self.Theta if Theta_t is None else np.atleast_2d(np.asarray(Theta_t, dtype=np.float64))
+        mu = self.mu if mu_t is None else np.atleast_1d(np.asarray(mu_t, dtype=np.float64))
+        sg = self.sg if sigma_t is None else np.atleast_2d(np.asarray(sigma_t, dtype=np.float64))
+        return LinearAux(-Th, Th @ mu, sg)
+
+
+class FHN(Model):
+    """FitzHugh–Nagumo in DiffusionDefinition's parametrisation, θ = (ϵ, s, γ, β, σ)
+    (/root/reference/docs/src/tutorials/preamble.md:77):
+    dY = (Y - Y^3 - X + s)/ϵ dt,  dX = (γY - X + β) dt + σ dW."""
+
+    kind = L.MODEL_FHN
+    d, m = 2, 1
+
+    def __init__(self, eps, s, gamma, beta, sigma):
+        self.eps, self.s, self.gamma, self.beta, self.sg = map(float, (eps, s, gamma, beta, sigma))
+
+    def theta_vec(self):
+        return np.array([1.0 / self.eps, self.s, self.gamma, self.beta])
+
+    def sigma(self):
+        return np.array([[0.0], [self.sg]])
+
+    def drift(self, x):
+        y, v = x
+        return np.array([(y - y ** 3 - v + self.s) / self.eps, self.gamma * y - v + self.beta])
+
+    def aux(self, yT):
+        """FitzHughNagumoAux: linearisation at the observed end value yT."""
+        e = self.eps
+        Bt = np.array([[(1 - 3 * yT ** 2) / e, -1 / e], [self.gamma, -1.0]])
+        beta = np.array([(self.s + 2 * yT ** 3) / e, self.beta])
+        return LinearAux(Bt, beta, self.sigma())
+
+
+class Lorenz(Model):
+    """Lorenz-63 with diagonal noise: b = (s(y-x), x(r-z)-y, xy-βz)."""
+
+    kind = L.MODEL_LORENZ
+    d, m = 3, 3
+
+    def __init__(self, s=10.0, r=28.0, beta=8.0 / 3.0, sigma=(1.0, 1.0, 1.0)):
+        self.s_, self.r, self.b = float(s), float(r), float(beta)
+        self.sg = np.diag(np.asarray(sigma, dtype=np.float64))
+
+    def theta_vec(self):
+        return np.array([self.s_, self.r, self.b])
+
+    def sigma(self):
+        return self.sg
+
+    def drift(self, x):
+        x0, x1, x2 = x
+        return np.array([self.s_ * (x1 - x0), x0 * (self.r - x2) - x1, x0 * x1 - self.b * x2])
+
+    def aux(self, v):
+        """Linearisation of the drift at the point v."""
+        x0, x1, x2 = v
+        J = np.array([[-self.s_, self.s_, 0.0], [self.r - x2, -1.0, -x0], [x1, x0, -self.b]])
+        beta = self.drift(v) - J @ np.asarray(v)
+        return LinearAux(J, beta, self.sg)
+
+
+# ------------------------------------------------------------------ observations, grids
+@dataclass
+class Observation:
+    """v ~ N(L x(t), Sigma) (ObservationSchemes LinearGsnObs)."""
+    t: float
+    v: np.ndarray
+    L: np.ndarray
+    Sigma: np.ndarray
+
+    def info(self):
+        """Terminal information (H, F, c) contributed by this observation."""
+        Lm = np.atleast_2d(np.asarray(self.L, dtype=np.float64))
+        S = np.atleast_2d(np.asarray(self.Sigma, dtype=np.float64))
+        v = np.atleast_1d(np.asarray(self.v, dtype=np.float64))
+        Si = np.linalg.inv(S)
+        k = v.size
+        H = Lm.T @ Si @ Lm
+        F = Lm.T @ Si @ v
+        c = 0.5 * v @ Si @ v + 0.5 * k * math.log(2 * math.pi) + 0.5 * math.log(np.linalg.det(S))
+        return H, F, c
+
+
+@dataclass
+class Recording:
+    """(P, obs, t0, x0) of ObservationSchemes (docs/src/get_started/overview.md:18-20);
+    KnownStartingPt x0."""
+    obs: list
+    t0: float
+    x0: np.ndarray
+    extra: dict = field(default_factory=dict)
+
+
+def standard_guid_prop_time_transf(t0, T, dt):
+    """Uniform grid t0:dt:T mapped by τ(t) = t0 + (t-t0)(2 - (t-t0)/(T-t0))
+    (GuidedProposals' standard time change, named at biblock/smoothing.md:27)."""
+    n = max(int(round((T - t0) / dt)), 1)
+    u = np.linspace(t0, T, n + 1)
+    s = u - t0
+    tau = t0 + s * (2.0 - s / (T - t0))
+    tau[0], tau[-1] = t0, T
+    return tau
+
+
+def setup_time_grids(recording: Recording, dt: float, transf=standard_guid_prop_time_transf):
+    """One grid per inter-observation interval (OBS.setup_time_grids)."""
+    grids, t0 = [], recording.t0
+    for ob in recording.obs:
+        grids.append(transf(t0, ob.t, dt))
+        t0 = ob.t
+    return grids
+
+
+def uniform_grid(t0, T, n):
+    return np.linspace(t0, T, n + 1)
+
+
+# ------------------------------------------------------------------ guiding terms
+def guiding_chain(auxes, grids, infos, H_in=None):
+    """Backward filter over the consecutive segments of one recording.
+
+    auxes[k]: LinearAux on segment k; grids[k]: its grid; infos[k]: (H, F, c) of the
+    observation(s) at the end of segment k.  Segment k's terminal condition is its own
+    observation information plus the guiding term of segment k+1 at its start
+    (GP.build_guid_prop / recompute_guiding_term!).  Returns per segment (H packed, F, c).
+    """
+    K = len(grids)
+    out = [None] * K
+    nxt = None
+    for k in range(K - 1, -1, -1):
+        d = len(auxes[k].beta)
+        HT, FT, cT = infos[k]
+        HT = np.array(HT, dtype=np.float64).reshape(d, d)
+        FT = np.array(FT, dtype=np.float64).reshape(d)
+        if nxt is not None:
+            Hn, Fn, cn = nxt
+            HT = HT + unpacked(Hn, d)
+            FT = FT + Fn
+            cT = cT + cn
+        H, F, c = guiding_linear(auxes[k].Bt, auxes[k].beta, packed(auxes[k].at), grids[k],
+                                 packed(HT), FT, cT)
+        out[k] = (H, F, c)
+        nxt = (H[0], F[0], c[0])
+    return out
+
+
+def artificial_obs_info(v, noise):
+    """Exact full-state artificial observation used by blocking laws
+    (guid_prop_for_blocking(…, artificial_noise = 1e-11), src/sampling_unit.jl:57,61-66)."""
+    v = np.asarray(v, dtype=np.float64)
+    d = v.size
+    return Observation(0.0, v, np.eye(d), noise * np.eye(d)).info()

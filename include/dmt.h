@@ -1,0 +1,249 @@
+/*
+ * dmt.h — C-ABI of libdmt, the MI355X-native guided-bridge imputation engine.
+ *
+ * This is the drop-in boundary for the hot path of DiffusionMCMCTools.jl
+ * (the reference).  The reference's API is Julia multiple dispatch on
+ * SamplingUnit / SamplingPair / BiBlock / BlockCollection / BlockEnsemble
+ * (exports at /root/reference/src/DiffusionMCMCTools.jl:28-60).  A Julia shim
+ * (diffusionmcmctools.jl_amd/julia/DiffusionMCMCToolsAMD.jl, see
+ * INTEGRATION.md) keeps those method names and `ccall`s the entry points below
+ * ONCE PER ENSEMBLE OPERATION: a BiBlock is a 1-block range of a layout, a
+ * BlockCollection the blocks of one recording, a BlockEnsemble all blocks.
+ *
+ * Conventions (mirroring the reference):
+ *  - every call returns dmt_status (0 = OK); numerical failure is NOT an
+ *    error: it is reported per block as success=0 and ll = -Inf, exactly as
+ *    upstream GP.rand!/solve_and_ll! return (false, -Inf)
+ *    (src/biblock.jl:81-86, src/block.jl:162-169,180-181);
+ *  - host pointers are borrowed for the duration of the call only;
+ *  - host array layout = the reference's in-memory layout: a segment's path
+ *    is Julia Vector{SVector{d,Float64}} == C double[npts][d]; segments are
+ *    concatenated recording-major (recording 0 seg 0, seg 1, …, recording 1 …);
+ *    Julia Bool == uint8_t, Int == int64_t;
+ *  - "mcmciter" is the reference's 1-based MCMC iteration index;
+ *  - a handle is not re-entrant; calls are ordered on the handle's HIP
+ *    stream; only fetch/download/sync calls block the host;
+ *  - dmt_last_error() returns a thread-local message for the last failure.
+ *
+ * fp32 ensembles (DMT_F32) still take double host buffers; values are
+ * rounded to float on upload.
+ */
+#ifndef DMT_H
+#define DMT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int32_t dmt_status;
+typedef struct dmt_ens dmt_ens;
+
+enum {
+    DMT_OK = 0,
+    DMT_ERR_INVALID = 1, /* bad argument / shape */
+    DMT_ERR_HIP = 2,     /* HIP runtime failure (no device, launch failure) */
+    DMT_ERR_OOM = 3,
+    DMT_ERR_STATE = 4,   /* call not valid in the current state (e.g. law not uploaded) */
+    DMT_ERR_COMM = 5     /* RCCL failure */
+};
+
+/* models (DiffusionDefinition.jl models used by the reference's tutorials and configs) */
+enum { DMT_MODEL_OU = 0, DMT_MODEL_FHN = 1, DMT_MODEL_LORENZ = 2 };
+enum { DMT_F64 = 0, DMT_F32 = 1 };
+/* units of a SamplingPair: u (accepted) and u° (proposal), src/sampling_pair.jl:36-55 */
+enum { DMT_U = 0, DMT_UPROP = 1 };
+/* law kinds of a SamplingUnit: PP (regular) and PPb (blocking), src/sampling_unit.jl:48-53 */
+enum { DMT_LAW_PP = 0, DMT_LAW_PPB = 1 };
+/* swap masks, src/biblock.jl:148-209 */
+enum { DMT_SWAP_XX = 1, DMT_SWAP_WW = 2, DMT_SWAP_PP = 4, DMT_SWAP_LL = 8 };
+/* per-block state arrays, src/block.jl:57-58, src/biblock.jl:233-234 */
+enum {
+    DMT_BLK_LL = 0,        /* b.ll            double[nblocks] */
+    DMT_BLK_LLPROP = 1,    /* b°.ll           double[nblocks] */
+    DMT_BLK_LL_HIST = 2,   /* b.ll_history    double[hist_len][nblocks] (iteration-major) */
+    DMT_BLK_LLPROP_HIST = 3,
+    DMT_BLK_ACC_HIST = 4   /* accpt_history   uint8[hist_len][nblocks] */
+};
+/* kernels whose device time can be queried (dmt_get_timing) */
+enum { DMT_K_DRAW = 0, DMT_K_ACCEPT = 1, DMT_K_PATHLL = 2, DMT_K_RECOMPUTE = 3,
+       DMT_K_REDUCE = 4, DMT_K_COUNT = 5 };
+
+/*
+ * Law record: one per segment per (unit, kind), DMT_LAW_STRIDE doubles.
+ * It carries the target-law parameters θ and the auxiliary (linear) law used
+ * by the Girsanov weight.  Offsets:
+ *   [0,16)  theta  model parameters
+ *             OU:     Theta (d×d row-major) at 0, mu at 9
+ *             FHN:    1/eps, s, gamma, beta      (σ goes in sigma)
+ *             Lorenz: s, r, beta
+ *   [16,25) sigma  d×m row-major (constant diffusion coefficient)
+ *   [25,31) a      packed upper-triangular σσᵀ (row-major upper: 00,01,(02),11,(12),22)
+ *   [31,40) Bt     auxiliary drift matrix B̃ (d×d row-major)
+ *   [40,43) beta   auxiliary drift offset β̃
+ *   [43,49) da     packed a − ã (used only when trace != 0)
+ *   49      c0     c(t0) of the segment's guiding term (for loglikhd_obs)
+ *   50      trace  1.0 if a ≠ ã (adds −½ tr[(a−ã)(H−rrᵀ)] to G)
+ */
+#define DMT_LAW_STRIDE 64
+#define DMT_LAW_THETA 0
+#define DMT_LAW_SIGMA 16
+#define DMT_LAW_A 25
+#define DMT_LAW_BT 31
+#define DMT_LAW_BETA 40
+#define DMT_LAW_DA 43
+#define DMT_LAW_C0 49
+#define DMT_LAW_TRACE 50
+
+typedef struct {
+    int32_t model;      /* DMT_MODEL_* */
+    int32_t precision;  /* DMT_F64 / DMT_F32 */
+    int32_t d;          /* state dimension (OU: 1..3, FHN: 2, Lorenz: 3) */
+    int32_t m;          /* noise dimension (OU: 1..3, FHN: 1, Lorenz: 3) */
+} dmt_model;
+
+typedef struct {
+    int64_t n_recordings;        /* R */
+    const int32_t* n_segments;   /* [R] segments per recording (= number of observations) */
+    const int32_t* n_points;     /* [G] grid points per segment (N_g + 1), recording-major */
+} dmt_structure;
+
+typedef struct {
+    uint64_t seed;               /* key of the device Philox4x32-10 streams (perf mode) */
+    int32_t device;              /* HIP device ordinal */
+    int32_t grid_shared;         /* 1: every recording has the same segment structure and time grid;
+                                    dmt_upload_grid then takes ONE recording's grid */
+} dmt_config;
+
+/* ---------------- lifetime (SamplingEnsemble / SamplingPair containers) ---------------- */
+
+/* Allocates the device containers of a SamplingEnsemble (src/sampling_ensemble.jl:17-41):
+ * paths XX/WW of u and u° (src/sampling_unit.jl:48-53, src/sampling_pair.jl:51). */
+dmt_status dmt_create(dmt_ens** h, const dmt_model* model, const dmt_structure* st,
+                      const dmt_config* cfg);
+dmt_status dmt_destroy(dmt_ens* h);
+
+/* Time grids tts (ObservationSchemes setup_time_grids, src/sampling_unit.jl:55): t[P] or,
+ * with grid_shared, t[points of recording 0]. */
+dmt_status dmt_upload_grid(dmt_ens* h, const double* t);
+
+/* Guiding-term tables of the laws u.PP/u°.PP (kind PP) or u.PPb/u°.PPb (kind PPB),
+ * built upstream by build_guid_prop / guid_prop_for_blocking (src/sampling_unit.jl:60-66)
+ * and recompute_guiding_term! (src/block.jl:102-110).
+ *   H[P][d(d+1)/2] packed (or, with H_shared, H[points of recording 0][…] shared by all),
+ *   F[P][d], laws[G][DMT_LAW_STRIDE].  Any of H/F/laws may be NULL to keep the previous one. */
+dmt_status dmt_upload_law(dmt_ens* h, int32_t unit, int32_t kind, const double* H,
+                          int32_t H_shared, const double* F, const double* laws);
+
+/* Paths of unit u / u°: X[P][d], W[P][m]; NULL keeps the current one.  Used by
+ * init_paths! (src/sampling_unit.jl:83-87) and find_W_for_X! (src/block.jl:118-131). */
+dmt_status dmt_set_paths(dmt_ens* h, int32_t unit, const double* X, const double* W);
+
+/* Download XX (what=0) / WW (what=1) of a unit, resolving all swaps, reference layout. */
+dmt_status dmt_download_paths(dmt_ens* h, int32_t unit, int32_t what, double* out);
+
+/* draw_proposal_path!(u::SamplingUnit) (src/sampling_unit.jl:118-120): rand! with no pCN
+ * (ρ = 0) under u.PP, in place, for recordings [r0, r1).  Z: [steps][m] for all segments
+ * in reference order (NULL → device Philox stream keyed by (seed, iter, salt)).
+ * ll_out (nullable, double[r1-r0]) / success_out (nullable). */
+dmt_status dmt_draw_unit(dmt_ens* h, int32_t unit, int64_t r0, int64_t r1, const double* Z,
+                         int64_t iter, uint32_t salt, double* ll_out, uint8_t* success_out);
+
+/* ---------------- block layouts (BiBlock / BlockCollection / BlockEnsemble views) ---------------- */
+
+/* Registers one layout of blocks over the ensemble (src/block_ensemble.jl:20-33,
+ * src/block_collection.jl:20-30, src/biblock.jl:49-62).  Blocks are listed
+ * recording-major; block i covers segments [seg_first[i], seg_last[i]] (0-based, local to
+ * its recording) with terminal flag last[i] (the L type parameter), pCN memory rho[i].
+ * hist_len = ll_hist_len (0 = no histories).  Non-terminal blocks need ≥ 2 segments
+ * (the reference indexes PP[1] of the block, src/block.jl:66,178). */
+dmt_status dmt_create_layout(dmt_ens* h, const int32_t* n_blocks /*[R]*/,
+                             const int32_t* seg_first, const int32_t* seg_last,
+                             const uint8_t* last, const double* rho, int64_t hist_len,
+                             int32_t* layout_id);
+dmt_status dmt_layout_size(dmt_ens* h, int32_t layout, int64_t* n_blocks);
+
+/* draw_proposal_path! for blocks [b0, b1) of a layout (src/biblock.jl:78-106,
+ * src/block_collection.jl:46, src/block_ensemble.jl:50).  pCN under the accepted law
+ * b.PP (+ b.P_last), proposal written to u°; ll° stored in the layout.
+ * Z: [steps][m] for all segments (parity mode) or NULL (device Philox, keyed by
+ * (seed, iter, salt, segment, step)).  success_out: uint8[b1-b0], nullable. */
+dmt_status dmt_draw_proposal(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
+                             const double* Z, int64_t iter, uint32_t salt,
+                             uint8_t* success_out);
+
+/* accept_reject_proposal_path!(·, mcmciter) (src/biblock.jl:121-127): E > -(ll° - ll),
+ * swap XX/WW, set_accepted!, save_ll! (both), swap ll.  E: double[b1-b0] (parity) or NULL
+ * (device Exp(1) stream keyed by (seed, mcmciter, salt, block)).  acc_out nullable. */
+dmt_status dmt_accept_reject(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
+                             const double* E, int64_t mcmciter, uint32_t salt,
+                             uint8_t* acc_out);
+
+/* loglikhd!(b) / loglikhd°!(b) (src/block.jl:138-152, src/biblock.jl:240,248). */
+dmt_status dmt_loglikhd(dmt_ens* h, int32_t layout, int32_t unit, int64_t b0, int64_t b1);
+
+/* recompute_path!(b°, b.WW; skip) (src/block.jl:159-187) as called by set_proposal_law!
+ * (src/biblock.jl:343): re-solve u° under u°.PP with the accepted Wiener paths. */
+dmt_status dmt_recompute_path(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
+                              int32_t skip, uint8_t* success_out);
+
+/* swap_XX!/swap_WW!/swap_PP!/swap_ll! (src/biblock.jl:148-209), what = DMT_SWAP_* mask. */
+dmt_status dmt_swap(dmt_ens* h, int32_t layout, int32_t what, int64_t b0, int64_t b1);
+
+/* save_ll!(·, i) (src/biblock.jl:256-259) and set_accepted!(·, i, v) (src/biblock.jl:135). */
+dmt_status dmt_save_ll(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int64_t mcmciter);
+dmt_status dmt_set_accepted(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
+                            int64_t mcmciter, const uint8_t* v);
+
+/* Read / write per-block state (DMT_BLK_*), out/in sized for blocks [b0, b1)
+ * (histories: [hist_len][b1-b0]). */
+dmt_status dmt_get_block_state(dmt_ens* h, int32_t layout, int32_t what, int64_t b0,
+                               int64_t b1, void* out);
+dmt_status dmt_set_block_state(dmt_ens* h, int32_t layout, int32_t what, int64_t b0,
+                               int64_t b1, const void* in);
+
+/* fetch_ll / fetch_ll° (src/block_collection.jl:144,156, src/block_ensemble.jl:140,152)
+ * over blocks [b0, b1), with the accepted count of iteration mcmciter (0 = skip).
+ * Deterministic: a fixed binary tree over the blocks.  With a communicator
+ * (dmt_comm_init) the three partials are combined over ranks with RCCL
+ * (all-gather + fixed rank-order tree, so the sum does not depend on the rank count
+ * when every rank holds a power-of-two number of blocks). */
+dmt_status dmt_fetch_ll(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
+                        int64_t mcmciter, double* ll, double* ll_prop, int64_t* n_acc);
+
+/* ---------------- guiding term (host set-up, GP.build_guid_prop) ---------------- */
+
+/* Exact discrete backward filter for a linear auxiliary law dX = (B̃X + β̃)dt + σ̃dW on
+ * one segment's grid t[npts] with terminal information (H_T, F_T, c_T):
+ * writes H[npts][d(d+1)/2], F[npts][d], c[npts].  at = packed σ̃σ̃ᵀ.
+ * Host-only (no device needed). */
+dmt_status dmt_guiding_linear(int32_t d, const double* Bt, const double* beta,
+                              const double* at, int32_t npts, const double* t,
+                              const double* HT, const double* FT, double cT,
+                              double* H, double* F, double* c);
+
+/* ---------------- multi-GPU (RCCL over xGMI) ---------------- */
+dmt_status dmt_comm_unique_id(uint8_t* id_out /*128 bytes*/);
+dmt_status dmt_comm_init(dmt_ens* h, int32_t nranks, int32_t rank, const uint8_t* id);
+
+/* ---------------- misc ---------------- */
+dmt_status dmt_sync(dmt_ens* h);
+dmt_status dmt_set_timing(dmt_ens* h, int32_t on);
+/* accumulated device time (ms) and launch count of a kernel since timing was switched on */
+dmt_status dmt_get_timing(dmt_ens* h, int32_t kernel, double* ms, int64_t* count);
+/* bytes of device memory held by the handle */
+dmt_status dmt_memory_bytes(dmt_ens* h, int64_t* bytes);
+/* Debug: raw Philox4x32-10 blocks computed on the device for n counters (ctr[n][4]). */
+dmt_status dmt_debug_philox(int32_t device, uint64_t seed, const uint32_t* ctr, int64_t n,
+                            uint32_t* out);
+/* Debug: device normal pairs (double) for n counters. */
+dmt_status dmt_debug_normals(int32_t device, uint64_t seed, const uint32_t* ctr, int64_t n,
+                             double* out);
+const char* dmt_last_error(void);
+const char* dmt_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DMT_H */

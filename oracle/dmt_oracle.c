@@ -1,0 +1,406 @@
+/*
+ * dmt_oracle.c — CPU restatement of the guided-bridge imputation hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product (libdmt, the Python host
+ * mirror, the Julia shim) links, loads or calls this file.  It is imported only
+ * by tests/, __graft_entry__.smoke() and the cpu_baseline leg of bench.py, as
+ * the checker and as the timed CPU baseline ("kind": "port").
+ *
+ * Parity status: the reference (DiffusionMCMCTools.jl) is pure Julia and its
+ * arithmetic lives in GuidedProposals.jl v0.1.0 (git-tree 65cd150e…) and
+ * DiffusionDefinition.jl v0.1.0 (git-tree 0ed61dbd…), pinned at
+ * /root/reference/Manifest.toml:131-135,200-206 and NOT vendored; no julia
+ * binary exists and the reference's own tests are empty
+ * (/root/reference/test/runtests.jl:4-6).  This restatement is therefore
+ * "parity unpinned" against reference outputs; it is pinned instead by the
+ * analytic known-answer tests in tests/test_oracle_kat.py and by an
+ * independent numpy restatement (oracle/np_oracle.py).
+ *
+ * What it restates (reference file:line → here):
+ *   GP.rand!(PP, X°, W°, W, ρ, Val(:ll), y1)   src/biblock.jl:94-106       orc_pcn_segment + orc_solve_segment
+ *   GP.solve_and_ll!(X, W, P, y1)              src/block.jl:165-167,180    orc_solve_segment
+ *   GP.loglikhd(P, X)                          src/block.jl:138-144        orc_path_ll_segment
+ *   GP.loglikhd_obs(P, y1)                     src/block.jl:178            orc_obs_term
+ *   rand(Exponential(1.0))                     src/biblock.jl:122          orc_exp1 (perf-mode stream)
+ *   randn inside rand!                         (upstream)                  orc_normal_pair (perf-mode stream)
+ *
+ * CANONICAL ARITHMETIC (the build's definition of one Euler step; the HIP
+ * kernels follow it operation for operation, so that paths and log-weights
+ * agree bit for bit under -ffp-contract=off with explicit fma):
+ *
+ *   dt      = t[i+1] - t[i]
+ *   dW_k    = W[i+1][k] - W[i][k]
+ *   r_a     = F_a ; r_a = fma(-H_ab, x_b, r_a)        for b = 0..d-1
+ *   b       = model drift (see orc_drift)
+ *   ar_a    = a_a0*r_0 ; ar_a = fma(a_ab, r_b, ar_a) for b = 1..d-1
+ *   bg_a    = b_a + ar_a
+ *   bt_a    = Bt_a-row · x + beta_a  (bt_a = beta_a ; fma(Bt_ab, x_b, bt_a))
+ *   db_a    = b_a - bt_a
+ *   G       = db_0*r_0 ; G = fma(db_a, r_a, G)
+ *   [trace] tr = Σ_a Σ_b da_ab*(H_ab - r_a r_b)  (tmp = fma(-r_a, r_b, H_ab);
+ *            first term tr = da_00*tmp, then tr = fma(da_ab, tmp, tr)); G = fma(-0.5, tr, G)
+ *   g       = G*dt           -> fed to the chunked pairwise sum
+ *   x'_a    = fma(bg_a, dt, x_a) ; x'_a = fma(sigma_ak, dW_k, x'_a)  for k = 0..m-1
+ *
+ *   Log-weight summation: within a segment the g's are summed in chunks of 64
+ *   consecutive steps by the adjacent-pair binary tree ((g0+g1)+(g2+g3))+…
+ *   (a partial last chunk is padded with zeros), each chunk sum is
+ *   canonicalised with "+ 0.0" and chunk sums are added left to right
+ *   starting from 0.  Block ll = obs term, then += each segment's sum.
+ *
+ *   pCN (cumulative form, A.4 of SURVEY.md):  wf_0 = 0;
+ *   wf_{q+1} = fma(sqrt(t[q+1]-t[q]), Z_q, wf_q);  W°_q = fma(rho, W_q, srho*wf_q)
+ *   with srho = sqrt(1 - rho*rho) computed in double by the host.
+ *
+ * Compiled twice: REAL=double (suffix _f64) and REAL=float (suffix _f32).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#ifndef REAL
+#define REAL double
+#define SFX(n) n##_f64
+#define FMA fma
+#define SQRT sqrt
+#define IS_F64 1
+#endif
+
+#define LAW_STRIDE 64
+#define L_THETA 0
+#define L_SIGMA 16
+#define L_A 25
+#define L_BT 31
+#define L_BETA 40
+#define L_DA 43
+#define L_C0 49
+#define L_TRACE 50
+
+enum { ORC_OU = 0, ORC_FHN = 1, ORC_LORENZ = 2 };
+
+/* packed upper-triangular index of a symmetric d×d matrix */
+static inline int pidx(int d, int a, int b) {
+    if (a > b) { int t = a; a = b; b = t; }
+    return a * d - (a * (a - 1)) / 2 + (b - a);
+}
+
+/* Model drifts (DiffusionDefinition models). */
+static void orc_drift(int model, int d, const REAL* th, const REAL* x, REAL* b) {
+    if (model == ORC_OU) {
+        /* theta: Theta (d×d row-major, 0..8), mu (9..11); b = -Theta (x - mu) */
+        REAL y[3];
+        for (int q = 0; q < d; ++q) y[q] = x[q] - th[9 + q];
+        for (int a = 0; a < d; ++a) {
+            REAL acc = (-th[a * d + 0]) * y[0];
+            for (int q = 1; q < d; ++q) acc = FMA(-th[a * d + q], y[q], acc);
+            b[a] = acc;
+        }
+    } else if (model == ORC_FHN) {
+        /* theta: 1/eps, s, gamma, beta.  dY = (Y - Y^3 - X + s)/eps, dX = (gamma Y - X + beta) */
+        REAL y = x[0], v = x[1];
+        REAL y3 = (y * y) * y;
+        REAL t0 = ((y - y3) - v) + th[1];
+        b[0] = t0 * th[0];
+        b[1] = FMA(th[2], y, th[3] - v);
+    } else { /* Lorenz-63: theta: s, r, beta */
+        b[0] = th[0] * (x[1] - x[0]);
+        b[1] = FMA(x[0], th[1] - x[2], -x[1]);
+        b[2] = FMA(x[0], x[1], -(th[2] * x[2]));
+    }
+}
+
+typedef struct { REAL s[7]; int n; REAL acc; } psum_t;
+
+static inline void ps_init(psum_t* p) { p->n = 0; p->acc = (REAL)0; }
+static inline void ps_add(psum_t* p, REAL v) {
+    int k = p->n, lvl = 0;
+    while (k & 1) { v = p->s[lvl] + v; k >>= 1; ++lvl; }
+    p->s[lvl] = v;
+    if (++p->n == 64) { p->acc = p->acc + (p->s[6] + (REAL)0); p->n = 0; }
+}
+static inline REAL ps_finish(psum_t* p) {
+    if (p->n > 0) {
+        int have = 0; REAL r = (REAL)0;
+        for (int lvl = 0; lvl < 6; ++lvl)
+            if ((p->n >> lvl) & 1) { r = have ? (p->s[lvl] + r) : p->s[lvl]; have = 1; }
+        p->acc = p->acc + (r + (REAL)0);
+        p->n = 0;
+    }
+    return p->acc;
+}
+
+static void load_law(const double* law, int d, int m, REAL* th, REAL* sg, REAL* a,
+                     REAL* Bt, REAL* beta, REAL* da, int* trace) {
+    for (int i = 0; i < 16; ++i) th[i] = (REAL)law[L_THETA + i];
+    for (int i = 0; i < 9; ++i) sg[i] = (REAL)law[L_SIGMA + i];
+    for (int i = 0; i < 6; ++i) a[i] = (REAL)law[L_A + i];
+    for (int i = 0; i < 9; ++i) Bt[i] = (REAL)law[L_BT + i];
+    for (int i = 0; i < 3; ++i) beta[i] = (REAL)law[L_BETA + i];
+    for (int i = 0; i < 6; ++i) da[i] = (REAL)law[L_DA + i];
+    *trace = law[L_TRACE] != 0.0;
+    (void)d; (void)m;
+}
+
+/* G(t_i, x) at a point (canonical), writes r and b for the caller. */
+static inline REAL g_at(int model, int d, const REAL* th, const REAL* a, const REAL* Bt,
+                        const REAL* beta, const REAL* da, int trace,
+                        const REAL* H, const REAL* F, const REAL* x, REAL* r, REAL* b) {
+    for (int p = 0; p < d; ++p) {
+        REAL acc = F[p];
+        for (int q = 0; q < d; ++q) acc = FMA(-H[pidx(d, p, q)], x[q], acc);
+        r[p] = acc;
+    }
+    orc_drift(model, d, th, x, b);
+    REAL db[3];
+    for (int p = 0; p < d; ++p) {
+        REAL bt = beta[p];
+        for (int q = 0; q < d; ++q) bt = FMA(Bt[p * d + q], x[q], bt);
+        db[p] = b[p] - bt;
+    }
+    REAL G = db[0] * r[0];
+    for (int p = 1; p < d; ++p) G = FMA(db[p], r[p], G);
+    if (trace) {
+        REAL tr = (REAL)0; int first = 1;
+        for (int p = 0; p < d; ++p)
+            for (int q = 0; q < d; ++q) {
+                REAL tmp = FMA(-r[p], r[q], H[pidx(d, p, q)]);
+                REAL w = da[pidx(d, p, q)];
+                tr = first ? (w * tmp) : FMA(w, tmp, tr);
+                first = 0;
+            }
+        G = FMA((REAL)-0.5, tr, G);
+    }
+    (void)a;
+    return G;
+}
+
+/* GP.solve_and_ll!(X, W, P, y1): Euler–Maruyama guided solve with given W and
+ * the Girsanov sum.  Returns 1 on success (finite end point and ll). */
+int SFX(orc_solve_segment)(int model, int d, int m, const double* law, int npts,
+                           const REAL* t, const REAL* H, const REAL* F, const REAL* W,
+                           const REAL* y1, REAL* X, REAL* ll_out) {
+    int h = d * (d + 1) / 2;
+    REAL th[16], sg[9], a[6], Bt[9], beta[3], da[6]; int trace;
+    load_law(law, d, m, th, sg, a, Bt, beta, da, &trace);
+    REAL x[3];
+    for (int p = 0; p < d; ++p) { x[p] = y1[p]; X[p] = x[p]; }
+    psum_t ps; ps_init(&ps);
+    for (int i = 0; i < npts - 1; ++i) {
+        REAL dt = t[i + 1] - t[i];
+        REAL dW[3];
+        for (int k = 0; k < m; ++k) dW[k] = W[(i + 1) * m + k] - W[i * m + k];
+        const REAL* Hi = H + (size_t)i * h;
+        const REAL* Fi = F + (size_t)i * d;
+        REAL r[3], b[3];
+        REAL G = g_at(model, d, th, a, Bt, beta, da, trace, Hi, Fi, x, r, b);
+        ps_add(&ps, G * dt);
+        REAL ar[3];
+        for (int p = 0; p < d; ++p) {
+            REAL acc = a[pidx(d, p, 0)] * r[0];
+            for (int q = 1; q < d; ++q) acc = FMA(a[pidx(d, p, q)], r[q], acc);
+            ar[p] = acc;
+        }
+        REAL xn[3];
+        for (int p = 0; p < d; ++p) {
+            REAL bg = b[p] + ar[p];
+            REAL v = FMA(bg, dt, x[p]);
+            for (int k = 0; k < m; ++k) v = FMA(sg[p * m + k], dW[k], v);
+            xn[p] = v;
+        }
+        for (int p = 0; p < d; ++p) { x[p] = xn[p]; X[(size_t)(i + 1) * d + p] = xn[p]; }
+    }
+    REAL ll = ps_finish(&ps);
+    *ll_out = ll;
+    int ok = isfinite(ll) ? 1 : 0;
+    for (int p = 0; p < d; ++p) ok &= isfinite(x[p]) ? 1 : 0;
+    return ok;
+}
+
+/* GP.loglikhd(P, X): Girsanov sum on a stored path (no state update). */
+REAL SFX(orc_path_ll_segment)(int model, int d, int m, const double* law, int npts,
+                              const REAL* t, const REAL* H, const REAL* F, const REAL* X) {
+    int h = d * (d + 1) / 2;
+    REAL th[16], sg[9], a[6], Bt[9], beta[3], da[6]; int trace;
+    load_law(law, d, m, th, sg, a, Bt, beta, da, &trace);
+    psum_t ps; ps_init(&ps);
+    for (int i = 0; i < npts - 1; ++i) {
+        REAL dt = t[i + 1] - t[i];
+        REAL r[3], b[3];
+        REAL G = g_at(model, d, th, a, Bt, beta, da, trace, H + (size_t)i * h,
+                      F + (size_t)i * d, X + (size_t)i * d, r, b);
+        ps_add(&ps, G * dt);
+    }
+    return ps_finish(&ps);
+}
+
+/* GP.loglikhd_obs(P, y1) = log rho~(t0, y1) = -c0 - 1/2 y'H y + F'y */
+REAL SFX(orc_obs_term)(int d, const double* law, const REAL* H0, const REAL* F0, const REAL* x) {
+    REAL Hx[3];
+    for (int p = 0; p < d; ++p) {
+        REAL acc = H0[pidx(d, p, 0)] * x[0];
+        for (int q = 1; q < d; ++q) acc = FMA(H0[pidx(d, p, q)], x[q], acc);
+        Hx[p] = acc;
+    }
+    REAL quad = x[0] * Hx[0];
+    for (int p = 1; p < d; ++p) quad = FMA(x[p], Hx[p], quad);
+    REAL lin = F0[0] * x[0];
+    for (int p = 1; p < d; ++p) lin = FMA(F0[p], x[p], lin);
+    REAL tmp = FMA((REAL)-0.5, quad, lin);
+    return tmp - (REAL)law[L_C0];
+}
+
+/* pCN mix of one segment (cumulative form). */
+void SFX(orc_pcn_segment)(int m, int npts, const REAL* t, const REAL* W, const REAL* Z,
+                          REAL rho, REAL srho, REAL* Wo) {
+    REAL wf[3] = {0, 0, 0};
+    for (int k = 0; k < m; ++k) Wo[k] = FMA(rho, W[k], srho * wf[k]);
+    for (int q = 0; q < npts - 1; ++q) {
+        REAL sdt = SQRT(t[q + 1] - t[q]);
+        for (int k = 0; k < m; ++k) {
+            wf[k] = FMA(sdt, Z[(size_t)q * m + k], wf[k]);
+            Wo[(size_t)(q + 1) * m + k] = FMA(rho, W[(size_t)(q + 1) * m + k], srho * wf[k]);
+        }
+    }
+}
+
+/*
+ * Whole-ensemble draw for single-segment terminal blocks (the synthetic
+ * configs C2-C5), OpenMP over blocks.  Reference layout: block b owns points
+ * [b*npts, (b+1)*npts).  Used as the timed CPU baseline and for big parity
+ * tests.  Z: [B][npts-1][m] (NULL -> perf-mode Philox stream with seed/iter).
+ * Each block may have its own tables (H_stride/F_stride = 0 means shared).
+ */
+void SFX(orc_normal_pair)(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                          REAL* z0, REAL* z1);
+
+int SFX(orc_draw_terminal_blocks)(int model, int d, int m, int64_t B, int npts,
+                                  const double* laws, int64_t law_stride,
+                                  const REAL* t, int64_t t_stride,
+                                  const REAL* H, int64_t H_stride,
+                                  const REAL* F, int64_t F_stride,
+                                  const REAL* Xacc, const REAL* Wacc, const REAL* Z,
+                                  uint64_t seed, int64_t iter, uint32_t salt,
+                                  const double* rho, REAL* Xo, REAL* Wo, double* ll_out,
+                                  int nthreads) {
+    int64_t nfail = 0;
+    (void)nthreads;
+#pragma omp parallel for schedule(static) reduction(+ : nfail) num_threads(nthreads)
+    for (int64_t blk = 0; blk < B; ++blk) {
+        const double* law = laws + blk * law_stride;
+        const REAL* tb = t + blk * t_stride;
+        const REAL* Hb = H + blk * H_stride;
+        const REAL* Fb = F + blk * F_stride;
+        const REAL* Xa = Xacc + (size_t)blk * npts * d;
+        const REAL* Wa = Wacc + (size_t)blk * npts * m;
+        REAL* Xp = Xo + (size_t)blk * npts * d;
+        REAL* Wp = Wo + (size_t)blk * npts * m;
+        double r = rho[blk];
+        REAL rr = (REAL)r, sr = (REAL)sqrt(1.0 - r * r);
+        /* pCN */
+        REAL wf[3] = {0, 0, 0};
+        for (int k = 0; k < m; ++k) Wp[k] = FMA(rr, Wa[k], sr * wf[k]);
+        REAL zc = 0; int have = 0;
+        for (int q = 0; q < npts - 1; ++q) {
+            REAL sdt = SQRT(tb[q + 1] - tb[q]);
+            for (int k = 0; k < m; ++k) {
+                REAL z;
+                if (Z) z = Z[((size_t)blk * (npts - 1) + q) * m + k];
+                else {
+                    uint32_t n = (uint32_t)(q * m + k);
+                    if (n & 1u) { z = zc; have = 0; }
+                    else {
+                        REAL z0, z1;
+                        SFX(orc_normal_pair)(seed, n >> 1, (uint32_t)blk, (uint32_t)iter,
+                                             salt << 1, &z0, &z1);
+                        z = z0; zc = z1; have = 1;
+                    }
+                }
+                wf[k] = FMA(sdt, z, wf[k]);
+                Wp[(size_t)(q + 1) * m + k] = FMA(rr, Wa[(size_t)(q + 1) * m + k], sr * wf[k]);
+            }
+        }
+        (void)have;
+        /* solve + ll (obs term + segment) */
+        REAL ll;
+        int ok = SFX(orc_solve_segment)(model, d, m, law, npts, tb, Hb, Fb, Wp, Xa, Xp, &ll);
+        REAL obs = SFX(orc_obs_term)(d, law, Hb, Fb, Xa);
+        REAL tot = obs + ll;
+        ll_out[blk] = ok ? (double)tot : -INFINITY;
+        nfail += ok ? 0 : 1;
+    }
+    return (int)nfail;
+}
+
+#if IS_F64
+/* ---- Philox4x32-10 (Salmon et al. 2011), shared by both precisions ---- */
+void orc_philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+    for (int r = 0; r < 10; ++r) {
+        uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+        uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+        uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0;
+        uint32_t n1 = (uint32_t)p1;
+        uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
+        uint32_t n3 = (uint32_t)p0;
+        c[0] = n0; c[1] = n1; c[2] = n2; c[3] = n3;
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+}
+#else
+void orc_philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1);
+#endif
+
+/* Box–Muller normal pair from one Philox block (perf-mode stream).
+ * counter = (c0, c1, c2, c3), key = seed. */
+void SFX(orc_normal_pair)(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                          REAL* z0, REAL* z1) {
+    uint32_t c[4] = {c0, c1, c2, c3};
+    orc_philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+#if IS_F64
+    uint64_t k1 = ((uint64_t)(c[0] >> 5) << 26) | (c[1] >> 6);
+    uint64_t k2 = ((uint64_t)(c[2] >> 5) << 26) | (c[3] >> 6);
+    double u1 = (double)(k1 + 1) * 0x1p-53;
+    double u2 = (double)k2 * 0x1p-53;
+    double rad = sqrt(-2.0 * log(u1));
+    double ang = 2.0 * M_PI * u2;
+    *z0 = rad * cos(ang);
+    *z1 = rad * sin(ang);
+#else
+    float u1 = (float)((c[0] >> 8) + 1u) * 0x1p-24f;
+    float u2 = (float)(c[2] >> 8) * 0x1p-24f;
+    float rad = sqrtf(-2.0f * logf(u1));
+    float ang = 6.28318530717958647692f * u2;
+    *z0 = rad * cosf(ang);
+    *z1 = rad * sinf(ang);
+#endif
+}
+
+#if IS_F64
+/* Exp(1) draw for the MH test of block `blk` (perf-mode stream). */
+double orc_exp1(uint64_t seed, uint32_t blk, uint32_t iter, uint32_t salt) {
+    uint32_t c[4] = {blk, 0xFFFFFFFFu, iter, (salt << 1) | 1u};
+    orc_philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    uint64_t k1 = ((uint64_t)(c[0] >> 5) << 26) | (c[1] >> 6);
+    double u = (double)(k1 + 1) * 0x1p-53;
+    return -log(u);
+}
+
+/* raw Philox block, for bit-exact checks of the device generator */
+void orc_philox_raw(uint64_t seed, const uint32_t* ctr, uint32_t* out) {
+    uint32_t c[4] = {ctr[0], ctr[1], ctr[2], ctr[3]};
+    orc_philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    memcpy(out, c, sizeof c);
+}
+#endif
+
+/* All perf-mode normals of one segment: Z[i*m + k] for steps i < nsteps
+ * (normal n uses pair n>>1 of counter (n>>1, g, iter, salt<<1)). */
+void SFX(orc_normals_segment)(uint64_t seed, uint32_t g, uint32_t iter, uint32_t salt,
+                              int nsteps, int m, REAL* Z) {
+    int n = nsteps * m;
+    for (int i = 0; i < n; i += 2) {
+        REAL z0, z1;
+        SFX(orc_normal_pair)(seed, (uint32_t)(i >> 1), g, iter, salt << 1, &z0, &z1);
+        Z[i] = z0;
+        if (i + 1 < n) Z[i + 1] = z1;
+    }
+}

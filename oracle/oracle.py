@@ -1,0 +1,473 @@
+"""Oracle for the guided-bridge hot path — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and the cpu_baseline leg of bench.py import this
+module; the product (libdmt, diffusionmcmctools.jl_amd) never does.
+
+Two parts:
+  * a ctypes binding of liboracle.so (oracle/dmt_oracle.c): the per-segment numerical
+    restatement (canonical arithmetic, see the C file header);
+  * ``OracleEnsemble``: a pure-Python restatement of the reference's CONTAINER semantics,
+    following the Julia sources line by line: SamplingPair u/u° with per-segment
+    containers (src/sampling_pair.jl:36-55), Block views (src/block.jl:49-79), BiBlock
+    imputation/accept/swaps/histories (src/biblock.jl:78-259), BlockCollection /
+    BlockEnsemble broadcasting (src/block_collection.jl, src/block_ensemble.jl).
+    Swaps exchange Python object references between u and u°, exactly as the Julia
+    code swaps container references.
+
+Parity status: "parity unpinned" against the reference itself (no Julia, upstream
+GuidedProposals/DiffusionDefinition not vendored, empty reference tests); pinned by
+the analytic known-answer tests in tests/test_oracle_kat.py and the independent
+numpy restatement in oracle/np_oracle.py.  See DESIGN.md §4.
+"""
+from __future__ import annotations
+
+import copy
+import ctypes as C
+import math
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liboracle.so")
+
+LAW_STRIDE = 64
+L_C0 = 49
+
+
+def build():
+    subprocess.run(["make", "-C", HERE, "-s"], check=True)
+
+
+def _load():
+    if not os.path.exists(LIB):
+        build()
+    lib = C.CDLL(LIB)
+    d_, i_, i64, u32, u64 = C.c_double, C.c_int, C.c_int64, C.c_uint32, C.c_uint64
+    P = C.c_void_p
+    for sfx, R in (("f64", C.c_double), ("f32", C.c_float)):
+        f = getattr(lib, f"orc_solve_segment_{sfx}")
+        f.argtypes = [i_, i_, i_, P, i_, P, P, P, P, P, P, P]
+        f.restype = i_
+        f = getattr(lib, f"orc_path_ll_segment_{sfx}")
+        f.argtypes = [i_, i_, i_, P, i_, P, P, P, P]
+        f.restype = R
+        f = getattr(lib, f"orc_obs_term_{sfx}")
+        f.argtypes = [i_, P, P, P, P]
+        f.restype = R
+        f = getattr(lib, f"orc_pcn_segment_{sfx}")
+        f.argtypes = [i_, i_, P, P, P, R, R, P]
+        f.restype = None
+        f = getattr(lib, f"orc_normals_segment_{sfx}")
+        f.argtypes = [u64, u32, u32, u32, i_, i_, P]
+        f.restype = None
+        f = getattr(lib, f"orc_draw_terminal_blocks_{sfx}")
+        f.argtypes = [i_, i_, i_, i64, i_, P, i64, P, i64, P, i64, P, i64, P, P, P, u64, i64,
+                      u32, P, P, P, P, i_]
+        f.restype = i_
+    lib.orc_normal_pair_f64.argtypes = [u64, u32, u32, u32, u32, P, P]
+    lib.orc_normal_pair_f64.restype = None
+    lib.orc_exp1.argtypes = [u64, u32, u32, u32]
+    lib.orc_exp1.restype = d_
+    lib.orc_philox_raw.argtypes = [u64, P, P]
+    lib.orc_philox_raw.restype = None
+    return lib
+
+
+lib = _load()
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def _dt(prec):
+    return np.float64 if prec == 0 else np.float32
+
+
+def _sfx(prec):
+    return "f64" if prec == 0 else "f32"
+
+
+# ------------------------------------------------------------------ per-segment numerics
+def solve_segment(model, d, m, law, t, H, F, W, y1, prec=0):
+    dt = _dt(prec)
+    t, H, F, W = (np.ascontiguousarray(a, dtype=dt) for a in (t, H, F, W))
+    y1 = np.ascontiguousarray(y1, dtype=dt)
+    law = np.ascontiguousarray(law, dtype=np.float64)
+    n = t.size
+    X = np.empty((n, d), dtype=dt)
+    ll = np.zeros(1, dtype=dt)
+    ok = getattr(lib, f"orc_solve_segment_{_sfx(prec)}")(model, d, m, _p(law), n, _p(t), _p(H),
+                                                          _p(F), _p(W), _p(y1), _p(X), _p(ll))
+    return X, dt(ll[0]), bool(ok)
+
+
+def path_ll_segment(model, d, m, law, t, H, F, X, prec=0):
+    dt = _dt(prec)
+    t, H, F, X = (np.ascontiguousarray(a, dtype=dt) for a in (t, H, F, X))
+    law = np.ascontiguousarray(law, dtype=np.float64)
+    return dt(getattr(lib, f"orc_path_ll_segment_{_sfx(prec)}")(model, d, m, _p(law), t.size,
+                                                                 _p(t), _p(H), _p(F), _p(X)))
+
+
+def obs_term(d, law, H0, F0, x, prec=0):
+    dt = _dt(prec)
+    H0, F0, x = (np.ascontiguousarray(a, dtype=dt) for a in (H0, F0, x))
+    law = np.ascontiguousarray(law, dtype=np.float64)
+    return dt(getattr(lib, f"orc_obs_term_{_sfx(prec)}")(d, _p(law), _p(H0), _p(F0), _p(x)))
+
+
+def pcn_segment(m, t, W, Z, rho, srho, prec=0):
+    dt = _dt(prec)
+    t, W, Z = (np.ascontiguousarray(a, dtype=dt) for a in (t, W, Z))
+    Wo = np.empty((t.size, m), dtype=dt)
+    getattr(lib, f"orc_pcn_segment_{_sfx(prec)}")(m, t.size, _p(t), _p(W), _p(Z), rho, srho,
+                                                  _p(Wo))
+    return Wo
+
+
+def normals_segment(seed, g, it, salt, nsteps, m, prec=0):
+    Z = np.empty(nsteps * m, dtype=_dt(prec))
+    getattr(lib, f"orc_normals_segment_{_sfx(prec)}")(seed, g, it & 0xFFFFFFFF, salt, nsteps, m,
+                                                      _p(Z))
+    return Z.reshape(nsteps, m)
+
+
+def normal_pair(seed, ctr):
+    """Box–Muller pair of one Philox block (fp64), counter ctr = (c0, c1, c2, c3)."""
+    z0, z1 = C.c_double(), C.c_double()
+    lib.orc_normal_pair_f64(seed, *[int(v) for v in ctr], C.byref(z0), C.byref(z1))
+    return z0.value, z1.value
+
+
+def exp1(seed, blk, it, salt):
+    return lib.orc_exp1(seed, blk, it & 0xFFFFFFFF, salt)
+
+
+def philox_raw(seed, ctr):
+    ctr = np.ascontiguousarray(ctr, dtype=np.uint32).reshape(-1, 4)
+    out = np.empty_like(ctr)
+    for i in range(ctr.shape[0]):
+        lib.orc_philox_raw(seed, _p(ctr[i]), _p(out[i]))
+    return out
+
+
+def pairwise_tree(vals):
+    """Complete adjacent-pair binary tree over vals padded with zeros to a power of two,
+    canonicalised with + 0.0 (fetch_ll reduction order)."""
+    v = [float(x) for x in vals]
+    n2 = 1
+    while n2 < len(v):
+        n2 *= 2
+    v = v + [0.0] * (n2 - len(v))
+    while len(v) > 1:
+        v = [v[2 * j] + v[2 * j + 1] for j in range(len(v) // 2)]
+    return (v[0] if v else 0.0) + 0.0
+
+
+def draw_terminal_blocks(model, d, m, npts, laws, t, H, F, Xacc, Wacc, rho, Z=None, seed=0,
+                         it=0, salt=0, prec=0, nthreads=1, t_shared=True, H_shared=False):
+    """Whole-ensemble draw for single-segment terminal blocks, OpenMP over blocks
+    (the timed CPU baseline).  Arrays in reference layout."""
+    dt = _dt(prec)
+    B = laws.shape[0]
+    t = np.ascontiguousarray(t, dtype=dt)
+    H = np.ascontiguousarray(H, dtype=dt)
+    F = np.ascontiguousarray(F, dtype=dt)
+    Xacc = np.ascontiguousarray(Xacc, dtype=dt)
+    Wacc = np.ascontiguousarray(Wacc, dtype=dt)
+    laws = np.ascontiguousarray(laws, dtype=np.float64)
+    rho = np.ascontiguousarray(rho, dtype=np.float64)
+    Zp = None if Z is None else np.ascontiguousarray(Z, dtype=dt)
+    hp = d * (d + 1) // 2
+    Xo = np.empty((B * npts, d), dtype=dt)
+    Wo = np.empty((B * npts, m), dtype=dt)
+    ll = np.empty(B)
+    nfail = getattr(lib, f"orc_draw_terminal_blocks_{_sfx(prec)}")(
+        model, d, m, B, npts, _p(laws), LAW_STRIDE, _p(t), 0 if t_shared else npts, _p(H),
+        0 if H_shared else npts * hp, _p(F), npts * d, _p(Xacc), _p(Wacc),
+        None if Zp is None else _p(Zp), seed, it, salt, _p(rho), _p(Xo), _p(Wo), _p(ll), nthreads)
+    return Xo, Wo, ll, nfail
+
+
+# ------------------------------------------------------------------ container semantics
+class _Law:
+    __slots__ = ("H", "F", "rec")
+
+    def __init__(self, H, F, rec):
+        self.H, self.F, self.rec = H, F, rec
+
+
+class _Unit:
+    """SamplingUnit containers (src/sampling_unit.jl:48-53): PP, PPb, WW, XX per segment."""
+
+    def __init__(self):
+        self.PP, self.PPb, self.WW, self.XX = [], [], [], []
+
+
+class _Block:
+    def __init__(self, rec, g0, g1, term, rho, hist_len):
+        self.rec, self.g0, self.g1, self.term = rec, g0, g1, bool(term)
+        self.rho = float(rho)
+        self.srho = math.sqrt(1.0 - self.rho * self.rho)
+        self.ll = -math.inf   # src/block.jl:75
+        self.llp = -math.inf
+        self.ll_hist = np.zeros(hist_len)
+        self.llp_hist = np.zeros(hist_len)
+        self.acc_hist = np.zeros(hist_len, dtype=bool)
+
+
+class OracleEnsemble:
+    """Restatement of SamplingEnsemble + BlockEnsemble semantics on reference-layout data.
+    Mirrors the libdmt call surface (diffusionmcmctools.jl_amd/engine.py) so tests can drive
+    both with the same calls."""
+
+    def __init__(self, model, d, m, n_points, prec=0, seed=0, grid_shared=False):
+        self.model, self.d, self.m, self.prec, self.seed = model, d, m, prec, seed
+        self.hp = d * (d + 1) // 2
+        self.dt = _dt(prec)
+        self.nseg = [len(r) for r in n_points]
+        self.npts = [int(n) for r in n_points for n in r]
+        self.R, self.G = len(self.nseg), len(self.npts)
+        self.rec_seg0 = np.concatenate([[0], np.cumsum(self.nseg)]).astype(np.int64)
+        self.pt_off = np.concatenate([[0], np.cumsum(self.npts)[:-1]]).astype(np.int64)
+        self.st_off = self.pt_off - np.arange(self.G)
+        self.P = int(sum(self.npts))
+        self.S = self.P - self.G
+        self.grid_shared = grid_shared
+        self.Q0 = int(sum(self.npts[: self.nseg[0]]))
+        self.t = [None] * self.G
+        self.u, self.up = _Unit(), _Unit()
+        for U_ in (self.u, self.up):
+            for g in range(self.G):
+                U_.XX.append(np.zeros((self.npts[g], d), dtype=self.dt))
+                U_.WW.append(np.zeros((self.npts[g], m), dtype=self.dt))
+            U_.PP = [None] * self.G
+            U_.PPb = [None] * self.G
+        self.layouts = []
+        # internal layout 0: whole recordings, terminal, rho 0 (draw_proposal_path!(u))
+        self.create_layout([1] * self.R, [0] * self.R, [n - 1 for n in self.nseg], [1] * self.R,
+                           [0.0] * self.R, 0)
+
+    def _seg_rows(self, arr, g, C_):
+        a = np.asarray(arr, dtype=np.float64).reshape(-1, C_)
+        return a[self.pt_off[g]: self.pt_off[g] + self.npts[g]].astype(self.dt)
+
+    def _unit(self, unit):
+        return self.u if unit == 0 else self.up
+
+    # ---- uploads
+    def upload_grid(self, t):
+        t = np.asarray(t, dtype=np.float64)
+        for g in range(self.G):
+            if self.grid_shared:
+                k = g - self.rec_seg0[np.searchsorted(self.rec_seg0, g, side="right") - 1]
+                off = int(sum(self.npts[:k]))
+                self.t[g] = t[off: off + self.npts[g]].astype(self.dt)
+            else:
+                self.t[g] = self._seg_rows(t, g, 1).ravel()
+
+    def upload_law(self, unit, kind, H=None, F=None, laws=None, H_shared=False):
+        me = self._unit(unit)
+        other = self._unit(1 - unit)
+        tab = me.PP if kind == 0 else me.PPb
+        otab = other.PP if kind == 0 else other.PPb
+        first = tab[0] is None
+        for g in range(self.G):
+            if tab[g] is None:
+                tab[g] = _Law(None, None, None)
+            lw = tab[g]
+            if H is not None:
+                if H_shared:
+                    k = g - self.rec_seg0[np.searchsorted(self.rec_seg0, g, side="right") - 1]
+                    off = int(sum(self.npts[self.rec_seg0[0]: self.rec_seg0[0] + k]))
+                    Hs = np.asarray(H, dtype=np.float64).reshape(-1, self.hp)
+                    lw.H = Hs[off: off + self.npts[g]].astype(self.dt)
+                else:
+                    lw.H = self._seg_rows(H, g, self.hp)
+            if F is not None:
+                lw.F = self._seg_rows(F, g, self.d)
+            if laws is not None:
+                lw.rec = np.asarray(laws, dtype=np.float64).reshape(self.G, LAW_STRIDE)[g].copy()
+        if first:  # u° = deepcopy(u) (src/sampling_pair.jl:51)
+            for g in range(self.G):
+                otab[g] = copy.deepcopy(tab[g])
+
+    def set_paths(self, unit, X=None, W=None):
+        me = self._unit(unit)
+        for g in range(self.G):
+            if X is not None:
+                me.XX[g][...] = self._seg_rows(X, g, self.d)
+            if W is not None:
+                me.WW[g][...] = self._seg_rows(W, g, self.m)
+
+    def download_paths(self, unit, what):
+        me = self._unit(unit)
+        src = me.XX if what == 0 else me.WW
+        return np.concatenate(src).astype(np.float64)
+
+    # ---- layouts (BlockEnsemble ranges)
+    def create_layout(self, n_blocks, seg_first, seg_last, last, rho, hist_len=0):
+        blocks, b = [], 0
+        for r in range(self.R):
+            for _ in range(n_blocks[r]):
+                g0 = int(self.rec_seg0[r] + seg_first[b])
+                g1 = int(self.rec_seg0[r] + seg_last[b])
+                blocks.append(_Block(r, g0, g1, last[b], rho[b], hist_len))
+                b += 1
+        self.layouts.append(blocks)
+        return len(self.layouts) - 1
+
+    # ---- the hot path, restated
+    def _Zseg(self, Z, g, it, salt):
+        n = self.npts[g] - 1
+        if Z is not None:
+            Zf = np.asarray(Z, dtype=np.float64).reshape(-1, self.m)
+            return Zf[self.st_off[g]: self.st_off[g] + n].astype(self.dt)
+        return normals_segment(self.seed, g, it, salt, n, self.m, self.prec)
+
+    def _law(self, unit, bk, g):
+        me = self._unit(unit)
+        return me.PPb[g] if (not bk.term and g == bk.g1) else me.PP[g]
+
+    def _solve_block(self, bk, law_unit, start_unit, w_unit, out_unit, mode, Z, it, salt):
+        """mode: 'pcn' (rand! with ρ), 'given' (solve_and_ll! with W), 'fresh' (ρ = 0)."""
+        dt = self.dt
+        src = self._unit(start_unit)
+        y1 = src.XX[bk.g0][0].copy()
+        law0 = self._unit(law_unit).PP[bk.g0]
+        ll = obs_term(self.d, law0.rec, law0.H[0], law0.F[0], y1, self.prec)
+        x = y1
+        ok_all = True
+        out = self._unit(out_unit)
+        win = self._unit(w_unit)
+        for g in range(bk.g0, bk.g1 + 1):
+            lw = self._law(law_unit, bk, g)
+            t = self.t[g]
+            if mode == "given":
+                Wuse = win.WW[g]
+            else:
+                Zg = self._Zseg(Z, g, it, salt)
+                if mode == "fresh":
+                    Wuse = pcn_segment(self.m, t, np.zeros_like(win.WW[g]), Zg, dt(0.0), dt(1.0),
+                                       self.prec)
+                else:
+                    Wuse = pcn_segment(self.m, t, win.WW[g], Zg, dt(bk.rho), dt(bk.srho),
+                                       self.prec)
+                out.WW[g][...] = Wuse
+            X, sl, ok = solve_segment(self.model, self.d, self.m, lw.rec, t, lw.H, lw.F, Wuse, x,
+                                      self.prec)
+            out.XX[g][...] = X
+            if not ok:
+                ok_all = False
+                break
+            ll = dt(ll + sl)
+            x = X[-1].copy()
+        return (float(ll) if ok_all else -math.inf), ok_all
+
+    def draw_unit(self, unit, r0=0, r1=None, Z=None, iter=0, salt=0):
+        """draw_proposal_path!(u::SamplingUnit), src/sampling_unit.jl:118-120."""
+        r1 = self.R if r1 is None else r1
+        lls, oks = [], []
+        for r in range(r0, r1):
+            bk = self.layouts[0][r]
+            ll, ok = self._solve_block(bk, unit, unit, unit, unit, "fresh", Z, iter, salt)
+            lls.append(ll)
+            oks.append(ok)
+        return np.array(lls), np.array(oks)
+
+    def draw_proposal(self, layout, b0, b1, Z=None, iter=0, salt=0, want_success=False):
+        """draw_proposal_path!(bb::BiBlock), src/biblock.jl:78-106: proposal drawn under the
+        ACCEPTED law bb.b.PP into bb.b°, starting at bb.b.XX[1].x[1]."""
+        oks = []
+        for bk in self.layouts[layout][b0:b1]:
+            bk.llp, ok = self._solve_block(bk, 0, 0, 0, 1, "pcn", Z, iter, salt)
+            oks.append(ok)
+        return np.array(oks) if want_success else None
+
+    def accept_reject(self, layout, b0, b1, mcmciter, E=None, salt=0, want_acc=False):
+        """accept_reject_proposal_path!(bb, i), src/biblock.jl:121-127."""
+        accs = []
+        for j, bk in enumerate(self.layouts[layout][b0:b1]):
+            blk = b0 + j
+            e = float(E[j]) if E is not None else exp1(self.seed, blk, mcmciter, salt)
+            acc = e > -(bk.llp - bk.ll)
+            if acc:  # swap_paths!: XX and WW element swaps (src/biblock.jl:148-173)
+                for g in range(bk.g0, bk.g1 + 1):
+                    self.u.XX[g], self.up.XX[g] = self.up.XX[g], self.u.XX[g]
+                    self.u.WW[g], self.up.WW[g] = self.up.WW[g], self.u.WW[g]
+            if len(bk.acc_hist):
+                bk.acc_hist[mcmciter - 1] = acc   # set_accepted!
+                bk.ll_hist[mcmciter - 1] = bk.ll  # save_ll! on b and b°
+                bk.llp_hist[mcmciter - 1] = bk.llp
+            if acc:
+                bk.ll, bk.llp = bk.llp, bk.ll     # swap_ll!
+            accs.append(acc)
+        return np.array(accs) if want_acc else None
+
+    def loglikhd(self, layout, unit, b0, b1):
+        """loglikhd!(b) (src/block.jl:138-152): obs term + Girsanov sums on stored paths."""
+        me = self._unit(unit)
+        dt = self.dt
+        for bk in self.layouts[layout][b0:b1]:
+            law0 = me.PP[bk.g0]
+            ll = obs_term(self.d, law0.rec, law0.H[0], law0.F[0], me.XX[bk.g0][0], self.prec)
+            for g in range(bk.g0, bk.g1 + 1):
+                lw = self._law(unit, bk, g)
+                ll = dt(ll + path_ll_segment(self.model, self.d, self.m, lw.rec, self.t[g], lw.H,
+                                             lw.F, me.XX[g], self.prec))
+            if unit == 0:
+                bk.ll = float(ll)
+            else:
+                bk.llp = float(ll)
+
+    def recompute_path(self, layout, b0, b1, skip=0, want_success=False):
+        """recompute_path!(b°, b.WW) (src/block.jl:159-187) under u°.PP."""
+        assert skip == 0
+        oks = []
+        for bk in self.layouts[layout][b0:b1]:
+            bk.llp, ok = self._solve_block(bk, 1, 1, 0, 1, "given", None, 0, 0)
+            oks.append(ok)
+        return np.array(oks) if want_success else None
+
+    def swap(self, layout, what, b0, b1):
+        for bk in self.layouts[layout][b0:b1]:
+            for g in range(bk.g0, bk.g1 + 1):
+                if what & 1:
+                    self.u.XX[g], self.up.XX[g] = self.up.XX[g], self.u.XX[g]
+                if what & 2:
+                    self.u.WW[g], self.up.WW[g] = self.up.WW[g], self.u.WW[g]
+                if what & 4:  # swap_PP! (src/biblock.jl:180-199)
+                    self.u.PP[g], self.up.PP[g] = self.up.PP[g], self.u.PP[g]
+                    if not bk.term:
+                        self.u.PPb[g], self.up.PPb[g] = self.up.PPb[g], self.u.PPb[g]
+            if what & 8:
+                bk.ll, bk.llp = bk.llp, bk.ll
+
+    def save_ll(self, layout, b0, b1, mcmciter):
+        for bk in self.layouts[layout][b0:b1]:
+            bk.ll_hist[mcmciter - 1] = bk.ll
+            bk.llp_hist[mcmciter - 1] = bk.llp
+
+    def set_accepted(self, layout, b0, b1, mcmciter, v):
+        v = np.broadcast_to(np.asarray(v, dtype=bool), (b1 - b0,))
+        for j, bk in enumerate(self.layouts[layout][b0:b1]):
+            bk.acc_hist[mcmciter - 1] = v[j]
+
+    def block_ll(self, layout, b0, b1):
+        bks = self.layouts[layout][b0:b1]
+        return np.array([b.ll for b in bks]), np.array([b.llp for b in bks])
+
+    def histories(self, layout, b0, b1):
+        bks = self.layouts[layout][b0:b1]
+        return (np.stack([b.ll_hist for b in bks], 1), np.stack([b.llp_hist for b in bks], 1),
+                np.stack([b.acc_hist for b in bks], 1))
+
+    def fetch_ll(self, layout, b0, b1, mcmciter=0):
+        bks = self.layouts[layout][b0:b1]
+        a = pairwise_tree([b.ll for b in bks])
+        p = pairwise_tree([b.llp for b in bks])
+        n = int(sum(bool(b.acc_hist[mcmciter - 1]) for b in bks)) if mcmciter > 0 else 0
+        return a, p, n

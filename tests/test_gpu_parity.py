@@ -1,0 +1,238 @@
+"""Parity of the HIP hot path (through the C-ABI) with the CPU oracle on identical inputs.
+
+Bar: paths X/W, log-weights ll/ll°, MH decisions, histories and fetch_ll are
+BIT-IDENTICAL to the oracle in parity mode (host-supplied normals Z and Exp(1) draws E), in fp64
+and in fp32.  Device-RNG (perf) mode is compared within a stated tolerance because the
+Box–Muller transcendental (log, sincospi) rounds differently in glibc and in the device libm:
+|ΔX| ≤ 1e-9 (1 + |X|), |Δll| ≤ 1e-8 (1 + |ll|), and the Philox integer stream is bit-identical.
+"""
+import math
+
+import numpy as np
+import pytest
+
+import _cases as cs
+import oracle as orc
+from diffusionmcmctools_amd import _lib as L
+from diffusionmcmctools_amd import workloads as W
+
+pytestmark = pytest.mark.gpu
+
+
+def run_mcmc_parity(w, iters, seed=3, hist_len=None, exact=True, check_every=True):
+    hist_len = iters if hist_len is None else hist_len
+    dev, ora, lay = cs.both(w, hist_len=hist_len)
+    nb = w.nblocks
+    rng = np.random.default_rng(seed)
+    for e in (dev, ora):
+        e.loglikhd(lay, L.U, 0, nb)
+    cs.assert_ll_equal(dev, ora, lay, nb)
+    for i in range(1, iters + 1):
+        Z = rng.standard_normal((w.steps_per_iter, w.m))
+        E = rng.exponential(1.0, nb)
+        okd = dev.draw_proposal(lay, 0, nb, Z=Z, iter=i, want_success=True)
+        oko = ora.draw_proposal(lay, 0, nb, Z=Z, iter=i, want_success=True)
+        assert np.array_equal(okd, oko)
+        ad = dev.accept_reject(lay, 0, nb, i, E=E, want_acc=True)
+        ao = ora.accept_reject(lay, 0, nb, i, E=E, want_acc=True)
+        assert np.array_equal(ad, ao), f"iteration {i}: decisions differ"
+        if check_every or i == iters:
+            cs.assert_paths_equal(dev, ora)
+            cs.assert_ll_equal(dev, ora, lay, nb)
+    if hist_len:
+        llh, llph, acch = ora.histories(lay, 0, nb)
+        assert np.array_equal(dev.get_block_state(lay, L.BLK_LL_HIST, 0, nb, hist_len), llh)
+        assert np.array_equal(dev.get_block_state(lay, L.BLK_LLPROP_HIST, 0, nb, hist_len), llph)
+        assert np.array_equal(dev.get_block_state(lay, L.BLK_ACC_HIST, 0, nb, hist_len).astype(bool), acch)
+        for it in (1, iters):
+            assert dev.fetch_ll(lay, 0, nb, it) == ora.fetch_ll(lay, 0, nb, it)
+    return dev, ora, lay
+
+
+def test_c1_ou1d_mcmc_bit_exact():
+    run_mcmc_parity(W.c1_ou1d(), iters=40)
+
+
+def test_c2_ou2d_ragged_tile_bit_exact():
+    # 200 blocks: 3 full recording tiles + a partial one
+    run_mcmc_parity(W.c2_ou2d(B=200, N=500), iters=4)
+
+
+def test_c3_fhn_reduced_bit_exact():
+    run_mcmc_parity(W.c3_fhn(B=130, N=1000, T_burn=0.05), iters=3, check_every=False)
+
+
+def test_c5_lorenz_fp32_reduced_bit_exact():
+    run_mcmc_parity(W.c5_lorenz(B=70, N=2000), iters=3, check_every=False)
+
+
+def test_ragged_blocking_layouts_bit_exact():
+    """Multi-segment recordings, non-terminal blocks with P_last laws, two alternating block
+    layouts aliasing the same SamplingPair (src/block.jl:66-72), swaps, loglikhd of both units,
+    a proposal law and recompute_path! (src/biblock.jl:334-344)."""
+    case, dev, ora, ((A, nA), (B, nB)) = cs.ragged_pair()
+    rng = np.random.default_rng(9)
+    S = case["t"].size - sum(case["nsegs"])
+    for e in (dev, ora):
+        e.loglikhd(A, L.U, 0, nA)
+        e.loglikhd(B, L.U, 0, nB)
+    for i in range(1, 7):
+        for lay, nb in ((A, nA), (B, nB)):
+            Z = rng.standard_normal((S, 1))
+            E = rng.exponential(1.0, nb)
+            for e in (dev, ora):
+                e.loglikhd(lay, L.U, 0, nb)
+                e.draw_proposal(lay, 0, nb, Z=Z, iter=i)
+            assert np.array_equal(dev.accept_reject(lay, 0, nb, i, E=E, want_acc=True),
+                                  ora.accept_reject(lay, 0, nb, i, E=E, want_acc=True))
+            cs.assert_paths_equal(dev, ora)
+            cs.assert_ll_equal(dev, ora, lay, nb)
+    # sub-ranges (a BiBlock is a 1-block range, a BlockCollection one recording's blocks)
+    Z = rng.standard_normal((S, 1))
+    for e in (dev, ora):
+        e.draw_proposal(A, 2, 5, Z=Z, iter=7)
+    cs.assert_ll_equal(dev, ora, A, nA)
+    cs.assert_paths_equal(dev, ora)
+    # swaps
+    for what in (L.SWAP_XX, L.SWAP_WW | L.SWAP_LL, L.SWAP_XX | L.SWAP_WW):
+        for e in (dev, ora):
+            e.swap(A, what, 1, 4)
+        cs.assert_paths_equal(dev, ora)
+        cs.assert_ll_equal(dev, ora, A, nA)
+    # proposal law (θ° with a different γ), recompute_path!, ll of u°, swap_PP!
+    lawsp = case["laws"].copy()
+    lawsp[:, 2] = 1.7
+    for e in (dev, ora):
+        e.upload_law(L.UPROP, L.LAW_PP, laws=lawsp)
+    okd = dev.recompute_path(A, 0, nA, want_success=True)
+    oko = ora.recompute_path(A, 0, nA, want_success=True)
+    assert np.array_equal(okd, oko)
+    cs.assert_paths_equal(dev, ora)
+    cs.assert_ll_equal(dev, ora, A, nA)
+    for e in (dev, ora):
+        e.loglikhd(A, L.UPROP, 0, nA)
+        e.swap(A, L.SWAP_PP | L.SWAP_XX | L.SWAP_LL, 0, 3)
+        e.loglikhd(A, L.U, 0, nA)
+        e.loglikhd(B, L.UPROP, 0, nB)
+    cs.assert_ll_equal(dev, ora, A, nA)
+    cs.assert_ll_equal(dev, ora, B, nB)
+    assert dev.fetch_ll(A, 0, nA) == ora.fetch_ll(A, 0, nA)
+
+
+def test_fetch_ll_tree_bit_exact():
+    w = W.c2_ou2d(B=64 * 80, N=8)
+    dev, ora, lay = cs.both(w, hist_len=2)
+    rng = np.random.default_rng(0)
+    nb = w.nblocks
+    vals = rng.standard_normal(nb) * 10.0 ** rng.integers(-3, 6, nb)
+    valsp = rng.standard_normal(nb) * 1e3
+    dev.set_block_state(lay, L.BLK_LL, 0, nb, vals)
+    dev.set_block_state(lay, L.BLK_LLPROP, 0, nb, valsp)
+    acc = (rng.random((2, nb)) < 0.4).astype(np.uint8)
+    dev.set_block_state(lay, L.BLK_ACC_HIST, 0, nb, acc)
+    for b0, b1 in ((0, 1), (0, 63), (0, 64), (3, 68), (0, 1000), (17, nb), (0, nb)):
+        a, p, n = dev.fetch_ll(lay, b0, b1, 2)
+        assert a == orc.pairwise_tree(vals[b0:b1])
+        assert p == orc.pairwise_tree(valsp[b0:b1])
+        assert n == int(acc[1, b0:b1].sum())
+
+
+def test_philox_stream_bit_exact(dmt):
+    rng = np.random.default_rng(1)
+    ctr = rng.integers(0, 2 ** 32, (4096, 4), dtype=np.uint64).astype(np.uint32)
+    seed = 0x1234_5678_9ABC_DEF0
+    from diffusionmcmctools_amd.engine import debug_normals, debug_philox
+    assert np.array_equal(debug_philox(seed, ctr), orc.philox_raw(seed, ctr))
+    zd = debug_normals(seed, ctr)
+    zo = np.array([orc.normal_pair(seed, c) for c in ctr])
+    np.testing.assert_allclose(zd, zo, rtol=1e-13, atol=1e-13)
+
+
+def test_device_rng_mode_matches_oracle_within_tolerance():
+    w = W.c2_ou2d(B=100, N=500)
+    dev, ora, lay = cs.both(w, hist_len=3)
+    nb = w.nblocks
+    for e in (dev, ora):
+        e.loglikhd(lay, L.U, 0, nb)
+    for i in (1, 2, 3):
+        for e in (dev, ora):
+            e.draw_proposal(lay, 0, nb, iter=i, salt=5)
+        a, b = dev.get_block_state(lay, L.BLK_LLPROP, 0, nb), ora.block_ll(lay, 0, nb)[1]
+        assert np.all(np.abs(a - b) <= 1e-8 * (1 + np.abs(b)))
+        Xd, Xo = dev.download_paths(L.UPROP, 0), ora.download_paths(L.UPROP, 0)
+        assert np.all(np.abs(Xd - Xo) <= 1e-9 * (1 + np.abs(Xo)))
+        # identical device Exp(1) stream on both sides; decisions equal unless a near-tie
+        ll_o, llp_o = ora.block_ll(lay, 0, nb)
+        margin = np.array([orc.exp1(11, j, i, 5) for j in range(nb)]) + (llp_o - ll_o)
+        ad = dev.accept_reject(lay, 0, nb, i, salt=5, want_acc=True)
+        ao = ora.accept_reject(lay, 0, nb, i, salt=5, want_acc=True)
+        assert np.all((ad == ao) | (np.abs(margin) < 1e-6))
+        if not np.array_equal(ad, ao):
+            pytest.skip("near-tie decision in perf mode")
+        # re-synchronise the two sides exactly so the next iteration starts from equal state
+        X = ora.download_paths(L.U, 0); Wp = ora.download_paths(L.U, 1)
+        dev.set_paths(L.U, X=X, W=Wp)
+        dev.set_block_state(lay, L.BLK_LL, 0, nb, ora.block_ll(lay, 0, nb)[0])
+
+
+def test_failure_gives_minus_inf_and_rejects():
+    w = W.c1_ou1d()
+    dev, ora, lay = cs.both(w, hist_len=2)
+    Z = np.full((w.steps_per_iter, 1), 1e300)   # overflows the path
+    for e in (dev, ora):
+        e.loglikhd(lay, L.U, 0, 1)
+    okd = dev.draw_proposal(lay, 0, 1, Z=Z, iter=1, want_success=True)
+    oko = ora.draw_proposal(lay, 0, 1, Z=Z, iter=1, want_success=True)
+    assert not okd[0] and not oko[0]
+    assert dev.get_block_state(lay, L.BLK_LLPROP, 0, 1)[0] == -math.inf
+    assert not dev.accept_reject(lay, 0, 1, 1, E=np.array([1e-300]), want_acc=True)[0]
+
+
+def test_first_proposal_auto_accepted_without_loglikhd():
+    """ll = -Inf initially (src/block.jl:75) so the first proposal is accepted unless
+    loglikhd! ran first (Appendix B.2 of SURVEY.md)."""
+    w = W.c2_ou2d(B=64, N=50)
+    dev, ora, lay = cs.both(w, hist_len=1)
+    rng = np.random.default_rng(2)
+    Z = rng.standard_normal((w.steps_per_iter, 2))
+    E = rng.exponential(1.0, 64)
+    for e in (dev, ora):
+        e.draw_proposal(lay, 0, 64, Z=Z, iter=1)
+    assert np.all(dev.accept_reject(lay, 0, 64, 1, E=E, want_acc=True))
+    assert np.all(ora.accept_reject(lay, 0, 64, 1, E=E, want_acc=True))
+    cs.assert_paths_equal(dev, ora)
+
+
+# ---------------------------------------------------------------- full-size properties
+@pytest.mark.parametrize("cfg", ["c2", "c3"])
+def test_full_size_properties(cfg):
+    """At BASELINE.json's full sizes (oracle too slow here): size-independent invariants."""
+    w = W.c2_ou2d() if cfg == "c2" else W.c3_fhn(T_burn=0.2)
+    import diffusionmcmctools_amd as d
+    dev = d.Ensemble(w.model.kind, w.d, w.m, w.n_points, precision=w.precision, seed=4,
+                     grid_shared=w.grid_shared)
+    w.meta["hist_len"] = 4
+    lay = W.fill(dev, w, init_Z=False)
+    nb = w.nblocks
+    dev.loglikhd(lay, L.U, 0, nb)
+    ll0 = dev.get_block_state(lay, L.BLK_LL, 0, nb)
+    assert np.all(np.isfinite(ll0))
+    for i in (1, 2, 3):
+        ok = dev.draw_proposal(lay, 0, nb, iter=i, want_success=True)
+        assert ok.mean() > 0.99
+        llp = dev.get_block_state(lay, L.BLK_LLPROP, 0, nb)
+        # the weight accumulated during the draw == loglikhd° of the stored proposal, bit for bit
+        dev.loglikhd(lay, L.UPROP, 0, nb)
+        assert np.array_equal(dev.get_block_state(lay, L.BLK_LLPROP, 0, nb), llp)
+        acc = dev.accept_reject(lay, 0, nb, i, want_acc=True)
+        assert 0.02 < acc.mean() <= 1.0
+        ll = dev.get_block_state(lay, L.BLK_LL, 0, nb)
+        dev.loglikhd(lay, L.U, 0, nb)
+        assert np.array_equal(dev.get_block_state(lay, L.BLK_LL, 0, nb), ll)
+    # ρ = 1: the pCN proposal reproduces the accepted path exactly
+    lay1 = dev.create_layout(w.n_blocks, w.seg_first, w.seg_last, w.last, np.ones(nb), 1)
+    dev.loglikhd(lay1, L.U, 0, nb)
+    dev.draw_proposal(lay1, 0, nb, iter=9)
+    assert np.array_equal(dev.download_paths(L.UPROP, 0), dev.download_paths(L.U, 0))
+    assert np.array_equal(dev.get_block_state(lay1, L.BLK_LLPROP, 0, nb),
+                          dev.get_block_state(lay1, L.BLK_LL, 0, nb))

@@ -1,0 +1,201 @@
+"""Known-answer tests that pin the oracle (and libdmt's host set-up) without the reference.
+
+The reference cannot run here and its own tests are empty (/root/reference/test/runtests.jl:4-6),
+so these analytic KATs are what pins the arithmetic.  CPU only.
+"""
+import math
+
+import numpy as np
+import pytest
+
+import np_oracle as npo
+import oracle as orc
+
+
+def _packed(M):
+    d = M.shape[0]
+    return np.array([M[a, b] for a in range(d) for b in range(a, d)])
+
+
+# ---------------------------------------------------------------- Philox (Random123 KATs)
+@pytest.mark.parametrize("ctr,key,want", [
+    ((0, 0, 0, 0), (0, 0), (0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8)),
+    ((0xffffffff,) * 4, (0xffffffff, 0xffffffff), (0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd)),
+    ((0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344), (0xa4093822, 0x299f31d0),
+     (0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1)),
+])
+def test_philox4x32_10_known_answers(ctr, key, want):
+    seed = key[0] | (key[1] << 32)
+    out = orc.philox_raw(seed, np.array(ctr, dtype=np.uint32))
+    assert tuple(int(v) for v in out[0]) == want
+
+
+def test_normals_moments():
+    Z = orc.normals_segment(123, 7, 3, 0, 200000, 1)
+    assert abs(Z.mean()) < 0.01 and abs(Z.std() - 1) < 0.01
+    E = np.array([orc.exp1(1, b, 5, 0) for b in range(20000)])
+    assert abs(E.mean() - 1) < 0.03 and E.min() > 0
+
+
+# ---------------------------------------------------------------- guiding term
+def test_guiding_ou1d_closed_form(dmt):
+    theta, mu, sigma, T, v, Sig = 0.5, 0.2, 0.7, 1.0, 0.3, 0.01
+    t = np.linspace(0, T, 101) ** 1.3
+    t = t / t[-1] * T
+    Hc, Fc, cc = npo.ou1d_guiding(theta, mu, sigma, T, t, v, Sig)
+    HT, FT = 1 / Sig, v / Sig
+    cT = 0.5 * v * v / Sig + 0.5 * math.log(2 * math.pi * Sig)
+    H, F, c = dmt.guiding_linear([[-theta]], [theta * mu], [sigma ** 2], t, [HT], [FT], cT)
+    np.testing.assert_allclose(H[:, 0], Hc, rtol=1e-12)
+    np.testing.assert_allclose(F[:, 0], Fc, rtol=1e-12)
+    np.testing.assert_allclose(c, cc, rtol=1e-12)
+
+
+@pytest.mark.parametrize("case", ["ou2d", "fhn", "fhn_blocking", "lorenz"])
+def test_guiding_matches_expm_filter(dmt, case):
+    rng = np.random.default_rng(0)
+    if case == "ou2d":
+        B = -np.diag([0.5, 0.5]); beta = np.zeros(2); at = 0.25 * np.eye(2)
+        HT = np.eye(2) / 0.01; FT = np.array([0.3, -0.2]) / 0.01; cT = 1.0; T = 1.0
+    elif case in ("fhn", "fhn_blocking"):
+        from diffusionmcmctools_amd.models import FHN
+        m = FHN(0.1, -0.8, 1.5, 0.0, 0.3)
+        aux = m.aux(-0.7)
+        B, beta, at = aux.Bt, aux.beta, aux.at
+        if case == "fhn":
+            HT = np.array([[100.0, 0], [0, 0]]); FT = np.array([-70.0, 0]); cT = 2.0
+        else:  # exact full-state artificial observation, noise 1e-11 (src/sampling_unit.jl:57)
+            HT = np.eye(2) / 1e-11; FT = np.array([-0.7, -0.4]) / 1e-11; cT = 0.0
+        T = 0.1
+    else:
+        from diffusionmcmctools_amd.models import Lorenz
+        m = Lorenz()
+        aux = m.aux(np.array([1.0, 2.0, 20.0]))
+        B, beta, at = aux.Bt, aux.beta, aux.at
+        HT = np.eye(3) / 0.1; FT = np.array([1.0, 2.0, 20.0]) / 0.1; cT = 0.5; T = 0.2
+    from diffusionmcmctools_amd.models import standard_guid_prop_time_transf
+    t = standard_guid_prop_time_transf(0.0, T, T / 200)
+    H, F, c = dmt.guiding_linear(B, beta, _packed(at), t, _packed(HT), FT, cT)
+    He, Fe, ce = npo.backward_filter_expm(B, beta, at, t, HT, FT, cT)
+    d = len(beta)
+    Hp = np.stack([_packed(He[i]) for i in range(len(t))])
+    # relative to the scale of each quantity (H spans 1e11 in the blocking case)
+    np.testing.assert_allclose(H, Hp, rtol=1e-8, atol=1e-9 * np.abs(Hp).max())
+    np.testing.assert_allclose(F, Fe, rtol=1e-8, atol=1e-9 * np.abs(Fe).max())
+    np.testing.assert_allclose(c, ce, rtol=1e-8, atol=1e-8 * max(1.0, np.abs(ce).max()))
+    assert d in (2, 3)
+
+
+def test_obs_term_is_gaussian_density(dmt):
+    """log rho~(t0, x0) == log N(v; L mu_T(x0), L Sigma_T L' + Sigma) for a linear aux law."""
+    Th = np.array([[0.5, 0.1], [-0.2, 0.7]]); mu = np.array([0.1, -0.3]); sg = 0.4 * np.eye(2)
+    B = -Th; beta = Th @ mu; at = sg @ sg.T
+    L = np.array([[1.0, 0.5]]); Sig = np.array([[0.02]]); v = np.array([0.4])
+    Si = np.linalg.inv(Sig)
+    HT = L.T @ Si @ L; FT = L.T @ Si @ v
+    cT = 0.5 * v @ Si @ v + 0.5 * math.log(2 * math.pi) + 0.5 * math.log(np.linalg.det(Sig))
+    t = np.linspace(0, 1.0, 51)
+    H, F, c = dmt.guiding_linear(B, beta, _packed(at), t, _packed(HT), FT, cT)
+    x0 = np.array([0.3, -0.1])
+    law = np.zeros(64); law[49] = c[0]
+    lo = orc.obs_term(2, law, H[0], F[0], x0)
+    Phi, m_, K = npo.transition_expm(B, beta, at, 1.0)
+    want = npo.gaussian_logpdf(v, L @ (Phi @ x0 + m_), L @ K @ L.T + Sig)
+    assert abs(lo - want) < 1e-11
+
+
+# ---------------------------------------------------------------- Euler recursion + weight
+def _law(model, d, m, theta, sigma, Bt, beta, at_tilde, c0=0.0):
+    from diffusionmcmctools_amd import _lib as L
+    rec = np.zeros(64)
+    rec[:len(theta)] = theta
+    sg = np.asarray(sigma).reshape(d, m)
+    rec[16:16 + d * m] = sg.ravel()
+    a = sg @ sg.T
+    rec[25:25 + d * (d + 1) // 2] = _packed(a)
+    rec[31:31 + d * d] = np.asarray(Bt).ravel()
+    rec[40:40 + d] = beta
+    da = a - at_tilde
+    rec[43:43 + d * (d + 1) // 2] = _packed(da)
+    rec[49] = c0
+    rec[50] = 1.0 if np.any(da != 0) else 0.0
+    assert L.LAW_STRIDE == 64
+    return rec
+
+
+@pytest.mark.parametrize("model", ["ou", "fhn", "lorenz", "ou_trace"])
+def test_c_oracle_matches_naive_numpy(dmt, model):
+    rng = np.random.default_rng(3)
+    from diffusionmcmctools_amd.models import FHN, OU, Lorenz
+    if model in ("ou", "ou_trace"):
+        M = OU([[1.0, 0.3], [-0.3, 0.8]], [0.1, 0.0], 0.5 * np.eye(2))
+        aux = M.aux(Theta_t=np.diag([0.5, 0.5]), sigma_t=(0.6 * np.eye(2) if model == "ou_trace" else None))
+        kind = 0
+    elif model == "fhn":
+        M = FHN(0.1, -0.8, 1.5, 0.0, 0.3); aux = M.aux(-0.8); kind = 1
+    else:
+        M = Lorenz(); aux = M.aux(np.array([1.0, 2.0, 20.0])); kind = 2
+    d, m = M.d, M.m
+    n = 301
+    t = np.linspace(0, 0.1, n)
+    H = rng.uniform(0.5, 2.0, (n, d * (d + 1) // 2)); H[:, 0] += 3
+    F = rng.standard_normal((n, d))
+    W = np.vstack([np.zeros(m), np.cumsum(rng.standard_normal((n - 1, m)) * np.sqrt(np.diff(t))[:, None], 0)])
+    law = M.law_record(aux)
+    y1 = rng.standard_normal(d) * 0.3
+    X, ll, ok = orc.solve_segment(kind, d, m, law, t, H, F, W, y1)
+    Xn, lln = npo.solve_segment_naive(kind, d, m, law, t, H, F, W, y1)
+    assert ok
+    np.testing.assert_allclose(X, Xn, rtol=1e-11, atol=1e-12)
+    assert abs(ll - lln) <= 1e-11 * (1 + abs(lln))
+    # stored-path weight == weight accumulated during the solve (same order, bit for bit)
+    assert orc.path_ll_segment(kind, d, m, law, t, H, F, X) == ll
+
+
+def test_weight_vanishes_when_target_is_aux():
+    """Linear target equal to the auxiliary law: G ≡ 0 up to rounding."""
+    d = m = 2
+    Th = np.array([[1.0, 0.3], [-0.3, 0.8]]); mu = np.zeros(2); sg = 0.5 * np.eye(2)
+    theta = np.zeros(12); theta[:4] = Th.ravel()
+    law = _law(0, d, m, theta, sg, -Th, Th @ mu, sg @ sg.T)
+    rng = np.random.default_rng(1)
+    n = 501; t = np.linspace(0, 1, n)
+    H = np.tile([4.0, 0.5, 3.0], (n, 1)); F = rng.standard_normal((n, 2))
+    W = np.vstack([np.zeros(2), np.cumsum(rng.standard_normal((n - 1, 2)) * 0.0447, 0)])
+    _, ll, ok = orc.solve_segment(0, d, m, law, t, H, F, W, np.zeros(2))
+    assert ok and abs(ll) < 1e-13
+
+
+def test_pcn_limits():
+    rng = np.random.default_rng(2)
+    n, m = 101, 2
+    t = np.linspace(0, 1, n) ** 1.5
+    W = np.vstack([np.zeros(m), np.cumsum(rng.standard_normal((n - 1, m)), 0)])
+    Z = rng.standard_normal((n - 1, m))
+    assert np.array_equal(orc.pcn_segment(m, t, W, Z, 1.0, 0.0), W)          # ρ = 1 reuses W
+    fresh = np.vstack([np.zeros(m), np.cumsum(Z * np.sqrt(np.diff(t))[:, None], 0)])
+    np.testing.assert_allclose(orc.pcn_segment(m, t, W, Z, 0.0, 1.0), fresh, rtol=0, atol=1e-13)
+    rho = 0.8
+    Wo = orc.pcn_segment(m, t, W, Z, rho, math.sqrt(1 - rho ** 2))
+    np.testing.assert_allclose(Wo, rho * W + math.sqrt(1 - rho ** 2) * fresh, atol=1e-13)
+
+
+def test_bridge_hits_endpoint_small_noise(dmt):
+    """Brownian target = aux, exact-ish end observation: the guided path ends at v."""
+    d = m = 1
+    law = _law(0, 1, 1, np.zeros(12), [[1.0]], [[0.0]], [0.0], np.eye(1))
+    n = 2001
+    t = np.linspace(0, 1, n)
+    v, Sig = 1.7, 1e-9
+    H, F, c = dmt.guiding_linear([[0.0]], [0.0], [1.0], t, [1 / Sig], [v / Sig], 0.0)
+    rng = np.random.default_rng(4)
+    W = np.concatenate([[0], np.cumsum(rng.standard_normal(n - 1) * math.sqrt(1 / (n - 1)))])[:, None]
+    X, ll, ok = orc.solve_segment(0, 1, 1, law, t, H, F, W, np.zeros(1))
+    assert ok and abs(X[-1, 0] - v) < 0.05
+
+
+def test_pairwise_tree_order():
+    v = [1e16, 1.0, -1e16, 1.0]
+    assert orc.pairwise_tree(v) == (1e16 + 1.0) + (-1e16 + 1.0)
+    assert orc.pairwise_tree([]) == 0.0
+    assert orc.pairwise_tree([3.0, 4.0, 5.0]) == (3.0 + 4.0) + (5.0 + 0.0)
