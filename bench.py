@@ -110,6 +110,8 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--mapping", default="auto", choices=["auto", "lane", "wave"],
+                    help="thread mapping of the Euler recursion (DESIGN.md §2)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -127,8 +129,10 @@ def main():
 
     w = build_workload(args.config, rank)
     w.meta["hist_len"] = args.warmup + args.steps
+    mapping = {"auto": L.MAP_AUTO, "lane": L.MAP_LANE, "wave": L.MAP_WAVE}[args.mapping]
     ens = dmt.Ensemble(w.model.kind, w.d, w.m, w.n_points, precision=w.precision,
-                       seed=0xD1FF + 7919 * rank, device=local_rank, grid_shared=w.grid_shared)
+                       seed=0xD1FF + 7919 * rank, device=local_rank, grid_shared=w.grid_shared,
+                       mapping=mapping)
     lay = W.fill(ens, w, init_Z=False)
     B = w.nblocks
     if world > 1:
@@ -195,6 +199,7 @@ def main():
             "config": {"workload": desc, "blocks_per_gpu": B,
                        "euler_steps_per_block": w.steps_per_iter // B, "rho": w.rho,
                        "parallelism": f"blockensemble-shard x{world}",
+                       "mapping": args.mapping,
                        "rng": "device Philox4x32-10 + Box-Muller (perf mode)"},
             "per_gpu": value / world,
             "accept_rate": accept_rate,

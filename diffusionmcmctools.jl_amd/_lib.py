@@ -18,6 +18,7 @@ INCLUDE_H = os.path.join(os.path.dirname(HERE), "include", "dmt.h")
 OK, ERR_INVALID, ERR_HIP, ERR_OOM, ERR_STATE, ERR_COMM = 0, 1, 2, 3, 4, 5
 MODEL_OU, MODEL_FHN, MODEL_LORENZ = 0, 1, 2
 F64, F32 = 0, 1
+MAP_AUTO, MAP_LANE, MAP_WAVE = 0, 1, 2
 U, UPROP = 0, 1
 LAW_PP, LAW_PPB = 0, 1
 SWAP_XX, SWAP_WW, SWAP_PP, SWAP_LL = 1, 2, 4, 8
@@ -54,7 +55,8 @@ class dmt_structure(C.Structure):
 
 
 class dmt_config(C.Structure):
-    _fields_ = [("seed", C.c_uint64), ("device", C.c_int32), ("grid_shared", C.c_int32)]
+    _fields_ = [("seed", C.c_uint64), ("device", C.c_int32), ("grid_shared", C.c_int32),
+                ("mapping", C.c_int32)]
 
 
 if not os.path.exists(LIB_PATH):

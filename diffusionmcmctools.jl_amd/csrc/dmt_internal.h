@@ -9,6 +9,8 @@ constexpr int kLanes = 64;  // one recording per lane of a wave64 ("recording ti
 // spare point rows at the end of every tile (and of shared tables): the software
 // prefetch reads up to 2*kChunk points past a segment end without bounds checks
 constexpr int kPadPoints = 16;
+// MAP_AUTO picks MAP_WAVE up to this many recordings (see DESIGN.md §2 for the measurement)
+constexpr int64_t kAutoWaveMaxRecordings = 8192;
 
 // Kernel modes of the per-block recursion kernel.
 enum Mode : int {
@@ -17,11 +19,18 @@ enum Mode : int {
   MODE_FRESH = 2,      // draw_proposal_path!(u::SamplingUnit): fresh W (ρ = 0), in place
 };
 
-// Arguments of the block kernels.  Device-path arrays are "recording-tile planes":
-// element (recording r, point q of r, component c) of an array with C components lives at
-//   ((tile_qoff[r/64] + q) * C + c) * 64 + r%64
-// so the 64 lanes of a wave (64 recordings of one tile, same block index) touch 64
-// consecutive elements per component: every load/store is a coalesced 512 B (fp64) access.
+// Thread mappings of the recursion (chosen per ensemble at dmt_create):
+//   MAP_LANE: one lane per (recording, block); tile width tw = 64 recordings
+//   MAP_WAVE: one wavefront per block, 64 consecutive steps per chunk; tw = 1
+enum Mapping : int { MAP_AUTO = 0, MAP_LANE = 1, MAP_WAVE = 2 };
+
+// Arguments of the block kernels.  Device-path arrays are "recording-tile planes" of tile
+// width tw: element (recording r, point q of r, component c) of an array with C components
+// lives at   ((tile_qoff[r/tw] + q) * C + c) * tw + r%tw.
+// tw = 64 (MAP_LANE): the 64 lanes of a wave (64 recordings of one tile, same block index)
+// touch 64 consecutive elements per component — one coalesced 512 B (fp64) access.
+// tw = 1 (MAP_WAVE): recording-major, point-major, components interleaved (the reference's
+// own Vector{SVector{d}} layout) — a wave's 64 lanes touch 64 consecutive points.
 template <class T>
 struct BlockArgs {
   int64_t R;
@@ -43,6 +52,7 @@ struct BlockArgs {
   const double* law[2][2];
   // layout
   const int64_t* blk_off;  // [R + 1]
+  const int32_t* blk_rec;  // [nblocks] recording of each block
   const int32_t* gfirst;   // [nblocks] global segment ids
   const int32_t* glast;
   const uint8_t* term;
@@ -85,16 +95,17 @@ struct ModelKey {
 };
 
 // launchers (dmt_kernels.hip)
-hipError_t launch_block_kernel(const ModelKey& k, int mode, const void* args, int64_t nwaves,
-                               hipStream_t s);
-hipError_t launch_pathll_kernel(const ModelKey& k, const void* args, int64_t nwaves, hipStream_t s);
+hipError_t launch_block_kernel(const ModelKey& k, int mapping, int mode, const void* args,
+                               int64_t nwaves, hipStream_t s);
+hipError_t launch_pathll_kernel(const ModelKey& k, int mapping, const void* args, int64_t nwaves,
+                                hipStream_t s);
 hipError_t launch_accept(const AcceptArgs& a, hipStream_t s);
-hipError_t launch_to_planes(int precision, const double* src, void* dst0, void* dst1,
+hipError_t launch_to_planes(int precision, int tw, const double* src, void* dst0, void* dst1,
                             const uint8_t* sel, int flip, int C, int64_t P, const int64_t* pt_off,
                             int64_t G, const int32_t* seg_rec, const int32_t* seg_q,
                             const int64_t* tile_qoff, hipStream_t s);
-hipError_t launch_from_planes(int precision, double* dst, const void* src0, const void* src1,
-                              const uint8_t* sel, int flip, int C, int64_t P,
+hipError_t launch_from_planes(int precision, int tw, double* dst, const void* src0,
+                              const void* src1, const uint8_t* sel, int flip, int C, int64_t P,
                               const int64_t* pt_off, int64_t G, const int32_t* seg_rec,
                               const int32_t* seg_q, const int64_t* tile_qoff, hipStream_t s);
 hipError_t launch_cast(int precision, const double* src, void* dst, int64_t n, hipStream_t s);

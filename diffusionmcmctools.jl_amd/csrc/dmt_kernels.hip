@@ -278,6 +278,275 @@ __global__ __launch_bounds__(64) void k_pathll(const BlockArgs<T> a) {
   a.ll_out[blk] = (double)ll;
 }
 
+// ================================================================ MAP_WAVE kernels
+// One wavefront per block (tw = 1 layout).  Per chunk of 64 consecutive steps:
+//   phase A (lane-parallel): lane j loads step c0+j's grid, guiding term and accepted W,
+//            draws its normals (Philox + Box–Muller) and writes one LDS row;
+//   phase S (serial, uniform): the Euler recursion over the 64 rows, every lane computing
+//            the same values from broadcast LDS reads; lane j captures x_j and W°_{j+1};
+//   phase B (lane-parallel): lane j evaluates G(t_j, x_j)·dt_j, a 64-lane adjacent-pair
+//            xor-shuffle tree gives the chunk sum (= the canonical chunk tree), and every
+//            lane stores its point: coalesced writes of the path.
+template <class T>
+__device__ __forceinline__ T wave_tree_sum(T v) {
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) v = v + __shfl_xor(v, off, 64);
+  return v;
+}
+
+template <class Mdl, class T, int MODE>
+__device__ __forceinline__ bool run_segment_wave(
+    const Law<Mdl, T>& L, const T* __restrict__ tpl, const int t_sh, const T* __restrict__ Ht,
+    const int H_sh, const T* __restrict__ Ft, const T* __restrict__ Ws, T* __restrict__ Wd,
+    T* __restrict__ Xd, const double* __restrict__ Zg, const uint64_t seed, const uint32_t g,
+    const uint32_t iter, const uint32_t salt, const int64_t row, const int64_t q0, const int np,
+    const int lane, const T rho, const T srho, T* x, T& sl, T* lds) {
+  constexpr int D = Mdl::D, M = Mdl::M, HP = D * (D + 1) / 2;
+  constexpr int NR = 2 + 2 * M + HP + D;  // dt, sdt, Z[M], W[M], H[HP], F[D]
+  constexpr int NRP = (NR + 1) & ~1;      // 16-byte rows for fp64
+  const T* tb = t_sh ? tpl + q0 : tpl + row;
+  const T* Hb = H_sh ? Ht + q0 * HP : Ht + row * HP;
+  const T* Fb = Ft + row * D;
+  const T* Wsb = Ws + row * M;
+  T* Wdb = Wd + row * M;
+  T* Xdb = Xd + row * D;
+  const int nst = np - 1;
+
+  T wf[M], wprev[M];
+#pragma unroll
+  for (int k = 0; k < M; ++k) {
+    wf[k] = (T)0;
+    T w0 = (MODE == MODE_FRESH) ? (T)0 : Wsb[k];
+    wprev[k] = (MODE == MODE_RECOMPUTE) ? w0 : dfma(rho, w0, srho * wf[k]);
+  }
+  if (MODE != MODE_RECOMPUTE && lane == 0) {
+#pragma unroll
+    for (int k = 0; k < M; ++k) Wdb[k] = wprev[k];
+  }
+  T acc = (T)0;
+  const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32), c3 = salt << 1;
+  for (int c0 = 0; c0 < nst; c0 += 64) {
+    const int cnt = nst - c0 < 64 ? nst - c0 : 64;
+    const bool valid = lane < cnt;
+    const int i = c0 + (valid ? lane : cnt - 1);
+    // ---- phase A
+    const T tl = tb[i], tr = tb[i + 1];
+    const T dt = tr - tl;
+    T Hi[HP], Fi[D], Wi[M], Zi[M];
+#pragma unroll
+    for (int c = 0; c < HP; ++c) Hi[c] = Hb[(int64_t)i * HP + c];
+#pragma unroll
+    for (int c = 0; c < D; ++c) Fi[c] = Fb[(int64_t)i * D + c];
+#pragma unroll
+    for (int k = 0; k < M; ++k) Wi[k] = (MODE == MODE_FRESH) ? (T)0 : Wsb[(int64_t)(i + 1) * M + k];
+    T sdt = (T)0;
+    if (MODE != MODE_RECOMPUTE) {
+      sdt = sqrt(dt);
+      uint32_t have = 0xFFFFFFFFu;
+      T z0 = (T)0, z1 = (T)0;
+#pragma unroll
+      for (int k = 0; k < M; ++k) {
+        const uint32_t n = (uint32_t)(i * M + k);
+        if (Zg) {
+          Zi[k] = (T)Zg[(int64_t)i * M + k];
+        } else {
+          if ((n >> 1) != have) {
+            U4 o = philox4x32_10(U4{n >> 1, g, iter, c3}, k0, k1);
+            normal_pair(o, z0, z1);
+            have = n >> 1;
+          }
+          Zi[k] = (n & 1u) ? z1 : z0;
+        }
+      }
+    }
+    T* rw = lds + lane * NRP;
+    rw[0] = dt;
+    rw[1] = sdt;
+#pragma unroll
+    for (int k = 0; k < M; ++k) { rw[2 + k] = (MODE == MODE_RECOMPUTE) ? (T)0 : Zi[k]; rw[2 + M + k] = Wi[k]; }
+#pragma unroll
+    for (int c = 0; c < HP; ++c) rw[2 + 2 * M + c] = Hi[c];
+#pragma unroll
+    for (int c = 0; c < D; ++c) rw[2 + 2 * M + HP + c] = Fi[c];
+    __syncthreads();
+    // ---- phase S
+    T xc[D], wc[M];
+#pragma unroll
+    for (int p = 0; p < D; ++p) xc[p] = x[p];
+#pragma unroll
+    for (int k = 0; k < M; ++k) wc[k] = wprev[k];
+#pragma unroll 4
+    for (int s = 0; s < cnt; ++s) {
+      const T* q = lds + s * NRP;
+      const T dts = q[0];
+      T dW[M];
+#pragma unroll
+      for (int k = 0; k < M; ++k) {
+        T wn;
+        if (MODE == MODE_RECOMPUTE) {
+          wn = q[2 + M + k];
+        } else {
+          wf[k] = dfma(q[1], q[2 + k], wf[k]);
+          wn = dfma(rho, q[2 + M + k], srho * wf[k]);
+        }
+        dW[k] = wn - wprev[k];
+        wprev[k] = wn;
+      }
+      T r[D], b[D];
+#pragma unroll
+      for (int p = 0; p < D; ++p) {
+        T a_ = q[2 + 2 * M + HP + p];
+#pragma unroll
+        for (int c = 0; c < D; ++c) a_ = dfma(-q[2 + 2 * M + packed_idx(D, p, c)], x[c], a_);
+        r[p] = a_;
+      }
+      Mdl::drift(L.th, x, b);
+      const bool mine = (lane == s);
+#pragma unroll
+      for (int p = 0; p < D; ++p) xc[p] = mine ? x[p] : xc[p];
+#pragma unroll
+      for (int k = 0; k < M; ++k) wc[k] = mine ? wprev[k] : wc[k];
+      euler_step<Mdl, T>(L, r, b, dts, dW, x);
+    }
+    __syncthreads();
+    // ---- phase B
+    T rr[D], bb[D];
+    const T G = g_at<Mdl, T>(L, Hi, Fi, xc, rr, bb);
+    const T csum = wave_tree_sum<T>(valid ? G * dt : (T)0);
+    acc = acc + (csum + (T)0);
+    if (valid) {
+#pragma unroll
+      for (int p = 0; p < D; ++p) Xdb[(int64_t)i * D + p] = xc[p];
+      if (MODE != MODE_RECOMPUTE) {
+#pragma unroll
+        for (int k = 0; k < M; ++k) Wdb[(int64_t)(i + 1) * M + k] = wc[k];
+      }
+    }
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int p = 0; p < D; ++p) Xdb[(int64_t)nst * D + p] = x[p];
+  }
+  sl = acc;
+  bool ok = isfinite(sl);
+#pragma unroll
+  for (int p = 0; p < D; ++p) ok = ok && isfinite(x[p]);
+  return ok;
+}
+
+template <class Mdl, class T, int MODE>
+__global__ __launch_bounds__(64) void k_block_wave(const BlockArgs<T> a) {
+  constexpr int D = Mdl::D, M = Mdl::M, HP = D * (D + 1) / 2;
+  constexpr int NRP = ((2 + 2 * M + HP + D) + 1) & ~1;
+  __shared__ T lds[64 * NRP];
+  const int lane = threadIdx.x;
+  const int64_t blk = a.b0 + (int64_t)blockIdx.x;
+  if (blk >= a.b1) return;
+  const int64_t r = a.blk_rec[blk];
+  const int64_t tq = a.tile_qoff[r];
+  const int g0 = a.gfirst[blk], g1 = a.glast[blk];
+  const bool term = a.term[blk] != 0;
+  T x[D];
+  {
+    const T* Xs = a.X[a.selX[g0] ^ a.xs_flip];
+    const int64_t q = a.seg_q[g0];
+#pragma unroll
+    for (int p = 0; p < D; ++p) x[p] = Xs[(tq + q) * D + p];
+  }
+  T ll;
+  {
+    const int ls = a.selPP[g0] ^ a.law_flip;
+    const double* Lr = a.law[ls][0] + (int64_t)g0 * DMT_LAW_STRIDE;
+    const int64_t q = a.seg_q[g0];
+    T H0[HP], F0[D];
+#pragma unroll
+    for (int c = 0; c < HP; ++c)
+      H0[c] = a.H_shared[ls][0] ? a.H[ls][0][q * HP + c] : a.H[ls][0][(tq + q) * HP + c];
+#pragma unroll
+    for (int c = 0; c < D; ++c) F0[c] = a.F[ls][0][(tq + q) * D + c];
+    ll = obs_term<D, T>(H0, F0, x, (T)Lr[DMT_LAW_C0]);
+  }
+  bool ok = true;
+  const T rho = (MODE == MODE_FRESH) ? (T)0 : (T)a.rho[blk];
+  const T srho = (MODE == MODE_FRESH) ? (T)1 : (T)a.srho[blk];
+  for (int g = g0; g <= g1; ++g) {
+    const int kind = (!term && g == g1) ? 1 : 0;
+    const int ls = (kind ? a.selPPB[g] : a.selPP[g]) ^ a.law_flip;
+    Law<Mdl, T> L;
+    L.load(a.law[ls][kind] + (int64_t)g * DMT_LAW_STRIDE);
+    const double* Zg = a.Z ? a.Z + a.st_off[g] * M : nullptr;
+    T* Xd = a.X[a.selX[g] ^ a.xd_flip];
+    const T* Ws = a.W[a.selW[g] ^ a.ws_flip];
+    T* Wd = a.W[a.selW[g] ^ a.wd_flip];
+    const int64_t q0 = a.seg_q[g];
+    T sl;
+    const bool sok = run_segment_wave<Mdl, T, MODE>(
+        L, a.t, a.t_shared, a.H[ls][kind], a.H_shared[ls][kind], a.F[ls][kind], Ws, Wd, Xd, Zg,
+        a.seed, (uint32_t)g, a.iter, a.salt, tq + q0, q0, a.seg_np[g], lane, rho, srho, x, sl, lds);
+    if (!sok) { ok = false; break; }
+    ll = ll + sl;
+  }
+  if (lane == 0) {
+    a.ll_out[blk] = ok ? (double)ll : -INFINITY;
+    if (a.success) a.success[blk] = ok ? 1 : 0;
+  }
+}
+
+template <class Mdl, class T>
+__global__ __launch_bounds__(64) void k_pathll_wave(const BlockArgs<T> a) {
+  constexpr int D = Mdl::D, HP = D * (D + 1) / 2;
+  const int lane = threadIdx.x;
+  const int64_t blk = a.b0 + (int64_t)blockIdx.x;
+  if (blk >= a.b1) return;
+  const int64_t r = a.blk_rec[blk];
+  const int64_t tq = a.tile_qoff[r];
+  const int g0 = a.gfirst[blk], g1 = a.glast[blk];
+  const bool term = a.term[blk] != 0;
+  T ll;
+  {
+    const int ls = a.selPP[g0] ^ a.law_flip;
+    const double* Lr = a.law[ls][0] + (int64_t)g0 * DMT_LAW_STRIDE;
+    const T* Xs = a.X[a.selX[g0] ^ a.xs_flip];
+    const int64_t q = a.seg_q[g0];
+    T H0[HP], F0[D], x0[D];
+#pragma unroll
+    for (int c = 0; c < HP; ++c)
+      H0[c] = a.H_shared[ls][0] ? a.H[ls][0][q * HP + c] : a.H[ls][0][(tq + q) * HP + c];
+#pragma unroll
+    for (int c = 0; c < D; ++c) { F0[c] = a.F[ls][0][(tq + q) * D + c]; x0[c] = Xs[(tq + q) * D + c]; }
+    ll = obs_term<D, T>(H0, F0, x0, (T)Lr[DMT_LAW_C0]);
+  }
+  for (int g = g0; g <= g1; ++g) {
+    const int kind = (!term && g == g1) ? 1 : 0;
+    const int ls = (kind ? a.selPPB[g] : a.selPP[g]) ^ a.law_flip;
+    Law<Mdl, T> L;
+    L.load(a.law[ls][kind] + (int64_t)g * DMT_LAW_STRIDE);
+    const int64_t q0 = a.seg_q[g], row = tq + q0;
+    const T* tb = a.t_shared ? a.t + q0 : a.t + row;
+    const T* Hb = a.H_shared[ls][kind] ? a.H[ls][kind] + q0 * HP : a.H[ls][kind] + row * HP;
+    const T* Fb = a.F[ls][kind] + row * D;
+    const T* Xb = a.X[a.selX[g] ^ a.xs_flip] + row * D;
+    const int nst = a.seg_np[g] - 1;
+    T acc = (T)0;
+    for (int c0 = 0; c0 < nst; c0 += 64) {
+      const int cnt = nst - c0 < 64 ? nst - c0 : 64;
+      const bool valid = lane < cnt;
+      const int i = c0 + (valid ? lane : cnt - 1);
+      const T dt = tb[i + 1] - tb[i];
+      T Hi[HP], Fi[D], xi[D], rr[D], bb[D];
+#pragma unroll
+      for (int c = 0; c < HP; ++c) Hi[c] = Hb[(int64_t)i * HP + c];
+#pragma unroll
+      for (int c = 0; c < D; ++c) { Fi[c] = Fb[(int64_t)i * D + c]; xi[c] = Xb[(int64_t)i * D + c]; }
+      const T G = g_at<Mdl, T>(L, Hi, Fi, xi, rr, bb);
+      const T csum = wave_tree_sum<T>(valid ? G * dt : (T)0);
+      acc = acc + (csum + (T)0);
+    }
+    ll = ll + acc;
+  }
+  if (lane == 0) a.ll_out[blk] = (double)ll;
+}
+
 // ---------------------------------------------------------------- accept / reject
 __global__ __launch_bounds__(256) void k_accept(const AcceptArgs a) {
   const int64_t blk = a.b0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -340,7 +609,7 @@ __device__ __forceinline__ int64_t find_seg(const int64_t* pt_off, int64_t G, in
 }
 
 template <class T>
-__global__ void k_to_planes(const double* __restrict__ src, T* dst0, T* dst1,
+__global__ void k_to_planes(const int tw, const double* __restrict__ src, T* dst0, T* dst1,
                             const uint8_t* __restrict__ sel, int flip, int C, int64_t P,
                             const int64_t* __restrict__ pt_off, int64_t G,
                             const int32_t* __restrict__ seg_rec, const int32_t* __restrict__ seg_q,
@@ -352,13 +621,13 @@ __global__ void k_to_planes(const double* __restrict__ src, T* dst0, T* dst1,
   const int64_t g = find_seg(pt_off, G, p);
   const int64_t r = seg_rec[g];
   const int64_t q = seg_q[g] + (p - pt_off[g]);
-  const int64_t o = ((tile_qoff[r >> 6] + q) * C + c) * kLanes + (r & 63);
+  const int64_t o = ((tile_qoff[r / tw] + q) * C + c) * tw + (r % tw);
   const int slot = sel ? ((sel[g] ^ flip) & 1) : 0;
   (slot ? dst1 : dst0)[o] = (T)src[e];
 }
 
 template <class T>
-__global__ void k_from_planes(double* __restrict__ dst, const T* src0, const T* src1,
+__global__ void k_from_planes(const int tw, double* __restrict__ dst, const T* src0, const T* src1,
                               const uint8_t* __restrict__ sel, int flip, int C, int64_t P,
                               const int64_t* __restrict__ pt_off, int64_t G,
                               const int32_t* __restrict__ seg_rec,
@@ -371,7 +640,7 @@ __global__ void k_from_planes(double* __restrict__ dst, const T* src0, const T* 
   const int64_t g = find_seg(pt_off, G, p);
   const int64_t r = seg_rec[g];
   const int64_t q = seg_q[g] + (p - pt_off[g]);
-  const int64_t o = ((tile_qoff[r >> 6] + q) * C + c) * kLanes + (r & 63);
+  const int64_t o = ((tile_qoff[r / tw] + q) * C + c) * tw + (r % tw);
   const int slot = sel ? ((sel[g] ^ flip) & 1) : 0;
   dst[e] = (double)(slot ? src1 : src0)[o];
 }
@@ -462,10 +731,20 @@ static inline unsigned nblk(int64_t n, int bs) { return (unsigned)((n + bs - 1) 
 constexpr int kChunk = 4;
 
 template <class Mdl, class T>
-static hipError_t launch_block_t(int mode, const void* args, int64_t nwaves, hipStream_t s) {
+static hipError_t launch_block_t(int mapping, int mode, const void* args, int64_t nwaves,
+                                 hipStream_t s) {
   const BlockArgs<T>& a = *static_cast<const BlockArgs<T>*>(args);
   if (nwaves <= 0) return hipSuccess;
   dim3 grid((unsigned)nwaves), block(64);
+  if (mapping == MAP_WAVE) {
+    switch (mode) {
+      case MODE_PCN: k_block_wave<Mdl, T, MODE_PCN><<<grid, block, 0, s>>>(a); break;
+      case MODE_RECOMPUTE: k_block_wave<Mdl, T, MODE_RECOMPUTE><<<grid, block, 0, s>>>(a); break;
+      case MODE_FRESH: k_block_wave<Mdl, T, MODE_FRESH><<<grid, block, 0, s>>>(a); break;
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
   switch (mode) {
     case MODE_PCN: k_block<Mdl, T, MODE_PCN, kChunk><<<grid, block, 0, s>>>(a); break;
     case MODE_RECOMPUTE: k_block<Mdl, T, MODE_RECOMPUTE, kChunk><<<grid, block, 0, s>>>(a); break;
@@ -476,10 +755,13 @@ static hipError_t launch_block_t(int mode, const void* args, int64_t nwaves, hip
 }
 
 template <class Mdl, class T>
-static hipError_t launch_pathll_t(const void* args, int64_t nwaves, hipStream_t s) {
+static hipError_t launch_pathll_t(int mapping, const void* args, int64_t nwaves, hipStream_t s) {
   const BlockArgs<T>& a = *static_cast<const BlockArgs<T>*>(args);
   if (nwaves <= 0) return hipSuccess;
-  k_pathll<Mdl, T, kChunk><<<dim3((unsigned)nwaves), dim3(64), 0, s>>>(a);
+  if (mapping == MAP_WAVE)
+    k_pathll_wave<Mdl, T><<<dim3((unsigned)nwaves), dim3(64), 0, s>>>(a);
+  else
+    k_pathll<Mdl, T, kChunk><<<dim3((unsigned)nwaves), dim3(64), 0, s>>>(a);
   return hipGetLastError();
 }
 
@@ -513,14 +795,14 @@ static hipError_t launch_pathll_t(const void* args, int64_t nwaves, hipStream_t 
     return hipErrorInvalidValue;                                                       \
   } while (0)
 
-hipError_t launch_block_kernel(const ModelKey& k, int mode, const void* args, int64_t nwaves,
-                               hipStream_t s) {
-  DMT_DISPATCH(k, (launch_block_t<Mdl, T>(mode, args, nwaves, s)));
+hipError_t launch_block_kernel(const ModelKey& k, int mapping, int mode, const void* args,
+                               int64_t nwaves, hipStream_t s) {
+  DMT_DISPATCH(k, (launch_block_t<Mdl, T>(mapping, mode, args, nwaves, s)));
 }
 
-hipError_t launch_pathll_kernel(const ModelKey& k, const void* args, int64_t nwaves,
+hipError_t launch_pathll_kernel(const ModelKey& k, int mapping, const void* args, int64_t nwaves,
                                 hipStream_t s) {
-  DMT_DISPATCH(k, (launch_pathll_t<Mdl, T>(args, nwaves, s)));
+  DMT_DISPATCH(k, (launch_pathll_t<Mdl, T>(mapping, args, nwaves, s)));
 }
 
 hipError_t launch_accept(const AcceptArgs& a, hipStream_t s) {
@@ -530,33 +812,33 @@ hipError_t launch_accept(const AcceptArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_to_planes(int precision, const double* src, void* dst0, void* dst1,
+hipError_t launch_to_planes(int precision, int tw, const double* src, void* dst0, void* dst1,
                             const uint8_t* sel, int flip, int C, int64_t P, const int64_t* pt_off,
                             int64_t G, const int32_t* seg_rec, const int32_t* seg_q,
                             const int64_t* tile_qoff, hipStream_t s) {
   const int64_t n = P * C;
   if (n <= 0) return hipSuccess;
   if (precision == DMT_F64)
-    k_to_planes<double><<<nblk(n, 256), 256, 0, s>>>(src, (double*)dst0, (double*)dst1, sel, flip,
+    k_to_planes<double><<<nblk(n, 256), 256, 0, s>>>(tw, src, (double*)dst0, (double*)dst1, sel, flip,
                                                       C, P, pt_off, G, seg_rec, seg_q, tile_qoff);
   else
-    k_to_planes<float><<<nblk(n, 256), 256, 0, s>>>(src, (float*)dst0, (float*)dst1, sel, flip, C,
+    k_to_planes<float><<<nblk(n, 256), 256, 0, s>>>(tw, src, (float*)dst0, (float*)dst1, sel, flip, C,
                                                      P, pt_off, G, seg_rec, seg_q, tile_qoff);
   return hipGetLastError();
 }
 
-hipError_t launch_from_planes(int precision, double* dst, const void* src0, const void* src1,
+hipError_t launch_from_planes(int precision, int tw, double* dst, const void* src0, const void* src1,
                               const uint8_t* sel, int flip, int C, int64_t P,
                               const int64_t* pt_off, int64_t G, const int32_t* seg_rec,
                               const int32_t* seg_q, const int64_t* tile_qoff, hipStream_t s) {
   const int64_t n = P * C;
   if (n <= 0) return hipSuccess;
   if (precision == DMT_F64)
-    k_from_planes<double><<<nblk(n, 256), 256, 0, s>>>(dst, (const double*)src0,
+    k_from_planes<double><<<nblk(n, 256), 256, 0, s>>>(tw, dst, (const double*)src0,
                                                         (const double*)src1, sel, flip, C, P,
                                                         pt_off, G, seg_rec, seg_q, tile_qoff);
   else
-    k_from_planes<float><<<nblk(n, 256), 256, 0, s>>>(dst, (const float*)src0, (const float*)src1,
+    k_from_planes<float><<<nblk(n, 256), 256, 0, s>>>(tw, dst, (const float*)src0, (const float*)src1,
                                                        sel, flip, C, P, pt_off, G, seg_rec, seg_q,
                                                        tile_qoff);
   return hipGetLastError();

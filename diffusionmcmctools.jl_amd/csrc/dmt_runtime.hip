@@ -51,9 +51,10 @@ struct Layout {
   int32_t MB = 0;
   int64_t hist_len = 0;
   std::vector<int64_t> blk_off;  // [R + 1]
-  std::vector<int32_t> gfirst, glast;
+  std::vector<int32_t> gfirst, glast, blk_rec;
   std::vector<uint8_t> term;
   int64_t* d_blk_off = nullptr;
+  int32_t* d_blk_rec = nullptr;
   int32_t* d_gfirst = nullptr;
   int32_t* d_glast = nullptr;
   uint8_t* d_term = nullptr;
@@ -67,7 +68,7 @@ struct Layout {
   uint8_t* d_success = nullptr;
   uint8_t* d_acc = nullptr;
   void release() {
-    void* ps[] = {d_blk_off, d_gfirst, d_glast, d_term, d_rho, d_srho, d_ll,
+    void* ps[] = {d_blk_off, d_blk_rec, d_gfirst, d_glast, d_term, d_rho, d_srho, d_ll,
                   d_llp,     d_llh,    d_llph,  d_acch, d_success, d_acc};
     for (void* p : ps)
       if (p) (void)hipFree(p);
@@ -83,6 +84,8 @@ struct dmt_ens {
   int device = 0;
   uint64_t seed = 0;
   int grid_shared = 0;
+  int mapping = MAP_LANE;  // thread mapping of the recursion kernels
+  int tw = kLanes;         // tile width of the device layout (64 lane-mapped, 1 wave-mapped)
   hipStream_t stream = nullptr;
   // structure
   int64_t R = 0, G = 0, P = 0, S = 0, ntiles = 0, Ptile = 0, Q0 = 0;
@@ -220,7 +223,7 @@ dmt_status ensure_Z(dmt_ens* h, int64_t n) {
   return DMT_OK;
 }
 
-int64_t plane_elems(const dmt_ens* h, int C) { return h->Ptile * C * kLanes; }
+int64_t plane_elems(const dmt_ens* h, int C) { return h->Ptile * C * h->tw; }
 
 dmt_status check_h(dmt_ens* h) {
   if (!h) return fail(DMT_ERR_INVALID, "null handle");
@@ -285,6 +288,7 @@ void fill_common(dmt_ens* h, const Layout* L, BlockArgs<T>& a) {
   a.t = (const T*)h->d_t;
   a.t_shared = h->grid_shared;
   a.blk_off = L->d_blk_off;
+  a.blk_rec = L->d_blk_rec;
   a.gfirst = L->d_gfirst;
   a.glast = L->d_glast;
   a.term = L->d_term;
@@ -303,7 +307,8 @@ dmt_status run_block_kernel(dmt_ens* h, const Layout* L, int mode, int kind_time
   if (b1 <= b0) return DMT_OK;
   const int64_t r0 = rec_of_block(L, b0), r1 = rec_of_block(L, b1 - 1);
   const int64_t tile0 = r0 / kLanes, tile1 = r1 / kLanes + 1;
-  const int64_t nwaves = (tile1 - tile0) * (int64_t)L->MB;
+  // MAP_LANE: one wave per (recording tile, block index); MAP_WAVE: one wave per block
+  const int64_t nwaves = h->mapping == MAP_WAVE ? (b1 - b0) : (tile1 - tile0) * (int64_t)L->MB;
   TimedScope ts(h, kind_timer);
   hipError_t e;
   auto fill = [&](auto& a) {
@@ -326,13 +331,13 @@ dmt_status run_block_kernel(dmt_ens* h, const Layout* L, int mode, int kind_time
   if (h->key.precision == DMT_F64) {
     BlockArgs<double> a{};
     fill(a);
-    e = pathll ? launch_pathll_kernel(h->key, &a, nwaves, h->stream)
-               : launch_block_kernel(h->key, mode, &a, nwaves, h->stream);
+    e = pathll ? launch_pathll_kernel(h->key, h->mapping, &a, nwaves, h->stream)
+               : launch_block_kernel(h->key, h->mapping, mode, &a, nwaves, h->stream);
   } else {
     BlockArgs<float> a{};
     fill(a);
-    e = pathll ? launch_pathll_kernel(h->key, &a, nwaves, h->stream)
-               : launch_block_kernel(h->key, mode, &a, nwaves, h->stream);
+    e = pathll ? launch_pathll_kernel(h->key, h->mapping, &a, nwaves, h->stream)
+               : launch_block_kernel(h->key, h->mapping, mode, &a, nwaves, h->stream);
   }
   if (e != hipSuccess) return fail(DMT_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(e));
   return DMT_OK;
@@ -362,6 +367,7 @@ dmt_status build_layout(dmt_ens* h, const int32_t* n_blocks, const int32_t* seg_
   L->hist_len = hist_len < 0 ? 0 : hist_len;
   L->gfirst.resize(L->nblocks);
   L->glast.resize(L->nblocks);
+  L->blk_rec.resize(L->nblocks);
   L->term.resize(L->nblocks);
   std::vector<double> srho(L->nblocks), rr(L->nblocks);
   for (int64_t r = 0; r < h->R; ++r) {
@@ -375,6 +381,7 @@ dmt_status build_layout(dmt_ens* h, const int32_t* n_blocks, const int32_t* seg_
       L->gfirst[b] = (int32_t)(h->rec_seg0[r] + seg_first[b]);
       L->glast[b] = (int32_t)(h->rec_seg0[r] + seg_last[b]);
       L->term[b] = last[b] ? 1 : 0;
+      L->blk_rec[b] = (int32_t)r;
       rr[b] = rho[b];
       if (!(rho[b] >= 0.0 && rho[b] <= 1.0)) return fail(DMT_ERR_INVALID, "rho outside [0,1]");
       srho[b] = std::sqrt(1.0 - rho[b] * rho[b]);
@@ -383,6 +390,7 @@ dmt_status build_layout(dmt_ens* h, const int32_t* n_blocks, const int32_t* seg_
   const int64_t nb = L->nblocks;
   DMT_TRY(ens_alloc(h, &L->d_blk_off, h->R + 1));
   DMT_TRY(ens_alloc(h, &L->d_gfirst, nb));
+  DMT_TRY(ens_alloc(h, &L->d_blk_rec, nb));
   DMT_TRY(ens_alloc(h, &L->d_glast, nb));
   DMT_TRY(ens_alloc(h, &L->d_term, nb));
   DMT_TRY(ens_alloc(h, &L->d_rho, nb));
@@ -402,6 +410,7 @@ dmt_status build_layout(dmt_ens* h, const int32_t* n_blocks, const int32_t* seg_
   HIP_OK(hipMemcpy(L->d_blk_off, L->blk_off.data(), (h->R + 1) * 8, hipMemcpyHostToDevice));
   if (nb > 0) {
     HIP_OK(hipMemcpy(L->d_gfirst, L->gfirst.data(), nb * 4, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(L->d_blk_rec, L->blk_rec.data(), nb * 4, hipMemcpyHostToDevice));
     HIP_OK(hipMemcpy(L->d_glast, L->glast.data(), nb * 4, hipMemcpyHostToDevice));
     HIP_OK(hipMemcpy(L->d_term, L->term.data(), nb, hipMemcpyHostToDevice));
     HIP_OK(hipMemcpy(L->d_rho, rr.data(), nb * 8, hipMemcpyHostToDevice));
@@ -596,11 +605,17 @@ dmt_status dmt_create(dmt_ens** out, const dmt_model* model, const dmt_structure
           return fail(DMT_ERR_INVALID, "grid_shared requires identical segment structure");
     }
   }
-  h->ntiles = (h->R + kLanes - 1) / kLanes;
+  // Mapping: MAP_WAVE (one wavefront per block) while the ensemble is too small to give every
+  // SIMD several 64-recording lane tiles; MAP_LANE (one lane per block) beyond that.
+  if (cfg->mapping == MAP_LANE || cfg->mapping == MAP_WAVE) h->mapping = cfg->mapping;
+  else if (cfg->mapping == MAP_AUTO) h->mapping = h->R <= kAutoWaveMaxRecordings ? MAP_WAVE : MAP_LANE;
+  else return fail(DMT_ERR_INVALID, "bad mapping");
+  h->tw = h->mapping == MAP_WAVE ? 1 : kLanes;
+  h->ntiles = (h->R + h->tw - 1) / h->tw;
   h->tile_qoff.assign(h->ntiles + 1, 0);
   for (int64_t t = 0; t < h->ntiles; ++t) {
     int64_t mx = 0;
-    for (int64_t r = t * kLanes; r < std::min<int64_t>(h->R, (t + 1) * kLanes); ++r) mx = std::max(mx, recQ[r]);
+    for (int64_t r = t * h->tw; r < std::min<int64_t>(h->R, (t + 1) * h->tw); ++r) mx = std::max(mx, recQ[r]);
     h->tile_qoff[t + 1] = h->tile_qoff[t] + mx + kPadPoints;
   }
   h->Ptile = h->tile_qoff[h->ntiles];
@@ -689,7 +704,7 @@ dmt_status dmt_upload_grid(dmt_ens* h, const double* t) {
     }
     DMT_TRY(ensure_stage(h, h->P));
     HIP_OK(hipMemcpyAsync(h->d_stage, t, h->P * 8, hipMemcpyHostToDevice, h->stream));
-    HIP_OK(launch_to_planes(h->key.precision, h->d_stage, h->d_t, h->d_t, nullptr, 0, 1, h->P,
+    HIP_OK(launch_to_planes(h->key.precision, h->tw, h->d_stage, h->d_t, h->d_t, nullptr, 0, 1, h->P,
                             h->d_pt_off, h->G, h->d_seg_rec, h->d_seg_q, h->d_tile_qoff, h->stream));
   }
   HIP_OK(hipStreamSynchronize(h->stream));
@@ -757,7 +772,7 @@ dmt_status dmt_upload_law(dmt_ens* h, int32_t unit, int32_t kind, const double* 
       DMT_TRY(ensure_stage(h, h->P * h->hp));
       HIP_OK(hipMemcpyAsync(h->d_stage, H, h->P * h->hp * 8, hipMemcpyHostToDevice, h->stream));
       for (int pass = 0; pass < (seeded ? 1 : 2); ++pass)
-        HIP_OK(launch_to_planes(h->key.precision, h->d_stage, h->d_H[0][kind], h->d_H[1][kind], sel,
+        HIP_OK(launch_to_planes(h->key.precision, h->tw, h->d_stage, h->d_H[0][kind], h->d_H[1][kind], sel,
                                 unit ^ pass, h->hp, h->P, h->d_pt_off, h->G, h->d_seg_rec, h->d_seg_q,
                                 h->d_tile_qoff, h->stream));
     }
@@ -771,7 +786,7 @@ dmt_status dmt_upload_law(dmt_ens* h, int32_t unit, int32_t kind, const double* 
     DMT_TRY(ensure_stage(h, h->P * h->d));
     HIP_OK(hipMemcpyAsync(h->d_stage, F, h->P * h->d * 8, hipMemcpyHostToDevice, h->stream));
     for (int pass = 0; pass < (seeded ? 1 : 2); ++pass)
-      HIP_OK(launch_to_planes(h->key.precision, h->d_stage, h->d_F[0][kind], h->d_F[1][kind], sel,
+      HIP_OK(launch_to_planes(h->key.precision, h->tw, h->d_stage, h->d_F[0][kind], h->d_F[1][kind], sel,
                               unit ^ pass, h->d, h->P, h->d_pt_off, h->G, h->d_seg_rec, h->d_seg_q,
                               h->d_tile_qoff, h->stream));
   }
@@ -805,7 +820,7 @@ dmt_status dmt_set_paths(dmt_ens* h, int32_t unit, const double* X, const double
     DMT_TRY(ensure_stage(h, h->P * C[w]));
     HIP_OK(hipMemcpyAsync(h->d_stage, src[w], h->P * C[w] * 8, hipMemcpyHostToDevice, h->stream));
     void** dst = w == 0 ? h->d_X : h->d_W;
-    HIP_OK(launch_to_planes(h->key.precision, h->d_stage, dst[0], dst[1], h->d_sel[w], unit, C[w],
+    HIP_OK(launch_to_planes(h->key.precision, h->tw, h->d_stage, dst[0], dst[1], h->d_sel[w], unit, C[w],
                             h->P, h->d_pt_off, h->G, h->d_seg_rec, h->d_seg_q, h->d_tile_qoff,
                             h->stream));
   }
@@ -820,7 +835,7 @@ dmt_status dmt_download_paths(dmt_ens* h, int32_t unit, int32_t what, double* ou
   const int C = what == 0 ? h->d : h->m;
   DMT_TRY(ensure_stage(h, h->P * C));
   void** src = what == 0 ? h->d_X : h->d_W;
-  HIP_OK(launch_from_planes(h->key.precision, h->d_stage, src[0], src[1], h->d_sel[what], unit, C,
+  HIP_OK(launch_from_planes(h->key.precision, h->tw, h->d_stage, src[0], src[1], h->d_sel[what], unit, C,
                             h->P, h->d_pt_off, h->G, h->d_seg_rec, h->d_seg_q, h->d_tile_qoff,
                             h->stream));
   HIP_OK(hipMemcpyAsync(out, h->d_stage, h->P * C * 8, hipMemcpyDeviceToHost, h->stream));

@@ -17,7 +17,8 @@ class Ensemble:
     """Device containers of a SamplingEnsemble (u and u°) plus its block layouts."""
 
     def __init__(self, model: int, d: int, m: int, n_points, precision: int = L.F64,
-                 seed: int = 0, device: int = 0, grid_shared: bool = False):
+                 seed: int = 0, device: int = 0, grid_shared: bool = False,
+                 mapping: int = L.MAP_AUTO):
         # n_points: list (per recording) of lists (per segment) of grid-point counts
         self.model, self.d, self.m, self.precision = int(model), int(d), int(m), int(precision)
         self.hp = self.d * (self.d + 1) // 2
@@ -35,7 +36,9 @@ class Ensemble:
         self._h = C.c_void_p()
         mdl = L.dmt_model(self.model, self.precision, self.d, self.m)
         st = L.dmt_structure(self.R, L.i32p(self.nseg), L.i32p(self.npts))
-        cfg = L.dmt_config(int(seed) & (2**64 - 1), int(device), 1 if grid_shared else 0)
+        cfg = L.dmt_config(int(seed) & (2**64 - 1), int(device), 1 if grid_shared else 0,
+                           int(mapping))
+        self.mapping = int(mapping)
         L.call("dmt_create", C.byref(self._h), C.byref(mdl), C.byref(st), C.byref(cfg))
 
     # ---------------------------------------------------------------- lifetime

@@ -137,7 +137,7 @@ def c2_ou2d(B=1024, N=500, seed=1, block_offset=0):
     return w
 
 
-def _fhn_states(model, B, seed, T_burn=1.0, dt_burn=1e-4, T_obs=0.1, dt_obs=1e-5):
+def _fhn_states(model, B, seed, T_burn=1.0, dt_burn=1e-3, T_obs=0.1, dt_obs=1e-4):
     """Start points from a burned-in target run; end values from a fine forward simulation
     over the observation interval (vectorised Euler–Maruyama over B chains)."""
     rng = np.random.default_rng(seed)
@@ -200,13 +200,13 @@ def c5_lorenz(B=32768, N=2000, seed=7, block_offset=0, T=0.2):
 CONFIGS = {"c1": c1_ou1d, "c2": c2_ou2d, "c3": c3_fhn, "c5": c5_lorenz}
 
 
-def load_device(w: Workload, seed=0, device=0, init_Z=True):
+def load_device(w: Workload, seed=0, device=0, init_Z=True, mapping=L.MAP_AUTO):
     """Create a libdmt ensemble holding the workload; initial paths by a fresh draw of u
     (init_paths!, src/sampling_unit.jl:83-87) with the workload's normals (or the device
     stream when init_Z is False), then u° = deepcopy(u) (src/sampling_pair.jl:51)."""
     from .engine import Ensemble
     ens = Ensemble(w.model.kind, w.d, w.m, w.n_points, precision=w.precision, seed=seed,
-                   device=device, grid_shared=w.grid_shared)
+                   device=device, grid_shared=w.grid_shared, mapping=mapping)
     fill(ens, w, init_Z=init_Z)
     return ens
 

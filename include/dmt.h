@@ -52,6 +52,10 @@ enum {
 /* models (DiffusionDefinition.jl models used by the reference's tutorials and configs) */
 enum { DMT_MODEL_OU = 0, DMT_MODEL_FHN = 1, DMT_MODEL_LORENZ = 2 };
 enum { DMT_F64 = 0, DMT_F32 = 1 };
+/* thread mapping of the recursion kernels: AUTO picks WAVE (one wavefront per block, for
+ * small ensembles, latency-bound) or LANE (one lane per block, for large ensembles,
+ * bandwidth-bound); both give bit-identical results */
+enum { DMT_MAP_AUTO = 0, DMT_MAP_LANE = 1, DMT_MAP_WAVE = 2 };
 /* units of a SamplingPair: u (accepted) and u° (proposal), src/sampling_pair.jl:36-55 */
 enum { DMT_U = 0, DMT_UPROP = 1 };
 /* law kinds of a SamplingUnit: PP (regular) and PPb (blocking), src/sampling_unit.jl:48-53 */
@@ -114,6 +118,7 @@ typedef struct {
     int32_t device;              /* HIP device ordinal */
     int32_t grid_shared;         /* 1: every recording has the same segment structure and time grid;
                                     dmt_upload_grid then takes ONE recording's grid */
+    int32_t mapping;             /* DMT_MAP_*: thread mapping of the Euler recursion */
 } dmt_config;
 
 /* ---------------- lifetime (SamplingEnsemble / SamplingPair containers) ---------------- */

@@ -14,11 +14,11 @@ from diffusionmcmctools_amd.models import (FHN, OU, Observation, artificial_obs_
 import oracle as orc
 
 
-def both(w, seed=11, hist_len=0, init_Z=True):
+def both(w, seed=11, hist_len=0, init_Z=True, mapping=L.MAP_AUTO):
     """Device ensemble + oracle ensemble holding the same workload; returns (dev, ora, layout)."""
     w.meta["hist_len"] = hist_len
     dev = dmt.Ensemble(w.model.kind, w.d, w.m, w.n_points, precision=w.precision, seed=seed,
-                       grid_shared=w.grid_shared)
+                       grid_shared=w.grid_shared, mapping=mapping)
     lay_d = W.fill(dev, w, init_Z=init_Z)
     ora = orc.OracleEnsemble(w.model.kind, w.d, w.m, w.n_points, prec=w.precision, seed=seed,
                              grid_shared=w.grid_shared)
@@ -111,10 +111,11 @@ def load_ragged(ens, case):
     ens.set_paths(L.UPROP, X=X, W=Wp)
 
 
-def ragged_pair(seed=11, hist_len=8):
+def ragged_pair(seed=11, hist_len=8, mapping=L.MAP_AUTO):
     case = ragged_case()
     m = case["model"]
-    dev = dmt.Ensemble(m.kind, m.d, m.m, case["n_points"], precision=case["prec"], seed=seed)
+    dev = dmt.Ensemble(m.kind, m.d, m.m, case["n_points"], precision=case["prec"], seed=seed,
+                       mapping=mapping)
     ora = orc.OracleEnsemble(m.kind, m.d, m.m, case["n_points"], prec=case["prec"], seed=seed)
     for e in (dev, ora):
         load_ragged(e, case)

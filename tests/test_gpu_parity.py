@@ -18,10 +18,14 @@ from diffusionmcmctools_amd import workloads as W
 
 pytestmark = pytest.mark.gpu
 
+# every parity test runs under both thread mappings of the recursion
+MAPPINGS = [pytest.param(L.MAP_LANE, id="lane"), pytest.param(L.MAP_WAVE, id="wave")]
 
-def run_mcmc_parity(w, iters, seed=3, hist_len=None, exact=True, check_every=True):
+
+def run_mcmc_parity(w, iters, seed=3, hist_len=None, exact=True, check_every=True,
+                    mapping=L.MAP_AUTO):
     hist_len = iters if hist_len is None else hist_len
-    dev, ora, lay = cs.both(w, hist_len=hist_len)
+    dev, ora, lay = cs.both(w, hist_len=hist_len, mapping=mapping)
     nb = w.nblocks
     rng = np.random.default_rng(seed)
     for e in (dev, ora):
@@ -49,28 +53,33 @@ def run_mcmc_parity(w, iters, seed=3, hist_len=None, exact=True, check_every=Tru
     return dev, ora, lay
 
 
-def test_c1_ou1d_mcmc_bit_exact():
-    run_mcmc_parity(W.c1_ou1d(), iters=40)
+@pytest.mark.parametrize("mapping", MAPPINGS)
+def test_c1_ou1d_mcmc_bit_exact(mapping):
+    run_mcmc_parity(W.c1_ou1d(), iters=40, mapping=mapping)
 
 
-def test_c2_ou2d_ragged_tile_bit_exact():
+@pytest.mark.parametrize("mapping", MAPPINGS)
+def test_c2_ou2d_ragged_tile_bit_exact(mapping):
     # 200 blocks: 3 full recording tiles + a partial one
-    run_mcmc_parity(W.c2_ou2d(B=200, N=500), iters=4)
+    run_mcmc_parity(W.c2_ou2d(B=200, N=500), iters=4, mapping=mapping)
 
 
-def test_c3_fhn_reduced_bit_exact():
-    run_mcmc_parity(W.c3_fhn(B=130, N=1000, T_burn=0.05), iters=3, check_every=False)
+@pytest.mark.parametrize("mapping", MAPPINGS)
+def test_c3_fhn_reduced_bit_exact(mapping):
+    run_mcmc_parity(W.c3_fhn(B=130, N=1000, T_burn=0.05), iters=3, check_every=False, mapping=mapping)
 
 
-def test_c5_lorenz_fp32_reduced_bit_exact():
-    run_mcmc_parity(W.c5_lorenz(B=70, N=2000), iters=3, check_every=False)
+@pytest.mark.parametrize("mapping", MAPPINGS)
+def test_c5_lorenz_fp32_reduced_bit_exact(mapping):
+    run_mcmc_parity(W.c5_lorenz(B=70, N=2000), iters=3, check_every=False, mapping=mapping)
 
 
-def test_ragged_blocking_layouts_bit_exact():
+@pytest.mark.parametrize("mapping", MAPPINGS)
+def test_ragged_blocking_layouts_bit_exact(mapping):
     """Multi-segment recordings, non-terminal blocks with P_last laws, two alternating block
     layouts aliasing the same SamplingPair (src/block.jl:66-72), swaps, loglikhd of both units,
     a proposal law and recompute_path! (src/biblock.jl:334-344)."""
-    case, dev, ora, ((A, nA), (B, nB)) = cs.ragged_pair()
+    case, dev, ora, ((A, nA), (B, nB)) = cs.ragged_pair(mapping=mapping)
     rng = np.random.default_rng(9)
     S = case["t"].size - sum(case["nsegs"])
     for e in (dev, ora):
@@ -119,9 +128,10 @@ def test_ragged_blocking_layouts_bit_exact():
     assert dev.fetch_ll(A, 0, nA) == ora.fetch_ll(A, 0, nA)
 
 
-def test_fetch_ll_tree_bit_exact():
+@pytest.mark.parametrize("mapping", MAPPINGS)
+def test_fetch_ll_tree_bit_exact(mapping):
     w = W.c2_ou2d(B=64 * 80, N=8)
-    dev, ora, lay = cs.both(w, hist_len=2)
+    dev, ora, lay = cs.both(w, hist_len=2, mapping=mapping)
     rng = np.random.default_rng(0)
     nb = w.nblocks
     vals = rng.standard_normal(nb) * 10.0 ** rng.integers(-3, 6, nb)
@@ -148,9 +158,10 @@ def test_philox_stream_bit_exact(dmt):
     np.testing.assert_allclose(zd, zo, rtol=1e-13, atol=1e-13)
 
 
-def test_device_rng_mode_matches_oracle_within_tolerance():
+@pytest.mark.parametrize("mapping", MAPPINGS)
+def test_device_rng_mode_matches_oracle_within_tolerance(mapping):
     w = W.c2_ou2d(B=100, N=500)
-    dev, ora, lay = cs.both(w, hist_len=3)
+    dev, ora, lay = cs.both(w, hist_len=3, mapping=mapping)
     nb = w.nblocks
     for e in (dev, ora):
         e.loglikhd(lay, L.U, 0, nb)
@@ -175,9 +186,10 @@ def test_device_rng_mode_matches_oracle_within_tolerance():
         dev.set_block_state(lay, L.BLK_LL, 0, nb, ora.block_ll(lay, 0, nb)[0])
 
 
-def test_failure_gives_minus_inf_and_rejects():
+@pytest.mark.parametrize("mapping", MAPPINGS)
+def test_failure_gives_minus_inf_and_rejects(mapping):
     w = W.c1_ou1d()
-    dev, ora, lay = cs.both(w, hist_len=2)
+    dev, ora, lay = cs.both(w, hist_len=2, mapping=mapping)
     Z = np.full((w.steps_per_iter, 1), 1e300)   # overflows the path
     for e in (dev, ora):
         e.loglikhd(lay, L.U, 0, 1)
@@ -188,11 +200,12 @@ def test_failure_gives_minus_inf_and_rejects():
     assert not dev.accept_reject(lay, 0, 1, 1, E=np.array([1e-300]), want_acc=True)[0]
 
 
-def test_first_proposal_auto_accepted_without_loglikhd():
+@pytest.mark.parametrize("mapping", MAPPINGS)
+def test_first_proposal_auto_accepted_without_loglikhd(mapping):
     """ll = -Inf initially (src/block.jl:75) so the first proposal is accepted unless
     loglikhd! ran first (Appendix B.2 of SURVEY.md)."""
     w = W.c2_ou2d(B=64, N=50)
-    dev, ora, lay = cs.both(w, hist_len=1)
+    dev, ora, lay = cs.both(w, hist_len=1, mapping=mapping)
     rng = np.random.default_rng(2)
     Z = rng.standard_normal((w.steps_per_iter, 2))
     E = rng.exponential(1.0, 64)
@@ -204,13 +217,14 @@ def test_first_proposal_auto_accepted_without_loglikhd():
 
 
 # ---------------------------------------------------------------- full-size properties
+@pytest.mark.parametrize("mapping", MAPPINGS)
 @pytest.mark.parametrize("cfg", ["c2", "c3"])
-def test_full_size_properties(cfg):
+def test_full_size_properties(cfg, mapping):
     """At BASELINE.json's full sizes (oracle too slow here): size-independent invariants."""
     w = W.c2_ou2d() if cfg == "c2" else W.c3_fhn(T_burn=0.2)
     import diffusionmcmctools_amd as d
     dev = d.Ensemble(w.model.kind, w.d, w.m, w.n_points, precision=w.precision, seed=4,
-                     grid_shared=w.grid_shared)
+                     grid_shared=w.grid_shared, mapping=mapping)
     w.meta["hist_len"] = 4
     lay = W.fill(dev, w, init_Z=False)
     nb = w.nblocks
