@@ -12,8 +12,10 @@
 
 namespace dmt {
 
+// packed upper-triangular index of a symmetric d×d matrix (non-recursive so that it folds to
+// a constant inside unrolled loops: a runtime index into a register array spills to scratch)
 __host__ __device__ constexpr int packed_idx(int d, int a, int b) {
-  return (a > b) ? packed_idx(d, b, a) : a * d - (a * (a - 1)) / 2 + (b - a);
+  return (a < b ? a : b) * d - ((a < b ? a : b) * ((a < b ? a : b) - 1)) / 2 + ((a < b ? b : a) - (a < b ? a : b));
 }
 
 __device__ __forceinline__ double dfma(double a, double b, double c) { return __builtin_fma(a, b, c); }
@@ -178,32 +180,49 @@ __device__ __forceinline__ T obs_term(const T* H0, const T* F0, const T* x, T c0
 // Streaming form of the adjacent-pair tree over chunks of 64 steps.
 template <class T>
 struct PSum {
+  // s[j] holds the sum of the last complete aligned group of 2^j leaves while bit j of n is
+  // set.  Updates are branch-free selects on the (wave-uniform) counter: no dynamic register
+  // indexing (which would go through scratch memory).
   T s[7];
   int n;
   T acc;
-  __device__ __forceinline__ void init() { n = 0; acc = (T)0; }
-  __device__ __forceinline__ void add(T v) {
-    int lvl = 0;
+  __device__ __forceinline__ void init() {
+    n = 0;
+    acc = (T)0;
+#pragma unroll
+    for (int j = 0; j < 7; ++j) s[j] = (T)0;
+  }
+  template <int LOG0>
+  __device__ __forceinline__ void insert(T v) {  // a group of 2^LOG0 leaves, n % 2^LOG0 == 0
     bool go = true;
 #pragma unroll
-    for (int j = 0; j < 6; ++j) {  // binary counter: merge while the low bits of n are 1
-      if (go && ((n >> j) & 1)) { v = s[j] + v; lvl = j + 1; }
-      else go = false;
+    for (int j = LOG0; j < 6; ++j) {
+      const bool bit = (n >> j) & 1;
+      const T merged = s[j] + v;
+      s[j] = (go && !bit) ? v : s[j];
+      v = (go && bit) ? merged : v;
+      go = go && bit;
     }
-    // lvl is at most 6; write via a switch to keep s[] in registers
-    switch (lvl) {
-      case 0: s[0] = v; break; case 1: s[1] = v; break; case 2: s[2] = v; break;
-      case 3: s[3] = v; break; case 4: s[4] = v; break; case 5: s[5] = v; break;
-      default: s[6] = v; break;
-    }
-    if (++n == 64) { acc = acc + (s[6] + (T)0); n = 0; }
+    s[6] = go ? v : s[6];
+    n += 1 << LOG0;
+    if (n == 64) { acc = acc + (s[6] + (T)0); n = 0; }
   }
+  __device__ __forceinline__ void add(T v) { insert<0>(v); }
+  // Insert the sum of K consecutive leaves (an aligned subtree, K a power of two dividing 64,
+  // n a multiple of K): identical to K single add()s.
+  template <int LOGK>
+  __device__ __forceinline__ void add_subtree(T v) { insert<LOGK>(v); }
   __device__ __forceinline__ T finish() {
     if (n > 0) {
-      bool have = false; T r = (T)0;
+      bool have = false;
+      T r = (T)0;
 #pragma unroll
-      for (int lvl = 0; lvl < 6; ++lvl)
-        if ((n >> lvl) & 1) { r = have ? (s[lvl] + r) : s[lvl]; have = true; }
+      for (int lvl = 0; lvl < 6; ++lvl) {
+        const bool bit = (n >> lvl) & 1;
+        const T m = have ? (s[lvl] + r) : s[lvl];
+        r = bit ? m : r;
+        have = have || bit;
+      }
       acc = acc + (r + (T)0);
       n = 0;
     }

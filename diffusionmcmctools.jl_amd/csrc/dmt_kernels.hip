@@ -22,7 +22,30 @@
 
 namespace dmt {
 
-template <class Mdl, class T, int MODE, int K>
+template <int K>
+struct Log2 { static constexpr int v = K == 1 ? 0 : 1 + Log2<(K > 1 ? K / 2 : 1)>::v; };
+template <>
+struct Log2<1> { static constexpr int v = 0; };
+
+// Adjacent-pair tree over K values (K a power of two), in place: v[0] = ((v0+v1)+(v2+v3))…
+template <class T, int K>
+__device__ __forceinline__ T tree_sum(T* v) {
+#pragma unroll
+  for (int w = K; w > 1; w >>= 1) {
+#pragma unroll
+    for (int j = 0; j < w / 2; ++j) v[j] = v[2 * j] + v[2 * j + 1];
+  }
+  return v[0];
+}
+
+// One lane integrates one segment.  Main loop: full chunks of K steps, branch-free, with the
+// next chunk's inputs (t, H, F, accepted W, and Z in parity mode) loaded into registers
+// before the current chunk is integrated (prefetch distance K; no memory operation sits in
+// a branch, so the waitcnt pass can count outstanding loads exactly).  Normals of a chunk
+// come in whole Box–Muller pairs (K·M even); the chunk's K Girsanov terms are summed as an
+// aligned subtree and inserted into the 64-step pairwise counter.  A tail of < K steps
+// runs through the single-step path.
+template <class Mdl, class T, int MODE, bool PARITY, int K>
 __device__ __forceinline__ bool run_segment(const Law<Mdl, T>& L, const T* __restrict__ tpl,
                                             const int t_sh, const T* __restrict__ Ht,
                                             const int H_sh, const T* __restrict__ Ft,
@@ -32,9 +55,9 @@ __device__ __forceinline__ bool run_segment(const Law<Mdl, T>& L, const T* __res
                                             const int np, const int lane, const T rho,
                                             const T srho, T* x, T& sl) {
   constexpr int D = Mdl::D, M = Mdl::M, HP = D * (D + 1) / 2;
-  // Per-segment base pointers: point i, component c of an array with C components sits at
-  // base + (i*C + c)*64.  Tiles carry kPadPoints spare rows, so the prefetch of the chunk
-  // after the last one never leaves the allocation (its values are not used).
+  constexpr bool DRAW = MODE != MODE_RECOMPUTE;
+  constexpr bool READW = MODE != MODE_FRESH;
+  static_assert((K * M) % 2 == 0 && 64 % K == 0, "chunk must hold whole normal pairs");
   const int64_t row = tq + q0;
   const T* tb = t_sh ? tpl + q0 : tpl + row * kLanes + lane;
   const int tst = t_sh ? 1 : kLanes;
@@ -53,80 +76,98 @@ __device__ __forceinline__ bool run_segment(const Law<Mdl, T>& L, const T* __res
 #pragma unroll
   for (int k = 0; k < M; ++k) {
     wf[k] = (T)0;
-    T w0 = (MODE == MODE_FRESH) ? (T)0 : Wsb[k * kLanes];
-    T wo = (MODE == MODE_RECOMPUTE) ? w0 : dfma(rho, w0, srho * wf[k]);
-    if (MODE != MODE_RECOMPUTE) Wdb[k * kLanes] = wo;
+    T w0 = READW ? Wsb[k * kLanes] : (T)0;
+    T wo = DRAW ? dfma(rho, w0, srho * wf[k]) : w0;
+    if (DRAW) Wdb[k * kLanes] = wo;
     wprev[k] = wo;
   }
   PSum<T> ps;
   ps.init();
 
-  T bt[K], bH[K][HP], bF[K][D], bW[K][M];
-  auto load_chunk = [&](int c0, T* vt, T (*vH)[HP], T (*vF)[D], T (*vW)[M]) {
+  struct Chunk {
+    T t[K], H[K][HP], F[K][D], W[K][M], Z[K][M];
+  };
+  auto load = [&](int c0, Chunk& c) {
 #pragma unroll
     for (int j = 0; j < K; ++j) {
       const int64_t i = c0 + j;
-      vt[j] = tb[(i + 1) * tst];
+      c.t[j] = tb[(i + 1) * tst];
 #pragma unroll
-      for (int c = 0; c < HP; ++c) vH[j][c] = Hb[(i * HP + c) * hst];
+      for (int e = 0; e < HP; ++e) c.H[j][e] = Hb[(i * HP + e) * hst];
 #pragma unroll
-      for (int c = 0; c < D; ++c) vF[j][c] = Fb[(i * D + c) * kLanes];
-      if (MODE != MODE_FRESH) {
+      for (int e = 0; e < D; ++e) c.F[j][e] = Fb[(i * D + e) * kLanes];
 #pragma unroll
-        for (int k = 0; k < M; ++k) vW[j][k] = Wsb[((i + 1) * M + k) * kLanes];
+      for (int k = 0; k < M; ++k) {
+        c.W[j][k] = READW ? Wsb[((i + 1) * M + k) * kLanes] : (T)0;
+        c.Z[j][k] = (PARITY && DRAW) ? (T)Zg[i * M + k] : (T)0;
       }
     }
   };
-  if (nst > 0) load_chunk(0, bt, bH, bF, bW);
-  for (int c0 = 0; c0 < nst; c0 += K) {
-    T nt[K], nH[K][HP], nF[K][D], nW[K][M];
-    load_chunk(c0 + K, nt, nH, nF, nW);  // prefetch (padded rows keep it in bounds)
+  // one Euler step from registers; returns the Girsanov term G·dt
+  auto step = [&](int i, T tn, const T* Hi, const T* Fi, const T* Wi, const T* Zi) -> T {
+    const T dt = tn - tcur;
+    T dW[M];
+    if (!DRAW) {
 #pragma unroll
-    for (int j = 0; j < K; ++j) {
-      const int i = c0 + j;
-      if (i < nst) {
-        const T dt = bt[j] - tcur;
-        T dW[M];
-        if (MODE == MODE_RECOMPUTE) {
+      for (int k = 0; k < M; ++k) { dW[k] = Wi[k] - wprev[k]; wprev[k] = Wi[k]; }
+    } else {
+      const T sdt = sqrt(dt);
 #pragma unroll
-          for (int k = 0; k < M; ++k) {
-            T wn = bW[j][k];
-            dW[k] = wn - wprev[k];
-            wprev[k] = wn;
-          }
-        } else {
-          const T sdt = sqrt(dt);
-#pragma unroll
-          for (int k = 0; k < M; ++k) {
-            const uint32_t n = (uint32_t)(i * M + k);
-            T z = Zg ? (T)Zg[(int64_t)i * M + k] : ns.get(n);
-            wf[k] = dfma(sdt, z, wf[k]);
-            T w = (MODE == MODE_FRESH) ? (T)0 : bW[j][k];
-            T wn = dfma(rho, w, srho * wf[k]);
-            Wdb[((int64_t)(i + 1) * M + k) * kLanes] = wn;
-            dW[k] = wn - wprev[k];
-            wprev[k] = wn;
-          }
-        }
-        T r[D], b[D];
-        const T G = g_at<Mdl, T>(L, bH[j], bF[j], x, r, b);
-        ps.add(G * dt);
-        euler_step<Mdl, T>(L, r, b, dt, dW, x);
-#pragma unroll
-        for (int p = 0; p < D; ++p) Xdb[((int64_t)(i + 1) * D + p) * kLanes] = x[p];
-        tcur = bt[j];
+      for (int k = 0; k < M; ++k) {
+        wf[k] = dfma(sdt, Zi[k], wf[k]);
+        const T wn = dfma(rho, Wi[k], srho * wf[k]);
+        Wdb[((int64_t)(i + 1) * M + k) * kLanes] = wn;
+        dW[k] = wn - wprev[k];
+        wprev[k] = wn;
       }
     }
+    T r[D], b[D];
+    const T G = g_at<Mdl, T>(L, Hi, Fi, x, r, b);
+    euler_step<Mdl, T>(L, r, b, dt, dW, x);
 #pragma unroll
-    for (int j = 0; j < K; ++j) {
-      bt[j] = nt[j];
+    for (int p = 0; p < D; ++p) Xdb[((int64_t)(i + 1) * D + p) * kLanes] = x[p];
+    tcur = tn;
+    return G * dt;
+  };
+
+  const int nfull = nst - nst % K;
+  if (nfull > 0) {
+    Chunk cur, nxt;
+    load(0, cur);
+    for (int c0 = 0; c0 < nfull; c0 += K) {
+      load(c0 + K, nxt);  // prefetch; padded rows keep the last one in bounds
+      if (DRAW && !PARITY) {  // whole Box–Muller pairs of this chunk, straight-line
 #pragma unroll
-      for (int c = 0; c < HP; ++c) bH[j][c] = nH[j][c];
+        for (int pp = 0; pp < K * M / 2; ++pp) {
+          const uint32_t pair = (uint32_t)((c0 * M) / 2 + pp);
+          U4 o = philox4x32_10(U4{pair, ns.seg, ns.iter, ns.c3}, ns.k0, ns.k1);
+          T z0, z1;
+          normal_pair(o, z0, z1);
+          cur.Z[(2 * pp) / M][(2 * pp) % M] = z0;
+          cur.Z[(2 * pp + 1) / M][(2 * pp + 1) % M] = z1;
+        }
+      }
+      T gv[K];
 #pragma unroll
-      for (int c = 0; c < D; ++c) bF[j][c] = nF[j][c];
-#pragma unroll
-      for (int k = 0; k < M; ++k) bW[j][k] = nW[j][k];
+      for (int j = 0; j < K; ++j)
+        gv[j] = step(c0 + j, cur.t[j], cur.H[j], cur.F[j], cur.W[j], cur.Z[j]);
+      ps.template add_subtree<Log2<K>::v>(tree_sum<T, K>(gv));
+      cur = nxt;
     }
+  }
+  for (int i = nfull; i < nst; ++i) {  // tail (< K steps): single-step path
+    const int64_t q = i;
+    T Hi[HP], Fi[D], Wi[M], Zi[M];
+#pragma unroll
+    for (int e = 0; e < HP; ++e) Hi[e] = Hb[(q * HP + e) * hst];
+#pragma unroll
+    for (int e = 0; e < D; ++e) Fi[e] = Fb[(q * D + e) * kLanes];
+#pragma unroll
+    for (int k = 0; k < M; ++k) {
+      Wi[k] = READW ? Wsb[((q + 1) * M + k) * kLanes] : (T)0;
+      Zi[k] = DRAW ? (PARITY ? (T)Zg[q * M + k] : ns.get((uint32_t)(i * M + k))) : (T)0;
+    }
+    ps.add(step(i, tb[(q + 1) * tst], Hi, Fi, Wi, Zi));
   }
   sl = ps.finish();
   bool ok = isfinite(sl);
@@ -150,7 +191,7 @@ __device__ __forceinline__ bool map_block(const BlockArgs<T>& a, int64_t& tile, 
   return true;
 }
 
-template <class Mdl, class T, int MODE, int K>
+template <class Mdl, class T, int MODE, bool PARITY, int K>
 __global__ __launch_bounds__(64) void k_block(const BlockArgs<T> a) {
   constexpr int D = Mdl::D, M = Mdl::M, HP = D * (D + 1) / 2;
   int64_t tile, blk;
@@ -197,7 +238,7 @@ __global__ __launch_bounds__(64) void k_block(const BlockArgs<T> a) {
     const T* Ws = a.W[a.selW[g] ^ a.ws_flip];
     T* Wd = a.W[a.selW[g] ^ a.wd_flip];
     T sl;
-    const bool sok = run_segment<Mdl, T, MODE, K>(
+    const bool sok = run_segment<Mdl, T, MODE, PARITY, K>(
         L, a.t, a.t_shared, a.H[ls][kind], a.H_shared[ls][kind], a.F[ls][kind], Ws, Wd, Xd, Zg,
         ns, tq, a.seg_q[g], a.seg_np[g], lane, rho, srho, x, sl);
     if (!sok) { ok = false; break; }
@@ -745,10 +786,17 @@ static hipError_t launch_block_t(int mapping, int mode, const void* args, int64_
     }
     return hipGetLastError();
   }
+  const bool par = a.Z != nullptr;
   switch (mode) {
-    case MODE_PCN: k_block<Mdl, T, MODE_PCN, kChunk><<<grid, block, 0, s>>>(a); break;
-    case MODE_RECOMPUTE: k_block<Mdl, T, MODE_RECOMPUTE, kChunk><<<grid, block, 0, s>>>(a); break;
-    case MODE_FRESH: k_block<Mdl, T, MODE_FRESH, kChunk><<<grid, block, 0, s>>>(a); break;
+    case MODE_PCN:
+      if (par) k_block<Mdl, T, MODE_PCN, true, kChunk><<<grid, block, 0, s>>>(a);
+      else k_block<Mdl, T, MODE_PCN, false, kChunk><<<grid, block, 0, s>>>(a);
+      break;
+    case MODE_RECOMPUTE: k_block<Mdl, T, MODE_RECOMPUTE, false, kChunk><<<grid, block, 0, s>>>(a); break;
+    case MODE_FRESH:
+      if (par) k_block<Mdl, T, MODE_FRESH, true, kChunk><<<grid, block, 0, s>>>(a);
+      else k_block<Mdl, T, MODE_FRESH, false, kChunk><<<grid, block, 0, s>>>(a);
+      break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

@@ -347,7 +347,7 @@ dmt_status upload_Z(dmt_ens* h, const double* Z, const double** dZ) {
   *dZ = nullptr;
   if (!Z) return DMT_OK;
   const int64_t n = h->S * h->m;
-  DMT_TRY(ensure_Z(h, n));
+  DMT_TRY(ensure_Z(h, n + 2 * kPadPoints * h->m));  // chunk prefetch may read past the end
   HIP_OK(hipMemcpyAsync(h->d_Z, Z, (size_t)n * 8, hipMemcpyHostToDevice, h->stream));
   *dZ = h->d_Z;
   return DMT_OK;
