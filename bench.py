@@ -65,7 +65,10 @@ def cpu_baseline(w, ens, lay, budget_s=12.0):
     B = w.nblocks
     npts = w.n_points[0][0]
     X = ens.download_paths(L.U, 0)
-    Wp = ens.download_paths(L.U, 1)
+    Wc = ens.download_paths(L.U, 1).reshape(B, npts, w.m)  # cumulative Wiener paths
+    Wp = Wc.copy()                                          # the oracle holds increments
+    Wp[:, 1:] = Wc[:, 1:] - Wc[:, :-1]
+    Wp = Wp.reshape(B * npts, w.m)
     ens.loglikhd(lay, L.U, 0, B)
     ll = ens.get_block_state(lay, L.BLK_LL, 0, B)
     rho = np.full(B, w.rho)
@@ -142,9 +145,8 @@ def main():
     ens.loglikhd(lay, L.U, 0, B)
 
     def step(i):
-        ens.draw_proposal(lay, 0, B, iter=i)
-        ens.accept_reject(lay, 0, B, i)
-        return ens.fetch_ll(lay, 0, B, i)
+        # draw_proposal_path!(be); accept_reject_proposal_path!(be, i); fetch_ll(be) — one call
+        return ens.mcmc_step(lay, 0, B, i)
 
     def barrier():
         ens.sync()

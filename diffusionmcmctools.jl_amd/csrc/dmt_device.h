@@ -26,6 +26,7 @@ __device__ __forceinline__ float dfma(float a, float b, float c) { return __buil
 template <class T, int D_, int M_>
 struct OU {
   static constexpr int D = D_, M = M_, NTH = 12;
+  static constexpr bool kLinear = true;  // drift folded into the guiding coefficients
   // theta: Theta (d×d row-major) at 0, mu at 9
   __device__ __forceinline__ static void drift(const T* th, const T* x, T* b) {
     T y[D];
@@ -44,6 +45,7 @@ struct OU {
 template <class T>
 struct FHN {
   static constexpr int D = 2, M = 1, NTH = 4;
+  static constexpr bool kLinear = false;
   // theta: 1/eps, s, gamma, beta
   __device__ __forceinline__ static void drift(const T* th, const T* x, T* b) {
     T y = x[0], v = x[1];
@@ -57,6 +59,7 @@ struct FHN {
 template <class T>
 struct Lorenz {
   static constexpr int D = 3, M = 3, NTH = 3;
+  static constexpr bool kLinear = false;
   // theta: s, r, beta
   __device__ __forceinline__ static void drift(const T* th, const T* x, T* b) {
     b[0] = th[0] * (x[1] - x[0]);
@@ -75,6 +78,7 @@ struct Law {
   T Bt[D * D];
   T beta[D];
   T da[HP];
+  T thmu[D];  // Theta·mu of a linear (OU) drift, canonical order
   bool trace;
   __device__ __forceinline__ void load(const double* L) {
 #pragma unroll
@@ -92,8 +96,39 @@ struct Law {
 #pragma unroll
     for (int i = 0; i < HP; ++i) da[i] = (T)L[DMT_LAW_DA + i];
     trace = L[DMT_LAW_TRACE] != 0.0;
+    if (Mdl::kLinear) {
+#pragma unroll
+      for (int p = 0; p < D; ++p) {
+        T tm = th[p * D + 0] * th[9 + 0];
+#pragma unroll
+        for (int c = 1; c < D; ++c) tm = dfma(th[p * D + c], th[9 + c], tm);
+        thmu[p] = tm;
+      }
+    }
   }
 };
+
+// Guiding coefficients of one step (independent of x): M = a·H (+ Theta for a linear
+// drift), c = a·F (+ Theta·mu), canonical order.
+template <class Mdl, class T>
+__device__ __forceinline__ void guide_coeffs(const Law<Mdl, T>& L, const T* H, const T* F, T* Mg,
+                                             T* cg) {
+  constexpr int D = Mdl::D;
+#pragma unroll
+  for (int p = 0; p < D; ++p) {
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+      T v = L.a[packed_idx(D, p, 0)] * H[packed_idx(D, 0, q)];
+#pragma unroll
+      for (int c = 1; c < D; ++c) v = dfma(L.a[packed_idx(D, p, c)], H[packed_idx(D, c, q)], v);
+      Mg[p * D + q] = Mdl::kLinear ? (L.th[p * D + q] + v) : v;
+    }
+    T f = L.a[packed_idx(D, p, 0)] * F[0];
+#pragma unroll
+    for (int c = 1; c < D; ++c) f = dfma(L.a[packed_idx(D, p, c)], F[c], f);
+    cg[p] = Mdl::kLinear ? (L.thmu[p] + f) : f;
+  }
+}
 
 // G(t_i, x_i) of the Girsanov weight; returns G, writes r = F - Hx and the drift b.
 template <class Mdl, class T>
@@ -134,22 +169,34 @@ __device__ __forceinline__ T g_at(const Law<Mdl, T>& L, const T* H, const T* F, 
   return G;
 }
 
-// One guided Euler–Maruyama step (left point), canonical order.
+// sigma·dW of one step (canonical: sdW_a = s_a0 dW_0, then fma over k)
 template <class Mdl, class T>
-__device__ __forceinline__ void euler_step(const Law<Mdl, T>& L, const T* r, const T* b, T dt,
-                                           const T* dW, T* x) {
+__device__ __forceinline__ void sigma_dw(const Law<Mdl, T>& L, const T* dW, T* sdW) {
   constexpr int D = Mdl::D, M = Mdl::M;
+#pragma unroll
+  for (int p = 0; p < D; ++p) {
+    T v = L.sg[p * M + 0] * dW[0];
+#pragma unroll
+    for (int k = 1; k < M; ++k) v = dfma(L.sg[p * M + k], dW[k], v);
+    sdW[p] = v;
+  }
+}
+
+// One guided Euler–Maruyama step (left point), canonical order:
+//   u_a = c_a - Σ_b M_ab x_b ;  bg = u (linear drift) or b(x) + u ;  x'_a = fma(bg_a, dt, x_a + sdW_a)
+// b is the model drift at x (ignored for a linear drift, which M, c already contain).
+template <class Mdl, class T>
+__device__ __forceinline__ void euler_step(const T* Mg, const T* cg, const T* b, T dt,
+                                           const T* sdW, T* x) {
+  constexpr int D = Mdl::D;
   T xn[D];
 #pragma unroll
   for (int p = 0; p < D; ++p) {
-    T ar = L.a[packed_idx(D, p, 0)] * r[0];
+    T u = cg[p];
 #pragma unroll
-    for (int q = 1; q < D; ++q) ar = dfma(L.a[packed_idx(D, p, q)], r[q], ar);
-    T bg = b[p] + ar;
-    T v = dfma(bg, dt, x[p]);
-#pragma unroll
-    for (int k = 0; k < M; ++k) v = dfma(L.sg[p * M + k], dW[k], v);
-    xn[p] = v;
+    for (int q = 0; q < D; ++q) u = dfma(-Mg[p * D + q], x[q], u);
+    const T bg = Mdl::kLinear ? u : (b[p] + u);
+    xn[p] = dfma(bg, dt, x[p] + sdW[p]);
   }
 #pragma unroll
   for (int p = 0; p < D; ++p) x[p] = xn[p];

@@ -103,14 +103,20 @@ hipError_t launch_accept(const AcceptArgs& a, hipStream_t s);
 hipError_t launch_to_planes(int precision, int tw, const double* src, void* dst0, void* dst1,
                             const uint8_t* sel, int flip, int C, int64_t P, const int64_t* pt_off,
                             int64_t G, const int32_t* seg_rec, const int32_t* seg_q,
-                            const int64_t* tile_qoff, hipStream_t s);
+                            const int64_t* tile_qoff, hipStream_t s, int incr = 0);
+hipError_t launch_from_planes_incr(int precision, int tw, double* dst, const void* src0,
+                                   const void* src1, const uint8_t* sel, int flip, int C,
+                                   int64_t G, const int64_t* pt_off, const int32_t* seg_np,
+                                   const int32_t* seg_rec, const int32_t* seg_q,
+                                   const int64_t* tile_qoff, hipStream_t s);
 hipError_t launch_from_planes(int precision, int tw, double* dst, const void* src0,
                               const void* src1, const uint8_t* sel, int flip, int C, int64_t P,
                               const int64_t* pt_off, int64_t G, const int32_t* seg_rec,
                               const int32_t* seg_q, const int64_t* tile_qoff, hipStream_t s);
 hipError_t launch_cast(int precision, const double* src, void* dst, int64_t n, hipStream_t s);
 hipError_t launch_block_sum(const double* ll, const double* llp, const uint8_t* acc, int64_t n,
-                            double* out3, hipStream_t s);
+                            double* work, double* out3, hipStream_t s);
+hipError_t launch_accept_reduce(const AcceptArgs& a, double* work, double* out3, hipStream_t s);
 hipError_t launch_flip(uint8_t* sel0, uint8_t* sel1, uint8_t* sel2, uint8_t* sel3,
                        const int32_t* gfirst, const int32_t* glast, const uint8_t* term,
                        int32_t swap_ppb_nonterm_only, int64_t b0, int64_t b1, hipStream_t s);

@@ -16,6 +16,9 @@
 // registers while the current K steps are integrated (software pipeline, prefetch
 // distance K), which is what hides HBM latency at one wave per SIMD.
 #include <math.h>
+#include <stdlib.h>
+
+#include <type_traits>
 
 #include "dmt_device.h"
 #include "dmt_internal.h"
@@ -68,18 +71,14 @@ __device__ __forceinline__ bool run_segment(const Law<Mdl, T>& L, const T* __res
   T* Wdb = Wd + row * M * kLanes + lane;
   T* Xdb = Xd + row * D * kLanes + lane;
 
+  // W planes hold increments: row 0 = W(t0), row i+1 = dW_i
   const int nst = np - 1;
-  T wprev[M], wf[M];
   T tcur = tb[0];
 #pragma unroll
   for (int p = 0; p < D; ++p) Xdb[p * kLanes] = x[p];
+  if (DRAW) {
 #pragma unroll
-  for (int k = 0; k < M; ++k) {
-    wf[k] = (T)0;
-    T w0 = READW ? Wsb[k * kLanes] : (T)0;
-    T wo = DRAW ? dfma(rho, w0, srho * wf[k]) : w0;
-    if (DRAW) Wdb[k * kLanes] = wo;
-    wprev[k] = wo;
+    for (int k = 0; k < M; ++k) Wdb[k * kLanes] = rho * (READW ? Wsb[k * kLanes] : (T)0);
   }
   PSum<T> ps;
   ps.init();
@@ -109,21 +108,20 @@ __device__ __forceinline__ bool run_segment(const Law<Mdl, T>& L, const T* __res
     T dW[M];
     if (!DRAW) {
 #pragma unroll
-      for (int k = 0; k < M; ++k) { dW[k] = Wi[k] - wprev[k]; wprev[k] = Wi[k]; }
+      for (int k = 0; k < M; ++k) dW[k] = Wi[k];
     } else {
       const T sdt = sqrt(dt);
 #pragma unroll
       for (int k = 0; k < M; ++k) {
-        wf[k] = dfma(sdt, Zi[k], wf[k]);
-        const T wn = dfma(rho, Wi[k], srho * wf[k]);
-        Wdb[((int64_t)(i + 1) * M + k) * kLanes] = wn;
-        dW[k] = wn - wprev[k];
-        wprev[k] = wn;
+        dW[k] = dfma(rho, Wi[k], srho * (sdt * Zi[k]));
+        Wdb[((int64_t)(i + 1) * M + k) * kLanes] = dW[k];
       }
     }
-    T r[D], b[D];
+    T r[D], b[D], sdW[D], Mg[D * D], cg[D];
     const T G = g_at<Mdl, T>(L, Hi, Fi, x, r, b);
-    euler_step<Mdl, T>(L, r, b, dt, dW, x);
+    sigma_dw<Mdl, T>(L, dW, sdW);
+    guide_coeffs<Mdl, T>(L, Hi, Fi, Mg, cg);
+    euler_step<Mdl, T>(Mg, cg, b, dt, sdW, x);
 #pragma unroll
     for (int p = 0; p < D; ++p) Xdb[((int64_t)(i + 1) * D + p) * kLanes] = x[p];
     tcur = tn;
@@ -335,158 +333,57 @@ __device__ __forceinline__ T wave_tree_sum(T v) {
   return v;
 }
 
-template <class Mdl, class T, int MODE>
-__device__ __forceinline__ bool run_segment_wave(
-    const Law<Mdl, T>& L, const T* __restrict__ tpl, const int t_sh, const T* __restrict__ Ht,
-    const int H_sh, const T* __restrict__ Ft, const T* __restrict__ Ws, T* __restrict__ Wd,
-    T* __restrict__ Xd, const double* __restrict__ Zg, const uint64_t seed, const uint32_t g,
-    const uint32_t iter, const uint32_t salt, const int64_t row, const int64_t q0, const int np,
-    const int lane, const T rho, const T srho, T* x, T& sl, T* lds) {
-  constexpr int D = Mdl::D, M = Mdl::M, HP = D * (D + 1) / 2;
-  constexpr int NR = 2 + 2 * M + HP + D;  // dt, sdt, Z[M], W[M], H[HP], F[D]
-  constexpr int NRP = (NR + 1) & ~1;      // 16-byte rows for fp64
-  const T* tb = t_sh ? tpl + q0 : tpl + row;
-  const T* Hb = H_sh ? Ht + q0 * HP : Ht + row * HP;
-  const T* Fb = Ft + row * D;
-  const T* Wsb = Ws + row * M;
-  T* Wdb = Wd + row * M;
-  T* Xdb = Xd + row * D;
-  const int nst = np - 1;
+// ---- MAP_WAVE block kernel: a 2-wave workgroup per block, software-pipelined by chunk.
+// Wave S (serial) integrates chunk k from LDS rows {dt, σdW, H, F} and captures x_j per lane;
+// it issues no global memory operation.  Wave P, in the same period, first finishes chunk
+// k-1 (Girsanov terms G(t_j, x_j)·dt_j, the 64-lane adjacent-pair tree, every global store of
+// the chunk, the per-segment success test) and then prepares chunk k+1 (loads, Philox /
+// Box–Muller normals, the increment-form pCN dW° = fma(ρ, dW, √(1-ρ²)·√dt·Z), σ·dW°) — all
+// lane-parallel.  One __syncthreads per period.  Canonical arithmetic.
+template <class T, int D, int M, int HP>
+struct WaveLds {
+  static constexpr int NR = ((1 + D + D * D + D) + 1) & ~1;  // dt, sdW[D], M[D*D], c[D]
+  static constexpr int NB = 1 + HP + D;                      // dt, H[HP], F[D] (phase B)
+  T rows[2][64][NR];
+  T rowsB[2][64][NB];
+  T xcap[2][64][D];
+  T wcap[2][64][M];  // dW° of each step (stored to W° by phase B)
+  T xend[2][D];
+  T w0[2][M];
+};
 
-  T wf[M], wprev[M];
-#pragma unroll
-  for (int k = 0; k < M; ++k) {
-    wf[k] = (T)0;
-    T w0 = (MODE == MODE_FRESH) ? (T)0 : Wsb[k];
-    wprev[k] = (MODE == MODE_RECOMPUTE) ? w0 : dfma(rho, w0, srho * wf[k]);
+struct ChunkIt {  // (segment, first step) iterator over a block's chunks of 64 steps
+  int g, c0, nst;
+  __device__ __forceinline__ void next(const int32_t* seg_np) {
+    c0 += 64;
+    if (c0 >= nst) { ++g; c0 = 0; nst = seg_np[g] - 1; }
   }
-  if (MODE != MODE_RECOMPUTE && lane == 0) {
-#pragma unroll
-    for (int k = 0; k < M; ++k) Wdb[k] = wprev[k];
-  }
-  T acc = (T)0;
-  const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32), c3 = salt << 1;
-  for (int c0 = 0; c0 < nst; c0 += 64) {
-    const int cnt = nst - c0 < 64 ? nst - c0 : 64;
-    const bool valid = lane < cnt;
-    const int i = c0 + (valid ? lane : cnt - 1);
-    // ---- phase A
-    const T tl = tb[i], tr = tb[i + 1];
-    const T dt = tr - tl;
-    T Hi[HP], Fi[D], Wi[M], Zi[M];
-#pragma unroll
-    for (int c = 0; c < HP; ++c) Hi[c] = Hb[(int64_t)i * HP + c];
-#pragma unroll
-    for (int c = 0; c < D; ++c) Fi[c] = Fb[(int64_t)i * D + c];
-#pragma unroll
-    for (int k = 0; k < M; ++k) Wi[k] = (MODE == MODE_FRESH) ? (T)0 : Wsb[(int64_t)(i + 1) * M + k];
-    T sdt = (T)0;
-    if (MODE != MODE_RECOMPUTE) {
-      sdt = sqrt(dt);
-      uint32_t have = 0xFFFFFFFFu;
-      T z0 = (T)0, z1 = (T)0;
-#pragma unroll
-      for (int k = 0; k < M; ++k) {
-        const uint32_t n = (uint32_t)(i * M + k);
-        if (Zg) {
-          Zi[k] = (T)Zg[(int64_t)i * M + k];
-        } else {
-          if ((n >> 1) != have) {
-            U4 o = philox4x32_10(U4{n >> 1, g, iter, c3}, k0, k1);
-            normal_pair(o, z0, z1);
-            have = n >> 1;
-          }
-          Zi[k] = (n & 1u) ? z1 : z0;
-        }
-      }
-    }
-    T* rw = lds + lane * NRP;
-    rw[0] = dt;
-    rw[1] = sdt;
-#pragma unroll
-    for (int k = 0; k < M; ++k) { rw[2 + k] = (MODE == MODE_RECOMPUTE) ? (T)0 : Zi[k]; rw[2 + M + k] = Wi[k]; }
-#pragma unroll
-    for (int c = 0; c < HP; ++c) rw[2 + 2 * M + c] = Hi[c];
-#pragma unroll
-    for (int c = 0; c < D; ++c) rw[2 + 2 * M + HP + c] = Fi[c];
-    __syncthreads();
-    // ---- phase S
-    T xc[D], wc[M];
-#pragma unroll
-    for (int p = 0; p < D; ++p) xc[p] = x[p];
-#pragma unroll
-    for (int k = 0; k < M; ++k) wc[k] = wprev[k];
-#pragma unroll 4
-    for (int s = 0; s < cnt; ++s) {
-      const T* q = lds + s * NRP;
-      const T dts = q[0];
-      T dW[M];
-#pragma unroll
-      for (int k = 0; k < M; ++k) {
-        T wn;
-        if (MODE == MODE_RECOMPUTE) {
-          wn = q[2 + M + k];
-        } else {
-          wf[k] = dfma(q[1], q[2 + k], wf[k]);
-          wn = dfma(rho, q[2 + M + k], srho * wf[k]);
-        }
-        dW[k] = wn - wprev[k];
-        wprev[k] = wn;
-      }
-      T r[D], b[D];
-#pragma unroll
-      for (int p = 0; p < D; ++p) {
-        T a_ = q[2 + 2 * M + HP + p];
-#pragma unroll
-        for (int c = 0; c < D; ++c) a_ = dfma(-q[2 + 2 * M + packed_idx(D, p, c)], x[c], a_);
-        r[p] = a_;
-      }
-      Mdl::drift(L.th, x, b);
-      const bool mine = (lane == s);
-#pragma unroll
-      for (int p = 0; p < D; ++p) xc[p] = mine ? x[p] : xc[p];
-#pragma unroll
-      for (int k = 0; k < M; ++k) wc[k] = mine ? wprev[k] : wc[k];
-      euler_step<Mdl, T>(L, r, b, dts, dW, x);
-    }
-    __syncthreads();
-    // ---- phase B
-    T rr[D], bb[D];
-    const T G = g_at<Mdl, T>(L, Hi, Fi, xc, rr, bb);
-    const T csum = wave_tree_sum<T>(valid ? G * dt : (T)0);
-    acc = acc + (csum + (T)0);
-    if (valid) {
-#pragma unroll
-      for (int p = 0; p < D; ++p) Xdb[(int64_t)i * D + p] = xc[p];
-      if (MODE != MODE_RECOMPUTE) {
-#pragma unroll
-        for (int k = 0; k < M; ++k) Wdb[(int64_t)(i + 1) * M + k] = wc[k];
-      }
-    }
-  }
-  if (lane == 0) {
-#pragma unroll
-    for (int p = 0; p < D; ++p) Xdb[(int64_t)nst * D + p] = x[p];
-  }
-  sl = acc;
-  bool ok = isfinite(sl);
-#pragma unroll
-  for (int p = 0; p < D; ++p) ok = ok && isfinite(x[p]);
-  return ok;
-}
+};
 
-template <class Mdl, class T, int MODE>
-__global__ __launch_bounds__(64) void k_block_wave(const BlockArgs<T> a) {
+// DIAG (timing diagnostics only, never selected in production): bit 0 = S skips its
+// recursion, bit 1 = P skips phase A, bit 2 = P skips phase B.
+template <class Mdl, class T, int MODE, int DIAG = 0>
+__global__ __launch_bounds__(128) void k_block_wave(const BlockArgs<T> a) {
   constexpr int D = Mdl::D, M = Mdl::M, HP = D * (D + 1) / 2;
-  constexpr int NRP = ((2 + 2 * M + HP + D) + 1) & ~1;
-  __shared__ T lds[64 * NRP];
-  const int lane = threadIdx.x;
+  using Lds = WaveLds<T, D, M, HP>;
+  constexpr int NR = Lds::NR;
+  __shared__ Lds sh;
+  const int lane = threadIdx.x & 63;
+  const bool is_s = threadIdx.x < 64;
   const int64_t blk = a.b0 + (int64_t)blockIdx.x;
   if (blk >= a.b1) return;
   const int64_t r = a.blk_rec[blk];
   const int64_t tq = a.tile_qoff[r];
   const int g0 = a.gfirst[blk], g1 = a.glast[blk];
   const bool term = a.term[blk] != 0;
+  const T rho = (MODE == MODE_FRESH) ? (T)0 : (T)a.rho[blk];
+  const T srho = (MODE == MODE_FRESH) ? (T)1 : (T)a.srho[blk];
+  int ktot = 0;
+  for (int g = g0; g <= g1; ++g) ktot += (a.seg_np[g] - 1 + 63) / 64;
+  auto law_of = [&](int g, int& kind) -> int {
+    kind = (!term && g == g1) ? 1 : 0;
+    return (kind ? a.selPPB[g] : a.selPP[g]) ^ a.law_flip;
+  };
   T x[D];
   {
     const T* Xs = a.X[a.selX[g0] ^ a.xs_flip];
@@ -494,39 +391,219 @@ __global__ __launch_bounds__(64) void k_block_wave(const BlockArgs<T> a) {
 #pragma unroll
     for (int p = 0; p < D; ++p) x[p] = Xs[(tq + q) * D + p];
   }
+
+  if (is_s) {
+    // ======================= wave S
+    ChunkIt it{g0, 0, a.seg_np[g0] - 1};
+    Law<Mdl, T> L;
+    int lg = -1;
+    __syncthreads();  // period 0: P prepares chunk 0
+    for (int k = 0; k < ktot; ++k) {
+      if (it.g != lg) {
+        int kind;
+        const int ls = law_of(it.g, kind);
+        L.load(a.law[ls][kind] + (int64_t)it.g * DMT_LAW_STRIDE);
+        lg = it.g;
+      }
+      const int cnt = (DIAG & 1) ? 0 : min(64, it.nst - it.c0);
+      const T(*rw)[NR] = sh.rows[k & 1];
+      T xc[D];
+#pragma unroll
+      for (int p = 0; p < D; ++p) xc[p] = x[p];
+#pragma unroll 4
+      for (int s = 0; s < cnt; ++s) {
+        const T* q = rw[s];
+        T b_[D];
+        if (!Mdl::kLinear) Mdl::drift(L.th, x, b_);
+        const bool mine = lane == s;
+#pragma unroll
+        for (int p = 0; p < D; ++p) xc[p] = mine ? x[p] : xc[p];
+        euler_step<Mdl, T>(q + 1 + D, q + 1 + D + D * D, b_, q[0], q + 1, x);
+      }
+#pragma unroll
+      for (int p = 0; p < D; ++p) sh.xcap[k & 1][lane][p] = xc[p];
+      const bool seg_end = it.c0 + 64 >= it.nst;
+      if (seg_end && lane == 0) {
+#pragma unroll
+        for (int p = 0; p < D; ++p) sh.xend[k & 1][p] = x[p];
+      }
+      if (k + 1 < ktot) it.next(a.seg_np);
+      __syncthreads();
+    }
+    __syncthreads();  // period ktot+1: P finishes the last chunk
+    return;
+  }
+
+  // ======================= wave P
+  ChunkIt ia{g0, 0, a.seg_np[g0] - 1};  // chunk being prepared (A)
+  ChunkIt ib{g0, 0, a.seg_np[g0] - 1};  // chunk being finished (B)
   T ll;
   {
-    const int ls = a.selPP[g0] ^ a.law_flip;
-    const double* Lr = a.law[ls][0] + (int64_t)g0 * DMT_LAW_STRIDE;
     const int64_t q = a.seg_q[g0];
+    const int lsp = a.selPP[g0] ^ a.law_flip;
     T H0[HP], F0[D];
 #pragma unroll
     for (int c = 0; c < HP; ++c)
-      H0[c] = a.H_shared[ls][0] ? a.H[ls][0][q * HP + c] : a.H[ls][0][(tq + q) * HP + c];
+      H0[c] = a.H_shared[lsp][0] ? a.H[lsp][0][q * HP + c] : a.H[lsp][0][(tq + q) * HP + c];
 #pragma unroll
-    for (int c = 0; c < D; ++c) F0[c] = a.F[ls][0][(tq + q) * D + c];
-    ll = obs_term<D, T>(H0, F0, x, (T)Lr[DMT_LAW_C0]);
+    for (int c = 0; c < D; ++c) F0[c] = a.F[lsp][0][(tq + q) * D + c];
+    ll = obs_term<D, T>(H0, F0, x, (T)a.law[lsp][0][(int64_t)g0 * DMT_LAW_STRIDE + DMT_LAW_C0]);
   }
   bool ok = true;
-  const T rho = (MODE == MODE_FRESH) ? (T)0 : (T)a.rho[blk];
-  const T srho = (MODE == MODE_FRESH) ? (T)1 : (T)a.srho[blk];
-  for (int g = g0; g <= g1; ++g) {
-    const int kind = (!term && g == g1) ? 1 : 0;
-    const int ls = (kind ? a.selPPB[g] : a.selPP[g]) ^ a.law_flip;
-    Law<Mdl, T> L;
-    L.load(a.law[ls][kind] + (int64_t)g * DMT_LAW_STRIDE);
-    const double* Zg = a.Z ? a.Z + a.st_off[g] * M : nullptr;
-    T* Xd = a.X[a.selX[g] ^ a.xd_flip];
-    const T* Ws = a.W[a.selW[g] ^ a.ws_flip];
-    T* Wd = a.W[a.selW[g] ^ a.wd_flip];
-    const int64_t q0 = a.seg_q[g];
-    T sl;
-    const bool sok = run_segment_wave<Mdl, T, MODE>(
-        L, a.t, a.t_shared, a.H[ls][kind], a.H_shared[ls][kind], a.F[ls][kind], Ws, Wd, Xd, Zg,
-        a.seed, (uint32_t)g, a.iter, a.salt, tq + q0, q0, a.seg_np[g], lane, rho, srho, x, sl, lds);
-    if (!sok) { ok = false; break; }
-    ll = ll + sl;
+  int stop_after = 0x7fffffff;  // chunks after a failed segment store nothing
+  T seg_acc = (T)0;
+  Law<Mdl, T> LB;
+  int lgb = -1;
+  Law<Mdl, T> LA;  // law of the chunk being prepared (sigma, a, linear drift)
+  int lga = -1;
+  const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32), c3 = a.salt << 1;
+
+  auto prepare = [&](int k) {  // phase A of chunk k (iterator ia), lane-parallel
+    const int g = ia.g, c0 = ia.c0, nst = ia.nst;
+    int kind;
+    const int ls = law_of(g, kind);
+    if (g != lga) {
+      LA.load(a.law[ls][kind] + (int64_t)g * DMT_LAW_STRIDE);
+      lga = g;
+    }
+    const int64_t q0 = a.seg_q[g], row = tq + q0;
+    const T* tb = a.t_shared ? a.t + q0 : a.t + row;
+    const T* Hb = a.H_shared[ls][kind] ? a.H[ls][kind] + q0 * HP : a.H[ls][kind] + row * HP;
+    const T* Fb = a.F[ls][kind] + row * D;
+    const T* Wsb = a.W[a.selW[g] ^ a.ws_flip] + row * M;
+    const int cnt = min(64, nst - c0);
+    const bool valid = lane < cnt;
+    const int i = c0 + (valid ? lane : cnt - 1);
+    if (MODE != MODE_RECOMPUTE && c0 == 0 && lane == 0) {
+#pragma unroll
+      for (int kk = 0; kk < M; ++kk) sh.w0[k & 1][kk] = rho * ((MODE == MODE_FRESH) ? (T)0 : Wsb[kk]);
+    }
+    const T dt = tb[i + 1] - tb[i];
+    T dW[M];
+    if (MODE == MODE_RECOMPUTE) {
+#pragma unroll
+      for (int kk = 0; kk < M; ++kk) dW[kk] = Wsb[(int64_t)(i + 1) * M + kk];
+    } else {
+      const double* Zg = a.Z ? a.Z + a.st_off[g] * M : nullptr;
+      uint32_t have = 0xFFFFFFFFu;
+      T z0 = (T)0, z1 = (T)0;
+      const T sdt = sqrt(dt);
+#pragma unroll
+      for (int kk = 0; kk < M; ++kk) {
+        const uint32_t n = (uint32_t)(i * M + kk);
+        T z;
+        if (Zg) {
+          z = (T)Zg[(int64_t)i * M + kk];
+        } else {
+          if ((n >> 1) != have) {
+            U4 o = philox4x32_10(U4{n >> 1, (uint32_t)g, a.iter, c3}, k0, k1);
+            normal_pair(o, z0, z1);
+            have = n >> 1;
+          }
+          z = (n & 1u) ? z1 : z0;
+        }
+        const T w = (MODE == MODE_FRESH) ? (T)0 : Wsb[(int64_t)(i + 1) * M + kk];
+        dW[kk] = dfma(rho, w, srho * (sdt * z));
+      }
+    }
+    T Hi[HP], Fi[D], Mg[D * D], cg[D], sdW[D];
+#pragma unroll
+    for (int c = 0; c < HP; ++c) Hi[c] = Hb[(int64_t)i * HP + c];
+#pragma unroll
+    for (int c = 0; c < D; ++c) Fi[c] = Fb[(int64_t)i * D + c];
+    sigma_dw<Mdl, T>(LA, dW, sdW);
+    guide_coeffs<Mdl, T>(LA, Hi, Fi, Mg, cg);
+    T* rw = sh.rows[k & 1][lane];
+    rw[0] = dt;
+#pragma unroll
+    for (int p = 0; p < D; ++p) rw[1 + p] = sdW[p];
+#pragma unroll
+    for (int e = 0; e < D * D; ++e) rw[1 + D + e] = Mg[e];
+#pragma unroll
+    for (int p = 0; p < D; ++p) rw[1 + D + D * D + p] = cg[p];
+    T* rb = sh.rowsB[k & 1][lane];
+    rb[0] = dt;
+#pragma unroll
+    for (int c = 0; c < HP; ++c) rb[1 + c] = Hi[c];
+#pragma unroll
+    for (int c = 0; c < D; ++c) rb[1 + HP + c] = Fi[c];
+#pragma unroll
+    for (int kk = 0; kk < M; ++kk) sh.wcap[k & 1][lane][kk] = dW[kk];
+  };
+
+  auto finish = [&](int k) {  // phase B of chunk k (iterator ib)
+    const int g = ib.g, c0 = ib.c0, nst = ib.nst;
+    int kind;
+    const int ls = law_of(g, kind);
+    if (g != lgb) {
+      LB.load(a.law[ls][kind] + (int64_t)g * DMT_LAW_STRIDE);
+      lgb = g;
+    }
+    const int cnt = min(64, nst - c0);
+    const bool valid = lane < cnt;
+    const T* rw = sh.rowsB[k & 1][lane];
+    T Hi[HP], Fi[D], xi[D], rr[D], bb[D];
+#pragma unroll
+    for (int c = 0; c < HP; ++c) Hi[c] = rw[1 + c];
+#pragma unroll
+    for (int c = 0; c < D; ++c) { Fi[c] = rw[1 + HP + c]; xi[c] = sh.xcap[k & 1][lane][c]; }
+    const T G = g_at<Mdl, T>(LB, Hi, Fi, xi, rr, bb);
+    const T csum = wave_tree_sum<T>(valid ? G * rw[0] : (T)0);
+    seg_acc = seg_acc + (csum + (T)0);
+    const bool seg_end = c0 + 64 >= nst;
+    if (k <= stop_after) {
+      const int64_t row = tq + a.seg_q[g];
+      T* Xdb = a.X[a.selX[g] ^ a.xd_flip] + row * D;
+      T* Wdb = a.W[a.selW[g] ^ a.wd_flip] + row * M;
+      if (valid) {
+        const int i = c0 + lane;
+#pragma unroll
+        for (int p = 0; p < D; ++p) Xdb[(int64_t)i * D + p] = xi[p];
+        if (MODE != MODE_RECOMPUTE) {
+#pragma unroll
+          for (int kk = 0; kk < M; ++kk) Wdb[(int64_t)(i + 1) * M + kk] = sh.wcap[k & 1][lane][kk];
+        }
+      }
+      if (lane == 0) {
+        if (MODE != MODE_RECOMPUTE && c0 == 0) {
+#pragma unroll
+          for (int kk = 0; kk < M; ++kk) Wdb[kk] = sh.w0[k & 1][kk];
+        }
+        if (seg_end) {
+#pragma unroll
+          for (int p = 0; p < D; ++p) Xdb[(int64_t)nst * D + p] = sh.xend[k & 1][p];
+        }
+      }
+    }
+    if (seg_end) {
+      if (k <= stop_after) {
+        bool sok = isfinite(seg_acc);
+#pragma unroll
+        for (int p = 0; p < D; ++p) sok = sok && isfinite(sh.xend[k & 1][p]);
+        if (sok) {
+          ll = ll + seg_acc;
+        } else {
+          ok = false;
+          stop_after = k;
+        }
+      }
+      seg_acc = (T)0;
+    }
+  };
+
+  for (int p = 0; p <= ktot; ++p) {
+    if (p >= 2) {
+      if (!(DIAG & 4)) finish(p - 2);
+      if (p - 2 + 1 < ktot) ib.next(a.seg_np);
+    }
+    if (p < ktot) {
+      if (!(DIAG & 2)) prepare(p);
+      if (p + 1 < ktot) ia.next(a.seg_np);
+    }
+    __syncthreads();
   }
+  finish(ktot - 1);
+  __syncthreads();
   if (lane == 0) {
     a.ll_out[blk] = ok ? (double)ll : -INFINITY;
     if (a.success) a.success[blk] = ok ? 1 : 0;
@@ -615,6 +692,75 @@ __global__ __launch_bounds__(256) void k_accept(const AcceptArgs a) {
   if (a.acc_out) a.acc_out[blk - a.b0] = acc ? 1 : 0;
 }
 
+// accept_reject + the first level of the fetch_ll tree in one pass: each thread decides its
+// block (as k_accept), then the 1024-block group reduces (ll, ll°, accepted) exactly as
+// k_tree_level<true> does on the post-decision values.  With one group the final
+// canonicalised result is written directly.
+__global__ __launch_bounds__(1024) void k_accept_reduce(const AcceptArgs a, double* __restrict__ out,
+                                                        int64_t nout, double* __restrict__ out3) {
+  __shared__ double w0[16], w1[16], w2[16];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int64_t blk = a.b0 + (int64_t)blockIdx.x * 1024 + tid;
+  double v0 = 0.0, v1 = 0.0, v2 = 0.0;
+  if (blk < a.b1) {
+    const double E = a.E ? a.E[blk - a.b0]
+                         : exp1_draw(a.seed, (uint32_t)blk, (uint32_t)a.mcmciter, a.salt);
+    double ll = a.ll[blk], llp = a.llp[blk];
+    const bool acc = E > -(llp - ll);
+    if (acc) {
+      for (int g = a.gfirst[blk]; g <= a.glast[blk]; ++g) {
+        a.selX[g] ^= 1;
+        a.selW[g] ^= 1;
+      }
+    }
+    if (a.hist_len > 0) {
+      const int64_t o = (a.mcmciter - 1) * a.nblocks + blk;
+      a.acc_hist[o] = acc ? 1 : 0;
+      a.ll_hist[o] = ll;
+      a.llp_hist[o] = llp;
+    }
+    if (acc) {
+      a.ll[blk] = llp;
+      a.llp[blk] = ll;
+      const double t = ll; ll = llp; llp = t;
+    }
+    if (a.acc_out) a.acc_out[blk - a.b0] = acc ? 1 : 0;
+    v0 = ll;
+    v1 = llp;
+    v2 = acc ? 1.0 : 0.0;
+  }
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    v0 = v0 + __shfl_xor(v0, off, 64);
+    v1 = v1 + __shfl_xor(v1, off, 64);
+    v2 = v2 + __shfl_xor(v2, off, 64);
+  }
+  if (lane == 0) { w0[wv] = v0; w1[wv] = v1; w2[wv] = v2; }
+  __syncthreads();
+  if (wv == 0) {
+    v0 = lane < 16 ? w0[lane] : 0.0;
+    v1 = lane < 16 ? w1[lane] : 0.0;
+    v2 = lane < 16 ? w2[lane] : 0.0;
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) {
+      v0 = v0 + __shfl_xor(v0, off, 64);
+      v1 = v1 + __shfl_xor(v1, off, 64);
+      v2 = v2 + __shfl_xor(v2, off, 64);
+    }
+    if (lane == 0) {
+      if (nout == 1) {
+        out3[0] = v0 + 0.0;
+        out3[1] = v1 + 0.0;
+        out3[2] = v2;
+      } else {
+        out[blockIdx.x] = v0;
+        out[nout + blockIdx.x] = v1;
+        out[2 * nout + blockIdx.x] = v2;
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------- small utility kernels
 __global__ void k_flip(uint8_t* sel, const int32_t* gfirst, const int32_t* glast,
                        const uint8_t* term, int only_nonterm, int64_t b0, int64_t b1) {
@@ -649,12 +795,14 @@ __device__ __forceinline__ int64_t find_seg(const int64_t* pt_off, int64_t G, in
   return lo;
 }
 
+// Reference layout -> planes.  incr: the source is a cumulative Wiener path; the planes get
+// row 0 = W(t0) and row i+1 = W(t_{i+1}) - W(t_i), computed in the working precision.
 template <class T>
 __global__ void k_to_planes(const int tw, const double* __restrict__ src, T* dst0, T* dst1,
                             const uint8_t* __restrict__ sel, int flip, int C, int64_t P,
                             const int64_t* __restrict__ pt_off, int64_t G,
                             const int32_t* __restrict__ seg_rec, const int32_t* __restrict__ seg_q,
-                            const int64_t* __restrict__ tile_qoff) {
+                            const int64_t* __restrict__ tile_qoff, int incr) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= P * C) return;
   const int64_t p = e / C;
@@ -664,7 +812,33 @@ __global__ void k_to_planes(const int tw, const double* __restrict__ src, T* dst
   const int64_t q = seg_q[g] + (p - pt_off[g]);
   const int64_t o = ((tile_qoff[r / tw] + q) * C + c) * tw + (r % tw);
   const int slot = sel ? ((sel[g] ^ flip) & 1) : 0;
-  (slot ? dst1 : dst0)[o] = (T)src[e];
+  T v = (T)src[e];
+  if (incr && p > pt_off[g]) v = v - (T)src[e - C];
+  (slot ? dst1 : dst0)[o] = v;
+}
+
+// planes (increments) -> cumulative reference layout: one thread per (segment, component)
+template <class T>
+__global__ void k_from_planes_incr(const int tw, double* __restrict__ dst, const T* src0,
+                                   const T* src1, const uint8_t* __restrict__ sel, int flip, int C,
+                                   int64_t G, const int64_t* __restrict__ pt_off,
+                                   const int32_t* __restrict__ seg_np,
+                                   const int32_t* __restrict__ seg_rec,
+                                   const int32_t* __restrict__ seg_q,
+                                   const int64_t* __restrict__ tile_qoff) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= G * C) return;
+  const int64_t g = e / C;
+  const int c = (int)(e % C);
+  const int64_t r = seg_rec[g];
+  const int slot = sel ? ((sel[g] ^ flip) & 1) : 0;
+  const T* src = slot ? src1 : src0;
+  T acc = (T)0;
+  for (int i = 0; i < seg_np[g]; ++i) {
+    const int64_t o = ((tile_qoff[r / tw] + seg_q[g] + i) * C + c) * tw + (r % tw);
+    acc = i == 0 ? src[o] : acc + src[o];
+    dst[(pt_off[g] + i) * C + c] = (double)acc;
+  }
 }
 
 template <class T>
@@ -692,65 +866,61 @@ __global__ void k_cast(const double* __restrict__ src, T* __restrict__ dst, int6
   if (e < n) dst[e] = (T)src[e];
 }
 
-// Deterministic sum over n leaves: the complete adjacent-pair binary tree over the
-// leaves padded with zeros to a power of two, one workgroup of 1024.
-__global__ __launch_bounds__(1024) void k_block_sum(const double* __restrict__ ll,
-                                                    const double* __restrict__ llp,
-                                                    const uint8_t* __restrict__ acc, int64_t n,
-                                                    double* __restrict__ out3) {
-  __shared__ double s0[1024], s1[1024];
-  __shared__ long long sc[1024];
-  const int tid = threadIdx.x;
-  int64_t n2 = 1;
-  while (n2 < n) n2 <<= 1;
-  const int64_t per = n2 > 1024 ? n2 / 1024 : 1;  // leaves per thread (power of two)
-  const int nthr = (int)(n2 > 1024 ? 1024 : n2);
-  double a = 0.0, b = 0.0;
-  long long c = 0;
-  if (tid < nthr) {
-    PSum<double> pa, pb;  // stack pairwise over exactly `per` leaves (zeros padded)
-    pa.init(); pb.init();
-    int64_t base = (int64_t)tid * per;
-    double ra = 0.0, rb = 0.0;
-    if (per == 1) {
-      ra = base < n ? ll[base] : 0.0;
-      rb = base < n ? llp[base] : 0.0;
-      if (acc && base < n) c = acc[base];
+// Deterministic sum over n leaves: the complete adjacent-pair binary tree over the leaves
+// padded with zeros to a power of two.  One level reduces aligned groups of
+// 1024 leaves per workgroup (64-lane xor-shuffle trees, then a 16-leaf tree of the wave
+// sums); levels repeat until one value is left.  A zero-padded group equals the smaller
+// power-of-two tree up to the sign of a zero, which the final "+ 0.0" canonicalises.
+template <bool FIRST>
+__global__ __launch_bounds__(1024) void k_tree_level(const double* __restrict__ a0,
+                                                     const double* __restrict__ a1,
+                                                     const uint8_t* __restrict__ acc, int64_t n,
+                                                     double* __restrict__ out, int64_t nout) {
+  __shared__ double w0[16], w1[16], w2[16];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int64_t i = (int64_t)blockIdx.x * 1024 + tid;
+  double v0 = 0.0, v1 = 0.0, v2 = 0.0;
+  if (i < n) {
+    if (FIRST) {
+      v0 = a0[i];
+      v1 = a1[i];
+      v2 = acc ? (double)acc[i] : 0.0;
     } else {
-      // `per` is a power of two >= 2: adjacent-pair tree over the run by a binary counter
-      double sa[48], sb[48];
-      for (int64_t j = 0; j < per; ++j) {
-        const int64_t i = base + j;
-        double va = i < n ? ll[i] : 0.0;
-        double vb = i < n ? llp[i] : 0.0;
-        if (acc && i < n) c += acc[i];
-        int lvl = 0;
-        for (int64_t k = j; k & 1; k >>= 1, ++lvl) { va = sa[lvl] + va; vb = sb[lvl] + vb; }
-        sa[lvl] = va;
-        sb[lvl] = vb;
-      }
-      int top = 0;
-      while (((int64_t)1 << top) < per) ++top;
-      ra = sa[top];
-      rb = sb[top];
+      v0 = a0[i];
+      v1 = a0[n + i];
+      v2 = a0[2 * n + i];
     }
-    a = ra; b = rb;
   }
-  s0[tid] = a; s1[tid] = b; sc[tid] = c;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    v0 = v0 + __shfl_xor(v0, off, 64);
+    v1 = v1 + __shfl_xor(v1, off, 64);
+    v2 = v2 + __shfl_xor(v2, off, 64);
+  }
+  if (lane == 0) { w0[wv] = v0; w1[wv] = v1; w2[wv] = v2; }
   __syncthreads();
-  for (int w = 1024; w > 1; w >>= 1) {
-    if (tid < w / 2) {
-      s0[tid] = s0[2 * tid] + s0[2 * tid + 1];
-      s1[tid] = s1[2 * tid] + s1[2 * tid + 1];
-      sc[tid] = sc[2 * tid] + sc[2 * tid + 1];
+  if (wv == 0) {
+    v0 = lane < 16 ? w0[lane] : 0.0;
+    v1 = lane < 16 ? w1[lane] : 0.0;
+    v2 = lane < 16 ? w2[lane] : 0.0;
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) {
+      v0 = v0 + __shfl_xor(v0, off, 64);
+      v1 = v1 + __shfl_xor(v1, off, 64);
+      v2 = v2 + __shfl_xor(v2, off, 64);
     }
-    __syncthreads();
+    if (lane == 0) {
+      out[blockIdx.x] = v0;
+      out[nout + blockIdx.x] = v1;
+      out[2 * nout + blockIdx.x] = v2;
+    }
   }
-  if (tid == 0) {
-    out3[0] = s0[0] + 0.0;
-    out3[1] = s1[0] + 0.0;
-    out3[2] = (double)sc[0];
-  }
+}
+
+__global__ void k_tree_final(const double* __restrict__ in, int64_t nout, double* __restrict__ out3) {
+  out3[0] = in[0] + 0.0;
+  out3[1] = in[nout] + 0.0;
+  out3[2] = in[2 * nout];
 }
 
 __global__ void k_debug_philox(uint64_t seed, const uint32_t* ctr, int64_t n, uint32_t* out,
@@ -769,6 +939,15 @@ __global__ void k_debug_philox(uint64_t seed, const uint32_t* ctr, int64_t n, ui
 // ---------------------------------------------------------------- launchers
 static inline unsigned nblk(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
 
+// DMT_DIAG: timing-diagnostic kernel variants (see k_block_wave); 0 in production.
+static int diag_flags() {
+  static int v = [] {
+    const char* e = getenv("DMT_DIAG");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 constexpr int kChunk = 4;
 
 template <class Mdl, class T>
@@ -778,10 +957,23 @@ static hipError_t launch_block_t(int mapping, int mode, const void* args, int64_
   if (nwaves <= 0) return hipSuccess;
   dim3 grid((unsigned)nwaves), block(64);
   if (mapping == MAP_WAVE) {
+    const dim3 wblock(128);
+    if (diag_flags() != 0 && mode == MODE_PCN) {
+      if constexpr (std::is_same<Mdl, OU<double, 2, 2>>::value) {
+        switch (diag_flags()) {
+          case 1: k_block_wave<Mdl, T, MODE_PCN, 1><<<grid, wblock, 0, s>>>(a); break;
+          case 2: k_block_wave<Mdl, T, MODE_PCN, 2><<<grid, wblock, 0, s>>>(a); break;
+          case 4: k_block_wave<Mdl, T, MODE_PCN, 4><<<grid, wblock, 0, s>>>(a); break;
+          case 6: k_block_wave<Mdl, T, MODE_PCN, 6><<<grid, wblock, 0, s>>>(a); break;
+          default: k_block_wave<Mdl, T, MODE_PCN, 0><<<grid, wblock, 0, s>>>(a); break;
+        }
+        return hipGetLastError();
+      }
+    }
     switch (mode) {
-      case MODE_PCN: k_block_wave<Mdl, T, MODE_PCN><<<grid, block, 0, s>>>(a); break;
-      case MODE_RECOMPUTE: k_block_wave<Mdl, T, MODE_RECOMPUTE><<<grid, block, 0, s>>>(a); break;
-      case MODE_FRESH: k_block_wave<Mdl, T, MODE_FRESH><<<grid, block, 0, s>>>(a); break;
+      case MODE_PCN: k_block_wave<Mdl, T, MODE_PCN><<<grid, wblock, 0, s>>>(a); break;
+      case MODE_RECOMPUTE: k_block_wave<Mdl, T, MODE_RECOMPUTE><<<grid, wblock, 0, s>>>(a); break;
+      case MODE_FRESH: k_block_wave<Mdl, T, MODE_FRESH><<<grid, wblock, 0, s>>>(a); break;
       default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -863,15 +1055,33 @@ hipError_t launch_accept(const AcceptArgs& a, hipStream_t s) {
 hipError_t launch_to_planes(int precision, int tw, const double* src, void* dst0, void* dst1,
                             const uint8_t* sel, int flip, int C, int64_t P, const int64_t* pt_off,
                             int64_t G, const int32_t* seg_rec, const int32_t* seg_q,
-                            const int64_t* tile_qoff, hipStream_t s) {
+                            const int64_t* tile_qoff, hipStream_t s, int incr) {
   const int64_t n = P * C;
   if (n <= 0) return hipSuccess;
   if (precision == DMT_F64)
     k_to_planes<double><<<nblk(n, 256), 256, 0, s>>>(tw, src, (double*)dst0, (double*)dst1, sel, flip,
-                                                      C, P, pt_off, G, seg_rec, seg_q, tile_qoff);
+                                                      C, P, pt_off, G, seg_rec, seg_q, tile_qoff, incr);
   else
     k_to_planes<float><<<nblk(n, 256), 256, 0, s>>>(tw, src, (float*)dst0, (float*)dst1, sel, flip, C,
-                                                     P, pt_off, G, seg_rec, seg_q, tile_qoff);
+                                                     P, pt_off, G, seg_rec, seg_q, tile_qoff, incr);
+  return hipGetLastError();
+}
+
+hipError_t launch_from_planes_incr(int precision, int tw, double* dst, const void* src0,
+                                   const void* src1, const uint8_t* sel, int flip, int C,
+                                   int64_t G, const int64_t* pt_off, const int32_t* seg_np,
+                                   const int32_t* seg_rec, const int32_t* seg_q,
+                                   const int64_t* tile_qoff, hipStream_t s) {
+  const int64_t n = G * C;
+  if (n <= 0) return hipSuccess;
+  if (precision == DMT_F64)
+    k_from_planes_incr<double><<<nblk(n, 64), 64, 0, s>>>(tw, dst, (const double*)src0,
+                                                          (const double*)src1, sel, flip, C, G,
+                                                          pt_off, seg_np, seg_rec, seg_q, tile_qoff);
+  else
+    k_from_planes_incr<float><<<nblk(n, 64), 64, 0, s>>>(tw, dst, (const float*)src0,
+                                                         (const float*)src1, sel, flip, C, G,
+                                                         pt_off, seg_np, seg_rec, seg_q, tile_qoff);
   return hipGetLastError();
 }
 
@@ -902,8 +1112,42 @@ hipError_t launch_cast(int precision, const double* src, void* dst, int64_t n, h
 }
 
 hipError_t launch_block_sum(const double* ll, const double* llp, const uint8_t* acc, int64_t n,
-                            double* out3, hipStream_t s) {
-  k_block_sum<<<1, 1024, 0, s>>>(ll, llp, acc, n, out3);
+                            double* work, double* out3, hipStream_t s) {
+  // work: 2 × 3 × ceil(n/1024) doubles (ping-pong partials)
+  int64_t groups = (n + 1023) / 1024;
+  if (groups < 1) groups = 1;
+  double* bufs[2] = {work, work + 3 * groups};
+  k_tree_level<true><<<(unsigned)groups, 1024, 0, s>>>(ll, llp, acc, n, bufs[0], groups);
+  // (a single group still goes through k_tree_final for the canonical "+ 0.0")
+  int cur = 0;
+  int64_t m = groups;
+  while (m > 1) {
+    const int64_t g2 = (m + 1023) / 1024;
+    k_tree_level<false><<<(unsigned)g2, 1024, 0, s>>>(bufs[cur], nullptr, nullptr, m, bufs[cur ^ 1], g2);
+    cur ^= 1;
+    m = g2;
+  }
+  k_tree_final<<<1, 1, 0, s>>>(bufs[cur], m, out3);
+  return hipGetLastError();
+}
+
+// accept + fetch tree (ll, ll°, accepted of this iteration) over [b0, b1)
+hipError_t launch_accept_reduce(const AcceptArgs& a, double* work, double* out3, hipStream_t s) {
+  const int64_t n = a.b1 - a.b0;
+  int64_t groups = (n + 1023) / 1024;
+  if (groups < 1) groups = 1;
+  double* bufs[2] = {work, work + 3 * groups};
+  k_accept_reduce<<<(unsigned)groups, 1024, 0, s>>>(a, bufs[0], groups, out3);
+  if (groups == 1) return hipGetLastError();
+  int cur = 0;
+  int64_t m = groups;
+  while (m > 1) {
+    const int64_t g2 = (m + 1023) / 1024;
+    k_tree_level<false><<<(unsigned)g2, 1024, 0, s>>>(bufs[cur], nullptr, nullptr, m, bufs[cur ^ 1], g2);
+    cur ^= 1;
+    m = g2;
+  }
+  k_tree_final<<<1, 1, 0, s>>>(bufs[cur], m, out3);
   return hipGetLastError();
 }
 

@@ -115,6 +115,9 @@ struct dmt_ens {
   double* d_Z = nullptr;
   int64_t Z_n = 0;
   double* d_red = nullptr;  // [3] reduction output, [3 * nranks] gather
+  double* d_red_work = nullptr;
+  int64_t red_work_n = 0;
+  double* h_red = nullptr;  // pinned host copy of the 3 reduction results
   double* d_gather = nullptr;
   std::vector<std::unique_ptr<Layout>> layouts;  // layouts[0] = internal "unit" layout
   // timing
@@ -646,6 +649,7 @@ dmt_status dmt_create(dmt_ens** out, const dmt_model* model, const dmt_structure
     HIP_OK(hipMemset(hp->d_W[s], 0, plane_elems(hp, hp->m) * hp->esz));
   }
   DMT_TRY(ens_alloc(hp, &hp->d_red, 3));
+  HIP_OK(hipHostMalloc((void**)&hp->h_red, 3 * sizeof(double), hipHostMallocDefault));
   // internal layout 0: one terminal block per recording over all its segments, ρ = 0
   // (the view draw_proposal_path!(u::SamplingUnit) acts on, src/sampling_unit.jl:118-120)
   {
@@ -671,7 +675,8 @@ dmt_status dmt_destroy(dmt_ens* h) {
     if (L) L->release();
   void* ps[] = {h->d_pt_off, h->d_st_off, h->d_tile_qoff, h->d_seg_rec, h->d_seg_q, h->d_seg_np,
                 h->d_sel[0], h->d_sel[1], h->d_sel[2], h->d_sel[3], h->d_X[0], h->d_X[1],
-                h->d_W[0], h->d_W[1], h->d_t, h->d_stage, h->d_Z, h->d_red, h->d_gather};
+                h->d_W[0], h->d_W[1], h->d_t, h->d_stage, h->d_Z, h->d_red, h->d_gather,
+                h->d_red_work};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   for (int s = 0; s < 2; ++s)
@@ -681,6 +686,7 @@ dmt_status dmt_destroy(dmt_ens* h) {
       if (h->d_law[s][k]) (void)hipFree(h->d_law[s][k]);
     }
   if (h->comm) (void)ncclCommDestroy(h->comm);
+  if (h->h_red) (void)hipHostFree(h->h_red);
   (void)hipStreamDestroy(h->stream);
   delete h;
   return DMT_OK;
@@ -820,9 +826,10 @@ dmt_status dmt_set_paths(dmt_ens* h, int32_t unit, const double* X, const double
     DMT_TRY(ensure_stage(h, h->P * C[w]));
     HIP_OK(hipMemcpyAsync(h->d_stage, src[w], h->P * C[w] * 8, hipMemcpyHostToDevice, h->stream));
     void** dst = w == 0 ? h->d_X : h->d_W;
+    // Wiener paths are held as increments on the device
     HIP_OK(launch_to_planes(h->key.precision, h->tw, h->d_stage, dst[0], dst[1], h->d_sel[w], unit, C[w],
                             h->P, h->d_pt_off, h->G, h->d_seg_rec, h->d_seg_q, h->d_tile_qoff,
-                            h->stream));
+                            h->stream, w == 1 ? 1 : 0));
   }
   HIP_OK(hipStreamSynchronize(h->stream));
   return DMT_OK;
@@ -835,9 +842,14 @@ dmt_status dmt_download_paths(dmt_ens* h, int32_t unit, int32_t what, double* ou
   const int C = what == 0 ? h->d : h->m;
   DMT_TRY(ensure_stage(h, h->P * C));
   void** src = what == 0 ? h->d_X : h->d_W;
-  HIP_OK(launch_from_planes(h->key.precision, h->tw, h->d_stage, src[0], src[1], h->d_sel[what], unit, C,
-                            h->P, h->d_pt_off, h->G, h->d_seg_rec, h->d_seg_q, h->d_tile_qoff,
-                            h->stream));
+  if (what == 0)
+    HIP_OK(launch_from_planes(h->key.precision, h->tw, h->d_stage, src[0], src[1], h->d_sel[what], unit,
+                              C, h->P, h->d_pt_off, h->G, h->d_seg_rec, h->d_seg_q, h->d_tile_qoff,
+                              h->stream));
+  else  // increments -> cumulative Wiener path
+    HIP_OK(launch_from_planes_incr(h->key.precision, h->tw, h->d_stage, src[0], src[1], h->d_sel[what],
+                                   unit, C, h->G, h->d_pt_off, h->d_seg_np, h->d_seg_rec, h->d_seg_q,
+                                   h->d_tile_qoff, h->stream));
   HIP_OK(hipMemcpyAsync(out, h->d_stage, h->P * C * 8, hipMemcpyDeviceToHost, h->stream));
   HIP_OK(hipStreamSynchronize(h->stream));
   return DMT_OK;
@@ -901,20 +913,8 @@ dmt_status dmt_draw_proposal(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
   return DMT_OK;
 }
 
-dmt_status dmt_accept_reject(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, const double* E,
-                             int64_t mcmciter, uint32_t salt, uint8_t* acc_out) {
-  DMT_TRY(check_h(h));
-  Layout* L;
-  DMT_TRY(get_layout(h, layout, &L));
-  DMT_TRY(check_range(L, b0, b1));
-  if (L->hist_len > 0 && (mcmciter < 1 || mcmciter > L->hist_len))
-    return fail(DMT_ERR_INVALID, "mcmciter outside 1:ll_hist_len");
-  const double* dE = nullptr;
-  if (E) {
-    DMT_TRY(ensure_Z(h, std::max<int64_t>(b1 - b0, 1)));
-    HIP_OK(hipMemcpyAsync(h->d_Z, E, (b1 - b0) * 8, hipMemcpyHostToDevice, h->stream));
-    dE = h->d_Z;
-  }
+static AcceptArgs accept_args(dmt_ens* h, Layout* L, int64_t b0, int64_t b1, const double* dE,
+                              int64_t mcmciter, uint32_t salt, uint8_t* acc_dev) {
   AcceptArgs a{};
   a.b0 = b0;
   a.b1 = b1;
@@ -933,7 +933,91 @@ dmt_status dmt_accept_reject(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
   a.E = dE;
   a.seed = h->seed;
   a.salt = salt;
-  a.acc_out = acc_out ? L->d_acc : nullptr;
+  a.acc_out = acc_dev;
+  return a;
+}
+
+static dmt_status ensure_red_work(dmt_ens* h, int64_t n) {
+  const int64_t groups = std::max<int64_t>(1, (n + 1023) / 1024);
+  if (groups * 6 > h->red_work_n) {
+    if (h->d_red_work) { (void)hipFree(h->d_red_work); h->bytes -= h->red_work_n * 8; }
+    h->d_red_work = nullptr;
+    h->red_work_n = 0;
+    DMT_TRY(ens_alloc(h, &h->d_red_work, groups * 6));
+    h->red_work_n = groups * 6;
+  }
+  return DMT_OK;
+}
+
+// d_red (3 partials of this rank) -> host values, combined over ranks with RCCL
+static dmt_status finish_reduction(dmt_ens* h, double* v) {
+  if (h->comm && h->nranks > 1) {
+    if (!h->d_gather) DMT_TRY(ens_alloc(h, &h->d_gather, 3 * h->nranks));
+    if (ncclAllGather(h->d_red, h->d_gather, 3, ncclDouble, h->comm, h->stream) != ncclSuccess)
+      return fail(DMT_ERR_COMM, "ncclAllGather failed");
+    std::vector<double> all(3 * h->nranks);
+    HIP_OK(hipMemcpyAsync(all.data(), h->d_gather, 3 * h->nranks * 8, hipMemcpyDeviceToHost, h->stream));
+    HIP_OK(hipStreamSynchronize(h->stream));
+    // fixed rank-order adjacent-pair tree, ranks padded to a power of two
+    int n2 = 1;
+    while (n2 < h->nranks) n2 <<= 1;
+    for (int c = 0; c < 3; ++c) {
+      std::vector<double> lv(n2, 0.0);
+      for (int r = 0; r < h->nranks; ++r) lv[r] = all[3 * r + c];
+      for (int w = n2; w > 1; w >>= 1)
+        for (int j = 0; j < w / 2; ++j) lv[j] = lv[2 * j] + lv[2 * j + 1];
+      v[c] = lv[0] + 0.0;
+    }
+  } else {
+    HIP_OK(hipMemcpyAsync(h->h_red, h->d_red, 24, hipMemcpyDeviceToHost, h->stream));
+    HIP_OK(hipStreamSynchronize(h->stream));
+    v[0] = h->h_red[0];
+    v[1] = h->h_red[1];
+    v[2] = h->h_red[2];
+  }
+  return DMT_OK;
+}
+
+dmt_status dmt_mcmc_step(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int64_t mcmciter,
+                         uint32_t salt, double* ll, double* ll_prop, int64_t* n_acc) {
+  DMT_TRY(check_h(h));
+  Layout* L;
+  DMT_TRY(get_layout(h, layout, &L));
+  DMT_TRY(check_range(L, b0, b1));
+  DMT_TRY(law_ready(h, 0, L, b0, b1));
+  if (L->hist_len > 0 && (mcmciter < 1 || mcmciter > L->hist_len))
+    return fail(DMT_ERR_INVALID, "mcmciter outside 1:ll_hist_len");
+  DMT_TRY(run_block_kernel(h, L, MODE_PCN, DMT_K_DRAW, b0, b1, 0, 0, 1, 0, 1, nullptr, mcmciter,
+                           salt, L->d_llp, nullptr, false));
+  DMT_TRY(ensure_red_work(h, b1 - b0));
+  {
+    TimedScope ts(h, DMT_K_ACCEPT);
+    HIP_OK(launch_accept_reduce(accept_args(h, L, b0, b1, nullptr, mcmciter, salt, nullptr),
+                                h->d_red_work, h->d_red, h->stream));
+  }
+  double v[3];
+  DMT_TRY(finish_reduction(h, v));
+  if (ll) *ll = v[0];
+  if (ll_prop) *ll_prop = v[1];
+  if (n_acc) *n_acc = (int64_t)v[2];
+  return DMT_OK;
+}
+
+dmt_status dmt_accept_reject(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, const double* E,
+                             int64_t mcmciter, uint32_t salt, uint8_t* acc_out) {
+  DMT_TRY(check_h(h));
+  Layout* L;
+  DMT_TRY(get_layout(h, layout, &L));
+  DMT_TRY(check_range(L, b0, b1));
+  if (L->hist_len > 0 && (mcmciter < 1 || mcmciter > L->hist_len))
+    return fail(DMT_ERR_INVALID, "mcmciter outside 1:ll_hist_len");
+  const double* dE = nullptr;
+  if (E) {
+    DMT_TRY(ensure_Z(h, std::max<int64_t>(b1 - b0, 1)));
+    HIP_OK(hipMemcpyAsync(h->d_Z, E, (b1 - b0) * 8, hipMemcpyHostToDevice, h->stream));
+    dE = h->d_Z;
+  }
+  AcceptArgs a = accept_args(h, L, b0, b1, dE, mcmciter, salt, acc_out ? L->d_acc : nullptr);
   {
     TimedScope ts(h, DMT_K_ACCEPT);
     HIP_OK(launch_accept(a, h->stream));
@@ -1092,32 +1176,14 @@ dmt_status dmt_fetch_ll(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int6
     if (mcmciter > L->hist_len) return fail(DMT_ERR_INVALID, "mcmciter outside 1:ll_hist_len");
     acc = L->d_acch + (mcmciter - 1) * L->nblocks + b0;
   }
+  DMT_TRY(ensure_red_work(h, b1 - b0));
   {
     TimedScope ts(h, DMT_K_REDUCE);
-    HIP_OK(launch_block_sum(L->d_ll + b0, L->d_llp + b0, acc, b1 - b0, h->d_red, h->stream));
+    HIP_OK(launch_block_sum(L->d_ll + b0, L->d_llp + b0, acc, b1 - b0, h->d_red_work, h->d_red,
+                            h->stream));
   }
   double v[3];
-  if (h->comm && h->nranks > 1) {
-    if (!h->d_gather) DMT_TRY(ens_alloc(h, &h->d_gather, 3 * h->nranks));
-    if (ncclAllGather(h->d_red, h->d_gather, 3, ncclDouble, h->comm, h->stream) != ncclSuccess)
-      return fail(DMT_ERR_COMM, "ncclAllGather failed");
-    std::vector<double> all(3 * h->nranks);
-    HIP_OK(hipMemcpyAsync(all.data(), h->d_gather, 3 * h->nranks * 8, hipMemcpyDeviceToHost, h->stream));
-    HIP_OK(hipStreamSynchronize(h->stream));
-    // fixed rank-order adjacent-pair tree, ranks padded to a power of two
-    int n2 = 1;
-    while (n2 < h->nranks) n2 <<= 1;
-    for (int c = 0; c < 3; ++c) {
-      std::vector<double> lv(n2, 0.0);
-      for (int r = 0; r < h->nranks; ++r) lv[r] = all[3 * r + c];
-      for (int w = n2; w > 1; w >>= 1)
-        for (int j = 0; j < w / 2; ++j) lv[j] = lv[2 * j] + lv[2 * j + 1];
-      v[c] = lv[0] + 0.0;
-    }
-  } else {
-    HIP_OK(hipMemcpyAsync(v, h->d_red, 24, hipMemcpyDeviceToHost, h->stream));
-    HIP_OK(hipStreamSynchronize(h->stream));
-  }
+  DMT_TRY(finish_reduction(h, v));
   if (ll) *ll = v[0];
   if (ll_prop) *ll_prop = v[1];
   if (n_acc) *n_acc = (int64_t)v[2];

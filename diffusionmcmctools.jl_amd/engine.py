@@ -192,6 +192,13 @@ class Ensemble:
                C.byref(n))
         return a.value, b.value, n.value
 
+    def mcmc_step(self, layout, b0, b1, mcmciter, salt=0):
+        """draw_proposal (device RNG) + accept_reject + fetch_ll in one call."""
+        a, b, n = C.c_double(), C.c_double(), C.c_int64()
+        L.call("dmt_mcmc_step", self._h, layout, b0, b1, int(mcmciter), int(salt), C.byref(a),
+               C.byref(b), C.byref(n))
+        return a.value, b.value, n.value
+
     # ---------------------------------------------------------------- misc
     def sync(self):
         L.call("dmt_sync", self._h)

@@ -217,6 +217,16 @@ dmt_status dmt_set_block_state(dmt_ens* h, int32_t layout, int32_t what, int64_t
 dmt_status dmt_fetch_ll(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
                         int64_t mcmciter, double* ll, double* ll_prop, int64_t* n_acc);
 
+/* One MCMC path-imputation iteration over blocks [b0, b1), device RNG: exactly
+ *   dmt_draw_proposal(Z = NULL, iter = mcmciter) ; dmt_accept_reject(E = NULL, mcmciter) ;
+ *   dmt_fetch_ll(mcmciter)
+ * (draw_proposal_path!(be); accept_reject_proposal_path!(be, i); fetch_ll(be), fetch_ll°(be)
+ * and the accepted count — src/block_ensemble.jl:50,63-67,140,152) issued as one call with
+ * the decision and the first reduction level fused in one kernel.  Results are identical to
+ * the three separate calls. */
+dmt_status dmt_mcmc_step(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int64_t mcmciter,
+                         uint32_t salt, double* ll, double* ll_prop, int64_t* n_acc);
+
 /* ---------------- guiding term (host set-up, GP.build_guid_prop) ---------------- */
 
 /* Exact discrete backward filter for a linear auxiliary law dX = (B̃X + β̃)dt + σ̃dW on

@@ -28,19 +28,29 @@
  * kernels follow it operation for operation, so that paths and log-weights
  * agree bit for bit under -ffp-contract=off with explicit fma):
  *
+ *   Wiener paths are held as INCREMENTS: row 0 of a segment's W holds W(t_0), row i+1
+ *   holds dW_i = W(t_{i+1}) - W(t_i).  Cumulative paths are converted at the boundary
+ *   (dW_i = W[i+1] - W[i] on upload, W[i+1] = W[i] + dW_i on download).
+ *
  *   dt      = t[i+1] - t[i]
- *   dW_k    = W[i+1][k] - W[i][k]
  *   r_a     = F_a ; r_a = fma(-H_ab, x_b, r_a)        for b = 0..d-1
  *   b       = model drift (see orc_drift)
- *   ar_a    = a_a0*r_0 ; ar_a = fma(a_ab, r_b, ar_a) for b = 1..d-1
- *   bg_a    = b_a + ar_a
+ *   guiding coefficients of the step (no dependence on x):
+ *     aH_ab = a_a0*H_0b ; aH_ab = fma(a_ac, H_cb, aH_ab)  for c = 1..d-1
+ *     aF_a  = a_a0*F_0  ; aF_a  = fma(a_ac, F_c, aF_a)
+ *     linear drift (OU, b = -Theta(x - mu)):  M_ab = Theta_ab + aH_ab ; c_a = (Theta mu)_a + aF_a
+ *       with (Theta mu)_a = Theta_a0*mu_0 ; fma(Theta_ac, mu_c, .)
+ *     otherwise:                              M_ab = aH_ab ; c_a = aF_a
+ *   u_a     = c_a ; u_a = fma(-M_ab, x_b, u_a)       for b = 0..d-1
+ *   bg_a    = u_a (linear drift)  or  b_a + u_a      (= b + a(F - Hx) in exact arithmetic)
  *   bt_a    = Bt_a-row · x + beta_a  (bt_a = beta_a ; fma(Bt_ab, x_b, bt_a))
  *   db_a    = b_a - bt_a
  *   G       = db_0*r_0 ; G = fma(db_a, r_a, G)
  *   [trace] tr = Σ_a Σ_b da_ab*(H_ab - r_a r_b)  (tmp = fma(-r_a, r_b, H_ab);
  *            first term tr = da_00*tmp, then tr = fma(da_ab, tmp, tr)); G = fma(-0.5, tr, G)
  *   g       = G*dt           -> fed to the chunked pairwise sum
- *   x'_a    = fma(bg_a, dt, x_a) ; x'_a = fma(sigma_ak, dW_k, x'_a)  for k = 0..m-1
+ *   sdW_a   = sigma_a0*dW_0 ; sdW_a = fma(sigma_ak, dW_k, sdW_a)  for k = 1..m-1
+ *   x'_a    = fma(bg_a, dt, x_a + sdW_a)
  *
  *   Log-weight summation: within a segment the g's are summed in chunks of 64
  *   consecutive steps by the adjacent-pair binary tree ((g0+g1)+(g2+g3))+…
@@ -48,9 +58,10 @@
  *   canonicalised with "+ 0.0" and chunk sums are added left to right
  *   starting from 0.  Block ll = obs term, then += each segment's sum.
  *
- *   pCN (cumulative form, A.4 of SURVEY.md):  wf_0 = 0;
- *   wf_{q+1} = fma(sqrt(t[q+1]-t[q]), Z_q, wf_q);  W°_q = fma(rho, W_q, srho*wf_q)
- *   with srho = sqrt(1 - rho*rho) computed in double by the host.
+ *   pCN (increment form, A.4 of SURVEY.md):  W°(t_0) = rho*W(t_0);
+ *   dW°_i = fma(rho, dW_i, srho*(sqrt(t[i+1]-t[i])*Z_i))
+ *   with srho = sqrt(1 - rho*rho) computed in double by the host (rho = 0, srho = 1 is a
+ *   fresh draw; rho = 1, srho = 0 reproduces dW exactly).
  *
  * Compiled twice: REAL=double (suffix _f64) and REAL=float (suffix _f32).
  */
@@ -174,6 +185,29 @@ static inline REAL g_at(int model, int d, const REAL* th, const REAL* a, const R
     return G;
 }
 
+/* Per-step guiding coefficients M (d×d row-major) and c (d) of the Euler update. */
+static inline void guide_coeffs(int model, int d, const REAL* th, const REAL* a, const REAL* H,
+                                const REAL* F, REAL* Mg, REAL* cg) {
+    for (int p = 0; p < d; ++p) {
+        for (int q = 0; q < d; ++q) {
+            REAL v = a[pidx(d, p, 0)] * H[pidx(d, 0, q)];
+            for (int c = 1; c < d; ++c) v = FMA(a[pidx(d, p, c)], H[pidx(d, c, q)], v);
+            Mg[p * d + q] = v;
+        }
+        REAL f = a[pidx(d, p, 0)] * F[0];
+        for (int c = 1; c < d; ++c) f = FMA(a[pidx(d, p, c)], F[c], f);
+        cg[p] = f;
+    }
+    if (model == ORC_OU) { /* linear drift b = -Theta(x - mu) folded in */
+        for (int p = 0; p < d; ++p) {
+            REAL tm = th[p * d + 0] * th[9 + 0];
+            for (int c = 1; c < d; ++c) tm = FMA(th[p * d + c], th[9 + c], tm);
+            for (int q = 0; q < d; ++q) Mg[p * d + q] = th[p * d + q] + Mg[p * d + q];
+            cg[p] = tm + cg[p];
+        }
+    }
+}
+
 /* GP.solve_and_ll!(X, W, P, y1): Euler–Maruyama guided solve with given W and
  * the Girsanov sum.  Returns 1 on success (finite end point and ll). */
 int SFX(orc_solve_segment)(int model, int d, int m, const double* law, int npts,
@@ -187,25 +221,22 @@ int SFX(orc_solve_segment)(int model, int d, int m, const double* law, int npts,
     psum_t ps; ps_init(&ps);
     for (int i = 0; i < npts - 1; ++i) {
         REAL dt = t[i + 1] - t[i];
-        REAL dW[3];
-        for (int k = 0; k < m; ++k) dW[k] = W[(i + 1) * m + k] - W[i * m + k];
+        const REAL* dW = W + (size_t)(i + 1) * m;  /* increments */
         const REAL* Hi = H + (size_t)i * h;
         const REAL* Fi = F + (size_t)i * d;
         REAL r[3], b[3];
         REAL G = g_at(model, d, th, a, Bt, beta, da, trace, Hi, Fi, x, r, b);
         ps_add(&ps, G * dt);
-        REAL ar[3];
-        for (int p = 0; p < d; ++p) {
-            REAL acc = a[pidx(d, p, 0)] * r[0];
-            for (int q = 1; q < d; ++q) acc = FMA(a[pidx(d, p, q)], r[q], acc);
-            ar[p] = acc;
-        }
+        REAL Mg[9], cg[3];
+        guide_coeffs(model, d, th, a, Hi, Fi, Mg, cg);
         REAL xn[3];
         for (int p = 0; p < d; ++p) {
-            REAL bg = b[p] + ar[p];
-            REAL v = FMA(bg, dt, x[p]);
-            for (int k = 0; k < m; ++k) v = FMA(sg[p * m + k], dW[k], v);
-            xn[p] = v;
+            REAL u = cg[p];
+            for (int q = 0; q < d; ++q) u = FMA(-Mg[p * d + q], x[q], u);
+            REAL bg = (model == ORC_OU) ? u : (b[p] + u);
+            REAL sdw = sg[p * m + 0] * dW[0];
+            for (int k = 1; k < m; ++k) sdw = FMA(sg[p * m + k], dW[k], sdw);
+            xn[p] = FMA(bg, dt, x[p] + sdw);
         }
         for (int p = 0; p < d; ++p) { x[p] = xn[p]; X[(size_t)(i + 1) * d + p] = xn[p]; }
     }
@@ -249,18 +280,31 @@ REAL SFX(orc_obs_term)(int d, const double* law, const REAL* H0, const REAL* F0,
     return tmp - (REAL)law[L_C0];
 }
 
-/* pCN mix of one segment (cumulative form). */
+/* pCN mix of one segment (increment form). */
 void SFX(orc_pcn_segment)(int m, int npts, const REAL* t, const REAL* W, const REAL* Z,
                           REAL rho, REAL srho, REAL* Wo) {
-    REAL wf[3] = {0, 0, 0};
-    for (int k = 0; k < m; ++k) Wo[k] = FMA(rho, W[k], srho * wf[k]);
+    for (int k = 0; k < m; ++k) Wo[k] = rho * W[k];
     for (int q = 0; q < npts - 1; ++q) {
         REAL sdt = SQRT(t[q + 1] - t[q]);
         for (int k = 0; k < m; ++k) {
-            wf[k] = FMA(sdt, Z[(size_t)q * m + k], wf[k]);
-            Wo[(size_t)(q + 1) * m + k] = FMA(rho, W[(size_t)(q + 1) * m + k], srho * wf[k]);
+            REAL zi = sdt * Z[(size_t)q * m + k];
+            Wo[(size_t)(q + 1) * m + k] = FMA(rho, W[(size_t)(q + 1) * m + k], srho * zi);
         }
     }
+}
+
+/* cumulative <-> increment conversion of one segment's Wiener path (m components) */
+void SFX(orc_w_to_increments)(int m, int npts, const REAL* W, REAL* dW) {
+    for (int k = 0; k < m; ++k) dW[k] = W[k];
+    for (int q = 0; q < npts - 1; ++q)
+        for (int k = 0; k < m; ++k)
+            dW[(size_t)(q + 1) * m + k] = W[(size_t)(q + 1) * m + k] - W[(size_t)q * m + k];
+}
+void SFX(orc_w_from_increments)(int m, int npts, const REAL* dW, REAL* W) {
+    for (int k = 0; k < m; ++k) W[k] = dW[k];
+    for (int q = 0; q < npts - 1; ++q)
+        for (int k = 0; k < m; ++k)
+            W[(size_t)(q + 1) * m + k] = W[(size_t)q * m + k] + dW[(size_t)(q + 1) * m + k];
 }
 
 /*
@@ -296,9 +340,8 @@ int SFX(orc_draw_terminal_blocks)(int model, int d, int m, int64_t B, int npts,
         REAL* Wp = Wo + (size_t)blk * npts * m;
         double r = rho[blk];
         REAL rr = (REAL)r, sr = (REAL)sqrt(1.0 - r * r);
-        /* pCN */
-        REAL wf[3] = {0, 0, 0};
-        for (int k = 0; k < m; ++k) Wp[k] = FMA(rr, Wa[k], sr * wf[k]);
+        /* pCN (increment form; W arrays hold increments) */
+        for (int k = 0; k < m; ++k) Wp[k] = rr * Wa[k];
         REAL zc = 0; int have = 0;
         for (int q = 0; q < npts - 1; ++q) {
             REAL sdt = SQRT(tb[q + 1] - tb[q]);
@@ -315,8 +358,8 @@ int SFX(orc_draw_terminal_blocks)(int model, int d, int m, int64_t B, int npts,
                         z = z0; zc = z1; have = 1;
                     }
                 }
-                wf[k] = FMA(sdt, z, wf[k]);
-                Wp[(size_t)(q + 1) * m + k] = FMA(rr, Wa[(size_t)(q + 1) * m + k], sr * wf[k]);
+                REAL zi = sdt * z;
+                Wp[(size_t)(q + 1) * m + k] = FMA(rr, Wa[(size_t)(q + 1) * m + k], sr * zi);
             }
         }
         (void)have;

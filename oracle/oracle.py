@@ -59,6 +59,10 @@ def _load():
         f = getattr(lib, f"orc_pcn_segment_{sfx}")
         f.argtypes = [i_, i_, P, P, P, R, R, P]
         f.restype = None
+        for nm in ("orc_w_to_increments", "orc_w_from_increments"):
+            f = getattr(lib, f"{nm}_{sfx}")
+            f.argtypes = [i_, i_, P, P]
+            f.restype = None
         f = getattr(lib, f"orc_normals_segment_{sfx}")
         f.argtypes = [u64, u32, u32, u32, i_, i_, P]
         f.restype = None
@@ -126,6 +130,23 @@ def pcn_segment(m, t, W, Z, rho, srho, prec=0):
     getattr(lib, f"orc_pcn_segment_{_sfx(prec)}")(m, t.size, _p(t), _p(W), _p(Z), rho, srho,
                                                   _p(Wo))
     return Wo
+
+
+def w_to_increments(W, prec=0):
+    """Cumulative Wiener path (npts × m) -> row 0 = W(t0), row i+1 = increment i."""
+    dt = _dt(prec)
+    W = np.ascontiguousarray(W, dtype=dt)
+    out = np.empty_like(W)
+    getattr(lib, f"orc_w_to_increments_{_sfx(prec)}")(W.shape[1], W.shape[0], _p(W), _p(out))
+    return out
+
+
+def w_from_increments(dW, prec=0):
+    dt = _dt(prec)
+    dW = np.ascontiguousarray(dW, dtype=dt)
+    out = np.empty_like(dW)
+    getattr(lib, f"orc_w_from_increments_{_sfx(prec)}")(dW.shape[1], dW.shape[0], _p(dW), _p(out))
+    return out
 
 
 def normals_segment(seed, g, it, salt, nsteps, m, prec=0):
@@ -296,17 +317,19 @@ class OracleEnsemble:
                 otab[g] = copy.deepcopy(tab[g])
 
     def set_paths(self, unit, X=None, W=None):
+        """Host W is cumulative (the reference's Wiener trajectories); held as increments."""
         me = self._unit(unit)
         for g in range(self.G):
             if X is not None:
                 me.XX[g][...] = self._seg_rows(X, g, self.d)
             if W is not None:
-                me.WW[g][...] = self._seg_rows(W, g, self.m)
+                me.WW[g][...] = w_to_increments(self._seg_rows(W, g, self.m), self.prec)
 
     def download_paths(self, unit, what):
         me = self._unit(unit)
-        src = me.XX if what == 0 else me.WW
-        return np.concatenate(src).astype(np.float64)
+        if what == 0:
+            return np.concatenate(me.XX).astype(np.float64)
+        return np.concatenate([w_from_increments(w, self.prec) for w in me.WW]).astype(np.float64)
 
     # ---- layouts (BlockEnsemble ranges)
     def create_layout(self, n_blocks, seg_first, seg_last, last, rho, hist_len=0):

@@ -250,3 +250,26 @@ def test_full_size_properties(cfg, mapping):
     assert np.array_equal(dev.download_paths(L.UPROP, 0), dev.download_paths(L.U, 0))
     assert np.array_equal(dev.get_block_state(lay1, L.BLK_LLPROP, 0, nb),
                           dev.get_block_state(lay1, L.BLK_LL, 0, nb))
+
+
+@pytest.mark.parametrize("mapping", MAPPINGS)
+@pytest.mark.parametrize("B", [100, 2500])
+def test_mcmc_step_equals_separate_calls(mapping, B):
+    """dmt_mcmc_step == draw_proposal + accept_reject + fetch_ll, bit for bit."""
+    import diffusionmcmctools_amd as d
+    w = W.c2_ou2d(B=B, N=60)
+    w.meta["hist_len"] = 4
+    ens = []
+    for _ in range(2):
+        e = d.Ensemble(w.model.kind, w.d, w.m, w.n_points, precision=w.precision, seed=21,
+                       grid_shared=w.grid_shared, mapping=mapping)
+        lay = W.fill(e, w)
+        e.loglikhd(lay, L.U, 0, B)
+        ens.append(e)
+    for i in (1, 2, 3, 4):
+        ens[0].draw_proposal(lay, 0, B, iter=i, salt=3)
+        ens[0].accept_reject(lay, 0, B, i, salt=3)
+        r0 = ens[0].fetch_ll(lay, 0, B, i)
+        r1 = ens[1].mcmc_step(lay, 0, B, i, salt=3)
+        assert r0 == r1
+    cs.assert_paths_equal(ens[0], ens[1])

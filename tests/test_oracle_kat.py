@@ -143,7 +143,7 @@ def test_c_oracle_matches_naive_numpy(dmt, model):
     W = np.vstack([np.zeros(m), np.cumsum(rng.standard_normal((n - 1, m)) * np.sqrt(np.diff(t))[:, None], 0)])
     law = M.law_record(aux)
     y1 = rng.standard_normal(d) * 0.3
-    X, ll, ok = orc.solve_segment(kind, d, m, law, t, H, F, W, y1)
+    X, ll, ok = orc.solve_segment(kind, d, m, law, t, H, F, orc.w_to_increments(W), y1)
     Xn, lln = npo.solve_segment_naive(kind, d, m, law, t, H, F, W, y1)
     assert ok
     np.testing.assert_allclose(X, Xn, rtol=1e-11, atol=1e-12)
@@ -162,22 +162,25 @@ def test_weight_vanishes_when_target_is_aux():
     n = 501; t = np.linspace(0, 1, n)
     H = np.tile([4.0, 0.5, 3.0], (n, 1)); F = rng.standard_normal((n, 2))
     W = np.vstack([np.zeros(2), np.cumsum(rng.standard_normal((n - 1, 2)) * 0.0447, 0)])
-    _, ll, ok = orc.solve_segment(0, d, m, law, t, H, F, W, np.zeros(2))
+    _, ll, ok = orc.solve_segment(0, d, m, law, t, H, F, orc.w_to_increments(W), np.zeros(2))
     assert ok and abs(ll) < 1e-13
 
 
 def test_pcn_limits():
+    """Increment-form pCN: rho = 1 reuses dW exactly, rho = 0 is a fresh draw sqrt(dt) Z,
+    and the cumulative path is rho W + sqrt(1-rho^2) W_fresh up to rounding."""
     rng = np.random.default_rng(2)
     n, m = 101, 2
     t = np.linspace(0, 1, n) ** 1.5
     W = np.vstack([np.zeros(m), np.cumsum(rng.standard_normal((n - 1, m)), 0)])
+    dW = orc.w_to_increments(W)
     Z = rng.standard_normal((n - 1, m))
-    assert np.array_equal(orc.pcn_segment(m, t, W, Z, 1.0, 0.0), W)          # ρ = 1 reuses W
-    fresh = np.vstack([np.zeros(m), np.cumsum(Z * np.sqrt(np.diff(t))[:, None], 0)])
-    np.testing.assert_allclose(orc.pcn_segment(m, t, W, Z, 0.0, 1.0), fresh, rtol=0, atol=1e-13)
+    assert np.array_equal(orc.pcn_segment(m, t, dW, Z, 1.0, 0.0), dW)
+    fresh = np.vstack([np.zeros(m), Z * np.sqrt(np.diff(t))[:, None]])
+    assert np.array_equal(orc.pcn_segment(m, t, dW, Z, 0.0, 1.0), fresh)
     rho = 0.8
-    Wo = orc.pcn_segment(m, t, W, Z, rho, math.sqrt(1 - rho ** 2))
-    np.testing.assert_allclose(Wo, rho * W + math.sqrt(1 - rho ** 2) * fresh, atol=1e-13)
+    Wo = orc.w_from_increments(orc.pcn_segment(m, t, dW, Z, rho, math.sqrt(1 - rho ** 2)))
+    np.testing.assert_allclose(Wo, rho * W + math.sqrt(1 - rho ** 2) * np.cumsum(fresh, 0), atol=1e-12)
 
 
 def test_bridge_hits_endpoint_small_noise(dmt):
@@ -190,7 +193,7 @@ def test_bridge_hits_endpoint_small_noise(dmt):
     H, F, c = dmt.guiding_linear([[0.0]], [0.0], [1.0], t, [1 / Sig], [v / Sig], 0.0)
     rng = np.random.default_rng(4)
     W = np.concatenate([[0], np.cumsum(rng.standard_normal(n - 1) * math.sqrt(1 / (n - 1)))])[:, None]
-    X, ll, ok = orc.solve_segment(0, 1, 1, law, t, H, F, W, np.zeros(1))
+    X, ll, ok = orc.solve_segment(0, 1, 1, law, t, H, F, orc.w_to_increments(W), np.zeros(1))
     assert ok and abs(X[-1, 0] - v) < 0.05
 
 
