@@ -10,8 +10,10 @@ BlockEnsemble level (src/block_ensemble.jl:50,63-67,140).  Throughput unit: brid
 Euler steps (one grid increment of one segment) per second, whole job.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c5]
-Multi-GPU: launched by torch.distributed.run, one rank per GPU, weak scaling (each rank owns
-a full per-GPU ensemble, blocks keyed by global id; no data-path collective besides fetch_ll).
+Multi-GPU: launched by torch.distributed.run, one rank per GPU, weak scaling: rank r owns
+recording shard r of a global ensemble of N x B blocks (RNG keyed by global segment ids,
+diffusionmcmctools.jl_amd/shard.py); the only collective is fetch_ll's RCCL all-gather of
+3 doubles per iteration.
 """
 from __future__ import annotations
 
@@ -134,8 +136,11 @@ def main():
     w.meta["hist_len"] = args.warmup + args.steps
     mapping = {"auto": L.MAP_AUTO, "lane": L.MAP_LANE, "wave": L.MAP_WAVE}[args.mapping]
     ens = dmt.Ensemble(w.model.kind, w.d, w.m, w.n_points, precision=w.precision,
-                       seed=0xD1FF + 7919 * rank, device=local_rank, grid_shared=w.grid_shared,
+                       seed=0xD1FF, device=local_rank, grid_shared=w.grid_shared,
                        mapping=mapping)
+    # rank r holds recording shard r of the global ensemble: RNG streams keyed by global
+    # segment ids (shard.py), so the N-GPU job equals one ensemble of N x B blocks
+    ens.set_shard(rank * ens.G)
     lay = W.fill(ens, w, init_Z=False)
     B = w.nblocks
     if world > 1:

@@ -1,0 +1,343 @@
+"""Host-side mirror of the reference's composite-unit interface, backed by libdmt.
+
+Same objects and method names as DiffusionMCMCTools.jl (``!`` dropped, ``°`` spelled
+``_prop``), same argument meaning (``mcmciter`` is the 1-based MCMC iteration), same
+results: every method is one C-ABI call over the block range the object covers.
+
+  reference (src/…)                              here
+  SamplingUnit            sampling_unit.jl:48     SamplingUnit     (u or u° of one recording)
+  SamplingPair            sampling_pair.jl:33     SamplingPair     (u, u° of one recording)
+  SamplingEnsemble        sampling_ensemble.jl:13 SamplingEnsemble (owns the device handle)
+  BiBlock{L}              biblock.jl:42           BiBlock          (one block, L = is_last)
+  BlockCollection         block_collection.jl:19  BlockCollection  (the blocks of a recording)
+  BlockEnsemble           block_ensemble.jl:17    BlockEnsemble    (all recordings' blocks)
+
+Ranges are 0-based half-open Python ``range``s over a recording's inter-observation segments
+(the reference's ``ranges[i]`` are 1-based ``UnitRange``s of the same segments).  Path
+containers live on the GPU; ``XX``/``WW`` download them in the reference layout.
+Draws: by default the device Philox stream (keyed by ``mcmciter`` / an explicit ``iter``);
+pass ``Z``/``E`` to supply the normals / Exp(1) variables yourself (parity mode).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _lib as L
+from .engine import Ensemble
+
+__all__ = ["SamplingEnsemble", "SamplingPair", "SamplingUnit", "BlockEnsemble",
+           "BlockCollection", "BiBlock"]
+
+
+# ============================================================================ sampling units
+class SamplingEnsemble:
+    """``SamplingEnsemble(aux_laws, recordings, tts, …)`` (src/sampling_ensemble.jl:13-41):
+    the u/u° containers of every recording, resident on one GPU.
+
+    ``model`` is a :class:`diffusionmcmctools_amd.models.Model`; ``n_points[r][k]`` the grid
+    size of segment k of recording r.  Guiding terms, laws and the grid are uploaded with
+    :meth:`set_guiding` / :meth:`upload_grid` (host filter: ``models.guiding_chain``)."""
+
+    def __init__(self, model, n_points, precision=L.F64, seed=0, device=0, grid_shared=False,
+                 mapping=L.MAP_AUTO, _engine=None):
+        self.model = model
+        self.n_points = [list(r) for r in n_points]
+        # _engine: test seam for driving the host logic on another backend; the product
+        # path is always the HIP library (no CPU fallback).
+        self.ens = _engine if _engine is not None else Ensemble(
+            model.kind, model.d, model.m, n_points, precision=precision, seed=seed,
+            device=device, grid_shared=grid_shared, mapping=mapping)
+        self.recordings = [SamplingPair(self, r) for r in range(len(self.n_points))]
+
+    def num_recordings(self):
+        return len(self.recordings)
+
+    def upload_grid(self, t):
+        self.ens.upload_grid(t)
+
+    def set_guiding(self, H, F, laws, Hb=None, Fb=None, lawsb=None, H_shared=False,
+                    unit=L.U):
+        """Upload the guiding terms of ``PP`` (and ``PPb``, the blocking laws with an
+        artificial end observation, src/sampling_unit.jl:61-66) of ``unit``; the first
+        upload also seeds the other unit (u° = deepcopy(u), src/sampling_pair.jl:51)."""
+        self.ens.upload_law(unit, L.LAW_PP, H=H, F=F, laws=laws, H_shared=H_shared)
+        if Hb is not None or Fb is not None or lawsb is not None:
+            self.ens.upload_law(unit, L.LAW_PPB, H=Hb, F=Fb, laws=lawsb, H_shared=H_shared)
+
+    def init_paths(self, x0, Z=None, iter=0, salt=0xFFFF):
+        """``init_paths!`` (src/sampling_unit.jl:83-87) for every recording, then
+        u° ← u (src/sampling_pair.jl:51).  ``x0``: per-recording start points (R × d)."""
+        x0 = np.asarray(x0, dtype=np.float64).reshape(-1, self.model.d)
+        X = np.zeros((self.ens.P, self.model.d))
+        X[self.ens.pt_off[self.ens.rec_seg0[:-1]]] = x0
+        self.ens.set_paths(L.U, X=X)
+        ll, ok = self.ens.draw_unit(L.U, Z=Z, iter=iter, salt=salt)
+        self.ens.set_paths(L.UPROP, X=self.ens.download_paths(L.U, 0),
+                           W=self.ens.download_paths(L.U, 1))
+        return ll, ok
+
+    def close(self):
+        self.ens.close()
+
+
+class SamplingPair:
+    """``SamplingPair`` (src/sampling_pair.jl:33-57): ``u`` (accepted) and ``u°`` of one
+    recording."""
+
+    def __init__(self, se: SamplingEnsemble, r: int):
+        self.se, self.r = se, r
+        self.u = SamplingUnit(se, r, L.U)
+        self.u_prop = SamplingUnit(se, r, L.UPROP)
+
+
+class SamplingUnit:
+    """``SamplingUnit`` (src/sampling_unit.jl:48-81) view: PP, PPb, WW, XX of one recording."""
+
+    def __init__(self, se: SamplingEnsemble, r: int, unit: int):
+        self.se, self.r, self.unit = se, r, unit
+
+    def _rows(self):
+        e = self.se.ens
+        g0, g1 = e.rec_seg0[self.r], e.rec_seg0[self.r + 1]
+        p0 = e.pt_off[g0]
+        p1 = e.pt_off[g1 - 1] + e.npts[g1 - 1]
+        return p0, p1, g0, g1
+
+    def _split(self, A):
+        p0, _, g0, g1 = self._rows()
+        e = self.se.ens
+        return [A[e.pt_off[g]:e.pt_off[g] + e.npts[g]] for g in range(g0, g1)]
+
+    @property
+    def XX(self):
+        """Sampled trajectories, one (npts × d) array per segment."""
+        return self._split(self.se.ens.download_paths(self.unit, 0))
+
+    @property
+    def WW(self):
+        """Wiener trajectories (cumulative, as the reference holds them), per segment."""
+        return self._split(self.se.ens.download_paths(self.unit, 1))
+
+    def draw_proposal_path(self, Z=None, iter=0, salt=0):
+        """``draw_proposal_path!(u::SamplingUnit)`` (src/sampling_unit.jl:118-120): fresh
+        Wiener draw and guided solve of the whole recording.  Returns (success, ll)."""
+        ll, ok = self.se.ens.draw_unit(self.unit, self.r, self.r + 1, Z=Z, iter=iter, salt=salt)
+        return bool(ok[0]), float(ll[0])
+
+
+# ============================================================================ blocks
+class _BlockRange:
+    """Shared implementation: blocks [b0, b1) of a layout (a BlockEnsemble, one of its
+    BlockCollections, or one BiBlock)."""
+
+    def __init__(self, ens, layout, b0, b1, hist_len):
+        self._ens, self._layout, self._b0, self._b1 = ens, layout, b0, b1
+        self.ll_hist_len = hist_len
+
+    @property
+    def num_blocks(self):
+        return self._b1 - self._b0
+
+    def _call(self, name, *a, **k):
+        return getattr(self._ens, name)(self._layout, self._b0, self._b1, *a, **k)
+
+    def _call_what(self, name, what, **k):
+        # engine methods whose selector precedes the block range: (layout, what, b0, b1)
+        return getattr(self._ens, name)(self._layout, what, self._b0, self._b1, **k)
+
+    # ---- imputation (biblock.jl:78-106, block_collection.jl:46, block_ensemble.jl:50)
+    def draw_proposal_path(self, Z=None, iter=None, salt=0):
+        """pCN proposal under the accepted law into u°, ll° along the way.  Returns the
+        per-block success flags.  ``iter`` keys the device normals (default 0); ``Z`` (steps
+        × m, whole ensemble) supplies them."""
+        return self._call("draw_proposal", Z=Z, iter=0 if iter is None else iter, salt=salt,
+                          want_success=True)
+
+    # ---- accept / reject (biblock.jl:121-127)
+    def accept_reject_proposal_path(self, mcmciter, E=None, salt=0):
+        """MH decision per block: E > −(ll° − ll), E ~ Exp(1) (device stream keyed by
+        ``mcmciter`` unless ``E`` is given); swap_paths!, set_accepted!, save_ll!, swap_ll!
+        in the reference order.  Returns the per-block decisions."""
+        return self._call("accept_reject", mcmciter, E=E, salt=salt, want_acc=True)
+
+    def set_accepted(self, i, v):
+        self._call("set_accepted", i, v)
+
+    # ---- swaps (biblock.jl:148-208)
+    def swap_paths(self):
+        self._call_what("swap", L.SWAP_XX | L.SWAP_WW)
+
+    def swap_XX(self):
+        self._call_what("swap", L.SWAP_XX)
+
+    def swap_WW(self):
+        self._call_what("swap", L.SWAP_WW)
+
+    def swap_PP(self):
+        """PP (and, for non-terminal blocks, the P_last law) of the block's segments."""
+        self._call_what("swap", L.SWAP_PP)
+
+    def swap_ll(self):
+        self._call_what("swap", L.SWAP_LL)
+
+    # ---- log-likelihoods (block.jl:138-152, biblock.jl:233-249, block_collection.jl:166-197)
+    def loglikhd(self):
+        self._call_what("loglikhd", L.U)
+
+    def loglikhd_prop(self):
+        self._call_what("loglikhd", L.UPROP)
+
+    def recompute_path(self, skip=0):
+        """``recompute_path!(bb.b°, bb.b.WW; skip)`` (src/block.jl:155-187): u° re-solved
+        under u°'s laws with u's Wiener path; ll° stored.  Returns per-block success."""
+        return self._call("recompute_path", skip=skip, want_success=True)
+
+    def save_ll(self, i):
+        self._call("save_ll", i)
+
+    def fetch_ll(self):
+        """Σ ll over the blocks (deterministic pairwise tree)."""
+        return self._call("fetch_ll")[0]
+
+    def fetch_ll_prop(self):
+        return self._call("fetch_ll")[1]
+
+    # ---- state
+    @property
+    def ll(self):
+        return self._call_what("get_block_state", L.BLK_LL)
+
+    @property
+    def ll_prop(self):
+        return self._call_what("get_block_state", L.BLK_LLPROP)
+
+    def _hist(self, what):
+        return self._call_what("get_block_state", what, hist_len=self.ll_hist_len)
+
+    @property
+    def ll_history(self):
+        return self._hist(L.BLK_LL_HIST)
+
+    @property
+    def ll_prop_history(self):
+        return self._hist(L.BLK_LLPROP_HIST)
+
+    @property
+    def accpt_history(self):
+        return self._hist(L.BLK_ACC_HIST).astype(bool)
+
+    def ll_of_accepted(self, i):
+        """Per block: ll° history if iteration i was accepted, else ll history
+        (src/biblock.jl:221-223)."""
+        acc = self.accpt_history[i - 1]
+        return np.where(acc, self.ll_prop_history[i - 1], self.ll_history[i - 1])
+
+    def accpt_rate(self, rng):
+        """Per block: mean of accpt_history over the 1-based iterations in ``rng``
+        (src/biblock.jl:230)."""
+        idx = np.asarray(list(rng), dtype=np.int64) - 1
+        return self.accpt_history[idx].sum(axis=0) / len(idx)
+
+    # ---- parameter updates (block_collection.jl:306-334): law upload + re-solve
+    def set_proposal_law(self, H=None, F=None, laws=None, Hb=None, Fb=None, lawsb=None,
+                         H_shared=False, skip=0):
+        """Install the proposal law's guiding terms in u° (ensemble-wide tables, as the host
+        filter produces them) and ``recompute_path!`` the blocks under it."""
+        if H is not None or F is not None or laws is not None:
+            self._ens.upload_law(L.UPROP, L.LAW_PP, H=H, F=F, laws=laws, H_shared=H_shared)
+        if Hb is not None or Fb is not None or lawsb is not None:
+            self._ens.upload_law(L.UPROP, L.LAW_PPB, H=Hb, F=Fb, laws=lawsb, H_shared=H_shared)
+        return self.recompute_path(skip=skip)
+
+    def mcmc_step(self, mcmciter, salt=0):
+        """``draw_proposal_path!`` + ``accept_reject_proposal_path!(·, mcmciter)`` +
+        ``fetch_ll`` fused into one call (device RNG).  Returns (ll, ll°, n_accepted)."""
+        return self._call("mcmc_step", mcmciter, salt=salt)
+
+
+class BiBlock(_BlockRange):
+    """``BiBlock{L}`` (src/biblock.jl:42-63): one block b / b° with pCN memory ρ."""
+
+    def __init__(self, ens, layout, b, hist_len, is_last, rho, segments):
+        super().__init__(ens, layout, b, b + 1, hist_len)
+        self.is_last, self.rho, self.segments = bool(is_last), float(rho), segments
+
+    def fetch_ll(self):
+        return float(self.ll[0])
+
+    def fetch_ll_prop(self):
+        return float(self.ll_prop[0])
+
+    def ll_of_accepted(self, i):
+        return float(super().ll_of_accepted(i)[0])
+
+    def accpt_rate(self, rng):
+        return float(super().accpt_rate(rng)[0])
+
+
+class BlockCollection(_BlockRange):
+    """``BlockCollection`` (src/block_collection.jl:19-38): the blocks of one recording; the
+    last one is terminal (``BiBlock{true}``)."""
+
+    def __init__(self, ens, layout, b0, blocks, hist_len):
+        super().__init__(ens, layout, b0, b0 + len(blocks), hist_len)
+        self.blocks = blocks
+
+
+class BlockEnsemble(_BlockRange):
+    """``BlockEnsemble(se, ranges, ρρ=0.0, ll_hist_len=0)`` (src/block_ensemble.jl:17-38).
+
+    ``ranges[r]`` lists recording r's blocks as contiguous ranges of its segments covering
+    it in order; ``rho`` a scalar, or per recording (scalar or per block)."""
+
+    def __init__(self, se: SamplingEnsemble, ranges, rho=0.0, ll_hist_len=0):
+        R = se.num_recordings()
+        if len(ranges) != R:
+            raise ValueError(f"ranges needs one entry per recording ({R})")
+        rho_r = rho if isinstance(rho, (list, tuple, np.ndarray)) else [rho] * R
+        n_blocks, sf, sl, last, rhos = [], [], [], [], []
+        for r, rr in enumerate(ranges):
+            rr = [range(x.start, x.stop) if isinstance(x, range) else range(x[0], x[1] + 1)
+                  for x in rr]
+            nseg = len(se.n_points[r])
+            pos = 0
+            for x in rr:
+                if x.start != pos or x.stop <= x.start:
+                    raise ValueError(f"recording {r}: ranges must tile its {nseg} segments")
+                pos = x.stop
+            if pos != nseg:
+                raise ValueError(f"recording {r}: ranges must tile its {nseg} segments")
+            rb = rho_r[r]
+            rb = list(rb) if isinstance(rb, (list, tuple, np.ndarray)) else [rb] * len(rr)
+            n_blocks.append(len(rr))
+            for i, x in enumerate(rr):
+                sf.append(x.start)
+                sl.append(x.stop - 1)
+                last.append(1 if i == len(rr) - 1 else 0)
+                rhos.append(float(rb[i]))
+        ens = se.ens
+        layout = ens.create_layout(n_blocks, sf, sl, last, rhos, hist_len=ll_hist_len)
+        nb = len(sf)
+        super().__init__(ens, layout, 0, nb, ll_hist_len)
+        self.se = se
+        self.recordings = []
+        b = 0
+        for r in range(R):
+            blocks = []
+            for _ in range(n_blocks[r]):
+                blocks.append(BiBlock(ens, layout, b, ll_hist_len, last[b], rhos[b],
+                                      range(sf[b], sl[b] + 1)))
+                b += 1
+            self.recordings.append(BlockCollection(ens, layout, b - len(blocks), blocks,
+                                                   ll_hist_len))
+
+    def num_recordings(self):
+        return len(self.recordings)
+
+    def ll_of_accepted(self, i):
+        flat = super().ll_of_accepted(i)
+        return [flat[c._b0:c._b1] for c in self.recordings]
+
+    def accpt_rate(self, rng):
+        flat = super().accpt_rate(rng)
+        return [flat[c._b0:c._b1] for c in self.recordings]

@@ -66,6 +66,7 @@ struct BlockArgs {
   const double* Z;  // parity mode normals, reference step order, or nullptr
   uint64_t seed;
   uint32_t iter, salt;
+  uint32_t seg_base;  // global id of local segment 0 (RNG streams; dmt_set_shard)
   double* ll_out;     // [nblocks]
   uint8_t* success;   // [nblocks] or nullptr
 };
@@ -86,6 +87,7 @@ struct AcceptArgs {
   const double* E;   // [b1-b0] or nullptr
   uint64_t seed;
   uint32_t salt;
+  uint32_t seg_base;
   uint8_t* acc_out;  // [b1-b0] or nullptr
 };
 

@@ -230,7 +230,7 @@ __global__ __launch_bounds__(64) void k_block(const BlockArgs<T> a) {
     Law<Mdl, T> L;
     L.load(a.law[ls][kind] + (int64_t)g * DMT_LAW_STRIDE);
     NormalStream<T> ns;
-    ns.init(a.seed, (uint32_t)g, a.iter, a.salt);
+    ns.init(a.seed, (uint32_t)g + a.seg_base, a.iter, a.salt);
     const double* Zg = a.Z ? a.Z + a.st_off[g] * M : nullptr;
     T* Xd = a.X[a.selX[g] ^ a.xd_flip];
     const T* Ws = a.W[a.selW[g] ^ a.ws_flip];
@@ -496,7 +496,7 @@ __global__ __launch_bounds__(128) void k_block_wave(const BlockArgs<T> a) {
           z = (T)Zg[(int64_t)i * M + kk];
         } else {
           if ((n >> 1) != have) {
-            U4 o = philox4x32_10(U4{n >> 1, (uint32_t)g, a.iter, c3}, k0, k1);
+            U4 o = philox4x32_10(U4{n >> 1, (uint32_t)g + a.seg_base, a.iter, c3}, k0, k1);
             normal_pair(o, z0, z1);
             have = n >> 1;
           }
@@ -670,7 +670,7 @@ __global__ __launch_bounds__(256) void k_accept(const AcceptArgs a) {
   const int64_t blk = a.b0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (blk >= a.b1) return;
   const double E = a.E ? a.E[blk - a.b0]
-                       : exp1_draw(a.seed, (uint32_t)blk, (uint32_t)a.mcmciter, a.salt);
+                       : exp1_draw(a.seed, (uint32_t)a.gfirst[blk] + a.seg_base, (uint32_t)a.mcmciter, a.salt);
   const double ll = a.ll[blk], llp = a.llp[blk];
   const bool acc = E > -(llp - ll);
   if (acc) {
@@ -704,7 +704,7 @@ __global__ __launch_bounds__(1024) void k_accept_reduce(const AcceptArgs a, doub
   double v0 = 0.0, v1 = 0.0, v2 = 0.0;
   if (blk < a.b1) {
     const double E = a.E ? a.E[blk - a.b0]
-                         : exp1_draw(a.seed, (uint32_t)blk, (uint32_t)a.mcmciter, a.salt);
+                         : exp1_draw(a.seed, (uint32_t)a.gfirst[blk] + a.seg_base, (uint32_t)a.mcmciter, a.salt);
     double ll = a.ll[blk], llp = a.llp[blk];
     const bool acc = E > -(llp - ll);
     if (acc) {

@@ -83,6 +83,7 @@ struct dmt_ens {
   size_t esz = 8;
   int device = 0;
   uint64_t seed = 0;
+  uint32_t seg_base = 0;  // dmt_set_shard
   int grid_shared = 0;
   int mapping = MAP_LANE;  // thread mapping of the recursion kernels
   int tw = kLanes;         // tile width of the device layout (64 lane-mapped, 1 wave-mapped)
@@ -299,6 +300,7 @@ void fill_common(dmt_ens* h, const Layout* L, BlockArgs<T>& a) {
   a.srho = L->d_srho;
   a.MB = L->MB;
   a.seed = h->seed;
+  a.seg_base = h->seg_base;
   a.Z = nullptr;
   a.success = nullptr;
 }
@@ -932,6 +934,7 @@ static AcceptArgs accept_args(dmt_ens* h, Layout* L, int64_t b0, int64_t b1, con
   a.mcmciter = mcmciter;
   a.E = dE;
   a.seed = h->seed;
+  a.seg_base = h->seg_base;
   a.salt = salt;
   a.acc_out = acc_dev;
   return a;
@@ -1277,6 +1280,14 @@ dmt_status dmt_comm_init(dmt_ens* h, int32_t nranks, int32_t rank, const uint8_t
   std::memcpy(&uid, id, 128);
   if (ncclCommInitRank(&h->comm, nranks, uid, rank) != ncclSuccess)
     return fail(DMT_ERR_COMM, "ncclCommInitRank failed");
+  return DMT_OK;
+}
+
+dmt_status dmt_set_shard(dmt_ens* h, int64_t seg_base) {
+  DMT_TRY(check_h(h));
+  if (seg_base < 0 || seg_base + h->G > (int64_t)UINT32_MAX)
+    return fail(DMT_ERR_INVALID, "seg_base out of range");
+  h->seg_base = (uint32_t)seg_base;
   return DMT_OK;
 }
 

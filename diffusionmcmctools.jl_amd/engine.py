@@ -221,6 +221,11 @@ class Ensemble:
         L.call("dmt_comm_init", self._h, int(nranks), int(rank), buf)
 
 
+    def set_shard(self, seg_base):
+        """This handle holds a shard whose local segment 0 is global segment ``seg_base``."""
+        L.call("dmt_set_shard", self._h, int(seg_base))
+
+
 def comm_unique_id() -> bytes:
     buf = (C.c_uint8 * 128)()
     L.call("dmt_comm_unique_id", buf)

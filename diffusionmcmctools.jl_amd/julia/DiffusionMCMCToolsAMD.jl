@@ -1,0 +1,306 @@
+#= DiffusionMCMCToolsAMD — Julia binding of libdmt (include/dmt.h) for DiffusionMCMCTools.jl.
+
+Device-resident counterparts of SamplingEnsemble / BlockEnsemble / BlockCollection / BiBlock
+whose methods carry the reference's names and argument meaning, each one `ccall` over a block
+range.  The host arrays passed in are the reference's own containers reinterpreted
+(Vector{SVector{d,Float64}} == double[npts][d]).
+
+No Julia toolchain exists in the build image, so this file is shipped as source and is not
+exercised by the test suite; the Python mirror (../api.py) calls the same entry points and is
+tested.  See INTEGRATION.md for the wiring into the reference package.
+=#
+module DiffusionMCMCToolsAMD
+
+using StaticArrays
+
+import DiffusionMCMCTools: draw_proposal_path!, accept_reject_proposal_path!, loglikhd!,
+    loglikhd°!, fetch_ll, fetch_ll°, save_ll!, set_accepted!, swap_paths!, swap_XX!,
+    swap_WW!, swap_PP!, swap_ll!, ll_of_accepted, accpt_rate, recompute_path!
+
+export DeviceSamplingEnsemble, DeviceBlockEnsemble, DeviceBlockCollection, DeviceBiBlock,
+    mcmc_step!, download_XX, download_WW
+
+const libdmt = get(ENV, "DMT_LIB", joinpath(@__DIR__, "..", "libdmt.so"))
+
+# ---- constants (include/dmt.h)
+const DMT_MODEL_OU, DMT_MODEL_FHN, DMT_MODEL_LORENZ = Int32(0), Int32(1), Int32(2)
+const DMT_F64, DMT_F32 = Int32(0), Int32(1)
+const DMT_MAP_AUTO = Int32(0)
+const DMT_U, DMT_UPROP = Int32(0), Int32(1)
+const DMT_LAW_PP, DMT_LAW_PPB = Int32(0), Int32(1)
+const DMT_SWAP_XX, DMT_SWAP_WW, DMT_SWAP_PP, DMT_SWAP_LL = Int32(1), Int32(2), Int32(4), Int32(8)
+const DMT_BLK_LL, DMT_BLK_LLPROP, DMT_BLK_LL_HIST, DMT_BLK_LLPROP_HIST, DMT_BLK_ACC_HIST =
+    Int32(0), Int32(1), Int32(2), Int32(3), Int32(4)
+const DMT_LAW_STRIDE = 64
+
+struct dmt_model
+    model::Int32
+    precision::Int32
+    d::Int32
+    m::Int32
+end
+
+struct dmt_structure
+    n_recordings::Int64
+    n_segments::Ptr{Int32}
+    n_points::Ptr{Int32}
+end
+
+struct dmt_config
+    seed::UInt64
+    device::Int32
+    grid_shared::Int32
+    mapping::Int32
+end
+
+function check(st::Int32)
+    st == 0 && return nothing
+    msg = unsafe_string(ccall((:dmt_last_error, libdmt), Cstring, ()))
+    error("libdmt error $st: $msg")
+end
+
+# ============================================================ SamplingEnsemble (device)
+"""
+    DeviceSamplingEnsemble(model, d, m, n_points; precision, seed, device, grid_shared)
+
+Device containers of a `SamplingEnsemble` (src/sampling_ensemble.jl:13-41): XX/WW of `u` and
+`u°` for every recording.  `n_points[r][k]` = grid points of segment k of recording r.
+"""
+mutable struct DeviceSamplingEnsemble
+    h::Ptr{Cvoid}
+    d::Int
+    m::Int
+    n_points::Vector{Vector{Int}}
+    P::Int
+    function DeviceSamplingEnsemble(model::Integer, d::Integer, m::Integer, n_points;
+                                    precision=DMT_F64, seed::Integer=0, device::Integer=0,
+                                    grid_shared::Bool=false, mapping=DMT_MAP_AUTO)
+        nseg = Int32[length(r) for r in n_points]
+        npts = Int32[n for r in n_points for n in r]
+        h = Ref{Ptr{Cvoid}}(C_NULL)
+        mdl = Ref(dmt_model(model, precision, d, m))
+        GC.@preserve nseg npts begin
+            st = Ref(dmt_structure(length(nseg), pointer(nseg), pointer(npts)))
+            cfg = Ref(dmt_config(UInt64(seed), device, grid_shared, mapping))
+            check(ccall((:dmt_create, libdmt), Int32,
+                        (Ref{Ptr{Cvoid}}, Ref{dmt_model}, Ref{dmt_structure}, Ref{dmt_config}),
+                        h, mdl, st, cfg))
+        end
+        se = new(h[], d, m, [collect(Int, r) for r in n_points], sum(npts))
+        finalizer(se) do x
+            x.h == C_NULL || ccall((:dmt_destroy, libdmt), Int32, (Ptr{Cvoid},), x.h)
+            x.h = C_NULL
+        end
+        se
+    end
+end
+
+"Concatenate per-segment trajectories (Vector{SVector}) recording-major into one flat buffer."
+flatten_paths(segs) = reduce(vcat, (collect(reinterpret(Float64, s)) for s in segs))
+
+upload_grid!(se::DeviceSamplingEnsemble, t::Vector{Float64}) =
+    check(ccall((:dmt_upload_grid, libdmt), Int32, (Ptr{Cvoid}, Ptr{Float64}), se.h, t))
+
+"""
+    upload_law!(se, unit, kind, H, F, laws; H_shared=false)
+
+Guiding-term tables of `u.PP`/`u°.PP` (kind `DMT_LAW_PP`) or `PPb` (`DMT_LAW_PPB`): packed
+`H` (upper triangle, row-major, per grid point), `F`, and one law record per segment
+(`DMT_LAW_STRIDE` doubles, layout in include/dmt.h).  Pass `nothing` to keep a table.
+"""
+function upload_law!(se::DeviceSamplingEnsemble, unit, kind, H, F, laws; H_shared=false)
+    p(x) = x === nothing ? Ptr{Float64}(C_NULL) : pointer(x)
+    GC.@preserve H F laws check(ccall((:dmt_upload_law, libdmt), Int32,
+        (Ptr{Cvoid}, Int32, Int32, Ptr{Float64}, Int32, Ptr{Float64}, Ptr{Float64}),
+        se.h, unit, kind, p(H), H_shared, p(F), p(laws)))
+end
+
+"init_paths!-style upload: X (and W, cumulative) of a unit, flat reference layout."
+function set_paths!(se::DeviceSamplingEnsemble, unit, X, W=nothing)
+    p(x) = x === nothing ? Ptr{Float64}(C_NULL) : pointer(x)
+    GC.@preserve X W check(ccall((:dmt_set_paths, libdmt), Int32,
+        (Ptr{Cvoid}, Int32, Ptr{Float64}, Ptr{Float64}), se.h, unit, p(X), p(W)))
+end
+
+function _download(se::DeviceSamplingEnsemble, unit, what, C)
+    out = Vector{Float64}(undef, se.P * C)
+    check(ccall((:dmt_download_paths, libdmt), Int32, (Ptr{Cvoid}, Int32, Int32, Ptr{Float64}),
+                se.h, unit, what, out))
+    collect(reinterpret(SVector{C,Float64}, out))
+end
+download_XX(se::DeviceSamplingEnsemble, unit=DMT_U) = _download(se, unit, 0, se.d)
+download_WW(se::DeviceSamplingEnsemble, unit=DMT_U) = _download(se, unit, 1, se.m)
+
+"draw_proposal_path!(u::SamplingUnit) for recordings r0+1:r1 (src/sampling_unit.jl:118)."
+function draw_unit!(se::DeviceSamplingEnsemble, unit, r0, r1; Z=nothing, iter=0, salt=0)
+    ll = Vector{Float64}(undef, r1 - r0)
+    ok = Vector{UInt8}(undef, r1 - r0)
+    pz = Z === nothing ? Ptr{Float64}(C_NULL) : pointer(Z)
+    GC.@preserve Z check(ccall((:dmt_draw_unit, libdmt), Int32,
+        (Ptr{Cvoid}, Int32, Int64, Int64, Ptr{Float64}, Int64, UInt32, Ptr{Float64}, Ptr{UInt8}),
+        se.h, unit, r0, r1, pz, iter, salt, ll, ok))
+    Bool.(ok), ll
+end
+
+# ============================================================ blocks
+abstract type DeviceBlocks end
+
+struct DeviceBlockEnsemble <: DeviceBlocks
+    se::DeviceSamplingEnsemble
+    layout::Int32
+    b0::Int64
+    b1::Int64
+    hist_len::Int64
+    recordings::Vector{Any}
+end
+
+struct DeviceBlockCollection <: DeviceBlocks
+    se::DeviceSamplingEnsemble
+    layout::Int32
+    b0::Int64
+    b1::Int64
+    hist_len::Int64
+    blocks::Vector{Any}
+end
+
+struct DeviceBiBlock{L} <: DeviceBlocks
+    se::DeviceSamplingEnsemble
+    layout::Int32
+    b0::Int64
+    b1::Int64
+    hist_len::Int64
+    ρ::Float64
+end
+
+"""
+    DeviceBlockEnsemble(se, ranges, ρρ=0.0, ll_hist_len=0)
+
+Same arguments as `BlockEnsemble(se, ranges, ρρ, ll_hist_len)` (src/block_ensemble.jl:20):
+`ranges[r]` = the 1-based segment ranges of recording r's blocks; ρρ scalar, per recording,
+or per recording per block.
+"""
+function DeviceBlockEnsemble(se::DeviceSamplingEnsemble, ranges, ρρ=0.0, ll_hist_len=0)
+    R = length(ranges)
+    n_blocks = Int32[length(rr) for rr in ranges]
+    sf, sl, islast, rho = Int32[], Int32[], UInt8[], Float64[]
+    for r in 1:R
+        N = length(ranges[r])
+        ρr = ρρ isa Number ? fill(ρρ, N) : (ρρ[r] isa Number ? fill(ρρ[r], N) : ρρ[r])
+        for (i, rg) in enumerate(ranges[r])
+            push!(sf, first(rg) - 1); push!(sl, last(rg) - 1)
+            push!(islast, i == N); push!(rho, ρr[i])
+        end
+    end
+    id = Ref{Int32}(0)
+    check(ccall((:dmt_create_layout, libdmt), Int32,
+        (Ptr{Cvoid}, Ptr{Int32}, Ptr{Int32}, Ptr{Int32}, Ptr{UInt8}, Ptr{Float64}, Int64,
+         Ref{Int32}), se.h, n_blocks, sf, sl, islast, rho, ll_hist_len, id))
+    recs = Any[]
+    b = 0
+    for r in 1:R
+        blocks = Any[DeviceBiBlock{Bool(islast[b+i])}(se, id[], b + i - 1, b + i, ll_hist_len,
+                                                     rho[b+i]) for i in 1:n_blocks[r]]
+        push!(recs, DeviceBlockCollection(se, id[], b, b + n_blocks[r], ll_hist_len, blocks))
+        b += n_blocks[r]
+    end
+    DeviceBlockEnsemble(se, id[], 0, b, ll_hist_len, recs)
+end
+
+_n(x::DeviceBlocks) = x.b1 - x.b0
+
+# ---- imputation and MH (src/biblock.jl:78-127, block_collection.jl:46-68, block_ensemble.jl:50-69)
+function draw_proposal_path!(x::DeviceBlocks; Z=nothing, iter=0, salt=0)
+    ok = Vector{UInt8}(undef, _n(x))
+    pz = Z === nothing ? Ptr{Float64}(C_NULL) : pointer(Z)
+    GC.@preserve Z check(ccall((:dmt_draw_proposal, libdmt), Int32,
+        (Ptr{Cvoid}, Int32, Int64, Int64, Ptr{Float64}, Int64, UInt32, Ptr{UInt8}),
+        x.se.h, x.layout, x.b0, x.b1, pz, iter, salt, ok))
+    x isa DeviceBiBlock ? Bool(ok[1]) : Bool.(ok)
+end
+
+function accept_reject_proposal_path!(x::DeviceBlocks, mcmciter; E=nothing, salt=0)
+    acc = Vector{UInt8}(undef, _n(x))
+    pe = E === nothing ? Ptr{Float64}(C_NULL) : pointer(E)
+    GC.@preserve E check(ccall((:dmt_accept_reject, libdmt), Int32,
+        (Ptr{Cvoid}, Int32, Int64, Int64, Ptr{Float64}, Int64, UInt32, Ptr{UInt8}),
+        x.se.h, x.layout, x.b0, x.b1, pe, mcmciter, salt, acc))
+    nothing
+end
+
+"draw_proposal_path! + accept_reject_proposal_path!(·, i) + (fetch_ll, fetch_ll°, #accepted)."
+function mcmc_step!(x::DeviceBlocks, mcmciter; salt=0)
+    a, b, n = Ref(0.0), Ref(0.0), Ref{Int64}(0)
+    check(ccall((:dmt_mcmc_step, libdmt), Int32,
+        (Ptr{Cvoid}, Int32, Int64, Int64, Int64, UInt32, Ref{Float64}, Ref{Float64}, Ref{Int64}),
+        x.se.h, x.layout, x.b0, x.b1, mcmciter, salt, a, b, n))
+    a[], b[], n[]
+end
+
+# ---- log-likelihoods (src/block.jl:138-152; biblock.jl:240,248; block_collection.jl:166-197)
+_ll!(x, unit) = check(ccall((:dmt_loglikhd, libdmt), Int32,
+    (Ptr{Cvoid}, Int32, Int32, Int64, Int64), x.se.h, x.layout, unit, x.b0, x.b1))
+loglikhd!(x::DeviceBlocks) = _ll!(x, DMT_U)
+loglikhd°!(x::DeviceBlocks) = _ll!(x, DMT_UPROP)
+
+function _fetch(x::DeviceBlocks)
+    a, b, n = Ref(0.0), Ref(0.0), Ref{Int64}(0)
+    check(ccall((:dmt_fetch_ll, libdmt), Int32,
+        (Ptr{Cvoid}, Int32, Int64, Int64, Int64, Ref{Float64}, Ref{Float64}, Ref{Int64}),
+        x.se.h, x.layout, x.b0, x.b1, 0, a, b, n))
+    a[], b[]
+end
+fetch_ll(x::DeviceBlocks) = _fetch(x)[1]
+fetch_ll°(x::DeviceBlocks) = _fetch(x)[2]
+
+"recompute_path!(bb.b°, bb.b.WW; skip) over the blocks (src/block.jl:159-187)."
+function recompute_path!(x::DeviceBlocks; skip=0)
+    ok = Vector{UInt8}(undef, _n(x))
+    check(ccall((:dmt_recompute_path, libdmt), Int32,
+        (Ptr{Cvoid}, Int32, Int64, Int64, Int32, Ptr{UInt8}),
+        x.se.h, x.layout, x.b0, x.b1, skip, ok))
+    Bool.(ok)
+end
+
+# ---- swaps, histories (src/biblock.jl:135-259)
+_swap!(x, what) = check(ccall((:dmt_swap, libdmt), Int32,
+    (Ptr{Cvoid}, Int32, Int32, Int64, Int64), x.se.h, x.layout, what, x.b0, x.b1))
+swap_paths!(x::DeviceBlocks) = _swap!(x, DMT_SWAP_XX | DMT_SWAP_WW)
+swap_XX!(x::DeviceBlocks) = _swap!(x, DMT_SWAP_XX)
+swap_WW!(x::DeviceBlocks) = _swap!(x, DMT_SWAP_WW)
+swap_PP!(x::DeviceBlocks) = _swap!(x, DMT_SWAP_PP)
+swap_ll!(x::DeviceBlocks) = _swap!(x, DMT_SWAP_LL)
+
+save_ll!(x::DeviceBlocks, i::Int) = check(ccall((:dmt_save_ll, libdmt), Int32,
+    (Ptr{Cvoid}, Int32, Int64, Int64, Int64), x.se.h, x.layout, x.b0, x.b1, i))
+
+function set_accepted!(x::DeviceBlocks, i::Int, v)
+    vv = fill(UInt8(v), _n(x))
+    check(ccall((:dmt_set_accepted, libdmt), Int32,
+        (Ptr{Cvoid}, Int32, Int64, Int64, Int64, Ptr{UInt8}), x.se.h, x.layout, x.b0, x.b1, i, vv))
+end
+
+function _state(x::DeviceBlocks, what, T, dims...)
+    out = Array{T}(undef, dims...)
+    check(ccall((:dmt_get_block_state, libdmt), Int32,
+        (Ptr{Cvoid}, Int32, Int32, Int64, Int64, Ptr{Cvoid}),
+        x.se.h, x.layout, what, x.b0, x.b1, out))
+    out
+end
+# histories come back iteration-major: [hist_len][nblocks] == Julia (nblocks, hist_len)
+_hist(x, what, T) = _state(x, what, T, _n(x), x.hist_len)
+
+function ll_of_accepted(x::DeviceBlocks, i)
+    acc = _hist(x, DMT_BLK_ACC_HIST, UInt8)[:, i] .!= 0
+    llh = _hist(x, DMT_BLK_LL_HIST, Float64)[:, i]
+    llph = _hist(x, DMT_BLK_LLPROP_HIST, Float64)[:, i]
+    v = ifelse.(acc, llph, llh)
+    x isa DeviceBiBlock ? v[1] : v
+end
+
+function accpt_rate(x::DeviceBlocks, range)
+    acc = _hist(x, DMT_BLK_ACC_HIST, UInt8)[:, range] .!= 0
+    v = vec(sum(acc; dims=2)) ./ length(range)
+    x isa DeviceBiBlock ? v[1] : v
+end
+
+end # module

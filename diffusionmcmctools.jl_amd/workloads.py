@@ -223,3 +223,23 @@ def fill(ens, w: Workload, init_Z=True):
     lay = ens.create_layout(w.n_blocks, w.seg_first, w.seg_last, w.last,
                             np.full(w.nblocks, w.rho), hist_len=w.meta.get("hist_len", 0))
     return lay
+
+
+def concat_workloads(ws):
+    """The global workload whose recording shards are ``ws`` (in rank order).  Shared grids
+    and shared guiding tables must agree between shards."""
+    w0 = ws[0]
+    for w in ws[1:]:
+        assert w.grid_shared == w0.grid_shared and w.H_shared == w0.H_shared
+        if w0.grid_shared:
+            assert np.array_equal(w.t, w0.t)
+        if w0.H_shared:
+            assert np.array_equal(w.H, w0.H)
+    cat = lambda k: np.concatenate([getattr(w, k) for w in ws])  # noqa: E731
+    g = Workload(w0.name, w0.model, w0.precision, [r for w in ws for r in w.n_points],
+                 w0.t if w0.grid_shared else cat("t"), w0.grid_shared,
+                 w0.H if w0.H_shared else cat("H"), w0.H_shared, cat("F"), cat("laws"),
+                 cat("X0"), cat("Z0"), w0.rho)
+    g.n_blocks, g.seg_first, g.seg_last, g.last = (cat(k) for k in
+                                                   ("n_blocks", "seg_first", "seg_last", "last"))
+    return g

@@ -180,7 +180,8 @@ dmt_status dmt_draw_proposal(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
 
 /* accept_reject_proposal_path!(·, mcmciter) (src/biblock.jl:121-127): E > -(ll° - ll),
  * swap XX/WW, set_accepted!, save_ll! (both), swap ll.  E: double[b1-b0] (parity) or NULL
- * (device Exp(1) stream keyed by (seed, mcmciter, salt, block)).  acc_out nullable. */
+ * (device Exp(1) stream keyed by (seed, mcmciter, salt, global id of the block's first
+ * segment)).  acc_out nullable. */
 dmt_status dmt_accept_reject(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
                              const double* E, int64_t mcmciter, uint32_t salt,
                              uint8_t* acc_out);
@@ -241,6 +242,12 @@ dmt_status dmt_guiding_linear(int32_t d, const double* Bt, const double* beta,
 /* ---------------- multi-GPU (RCCL over xGMI) ---------------- */
 dmt_status dmt_comm_unique_id(uint8_t* id_out /*128 bytes*/);
 dmt_status dmt_comm_init(dmt_ens* h, int32_t nranks, int32_t rank, const uint8_t* id);
+/* Declare this handle a shard of a larger SamplingEnsemble: its local segment 0 is global
+ * segment seg_base.  Device RNG streams are keyed by global segment ids, so a sharded
+ * ensemble draws exactly the normals / Exp(1) variables of the unsharded one (weak-scaling
+ * shards are bit-identical to the corresponding blocks of one big ensemble).  Default 0.
+ * No reference counterpart (the reference is single-process). */
+dmt_status dmt_set_shard(dmt_ens* h, int64_t seg_base);
 
 /* ---------------- misc ---------------- */
 dmt_status dmt_sync(dmt_ens* h);

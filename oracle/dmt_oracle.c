@@ -162,7 +162,7 @@ static inline REAL g_at(int model, int d, const REAL* th, const REAL* a, const R
         r[p] = acc;
     }
     orc_drift(model, d, th, x, b);
-    REAL db[3];
+    REAL db[3] = {0, 0, 0};
     for (int p = 0; p < d; ++p) {
         REAL bt = beta[p];
         for (int q = 0; q < d; ++q) bt = FMA(Bt[p * d + q], x[q], bt);
@@ -266,7 +266,7 @@ REAL SFX(orc_path_ll_segment)(int model, int d, int m, const double* law, int np
 
 /* GP.loglikhd_obs(P, y1) = log rho~(t0, y1) = -c0 - 1/2 y'H y + F'y */
 REAL SFX(orc_obs_term)(int d, const double* law, const REAL* H0, const REAL* F0, const REAL* x) {
-    REAL Hx[3];
+    REAL Hx[3] = {0, 0, 0};
     for (int p = 0; p < d; ++p) {
         REAL acc = H0[pidx(d, p, 0)] * x[0];
         for (int q = 1; q < d; ++q) acc = FMA(H0[pidx(d, p, q)], x[q], acc);
@@ -418,7 +418,8 @@ void SFX(orc_normal_pair)(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2, 
 }
 
 #if IS_F64
-/* Exp(1) draw for the MH test of block `blk` (perf-mode stream). */
+/* Exp(1) draw for the MH test of a block (perf-mode stream); `blk` = global id of the
+ * block's first segment. */
 double orc_exp1(uint64_t seed, uint32_t blk, uint32_t iter, uint32_t salt) {
     uint32_t c[4] = {blk, 0xFFFFFFFFu, iter, (salt << 1) | 1u};
     orc_philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));

@@ -268,6 +268,7 @@ class OracleEnsemble:
             U_.PP = [None] * self.G
             U_.PPb = [None] * self.G
         self.layouts = []
+        self.seg_base = 0  # dmt_set_shard
         # internal layout 0: whole recordings, terminal, rho 0 (draw_proposal_path!(u))
         self.create_layout([1] * self.R, [0] * self.R, [n - 1 for n in self.nseg], [1] * self.R,
                            [0.0] * self.R, 0)
@@ -349,7 +350,7 @@ class OracleEnsemble:
         if Z is not None:
             Zf = np.asarray(Z, dtype=np.float64).reshape(-1, self.m)
             return Zf[self.st_off[g]: self.st_off[g] + n].astype(self.dt)
-        return normals_segment(self.seed, g, it, salt, n, self.m, self.prec)
+        return normals_segment(self.seed, g + self.seg_base, it, salt, n, self.m, self.prec)
 
     def _law(self, unit, bk, g):
         me = self._unit(unit)
@@ -414,8 +415,8 @@ class OracleEnsemble:
         """accept_reject_proposal_path!(bb, i), src/biblock.jl:121-127."""
         accs = []
         for j, bk in enumerate(self.layouts[layout][b0:b1]):
-            blk = b0 + j
-            e = float(E[j]) if E is not None else exp1(self.seed, blk, mcmciter, salt)
+            e = (float(E[j]) if E is not None
+                 else exp1(self.seed, bk.g0 + self.seg_base, mcmciter, salt))
             acc = e > -(bk.llp - bk.ll)
             if acc:  # swap_paths!: XX and WW element swaps (src/biblock.jl:148-173)
                 for g in range(bk.g0, bk.g1 + 1):
@@ -487,6 +488,32 @@ class OracleEnsemble:
         bks = self.layouts[layout][b0:b1]
         return (np.stack([b.ll_hist for b in bks], 1), np.stack([b.llp_hist for b in bks], 1),
                 np.stack([b.acc_hist for b in bks], 1))
+
+    def set_shard(self, seg_base):
+        self.seg_base = int(seg_base)
+
+    def get_block_state(self, layout, what, b0, b1, hist_len=None):
+        """Same contract as dmt_get_block_state (histories iteration-major)."""
+        bks = self.layouts[layout][b0:b1]
+        if what == 0:
+            return np.array([b.ll for b in bks])
+        if what == 1:
+            return np.array([b.llp for b in bks])
+        h = {2: "ll_hist", 3: "llp_hist", 4: "acc_hist"}[what]
+        out = np.stack([getattr(b, h) for b in bks], 1)
+        return out.astype(np.uint8) if what == 4 else out
+
+    def set_block_state(self, layout, what, b0, b1, values):
+        bks = self.layouts[layout][b0:b1]
+        v = np.asarray(values)
+        for j, b in enumerate(bks):
+            if what == 0:
+                b.ll = float(v[j])
+            elif what == 1:
+                b.llp = float(v[j])
+            else:
+                h = {2: "ll_hist", 3: "llp_hist", 4: "acc_hist"}[what]
+                getattr(b, h)[...] = v[:, j]
 
     def fetch_ll(self, layout, b0, b1, mcmciter=0):
         bks = self.layouts[layout][b0:b1]

@@ -1,0 +1,190 @@
+"""The host mirror of the reference interface (diffusionmcmctools.jl_amd/api.py).
+
+CPU tests drive the API's host logic (range bookkeeping, BiBlock/BlockCollection/BlockEnsemble
+dispatch, ll_of_accepted / accpt_rate / fetch_ll semantics) over the oracle backend through the
+``_engine`` test seam; the GPU test runs the same reference-style MCMC program through libdmt and
+through the oracle and requires bit-identical results."""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import pytest
+
+import diffusionmcmctools_amd as dmt
+from diffusionmcmctools_amd import _lib as L
+import oracle as orc
+
+from _cases import ragged_case
+
+RANGES_A = [[range(0, 2), range(2, 4)],
+            [range(0, 2), range(2, 4), range(4, 6)],
+            [range(0, 3), range(3, 5)]]
+RANGES_B = [[range(0, 4)], [range(0, 3), range(3, 6)], [range(0, 2), range(2, 5)]]
+
+
+def _sampling_ensemble(case, backend, seed=11):
+    m = case["model"]
+    if backend == "oracle":
+        eng = orc.OracleEnsemble(m.kind, m.d, m.m, case["n_points"], prec=case["prec"], seed=seed)
+        se = dmt.SamplingEnsemble(m, case["n_points"], _engine=eng)
+    else:
+        se = dmt.SamplingEnsemble(m, case["n_points"], precision=case["prec"], seed=seed)
+    se.upload_grid(case["t"])
+    se.set_guiding(case["H"], case["F"], case["laws"], Hb=case["Hb"], Fb=case["Fb"],
+                   lawsb=case["lawsb"])
+    X0 = case["X0"]
+    e = se.ens
+    x0 = X0[e.pt_off[e.rec_seg0[:-1]]]
+    se.init_paths(x0, Z=case["Z0"], iter=0, salt=1)
+    return se
+
+
+def _program(se, niter=6, seed=3):
+    """The reference's smoothing-with-blocking loop (docs/src/tutorials/biblock/
+    smoothing_with_blocking.md:60-75): alternate two blockings; per iteration draw, MH decide,
+    record fetch_ll.  Parity-mode draws (Z, E supplied)."""
+    rng = np.random.default_rng(seed)
+    e = se.ens
+    beA = dmt.BlockEnsemble(se, RANGES_A, rho=0.7, ll_hist_len=niter)
+    beB = dmt.BlockEnsemble(se, RANGES_B, rho=[0.3, [0.2, 0.5], 0.4], ll_hist_len=niter)
+    out = []
+    for be in (beA, beB):
+        be.loglikhd()
+    for i in range(1, niter + 1):
+        be = beA if i % 2 else beB
+        Z = rng.standard_normal((e.S, 1))
+        E = rng.exponential(1.0, be.num_blocks)
+        ok = be.draw_proposal_path(Z=Z)
+        acc = be.accept_reject_proposal_path(i, E=E)
+        out.append((ok, acc, be.fetch_ll(), be.fetch_ll_prop(),
+                    [c.fetch_ll() for c in be.recordings], be.ll.copy(), be.ll_prop.copy()))
+        # one BiBlock-level step on the first block of recording 1
+        bb = be.recordings[1].blocks[0]
+        Zb = rng.standard_normal((e.S, 1))
+        bb.draw_proposal_path(Z=Zb, iter=100 + i)
+        bb.loglikhd_prop()
+        out.append((bb.fetch_ll(), bb.fetch_ll_prop()))
+    return beA, beB, out
+
+
+def test_block_ensemble_structure():
+    case = ragged_case()
+    se = _sampling_ensemble(case, "oracle")
+    be = dmt.BlockEnsemble(se, RANGES_A, rho=0.7, ll_hist_len=4)
+    assert be.num_recordings() == 3
+    assert [len(c.blocks) for c in be.recordings] == [2, 3, 2]
+    assert be.num_blocks == 7
+    lasts = [[b.is_last for b in c.blocks] for c in be.recordings]
+    assert lasts == [[False, True], [False, False, True], [False, True]]
+    assert be.recordings[2].blocks[0].segments == range(0, 3)
+    assert all(b.rho == 0.7 for c in be.recordings for b in c.blocks)
+    assert be.ll.shape == (7,) and np.all(be.ll == -math.inf)  # src/block.jl:75
+
+
+@pytest.mark.parametrize("bad", [
+    [[range(0, 2), range(3, 4)], [range(0, 6)], [range(0, 5)]],   # gap
+    [[range(0, 4)], [range(0, 5)], [range(0, 5)]],                # short
+    [[range(0, 4)], [range(0, 6)]],                               # missing recording
+])
+def test_block_ensemble_rejects_bad_ranges(bad):
+    case = ragged_case()
+    se = _sampling_ensemble(case, "oracle")
+    with pytest.raises(ValueError):
+        dmt.BlockEnsemble(se, bad)
+
+
+def test_mcmc_semantics_on_host():
+    """ll_of_accepted / accpt_rate / histories / fetch_ll follow the reference definitions."""
+    case = ragged_case()
+    se = _sampling_ensemble(case, "oracle")
+    beA, beB, out = _program(se, niter=6)
+    for be in (beA, beB):
+        llh, llph, acch = be.ll_history, be.ll_prop_history, be.accpt_history
+        for i in range(1, 7):
+            if not acch[i - 1].any() and not (llh[i - 1] != 0).any():
+                continue  # this blocking was not used at iteration i
+            got = be.ll_of_accepted(i)
+            want = np.where(acch[i - 1], llph[i - 1], llh[i - 1])
+            np.testing.assert_array_equal(np.concatenate(got), want)
+        rate = np.concatenate(be.accpt_rate(range(1, 7)))
+        np.testing.assert_array_equal(rate, acch.sum(0) / 6)
+    ok, acc, f, fp, per_rec, ll, llp = out[0]
+    assert ok.all() and 0 < acc.sum() < acc.size
+    # fetch_ll of the ensemble is the pairwise tree over its blocks; per recording likewise
+    np.testing.assert_equal(f, orc.pairwise_tree(list(ll)))
+    np.testing.assert_equal(per_rec[1], orc.pairwise_tree(list(ll[2:5])))
+    assert math.isfinite(f) and math.isfinite(fp)
+    # BiBlock fetch_ll is its own ll
+    b = beA.recordings[0].blocks[1]
+    assert b.fetch_ll() == beA.ll[1]
+
+
+def test_accept_order_matches_reference():
+    """accept_reject_proposal_path!: save_ll! records PRE-swap values (src/biblock.jl:121-127)."""
+    case = ragged_case()
+    se = _sampling_ensemble(case, "oracle")
+    be = dmt.BlockEnsemble(se, RANGES_A, rho=0.5, ll_hist_len=3)
+    be.loglikhd()
+    rng = np.random.default_rng(0)
+    for i in (1, 2):
+        be.draw_proposal_path(Z=rng.standard_normal((se.ens.S, 1)))
+        ll0, llp0 = be.ll.copy(), be.ll_prop.copy()
+        E = rng.exponential(1.0, be.num_blocks)
+        acc = be.accept_reject_proposal_path(i, E=E)
+        np.testing.assert_array_equal(acc, E > -(llp0 - ll0))
+        np.testing.assert_array_equal(be.ll_history[i - 1], ll0)
+        np.testing.assert_array_equal(be.ll_prop_history[i - 1], llp0)
+        np.testing.assert_array_equal(be.ll, np.where(acc, llp0, ll0))
+        np.testing.assert_array_equal(be.ll_prop, np.where(acc, ll0, llp0))
+
+
+def test_swaps_and_set_accepted():
+    case = ragged_case()
+    se = _sampling_ensemble(case, "oracle")
+    be = dmt.BlockEnsemble(se, RANGES_B, rho=0.5, ll_hist_len=2)
+    be.loglikhd()
+    be.draw_proposal_path(Z=np.random.default_rng(1).standard_normal((se.ens.S, 1)))
+    X_u = se.recordings[1].u.XX
+    X_p = se.recordings[1].u_prop.XX
+    coll = be.recordings[1]
+    coll.swap_XX()
+    for a, b in zip(se.recordings[1].u.XX, X_p):
+        np.testing.assert_array_equal(a, b)
+    for a, b in zip(se.recordings[1].u_prop.XX, X_u):
+        np.testing.assert_array_equal(a, b)
+    coll.swap_XX()
+    ll, llp = coll.ll.copy(), coll.ll_prop.copy()
+    coll.swap_ll()
+    np.testing.assert_array_equal(coll.ll, llp)
+    np.testing.assert_array_equal(coll.ll_prop, ll)
+    coll.blocks[1].set_accepted(2, True)
+    assert coll.blocks[1].accpt_history[1] and not coll.blocks[0].accpt_history[1]
+
+
+@pytest.mark.gpu
+def test_api_program_gpu_matches_oracle():
+    case = ragged_case()
+    se_d = _sampling_ensemble(case, "gpu")
+    se_o = _sampling_ensemble(case, "oracle")
+    beA_d, beB_d, out_d = _program(se_d)
+    beA_o, beB_o, out_o = _program(se_o)
+    for a, b in zip(out_d, out_o):
+        for x, y in zip(a, b):
+            if isinstance(x, list):
+                for xx, yy in zip(x, y):
+                    np.testing.assert_array_equal(np.asarray(xx), np.asarray(yy))
+            else:
+                np.testing.assert_array_equal(np.asarray(x), np.asarray(y))
+    for r in range(3):
+        for unit in ("u", "u_prop"):
+            for a, b in zip(getattr(se_d.recordings[r], unit).XX,
+                            getattr(se_o.recordings[r], unit).XX):
+                np.testing.assert_array_equal(a, b)
+            for a, b in zip(getattr(se_d.recordings[r], unit).WW,
+                            getattr(se_o.recordings[r], unit).WW):
+                np.testing.assert_array_equal(a, b)
+    for bd, bo in ((beA_d, beA_o), (beB_d, beB_o)):
+        np.testing.assert_array_equal(bd.ll_history, bo.ll_history)
+        np.testing.assert_array_equal(bd.accpt_history, bo.accpt_history)
+    se_d.close()

@@ -1,0 +1,115 @@
+"""Multi-rank sharding on CPU (gloo, world_size 2): a BlockEnsemble split into recording
+shards, each rank keyed by global segment ids (set_shard) and combining fetch_ll partials in
+rank order, reproduces the unsharded ensemble bit for bit (shard.py).  The
+numerics run on the oracle backend here; the GPU test drives two libdmt shards on one device."""
+from __future__ import annotations
+
+import os
+import socket
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+B_LOCAL, N, ITERS, SEED = 8, 40, 3, 77
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run(ens, lay, nb):
+    """Perf-mode MCMC iterations (device-RNG streams), returning per-iteration partials."""
+    ens.loglikhd(lay, 0, 0, nb)
+    parts = []
+    for i in range(1, ITERS + 1):
+        ens.draw_proposal(lay, 0, nb, Z=None, iter=i)
+        ens.accept_reject(lay, 0, nb, i)
+        parts.append(ens.fetch_ll(lay, 0, nb, i))
+    ll = ens.get_block_state(lay, 0, 0, nb)
+    return parts, ll
+
+
+def _worker(rank, world, port, out_dir):
+    import sys
+    for p in (ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
+        sys.path.insert(0, p)
+    import torch.distributed as dist
+    import oracle as orc
+    from diffusionmcmctools_amd import workloads as W
+    from diffusionmcmctools_amd import shard
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    w = W.c2_ou2d(B=B_LOCAL, N=N, block_offset=rank)
+    w.meta["hist_len"] = ITERS
+    ens = orc.OracleEnsemble(w.model.kind, w.d, w.m, w.n_points, prec=w.precision, seed=SEED,
+                             grid_shared=w.grid_shared)
+    ens.set_shard(shard.segment_base([len(r) for r in w.n_points] * world, rank * B_LOCAL))
+    lay = W.fill(ens, w, init_Z=True)
+    parts, ll = _run(ens, lay, w.nblocks)
+    glob = [shard.combine_partials(p) for p in parts]
+    np.save(os.path.join(out_dir, f"ll{rank}.npy"), ll)
+    np.save(os.path.join(out_dir, f"glob{rank}.npy"), np.array(glob))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_shard_helpers():
+    from diffusionmcmctools_amd import shard
+    assert [shard.shard_range(10, 4, r) for r in range(4)] == [(0, 3), (3, 6), (6, 8), (8, 10)]
+    assert shard.segment_base([4, 6, 5], 2) == 10
+    assert shard.rank_tree([1.0, 2.0, 3.0]) == (1.0 + 2.0) + (3.0 + 0.0)
+
+
+def test_two_rank_shards_match_unsharded(tmp_path):
+    import torch.multiprocessing as mp
+    import oracle as orc
+    from diffusionmcmctools_amd import workloads as W
+    world = 2
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+                       join=True, start_method="spawn")
+    ws = [W.c2_ou2d(B=B_LOCAL, N=N, block_offset=r) for r in range(world)]
+    g = W.concat_workloads(ws)
+    g.meta["hist_len"] = ITERS
+    ens = orc.OracleEnsemble(g.model.kind, g.d, g.m, g.n_points, prec=g.precision, seed=SEED,
+                             grid_shared=g.grid_shared)
+    lay = W.fill(ens, g, init_Z=True)
+    parts, ll = _run(ens, lay, g.nblocks)
+    ll_sharded = np.concatenate([np.load(tmp_path / f"ll{r}.npy") for r in range(world)])
+    np.testing.assert_array_equal(ll_sharded, ll)
+    for r in range(world):
+        glob = np.load(tmp_path / f"glob{r}.npy")
+        np.testing.assert_array_equal(glob, np.array(parts, dtype=np.float64))
+
+
+@pytest.mark.gpu
+def test_gpu_shards_match_unsharded():
+    """Two libdmt shards (set_shard) on one GPU vs one ensemble holding both: identical paths,
+    ll and decisions; host rank tree of the shard partials == the unsharded fetch_ll."""
+    import diffusionmcmctools_amd as dmt
+    from diffusionmcmctools_amd import workloads as W
+    from diffusionmcmctools_amd import shard
+    world, B = 2, 256
+    ws = [W.c2_ou2d(B=B, N=100, block_offset=r) for r in range(world)]
+    g = W.concat_workloads(ws)
+    for w in ws + [g]:
+        w.meta["hist_len"] = ITERS
+
+    def make(w, base):
+        e = dmt.Ensemble(w.model.kind, w.d, w.m, w.n_points, precision=w.precision, seed=SEED,
+                         grid_shared=w.grid_shared)
+        e.set_shard(base)
+        return e, W.fill(e, w, init_Z=True)
+
+    shards = [make(w, r * B) for r, w in enumerate(ws)]
+    full, lay = make(g, 0)
+    res_s = [_run(e, l, B) for e, l in shards]
+    parts, ll = _run(full, lay, g.nblocks)
+    np.testing.assert_array_equal(np.concatenate([r[1] for r in res_s]), ll)
+    for i in range(ITERS):
+        comb = tuple(shard.rank_tree([res_s[r][0][i][c] for r in range(world)]) for c in range(3))
+        assert comb == tuple(float(x) for x in parts[i])
+    X = np.concatenate([e.download_paths(1, 0) for e, _ in shards])
+    np.testing.assert_array_equal(X, full.download_paths(1, 0))
