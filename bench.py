@@ -29,7 +29,8 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+PEAK_HBM_GBS = 8000.0
+EXTRA_ITERS = 5  # untimed iterations after the timed region (accept-kernel event timing)  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 
 WORKLOADS = {
     "c2": ("C2: 2D OU guided bridge, 1024 blocks x 500 Euler steps per GPU, fp64", "f64"),
@@ -55,6 +56,20 @@ def algorithmic_bytes_per_step(w):
     s = 8 if w.precision == 0 else 4
     h = 0 if w.H_shared else w.d * (w.d + 1) // 2
     return s * (2 * w.m + 2 * w.d + h)
+
+
+def measured_traffic(config, kernel_substr):
+    """HBM bytes per launch of the draw kernel from the newest committed PMC summary
+    (profiles/rNN_traffic_<config>.json, scripts/pmc_traffic.py: separate FETCH_SIZE and
+    WRITE_SIZE rocprofv3 passes, calibrated with scripts/calib_stream); None if absent."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_traffic_{config}.json")))
+    for path in reversed(files):
+        with open(path) as f:
+            t = json.load(f)
+        if kernel_substr in t.get("kernel", ""):
+            return t["traffic_bytes_per_launch"], os.path.relpath(path, ROOT)
+    return None, None
 
 
 def cpu_baseline(w, ens, lay, budget_s=12.0):
@@ -133,7 +148,7 @@ def main():
     from diffusionmcmctools_amd import workloads as W
 
     w = build_workload(args.config, rank)
-    w.meta["hist_len"] = args.warmup + args.steps
+    w.meta["hist_len"] = args.warmup + args.steps + EXTRA_ITERS
     mapping = {"auto": L.MAP_AUTO, "lane": L.MAP_LANE, "wave": L.MAP_WAVE}[args.mapping]
     ens = dmt.Ensemble(w.model.kind, w.d, w.m, w.n_points, precision=w.precision,
                        seed=0xD1FF, device=local_rank, grid_shared=w.grid_shared,
@@ -149,28 +164,30 @@ def main():
         ens.comm_init(world, rank, uid[0])
     ens.loglikhd(lay, L.U, 0, B)
 
-    def step(i):
-        # draw_proposal_path!(be); accept_reject_proposal_path!(be, i); fetch_ll(be) — one call
-        return ens.mcmc_step(lay, 0, B, i)
+    # one step = draw_proposal_path!(be); accept_reject_proposal_path!(be, i); fetch_ll(be).
+    # The K timed steps are queued back to back on the device (dmt_mcmc_run: no host round
+    # trip per iteration; every iteration's fetch_ll values come back at the end).
 
     def barrier():
         ens.sync()
         if dist is not None:
             dist.barrier()
 
-    for i in range(1, args.warmup + 1):
-        step(i)
+    if args.warmup:
+        ens.mcmc_run(lay, 0, B, 1, args.warmup)
     barrier()
-    ens.set_timing(True)
+    # HIP events around the dominant (draw) kernel over the timed region, on libdmt's stream
+    ens.set_timing(True, kernels=[L.K_DRAW])
     barrier()
     t0 = time.perf_counter()
-    n_acc = 0
-    for i in range(args.warmup + 1, args.warmup + args.steps + 1):
-        _, _, na = step(i)
-        n_acc += na
+    res = ens.mcmc_run(lay, 0, B, args.warmup + 1, args.steps)
     barrier()
     el = time.perf_counter() - t0
+    n_acc = float(res[:, 2].sum())
     k_ms, k_n = ens.get_timing(L.K_DRAW)
+    # the accept+reduce kernel, timed on a few extra iterations after the timed region
+    ens.set_timing(True, kernels=[L.K_ACCEPT])
+    ens.mcmc_run(lay, 0, B, args.warmup + args.steps + 1, EXTRA_ITERS)
     a_ms, a_n = ens.get_timing(L.K_ACCEPT)
     ens.set_timing(False)
     if dist is not None:
@@ -185,6 +202,10 @@ def main():
     bytes_launch = algorithmic_bytes_per_step(w) * w.steps_per_iter
     achieved = bytes_launch / k_avg_s / 1e9 if k_avg_s > 0 else 0.0
     accept_rate = n_acc / (B * world * args.steps)  # n_acc is already global (fetch_ll over ranks)
+    # the mapping libdmt resolves for MAP_AUTO (kAutoWaveMaxRecordings, dmt_internal.h)
+    wave = args.mapping == "wave" or (args.mapping == "auto" and len(w.n_points) <= 8192)
+    kname = "k_block_wave" if wave else "k_block<"
+    traffic, traffic_src = measured_traffic(args.config, kname)
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
@@ -206,13 +227,14 @@ def main():
             "config": {"workload": desc, "blocks_per_gpu": B,
                        "euler_steps_per_block": w.steps_per_iter // B, "rho": w.rho,
                        "parallelism": f"blockensemble-shard x{world}",
-                       "mapping": args.mapping,
+                       "mapping": "wave" if wave else "lane",
                        "rng": "device Philox4x32-10 + Box-Muller (perf mode)"},
             "per_gpu": value / world,
             "accept_rate": accept_rate,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS,
-                         "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS, "traffic": None,
-                         "kernel": "k_block (draw_proposal)", "kernel_avg_us": k_avg_s * 1e6,
+                         "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
+                         "traffic_source": traffic_src,
+                         "kernel": kname + " (draw_proposal_path!)", "kernel_avg_us": k_avg_s * 1e6,
                          "algorithmic_bytes_per_launch": bytes_launch,
                          "bytes_per_step": algorithmic_bytes_per_step(w)},
             "accept_kernel_avg_us": (a_ms / max(a_n, 1)) * 1e3,

@@ -11,7 +11,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libdmt.so")
+# DMT_LIB_PATH: alternative build of the same library (kernel-variant experiments)
+LIB_PATH = os.environ.get("DMT_LIB_PATH") or os.path.join(HERE, "libdmt.so")
 INCLUDE_H = os.path.join(os.path.dirname(HERE), "include", "dmt.h")
 
 # ---- constants (mirror include/dmt.h) ----
@@ -33,7 +34,7 @@ SYMBOLS = [
     "dmt_download_paths", "dmt_draw_unit", "dmt_create_layout", "dmt_layout_size",
     "dmt_draw_proposal", "dmt_accept_reject", "dmt_loglikhd", "dmt_recompute_path", "dmt_swap",
     "dmt_save_ll", "dmt_set_accepted", "dmt_get_block_state", "dmt_set_block_state",
-    "dmt_fetch_ll", "dmt_mcmc_step", "dmt_guiding_linear", "dmt_comm_unique_id", "dmt_comm_init", "dmt_set_shard", "dmt_sync",
+    "dmt_fetch_ll", "dmt_mcmc_step", "dmt_mcmc_run", "dmt_guiding_linear", "dmt_comm_unique_id", "dmt_comm_init", "dmt_set_shard", "dmt_sync",
     "dmt_set_timing", "dmt_get_timing", "dmt_memory_bytes", "dmt_debug_philox",
     "dmt_debug_normals", "dmt_last_error", "dmt_version",
 ]
@@ -98,6 +99,7 @@ _SIGS = {
     "dmt_guiding_linear": [_i32, _pd, _pd, _pd, _i32, _pd, _pd, _pd, C.c_double, _pd, _pd, _pd],
     "dmt_comm_unique_id": [_pu8],
     "dmt_comm_init": [_P, _i32, _i32, _pu8],
+    "dmt_mcmc_run": [_P, _i32, _i64, _i64, _i64, _i64, _u32, _pd],
     "dmt_set_shard": [_P, _i64],
     "dmt_sync": [_P],
     "dmt_set_timing": [_P, _i32],

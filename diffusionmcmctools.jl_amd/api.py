@@ -254,6 +254,13 @@ class _BlockRange:
         ``fetch_ll`` fused into one call (device RNG).  Returns (ll, ll°, n_accepted)."""
         return self._call("mcmc_step", mcmciter, salt=salt)
 
+    def mcmc_run(self, iter0, n_iter, salt=0):
+        """``n_iter`` consecutive :meth:`mcmc_step` iterations starting at ``iter0``, queued on
+        the device without host round trips; returns an (n_iter, 3) array of (fetch_ll,
+        fetch_ll°, accepted count) — the sampling loop of
+        docs/src/tutorials/biblock/smoothing.md:40-44."""
+        return self._call("mcmc_run", iter0, n_iter, salt=salt)
+
 
 class BiBlock(_BlockRange):
     """``BiBlock{L}`` (src/biblock.jl:42-63): one block b / b° with pCN memory ρ."""

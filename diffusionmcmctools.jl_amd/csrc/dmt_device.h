@@ -21,6 +21,14 @@ __host__ __device__ constexpr int packed_idx(int d, int a, int b) {
 __device__ __forceinline__ double dfma(double a, double b, double c) { return __builtin_fma(a, b, c); }
 __device__ __forceinline__ float dfma(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
 
+// Load through the constant address space: for data a kernel only reads (law records,
+// structure arrays, selectors inside the block kernels) with a wave-uniform address this
+// becomes a scalar load into SGPRs instead of a vector load into VGPRs.
+template <class T>
+__device__ __forceinline__ T ldc(const T* p) {
+  return *(const __attribute__((address_space(4))) T*)(p);
+}
+
 // ---------------------------------------------------------------- models
 // Drifts of the DiffusionDefinition models.
 template <class T, int D_, int M_>
@@ -82,20 +90,20 @@ struct Law {
   bool trace;
   __device__ __forceinline__ void load(const double* L) {
 #pragma unroll
-    for (int i = 0; i < Mdl::NTH; ++i) th[i] = (T)L[DMT_LAW_THETA + i];
+    for (int i = 0; i < Mdl::NTH; ++i) th[i] = (T)ldc(L + DMT_LAW_THETA + i);
 #pragma unroll
     for (int p = 0; p < D; ++p)
 #pragma unroll
-      for (int k = 0; k < M; ++k) sg[p * M + k] = (T)L[DMT_LAW_SIGMA + p * M + k];
+      for (int k = 0; k < M; ++k) sg[p * M + k] = (T)ldc(L + DMT_LAW_SIGMA + p * M + k);
 #pragma unroll
-    for (int i = 0; i < HP; ++i) a[i] = (T)L[DMT_LAW_A + i];
+    for (int i = 0; i < HP; ++i) a[i] = (T)ldc(L + DMT_LAW_A + i);
 #pragma unroll
-    for (int i = 0; i < D * D; ++i) Bt[i] = (T)L[DMT_LAW_BT + i];
+    for (int i = 0; i < D * D; ++i) Bt[i] = (T)ldc(L + DMT_LAW_BT + i);
 #pragma unroll
-    for (int i = 0; i < D; ++i) beta[i] = (T)L[DMT_LAW_BETA + i];
+    for (int i = 0; i < D; ++i) beta[i] = (T)ldc(L + DMT_LAW_BETA + i);
 #pragma unroll
-    for (int i = 0; i < HP; ++i) da[i] = (T)L[DMT_LAW_DA + i];
-    trace = L[DMT_LAW_TRACE] != 0.0;
+    for (int i = 0; i < HP; ++i) da[i] = (T)ldc(L + DMT_LAW_DA + i);
+    trace = ldc(L + DMT_LAW_TRACE) != 0.0;
     if (Mdl::kLinear) {
 #pragma unroll
       for (int p = 0; p < D; ++p) {
@@ -200,6 +208,53 @@ __device__ __forceinline__ void euler_step(const T* Mg, const T* cg, const T* b,
   }
 #pragma unroll
   for (int p = 0; p < D; ++p) x[p] = xn[p];
+}
+
+// ---------------------------------------------------------------- affine form (linear drift)
+// With a linear drift the guided Euler step is affine in x:
+//   x' = A x + e,   A_ab = fma(-M_ab, dt, δ_ab),   e_a = fma(c_a, dt, sdW_a).
+template <int D, class T>
+__device__ __forceinline__ void affine_step(const T* Mg, const T* cg, T dt, const T* sdW, T* A,
+                                            T* e) {
+#pragma unroll
+  for (int p = 0; p < D; ++p) {
+#pragma unroll
+    for (int q = 0; q < D; ++q) A[p * D + q] = dfma(-Mg[p * D + q], dt, p == q ? (T)1 : (T)0);
+    e[p] = dfma(cg[p], dt, sdW[p]);
+  }
+}
+
+// (A2, e2) ∘ (A1, e1): apply map 1, then map 2.  A = A2·A1, e = A2·e1 + e2, canonical order:
+//   A_ab = A2_a0·A1_0b ; fma(A2_ac, A1_cb, ·) for c = 1..D-1 ;  e_a = e2_a ; fma(A2_ac, e1_c, ·)
+template <int D, class T>
+__device__ __forceinline__ void affine_compose(const T* A2, const T* e2, const T* A1, const T* e1,
+                                               T* A, T* e) {
+#pragma unroll
+  for (int p = 0; p < D; ++p) {
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+      T v = A2[p * D + 0] * A1[0 * D + q];
+#pragma unroll
+      for (int c = 1; c < D; ++c) v = dfma(A2[p * D + c], A1[c * D + q], v);
+      A[p * D + q] = v;
+    }
+    T u = e2[p];
+#pragma unroll
+    for (int c = 0; c < D; ++c) u = dfma(A2[p * D + c], e1[c], u);
+    e[p] = u;
+  }
+}
+
+// y = A x + e:  y_a = e_a ; fma(A_ac, x_c, ·) for c = 0..D-1
+template <int D, class T>
+__device__ __forceinline__ void affine_apply(const T* A, const T* e, const T* x, T* y) {
+#pragma unroll
+  for (int p = 0; p < D; ++p) {
+    T u = e[p];
+#pragma unroll
+    for (int c = 0; c < D; ++c) u = dfma(A[p * D + c], x[c], u);
+    y[p] = u;
+  }
 }
 
 // loglikhd_obs = -c0 - 1/2 x'H x + F'x

@@ -31,8 +31,22 @@ enum Mapping : int { MAP_AUTO = 0, MAP_LANE = 1, MAP_WAVE = 2 };
 // touch 64 consecutive elements per component — one coalesced 512 B (fp64) access.
 // tw = 1 (MAP_WAVE): recording-major, point-major, components interleaved (the reference's
 // own Vector{SVector{d}} layout) — a wave's 64 lanes touch 64 consecutive points.
+// Per-block record of a layout, precomputed on the host (one scalar load per block).
+struct BlkInfo {
+  int64_t tq;      // first point row of the block's recording tile
+  int32_t g0, g1;  // global first / last segment
+  int32_t ktot;    // chunks of 64 steps over the block's segments
+  int32_t term;    // terminal block (BiBlock{true})
+  int32_t np0;     // points of the first segment
+  int32_t q0;      // seg_q of the first segment
+  int32_t kfirst;  // chunks of the first segment
+  int32_t pad_;
+  double rho, srho;
+};
+
 template <class T>
 struct BlockArgs {
+  const BlkInfo* binfo;  // [nblocks] of the layout
   int64_t R;
   const int64_t* tile_qoff;  // [ntiles + 1]
   const int32_t* seg_q;      // [G] first point of the segment within its recording

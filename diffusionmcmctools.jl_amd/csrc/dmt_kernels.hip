@@ -356,7 +356,7 @@ struct ChunkIt {  // (segment, first step) iterator over a block's chunks of 64 
   int g, c0, nst;
   __device__ __forceinline__ void next(const int32_t* seg_np) {
     c0 += 64;
-    if (c0 >= nst) { ++g; c0 = 0; nst = seg_np[g] - 1; }
+    if (c0 >= nst) { ++g; c0 = 0; nst = ldc(seg_np + g) - 1; }
   }
 };
 
@@ -605,6 +605,324 @@ __global__ __launch_bounds__(128) void k_block_wave(const BlockArgs<T> a) {
   finish(ktot - 1);
   __syncthreads();
   if (lane == 0) {
+    a.ll_out[blk] = ok ? (double)ll : -INFINITY;
+    if (a.success) a.success[blk] = ok ? 1 : 0;
+  }
+}
+
+// ---- linear-drift block kernel: parallel-in-time Euler recursion.
+// With a linear drift (OU) every guided Euler step is an affine map x ↦ A_i x + e_i whose
+// coefficients do not depend on x, so a chunk of 64 steps is one Kogge–Stone prefix scan of
+// affine maps across the 64 lanes of a wave.  A workgroup of kScanWaves waves owns one block;
+// wave w takes chunk k = round·kScanWaves + w and, lane-parallel, draws its normals
+// (Philox/Box–Muller), forms the pCN increments, σ·dW°, the guiding coefficients and the
+// step maps, and scans them.  The only serial work left is one affine application per chunk
+// (the carry of the chunk start points), done by one thread between two barriers.  Then every
+// lane evaluates its point, the Girsanov terms and the 64-lane tree sum, and stores.
+#ifndef DMT_SCAN_MINW
+#define DMT_SCAN_MINW 1
+#endif
+#ifndef DMT_SCAN_WAVES
+#define DMT_SCAN_WAVES 8
+#endif
+constexpr int kScanWaves = DMT_SCAN_WAVES;
+
+template <class T>
+__device__ __forceinline__ T shfl_up_T(T v, int o) { return __shfl_up(v, (unsigned)o, 64); }
+
+// Store one point's N components (16-byte stores when N is even and T is double).
+template <int N, class T>
+__device__ __forceinline__ void store_row(T* p, const T* v) {
+  if constexpr (std::is_same<T, double>::value && N % 2 == 0) {
+#pragma unroll
+    for (int c = 0; c < N; c += 2) *reinterpret_cast<double2*>(p + c) = make_double2(v[c], v[c + 1]);
+  } else {
+#pragma unroll
+    for (int c = 0; c < N; ++c) p[c] = v[c];
+  }
+}
+
+template <class Mdl, class T, int MODE>
+__global__ __launch_bounds__(64 * kScanWaves, DMT_SCAN_MINW) void k_block_scan(const BlockArgs<T> a) {
+  constexpr int D = Mdl::D, M = Mdl::M, HP = D * (D + 1) / 2, NA = D * D + D;
+  static_assert(Mdl::kLinear, "k_block_scan needs a linear drift");
+  __shared__ T s_tot[kScanWaves][NA];     // chunk maps (Φ, ψ)
+  __shared__ T s_xs[kScanWaves + 1][D];   // chunk start points; [w+1] = end of chunk w
+  __shared__ T s_csum[kScanWaves];        // chunk sums of G·dt
+  __shared__ int s_segend[kScanWaves];
+  __shared__ int s_allow, s_done;
+  // the wave index is wave-uniform: keep it (and everything derived from it) scalar
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t blk = a.b0 + (int64_t)blockIdx.x;
+  if (blk >= a.b1) return;
+#ifdef DMT_STAMPS  // timing diagnostics (variant builds only): s_memtime per phase
+  uint64_t st[12];
+  int nst_ = 0;
+#define STAMP() (st[nst_++] = __builtin_amdgcn_s_memtime())
+  STAMP();
+#else
+#define STAMP() ((void)0)
+#endif
+  const BlkInfo* bi = a.binfo + blk;
+  const int64_t tq = ldc(&bi->tq);
+  const int g0 = ldc(&bi->g0), g1 = ldc(&bi->g1), ktot = ldc(&bi->ktot);
+  const int kfirst = ldc(&bi->kfirst), bq0 = ldc(&bi->q0);
+  const bool term = ldc(&bi->term) != 0;
+  const T rho = (MODE == MODE_FRESH) ? (T)0 : (T)ldc(&bi->rho);
+  const T srho = (MODE == MODE_FRESH) ? (T)1 : (T)ldc(&bi->srho);
+  // law slot / kind of segment g (uniform)
+  auto law_sel = [&](int g, int& kind) -> int {
+    kind = __builtin_amdgcn_readfirstlane((!term && g == g1) ? 1 : 0);
+    return __builtin_amdgcn_readfirstlane((kind ? ldc(a.selPPB + g) : ldc(a.selPP + g)) ^ a.law_flip);
+  };
+  // thread 0 keeps the block's running state; its start-point loads are issued here and
+  // consumed only after the first prepare phase
+  T ll = (T)0, seg_acc = (T)0;
+  bool ok = true;
+  T x0[D], H0[HP], F0[D], c00 = (T)0;
+  if (threadIdx.x == 0) {
+    const T* Xs = a.X[ldc(a.selX + g0) ^ a.xs_flip];
+    const int64_t q = bq0;
+    const int lsp = ldc(a.selPP + g0) ^ a.law_flip;
+#pragma unroll
+    for (int p = 0; p < D; ++p) x0[p] = Xs[(tq + q) * D + p];
+#pragma unroll
+    for (int c = 0; c < HP; ++c)
+      H0[c] = a.H_shared[lsp][0] ? a.H[lsp][0][q * HP + c] : a.H[lsp][0][(tq + q) * HP + c];
+#pragma unroll
+    for (int c = 0; c < D; ++c) F0[c] = a.F[lsp][0][(tq + q) * D + c];
+    c00 = (T)a.law[lsp][0][(int64_t)g0 * DMT_LAW_STRIDE + DMT_LAW_C0];
+    s_done = 0;
+  }
+  // this wave's chunk iterator: chunk w of the block
+  ChunkIt it{g0, 0, ldc(&bi->np0) - 1};
+  for (int j = 0; j < w && j + 1 < ktot; ++j) it.next(a.seg_np);
+  const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32), c3 = a.salt << 1;
+
+  for (int kb = 0; kb < ktot; kb += kScanWaves) {
+    const int k = kb + w;
+    const bool act = k < ktot;
+    const int nact = min(kScanWaves, ktot - kb);
+    const int g = __builtin_amdgcn_readfirstlane(it.g);
+    const int c0 = __builtin_amdgcn_readfirstlane(it.c0);
+    const int nst = __builtin_amdgcn_readfirstlane(it.nst);
+    const int cnt = act ? min(64, nst - c0) : 0;
+    const bool valid = lane < cnt;
+    const int i = c0 + (valid ? lane : max(cnt - 1, 0));
+    int kind = 0;
+    const int ls = act ? law_sel(g, kind) : 0;
+    const int64_t q0 = !act ? 0 : (g == g0 ? (int64_t)bq0 : (int64_t)ldc(a.seg_q + g));
+    const int64_t row = tq + q0;
+    const T* tb = a.t_shared ? a.t + q0 : a.t + row;
+    const T* Hb = a.H_shared[ls][kind] ? a.H[ls][kind] + q0 * HP : a.H[ls][kind] + row * HP;
+    const T* Fb = a.F[ls][kind] + row * D;
+    const double* lawp = a.law[ls][kind] + (int64_t)g * DMT_LAW_STRIDE;
+    // chunks of the block's first segment store right after their sums (no earlier segment
+    // can have failed); later ones wait for the in-order success test
+    const bool early = k < kfirst;
+    const bool need_b4 = (kb + nact > kfirst) || (kb + nact < ktot);
+    T* const Xdb = a.X[ldc(a.selX + g) ^ a.xd_flip] + row * D;
+    T* const Wdb = a.W[ldc(a.selW + g) ^ a.wd_flip] + row * M;
+    T A[D * D], e[D], dW[M], w0v[M];
+    STAMP();
+    if (act) {  // ---- prepare (lane-parallel): normals, pCN, σ·dW°, step maps; then the scan
+      const T* Wsb = a.W[ldc(a.selW + g) ^ a.ws_flip] + row * M;
+      if (MODE != MODE_RECOMPUTE && c0 == 0) {
+#pragma unroll
+        for (int kk = 0; kk < M; ++kk) w0v[kk] = rho * ((MODE == MODE_FRESH) ? (T)0 : Wsb[kk]);
+      }
+      const T dt = tb[i + 1] - tb[i];
+      Law<Mdl, T> LA;
+      LA.load(lawp);
+#ifdef DMT_STAMPS
+      if (dt == (T)-12345) a.ll_out[0] = LA.sg[0];  // forces the loads to land before the stamp
+#endif
+      STAMP();
+      if (MODE == MODE_RECOMPUTE) {
+#pragma unroll
+        for (int kk = 0; kk < M; ++kk) dW[kk] = Wsb[(int64_t)(i + 1) * M + kk];
+      } else {
+        const double* Zg = a.Z ? a.Z + ldc(a.st_off + g) * M : nullptr;
+        uint32_t have = 0xFFFFFFFFu;
+        T z0 = (T)0, z1 = (T)0;
+        const T sdt = sqrt(dt);
+#pragma unroll
+        for (int kk = 0; kk < M; ++kk) {
+          const uint32_t n = (uint32_t)(i * M + kk);
+          T z;
+          if (Zg) {
+            z = (T)Zg[(int64_t)i * M + kk];
+          } else {
+            if ((n >> 1) != have) {
+              U4 o = philox4x32_10(U4{n >> 1, (uint32_t)g + a.seg_base, a.iter, c3}, k0, k1);
+              normal_pair(o, z0, z1);
+              have = n >> 1;
+            }
+            z = (n & 1u) ? z1 : z0;
+          }
+          const T wv = (MODE == MODE_FRESH) ? (T)0 : Wsb[(int64_t)(i + 1) * M + kk];
+          dW[kk] = dfma(rho, wv, srho * (sdt * z));
+        }
+      }
+      T Hi[HP], Fi[D], sdW[D], Mg[D * D], cg[D];
+#pragma unroll
+      for (int c = 0; c < HP; ++c) Hi[c] = Hb[(int64_t)i * HP + c];
+#pragma unroll
+      for (int c = 0; c < D; ++c) Fi[c] = Fb[(int64_t)i * D + c];
+      sigma_dw<Mdl, T>(LA, dW, sdW);
+      guide_coeffs<Mdl, T>(LA, Hi, Fi, Mg, cg);
+      affine_step<D, T>(Mg, cg, dt, sdW, A, e);
+      STAMP();
+      if (!valid) {  // identity beyond the chunk's last step
+#pragma unroll
+        for (int p = 0; p < D; ++p) {
+#pragma unroll
+          for (int q = 0; q < D; ++q) A[p * D + q] = p == q ? (T)1 : (T)0;
+          e[p] = (T)0;
+        }
+      }
+      // inclusive Kogge–Stone scan over the lanes: lane j ← map_j ∘ … ∘ map_0
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        T Ap[D * D], ep[D], An[D * D], en[D];
+#pragma unroll
+        for (int c = 0; c < D * D; ++c) Ap[c] = shfl_up_T(A[c], o);
+#pragma unroll
+        for (int c = 0; c < D; ++c) ep[c] = shfl_up_T(e[c], o);
+        affine_compose<D, T>(A, e, Ap, ep, An, en);
+        const bool take = lane >= o;
+#pragma unroll
+        for (int c = 0; c < D * D; ++c) A[c] = take ? An[c] : A[c];
+#pragma unroll
+        for (int c = 0; c < D; ++c) e[c] = take ? en[c] : e[c];
+      }
+      if (lane == cnt - 1) {
+#pragma unroll
+        for (int c = 0; c < D * D; ++c) s_tot[w][c] = A[c];
+#pragma unroll
+        for (int c = 0; c < D; ++c) s_tot[w][D * D + c] = e[c];
+      }
+      if (lane == 0) s_segend[w] = (c0 + 64 >= nst) ? 1 : 0;
+    }
+    if (threadIdx.x == 0 && kb == 0) {  // block start point and loglikhd_obs
+#pragma unroll
+      for (int p = 0; p < D; ++p) s_xs[0][p] = x0[p];
+      ll = obs_term<D, T>(H0, F0, x0, c00);
+    }
+    STAMP();
+    __syncthreads();
+    STAMP();
+    // the guiding-table values of the step, re-read (L2) while thread 0 runs the carry
+    T Hi[HP], Fi[D], dt = (T)0;
+    if (act) {
+      dt = tb[i + 1] - tb[i];
+#pragma unroll
+      for (int c = 0; c < HP; ++c) Hi[c] = Hb[(int64_t)i * HP + c];
+#pragma unroll
+      for (int c = 0; c < D; ++c) Fi[c] = Fb[(int64_t)i * D + c];
+    }
+    if (threadIdx.x == 0) {  // ---- carry: chunk start points, in order
+      T xc[D];
+#pragma unroll
+      for (int p = 0; p < D; ++p) xc[p] = s_xs[0][p];
+#pragma unroll
+      for (int ww = 0; ww < kScanWaves; ++ww) {
+        if (ww < nact) {
+          T tA[D * D], te[D], xn[D];
+#pragma unroll
+          for (int c = 0; c < D * D; ++c) tA[c] = s_tot[ww][c];
+#pragma unroll
+          for (int c = 0; c < D; ++c) te[c] = s_tot[ww][D * D + c];
+          affine_apply<D, T>(tA, te, xc, xn);
+#pragma unroll
+          for (int p = 0; p < D; ++p) {
+            xc[p] = xn[p];
+            s_xs[ww + 1][p] = xn[p];
+          }
+        }
+      }
+    }
+    __syncthreads();
+    STAMP();
+    T xpost[D], xpre[D];
+    if (act) {  // ---- points, Girsanov terms, chunk sum
+      T xs[D];
+#pragma unroll
+      for (int p = 0; p < D; ++p) xs[p] = s_xs[w][p];
+      affine_apply<D, T>(A, e, xs, xpost);
+#pragma unroll
+      for (int p = 0; p < D; ++p) {
+        const T up = shfl_up_T(xpost[p], 1);
+        xpre[p] = lane == 0 ? xs[p] : up;
+      }
+      Law<Mdl, T> LB;
+      LB.load(lawp);
+      T rr[D], bb[D];
+      const T G = g_at<Mdl, T>(LB, Hi, Fi, xpre, rr, bb);
+      const T csum = wave_tree_sum<T>(valid ? G * dt : (T)0);
+      if (lane == 0) s_csum[w] = csum;
+    }
+    auto store_chunk = [&]() {  // coalesced: 64 consecutive points per wave
+      if (valid) {
+        store_row<D, T>(Xdb + (int64_t)i * D, xpre);
+        if (MODE != MODE_RECOMPUTE) store_row<M, T>(Wdb + (int64_t)(i + 1) * M, dW);
+      }
+      if (MODE != MODE_RECOMPUTE && c0 == 0 && lane == 0) store_row<M, T>(Wdb, w0v);
+      if (c0 + 64 >= nst && lane == cnt - 1) store_row<D, T>(Xdb + (int64_t)nst * D, xpost);
+    };
+    if (act && early) store_chunk();
+    STAMP();
+    __syncthreads();
+    STAMP();
+    if (threadIdx.x == 0) {  // ---- segment sums and success, in chunk order
+      T cs[kScanWaves];
+      int se[kScanWaves];
+#pragma unroll
+      for (int ww = 0; ww < kScanWaves; ++ww) {
+        cs[ww] = ww < nact ? s_csum[ww] : (T)0;
+        se[ww] = ww < nact ? s_segend[ww] : 0;
+      }
+      int allow = nact;
+#pragma unroll
+      for (int ww = 0; ww < kScanWaves; ++ww) {
+        if (ww < nact && allow == nact) {
+          seg_acc = seg_acc + (cs[ww] + (T)0);
+          if (se[ww]) {
+            bool sok = isfinite(seg_acc);
+#pragma unroll
+            for (int p = 0; p < D; ++p) sok = sok && isfinite(s_xs[ww + 1][p]);
+            if (sok) {
+              ll = ll + seg_acc;
+            } else {
+              ok = false;
+              allow = ww + 1;
+            }
+            seg_acc = (T)0;
+          }
+        }
+      }
+      s_allow = allow;
+      if (!ok) s_done = 1;
+#pragma unroll
+      for (int p = 0; p < D; ++p) s_xs[0][p] = s_xs[nact][p];
+    }
+    if (!need_b4) break;  // last round, every chunk already stored
+    __syncthreads();
+    STAMP();
+    if (act && !early && w < s_allow) store_chunk();
+    if (__builtin_amdgcn_readfirstlane(s_done)) break;  // uniform exit keeps `it` scalar
+    for (int j = 0; j < kScanWaves && k + j + 1 < ktot; ++j) it.next(a.seg_np);
+  }
+  STAMP();
+#ifdef DMT_STAMPS
+  if (lane == 0 && a.iter == 7 && (blockIdx.x < 2 || blockIdx.x == gridDim.x - 1 || blockIdx.x == 500)) {
+    printf("STAMP blk %d w %d n %d : %lu %lu %lu %lu %lu %lu %lu %lu %lu %lu %lu\n", (int)blockIdx.x, w, nst_,
+           st[1] - st[0], st[2] - st[0], st[3] - st[0], st[4] - st[0], st[5] - st[0], st[6] - st[0],
+           st[7] - st[0], st[8] - st[0], st[9] - st[0], st[10] - st[0], st[nst_ - 1] - st[0]);
+  }
+#endif
+#undef STAMP
+  if (threadIdx.x == 0) {
     a.ll_out[blk] = ok ? (double)ll : -INFINITY;
     if (a.success) a.success[blk] = ok ? 1 : 0;
   }
@@ -939,15 +1257,6 @@ __global__ void k_debug_philox(uint64_t seed, const uint32_t* ctr, int64_t n, ui
 // ---------------------------------------------------------------- launchers
 static inline unsigned nblk(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
 
-// DMT_DIAG: timing-diagnostic kernel variants (see k_block_wave); 0 in production.
-static int diag_flags() {
-  static int v = [] {
-    const char* e = getenv("DMT_DIAG");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
-
 constexpr int kChunk = 4;
 
 template <class Mdl, class T>
@@ -955,52 +1264,52 @@ static hipError_t launch_block_t(int mapping, int mode, const void* args, int64_
                                  hipStream_t s) {
   const BlockArgs<T>& a = *static_cast<const BlockArgs<T>*>(args);
   if (nwaves <= 0) return hipSuccess;
-  dim3 grid((unsigned)nwaves), block(64);
-  if (mapping == MAP_WAVE) {
-    const dim3 wblock(128);
-    if (diag_flags() != 0 && mode == MODE_PCN) {
-      if constexpr (std::is_same<Mdl, OU<double, 2, 2>>::value) {
-        switch (diag_flags()) {
-          case 1: k_block_wave<Mdl, T, MODE_PCN, 1><<<grid, wblock, 0, s>>>(a); break;
-          case 2: k_block_wave<Mdl, T, MODE_PCN, 2><<<grid, wblock, 0, s>>>(a); break;
-          case 4: k_block_wave<Mdl, T, MODE_PCN, 4><<<grid, wblock, 0, s>>>(a); break;
-          case 6: k_block_wave<Mdl, T, MODE_PCN, 6><<<grid, wblock, 0, s>>>(a); break;
-          default: k_block_wave<Mdl, T, MODE_PCN, 0><<<grid, wblock, 0, s>>>(a); break;
-        }
-        return hipGetLastError();
-      }
-    }
+  const dim3 grid((unsigned)nwaves);
+  if constexpr (Mdl::kLinear) {  // one workgroup per block, always
+    const dim3 sblock(64 * kScanWaves);
     switch (mode) {
-      case MODE_PCN: k_block_wave<Mdl, T, MODE_PCN><<<grid, wblock, 0, s>>>(a); break;
-      case MODE_RECOMPUTE: k_block_wave<Mdl, T, MODE_RECOMPUTE><<<grid, wblock, 0, s>>>(a); break;
-      case MODE_FRESH: k_block_wave<Mdl, T, MODE_FRESH><<<grid, wblock, 0, s>>>(a); break;
+      case MODE_PCN: k_block_scan<Mdl, T, MODE_PCN><<<grid, sblock, 0, s>>>(a); break;
+      case MODE_RECOMPUTE: k_block_scan<Mdl, T, MODE_RECOMPUTE><<<grid, sblock, 0, s>>>(a); break;
+      case MODE_FRESH: k_block_scan<Mdl, T, MODE_FRESH><<<grid, sblock, 0, s>>>(a); break;
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  } else {
+    if (mapping == MAP_WAVE) {
+      const dim3 wblock(128);
+      switch (mode) {
+        case MODE_PCN: k_block_wave<Mdl, T, MODE_PCN><<<grid, wblock, 0, s>>>(a); break;
+        case MODE_RECOMPUTE: k_block_wave<Mdl, T, MODE_RECOMPUTE><<<grid, wblock, 0, s>>>(a); break;
+        case MODE_FRESH: k_block_wave<Mdl, T, MODE_FRESH><<<grid, wblock, 0, s>>>(a); break;
+        default: return hipErrorInvalidValue;
+      }
+      return hipGetLastError();
+    }
+    const dim3 block(64);
+    const bool par = a.Z != nullptr;
+    switch (mode) {
+      case MODE_PCN:
+        if (par) k_block<Mdl, T, MODE_PCN, true, kChunk><<<grid, block, 0, s>>>(a);
+        else k_block<Mdl, T, MODE_PCN, false, kChunk><<<grid, block, 0, s>>>(a);
+        break;
+      case MODE_RECOMPUTE: k_block<Mdl, T, MODE_RECOMPUTE, false, kChunk><<<grid, block, 0, s>>>(a); break;
+      case MODE_FRESH:
+        if (par) k_block<Mdl, T, MODE_FRESH, true, kChunk><<<grid, block, 0, s>>>(a);
+        else k_block<Mdl, T, MODE_FRESH, false, kChunk><<<grid, block, 0, s>>>(a);
+        break;
       default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
   }
-  const bool par = a.Z != nullptr;
-  switch (mode) {
-    case MODE_PCN:
-      if (par) k_block<Mdl, T, MODE_PCN, true, kChunk><<<grid, block, 0, s>>>(a);
-      else k_block<Mdl, T, MODE_PCN, false, kChunk><<<grid, block, 0, s>>>(a);
-      break;
-    case MODE_RECOMPUTE: k_block<Mdl, T, MODE_RECOMPUTE, false, kChunk><<<grid, block, 0, s>>>(a); break;
-    case MODE_FRESH:
-      if (par) k_block<Mdl, T, MODE_FRESH, true, kChunk><<<grid, block, 0, s>>>(a);
-      else k_block<Mdl, T, MODE_FRESH, false, kChunk><<<grid, block, 0, s>>>(a);
-      break;
-    default: return hipErrorInvalidValue;
-  }
-  return hipGetLastError();
 }
 
 template <class Mdl, class T>
 static hipError_t launch_pathll_t(int mapping, const void* args, int64_t nwaves, hipStream_t s) {
   const BlockArgs<T>& a = *static_cast<const BlockArgs<T>*>(args);
   if (nwaves <= 0) return hipSuccess;
-  if (mapping == MAP_WAVE)
+  if (Mdl::kLinear || mapping == MAP_WAVE)
     k_pathll_wave<Mdl, T><<<dim3((unsigned)nwaves), dim3(64), 0, s>>>(a);
-  else
+  else if constexpr (!Mdl::kLinear)
     k_pathll<Mdl, T, kChunk><<<dim3((unsigned)nwaves), dim3(64), 0, s>>>(a);
   return hipGetLastError();
 }

@@ -54,6 +54,7 @@ struct Layout {
   std::vector<int32_t> gfirst, glast, blk_rec;
   std::vector<uint8_t> term;
   int64_t* d_blk_off = nullptr;
+  BlkInfo* d_binfo = nullptr;
   int32_t* d_blk_rec = nullptr;
   int32_t* d_gfirst = nullptr;
   int32_t* d_glast = nullptr;
@@ -68,7 +69,7 @@ struct Layout {
   uint8_t* d_success = nullptr;
   uint8_t* d_acc = nullptr;
   void release() {
-    void* ps[] = {d_blk_off, d_blk_rec, d_gfirst, d_glast, d_term, d_rho, d_srho, d_ll,
+    void* ps[] = {d_blk_off, d_binfo, d_blk_rec, d_gfirst, d_glast, d_term, d_rho, d_srho, d_ll,
                   d_llp,     d_llh,    d_llph,  d_acch, d_success, d_acc};
     for (void* p : ps)
       if (p) (void)hipFree(p);
@@ -120,9 +121,12 @@ struct dmt_ens {
   int64_t red_work_n = 0;
   double* h_red = nullptr;  // pinned host copy of the 3 reduction results
   double* d_gather = nullptr;
+  double* d_run = nullptr;         // dmt_mcmc_run: [n][3] per-iteration reductions
+  double* d_run_gather = nullptr;  // [n][nranks][3]
+  int64_t run_cap = 0;
   std::vector<std::unique_ptr<Layout>> layouts;  // layouts[0] = internal "unit" layout
   // timing
-  bool timing = false;
+  uint32_t timing = 0;  // bit k: time kernel class k (dmt_set_timing)
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending[DMT_K_COUNT];
   double t_ms[DMT_K_COUNT] = {0, 0, 0, 0, 0};
   int64_t t_cnt[DMT_K_COUNT] = {0, 0, 0, 0, 0};
@@ -186,13 +190,13 @@ struct TimedScope {
   int k;
   hipEvent_t e0 = nullptr;
   TimedScope(dmt_ens* h_, int k_) : h(h_), k(k_) {
-    if (h->timing) {
+    if (h->timing >> k & 1u) {
       e0 = get_event(h);
       (void)hipEventRecord(e0, h->stream);
     }
   }
   ~TimedScope() {
-    if (h->timing) {
+    if (e0) {
       hipEvent_t e1 = get_event(h);
       (void)hipEventRecord(e1, h->stream);
       h->pending[k].push_back({e0, e1});
@@ -293,6 +297,7 @@ void fill_common(dmt_ens* h, const Layout* L, BlockArgs<T>& a) {
   a.t_shared = h->grid_shared;
   a.blk_off = L->d_blk_off;
   a.blk_rec = L->d_blk_rec;
+  a.binfo = L->d_binfo;
   a.gfirst = L->d_gfirst;
   a.glast = L->d_glast;
   a.term = L->d_term;
@@ -396,6 +401,7 @@ dmt_status build_layout(dmt_ens* h, const int32_t* n_blocks, const int32_t* seg_
   DMT_TRY(ens_alloc(h, &L->d_blk_off, h->R + 1));
   DMT_TRY(ens_alloc(h, &L->d_gfirst, nb));
   DMT_TRY(ens_alloc(h, &L->d_blk_rec, nb));
+  DMT_TRY(ens_alloc_bytes(h, (void**)&L->d_binfo, std::max<int64_t>(nb, 1) * (int64_t)sizeof(BlkInfo)));
   DMT_TRY(ens_alloc(h, &L->d_glast, nb));
   DMT_TRY(ens_alloc(h, &L->d_term, nb));
   DMT_TRY(ens_alloc(h, &L->d_rho, nb));
@@ -416,6 +422,24 @@ dmt_status build_layout(dmt_ens* h, const int32_t* n_blocks, const int32_t* seg_
   if (nb > 0) {
     HIP_OK(hipMemcpy(L->d_gfirst, L->gfirst.data(), nb * 4, hipMemcpyHostToDevice));
     HIP_OK(hipMemcpy(L->d_blk_rec, L->blk_rec.data(), nb * 4, hipMemcpyHostToDevice));
+    std::vector<BlkInfo> bi(nb);
+    for (int64_t b = 0; b < nb; ++b) {
+      const int64_t r = L->blk_rec[b];
+      bi[b].tq = h->tile_qoff[r / h->tw];
+      bi[b].g0 = L->gfirst[b];
+      bi[b].g1 = L->glast[b];
+      int32_t kt = 0;
+      for (int32_t g = L->gfirst[b]; g <= L->glast[b]; ++g) kt += (h->seg_np[g] - 1 + 63) / 64;
+      bi[b].ktot = kt;
+      bi[b].term = L->term[b];
+      bi[b].np0 = h->seg_np[L->gfirst[b]];
+      bi[b].q0 = h->seg_q[L->gfirst[b]];
+      bi[b].kfirst = (bi[b].np0 - 1 + 63) / 64;
+      bi[b].pad_ = 0;
+      bi[b].rho = rr[b];
+      bi[b].srho = srho[b];
+    }
+    HIP_OK(hipMemcpy(L->d_binfo, bi.data(), nb * sizeof(BlkInfo), hipMemcpyHostToDevice));
     HIP_OK(hipMemcpy(L->d_glast, L->glast.data(), nb * 4, hipMemcpyHostToDevice));
     HIP_OK(hipMemcpy(L->d_term, L->term.data(), nb, hipMemcpyHostToDevice));
     HIP_OK(hipMemcpy(L->d_rho, rr.data(), nb * 8, hipMemcpyHostToDevice));
@@ -615,6 +639,8 @@ dmt_status dmt_create(dmt_ens** out, const dmt_model* model, const dmt_structure
   if (cfg->mapping == MAP_LANE || cfg->mapping == MAP_WAVE) h->mapping = cfg->mapping;
   else if (cfg->mapping == MAP_AUTO) h->mapping = h->R <= kAutoWaveMaxRecordings ? MAP_WAVE : MAP_LANE;
   else return fail(DMT_ERR_INVALID, "bad mapping");
+  // linear drift (OU): the recursion is an affine scan, always one workgroup per block
+  if (model->model == DMT_MODEL_OU) h->mapping = MAP_WAVE;
   h->tw = h->mapping == MAP_WAVE ? 1 : kLanes;
   h->ntiles = (h->R + h->tw - 1) / h->tw;
   h->tile_qoff.assign(h->ntiles + 1, 0);
@@ -678,7 +704,7 @@ dmt_status dmt_destroy(dmt_ens* h) {
   void* ps[] = {h->d_pt_off, h->d_st_off, h->d_tile_qoff, h->d_seg_rec, h->d_seg_q, h->d_seg_np,
                 h->d_sel[0], h->d_sel[1], h->d_sel[2], h->d_sel[3], h->d_X[0], h->d_X[1],
                 h->d_W[0], h->d_W[1], h->d_t, h->d_stage, h->d_Z, h->d_red, h->d_gather,
-                h->d_red_work};
+                h->d_red_work, h->d_run, h->d_run_gather};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   for (int s = 0; s < 2; ++s)
@@ -1006,6 +1032,75 @@ dmt_status dmt_mcmc_step(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int
   return DMT_OK;
 }
 
+dmt_status dmt_mcmc_run(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int64_t iter0,
+                        int64_t n_iter, uint32_t salt, double* out) {
+  DMT_TRY(check_h(h));
+  Layout* L;
+  DMT_TRY(get_layout(h, layout, &L));
+  DMT_TRY(check_range(L, b0, b1));
+  DMT_TRY(law_ready(h, 0, L, b0, b1));
+  if (n_iter < 0 || iter0 < 1) return fail(DMT_ERR_INVALID, "bad iteration range");
+  if (n_iter == 0) return DMT_OK;
+  if (L->hist_len > 0 && iter0 + n_iter - 1 > L->hist_len)
+    return fail(DMT_ERR_INVALID, "iterations outside 1:ll_hist_len");
+  const bool multi = h->comm && h->nranks > 1;
+  if (n_iter > h->run_cap) {
+    if (h->d_run) { (void)hipFree(h->d_run); h->bytes -= h->run_cap * 24; h->d_run = nullptr; }
+    if (h->d_run_gather) {
+      (void)hipFree(h->d_run_gather);
+      h->bytes -= h->run_cap * 24 * h->nranks;
+      h->d_run_gather = nullptr;
+    }
+    h->run_cap = 0;
+    DMT_TRY(ens_alloc(h, &h->d_run, 3 * n_iter));
+    if (multi) DMT_TRY(ens_alloc(h, &h->d_run_gather, 3 * n_iter * h->nranks));
+    h->run_cap = n_iter;
+  } else if (multi && !h->d_run_gather) {
+    DMT_TRY(ens_alloc(h, &h->d_run_gather, 3 * h->run_cap * h->nranks));
+  }
+  DMT_TRY(ensure_red_work(h, b1 - b0));
+  // every iteration is stream-ordered: no host synchronisation until the end
+  for (int64_t i = 0; i < n_iter; ++i) {
+    const int64_t it = iter0 + i;
+    DMT_TRY(run_block_kernel(h, L, MODE_PCN, DMT_K_DRAW, b0, b1, 0, 0, 1, 0, 1, nullptr, it,
+                             salt, L->d_llp, nullptr, false));
+    {
+      TimedScope ts(h, DMT_K_ACCEPT);
+      HIP_OK(launch_accept_reduce(accept_args(h, L, b0, b1, nullptr, it, salt, nullptr),
+                                  h->d_red_work, h->d_run + 3 * i, h->stream));
+    }
+    if (multi &&
+        ncclAllGather(h->d_run + 3 * i, h->d_run_gather + 3 * h->nranks * i, 3, ncclDouble,
+                      h->comm, h->stream) != ncclSuccess)
+      return fail(DMT_ERR_COMM, "ncclAllGather failed");
+  }
+  if (!out) {
+    HIP_OK(hipStreamSynchronize(h->stream));
+    return DMT_OK;
+  }
+  if (!multi) {
+    HIP_OK(hipMemcpyAsync(out, h->d_run, 24 * n_iter, hipMemcpyDeviceToHost, h->stream));
+    HIP_OK(hipStreamSynchronize(h->stream));
+    return DMT_OK;
+  }
+  std::vector<double> all(3 * h->nranks * n_iter);
+  HIP_OK(hipMemcpyAsync(all.data(), h->d_run_gather, all.size() * 8, hipMemcpyDeviceToHost,
+                        h->stream));
+  HIP_OK(hipStreamSynchronize(h->stream));
+  int n2 = 1;
+  while (n2 < h->nranks) n2 <<= 1;
+  std::vector<double> lv(n2);
+  for (int64_t i = 0; i < n_iter; ++i)
+    for (int c = 0; c < 3; ++c) {  // the rank-order tree of finish_reduction
+      std::fill(lv.begin(), lv.end(), 0.0);
+      for (int r = 0; r < h->nranks; ++r) lv[r] = all[3 * h->nranks * i + 3 * r + c];
+      for (int w = n2; w > 1; w >>= 1)
+        for (int j = 0; j < w / 2; ++j) lv[j] = lv[2 * j] + lv[2 * j + 1];
+      out[3 * i + c] = lv[0] + 0.0;
+    }
+  return DMT_OK;
+}
+
 dmt_status dmt_accept_reject(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, const double* E,
                              int64_t mcmciter, uint32_t salt, uint8_t* acc_out) {
   DMT_TRY(check_h(h));
@@ -1302,7 +1397,7 @@ dmt_status dmt_set_timing(dmt_ens* h, int32_t on) {
   HIP_OK(hipStreamSynchronize(h->stream));
   drain_timing(h);
   for (int k = 0; k < DMT_K_COUNT; ++k) { h->t_ms[k] = 0; h->t_cnt[k] = 0; }
-  h->timing = on != 0;
+  h->timing = on < 0 ? 0xFFFFFFFFu : (uint32_t)on;
   return DMT_OK;
 }
 

@@ -199,12 +199,22 @@ class Ensemble:
                C.byref(b), C.byref(n))
         return a.value, b.value, n.value
 
+    def mcmc_run(self, layout, b0, b1, iter0, n_iter, salt=0):
+        """n_iter mcmc_step iterations without host synchronisation in between; returns
+        (n_iter, 3): fetch_ll, fetch_ll°, accepted count per iteration."""
+        out = np.empty((int(n_iter), 3), dtype=np.float64)
+        L.call("dmt_mcmc_run", self._h, layout, b0, b1, int(iter0), int(n_iter), int(salt),
+               L.f64p(out))
+        return out
+
     # ---------------------------------------------------------------- misc
     def sync(self):
         L.call("dmt_sync", self._h)
 
-    def set_timing(self, on=True):
-        L.call("dmt_set_timing", self._h, 1 if on else 0)
+    def set_timing(self, on=True, kernels=None):
+        """Event timing of kernel classes ``kernels`` (iterable of K_*; default all)."""
+        mask = 0 if not on else (-1 if kernels is None else sum(1 << k for k in kernels))
+        L.call("dmt_set_timing", self._h, int(mask))
 
     def get_timing(self, kernel):
         ms, n = C.c_double(), C.c_int64()

@@ -18,7 +18,7 @@ import DiffusionMCMCTools: draw_proposal_path!, accept_reject_proposal_path!, lo
     swap_WW!, swap_PP!, swap_ll!, ll_of_accepted, accpt_rate, recompute_path!
 
 export DeviceSamplingEnsemble, DeviceBlockEnsemble, DeviceBlockCollection, DeviceBiBlock,
-    mcmc_step!, download_XX, download_WW
+    mcmc_step!, mcmc_run!, download_XX, download_WW
 
 const libdmt = get(ENV, "DMT_LIB", joinpath(@__DIR__, "..", "libdmt.so"))
 
@@ -234,6 +234,15 @@ function mcmc_step!(x::DeviceBlocks, mcmciter; salt=0)
         (Ptr{Cvoid}, Int32, Int64, Int64, Int64, UInt32, Ref{Float64}, Ref{Float64}, Ref{Int64}),
         x.se.h, x.layout, x.b0, x.b1, mcmciter, salt, a, b, n))
     a[], b[], n[]
+end
+
+"n_iter iterations of mcmc_step! from iter0 on, no host round trips; (n_iter, 3) results."
+function mcmc_run!(x::DeviceBlocks, iter0, n_iter; salt=0)
+    out = Matrix{Float64}(undef, 3, n_iter)
+    check(ccall((:dmt_mcmc_run, libdmt), Int32,
+        (Ptr{Cvoid}, Int32, Int64, Int64, Int64, Int64, UInt32, Ptr{Float64}),
+        x.se.h, x.layout, x.b0, x.b1, iter0, n_iter, salt, out))
+    permutedims(out)
 end
 
 # ---- log-likelihoods (src/block.jl:138-152; biblock.jl:240,248; block_collection.jl:166-197)

@@ -52,9 +52,11 @@ enum {
 /* models (DiffusionDefinition.jl models used by the reference's tutorials and configs) */
 enum { DMT_MODEL_OU = 0, DMT_MODEL_FHN = 1, DMT_MODEL_LORENZ = 2 };
 enum { DMT_F64 = 0, DMT_F32 = 1 };
-/* thread mapping of the recursion kernels: AUTO picks WAVE (one wavefront per block, for
- * small ensembles, latency-bound) or LANE (one lane per block, for large ensembles,
- * bandwidth-bound); both give bit-identical results */
+/* thread mapping of the recursion kernels of non-linear models (FHN, Lorenz): AUTO picks
+ * WAVE (a 2-wave workgroup per block, for small ensembles, latency-bound) or LANE (one lane
+ * per block, for large ensembles, bandwidth-bound); both give bit-identical results.
+ * Linear-drift models (OU) ignore it: their recursion is a parallel affine scan, one
+ * workgroup per block. */
 enum { DMT_MAP_AUTO = 0, DMT_MAP_LANE = 1, DMT_MAP_WAVE = 2 };
 /* units of a SamplingPair: u (accepted) and u° (proposal), src/sampling_pair.jl:36-55 */
 enum { DMT_U = 0, DMT_UPROP = 1 };
@@ -228,6 +230,14 @@ dmt_status dmt_fetch_ll(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
 dmt_status dmt_mcmc_step(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int64_t mcmciter,
                          uint32_t salt, double* ll, double* ll_prop, int64_t* n_acc);
 
+/* n_iter consecutive dmt_mcmc_step iterations (mcmciter = iter0 … iter0+n_iter-1) queued
+ * back to back on the device with no host synchronisation in between: the body of the
+ * reference's sampling loop (docs/src/tutorials/biblock/smoothing.md:40-44, which pushes
+ * fetch_ll(be) every iteration).  out (nullable): double[n_iter][3] = (fetch_ll, fetch_ll°,
+ * accepted count) of every iteration, identical to what the single-step calls return. */
+dmt_status dmt_mcmc_run(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int64_t iter0,
+                        int64_t n_iter, uint32_t salt, double* out);
+
 /* ---------------- guiding term (host set-up, GP.build_guid_prop) ---------------- */
 
 /* Exact discrete backward filter for a linear auxiliary law dX = (B̃X + β̃)dt + σ̃dW on
@@ -251,7 +261,9 @@ dmt_status dmt_set_shard(dmt_ens* h, int64_t seg_base);
 
 /* ---------------- misc ---------------- */
 dmt_status dmt_sync(dmt_ens* h);
-dmt_status dmt_set_timing(dmt_ens* h, int32_t on);
+/* Kernel timing with HIP events on the handle's stream: bit k of `mask` times the kernels of
+ * class k (DMT_K_*); -1 = all, 0 = off.  Resets the accumulators. */
+dmt_status dmt_set_timing(dmt_ens* h, int32_t mask);
 /* accumulated device time (ms) and launch count of a kernel since timing was switched on */
 dmt_status dmt_get_timing(dmt_ens* h, int32_t kernel, double* ms, int64_t* count);
 /* bytes of device memory held by the handle */

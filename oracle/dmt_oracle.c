@@ -52,6 +52,11 @@
  *   sdW_a   = sigma_a0*dW_0 ; sdW_a = fma(sigma_ak, dW_k, sdW_a)  for k = 1..m-1
  *   x'_a    = fma(bg_a, dt, x_a + sdW_a)
  *
+ *   LINEAR DRIFT (OU): the step is affine, x' = A x + e with A_ab = fma(-M_ab, dt, δ_ab),
+ *   e_a = fma(c_a, dt, sdW_a), and the segment is evaluated as chunked Kogge–Stone prefix
+ *   scans of these maps (solve_segment_scan below) — this REPLACES the last line above
+ *   for OU models.  FHN / Lorenz use the step-by-step form.
+ *
  *   Log-weight summation: within a segment the g's are summed in chunks of 64
  *   consecutive steps by the adjacent-pair binary tree ((g0+g1)+(g2+g3))+…
  *   (a partial last chunk is padded with zeros), each chunk sum is
@@ -208,6 +213,102 @@ static inline void guide_coeffs(int model, int d, const REAL* th, const REAL* a,
     }
 }
 
+/* Affine form of a linear-drift step and its composition (CANONICAL ARITHMETIC, scan form):
+ *   A_ab = fma(-M_ab, dt, δ_ab), e_a = fma(c_a, dt, sdW_a)            x' = A x + e
+ *   (A2,e2)∘(A1,e1): A_ab = A2_a0*A1_0b ; fma(A2_ac, A1_cb, .) c=1..d-1
+ *                    e_a  = e2_a ; fma(A2_ac, e1_c, .) c=0..d-1
+ *   apply:           y_a  = e_a ; fma(A_ac, x_c, .) c=0..d-1 */
+static void aff_compose(int d, const REAL* A2, const REAL* e2, const REAL* A1, const REAL* e1,
+                        REAL* A, REAL* e) {
+    for (int p = 0; p < d; ++p) {
+        for (int q = 0; q < d; ++q) {
+            REAL v = A2[p * d + 0] * A1[0 * d + q];
+            for (int c = 1; c < d; ++c) v = FMA(A2[p * d + c], A1[c * d + q], v);
+            A[p * d + q] = v;
+        }
+        REAL u = e2[p];
+        for (int c = 0; c < d; ++c) u = FMA(A2[p * d + c], e1[c], u);
+        e[p] = u;
+    }
+}
+static void aff_apply(int d, const REAL* A, const REAL* e, const REAL* x, REAL* y) {
+    for (int p = 0; p < d; ++p) {
+        REAL u = e[p];
+        for (int c = 0; c < d; ++c) u = FMA(A[p * d + c], x[c], u);
+        y[p] = u;
+    }
+}
+
+/* Linear drift (OU): the guided Euler recursion is affine, x_{i+1} = A_i x_i + e_i.  The
+ * canonical evaluation (the HIP kernel's k_block_scan) cuts the segment into chunks of 64
+ * steps; within a chunk the maps are combined by an inclusive Kogge–Stone scan (level o =
+ * 1,2,4,...,32: element j ← element j ∘ element j-o for j ≥ o, all reading the previous
+ * level), x_{c0+j+1} = Φ_j x_{c0} + ψ_j, and the next chunk starts at x_{c0+cnt}. */
+static int solve_segment_scan(int d, int m, const REAL* th, const REAL* sg, const REAL* a,
+                              const REAL* Bt, const REAL* beta, const REAL* da, int trace,
+                              int npts, const REAL* t, const REAL* H, const REAL* F,
+                              const REAL* W, const REAL* y1, REAL* X, REAL* ll_out) {
+    int h = d * (d + 1) / 2;
+    int n = npts - 1;
+    REAL xs[3];
+    for (int p = 0; p < d; ++p) { xs[p] = y1[p]; X[p] = xs[p]; }
+    psum_t ps; ps_init(&ps);
+    static __thread REAL A[64][9], e[64][3], An[64][9], en[64][3];
+    for (int c0 = 0; c0 < n; c0 += 64) {
+        int cnt = n - c0 < 64 ? n - c0 : 64;
+        for (int j = 0; j < 64; ++j) {
+            if (j < cnt) {
+                int i = c0 + j;
+                REAL dt = t[i + 1] - t[i];
+                const REAL* dW = W + (size_t)(i + 1) * m;
+                REAL Mg[9], cg[3], sdw[3];
+                guide_coeffs(ORC_OU, d, th, a, H + (size_t)i * h, F + (size_t)i * d, Mg, cg);
+                for (int p = 0; p < d; ++p) {
+                    REAL v = sg[p * m + 0] * dW[0];
+                    for (int k = 1; k < m; ++k) v = FMA(sg[p * m + k], dW[k], v);
+                    sdw[p] = v;
+                }
+                for (int p = 0; p < d; ++p) {
+                    for (int q = 0; q < d; ++q)
+                        A[j][p * d + q] = FMA(-Mg[p * d + q], dt, p == q ? (REAL)1 : (REAL)0);
+                    e[j][p] = FMA(cg[p], dt, sdw[p]);
+                }
+            } else {
+                for (int p = 0; p < d; ++p) {
+                    for (int q = 0; q < d; ++q) A[j][p * d + q] = p == q ? (REAL)1 : (REAL)0;
+                    e[j][p] = (REAL)0;
+                }
+            }
+        }
+        for (int o = 1; o < 64; o <<= 1) {
+            for (int j = o; j < 64; ++j) aff_compose(d, A[j], e[j], A[j - o], e[j - o], An[j], en[j]);
+            for (int j = o; j < 64; ++j) {
+                memcpy(A[j], An[j], sizeof(REAL) * d * d);
+                memcpy(e[j], en[j], sizeof(REAL) * d);
+            }
+        }
+        REAL xpre[3];
+        for (int p = 0; p < d; ++p) xpre[p] = xs[p];
+        for (int j = 0; j < cnt; ++j) {
+            int i = c0 + j;
+            REAL dt = t[i + 1] - t[i];
+            REAL r[3] = {0, 0, 0}, b[3] = {0, 0, 0};
+            REAL G = g_at(ORC_OU, d, th, a, Bt, beta, da, trace, H + (size_t)i * h,
+                          F + (size_t)i * d, xpre, r, b);
+            ps_add(&ps, G * dt);
+            REAL xp[3];
+            aff_apply(d, A[j], e[j], xs, xp);
+            for (int p = 0; p < d; ++p) { X[(size_t)(i + 1) * d + p] = xp[p]; xpre[p] = xp[p]; }
+        }
+        for (int p = 0; p < d; ++p) xs[p] = xpre[p];
+    }
+    REAL ll = ps_finish(&ps);
+    *ll_out = ll;
+    int ok = isfinite(ll) ? 1 : 0;
+    for (int p = 0; p < d; ++p) ok &= isfinite(xs[p]) ? 1 : 0;
+    return ok;
+}
+
 /* GP.solve_and_ll!(X, W, P, y1): Euler–Maruyama guided solve with given W and
  * the Girsanov sum.  Returns 1 on success (finite end point and ll). */
 int SFX(orc_solve_segment)(int model, int d, int m, const double* law, int npts,
@@ -216,6 +317,9 @@ int SFX(orc_solve_segment)(int model, int d, int m, const double* law, int npts,
     int h = d * (d + 1) / 2;
     REAL th[16], sg[9], a[6], Bt[9], beta[3], da[6]; int trace;
     load_law(law, d, m, th, sg, a, Bt, beta, da, &trace);
+    if (model == ORC_OU)
+        return solve_segment_scan(d, m, th, sg, a, Bt, beta, da, trace, npts, t, H, F, W, y1,
+                                  X, ll_out);
     REAL x[3];
     for (int p = 0; p < d; ++p) { x[p] = y1[p]; X[p] = x[p]; }
     psum_t ps; ps_init(&ps);
@@ -224,7 +328,7 @@ int SFX(orc_solve_segment)(int model, int d, int m, const double* law, int npts,
         const REAL* dW = W + (size_t)(i + 1) * m;  /* increments */
         const REAL* Hi = H + (size_t)i * h;
         const REAL* Fi = F + (size_t)i * d;
-        REAL r[3], b[3];
+        REAL r[3] = {0, 0, 0}, b[3] = {0, 0, 0};
         REAL G = g_at(model, d, th, a, Bt, beta, da, trace, Hi, Fi, x, r, b);
         ps_add(&ps, G * dt);
         REAL Mg[9], cg[3];
@@ -256,7 +360,7 @@ REAL SFX(orc_path_ll_segment)(int model, int d, int m, const double* law, int np
     psum_t ps; ps_init(&ps);
     for (int i = 0; i < npts - 1; ++i) {
         REAL dt = t[i + 1] - t[i];
-        REAL r[3], b[3];
+        REAL r[3] = {0, 0, 0}, b[3] = {0, 0, 0};
         REAL G = g_at(model, d, th, a, Bt, beta, da, trace, H + (size_t)i * h,
                       F + (size_t)i * d, X + (size_t)i * d, r, b);
         ps_add(&ps, G * dt);

@@ -1,0 +1,64 @@
+#!/usr/bin/env python3
+"""HBM traffic per launch of the dominant kernel from rocprofv3 PMC passes.
+
+  python scripts/pmc_traffic.py --fetch F.csv --write W.csv --kernel SUBSTR \
+      [--calib-fetch CF.csv --calib-write CW.csv] --out profiles/rNN_traffic_<cfg>.json
+
+FETCH_SIZE / WRITE_SIZE are in KiB per dispatch (rocprofv3 counter_collection.csv).  Each is
+corrected by a factor measured with scripts/calib_stream (a known 1 GiB read + 1 GiB write at
+the same access width, fp64 8 B/lane or fp32 4 B/lane), as MI355X_MICROARCH.md prescribes for
+widths it does not calibrate.  Output: median corrected bytes per launch of the matching kernel.
+"""
+import argparse
+import csv
+import json
+import statistics
+
+
+def per_kernel(path, counter, substr):
+    vals = []
+    with open(path, newline="") as f:
+        for row in csv.DictReader(f):
+            if row["Counter_Name"] == counter and substr in row["Kernel_Name"]:
+                vals.append(float(row["Counter_Value"]))
+    return vals
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--fetch", required=True)
+    ap.add_argument("--write", required=True)
+    ap.add_argument("--kernel", required=True, help="substring of the kernel name")
+    ap.add_argument("--calib-fetch")
+    ap.add_argument("--calib-write")
+    ap.add_argument("--calib-kernel", default="k_stream<double>")
+    ap.add_argument("--config", default="")
+    ap.add_argument("--out", required=True)
+    a = ap.parse_args()
+    fk = per_kernel(a.fetch, "FETCH_SIZE", a.kernel)
+    wk = per_kernel(a.write, "WRITE_SIZE", a.kernel)
+    if not fk or not wk:
+        raise SystemExit(f"no dispatches of {a.kernel!r} in the PMC files")
+    cf = cw = 1.0
+    calib = None
+    if a.calib_fetch and a.calib_write:
+        gib = float(1 << 30)
+        cfv = per_kernel(a.calib_fetch, "FETCH_SIZE", a.calib_kernel)
+        cwv = per_kernel(a.calib_write, "WRITE_SIZE", a.calib_kernel)
+        cf = gib / (statistics.median(cfv) * 1024.0)
+        cw = gib / (statistics.median(cwv) * 1024.0)
+        calib = {"kernel": a.calib_kernel, "fetch_factor": cf, "write_factor": cw,
+                 "fetch_kib_raw": statistics.median(cfv), "write_kib_raw": statistics.median(cwv)}
+    f_b = statistics.median(fk) * 1024.0 * cf
+    w_b = statistics.median(wk) * 1024.0 * cw
+    out = {"config": a.config, "kernel": a.kernel, "dispatches": [len(fk), len(wk)],
+           "fetch_bytes": f_b, "write_bytes": w_b, "traffic_bytes_per_launch": f_b + w_b,
+           "fetch_kib_raw_median": statistics.median(fk),
+           "write_kib_raw_median": statistics.median(wk), "calibration": calib}
+    with open(a.out, "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

@@ -273,3 +273,28 @@ def test_mcmc_step_equals_separate_calls(mapping, B):
         r1 = ens[1].mcmc_step(lay, 0, B, i, salt=3)
         assert r0 == r1
     cs.assert_paths_equal(ens[0], ens[1])
+
+
+@pytest.mark.parametrize("B", [100, 2500])
+def test_mcmc_run_equals_step_sequence(B):
+    """dmt_mcmc_run(iter0, n) == n dmt_mcmc_step calls, bit for bit (results, paths, ll,
+    histories)."""
+    import diffusionmcmctools_amd as d
+    w = W.c2_ou2d(B=B, N=60)
+    w.meta["hist_len"] = 6
+    ens = []
+    for _ in range(2):
+        e = d.Ensemble(w.model.kind, w.d, w.m, w.n_points, precision=w.precision, seed=23,
+                       grid_shared=w.grid_shared)
+        lay = W.fill(e, w)
+        e.loglikhd(lay, L.U, 0, B)
+        ens.append(e)
+    steps = [ens[0].mcmc_step(lay, 0, B, i, salt=5) for i in range(1, 7)]
+    run = ens[1].mcmc_run(lay, 0, B, 1, 6, salt=5)
+    assert np.array_equal(np.array(steps, dtype=np.float64), run)
+    cs.assert_paths_equal(ens[0], ens[1])
+    for what in (L.BLK_LL, L.BLK_LLPROP):
+        assert np.array_equal(ens[0].get_block_state(lay, what, 0, B),
+                              ens[1].get_block_state(lay, what, 0, B))
+    assert np.array_equal(ens[0].get_block_state(lay, L.BLK_ACC_HIST, 0, B, 6),
+                          ens[1].get_block_state(lay, L.BLK_ACC_HIST, 0, B, 6))
