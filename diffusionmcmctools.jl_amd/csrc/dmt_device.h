@@ -338,9 +338,10 @@ struct U4 { uint32_t x, y, z, w; };
 __device__ __forceinline__ U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
-    uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
-    uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
-    U4 n = {hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    // full 64-bit products: one v_mad_u64_u32 each instead of a mul_lo + mul_hi pair
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
+    U4 n = {(uint32_t)(p1 >> 32) ^ c.y ^ k0, (uint32_t)p1, (uint32_t)(p0 >> 32) ^ c.w ^ k1,
+            (uint32_t)p0};
     c = n;
     k0 += 0x9E3779B9u;
     k1 += 0xBB67AE85u;
@@ -348,23 +349,149 @@ __device__ __forceinline__ U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
   return c;
 }
 
+// ---------------------------------------------------------------- canonical transcendentals
+// The normal and exponential draws use these explicit polynomial kernels (not the device
+// libm), restated operation for operation in oracle/dmt_oracle.c, so that device-RNG draws
+// are bit-identical to the CPU restatement.
+#define RNG_SQRT_HALF 0x1.6a09e667f3bcdp-1
+#define RNG_LN2_HI 0x1.62e42p-1
+#define RNG_LN2_LO 0x1.fdf473de6af28p-22
+#define RNG_P1 0x1.5555555555555p-1
+#define RNG_P2 0x1.999999999999ap-2
+#define RNG_P3 0x1.2492492492492p-2
+#define RNG_P4 0x1.c71c71c71c71cp-3
+#define RNG_P5 0x1.745d1745d1746p-3
+#define RNG_P6 0x1.3b13b13b13b14p-3
+#define RNG_P7 0x1.1111111111111p-3
+#define RNG_P8 0x1.e1e1e1e1e1e1ep-4
+#define RNG_P9 0x1.af286bca1af28p-4
+#define RNG_P10 0x1.8618618618618p-4
+#define RNG_P11 0x1.642c8590b2164p-4
+#define RNG_S0 0x1.921fb54442d18p+1
+#define RNG_S1 -0x1.4abbce625be53p+2
+#define RNG_S2 0x1.466bc6775aae2p+1
+#define RNG_S3 -0x1.32d2cce62bd86p-1
+#define RNG_S4 0x1.50783487ee782p-4
+#define RNG_S5 -0x1.e3074fde8871fp-8
+#define RNG_S6 0x1.e8f434d018d63p-12
+#define RNG_S7 -0x1.6fadb9f155744p-16
+#define RNG_S8 0x1.aaec32af93359p-21
+#define RNG_C1 -0x1.3bd3cc9be45dep+2
+#define RNG_C2 0x1.03c1f081b5ac4p+2
+#define RNG_C3 -0x1.55d3c7e3cbffap+0
+#define RNG_C4 0x1.e1f506891babbp-3
+#define RNG_C5 -0x1.a6d1f2a204a8cp-6
+#define RNG_C6 0x1.f9d38a3763cc3p-10
+#define RNG_C7 -0x1.b6e24f44b128fp-14
+#define RNG_C8 0x1.20c62c2f2d7f5p-18
+#define RNG_C9 -0x1.2a0c591af8314p-23
+#define RNGF_SQRT_HALF 0x1.6a09e6p-1f
+#define RNGF_LN2_HI 0x1.62ep-1f
+#define RNGF_LN2_LO 0x1.0bfbe8p-15f
+#define RNGF_P1 0x1.555556p-1f
+#define RNGF_P2 0x1.99999ap-2f
+#define RNGF_P3 0x1.24924ap-2f
+#define RNGF_P4 0x1.c71c72p-3f
+#define RNGF_P5 0x1.745d18p-3f
+#define RNGF_S0 0x1.921fb6p+1f
+#define RNGF_S1 -0x1.4abbcep+2f
+#define RNGF_S2 0x1.466bc6p+1f
+#define RNGF_S3 -0x1.32d2ccp-1f
+#define RNGF_S4 0x1.507834p-4f
+#define RNGF_C1 -0x1.3bd3ccp+2f
+#define RNGF_C2 0x1.03c1f0p+2f
+#define RNGF_C3 -0x1.55d3c8p+0f
+#define RNGF_C4 0x1.e1f506p-3f
+#define RNGF_C5 -0x1.a6d1f2p-6f
+/* log(u) for finite u > 0: u = m·2^e with m in [√½, √2); s = (m-1)/(m+1);
+ * log(m) = 2s + s·z·P(z), z = s², P(z) = Σ_k 2/(2k+1) z^(k-1) (k = 1..11, Horner with fma);
+ * log(u) = e·ln2_hi + (e·ln2_lo + log(m)). */
+__device__ __forceinline__ double rng_log(double u) {
+    int e;
+    double m = __builtin_frexp(u, &e);
+    const int lo = m < RNG_SQRT_HALF;
+    m = lo ? m * 2.0 : m;
+    e = lo ? e - 1 : e;
+    const double f = m - 1.0;
+    const double s = f / (2.0 + f);
+    const double z = s * s;
+    double p = RNG_P11;
+    p = __builtin_fma(p, z, RNG_P10); p = __builtin_fma(p, z, RNG_P9); p = __builtin_fma(p, z, RNG_P8);
+    p = __builtin_fma(p, z, RNG_P7); p = __builtin_fma(p, z, RNG_P6); p = __builtin_fma(p, z, RNG_P5);
+    p = __builtin_fma(p, z, RNG_P4); p = __builtin_fma(p, z, RNG_P3); p = __builtin_fma(p, z, RNG_P2);
+    p = __builtin_fma(p, z, RNG_P1);
+    const double lm = __builtin_fma(s, z * p, 2.0 * s);
+    const double de = (double)e;
+    return __builtin_fma(de, RNG_LN2_HI, __builtin_fma(de, RNG_LN2_LO, lm));
+}
+/* sin(πx), cos(πx) for x in [0, 2]: n = rint(2x), r = x - n/2 in [-1/4, 1/4] (exact),
+ * sin(πr) = r·S(r²), cos(πr) = 1 + r²·C(r²) (Taylor, Horner with fma), quadrant n mod 4. */
+__device__ __forceinline__ void rng_sincospi(double x, double* sn, double* cs) {
+    const double n = __builtin_rint(2.0 * x);
+    const double r = __builtin_fma(-0.5, n, x);
+    const double z = r * r;
+    double sp = RNG_S8;
+    sp = __builtin_fma(sp, z, RNG_S7); sp = __builtin_fma(sp, z, RNG_S6); sp = __builtin_fma(sp, z, RNG_S5);
+    sp = __builtin_fma(sp, z, RNG_S4); sp = __builtin_fma(sp, z, RNG_S3); sp = __builtin_fma(sp, z, RNG_S2);
+    sp = __builtin_fma(sp, z, RNG_S1); sp = __builtin_fma(sp, z, RNG_S0);
+    double cp = RNG_C9;
+    cp = __builtin_fma(cp, z, RNG_C8); cp = __builtin_fma(cp, z, RNG_C7); cp = __builtin_fma(cp, z, RNG_C6);
+    cp = __builtin_fma(cp, z, RNG_C5); cp = __builtin_fma(cp, z, RNG_C4); cp = __builtin_fma(cp, z, RNG_C3);
+    cp = __builtin_fma(cp, z, RNG_C2); cp = __builtin_fma(cp, z, RNG_C1);
+    const double s0 = r * sp, c0 = __builtin_fma(cp, z, 1.0);
+    const int q = (int)n & 3;
+    *sn = q == 0 ? s0 : q == 1 ? c0 : q == 2 ? -s0 : -c0;
+    *cs = q == 0 ? c0 : q == 1 ? -s0 : q == 2 ? -c0 : s0;
+}
+__device__ __forceinline__ float rng_logf(float u) {
+    int e;
+    float m = __builtin_frexpf(u, &e);
+    const int lo = m < RNGF_SQRT_HALF;
+    m = lo ? m * 2.0f : m;
+    e = lo ? e - 1 : e;
+    const float f = m - 1.0f;
+    const float s = f / (2.0f + f);
+    const float z = s * s;
+    float p = RNGF_P5;
+    p = __builtin_fmaf(p, z, RNGF_P4); p = __builtin_fmaf(p, z, RNGF_P3); p = __builtin_fmaf(p, z, RNGF_P2);
+    p = __builtin_fmaf(p, z, RNGF_P1);
+    const float lm = __builtin_fmaf(s, z * p, 2.0f * s);
+    const float de = (float)e;
+    return __builtin_fmaf(de, RNGF_LN2_HI, __builtin_fmaf(de, RNGF_LN2_LO, lm));
+}
+__device__ __forceinline__ void rng_sincospif(float x, float* sn, float* cs) {
+    const float n = __builtin_rintf(2.0f * x);
+    const float r = __builtin_fmaf(-0.5f, n, x);
+    const float z = r * r;
+    float sp = RNGF_S4;
+    sp = __builtin_fmaf(sp, z, RNGF_S3); sp = __builtin_fmaf(sp, z, RNGF_S2); sp = __builtin_fmaf(sp, z, RNGF_S1);
+    sp = __builtin_fmaf(sp, z, RNGF_S0);
+    float cp = RNGF_C5;
+    cp = __builtin_fmaf(cp, z, RNGF_C4); cp = __builtin_fmaf(cp, z, RNGF_C3); cp = __builtin_fmaf(cp, z, RNGF_C2);
+    cp = __builtin_fmaf(cp, z, RNGF_C1);
+    const float s0 = r * sp, c0 = __builtin_fmaf(cp, z, 1.0f);
+    const int q = (int)n & 3;
+    *sn = q == 0 ? s0 : q == 1 ? c0 : q == 2 ? -s0 : -c0;
+    *cs = q == 0 ? c0 : q == 1 ? -s0 : q == 2 ? -c0 : s0;
+}
+
 __device__ __forceinline__ void normal_pair(U4 o, double& z0, double& z1) {
   uint64_t k1 = ((uint64_t)(o.x >> 5) << 26) | (o.y >> 6);
   uint64_t k2 = ((uint64_t)(o.z >> 5) << 26) | (o.w >> 6);
   double u1 = (double)(k1 + 1) * 0x1p-53;
   double u2 = (double)k2 * 0x1p-53;
-  double rad = sqrt(-2.0 * log(u1));
+  double rad = sqrt(-2.0 * rng_log(u1));
   double s, c;
-  sincospi(2.0 * u2, &s, &c);
+  rng_sincospi(2.0 * u2, &s, &c);
   z0 = rad * c;
   z1 = rad * s;
 }
 __device__ __forceinline__ void normal_pair(U4 o, float& z0, float& z1) {
   float u1 = (float)((o.x >> 8) + 1u) * 0x1p-24f;
   float u2 = (float)(o.z >> 8) * 0x1p-24f;
-  float rad = sqrtf(-2.0f * logf(u1));
+  float rad = sqrtf(-2.0f * rng_logf(u1));
   float s, c;
-  sincospif(2.0f * u2, &s, &c);
+  rng_sincospif(2.0f * u2, &s, &c);
   z0 = rad * c;
   z1 = rad * s;
 }
@@ -375,7 +502,7 @@ __device__ __forceinline__ double exp1_draw(uint64_t seed, uint32_t blk, uint32_
                        (uint32_t)(seed >> 32));
   uint64_t k1 = ((uint64_t)(o.x >> 5) << 26) | (o.y >> 6);
   double u = (double)(k1 + 1) * 0x1p-53;
-  return -log(u);
+  return -rng_log(u);
 }
 
 // Normal stream of one segment: normal n = step*M + k uses pair n>>1 of Philox block

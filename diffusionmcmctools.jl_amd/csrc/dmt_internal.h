@@ -132,7 +132,10 @@ hipError_t launch_from_planes(int precision, int tw, double* dst, const void* sr
 hipError_t launch_cast(int precision, const double* src, void* dst, int64_t n, hipStream_t s);
 hipError_t launch_block_sum(const double* ll, const double* llp, const uint8_t* acc, int64_t n,
                             double* work, double* out3, hipStream_t s);
-hipError_t launch_accept_reduce(const AcceptArgs& a, double* work, double* out3, hipStream_t s);
+// work: multi-level tree scratch (6 per 1024-block group); lb: single-launch scratch
+// (3 x 256 partials + a counter, zero-initialised once)
+hipError_t launch_accept_reduce(const AcceptArgs& a, double* work, double* lb, double* out3,
+                                hipStream_t s);
 hipError_t launch_flip(uint8_t* sel0, uint8_t* sel1, uint8_t* sel2, uint8_t* sel3,
                        const int32_t* gfirst, const int32_t* glast, const uint8_t* term,
                        int32_t swap_ppb_nonterm_only, int64_t b0, int64_t b1, hipStream_t s);

@@ -19,6 +19,7 @@
 #include <stdlib.h>
 
 #include <type_traits>
+#include <algorithm>
 
 #include "dmt_device.h"
 #include "dmt_internal.h"
@@ -620,15 +621,28 @@ __global__ __launch_bounds__(128) void k_block_wave(const BlockArgs<T> a) {
 // (the carry of the chunk start points), done by one thread between two barriers.  Then every
 // lane evaluates its point, the Girsanov terms and the 64-lane tree sum, and stores.
 #ifndef DMT_SCAN_MINW
-#define DMT_SCAN_MINW 1
+#define DMT_SCAN_MINW 4
 #endif
 #ifndef DMT_SCAN_WAVES
-#define DMT_SCAN_WAVES 8
+#define DMT_SCAN_WAVES 4
 #endif
 constexpr int kScanWaves = DMT_SCAN_WAVES;
 
 template <class T>
 __device__ __forceinline__ T shfl_up_T(T v, int o) { return __shfl_up(v, (unsigned)o, 64); }
+
+// Raw cross-lane read: the value of lane `src` (ds_bpermute, no range fix-up; the caller
+// selects).  `addr` = 4 * src lane.
+__device__ __forceinline__ double lane_read(double v, int addr) {
+  const int2 p = __builtin_bit_cast(int2, v);
+  int2 r;
+  r.x = __builtin_amdgcn_ds_bpermute(addr, p.x);
+  r.y = __builtin_amdgcn_ds_bpermute(addr, p.y);
+  return __builtin_bit_cast(double, r);
+}
+__device__ __forceinline__ float lane_read(float v, int addr) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(addr, __builtin_bit_cast(int, v)));
+}
 
 // Store one point's N components (16-byte stores when N is even and T is double).
 template <int N, class T>
@@ -742,6 +756,7 @@ __global__ __launch_bounds__(64 * kScanWaves, DMT_SCAN_MINW) void k_block_scan(c
 #pragma unroll
         for (int kk = 0; kk < M; ++kk) dW[kk] = Wsb[(int64_t)(i + 1) * M + kk];
       } else {
+        __builtin_amdgcn_sched_barrier(0);
         const double* Zg = a.Z ? a.Z + ldc(a.st_off + g) * M : nullptr;
         uint32_t have = 0xFFFFFFFFu;
         T z0 = (T)0, z1 = (T)0;
@@ -763,6 +778,7 @@ __global__ __launch_bounds__(64 * kScanWaves, DMT_SCAN_MINW) void k_block_scan(c
           const T wv = (MODE == MODE_FRESH) ? (T)0 : Wsb[(int64_t)(i + 1) * M + kk];
           dW[kk] = dfma(rho, wv, srho * (sdt * z));
         }
+        __builtin_amdgcn_sched_barrier(0);
       }
       T Hi[HP], Fi[D], sdW[D], Mg[D * D], cg[D];
 #pragma unroll
@@ -785,10 +801,11 @@ __global__ __launch_bounds__(64 * kScanWaves, DMT_SCAN_MINW) void k_block_scan(c
 #pragma unroll
       for (int o = 1; o < 64; o <<= 1) {
         T Ap[D * D], ep[D], An[D * D], en[D];
+        const int src = 4 * (lane - o);  // lanes < o read garbage and keep their own map
 #pragma unroll
-        for (int c = 0; c < D * D; ++c) Ap[c] = shfl_up_T(A[c], o);
+        for (int c = 0; c < D * D; ++c) Ap[c] = lane_read(A[c], src);
 #pragma unroll
-        for (int c = 0; c < D; ++c) ep[c] = shfl_up_T(e[c], o);
+        for (int c = 0; c < D; ++c) ep[c] = lane_read(e[c], src);
         affine_compose<D, T>(A, e, Ap, ep, An, en);
         const bool take = lane >= o;
 #pragma unroll
@@ -852,7 +869,7 @@ __global__ __launch_bounds__(64 * kScanWaves, DMT_SCAN_MINW) void k_block_scan(c
       affine_apply<D, T>(A, e, xs, xpost);
 #pragma unroll
       for (int p = 0; p < D; ++p) {
-        const T up = shfl_up_T(xpost[p], 1);
+        const T up = lane_read(xpost[p], 4 * (lane - 1));
         xpre[p] = lane == 0 ? xs[p] : up;
       }
       Law<Mdl, T> LB;
@@ -1076,6 +1093,80 @@ __global__ __launch_bounds__(1024) void k_accept_reduce(const AcceptArgs a, doub
         out[2 * nout + blockIdx.x] = v2;
       }
     }
+  }
+}
+
+// Single-launch form for up to 256 groups of 256 blocks: every workgroup decides its 256
+// blocks and reduces them (4 wave trees + one 4-leaf tree = the aligned 256-leaf subtree of
+// the fetch_ll tree); the last workgroup to finish (device-scope counter) reduces the group
+// partials in group order with the same tree and writes the canonicalised result.
+constexpr int kAccGroup = 256;
+__global__ __launch_bounds__(kAccGroup) void k_accept_reduce_lb(const AcceptArgs a,
+                                                                double* __restrict__ part,
+                                                                unsigned* __restrict__ counter,
+                                                                double* __restrict__ out3) {
+  __shared__ double w0[4], w1[4], w2[4];
+  __shared__ int s_last;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int64_t blk = a.b0 + (int64_t)blockIdx.x * kAccGroup + tid;
+  double v0 = 0.0, v1 = 0.0, v2 = 0.0;
+  if (blk < a.b1) {
+    const double E = a.E ? a.E[blk - a.b0]
+                         : exp1_draw(a.seed, (uint32_t)a.gfirst[blk] + a.seg_base, (uint32_t)a.mcmciter, a.salt);
+    double ll = a.ll[blk], llp = a.llp[blk];
+    const bool acc = E > -(llp - ll);
+    if (acc) {
+      for (int g = a.gfirst[blk]; g <= a.glast[blk]; ++g) {
+        a.selX[g] ^= 1;
+        a.selW[g] ^= 1;
+      }
+    }
+    if (a.hist_len > 0) {
+      const int64_t o = (a.mcmciter - 1) * a.nblocks + blk;
+      a.acc_hist[o] = acc ? 1 : 0;
+      a.ll_hist[o] = ll;
+      a.llp_hist[o] = llp;
+    }
+    if (acc) {
+      a.ll[blk] = llp;
+      a.llp[blk] = ll;
+      const double t = ll; ll = llp; llp = t;
+    }
+    if (a.acc_out) a.acc_out[blk - a.b0] = acc ? 1 : 0;
+    v0 = ll;
+    v1 = llp;
+    v2 = acc ? 1.0 : 0.0;
+  }
+  v0 = wave_tree_sum<double>(v0);
+  v1 = wave_tree_sum<double>(v1);
+  v2 = wave_tree_sum<double>(v2);
+  if (lane == 0) { w0[wv] = v0; w1[wv] = v1; w2[wv] = v2; }
+  __syncthreads();
+  if (tid == 0) {
+    part[3 * blockIdx.x + 0] = (w0[0] + w0[1]) + (w0[2] + w0[3]);
+    part[3 * blockIdx.x + 1] = (w1[0] + w1[1]) + (w1[2] + w1[3]);
+    part[3 * blockIdx.x + 2] = (w2[0] + w2[1]) + (w2[2] + w2[3]);
+    __threadfence();
+    s_last = atomicAdd(counter, 1u) == gridDim.x - 1 ? 1 : 0;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  const int G = (int)gridDim.x;
+  v0 = tid < G ? part[3 * tid + 0] : 0.0;
+  v1 = tid < G ? part[3 * tid + 1] : 0.0;
+  v2 = tid < G ? part[3 * tid + 2] : 0.0;
+  v0 = wave_tree_sum<double>(v0);
+  v1 = wave_tree_sum<double>(v1);
+  v2 = wave_tree_sum<double>(v2);
+  __syncthreads();
+  if (lane == 0) { w0[wv] = v0; w1[wv] = v1; w2[wv] = v2; }
+  __syncthreads();
+  if (tid == 0) {
+    out3[0] = ((w0[0] + w0[1]) + (w0[2] + w0[3])) + 0.0;
+    out3[1] = ((w1[0] + w1[1]) + (w1[2] + w1[3])) + 0.0;
+    out3[2] = (w2[0] + w2[1]) + (w2[2] + w2[3]);
+    *counter = 0u;  // ready for the next launch (stream-ordered)
   }
 }
 
@@ -1441,8 +1532,18 @@ hipError_t launch_block_sum(const double* ll, const double* llp, const uint8_t* 
 }
 
 // accept + fetch tree (ll, ll°, accepted of this iteration) over [b0, b1)
-hipError_t launch_accept_reduce(const AcceptArgs& a, double* work, double* out3, hipStream_t s) {
+hipError_t launch_accept_reduce(const AcceptArgs& a, double* work, double* lb, double* out3,
+                                hipStream_t s) {
   const int64_t n = a.b1 - a.b0;
+  {  // single launch while the group partials fit one workgroup
+    const int64_t groups = std::max<int64_t>(1, (n + kAccGroup - 1) / kAccGroup);
+    if (groups <= kAccGroup) {
+      // work layout: [3 * 256] partials, then the counter
+      k_accept_reduce_lb<<<(unsigned)groups, kAccGroup, 0, s>>>(
+          a, lb, reinterpret_cast<unsigned*>(lb + 3 * kAccGroup), out3);
+      return hipGetLastError();
+    }
+  }
   int64_t groups = (n + 1023) / 1024;
   if (groups < 1) groups = 1;
   double* bufs[2] = {work, work + 3 * groups};

@@ -118,6 +118,7 @@ struct dmt_ens {
   int64_t Z_n = 0;
   double* d_red = nullptr;  // [3] reduction output, [3 * nranks] gather
   double* d_red_work = nullptr;
+  double* d_red_lb = nullptr;
   int64_t red_work_n = 0;
   double* h_red = nullptr;  // pinned host copy of the 3 reduction results
   double* d_gather = nullptr;
@@ -704,7 +705,7 @@ dmt_status dmt_destroy(dmt_ens* h) {
   void* ps[] = {h->d_pt_off, h->d_st_off, h->d_tile_qoff, h->d_seg_rec, h->d_seg_q, h->d_seg_np,
                 h->d_sel[0], h->d_sel[1], h->d_sel[2], h->d_sel[3], h->d_X[0], h->d_X[1],
                 h->d_W[0], h->d_W[1], h->d_t, h->d_stage, h->d_Z, h->d_red, h->d_gather,
-                h->d_red_work, h->d_run, h->d_run_gather};
+                h->d_red_work, h->d_run, h->d_run_gather, h->d_red_lb};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   for (int s = 0; s < 2; ++s)
@@ -968,12 +969,19 @@ static AcceptArgs accept_args(dmt_ens* h, Layout* L, int64_t b0, int64_t b1, con
 
 static dmt_status ensure_red_work(dmt_ens* h, int64_t n) {
   const int64_t groups = std::max<int64_t>(1, (n + 1023) / 1024);
-  if (groups * 6 > h->red_work_n) {
+  // multi-level tree: 2 x 3 doubles per group; single-launch form (k_accept_reduce_lb):
+  // 3 x 256 partials + a zeroed counter
+  if (!h->d_red_lb) {
+    DMT_TRY(ens_alloc(h, &h->d_red_lb, 3 * 256 + 2));
+    HIP_OK(hipMemsetAsync(h->d_red_lb, 0, (3 * 256 + 2) * 8, h->stream));
+  }
+  const int64_t need = groups * 6;
+  if (need > h->red_work_n) {
     if (h->d_red_work) { (void)hipFree(h->d_red_work); h->bytes -= h->red_work_n * 8; }
     h->d_red_work = nullptr;
     h->red_work_n = 0;
-    DMT_TRY(ens_alloc(h, &h->d_red_work, groups * 6));
-    h->red_work_n = groups * 6;
+    DMT_TRY(ens_alloc(h, &h->d_red_work, need));
+    h->red_work_n = need;
   }
   return DMT_OK;
 }
@@ -1022,7 +1030,7 @@ dmt_status dmt_mcmc_step(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int
   {
     TimedScope ts(h, DMT_K_ACCEPT);
     HIP_OK(launch_accept_reduce(accept_args(h, L, b0, b1, nullptr, mcmciter, salt, nullptr),
-                                h->d_red_work, h->d_red, h->stream));
+                                h->d_red_work, h->d_red_lb, h->d_red, h->stream));
   }
   double v[3];
   DMT_TRY(finish_reduction(h, v));
@@ -1067,7 +1075,7 @@ dmt_status dmt_mcmc_run(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int6
     {
       TimedScope ts(h, DMT_K_ACCEPT);
       HIP_OK(launch_accept_reduce(accept_args(h, L, b0, b1, nullptr, it, salt, nullptr),
-                                  h->d_red_work, h->d_run + 3 * i, h->stream));
+                                  h->d_red_work, h->d_red_lb, h->d_run + 3 * i, h->stream));
     }
     if (multi &&
         ncclAllGather(h->d_run + 3 * i, h->d_run_gather + 3 * h->nranks * i, 3, ncclDouble,

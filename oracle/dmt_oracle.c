@@ -496,6 +496,129 @@ void orc_philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
 void orc_philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1);
 #endif
 
+/* ---- canonical transcendental kernels of the draws (identical to dmt_device.h) ---- */
+#define RNG_SQRT_HALF 0x1.6a09e667f3bcdp-1
+#define RNG_LN2_HI 0x1.62e42p-1
+#define RNG_LN2_LO 0x1.fdf473de6af28p-22
+#define RNG_P1 0x1.5555555555555p-1
+#define RNG_P2 0x1.999999999999ap-2
+#define RNG_P3 0x1.2492492492492p-2
+#define RNG_P4 0x1.c71c71c71c71cp-3
+#define RNG_P5 0x1.745d1745d1746p-3
+#define RNG_P6 0x1.3b13b13b13b14p-3
+#define RNG_P7 0x1.1111111111111p-3
+#define RNG_P8 0x1.e1e1e1e1e1e1ep-4
+#define RNG_P9 0x1.af286bca1af28p-4
+#define RNG_P10 0x1.8618618618618p-4
+#define RNG_P11 0x1.642c8590b2164p-4
+#define RNG_S0 0x1.921fb54442d18p+1
+#define RNG_S1 -0x1.4abbce625be53p+2
+#define RNG_S2 0x1.466bc6775aae2p+1
+#define RNG_S3 -0x1.32d2cce62bd86p-1
+#define RNG_S4 0x1.50783487ee782p-4
+#define RNG_S5 -0x1.e3074fde8871fp-8
+#define RNG_S6 0x1.e8f434d018d63p-12
+#define RNG_S7 -0x1.6fadb9f155744p-16
+#define RNG_S8 0x1.aaec32af93359p-21
+#define RNG_C1 -0x1.3bd3cc9be45dep+2
+#define RNG_C2 0x1.03c1f081b5ac4p+2
+#define RNG_C3 -0x1.55d3c7e3cbffap+0
+#define RNG_C4 0x1.e1f506891babbp-3
+#define RNG_C5 -0x1.a6d1f2a204a8cp-6
+#define RNG_C6 0x1.f9d38a3763cc3p-10
+#define RNG_C7 -0x1.b6e24f44b128fp-14
+#define RNG_C8 0x1.20c62c2f2d7f5p-18
+#define RNG_C9 -0x1.2a0c591af8314p-23
+#define RNGF_SQRT_HALF 0x1.6a09e6p-1f
+#define RNGF_LN2_HI 0x1.62ep-1f
+#define RNGF_LN2_LO 0x1.0bfbe8p-15f
+#define RNGF_P1 0x1.555556p-1f
+#define RNGF_P2 0x1.99999ap-2f
+#define RNGF_P3 0x1.24924ap-2f
+#define RNGF_P4 0x1.c71c72p-3f
+#define RNGF_P5 0x1.745d18p-3f
+#define RNGF_S0 0x1.921fb6p+1f
+#define RNGF_S1 -0x1.4abbcep+2f
+#define RNGF_S2 0x1.466bc6p+1f
+#define RNGF_S3 -0x1.32d2ccp-1f
+#define RNGF_S4 0x1.507834p-4f
+#define RNGF_C1 -0x1.3bd3ccp+2f
+#define RNGF_C2 0x1.03c1f0p+2f
+#define RNGF_C3 -0x1.55d3c8p+0f
+#define RNGF_C4 0x1.e1f506p-3f
+#define RNGF_C5 -0x1.a6d1f2p-6f
+/* log(u) for finite u > 0: u = m·2^e with m in [√½, √2); s = (m-1)/(m+1);
+ * log(m) = 2s + s·z·P(z), z = s², P(z) = Σ_k 2/(2k+1) z^(k-1) (k = 1..11, Horner with fma);
+ * log(u) = e·ln2_hi + (e·ln2_lo + log(m)). */
+static inline double rng_log(double u) {
+    int e;
+    double m = frexp(u, &e);
+    const int lo = m < RNG_SQRT_HALF;
+    m = lo ? m * 2.0 : m;
+    e = lo ? e - 1 : e;
+    const double f = m - 1.0;
+    const double s = f / (2.0 + f);
+    const double z = s * s;
+    double p = RNG_P11;
+    p = fma(p, z, RNG_P10); p = fma(p, z, RNG_P9); p = fma(p, z, RNG_P8);
+    p = fma(p, z, RNG_P7); p = fma(p, z, RNG_P6); p = fma(p, z, RNG_P5);
+    p = fma(p, z, RNG_P4); p = fma(p, z, RNG_P3); p = fma(p, z, RNG_P2);
+    p = fma(p, z, RNG_P1);
+    const double lm = fma(s, z * p, 2.0 * s);
+    const double de = (double)e;
+    return fma(de, RNG_LN2_HI, fma(de, RNG_LN2_LO, lm));
+}
+/* sin(πx), cos(πx) for x in [0, 2]: n = rint(2x), r = x - n/2 in [-1/4, 1/4] (exact),
+ * sin(πr) = r·S(r²), cos(πr) = 1 + r²·C(r²) (Taylor, Horner with fma), quadrant n mod 4. */
+static inline void rng_sincospi(double x, double* sn, double* cs) {
+    const double n = rint(2.0 * x);
+    const double r = fma(-0.5, n, x);
+    const double z = r * r;
+    double sp = RNG_S8;
+    sp = fma(sp, z, RNG_S7); sp = fma(sp, z, RNG_S6); sp = fma(sp, z, RNG_S5);
+    sp = fma(sp, z, RNG_S4); sp = fma(sp, z, RNG_S3); sp = fma(sp, z, RNG_S2);
+    sp = fma(sp, z, RNG_S1); sp = fma(sp, z, RNG_S0);
+    double cp = RNG_C9;
+    cp = fma(cp, z, RNG_C8); cp = fma(cp, z, RNG_C7); cp = fma(cp, z, RNG_C6);
+    cp = fma(cp, z, RNG_C5); cp = fma(cp, z, RNG_C4); cp = fma(cp, z, RNG_C3);
+    cp = fma(cp, z, RNG_C2); cp = fma(cp, z, RNG_C1);
+    const double s0 = r * sp, c0 = fma(cp, z, 1.0);
+    const int q = (int)n & 3;
+    *sn = q == 0 ? s0 : q == 1 ? c0 : q == 2 ? -s0 : -c0;
+    *cs = q == 0 ? c0 : q == 1 ? -s0 : q == 2 ? -c0 : s0;
+}
+static inline float rng_logf(float u) {
+    int e;
+    float m = frexpf(u, &e);
+    const int lo = m < RNGF_SQRT_HALF;
+    m = lo ? m * 2.0f : m;
+    e = lo ? e - 1 : e;
+    const float f = m - 1.0f;
+    const float s = f / (2.0f + f);
+    const float z = s * s;
+    float p = RNGF_P5;
+    p = fmaf(p, z, RNGF_P4); p = fmaf(p, z, RNGF_P3); p = fmaf(p, z, RNGF_P2);
+    p = fmaf(p, z, RNGF_P1);
+    const float lm = fmaf(s, z * p, 2.0f * s);
+    const float de = (float)e;
+    return fmaf(de, RNGF_LN2_HI, fmaf(de, RNGF_LN2_LO, lm));
+}
+static inline void rng_sincospif(float x, float* sn, float* cs) {
+    const float n = rintf(2.0f * x);
+    const float r = fmaf(-0.5f, n, x);
+    const float z = r * r;
+    float sp = RNGF_S4;
+    sp = fmaf(sp, z, RNGF_S3); sp = fmaf(sp, z, RNGF_S2); sp = fmaf(sp, z, RNGF_S1);
+    sp = fmaf(sp, z, RNGF_S0);
+    float cp = RNGF_C5;
+    cp = fmaf(cp, z, RNGF_C4); cp = fmaf(cp, z, RNGF_C3); cp = fmaf(cp, z, RNGF_C2);
+    cp = fmaf(cp, z, RNGF_C1);
+    const float s0 = r * sp, c0 = fmaf(cp, z, 1.0f);
+    const int q = (int)n & 3;
+    *sn = q == 0 ? s0 : q == 1 ? c0 : q == 2 ? -s0 : -c0;
+    *cs = q == 0 ? c0 : q == 1 ? -s0 : q == 2 ? -c0 : s0;
+}
+
 /* Box–Muller normal pair from one Philox block (perf-mode stream).
  * counter = (c0, c1, c2, c3), key = seed. */
 void SFX(orc_normal_pair)(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
@@ -507,17 +630,19 @@ void SFX(orc_normal_pair)(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2, 
     uint64_t k2 = ((uint64_t)(c[2] >> 5) << 26) | (c[3] >> 6);
     double u1 = (double)(k1 + 1) * 0x1p-53;
     double u2 = (double)k2 * 0x1p-53;
-    double rad = sqrt(-2.0 * log(u1));
-    double ang = 2.0 * M_PI * u2;
-    *z0 = rad * cos(ang);
-    *z1 = rad * sin(ang);
+    double rad = sqrt(-2.0 * rng_log(u1));
+    double sn, cs;
+    rng_sincospi(2.0 * u2, &sn, &cs);
+    *z0 = rad * cs;
+    *z1 = rad * sn;
 #else
     float u1 = (float)((c[0] >> 8) + 1u) * 0x1p-24f;
     float u2 = (float)(c[2] >> 8) * 0x1p-24f;
-    float rad = sqrtf(-2.0f * logf(u1));
-    float ang = 6.28318530717958647692f * u2;
-    *z0 = rad * cosf(ang);
-    *z1 = rad * sinf(ang);
+    float rad = sqrtf(-2.0f * rng_logf(u1));
+    float sn, cs;
+    rng_sincospif(2.0f * u2, &sn, &cs);
+    *z0 = rad * cs;
+    *z1 = rad * sn;
 #endif
 }
 
@@ -529,7 +654,7 @@ double orc_exp1(uint64_t seed, uint32_t blk, uint32_t iter, uint32_t salt) {
     orc_philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
     uint64_t k1 = ((uint64_t)(c[0] >> 5) << 26) | (c[1] >> 6);
     double u = (double)(k1 + 1) * 0x1p-53;
-    return -log(u);
+    return -rng_log(u);
 }
 
 /* raw Philox block, for bit-exact checks of the device generator */
