@@ -102,7 +102,7 @@ def cpu_baseline(w, ens, lay, budget_s=12.0):
             Xo, Wo, llp, _ = orc.draw_terminal_blocks(
                 w.model.kind, w.d, w.m, npts, w.laws, w.t, w.H, w.F, Xa, Wa, rho, Z=None,
                 seed=1234, it=it, salt=0, prec=prec, nthreads=nt, t_shared=True,
-                H_shared=w.H_shared)
+                H_shared=w.H_shared, sequential=True)
             E = rng.exponential(1.0, B)
             acc = E > -(llp - lla)
             sel = np.repeat(acc, npts)
@@ -118,7 +118,8 @@ def cpu_baseline(w, ens, lay, budget_s=12.0):
     v1 = res[1][0]
     return {"value": v, "unit": "steps/s", "cores": nthreads, "kind": "port",
             "sample": f"{its} full MCMC iterations (draw + MH accept) of the same per-GPU workload "
-                      f"({B} blocks x {npts - 1} steps), device-equivalent Philox/Box-Muller normals",
+                      f"({B} blocks x {npts - 1} steps), step-by-step Euler loop, same "
+                      f"Philox/Box-Muller normals, OpenMP over blocks",
             "value_1thread": v1, "accept_rate": ar}
 
 
@@ -204,7 +205,10 @@ def main():
     accept_rate = n_acc / (B * world * args.steps)  # n_acc is already global (fetch_ll over ranks)
     # the mapping libdmt resolves for MAP_AUTO (kAutoWaveMaxRecordings, dmt_internal.h)
     wave = args.mapping == "wave" or (args.mapping == "auto" and len(w.n_points) <= 8192)
-    kname = "k_block_wave" if wave else "k_block<"
+    if w.model.kind == L.MODEL_OU:  # linear drift: always the affine-scan kernel
+        wave, kname = True, "k_block_scan"
+    else:
+        kname = "k_block_wave" if wave else "k_block<"
     traffic, traffic_src = measured_traffic(args.config, kname)
     if rank == 0:
         cpu = None
@@ -227,7 +231,8 @@ def main():
             "config": {"workload": desc, "blocks_per_gpu": B,
                        "euler_steps_per_block": w.steps_per_iter // B, "rho": w.rho,
                        "parallelism": f"blockensemble-shard x{world}",
-                       "mapping": "wave" if wave else "lane",
+                       "mapping": ("scan" if kname == "k_block_scan" else
+                                   "wave" if wave else "lane"),
                        "rng": "device Philox4x32-10 + Box-Muller (perf mode)"},
             "per_gpu": value / world,
             "accept_rate": accept_rate,

@@ -105,6 +105,13 @@ struct AcceptArgs {
   uint8_t* acc_out;  // [b1-b0] or nullptr
 };
 
+// Timing events attached to the next kernel dispatch (hipExtLaunchKernel): armed by the
+// runtime for a timed launch, consumed (and cleared) by that kernel's launcher.
+struct DispatchEvents {
+  hipEvent_t start = nullptr, stop = nullptr;
+};
+extern thread_local DispatchEvents g_dispatch_events;
+
 // Model/precision dispatch keys.
 struct ModelKey {
   int model, precision, d, m;

@@ -19,6 +19,7 @@
 #include <stdlib.h>
 
 #include <type_traits>
+#include <hip/hip_ext.h>
 #include <algorithm>
 
 #include "dmt_device.h"
@@ -1348,6 +1349,22 @@ __global__ void k_debug_philox(uint64_t seed, const uint32_t* ctr, int64_t n, ui
 // ---------------------------------------------------------------- launchers
 static inline unsigned nblk(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
 
+thread_local DispatchEvents g_dispatch_events;
+
+// Launch; when the runtime has armed dispatch events (timed launch), they are attached to
+// the kernel's own dispatch packet (hipExtLaunchKernel), so the measured time is the
+// kernel's execution as the profiler sees it, without the stream's event-packet overheads.
+template <class... KArgs, class... Args>
+static void dlaunch(void (*k)(KArgs...), dim3 grid, dim3 block, hipStream_t s, Args... args) {
+  if (g_dispatch_events.start) {
+    const DispatchEvents ev = g_dispatch_events;
+    g_dispatch_events = DispatchEvents{};
+    hipExtLaunchKernelGGL(k, grid, block, 0, s, ev.start, ev.stop, 0, args...);
+  } else {
+    hipLaunchKernelGGL(k, grid, block, 0, s, args...);
+  }
+}
+
 constexpr int kChunk = 4;
 
 template <class Mdl, class T>
@@ -1359,9 +1376,9 @@ static hipError_t launch_block_t(int mapping, int mode, const void* args, int64_
   if constexpr (Mdl::kLinear) {  // one workgroup per block, always
     const dim3 sblock(64 * kScanWaves);
     switch (mode) {
-      case MODE_PCN: k_block_scan<Mdl, T, MODE_PCN><<<grid, sblock, 0, s>>>(a); break;
-      case MODE_RECOMPUTE: k_block_scan<Mdl, T, MODE_RECOMPUTE><<<grid, sblock, 0, s>>>(a); break;
-      case MODE_FRESH: k_block_scan<Mdl, T, MODE_FRESH><<<grid, sblock, 0, s>>>(a); break;
+      case MODE_PCN: dlaunch(k_block_scan<Mdl, T, MODE_PCN>, grid, sblock, s, a); break;
+      case MODE_RECOMPUTE: dlaunch(k_block_scan<Mdl, T, MODE_RECOMPUTE>, grid, sblock, s, a); break;
+      case MODE_FRESH: dlaunch(k_block_scan<Mdl, T, MODE_FRESH>, grid, sblock, s, a); break;
       default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -1369,9 +1386,9 @@ static hipError_t launch_block_t(int mapping, int mode, const void* args, int64_
     if (mapping == MAP_WAVE) {
       const dim3 wblock(128);
       switch (mode) {
-        case MODE_PCN: k_block_wave<Mdl, T, MODE_PCN><<<grid, wblock, 0, s>>>(a); break;
-        case MODE_RECOMPUTE: k_block_wave<Mdl, T, MODE_RECOMPUTE><<<grid, wblock, 0, s>>>(a); break;
-        case MODE_FRESH: k_block_wave<Mdl, T, MODE_FRESH><<<grid, wblock, 0, s>>>(a); break;
+        case MODE_PCN: dlaunch(k_block_wave<Mdl, T, MODE_PCN>, grid, wblock, s, a); break;
+        case MODE_RECOMPUTE: dlaunch(k_block_wave<Mdl, T, MODE_RECOMPUTE>, grid, wblock, s, a); break;
+        case MODE_FRESH: dlaunch(k_block_wave<Mdl, T, MODE_FRESH>, grid, wblock, s, a); break;
         default: return hipErrorInvalidValue;
       }
       return hipGetLastError();
@@ -1380,13 +1397,13 @@ static hipError_t launch_block_t(int mapping, int mode, const void* args, int64_
     const bool par = a.Z != nullptr;
     switch (mode) {
       case MODE_PCN:
-        if (par) k_block<Mdl, T, MODE_PCN, true, kChunk><<<grid, block, 0, s>>>(a);
-        else k_block<Mdl, T, MODE_PCN, false, kChunk><<<grid, block, 0, s>>>(a);
+        if (par) dlaunch(k_block<Mdl, T, MODE_PCN, true, kChunk>, grid, block, s, a);
+        else dlaunch(k_block<Mdl, T, MODE_PCN, false, kChunk>, grid, block, s, a);
         break;
-      case MODE_RECOMPUTE: k_block<Mdl, T, MODE_RECOMPUTE, false, kChunk><<<grid, block, 0, s>>>(a); break;
+      case MODE_RECOMPUTE: dlaunch(k_block<Mdl, T, MODE_RECOMPUTE, false, kChunk>, grid, block, s, a); break;
       case MODE_FRESH:
-        if (par) k_block<Mdl, T, MODE_FRESH, true, kChunk><<<grid, block, 0, s>>>(a);
-        else k_block<Mdl, T, MODE_FRESH, false, kChunk><<<grid, block, 0, s>>>(a);
+        if (par) dlaunch(k_block<Mdl, T, MODE_FRESH, true, kChunk>, grid, block, s, a);
+        else dlaunch(k_block<Mdl, T, MODE_FRESH, false, kChunk>, grid, block, s, a);
         break;
       default: return hipErrorInvalidValue;
     }
@@ -1399,9 +1416,9 @@ static hipError_t launch_pathll_t(int mapping, const void* args, int64_t nwaves,
   const BlockArgs<T>& a = *static_cast<const BlockArgs<T>*>(args);
   if (nwaves <= 0) return hipSuccess;
   if (Mdl::kLinear || mapping == MAP_WAVE)
-    k_pathll_wave<Mdl, T><<<dim3((unsigned)nwaves), dim3(64), 0, s>>>(a);
+    dlaunch(k_pathll_wave<Mdl, T>, dim3((unsigned)nwaves), dim3(64), s, a);
   else if constexpr (!Mdl::kLinear)
-    k_pathll<Mdl, T, kChunk><<<dim3((unsigned)nwaves), dim3(64), 0, s>>>(a);
+    dlaunch(k_pathll<Mdl, T, kChunk>, dim3((unsigned)nwaves), dim3(64), s, a);
   return hipGetLastError();
 }
 
@@ -1448,7 +1465,7 @@ hipError_t launch_pathll_kernel(const ModelKey& k, int mapping, const void* args
 hipError_t launch_accept(const AcceptArgs& a, hipStream_t s) {
   const int64_t n = a.b1 - a.b0;
   if (n <= 0) return hipSuccess;
-  k_accept<<<nblk(n, 256), 256, 0, s>>>(a);
+  dlaunch(k_accept, dim3(nblk(n, 256)), dim3(256), s, a);
   return hipGetLastError();
 }
 
@@ -1539,15 +1556,15 @@ hipError_t launch_accept_reduce(const AcceptArgs& a, double* work, double* lb, d
     const int64_t groups = std::max<int64_t>(1, (n + kAccGroup - 1) / kAccGroup);
     if (groups <= kAccGroup) {
       // work layout: [3 * 256] partials, then the counter
-      k_accept_reduce_lb<<<(unsigned)groups, kAccGroup, 0, s>>>(
-          a, lb, reinterpret_cast<unsigned*>(lb + 3 * kAccGroup), out3);
+      dlaunch(k_accept_reduce_lb, dim3((unsigned)groups), dim3(kAccGroup), s, a, lb,
+              reinterpret_cast<unsigned*>(lb + 3 * kAccGroup), out3);
       return hipGetLastError();
     }
   }
   int64_t groups = (n + 1023) / 1024;
   if (groups < 1) groups = 1;
   double* bufs[2] = {work, work + 3 * groups};
-  k_accept_reduce<<<(unsigned)groups, 1024, 0, s>>>(a, bufs[0], groups, out3);
+  dlaunch(k_accept_reduce, dim3((unsigned)groups), dim3(1024), s, a, bufs[0], groups, out3);
   if (groups == 1) return hipGetLastError();
   int cur = 0;
   int64_t m = groups;

@@ -186,20 +186,35 @@ void drain_timing(dmt_ens* h) {
   }
 }
 
+// Times the kernel launched inside the scope.  dispatch = true: the events ride on that
+// kernel's dispatch packet (the launcher uses hipExtLaunchKernel; the time is the kernel's
+// execution, as rocprofv3 reports it); otherwise they are recorded on the stream around it.
 struct TimedScope {
   dmt_ens* h;
   int k;
-  hipEvent_t e0 = nullptr;
-  TimedScope(dmt_ens* h_, int k_) : h(h_), k(k_) {
+  bool dispatch;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  TimedScope(dmt_ens* h_, int k_, bool dispatch_ = true) : h(h_), k(k_), dispatch(dispatch_) {
     if (h->timing >> k & 1u) {
       e0 = get_event(h);
-      (void)hipEventRecord(e0, h->stream);
+      e1 = get_event(h);
+      if (dispatch) {
+        g_dispatch_events.start = e0;
+        g_dispatch_events.stop = e1;
+      } else {
+        (void)hipEventRecord(e0, h->stream);
+      }
     }
   }
   ~TimedScope() {
     if (e0) {
-      hipEvent_t e1 = get_event(h);
-      (void)hipEventRecord(e1, h->stream);
+      if (dispatch && g_dispatch_events.start) {  // no kernel consumed them (empty range)
+        g_dispatch_events = DispatchEvents{};
+        (void)hipEventRecord(e0, h->stream);
+        (void)hipEventRecord(e1, h->stream);
+      } else if (!dispatch) {
+        (void)hipEventRecord(e1, h->stream);
+      }
       h->pending[k].push_back({e0, e1});
       if (h->pending[k].size() > 512) drain_timing(h);
     }
@@ -1284,7 +1299,7 @@ dmt_status dmt_fetch_ll(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int6
   }
   DMT_TRY(ensure_red_work(h, b1 - b0));
   {
-    TimedScope ts(h, DMT_K_REDUCE);
+    TimedScope ts(h, DMT_K_REDUCE, false);  // several tree launches
     HIP_OK(launch_block_sum(L->d_ll + b0, L->d_llp + b0, acc, b1 - b0, h->d_red_work, h->d_red,
                             h->stream));
   }

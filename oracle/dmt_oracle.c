@@ -309,6 +309,16 @@ static int solve_segment_scan(int d, int m, const REAL* th, const REAL* sg, cons
     return ok;
 }
 
+/* CPU-baseline switch (bench.py's cpu_baseline only): 1 = evaluate linear-drift segments
+ * with the plain step-by-step Euler loop — the natural CPU algorithm, as the reference runs
+ * it — instead of the canonical chunked scan (equal up to rounding; not used for parity). */
+#if IS_F64
+int orc_sequential_ou = 0;
+void orc_set_sequential_ou(int on) { orc_sequential_ou = on; }
+#else
+extern int orc_sequential_ou;
+#endif
+
 /* GP.solve_and_ll!(X, W, P, y1): Euler–Maruyama guided solve with given W and
  * the Girsanov sum.  Returns 1 on success (finite end point and ll). */
 int SFX(orc_solve_segment)(int model, int d, int m, const double* law, int npts,
@@ -317,7 +327,7 @@ int SFX(orc_solve_segment)(int model, int d, int m, const double* law, int npts,
     int h = d * (d + 1) / 2;
     REAL th[16], sg[9], a[6], Bt[9], beta[3], da[6]; int trace;
     load_law(law, d, m, th, sg, a, Bt, beta, da, &trace);
-    if (model == ORC_OU)
+    if (model == ORC_OU && !orc_sequential_ou)
         return solve_segment_scan(d, m, th, sg, a, Bt, beta, da, trace, npts, t, H, F, W, y1,
                                   X, ll_out);
     REAL x[3];

@@ -74,6 +74,8 @@ def _load():
     lib.orc_normal_pair_f64.restype = None
     lib.orc_exp1.argtypes = [u64, u32, u32, u32]
     lib.orc_exp1.restype = d_
+    lib.orc_set_sequential_ou.argtypes = [i_]
+    lib.orc_set_sequential_ou.restype = None
     lib.orc_philox_raw.argtypes = [u64, P, P]
     lib.orc_philox_raw.restype = None
     return lib
@@ -189,9 +191,12 @@ def pairwise_tree(vals):
 
 
 def draw_terminal_blocks(model, d, m, npts, laws, t, H, F, Xacc, Wacc, rho, Z=None, seed=0,
-                         it=0, salt=0, prec=0, nthreads=1, t_shared=True, H_shared=False):
+                         it=0, salt=0, prec=0, nthreads=1, t_shared=True, H_shared=False,
+                         sequential=False):
     """Whole-ensemble draw for single-segment terminal blocks, OpenMP over blocks
-    (the timed CPU baseline).  Arrays in reference layout."""
+    (the timed CPU baseline).  Arrays in reference layout.  sequential=True: linear-drift
+    segments by the plain Euler loop (the CPU algorithm), not the canonical scan."""
+    lib.orc_set_sequential_ou(1 if sequential else 0)
     dt = _dt(prec)
     B = laws.shape[0]
     t = np.ascontiguousarray(t, dtype=dt)
@@ -210,6 +215,7 @@ def draw_terminal_blocks(model, d, m, npts, laws, t, H, F, Xacc, Wacc, rho, Z=No
         model, d, m, B, npts, _p(laws), LAW_STRIDE, _p(t), 0 if t_shared else npts, _p(H),
         0 if H_shared else npts * hp, _p(F), npts * d, _p(Xacc), _p(Wacc),
         None if Zp is None else _p(Zp), seed, it, salt, _p(rho), _p(Xo), _p(Wo), _p(ll), nthreads)
+    lib.orc_set_sequential_ou(0)
     return Xo, Wo, ll, nfail
 
 
