@@ -52,8 +52,9 @@ struct BlockArgs {
   const int32_t* seg_q;      // [G] first point of the segment within its recording
   const int32_t* seg_np;     // [G] points of the segment
   const int64_t* st_off;     // [G] first step of the segment in reference (Z) order
-  const uint8_t* selX;       // [G] physical buffer holding u.XX[g]; u° holds the other
-  const uint8_t* selW;
+  uint8_t* selX;             // [G] physical buffer holding u.XX[g]; u° holds the other
+                             // (the lane kernel re-points them when it moves a path)
+  uint8_t* selW;
   const uint8_t* selPP;
   const uint8_t* selPPB;
   T* X[2];

@@ -54,8 +54,8 @@ template <class Mdl, class T, int MODE, bool PARITY, int K>
 __device__ __forceinline__ bool run_segment(const Law<Mdl, T>& L, const T* __restrict__ tpl,
                                             const int t_sh, const T* __restrict__ Ht,
                                             const int H_sh, const T* __restrict__ Ft,
-                                            const T* __restrict__ Ws, T* __restrict__ Wd,
-                                            T* __restrict__ Xd, const double* __restrict__ Zg,
+                                            const T* Ws, T* Wd, T* Xd, const double* __restrict__ Zg,
+                                            const T* Xcs, T* Xcd, T* Wcd,
                                             NormalStream<T>& ns, const int64_t tq, const int64_t q0,
                                             const int np, const int lane, const T rho,
                                             const T srho, T* x, T& sl) {
@@ -72,21 +72,36 @@ __device__ __forceinline__ bool run_segment(const Law<Mdl, T>& L, const T* __res
   const T* Wsb = Ws + row * M * kLanes + lane;
   T* Wdb = Wd + row * M * kLanes + lane;
   T* Xdb = Xd + row * D * kLanes + lane;
+  // tile-phase repair: a lane whose u lives in the "wrong" buffer copies u.X
+  // (Xcs -> Xcd) and u.W (-> Wcd) to the tile's u buffer while its proposal goes to the
+  // tile's proposal buffer; nullptr = nothing to copy
+  const bool cpx = Xcd != nullptr, cpw = Wcd != nullptr;
+  const T* Xcsb = cpx ? Xcs + row * D * kLanes + lane : nullptr;
+  T* Xcdb = cpx ? Xcd + row * D * kLanes + lane : nullptr;
+  T* Wcdb = cpw ? Wcd + row * M * kLanes + lane : nullptr;
 
   // W planes hold increments: row 0 = W(t0), row i+1 = dW_i
   const int nst = np - 1;
   T tcur = tb[0];
+  if (cpx) {
+#pragma unroll
+    for (int p = 0; p < D; ++p) Xcdb[p * kLanes] = Xcsb[p * kLanes];
+  }
 #pragma unroll
   for (int p = 0; p < D; ++p) Xdb[p * kLanes] = x[p];
   if (DRAW) {
 #pragma unroll
-    for (int k = 0; k < M; ++k) Wdb[k * kLanes] = rho * (READW ? Wsb[k * kLanes] : (T)0);
+    for (int k = 0; k < M; ++k) {
+      const T w0 = READW ? Wsb[k * kLanes] : (T)0;
+      if (cpw) Wcdb[k * kLanes] = w0;
+      Wdb[k * kLanes] = rho * w0;
+    }
   }
   PSum<T> ps;
   ps.init();
 
   struct Chunk {
-    T t[K], H[K][HP], F[K][D], W[K][M], Z[K][M];
+    T t[K], H[K][HP], F[K][D], W[K][M], Z[K][M], Xu[K][D];
   };
   auto load = [&](int c0, Chunk& c) {
 #pragma unroll
@@ -102,12 +117,21 @@ __device__ __forceinline__ bool run_segment(const Law<Mdl, T>& L, const T* __res
         c.W[j][k] = READW ? Wsb[((i + 1) * M + k) * kLanes] : (T)0;
         c.Z[j][k] = (PARITY && DRAW) ? (T)Zg[i * M + k] : (T)0;
       }
+      if (cpx) {  // u.X of the points this chunk overwrites (read before they are)
+#pragma unroll
+        for (int e = 0; e < D; ++e) c.Xu[j][e] = Xcsb[((i + 1) * D + e) * kLanes];
+      }
     }
   };
   // one Euler step from registers; returns the Girsanov term G·dt
-  auto step = [&](int i, T tn, const T* Hi, const T* Fi, const T* Wi, const T* Zi) -> T {
+  auto step = [&](int i, T tn, const T* Hi, const T* Fi, const T* Wi, const T* Zi,
+                  const T* Xui) -> T {
     const T dt = tn - tcur;
     T dW[M];
+    if (cpx) {
+#pragma unroll
+      for (int e = 0; e < D; ++e) Xcdb[((int64_t)(i + 1) * D + e) * kLanes] = Xui[e];
+    }
     if (!DRAW) {
 #pragma unroll
       for (int k = 0; k < M; ++k) dW[k] = Wi[k];
@@ -115,6 +139,7 @@ __device__ __forceinline__ bool run_segment(const Law<Mdl, T>& L, const T* __res
       const T sdt = sqrt(dt);
 #pragma unroll
       for (int k = 0; k < M; ++k) {
+        if (cpw) Wcdb[((int64_t)(i + 1) * M + k) * kLanes] = Wi[k];
         dW[k] = dfma(rho, Wi[k], srho * (sdt * Zi[k]));
         Wdb[((int64_t)(i + 1) * M + k) * kLanes] = dW[k];
       }
@@ -150,14 +175,16 @@ __device__ __forceinline__ bool run_segment(const Law<Mdl, T>& L, const T* __res
       T gv[K];
 #pragma unroll
       for (int j = 0; j < K; ++j)
-        gv[j] = step(c0 + j, cur.t[j], cur.H[j], cur.F[j], cur.W[j], cur.Z[j]);
+        gv[j] = step(c0 + j, cur.t[j], cur.H[j], cur.F[j], cur.W[j], cur.Z[j], cur.Xu[j]);
       ps.template add_subtree<Log2<K>::v>(tree_sum<T, K>(gv));
       cur = nxt;
     }
   }
   for (int i = nfull; i < nst; ++i) {  // tail (< K steps): single-step path
     const int64_t q = i;
-    T Hi[HP], Fi[D], Wi[M], Zi[M];
+    T Hi[HP], Fi[D], Wi[M], Zi[M], Xui[D];
+#pragma unroll
+    for (int e = 0; e < D; ++e) Xui[e] = cpx ? Xcsb[((q + 1) * D + e) * kLanes] : (T)0;
 #pragma unroll
     for (int e = 0; e < HP; ++e) Hi[e] = Hb[(q * HP + e) * hst];
 #pragma unroll
@@ -167,7 +194,7 @@ __device__ __forceinline__ bool run_segment(const Law<Mdl, T>& L, const T* __res
       Wi[k] = READW ? Wsb[((q + 1) * M + k) * kLanes] : (T)0;
       Zi[k] = DRAW ? (PARITY ? (T)Zg[q * M + k] : ns.get((uint32_t)(i * M + k))) : (T)0;
     }
-    ps.add(step(i, tb[(q + 1) * tst], Hi, Fi, Wi, Zi));
+    ps.add(step(i, tb[(q + 1) * tst], Hi, Fi, Wi, Zi, Xui));
   }
   sl = ps.finish();
   bool ok = isfinite(sl);
@@ -190,6 +217,9 @@ __device__ __forceinline__ bool map_block(const BlockArgs<T>& a, int64_t& tile, 
   if (blk >= a.blk_off[r + 1] || blk < a.b0 || blk >= a.b1) return false;
   return true;
 }
+
+// tile-phase repair only while the minority is at most 1/kRepairMaxMinority of the wave
+constexpr int kRepairMaxMinority = 4;
 
 template <class Mdl, class T, int MODE, bool PARITY, int K>
 __global__ __launch_bounds__(64) void k_block(const BlockArgs<T> a) {
@@ -234,13 +264,41 @@ __global__ __launch_bounds__(64) void k_block(const BlockArgs<T> a) {
     NormalStream<T> ns;
     ns.init(a.seed, (uint32_t)g + a.seg_base, a.iter, a.salt);
     const double* Zg = a.Z ? a.Z + a.st_off[g] * M : nullptr;
-    T* Xd = a.X[a.selX[g] ^ a.xd_flip];
-    const T* Ws = a.W[a.selW[g] ^ a.ws_flip];
-    T* Wd = a.W[a.selW[g] ^ a.wd_flip];
+    const int sx = a.selX[g], sw = a.selW[g];
+    T* Xd = a.X[sx ^ a.xd_flip];
+    const T* Ws = a.W[sw ^ a.ws_flip];
+    T* Wd = a.W[sw ^ a.wd_flip];
+    const T* Xcs = nullptr;
+    T *Xcd = nullptr, *Wcd = nullptr;
+    int nsx = sx, nsw = sw;
+    if (MODE == MODE_PCN) {
+      // Tile-phase repair: proposals of all active lanes go to the buffer opposite the
+      // majority's u; a minority lane first moves its u there (copy during the sweep) and
+      // re-points its selector, so the wave's stores stay full-line.
+      // Only worth it while the minority is small: a copied lane costs its path once more
+      // (read u.X, write u.X and u.W), mixed lanes cost partial lines for the whole wave.
+      const uint64_t act = __ballot(1);
+      const int nact = __popcll(act);
+      const int ox = __popcll(__ballot(sx != 0)), ow = __popcll(__ballot(sw != 0));
+      const int px = 2 * ox > nact ? 1 : 0, pw = 2 * ow > nact ? 1 : 0;
+      const int mx = px ? nact - ox : ox, mw = pw ? nact - ow : ow;  // minority sizes
+      if (kRepairMaxMinority * mx <= nact) {
+        Xd = a.X[px ^ a.xd_flip];
+        if (sx != px) { Xcs = a.X[sx ^ a.xs_flip]; Xcd = a.X[px ^ a.xs_flip]; nsx = px; }
+      }
+      if (kRepairMaxMinority * mw <= nact) {
+        Wd = a.W[pw ^ a.wd_flip];
+        if (sw != pw) { Wcd = a.W[pw ^ a.ws_flip]; nsw = pw; }
+      }
+    }
     T sl;
     const bool sok = run_segment<Mdl, T, MODE, PARITY, K>(
         L, a.t, a.t_shared, a.H[ls][kind], a.H_shared[ls][kind], a.F[ls][kind], Ws, Wd, Xd, Zg,
-        ns, tq, a.seg_q[g], a.seg_np[g], lane, rho, srho, x, sl);
+        Xcs, Xcd, Wcd, ns, tq, a.seg_q[g], a.seg_np[g], lane, rho, srho, x, sl);
+    if (MODE == MODE_PCN) {
+      if (nsx != sx) a.selX[g] = (uint8_t)nsx;
+      if (nsw != sw) a.selW[g] = (uint8_t)nsw;
+    }
     if (!sok) { ok = false; break; }
     ll = ll + sl;
   }
