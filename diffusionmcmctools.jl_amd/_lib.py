@@ -27,12 +27,13 @@ BLK_LL, BLK_LLPROP, BLK_LL_HIST, BLK_LLPROP_HIST, BLK_ACC_HIST = 0, 1, 2, 3, 4
 K_DRAW, K_ACCEPT, K_PATHLL, K_RECOMPUTE, K_REDUCE = 0, 1, 2, 3, 4
 LAW_STRIDE = 64
 LAW_THETA, LAW_SIGMA, LAW_A, LAW_BT, LAW_BETA, LAW_DA, LAW_C0, LAW_TRACE = 0, 16, 25, 31, 40, 43, 49, 50
+LAW_SIGINV = 51
 
 # exported symbols (checked against include/dmt.h by tests/test_abi.py)
 SYMBOLS = [
     "dmt_create", "dmt_destroy", "dmt_upload_grid", "dmt_upload_law", "dmt_set_paths",
     "dmt_download_paths", "dmt_draw_unit", "dmt_create_layout", "dmt_layout_size",
-    "dmt_draw_proposal", "dmt_accept_reject", "dmt_loglikhd", "dmt_recompute_path", "dmt_swap",
+    "dmt_draw_proposal", "dmt_accept_reject", "dmt_loglikhd", "dmt_recompute_path", "dmt_find_W_for_X", "dmt_swap",
     "dmt_save_ll", "dmt_set_accepted", "dmt_get_block_state", "dmt_set_block_state",
     "dmt_fetch_ll", "dmt_mcmc_step", "dmt_mcmc_run", "dmt_guiding_linear", "dmt_comm_unique_id", "dmt_comm_init", "dmt_set_shard", "dmt_sync",
     "dmt_set_timing", "dmt_get_timing", "dmt_memory_bytes", "dmt_debug_philox",
@@ -89,6 +90,7 @@ _SIGS = {
     "dmt_accept_reject": [_P, _i32, _i64, _i64, _pd, _i64, _u32, _pu8],
     "dmt_loglikhd": [_P, _i32, _i32, _i64, _i64],
     "dmt_recompute_path": [_P, _i32, _i64, _i64, _i32, _pu8],
+    "dmt_find_W_for_X": [_P, _i32, _i64, _i64],
     "dmt_swap": [_P, _i32, _i32, _i64, _i64],
     "dmt_save_ll": [_P, _i32, _i64, _i64, _i64],
     "dmt_set_accepted": [_P, _i32, _i64, _i64, _i64, _pu8],

@@ -192,6 +192,11 @@ class _BlockRange:
         under u°'s laws with u's Wiener path; ll° stored.  Returns per-block success."""
         return self._call("recompute_path", skip=skip, want_success=True)
 
+    def find_W_for_X(self):
+        """``find_W_for_X!`` (src/block.jl:118-131): u.WW ← the Wiener increments that reproduce
+        u.XX under the accepted laws u.PP (+ P_last) — DD.invsolve!, parallel in time."""
+        self._call("find_W_for_X")
+
     def save_ll(self, i):
         self._call("save_ll", i)
 

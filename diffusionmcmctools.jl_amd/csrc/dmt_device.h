@@ -35,6 +35,7 @@ template <class T, int D_, int M_>
 struct OU {
   static constexpr int D = D_, M = M_, NTH = 12;
   static constexpr bool kLinear = true;  // drift folded into the guiding coefficients
+  static constexpr int kNoiseCoord = -1;  // σ invertible (d = m)
   // theta: Theta (d×d row-major) at 0, mu at 9
   __device__ __forceinline__ static void drift(const T* th, const T* x, T* b) {
     T y[D];
@@ -54,6 +55,7 @@ template <class T>
 struct FHN {
   static constexpr int D = 2, M = 1, NTH = 4;
   static constexpr bool kLinear = false;
+  static constexpr int kNoiseCoord = 1;  // hypoelliptic: the noise enters coordinate 1 only
   // theta: 1/eps, s, gamma, beta
   __device__ __forceinline__ static void drift(const T* th, const T* x, T* b) {
     T y = x[0], v = x[1];
@@ -68,6 +70,7 @@ template <class T>
 struct Lorenz {
   static constexpr int D = 3, M = 3, NTH = 3;
   static constexpr bool kLinear = false;
+  static constexpr int kNoiseCoord = -1;
   // theta: s, r, beta
   __device__ __forceinline__ static void drift(const T* th, const T* x, T* b) {
     b[0] = th[0] * (x[1] - x[0]);
@@ -254,6 +257,40 @@ __device__ __forceinline__ void affine_apply(const T* A, const T* e, const T* x,
 #pragma unroll
     for (int c = 0; c < D; ++c) u = dfma(A[p * D + c], x[c], u);
     y[p] = u;
+  }
+}
+
+// One step of DD.invsolve! (find_W_for_X!): the increment that maps x to xn under the guided
+// Euler step, canonical order:
+//   r_a  = fma(−bg_a, dt, xn_a − x_a)      (bg = c − Mx [+ b(x)], as in euler_step)
+//   ΔW_k = σinv_k0·r_0 ; fma(σinv_ka, r_a, ·)     (d = m)
+//   ΔW_0 = r_j / σ_j0                             (one noise on coordinate j = kNoiseCoord)
+template <class Mdl, class T>
+__device__ __forceinline__ void inv_step(const Law<Mdl, T>& L, const T* siginv, const T* Hi,
+                                         const T* Fi, T dt, const T* x, const T* xn, T* dW) {
+  constexpr int D = Mdl::D, M = Mdl::M;
+  T Mg[D * D], cg[D], b[D];
+  guide_coeffs<Mdl, T>(L, Hi, Fi, Mg, cg);
+  if (!Mdl::kLinear) Mdl::drift(L.th, x, b);
+  T r[D];
+#pragma unroll
+  for (int p = 0; p < D; ++p) {
+    T u = cg[p];
+#pragma unroll
+    for (int q = 0; q < D; ++q) u = dfma(-Mg[p * D + q], x[q], u);
+    const T bg = Mdl::kLinear ? u : (b[p] + u);
+    r[p] = dfma(-bg, dt, xn[p] - x[p]);
+  }
+  if constexpr (Mdl::kNoiseCoord >= 0) {
+    dW[0] = r[Mdl::kNoiseCoord] / L.sg[Mdl::kNoiseCoord * M + 0];
+  } else {
+#pragma unroll
+    for (int k = 0; k < M; ++k) {
+      T v = siginv[k * D + 0] * r[0];
+#pragma unroll
+      for (int a = 1; a < D; ++a) v = dfma(siginv[k * D + a], r[a], v);
+      dW[k] = v;
+    }
   }
 }
 

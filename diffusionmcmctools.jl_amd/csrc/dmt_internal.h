@@ -121,6 +121,8 @@ struct ModelKey {
 // launchers (dmt_kernels.hip)
 hipError_t launch_block_kernel(const ModelKey& k, int mapping, int mode, const void* args,
                                int64_t nwaves, hipStream_t s);
+hipError_t launch_invsolve_kernel(const ModelKey& k, int mapping, const void* args,
+                                  int64_t nwaves, hipStream_t s);
 hipError_t launch_pathll_kernel(const ModelKey& k, int mapping, const void* args, int64_t nwaves,
                                 hipStream_t s);
 hipError_t launch_accept(const AcceptArgs& a, hipStream_t s);

@@ -1469,6 +1469,120 @@ static hipError_t launch_block_t(int mapping, int mode, const void* args, int64_
   }
 }
 
+// find_W_for_X! on the lane layout: lane = recording tile slot, steps in order (x carried).
+template <class Mdl, class T>
+__global__ __launch_bounds__(64) void k_invsolve(const BlockArgs<T> a) {
+  constexpr int D = Mdl::D, M = Mdl::M, HP = D * (D + 1) / 2;
+  int64_t tile, blk;
+  if (!map_block(a, tile, blk)) return;
+  const int lane = threadIdx.x;
+  const int64_t tq = a.tile_qoff[tile];
+  auto idx = [&](int64_t q, int c, int C) -> int64_t { return ((tq + q) * C + c) * kLanes + lane; };
+  auto tload = [&](int64_t q) -> T { return a.t_shared ? a.t[q] : a.t[idx(q, 0, 1)]; };
+  const int g0 = a.gfirst[blk], g1 = a.glast[blk];
+  const bool term = a.term[blk] != 0;
+  for (int g = g0; g <= g1; ++g) {
+    const int kind = (!term && g == g1) ? 1 : 0;
+    const int ls = (kind ? a.selPPB[g] : a.selPP[g]) ^ a.law_flip;
+    const double* lr = a.law[ls][kind] + (int64_t)g * DMT_LAW_STRIDE;
+    Law<Mdl, T> L;
+    L.load(lr);
+    T siginv[D * D];
+#pragma unroll
+    for (int c = 0; c < D * D; ++c) siginv[c] = (T)lr[DMT_LAW_SIGINV + c];
+    const T* Ht = a.H[ls][kind];
+    const T* Ft = a.F[ls][kind];
+    const int Hsh = a.H_shared[ls][kind];
+    const T* Xs = a.X[a.selX[g] ^ a.xs_flip];
+    T* Wd = a.W[a.selW[g] ^ a.wd_flip];
+    const int64_t q0 = a.seg_q[g];
+    const int nst = a.seg_np[g] - 1;
+#pragma unroll
+    for (int k = 0; k < M; ++k) Wd[idx(q0, k, M)] = (T)0;  // W(t0) = 0
+    T x[D];
+#pragma unroll
+    for (int c = 0; c < D; ++c) x[c] = Xs[idx(q0, c, D)];
+    T tcur = tload(q0);
+    for (int i = 0; i < nst; ++i) {
+      const int64_t q = q0 + i;
+      T Hi[HP], Fi[D], xn[D], dW[M];
+#pragma unroll
+      for (int c = 0; c < HP; ++c) Hi[c] = Hsh ? Ht[q * HP + c] : Ht[idx(q, c, HP)];
+#pragma unroll
+      for (int c = 0; c < D; ++c) { Fi[c] = Ft[idx(q, c, D)]; xn[c] = Xs[idx(q + 1, c, D)]; }
+      const T tn = tload(q + 1);
+      inv_step<Mdl, T>(L, siginv, Hi, Fi, tn - tcur, x, xn, dW);
+#pragma unroll
+      for (int k = 0; k < M; ++k) Wd[idx(q + 1, k, M)] = dW[k];
+#pragma unroll
+      for (int c = 0; c < D; ++c) x[c] = xn[c];
+      tcur = tn;
+    }
+  }
+}
+
+// find_W_for_X! on the wave layout: a wave per block, 64 consecutive steps per pass.
+template <class Mdl, class T>
+__global__ __launch_bounds__(64) void k_invsolve_wave(const BlockArgs<T> a) {
+  constexpr int D = Mdl::D, M = Mdl::M, HP = D * (D + 1) / 2;
+  const int lane = threadIdx.x;
+  const int64_t blk = a.b0 + (int64_t)blockIdx.x;
+  if (blk >= a.b1) return;
+  const int64_t r = a.blk_rec[blk];
+  const int64_t tq = a.tile_qoff[r];
+  const int g0 = a.gfirst[blk], g1 = a.glast[blk];
+  const bool term = a.term[blk] != 0;
+  for (int g = g0; g <= g1; ++g) {
+    const int kind = (!term && g == g1) ? 1 : 0;
+    const int ls = (kind ? a.selPPB[g] : a.selPP[g]) ^ a.law_flip;
+    const double* lr = a.law[ls][kind] + (int64_t)g * DMT_LAW_STRIDE;
+    Law<Mdl, T> L;
+    L.load(lr);
+    T siginv[D * D];
+#pragma unroll
+    for (int c = 0; c < D * D; ++c) siginv[c] = (T)lr[DMT_LAW_SIGINV + c];
+    const int64_t q0 = a.seg_q[g], row = tq + q0;
+    const T* tb = a.t_shared ? a.t + q0 : a.t + row;
+    const T* Hb = a.H_shared[ls][kind] ? a.H[ls][kind] + q0 * HP : a.H[ls][kind] + row * HP;
+    const T* Fb = a.F[ls][kind] + row * D;
+    const T* Xb = a.X[a.selX[g] ^ a.xs_flip] + row * D;
+    T* Wb = a.W[a.selW[g] ^ a.wd_flip] + row * M;
+    const int nst = a.seg_np[g] - 1;
+    if (lane == 0) {
+#pragma unroll
+      for (int k = 0; k < M; ++k) Wb[k] = (T)0;  // W(t0) = 0
+    }
+    for (int c0 = 0; c0 < nst; c0 += 64) {
+      const int i = c0 + lane;
+      if (i < nst) {
+        T Hi[HP], Fi[D], x[D], xn[D], dW[M];
+#pragma unroll
+        for (int c = 0; c < HP; ++c) Hi[c] = Hb[(int64_t)i * HP + c];
+#pragma unroll
+        for (int c = 0; c < D; ++c) {
+          Fi[c] = Fb[(int64_t)i * D + c];
+          x[c] = Xb[(int64_t)i * D + c];
+          xn[c] = Xb[(int64_t)(i + 1) * D + c];
+        }
+        inv_step<Mdl, T>(L, siginv, Hi, Fi, tb[i + 1] - tb[i], x, xn, dW);
+#pragma unroll
+        for (int k = 0; k < M; ++k) Wb[(int64_t)(i + 1) * M + k] = dW[k];
+      }
+    }
+  }
+}
+
+template <class Mdl, class T>
+static hipError_t launch_invsolve_t(int mapping, const void* args, int64_t nwaves, hipStream_t s) {
+  const BlockArgs<T>& a = *static_cast<const BlockArgs<T>*>(args);
+  if (nwaves <= 0) return hipSuccess;
+  if (Mdl::kLinear || mapping == MAP_WAVE)
+    dlaunch(k_invsolve_wave<Mdl, T>, dim3((unsigned)nwaves), dim3(64), s, a);
+  else
+    dlaunch(k_invsolve<Mdl, T>, dim3((unsigned)nwaves), dim3(64), s, a);
+  return hipGetLastError();
+}
+
 template <class Mdl, class T>
 static hipError_t launch_pathll_t(int mapping, const void* args, int64_t nwaves, hipStream_t s) {
   const BlockArgs<T>& a = *static_cast<const BlockArgs<T>*>(args);
@@ -1513,6 +1627,11 @@ static hipError_t launch_pathll_t(int mapping, const void* args, int64_t nwaves,
 hipError_t launch_block_kernel(const ModelKey& k, int mapping, int mode, const void* args,
                                int64_t nwaves, hipStream_t s) {
   DMT_DISPATCH(k, (launch_block_t<Mdl, T>(mapping, mode, args, nwaves, s)));
+}
+
+hipError_t launch_invsolve_kernel(const ModelKey& k, int mapping, const void* args,
+                                  int64_t nwaves, hipStream_t s) {
+  DMT_DISPATCH(k, (launch_invsolve_t<Mdl, T>(mapping, args, nwaves, s)));
 }
 
 hipError_t launch_pathll_kernel(const ModelKey& k, int mapping, const void* args, int64_t nwaves,

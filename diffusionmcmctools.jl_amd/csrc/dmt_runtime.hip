@@ -329,7 +329,7 @@ void fill_common(dmt_ens* h, const Layout* L, BlockArgs<T>& a) {
 dmt_status run_block_kernel(dmt_ens* h, const Layout* L, int mode, int kind_timer, int64_t b0,
                             int64_t b1, int law_flip, int xs, int xd, int ws, int wd,
                             const double* dZ, int64_t iter, uint32_t salt, double* ll_out,
-                            uint8_t* success, bool pathll) {
+                            uint8_t* success, int op /* 0 draw/solve, 1 loglikhd, 2 invsolve */) {
   if (b1 <= b0) return DMT_OK;
   const int64_t r0 = rec_of_block(L, b0), r1 = rec_of_block(L, b1 - 1);
   const int64_t tile0 = r0 / kLanes, tile1 = r1 / kLanes + 1;
@@ -357,13 +357,15 @@ dmt_status run_block_kernel(dmt_ens* h, const Layout* L, int mode, int kind_time
   if (h->key.precision == DMT_F64) {
     BlockArgs<double> a{};
     fill(a);
-    e = pathll ? launch_pathll_kernel(h->key, h->mapping, &a, nwaves, h->stream)
-               : launch_block_kernel(h->key, h->mapping, mode, &a, nwaves, h->stream);
+    e = op == 1 ? launch_pathll_kernel(h->key, h->mapping, &a, nwaves, h->stream)
+        : op == 2 ? launch_invsolve_kernel(h->key, h->mapping, &a, nwaves, h->stream)
+                  : launch_block_kernel(h->key, h->mapping, mode, &a, nwaves, h->stream);
   } else {
     BlockArgs<float> a{};
     fill(a);
-    e = pathll ? launch_pathll_kernel(h->key, h->mapping, &a, nwaves, h->stream)
-               : launch_block_kernel(h->key, h->mapping, mode, &a, nwaves, h->stream);
+    e = op == 1 ? launch_pathll_kernel(h->key, h->mapping, &a, nwaves, h->stream)
+        : op == 2 ? launch_invsolve_kernel(h->key, h->mapping, &a, nwaves, h->stream)
+                  : launch_block_kernel(h->key, h->mapping, mode, &a, nwaves, h->stream);
   }
   if (e != hipSuccess) return fail(DMT_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(e));
   return DMT_OK;
@@ -1181,6 +1183,18 @@ dmt_status dmt_recompute_path(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1
     HIP_OK(hipMemcpyAsync(success_out, L->d_success + b0, b1 - b0, hipMemcpyDeviceToHost, h->stream));
     HIP_OK(hipStreamSynchronize(h->stream));
   }
+  return DMT_OK;
+}
+
+dmt_status dmt_find_W_for_X(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1) {
+  DMT_TRY(check_h(h));
+  Layout* L;
+  DMT_TRY(get_layout(h, layout, &L));
+  DMT_TRY(check_range(L, b0, b1));
+  DMT_TRY(law_ready(h, 0, L, b0, b1));
+  // laws u.PP (+ P_last) (flip 0); read u.XX (flip 0); write u.WW in place (flip 0)
+  DMT_TRY(run_block_kernel(h, L, MODE_RECOMPUTE, DMT_K_RECOMPUTE, b0, b1, 0, 0, 0, 0, 0, nullptr, 0,
+                           0, nullptr, nullptr, 2));
   return DMT_OK;
 }
 

@@ -160,6 +160,10 @@ class Ensemble:
         L.call("dmt_recompute_path", self._h, layout, b0, b1, int(skip), L.u8p(ok))
         return None if ok is None else ok.astype(bool)
 
+    def find_W_for_X(self, layout, b0, b1):
+        """find_W_for_X!: u.WW ← the increments reproducing u.XX under u's laws."""
+        L.call("dmt_find_W_for_X", self._h, layout, b0, b1)
+
     def swap(self, layout, what, b0, b1):
         L.call("dmt_swap", self._h, layout, int(what), b0, b1)
 

@@ -15,7 +15,7 @@ using StaticArrays
 
 import DiffusionMCMCTools: draw_proposal_path!, accept_reject_proposal_path!, loglikhd!,
     loglikhd°!, fetch_ll, fetch_ll°, save_ll!, set_accepted!, swap_paths!, swap_XX!,
-    swap_WW!, swap_PP!, swap_ll!, ll_of_accepted, accpt_rate, recompute_path!
+    swap_WW!, swap_PP!, swap_ll!, ll_of_accepted, accpt_rate, recompute_path!, find_W_for_X!
 
 export DeviceSamplingEnsemble, DeviceBlockEnsemble, DeviceBlockCollection, DeviceBiBlock,
     mcmc_step!, mcmc_run!, download_XX, download_WW
@@ -269,6 +269,10 @@ function recompute_path!(x::DeviceBlocks; skip=0)
         x.se.h, x.layout, x.b0, x.b1, skip, ok))
     Bool.(ok)
 end
+
+"find_W_for_X!(b) (src/block.jl:118-131): u.WW from u.XX under the accepted laws."
+find_W_for_X!(x::DeviceBlocks) = check(ccall((:dmt_find_W_for_X, libdmt), Int32,
+    (Ptr{Cvoid}, Int32, Int64, Int64), x.se.h, x.layout, x.b0, x.b1))
 
 # ---- swaps, histories (src/biblock.jl:135-259)
 _swap!(x, what) = check(ccall((:dmt_swap, libdmt), Int32,

@@ -77,6 +77,8 @@ class Model:
         rec[L.LAW_DA:L.LAW_DA + hp] = packed(da)
         rec[L.LAW_C0] = c0
         rec[L.LAW_TRACE] = 1.0 if np.any(da != 0.0) else 0.0
+        if self.d == self.m:  # σ⁻¹ for find_W_for_X! (invsolve)
+            rec[L.LAW_SIGINV:L.LAW_SIGINV + self.d * self.d] = np.linalg.inv(sg).ravel()
         return rec
 
     def simulate(self, t, x0, rng, substeps=1):

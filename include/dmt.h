@@ -91,6 +91,8 @@ enum { DMT_K_DRAW = 0, DMT_K_ACCEPT = 1, DMT_K_PATHLL = 2, DMT_K_RECOMPUTE = 3,
  *   [43,49) da     packed a − ã (used only when trace != 0)
  *   49      c0     c(t0) of the segment's guiding term (for loglikhd_obs)
  *   50      trace  1.0 if a ≠ ã (adds −½ tr[(a−ã)(H−rrᵀ)] to G)
+ *   [51,60) siginv σ⁻¹ (d×d row-major) when d = m (find_W_for_X!; unused for FHN, whose
+ *                  single noise enters coordinate 1)
  */
 #define DMT_LAW_STRIDE 64
 #define DMT_LAW_THETA 0
@@ -101,6 +103,7 @@ enum { DMT_K_DRAW = 0, DMT_K_ACCEPT = 1, DMT_K_PATHLL = 2, DMT_K_RECOMPUTE = 3,
 #define DMT_LAW_DA 43
 #define DMT_LAW_C0 49
 #define DMT_LAW_TRACE 50
+#define DMT_LAW_SIGINV 51
 
 typedef struct {
     int32_t model;      /* DMT_MODEL_* */
@@ -195,6 +198,14 @@ dmt_status dmt_loglikhd(dmt_ens* h, int32_t layout, int32_t unit, int64_t b0, in
  * (src/biblock.jl:343): re-solve u° under u°.PP with the accepted Wiener paths. */
 dmt_status dmt_recompute_path(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
                               int32_t skip, uint8_t* success_out);
+
+/* find_W_for_X!(b) (src/block.jl:118-131, BiBlock src/biblock.jl:300, broadcasts
+ * src/block_collection.jl:229, src/block_ensemble.jl:212): the Wiener increments that
+ * reproduce the accepted path u.XX under the accepted laws u.PP (+ P_last), written to
+ * u.WW in place — DD.invsolve! restated:
+ *   ΔW_i = σ⁻¹ (x_{i+1} − x_i − b°(t_i, x_i)·dt_i)   (FHN: on coordinate 1, / σ_1),
+ * W(t0) = 0.  Parallel in time. */
+dmt_status dmt_find_W_for_X(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1);
 
 /* swap_XX!/swap_WW!/swap_PP!/swap_ll! (src/biblock.jl:148-209), what = DMT_SWAP_* mask. */
 dmt_status dmt_swap(dmt_ens* h, int32_t layout, int32_t what, int64_t b0, int64_t b1);

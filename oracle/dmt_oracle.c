@@ -361,6 +361,45 @@ int SFX(orc_solve_segment)(int model, int d, int m, const double* law, int npts,
     return ok;
 }
 
+/* DD.invsolve!(X, W, P) (find_W_for_X!, src/block.jl:118-131): increments reproducing X
+ * under the guided Euler step of law P (canonical order):
+ *   r_a = fma(-bg_a, dt, x_{i+1,a} - x_{i,a});  dW = siginv·r (d = m), or r_1 / sigma_10 (FHN).
+ * W is written as increments with W(t0) = 0. */
+void SFX(orc_invsolve_segment)(int model, int d, int m, const double* law, int npts,
+                               const REAL* t, const REAL* H, const REAL* F, const REAL* X,
+                               REAL* W) {
+    int h = d * (d + 1) / 2;
+    REAL th[16], sg[9], a[6], Bt[9], beta[3], da[6]; int trace;
+    load_law(law, d, m, th, sg, a, Bt, beta, da, &trace);
+    REAL siginv[9];
+    for (int i = 0; i < 9; ++i) siginv[i] = (REAL)law[51 + i];
+    for (int k = 0; k < m; ++k) W[k] = (REAL)0;
+    for (int i = 0; i < npts - 1; ++i) {
+        REAL dt = t[i + 1] - t[i];
+        const REAL* x = X + (size_t)i * d;
+        const REAL* xn = X + (size_t)(i + 1) * d;
+        REAL Mg[9], cg[3], b[3] = {0, 0, 0}, r[3];
+        guide_coeffs(model, d, th, a, H + (size_t)i * h, F + (size_t)i * d, Mg, cg);
+        if (model != ORC_OU) orc_drift(model, d, th, x, b);
+        for (int p = 0; p < d; ++p) {
+            REAL u = cg[p];
+            for (int q = 0; q < d; ++q) u = FMA(-Mg[p * d + q], x[q], u);
+            REAL bg = (model == ORC_OU) ? u : (b[p] + u);
+            r[p] = FMA(-bg, dt, xn[p] - x[p]);
+        }
+        REAL* dW = W + (size_t)(i + 1) * m;
+        if (model == ORC_FHN) {
+            dW[0] = r[1] / sg[1 * m + 0];
+        } else {
+            for (int k = 0; k < m; ++k) {
+                REAL v = siginv[k * d + 0] * r[0];
+                for (int q = 1; q < d; ++q) v = FMA(siginv[k * d + q], r[q], v);
+                dW[k] = v;
+            }
+        }
+    }
+}
+
 /* GP.loglikhd(P, X): Girsanov sum on a stored path (no state update). */
 REAL SFX(orc_path_ll_segment)(int model, int d, int m, const double* law, int npts,
                               const REAL* t, const REAL* H, const REAL* F, const REAL* X) {

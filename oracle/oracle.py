@@ -50,6 +50,9 @@ def _load():
         f = getattr(lib, f"orc_solve_segment_{sfx}")
         f.argtypes = [i_, i_, i_, P, i_, P, P, P, P, P, P, P]
         f.restype = i_
+        f = getattr(lib, f"orc_invsolve_segment_{sfx}")
+        f.argtypes = [i_, i_, i_, P, i_, P, P, P, P, P]
+        f.restype = None
         f = getattr(lib, f"orc_path_ll_segment_{sfx}")
         f.argtypes = [i_, i_, i_, P, i_, P, P, P, P]
         f.restype = R
@@ -108,6 +111,17 @@ def solve_segment(model, d, m, law, t, H, F, W, y1, prec=0):
     ok = getattr(lib, f"orc_solve_segment_{_sfx(prec)}")(model, d, m, _p(law), n, _p(t), _p(H),
                                                           _p(F), _p(W), _p(y1), _p(X), _p(ll))
     return X, dt(ll[0]), bool(ok)
+
+
+def invsolve_segment(model, d, m, law, t, H, F, X, prec=0):
+    """DD.invsolve!: Wiener increments (row 0 = W(t0) = 0) reproducing X under the law."""
+    dt = _dt(prec)
+    t, H, F, X = (np.ascontiguousarray(a, dtype=dt) for a in (t, H, F, X))
+    law = np.ascontiguousarray(law, dtype=np.float64)
+    W = np.empty((t.size, m), dtype=dt)
+    getattr(lib, f"orc_invsolve_segment_{_sfx(prec)}")(model, d, m, _p(law), t.size, _p(t), _p(H),
+                                                      _p(F), _p(X), _p(W))
+    return W
 
 
 def path_ll_segment(model, d, m, law, t, H, F, X, prec=0):
@@ -461,6 +475,14 @@ class OracleEnsemble:
             bk.llp, ok = self._solve_block(bk, 1, 1, 0, 1, "given", None, 0, 0)
             oks.append(ok)
         return np.array(oks) if want_success else None
+
+    def find_W_for_X(self, layout, b0, b1):
+        """find_W_for_X!(b) (src/block.jl:118-131): u.WW[g] ← invsolve(u.XX[g], law of g)."""
+        for bk in self.layouts[layout][b0:b1]:
+            for g in range(bk.g0, bk.g1 + 1):
+                lw = self._law(0, bk, g)
+                self.u.WW[g][...] = invsolve_segment(self.model, self.d, self.m, lw.rec, self.t[g],
+                                                     lw.H, lw.F, self.u.XX[g], self.prec)
 
     def swap(self, layout, what, b0, b1):
         for bk in self.layouts[layout][b0:b1]:

@@ -306,3 +306,40 @@ def test_mcmc_run_equals_step_sequence(B):
                               ens[1].get_block_state(lay, what, 0, B))
     assert np.array_equal(ens[0].get_block_state(lay, L.BLK_ACC_HIST, 0, B, 6),
                           ens[1].get_block_state(lay, L.BLK_ACC_HIST, 0, B, 6))
+
+
+@pytest.mark.parametrize("mapping", MAPPINGS)
+@pytest.mark.parametrize("cfg", ["c1", "c2", "c3", "c5"])
+def test_find_W_for_X_bit_exact(cfg, mapping):
+    """find_W_for_X! (DD.invsolve!) on the device == the oracle, bit for bit, then one more
+    MCMC iteration from the reconstructed W agrees too."""
+    w = {"c1": lambda: W.c1_ou1d(),
+         "c2": lambda: W.c2_ou2d(B=200, N=300),
+         "c3": lambda: W.c3_fhn(B=130, N=300, T_burn=0.1),
+         "c5": lambda: W.c5_lorenz(B=70, N=300)}[cfg]()
+    dev, ora, lay = cs.both(w, hist_len=1, mapping=mapping)
+    nb = w.nblocks
+    for e in (dev, ora):
+        e.find_W_for_X(lay, 0, nb)
+    cs.assert_paths_equal(dev, ora)
+    rng = np.random.default_rng(4)
+    Z = rng.standard_normal((w.steps_per_iter, w.m))
+    E = rng.exponential(1.0, nb)
+    for e in (dev, ora):
+        e.loglikhd(lay, L.U, 0, nb)
+        e.draw_proposal(lay, 0, nb, Z=Z, iter=1)
+    assert np.array_equal(dev.accept_reject(lay, 0, nb, 1, E=E, want_acc=True),
+                          ora.accept_reject(lay, 0, nb, 1, E=E, want_acc=True))
+    cs.assert_paths_equal(dev, ora)
+    cs.assert_ll_equal(dev, ora, lay, nb)
+
+
+@pytest.mark.parametrize("mapping", MAPPINGS)
+def test_find_W_for_X_blocking_layouts(mapping):
+    """Ragged multi-segment FHN with P_last laws: invsolve uses PPb on the last segment of
+    non-terminal blocks (src/block.jl:118-124)."""
+    case, dev, ora, ids = cs.ragged_pair(mapping=mapping)
+    for lid, nb in ids:
+        for e in (dev, ora):
+            e.find_W_for_X(lid, 0, nb)
+        cs.assert_paths_equal(dev, ora)

@@ -202,3 +202,29 @@ def test_pairwise_tree_order():
     assert orc.pairwise_tree(v) == (1e16 + 1.0) + (-1e16 + 1.0)
     assert orc.pairwise_tree([]) == 0.0
     assert orc.pairwise_tree([3.0, 4.0, 5.0]) == (3.0 + 4.0) + (5.0 + 0.0)
+
+
+# ---------------------------------------------------------------- find_W_for_X! (invsolve)
+@pytest.mark.parametrize("cfg", ["ou2d", "fhn", "lorenz"])
+def test_invsolve_inverts_the_forward_solve(cfg):
+    """DD.invsolve! restated: increments recovered from a forward-solved path reproduce the
+    drawn increments (up to cancellation rounding) and re-solve to the same path."""
+    from diffusionmcmctools_amd import workloads as W
+    w = {"ou2d": lambda: W.c2_ou2d(B=1, N=300),
+         "fhn": lambda: W.c3_fhn(B=1, N=300, T_burn=0.1),
+         "lorenz": lambda: W.c5_lorenz(B=1, N=300)}[cfg]()
+    prec = w.precision
+    npts = w.n_points[0][0]
+    rng = np.random.default_rng(3)
+    dW = np.zeros((npts, w.m))
+    dW[1:] = rng.standard_normal((npts - 1, w.m)) * np.sqrt(np.diff(w.t))[:, None]
+    H = w.H if not w.H_shared else w.H
+    X, ll, ok = orc.solve_segment(w.model.kind, w.d, w.m, w.laws[0], w.t, H, w.F, dW, w.X0[0], prec)
+    assert ok
+    W2 = orc.invsolve_segment(w.model.kind, w.d, w.m, w.laws[0], w.t, H, w.F, X, prec)
+    tol = 1e-9 if prec == 0 else 2e-3
+    np.testing.assert_allclose(W2[1:], dW[1:], rtol=tol, atol=tol * 1e-2)
+    assert np.all(W2[0] == 0)
+    X2, _, ok2 = orc.solve_segment(w.model.kind, w.d, w.m, w.laws[0], w.t, H, w.F, W2, w.X0[0], prec)
+    assert ok2
+    np.testing.assert_allclose(X2, X, rtol=tol, atol=tol)
