@@ -33,7 +33,8 @@ LAW_SIGINV = 51
 SYMBOLS = [
     "dmt_create", "dmt_destroy", "dmt_upload_grid", "dmt_upload_law", "dmt_set_paths",
     "dmt_download_paths", "dmt_draw_unit", "dmt_create_layout", "dmt_layout_size",
-    "dmt_draw_proposal", "dmt_accept_reject", "dmt_loglikhd", "dmt_recompute_path", "dmt_find_W_for_X", "dmt_swap",
+    "dmt_draw_proposal", "dmt_accept_reject", "dmt_loglikhd", "dmt_recompute_path", "dmt_find_W_for_X", "dmt_upload_obs", "dmt_set_obs",
+    "dmt_recompute_guiding_term", "dmt_download_law", "dmt_swap",
     "dmt_save_ll", "dmt_set_accepted", "dmt_get_block_state", "dmt_set_block_state",
     "dmt_fetch_ll", "dmt_mcmc_step", "dmt_mcmc_run", "dmt_guiding_linear", "dmt_comm_unique_id", "dmt_comm_init", "dmt_set_shard", "dmt_sync",
     "dmt_set_timing", "dmt_get_timing", "dmt_memory_bytes", "dmt_debug_philox",
@@ -91,6 +92,10 @@ _SIGS = {
     "dmt_loglikhd": [_P, _i32, _i32, _i64, _i64],
     "dmt_recompute_path": [_P, _i32, _i64, _i64, _i32, _pu8],
     "dmt_find_W_for_X": [_P, _i32, _i64, _i64],
+    "dmt_upload_obs": [_P, _pd, _pd, _pd, C.c_double],
+    "dmt_set_obs": [_P, _i32, _i64, _i64],
+    "dmt_download_law": [_P, _i32, _i32, _pd, _pd, _pd],
+    "dmt_recompute_guiding_term": [_P, _i32, _i64, _i64, _i32],
     "dmt_swap": [_P, _i32, _i32, _i64, _i64],
     "dmt_save_ll": [_P, _i32, _i64, _i64, _i64],
     "dmt_set_accepted": [_P, _i32, _i64, _i64, _i64, _pu8],

@@ -64,6 +64,12 @@ class SamplingEnsemble:
         if Hb is not None or Fb is not None or lawsb is not None:
             self.ens.upload_law(unit, L.LAW_PPB, H=Hb, F=Fb, laws=lawsb, H_shared=H_shared)
 
+    def set_observations(self, Hobs, Fobs, cobs, artificial_noise=1e-11):
+        """Information of the observation at every segment end (packed H, F, c) and the
+        artificial noise of the blocking laws (src/sampling_unit.jl:57): enables
+        ``set_obs`` / ``recompute_guiding_term`` on the device."""
+        self.ens.upload_obs(Hobs, Fobs, cobs, artificial_noise)
+
     def init_paths(self, x0, Z=None, iter=0, salt=0xFFFF):
         """``init_paths!`` (src/sampling_unit.jl:83-87) for every recording, then
         u° ← u (src/sampling_pair.jl:51).  ``x0``: per-recording start points (R × d)."""
@@ -191,6 +197,16 @@ class _BlockRange:
         """``recompute_path!(bb.b°, bb.b.WW; skip)`` (src/block.jl:155-187): u° re-solved
         under u°'s laws with u's Wiener path; ll° stored.  Returns per-block success."""
         return self._call("recompute_path", skip=skip, want_success=True)
+
+    def set_obs(self):
+        """``GP.set_obs!`` (src/biblock.jl:273-280): freeze the accepted end point of every
+        non-terminal block as the artificial observation of its P_last law."""
+        self._call("set_obs")
+
+    def recompute_guiding_term(self, unit=L.U):
+        """``GP.recompute_guiding_term!(bb.b)`` (``unit=U``) or of ``bb.b°`` (``UPROP``)
+        (src/block.jl:102-110): device backward filter of the blocks' laws."""
+        self._call("recompute_guiding_term", unit=unit)
 
     def find_W_for_X(self):
         """``find_W_for_X!`` (src/block.jl:118-131): u.WW ← the Wiener increments that reproduce

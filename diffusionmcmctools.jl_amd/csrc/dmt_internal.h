@@ -113,6 +113,32 @@ struct DispatchEvents {
 };
 extern thread_local DispatchEvents g_dispatch_events;
 
+// recompute_guiding_term! on the device (k_backward_filter): one thread per block.
+struct FilterArgs {
+  int d, tw, unit;
+  const int64_t* tile_qoff;
+  const int32_t* seg_rec;
+  const int32_t* seg_q;
+  const int32_t* seg_np;
+  const int32_t* gfirst;
+  const int32_t* glast;
+  const uint8_t* term;
+  const uint8_t* selPP;
+  const uint8_t* selPPB;
+  int64_t b0, b1;
+  void* H[2][2];  // [slot][kind] per-point tables (T)
+  void* F[2][2];
+  double* law[2][2];
+  const void* t;  // grid (T)
+  int t_shared;
+  const double* obsH;  // [G][hp] information of the observation at each segment's end
+  const double* obsF;  // [G][d]
+  const double* obsc;  // [G]
+  const double* obsv;  // [G][d] artificial observation (set_obs!) of a P_last segment
+  double art_eps;      // its variance (artificial_noise)
+  int* fail;           // set to 1 if a filter step is singular
+};
+
 // Model/precision dispatch keys.
 struct ModelKey {
   int model, precision, d, m;
@@ -126,6 +152,12 @@ hipError_t launch_invsolve_kernel(const ModelKey& k, int mapping, const void* ar
 hipError_t launch_pathll_kernel(const ModelKey& k, int mapping, const void* args, int64_t nwaves,
                                 hipStream_t s);
 hipError_t launch_accept(const AcceptArgs& a, hipStream_t s);
+hipError_t launch_backward_filter(int precision, const FilterArgs& a, hipStream_t s);
+hipError_t launch_set_obs(int precision, int tw, int d, const void* X0, const void* X1,
+                          const uint8_t* selX,
+                          const int64_t* tile_qoff, const int32_t* seg_rec, const int32_t* seg_q,
+                          const int32_t* seg_np, const int32_t* glast, const uint8_t* term,
+                          int64_t b0, int64_t b1, double* obsv, hipStream_t s);
 hipError_t launch_to_planes(int precision, int tw, const double* src, void* dst0, void* dst1,
                             const uint8_t* sel, int flip, int C, int64_t P, const int64_t* pt_off,
                             int64_t G, const int32_t* seg_rec, const int32_t* seg_q,
@@ -140,6 +172,7 @@ hipError_t launch_from_planes(int precision, int tw, double* dst, const void* sr
                               const int64_t* pt_off, int64_t G, const int32_t* seg_rec,
                               const int32_t* seg_q, const int64_t* tile_qoff, hipStream_t s);
 hipError_t launch_cast(int precision, const double* src, void* dst, int64_t n, hipStream_t s);
+hipError_t launch_cast_back(int precision, const void* src, double* dst, int64_t n, hipStream_t s);
 hipError_t launch_block_sum(const double* ll, const double* llp, const uint8_t* acc, int64_t n,
                             double* work, double* out3, hipStream_t s);
 // work: multi-level tree scratch (6 per 1024-block group); lb: single-launch scratch

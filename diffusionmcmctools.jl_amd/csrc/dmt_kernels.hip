@@ -24,6 +24,7 @@
 
 #include "dmt_device.h"
 #include "dmt_internal.h"
+#include "dmt_filter.h"
 
 namespace dmt {
 
@@ -1229,6 +1230,102 @@ __global__ __launch_bounds__(kAccGroup) void k_accept_reduce_lb(const AcceptArgs
   }
 }
 
+// ---------------------------------------------------------------- guiding term on the device
+// recompute_guiding_term!(b) for linear auxiliary laws (src/block.jl:102-110; the exact
+// discrete filter of dmt_filter.h, identical to the host dmt_guiding_linear): one thread per
+// block, segments backward from the block end; the last segment of a non-terminal block uses
+// its PPb law with the artificial end observation frozen by set_obs!.
+template <class T>
+__global__ __launch_bounds__(128) void k_backward_filter(const FilterArgs a) {
+  const int64_t blk = a.b0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (blk >= a.b1) return;
+  const int d = a.d, hp = d * (d + 1) / 2;
+  const int g0 = a.gfirst[blk], g1 = a.glast[blk];
+  const bool term = a.term[blk] != 0;
+  using flt::Mat;
+  Mat Hc = flt::mzero(d);
+  double Fc[3] = {0, 0, 0}, cc = 0.0;
+  for (int g = g1; g >= g0; --g) {
+    const int kind = (!term && g == g1) ? 1 : 0;
+    const int slot = (kind ? a.selPPB[g] : a.selPP[g]) ^ a.unit;
+    const double* lr = a.law[slot][kind] + (int64_t)g * DMT_LAW_STRIDE;
+    // terminal information of the segment: its observation (+ the artificial one of a
+    // P_last segment, or + the guiding term at the start of the next segment of the block)
+    Mat HT = flt::mzero(d);
+    double FT[3] = {0, 0, 0}, cT = a.obsc[g];
+    for (int p = 0; p < d; ++p) {
+      FT[p] = a.obsF[(int64_t)g * d + p];
+      for (int q = 0; q < d; ++q) HT(p, q) = a.obsH[(int64_t)g * hp + flt::packed_ix(d, p, q)];
+    }
+    if (kind == 1) {
+      const double inv = 1.0 / a.art_eps;
+      double vv = 0.0;
+      for (int p = 0; p < d; ++p) {
+        const double v = a.obsv[(int64_t)g * d + p];
+        HT(p, p) += inv;
+        FT[p] += inv * v;
+        vv += v * v;
+      }
+      cT += 0.5 * inv * vv + 0.5 * d * (0x1.d67f1c864beb4p+0 + flt::flt_log(a.art_eps));
+    } else if (g < g1) {
+      HT = flt::madd(HT, Hc);
+      for (int p = 0; p < d; ++p) FT[p] += Fc[p];
+      cT += cc;
+    }
+    Mat B = flt::mzero(d), At = flt::mzero(d);
+    double beta[3] = {0, 0, 0};
+    for (int p = 0; p < d; ++p) {
+      beta[p] = lr[DMT_LAW_BETA + p];
+      for (int q = 0; q < d; ++q) {
+        B(p, q) = lr[DMT_LAW_BT + p * d + q];
+        const int e = flt::packed_ix(d, p, q);
+        At(p, q) = lr[DMT_LAW_A + e] - lr[DMT_LAW_DA + e];  // ã = a − (a − ã)
+      }
+    }
+    const int64_t r = a.seg_rec[g];
+    const int64_t tq = a.tile_qoff[r / a.tw];
+    const int lane = (int)(r % a.tw);
+    auto ix = [&](int64_t q, int c, int C) -> int64_t { return ((tq + q) * C + c) * a.tw + lane; };
+    const T* tt = (const T*)a.t;
+    const int64_t q0 = a.seg_q[g];
+    const int np = a.seg_np[g];
+    auto tat = [&](int i) -> double { return a.t_shared ? (double)tt[q0 + i] : (double)tt[ix(q0 + i, 0, 1)]; };
+    T* Ht = (T*)a.H[slot][kind];
+    T* Ft = (T*)a.F[slot][kind];
+    Hc = HT;
+    for (int p = 0; p < d; ++p) Fc[p] = FT[p];
+    cc = cT;
+    auto store = [&](int i) {
+      for (int p = 0; p < d; ++p)
+        for (int q = p; q < d; ++q) Ht[ix(q0 + i, flt::packed_ix(d, p, q), hp)] = (T)Hc(p, q);
+      for (int p = 0; p < d; ++p) Ft[ix(q0 + i, p, d)] = (T)Fc[p];
+    };
+    store(np - 1);
+    for (int i = np - 2; i >= 0; --i) {
+      if (!flt::filter_step(B, beta, At, tat(i + 1) - tat(i), Hc, Fc, cc)) { *a.fail = 1; return; }
+      store(i);
+    }
+    a.law[slot][kind][(int64_t)g * DMT_LAW_STRIDE + DMT_LAW_C0] = cc;
+  }
+}
+
+// set_obs!(bb) (src/biblock.jl:273-280): the artificial observation of a non-terminal block's
+// P_last is the end point of its accepted path.
+template <class T>
+__global__ void k_set_obs(int tw, int d, const T* X0, const T* X1, const uint8_t* selX,
+                          const int64_t* tile_qoff, const int32_t* seg_rec, const int32_t* seg_q,
+                          const int32_t* seg_np, const int32_t* glast, const uint8_t* term,
+                          int64_t b0, int64_t b1, double* obsv) {
+  const int64_t blk = b0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (blk >= b1 || term[blk]) return;
+  const int g = glast[blk];
+  const T* X = selX[g] ? X1 : X0;  // u.XX
+  const int64_t r = seg_rec[g];
+  const int64_t q = seg_q[g] + seg_np[g] - 1;
+  for (int p = 0; p < d; ++p)
+    obsv[(int64_t)g * d + p] = (double)X[((tile_qoff[r / tw] + q) * d + p) * tw + r % tw];
+}
+
 // ---------------------------------------------------------------- small utility kernels
 __global__ void k_flip(uint8_t* sel, const int32_t* gfirst, const int32_t* glast,
                        const uint8_t* term, int only_nonterm, int64_t b0, int64_t b1) {
@@ -1639,6 +1736,32 @@ hipError_t launch_pathll_kernel(const ModelKey& k, int mapping, const void* args
   DMT_DISPATCH(k, (launch_pathll_t<Mdl, T>(mapping, args, nwaves, s)));
 }
 
+hipError_t launch_backward_filter(int precision, const FilterArgs& a, hipStream_t s) {
+  const int64_t n = a.b1 - a.b0;
+  if (n <= 0) return hipSuccess;
+  if (precision == DMT_F64) dlaunch(k_backward_filter<double>, dim3(nblk(n, 128)), dim3(128), s, a);
+  else dlaunch(k_backward_filter<float>, dim3(nblk(n, 128)), dim3(128), s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_set_obs(int precision, int tw, int d, const void* X0, const void* X1,
+                          const uint8_t* selX, const int64_t* tile_qoff, const int32_t* seg_rec,
+                          const int32_t* seg_q, const int32_t* seg_np, const int32_t* glast,
+                          const uint8_t* term, int64_t b0, int64_t b1, double* obsv,
+                          hipStream_t s) {
+  const int64_t n = b1 - b0;
+  if (n <= 0) return hipSuccess;
+  if (precision == DMT_F64)
+    k_set_obs<double><<<nblk(n, 256), 256, 0, s>>>(tw, d, (const double*)X0, (const double*)X1,
+                                                   selX, tile_qoff, seg_rec, seg_q, seg_np, glast,
+                                                   term, b0, b1, obsv);
+  else
+    k_set_obs<float><<<nblk(n, 256), 256, 0, s>>>(tw, d, (const float*)X0, (const float*)X1, selX,
+                                                  tile_qoff, seg_rec, seg_q, seg_np, glast, term,
+                                                  b0, b1, obsv);
+  return hipGetLastError();
+}
+
 hipError_t launch_accept(const AcceptArgs& a, hipStream_t s) {
   const int64_t n = a.b1 - a.b0;
   if (n <= 0) return hipSuccess;
@@ -1702,6 +1825,21 @@ hipError_t launch_cast(int precision, const double* src, void* dst, int64_t n, h
     k_cast<double><<<nblk(n, 256), 256, 0, s>>>(src, (double*)dst, n);
   else
     k_cast<float><<<nblk(n, 256), 256, 0, s>>>(src, (float*)dst, n);
+  return hipGetLastError();
+}
+
+template <class T>
+__global__ void k_cast_back(const T* __restrict__ src, double* __restrict__ dst, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = (double)src[i];
+}
+
+hipError_t launch_cast_back(int precision, const void* src, double* dst, int64_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  if (precision == DMT_F64)
+    k_cast_back<double><<<nblk(n, 256), 256, 0, s>>>((const double*)src, dst, n);
+  else
+    k_cast_back<float><<<nblk(n, 256), 256, 0, s>>>((const float*)src, dst, n);
   return hipGetLastError();
 }
 

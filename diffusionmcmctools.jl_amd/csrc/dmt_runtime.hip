@@ -20,6 +20,7 @@
 
 #include "../../include/dmt.h"
 #include "dmt_internal.h"
+#include "dmt_filter.h"
 
 using namespace dmt;
 
@@ -111,6 +112,13 @@ struct dmt_ens {
   void* d_F[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
   double* d_law[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
   bool have_law[2][2] = {{false, false}, {false, false}};  // [unit][kind] uploaded at least once
+  // observation information for the device backward filter (dmt_upload_obs / dmt_set_obs)
+  double* d_obsH = nullptr;  // [G][hp]
+  double* d_obsF = nullptr;  // [G][d]
+  double* d_obsc = nullptr;  // [G]
+  double* d_obsv = nullptr;  // [G][d] artificial observations of P_last segments
+  int* d_fail = nullptr;
+  double art_eps = 1e-11;    // artificial_noise (src/sampling_unit.jl:57)
   // staging
   double* d_stage = nullptr;
   int64_t stage_n = 0;
@@ -488,97 +496,13 @@ bool supported(const dmt_model* m) {
   return false;
 }
 
-// ------------------------------------------------------------ backward filter (host)
-// Small dense helpers, row-major d×d with d ≤ 3.
-struct Mat {
-  int n;
-  double a[9];
-  double& operator()(int i, int j) { return a[i * n + j]; }
-  double operator()(int i, int j) const { return a[i * n + j]; }
-};
-Mat mzero(int n) { Mat m; m.n = n; std::memset(m.a, 0, sizeof m.a); return m; }
-Mat meye(int n) { Mat m = mzero(n); for (int i = 0; i < n; ++i) m(i, i) = 1; return m; }
-Mat mmul(const Mat& A, const Mat& B) {
-  Mat C = mzero(A.n);
-  for (int i = 0; i < A.n; ++i)
-    for (int j = 0; j < A.n; ++j) {
-      double s = 0;
-      for (int k = 0; k < A.n; ++k) s += A(i, k) * B(k, j);
-      C(i, j) = s;
-    }
-  return C;
-}
-Mat mT(const Mat& A) { Mat C = mzero(A.n); for (int i = 0; i < A.n; ++i) for (int j = 0; j < A.n; ++j) C(i, j) = A(j, i); return C; }
-Mat madd(const Mat& A, const Mat& B, double s = 1.0) { Mat C = A; for (int i = 0; i < A.n * A.n; ++i) C.a[i] += s * B.a[i]; return C; }
-void mvec(const Mat& A, const double* x, double* y) {
-  for (int i = 0; i < A.n; ++i) { double s = 0; for (int k = 0; k < A.n; ++k) s += A(i, k) * x[k]; y[i] = s; }
-}
-double mnorm(const Mat& A) { double s = 0; for (int i = 0; i < A.n * A.n; ++i) s = std::max(s, std::fabs(A.a[i])); return s * A.n; }
-// inverse and log|det| by Gauss-Jordan with partial pivoting
-bool minv(const Mat& A, Mat& Inv, double& logabsdet) {
-  int n = A.n;
-  double w[3][6];
-  for (int i = 0; i < n; ++i) for (int j = 0; j < n; ++j) { w[i][j] = A(i, j); w[i][n + j] = (i == j); }
-  logabsdet = 0;
-  for (int c = 0; c < n; ++c) {
-    int p = c;
-    for (int i = c + 1; i < n; ++i) if (std::fabs(w[i][c]) > std::fabs(w[p][c])) p = i;
-    if (w[p][c] == 0.0) return false;
-    if (p != c) for (int j = 0; j < 2 * n; ++j) std::swap(w[p][j], w[c][j]);
-    double piv = w[c][c];
-    logabsdet += std::log(std::fabs(piv));
-    for (int j = 0; j < 2 * n; ++j) w[c][j] /= piv;
-    for (int i = 0; i < n; ++i) if (i != c) {
-      double f = w[i][c];
-      if (f != 0.0) for (int j = 0; j < 2 * n; ++j) w[i][j] -= f * w[c][j];
-    }
-  }
-  Inv = mzero(n);
-  for (int i = 0; i < n; ++i) for (int j = 0; j < n; ++j) Inv(i, j) = w[i][n + j];
-  return true;
-}
-
-// Exact transition of dX = (BX + beta)dt + sigma dW over a step h:
-// X_{t+h} = Phi X_t + mu + N(0, K).  Series with scaling-and-squaring.
-void transition(const Mat& B, const double* beta, const Mat& At, double h, Mat& Phi, double* mu, Mat& K) {
-  const int n = B.n;
-  int sq = 0;
-  double hs = h;
-  while (mnorm(B) * hs > 0.25 && sq < 40) { hs *= 0.5; ++sq; }
-  Mat A = B;
-  for (int i = 0; i < n * n; ++i) A.a[i] *= hs;
-  // Phi = sum A^k/k!, mu = hs sum A^k/(k+1)! beta, K = sum hs^{k+1}/(k+1)! L^k(At)
-  Phi = meye(n);
-  Mat term = meye(n);
-  Mat S1 = meye(n);  // sum A^k/(k+1)!
-  Mat Lk = At;       // L^k(At) * hs^k / k!   (L(X) = BX + XB^T)
-  K = mzero(n);
-  for (int i = 0; i < n * n; ++i) K.a[i] = hs * Lk.a[i];
-  for (int k = 1; k <= 30; ++k) {
-    term = mmul(term, A);
-    for (int i = 0; i < n * n; ++i) term.a[i] /= k;
-    Phi = madd(Phi, term);
-    Mat t2 = term;
-    for (int i = 0; i < n * n; ++i) t2.a[i] /= (k + 1);
-    S1 = madd(S1, t2);
-    Mat nl = madd(mmul(B, Lk), mmul(Lk, mT(B)));
-    for (int i = 0; i < n * n; ++i) nl.a[i] *= hs / k;
-    Lk = nl;
-    for (int i = 0; i < n * n; ++i) K.a[i] += hs * Lk.a[i] / (k + 1);
-    if (mnorm(term) < 1e-18 && mnorm(Lk) * hs < 1e-18 * (1.0 + mnorm(K))) break;
-  }
-  double sb[3];
-  mvec(S1, beta, sb);
-  for (int i = 0; i < n; ++i) mu[i] = hs * sb[i];
-  for (int s = 0; s < sq; ++s) {  // compose two half steps
-    double m2[3];
-    mvec(Phi, mu, m2);
-    for (int i = 0; i < n; ++i) mu[i] = m2[i] + mu[i];
-    K = madd(mmul(mmul(Phi, K), mT(Phi)), K);
-    Phi = mmul(Phi, Phi);
-  }
-  for (int i = 0; i < n; ++i) for (int j = i + 1; j < n; ++j) { double v = 0.5 * (K(i, j) + K(j, i)); K(i, j) = v; K(j, i) = v; }
-}
+// ------------------------------------------------------------ backward filter
+// (dmt_filter.h: shared with the device kernel k_backward_filter)
+using flt::Mat;
+using flt::madd;
+using flt::meye;
+using flt::mmul;
+using flt::mzero;
 
 }  // namespace
 
@@ -722,7 +646,8 @@ dmt_status dmt_destroy(dmt_ens* h) {
   void* ps[] = {h->d_pt_off, h->d_st_off, h->d_tile_qoff, h->d_seg_rec, h->d_seg_q, h->d_seg_np,
                 h->d_sel[0], h->d_sel[1], h->d_sel[2], h->d_sel[3], h->d_X[0], h->d_X[1],
                 h->d_W[0], h->d_W[1], h->d_t, h->d_stage, h->d_Z, h->d_red, h->d_gather,
-                h->d_red_work, h->d_run, h->d_run_gather, h->d_red_lb};
+                h->d_red_work, h->d_run, h->d_run_gather, h->d_red_lb, h->d_obsH,
+                h->d_obsF, h->d_obsc, h->d_obsv, h->d_fail};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   for (int s = 0; s < 2; ++s)
@@ -898,6 +823,52 @@ dmt_status dmt_download_paths(dmt_ens* h, int32_t unit, int32_t what, double* ou
                                    h->d_tile_qoff, h->stream));
   HIP_OK(hipMemcpyAsync(out, h->d_stage, h->P * C * 8, hipMemcpyDeviceToHost, h->stream));
   HIP_OK(hipStreamSynchronize(h->stream));
+  return DMT_OK;
+}
+
+dmt_status dmt_download_law(dmt_ens* h, int32_t unit, int32_t kind, double* H, double* F,
+                            double* laws) {
+  DMT_TRY(check_h(h));
+  if ((unit != DMT_U && unit != DMT_UPROP) || (kind != DMT_LAW_PP && kind != DMT_LAW_PPB))
+    return fail(DMT_ERR_INVALID, "bad unit/kind");
+  if (!h->have_law[0][kind] && !h->have_law[1][kind]) return fail(DMT_ERR_STATE, "law not uploaded");
+  const uint8_t* sel = h->d_sel[2 + kind];
+  if (H) {
+    if (h->H_shared[kind]) {
+      const std::vector<uint8_t>& hsel = kind == 0 ? h->h_selPP : h->h_selPPB;
+      DMT_TRY(ensure_stage(h, h->Q0 * h->hp));
+      HIP_OK(launch_cast_back(h->key.precision, h->d_H[hsel[0] ^ unit][kind], h->d_stage,
+                              h->Q0 * h->hp, h->stream));
+      HIP_OK(hipMemcpyAsync(H, h->d_stage, h->Q0 * h->hp * 8, hipMemcpyDeviceToHost, h->stream));
+    } else {
+      DMT_TRY(ensure_stage(h, h->P * h->hp));
+      HIP_OK(launch_from_planes(h->key.precision, h->tw, h->d_stage, h->d_H[0][kind], h->d_H[1][kind],
+                                sel, unit, h->hp, h->P, h->d_pt_off, h->G, h->d_seg_rec, h->d_seg_q,
+                                h->d_tile_qoff, h->stream));
+      HIP_OK(hipMemcpyAsync(H, h->d_stage, h->P * h->hp * 8, hipMemcpyDeviceToHost, h->stream));
+    }
+    HIP_OK(hipStreamSynchronize(h->stream));
+  }
+  if (F) {
+    DMT_TRY(ensure_stage(h, h->P * h->d));
+    HIP_OK(launch_from_planes(h->key.precision, h->tw, h->d_stage, h->d_F[0][kind], h->d_F[1][kind],
+                              sel, unit, h->d, h->P, h->d_pt_off, h->G, h->d_seg_rec, h->d_seg_q,
+                              h->d_tile_qoff, h->stream));
+    HIP_OK(hipMemcpyAsync(F, h->d_stage, h->P * h->d * 8, hipMemcpyDeviceToHost, h->stream));
+    HIP_OK(hipStreamSynchronize(h->stream));
+  }
+  if (laws) {
+    std::vector<double> l0(h->G * DMT_LAW_STRIDE), l1(h->G * DMT_LAW_STRIDE);
+    std::vector<uint8_t> hs(h->G);
+    HIP_OK(hipMemcpyAsync(l0.data(), h->d_law[0][kind], l0.size() * 8, hipMemcpyDeviceToHost, h->stream));
+    HIP_OK(hipMemcpyAsync(l1.data(), h->d_law[1][kind], l1.size() * 8, hipMemcpyDeviceToHost, h->stream));
+    HIP_OK(hipMemcpyAsync(hs.data(), sel, h->G, hipMemcpyDeviceToHost, h->stream));
+    HIP_OK(hipStreamSynchronize(h->stream));
+    for (int64_t g = 0; g < h->G; ++g) {
+      const std::vector<double>& src = (hs[g] ^ unit) ? l1 : l0;
+      std::memcpy(laws + g * DMT_LAW_STRIDE, src.data() + g * DMT_LAW_STRIDE, DMT_LAW_STRIDE * 8);
+    }
+  }
   return DMT_OK;
 }
 
@@ -1198,6 +1169,94 @@ dmt_status dmt_find_W_for_X(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1) 
   return DMT_OK;
 }
 
+dmt_status dmt_upload_obs(dmt_ens* h, const double* Hobs, const double* Fobs, const double* cobs,
+                          double artificial_noise) {
+  DMT_TRY(check_h(h));
+  if (!Hobs || !Fobs || !cobs || !(artificial_noise > 0.0))
+    return fail(DMT_ERR_INVALID, "bad arguments to dmt_upload_obs");
+  if (!h->d_obsH) {
+    DMT_TRY(ens_alloc(h, &h->d_obsH, h->G * h->hp));
+    DMT_TRY(ens_alloc(h, &h->d_obsF, h->G * h->d));
+    DMT_TRY(ens_alloc(h, &h->d_obsc, h->G));
+    DMT_TRY(ens_alloc(h, &h->d_obsv, h->G * h->d));
+    DMT_TRY(ens_alloc(h, &h->d_fail, 1));
+    HIP_OK(hipMemsetAsync(h->d_obsv, 0, h->G * h->d * 8, h->stream));
+  }
+  HIP_OK(hipMemcpyAsync(h->d_obsH, Hobs, h->G * h->hp * 8, hipMemcpyHostToDevice, h->stream));
+  HIP_OK(hipMemcpyAsync(h->d_obsF, Fobs, h->G * h->d * 8, hipMemcpyHostToDevice, h->stream));
+  HIP_OK(hipMemcpyAsync(h->d_obsc, cobs, h->G * 8, hipMemcpyHostToDevice, h->stream));
+  h->art_eps = artificial_noise;
+  HIP_OK(hipStreamSynchronize(h->stream));
+  return DMT_OK;
+}
+
+dmt_status dmt_set_obs(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1) {
+  DMT_TRY(check_h(h));
+  if (!h->d_obsv) return fail(DMT_ERR_STATE, "dmt_upload_obs first");
+  Layout* L;
+  DMT_TRY(get_layout(h, layout, &L));
+  DMT_TRY(check_range(L, b0, b1));
+  HIP_OK(launch_set_obs(h->key.precision, h->tw, h->d, h->d_X[0], h->d_X[1], h->d_sel[0],
+                        h->d_tile_qoff, h->d_seg_rec, h->d_seg_q, h->d_seg_np, L->d_glast,
+                        L->d_term, b0, b1, h->d_obsv, h->stream));
+  return DMT_OK;
+}
+
+dmt_status dmt_recompute_guiding_term(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
+                                      int32_t unit) {
+  DMT_TRY(check_h(h));
+  if (unit != DMT_U && unit != DMT_UPROP) return fail(DMT_ERR_INVALID, "bad unit");
+  if (!h->d_obsH) return fail(DMT_ERR_STATE, "dmt_upload_obs first");
+  Layout* L;
+  DMT_TRY(get_layout(h, layout, &L));
+  DMT_TRY(check_range(L, b0, b1));
+  DMT_TRY(law_ready(h, unit, L, b0, b1));
+  if (!h->d_t) return fail(DMT_ERR_STATE, "time grid not uploaded");
+  for (int k = 0; k < 2; ++k)
+    if (h->d_H[0][k] && h->H_shared[k])
+      return fail(DMT_ERR_STATE, "the device filter writes per-point guiding tables; upload H per "
+                                 "segment (not shared) to use recompute_guiding_term");
+  FilterArgs a{};
+  a.d = h->d;
+  a.tw = h->tw;
+  a.unit = unit;
+  a.tile_qoff = h->d_tile_qoff;
+  a.seg_rec = h->d_seg_rec;
+  a.seg_q = h->d_seg_q;
+  a.seg_np = h->d_seg_np;
+  a.gfirst = L->d_gfirst;
+  a.glast = L->d_glast;
+  a.term = L->d_term;
+  a.selPP = h->d_sel[2];
+  a.selPPB = h->d_sel[3];
+  a.b0 = b0;
+  a.b1 = b1;
+  for (int s = 0; s < 2; ++s)
+    for (int k = 0; k < 2; ++k) {
+      a.H[s][k] = h->d_H[s][k];
+      a.F[s][k] = h->d_F[s][k];
+      a.law[s][k] = h->d_law[s][k];
+    }
+  a.t = h->d_t;
+  a.t_shared = h->grid_shared;
+  a.obsH = h->d_obsH;
+  a.obsF = h->d_obsF;
+  a.obsc = h->d_obsc;
+  a.obsv = h->d_obsv;
+  a.art_eps = h->art_eps;
+  a.fail = h->d_fail;
+  HIP_OK(hipMemsetAsync(h->d_fail, 0, sizeof(int), h->stream));
+  {
+    TimedScope ts(h, DMT_K_RECOMPUTE);
+    HIP_OK(launch_backward_filter(h->key.precision, a, h->stream));
+  }
+  int failed = 0;
+  HIP_OK(hipMemcpyAsync(&failed, h->d_fail, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+  HIP_OK(hipStreamSynchronize(h->stream));
+  if (failed) return fail(DMT_ERR_INVALID, "singular I + HK in the device backward filter");
+  return DMT_OK;
+}
+
 dmt_status dmt_swap(dmt_ens* h, int32_t layout, int32_t what, int64_t b0, int64_t b1) {
   DMT_TRY(check_h(h));
   Layout* L;
@@ -1351,39 +1410,8 @@ dmt_status dmt_guiding_linear(int32_t d, const double* Bt, const double* beta, c
   for (int i = npts - 2; i >= 0; --i) {
     const double hstep = t[i + 1] - t[i];
     if (!(hstep > 0)) return fail(DMT_ERR_INVALID, "time grid must be strictly increasing");
-    Mat Phi, K;
-    double mu[3];
-    transition(B, beta, A, hstep, Phi, mu, K);
-    // Gaussian integral over X_{t+h} ~ N(Phi x + mu, K) of exp(-c - x'Hx/2 + F'x)
-    Mat IHK = madd(meye(d), mmul(Hc, K));
-    Mat S;
-    double lad;
-    if (!minv(IHK, S, lad)) return fail(DMT_ERR_INVALID, "singular I + HK in backward filter");
-    Mat Hh = mmul(S, Hc);
-    for (int p = 0; p < d; ++p)
-      for (int q = p + 1; q < d; ++q) { double v = 0.5 * (Hh(p, q) + Hh(q, p)); Hh(p, q) = v; Hh(q, p) = v; }
-    double Fh[3], KF[3];
-    mvec(S, Fc, Fh);
-    mvec(K, Fc, KF);
-    double fkf = 0;
-    for (int p = 0; p < d; ++p) fkf += Fh[p] * KF[p];
-    double ch = cc + 0.5 * lad - 0.5 * fkf;
-    // shift by m = Phi x + mu
-    double Hmu[3];
-    mvec(Hh, mu, Hmu);
-    double g[3];
-    for (int p = 0; p < d; ++p) g[p] = Fh[p] - Hmu[p];
-    Mat PhT = mT(Phi);
-    double Fn[3];
-    mvec(PhT, g, Fn);
-    Mat Hn = mmul(mmul(PhT, Hh), Phi);
-    for (int p = 0; p < d; ++p)
-      for (int q = p + 1; q < d; ++q) { double v = 0.5 * (Hn(p, q) + Hn(q, p)); Hn(p, q) = v; Hn(q, p) = v; }
-    double fmu = 0, muHmu = 0;
-    for (int p = 0; p < d; ++p) { fmu += Fh[p] * mu[p]; muHmu += mu[p] * Hmu[p]; }
-    cc = ch - fmu + 0.5 * muHmu;
-    Hc = Hn;
-    for (int p = 0; p < d; ++p) Fc[p] = Fn[p];
+    if (!flt::filter_step(B, beta, A, hstep, Hc, Fc, cc))
+      return fail(DMT_ERR_INVALID, "singular I + HK in backward filter");
     store(i);
   }
   return DMT_OK;

@@ -164,6 +164,32 @@ class Ensemble:
         """find_W_for_X!: u.WW ← the increments reproducing u.XX under u's laws."""
         L.call("dmt_find_W_for_X", self._h, layout, b0, b1)
 
+    def upload_obs(self, Hobs, Fobs, cobs, artificial_noise=1e-11):
+        """Information of the observation at each segment end (packed H, F, c) for the
+        device backward filter."""
+        Hobs = np.ascontiguousarray(Hobs, dtype=np.float64)
+        Fobs = np.ascontiguousarray(Fobs, dtype=np.float64)
+        cobs = np.ascontiguousarray(cobs, dtype=np.float64)
+        if Hobs.size != self.G * self.hp or Fobs.size != self.G * self.d or cobs.size != self.G:
+            raise ValueError("observation information has the wrong size")
+        L.call("dmt_upload_obs", self._h, L.f64p(Hobs), L.f64p(Fobs), L.f64p(cobs),
+               float(artificial_noise))
+
+    def download_law(self, unit, kind, H_shared=False):
+        """(H, F, laws) of a unit's PP / PPb laws in the reference layout."""
+        Hn = (self.Q0 if H_shared else self.P) * self.hp
+        H = np.empty(Hn)
+        F = np.empty(self.P * self.d)
+        laws = np.empty(self.G * L.LAW_STRIDE)
+        L.call("dmt_download_law", self._h, unit, kind, L.f64p(H), L.f64p(F), L.f64p(laws))
+        return H.reshape(-1, self.hp), F.reshape(-1, self.d), laws.reshape(self.G, L.LAW_STRIDE)
+
+    def set_obs(self, layout, b0, b1):
+        L.call("dmt_set_obs", self._h, layout, b0, b1)
+
+    def recompute_guiding_term(self, layout, b0, b1, unit=L.U):
+        L.call("dmt_recompute_guiding_term", self._h, layout, b0, b1, unit)
+
     def swap(self, layout, what, b0, b1):
         L.call("dmt_swap", self._h, layout, int(what), b0, b1)
 

@@ -18,7 +18,8 @@ import DiffusionMCMCTools: draw_proposal_path!, accept_reject_proposal_path!, lo
     swap_WW!, swap_PP!, swap_ll!, ll_of_accepted, accpt_rate, recompute_path!, find_W_for_X!
 
 export DeviceSamplingEnsemble, DeviceBlockEnsemble, DeviceBlockCollection, DeviceBiBlock,
-    mcmc_step!, mcmc_run!, download_XX, download_WW
+    mcmc_step!, mcmc_run!, download_XX, download_WW, upload_obs!, set_obs!,
+    recompute_guiding_term!
 
 const libdmt = get(ENV, "DMT_LIB", joinpath(@__DIR__, "..", "libdmt.so"))
 
@@ -269,6 +270,21 @@ function recompute_path!(x::DeviceBlocks; skip=0)
         x.se.h, x.layout, x.b0, x.b1, skip, ok))
     Bool.(ok)
 end
+
+"Observation information at every segment end (packed H, F, c) + artificial noise."
+upload_obs!(se::DeviceSamplingEnsemble, Hobs, Fobs, cobs; artificial_noise=1e-11) =
+    GC.@preserve Hobs Fobs cobs check(ccall((:dmt_upload_obs, libdmt), Int32,
+        (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Float64),
+        se.h, Hobs, Fobs, cobs, artificial_noise))
+
+"GP.set_obs!(bb) (src/biblock.jl:273-280) over the blocks."
+set_obs!(x::DeviceBlocks) = check(ccall((:dmt_set_obs, libdmt), Int32,
+    (Ptr{Cvoid}, Int32, Int64, Int64), x.se.h, x.layout, x.b0, x.b1))
+
+"GP.recompute_guiding_term!(bb.b) (unit = DMT_U) or of bb.b° (DMT_UPROP) on the device."
+recompute_guiding_term!(x::DeviceBlocks, unit=DMT_U) = check(ccall(
+    (:dmt_recompute_guiding_term, libdmt), Int32, (Ptr{Cvoid}, Int32, Int64, Int64, Int32),
+    x.se.h, x.layout, x.b0, x.b1, unit))
 
 "find_W_for_X!(b) (src/block.jl:118-131): u.WW from u.XX under the accepted laws."
 find_W_for_X!(x::DeviceBlocks) = check(ccall((:dmt_find_W_for_X, libdmt), Int32,

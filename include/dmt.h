@@ -150,6 +150,12 @@ dmt_status dmt_upload_law(dmt_ens* h, int32_t unit, int32_t kind, const double* 
  * init_paths! (src/sampling_unit.jl:83-87) and find_W_for_X! (src/block.jl:118-131). */
 dmt_status dmt_set_paths(dmt_ens* h, int32_t unit, const double* X, const double* W);
 
+/* Download the guiding tables and law records of u.PP/u°.PP (kind PP) or PPb, resolving
+ * swap_PP!: H[P][hp] (or H[points of recording 0][hp] when shared), F[P][d], laws[G][64];
+ * any pointer may be NULL. */
+dmt_status dmt_download_law(dmt_ens* h, int32_t unit, int32_t kind, double* H, double* F,
+                            double* laws);
+
 /* Download XX (what=0) / WW (what=1) of a unit, resolving all swaps, reference layout. */
 dmt_status dmt_download_paths(dmt_ens* h, int32_t unit, int32_t what, double* out);
 
@@ -206,6 +212,26 @@ dmt_status dmt_recompute_path(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1
  *   ΔW_i = σ⁻¹ (x_{i+1} − x_i − b°(t_i, x_i)·dt_i)   (FHN: on coordinate 1, / σ_1),
  * W(t0) = 0.  Parallel in time. */
 dmt_status dmt_find_W_for_X(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1);
+
+/* ---- guiding terms on the device ----
+ * Information of the (real) observation at the end of every segment, packed like H:
+ * Hobs[G][d(d+1)/2] = LᵀΣ⁻¹L, Fobs[G][d] = LᵀΣ⁻¹v, cobs[G] = ½vᵀΣ⁻¹v + (k/2)log2π + ½log|Σ|
+ * (SURVEY.md A.5), and the variance of the artificial exact end observation of blocking laws
+ * (artificial_noise, src/sampling_unit.jl:57, default 1e-11). */
+dmt_status dmt_upload_obs(dmt_ens* h, const double* Hobs, const double* Fobs, const double* cobs,
+                          double artificial_noise);
+/* GP.set_obs!(bb) (src/biblock.jl:273-280, broadcasts src/block_collection.jl:199,
+ * src/block_ensemble.jl:186): freeze the end point of each non-terminal block's accepted
+ * path as the artificial observation of its P_last law (both units; terminal blocks: no-op). */
+dmt_status dmt_set_obs(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1);
+/* GP.recompute_guiding_term!(b) for the blocks' laws of `unit` (u: bb.b, u°: bb.b°)
+ * (src/block.jl:102-110, src/biblock.jl:288-291, src/block_collection.jl:208-221): exact
+ * discrete backward filter of the linear auxiliary law (law record B̃, β̃, ã) over each segment,
+ * backward from the block end — P_last: observation + artificial observation; other segments:
+ * observation + the guiding term at the start of the next segment.  Writes H, F at every point
+ * and c(t0) into the law record.  Needs per-segment (not shared) H tables. */
+dmt_status dmt_recompute_guiding_term(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
+                                      int32_t unit);
 
 /* swap_XX!/swap_WW!/swap_PP!/swap_ll! (src/biblock.jl:148-209), what = DMT_SWAP_* mask. */
 dmt_status dmt_swap(dmt_ens* h, int32_t layout, int32_t what, int64_t b0, int64_t b1);

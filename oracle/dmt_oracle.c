@@ -361,6 +361,7 @@ int SFX(orc_solve_segment)(int model, int d, int m, const double* law, int npts,
     return ok;
 }
 
+
 /* DD.invsolve!(X, W, P) (find_W_for_X!, src/block.jl:118-131): increments reproducing X
  * under the guided Euler step of law P (canonical order):
  *   r_a = fma(-bg_a, dt, x_{i+1,a} - x_{i,a});  dW = siginv·r (d = m), or r_1 / sigma_10 (FHN).
@@ -726,3 +727,158 @@ void SFX(orc_normals_segment)(uint64_t seed, uint32_t g, uint32_t iter, uint32_t
         if (i + 1 < n) Z[i + 1] = z1;
     }
 }
+
+#if IS_F64
+/* ---- exact discrete backward filter of a linear auxiliary law (recompute_guiding_term!,
+ * SURVEY.md A.5), restating the build's algorithm: Taylor series with scaling and squaring
+ * for the transition (Phi, mu, K), Gaussian update with Gauss-Jordan inverse; plain IEEE
+ * operations in the same order, log|det| through rng_log.  Double only. */
+typedef struct { int n; double a[9]; } fm_t;
+static fm_t fm_zero(int n) { fm_t m; m.n = n; for (int i = 0; i < 9; ++i) m.a[i] = 0.0; return m; }
+static fm_t fm_eye(int n) { fm_t m = fm_zero(n); for (int i = 0; i < n; ++i) m.a[i * n + i] = 1.0; return m; }
+static fm_t fm_mul(const fm_t* A, const fm_t* B) {
+    int n = A->n; fm_t C = fm_zero(n);
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) {
+            double s = 0.0;
+            for (int k = 0; k < n; ++k) s += A->a[i * n + k] * B->a[k * n + j];
+            C.a[i * n + j] = s;
+        }
+    return C;
+}
+static fm_t fm_T(const fm_t* A) {
+    int n = A->n; fm_t C = fm_zero(n);
+    for (int i = 0; i < n; ++i) for (int j = 0; j < n; ++j) C.a[i * n + j] = A->a[j * n + i];
+    return C;
+}
+static fm_t fm_add(const fm_t* A, const fm_t* B) {
+    fm_t C = *A; for (int i = 0; i < A->n * A->n; ++i) C.a[i] += B->a[i]; return C;
+}
+static void fm_vec(const fm_t* A, const double* x, double* y) {
+    int n = A->n;
+    for (int i = 0; i < n; ++i) { double s = 0.0; for (int k = 0; k < n; ++k) s += A->a[i * n + k] * x[k]; y[i] = s; }
+}
+static double fm_norm(const fm_t* A) {
+    double s = 0.0; for (int i = 0; i < A->n * A->n; ++i) s = fmax(s, fabs(A->a[i])); return s * A->n;
+}
+static int fm_inv(const fm_t* A, fm_t* Inv, double* lad) {
+    int n = A->n; double w[3][6];
+    for (int i = 0; i < n; ++i) for (int j = 0; j < n; ++j) { w[i][j] = A->a[i * n + j]; w[i][n + j] = (i == j) ? 1.0 : 0.0; }
+    *lad = 0.0;
+    for (int c = 0; c < n; ++c) {
+        int p = c;
+        for (int i = c + 1; i < n; ++i) if (fabs(w[i][c]) > fabs(w[p][c])) p = i;
+        if (w[p][c] == 0.0) return 0;
+        if (p != c) for (int j = 0; j < 2 * n; ++j) { double t = w[p][j]; w[p][j] = w[c][j]; w[c][j] = t; }
+        double piv = w[c][c];
+        *lad += rng_log(fabs(piv));
+        for (int j = 0; j < 2 * n; ++j) w[c][j] /= piv;
+        for (int i = 0; i < n; ++i) if (i != c) {
+            double f = w[i][c];
+            if (f != 0.0) for (int j = 0; j < 2 * n; ++j) w[i][j] -= f * w[c][j];
+        }
+    }
+    *Inv = fm_zero(n);
+    for (int i = 0; i < n; ++i) for (int j = 0; j < n; ++j) Inv->a[i * n + j] = w[i][n + j];
+    return 1;
+}
+static void fm_transition(const fm_t* B, const double* beta, const fm_t* At, double h,
+                          fm_t* Phi, double* mu, fm_t* K) {
+    int n = B->n, sq = 0;
+    double hs = h;
+    double nb = fm_norm(B);
+    while (nb * hs > 0.25 && sq < 40) { hs *= 0.5; ++sq; }
+    fm_t A = *B;
+    for (int i = 0; i < n * n; ++i) A.a[i] *= hs;
+    *Phi = fm_eye(n);
+    fm_t term = fm_eye(n), S1 = fm_eye(n), Lk = *At;
+    *K = fm_zero(n);
+    for (int i = 0; i < n * n; ++i) K->a[i] = hs * Lk.a[i];
+    fm_t BT = fm_T(B);
+    for (int k = 1; k <= 30; ++k) {
+        term = fm_mul(&term, &A);
+        for (int i = 0; i < n * n; ++i) term.a[i] /= k;
+        *Phi = fm_add(Phi, &term);
+        fm_t t2 = term;
+        for (int i = 0; i < n * n; ++i) t2.a[i] /= (k + 1);
+        S1 = fm_add(&S1, &t2);
+        fm_t l1 = fm_mul(B, &Lk), l2 = fm_mul(&Lk, &BT);
+        fm_t nl = fm_add(&l1, &l2);
+        for (int i = 0; i < n * n; ++i) nl.a[i] *= hs / k;
+        Lk = nl;
+        for (int i = 0; i < n * n; ++i) K->a[i] += hs * Lk.a[i] / (k + 1);
+        if (fm_norm(&term) < 1e-18 && fm_norm(&Lk) * hs < 1e-18 * (1.0 + fm_norm(K))) break;
+    }
+    double sb[3];
+    fm_vec(&S1, beta, sb);
+    for (int i = 0; i < n; ++i) mu[i] = hs * sb[i];
+    for (int s = 0; s < sq; ++s) {
+        double m2[3];
+        fm_vec(Phi, mu, m2);
+        for (int i = 0; i < n; ++i) mu[i] = m2[i] + mu[i];
+        fm_t PK = fm_mul(Phi, K), PT = fm_T(Phi), PKP = fm_mul(&PK, &PT);
+        *K = fm_add(&PKP, K);
+        *Phi = fm_mul(Phi, Phi);
+    }
+    for (int i = 0; i < n; ++i)
+        for (int j = i + 1; j < n; ++j) { double v = 0.5 * (K->a[i * n + j] + K->a[j * n + i]); K->a[i * n + j] = v; K->a[j * n + i] = v; }
+}
+static int fm_filter_step(const fm_t* B, const double* beta, const fm_t* A, double h, fm_t* Hc,
+                          double* Fc, double* cc) {
+    int d = B->n;
+    fm_t Phi, K; double mu[3];
+    fm_transition(B, beta, A, h, &Phi, mu, &K);
+    fm_t HK = fm_mul(Hc, &K), I = fm_eye(d);
+    fm_t IHK = fm_add(&I, &HK);
+    fm_t S; double lad;
+    if (!fm_inv(&IHK, &S, &lad)) return 0;
+    fm_t Hh = fm_mul(&S, Hc);
+    for (int p = 0; p < d; ++p)
+        for (int q = p + 1; q < d; ++q) { double v = 0.5 * (Hh.a[p * d + q] + Hh.a[q * d + p]); Hh.a[p * d + q] = v; Hh.a[q * d + p] = v; }
+    double Fh[3], KF[3];
+    fm_vec(&S, Fc, Fh);
+    fm_vec(&K, Fc, KF);
+    double fkf = 0.0;
+    for (int p = 0; p < d; ++p) fkf += Fh[p] * KF[p];
+    double ch = *cc + 0.5 * lad - 0.5 * fkf;
+    double Hmu[3], g[3], Fn[3];
+    fm_vec(&Hh, mu, Hmu);
+    for (int p = 0; p < d; ++p) g[p] = Fh[p] - Hmu[p];
+    fm_t PhT = fm_T(&Phi);
+    fm_vec(&PhT, g, Fn);
+    fm_t t1 = fm_mul(&PhT, &Hh);
+    fm_t Hn = fm_mul(&t1, &Phi);
+    for (int p = 0; p < d; ++p)
+        for (int q = p + 1; q < d; ++q) { double v = 0.5 * (Hn.a[p * d + q] + Hn.a[q * d + p]); Hn.a[p * d + q] = v; Hn.a[q * d + p] = v; }
+    double fmu = 0.0, muHmu = 0.0;
+    for (int p = 0; p < d; ++p) { fmu += Fh[p] * mu[p]; muHmu += mu[p] * Hmu[p]; }
+    *cc = ch - fmu + 0.5 * muHmu;
+    *Hc = Hn;
+    for (int p = 0; p < d; ++p) Fc[p] = Fn[p];
+    return 1;
+}
+
+/* Backward filter over one segment's grid t[npts] from the terminal information (HT packed,
+ * FT, cT): H[npts][hp] packed, F[npts][d], c[npts] (double).  Returns 0 if singular. */
+int orc_backward_filter_segment(int d, const double* Bt, const double* beta, const double* at,
+                                int npts, const double* t, const double* HT, const double* FT,
+                                double cT, double* H, double* F, double* c) {
+    int hp = d * (d + 1) / 2;
+    fm_t B = fm_zero(d), A = fm_zero(d), Hc = fm_zero(d);
+    for (int i = 0; i < d * d; ++i) B.a[i] = Bt[i];
+    for (int i = 0; i < d; ++i)
+        for (int j = 0; j < d; ++j) { A.a[i * d + j] = at[pidx(d, i, j)]; Hc.a[i * d + j] = HT[pidx(d, i, j)]; }
+    double Fc[3] = {0, 0, 0}, cc = cT;
+    for (int i = 0; i < d; ++i) Fc[i] = FT[i];
+    for (int i = npts - 1; i >= 0; --i) {
+        if (i < npts - 1 && !fm_filter_step(&B, beta, &A, t[i + 1] - t[i], &Hc, Fc, &cc)) return 0;
+        for (int p = 0; p < d; ++p)
+            for (int q = p; q < d; ++q) H[(size_t)i * hp + pidx(d, p, q)] = Hc.a[p * d + q];
+        for (int p = 0; p < d; ++p) F[(size_t)i * d + p] = Fc[p];
+        c[i] = cc;
+    }
+    return 1;
+}
+/* the canonical log kernel, exposed for the Python container restatement */
+double orc_rng_log(double u) { return rng_log(u); }
+#endif

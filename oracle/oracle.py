@@ -79,6 +79,10 @@ def _load():
     lib.orc_exp1.restype = d_
     lib.orc_set_sequential_ou.argtypes = [i_]
     lib.orc_set_sequential_ou.restype = None
+    lib.orc_backward_filter_segment.argtypes = [i_, P, P, P, i_, P, P, P, d_, P, P, P]
+    lib.orc_backward_filter_segment.restype = i_
+    lib.orc_rng_log.argtypes = [d_]
+    lib.orc_rng_log.restype = d_
     lib.orc_philox_raw.argtypes = [u64, P, P]
     lib.orc_philox_raw.restype = None
     return lib
@@ -111,6 +115,24 @@ def solve_segment(model, d, m, law, t, H, F, W, y1, prec=0):
     ok = getattr(lib, f"orc_solve_segment_{_sfx(prec)}")(model, d, m, _p(law), n, _p(t), _p(H),
                                                           _p(F), _p(W), _p(y1), _p(X), _p(ll))
     return X, dt(ll[0]), bool(ok)
+
+
+LOG2PI = float.fromhex("0x1.d67f1c864beb4p+0")
+
+
+def backward_filter_segment(d, Bt, beta, at_packed, t, HT_packed, FT, cT):
+    """Exact discrete backward filter of a linear auxiliary law over one grid (double):
+    returns H (npts × hp packed), F (npts × d), c (npts)."""
+    t = np.ascontiguousarray(t, dtype=np.float64)
+    n = t.size
+    hp = d * (d + 1) // 2
+    H = np.empty((n, hp)); F = np.empty((n, d)); c = np.empty(n)
+    args = [np.ascontiguousarray(a, dtype=np.float64) for a in (Bt, beta, at_packed, HT_packed, FT)]
+    ok = lib.orc_backward_filter_segment(d, _p(args[0]), _p(args[1]), _p(args[2]), n, _p(t),
+                                         _p(args[3]), _p(args[4]), float(cT), _p(H), _p(F), _p(c))
+    if not ok:
+        raise FloatingPointError("singular I + HK in the backward filter")
+    return H, F, c
 
 
 def invsolve_segment(model, d, m, law, t, H, F, X, prec=0):
@@ -189,6 +211,22 @@ def philox_raw(seed, ctr):
     for i in range(ctr.shape[0]):
         lib.orc_philox_raw(seed, _p(ctr[i]), _p(out[i]))
     return out
+
+
+def unpacked(hp_vec, d):
+    """Packed upper triangle (row-major) -> full symmetric d×d."""
+    M = np.empty((d, d))
+    k = 0
+    for a in range(d):
+        for b in range(a, d):
+            M[a, b] = M[b, a] = hp_vec[k]
+            k += 1
+    return M
+
+
+def packed_sym(M):
+    d = M.shape[0]
+    return np.array([M[a, b] for a in range(d) for b in range(a, d)])
 
 
 def pairwise_tree(vals):
@@ -475,6 +513,67 @@ class OracleEnsemble:
             bk.llp, ok = self._solve_block(bk, 1, 1, 0, 1, "given", None, 0, 0)
             oks.append(ok)
         return np.array(oks) if want_success else None
+
+    # ---- guiding terms (recompute_guiding_term!, set_obs!)
+    def upload_obs(self, Hobs, Fobs, cobs, artificial_noise=1e-11):
+        self.obsH = np.asarray(Hobs, dtype=np.float64).reshape(self.G, self.hp).copy()
+        self.obsF = np.asarray(Fobs, dtype=np.float64).reshape(self.G, self.d).copy()
+        self.obsc = np.asarray(cobs, dtype=np.float64).reshape(self.G).copy()
+        self.art_eps = float(artificial_noise)
+        if not hasattr(self, "obsv"):
+            self.obsv = np.zeros((self.G, self.d))
+
+    def download_law(self, unit, kind, H_shared=False):
+        me = self._unit(unit)
+        tab = me.PP if kind == 0 else me.PPb
+        H = np.concatenate([lw.H for lw in tab]).astype(np.float64)
+        F = np.concatenate([lw.F for lw in tab]).astype(np.float64)
+        laws = np.stack([lw.rec for lw in tab])
+        return H, F, laws
+
+    def set_obs(self, layout, b0, b1):
+        """GP.set_obs!(bb) (src/biblock.jl:273-280): P_last observes the accepted end point."""
+        for bk in self.layouts[layout][b0:b1]:
+            if not bk.term:
+                self.obsv[bk.g1] = self.u.XX[bk.g1][-1].astype(np.float64)
+
+    def recompute_guiding_term(self, layout, b0, b1, unit=0):
+        """GP.recompute_guiding_term!(b) (src/block.jl:102-110) for `unit`'s laws: segments
+        backward from the block end, P_last with observation + artificial observation, the
+        others with observation + the next segment's guiding term at its start."""
+        d, hp = self.d, self.hp
+        for bk in self.layouts[layout][b0:b1]:
+            nxt = None
+            for g in range(bk.g1, bk.g0 - 1, -1):
+                lw = self._law(unit, bk, g)
+                last_b = (not bk.term) and g == bk.g1
+                HT = unpacked(self.obsH[g], d)
+                FT = self.obsF[g].copy()
+                cT = float(self.obsc[g])
+                if last_b:
+                    inv = 1.0 / self.art_eps
+                    vv = 0.0
+                    for p in range(d):
+                        v = float(self.obsv[g, p])
+                        HT[p, p] += inv
+                        FT[p] += inv * v
+                        vv += v * v
+                    cT += 0.5 * inv * vv + 0.5 * d * (LOG2PI + lib.orc_rng_log(self.art_eps))
+                elif g < bk.g1:
+                    Hn, Fn, cn = nxt
+                    HT = HT + Hn
+                    FT = FT + Fn
+                    cT += cn
+                rec = lw.rec
+                Bt = rec[31:31 + d * d]
+                beta = rec[40:40 + d]
+                at = rec[25:25 + hp] - rec[43:43 + hp]
+                H, F, c = backward_filter_segment(d, Bt, beta, at, self.t[g].astype(np.float64),
+                                                  packed_sym(HT), FT, cT)
+                lw.H = H.astype(self.dt)
+                lw.F = F.astype(self.dt)
+                lw.rec[L_C0] = c[0]
+                nxt = (unpacked(H[0], d), F[0].copy(), float(c[0]))
 
     def find_W_for_X(self, layout, b0, b1):
         """find_W_for_X!(b) (src/block.jl:118-131): u.WW[g] ← invsolve(u.XX[g], law of g)."""

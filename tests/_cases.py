@@ -61,6 +61,7 @@ def ragged_case(seed=5, prec=L.F64):
     model = FHN(0.1, -0.8, 1.5, 0.0, 0.3)
     nsegs = [4, 6, 5]
     n_points, grids, laws_pp, H_pp, F_pp, H_b, F_b, laws_b, X0 = [], [], [], [], [], [], [], [], []
+    Hobs, Fobs, cobs = [], [], []
     for r, K in enumerate(nsegs):
         t0 = 0.0
         obs_t = np.cumsum(rng.uniform(0.05, 0.12, K))
@@ -75,6 +76,9 @@ def ragged_case(seed=5, prec=L.F64):
             Ho, Fo, co = infos[-1]
             binfo.append((Ha + Ho, Fa + Fo, ca + co))
             t0 = obs_t[k]
+        for inf in infos:  # the observation at each segment end (for the device filter)
+            Hobs.append(packed(inf[0])); Fobs.append(np.asarray(inf[1], dtype=np.float64))
+            cobs.append(float(inf[2]))
         chain = guiding_chain(auxes, gr, infos)
         for k in range(K):
             H, F, c = chain[k]
@@ -93,7 +97,8 @@ def ragged_case(seed=5, prec=L.F64):
     case = dict(model=model, n_points=npts_nested, t=np.concatenate(grids),
                 H=np.concatenate(H_pp), F=np.concatenate(F_pp), laws=np.stack(laws_pp),
                 Hb=np.concatenate(H_b), Fb=np.concatenate(F_b), lawsb=np.stack(laws_b),
-                X0=np.concatenate(X0), prec=prec, nsegs=nsegs)
+                X0=np.concatenate(X0), prec=prec, nsegs=nsegs, Hobs=np.stack(Hobs),
+                Fobs=np.stack(Fobs), cobs=np.array(cobs))
     P = case["t"].size
     G = sum(nsegs)
     case["Z0"] = rng.standard_normal((P - G, 1))

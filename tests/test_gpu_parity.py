@@ -343,3 +343,55 @@ def test_find_W_for_X_blocking_layouts(mapping):
         for e in (dev, ora):
             e.find_W_for_X(lid, 0, nb)
         cs.assert_paths_equal(dev, ora)
+
+
+@pytest.mark.parametrize("mapping", MAPPINGS)
+def test_device_guiding_term_reproduces_uploaded_tables(mapping):
+    """recompute_guiding_term! on the device over whole-recording terminal blocks rebuilds the
+    uploaded PP tables bit for bit (same chained filter as the host set-up)."""
+    import diffusionmcmctools_amd as d
+    case = cs.ragged_case()
+    m = case["model"]
+    dev = d.Ensemble(m.kind, m.d, m.m, case["n_points"], precision=case["prec"], seed=1,
+                     mapping=mapping)
+    cs.load_ragged(dev, case)
+    H0, F0, laws0 = dev.download_law(L.U, L.LAW_PP)
+    R = len(case["nsegs"])
+    lay = dev.create_layout([1] * R, [0] * R, [k - 1 for k in case["nsegs"]], [1] * R,
+                            [0.5] * R, 0)
+    dev.upload_obs(case["Hobs"], case["Fobs"], case["cobs"])
+    dev.recompute_guiding_term(lay, 0, R, unit=L.U)
+    H1, F1, laws1 = dev.download_law(L.U, L.LAW_PP)
+    assert np.array_equal(H1, H0) and np.array_equal(F1, F0)
+    assert np.array_equal(laws1[:, L.LAW_C0], laws0[:, L.LAW_C0])
+
+
+@pytest.mark.parametrize("mapping", MAPPINGS)
+def test_blocking_loop_bit_exact(mapping):
+    """The reference's smoothing-with-blocking iteration (docs/src/tutorials/biblock/
+    smoothing_with_blocking.md:34-44): set_obs!, recompute_guiding_term!(bb.b),
+    find_W_for_X!, loglikhd!, draw_proposal_path!, accept_reject_proposal_path! — alternating
+    two blockings, device == oracle bit for bit (laws, paths, ll, decisions)."""
+    case, dev, ora, ids = cs.ragged_pair(mapping=mapping, hist_len=6)
+    for e in (dev, ora):
+        e.upload_obs(case["Hobs"], case["Fobs"], case["cobs"])
+    rng = np.random.default_rng(8)
+    S = dev.S
+    for i in range(1, 7):
+        lid, nb = ids[(i - 1) % 2]
+        Z = rng.standard_normal((S, 1))
+        E = rng.exponential(1.0, nb)
+        for e in (dev, ora):
+            e.set_obs(lid, 0, nb)
+            e.recompute_guiding_term(lid, 0, nb, unit=L.U)
+            e.find_W_for_X(lid, 0, nb)
+            e.loglikhd(lid, L.U, 0, nb)
+            e.draw_proposal(lid, 0, nb, Z=Z, iter=i)
+        for kind in (L.LAW_PP, L.LAW_PPB):
+            for a_, b_ in zip(dev.download_law(L.U, kind), ora.download_law(L.U, kind)):
+                assert np.array_equal(a_, b_), f"iteration {i}, law kind {kind}"
+        ad = dev.accept_reject(lid, 0, nb, i, E=E, want_acc=True)
+        ao = ora.accept_reject(lid, 0, nb, i, E=E, want_acc=True)
+        assert np.array_equal(ad, ao), f"iteration {i}"
+        cs.assert_paths_equal(dev, ora)
+        cs.assert_ll_equal(dev, ora, lid, nb)

@@ -84,6 +84,11 @@ def test_guiding_matches_expm_filter(dmt, case):
     np.testing.assert_allclose(F, Fe, rtol=1e-8, atol=1e-9 * np.abs(Fe).max())
     np.testing.assert_allclose(c, ce, rtol=1e-8, atol=1e-8 * max(1.0, np.abs(ce).max()))
     assert d in (2, 3)
+    # the oracle's C restatement of the filter (used for the device recompute_guiding_term
+    # parity) is the same arithmetic as the product's host filter: bit for bit
+    Ho, Fo, co = orc.backward_filter_segment(d, np.asarray(B).ravel(), beta, _packed(at), t,
+                                             _packed(HT), FT, cT)
+    assert np.array_equal(Ho, H) and np.array_equal(Fo, F) and np.array_equal(co, c)
 
 
 def test_obs_term_is_gaussian_density(dmt):
@@ -228,3 +233,23 @@ def test_invsolve_inverts_the_forward_solve(cfg):
     X2, _, ok2 = orc.solve_segment(w.model.kind, w.d, w.m, w.laws[0], w.t, H, w.F, W2, w.X0[0], prec)
     assert ok2
     np.testing.assert_allclose(X2, X, rtol=tol, atol=tol)
+
+
+def test_oracle_recompute_guiding_term_reproduces_uploaded_tables():
+    """recompute_guiding_term! restated on whole-recording terminal blocks, from the per-segment
+    observation information, rebuilds exactly the PP tables the set-up uploaded (both are the
+    same chained backward filter)."""
+    import _cases as cs
+    case = cs.ragged_case()
+    m = case["model"]
+    ora = orc.OracleEnsemble(m.kind, m.d, m.m, case["n_points"], prec=case["prec"], seed=1)
+    cs.load_ragged(ora, case)
+    H0, F0, laws0 = ora.download_law(0, 0)
+    R = len(case["nsegs"])
+    lay = ora.create_layout([1] * R, [0] * R, [k - 1 for k in case["nsegs"]], [1] * R,
+                            [0.5] * R, 0)
+    ora.upload_obs(case["Hobs"], case["Fobs"], case["cobs"])
+    ora.recompute_guiding_term(lay, 0, R, unit=0)
+    H1, F1, laws1 = ora.download_law(0, 0)
+    assert np.array_equal(H1, H0) and np.array_equal(F1, F0)
+    assert np.array_equal(laws1[:, 49], laws0[:, 49])
