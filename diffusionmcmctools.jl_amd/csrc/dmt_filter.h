@@ -16,45 +16,75 @@
 namespace dmt {
 namespace flt {
 
+// Dimension N is a compile-time constant (1, 2 or 3): fixed-size arrays, fully unrolled
+// loops — registers, never scratch, on the device.
+template <int N>
 struct Mat {
-  int n;
-  double a[9];
-  DMT_HD double& operator()(int i, int j) { return a[i * n + j]; }
-  DMT_HD double operator()(int i, int j) const { return a[i * n + j]; }
+  static constexpr int n = N;
+  double a[N * N];
+  DMT_HD double& operator()(int i, int j) { return a[i * N + j]; }
+  DMT_HD double operator()(int i, int j) const { return a[i * N + j]; }
 };
-DMT_HD Mat mzero(int n) { Mat m; m.n = n; for (int i = 0; i < 9; ++i) m.a[i] = 0.0; return m; }
-DMT_HD Mat meye(int n) { Mat m = mzero(n); for (int i = 0; i < n; ++i) m(i, i) = 1.0; return m; }
-DMT_HD Mat mmul(const Mat& A, const Mat& B) {
-  Mat C = mzero(A.n);
-  for (int i = 0; i < A.n; ++i)
-    for (int j = 0; j < A.n; ++j) {
+template <int N>
+DMT_HD Mat<N> mzero() {
+  Mat<N> m;
+#pragma unroll
+  for (int i = 0; i < N * N; ++i) m.a[i] = 0.0;
+  return m;
+}
+template <int N>
+DMT_HD Mat<N> meye() {
+  Mat<N> m = mzero<N>();
+#pragma unroll
+  for (int i = 0; i < N; ++i) m(i, i) = 1.0;
+  return m;
+}
+template <int N>
+DMT_HD Mat<N> mmul(const Mat<N>& A, const Mat<N>& B) {
+  Mat<N> C;
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
       double s = 0.0;
-      for (int k = 0; k < A.n; ++k) s += A(i, k) * B(k, j);
+#pragma unroll
+      for (int k = 0; k < N; ++k) s += A(i, k) * B(k, j);
       C(i, j) = s;
     }
   return C;
 }
-DMT_HD Mat mT(const Mat& A) {
-  Mat C = mzero(A.n);
-  for (int i = 0; i < A.n; ++i) for (int j = 0; j < A.n; ++j) C(i, j) = A(j, i);
+template <int N>
+DMT_HD Mat<N> mT(const Mat<N>& A) {
+  Mat<N> C;
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+#pragma unroll
+    for (int j = 0; j < N; ++j) C(i, j) = A(j, i);
   return C;
 }
-DMT_HD Mat madd(const Mat& A, const Mat& B) {
-  Mat C = A;
-  for (int i = 0; i < A.n * A.n; ++i) C.a[i] += B.a[i];
+template <int N>
+DMT_HD Mat<N> madd(const Mat<N>& A, const Mat<N>& B) {
+  Mat<N> C = A;
+#pragma unroll
+  for (int i = 0; i < N * N; ++i) C.a[i] += B.a[i];
   return C;
 }
-DMT_HD void mvec(const Mat& A, const double* x, double* y) {
-  for (int i = 0; i < A.n; ++i) {
+template <int N>
+DMT_HD void mvec(const Mat<N>& A, const double* x, double* y) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
     double s = 0.0;
-    for (int k = 0; k < A.n; ++k) s += A(i, k) * x[k];
+#pragma unroll
+    for (int k = 0; k < N; ++k) s += A(i, k) * x[k];
     y[i] = s;
   }
 }
-DMT_HD double mnorm(const Mat& A) {
+template <int N>
+DMT_HD double mnorm(const Mat<N>& A) {
   double s = 0.0;
-  for (int i = 0; i < A.n * A.n; ++i) s = fmax(s, fabs(A.a[i]));
-  return s * A.n;
+#pragma unroll
+  for (int i = 0; i < N * N; ++i) s = fmax(s, fabs(A.a[i]));
+  return s * N;
 }
 
 // log(u), u > 0 finite: the rng_log polynomial kernel (dmt_device.h), as host/device code
@@ -78,108 +108,153 @@ DMT_HD double flt_log(double u) {
   return fma(de, 0x1.62e42p-1, fma(de, 0x1.fdf473de6af28p-22, lm));
 }
 
-// inverse and log|det| by Gauss–Jordan with partial pivoting; false if singular
-DMT_HD bool minv(const Mat& A, Mat& Inv, double& logabsdet) {
-  const int n = A.n;
-  double w[3][6];
-  for (int i = 0; i < n; ++i)
-    for (int j = 0; j < n; ++j) { w[i][j] = A(i, j); w[i][n + j] = (i == j) ? 1.0 : 0.0; }
+// inverse and log|det| by Gauss–Jordan with partial pivoting; false if singular.  Row swaps
+// are done with selects over all rows (no dynamic register indexing).
+template <int N>
+DMT_HD bool minv(const Mat<N>& A, Mat<N>& Inv, double& logabsdet) {
+  double w[N][2 * N];
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+#pragma unroll
+    for (int j = 0; j < N; ++j) { w[i][j] = A(i, j); w[i][N + j] = (i == j) ? 1.0 : 0.0; }
   logabsdet = 0.0;
-  for (int c = 0; c < n; ++c) {
+#pragma unroll
+  for (int c = 0; c < N; ++c) {
     int p = c;
-    for (int i = c + 1; i < n; ++i) if (fabs(w[i][c]) > fabs(w[p][c])) p = i;
-    if (w[p][c] == 0.0) return false;
-    if (p != c)
-      for (int j = 0; j < 2 * n; ++j) { const double tmp = w[p][j]; w[p][j] = w[c][j]; w[c][j] = tmp; }
+    double best = fabs(w[c][c]);
+#pragma unroll
+    for (int i = c + 1; i < N; ++i) {
+      const double v = fabs(w[i][c]);
+      if (v > best) { best = v; p = i; }
+    }
+    double prow[2 * N];
+#pragma unroll
+    for (int j = 0; j < 2 * N; ++j) {
+      double v = w[c][j];
+#pragma unroll
+      for (int i = c + 1; i < N; ++i) v = (p == i) ? w[i][j] : v;
+      prow[j] = v;
+    }
+    if (prow[c] == 0.0) return false;
+#pragma unroll
+    for (int i = c + 1; i < N; ++i)  // the swapped-out row takes pivot row c's place
+#pragma unroll
+      for (int j = 0; j < 2 * N; ++j) w[i][j] = (p == i) ? w[c][j] : w[i][j];
+#pragma unroll
+    for (int j = 0; j < 2 * N; ++j) w[c][j] = prow[j];
     const double piv = w[c][c];
     logabsdet += flt_log(fabs(piv));
-    for (int j = 0; j < 2 * n; ++j) w[c][j] /= piv;
-    for (int i = 0; i < n; ++i)
+#pragma unroll
+    for (int j = 0; j < 2 * N; ++j) w[c][j] /= piv;
+#pragma unroll
+    for (int i = 0; i < N; ++i)
       if (i != c) {
         const double f = w[i][c];
-        if (f != 0.0) for (int j = 0; j < 2 * n; ++j) w[i][j] -= f * w[c][j];
+        if (f != 0.0) {
+#pragma unroll
+          for (int j = 0; j < 2 * N; ++j) w[i][j] -= f * w[c][j];
+        }
       }
   }
-  Inv = mzero(n);
-  for (int i = 0; i < n; ++i) for (int j = 0; j < n; ++j) Inv(i, j) = w[i][n + j];
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+#pragma unroll
+    for (int j = 0; j < N; ++j) Inv(i, j) = w[i][N + j];
   return true;
 }
 
 // Exact transition of dX = (BX + beta)dt + sigma dW over a step h:
-// X_{t+h} = Phi X_t + mu + N(0, K).  Taylor series with scaling and squaring.
-DMT_HD void transition(const Mat& B, const double* beta, const Mat& At, double h, Mat& Phi,
-                       double* mu, Mat& K) {
-  const int n = B.n;
+// X_{t+h} = Phi X_t + mu + N(0, K).  Taylor series with scaling and squaring; the series
+// multiplies by the correctly rounded reciprocals 1/k (no per-element divisions).
+template <int N>
+DMT_HD void transition(const Mat<N>& B, const double* beta, const Mat<N>& At, double h,
+                       Mat<N>& Phi, double* mu, Mat<N>& K) {
+  constexpr int n = N;
   int sq = 0;
   double hs = h;
   const double nb = mnorm(B);
   while (nb * hs > 0.25 && sq < 40) { hs *= 0.5; ++sq; }
-  Mat A = B;
+  Mat<N> A = B;
+#pragma unroll
   for (int i = 0; i < n * n; ++i) A.a[i] *= hs;
-  Phi = meye(n);
-  Mat term = meye(n);
-  Mat S1 = meye(n);  // sum A^k/(k+1)!
-  Mat Lk = At;       // L^k(At) hs^k / k!,  L(X) = BX + XB^T
-  K = mzero(n);
+  Phi = meye<N>();
+  Mat<N> term = meye<N>();
+  Mat<N> S1 = meye<N>();  // sum A^k/(k+1)!
+  Mat<N> Lk = At;         // L^k(At) hs^k / k!,  L(X) = BX + XB^T
+  K = mzero<N>();
+#pragma unroll
   for (int i = 0; i < n * n; ++i) K.a[i] = hs * Lk.a[i];
-  const Mat BT = mT(B);
+  const Mat<N> BT = mT(B);
+  double rk = 1.0;  // 1/k, correctly rounded; one division per term
   for (int k = 1; k <= 30; ++k) {
+    const double rk1 = 1.0 / (double)(k + 1);
     term = mmul(term, A);
-    for (int i = 0; i < n * n; ++i) term.a[i] /= k;
+#pragma unroll
+    for (int i = 0; i < n * n; ++i) term.a[i] *= rk;
     Phi = madd(Phi, term);
-    Mat t2 = term;
-    for (int i = 0; i < n * n; ++i) t2.a[i] /= (k + 1);
+    Mat<N> t2 = term;
+#pragma unroll
+    for (int i = 0; i < n * n; ++i) t2.a[i] *= rk1;
     S1 = madd(S1, t2);
-    Mat nl = madd(mmul(B, Lk), mmul(Lk, BT));
-    for (int i = 0; i < n * n; ++i) nl.a[i] *= hs / k;
+    Mat<N> nl = madd(mmul(B, Lk), mmul(Lk, BT));
+    const double c0 = hs * rk, c1 = hs * rk1;
+#pragma unroll
+    for (int i = 0; i < n * n; ++i) nl.a[i] *= c0;
     Lk = nl;
-    for (int i = 0; i < n * n; ++i) K.a[i] += hs * Lk.a[i] / (k + 1);
+#pragma unroll
+    for (int i = 0; i < n * n; ++i) K.a[i] += Lk.a[i] * c1;
     if (mnorm(term) < 1e-18 && mnorm(Lk) * hs < 1e-18 * (1.0 + mnorm(K))) break;
+    rk = rk1;
   }
-  double sb[3];
+  double sb[N];
   mvec(S1, beta, sb);
+#pragma unroll
   for (int i = 0; i < n; ++i) mu[i] = hs * sb[i];
   for (int s = 0; s < sq; ++s) {  // compose two half steps
-    double m2[3];
+    double m2[N];
     mvec(Phi, mu, m2);
+#pragma unroll
     for (int i = 0; i < n; ++i) mu[i] = m2[i] + mu[i];
     K = madd(mmul(mmul(Phi, K), mT(Phi)), K);
     Phi = mmul(Phi, Phi);
   }
+#pragma unroll
   for (int i = 0; i < n; ++i)
+#pragma unroll
     for (int j = i + 1; j < n; ++j) { const double v = 0.5 * (K(i, j) + K(j, i)); K(i, j) = v; K(j, i) = v; }
 }
 
 // One backward step of the filter: (H, F, c) at t_{i+1} -> at t_i over the step h.
 // Returns false if I + HK is singular.
-DMT_HD bool filter_step(const Mat& B, const double* beta, const Mat& A, double h, Mat& Hc,
-                        double* Fc, double& cc) {
-  const int d = B.n;
-  Mat Phi, K;
-  double mu[3];
+template <int N>
+DMT_HD bool filter_step(const Mat<N>& B, const double* beta, const Mat<N>& A, double h,
+                        Mat<N>& Hc, double* Fc, double& cc) {
+  constexpr int d = N;
+  Mat<N> Phi, K;
+  double mu[N];
   transition(B, beta, A, h, Phi, mu, K);
   // Gaussian integral over X_{t+h} ~ N(Phi x + mu, K) of exp(-c - x'Hx/2 + F'x)
-  const Mat IHK = madd(meye(d), mmul(Hc, K));
-  Mat S;
+  const Mat<N> IHK = madd(meye<N>(), mmul(Hc, K));
+  Mat<N> S;
   double lad;
   if (!minv(IHK, S, lad)) return false;
-  Mat Hh = mmul(S, Hc);
+  Mat<N> Hh = mmul(S, Hc);
   for (int p = 0; p < d; ++p)
     for (int q = p + 1; q < d; ++q) { const double v = 0.5 * (Hh(p, q) + Hh(q, p)); Hh(p, q) = v; Hh(q, p) = v; }
-  double Fh[3], KF[3];
+  double Fh[N], KF[N];
   mvec(S, Fc, Fh);
   mvec(K, Fc, KF);
   double fkf = 0.0;
   for (int p = 0; p < d; ++p) fkf += Fh[p] * KF[p];
   const double ch = cc + 0.5 * lad - 0.5 * fkf;
-  double Hmu[3];
+  double Hmu[N];
   mvec(Hh, mu, Hmu);
-  double g[3];
+  double g[N];
   for (int p = 0; p < d; ++p) g[p] = Fh[p] - Hmu[p];
-  const Mat PhT = mT(Phi);
-  double Fn[3];
+  const Mat<N> PhT = mT(Phi);
+  double Fn[N];
   mvec(PhT, g, Fn);
-  Mat Hn = mmul(mmul(PhT, Hh), Phi);
+  Mat<N> Hn = mmul(mmul(PhT, Hh), Phi);
   for (int p = 0; p < d; ++p)
     for (int q = p + 1; q < d; ++q) { const double v = 0.5 * (Hn(p, q) + Hn(q, p)); Hn(p, q) = v; Hn(q, p) = v; }
   double fmu = 0.0, muHmu = 0.0;

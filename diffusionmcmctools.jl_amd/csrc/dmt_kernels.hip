@@ -1235,24 +1235,25 @@ __global__ __launch_bounds__(kAccGroup) void k_accept_reduce_lb(const AcceptArgs
 // discrete filter of dmt_filter.h, identical to the host dmt_guiding_linear): one thread per
 // block, segments backward from the block end; the last segment of a non-terminal block uses
 // its PPb law with the artificial end observation frozen by set_obs!.
-template <class T>
-__global__ __launch_bounds__(128) void k_backward_filter(const FilterArgs a) {
+template <class T, int D>
+__global__ __launch_bounds__(64) void k_backward_filter(const FilterArgs a) {
   const int64_t blk = a.b0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (blk >= a.b1) return;
-  const int d = a.d, hp = d * (d + 1) / 2;
+  constexpr int d = D, hp = d * (d + 1) / 2;
   const int g0 = a.gfirst[blk], g1 = a.glast[blk];
   const bool term = a.term[blk] != 0;
-  using flt::Mat;
-  Mat Hc = flt::mzero(d);
-  double Fc[3] = {0, 0, 0}, cc = 0.0;
+  using M = flt::Mat<D>;
+  M Hc = flt::mzero<D>();
+  double Fc[D], cc = 0.0;
+  for (int p = 0; p < d; ++p) Fc[p] = 0.0;
   for (int g = g1; g >= g0; --g) {
     const int kind = (!term && g == g1) ? 1 : 0;
     const int slot = (kind ? a.selPPB[g] : a.selPP[g]) ^ a.unit;
     const double* lr = a.law[slot][kind] + (int64_t)g * DMT_LAW_STRIDE;
     // terminal information of the segment: its observation (+ the artificial one of a
     // P_last segment, or + the guiding term at the start of the next segment of the block)
-    Mat HT = flt::mzero(d);
-    double FT[3] = {0, 0, 0}, cT = a.obsc[g];
+    M HT = flt::mzero<D>();
+    double FT[D], cT = a.obsc[g];
     for (int p = 0; p < d; ++p) {
       FT[p] = a.obsF[(int64_t)g * d + p];
       for (int q = 0; q < d; ++q) HT(p, q) = a.obsH[(int64_t)g * hp + flt::packed_ix(d, p, q)];
@@ -1272,8 +1273,8 @@ __global__ __launch_bounds__(128) void k_backward_filter(const FilterArgs a) {
       for (int p = 0; p < d; ++p) FT[p] += Fc[p];
       cT += cc;
     }
-    Mat B = flt::mzero(d), At = flt::mzero(d);
-    double beta[3] = {0, 0, 0};
+    M B = flt::mzero<D>(), At = flt::mzero<D>();
+    double beta[D];
     for (int p = 0; p < d; ++p) {
       beta[p] = lr[DMT_LAW_BETA + p];
       for (int q = 0; q < d; ++q) {
@@ -1739,8 +1740,18 @@ hipError_t launch_pathll_kernel(const ModelKey& k, int mapping, const void* args
 hipError_t launch_backward_filter(int precision, const FilterArgs& a, hipStream_t s) {
   const int64_t n = a.b1 - a.b0;
   if (n <= 0) return hipSuccess;
-  if (precision == DMT_F64) dlaunch(k_backward_filter<double>, dim3(nblk(n, 128)), dim3(128), s, a);
-  else dlaunch(k_backward_filter<float>, dim3(nblk(n, 128)), dim3(128), s, a);
+  // one thread per block, 64-thread workgroups: spread the (few) waves over all CUs
+#define DMT_FILTER_LAUNCH(T, D) dlaunch(k_backward_filter<T, D>, dim3(nblk(n, 64)), dim3(64), s, a)
+  if (precision == DMT_F64) {
+    if (a.d == 1) DMT_FILTER_LAUNCH(double, 1);
+    else if (a.d == 2) DMT_FILTER_LAUNCH(double, 2);
+    else DMT_FILTER_LAUNCH(double, 3);
+  } else {
+    if (a.d == 1) DMT_FILTER_LAUNCH(float, 1);
+    else if (a.d == 2) DMT_FILTER_LAUNCH(float, 2);
+    else DMT_FILTER_LAUNCH(float, 3);
+  }
+#undef DMT_FILTER_LAUNCH
   return hipGetLastError();
 }
 

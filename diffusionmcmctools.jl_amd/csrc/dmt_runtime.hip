@@ -498,11 +498,6 @@ bool supported(const dmt_model* m) {
 
 // ------------------------------------------------------------ backward filter
 // (dmt_filter.h: shared with the device kernel k_backward_filter)
-using flt::Mat;
-using flt::madd;
-using flt::meye;
-using flt::mmul;
-using flt::mzero;
 
 }  // namespace
 
@@ -1384,20 +1379,22 @@ dmt_status dmt_fetch_ll(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int6
   return DMT_OK;
 }
 
-dmt_status dmt_guiding_linear(int32_t d, const double* Bt, const double* beta, const double* at,
-                              int32_t npts, const double* t, const double* HT, const double* FT,
-                              double cT, double* H, double* F, double* c) {
-  if (d < 1 || d > 3 || npts < 1 || !Bt || !beta || !at || !t || !HT || !FT || !H || !F || !c)
-    return fail(DMT_ERR_INVALID, "bad arguments to dmt_guiding_linear");
-  const int hp = d * (d + 1) / 2;
-  Mat B = mzero(d), A = mzero(d), Hc = mzero(d);
+}  // extern "C"
+
+template <int D>
+static dmt_status guiding_linear_impl(const double* Bt, const double* beta, const double* at,
+                                      int32_t npts, const double* t, const double* HT,
+                                      const double* FT, double cT, double* H, double* F,
+                                      double* c) {
+  constexpr int d = D, hp = d * (d + 1) / 2;
+  flt::Mat<D> B = flt::mzero<D>(), A = flt::mzero<D>(), Hc = flt::mzero<D>();
   for (int i = 0; i < d * d; ++i) B.a[i] = Bt[i];
   for (int i = 0; i < d; ++i)
     for (int j = 0; j < d; ++j) {
       A(i, j) = at[dmt_packed(d, i, j)];
       Hc(i, j) = HT[dmt_packed(d, i, j)];
     }
-  double Fc[3] = {0, 0, 0};
+  double Fc[D];
   for (int i = 0; i < d; ++i) Fc[i] = FT[i];
   double cc = cT;
   auto store = [&](int i) {
@@ -1415,6 +1412,18 @@ dmt_status dmt_guiding_linear(int32_t d, const double* Bt, const double* beta, c
     store(i);
   }
   return DMT_OK;
+}
+
+extern "C" {
+
+dmt_status dmt_guiding_linear(int32_t d, const double* Bt, const double* beta, const double* at,
+                              int32_t npts, const double* t, const double* HT, const double* FT,
+                              double cT, double* H, double* F, double* c) {
+  if (d < 1 || d > 3 || npts < 1 || !Bt || !beta || !at || !t || !HT || !FT || !H || !F || !c)
+    return fail(DMT_ERR_INVALID, "bad arguments to dmt_guiding_linear");
+  if (d == 1) return guiding_linear_impl<1>(Bt, beta, at, npts, t, HT, FT, cT, H, F, c);
+  if (d == 2) return guiding_linear_impl<2>(Bt, beta, at, npts, t, HT, FT, cT, H, F, c);
+  return guiding_linear_impl<3>(Bt, beta, at, npts, t, HT, FT, cT, H, F, c);
 }
 
 dmt_status dmt_comm_unique_id(uint8_t* id_out) {

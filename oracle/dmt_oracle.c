@@ -795,19 +795,23 @@ static void fm_transition(const fm_t* B, const double* beta, const fm_t* At, dou
     *K = fm_zero(n);
     for (int i = 0; i < n * n; ++i) K->a[i] = hs * Lk.a[i];
     fm_t BT = fm_T(B);
+    double rk = 1.0;
     for (int k = 1; k <= 30; ++k) {
+        double rk1 = 1.0 / (double)(k + 1);
         term = fm_mul(&term, &A);
-        for (int i = 0; i < n * n; ++i) term.a[i] /= k;
+        for (int i = 0; i < n * n; ++i) term.a[i] *= rk;
         *Phi = fm_add(Phi, &term);
         fm_t t2 = term;
-        for (int i = 0; i < n * n; ++i) t2.a[i] /= (k + 1);
+        for (int i = 0; i < n * n; ++i) t2.a[i] *= rk1;
         S1 = fm_add(&S1, &t2);
         fm_t l1 = fm_mul(B, &Lk), l2 = fm_mul(&Lk, &BT);
         fm_t nl = fm_add(&l1, &l2);
-        for (int i = 0; i < n * n; ++i) nl.a[i] *= hs / k;
+        double c0 = hs * rk, c1 = hs * rk1;
+        for (int i = 0; i < n * n; ++i) nl.a[i] *= c0;
         Lk = nl;
-        for (int i = 0; i < n * n; ++i) K->a[i] += hs * Lk.a[i] / (k + 1);
+        for (int i = 0; i < n * n; ++i) K->a[i] += Lk.a[i] * c1;
         if (fm_norm(&term) < 1e-18 && fm_norm(&Lk) * hs < 1e-18 * (1.0 + fm_norm(K))) break;
+        rk = rk1;
     }
     double sb[3];
     fm_vec(&S1, beta, sb);
