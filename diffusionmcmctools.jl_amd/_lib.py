@@ -28,13 +28,18 @@ K_DRAW, K_ACCEPT, K_PATHLL, K_RECOMPUTE, K_REDUCE = 0, 1, 2, 3, 4
 LAW_STRIDE = 64
 LAW_THETA, LAW_SIGMA, LAW_A, LAW_BT, LAW_BETA, LAW_DA, LAW_C0, LAW_TRACE = 0, 16, 25, 31, 40, 43, 49, 50
 LAW_SIGINV = 51
+LAW_ANCHOR = 60
+LAW_AUXLIN = 63
+# set_proposal_law! parameter names (include/dmt.h DMT_PAR_*)
+PAR_FHN = {"eps": 0, "s": 1, "gamma": 2, "beta": 3, "sigma": 4}
+PAR_LORENZ = {"s": 0, "r": 1, "beta": 2}
 
 # exported symbols (checked against include/dmt.h by tests/test_abi.py)
 SYMBOLS = [
     "dmt_create", "dmt_destroy", "dmt_upload_grid", "dmt_upload_law", "dmt_set_paths",
     "dmt_download_paths", "dmt_draw_unit", "dmt_create_layout", "dmt_layout_size",
     "dmt_draw_proposal", "dmt_accept_reject", "dmt_loglikhd", "dmt_recompute_path", "dmt_find_W_for_X", "dmt_upload_obs", "dmt_set_obs",
-    "dmt_recompute_guiding_term", "dmt_download_law", "dmt_swap",
+    "dmt_recompute_guiding_term", "dmt_set_proposal_law", "dmt_download_law", "dmt_swap",
     "dmt_save_ll", "dmt_set_accepted", "dmt_get_block_state", "dmt_set_block_state",
     "dmt_fetch_ll", "dmt_mcmc_step", "dmt_mcmc_run", "dmt_guiding_linear", "dmt_comm_unique_id", "dmt_comm_init", "dmt_set_shard", "dmt_sync",
     "dmt_set_timing", "dmt_get_timing", "dmt_memory_bytes", "dmt_debug_philox",
@@ -96,6 +101,7 @@ _SIGS = {
     "dmt_set_obs": [_P, _i32, _i64, _i64],
     "dmt_download_law": [_P, _i32, _i32, _pd, _pd, _pd],
     "dmt_recompute_guiding_term": [_P, _i32, _i64, _i64, _i32],
+    "dmt_set_proposal_law": [_P, _i32, _i64, _i64, _i32, _P, _P, _i32, _P, _P],
     "dmt_swap": [_P, _i32, _i32, _i64, _i64],
     "dmt_save_ll": [_P, _i32, _i64, _i64, _i64],
     "dmt_set_accepted": [_P, _i32, _i64, _i64, _i64, _pu8],

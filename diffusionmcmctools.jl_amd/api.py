@@ -259,11 +259,19 @@ class _BlockRange:
         idx = np.asarray(list(rng), dtype=np.int64) - 1
         return self.accpt_history[idx].sum(axis=0) / len(idx)
 
-    # ---- parameter updates (block_collection.jl:306-334): law upload + re-solve
-    def set_proposal_law(self, H=None, F=None, laws=None, Hb=None, Fb=None, lawsb=None,
-                         H_shared=False, skip=0):
-        """Install the proposal law's guiding terms in u° (ensemble-wide tables, as the host
-        filter produces them) and ``recompute_path!`` the blocks under it."""
+    # ---- parameter updates (biblock.jl:334-375, block_collection.jl:306-334)
+    def set_proposal_law(self, theta=None, H=None, F=None, laws=None, Hb=None, Fb=None,
+                         lawsb=None, H_shared=False, skip=0):
+        """``set_proposal_law!(bb, θ°, pnames; skip)``.
+
+        With ``theta`` ({parameter name or DMT_PAR_* index: value}; names as in
+        ``_lib.PAR_FHN`` / ``PAR_LORENZ``, OU indices Θ[i][j] = i·d + j, μ[i] = d² + i) it runs
+        on the device: u°'s laws ← u's with θ° set and the auxiliary law re-derived,
+        ``recompute_guiding_term!(b°)`` where that changed, then ``recompute_path!(b°, b.WW)``;
+        returns (success, critical) per block.  Without ``theta`` it installs host-made tables
+        in u° (ensemble-wide upload) and re-solves; returns the success flags."""
+        if theta is not None:
+            return self._call("set_proposal_law", _param_indices(self._ens, theta), skip=skip)
         if H is not None or F is not None or laws is not None:
             self._ens.upload_law(L.UPROP, L.LAW_PP, H=H, F=F, laws=laws, H_shared=H_shared)
         if Hb is not None or Fb is not None or lawsb is not None:
@@ -281,6 +289,19 @@ class _BlockRange:
         fetch_ll°, accepted count) — the sampling loop of
         docs/src/tutorials/biblock/smoothing.md:40-44."""
         return self._call("mcmc_run", iter0, n_iter, salt=salt)
+
+
+def _param_indices(ens, theta):
+    """Map parameter names to DMT_PAR_* indices for the ensemble's model."""
+    names = {L.MODEL_FHN: L.PAR_FHN, L.MODEL_LORENZ: L.PAR_LORENZ}.get(int(ens.model), {})
+    out = {}
+    for k, v in theta.items():
+        if isinstance(k, str):
+            if k not in names:
+                raise KeyError(f"unknown parameter {k!r} for model {ens.model}")
+            k = names[k]
+        out[int(k)] = float(v)
+    return out
 
 
 class BiBlock(_BlockRange):

@@ -137,6 +137,24 @@ struct FilterArgs {
   const double* obsv;  // [G][d] artificial observation (set_obs!) of a P_last segment
   double art_eps;      // its variance (artificial_noise)
   int* fail;           // set to 1 if a filter step is singular
+  const uint8_t* only;  // [nblocks] nullable: filter only the blocks flagged here
+};
+
+// set_proposal_law! on the device (k_set_prop_law): one thread per block.
+constexpr int kMaxParams = 16;
+struct ParamArgs {
+  int model, d, m, n;
+  int32_t idx[kMaxParams];
+  double val[kMaxParams];
+  const int32_t* gfirst;
+  const int32_t* glast;
+  const uint8_t* term;
+  const uint8_t* selPP;
+  const uint8_t* selPPB;
+  double* law[2][2];  // [slot][kind]; law[·][1] null without PPb records
+  int64_t b0, b1;
+  uint8_t* crit;    // [nblocks] 1 if the block's auxiliary law (as the filter uses it) changed
+  uint32_t* ncrit;  // count of such blocks
 };
 
 // Model/precision dispatch keys.
@@ -153,6 +171,7 @@ hipError_t launch_pathll_kernel(const ModelKey& k, int mapping, const void* args
                                 hipStream_t s);
 hipError_t launch_accept(const AcceptArgs& a, hipStream_t s);
 hipError_t launch_backward_filter(int precision, const FilterArgs& a, hipStream_t s);
+hipError_t launch_set_prop_law(const ParamArgs& a, hipStream_t s);
 hipError_t launch_set_obs(int precision, int tw, int d, const void* X0, const void* X1,
                           const uint8_t* selX,
                           const int64_t* tile_qoff, const int32_t* seg_rec, const int32_t* seg_q,

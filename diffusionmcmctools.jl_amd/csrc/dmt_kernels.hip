@@ -1239,6 +1239,7 @@ template <class T, int D>
 __global__ __launch_bounds__(64) void k_backward_filter(const FilterArgs a) {
   const int64_t blk = a.b0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (blk >= a.b1) return;
+  if (a.only && !a.only[blk]) return;
   constexpr int d = D, hp = d * (d + 1) / 2;
   const int g0 = a.gfirst[blk], g1 = a.glast[blk];
   const bool term = a.term[blk] != 0;
@@ -1308,6 +1309,99 @@ __global__ __launch_bounds__(64) void k_backward_filter(const FilterArgs a) {
     }
     a.law[slot][kind][(int64_t)g * DMT_LAW_STRIDE + DMT_LAW_C0] = cc;
   }
+}
+
+// set_proposal_law!(bb, θ°, pnames) (src/biblock.jl:334-364): for every segment of the block
+// and both law kinds, u°'s record ← u's except c(t0) (equalize_law_params!), the named
+// parameters ← θ° (DD.set_parameters!), then the fields derived from θ, in this arithmetic
+// order (restated in oracle/oracle.py set_law_params):
+//   FHN     θ0 = 1/ϵ; σ = (0, σ); a = σσᵀ (packed, one product each);
+//           auxlin: B̃ = ((1 − 3(y·y))/ϵ, −1/ϵ; γ, −1), β̃ = ((s + 2((y·y)·y))/ϵ, β), a − ã = 0
+//   Lorenz  auxlin: J = (−s, s, 0; r − x2, −1, −x0; x1, x0, −b),
+//           β̃_i = f_i − ((J_i0 x0 + J_i1 x1) + J_i2 x2),  f = (s(x1 − x0), x0(r − x2) − x1,
+//           x0 x1 − b x2)
+//   OU      Θ, μ only (the auxiliary law is fixed)
+// crit[blk] = 1 when a record the backward filter uses for this block (PP, or PPb of a
+// non-terminal block's last segment) has a different auxiliary law (B̃, β̃, ã = a − (a − ã))
+// afterwards.
+__device__ void write_params(const ParamArgs& a, double* r) {
+  for (int k = 0; k < a.n; ++k) {
+    const int p = a.idx[k];
+    const double v = a.val[k];
+    if (a.model == DMT_MODEL_FHN) {
+      if (p == DMT_PAR_FHN_EPS) { r[DMT_LAW_THETA + 4] = v; r[DMT_LAW_THETA + 0] = 1.0 / v; }
+      else if (p == DMT_PAR_FHN_SIGMA) r[DMT_LAW_THETA + 5] = v;
+      else r[DMT_LAW_THETA + p] = v;
+    } else if (a.model == DMT_MODEL_LORENZ) {
+      r[DMT_LAW_THETA + p] = v;
+    } else {
+      const int dd = a.d * a.d;
+      r[DMT_LAW_THETA + (p < dd ? p : 9 + (p - dd))] = v;
+    }
+  }
+  if (a.model == DMT_MODEL_FHN) {
+    const double sg = r[DMT_LAW_THETA + 5];
+    r[DMT_LAW_SIGMA + 0] = 0.0;
+    r[DMT_LAW_SIGMA + 1] = sg;
+    r[DMT_LAW_A + 0] = 0.0 * 0.0;
+    r[DMT_LAW_A + 1] = 0.0 * sg;
+    r[DMT_LAW_A + 2] = sg * sg;
+    if (r[DMT_LAW_AUXLIN] != 0.0) {
+      const double e = r[DMT_LAW_THETA + 4], y = r[DMT_LAW_ANCHOR];
+      const double yy = y * y;
+      r[DMT_LAW_BT + 0] = (1.0 - 3.0 * yy) / e;
+      r[DMT_LAW_BT + 1] = -1.0 / e;
+      r[DMT_LAW_BT + 2] = r[DMT_LAW_THETA + 2];
+      r[DMT_LAW_BT + 3] = -1.0;
+      r[DMT_LAW_BETA + 0] = (r[DMT_LAW_THETA + 1] + 2.0 * (yy * y)) / e;
+      r[DMT_LAW_BETA + 1] = r[DMT_LAW_THETA + 3];
+      for (int i = 0; i < 3; ++i) r[DMT_LAW_DA + i] = 0.0;
+      r[DMT_LAW_TRACE] = 0.0;
+    }
+  } else if (a.model == DMT_MODEL_LORENZ && r[DMT_LAW_AUXLIN] != 0.0) {
+    const double s = r[DMT_LAW_THETA + 0], rr = r[DMT_LAW_THETA + 1], b = r[DMT_LAW_THETA + 2];
+    const double x0 = r[DMT_LAW_ANCHOR + 0], x1 = r[DMT_LAW_ANCHOR + 1],
+                 x2 = r[DMT_LAW_ANCHOR + 2];
+    const double J[9] = {-s, s, 0.0, rr - x2, -1.0, -x0, x1, x0, -b};
+    const double f[3] = {s * (x1 - x0), x0 * (rr - x2) - x1, x0 * x1 - b * x2};
+#pragma unroll
+    for (int i = 0; i < 9; ++i) r[DMT_LAW_BT + i] = J[i];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      r[DMT_LAW_BETA + i] = f[i] - ((J[3 * i] * x0 + J[3 * i + 1] * x1) + J[3 * i + 2] * x2);
+  }
+}
+
+__global__ void k_set_prop_law(const ParamArgs a) {
+  const int64_t blk = a.b0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (blk >= a.b1) return;
+  const int g0 = a.gfirst[blk], g1 = a.glast[blk];
+  const bool term = a.term[blk] != 0;
+  bool changed = false;
+  constexpr int kAux0 = DMT_LAW_A, kAux1 = DMT_LAW_TRACE + 1;  // a, B̃, β̃, a − ã, (c0), trace
+  for (int g = g0; g <= g1; ++g)
+    for (int kind = 0; kind < 2; ++kind) {
+      if (!a.law[0][kind]) continue;
+      const int s = kind ? a.selPPB[g] : a.selPP[g];
+      const double* src = a.law[s][kind] + (int64_t)g * DMT_LAW_STRIDE;
+      double* dst = a.law[s ^ 1][kind] + (int64_t)g * DMT_LAW_STRIDE;
+      double old[kAux1 - kAux0];
+#pragma unroll
+      for (int i = kAux0; i < kAux1; ++i) old[i - kAux0] = dst[i];
+      const double c0 = dst[DMT_LAW_C0];
+      for (int i = 0; i < DMT_LAW_STRIDE; ++i) dst[i] = src[i];
+      dst[DMT_LAW_C0] = c0;
+      write_params(a, dst);
+      const bool used = kind == ((!term && g == g1) ? 1 : 0);
+      if (used) {
+#pragma unroll
+        for (int i = kAux0; i < kAux1; ++i)
+          if (i != DMT_LAW_C0 && __double_as_longlong(old[i - kAux0]) != __double_as_longlong(dst[i]))
+            changed = true;
+      }
+    }
+  a.crit[blk] = changed ? 1 : 0;
+  if (changed) atomicAdd(a.ncrit, 1u);
 }
 
 // set_obs!(bb) (src/biblock.jl:273-280): the artificial observation of a non-terminal block's
@@ -1752,6 +1846,13 @@ hipError_t launch_backward_filter(int precision, const FilterArgs& a, hipStream_
     else DMT_FILTER_LAUNCH(float, 3);
   }
 #undef DMT_FILTER_LAUNCH
+  return hipGetLastError();
+}
+
+hipError_t launch_set_prop_law(const ParamArgs& a, hipStream_t s) {
+  const int64_t n = a.b1 - a.b0;
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_set_prop_law, dim3(nblk(n, 64)), dim3(64), 0, s, a);
   return hipGetLastError();
 }
 

@@ -69,9 +69,12 @@ struct Layout {
   uint8_t* d_acch = nullptr;
   uint8_t* d_success = nullptr;
   uint8_t* d_acc = nullptr;
+  uint8_t* d_crit = nullptr;    // [nblocks] set_proposal_law!'s critical-change flags
+  uint32_t* d_ncrit = nullptr;  // their count
   void release() {
-    void* ps[] = {d_blk_off, d_binfo, d_blk_rec, d_gfirst, d_glast, d_term, d_rho, d_srho, d_ll,
-                  d_llp,     d_llh,    d_llph,  d_acch, d_success, d_acc};
+    void* ps[] = {d_blk_off, d_binfo, d_blk_rec, d_gfirst, d_glast, d_term,  d_rho,
+                  d_srho,    d_ll,    d_llp,     d_llh,    d_llph,  d_acch,  d_success,
+                  d_acc,     d_crit,  d_ncrit};
     for (void* p : ps)
       if (p) (void)hipFree(p);
   }
@@ -435,6 +438,8 @@ dmt_status build_layout(dmt_ens* h, const int32_t* n_blocks, const int32_t* seg_
   DMT_TRY(ens_alloc(h, &L->d_ll, nb));
   DMT_TRY(ens_alloc(h, &L->d_llp, nb));
   DMT_TRY(ens_alloc(h, &L->d_success, nb));
+  DMT_TRY(ens_alloc(h, &L->d_crit, nb));
+  DMT_TRY(ens_alloc(h, &L->d_ncrit, 1));
   DMT_TRY(ens_alloc(h, &L->d_acc, nb));
   if (L->hist_len > 0) {
     DMT_TRY(ens_alloc(h, &L->d_llh, L->hist_len * nb));
@@ -1197,14 +1202,13 @@ dmt_status dmt_set_obs(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1) {
   return DMT_OK;
 }
 
-dmt_status dmt_recompute_guiding_term(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
-                                      int32_t unit) {
-  DMT_TRY(check_h(h));
-  if (unit != DMT_U && unit != DMT_UPROP) return fail(DMT_ERR_INVALID, "bad unit");
+}  // extern "C"
+
+// the device backward filter over blocks [b0, b1) of `unit` (only the blocks flagged in
+// `only`, when given)
+static dmt_status guiding_term_device(dmt_ens* h, Layout* L, int64_t b0, int64_t b1, int32_t unit,
+                                      const uint8_t* only) {
   if (!h->d_obsH) return fail(DMT_ERR_STATE, "dmt_upload_obs first");
-  Layout* L;
-  DMT_TRY(get_layout(h, layout, &L));
-  DMT_TRY(check_range(L, b0, b1));
   DMT_TRY(law_ready(h, unit, L, b0, b1));
   if (!h->d_t) return fail(DMT_ERR_STATE, "time grid not uploaded");
   for (int k = 0; k < 2; ++k)
@@ -1240,6 +1244,7 @@ dmt_status dmt_recompute_guiding_term(dmt_ens* h, int32_t layout, int64_t b0, in
   a.obsv = h->d_obsv;
   a.art_eps = h->art_eps;
   a.fail = h->d_fail;
+  a.only = only;
   HIP_OK(hipMemsetAsync(h->d_fail, 0, sizeof(int), h->stream));
   {
     TimedScope ts(h, DMT_K_RECOMPUTE);
@@ -1249,6 +1254,66 @@ dmt_status dmt_recompute_guiding_term(dmt_ens* h, int32_t layout, int64_t b0, in
   HIP_OK(hipMemcpyAsync(&failed, h->d_fail, sizeof(int), hipMemcpyDeviceToHost, h->stream));
   HIP_OK(hipStreamSynchronize(h->stream));
   if (failed) return fail(DMT_ERR_INVALID, "singular I + HK in the device backward filter");
+  return DMT_OK;
+}
+
+extern "C" {
+
+dmt_status dmt_recompute_guiding_term(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
+                                      int32_t unit) {
+  DMT_TRY(check_h(h));
+  if (unit != DMT_U && unit != DMT_UPROP) return fail(DMT_ERR_INVALID, "bad unit");
+  Layout* L;
+  DMT_TRY(get_layout(h, layout, &L));
+  DMT_TRY(check_range(L, b0, b1));
+  return guiding_term_device(h, L, b0, b1, unit, nullptr);
+}
+
+dmt_status dmt_set_proposal_law(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int32_t n,
+                                const int32_t* idx, const double* val, int32_t skip,
+                                uint8_t* success_out, uint8_t* critical_out) {
+  DMT_TRY(check_h(h));
+  Layout* L;
+  DMT_TRY(get_layout(h, layout, &L));
+  DMT_TRY(check_range(L, b0, b1));
+  if (n < 0 || n > kMaxParams || (n > 0 && (!idx || !val)))
+    return fail(DMT_ERR_INVALID, "bad parameter list");
+  const int npar = h->key.model == DMT_MODEL_FHN      ? 5
+                   : h->key.model == DMT_MODEL_LORENZ ? 3
+                                                      : h->d * h->d + h->d;
+  for (int k = 0; k < n; ++k)
+    if (idx[k] < 0 || idx[k] >= npar) return fail(DMT_ERR_INVALID, "unknown parameter index");
+  if (skip != 0)
+    return fail(DMT_ERR_INVALID, "skip != 0 is not supported (see dmt_recompute_path)");
+  DMT_TRY(law_ready(h, 1, L, b0, b1));
+  ParamArgs a{};
+  a.model = h->key.model;
+  a.d = h->d;
+  a.m = h->m;
+  a.n = n;
+  for (int k = 0; k < n; ++k) { a.idx[k] = idx[k]; a.val[k] = val[k]; }
+  a.gfirst = L->d_gfirst;
+  a.glast = L->d_glast;
+  a.term = L->d_term;
+  a.selPP = h->d_sel[2];
+  a.selPPB = h->d_sel[3];
+  for (int sl = 0; sl < 2; ++sl)
+    for (int k = 0; k < 2; ++k) a.law[sl][k] = h->d_law[sl][k];
+  if (!a.law[0][1] || !a.law[1][1]) a.law[0][1] = a.law[1][1] = nullptr;
+  a.b0 = b0;
+  a.b1 = b1;
+  a.crit = L->d_crit;
+  a.ncrit = L->d_ncrit;
+  HIP_OK(hipMemsetAsync(L->d_ncrit, 0, sizeof(uint32_t), h->stream));
+  HIP_OK(launch_set_prop_law(a, h->stream));
+  uint32_t ncrit = 0;
+  HIP_OK(hipMemcpyAsync(&ncrit, L->d_ncrit, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream));
+  HIP_OK(hipStreamSynchronize(h->stream));
+  if (ncrit > 0) DMT_TRY(guiding_term_device(h, L, b0, b1, DMT_UPROP, L->d_crit));
+  if (critical_out)
+    HIP_OK(hipMemcpyAsync(critical_out, L->d_crit + b0, b1 - b0, hipMemcpyDeviceToHost, h->stream));
+  DMT_TRY(dmt_recompute_path(h, layout, b0, b1, 0, success_out));
+  if (critical_out) HIP_OK(hipStreamSynchronize(h->stream));
   return DMT_OK;
 }
 

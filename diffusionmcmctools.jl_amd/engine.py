@@ -190,6 +190,18 @@ class Ensemble:
     def recompute_guiding_term(self, layout, b0, b1, unit=L.U):
         L.call("dmt_recompute_guiding_term", self._h, layout, b0, b1, unit)
 
+    def set_proposal_law(self, layout, b0, b1, params, skip=0):
+        """set_proposal_law!(bb, θ°, pnames; skip) on the device: params is {name index: value}
+        (DMT_PAR_*).  Returns (success[b1-b0], critical[b1-b0])."""
+        idx = np.ascontiguousarray(np.fromiter(params.keys(), dtype=np.int32, count=len(params)))
+        val = np.ascontiguousarray(np.fromiter(params.values(), dtype=np.float64, count=len(params)))
+        ok = np.empty(b1 - b0, dtype=np.uint8)
+        crit = np.empty(b1 - b0, dtype=np.uint8)
+        L.call("dmt_set_proposal_law", self._h, layout, b0, b1, len(params),
+               idx.ctypes.data_as(C.c_void_p), val.ctypes.data_as(C.c_void_p), int(skip),
+               ok.ctypes.data_as(C.c_void_p), crit.ctypes.data_as(C.c_void_p))
+        return ok.astype(bool), crit.astype(bool)
+
     def swap(self, layout, what, b0, b1):
         L.call("dmt_swap", self._h, layout, int(what), b0, b1)
 

@@ -41,6 +41,9 @@ class LinearAux:
     Bt: np.ndarray
     beta: np.ndarray
     sigma_t: np.ndarray  # d×m
+    # the point the model was linearised at (FHN's FitzHughNagumoAux, Lorenz): the device
+    # re-derives Bt, beta from θ and this point in set_proposal_law!; None = a fixed law
+    anchor: np.ndarray | None = None
 
     @property
     def at(self):
@@ -79,6 +82,10 @@ class Model:
         rec[L.LAW_TRACE] = 1.0 if np.any(da != 0.0) else 0.0
         if self.d == self.m:  # σ⁻¹ for find_W_for_X! (invsolve)
             rec[L.LAW_SIGINV:L.LAW_SIGINV + self.d * self.d] = np.linalg.inv(sg).ravel()
+        if aux.anchor is not None:
+            an = np.atleast_1d(np.asarray(aux.anchor, dtype=np.float64))
+            rec[L.LAW_ANCHOR:L.LAW_ANCHOR + an.size] = an
+            rec[L.LAW_AUXLIN] = 1.0
         return rec
 
     def simulate(self, t, x0, rng, substeps=1):
@@ -140,7 +147,8 @@ class FHN(Model):
         self.eps, self.s, self.gamma, self.beta, self.sg = map(float, (eps, s, gamma, beta, sigma))
 
     def theta_vec(self):
-        return np.array([1.0 / self.eps, self.s, self.gamma, self.beta])
+        # the kernels read 1/ϵ, s, γ, β; the raw ϵ and σ follow for set_proposal_law!
+        return np.array([1.0 / self.eps, self.s, self.gamma, self.beta, self.eps, self.sg])
 
     def sigma(self):
         return np.array([[0.0], [self.sg]])
@@ -150,11 +158,12 @@ class FHN(Model):
         return np.array([(y - y ** 3 - v + self.s) / self.eps, self.gamma * y - v + self.beta])
 
     def aux(self, yT):
-        """FitzHughNagumoAux: linearisation at the observed end value yT."""
-        e = self.eps
-        Bt = np.array([[(1 - 3 * yT ** 2) / e, -1 / e], [self.gamma, -1.0]])
-        beta = np.array([(self.s + 2 * yT ** 3) / e, self.beta])
-        return LinearAux(Bt, beta, self.sigma())
+        """FitzHughNagumoAux: linearisation at the observed end value yT (the arithmetic
+        order of the device's set_proposal_law! re-derivation)."""
+        e, y = self.eps, float(yT)
+        Bt = np.array([[(1.0 - 3.0 * (y * y)) / e, -1.0 / e], [self.gamma, -1.0]])
+        beta = np.array([(self.s + 2.0 * (y * y * y)) / e, self.beta])
+        return LinearAux(Bt, beta, self.sigma(), anchor=np.array([y]))
 
 
 class Lorenz(Model):
@@ -179,10 +188,11 @@ class Lorenz(Model):
 
     def aux(self, v):
         """Linearisation of the drift at the point v."""
-        x0, x1, x2 = v
+        x0, x1, x2 = (float(u) for u in v)
         J = np.array([[-self.s_, self.s_, 0.0], [self.r - x2, -1.0, -x0], [x1, x0, -self.b]])
-        beta = self.drift(v) - J @ np.asarray(v)
-        return LinearAux(J, beta, self.sg)
+        f = self.drift((x0, x1, x2))
+        beta = np.array([f[i] - ((J[i, 0] * x0 + J[i, 1] * x1) + J[i, 2] * x2) for i in range(3)])
+        return LinearAux(J, beta, self.sg, anchor=np.array([x0, x1, x2]))
 
 
 # ------------------------------------------------------------------ observations, grids

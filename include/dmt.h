@@ -82,7 +82,8 @@ enum { DMT_K_DRAW = 0, DMT_K_ACCEPT = 1, DMT_K_PATHLL = 2, DMT_K_RECOMPUTE = 3,
  * by the Girsanov weight.  Offsets:
  *   [0,16)  theta  model parameters
  *             OU:     Theta (d×d row-major) at 0, mu at 9
- *             FHN:    1/eps, s, gamma, beta      (σ goes in sigma)
+ *             FHN:    1/eps, s, gamma, beta, then the raw eps, σ at 4, 5
+ *                     (σ also goes in sigma)
  *             Lorenz: s, r, beta
  *   [16,25) sigma  d×m row-major (constant diffusion coefficient)
  *   [25,31) a      packed upper-triangular σσᵀ (row-major upper: 00,01,(02),11,(12),22)
@@ -93,6 +94,10 @@ enum { DMT_K_DRAW = 0, DMT_K_ACCEPT = 1, DMT_K_PATHLL = 2, DMT_K_RECOMPUTE = 3,
  *   50      trace  1.0 if a ≠ ã (adds −½ tr[(a−ã)(H−rrᵀ)] to G)
  *   [51,60) siginv σ⁻¹ (d×d row-major) when d = m (find_W_for_X!; unused for FHN, whose
  *                  single noise enters coordinate 1)
+ *   [60,63) anchor the point the auxiliary law is linearised at (FHN: the observed y_T at 60;
+ *                  Lorenz: the observed state)
+ *   63      auxlin 1.0 if B̃, β̃ are the model's linearisation at `anchor` (re-derived by
+ *                  dmt_set_proposal_law when θ changes); 0.0 if the auxiliary law is fixed
  */
 #define DMT_LAW_STRIDE 64
 #define DMT_LAW_THETA 0
@@ -104,6 +109,16 @@ enum { DMT_K_DRAW = 0, DMT_K_ACCEPT = 1, DMT_K_PATHLL = 2, DMT_K_RECOMPUTE = 3,
 #define DMT_LAW_C0 49
 #define DMT_LAW_TRACE 50
 #define DMT_LAW_SIGINV 51
+#define DMT_LAW_ANCHOR 60
+#define DMT_LAW_AUXLIN 63
+
+/* Parameter names of dmt_set_proposal_law (DiffusionDefinition's parameter order):
+ *   FHN    (eps, s, gamma, beta, sigma), docs/src/tutorials/preamble.md:77
+ *   Lorenz (s, r, beta)
+ *   OU     Theta[i][j] = i*d + j, mu[i] = d*d + i  (the auxiliary law stays fixed) */
+enum { DMT_PAR_FHN_EPS = 0, DMT_PAR_FHN_S = 1, DMT_PAR_FHN_GAMMA = 2, DMT_PAR_FHN_BETA = 3,
+       DMT_PAR_FHN_SIGMA = 4 };
+enum { DMT_PAR_LORENZ_S = 0, DMT_PAR_LORENZ_R = 1, DMT_PAR_LORENZ_BETA = 2 };
 
 typedef struct {
     int32_t model;      /* DMT_MODEL_* */
@@ -232,6 +247,22 @@ dmt_status dmt_set_obs(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1);
  * and c(t0) into the law record.  Needs per-segment (not shared) H tables. */
 dmt_status dmt_recompute_guiding_term(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
                                       int32_t unit);
+
+/* set_proposal_law!(bb, θ°, pnames; skip) (src/biblock.jl:334-345, broadcasts
+ * src/block_collection.jl, src/block_ensemble.jl) on the device.
+ * For every segment of blocks [b0, b1) and both law kinds:
+ *   1. u°'s law record ← u's (GP.equalize_law_params!, src/biblock.jl:390-431; c(t0) of u°
+ *      is kept),
+ *   2. the n named parameters idx[k] ← val[k] (DD.set_parameters!, :360-364; names
+ *      DMT_PAR_*), and the fields derived from θ: sigma, a, and — when auxlin — B̃, β̃ of the
+ *      auxiliary law linearised at its anchor (ã = a),
+ * then GP.recompute_guiding_term!(bb.b°) (:342) for the blocks whose auxiliary law changed
+ * (the "critical change"; needs dmt_upload_obs), and recompute_path!(bb.b°, bb.b.WW; skip)
+ * (:343).  success_out, critical_out: uint8[b1-b0], nullable.  Only u° changes: the
+ * proposal is taken by swap_PP! (dmt_swap DMT_SWAP_PP) on acceptance. */
+dmt_status dmt_set_proposal_law(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int32_t n,
+                                const int32_t* idx, const double* val, int32_t skip,
+                                uint8_t* success_out, uint8_t* critical_out);
 
 /* swap_XX!/swap_WW!/swap_PP!/swap_ll! (src/biblock.jl:148-209), what = DMT_SWAP_* mask. */
 dmt_status dmt_swap(dmt_ens* h, int32_t layout, int32_t what, int64_t b0, int64_t b1);

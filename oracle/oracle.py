@@ -34,6 +34,46 @@ LIB = os.path.join(HERE, "liboracle.so")
 
 LAW_STRIDE = 64
 L_C0 = 49
+L_BT, L_TRACE, L_A, L_SIGMA, L_ANCHOR, L_AUXLIN = 31, 50, 25, 16, 60, 63
+
+
+def set_law_params(model, d, rec, params):
+    """DD.set_parameters! on one law record + the fields derived from θ (FHN: σ, a and — for an
+    auxiliary law linearised at its anchor — B̃, β̃, a − ã = 0; Lorenz: B̃, β̃; OU: Θ, μ only).
+    Plain Python float arithmetic (IEEE double, no contraction) in the order the device's
+    k_set_prop_law uses; restates DESIGN.md §3's set_proposal_law! derivation.  In place."""
+    for p, v in params.items():
+        v = float(v)
+        if model == 1:  # FHN (eps, s, gamma, beta, sigma)
+            if p == 0:
+                rec[4], rec[0] = v, 1.0 / v
+            elif p == 4:
+                rec[5] = v
+            else:
+                rec[p] = v
+        elif model == 2:  # Lorenz (s, r, beta)
+            rec[p] = v
+        else:  # OU: Theta (row-major), mu
+            rec[p if p < d * d else 9 + (p - d * d)] = v
+    if model == 1:
+        sg = float(rec[5])
+        rec[L_SIGMA], rec[L_SIGMA + 1] = 0.0, sg
+        rec[L_A], rec[L_A + 1], rec[L_A + 2] = 0.0 * 0.0, 0.0 * sg, sg * sg
+        if rec[L_AUXLIN] != 0.0:
+            e, y = float(rec[4]), float(rec[L_ANCHOR])
+            yy = y * y
+            rec[L_BT:L_BT + 4] = [(1.0 - 3.0 * yy) / e, -1.0 / e, float(rec[2]), -1.0]
+            rec[40:42] = [(float(rec[1]) + 2.0 * (yy * y)) / e, float(rec[3])]
+            rec[43:46] = 0.0
+            rec[L_TRACE] = 0.0
+    elif model == 2 and rec[L_AUXLIN] != 0.0:
+        s_, r_, b_ = (float(rec[i]) for i in range(3))
+        x0, x1, x2 = (float(rec[L_ANCHOR + i]) for i in range(3))
+        J = [-s_, s_, 0.0, r_ - x2, -1.0, -x0, x1, x0, -b_]
+        f = [s_ * (x1 - x0), x0 * (r_ - x2) - x1, x0 * x1 - b_ * x2]
+        rec[L_BT:L_BT + 9] = J
+        rec[40:43] = [f[i] - ((J[3 * i] * x0 + J[3 * i + 1] * x1) + J[3 * i + 2] * x2)
+                      for i in range(3)]
 
 
 def build():
@@ -530,6 +570,37 @@ class OracleEnsemble:
         F = np.concatenate([lw.F for lw in tab]).astype(np.float64)
         laws = np.stack([lw.rec for lw in tab])
         return H, F, laws
+
+    def set_proposal_law(self, layout, b0, b1, params, skip=0):
+        """set_proposal_law!(bb, θ°, pnames; skip) (src/biblock.jl:334-345): u°'s law records ←
+        u's except c(t0) (equalize_law_params!, :390-431), the named parameters ← θ°
+        (DD.set_parameters!, :360-364), recompute_guiding_term!(b°) for the blocks whose
+        auxiliary law changed (:342), recompute_path!(b°, b.WW) (:343).
+        Returns (success, critical) per block."""
+        assert skip == 0
+        crit = np.zeros(b1 - b0, dtype=bool)
+        for j, bk in enumerate(self.layouts[layout][b0:b1]):
+            for g in range(bk.g0, bk.g1 + 1):
+                for kind in (0, 1):
+                    tab_p = self.up.PP if kind == 0 else self.up.PPb
+                    tab_u = self.u.PP if kind == 0 else self.u.PPb
+                    if not tab_u or tab_u[g] is None or tab_u[g].rec is None:
+                        continue
+                    dst = tab_p[g].rec
+                    old = dst[L_A:L_TRACE + 1].copy()
+                    c0 = dst[L_C0]
+                    dst[:] = tab_u[g].rec
+                    dst[L_C0] = c0
+                    set_law_params(self.model, self.d, dst, params)
+                    used = kind == (1 if (not bk.term and g == bk.g1) else 0)
+                    new = dst[L_A:L_TRACE + 1].copy()
+                    new[L_C0 - L_A] = old[L_C0 - L_A]
+                    if used and old.view(np.uint64).tolist() != new.view(np.uint64).tolist():
+                        crit[j] = True
+        for j in np.flatnonzero(crit):
+            self.recompute_guiding_term(layout, b0 + j, b0 + j + 1, unit=1)
+        ok = self.recompute_path(layout, b0, b1, want_success=True)
+        return ok, crit
 
     def set_obs(self, layout, b0, b1):
         """GP.set_obs!(bb) (src/biblock.jl:273-280): P_last observes the accepted end point."""

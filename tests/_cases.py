@@ -52,13 +52,13 @@ def assert_ll_equal(dev, ora, lay, nb, exact=True, rtol=0.0):
         np.testing.assert_allclose(ap, bp, rtol=rtol)
 
 
-def ragged_case(seed=5, prec=L.F64):
+def ragged_case(seed=5, prec=L.F64, model=None):
     """3 recordings of an FHN model with 4, 6 and 5 inter-observation segments of unequal
     lengths and point counts (non-shared grids), per-segment linearised auxiliary laws, PP laws
     chained over the whole recording and PPb laws with an artificial exact end observation
     (guid_prop_for_blocking, src/sampling_unit.jl:61-66)."""
     rng = np.random.default_rng(seed)
-    model = FHN(0.1, -0.8, 1.5, 0.0, 0.3)
+    model = FHN(0.1, -0.8, 1.5, 0.0, 0.3) if model is None else model
     nsegs = [4, 6, 5]
     n_points, grids, laws_pp, H_pp, F_pp, H_b, F_b, laws_b, X0 = [], [], [], [], [], [], [], [], []
     Hobs, Fobs, cobs = [], [], []
