@@ -19,7 +19,7 @@ import DiffusionMCMCTools: draw_proposal_path!, accept_reject_proposal_path!, lo
 
 export DeviceSamplingEnsemble, DeviceBlockEnsemble, DeviceBlockCollection, DeviceBiBlock,
     mcmc_step!, mcmc_run!, download_XX, download_WW, upload_obs!, set_obs!,
-    recompute_guiding_term!
+    recompute_guiding_term!, set_proposal_law!
 
 const libdmt = get(ENV, "DMT_LIB", joinpath(@__DIR__, "..", "libdmt.so"))
 
@@ -69,6 +69,7 @@ Device containers of a `SamplingEnsemble` (src/sampling_ensemble.jl:13-41): XX/W
 """
 mutable struct DeviceSamplingEnsemble
     h::Ptr{Cvoid}
+    model::Int32
     d::Int
     m::Int
     n_points::Vector{Vector{Int}}
@@ -87,7 +88,7 @@ mutable struct DeviceSamplingEnsemble
                         (Ref{Ptr{Cvoid}}, Ref{dmt_model}, Ref{dmt_structure}, Ref{dmt_config}),
                         h, mdl, st, cfg))
         end
-        se = new(h[], d, m, [collect(Int, r) for r in n_points], sum(npts))
+        se = new(h[], Int32(model), d, m, [collect(Int, r) for r in n_points], sum(npts))
         finalizer(se) do x
             x.h == C_NULL || ccall((:dmt_destroy, libdmt), Int32, (Ptr{Cvoid},), x.h)
             x.h = C_NULL
@@ -285,6 +286,29 @@ set_obs!(x::DeviceBlocks) = check(ccall((:dmt_set_obs, libdmt), Int32,
 recompute_guiding_term!(x::DeviceBlocks, unit=DMT_U) = check(ccall(
     (:dmt_recompute_guiding_term, libdmt), Int32, (Ptr{Cvoid}, Int32, Int64, Int64, Int32),
     x.se.h, x.layout, x.b0, x.b1, unit))
+
+"""
+    set_proposal_law!(x, θ°::AbstractVector, pnames::AbstractVector{Symbol}; skip=0)
+
+set_proposal_law! (src/biblock.jl:334-345) on the device: u°'s laws ← u's with the named
+parameters set to θ° (names as DiffusionDefinition's: FHN `:ϵ, :s, :γ, :β, :σ`, Lorenz
+`:s, :r, :β`), the guiding term recomputed where the auxiliary law changed, then
+recompute_path!(b°, b.WW).  Returns (success, critical) per block.
+"""
+const _PAR_NAMES = Dict(
+    DMT_MODEL_FHN => Dict(:ϵ => 0, :s => 1, :γ => 2, :β => 3, :σ => 4),
+    DMT_MODEL_LORENZ => Dict(:s => 0, :r => 1, :β => 2))
+function set_proposal_law!(x::DeviceBlocks, θ°::AbstractVector, pnames::AbstractVector; skip=0)
+    names = get(_PAR_NAMES, x.se.model, Dict{Symbol,Int}())
+    idx = Int32[p isa Symbol ? names[p] : Int32(p) for p in pnames]
+    val = Float64.(θ°)
+    ok = Vector{UInt8}(undef, x.b1 - x.b0)
+    crit = Vector{UInt8}(undef, x.b1 - x.b0)
+    check(ccall((:dmt_set_proposal_law, libdmt), Int32,
+        (Ptr{Cvoid}, Int32, Int64, Int64, Int32, Ptr{Int32}, Ptr{Float64}, Int32, Ptr{UInt8},
+         Ptr{UInt8}), x.se.h, x.layout, x.b0, x.b1, length(idx), idx, val, skip, ok, crit))
+    Bool.(ok), Bool.(crit)
+end
 
 "find_W_for_X!(b) (src/block.jl:118-131): u.WW from u.XX under the accepted laws."
 find_W_for_X!(x::DeviceBlocks) = check(ccall((:dmt_find_W_for_X, libdmt), Int32,
