@@ -205,7 +205,10 @@ def main():
     accept_rate = n_acc / (B * world * args.steps)  # n_acc is already global (fetch_ll over ranks)
     # the mapping libdmt resolves for MAP_AUTO (kAutoWaveMaxRecordings, dmt_internal.h)
     wave = args.mapping == "wave" or (args.mapping == "auto" and len(w.n_points) <= 8192)
-    if w.model.kind == L.MODEL_OU:  # linear drift: always the affine-scan kernel
+    persist = w.model.kind == L.MODEL_OU and os.environ.get("DMT_MCMC_PERSIST", "1") != "0"
+    if persist:  # linear drift: all K iterations in one k_mcmc_scan launch (dmt_mcmc_run)
+        wave, kname = True, "k_mcmc_scan"
+    elif w.model.kind == L.MODEL_OU:  # linear drift: the affine-scan kernel per iteration
         wave, kname = True, "k_block_scan"
     else:
         kname = "k_block_wave" if wave else "k_block<"
@@ -231,7 +234,8 @@ def main():
             "config": {"workload": desc, "blocks_per_gpu": B,
                        "euler_steps_per_block": w.steps_per_iter // B, "rho": w.rho,
                        "parallelism": f"blockensemble-shard x{world}",
-                       "mapping": ("scan" if kname == "k_block_scan" else
+                       "mapping": ("scan-persistent" if persist else
+                                   "scan" if kname == "k_block_scan" else
                                    "wave" if wave else "lane"),
                        "rng": "device Philox4x32-10 + Box-Muller (perf mode)"},
             "per_gpu": value / world,
@@ -239,10 +243,14 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS,
                          "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
                          "traffic_source": traffic_src,
-                         "kernel": kname + " (draw_proposal_path!)", "kernel_avg_us": k_avg_s * 1e6,
+                         "kernel": kname + (" (draw_proposal_path! + accept_reject_proposal_path!, "
+                                            "per iteration)" if persist else
+                                            " (draw_proposal_path!)"),
+                         "kernel_avg_us": k_avg_s * 1e6,
+                         "iterations_per_launch": args.steps if persist else 1,
                          "algorithmic_bytes_per_launch": bytes_launch,
                          "bytes_per_step": algorithmic_bytes_per_step(w)},
-            "accept_kernel_avg_us": (a_ms / max(a_n, 1)) * 1e3,
+            "accept_kernel_avg_us": (a_ms / a_n) * 1e3 if a_n else None,
             "cpu_baseline": cpu,
         }
         if cpu is not None:

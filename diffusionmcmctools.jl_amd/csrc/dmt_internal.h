@@ -170,6 +170,14 @@ hipError_t launch_invsolve_kernel(const ModelKey& k, int mapping, const void* ar
 hipError_t launch_pathll_kernel(const ModelKey& k, int mapping, const void* args, int64_t nwaves,
                                 hipStream_t s);
 hipError_t launch_accept(const AcceptArgs& a, hipStream_t s);
+// dmt_mcmc_run for linear drifts: n_iter iterations in one launch (k_mcmc_scan), per-iteration
+// (ll, ll°, accepted) partials to part[n_iter][3][nwaves]; then their fetch_ll trees
+constexpr int kPersistMaxSegments = 64;
+hipError_t launch_mcmc_persistent(const ModelKey& k, const void* args, const AcceptArgs& c,
+                                  int64_t iter0, int64_t n_iter, double* part, int64_t nwaves,
+                                  hipStream_t s);
+hipError_t launch_tree_batched(const double* part, int64_t nb, int64_t n_iter, double* out3,
+                               hipStream_t s);
 hipError_t launch_backward_filter(int precision, const FilterArgs& a, hipStream_t s);
 hipError_t launch_set_prop_law(const ParamArgs& a, hipStream_t s);
 hipError_t launch_set_obs(int precision, int tw, int d, const void* X0, const void* X1,

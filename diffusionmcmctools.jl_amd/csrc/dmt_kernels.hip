@@ -716,8 +716,29 @@ __device__ __forceinline__ void store_row(T* p, const T* v) {
   }
 }
 
-template <class Mdl, class T, int MODE>
-__global__ __launch_bounds__(64 * kScanWaves, DMT_SCAN_MINW) void k_block_scan(const BlockArgs<T> a) {
+// Path selectors of the scan kernels: read from the ensemble arrays (one launch per call) or
+// from the workgroup's LDS copy (k_mcmc_scan flips them between its iterations; scalar loads
+// would not see those writes).
+struct SelGlobal {
+  const uint8_t* sx;
+  const uint8_t* sw;
+  __device__ __forceinline__ int x(int g) const { return ldc(sx + g); }
+  __device__ __forceinline__ int w(int g) const { return ldc(sw + g); }
+};
+struct SelLds {
+  const uint8_t* sx;  // LDS, indexed g - g0
+  const uint8_t* sw;
+  int g0;
+  __device__ __forceinline__ int x(int g) const { return __builtin_amdgcn_readfirstlane(sx[g - g0]); }
+  __device__ __forceinline__ int w(int g) const { return __builtin_amdgcn_readfirstlane(sw[g - g0]); }
+};
+
+// One block's draw / re-solve by a workgroup of kScanWaves waves; thread 0 returns ll and
+// success.
+template <class Mdl, class T, int MODE, class Sel>
+__device__ __forceinline__ void scan_block(const BlockArgs<T>& a, const int64_t blk,
+                                           const uint32_t iter, const Sel& sel, T& ll_res,
+                                           bool& ok_res) {
   constexpr int D = Mdl::D, M = Mdl::M, HP = D * (D + 1) / 2, NA = D * D + D;
   static_assert(Mdl::kLinear, "k_block_scan needs a linear drift");
   __shared__ T s_tot[kScanWaves][NA];     // chunk maps (Φ, ψ)
@@ -727,8 +748,6 @@ __global__ __launch_bounds__(64 * kScanWaves, DMT_SCAN_MINW) void k_block_scan(c
   __shared__ int s_allow, s_done;
   // the wave index is wave-uniform: keep it (and everything derived from it) scalar
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t blk = a.b0 + (int64_t)blockIdx.x;
-  if (blk >= a.b1) return;
 #ifdef DMT_STAMPS  // timing diagnostics (variant builds only): s_memtime per phase
   uint64_t st[12];
   int nst_ = 0;
@@ -755,7 +774,7 @@ __global__ __launch_bounds__(64 * kScanWaves, DMT_SCAN_MINW) void k_block_scan(c
   bool ok = true;
   T x0[D], H0[HP], F0[D], c00 = (T)0;
   if (threadIdx.x == 0) {
-    const T* Xs = a.X[ldc(a.selX + g0) ^ a.xs_flip];
+    const T* Xs = a.X[sel.x(g0) ^ a.xs_flip];
     const int64_t q = bq0;
     const int lsp = ldc(a.selPP + g0) ^ a.law_flip;
 #pragma unroll
@@ -795,12 +814,12 @@ __global__ __launch_bounds__(64 * kScanWaves, DMT_SCAN_MINW) void k_block_scan(c
     // can have failed); later ones wait for the in-order success test
     const bool early = k < kfirst;
     const bool need_b4 = (kb + nact > kfirst) || (kb + nact < ktot);
-    T* const Xdb = a.X[ldc(a.selX + g) ^ a.xd_flip] + row * D;
-    T* const Wdb = a.W[ldc(a.selW + g) ^ a.wd_flip] + row * M;
+    T* const Xdb = a.X[sel.x(g) ^ a.xd_flip] + row * D;
+    T* const Wdb = a.W[sel.w(g) ^ a.wd_flip] + row * M;
     T A[D * D], e[D], dW[M], w0v[M];
     STAMP();
     if (act) {  // ---- prepare (lane-parallel): normals, pCN, σ·dW°, step maps; then the scan
-      const T* Wsb = a.W[ldc(a.selW + g) ^ a.ws_flip] + row * M;
+      const T* Wsb = a.W[sel.w(g) ^ a.ws_flip] + row * M;
       if (MODE != MODE_RECOMPUTE && c0 == 0) {
 #pragma unroll
         for (int kk = 0; kk < M; ++kk) w0v[kk] = rho * ((MODE == MODE_FRESH) ? (T)0 : Wsb[kk]);
@@ -829,7 +848,7 @@ __global__ __launch_bounds__(64 * kScanWaves, DMT_SCAN_MINW) void k_block_scan(c
             z = (T)Zg[(int64_t)i * M + kk];
           } else {
             if ((n >> 1) != have) {
-              U4 o = philox4x32_10(U4{n >> 1, (uint32_t)g + a.seg_base, a.iter, c3}, k0, k1);
+              U4 o = philox4x32_10(U4{n >> 1, (uint32_t)g + a.seg_base, iter, c3}, k0, k1);
               normal_pair(o, z0, z1);
               have = n >> 1;
             }
@@ -992,16 +1011,130 @@ __global__ __launch_bounds__(64 * kScanWaves, DMT_SCAN_MINW) void k_block_scan(c
   }
   STAMP();
 #ifdef DMT_STAMPS
-  if (lane == 0 && a.iter == 7 && (blockIdx.x < 2 || blockIdx.x == gridDim.x - 1 || blockIdx.x == 500)) {
+  if (lane == 0 && iter == 7 && (blockIdx.x < 2 || blockIdx.x == gridDim.x - 1 || blockIdx.x == 500)) {
     printf("STAMP blk %d w %d n %d : %lu %lu %lu %lu %lu %lu %lu %lu %lu %lu %lu\n", (int)blockIdx.x, w, nst_,
            st[1] - st[0], st[2] - st[0], st[3] - st[0], st[4] - st[0], st[5] - st[0], st[6] - st[0],
            st[7] - st[0], st[8] - st[0], st[9] - st[0], st[10] - st[0], st[nst_ - 1] - st[0]);
   }
 #endif
 #undef STAMP
+  ll_res = ll;
+  ok_res = ok;
+}
+
+template <class Mdl, class T, int MODE>
+__global__ __launch_bounds__(64 * kScanWaves, DMT_SCAN_MINW) void k_block_scan(const BlockArgs<T> a) {
+  const int64_t blk = a.b0 + (int64_t)blockIdx.x;
+  if (blk >= a.b1) return;
+  T ll;
+  bool ok;
+  scan_block<Mdl, T, MODE>(a, blk, a.iter, SelGlobal{a.selX, a.selW}, ll, ok);
   if (threadIdx.x == 0) {
     a.ll_out[blk] = ok ? (double)ll : -INFINITY;
     if (a.success) a.success[blk] = ok ? 1 : 0;
+  }
+}
+
+// dmt_mcmc_run for linear drifts: n_iter path-MCMC iterations in ONE launch.  Blocks are
+// independent across iterations (a block's next proposal depends only on its own accepted
+// state), so each workgroup loops over the iterations for its block: draw (scan_block, device
+// RNG), then — thread 0, exactly as k_accept — the MH decision, selector flips, histories and
+// the ll swap, with the block's selectors and ll kept on chip.  Per-iteration (ll, ll°,
+// accepted) go to part[n_iter][3][nb] for the batched fetch_ll tree (k_tree_batched).
+template <class Mdl, class T>
+__global__ __launch_bounds__(64 * kScanWaves, DMT_SCAN_MINW) void k_mcmc_scan(
+    const BlockArgs<T> a, const AcceptArgs c, const int64_t iter0, const int64_t n_iter,
+    double* __restrict__ part) {
+  __shared__ uint8_t s_sx[kPersistMaxSegments], s_sw[kPersistMaxSegments];
+  const int64_t blk = a.b0 + (int64_t)blockIdx.x;
+  if (blk >= a.b1) return;
+  const int g0 = ldc(&a.binfo[blk].g0), g1 = ldc(&a.binfo[blk].g1);
+  const int nseg = g1 - g0 + 1;
+  if ((int)threadIdx.x < nseg) {
+    s_sx[threadIdx.x] = a.selX[g0 + threadIdx.x];
+    s_sw[threadIdx.x] = a.selW[g0 + threadIdx.x];
+  }
+  double ll = 0.0, llp = 0.0;
+  if (threadIdx.x == 0) ll = c.ll[blk];
+  const int64_t nb = a.b1 - a.b0, j = blk - a.b0;
+  const SelLds sel{s_sx, s_sw, g0};
+  __syncthreads();
+  for (int64_t r = 0; r < n_iter; ++r) {
+    const int64_t it = iter0 + r;
+    T lp;
+    bool ok;
+    scan_block<Mdl, T, MODE_PCN>(a, blk, (uint32_t)it, sel, lp, ok);
+    __syncthreads();  // every wave's u° stores are complete before u/u° can swap
+    if (threadIdx.x == 0) {
+      llp = ok ? (double)lp : -INFINITY;
+      const double E = exp1_draw(c.seed, (uint32_t)g0 + c.seg_base, (uint32_t)it, c.salt);
+      const bool acc = E > -(llp - ll);
+      if (acc) {
+        for (int k = 0; k < nseg; ++k) {
+          s_sx[k] ^= 1;
+          s_sw[k] ^= 1;
+        }
+      }
+      if (c.hist_len > 0) {
+        const int64_t o = (it - 1) * c.nblocks + blk;
+        c.acc_hist[o] = acc ? 1 : 0;
+        c.ll_hist[o] = ll;
+        c.llp_hist[o] = llp;
+      }
+      if (acc) {
+        const double t = ll;
+        ll = llp;
+        llp = t;
+      }
+      part[(3 * r + 0) * nb + j] = ll;
+      part[(3 * r + 1) * nb + j] = llp;
+      part[(3 * r + 2) * nb + j] = acc ? 1.0 : 0.0;
+    }
+    __syncthreads();
+  }
+  if ((int)threadIdx.x < nseg) {
+    a.selX[g0 + threadIdx.x] = s_sx[threadIdx.x];
+    a.selW[g0 + threadIdx.x] = s_sw[threadIdx.x];
+  }
+  if (threadIdx.x == 0) {
+    c.ll[blk] = ll;
+    c.llp[blk] = llp;
+  }
+}
+
+// The fetch_ll tree of every iteration of a k_mcmc_scan run: workgroup r reduces row r of
+// part[n_iter][3][nb] with the canonical tree (complete adjacent-pair tree over the blocks,
+// zero-padded; each thread folds an aligned power-of-two run of leaves with the same pairing,
+// then 4 wave trees and a 4-leaf tree), + 0.0 on the two ll sums.
+__global__ __launch_bounds__(256) void k_tree_batched(const double* __restrict__ part, int64_t nb,
+                                                      int64_t run, double* __restrict__ out3) {
+  __shared__ double w0[4], w1[4], w2[4];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int64_t r = blockIdx.x;
+  double v[3];
+  for (int q = 0; q < 3; ++q) {
+    const double* row = part + (3 * r + q) * nb;
+    double stk[40];
+    double acc = 0.0;
+    for (int64_t k = 0; k < run; ++k) {
+      const int64_t leaf = (int64_t)tid * run + k;
+      double x = leaf < nb ? row[leaf] : 0.0;
+      int l = 0;
+      for (int64_t m = k; m & 1; m >>= 1, ++l) x = stk[l] + x;
+      stk[l] = x;
+      acc = x;
+    }
+    v[q] = acc;
+  }
+  v[0] = wave_tree_sum<double>(v[0]);
+  v[1] = wave_tree_sum<double>(v[1]);
+  v[2] = wave_tree_sum<double>(v[2]);
+  if (lane == 0) { w0[wv] = v[0]; w1[wv] = v[1]; w2[wv] = v[2]; }
+  __syncthreads();
+  if (tid == 0) {
+    out3[3 * r + 0] = ((w0[0] + w0[1]) + (w0[2] + w0[3])) + 0.0;
+    out3[3 * r + 1] = ((w1[0] + w1[1]) + (w1[2] + w1[3])) + 0.0;
+    out3[3 * r + 2] = (w2[0] + w2[1]) + (w2[2] + w2[3]);
   }
 }
 
@@ -1819,6 +1952,36 @@ static hipError_t launch_pathll_t(int mapping, const void* args, int64_t nwaves,
 hipError_t launch_block_kernel(const ModelKey& k, int mapping, int mode, const void* args,
                                int64_t nwaves, hipStream_t s) {
   DMT_DISPATCH(k, (launch_block_t<Mdl, T>(mapping, mode, args, nwaves, s)));
+}
+
+template <class Mdl, class T>
+static hipError_t launch_mcmc_t(const void* args, const AcceptArgs& c, int64_t iter0, int64_t n,
+                                double* part, int64_t nwaves, hipStream_t s) {
+  if constexpr (Mdl::kLinear) {
+    const BlockArgs<T>& a = *static_cast<const BlockArgs<T>*>(args);
+    if (nwaves <= 0) return hipSuccess;
+    dlaunch(k_mcmc_scan<Mdl, T>, dim3((unsigned)nwaves), dim3(64 * kScanWaves), s, a, c, iter0, n,
+            part);
+    return hipGetLastError();
+  } else {
+    return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_mcmc_persistent(const ModelKey& k, const void* args, const AcceptArgs& c,
+                                  int64_t iter0, int64_t n_iter, double* part, int64_t nwaves,
+                                  hipStream_t s) {
+  DMT_DISPATCH(k, (launch_mcmc_t<Mdl, T>(args, c, iter0, n_iter, part, nwaves, s)));
+}
+
+hipError_t launch_tree_batched(const double* part, int64_t nb, int64_t n_iter, double* out3,
+                               hipStream_t s) {
+  if (n_iter <= 0) return hipSuccess;
+  int64_t P = 1;
+  while (P < nb) P <<= 1;
+  const int64_t run = P > 256 ? P / 256 : 1;
+  hipLaunchKernelGGL(k_tree_batched, dim3((unsigned)n_iter), dim3(256), 0, s, part, nb, run, out3);
+  return hipGetLastError();
 }
 
 hipError_t launch_invsolve_kernel(const ModelKey& k, int mapping, const void* args,

@@ -12,6 +12,7 @@
 #include <atomic>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -134,12 +135,19 @@ struct dmt_ens {
   double* h_red = nullptr;  // pinned host copy of the 3 reduction results
   double* d_gather = nullptr;
   double* d_run = nullptr;         // dmt_mcmc_run: [n][3] per-iteration reductions
-  double* d_run_gather = nullptr;  // [n][nranks][3]
+  double* d_run_gather = nullptr;  // [n][nranks][3] (persistent path: [nranks][n][3])
   int64_t run_cap = 0;
+  double* d_part = nullptr;  // k_mcmc_scan per-iteration block partials [n][3][nb]
+  int64_t part_cap = 0;
+  bool persist = true;       // dmt_mcmc_run of a linear drift in one launch (DMT_MCMC_PERSIST=0: off)
   std::vector<std::unique_ptr<Layout>> layouts;  // layouts[0] = internal "unit" layout
   // timing
   uint32_t timing = 0;  // bit k: time kernel class k (dmt_set_timing)
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> pending[DMT_K_COUNT];
+  struct PendingTime {
+    hipEvent_t first, second;
+    int64_t units;  // kernel invocations the interval stands for (k_mcmc_scan: iterations)
+  };
+  std::vector<PendingTime> pending[DMT_K_COUNT];
   double t_ms[DMT_K_COUNT] = {0, 0, 0, 0, 0};
   int64_t t_cnt[DMT_K_COUNT] = {0, 0, 0, 0, 0};
   std::vector<hipEvent_t> free_events;
@@ -188,7 +196,7 @@ void drain_timing(dmt_ens* h) {
       if (hipEventSynchronize(pr.second) == hipSuccess &&
           hipEventElapsedTime(&ms, pr.first, pr.second) == hipSuccess) {
         h->t_ms[k] += ms;
-        h->t_cnt[k] += 1;
+        h->t_cnt[k] += pr.units;
       }
       h->free_events.push_back(pr.first);
       h->free_events.push_back(pr.second);
@@ -204,8 +212,10 @@ struct TimedScope {
   dmt_ens* h;
   int k;
   bool dispatch;
+  int64_t units;
   hipEvent_t e0 = nullptr, e1 = nullptr;
-  TimedScope(dmt_ens* h_, int k_, bool dispatch_ = true) : h(h_), k(k_), dispatch(dispatch_) {
+  TimedScope(dmt_ens* h_, int k_, bool dispatch_ = true, int64_t units_ = 1)
+      : h(h_), k(k_), dispatch(dispatch_), units(units_) {
     if (h->timing >> k & 1u) {
       e0 = get_event(h);
       e1 = get_event(h);
@@ -226,7 +236,7 @@ struct TimedScope {
       } else if (!dispatch) {
         (void)hipEventRecord(e1, h->stream);
       }
-      h->pending[k].push_back({e0, e1});
+      h->pending[k].push_back({e0, e1, units});
       if (h->pending[k].size() > 512) drain_timing(h);
     }
   }
@@ -583,6 +593,7 @@ dmt_status dmt_create(dmt_ens** out, const dmt_model* model, const dmt_structure
   else return fail(DMT_ERR_INVALID, "bad mapping");
   // linear drift (OU): the recursion is an affine scan, always one workgroup per block
   if (model->model == DMT_MODEL_OU) h->mapping = MAP_WAVE;
+  if (const char* e = std::getenv("DMT_MCMC_PERSIST")) h->persist = std::strcmp(e, "0") != 0;
   h->tw = h->mapping == MAP_WAVE ? 1 : kLanes;
   h->ntiles = (h->R + h->tw - 1) / h->tw;
   h->tile_qoff.assign(h->ntiles + 1, 0);
@@ -646,7 +657,7 @@ dmt_status dmt_destroy(dmt_ens* h) {
   void* ps[] = {h->d_pt_off, h->d_st_off, h->d_tile_qoff, h->d_seg_rec, h->d_seg_q, h->d_seg_np,
                 h->d_sel[0], h->d_sel[1], h->d_sel[2], h->d_sel[3], h->d_X[0], h->d_X[1],
                 h->d_W[0], h->d_W[1], h->d_t, h->d_stage, h->d_Z, h->d_red, h->d_gather,
-                h->d_red_work, h->d_run, h->d_run_gather, h->d_red_lb, h->d_obsH,
+                h->d_red_work, h->d_run, h->d_run_gather, h->d_part, h->d_red_lb, h->d_obsH,
                 h->d_obsF, h->d_obsc, h->d_obsv, h->d_fail};
   for (void* p : ps)
     if (p) (void)hipFree(p);
@@ -1055,20 +1066,68 @@ dmt_status dmt_mcmc_run(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int6
     DMT_TRY(ens_alloc(h, &h->d_run_gather, 3 * h->run_cap * h->nranks));
   }
   DMT_TRY(ensure_red_work(h, b1 - b0));
-  // every iteration is stream-ordered: no host synchronisation until the end
-  for (int64_t i = 0; i < n_iter; ++i) {
-    const int64_t it = iter0 + i;
-    DMT_TRY(run_block_kernel(h, L, MODE_PCN, DMT_K_DRAW, b0, b1, 0, 0, 1, 0, 1, nullptr, it,
-                             salt, L->d_llp, nullptr, false));
-    {
-      TimedScope ts(h, DMT_K_ACCEPT);
-      HIP_OK(launch_accept_reduce(accept_args(h, L, b0, b1, nullptr, it, salt, nullptr),
-                                  h->d_red_work, h->d_red_lb, h->d_run + 3 * i, h->stream));
+  const int64_t nb = b1 - b0;
+  bool persist = h->persist && h->key.model == DMT_MODEL_OU;
+  for (int64_t b = b0; b < b1 && persist; ++b)
+    persist = L->glast[b] - L->gfirst[b] + 1 <= kPersistMaxSegments;
+  if (persist) {
+    // the whole run in one launch per chunk of iterations (k_mcmc_scan), then one batched
+    // fetch_ll tree over all iterations and (multi-GPU) one all-gather
+    const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(n_iter, (int64_t(64) << 20) / (24 * nb)));
+    if (3 * nb * chunk > h->part_cap) {
+      if (h->d_part) { (void)hipFree(h->d_part); h->bytes -= h->part_cap * 8; h->d_part = nullptr; }
+      h->part_cap = 0;
+      DMT_TRY(ens_alloc(h, &h->d_part, 3 * nb * chunk));
+      h->part_cap = 3 * nb * chunk;
     }
-    if (multi &&
-        ncclAllGather(h->d_run + 3 * i, h->d_run_gather + 3 * h->nranks * i, 3, ncclDouble,
-                      h->comm, h->stream) != ncclSuccess)
+    for (int64_t i0 = 0; i0 < n_iter; i0 += chunk) {
+      const int64_t n = std::min(chunk, n_iter - i0);
+      const AcceptArgs c = accept_args(h, L, b0, b1, nullptr, iter0 + i0, salt, nullptr);
+      hipError_t e;
+      {
+        TimedScope ts(h, DMT_K_DRAW, true, n);
+        auto fill = [&](auto& a) {
+          fill_common(h, L, a);
+          a.b0 = b0;
+          a.b1 = b1;
+          a.tile0 = 0;
+          a.tile1 = 0;
+          a.xd_flip = 1;  // MODE_PCN: start u, write u°, read u.W, write u°.W
+          a.wd_flip = 1;
+          a.salt = salt;
+        };
+        if (h->key.precision == DMT_F64) {
+          BlockArgs<double> a{};
+          fill(a);
+          e = launch_mcmc_persistent(h->key, &a, c, iter0 + i0, n, h->d_part, nb, h->stream);
+        } else {
+          BlockArgs<float> a{};
+          fill(a);
+          e = launch_mcmc_persistent(h->key, &a, c, iter0 + i0, n, h->d_part, nb, h->stream);
+        }
+      }
+      if (e != hipSuccess) return fail(DMT_ERR_HIP, std::string("k_mcmc_scan: ") + hipGetErrorString(e));
+      HIP_OK(launch_tree_batched(h->d_part, nb, n, h->d_run + 3 * i0, h->stream));
+    }
+    if (multi && ncclAllGather(h->d_run, h->d_run_gather, 3 * n_iter, ncclDouble, h->comm,
+                               h->stream) != ncclSuccess)
       return fail(DMT_ERR_COMM, "ncclAllGather failed");
+  } else {
+    // every iteration is stream-ordered: no host synchronisation until the end
+    for (int64_t i = 0; i < n_iter; ++i) {
+      const int64_t it = iter0 + i;
+      DMT_TRY(run_block_kernel(h, L, MODE_PCN, DMT_K_DRAW, b0, b1, 0, 0, 1, 0, 1, nullptr, it,
+                               salt, L->d_llp, nullptr, false));
+      {
+        TimedScope ts(h, DMT_K_ACCEPT);
+        HIP_OK(launch_accept_reduce(accept_args(h, L, b0, b1, nullptr, it, salt, nullptr),
+                                    h->d_red_work, h->d_red_lb, h->d_run + 3 * i, h->stream));
+      }
+      if (multi &&
+          ncclAllGather(h->d_run + 3 * i, h->d_run_gather + 3 * h->nranks * i, 3, ncclDouble,
+                        h->comm, h->stream) != ncclSuccess)
+        return fail(DMT_ERR_COMM, "ncclAllGather failed");
+    }
   }
   if (!out) {
     HIP_OK(hipStreamSynchronize(h->stream));
@@ -1089,7 +1148,8 @@ dmt_status dmt_mcmc_run(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int6
   for (int64_t i = 0; i < n_iter; ++i)
     for (int c = 0; c < 3; ++c) {  // the rank-order tree of finish_reduction
       std::fill(lv.begin(), lv.end(), 0.0);
-      for (int r = 0; r < h->nranks; ++r) lv[r] = all[3 * h->nranks * i + 3 * r + c];
+      for (int r = 0; r < h->nranks; ++r)
+        lv[r] = persist ? all[(r * n_iter + i) * 3 + c] : all[3 * h->nranks * i + 3 * r + c];
       for (int w = n2; w > 1; w >>= 1)
         for (int j = 0; j < w / 2; ++j) lv[j] = lv[2 * j] + lv[2 * j + 1];
       out[3 * i + c] = lv[0] + 0.0;
