@@ -33,6 +33,9 @@ def main():
     ap.add_argument("--calib-write")
     ap.add_argument("--calib-kernel", default="k_stream<double>")
     ap.add_argument("--config", default="")
+    ap.add_argument("--units-per-launch", type=int, default=1,
+                    help="iterations one dispatch runs (k_mcmc_scan: --steps of the bench); "
+                         "bytes are reported per iteration, like bench.py's roofline")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     fk = per_kernel(a.fetch, "FETCH_SIZE", a.kernel)
@@ -49,9 +52,10 @@ def main():
         cw = gib / (statistics.median(cwv) * 1024.0)
         calib = {"kernel": a.calib_kernel, "fetch_factor": cf, "write_factor": cw,
                  "fetch_kib_raw": statistics.median(cfv), "write_kib_raw": statistics.median(cwv)}
-    f_b = statistics.median(fk) * 1024.0 * cf
-    w_b = statistics.median(wk) * 1024.0 * cw
+    f_b = statistics.median(fk) * 1024.0 * cf / a.units_per_launch
+    w_b = statistics.median(wk) * 1024.0 * cw / a.units_per_launch
     out = {"config": a.config, "kernel": a.kernel, "dispatches": [len(fk), len(wk)],
+           "units_per_launch": a.units_per_launch,
            "fetch_bytes": f_b, "write_bytes": w_b, "traffic_bytes_per_launch": f_b + w_b,
            "fetch_kib_raw_median": statistics.median(fk),
            "write_kib_raw_median": statistics.median(wk), "calibration": calib}
