@@ -206,7 +206,12 @@ def main():
     # the mapping libdmt resolves for MAP_AUTO (kAutoWaveMaxRecordings, dmt_internal.h)
     wave = args.mapping == "wave" or (args.mapping == "auto" and len(w.n_points) <= 8192)
     persist = w.model.kind == L.MODEL_OU and os.environ.get("DMT_MCMC_PERSIST", "1") != "0"
-    if persist:  # linear drift: all K iterations in one k_mcmc_scan launch (dmt_mcmc_run)
+    # single-segment blocks of <= 512 steps, d <= 2: register-resident kernel (dmt_internal.h)
+    resident = (persist and w.d <= 2 and os.environ.get("DMT_MCMC_RESIDENT", "1") != "0"
+                and all(len(r) == 1 and r[0] - 1 <= 512 for r in w.n_points))
+    if resident:  # linear drift: all K iterations in one k_mcmc_resident launch (dmt_mcmc_run)
+        wave, kname = True, "k_mcmc_resident"
+    elif persist:  # linear drift: all K iterations in one k_mcmc_scan launch (dmt_mcmc_run)
         wave, kname = True, "k_mcmc_scan"
     elif w.model.kind == L.MODEL_OU:  # linear drift: the affine-scan kernel per iteration
         wave, kname = True, "k_block_scan"
@@ -234,7 +239,8 @@ def main():
             "config": {"workload": desc, "blocks_per_gpu": B,
                        "euler_steps_per_block": w.steps_per_iter // B, "rho": w.rho,
                        "parallelism": f"blockensemble-shard x{world}",
-                       "mapping": ("scan-persistent" if persist else
+                       "mapping": ("scan-resident" if resident else
+                                   "scan-persistent" if persist else
                                    "scan" if kname == "k_block_scan" else
                                    "wave" if wave else "lane"),
                        "rng": "device Philox4x32-10 + Box-Muller (perf mode)"},

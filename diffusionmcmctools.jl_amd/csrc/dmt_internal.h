@@ -172,10 +172,13 @@ hipError_t launch_pathll_kernel(const ModelKey& k, int mapping, const void* args
 hipError_t launch_accept(const AcceptArgs& a, hipStream_t s);
 // dmt_mcmc_run for linear drifts: n_iter iterations in one launch (k_mcmc_scan), per-iteration
 // (ll, ll°, accepted) partials to part[n_iter][3][nwaves]; then their fetch_ll trees
+// (resident: every block is one segment of ≤ kResidentMaxSteps steps and d ≤ 2 —
+// k_mcmc_resident keeps the block's state in registers for the whole run)
 constexpr int kPersistMaxSegments = 64;
+constexpr int kResidentMaxSteps = 512;
 hipError_t launch_mcmc_persistent(const ModelKey& k, const void* args, const AcceptArgs& c,
                                   int64_t iter0, int64_t n_iter, double* part, int64_t nwaves,
-                                  hipStream_t s);
+                                  int resident, hipStream_t s);
 hipError_t launch_tree_batched(const double* part, int64_t nb, int64_t n_iter, double* out3,
                                hipStream_t s);
 hipError_t launch_backward_filter(int precision, const FilterArgs& a, hipStream_t s);

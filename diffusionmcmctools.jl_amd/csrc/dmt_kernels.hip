@@ -671,25 +671,39 @@ __global__ __launch_bounds__(128) void k_block_wave(const BlockArgs<T> a) {
   }
 }
 
-// ---- linear-drift block kernel: parallel-in-time Euler recursion.
+// ---- linear-drift block kernels: parallel-in-time Euler recursion.
 // With a linear drift (OU) every guided Euler step is an affine map x ↦ A_i x + e_i whose
-// coefficients do not depend on x, so a chunk of 64 steps is one Kogge–Stone prefix scan of
-// affine maps across the 64 lanes of a wave.  A workgroup of kScanWaves waves owns one block;
-// wave w takes chunk k = round·kScanWaves + w and, lane-parallel, draws its normals
-// (Philox/Box–Muller), forms the pCN increments, σ·dW°, the guiding coefficients and the
-// step maps, and scans them.  The only serial work left is one affine application per chunk
-// (the carry of the chunk start points), done by one thread between two barriers.  Then every
-// lane evaluates its point, the Girsanov terms and the 64-lane tree sum, and stores.
-#ifndef DMT_SCAN_MINW
-#define DMT_SCAN_MINW 4
-#endif
-#ifndef DMT_SCAN_WAVES
-#define DMT_SCAN_WAVES 4
-#endif
-constexpr int kScanWaves = DMT_SCAN_WAVES;
+// coefficients do not depend on x.  ONE WAVEFRONT OWNS ONE BLOCK (no barriers, no serial
+// carry between waves); a workgroup holds ScanCfg::WPB independent waves (one per SIMD).
+// A segment is cut into chunks of kSChunk = 512 steps; per chunk:
+//   phase 1 (coalesced, lane j ↔ step 64k + j, k = 0..7): normals (Philox/Box–Muller), the
+//            pCN increments, σ·dW°, the guiding coefficients and the step maps → LDS, W° stored;
+//   phase 2 (runs, lane j ↔ steps 8j … 8j+7): the lane composes its 8 step maps into one run
+//            map, an inclusive Kogge–Stone scan over the 64 run maps gives every run's start
+//            point, and the lane applies its step maps one by one → points to LDS;
+//   phase 3 (coalesced again): points back, Girsanov terms G·dt, the 64-step adjacent-pair tree
+//            sums (the canonical chunk sums), coalesced stores of the path.
+// The scan costs one 6-level Kogge–Stone per 8 steps (instead of per step) and the chunk carry
+// is the scan itself.
+constexpr int kRun = 8;                                 // steps per lane run
+constexpr int kSChunk = 64 * kRun;                      // steps per scan chunk
+constexpr int kSStride = kSChunk + kSChunk / kRun + 8;  // LDS row: 512 steps, a pad per 8, end point
 
-template <class T>
-__device__ __forceinline__ T shfl_up_T(T v, int o) { return __shfl_up(v, (unsigned)o, 64); }
+// LDS slot of chunk step s: one pad double per 8 steps, so that the run-order reads of phase 2
+// (lane stride 9 doubles) and the coalesced phase-1/3 accesses are both (nearly) conflict-free
+__device__ __forceinline__ int lds_ix(int s) { return s + (s >> 3); }
+
+template <int D, class T>
+struct ScanLds {
+  static constexpr int NA = D * D + D;
+  T map[NA][kSStride];  // step maps A (D×D), e (D) of the chunk, SoA
+  T pt[D][kSStride];    // pre-step points of the chunk (+ its end point at lds_ix(cnt))
+};
+template <int D, class T>
+struct ScanCfg {  // waves (= blocks) per workgroup: as many as 160 KiB of LDS allow, ≤ 4
+  static constexpr int kBytes = (int)sizeof(ScanLds<D, T>);
+  static constexpr int WPB = (4 * kBytes <= 160 * 1024) ? 4 : (2 * kBytes <= 160 * 1024) ? 2 : 1;
+};
 
 // Raw cross-lane read: the value of lane `src` (ds_bpermute, no range fix-up; the caller
 // selects).  `addr` = 4 * src lane.
@@ -716,320 +730,284 @@ __device__ __forceinline__ void store_row(T* p, const T* v) {
   }
 }
 
-// Path selectors of the scan kernels: read from the ensemble arrays (one launch per call) or
-// from the workgroup's LDS copy (k_mcmc_scan flips them between its iterations; scalar loads
-// would not see those writes).
+// Path selectors of the scan kernels: read from the ensemble arrays (one launch per call;
+// scalar loads) or kept as wave-uniform bit masks (k_mcmc_scan flips them between its
+// iterations; bit g - g0 = selector of segment g).
 struct SelGlobal {
   const uint8_t* sx;
   const uint8_t* sw;
   __device__ __forceinline__ int x(int g) const { return ldc(sx + g); }
   __device__ __forceinline__ int w(int g) const { return ldc(sw + g); }
 };
-struct SelLds {
-  const uint8_t* sx;  // LDS, indexed g - g0
-  const uint8_t* sw;
+struct SelMask {
+  uint64_t mx, mw;
   int g0;
-  __device__ __forceinline__ int x(int g) const { return __builtin_amdgcn_readfirstlane(sx[g - g0]); }
-  __device__ __forceinline__ int w(int g) const { return __builtin_amdgcn_readfirstlane(sw[g - g0]); }
+  __device__ __forceinline__ int x(int g) const { return (int)((mx >> (g - g0)) & 1u); }
+  __device__ __forceinline__ int w(int g) const { return (int)((mw >> (g - g0)) & 1u); }
 };
 
-// One block's draw / re-solve by a workgroup of kScanWaves waves; thread 0 returns ll and
-// success.
+__device__ __forceinline__ void wave_lds_sync() {
+  // LDS accesses of one wave are performed in order; this only keeps the compiler from moving
+  // an access across the phase boundary (other lanes' data)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// One block's draw / re-solve by one wave; every lane returns the block's ll and success.
 template <class Mdl, class T, int MODE, class Sel>
 __device__ __forceinline__ void scan_block(const BlockArgs<T>& a, const int64_t blk,
-                                           const uint32_t iter, const Sel& sel, T& ll_res,
-                                           bool& ok_res) {
-  constexpr int D = Mdl::D, M = Mdl::M, HP = D * (D + 1) / 2, NA = D * D + D;
-  static_assert(Mdl::kLinear, "k_block_scan needs a linear drift");
-  __shared__ T s_tot[kScanWaves][NA];     // chunk maps (Φ, ψ)
-  __shared__ T s_xs[kScanWaves + 1][D];   // chunk start points; [w+1] = end of chunk w
-  __shared__ T s_csum[kScanWaves];        // chunk sums of G·dt
-  __shared__ int s_segend[kScanWaves];
-  __shared__ int s_allow, s_done;
-  // the wave index is wave-uniform: keep it (and everything derived from it) scalar
-  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-#ifdef DMT_STAMPS  // timing diagnostics (variant builds only): s_memtime per phase
-  uint64_t st[12];
-  int nst_ = 0;
-#define STAMP() (st[nst_++] = __builtin_amdgcn_s_memtime())
-  STAMP();
-#else
-#define STAMP() ((void)0)
-#endif
+                                           const uint32_t iter, const Sel& sel,
+                                           ScanLds<Mdl::D, T>& S, T& ll_res, bool& ok_res) {
+  constexpr int D = Mdl::D, M = Mdl::M, HP = D * (D + 1) / 2;
+  static_assert(Mdl::kLinear, "scan_block needs a linear drift");
+  // D ≤ 2: the phase-1 guiding-table values stay in registers for phase 3; D = 3 re-reads them
+  constexpr bool kKeep = D <= 2;
+  const int lane = threadIdx.x & 63;
   const BlkInfo* bi = a.binfo + blk;
   const int64_t tq = ldc(&bi->tq);
-  const int g0 = ldc(&bi->g0), g1 = ldc(&bi->g1), ktot = ldc(&bi->ktot);
-  const int kfirst = ldc(&bi->kfirst), bq0 = ldc(&bi->q0);
+  const int g0 = ldc(&bi->g0), g1 = ldc(&bi->g1);
+  const int bq0 = ldc(&bi->q0);
   const bool term = ldc(&bi->term) != 0;
   const T rho = (MODE == MODE_FRESH) ? (T)0 : (T)ldc(&bi->rho);
   const T srho = (MODE == MODE_FRESH) ? (T)1 : (T)ldc(&bi->srho);
+  const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32), c3 = a.salt << 1;
   // law slot / kind of segment g (uniform)
   auto law_sel = [&](int g, int& kind) -> int {
-    kind = __builtin_amdgcn_readfirstlane((!term && g == g1) ? 1 : 0);
-    return __builtin_amdgcn_readfirstlane((kind ? ldc(a.selPPB + g) : ldc(a.selPP + g)) ^ a.law_flip);
+    kind = (!term && g == g1) ? 1 : 0;
+    return (kind ? ldc(a.selPPB + g) : ldc(a.selPP + g)) ^ a.law_flip;
   };
-  // thread 0 keeps the block's running state; its start-point loads are issued here and
-  // consumed only after the first prepare phase
-  T ll = (T)0, seg_acc = (T)0;
-  bool ok = true;
-  T x0[D], H0[HP], F0[D], c00 = (T)0;
-  if (threadIdx.x == 0) {
+  // block start point (u's path; every lane holds it) and loglikhd_obs of the first segment
+  T xc[D], ll;
+  {
     const T* Xs = a.X[sel.x(g0) ^ a.xs_flip];
-    const int64_t q = bq0;
     const int lsp = ldc(a.selPP + g0) ^ a.law_flip;
+    const int64_t q = bq0;
+    T H0[HP], F0[D];
 #pragma unroll
-    for (int p = 0; p < D; ++p) x0[p] = Xs[(tq + q) * D + p];
+    for (int p = 0; p < D; ++p) xc[p] = Xs[(tq + q) * D + p];
 #pragma unroll
     for (int c = 0; c < HP; ++c)
       H0[c] = a.H_shared[lsp][0] ? a.H[lsp][0][q * HP + c] : a.H[lsp][0][(tq + q) * HP + c];
 #pragma unroll
     for (int c = 0; c < D; ++c) F0[c] = a.F[lsp][0][(tq + q) * D + c];
-    c00 = (T)a.law[lsp][0][(int64_t)g0 * DMT_LAW_STRIDE + DMT_LAW_C0];
-    s_done = 0;
+    const T c00 = (T)ldc(a.law[lsp][0] + (int64_t)g0 * DMT_LAW_STRIDE + DMT_LAW_C0);
+    ll = obs_term<D, T>(H0, F0, xc, c00);
   }
-  // this wave's chunk iterator: chunk w of the block
-  ChunkIt it{g0, 0, ldc(&bi->np0) - 1};
-  for (int j = 0; j < w && j + 1 < ktot; ++j) it.next(a.seg_np);
-  const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32), c3 = a.salt << 1;
-
-  for (int kb = 0; kb < ktot; kb += kScanWaves) {
-    const int k = kb + w;
-    const bool act = k < ktot;
-    const int nact = min(kScanWaves, ktot - kb);
-    const int g = __builtin_amdgcn_readfirstlane(it.g);
-    const int c0 = __builtin_amdgcn_readfirstlane(it.c0);
-    const int nst = __builtin_amdgcn_readfirstlane(it.nst);
-    const int cnt = act ? min(64, nst - c0) : 0;
-    const bool valid = lane < cnt;
-    const int i = c0 + (valid ? lane : max(cnt - 1, 0));
-    int kind = 0;
-    const int ls = act ? law_sel(g, kind) : 0;
-    const int64_t q0 = !act ? 0 : (g == g0 ? (int64_t)bq0 : (int64_t)ldc(a.seg_q + g));
+  bool ok = true;
+  for (int g = g0; g <= g1; ++g) {
+    int kind;
+    const int ls = law_sel(g, kind);
+    const int nst = ldc(a.seg_np + g) - 1;
+    const int64_t q0 = g == g0 ? (int64_t)bq0 : (int64_t)ldc(a.seg_q + g);
     const int64_t row = tq + q0;
     const T* tb = a.t_shared ? a.t + q0 : a.t + row;
     const T* Hb = a.H_shared[ls][kind] ? a.H[ls][kind] + q0 * HP : a.H[ls][kind] + row * HP;
     const T* Fb = a.F[ls][kind] + row * D;
-    const double* lawp = a.law[ls][kind] + (int64_t)g * DMT_LAW_STRIDE;
-    // chunks of the block's first segment store right after their sums (no earlier segment
-    // can have failed); later ones wait for the in-order success test
-    const bool early = k < kfirst;
-    const bool need_b4 = (kb + nact > kfirst) || (kb + nact < ktot);
+    Law<Mdl, T> LA;
+    LA.load(a.law[ls][kind] + (int64_t)g * DMT_LAW_STRIDE);
+    const T* Wsb = a.W[sel.w(g) ^ a.ws_flip] + row * M;
     T* const Xdb = a.X[sel.x(g) ^ a.xd_flip] + row * D;
     T* const Wdb = a.W[sel.w(g) ^ a.wd_flip] + row * M;
-    T A[D * D], e[D], dW[M], w0v[M];
-    STAMP();
-    if (act) {  // ---- prepare (lane-parallel): normals, pCN, σ·dW°, step maps; then the scan
-      const T* Wsb = a.W[sel.w(g) ^ a.ws_flip] + row * M;
-      if (MODE != MODE_RECOMPUTE && c0 == 0) {
+    const double* Zg = a.Z ? a.Z + ldc(a.st_off + g) * M : nullptr;
+    if (MODE != MODE_RECOMPUTE && lane == 0) {  // W°(t0) = ρ·W(t0)
+      T w0v[M];
 #pragma unroll
-        for (int kk = 0; kk < M; ++kk) w0v[kk] = rho * ((MODE == MODE_FRESH) ? (T)0 : Wsb[kk]);
-      }
-      const T dt = tb[i + 1] - tb[i];
-      Law<Mdl, T> LA;
-      LA.load(lawp);
-#ifdef DMT_STAMPS
-      if (dt == (T)-12345) a.ll_out[0] = LA.sg[0];  // forces the loads to land before the stamp
-#endif
-      STAMP();
-      if (MODE == MODE_RECOMPUTE) {
+      for (int k = 0; k < M; ++k) w0v[k] = rho * ((MODE == MODE_FRESH) ? (T)0 : Wsb[k]);
+      store_row<M, T>(Wdb, w0v);
+    }
+    T seg_acc = (T)0;
+    for (int c0 = 0; c0 < nst; c0 += kSChunk) {
+      const int cnt = min(kSChunk, nst - c0);
+      // ---- phase 1 (coalesced): step maps of the chunk → LDS
+      T Hk[kKeep ? kRun : 1][HP], Fk[kKeep ? kRun : 1][D], dtk[kKeep ? kRun : 1];
 #pragma unroll
-        for (int kk = 0; kk < M; ++kk) dW[kk] = Wsb[(int64_t)(i + 1) * M + kk];
-      } else {
-        __builtin_amdgcn_sched_barrier(0);
-        const double* Zg = a.Z ? a.Z + ldc(a.st_off + g) * M : nullptr;
-        uint32_t have = 0xFFFFFFFFu;
-        T z0 = (T)0, z1 = (T)0;
-        const T sdt = sqrt(dt);
+      for (int k = 0; k < kRun; ++k) {
+        const int s = 64 * k + lane;
+        const bool v = s < cnt;
+        const int i = c0 + (v ? s : cnt - 1);
+        T Hi[HP], Fi[D];
+        const T dt = tb[i + 1] - tb[i];
 #pragma unroll
-        for (int kk = 0; kk < M; ++kk) {
-          const uint32_t n = (uint32_t)(i * M + kk);
-          T z;
-          if (Zg) {
-            z = (T)Zg[(int64_t)i * M + kk];
-          } else {
-            if ((n >> 1) != have) {
-              U4 o = philox4x32_10(U4{n >> 1, (uint32_t)g + a.seg_base, iter, c3}, k0, k1);
-              normal_pair(o, z0, z1);
-              have = n >> 1;
+        for (int c = 0; c < HP; ++c) Hi[c] = Hb[(int64_t)i * HP + c];
+#pragma unroll
+        for (int c = 0; c < D; ++c) Fi[c] = Fb[(int64_t)i * D + c];
+        if constexpr (kKeep) {
+          dtk[k] = dt;
+#pragma unroll
+          for (int c = 0; c < HP; ++c) Hk[k][c] = Hi[c];
+#pragma unroll
+          for (int c = 0; c < D; ++c) Fk[k][c] = Fi[c];
+        }
+        T dW[M];
+        if (MODE == MODE_RECOMPUTE) {
+#pragma unroll
+          for (int kk = 0; kk < M; ++kk) dW[kk] = Wsb[(int64_t)(i + 1) * M + kk];
+        } else {
+          uint32_t have = 0xFFFFFFFFu;
+          T z0 = (T)0, z1 = (T)0;
+          const T sdt = sqrt(dt);
+#pragma unroll
+          for (int kk = 0; kk < M; ++kk) {
+            const uint32_t n = (uint32_t)(i * M + kk);
+            T z;
+            if (Zg) {
+              z = (T)Zg[(int64_t)i * M + kk];
+            } else {
+              if ((n >> 1) != have) {
+                U4 o = philox4x32_10(U4{n >> 1, (uint32_t)g + a.seg_base, iter, c3}, k0, k1);
+                normal_pair(o, z0, z1);
+                have = n >> 1;
+              }
+              z = (n & 1u) ? z1 : z0;
             }
-            z = (n & 1u) ? z1 : z0;
+            const T wv = (MODE == MODE_FRESH) ? (T)0 : Wsb[(int64_t)(i + 1) * M + kk];
+            dW[kk] = dfma(rho, wv, srho * (sdt * z));
           }
-          const T wv = (MODE == MODE_FRESH) ? (T)0 : Wsb[(int64_t)(i + 1) * M + kk];
-          dW[kk] = dfma(rho, wv, srho * (sdt * z));
+          if (v) store_row<M, T>(Wdb + (int64_t)(i + 1) * M, dW);
         }
-        __builtin_amdgcn_sched_barrier(0);
+        T sdW[D], Mg[D * D], cg[D], A[D * D], e[D];
+        sigma_dw<Mdl, T>(LA, dW, sdW);
+        guide_coeffs<Mdl, T>(LA, Hi, Fi, Mg, cg);
+        affine_step<D, T>(Mg, cg, dt, sdW, A, e);
+        const int li = lds_ix(s);
+#pragma unroll
+        for (int c = 0; c < D * D; ++c) S.map[c][li] = v ? A[c] : (c % (D + 1) == 0 ? (T)1 : (T)0);
+#pragma unroll
+        for (int c = 0; c < D; ++c) S.map[D * D + c][li] = v ? e[c] : (T)0;
       }
-      T Hi[HP], Fi[D], sdW[D], Mg[D * D], cg[D];
+      wave_lds_sync();
+      // ---- phase 2 (runs): run maps, Kogge–Stone scan, start points, points
+      const int nv = max(0, min(kRun, cnt - kRun * lane));  // valid steps of this lane's run
+      T A8[kRun][D * D], e8[kRun][D];
 #pragma unroll
-      for (int c = 0; c < HP; ++c) Hi[c] = Hb[(int64_t)i * HP + c];
+      for (int r = 0; r < kRun; ++r) {
+        const int li = lds_ix(kRun * lane + r);
 #pragma unroll
-      for (int c = 0; c < D; ++c) Fi[c] = Fb[(int64_t)i * D + c];
-      sigma_dw<Mdl, T>(LA, dW, sdW);
-      guide_coeffs<Mdl, T>(LA, Hi, Fi, Mg, cg);
-      affine_step<D, T>(Mg, cg, dt, sdW, A, e);
-      STAMP();
-      if (!valid) {  // identity beyond the chunk's last step
+        for (int c = 0; c < D * D; ++c) A8[r][c] = S.map[c][li];
 #pragma unroll
-        for (int p = 0; p < D; ++p) {
-#pragma unroll
-          for (int q = 0; q < D; ++q) A[p * D + q] = p == q ? (T)1 : (T)0;
-          e[p] = (T)0;
-        }
+        for (int c = 0; c < D; ++c) e8[r][c] = S.map[D * D + c][li];
       }
-      // inclusive Kogge–Stone scan over the lanes: lane j ← map_j ∘ … ∘ map_0
+      T RA[D * D], Re[D];
+#pragma unroll
+      for (int c = 0; c < D * D; ++c) RA[c] = A8[0][c];
+#pragma unroll
+      for (int c = 0; c < D; ++c) Re[c] = e8[0][c];
+#pragma unroll
+      for (int r = 1; r < kRun; ++r) {  // run map = step_{nv-1} ∘ … ∘ step_0
+        T An[D * D], en[D];
+        affine_compose<D, T>(A8[r], e8[r], RA, Re, An, en);
+        const bool take = r < nv;
+#pragma unroll
+        for (int c = 0; c < D * D; ++c) RA[c] = take ? An[c] : RA[c];
+#pragma unroll
+        for (int c = 0; c < D; ++c) Re[c] = take ? en[c] : Re[c];
+      }
+      // inclusive Kogge–Stone scan over the lanes: lane j ← run_j ∘ … ∘ run_0
 #pragma unroll
       for (int o = 1; o < 64; o <<= 1) {
         T Ap[D * D], ep[D], An[D * D], en[D];
         const int src = 4 * (lane - o);  // lanes < o read garbage and keep their own map
 #pragma unroll
-        for (int c = 0; c < D * D; ++c) Ap[c] = lane_read(A[c], src);
+        for (int c = 0; c < D * D; ++c) Ap[c] = lane_read(RA[c], src);
 #pragma unroll
-        for (int c = 0; c < D; ++c) ep[c] = lane_read(e[c], src);
-        affine_compose<D, T>(A, e, Ap, ep, An, en);
+        for (int c = 0; c < D; ++c) ep[c] = lane_read(Re[c], src);
+        affine_compose<D, T>(RA, Re, Ap, ep, An, en);
         const bool take = lane >= o;
 #pragma unroll
-        for (int c = 0; c < D * D; ++c) A[c] = take ? An[c] : A[c];
+        for (int c = 0; c < D * D; ++c) RA[c] = take ? An[c] : RA[c];
 #pragma unroll
-        for (int c = 0; c < D; ++c) e[c] = take ? en[c] : e[c];
+        for (int c = 0; c < D; ++c) Re[c] = take ? en[c] : Re[c];
       }
-      if (lane == cnt - 1) {
+      // start of run j = prefix_{j-1} applied to the chunk start (lane 0: the chunk start)
+      T x[D];
+      {
+        T y[D];
+        affine_apply<D, T>(RA, Re, xc, y);
 #pragma unroll
-        for (int c = 0; c < D * D; ++c) s_tot[w][c] = A[c];
-#pragma unroll
-        for (int c = 0; c < D; ++c) s_tot[w][D * D + c] = e[c];
-      }
-      if (lane == 0) s_segend[w] = (c0 + 64 >= nst) ? 1 : 0;
-    }
-    if (threadIdx.x == 0 && kb == 0) {  // block start point and loglikhd_obs
-#pragma unroll
-      for (int p = 0; p < D; ++p) s_xs[0][p] = x0[p];
-      ll = obs_term<D, T>(H0, F0, x0, c00);
-    }
-    STAMP();
-    __syncthreads();
-    STAMP();
-    // the guiding-table values of the step, re-read (L2) while thread 0 runs the carry
-    T Hi[HP], Fi[D], dt = (T)0;
-    if (act) {
-      dt = tb[i + 1] - tb[i];
-#pragma unroll
-      for (int c = 0; c < HP; ++c) Hi[c] = Hb[(int64_t)i * HP + c];
-#pragma unroll
-      for (int c = 0; c < D; ++c) Fi[c] = Fb[(int64_t)i * D + c];
-    }
-    if (threadIdx.x == 0) {  // ---- carry: chunk start points, in order
-      T xc[D];
-#pragma unroll
-      for (int p = 0; p < D; ++p) xc[p] = s_xs[0][p];
-#pragma unroll
-      for (int ww = 0; ww < kScanWaves; ++ww) {
-        if (ww < nact) {
-          T tA[D * D], te[D], xn[D];
-#pragma unroll
-          for (int c = 0; c < D * D; ++c) tA[c] = s_tot[ww][c];
-#pragma unroll
-          for (int c = 0; c < D; ++c) te[c] = s_tot[ww][D * D + c];
-          affine_apply<D, T>(tA, te, xc, xn);
-#pragma unroll
-          for (int p = 0; p < D; ++p) {
-            xc[p] = xn[p];
-            s_xs[ww + 1][p] = xn[p];
-          }
+        for (int p = 0; p < D; ++p) {
+          const T up = lane_read(y[p], 4 * (lane - 1));
+          x[p] = lane == 0 ? xc[p] : up;
         }
       }
-    }
-    __syncthreads();
-    STAMP();
-    T xpost[D], xpre[D];
-    if (act) {  // ---- points, Girsanov terms, chunk sum
-      T xs[D];
 #pragma unroll
-      for (int p = 0; p < D; ++p) xs[p] = s_xs[w][p];
-      affine_apply<D, T>(A, e, xs, xpost);
+      for (int r = 0; r < kRun; ++r) {
+        if (r < nv) {
+          const int li = lds_ix(kRun * lane + r);
 #pragma unroll
-      for (int p = 0; p < D; ++p) {
-        const T up = lane_read(xpost[p], 4 * (lane - 1));
-        xpre[p] = lane == 0 ? xs[p] : up;
-      }
-      Law<Mdl, T> LB;
-      LB.load(lawp);
-      T rr[D], bb[D];
-      const T G = g_at<Mdl, T>(LB, Hi, Fi, xpre, rr, bb);
-      const T csum = wave_tree_sum<T>(valid ? G * dt : (T)0);
-      if (lane == 0) s_csum[w] = csum;
-    }
-    auto store_chunk = [&]() {  // coalesced: 64 consecutive points per wave
-      if (valid) {
-        store_row<D, T>(Xdb + (int64_t)i * D, xpre);
-        if (MODE != MODE_RECOMPUTE) store_row<M, T>(Wdb + (int64_t)(i + 1) * M, dW);
-      }
-      if (MODE != MODE_RECOMPUTE && c0 == 0 && lane == 0) store_row<M, T>(Wdb, w0v);
-      if (c0 + 64 >= nst && lane == cnt - 1) store_row<D, T>(Xdb + (int64_t)nst * D, xpost);
-    };
-    if (act && early) store_chunk();
-    STAMP();
-    __syncthreads();
-    STAMP();
-    if (threadIdx.x == 0) {  // ---- segment sums and success, in chunk order
-      T cs[kScanWaves];
-      int se[kScanWaves];
+          for (int p = 0; p < D; ++p) S.pt[p][li] = x[p];
+          T xn[D];
+          affine_apply<D, T>(A8[r], e8[r], x, xn);
 #pragma unroll
-      for (int ww = 0; ww < kScanWaves; ++ww) {
-        cs[ww] = ww < nact ? s_csum[ww] : (T)0;
-        se[ww] = ww < nact ? s_segend[ww] : 0;
-      }
-      int allow = nact;
-#pragma unroll
-      for (int ww = 0; ww < kScanWaves; ++ww) {
-        if (ww < nact && allow == nact) {
-          seg_acc = seg_acc + (cs[ww] + (T)0);
-          if (se[ww]) {
-            bool sok = isfinite(seg_acc);
-#pragma unroll
-            for (int p = 0; p < D; ++p) sok = sok && isfinite(s_xs[ww + 1][p]);
-            if (sok) {
-              ll = ll + seg_acc;
-            } else {
-              ok = false;
-              allow = ww + 1;
-            }
-            seg_acc = (T)0;
-          }
+          for (int p = 0; p < D; ++p) x[p] = xn[p];
         }
       }
-      s_allow = allow;
-      if (!ok) s_done = 1;
+      if (nv > 0 && kRun * lane + nv == cnt) {  // the lane holding the chunk's last step
 #pragma unroll
-      for (int p = 0; p < D; ++p) s_xs[0][p] = s_xs[nact][p];
+        for (int p = 0; p < D; ++p) S.pt[p][lds_ix(cnt)] = x[p];
+      }
+      wave_lds_sync();
+      // ---- phase 3 (coalesced): Girsanov terms, 64-step chunk sums, path stores
+#pragma unroll
+      for (int k = 0; k < kRun; ++k) {
+        if (64 * k < cnt) {  // uniform
+          const int s = 64 * k + lane;
+          const bool v = s < cnt;
+          const int li = lds_ix(s);
+          T xpre[D];
+#pragma unroll
+          for (int p = 0; p < D; ++p) xpre[p] = S.pt[p][li];
+          T Hi[HP], Fi[D], dt;
+          if constexpr (kKeep) {
+            dt = dtk[k];
+#pragma unroll
+            for (int c = 0; c < HP; ++c) Hi[c] = Hk[k][c];
+#pragma unroll
+            for (int c = 0; c < D; ++c) Fi[c] = Fk[k][c];
+          } else {
+            const int i = c0 + (v ? s : cnt - 1);
+            dt = tb[i + 1] - tb[i];
+#pragma unroll
+            for (int c = 0; c < HP; ++c) Hi[c] = Hb[(int64_t)i * HP + c];
+#pragma unroll
+            for (int c = 0; c < D; ++c) Fi[c] = Fb[(int64_t)i * D + c];
+          }
+          T rr[D], bb[D];
+          const T G = g_at<Mdl, T>(LA, Hi, Fi, xpre, rr, bb);
+          const T csum = wave_tree_sum<T>(v ? G * dt : (T)0);
+          seg_acc = seg_acc + (csum + (T)0);
+          if (v) store_row<D, T>(Xdb + (int64_t)(c0 + s) * D, xpre);
+        }
+      }
+#pragma unroll
+      for (int p = 0; p < D; ++p) xc[p] = S.pt[p][lds_ix(cnt)];
+      wave_lds_sync();
     }
-    if (!need_b4) break;  // last round, every chunk already stored
-    __syncthreads();
-    STAMP();
-    if (act && !early && w < s_allow) store_chunk();
-    if (__builtin_amdgcn_readfirstlane(s_done)) break;  // uniform exit keeps `it` scalar
-    for (int j = 0; j < kScanWaves && k + j + 1 < ktot; ++j) it.next(a.seg_np);
+    if (lane == 0) store_row<D, T>(Xdb + (int64_t)nst * D, xc);
+    bool sok = isfinite(seg_acc);
+#pragma unroll
+    for (int p = 0; p < D; ++p) sok = sok && isfinite(xc[p]);
+    if (!sok) {  // a failed segment ends the block (later segments untouched)
+      ok = false;
+      break;
+    }
+    ll = ll + seg_acc;
   }
-  STAMP();
-#ifdef DMT_STAMPS
-  if (lane == 0 && iter == 7 && (blockIdx.x < 2 || blockIdx.x == gridDim.x - 1 || blockIdx.x == 500)) {
-    printf("STAMP blk %d w %d n %d : %lu %lu %lu %lu %lu %lu %lu %lu %lu %lu %lu\n", (int)blockIdx.x, w, nst_,
-           st[1] - st[0], st[2] - st[0], st[3] - st[0], st[4] - st[0], st[5] - st[0], st[6] - st[0],
-           st[7] - st[0], st[8] - st[0], st[9] - st[0], st[10] - st[0], st[nst_ - 1] - st[0]);
-  }
-#endif
-#undef STAMP
   ll_res = ll;
   ok_res = ok;
 }
 
 template <class Mdl, class T, int MODE>
-__global__ __launch_bounds__(64 * kScanWaves, DMT_SCAN_MINW) void k_block_scan(const BlockArgs<T> a) {
-  const int64_t blk = a.b0 + (int64_t)blockIdx.x;
-  if (blk >= a.b1) return;
+__global__ __launch_bounds__((64 * ScanCfg<Mdl::D, T>::WPB), 1) void k_block_scan(const BlockArgs<T> a) {
+  using Cfg = ScanCfg<Mdl::D, T>;
+  __shared__ ScanLds<Mdl::D, T> lds[Cfg::WPB];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t blk = a.b0 + (int64_t)blockIdx.x * Cfg::WPB + w;
+  if (blk >= a.b1) return;  // whole wave: the waves of a workgroup never synchronise
   T ll;
   bool ok;
-  scan_block<Mdl, T, MODE>(a, blk, a.iter, SelGlobal{a.selX, a.selW}, ll, ok);
-  if (threadIdx.x == 0) {
+  scan_block<Mdl, T, MODE>(a, blk, a.iter, SelGlobal{a.selX, a.selW}, lds[w], ll, ok);
+  if ((threadIdx.x & 63) == 0) {
     a.ll_out[blk] = ok ? (double)ll : -INFINITY;
     if (a.success) a.success[blk] = ok ? 1 : 0;
   }
@@ -1037,66 +1015,332 @@ __global__ __launch_bounds__(64 * kScanWaves, DMT_SCAN_MINW) void k_block_scan(c
 
 // dmt_mcmc_run for linear drifts: n_iter path-MCMC iterations in ONE launch.  Blocks are
 // independent across iterations (a block's next proposal depends only on its own accepted
-// state), so each workgroup loops over the iterations for its block: draw (scan_block, device
-// RNG), then — thread 0, exactly as k_accept — the MH decision, selector flips, histories and
-// the ll swap, with the block's selectors and ll kept on chip.  Per-iteration (ll, ll°,
-// accepted) go to part[n_iter][3][nb] for the batched fetch_ll tree (k_tree_batched).
+// state), so each wave loops over the iterations of its block: draw (scan_block, device RNG),
+// then — uniformly, exactly as k_accept — the MH decision, selector flips (bit masks in
+// SGPRs), histories and the ll swap.  Per-iteration (ll, ll°, accepted) go to
+// part[n_iter][3][nb] for the batched fetch_ll tree (k_tree_batched).
 template <class Mdl, class T>
-__global__ __launch_bounds__(64 * kScanWaves, DMT_SCAN_MINW) void k_mcmc_scan(
+__global__ __launch_bounds__((64 * ScanCfg<Mdl::D, T>::WPB), 1) void k_mcmc_scan(
     const BlockArgs<T> a, const AcceptArgs c, const int64_t iter0, const int64_t n_iter,
     double* __restrict__ part) {
-  __shared__ uint8_t s_sx[kPersistMaxSegments], s_sw[kPersistMaxSegments];
-  const int64_t blk = a.b0 + (int64_t)blockIdx.x;
+  using Cfg = ScanCfg<Mdl::D, T>;
+  __shared__ ScanLds<Mdl::D, T> lds[Cfg::WPB];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int64_t blk = a.b0 + (int64_t)blockIdx.x * Cfg::WPB + w;
   if (blk >= a.b1) return;
   const int g0 = ldc(&a.binfo[blk].g0), g1 = ldc(&a.binfo[blk].g1);
-  const int nseg = g1 - g0 + 1;
-  if ((int)threadIdx.x < nseg) {
-    s_sx[threadIdx.x] = a.selX[g0 + threadIdx.x];
-    s_sw[threadIdx.x] = a.selW[g0 + threadIdx.x];
-  }
-  double ll = 0.0, llp = 0.0;
-  if (threadIdx.x == 0) ll = c.ll[blk];
+  const int nseg = g1 - g0 + 1;  // ≤ kPersistMaxSegments = 64 (host-checked)
+  const bool own = lane < nseg;
+  SelMask sel{__ballot(own && a.selX[g0 + (own ? lane : 0)] != 0),
+              __ballot(own && a.selW[g0 + (own ? lane : 0)] != 0), g0};
+  const uint64_t all = nseg >= 64 ? ~(uint64_t)0 : (((uint64_t)1 << nseg) - 1);
+  double ll = c.ll[blk], llp = 0.0;
   const int64_t nb = a.b1 - a.b0, j = blk - a.b0;
-  const SelLds sel{s_sx, s_sw, g0};
-  __syncthreads();
   for (int64_t r = 0; r < n_iter; ++r) {
     const int64_t it = iter0 + r;
+    const double E = exp1_draw(c.seed, (uint32_t)g0 + c.seg_base, (uint32_t)it, c.salt);
     T lp;
     bool ok;
-    scan_block<Mdl, T, MODE_PCN>(a, blk, (uint32_t)it, sel, lp, ok);
-    __syncthreads();  // every wave's u° stores are complete before u/u° can swap
-    if (threadIdx.x == 0) {
-      llp = ok ? (double)lp : -INFINITY;
-      const double E = exp1_draw(c.seed, (uint32_t)g0 + c.seg_base, (uint32_t)it, c.salt);
-      const bool acc = E > -(llp - ll);
-      if (acc) {
-        for (int k = 0; k < nseg; ++k) {
-          s_sx[k] ^= 1;
-          s_sw[k] ^= 1;
-        }
-      }
+    scan_block<Mdl, T, MODE_PCN>(a, blk, (uint32_t)it, sel, lds[w], lp, ok);
+    llp = ok ? (double)lp : -INFINITY;
+    const bool acc = E > -(llp - ll);
+    if (acc) {
+      sel.mx ^= all;
+      sel.mw ^= all;
+    }
+    if (lane == 0) {
       if (c.hist_len > 0) {
         const int64_t o = (it - 1) * c.nblocks + blk;
         c.acc_hist[o] = acc ? 1 : 0;
         c.ll_hist[o] = ll;
         c.llp_hist[o] = llp;
       }
-      if (acc) {
-        const double t = ll;
-        ll = llp;
-        llp = t;
-      }
-      part[(3 * r + 0) * nb + j] = ll;
-      part[(3 * r + 1) * nb + j] = llp;
+      part[(3 * r + 0) * nb + j] = acc ? llp : ll;
+      part[(3 * r + 1) * nb + j] = acc ? ll : llp;
       part[(3 * r + 2) * nb + j] = acc ? 1.0 : 0.0;
     }
-    __syncthreads();
+    if (acc) {
+      const double t = ll;
+      ll = llp;
+      llp = t;
+    }
+    // this wave's path stores of the iteration are complete before the next iteration reads
+    // the accepted path back
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   }
-  if ((int)threadIdx.x < nseg) {
-    a.selX[g0 + threadIdx.x] = s_sx[threadIdx.x];
-    a.selW[g0 + threadIdx.x] = s_sw[threadIdx.x];
+  if (own) {
+    a.selX[g0 + lane] = (uint8_t)sel.x(g0 + lane);
+    a.selW[g0 + lane] = (uint8_t)sel.w(g0 + lane);
   }
-  if (threadIdx.x == 0) {
+  if (lane == 0) {
+    c.ll[blk] = ll;
+    c.llp[blk] = llp;
+  }
+}
+
+// dmt_mcmc_run for linear drifts whose blocks are ONE segment of at most kSChunk steps (e.g.
+// C2): the same canonical arithmetic as scan_block, but the block's per-step constants stay
+// in registers for the whole run, in run order (lane j ↔ steps 8j … 8j+7): the step matrices
+// A_i, the guiding offsets c_i, dt_i, √dt_i, H_i, F_i, and u's Wiener increments (after a
+// decision they are the proposal's dW° or stay, both already in registers).  Per iteration the
+// wave only draws normals, forms e_i = fma(c_i, dt_i, σdW°_i), composes / scans / applies the
+// maps, evaluates G at the points (register-local 8-leaf trees + 3 cross-lane levels = the
+// 64-step chunk trees) and stores X°, W° — transposed through LDS so that the stores stay
+// coalesced.  Global memory is read once per launch.  The Exp(1) draws of 64 iterations are
+// computed at once, one per lane.
+template <int D, int M, class T>
+struct ResLds {
+  T pt[kSStride][D];  // pre-step points by LDS slot of the step (+ end point)
+  T dw[kSStride][M];  // W° increments by LDS slot of the step
+};
+template <int D, int M, class T>
+struct ResCfg {
+  static constexpr int WPB = 4;  // one wave per SIMD
+};
+
+template <class Mdl, class T>
+__global__ __launch_bounds__(256, 1) void k_mcmc_resident(const BlockArgs<T> a,
+                                                          const AcceptArgs c,
+                                                          const int64_t iter0,
+                                                          const int64_t n_iter,
+                                                          double* __restrict__ part) {
+  constexpr int D = Mdl::D, M = Mdl::M, HP = D * (D + 1) / 2;
+  static_assert(Mdl::kLinear, "k_mcmc_resident needs a linear drift");
+  __shared__ ResLds<D, M, T> lds[4];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int64_t blk = a.b0 + (int64_t)blockIdx.x * 4 + w;
+  if (blk >= a.b1) return;
+  ResLds<D, M, T>& S = lds[w];
+  const BlkInfo* bi = a.binfo + blk;
+  const int64_t tq = ldc(&bi->tq);
+  const int g = ldc(&bi->g0);  // the block's only segment (host-checked)
+  const int q0 = ldc(&bi->q0);
+  const bool term = ldc(&bi->term) != 0;  // a single-segment block: P_last law if non-terminal
+  const T rho = (T)ldc(&bi->rho), srho = (T)ldc(&bi->srho);
+  const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32), c3 = a.salt << 1;
+  const int nst = ldc(a.seg_np + g) - 1;  // ≤ kSChunk
+  const int64_t row = tq + q0;
+  const int kind = term ? 0 : 1;
+  const int ls = (kind ? ldc(a.selPPB + g) : ldc(a.selPP + g)) ^ a.law_flip;
+  Law<Mdl, T> LA;
+  LA.load(a.law[ls][kind] + (int64_t)g * DMT_LAW_STRIDE);
+  const T* tb = a.t_shared ? a.t + q0 : a.t + row;
+  const T* Hb = a.H_shared[ls][kind] ? a.H[ls][kind] + (int64_t)q0 * HP : a.H[ls][kind] + row * HP;
+  const T* Fb = a.F[ls][kind] + row * D;
+  SelMask sel{(uint64_t)(a.selX[g] & 1), (uint64_t)(a.selW[g] & 1), g};
+  // ---- per-launch state: start point, loglikhd_obs, per-step constants (run order)
+  T x0[D], w0[M], llobs;
+  {
+    const T* Xs = a.X[sel.x(g) ^ a.xs_flip] + row * D;
+    const T* Ws = a.W[sel.w(g) ^ a.ws_flip] + row * M;
+    const int lsp = ldc(a.selPP + g) ^ a.law_flip;  // loglikhd_obs uses PP[1] (block.jl:178)
+    T H0[HP], F0[D];
+#pragma unroll
+    for (int p = 0; p < D; ++p) x0[p] = Xs[p];
+#pragma unroll
+    for (int k = 0; k < M; ++k) w0[k] = Ws[k];
+#pragma unroll
+    for (int cc = 0; cc < HP; ++cc)
+      H0[cc] = a.H_shared[lsp][0] ? a.H[lsp][0][(int64_t)q0 * HP + cc] : a.H[lsp][0][row * HP + cc];
+#pragma unroll
+    for (int cc = 0; cc < D; ++cc) F0[cc] = a.F[lsp][0][row * D + cc];
+    const T c00 = (T)ldc(a.law[lsp][0] + (int64_t)g * DMT_LAW_STRIDE + DMT_LAW_C0);
+    llobs = obs_term<D, T>(H0, F0, x0, c00);
+  }
+  const int nv = max(0, min(kRun, nst - kRun * lane));  // valid steps of this lane's run
+  T Ac[kRun][D * D], cgs[kRun][D], dts[kRun], sdts[kRun], Hs[kRun][HP], Fs[kRun][D], wv[kRun][M];
+  {
+    const T* Ws = a.W[sel.w(g) ^ a.ws_flip] + row * M;
+#pragma unroll
+    for (int r = 0; r < kRun; ++r) {
+      const int s = min(kRun * lane + r, nst - 1);
+      dts[r] = tb[s + 1] - tb[s];
+      sdts[r] = sqrt(dts[r]);
+#pragma unroll
+      for (int cc = 0; cc < HP; ++cc) Hs[r][cc] = Hb[(int64_t)s * HP + cc];
+#pragma unroll
+      for (int cc = 0; cc < D; ++cc) Fs[r][cc] = Fb[(int64_t)s * D + cc];
+#pragma unroll
+      for (int k = 0; k < M; ++k) wv[r][k] = Ws[(int64_t)(s + 1) * M + k];
+      T Mg[D * D], zero[D] = {}, e_unused[D];
+      guide_coeffs<Mdl, T>(LA, Hs[r], Fs[r], Mg, cgs[r]);
+      affine_step<D, T>(Mg, cgs[r], dts[r], zero, Ac[r], e_unused);
+    }
+  }
+  const uint64_t all = 1;
+  double ll = c.ll[blk], llp = 0.0;
+  const int64_t nb = a.b1 - a.b0, j = blk - a.b0;
+  const int last_lane = (nst - 1) / kRun;
+  double Ev = 0.0;
+  for (int64_t r0 = 0; r0 < n_iter; ++r0) {
+    const int64_t it = iter0 + r0;
+    if ((r0 & 63) == 0)  // Exp(1) draws of the next 64 iterations, one per lane
+      Ev = exp1_draw(c.seed, (uint32_t)g + c.seg_base, (uint32_t)(it + lane), c.salt);
+    const double E = __builtin_bit_cast(
+        double, ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(
+                     (int)(__builtin_bit_cast(uint64_t, Ev) >> 32), (int)(r0 & 63)) << 32) |
+                    (uint32_t)__builtin_amdgcn_readlane((int)__builtin_bit_cast(uint64_t, Ev),
+                                                        (int)(r0 & 63)));
+    T* const Xdb = a.X[sel.x(g) ^ a.xd_flip] + row * D;
+    T* const Wdb = a.W[sel.w(g) ^ a.wd_flip] + row * M;
+    // ---- normals, pCN increments, e maps; run map
+    T dW[kRun][M], e[kRun][D];
+#pragma unroll
+    for (int r = 0; r < kRun; ++r) {
+      const int s = kRun * lane + r;
+      uint32_t have = 0xFFFFFFFFu;
+      T z0 = (T)0, z1 = (T)0;
+#pragma unroll
+      for (int kk = 0; kk < M; ++kk) {
+        const uint32_t n = (uint32_t)(s * M + kk);
+        if ((n >> 1) != have) {
+          U4 o = philox4x32_10(U4{n >> 1, (uint32_t)g + a.seg_base, (uint32_t)it, c3}, k0, k1);
+          normal_pair(o, z0, z1);
+          have = n >> 1;
+        }
+        const T z = (n & 1u) ? z1 : z0;
+        dW[r][kk] = dfma(rho, wv[r][kk], srho * (sdts[r] * z));
+      }
+      T sdW[D];
+      sigma_dw<Mdl, T>(LA, dW[r], sdW);
+#pragma unroll
+      for (int p = 0; p < D; ++p) e[r][p] = dfma(cgs[r][p], dts[r], sdW[p]);
+    }
+    T RA[D * D], Re[D];
+#pragma unroll
+    for (int cc = 0; cc < D * D; ++cc) RA[cc] = nv > 0 ? Ac[0][cc] : (cc % (D + 1) == 0 ? (T)1 : (T)0);
+#pragma unroll
+    for (int p = 0; p < D; ++p) Re[p] = nv > 0 ? e[0][p] : (T)0;
+#pragma unroll
+    for (int r = 1; r < kRun; ++r) {
+      T An[D * D], en[D];
+      affine_compose<D, T>(Ac[r], e[r], RA, Re, An, en);
+      const bool take = r < nv;
+#pragma unroll
+      for (int cc = 0; cc < D * D; ++cc) RA[cc] = take ? An[cc] : RA[cc];
+#pragma unroll
+      for (int p = 0; p < D; ++p) Re[p] = take ? en[p] : Re[p];
+    }
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      T Ap[D * D], ep[D], An[D * D], en[D];
+      const int src = 4 * (lane - o);
+#pragma unroll
+      for (int cc = 0; cc < D * D; ++cc) Ap[cc] = lane_read(RA[cc], src);
+#pragma unroll
+      for (int p = 0; p < D; ++p) ep[p] = lane_read(Re[p], src);
+      affine_compose<D, T>(RA, Re, Ap, ep, An, en);
+      const bool take = lane >= o;
+#pragma unroll
+      for (int cc = 0; cc < D * D; ++cc) RA[cc] = take ? An[cc] : RA[cc];
+#pragma unroll
+      for (int p = 0; p < D; ++p) Re[p] = take ? en[p] : Re[p];
+    }
+    T x[D];
+    {
+      T y[D];
+      affine_apply<D, T>(RA, Re, x0, y);
+#pragma unroll
+      for (int p = 0; p < D; ++p) {
+        const T up = lane_read(y[p], 4 * (lane - 1));
+        x[p] = lane == 0 ? x0[p] : up;
+      }
+    }
+    // ---- points, Girsanov terms (8-leaf register tree), LDS staging of X° and W°
+    T gl[kRun];
+#pragma unroll
+    for (int r = 0; r < kRun; ++r) {
+      const int li = lds_ix(kRun * lane + r);
+      const bool v = r < nv;
+      T rr[D], bb[D];
+      const T G = g_at<Mdl, T>(LA, Hs[r], Fs[r], x, rr, bb);
+      gl[r] = v ? G * dts[r] : (T)0;
+      if (v) {
+#pragma unroll
+        for (int p = 0; p < D; ++p) S.pt[li][p] = x[p];
+#pragma unroll
+        for (int k = 0; k < M; ++k) S.dw[li][k] = dW[r][k];
+        T xn[D];
+        affine_apply<D, T>(Ac[r], e[r], x, xn);
+#pragma unroll
+        for (int p = 0; p < D; ++p) x[p] = xn[p];
+      }
+    }
+    // end point of the segment (held by the lane of the last step) → every lane
+    T xe[D];
+#pragma unroll
+    for (int p = 0; p < D; ++p) xe[p] = lane_read(x[p], 4 * last_lane);
+    T tsum = ((gl[0] + gl[1]) + (gl[2] + gl[3])) + ((gl[4] + gl[5]) + (gl[6] + gl[7]));
+    tsum = tsum + __shfl_xor(tsum, 1, 64);
+    tsum = tsum + __shfl_xor(tsum, 2, 64);
+    tsum = tsum + __shfl_xor(tsum, 4, 64);
+    T seg_acc = (T)0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (64 * q < nst) seg_acc = seg_acc + (lane_read(tsum, 4 * 8 * q) + (T)0);
+    wave_lds_sync();
+    // ---- coalesced stores of the proposal: X°[0..nst], W°[0..nst]
+#pragma unroll
+    for (int k = 0; k < kRun; ++k) {
+      const int s = 64 * k + lane;
+      if (s < nst) {
+        const int li = lds_ix(s);
+        T xv[D], wd[M];
+#pragma unroll
+        for (int p = 0; p < D; ++p) xv[p] = S.pt[li][p];
+#pragma unroll
+        for (int kk = 0; kk < M; ++kk) wd[kk] = S.dw[li][kk];
+        store_row<D, T>(Xdb + (int64_t)s * D, xv);
+        store_row<M, T>(Wdb + (int64_t)(s + 1) * M, wd);
+      }
+    }
+    T w0n[M];
+#pragma unroll
+    for (int k = 0; k < M; ++k) w0n[k] = rho * w0[k];
+    if (lane == 0) {
+      store_row<D, T>(Xdb + (int64_t)nst * D, xe);
+      store_row<M, T>(Wdb, w0n);
+    }
+    wave_lds_sync();
+    // ---- MH decision (k_accept's order), selectors, histories, partials
+    bool sok = isfinite(seg_acc);
+#pragma unroll
+    for (int p = 0; p < D; ++p) sok = sok && isfinite(xe[p]);
+    llp = sok ? (double)(llobs + seg_acc) : -INFINITY;
+    const bool acc = E > -(llp - ll);
+    if (acc) {
+      sel.mx ^= all;
+      sel.mw ^= all;
+#pragma unroll
+      for (int r = 0; r < kRun; ++r)
+#pragma unroll
+        for (int k = 0; k < M; ++k) wv[r][k] = dW[r][k];
+#pragma unroll
+      for (int k = 0; k < M; ++k) w0[k] = w0n[k];
+    }
+    if (lane == 0) {
+      if (c.hist_len > 0) {
+        const int64_t o = (it - 1) * c.nblocks + blk;
+        c.acc_hist[o] = acc ? 1 : 0;
+        c.ll_hist[o] = ll;
+        c.llp_hist[o] = llp;
+      }
+      part[(3 * r0 + 0) * nb + j] = acc ? llp : ll;
+      part[(3 * r0 + 1) * nb + j] = acc ? ll : llp;
+      part[(3 * r0 + 2) * nb + j] = acc ? 1.0 : 0.0;
+    }
+    if (acc) {
+      const double t = ll;
+      ll = llp;
+      llp = t;
+    }
+  }
+  if (lane == 0) {
+    a.selX[g] = (uint8_t)sel.x(g);
+    a.selW[g] = (uint8_t)sel.w(g);
     c.ll[blk] = ll;
     c.llp[blk] = llp;
   }
@@ -1756,8 +2000,9 @@ static hipError_t launch_block_t(int mapping, int mode, const void* args, int64_
   const BlockArgs<T>& a = *static_cast<const BlockArgs<T>*>(args);
   if (nwaves <= 0) return hipSuccess;
   const dim3 grid((unsigned)nwaves);
-  if constexpr (Mdl::kLinear) {  // one workgroup per block, always
-    const dim3 sblock(64 * kScanWaves);
+  if constexpr (Mdl::kLinear) {  // one wave per block, always
+    constexpr int WPB = ScanCfg<Mdl::D, T>::WPB;
+    const dim3 grid((unsigned)((nwaves + WPB - 1) / WPB)), sblock(64 * WPB);
     switch (mode) {
       case MODE_PCN: dlaunch(k_block_scan<Mdl, T, MODE_PCN>, grid, sblock, s, a); break;
       case MODE_RECOMPUTE: dlaunch(k_block_scan<Mdl, T, MODE_RECOMPUTE>, grid, sblock, s, a); break;
@@ -1956,12 +2201,20 @@ hipError_t launch_block_kernel(const ModelKey& k, int mapping, int mode, const v
 
 template <class Mdl, class T>
 static hipError_t launch_mcmc_t(const void* args, const AcceptArgs& c, int64_t iter0, int64_t n,
-                                double* part, int64_t nwaves, hipStream_t s) {
+                                double* part, int64_t nwaves, int resident, hipStream_t s) {
   if constexpr (Mdl::kLinear) {
     const BlockArgs<T>& a = *static_cast<const BlockArgs<T>*>(args);
     if (nwaves <= 0) return hipSuccess;
-    dlaunch(k_mcmc_scan<Mdl, T>, dim3((unsigned)nwaves), dim3(64 * kScanWaves), s, a, c, iter0, n,
-            part);
+    if constexpr (Mdl::D <= 2) {
+      if (resident) {
+        dlaunch(k_mcmc_resident<Mdl, T>, dim3((unsigned)((nwaves + 3) / 4)), dim3(256), s, a, c,
+                iter0, n, part);
+        return hipGetLastError();
+      }
+    }
+    constexpr int WPB = ScanCfg<Mdl::D, T>::WPB;
+    dlaunch(k_mcmc_scan<Mdl, T>, dim3((unsigned)((nwaves + WPB - 1) / WPB)), dim3(64 * WPB), s, a,
+            c, iter0, n, part);
     return hipGetLastError();
   } else {
     return hipErrorInvalidValue;
@@ -1970,8 +2223,8 @@ static hipError_t launch_mcmc_t(const void* args, const AcceptArgs& c, int64_t i
 
 hipError_t launch_mcmc_persistent(const ModelKey& k, const void* args, const AcceptArgs& c,
                                   int64_t iter0, int64_t n_iter, double* part, int64_t nwaves,
-                                  hipStream_t s) {
-  DMT_DISPATCH(k, (launch_mcmc_t<Mdl, T>(args, c, iter0, n_iter, part, nwaves, s)));
+                                  int resident, hipStream_t s) {
+  DMT_DISPATCH(k, (launch_mcmc_t<Mdl, T>(args, c, iter0, n_iter, part, nwaves, resident, s)));
 }
 
 hipError_t launch_tree_batched(const double* part, int64_t nb, int64_t n_iter, double* out3,

@@ -140,6 +140,7 @@ struct dmt_ens {
   double* d_part = nullptr;  // k_mcmc_scan per-iteration block partials [n][3][nb]
   int64_t part_cap = 0;
   bool persist = true;       // dmt_mcmc_run of a linear drift in one launch (DMT_MCMC_PERSIST=0: off)
+  bool resident = true;      // ... with register-resident block state when eligible (DMT_MCMC_RESIDENT=0: off)
   std::vector<std::unique_ptr<Layout>> layouts;  // layouts[0] = internal "unit" layout
   // timing
   uint32_t timing = 0;  // bit k: time kernel class k (dmt_set_timing)
@@ -594,6 +595,7 @@ dmt_status dmt_create(dmt_ens** out, const dmt_model* model, const dmt_structure
   // linear drift (OU): the recursion is an affine scan, always one workgroup per block
   if (model->model == DMT_MODEL_OU) h->mapping = MAP_WAVE;
   if (const char* e = std::getenv("DMT_MCMC_PERSIST")) h->persist = std::strcmp(e, "0") != 0;
+  if (const char* e = std::getenv("DMT_MCMC_RESIDENT")) h->resident = std::strcmp(e, "0") != 0;
   h->tw = h->mapping == MAP_WAVE ? 1 : kLanes;
   h->ntiles = (h->R + h->tw - 1) / h->tw;
   h->tile_qoff.assign(h->ntiles + 1, 0);
@@ -1070,6 +1072,9 @@ dmt_status dmt_mcmc_run(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int6
   bool persist = h->persist && h->key.model == DMT_MODEL_OU;
   for (int64_t b = b0; b < b1 && persist; ++b)
     persist = L->glast[b] - L->gfirst[b] + 1 <= kPersistMaxSegments;
+  bool resident = persist && h->key.d <= 2 && h->resident;
+  for (int64_t b = b0; b < b1 && resident; ++b)
+    resident = L->glast[b] == L->gfirst[b] && h->seg_np[L->gfirst[b]] - 1 <= kResidentMaxSteps;
   if (persist) {
     // the whole run in one launch per chunk of iterations (k_mcmc_scan), then one batched
     // fetch_ll tree over all iterations and (multi-GPU) one all-gather
@@ -1099,11 +1104,11 @@ dmt_status dmt_mcmc_run(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int6
         if (h->key.precision == DMT_F64) {
           BlockArgs<double> a{};
           fill(a);
-          e = launch_mcmc_persistent(h->key, &a, c, iter0 + i0, n, h->d_part, nb, h->stream);
+          e = launch_mcmc_persistent(h->key, &a, c, iter0 + i0, n, h->d_part, nb, resident, h->stream);
         } else {
           BlockArgs<float> a{};
           fill(a);
-          e = launch_mcmc_persistent(h->key, &a, c, iter0 + i0, n, h->d_part, nb, h->stream);
+          e = launch_mcmc_persistent(h->key, &a, c, iter0 + i0, n, h->d_part, nb, resident, h->stream);
         }
       }
       if (e != hipSuccess) return fail(DMT_ERR_HIP, std::string("k_mcmc_scan: ") + hipGetErrorString(e));

@@ -240,10 +240,19 @@ static void aff_apply(int d, const REAL* A, const REAL* e, const REAL* x, REAL* 
 }
 
 /* Linear drift (OU): the guided Euler recursion is affine, x_{i+1} = A_i x_i + e_i.  The
- * canonical evaluation (the HIP kernel's k_block_scan) cuts the segment into chunks of 64
- * steps; within a chunk the maps are combined by an inclusive Kogge–Stone scan (level o =
- * 1,2,4,...,32: element j ← element j ∘ element j-o for j ≥ o, all reading the previous
- * level), x_{c0+j+1} = Φ_j x_{c0} + ψ_j, and the next chunk starts at x_{c0+cnt}. */
+ * canonical evaluation (the HIP kernels' scan_block) cuts the segment into
+ * chunks of 512 steps and every chunk into 64 runs of 8 consecutive steps:
+ *   run map     R_j = step_{last valid} ∘ … ∘ step_first (sequential compose; identity when
+ *               the run has no valid step);
+ *   prefix      inclusive Kogge–Stone over the 64 run maps (level o = 1,2,4,…,32: element
+ *               j ← element j ∘ element j-o for j ≥ o, all reading the previous level);
+ *   run start   s_0 = x_{c0}, s_j = apply(P_{j-1}, x_{c0});
+ *   points      within a run, x_{i+1} = apply(step_i, x_i) one step at a time from s_j;
+ *   next chunk  starts at the end point of the chunk's last valid step.
+ * The Girsanov sum keeps the common order: adjacent-pair trees over 64-step chunks from the
+ * segment start, chunk sums added left to right (psum). */
+#define ORC_RUN 8
+#define ORC_SCHUNK 512
 static int solve_segment_scan(int d, int m, const REAL* th, const REAL* sg, const REAL* a,
                               const REAL* Bt, const REAL* beta, const REAL* da, int trace,
                               int npts, const REAL* t, const REAL* H, const REAL* F,
@@ -253,10 +262,11 @@ static int solve_segment_scan(int d, int m, const REAL* th, const REAL* sg, cons
     REAL xs[3];
     for (int p = 0; p < d; ++p) { xs[p] = y1[p]; X[p] = xs[p]; }
     psum_t ps; ps_init(&ps);
-    static __thread REAL A[64][9], e[64][3], An[64][9], en[64][3];
-    for (int c0 = 0; c0 < n; c0 += 64) {
-        int cnt = n - c0 < 64 ? n - c0 : 64;
-        for (int j = 0; j < 64; ++j) {
+    static __thread REAL A[ORC_SCHUNK][9], e[ORC_SCHUNK][3];
+    static __thread REAL RA[64][9], Re[64][3], An[64][9], en[64][3];
+    for (int c0 = 0; c0 < n; c0 += ORC_SCHUNK) {
+        int cnt = n - c0 < ORC_SCHUNK ? n - c0 : ORC_SCHUNK;
+        for (int j = 0; j < ORC_SCHUNK; ++j) {
             if (j < cnt) {
                 int i = c0 + j;
                 REAL dt = t[i + 1] - t[i];
@@ -280,28 +290,50 @@ static int solve_segment_scan(int d, int m, const REAL* th, const REAL* sg, cons
                 }
             }
         }
-        for (int o = 1; o < 64; o <<= 1) {
-            for (int j = o; j < 64; ++j) aff_compose(d, A[j], e[j], A[j - o], e[j - o], An[j], en[j]);
-            for (int j = o; j < 64; ++j) {
-                memcpy(A[j], An[j], sizeof(REAL) * d * d);
-                memcpy(e[j], en[j], sizeof(REAL) * d);
+        /* run maps */
+        for (int j = 0; j < 64; ++j) {
+            int s0 = ORC_RUN * j;
+            int nv = cnt - s0; nv = nv < 0 ? 0 : nv > ORC_RUN ? ORC_RUN : nv;
+            memcpy(RA[j], A[s0], sizeof(REAL) * d * d);
+            memcpy(Re[j], e[s0], sizeof(REAL) * d);
+            for (int r = 1; r < nv; ++r) {
+                REAL tA[9], te[3];
+                aff_compose(d, A[s0 + r], e[s0 + r], RA[j], Re[j], tA, te);
+                memcpy(RA[j], tA, sizeof(REAL) * d * d);
+                memcpy(Re[j], te, sizeof(REAL) * d);
             }
         }
-        REAL xpre[3];
-        for (int p = 0; p < d; ++p) xpre[p] = xs[p];
-        for (int j = 0; j < cnt; ++j) {
-            int i = c0 + j;
-            REAL dt = t[i + 1] - t[i];
-            REAL r[3] = {0, 0, 0}, b[3] = {0, 0, 0};
-            REAL G = g_at(ORC_OU, d, th, a, Bt, beta, da, trace, H + (size_t)i * h,
-                          F + (size_t)i * d, xpre, r, b);
-            ps_add(&ps, G * dt);
-            REAL xp[3];
-            aff_apply(d, A[j], e[j], xs, xp);
-            for (int p = 0; p < d; ++p) { X[(size_t)(i + 1) * d + p] = xp[p]; xpre[p] = xp[p]; }
+        for (int o = 1; o < 64; o <<= 1) {
+            for (int j = o; j < 64; ++j) aff_compose(d, RA[j], Re[j], RA[j - o], Re[j - o], An[j], en[j]);
+            for (int j = o; j < 64; ++j) {
+                memcpy(RA[j], An[j], sizeof(REAL) * d * d);
+                memcpy(Re[j], en[j], sizeof(REAL) * d);
+            }
         }
-        for (int p = 0; p < d; ++p) xs[p] = xpre[p];
+        REAL xend[3];
+        for (int j = 0; j < 64 && ORC_RUN * j < cnt; ++j) {
+            REAL x[3];
+            if (j == 0) { for (int p = 0; p < d; ++p) x[p] = xs[p]; }
+            else aff_apply(d, RA[j - 1], Re[j - 1], xs, x);
+            int s0 = ORC_RUN * j;
+            int nv = cnt - s0 > ORC_RUN ? ORC_RUN : cnt - s0;
+            for (int r = 0; r < nv; ++r) {
+                int i = c0 + s0 + r;
+                REAL dt = t[i + 1] - t[i];
+                REAL rr[3] = {0, 0, 0}, b[3] = {0, 0, 0};
+                if (i > 0) for (int p = 0; p < d; ++p) X[(size_t)i * d + p] = x[p];
+                REAL G = g_at(ORC_OU, d, th, a, Bt, beta, da, trace, H + (size_t)i * h,
+                              F + (size_t)i * d, x, rr, b);
+                ps_add(&ps, G * dt);
+                REAL xp[3];
+                aff_apply(d, A[s0 + r], e[s0 + r], x, xp);
+                for (int p = 0; p < d; ++p) x[p] = xp[p];
+            }
+            for (int p = 0; p < d; ++p) xend[p] = x[p];
+        }
+        for (int p = 0; p < d; ++p) xs[p] = xend[p];
     }
+    for (int p = 0; p < d; ++p) X[(size_t)n * d + p] = xs[p];
     REAL ll = ps_finish(&ps);
     *ll_out = ll;
     int ok = isfinite(ll) ? 1 : 0;

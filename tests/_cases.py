@@ -116,8 +116,17 @@ def load_ragged(ens, case):
     ens.set_paths(L.UPROP, X=X, W=Wp)
 
 
-def ragged_pair(seed=11, hist_len=8, mapping=L.MAP_AUTO):
-    case = ragged_case()
+def ou_ragged_model():
+    """A 2-D OU model with one noise (d = 2, m = 1) for the ragged case: its auxiliary law is
+    an OU law with Θ̃ = diag(0.7, 0.4) whatever the observation (G ≢ 0)."""
+    class _OU(OU):
+        def aux(self, v=None):
+            return OU.aux(self, Theta_t=np.diag([0.7, 0.4]))
+    return _OU([[1.0, 0.3], [-0.3, 0.8]], [0.1, -0.2], [[0.2], [0.5]])
+
+
+def ragged_pair(seed=11, hist_len=8, mapping=L.MAP_AUTO, model=None):
+    case = ragged_case(model=model)
     m = case["model"]
     dev = dmt.Ensemble(m.kind, m.d, m.m, case["n_points"], precision=case["prec"], seed=seed,
                        mapping=mapping)

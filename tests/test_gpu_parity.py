@@ -128,6 +128,121 @@ def test_ragged_blocking_layouts_bit_exact(mapping):
     assert dev.fetch_ll(A, 0, nA) == ora.fetch_ll(A, 0, nA)
 
 
+def test_ou_multichunk_bit_exact():
+    """Linear drift with segments longer than one 512-step scan chunk (1300 steps: two full
+    chunks and a partial one)."""
+    run_mcmc_parity(W.c2_ou2d(B=70, N=1300), iters=3, check_every=False)
+
+
+def test_ragged_ou_blocking_layouts_bit_exact():
+    """The ragged multi-segment case with a linear drift (2-D OU, one noise): scan kernels over
+    multi-segment blocks, P_last laws, two alternating layouts, sub-ranges."""
+    case, dev, ora, ((A, nA), (B, nB)) = cs.ragged_pair(model=cs.ou_ragged_model())
+    rng = np.random.default_rng(19)
+    S = case["t"].size - sum(case["nsegs"])
+    for i in range(1, 5):
+        for lay, nb in ((A, nA), (B, nB)):
+            Z = rng.standard_normal((S, 1))
+            E = rng.exponential(1.0, nb)
+            for e in (dev, ora):
+                e.loglikhd(lay, L.U, 0, nb)
+                e.draw_proposal(lay, 0, nb, Z=Z, iter=i)
+            assert np.array_equal(dev.accept_reject(lay, 0, nb, i, E=E, want_acc=True),
+                                  ora.accept_reject(lay, 0, nb, i, E=E, want_acc=True))
+            cs.assert_paths_equal(dev, ora)
+            cs.assert_ll_equal(dev, ora, lay, nb)
+    for e in (dev, ora):  # device RNG on a sub-range
+        e.draw_proposal(A, 2, 6, iter=5)
+    cs.assert_paths_equal(dev, ora)
+    cs.assert_ll_equal(dev, ora, A, nA)
+
+
+def _env_ensembles(build, env):
+    """Two identical ensembles, the second created under extra environment settings
+    (libdmt reads DMT_MCMC_* at dmt_create)."""
+    import os
+    out = []
+    for k in range(2):
+        saved = {v: os.environ.get(v) for v in env}
+        if k == 1:
+            os.environ.update(env)
+        try:
+            out.append(build())
+        finally:
+            for v, val in saved.items():
+                if val is None:
+                    os.environ.pop(v, None)
+                else:
+                    os.environ[v] = val
+    return out
+
+
+def _c2_build(B, N, hist):
+    import diffusionmcmctools_amd as d
+
+    def build():
+        w = W.c2_ou2d(B=B, N=N)
+        w.meta["hist_len"] = hist
+        e = d.Ensemble(w.model.kind, w.d, w.m, w.n_points, precision=w.precision, seed=29,
+                       grid_shared=w.grid_shared)
+        lay = W.fill(e, w)
+        e.loglikhd(lay, L.U, 0, B)
+        return e, lay, B
+    return build
+
+
+def _c1_build(hist):
+    import diffusionmcmctools_amd as d
+
+    def build():
+        w = W.c1_ou1d()
+        w.meta["hist_len"] = hist
+        e = d.Ensemble(w.model.kind, w.d, w.m, w.n_points, precision=w.precision, seed=31,
+                       grid_shared=w.grid_shared)
+        lay = W.fill(e, w)
+        e.loglikhd(lay, L.U, 0, 1)
+        return e, lay, 1
+    return build
+
+
+def _ragged_ou_build(hist):
+    def build():
+        _, dev, _, ((A, nA), _) = cs.ragged_pair(model=cs.ou_ragged_model(), hist_len=hist)
+        dev.loglikhd(A, L.U, 0, nA)
+        return dev, A, nA
+    return build
+
+
+@pytest.mark.parametrize("case", [
+    pytest.param(("c2", 100, 60, 6), id="c2-60steps-resident"),
+    pytest.param(("c2", 300, 500, 70), id="c2-500steps-resident-70iters"),
+    pytest.param(("c2", 40, 1300, 4), id="c2-1300steps-persistent-multichunk"),
+    pytest.param(("c1", 1, 200, 5), id="c1-resident-d1"),
+    pytest.param(("ragged", 0, 0, 5), id="ragged-ou-persistent-multisegment"),
+])
+def test_mcmc_run_persistent_paths_equal_step_path(case):
+    """dmt_mcmc_run through the persistent kernels (register-resident k_mcmc_resident for
+    single-segment blocks of ≤ 512 steps, k_mcmc_scan otherwise) == the per-iteration kernels
+    (DMT_MCMC_PERSIST=0), bit for bit: fetch_ll results, paths of u and u°, ll, ll°, histories."""
+    kind, B, N, n = case
+    build = (_c2_build(B, N, n + 1) if kind == "c2" else _c1_build(n + 1) if kind == "c1"
+             else _ragged_ou_build(n + 1))
+    (e0, lay, nb), (e1, _, _) = _env_ensembles(build, {"DMT_MCMC_PERSIST": "0"})
+    r0 = e0.mcmc_run(lay, 0, nb, 1, n, salt=7)
+    r1 = e1.mcmc_run(lay, 0, nb, 1, n, salt=7)
+    assert np.array_equal(r0, r1)
+    cs.assert_paths_equal(e0, e1)
+    for what in (L.BLK_LL, L.BLK_LLPROP):
+        assert np.array_equal(e0.get_block_state(lay, what, 0, nb), e1.get_block_state(lay, what, 0, nb))
+    for what in (L.BLK_ACC_HIST, L.BLK_LL_HIST, L.BLK_LLPROP_HIST):
+        assert np.array_equal(e0.get_block_state(lay, what, 0, nb, n + 1),
+                              e1.get_block_state(lay, what, 0, nb, n + 1))
+    # a second run continues from the state the first one left (selectors, ll on the device)
+    assert np.array_equal(e0.mcmc_run(lay, 0, nb, n + 1, 1, salt=7),
+                          e1.mcmc_run(lay, 0, nb, n + 1, 1, salt=7))
+    cs.assert_paths_equal(e0, e1)
+
+
 @pytest.mark.parametrize("mapping", MAPPINGS)
 def test_fetch_ll_tree_bit_exact(mapping):
     w = W.c2_ou2d(B=64 * 80, N=8)
