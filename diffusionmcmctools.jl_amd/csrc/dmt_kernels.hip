@@ -746,6 +746,28 @@ struct SelMask {
   __device__ __forceinline__ int w(int g) const { return (int)((mw >> (g - g0)) & 1u); }
 };
 
+// A value every lane of the wave holds (the compiler cannot always prove it): lane 0's copy
+// in SGPRs, so that branches, selectors and pointers derived from it stay scalar.
+__device__ __forceinline__ double wave_uniform(double v) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ float wave_uniform(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, v)));
+}
+// lane `l`'s value (l wave-uniform), in SGPRs
+__device__ __forceinline__ double lane_value(double v, int l) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)u, l);
+  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(u >> 32), l);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ float lane_value(float v, int l) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(uint32_t, v), l));
+}
+
 __device__ __forceinline__ void wave_lds_sync() {
   // LDS accesses of one wave are performed in order; this only keeps the compiler from moving
   // an access across the phase boundary (other lanes' data)
@@ -785,7 +807,7 @@ __device__ __forceinline__ void scan_block(const BlockArgs<T>& a, const int64_t 
     const int64_t q = bq0;
     T H0[HP], F0[D];
 #pragma unroll
-    for (int p = 0; p < D; ++p) xc[p] = Xs[(tq + q) * D + p];
+    for (int p = 0; p < D; ++p) xc[p] = wave_uniform(Xs[(tq + q) * D + p]);
 #pragma unroll
     for (int c = 0; c < HP; ++c)
       H0[c] = a.H_shared[lsp][0] ? a.H[lsp][0][q * HP + c] : a.H[lsp][0][(tq + q) * HP + c];
@@ -893,15 +915,17 @@ __device__ __forceinline__ void scan_block(const BlockArgs<T>& a, const int64_t 
       for (int c = 0; c < D * D; ++c) RA[c] = A8[0][c];
 #pragma unroll
       for (int c = 0; c < D; ++c) Re[c] = e8[0][c];
+      // run map = step_7 ∘ … ∘ step_0; identity maps past the segment end (exact for finite
+      // maps; only the lane holding the last step has any, and its run map feeds only the
+      // prefixes of lanes with no valid step, so no stored value depends on them)
 #pragma unroll
-      for (int r = 1; r < kRun; ++r) {  // run map = step_{nv-1} ∘ … ∘ step_0
+      for (int r = 1; r < kRun; ++r) {
         T An[D * D], en[D];
         affine_compose<D, T>(A8[r], e8[r], RA, Re, An, en);
-        const bool take = r < nv;
 #pragma unroll
-        for (int c = 0; c < D * D; ++c) RA[c] = take ? An[c] : RA[c];
+        for (int c = 0; c < D * D; ++c) RA[c] = An[c];
 #pragma unroll
-        for (int c = 0; c < D; ++c) Re[c] = take ? en[c] : Re[c];
+        for (int c = 0; c < D; ++c) Re[c] = en[c];
       }
       // inclusive Kogge–Stone scan over the lanes: lane j ← run_j ∘ … ∘ run_0
 #pragma unroll
@@ -974,13 +998,13 @@ __device__ __forceinline__ void scan_block(const BlockArgs<T>& a, const int64_t 
           }
           T rr[D], bb[D];
           const T G = g_at<Mdl, T>(LA, Hi, Fi, xpre, rr, bb);
-          const T csum = wave_tree_sum<T>(v ? G * dt : (T)0);
+          const T csum = wave_uniform(wave_tree_sum<T>(v ? G * dt : (T)0));
           seg_acc = seg_acc + (csum + (T)0);
           if (v) store_row<D, T>(Xdb + (int64_t)(c0 + s) * D, xpre);
         }
       }
 #pragma unroll
-      for (int p = 0; p < D; ++p) xc[p] = S.pt[p][lds_ix(cnt)];
+      for (int p = 0; p < D; ++p) xc[p] = wave_uniform(S.pt[p][lds_ix(cnt)]);
       wave_lds_sync();
     }
     if (lane == 0) store_row<D, T>(Xdb + (int64_t)nst * D, xc);
@@ -1035,7 +1059,7 @@ __global__ __launch_bounds__((64 * ScanCfg<Mdl::D, T>::WPB), 1) void k_mcmc_scan
   SelMask sel{__ballot(own && a.selX[g0 + (own ? lane : 0)] != 0),
               __ballot(own && a.selW[g0 + (own ? lane : 0)] != 0), g0};
   const uint64_t all = nseg >= 64 ? ~(uint64_t)0 : (((uint64_t)1 << nseg) - 1);
-  double ll = c.ll[blk], llp = 0.0;
+  double ll = wave_uniform(c.ll[blk]), llp = 0.0;
   const int64_t nb = a.b1 - a.b0, j = blk - a.b0;
   for (int64_t r = 0; r < n_iter; ++r) {
     const int64_t it = iter0 + r;
@@ -1079,6 +1103,7 @@ __global__ __launch_bounds__((64 * ScanCfg<Mdl::D, T>::WPB), 1) void k_mcmc_scan
     c.llp[blk] = llp;
   }
 }
+
 
 // dmt_mcmc_run for linear drifts whose blocks are ONE segment of at most kSChunk steps (e.g.
 // C2): the same canonical arithmetic as scan_block, but the block's per-step constants stay
@@ -1131,6 +1156,8 @@ __global__ __launch_bounds__(256, 1) void k_mcmc_resident(const BlockArgs<T> a,
   const T* Hb = a.H_shared[ls][kind] ? a.H[ls][kind] + (int64_t)q0 * HP : a.H[ls][kind] + row * HP;
   const T* Fb = a.F[ls][kind] + row * D;
   SelMask sel{(uint64_t)(a.selX[g] & 1), (uint64_t)(a.selW[g] & 1), g};
+  T* const Xd[2] = {a.X[0] + row * D, a.X[1] + row * D};
+  T* const Wd[2] = {a.W[0] + row * M, a.W[1] + row * M};
   // ---- per-launch state: start point, loglikhd_obs, per-step constants (run order)
   T x0[D], w0[M], llobs;
   {
@@ -1184,8 +1211,8 @@ __global__ __launch_bounds__(256, 1) void k_mcmc_resident(const BlockArgs<T> a,
                      (int)(__builtin_bit_cast(uint64_t, Ev) >> 32), (int)(r0 & 63)) << 32) |
                     (uint32_t)__builtin_amdgcn_readlane((int)__builtin_bit_cast(uint64_t, Ev),
                                                         (int)(r0 & 63)));
-    T* const Xdb = a.X[sel.x(g) ^ a.xd_flip] + row * D;
-    T* const Wdb = a.W[sel.w(g) ^ a.wd_flip] + row * M;
+    T* const Xdb = (sel.x(g) ^ a.xd_flip) ? Xd[1] : Xd[0];
+    T* const Wdb = (sel.w(g) ^ a.wd_flip) ? Wd[1] : Wd[0];
     // ---- normals, pCN increments, e maps; run map
     T dW[kRun][M], e[kRun][D];
 #pragma unroll
@@ -1211,18 +1238,19 @@ __global__ __launch_bounds__(256, 1) void k_mcmc_resident(const BlockArgs<T> a,
     }
     T RA[D * D], Re[D];
 #pragma unroll
-    for (int cc = 0; cc < D * D; ++cc) RA[cc] = nv > 0 ? Ac[0][cc] : (cc % (D + 1) == 0 ? (T)1 : (T)0);
+    for (int cc = 0; cc < D * D; ++cc) RA[cc] = Ac[0][cc];
 #pragma unroll
-    for (int p = 0; p < D; ++p) Re[p] = nv > 0 ? e[0][p] : (T)0;
+    for (int p = 0; p < D; ++p) Re[p] = e[0][p];
+    // steps past the segment end are composed too: only the lane holding the segment's last
+    // step has any, and its run map feeds only the prefixes of lanes with no valid step
 #pragma unroll
     for (int r = 1; r < kRun; ++r) {
       T An[D * D], en[D];
       affine_compose<D, T>(Ac[r], e[r], RA, Re, An, en);
-      const bool take = r < nv;
 #pragma unroll
-      for (int cc = 0; cc < D * D; ++cc) RA[cc] = take ? An[cc] : RA[cc];
+      for (int cc = 0; cc < D * D; ++cc) RA[cc] = An[cc];
 #pragma unroll
-      for (int p = 0; p < D; ++p) Re[p] = take ? en[p] : Re[p];
+      for (int p = 0; p < D; ++p) Re[p] = en[p];
     }
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -1356,16 +1384,28 @@ __global__ __launch_bounds__(256) void k_tree_batched(const double* __restrict__
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int64_t r = blockIdx.x;
   double v[3];
+  // binary-counter fold of the thread's aligned run of leaves (register stack: selects on the
+  // counter bits, no dynamic indexing, which would go through scratch memory)
+  constexpr int kLv = 24;  // run ≤ 2^24 leaves per thread
   for (int q = 0; q < 3; ++q) {
     const double* row = part + (3 * r + q) * nb;
-    double stk[40];
+    double stk[kLv];
+#pragma unroll
+    for (int l = 0; l < kLv; ++l) stk[l] = 0.0;
     double acc = 0.0;
     for (int64_t k = 0; k < run; ++k) {
       const int64_t leaf = (int64_t)tid * run + k;
       double x = leaf < nb ? row[leaf] : 0.0;
-      int l = 0;
-      for (int64_t m = k; m & 1; m >>= 1, ++l) x = stk[l] + x;
-      stk[l] = x;
+      bool carry = true;
+#pragma unroll
+      for (int l = 0; l < kLv; ++l) {
+        const bool bit = (k >> l) & 1;
+        const double y = stk[l] + x;
+        const bool add = carry && bit;
+        stk[l] = (carry && !bit) ? x : stk[l];
+        carry = add;
+        x = add ? y : x;
+      }
       acc = x;
     }
     v[q] = acc;
