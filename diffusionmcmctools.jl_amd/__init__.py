@@ -12,10 +12,10 @@ contains a dot).
 """
 from . import _lib  # noqa: F401  (raises ImportError if libdmt.so is missing)
 from ._lib import DMTError, version  # noqa: F401
-from .engine import Ensemble, comm_unique_id, guiding_linear  # noqa: F401
+from .engine import Ensemble, comm_unique_id, guiding_linear, read_snapshots  # noqa: F401
 from .api import (BiBlock, BlockCollection, BlockEnsemble, SamplingEnsemble,  # noqa: F401
                   SamplingPair, SamplingUnit)
 
-__all__ = ["Ensemble", "DMTError", "version", "comm_unique_id", "guiding_linear",
+__all__ = ["Ensemble", "DMTError", "version", "comm_unique_id", "guiding_linear", "read_snapshots",
            "SamplingEnsemble", "SamplingPair", "SamplingUnit", "BlockEnsemble",
            "BlockCollection", "BiBlock"]

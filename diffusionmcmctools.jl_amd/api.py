@@ -82,6 +82,36 @@ class SamplingEnsemble:
                            W=self.ens.download_paths(L.U, 1))
         return ll, ok
 
+    # ---- path snapshots: the tutorials' `append!(paths, [deepcopy(rec.u.XX) for rec in
+    # se.recordings])` (docs/src/tutorials/block_ensemble/inference.md:124), kept in HBM
+    def reserve_snapshots(self, n_slots, XX=True, WW=False):
+        self.ens.snapshot_reserve(n_slots, (1 if XX else 0) | (2 if WW else 0))
+
+    def snapshot_paths(self, slot, mcmciter=0, unit=L.U):
+        """deepcopy of every recording's ``unit.XX`` (and ``WW`` if reserved) into ``slot``."""
+        self.ens.snapshot_take(slot, mcmciter, unit)
+
+    def snapshot(self, slot, what=0):
+        """Slot contents as the reference holds them: per recording, the list of per-segment
+        paths (``Vector{Trajectory}`` x arrays), and the slot's MCMC iteration."""
+        A, it = self.ens.snapshot_download(slot, what)
+        out, p = [], 0
+        for r in self.n_points:
+            segs = []
+            for n in r:
+                segs.append(A[p:p + n])
+                p += n
+            out.append(segs)
+        return out, it
+
+    def write_snapshots(self, path, s0=0, s1=None):
+        """Stream slots [s0, s1) to ``path`` (DMTPATH1 format, include/dmt.h); read back with
+        :func:`diffusionmcmctools_amd.read_snapshots`."""
+        self.ens.snapshot_write(path, s0, self.ens_slots() if s1 is None else s1)
+
+    def ens_slots(self):
+        return getattr(self.ens, "_snap_slots", 0)
+
     def close(self):
         self.ens.close()
 

@@ -91,6 +91,11 @@ struct dmt_ens {
   uint64_t seed = 0;
   uint32_t seg_base = 0;  // dmt_set_shard
   int grid_shared = 0;
+  // path snapshots (dmt_snapshot_*): [slots][P][C] doubles in reference layout per kind
+  int snap_mask = 0;
+  int64_t snap_slots = 0;
+  double* d_snap[2] = {nullptr, nullptr};
+  std::vector<int64_t> snap_iter, snap_unit;
   int mapping = MAP_LANE;  // thread mapping of the recursion kernels
   int tw = kLanes;         // tile width of the device layout (64 lane-mapped, 1 wave-mapped)
   hipStream_t stream = nullptr;
@@ -669,6 +674,8 @@ dmt_status dmt_destroy(dmt_ens* h) {
       if (h->d_F[s][k]) (void)hipFree(h->d_F[s][k]);
       if (h->d_law[s][k]) (void)hipFree(h->d_law[s][k]);
     }
+  for (int k = 0; k < 2; ++k)
+    if (h->d_snap[k]) (void)hipFree(h->d_snap[k]);
   if (h->comm) (void)ncclCommDestroy(h->comm);
   if (h->h_red) (void)hipHostFree(h->h_red);
   (void)hipStreamDestroy(h->stream);
@@ -1650,6 +1657,177 @@ dmt_status dmt_debug_normals(int32_t device, uint64_t seed, const uint32_t* ctr,
   HIP_OK(launch_debug_philox(seed, dc, n, dout, dn, nullptr));
   HIP_OK(hipMemcpy(out, dn, n * 16, hipMemcpyDeviceToHost));
   (void)hipFree(dc); (void)hipFree(dout); (void)hipFree(dn);
+  return DMT_OK;
+}
+
+
+// ---------------------------------------------------------------- path snapshots (§8(f) rank 4)
+// The tutorials keep every k-th accepted path, `append!(paths, [deepcopy(bb.b.XX)])`
+// (docs/src/tutorials/biblock/smoothing.md:55, block_ensemble/inference.md:124).  Here the
+// copies stay in HBM (a ring of slots, reference layout, fp64), are taken on the handle's
+// stream without a host round trip, and are written to disk in one pass when wanted.
+
+dmt_status dmt_snapshot_reserve(dmt_ens* h, int32_t what_mask, int64_t n_slots) {
+  DMT_TRY(check_h(h));
+  if (what_mask < 1 || what_mask > 3 || n_slots < 1)
+    return fail(DMT_ERR_INVALID, "what_mask must be 1 (XX), 2 (WW) or 3, n_slots >= 1");
+  HIP_OK(hipStreamSynchronize(h->stream));
+  const int C[2] = {h->d, h->m};
+  for (int k = 0; k < 2; ++k) {
+    if (h->d_snap[k]) {
+      (void)hipFree(h->d_snap[k]);
+      h->bytes -= h->snap_slots * h->P * C[k] * 8;
+      h->d_snap[k] = nullptr;
+    }
+  }
+  h->snap_mask = 0;
+  h->snap_slots = 0;
+  for (int k = 0; k < 2; ++k)
+    if (what_mask >> k & 1) DMT_TRY(ens_alloc(h, &h->d_snap[k], n_slots * h->P * C[k]));
+  h->snap_mask = what_mask;
+  h->snap_slots = n_slots;
+  h->snap_iter.assign(n_slots, -1);
+  h->snap_unit.assign(n_slots, -1);
+  return DMT_OK;
+}
+
+dmt_status dmt_snapshot_take(dmt_ens* h, int32_t unit, int64_t slot, int64_t mcmciter) {
+  DMT_TRY(check_h(h));
+  if (unit != DMT_U && unit != DMT_UPROP) return fail(DMT_ERR_INVALID, "bad unit");
+  if (!h->snap_mask) return fail(DMT_ERR_STATE, "no snapshot slots (dmt_snapshot_reserve)");
+  if (slot < 0 || slot >= h->snap_slots) return fail(DMT_ERR_INVALID, "slot out of range");
+  for (int k = 0; k < 2; ++k) {
+    if (!(h->snap_mask >> k & 1)) continue;
+    const int C = k == 0 ? h->d : h->m;
+    double* dst = h->d_snap[k] + slot * h->P * C;
+    void** src = k == 0 ? h->d_X : h->d_W;
+    if (k == 0)
+      HIP_OK(launch_from_planes(h->key.precision, h->tw, dst, src[0], src[1], h->d_sel[0], unit, C,
+                                h->P, h->d_pt_off, h->G, h->d_seg_rec, h->d_seg_q, h->d_tile_qoff,
+                                h->stream));
+    else  // increments -> cumulative Wiener path, as dmt_download_paths
+      HIP_OK(launch_from_planes_incr(h->key.precision, h->tw, dst, src[0], src[1], h->d_sel[1], unit,
+                                     C, h->G, h->d_pt_off, h->d_seg_np, h->d_seg_rec, h->d_seg_q,
+                                     h->d_tile_qoff, h->stream));
+  }
+  h->snap_iter[slot] = mcmciter;
+  h->snap_unit[slot] = unit;
+  return DMT_OK;
+}
+
+dmt_status dmt_snapshot_download(dmt_ens* h, int32_t what, int64_t slot, double* out,
+                                 int64_t* mcmciter) {
+  DMT_TRY(check_h(h));
+  if ((what != 0 && what != 1) || !out) return fail(DMT_ERR_INVALID, "bad what/out");
+  if (!(h->snap_mask >> what & 1)) return fail(DMT_ERR_STATE, "that path kind is not snapshotted");
+  if (slot < 0 || slot >= h->snap_slots) return fail(DMT_ERR_INVALID, "slot out of range");
+  const int C = what == 0 ? h->d : h->m;
+  HIP_OK(hipMemcpyAsync(out, h->d_snap[what] + slot * h->P * C, h->P * C * 8,
+                        hipMemcpyDeviceToHost, h->stream));
+  HIP_OK(hipStreamSynchronize(h->stream));
+  if (mcmciter) *mcmciter = h->snap_iter[slot];
+  return DMT_OK;
+}
+
+dmt_status dmt_snapshot_write(dmt_ens* h, const char* path, int64_t s0, int64_t s1) {
+  DMT_TRY(check_h(h));
+  if (!path) return fail(DMT_ERR_INVALID, "null path");
+  if (!h->snap_mask) return fail(DMT_ERR_STATE, "no snapshot slots (dmt_snapshot_reserve)");
+  if (s0 < 0 || s1 > h->snap_slots || s0 > s1) return fail(DMT_ERR_INVALID, "bad slot range");
+  if (!h->have_t) return fail(DMT_ERR_STATE, "time grid not uploaded");
+  // the grid in reference layout (one recording's points when shared)
+  const int64_t nt = h->grid_shared ? h->Q0 : h->P;
+  std::vector<double> t(nt);
+  DMT_TRY(ensure_stage(h, nt));
+  if (h->grid_shared)
+    HIP_OK(launch_cast_back(h->key.precision, h->d_t, h->d_stage, nt, h->stream));
+  else
+    HIP_OK(launch_from_planes(h->key.precision, h->tw, h->d_stage, h->d_t, h->d_t, h->d_sel[0], 0,
+                              1, h->P, h->d_pt_off, h->G, h->d_seg_rec, h->d_seg_q, h->d_tile_qoff,
+                              h->stream));
+  HIP_OK(hipMemcpyAsync(t.data(), h->d_stage, nt * 8, hipMemcpyDeviceToHost, h->stream));
+  HIP_OK(hipStreamSynchronize(h->stream));
+  std::FILE* f = std::fopen(path, "wb");
+  if (!f) return fail(DMT_ERR_INVALID, std::string("cannot open ") + path);
+  dmt_snapshot_header hd{};
+  std::memcpy(hd.magic, "DMTPATH1", 8);
+  hd.version = 1;
+  hd.what_mask = (uint32_t)h->snap_mask;
+  hd.d = h->d;
+  hd.m = h->m;
+  hd.grid_shared = h->grid_shared;
+  hd.precision = h->key.precision;
+  hd.n_recordings = h->R;
+  hd.n_segments = h->G;
+  hd.n_points = h->P;
+  hd.n_t = nt;
+  hd.n_slots = s1 - s0;
+  hd.seg_base = h->seg_base;
+  std::vector<int32_t> nseg(h->R);
+  for (int64_t r = 0; r < h->R; ++r) nseg[r] = (int32_t)(h->rec_seg0[r + 1] - h->rec_seg0[r]);
+  bool ok = std::fwrite(&hd, sizeof hd, 1, f) == 1 &&
+            std::fwrite(nseg.data(), 4, h->R, f) == (size_t)h->R &&
+            std::fwrite(h->seg_np.data(), 4, h->G, f) == (size_t)h->G &&
+            std::fwrite(t.data(), 8, nt, f) == (size_t)nt;
+  // slots stream through two pinned buffers: the copy of piece k+1 overlaps the write of piece k
+  const int64_t piece = std::min<int64_t>(int64_t(8) << 20, std::max<int64_t>(h->P * 3, 1));  // doubles
+  double* pin[2] = {nullptr, nullptr};
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  for (int b = 0; b < 2 && ok; ++b) {
+    ok = hipHostMalloc((void**)&pin[b], piece * 8, hipHostMallocDefault) == hipSuccess &&
+         hipEventCreateWithFlags(&ev[b], hipEventDisableTiming) == hipSuccess;
+  }
+  struct Src { const double* p; int64_t n; };
+  std::vector<Src> pieces;
+  for (int64_t s = s0; s < s1 && ok; ++s) {
+    for (int k = 0; k < 2; ++k) {
+      if (!(h->snap_mask >> k & 1)) continue;
+      const int64_t n = h->P * (k == 0 ? h->d : h->m);
+      const double* base = h->d_snap[k] + s * n;
+      for (int64_t o = 0; o < n; o += piece) pieces.push_back({base + o, std::min(piece, n - o)});
+    }
+  }
+  // per slot: int64 mcmciter, int64 unit, then X (and/or W); the 16-byte slot header is
+  // written before the slot's first piece
+  std::vector<int64_t> first_piece_of_slot;
+  {
+    int64_t k = 0;
+    for (int64_t s = s0; s < s1; ++s) {
+      first_piece_of_slot.push_back(k);
+      for (int kk = 0; kk < 2; ++kk)
+        if (h->snap_mask >> kk & 1) {
+          const int64_t n = h->P * (kk == 0 ? h->d : h->m);
+          k += (n + piece - 1) / piece;
+        }
+    }
+  }
+  auto issue = [&](size_t k) -> bool {
+    const int b = (int)(k & 1);
+    return hipMemcpyAsync(pin[b], pieces[k].p, pieces[k].n * 8, hipMemcpyDeviceToHost, h->stream) ==
+               hipSuccess &&
+           hipEventRecord(ev[b], h->stream) == hipSuccess;
+  };
+  if (ok && !pieces.empty()) ok = issue(0);
+  size_t slot_i = 0;
+  for (size_t k = 0; k < pieces.size() && ok; ++k) {
+    const int b = (int)(k & 1);
+    ok = hipEventSynchronize(ev[b]) == hipSuccess;
+    if (ok && k + 1 < pieces.size()) ok = issue(k + 1);
+    if (ok && slot_i < first_piece_of_slot.size() && (int64_t)k == first_piece_of_slot[slot_i]) {
+      const int64_t s = s0 + (int64_t)slot_i;
+      const int64_t sh[2] = {h->snap_iter[s], h->snap_unit[s]};
+      ok = std::fwrite(sh, 8, 2, f) == 2;
+      ++slot_i;
+    }
+    if (ok) ok = std::fwrite(pin[b], 8, pieces[k].n, f) == (size_t)pieces[k].n;
+  }
+  (void)hipStreamSynchronize(h->stream);
+  for (int b = 0; b < 2; ++b) {
+    if (pin[b]) (void)hipHostFree(pin[b]);
+    if (ev[b]) (void)hipEventDestroy(ev[b]);
+  }
+  if (std::fclose(f) != 0) ok = false;
+  if (!ok) return fail(DMT_ERR_HIP, std::string("writing ") + path + " failed");
   return DMT_OK;
 }
 

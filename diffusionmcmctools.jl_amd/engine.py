@@ -98,6 +98,26 @@ class Ensemble:
     def XX(self, unit=L.U):
         return self.download_paths(unit, 0)
 
+    # ---------------------------------------------------------------- path snapshots
+    def snapshot_reserve(self, n_slots, what_mask=1):
+        """HBM ring of n_slots path copies: what_mask 1 = XX, 2 = WW, 3 = both."""
+        L.call("dmt_snapshot_reserve", self._h, int(what_mask), int(n_slots))
+        self._snap_slots = int(n_slots)
+
+    def snapshot_take(self, slot, mcmciter=0, unit=L.U):
+        """deepcopy(unit.XX) (docs/src/tutorials/biblock/smoothing.md:55), on the device."""
+        L.call("dmt_snapshot_take", self._h, int(unit), int(slot), int(mcmciter))
+
+    def snapshot_download(self, slot, what=0):
+        C_ = self.d if what == 0 else self.m
+        out = np.empty((self.P, C_), dtype=np.float64)
+        it = C.c_int64()
+        L.call("dmt_snapshot_download", self._h, int(what), int(slot), L.f64p(out), C.byref(it))
+        return out, it.value
+
+    def snapshot_write(self, path, s0, s1):
+        L.call("dmt_snapshot_write", self._h, str(path).encode(), int(s0), int(s1))
+
     def WW(self, unit=L.U):
         return self.download_paths(unit, 1)
 
@@ -314,3 +334,52 @@ def debug_normals(seed, ctr, device=0):
     out = np.empty((ctr.shape[0], 2), dtype=np.float64)
     L.call("dmt_debug_normals", device, int(seed), L.u32p(ctr), ctr.shape[0], L.f64p(out))
     return out
+
+
+# ---------------------------------------------------------------- snapshot files
+SNAPSHOT_HEADER = np.dtype([("magic", "S8"), ("version", "<u4"), ("what_mask", "<u4"),
+                            ("d", "<i4"), ("m", "<i4"), ("grid_shared", "<i4"),
+                            ("precision", "<i4"), ("n_recordings", "<i8"), ("n_segments", "<i8"),
+                            ("n_points", "<i8"), ("n_t", "<i8"), ("n_slots", "<i8"),
+                            ("seg_base", "<i8")])
+
+
+def read_snapshots(path, mmap=True):
+    """Reads a dmt_snapshot_write file (layout: include/dmt.h, dmt_snapshot_header).  Returns a
+    dict: header fields, ``n_points`` (per recording, per segment), ``t``, ``mcmciter`` and
+    ``unit`` per slot, ``X`` [slots][P][d] and/or ``W`` [slots][P][m] (memory-mapped), and
+    ``paths(slot, r)`` = recording r's XX as a list of per-segment [npts][d] arrays (the
+    reference's ``Vector{Trajectory}``)."""
+    hd = np.fromfile(path, dtype=SNAPSHOT_HEADER, count=1)[0]
+    if hd["magic"] != b"DMTPATH1" or hd["version"] != 1:
+        raise ValueError(f"{path}: not a DMTPATH1 snapshot file")
+    R, G, P, nt, ns = (int(hd[k]) for k in ("n_recordings", "n_segments", "n_points", "n_t", "n_slots"))
+    d, m, mask = int(hd["d"]), int(hd["m"]), int(hd["what_mask"])
+    off = SNAPSHOT_HEADER.itemsize
+    nseg = np.fromfile(path, dtype="<i4", count=R, offset=off); off += 4 * R
+    npts = np.fromfile(path, dtype="<i4", count=G, offset=off); off += 4 * G
+    t = np.fromfile(path, dtype="<f8", count=nt, offset=off); off += 8 * nt
+    per = (P * d if mask & 1 else 0) + (P * m if mask & 2 else 0)
+    rec = np.dtype([("mcmciter", "<i8"), ("unit", "<i8"), ("paths", "<f8", (per,))])
+    slots = (np.memmap(path, dtype=rec, mode="r", offset=off, shape=(ns,)) if mmap and ns
+             else np.fromfile(path, dtype=rec, count=ns, offset=off))
+    out = {k: hd[k].item() for k in SNAPSHOT_HEADER.names if k != "magic"}
+    seg0 = np.concatenate([[0], np.cumsum(nseg)])
+    out["n_points"] = [npts[seg0[r]:seg0[r + 1]].tolist() for r in range(R)]
+    out["t"] = t
+    out["mcmciter"] = np.asarray(slots["mcmciter"])
+    out["unit"] = np.asarray(slots["unit"])
+    body = slots["paths"]
+    if mask & 1:
+        out["X"] = body[:, : P * d].reshape(ns, P, d)
+    if mask & 2:
+        o = P * d if mask & 1 else 0
+        out["W"] = body[:, o: o + P * m].reshape(ns, P, m)
+    pt0 = np.concatenate([[0], np.cumsum(npts)])
+
+    def paths(slot, r, what="X"):
+        A = out[what][slot]
+        return [A[pt0[g]:pt0[g + 1]] for g in range(seg0[r], seg0[r + 1])]
+    out["paths"] = paths
+    return out
+

@@ -133,6 +133,26 @@ end
 download_XX(se::DeviceSamplingEnsemble, unit=DMT_U) = _download(se, unit, 0, se.d)
 download_WW(se::DeviceSamplingEnsemble, unit=DMT_U) = _download(se, unit, 1, se.m)
 
+# ---- path snapshots: `append!(paths, [deepcopy(bb.b.XX)])` (docs/src/tutorials/biblock/
+# smoothing.md:55) without leaving the GPU; slots are 0-based, what_mask 1 = XX, 2 = WW, 3 = both
+reserve_snapshots!(se::DeviceSamplingEnsemble, n_slots; what_mask=1) =
+    check(ccall((:dmt_snapshot_reserve, libdmt), Int32, (Ptr{Cvoid}, Int32, Int64),
+                se.h, what_mask, n_slots))
+snapshot!(se::DeviceSamplingEnsemble, slot, mcmciter; unit=DMT_U) =
+    check(ccall((:dmt_snapshot_take, libdmt), Int32, (Ptr{Cvoid}, Int32, Int64, Int64),
+                se.h, unit, slot, mcmciter))
+function snapshot(se::DeviceSamplingEnsemble, slot; what=0)
+    C = what == 0 ? se.d : se.m
+    out = Vector{Float64}(undef, se.P * C)
+    it = Ref{Int64}(0)
+    check(ccall((:dmt_snapshot_download, libdmt), Int32,
+                (Ptr{Cvoid}, Int32, Int64, Ptr{Float64}, Ref{Int64}), se.h, what, slot, out, it))
+    collect(reinterpret(SVector{C,Float64}, out)), it[]
+end
+write_snapshots(se::DeviceSamplingEnsemble, path::AbstractString, s0, s1) =
+    check(ccall((:dmt_snapshot_write, libdmt), Int32, (Ptr{Cvoid}, Cstring, Int64, Int64),
+                se.h, path, s0, s1))
+
 "draw_proposal_path!(u::SamplingUnit) for recordings r0+1:r1 (src/sampling_unit.jl:118)."
 function draw_unit!(se::DeviceSamplingEnsemble, unit, r0, r1; Z=nothing, iter=0, salt=0)
     ll = Vector{Float64}(undef, r1 - r0)

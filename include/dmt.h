@@ -327,6 +327,35 @@ dmt_status dmt_comm_init(dmt_ens* h, int32_t nranks, int32_t rank, const uint8_t
  * No reference counterpart (the reference is single-process). */
 dmt_status dmt_set_shard(dmt_ens* h, int64_t seg_base);
 
+/* ---------------- path snapshots ----------------
+ * The reference's callers keep every k-th accepted path, `append!(paths, [deepcopy(bb.b.XX)])`
+ * (docs/src/tutorials/biblock/smoothing.md:55; per recording, block_ensemble/inference.md:124).
+ * Snapshots are kept in HBM: a ring of n_slots copies of XX (what_mask bit 0) and/or WW
+ * (bit 1, cumulative Wiener paths) of one unit, reference layout, fp64, taken on the handle's
+ * stream without a host round trip (a C3-sized XX snapshot is 1.05 GB; 288 GB of HBM holds
+ * a whole smoothing run's worth).  dmt_snapshot_write streams slots [s0, s1) to a file:
+ *   dmt_snapshot_header, int32 n_segments[n_recordings], int32 n_points[n_segments],
+ *   double t[n_t] (n_t = points of one recording when grid_shared, else n_points total),
+ *   then per slot: int64 mcmciter, int64 unit, [double X[P][d]], [double W[P][m]]
+ * (little-endian; P = Σ n_points; segments recording-major, as every host array here). */
+typedef struct {
+    char magic[8];          /* "DMTPATH1" */
+    uint32_t version;       /* 1 */
+    uint32_t what_mask;     /* 1 XX, 2 WW, 3 both */
+    int32_t d, m;
+    int32_t grid_shared;
+    int32_t precision;      /* of the ensemble the paths come from (DMT_F64 / DMT_F32) */
+    int64_t n_recordings, n_segments, n_points, n_t, n_slots;
+    int64_t seg_base;       /* global id of local segment 0 (dmt_set_shard) */
+} dmt_snapshot_header;
+
+dmt_status dmt_snapshot_reserve(dmt_ens* h, int32_t what_mask, int64_t n_slots);
+/* deepcopy(unit.XX / unit.WW) into slot (after every queued kernel), tagged with mcmciter */
+dmt_status dmt_snapshot_take(dmt_ens* h, int32_t unit, int64_t slot, int64_t mcmciter);
+dmt_status dmt_snapshot_download(dmt_ens* h, int32_t what, int64_t slot, double* out,
+                                 int64_t* mcmciter);
+dmt_status dmt_snapshot_write(dmt_ens* h, const char* path, int64_t s0, int64_t s1);
+
 /* ---------------- misc ---------------- */
 dmt_status dmt_sync(dmt_ens* h);
 /* Kernel timing with HIP events on the handle's stream: bit k of `mask` times the kernels of
