@@ -84,6 +84,9 @@ struct BlockArgs {
   uint32_t seg_base;  // global id of local segment 0 (RNG streams; dmt_set_shard)
   double* ll_out;     // [nblocks]
   uint8_t* success;   // [nblocks] or nullptr
+  int repair_div;     // MAP_LANE tile-phase repair while the minority is <= 1/repair_div
+  int lane_split;     // MAP_LANE draws: producer/consumer waves (k_block_ps); the runtime sets
+                      // it only for layouts of single-segment blocks
 };
 
 struct AcceptArgs {

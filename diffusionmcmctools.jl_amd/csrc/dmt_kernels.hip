@@ -219,8 +219,8 @@ __device__ __forceinline__ bool map_block(const BlockArgs<T>& a, int64_t& tile, 
   return true;
 }
 
-// tile-phase repair only while the minority is at most 1/kRepairMaxMinority of the wave
-constexpr int kRepairMaxMinority = 4;
+// tile-phase repair only while the minority is at most 1/repair_div of the wave
+// (BlockArgs::repair_div; 4 by default, DMT_REPAIR_DIV)
 
 template <class Mdl, class T, int MODE, bool PARITY, int K>
 __global__ __launch_bounds__(64) void k_block(const BlockArgs<T> a) {
@@ -283,11 +283,11 @@ __global__ __launch_bounds__(64) void k_block(const BlockArgs<T> a) {
       const int ox = __popcll(__ballot(sx != 0)), ow = __popcll(__ballot(sw != 0));
       const int px = 2 * ox > nact ? 1 : 0, pw = 2 * ow > nact ? 1 : 0;
       const int mx = px ? nact - ox : ox, mw = pw ? nact - ow : ow;  // minority sizes
-      if (kRepairMaxMinority * mx <= nact) {
+      if (a.repair_div * mx <= nact) {
         Xd = a.X[px ^ a.xd_flip];
         if (sx != px) { Xcs = a.X[sx ^ a.xs_flip]; Xcd = a.X[px ^ a.xs_flip]; nsx = px; }
       }
-      if (kRepairMaxMinority * mw <= nact) {
+      if (a.repair_div * mw <= nact) {
         Wd = a.W[pw ^ a.wd_flip];
         if (sw != pw) { Wcd = a.W[pw ^ a.ws_flip]; nsw = pw; }
       }
@@ -305,6 +305,255 @@ __global__ __launch_bounds__(64) void k_block(const BlockArgs<T> a) {
   }
   a.ll_out[blk] = ok ? (double)ll : -INFINITY;
   if (a.success) a.success[blk] = ok ? 1 : 0;
+}
+
+// ---- MAP_LANE, split into a producer and a consumer wave.  For draws
+// (MODE_PCN, device RNG) over single-segment blocks.  One workgroup of two waves per
+// (recording tile, block index): the PRODUCER wave loads t and u's W, draws the normals
+// (Philox/Box–Muller), forms dW° = fma(ρ, dW, √(1−ρ²)·√dt·Z), stores W° and hands (dt, dW°)
+// to the CONSUMER through LDS, chunk by chunk (kPsChunk steps, double-buffered, one barrier per
+// chunk); the consumer runs the Euler recursion, the Girsanov terms, the pairwise sums and the
+// X° stores.  Each wave's instruction stream is about half the single-wave kernel's, which is
+// what bounds the lane mapping when the ensemble has fewer tiles than the chip has SIMDs (C5).
+// Same operations in the same order as k_block: bit-identical.
+constexpr int kPsChunk = 16;
+
+template <class Mdl, class T>
+__global__ __launch_bounds__(128) void k_block_ps(const BlockArgs<T> a) {
+  constexpr int D = Mdl::D, M = Mdl::M, HP = D * (D + 1) / 2;
+  constexpr int L = kPsChunk, K = 4;
+  static_assert(L % K == 0 && (L * M) % 2 == 0, "chunk must hold whole normal pairs");
+  __shared__ T s_dt[2][L][64];
+  __shared__ T s_dw[2][L][M][64];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int64_t tile = a.tile0 + blockIdx.x / a.MB;
+  const int bidx = (int)(blockIdx.x % a.MB);
+  if (tile >= a.tile1) return;  // whole workgroup
+  const int64_t r = tile * kLanes + lane;
+  int64_t blk = -1;
+  if (r < a.R) {
+    blk = a.blk_off[r] + bidx;
+    if (blk >= a.blk_off[r + 1] || blk < a.b0 || blk >= a.b1) blk = -1;
+  }
+  const bool act = blk >= 0;
+  const int64_t tq = a.tile_qoff[tile];
+  const int g = act ? a.gfirst[blk] : 0;  // the block's only segment (host-checked), terminal
+  const int nst = act ? a.seg_np[g] - 1 : 0;
+  // chunks: the longest lane of the tile (both waves compute the same count)
+  int nmax = nst;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) nmax = max(nmax, __shfl_xor(nmax, o, 64));
+  const int nch = (__builtin_amdgcn_readfirstlane(nmax) + L - 1) / L;
+  const int64_t row = tq + (act ? a.seg_q[g] : 0);
+  const T rho = act ? (T)a.rho[blk] : (T)0;
+  const T srho = act ? (T)a.srho[blk] : (T)1;
+  // selectors and the tile-phase repair decision (k_block), identical in both waves
+  const int sx = act ? a.selX[g] : 0, sw = act ? a.selW[g] : 0;
+  T* Xd = a.X[sx ^ a.xd_flip];
+  const T* Ws = a.W[sw ^ a.ws_flip];
+  T* Wd = a.W[sw ^ a.wd_flip];
+  const T *Xcs = nullptr;
+  T *Xcd = nullptr, *Wcd = nullptr;
+  int nsx = sx, nsw = sw;
+  {
+    const uint64_t am = __ballot(act);
+    const int nact = __popcll(am);
+    const int ox = __popcll(__ballot(act && sx != 0)), ow = __popcll(__ballot(act && sw != 0));
+    const int px = 2 * ox > nact ? 1 : 0, pw = 2 * ow > nact ? 1 : 0;
+    const int mx = px ? nact - ox : ox, mw = pw ? nact - ow : ow;
+    if (a.repair_div * mx <= nact) {
+      Xd = a.X[px ^ a.xd_flip];
+      if (sx != px) { Xcs = a.X[sx ^ a.xs_flip]; Xcd = a.X[px ^ a.xs_flip]; nsx = px; }
+    }
+    if (a.repair_div * mw <= nact) {
+      Wd = a.W[pw ^ a.wd_flip];
+      if (sw != pw) { Wcd = a.W[pw ^ a.ws_flip]; nsw = pw; }
+    }
+  }
+  auto idx = [&](int64_t q, int c, int C) -> int64_t { return ((row + q) * C + c) * kLanes + lane; };
+
+  if (w == 0) {
+    // ================= producer =================
+    const T* tb = a.t_shared ? a.t + (act ? a.seg_q[g] : 0) : a.t + row * kLanes + lane;
+    const int tst = a.t_shared ? 1 : kLanes;
+    const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
+    const uint32_t seg = (uint32_t)g + a.seg_base, c3 = a.salt << 1;
+    T tcur = tb[0];
+    if (act) {
+#pragma unroll
+      for (int k = 0; k < M; ++k) {
+        const T w0 = Ws[idx(0, k, M)];
+        if (Wcd) Wcd[idx(0, k, M)] = w0;
+        Wd[idx(0, k, M)] = rho * w0;
+      }
+    }
+    // prefetched inputs of the next chunk (rows past a segment end read padding: in bounds)
+    T pt[L], pw_[L][M];
+    auto load = [&](int c) {
+#pragma unroll
+      for (int j = 0; j < L; ++j) {
+        const int64_t i = (int64_t)c * L + j;
+        const int64_t ii = min<int64_t>(i, max(nst - 1, 0));
+        pt[j] = tb[(ii + 1) * tst];
+#pragma unroll
+        for (int k = 0; k < M; ++k) pw_[j][k] = Ws[idx(ii + 1, k, M)];
+      }
+    };
+    load(0);
+    for (int c = -1; c < nch; ++c) {
+      if (c + 1 < nch) {
+        const int cp = c + 1, buf = cp & 1;
+        T ct[L], cw[L][M];
+#pragma unroll
+        for (int j = 0; j < L; ++j) {
+          ct[j] = pt[j];
+#pragma unroll
+          for (int k = 0; k < M; ++k) cw[j][k] = pw_[j][k];
+        }
+        if (cp + 1 < nch) load(cp + 1);
+        T z[L][M];
+#pragma unroll
+        for (int pp = 0; pp < L * M / 2; ++pp) {
+          const uint32_t pair = (uint32_t)((cp * L * M) / 2 + pp);
+          U4 o = philox4x32_10(U4{pair, seg, a.iter, c3}, k0, k1);
+          T z0, z1;
+          normal_pair(o, z0, z1);
+          z[(2 * pp) / M][(2 * pp) % M] = z0;
+          z[(2 * pp + 1) / M][(2 * pp + 1) % M] = z1;
+        }
+#pragma unroll
+        for (int j = 0; j < L; ++j) {
+          const int64_t i = (int64_t)cp * L + j;
+          const bool v = act && i < nst;
+          const T dt = ct[j] - tcur;
+          const T sdt = sqrt(dt);
+          s_dt[buf][j][lane] = dt;
+#pragma unroll
+          for (int k = 0; k < M; ++k) {
+            const T dw = dfma(rho, cw[j][k], srho * (sdt * z[j][k]));
+            s_dw[buf][j][k][lane] = dw;
+            if (v) {
+              if (Wcd) Wcd[idx(i + 1, k, M)] = cw[j][k];
+              Wd[idx(i + 1, k, M)] = dw;
+            }
+          }
+          tcur = v ? ct[j] : tcur;
+        }
+      }
+      __syncthreads();
+    }
+  } else {
+    // ================= consumer =================
+    Law<Mdl, T> LA;
+    const int ls = act ? (a.selPP[g] ^ a.law_flip) : 0;
+    LA.load(a.law[ls][0] + (int64_t)g * DMT_LAW_STRIDE);
+    const T* Hb = a.H_shared[ls][0] ? a.H[ls][0] + (act ? a.seg_q[g] : 0) * HP : a.H[ls][0] + row * HP * kLanes + lane;
+    const int hst = a.H_shared[ls][0] ? 1 : kLanes;
+    const T* Fb = a.F[ls][0] + row * D * kLanes + lane;
+    T x[D];
+    {
+      const T* Xs = a.X[sx ^ a.xs_flip];
+#pragma unroll
+      for (int p = 0; p < D; ++p) x[p] = Xs[idx(0, p, D)];
+    }
+    T ll;
+    {
+      T H0[HP], F0[D];
+#pragma unroll
+      for (int e = 0; e < HP; ++e) H0[e] = Hb[e * hst];
+#pragma unroll
+      for (int e = 0; e < D; ++e) F0[e] = Fb[e * kLanes];
+      ll = obs_term<D, T>(H0, F0, x, (T)a.law[ls][0][(int64_t)g * DMT_LAW_STRIDE + DMT_LAW_C0]);
+    }
+    if (act) {
+      if (Xcd) {
+#pragma unroll
+        for (int p = 0; p < D; ++p) Xcd[idx(0, p, D)] = Xcs[idx(0, p, D)];
+      }
+#pragma unroll
+      for (int p = 0; p < D; ++p) Xd[idx(0, p, D)] = x[p];
+    }
+    PSum<T> ps;
+    ps.init();
+    const int nfull = nst - nst % K;
+    struct Sub { T H[K][HP], F[K][D], Xu[K][D]; };
+    auto load = [&](int64_t i0, Sub& s) {
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        const int64_t i = min<int64_t>(i0 + j, max(nst - 1, 0));
+#pragma unroll
+        for (int e = 0; e < HP; ++e) s.H[j][e] = Hb[(i * HP + e) * hst];
+#pragma unroll
+        for (int e = 0; e < D; ++e) s.F[j][e] = Fb[(i * D + e) * kLanes];
+        if (Xcd) {
+#pragma unroll
+          for (int e = 0; e < D; ++e) s.Xu[j][e] = Xcs[idx(i + 1, e, D)];
+        }
+      }
+    };
+    Sub cur, nxt;
+    load(0, cur);
+    for (int c = -1; c < nch; ++c) {
+      if (c >= 0) {
+        const int buf = c & 1;
+#pragma unroll
+        for (int q = 0; q < L / K; ++q) {
+          const int64_t i0 = (int64_t)c * L + q * K;
+          load(i0 + K, nxt);  // prefetch (the next chunk's first sub-chunk at q = L/K - 1)
+          T gv[K];
+#pragma unroll
+          for (int j = 0; j < K; ++j) {
+            const int64_t i = i0 + j;
+            const bool v = act && i < nst;
+            const T dt = s_dt[buf][q * K + j][lane];
+            T dW[M];
+#pragma unroll
+            for (int k = 0; k < M; ++k) dW[k] = s_dw[buf][q * K + j][k][lane];
+            T rr[D], b[D], sdW[D], Mg[D * D], cg[D];
+            const T G = g_at<Mdl, T>(LA, cur.H[j], cur.F[j], x, rr, b);
+            sigma_dw<Mdl, T>(LA, dW, sdW);
+            guide_coeffs<Mdl, T>(LA, cur.H[j], cur.F[j], Mg, cg);
+            T xn[D];
+#pragma unroll
+            for (int p = 0; p < D; ++p) xn[p] = x[p];
+            euler_step<Mdl, T>(Mg, cg, b, dt, sdW, xn);
+            if (v) {
+              if (Xcd) {
+#pragma unroll
+                for (int e = 0; e < D; ++e) Xcd[idx(i + 1, e, D)] = cur.Xu[j][e];
+              }
+#pragma unroll
+              for (int p = 0; p < D; ++p) {
+                x[p] = xn[p];
+                Xd[idx(i + 1, p, D)] = xn[p];
+              }
+            }
+            gv[j] = G * dt;
+          }
+          if (i0 + K <= nfull) {
+            ps.template add_subtree<Log2<K>::v>(tree_sum<T, K>(gv));
+          } else {
+#pragma unroll
+            for (int j = 0; j < K; ++j)
+              if (i0 + j < nst) ps.add(gv[j]);
+          }
+          cur = nxt;
+        }
+      }
+      __syncthreads();
+    }
+    if (act) {
+      const T sl = ps.finish();
+      bool ok = isfinite(sl);
+#pragma unroll
+      for (int p = 0; p < D; ++p) ok = ok && isfinite(x[p]);
+      if (nsx != sx) a.selX[g] = (uint8_t)nsx;
+      if (nsw != sw) a.selW[g] = (uint8_t)nsw;
+      a.ll_out[blk] = ok ? (double)(ll + sl) : -INFINITY;
+      if (a.success) a.success[blk] = ok ? 1 : 0;
+    }
+  }
 }
 
 // Girsanov log-weight of a stored path (loglikhd!), same summation order as k_block.
@@ -2063,6 +2312,10 @@ static hipError_t launch_block_t(int mapping, int mode, const void* args, int64_
     }
     const dim3 block(64);
     const bool par = a.Z != nullptr;
+    if (mode == MODE_PCN && !par && a.lane_split) {  // producer/consumer waves (k_block_ps)
+      dlaunch(k_block_ps<Mdl, T>, grid, dim3(128), s, a);
+      return hipGetLastError();
+    }
     switch (mode) {
       case MODE_PCN:
         if (par) dlaunch(k_block<Mdl, T, MODE_PCN, true, kChunk>, grid, block, s, a);

@@ -55,6 +55,7 @@ struct Layout {
   std::vector<int64_t> blk_off;  // [R + 1]
   std::vector<int32_t> gfirst, glast, blk_rec;
   std::vector<uint8_t> term;
+  bool single_seg = false;  // every block is one segment (the lane kernels' producer/consumer split)
   int64_t* d_blk_off = nullptr;
   BlkInfo* d_binfo = nullptr;
   int32_t* d_blk_rec = nullptr;
@@ -146,6 +147,10 @@ struct dmt_ens {
   int64_t part_cap = 0;
   bool persist = true;       // dmt_mcmc_run of a linear drift in one launch (DMT_MCMC_PERSIST=0: off)
   bool resident = true;      // ... with register-resident block state when eligible (DMT_MCMC_RESIDENT=0: off)
+  int lane_split = -1;       // MAP_LANE draws on producer/consumer waves: 1 on, 0 off, -1 auto
+                             // (when the draw has fewer waves than the device has SIMDs)
+  int64_t n_simd = 1024;
+  int repair_div = 4;        // MAP_LANE tile-phase repair threshold (DMT_REPAIR_DIV)
   std::vector<std::unique_ptr<Layout>> layouts;  // layouts[0] = internal "unit" layout
   // timing
   uint32_t timing = 0;  // bit k: time kernel class k (dmt_set_timing)
@@ -351,6 +356,8 @@ void fill_common(dmt_ens* h, const Layout* L, BlockArgs<T>& a) {
   a.seg_base = h->seg_base;
   a.Z = nullptr;
   a.success = nullptr;
+  a.repair_div = h->repair_div;
+  a.lane_split = 0;
 }
 
 dmt_status run_block_kernel(dmt_ens* h, const Layout* L, int mode, int kind_timer, int64_t b0,
@@ -380,6 +387,7 @@ dmt_status run_block_kernel(dmt_ens* h, const Layout* L, int mode, int kind_time
     a.salt = salt;
     a.ll_out = ll_out;
     a.success = success;
+    a.lane_split = L->single_seg && (h->lane_split == 1 || (h->lane_split < 0 && nwaves < h->n_simd));
   };
   if (h->key.precision == DMT_F64) {
     BlockArgs<double> a{};
@@ -442,6 +450,8 @@ dmt_status build_layout(dmt_ens* h, const int32_t* n_blocks, const int32_t* seg_
       srho[b] = std::sqrt(1.0 - rho[b] * rho[b]);
     }
   }
+  L->single_seg = true;
+  for (int64_t b = 0; b < L->nblocks && L->single_seg; ++b) L->single_seg = L->gfirst[b] == L->glast[b];
   const int64_t nb = L->nblocks;
   DMT_TRY(ens_alloc(h, &L->d_blk_off, h->R + 1));
   DMT_TRY(ens_alloc(h, &L->d_gfirst, nb));
@@ -601,6 +611,13 @@ dmt_status dmt_create(dmt_ens** out, const dmt_model* model, const dmt_structure
   if (model->model == DMT_MODEL_OU) h->mapping = MAP_WAVE;
   if (const char* e = std::getenv("DMT_MCMC_PERSIST")) h->persist = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("DMT_MCMC_RESIDENT")) h->resident = std::strcmp(e, "0") != 0;
+  if (const char* e = std::getenv("DMT_LANE_SPLIT")) h->lane_split = std::atoi(e);
+  if (const char* e = std::getenv("DMT_REPAIR_DIV")) h->repair_div = std::max(1, std::atoi(e));
+  {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, h->device) == hipSuccess)
+      h->n_simd = 4 * (int64_t)prop.multiProcessorCount;
+  }
   h->tw = h->mapping == MAP_WAVE ? 1 : kLanes;
   h->ntiles = (h->R + h->tw - 1) / h->tw;
   h->tile_qoff.assign(h->ntiles + 1, 0);
