@@ -8,7 +8,7 @@ namespace dmt {
 constexpr int kLanes = 64;  // one recording per lane of a wave64 ("recording tile")
 // spare point rows at the end of every tile (and of shared tables): the software
 // prefetch reads up to 2*kChunk points past a segment end without bounds checks
-constexpr int kPadPoints = 16;
+constexpr int kPadPoints = 32;
 // MAP_AUTO picks MAP_WAVE up to this many recordings (see DESIGN.md §2 for the measurement)
 constexpr int64_t kAutoWaveMaxRecordings = 8192;
 

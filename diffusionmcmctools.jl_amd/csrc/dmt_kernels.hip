@@ -1368,6 +1368,9 @@ template <int D, int M, class T>
 struct ResLds {
   T pt[kSStride][D];  // pre-step points by LDS slot of the step (+ end point)
   T dw[kSStride][M];  // W° increments by LDS slot of the step
+#ifndef DMT_RES_HF_REGS
+  T hf[kRun][D * (D + 1) / 2 + D][64];  // H_i, F_i of each lane's run (G's inputs), lane-minor
+#endif
 };
 template <int D, int M, class T>
 struct ResCfg {
@@ -1427,7 +1430,10 @@ __global__ __launch_bounds__(256, 1) void k_mcmc_resident(const BlockArgs<T> a,
     llobs = obs_term<D, T>(H0, F0, x0, c00);
   }
   const int nv = max(0, min(kRun, nst - kRun * lane));  // valid steps of this lane's run
-  T Ac[kRun][D * D], cgs[kRun][D], dts[kRun], sdts[kRun], Hs[kRun][HP], Fs[kRun][D], wv[kRun][M];
+  T Ac[kRun][D * D], cgs[kRun][D], dts[kRun], sdts[kRun], wv[kRun][M];
+#ifdef DMT_RES_HF_REGS
+  T Hs[kRun][HP], Fs[kRun][D];
+#endif
   {
     const T* Ws = a.W[sel.w(g) ^ a.ws_flip] + row * M;
 #pragma unroll
@@ -1435,6 +1441,9 @@ __global__ __launch_bounds__(256, 1) void k_mcmc_resident(const BlockArgs<T> a,
       const int s = min(kRun * lane + r, nst - 1);
       dts[r] = tb[s + 1] - tb[s];
       sdts[r] = sqrt(dts[r]);
+#ifndef DMT_RES_HF_REGS
+      T Hs[kRun][HP], Fs[kRun][D];
+#endif
 #pragma unroll
       for (int cc = 0; cc < HP; ++cc) Hs[r][cc] = Hb[(int64_t)s * HP + cc];
 #pragma unroll
@@ -1443,6 +1452,12 @@ __global__ __launch_bounds__(256, 1) void k_mcmc_resident(const BlockArgs<T> a,
       for (int k = 0; k < M; ++k) wv[r][k] = Ws[(int64_t)(s + 1) * M + k];
       T Mg[D * D], zero[D] = {}, e_unused[D];
       guide_coeffs<Mdl, T>(LA, Hs[r], Fs[r], Mg, cgs[r]);
+#ifndef DMT_RES_HF_REGS
+#pragma unroll
+      for (int cc = 0; cc < HP; ++cc) S.hf[r][cc][lane] = Hs[r][cc];
+#pragma unroll
+      for (int cc = 0; cc < D; ++cc) S.hf[r][HP + cc][lane] = Fs[r][cc];
+#endif
       affine_step<D, T>(Mg, cgs[r], dts[r], zero, Ac[r], e_unused);
     }
   }
@@ -1533,7 +1548,16 @@ __global__ __launch_bounds__(256, 1) void k_mcmc_resident(const BlockArgs<T> a,
       const int li = lds_ix(kRun * lane + r);
       const bool v = r < nv;
       T rr[D], bb[D];
+#ifdef DMT_RES_HF_REGS
       const T G = g_at<Mdl, T>(LA, Hs[r], Fs[r], x, rr, bb);
+#else
+      T Hr[HP], Fr[D];
+#pragma unroll
+      for (int cc = 0; cc < HP; ++cc) Hr[cc] = S.hf[r][cc][lane];
+#pragma unroll
+      for (int cc = 0; cc < D; ++cc) Fr[cc] = S.hf[r][HP + cc][lane];
+      const T G = g_at<Mdl, T>(LA, Hr, Fr, x, rr, bb);
+#endif
       gl[r] = v ? G * dts[r] : (T)0;
       if (v) {
 #pragma unroll
@@ -2281,7 +2305,11 @@ static void dlaunch(void (*k)(KArgs...), dim3 grid, dim3 block, hipStream_t s, A
   }
 }
 
-constexpr int kChunk = 4;
+#ifndef DMT_KCHUNK
+#define DMT_KCHUNK 4
+#endif
+constexpr int kChunk = DMT_KCHUNK;  // lane-kernel steps per prefetch chunk
+static_assert(2 * kChunk <= kPadPoints, "prefetch reads up to 2 chunks past a segment end");
 
 template <class Mdl, class T>
 static hipError_t launch_block_t(int mapping, int mode, const void* args, int64_t nwaves,
