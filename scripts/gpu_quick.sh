@@ -6,7 +6,7 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 O=gpurun_out/$1
 mkdir -p $O
-K=${2:+-k "$2"}
+K=""; [ -n "$2" ] && K="-k '$2'"
 scripts/gpu_session.sh \
  "timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread $K > $O/pytest_gpu.log 2>&1" \
  "timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench_c2.json 2> $O/bench_c2.err" \

@@ -27,13 +27,13 @@ def both(w, seed=11, hist_len=0, init_Z=True, mapping=L.MAP_AUTO):
     return dev, ora, lay_d
 
 
-def assert_paths_equal(dev, ora, exact=True, rtol=0.0, atol=0.0):
+def assert_paths_equal(dev, ora, exact=True, rtol=0.0, atol=0.0, equal_nan=False):
     for unit in (L.U, L.UPROP):
         for what in (0, 1):
             a = dev.download_paths(unit, what)
             b = ora.download_paths(unit, what)
             if exact:
-                assert np.array_equal(a, b), (
+                assert np.array_equal(a, b, equal_nan=equal_nan), (
                     f"unit {unit} {'XX' if what == 0 else 'WW'}: max |diff| "
                     f"{np.nanmax(np.abs(a - b))} at {np.unravel_index(np.nanargmax(np.abs(a - b)), a.shape)}")
             else:

@@ -243,6 +243,41 @@ def test_mcmc_run_persistent_paths_equal_step_path(case):
     cs.assert_paths_equal(e0, e1)
 
 
+def test_mcmc_run_with_failing_blocks_equals_step_path():
+    """Blocks whose proposals overflow (σ = 1e160, so a = σσᵀ = inf) fail every iteration
+    (ll° = −Inf, never accepted) inside dmt_mcmc_run's persistent kernel exactly as on the
+    per-iteration path; the other blocks are unaffected."""
+    bad = [0, 5, 17, 63, 64, 99]
+
+    def build():
+        import diffusionmcmctools_amd as d
+        w = W.c2_ou2d(B=100, N=60)
+        w.meta["hist_len"] = 8
+        laws = w.laws.copy()
+        for g in bad:
+            laws[g, L.LAW_SIGMA:L.LAW_SIGMA + 4] *= 1e160
+            laws[g, L.LAW_A:L.LAW_A + 3] = [np.inf, 0.0, np.inf]
+        w.laws = laws
+        e = d.Ensemble(w.model.kind, w.d, w.m, w.n_points, precision=w.precision, seed=37,
+                       grid_shared=w.grid_shared)
+        lay = W.fill(e, w)
+        return e, lay, 100
+    (e0, lay, nb), (e1, _, _) = _env_ensembles(build, {"DMT_MCMC_PERSIST": "0"})
+    r0 = e0.mcmc_run(lay, 0, nb, 1, 6)
+    r1 = e1.mcmc_run(lay, 0, nb, 1, 6)
+    assert np.array_equal(r0, r1, equal_nan=True)
+    cs.assert_paths_equal(e0, e1, equal_nan=True)
+    llp = e0.get_block_state(lay, L.BLK_LLPROP_HIST, 0, nb, 8)[:6]
+    assert np.all(llp[:, bad] == -math.inf)
+    acc = e0.get_block_state(lay, L.BLK_ACC_HIST, 0, nb, 8)[:6]
+    assert not acc[1:, bad].any()          # iteration 1 may auto-accept (ll = −Inf before)
+    good = np.setdiff1d(np.arange(nb), bad)
+    assert np.all(np.isfinite(llp[:, good])) and acc[:, good].mean() > 0.3
+    for what in (L.BLK_ACC_HIST, L.BLK_LL_HIST, L.BLK_LLPROP_HIST):
+        assert np.array_equal(e0.get_block_state(lay, what, 0, nb, 8),
+                              e1.get_block_state(lay, what, 0, nb, 8), equal_nan=True)
+
+
 @pytest.mark.parametrize("mapping", MAPPINGS)
 def test_fetch_ll_tree_bit_exact(mapping):
     w = W.c2_ou2d(B=64 * 80, N=8)
