@@ -185,11 +185,14 @@ def main():
     barrier()
     el = time.perf_counter() - t0
     n_acc = float(res[:, 2].sum())
-    k_ms, k_n = ens.get_timing(L.K_DRAW)
-    # the accept+reduce kernel, timed on a few extra iterations after the timed region
-    ens.set_timing(True, kernels=[L.K_ACCEPT])
-    ens.mcmc_run(lay, 0, B, args.warmup + args.steps + 1, EXTRA_ITERS)
-    a_ms, a_n = ens.get_timing(L.K_ACCEPT)
+    k_ms, k_n = ens.get_timing(L.K_DRAW)  # k_n counts iterations (persistent) or launches
+    persist = w.model.kind == L.MODEL_OU and os.environ.get("DMT_MCMC_PERSIST", "1") != "0"
+    a_ms = a_n = 0
+    if not persist:
+        # the accept+reduce kernel, timed on a few extra iterations after the timed region
+        ens.set_timing(True, kernels=[L.K_ACCEPT])
+        ens.mcmc_run(lay, 0, B, args.warmup + args.steps + 1, EXTRA_ITERS)
+        a_ms, a_n = ens.get_timing(L.K_ACCEPT)
     ens.set_timing(False)
     if dist is not None:
         import torch
@@ -199,13 +202,18 @@ def main():
 
     steps_total = w.steps_per_iter * args.steps * world
     value = steps_total / el
-    k_avg_s = (k_ms / max(k_n, 1)) * 1e-3
-    bytes_launch = algorithmic_bytes_per_step(w) * w.steps_per_iter
+    # launches of the dominant kernel in the timed region: one per iteration, or (persistent,
+    # dmt_mcmc_run) one per chunk of iterations (dmt_runtime.hip: ≤ 64 MiB of partials)
+    it_per_launch = min(args.steps, max(1, (64 << 20) // (24 * B))) if persist else 1
+    launches = -(-args.steps // it_per_launch)
+    k_avg_s = (k_ms / launches) * 1e-3          # average launch duration
+    k_iter_s = (k_ms / max(args.steps, 1)) * 1e-3
+    bytes_iter = algorithmic_bytes_per_step(w) * w.steps_per_iter
+    bytes_launch = bytes_iter * it_per_launch
     achieved = bytes_launch / k_avg_s / 1e9 if k_avg_s > 0 else 0.0
     accept_rate = n_acc / (B * world * args.steps)  # n_acc is already global (fetch_ll over ranks)
     # the mapping libdmt resolves for MAP_AUTO (kAutoWaveMaxRecordings, dmt_internal.h)
     wave = args.mapping == "wave" or (args.mapping == "auto" and len(w.n_points) <= 8192)
-    persist = w.model.kind == L.MODEL_OU and os.environ.get("DMT_MCMC_PERSIST", "1") != "0"
     # single-segment blocks of <= 512 steps, d <= 2: register-resident kernel (dmt_internal.h)
     resident = (persist and w.d <= 2 and os.environ.get("DMT_MCMC_RESIDENT", "1") != "0"
                 and all(len(r) == 1 and r[0] - 1 <= 512 for r in w.n_points))
@@ -217,7 +225,9 @@ def main():
         wave, kname = True, "k_block_scan"
     else:
         kname = "k_block_wave" if wave else "k_block<"
-    traffic, traffic_src = measured_traffic(args.config, kname)
+    traffic, traffic_src = measured_traffic(args.config, kname)  # HBM bytes per iteration
+    if traffic is not None:
+        traffic *= it_per_launch
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
@@ -249,12 +259,14 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS,
                          "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
                          "traffic_source": traffic_src,
-                         "kernel": kname + (" (draw_proposal_path! + accept_reject_proposal_path!, "
-                                            "per iteration)" if persist else
+                         "kernel": kname + (" (draw_proposal_path! + accept_reject_proposal_path! "
+                                            "of every iteration of the launch)" if persist else
                                             " (draw_proposal_path!)"),
                          "kernel_avg_us": k_avg_s * 1e6,
-                         "iterations_per_launch": args.steps if persist else 1,
+                         "kernel_us_per_iteration": k_iter_s * 1e6,
+                         "iterations_per_launch": it_per_launch,
                          "algorithmic_bytes_per_launch": bytes_launch,
+                         "algorithmic_bytes_per_iteration": bytes_iter,
                          "bytes_per_step": algorithmic_bytes_per_step(w)},
             "accept_kernel_avg_us": (a_ms / a_n) * 1e3 if a_n else None,
             "cpu_baseline": cpu,
