@@ -316,10 +316,16 @@ __global__ __launch_bounds__(64) void k_block(const BlockArgs<T> a) {
 // X° stores.  Each wave's instruction stream is about half the single-wave kernel's, which is
 // what bounds the lane mapping when the ensemble has fewer tiles than the chip has SIMDs (C5).
 // Same operations in the same order as k_block: bit-identical.
-constexpr int kPsChunk = 16;
+#ifndef DMT_PS_CHUNK
+#define DMT_PS_CHUNK 16
+#endif
+constexpr int kPsChunk = DMT_PS_CHUNK;
+#ifndef DMT_PS_MINW
+#define DMT_PS_MINW 1  // 2 (with DMT_PS_CHUNK 8, no spills) measured no better: 1 877 vs 1 749–1 782 µs on C5
+#endif
 
 template <class Mdl, class T>
-__global__ __launch_bounds__(128) void k_block_ps(const BlockArgs<T> a) {
+__global__ __launch_bounds__(128, DMT_PS_MINW) void k_block_ps(const BlockArgs<T> a) {
   constexpr int D = Mdl::D, M = Mdl::M, HP = D * (D + 1) / 2;
   constexpr int L = kPsChunk, K = 4;
   static_assert(L % K == 0 && (L * M) % 2 == 0, "chunk must hold whole normal pairs");
