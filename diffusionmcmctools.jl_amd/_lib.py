@@ -44,7 +44,7 @@ SYMBOLS = [
     "dmt_fetch_ll", "dmt_mcmc_step", "dmt_mcmc_run", "dmt_guiding_linear", "dmt_comm_unique_id", "dmt_comm_init", "dmt_set_shard", "dmt_sync",
     "dmt_set_timing", "dmt_get_timing", "dmt_memory_bytes", "dmt_debug_philox",
     "dmt_debug_normals", "dmt_last_error", "dmt_version", "dmt_snapshot_reserve",
-    "dmt_snapshot_take", "dmt_snapshot_download", "dmt_snapshot_write",
+    "dmt_snapshot_take", "dmt_snapshot_download", "dmt_snapshot_write", "dmt_set_ll",
 ]
 
 
@@ -125,6 +125,7 @@ _SIGS = {
     "dmt_snapshot_take": [_P, _i32, _i64, _i64],
     "dmt_snapshot_download": [_P, _i32, _i64, _pd, _pi64],
     "dmt_snapshot_write": [_P, C.c_char_p, _i64, _i64],
+    "dmt_set_ll": [_P, _i32, _i32, _i64, _i64, _i64, _pd],
 }
 for _name, _args in _SIGS.items():
     _f = getattr(lib, _name)

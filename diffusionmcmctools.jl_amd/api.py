@@ -246,6 +246,28 @@ class _BlockRange:
     def save_ll(self, i):
         self._call("save_ll", i)
 
+    def set_ll(self, i, v, unit=L.U):
+        """``set_ll!(b, i, v)`` (src/block.jl:82-86) on ``bb.b`` (``unit=U``) or ``bb.b°``:
+        ll_history[i] = v (a scalar or one value per block)."""
+        self._ens.set_ll(self._layout, unit, self._b0, self._b1, i, v)
+
+    def accept_reject_proposal_param(self, mcmciter, theta, theta_prop, E=None, rng=None):
+        """The tutorials' parameter Metropolis–Hastings step
+        (docs/src/tutorials/pnames/inference_with_biblock.md:17-25): accept θ° when
+        E > −(ll° − ll) with the range's total log-likelihoods (``fetch_ll``/``fetch_ll°``),
+        E ~ Exp(1) (``E`` given, or drawn from ``rng``); on acceptance swap_XX!, swap_PP!;
+        save_ll! of both units; swap_ll! on acceptance.  Returns (accepted, θ or θ°)."""
+        llp, ll = self.fetch_ll_prop(), self.fetch_ll()
+        if E is None:
+            E = (rng if rng is not None else np.random.default_rng()).exponential(1.0)
+        accepted = bool(E > -(llp - ll))
+        if accepted:
+            self._call_what("swap", L.SWAP_XX | L.SWAP_PP)
+        self.save_ll(mcmciter)
+        if accepted:
+            self.swap_ll()
+        return accepted, (np.array(theta_prop, copy=True) if accepted else np.array(theta, copy=True))
+
     def fetch_ll(self):
         """Σ ll over the blocks (deterministic pairwise tree)."""
         return self._call("fetch_ll")[0]

@@ -1454,6 +1454,22 @@ dmt_status dmt_set_accepted(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, 
   return DMT_OK;
 }
 
+dmt_status dmt_set_ll(dmt_ens* h, int32_t layout, int32_t unit, int64_t b0, int64_t b1,
+                      int64_t mcmciter, const double* v) {
+  DMT_TRY(check_h(h));
+  Layout* L;
+  DMT_TRY(get_layout(h, layout, &L));
+  DMT_TRY(check_range(L, b0, b1));
+  if (unit != DMT_U && unit != DMT_UPROP) return fail(DMT_ERR_INVALID, "bad unit");
+  if (mcmciter < 1 || mcmciter > L->hist_len) return fail(DMT_ERR_INVALID, "mcmciter outside 1:ll_hist_len");
+  if (!v) return fail(DMT_ERR_INVALID, "null values");
+  double* hist = unit == DMT_U ? L->d_llh : L->d_llph;
+  HIP_OK(hipMemcpyAsync(hist + (mcmciter - 1) * L->nblocks + b0, v, (b1 - b0) * 8,
+                        hipMemcpyHostToDevice, h->stream));
+  HIP_OK(hipStreamSynchronize(h->stream));
+  return DMT_OK;
+}
+
 static dmt_status block_state_ptr(Layout* L, int32_t what, void** p, size_t* esz, bool* hist) {
   *hist = false;
   switch (what) {

@@ -243,6 +243,11 @@ class Ensemble:
         L.call("dmt_get_block_state", self._h, layout, what, b0, b1, out.ctypes.data_as(C.c_void_p))
         return out
 
+    def set_ll(self, layout, unit, b0, b1, mcmciter, values):
+        """set_ll!(b, i, v) (src/block.jl:82-86) for blocks [b0, b1) of unit u (bb.b) or u°."""
+        v = np.ascontiguousarray(np.broadcast_to(np.asarray(values, dtype=np.float64), (b1 - b0,)))
+        L.call("dmt_set_ll", self._h, layout, int(unit), b0, b1, int(mcmciter), L.f64p(v))
+
     def set_block_state(self, layout, what, b0, b1, values):
         dt = np.uint8 if what == L.BLK_ACC_HIST else np.float64
         v = np.ascontiguousarray(values, dtype=dt)

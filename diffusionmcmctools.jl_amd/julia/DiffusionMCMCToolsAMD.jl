@@ -14,7 +14,7 @@ module DiffusionMCMCToolsAMD
 using StaticArrays
 
 import DiffusionMCMCTools: draw_proposal_path!, accept_reject_proposal_path!, loglikhd!,
-    loglikhd°!, fetch_ll, fetch_ll°, save_ll!, set_accepted!, swap_paths!, swap_XX!,
+    loglikhd°!, fetch_ll, fetch_ll°, save_ll!, set_ll!, set_accepted!, swap_paths!, swap_XX!,
     swap_WW!, swap_PP!, swap_ll!, ll_of_accepted, accpt_rate, recompute_path!, find_W_for_X!
 
 export DeviceSamplingEnsemble, DeviceBlockEnsemble, DeviceBlockCollection, DeviceBiBlock,
@@ -345,6 +345,15 @@ swap_ll!(x::DeviceBlocks) = _swap!(x, DMT_SWAP_LL)
 
 save_ll!(x::DeviceBlocks, i::Int) = check(ccall((:dmt_save_ll, libdmt), Int32,
     (Ptr{Cvoid}, Int32, Int64, Int64, Int64), x.se.h, x.layout, x.b0, x.b1, i))
+
+"set_ll!(b, i, v) (src/block.jl:82-86): ll_history[i] of bb.b (unit DMT_U) or bb.b°."
+function set_ll!(x::DeviceBlocks, i::Int, v; unit=DMT_U)
+    vals = Vector{Float64}(undef, x.b1 - x.b0)
+    vals .= v
+    check(ccall((:dmt_set_ll, libdmt), Int32,
+                (Ptr{Cvoid}, Int32, Int32, Int64, Int64, Int64, Ptr{Float64}),
+                x.se.h, x.layout, unit, x.b0, x.b1, i, vals))
+end
 
 function set_accepted!(x::DeviceBlocks, i::Int, v)
     vv = fill(UInt8(v), _n(x))

@@ -269,6 +269,10 @@ dmt_status dmt_swap(dmt_ens* h, int32_t layout, int32_t what, int64_t b0, int64_
 
 /* save_ll!(·, i) (src/biblock.jl:256-259) and set_accepted!(·, i, v) (src/biblock.jl:135). */
 dmt_status dmt_save_ll(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int64_t mcmciter);
+/* set_ll!(b, i, v) (src/block.jl:82-86): ll_history[i] = v of bb.b (unit DMT_U) or bb.b°
+ * (DMT_UPROP), v: double[b1-b0]. */
+dmt_status dmt_set_ll(dmt_ens* h, int32_t layout, int32_t unit, int64_t b0, int64_t b1,
+                      int64_t mcmciter, const double* v);
 dmt_status dmt_set_accepted(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
                             int64_t mcmciter, const uint8_t* v);
 

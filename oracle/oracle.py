@@ -673,6 +673,12 @@ class OracleEnsemble:
             bk.ll_hist[mcmciter - 1] = bk.ll
             bk.llp_hist[mcmciter - 1] = bk.llp
 
+    def set_ll(self, layout, unit, b0, b1, mcmciter, v):
+        """set_ll!(b, i, v), src/block.jl:82-86 (b = bb.b for U, bb.b° for UPROP)."""
+        v = np.broadcast_to(np.asarray(v, dtype=np.float64), (b1 - b0,))
+        for j, bk in enumerate(self.layouts[layout][b0:b1]):
+            (bk.ll_hist if unit == 0 else bk.llp_hist)[mcmciter - 1] = v[j]
+
     def set_accepted(self, layout, b0, b1, mcmciter, v):
         v = np.broadcast_to(np.asarray(v, dtype=bool), (b1 - b0,))
         for j, bk in enumerate(self.layouts[layout][b0:b1]):

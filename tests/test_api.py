@@ -65,6 +65,16 @@ def _program(se, niter=6, seed=3):
         bb.draw_proposal_path(Z=Zb, iter=100 + i)
         bb.loglikhd_prop()
         out.append((bb.fetch_ll(), bb.fetch_ll_prop()))
+    # parameter steps (docs/src/tutorials/pnames/inference_with_biblock.md:17-25): re-solve
+    # u° with u's W (recompute_path!), then the parameter MH decision, once accepted (E = 0
+    # accepts unless ll° = −Inf) and once rejected (E = 50)
+    for E in (0.0, 50.0):
+        beB.recompute_path()
+        acc, th = beB.accept_reject_proposal_param(niter, [1.5], [1.7], E=E)
+        out.append((acc, th, beB.fetch_ll(), beB.fetch_ll_prop(), beB.ll.copy()))
+    beA.set_ll(2, -7.5)
+    beA.recordings[1].blocks[2].set_ll(3, 1.25, unit=L.UPROP)
+    out.append((beA.ll_history.copy(), beA.ll_prop_history.copy()))
     return beA, beB, out
 
 
@@ -137,6 +147,36 @@ def test_accept_order_matches_reference():
         np.testing.assert_array_equal(be.ll_prop_history[i - 1], llp0)
         np.testing.assert_array_equal(be.ll, np.where(acc, llp0, ll0))
         np.testing.assert_array_equal(be.ll_prop, np.where(acc, ll0, llp0))
+
+
+def test_param_step_and_set_ll_on_host():
+    """accept_reject_proposal_param follows the tutorial helper (swap_XX!, swap_PP!, save_ll!
+    of both blocks, swap_ll! on acceptance; decision E > −(Σll° − Σll)); set_ll! writes one
+    history entry of b or b°."""
+    case = ragged_case()
+    se = _sampling_ensemble(case, "oracle")
+    be = dmt.BlockEnsemble(se, RANGES_B, rho=0.5, ll_hist_len=3)
+    be.loglikhd()
+    be.draw_proposal_path(Z=np.random.default_rng(2).standard_normal((se.ens.S, 1)))
+    be.loglikhd_prop()
+    ll, llp = be.fetch_ll(), be.fetch_ll_prop()
+    X_p = [a.copy() for a in se.recordings[0].u_prop.XX]
+    lb, lbp = be.ll.copy(), be.ll_prop.copy()
+    E = max(0.0, -(llp - ll)) + 1.0          # forces acceptance
+    acc, th = be.accept_reject_proposal_param(1, [1.5], [1.7], E=E)
+    assert acc and th.tolist() == [1.7]
+    for a, b in zip(se.recordings[0].u.XX, X_p):
+        np.testing.assert_array_equal(a, b)
+    np.testing.assert_array_equal(be.ll, lbp)
+    np.testing.assert_array_equal(be.ll_history[0], lb)   # save_ll! before swap_ll!
+    np.testing.assert_array_equal(be.ll_prop_history[0], lbp)
+    acc, th = be.accept_reject_proposal_param(2, [1.5], [1.7], E=-math.inf)
+    assert not acc and th.tolist() == [1.5]
+    be.set_ll(3, 2.5)
+    be.recordings[1].blocks[0].set_ll(3, -1.0, unit=L.UPROP)
+    assert np.all(be.ll_history[2] == 2.5)
+    assert np.ravel(be.recordings[1].blocks[0].ll_prop_history)[2] == -1.0
+    assert np.ravel(be.recordings[1].blocks[1].ll_prop_history)[2] != -1.0
 
 
 def test_swaps_and_set_accepted():
