@@ -1013,7 +1013,7 @@ static dmt_status ensure_red_work(dmt_ens* h, int64_t n) {
 
 // d_red (3 partials of this rank) -> host values, combined over ranks with RCCL
 static dmt_status finish_reduction(dmt_ens* h, double* v) {
-  if (h->comm && h->nranks > 1) {
+  if (h->comm) {
     if (!h->d_gather) DMT_TRY(ens_alloc(h, &h->d_gather, 3 * h->nranks));
     if (ncclAllGather(h->d_red, h->d_gather, 3, ncclDouble, h->comm, h->stream) != ncclSuccess)
       return fail(DMT_ERR_COMM, "ncclAllGather failed");
@@ -1076,7 +1076,7 @@ dmt_status dmt_mcmc_run(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int6
   if (n_iter == 0) return DMT_OK;
   if (L->hist_len > 0 && iter0 + n_iter - 1 > L->hist_len)
     return fail(DMT_ERR_INVALID, "iterations outside 1:ll_hist_len");
-  const bool multi = h->comm && h->nranks > 1;
+  const bool multi = h->comm != nullptr;
   if (n_iter > h->run_cap) {
     if (h->d_run) { (void)hipFree(h->d_run); h->bytes -= h->run_cap * 24; h->d_run = nullptr; }
     if (h->d_run_gather) {
@@ -1614,7 +1614,9 @@ dmt_status dmt_comm_init(dmt_ens* h, int32_t nranks, int32_t rank, const uint8_t
   }
   h->nranks = nranks;
   h->rank = rank;
-  if (nranks == 1) return DMT_OK;
+  // one rank needs no communicator; DMT_COMM_FORCE=1 makes one anyway, so that the RCCL
+  // all-gather path can be exercised on a single GPU (tests/test_multirank.py)
+  if (nranks == 1 && !std::getenv("DMT_COMM_FORCE")) return DMT_OK;
   ncclUniqueId uid;
   std::memcpy(&uid, id, 128);
   if (ncclCommInitRank(&h->comm, nranks, uid, rank) != ncclSuccess)

@@ -113,3 +113,33 @@ def test_gpu_shards_match_unsharded():
         assert comb == tuple(float(x) for x in parts[i])
     X = np.concatenate([e.download_paths(1, 0) for e, _ in shards])
     np.testing.assert_array_equal(X, full.download_paths(1, 0))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("persist", ["1", "0"])
+def test_rccl_allgather_path_single_rank(monkeypatch, persist):
+    """The RCCL path of fetch_ll / dmt_mcmc_run (ncclCommInitRank, ncclAllGather, the host
+    rank-order tree) on a one-rank communicator (DMT_COMM_FORCE): results identical to the
+    communicator-free path, for the persistent and the per-iteration MCMC kernels."""
+    import diffusionmcmctools_amd as dmt
+    from diffusionmcmctools_amd import workloads as W
+    monkeypatch.setenv("DMT_COMM_FORCE", "1")
+    monkeypatch.setenv("DMT_MCMC_PERSIST", persist)
+    w = W.c2_ou2d(B=300, N=100)
+    w.meta["hist_len"] = 12
+    ens = []
+    for k in range(2):
+        e = dmt.Ensemble(w.model.kind, w.d, w.m, w.n_points, precision=w.precision, seed=SEED,
+                         grid_shared=w.grid_shared)
+        lay = W.fill(e, w)
+        if k == 1:
+            e.comm_init(1, 0, dmt.comm_unique_id())
+        e.loglikhd(lay, 0, 0, w.nblocks)
+        ens.append(e)
+    r = [e.mcmc_run(lay, 0, w.nblocks, 1, 10) for e in ens]
+    np.testing.assert_array_equal(r[0], r[1])
+    f = [e.fetch_ll(lay, 0, w.nblocks, 10) for e in ens]
+    assert f[0] == f[1]
+    for e in ens:
+        e.close()
+
