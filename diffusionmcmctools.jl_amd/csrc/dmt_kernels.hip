@@ -1096,30 +1096,36 @@ __device__ __forceinline__ void scan_block(const BlockArgs<T>& a, const int64_t 
     T seg_acc = (T)0;
     for (int c0 = 0; c0 < nst; c0 += kSChunk) {
       const int cnt = min(kSChunk, nst - c0);
-      // ---- phase 1 (coalesced): step maps of the chunk → LDS
-      T Hk[kKeep ? kRun : 1][HP], Fk[kKeep ? kRun : 1][D], dtk[kKeep ? kRun : 1];
+      // ---- phase 1 (coalesced): step maps of the chunk → LDS.  Every input of the chunk is
+      // loaded first: the W° stores below may alias u's W as far as the compiler knows, so a
+      // load placed after one of them could not be hoisted above it (one exposed memory
+      // latency per row otherwise)
+      T Hk[kRun][HP], Fk[kRun][D], dtk[kRun], Wk[kRun][M], Zk[kRun][M];
+#pragma unroll
+      for (int k = 0; k < kRun; ++k) {
+        const int s = 64 * k + lane;
+        const int i = c0 + (s < cnt ? s : cnt - 1);
+        dtk[k] = tb[i + 1] - tb[i];
+#pragma unroll
+        for (int c = 0; c < HP; ++c) Hk[k][c] = Hb[(int64_t)i * HP + c];
+#pragma unroll
+        for (int c = 0; c < D; ++c) Fk[k][c] = Fb[(int64_t)i * D + c];
+#pragma unroll
+        for (int kk = 0; kk < M; ++kk) {
+          Wk[k][kk] = (MODE == MODE_FRESH) ? (T)0 : Wsb[(int64_t)(i + 1) * M + kk];
+          Zk[k][kk] = (MODE != MODE_RECOMPUTE && Zg) ? (T)Zg[(int64_t)i * M + kk] : (T)0;
+        }
+      }
 #pragma unroll
       for (int k = 0; k < kRun; ++k) {
         const int s = 64 * k + lane;
         const bool v = s < cnt;
         const int i = c0 + (v ? s : cnt - 1);
-        T Hi[HP], Fi[D];
-        const T dt = tb[i + 1] - tb[i];
-#pragma unroll
-        for (int c = 0; c < HP; ++c) Hi[c] = Hb[(int64_t)i * HP + c];
-#pragma unroll
-        for (int c = 0; c < D; ++c) Fi[c] = Fb[(int64_t)i * D + c];
-        if constexpr (kKeep) {
-          dtk[k] = dt;
-#pragma unroll
-          for (int c = 0; c < HP; ++c) Hk[k][c] = Hi[c];
-#pragma unroll
-          for (int c = 0; c < D; ++c) Fk[k][c] = Fi[c];
-        }
+        const T dt = dtk[k];
         T dW[M];
         if (MODE == MODE_RECOMPUTE) {
 #pragma unroll
-          for (int kk = 0; kk < M; ++kk) dW[kk] = Wsb[(int64_t)(i + 1) * M + kk];
+          for (int kk = 0; kk < M; ++kk) dW[kk] = Wk[k][kk];
         } else {
           uint32_t have = 0xFFFFFFFFu;
           T z0 = (T)0, z1 = (T)0;
@@ -1129,7 +1135,7 @@ __device__ __forceinline__ void scan_block(const BlockArgs<T>& a, const int64_t 
             const uint32_t n = (uint32_t)(i * M + kk);
             T z;
             if (Zg) {
-              z = (T)Zg[(int64_t)i * M + kk];
+              z = Zk[k][kk];
             } else {
               if ((n >> 1) != have) {
                 U4 o = philox4x32_10(U4{n >> 1, (uint32_t)g + a.seg_base, iter, c3}, k0, k1);
@@ -1138,14 +1144,13 @@ __device__ __forceinline__ void scan_block(const BlockArgs<T>& a, const int64_t 
               }
               z = (n & 1u) ? z1 : z0;
             }
-            const T wv = (MODE == MODE_FRESH) ? (T)0 : Wsb[(int64_t)(i + 1) * M + kk];
-            dW[kk] = dfma(rho, wv, srho * (sdt * z));
+            dW[kk] = dfma(rho, Wk[k][kk], srho * (sdt * z));
           }
           if (v) store_row<M, T>(Wdb + (int64_t)(i + 1) * M, dW);
         }
         T sdW[D], Mg[D * D], cg[D], A[D * D], e[D];
         sigma_dw<Mdl, T>(LA, dW, sdW);
-        guide_coeffs<Mdl, T>(LA, Hi, Fi, Mg, cg);
+        guide_coeffs<Mdl, T>(LA, Hk[k], Fk[k], Mg, cg);
         affine_step<D, T>(Mg, cg, dt, sdW, A, e);
         const int li = lds_ix(s);
 #pragma unroll
@@ -1226,37 +1231,47 @@ __device__ __forceinline__ void scan_block(const BlockArgs<T>& a, const int64_t 
         for (int p = 0; p < D; ++p) S.pt[p][lds_ix(cnt)] = x[p];
       }
       wave_lds_sync();
-      // ---- phase 3 (coalesced): Girsanov terms, 64-step chunk sums, path stores
+      // ---- phase 3 (coalesced): Girsanov terms, 64-step chunk sums, path stores.  The 8 rows'
+      // terms first, then their 8 xor-shuffle trees level by level (independent shuffles in
+      // flight together instead of 8 dependent 6-level chains), then the stores
+      T gk[kRun], xk[kRun][D];
 #pragma unroll
       for (int k = 0; k < kRun; ++k) {
-        if (64 * k < cnt) {  // uniform
-          const int s = 64 * k + lane;
-          const bool v = s < cnt;
-          const int li = lds_ix(s);
-          T xpre[D];
+        const int s = 64 * k + lane;
+        const bool v = s < cnt;
+        const int li = lds_ix(s);
 #pragma unroll
-          for (int p = 0; p < D; ++p) xpre[p] = S.pt[p][li];
-          T Hi[HP], Fi[D], dt;
-          if constexpr (kKeep) {
-            dt = dtk[k];
+        for (int p = 0; p < D; ++p) xk[k][p] = S.pt[p][li];
+        T Hi[HP], Fi[D], dt;
+        if constexpr (kKeep) {
+          dt = dtk[k];
 #pragma unroll
-            for (int c = 0; c < HP; ++c) Hi[c] = Hk[k][c];
+          for (int c = 0; c < HP; ++c) Hi[c] = Hk[k][c];
 #pragma unroll
-            for (int c = 0; c < D; ++c) Fi[c] = Fk[k][c];
-          } else {
-            const int i = c0 + (v ? s : cnt - 1);
-            dt = tb[i + 1] - tb[i];
+          for (int c = 0; c < D; ++c) Fi[c] = Fk[k][c];
+        } else {
+          const int i = c0 + (v ? s : cnt - 1);
+          dt = tb[i + 1] - tb[i];
 #pragma unroll
-            for (int c = 0; c < HP; ++c) Hi[c] = Hb[(int64_t)i * HP + c];
+          for (int c = 0; c < HP; ++c) Hi[c] = Hb[(int64_t)i * HP + c];
 #pragma unroll
-            for (int c = 0; c < D; ++c) Fi[c] = Fb[(int64_t)i * D + c];
-          }
-          T rr[D], bb[D];
-          const T G = g_at<Mdl, T>(LA, Hi, Fi, xpre, rr, bb);
-          const T csum = wave_uniform(wave_tree_sum<T>(v ? G * dt : (T)0));
-          seg_acc = seg_acc + (csum + (T)0);
-          if (v) store_row<D, T>(Xdb + (int64_t)(c0 + s) * D, xpre);
+          for (int c = 0; c < D; ++c) Fi[c] = Fb[(int64_t)i * D + c];
         }
+        T rr[D], bb[D];
+        const T G = g_at<Mdl, T>(LA, Hi, Fi, xk[k], rr, bb);
+        gk[k] = v ? G * dt : (T)0;
+      }
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1)
+#pragma unroll
+        for (int k = 0; k < kRun; ++k) gk[k] = gk[k] + __shfl_xor(gk[k], off, 64);
+#pragma unroll
+      for (int k = 0; k < kRun; ++k)
+        if (64 * k < cnt) seg_acc = seg_acc + (wave_uniform(gk[k]) + (T)0);  // uniform
+#pragma unroll
+      for (int k = 0; k < kRun; ++k) {
+        const int s = 64 * k + lane;
+        if (s < cnt) store_row<D, T>(Xdb + (int64_t)(c0 + s) * D, xk[k]);
       }
 #pragma unroll
       for (int p = 0; p < D; ++p) xc[p] = wave_uniform(S.pt[p][lds_ix(cnt)]);
@@ -2728,6 +2743,10 @@ hipError_t launch_block_sum(const double* ll, const double* llp, const uint8_t* 
 hipError_t launch_accept_reduce(const AcceptArgs& a, double* work, double* lb, double* out3,
                                 hipStream_t s) {
   const int64_t n = a.b1 - a.b0;
+  if (n <= 1024) {  // one 1024-thread workgroup: decisions and the whole tree, no second pass
+    dlaunch(k_accept_reduce, dim3(1), dim3(1024), s, a, work, (int64_t)1, out3);
+    return hipGetLastError();
+  }
   {  // single launch while the group partials fit one workgroup
     const int64_t groups = std::max<int64_t>(1, (n + kAccGroup - 1) / kAccGroup);
     if (groups <= kAccGroup) {
