@@ -214,13 +214,16 @@ def main():
     accept_rate = n_acc / (B * world * args.steps)  # n_acc is already global (fetch_ll over ranks)
     # the mapping libdmt resolves for MAP_AUTO (kAutoWaveMaxRecordings, dmt_internal.h)
     wave = args.mapping == "wave" or (args.mapping == "auto" and len(w.n_points) <= 8192)
-    # single-segment blocks of <= 512 steps, d <= 2: register-resident kernel (dmt_internal.h)
-    resident = (persist and w.d <= 2 and os.environ.get("DMT_MCMC_RESIDENT", "1") != "0"
-                and all(len(r) == 1 and r[0] - 1 <= 512 for r in w.n_points))
+    # single-segment blocks of <= 512 steps, d <= 2: register-resident kernels (dmt_internal.h)
+    short1 = (w.model.kind == L.MODEL_OU and w.d <= 2
+              and all(len(r) == 1 and r[0] - 1 <= 512 for r in w.n_points))
+    resident = persist and short1 and os.environ.get("DMT_MCMC_RESIDENT", "1") != "0"
     if resident:  # linear drift: all K iterations in one k_mcmc_resident launch (dmt_mcmc_run)
         wave, kname = True, "k_mcmc_resident"
     elif persist:  # linear drift: all K iterations in one k_mcmc_scan launch (dmt_mcmc_run)
         wave, kname = True, "k_mcmc_scan"
+    elif short1 and os.environ.get("DMT_SCAN_RESIDENT", "1") != "0":  # one launch per iteration
+        wave, kname = True, "k_block_resident"
     elif w.model.kind == L.MODEL_OU:  # linear drift: the affine-scan kernel per iteration
         wave, kname = True, "k_block_scan"
     else:
@@ -251,6 +254,7 @@ def main():
                        "parallelism": f"blockensemble-shard x{world}",
                        "mapping": ("scan-resident" if resident else
                                    "scan-persistent" if persist else
+                                   "scan-resident-per-iteration" if kname == "k_block_resident" else
                                    "scan" if kname == "k_block_scan" else
                                    "wave" if wave else "lane"),
                        "rng": "device Philox4x32-10 + Box-Muller (perf mode)"},

@@ -85,6 +85,8 @@ struct BlockArgs {
   double* ll_out;     // [nblocks]
   uint8_t* success;   // [nblocks] or nullptr
   int repair_div;     // MAP_LANE tile-phase repair while the minority is <= 1/repair_div
+  int resident1;      // linear drift, layout of single-segment blocks of <= kResidentMaxSteps
+                      // steps: one-shot draws on k_block_resident
   int lane_split;     // MAP_LANE draws: producer/consumer waves (k_block_ps); the runtime sets
                       // it only for layouts of single-segment blocks
 };

@@ -1398,26 +1398,25 @@ struct ResCfg {
   static constexpr int WPB = 4;  // one wave per SIMD
 };
 
-template <class Mdl, class T>
-__global__ __launch_bounds__(256, 1) void k_mcmc_resident(const BlockArgs<T> a,
-                                                          const AcceptArgs c,
-                                                          const int64_t iter0,
-                                                          const int64_t n_iter,
-                                                          double* __restrict__ part) {
+// MCMC: n_iter iterations with the in-kernel MH decision (dmt_mcmc_run); otherwise one draw /
+// re-solve in mode MODE (k_block_resident: dmt_draw_proposal, dmt_draw_unit,
+// dmt_recompute_path), ll and success written like k_block_scan.
+template <class Mdl, class T, int MODE, bool MCMC>
+__device__ __forceinline__ void resident_block(const BlockArgs<T>& a, const AcceptArgs& c,
+                                               const int64_t iter0, const int64_t n_iter,
+                                               double* __restrict__ part, const int64_t blk,
+                                               ResLds<Mdl::D, Mdl::M, T>& S) {
   constexpr int D = Mdl::D, M = Mdl::M, HP = D * (D + 1) / 2;
-  static_assert(Mdl::kLinear, "k_mcmc_resident needs a linear drift");
-  __shared__ ResLds<D, M, T> lds[4];
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  static_assert(Mdl::kLinear, "resident_block needs a linear drift");
+  static_assert(!MCMC || MODE == MODE_PCN, "MCMC runs draw pCN proposals");
   const int lane = threadIdx.x & 63;
-  const int64_t blk = a.b0 + (int64_t)blockIdx.x * 4 + w;
-  if (blk >= a.b1) return;
-  ResLds<D, M, T>& S = lds[w];
   const BlkInfo* bi = a.binfo + blk;
   const int64_t tq = ldc(&bi->tq);
   const int g = ldc(&bi->g0);  // the block's only segment (host-checked)
   const int q0 = ldc(&bi->q0);
   const bool term = ldc(&bi->term) != 0;  // a single-segment block: P_last law if non-terminal
-  const T rho = (T)ldc(&bi->rho), srho = (T)ldc(&bi->srho);
+  const T rho = (MODE == MODE_FRESH) ? (T)0 : (T)ldc(&bi->rho);
+  const T srho = (MODE == MODE_FRESH) ? (T)1 : (T)ldc(&bi->srho);
   const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32), c3 = a.salt << 1;
   const int nst = ldc(a.seg_np + g) - 1;  // ≤ kSChunk
   const int64_t row = tq + q0;
@@ -1441,7 +1440,7 @@ __global__ __launch_bounds__(256, 1) void k_mcmc_resident(const BlockArgs<T> a,
 #pragma unroll
     for (int p = 0; p < D; ++p) x0[p] = Xs[p];
 #pragma unroll
-    for (int k = 0; k < M; ++k) w0[k] = Ws[k];
+    for (int k = 0; k < M; ++k) w0[k] = (MODE == MODE_FRESH) ? (T)0 : Ws[k];
 #pragma unroll
     for (int cc = 0; cc < HP; ++cc)
       H0[cc] = a.H_shared[lsp][0] ? a.H[lsp][0][(int64_t)q0 * HP + cc] : a.H[lsp][0][row * HP + cc];
@@ -1470,7 +1469,7 @@ __global__ __launch_bounds__(256, 1) void k_mcmc_resident(const BlockArgs<T> a,
 #pragma unroll
       for (int cc = 0; cc < D; ++cc) Fs[r][cc] = Fb[(int64_t)s * D + cc];
 #pragma unroll
-      for (int k = 0; k < M; ++k) wv[r][k] = Ws[(int64_t)(s + 1) * M + k];
+      for (int k = 0; k < M; ++k) wv[r][k] = (MODE == MODE_FRESH) ? (T)0 : Ws[(int64_t)(s + 1) * M + k];
       T Mg[D * D], zero[D] = {}, e_unused[D];
       guide_coeffs<Mdl, T>(LA, Hs[r], Fs[r], Mg, cgs[r]);
 #ifndef DMT_RES_HF_REGS
@@ -1483,7 +1482,8 @@ __global__ __launch_bounds__(256, 1) void k_mcmc_resident(const BlockArgs<T> a,
     }
   }
   const uint64_t all = 1;
-  double ll = c.ll[blk], llp = 0.0;
+  double ll = MCMC ? c.ll[blk] : 0.0, llp = 0.0;
+  const double* Zg = a.Z ? a.Z + ldc(a.st_off + g) * M : nullptr;  // parity-mode normals
   const int64_t nb = a.b1 - a.b0, j = blk - a.b0;
   const int last_lane = (nst - 1) / kRun;
   double Ev = 0.0;
@@ -1506,7 +1506,7 @@ __global__ __launch_bounds__(256, 1) void k_mcmc_resident(const BlockArgs<T> a,
   // measured slower: 8.46 vs 8.12 µs per C2 iteration — register pressure)
   for (int64_t r0 = 0; r0 < n_iter; ++r0) {
     const int64_t it = iter0 + r0;
-    if ((r0 & 63) == 0)  // Exp(1) draws of the next 64 iterations, one per lane
+    if (MCMC && (r0 & 63) == 0)  // Exp(1) draws of the next 64 iterations, one per lane
       Ev = exp1_draw(c.seed, (uint32_t)g + c.seg_base, (uint32_t)(it + lane), c.salt);
     const double E = __builtin_bit_cast(
         double, ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(
@@ -1518,11 +1518,23 @@ __global__ __launch_bounds__(256, 1) void k_mcmc_resident(const BlockArgs<T> a,
     // ---- normals, pCN increments, e maps; run map
     T dW[kRun][M], e[kRun][D];
     T zc[kRun][M];
-    draw_z((uint32_t)it, zc);
+    if (MODE != MODE_RECOMPUTE) {
+      if (Zg) {
+#pragma unroll
+        for (int r = 0; r < kRun; ++r)
+#pragma unroll
+          for (int kk = 0; kk < M; ++kk)
+            zc[r][kk] = (T)Zg[(int64_t)min(kRun * lane + r, nst - 1) * M + kk];
+      } else {
+        draw_z((uint32_t)it, zc);
+      }
+    }
 #pragma unroll
     for (int r = 0; r < kRun; ++r) {
 #pragma unroll
-      for (int kk = 0; kk < M; ++kk) dW[r][kk] = dfma(rho, wv[r][kk], srho * (sdts[r] * zc[r][kk]));
+      for (int kk = 0; kk < M; ++kk)
+        dW[r][kk] = (MODE == MODE_RECOMPUTE) ? wv[r][kk]
+                                              : dfma(rho, wv[r][kk], srho * (sdts[r] * zc[r][kk]));
       T sdW[D];
       sigma_dw<Mdl, T>(LA, dW[r], sdW);
 #pragma unroll
@@ -1622,7 +1634,7 @@ __global__ __launch_bounds__(256, 1) void k_mcmc_resident(const BlockArgs<T> a,
 #pragma unroll
         for (int kk = 0; kk < M; ++kk) wd[kk] = S.dw[li][kk];
         store_row<D, T>(Xdb + (int64_t)s * D, xv);
-        store_row<M, T>(Wdb + (int64_t)(s + 1) * M, wd);
+        if (MODE != MODE_RECOMPUTE) store_row<M, T>(Wdb + (int64_t)(s + 1) * M, wd);
       }
     }
     T w0n[M];
@@ -1630,13 +1642,20 @@ __global__ __launch_bounds__(256, 1) void k_mcmc_resident(const BlockArgs<T> a,
     for (int k = 0; k < M; ++k) w0n[k] = rho * w0[k];
     if (lane == 0) {
       store_row<D, T>(Xdb + (int64_t)nst * D, xe);
-      store_row<M, T>(Wdb, w0n);
+      if (MODE != MODE_RECOMPUTE) store_row<M, T>(Wdb, w0n);
     }
     wave_lds_sync();
-    // ---- MH decision (k_accept's order), selectors, histories, partials
     bool sok = isfinite(seg_acc);
 #pragma unroll
     for (int p = 0; p < D; ++p) sok = sok && isfinite(xe[p]);
+    if constexpr (!MCMC) {  // one draw / re-solve: ll and success, as k_block_scan
+      if (lane == 0) {
+        a.ll_out[blk] = sok ? (double)(llobs + seg_acc) : -INFINITY;
+        if (a.success) a.success[blk] = sok ? 1 : 0;
+      }
+      return;
+    }
+    // ---- MH decision (k_accept's order), selectors, histories, partials
     llp = sok ? (double)(llobs + seg_acc) : -INFINITY;
     const bool acc = E > -(llp - ll);
     if (acc) {
@@ -1666,12 +1685,37 @@ __global__ __launch_bounds__(256, 1) void k_mcmc_resident(const BlockArgs<T> a,
       llp = t;
     }
   }
-  if (lane == 0) {
+  if (MCMC && lane == 0) {
     a.selX[g] = (uint8_t)sel.x(g);
     a.selW[g] = (uint8_t)sel.w(g);
     c.ll[blk] = ll;
     c.llp[blk] = llp;
   }
+}
+
+template <class Mdl, class T>
+__global__ __launch_bounds__(256, 1) void k_mcmc_resident(const BlockArgs<T> a,
+                                                          const AcceptArgs c,
+                                                          const int64_t iter0,
+                                                          const int64_t n_iter,
+                                                          double* __restrict__ part) {
+  __shared__ ResLds<Mdl::D, Mdl::M, T> lds[4];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t blk = a.b0 + (int64_t)blockIdx.x * 4 + w;
+  if (blk >= a.b1) return;
+  resident_block<Mdl, T, MODE_PCN, true>(a, c, iter0, n_iter, part, blk, lds[w]);
+}
+
+// One draw / re-solve (dmt_draw_proposal, dmt_draw_unit, dmt_recompute_path) of single-segment
+// blocks of at most kSChunk steps (d <= 2) with the resident kernel's run-order arithmetic:
+// no LDS transposition of the step maps, register-local run trees.
+template <class Mdl, class T, int MODE>
+__global__ __launch_bounds__(256, 1) void k_block_resident(const BlockArgs<T> a) {
+  __shared__ ResLds<Mdl::D, Mdl::M, T> lds[4];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t blk = a.b0 + (int64_t)blockIdx.x * 4 + w;
+  if (blk >= a.b1) return;
+  resident_block<Mdl, T, MODE, false>(a, AcceptArgs{}, (int64_t)a.iter, 1, nullptr, blk, lds[w]);
 }
 
 // The fetch_ll tree of every iteration of a k_mcmc_scan run: workgroup r reduces row r of
@@ -2345,6 +2389,18 @@ static hipError_t launch_block_t(int mapping, int mode, const void* args, int64_
   if (nwaves <= 0) return hipSuccess;
   const dim3 grid((unsigned)nwaves);
   if constexpr (Mdl::kLinear) {  // one wave per block, always
+    if constexpr (Mdl::D <= 2) {
+      if (a.resident1) {  // single-segment blocks of <= kSChunk steps: run-order kernel
+        const dim3 rgrid((unsigned)((nwaves + 3) / 4)), rblock(256);
+        switch (mode) {
+          case MODE_PCN: dlaunch(k_block_resident<Mdl, T, MODE_PCN>, rgrid, rblock, s, a); break;
+          case MODE_RECOMPUTE: dlaunch(k_block_resident<Mdl, T, MODE_RECOMPUTE>, rgrid, rblock, s, a); break;
+          case MODE_FRESH: dlaunch(k_block_resident<Mdl, T, MODE_FRESH>, rgrid, rblock, s, a); break;
+          default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+      }
+    }
     constexpr int WPB = ScanCfg<Mdl::D, T>::WPB;
     const dim3 grid((unsigned)((nwaves + WPB - 1) / WPB)), sblock(64 * WPB);
     switch (mode) {

@@ -56,6 +56,7 @@ struct Layout {
   std::vector<int32_t> gfirst, glast, blk_rec;
   std::vector<uint8_t> term;
   bool single_seg = false;  // every block is one segment (the lane kernels' producer/consumer split)
+  int32_t max_steps = 0;    // longest segment of any block (single-segment layouts)
   int64_t* d_blk_off = nullptr;
   BlkInfo* d_binfo = nullptr;
   int32_t* d_blk_rec = nullptr;
@@ -151,6 +152,7 @@ struct dmt_ens {
                              // (when the draw has fewer waves than the device has SIMDs)
   int64_t n_simd = 1024;
   int repair_div = 4;        // MAP_LANE tile-phase repair threshold (DMT_REPAIR_DIV)
+  bool scan_resident = true; // one-shot OU draws on k_block_resident when eligible (DMT_SCAN_RESIDENT=0: off)
   std::vector<std::unique_ptr<Layout>> layouts;  // layouts[0] = internal "unit" layout
   // timing
   uint32_t timing = 0;  // bit k: time kernel class k (dmt_set_timing)
@@ -358,6 +360,7 @@ void fill_common(dmt_ens* h, const Layout* L, BlockArgs<T>& a) {
   a.success = nullptr;
   a.repair_div = h->repair_div;
   a.lane_split = 0;
+  a.resident1 = 0;
 }
 
 dmt_status run_block_kernel(dmt_ens* h, const Layout* L, int mode, int kind_timer, int64_t b0,
@@ -387,6 +390,8 @@ dmt_status run_block_kernel(dmt_ens* h, const Layout* L, int mode, int kind_time
     a.salt = salt;
     a.ll_out = ll_out;
     a.success = success;
+    a.resident1 = h->scan_resident && h->key.model == DMT_MODEL_OU && h->key.d <= 2 &&
+                  L->single_seg && L->max_steps <= kResidentMaxSteps;
     a.lane_split = L->single_seg && (h->lane_split == 1 || (h->lane_split < 0 && nwaves < h->n_simd));
   };
   if (h->key.precision == DMT_F64) {
@@ -452,6 +457,9 @@ dmt_status build_layout(dmt_ens* h, const int32_t* n_blocks, const int32_t* seg_
   }
   L->single_seg = true;
   for (int64_t b = 0; b < L->nblocks && L->single_seg; ++b) L->single_seg = L->gfirst[b] == L->glast[b];
+  L->max_steps = 0;
+  for (int64_t b = 0; b < L->nblocks && L->single_seg; ++b)
+    L->max_steps = std::max(L->max_steps, h->seg_np[L->gfirst[b]] - 1);
   const int64_t nb = L->nblocks;
   DMT_TRY(ens_alloc(h, &L->d_blk_off, h->R + 1));
   DMT_TRY(ens_alloc(h, &L->d_gfirst, nb));
@@ -613,6 +621,7 @@ dmt_status dmt_create(dmt_ens** out, const dmt_model* model, const dmt_structure
   if (const char* e = std::getenv("DMT_MCMC_RESIDENT")) h->resident = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("DMT_LANE_SPLIT")) h->lane_split = std::atoi(e);
   if (const char* e = std::getenv("DMT_REPAIR_DIV")) h->repair_div = std::max(1, std::atoi(e));
+  if (const char* e = std::getenv("DMT_SCAN_RESIDENT")) h->scan_resident = std::strcmp(e, "0") != 0;
   {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, h->device) == hipSuccess)

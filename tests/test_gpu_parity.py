@@ -59,9 +59,14 @@ def test_c1_ou1d_mcmc_bit_exact(mapping):
 
 
 @pytest.mark.parametrize("mapping", MAPPINGS)
-def test_c2_ou2d_ragged_tile_bit_exact(mapping):
-    # 200 blocks: 3 full recording tiles + a partial one
+@pytest.mark.parametrize("resident", ["1", "0"])
+def test_c2_ou2d_ragged_tile_bit_exact(mapping, resident, monkeypatch):
+    # 200 blocks: 3 full recording tiles + a partial one; one-shot draws on k_block_resident
+    # (single-segment blocks of <= 512 steps) and on the general k_block_scan
+    monkeypatch.setenv("DMT_SCAN_RESIDENT", resident)
     run_mcmc_parity(W.c2_ou2d(B=200, N=500), iters=4, mapping=mapping)
+    if resident == "1":
+        run_mcmc_parity(W.c1_ou1d(), iters=3, mapping=mapping)
 
 
 @pytest.mark.parametrize("mapping", MAPPINGS)
@@ -227,7 +232,8 @@ def test_mcmc_run_persistent_paths_equal_step_path(case):
     kind, B, N, n = case
     build = (_c2_build(B, N, n + 1) if kind == "c2" else _c1_build(n + 1) if kind == "c1"
              else _ragged_ou_build(n + 1))
-    (e0, lay, nb), (e1, _, _) = _env_ensembles(build, {"DMT_MCMC_PERSIST": "0"})
+    (e0, lay, nb), (e1, _, _) = _env_ensembles(build, {"DMT_MCMC_PERSIST": "0",
+                                                        "DMT_SCAN_RESIDENT": "0"})
     r0 = e0.mcmc_run(lay, 0, nb, 1, n, salt=7)
     r1 = e1.mcmc_run(lay, 0, nb, 1, n, salt=7)
     assert np.array_equal(r0, r1)
