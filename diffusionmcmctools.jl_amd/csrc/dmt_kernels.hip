@@ -1389,13 +1389,9 @@ template <int D, int M, class T>
 struct ResLds {
   T pt[kSStride][D];  // pre-step points by LDS slot of the step (+ end point)
   T dw[kSStride][M];  // W° increments by LDS slot of the step
-#ifndef DMT_RES_HF_REGS
-  T hf[kRun][D * (D + 1) / 2 + D][64];  // H_i, F_i of each lane's run (G's inputs), lane-minor
-#endif
-};
-template <int D, int M, class T>
-struct ResCfg {
-  static constexpr int WPB = 4;  // one wave per SIMD
+  // H_i, F_i of each lane's run (G's inputs), lane-minor: in LDS rather than registers, which
+  // the run's other constants fill (fewer AGPR round trips, −5 % VALU instructions)
+  T hf[kRun][D * (D + 1) / 2 + D][64];
 };
 
 // MCMC: n_iter iterations with the in-kernel MH decision (dmt_mcmc_run); otherwise one draw /
@@ -1451,9 +1447,6 @@ __device__ __forceinline__ void resident_block(const BlockArgs<T>& a, const Acce
   }
   const int nv = max(0, min(kRun, nst - kRun * lane));  // valid steps of this lane's run
   T Ac[kRun][D * D], cgs[kRun][D], dts[kRun], sdts[kRun], wv[kRun][M];
-#ifdef DMT_RES_HF_REGS
-  T Hs[kRun][HP], Fs[kRun][D];
-#endif
   {
     const T* Ws = a.W[sel.w(g) ^ a.ws_flip] + row * M;
 #pragma unroll
@@ -1461,9 +1454,7 @@ __device__ __forceinline__ void resident_block(const BlockArgs<T>& a, const Acce
       const int s = min(kRun * lane + r, nst - 1);
       dts[r] = tb[s + 1] - tb[s];
       sdts[r] = sqrt(dts[r]);
-#ifndef DMT_RES_HF_REGS
       T Hs[kRun][HP], Fs[kRun][D];
-#endif
 #pragma unroll
       for (int cc = 0; cc < HP; ++cc) Hs[r][cc] = Hb[(int64_t)s * HP + cc];
 #pragma unroll
@@ -1472,12 +1463,10 @@ __device__ __forceinline__ void resident_block(const BlockArgs<T>& a, const Acce
       for (int k = 0; k < M; ++k) wv[r][k] = (MODE == MODE_FRESH) ? (T)0 : Ws[(int64_t)(s + 1) * M + k];
       T Mg[D * D], zero[D] = {}, e_unused[D];
       guide_coeffs<Mdl, T>(LA, Hs[r], Fs[r], Mg, cgs[r]);
-#ifndef DMT_RES_HF_REGS
 #pragma unroll
       for (int cc = 0; cc < HP; ++cc) S.hf[r][cc][lane] = Hs[r][cc];
 #pragma unroll
       for (int cc = 0; cc < D; ++cc) S.hf[r][HP + cc][lane] = Fs[r][cc];
-#endif
       affine_step<D, T>(Mg, cgs[r], dts[r], zero, Ac[r], e_unused);
     }
   }
@@ -1588,16 +1577,12 @@ __device__ __forceinline__ void resident_block(const BlockArgs<T>& a, const Acce
       const int li = lds_ix(kRun * lane + r);
       const bool v = r < nv;
       T rr[D], bb[D];
-#ifdef DMT_RES_HF_REGS
-      const T G = g_at<Mdl, T>(LA, Hs[r], Fs[r], x, rr, bb);
-#else
       T Hr[HP], Fr[D];
 #pragma unroll
       for (int cc = 0; cc < HP; ++cc) Hr[cc] = S.hf[r][cc][lane];
 #pragma unroll
       for (int cc = 0; cc < D; ++cc) Fr[cc] = S.hf[r][HP + cc][lane];
       const T G = g_at<Mdl, T>(LA, Hr, Fr, x, rr, bb);
-#endif
       gl[r] = v ? G * dts[r] : (T)0;
       // branch-free: slots of steps past the segment end are written but never read
 #pragma unroll
