@@ -70,14 +70,37 @@ class SamplingEnsemble:
         ``set_obs`` / ``recompute_guiding_term`` on the device."""
         self.ens.upload_obs(Hobs, Fobs, cobs, artificial_noise)
 
-    def init_paths(self, x0, Z=None, iter=0, salt=0xFFFF):
+    def init_paths(self, x0, Z=None, iter=0, salt=0xFFFF, x0_prior=None, max_tries=1000):
         """``init_paths!`` (src/sampling_unit.jl:83-87) for every recording, then
-        u° ← u (src/sampling_pair.jl:51).  ``x0``: per-recording start points (R × d)."""
-        x0 = np.asarray(x0, dtype=np.float64).reshape(-1, self.model.d)
-        X = np.zeros((self.ens.P, self.model.d))
-        X[self.ens.pt_off[self.ens.rec_seg0[:-1]]] = x0
+        u° ← u (src/sampling_pair.jl:51).  ``x0``: per-recording start points (R × d).
+
+        Like the reference, which repeats ``forward_guide!`` with a fresh ``x0 ~ x0_prior``
+        until it succeeds, a recording whose draw fails is drawn again — with the next device
+        normal stream (``iter + k``) and, when ``x0_prior`` (``k -> start point``) is given, a new
+        start point — up to ``max_tries`` draws (the reference loops without a bound).
+        Parity-mode normals ``Z`` are fixed inputs: no retry.  Returns (ll, success)."""
+        d = self.model.d
+        x0 = np.asarray(x0, dtype=np.float64).reshape(-1, d)
+        starts = self.ens.pt_off[self.ens.rec_seg0[:-1]]
+        X = np.zeros((self.ens.P, d))
+        X[starts] = x0
         self.ens.set_paths(L.U, X=X)
         ll, ok = self.ens.draw_unit(L.U, Z=Z, iter=iter, salt=salt)
+        ll, ok = np.array(ll), np.array(ok)
+        tries = 1
+        while Z is None and not ok.all():
+            if tries >= max_tries:
+                raise RuntimeError(f"init_paths: {int((~ok).sum())} recording(s) still failing "
+                                   f"after {max_tries} draws")
+            if x0_prior is not None:
+                X = self.ens.download_paths(L.U, 0)
+                for r in np.nonzero(~ok)[0]:
+                    X[starts[r]] = np.asarray(x0_prior(tries), dtype=np.float64).reshape(d)
+                self.ens.set_paths(L.U, X=X)
+            for r in np.nonzero(~ok)[0]:
+                llr, okr = self.ens.draw_unit(L.U, int(r), int(r) + 1, iter=iter + tries, salt=salt)
+                ll[r], ok[r] = llr[0], okr[0]
+            tries += 1
         self.ens.set_paths(L.UPROP, X=self.ens.download_paths(L.U, 0),
                            W=self.ens.download_paths(L.U, 1))
         return ll, ok

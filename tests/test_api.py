@@ -179,6 +179,47 @@ def test_param_step_and_set_ll_on_host():
     assert np.ravel(be.recordings[1].blocks[1].ll_prop_history)[2] != -1.0
 
 
+def test_init_paths_retries_failed_recordings():
+    """init_paths! repeats forward_guide! until it succeeds (src/sampling_unit.jl:83-87): a
+    recording whose draw fails is drawn again with the next normal stream (and a new start
+    point from x0_prior), the others are left alone."""
+    case = ragged_case()
+    m = case["model"]
+    eng = orc.OracleEnsemble(m.kind, m.d, m.m, case["n_points"], prec=case["prec"], seed=11)
+    calls = []
+
+    class Flaky:  # fails recording 1's first two draws
+        def __getattr__(self, k):
+            return getattr(eng, k)
+
+        def draw_unit(self, unit, r0=0, r1=None, Z=None, iter=0, salt=0):
+            r1 = eng.R if r1 is None else r1
+            ll, ok = eng.draw_unit(unit, r0, r1, Z=Z, iter=iter, salt=salt)
+            calls.append((r0, r1, iter))
+            ok = np.array(ok)
+            if r0 <= 1 < r1 and sum(1 for c in calls if c[0] <= 1 < c[1]) <= 2:
+                ok[1 - r0] = False
+            return ll, ok
+
+    se = dmt.SamplingEnsemble(m, case["n_points"], _engine=Flaky())
+    se.upload_grid(case["t"])
+    se.set_guiding(case["H"], case["F"], case["laws"], Hb=case["Hb"], Fb=case["Fb"],
+                   lawsb=case["lawsb"])
+    starts = eng.pt_off[eng.rec_seg0[:-1]]
+    x0 = case["X0"][starts]
+    new_x0 = np.array([0.25, -0.5])
+    ll, ok = se.init_paths(x0, iter=5, x0_prior=lambda k: new_x0)
+    assert ok.all()
+    assert calls == [(0, 3, 5), (1, 2, 6), (1, 2, 7)]
+    X = eng.download_paths(L.U, 0)
+    np.testing.assert_array_equal(X[starts[1]], new_x0)
+    np.testing.assert_array_equal(X[starts[0]], x0[0])
+    np.testing.assert_array_equal(eng.download_paths(L.UPROP, 0), X)
+    with pytest.raises(RuntimeError):
+        calls.clear()
+        se.init_paths(x0, iter=5, max_tries=2)
+
+
 def test_swaps_and_set_accepted():
     case = ragged_case()
     se = _sampling_ensemble(case, "oracle")
