@@ -224,44 +224,126 @@ DMT_HD void transition(const Mat<N>& B, const double* beta, const Mat<N>& At, do
     for (int j = i + 1; j < n; ++j) { const double v = 0.5 * (K(i, j) + K(j, i)); K(i, j) = v; K(j, i) = v; }
 }
 
-// One backward step of the filter: (H, F, c) at t_{i+1} -> at t_i over the step h.
+// Transition (Phi, mu, K) of the auxiliary law over one step or a run of steps.
+template <int N>
+struct Trans {
+  Mat<N> Phi;
+  double mu[N];
+  Mat<N> K;
+};
+
+template <int N>
+DMT_HD Trans<N> step_trans(const Mat<N>& B, const double* beta, const Mat<N>& A, double h) {
+  Trans<N> r;
+  transition(B, beta, A, h, r.Phi, r.mu, r.K);
+  return r;
+}
+
+// The transition over `f` then `s`: (Phi_s Phi_f, Phi_s mu_f + mu_s, Phi_s K_f Phi_s' + K_s).
+template <int N>
+DMT_HD Trans<N> compose(const Trans<N>& f, const Trans<N>& s) {
+  constexpr int n = N;
+  Trans<N> r;
+  r.Phi = mmul(s.Phi, f.Phi);
+  double m[N];
+  mvec(s.Phi, f.mu, m);
+#pragma unroll
+  for (int i = 0; i < n; ++i) r.mu[i] = m[i] + s.mu[i];
+  r.K = madd(mmul(mmul(s.Phi, f.K), mT(s.Phi)), s.K);
+#pragma unroll
+  for (int i = 0; i < n; ++i)
+#pragma unroll
+    for (int j = i + 1; j < n; ++j) { const double v = 0.5 * (r.K(i, j) + r.K(j, i)); r.K(i, j) = v; r.K(j, i) = v; }
+  return r;
+}
+
+// The guiding term (H, F, c) at the start of a transition q from the one at its end:
+// the Gaussian integral over X_end ~ N(Phi x + mu, K) of exp(-c - x'Hx/2 + F'x).
 // Returns false if I + HK is singular.
 template <int N>
-DMT_HD bool filter_step(const Mat<N>& B, const double* beta, const Mat<N>& A, double h,
-                        Mat<N>& Hc, double* Fc, double& cc) {
+DMT_HD bool filter_combine(const Trans<N>& q, Mat<N>& Hc, double* Fc, double& cc) {
   constexpr int d = N;
-  Mat<N> Phi, K;
-  double mu[N];
-  transition(B, beta, A, h, Phi, mu, K);
-  // Gaussian integral over X_{t+h} ~ N(Phi x + mu, K) of exp(-c - x'Hx/2 + F'x)
+  const Mat<N>& Phi = q.Phi;
+  const Mat<N>& K = q.K;
+  const double* mu = q.mu;
   const Mat<N> IHK = madd(meye<N>(), mmul(Hc, K));
   Mat<N> S;
   double lad;
   if (!minv(IHK, S, lad)) return false;
   Mat<N> Hh = mmul(S, Hc);
+#pragma unroll
   for (int p = 0; p < d; ++p)
-    for (int q = p + 1; q < d; ++q) { const double v = 0.5 * (Hh(p, q) + Hh(q, p)); Hh(p, q) = v; Hh(q, p) = v; }
+#pragma unroll
+    for (int r = p + 1; r < d; ++r) { const double v = 0.5 * (Hh(p, r) + Hh(r, p)); Hh(p, r) = v; Hh(r, p) = v; }
   double Fh[N], KF[N];
   mvec(S, Fc, Fh);
   mvec(K, Fc, KF);
   double fkf = 0.0;
+#pragma unroll
   for (int p = 0; p < d; ++p) fkf += Fh[p] * KF[p];
   const double ch = cc + 0.5 * lad - 0.5 * fkf;
   double Hmu[N];
   mvec(Hh, mu, Hmu);
   double g[N];
+#pragma unroll
   for (int p = 0; p < d; ++p) g[p] = Fh[p] - Hmu[p];
   const Mat<N> PhT = mT(Phi);
   double Fn[N];
   mvec(PhT, g, Fn);
   Mat<N> Hn = mmul(mmul(PhT, Hh), Phi);
+#pragma unroll
   for (int p = 0; p < d; ++p)
-    for (int q = p + 1; q < d; ++q) { const double v = 0.5 * (Hn(p, q) + Hn(q, p)); Hn(p, q) = v; Hn(q, p) = v; }
+#pragma unroll
+    for (int r = p + 1; r < d; ++r) { const double v = 0.5 * (Hn(p, r) + Hn(r, p)); Hn(p, r) = v; Hn(r, p) = v; }
   double fmu = 0.0, muHmu = 0.0;
+#pragma unroll
   for (int p = 0; p < d; ++p) { fmu += Fh[p] * mu[p]; muHmu += mu[p] * Hmu[p]; }
   cc = ch - fmu + 0.5 * muHmu;
   Hc = Hn;
+#pragma unroll
   for (int p = 0; p < d; ++p) Fc[p] = Fn[p];
+  return true;
+}
+
+// The canonical chunked filter of one segment.  The steps are cut into chunks
+// of kFiltChunk counted from the segment end; inside a chunk, every step's transition is
+// composed with the rest of the chunk by an inclusive Kogge–Stone suffix scan (stage k: step l
+// takes compose(Q_l, Q_{l+k}) when l + k < cnt, from the previous stage's values), and every
+// point of the chunk gets its (H, F, c) by one filter_combine from the chunk end's guiding
+// term; the chunk's first point is the next chunk's end.  The device runs a chunk on one wave
+// (k_filter_scan / k_filter_chain); this is the serial host statement of the same arithmetic.
+constexpr int kFiltChunk = 64;
+
+template <int N, class TimeAt, class Store>
+inline bool filter_segment(const Mat<N>& B, const double* beta, const Mat<N>& A, int npts,
+                           TimeAt tat, Mat<N>& Hc, double* Fc, double& cc, Store store) {
+  store(npts - 1, Hc, Fc, cc);
+  Trans<N> Q[kFiltChunk], Qn[kFiltChunk];
+  for (int hi = npts - 1; hi > 0; hi -= kFiltChunk) {
+    const int lo = hi > kFiltChunk ? hi - kFiltChunk : 0, cnt = hi - lo;
+    for (int l = 0; l < cnt; ++l) Q[l] = step_trans(B, beta, A, tat(lo + l + 1) - tat(lo + l));
+    for (int k = 1; k < kFiltChunk; k *= 2) {
+      for (int l = 0; l < cnt; ++l) Qn[l] = (l + k < cnt) ? compose(Q[l], Q[l + k]) : Q[l];
+      for (int l = 0; l < cnt; ++l) Q[l] = Qn[l];
+    }
+    const Mat<N> H0 = Hc;
+    double F0[N];
+    for (int p = 0; p < N; ++p) F0[p] = Fc[p];
+    const double c0 = cc;
+    for (int l = cnt - 1; l >= 0; --l) {
+      Mat<N> H = H0;
+      double F[N];
+      for (int p = 0; p < N; ++p) F[p] = F0[p];
+      double c = c0;
+      if (!filter_combine(Q[l], H, F, c)) return false;
+      store(lo + l, H, F, c);
+      if (l == 0) {
+        Hc = H;
+        for (int p = 0; p < N; ++p) Fc[p] = F[p];
+        cc = c;
+      }
+    }
+  }
   return true;
 }
 

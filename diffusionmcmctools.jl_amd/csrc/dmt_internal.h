@@ -143,7 +143,16 @@ struct FilterArgs {
   double art_eps;      // its variance (artificial_noise)
   int* fail;           // set to 1 if a filter step is singular
   const uint8_t* only;  // [nblocks] nullable: filter only the blocks flagged here
+  // chunked filter: one batch of blocks [b0, b1) covering segments [gA, gB]
+  const int64_t* pt_off;      // [G] first point of each segment
+  const int64_t* fchunk_off;  // [G + 1] prefix of the segments' chunk counts
+  uint8_t* segsel;            // [G] 0 skip, 1 PP, 2 PPb (k_filter_mark)
+  double* qbuf;               // [kFiltNQ(d)][qcap] composed transitions, point p at p − pA
+  int64_t qcap, pA;
+  int32_t gA, gB;
+  int64_t fchunk_off_h0, fchunk_off_h1;  // fchunk_off[gA], fchunk_off[gB + 1] (host copies)
 };
+constexpr int kFiltNQ(int d) { return d * d + d + d * (d + 1) / 2; }
 
 // set_proposal_law! on the device (k_set_prop_law): one thread per block.
 constexpr int kMaxParams = 16;
@@ -180,6 +189,8 @@ hipError_t launch_accept(const AcceptArgs& a, hipStream_t s);
 // (resident: every block is one segment of ≤ kResidentMaxSteps steps and d ≤ 2 —
 // k_mcmc_resident keeps the block's state in registers for the whole run)
 constexpr int kPersistMaxSegments = 64;
+// points per batch of the chunked device filter (its transition scratch: kFiltNQ(d) doubles each)
+constexpr int64_t kFiltBatchPoints = int64_t(1) << 24;
 constexpr int kResidentMaxSteps = 512;
 hipError_t launch_mcmc_persistent(const ModelKey& k, const void* args, const AcceptArgs& c,
                                   int64_t iter0, int64_t n_iter, double* part, int64_t nwaves,

@@ -1977,37 +1977,183 @@ __global__ __launch_bounds__(kAccGroup) void k_accept_reduce_lb(const AcceptArgs
 }
 
 // ---------------------------------------------------------------- guiding term on the device
-// recompute_guiding_term!(b) for linear auxiliary laws (src/block.jl:102-110; the exact
-// discrete filter of dmt_filter.h, identical to the host dmt_guiding_linear): one thread per
-// block, segments backward from the block end; the last segment of a non-terminal block uses
-// its PPb law with the artificial end observation frozen by set_obs!.
-template <class T, int D>
-__global__ __launch_bounds__(64) void k_backward_filter(const FilterArgs a) {
+// recompute_guiding_term!(b) for linear auxiliary laws (src/block.jl:102-110), in the
+// canonical chunked form of dmt_filter.h (identical to the host
+// dmt_guiding_linear).  Three launches per batch of blocks:
+//   k_filter_mark   which law (PP / PPb of a non-terminal block's last segment) each segment uses
+//   k_filter_scan   one wave per 64-step chunk: the step transitions, their suffix scan → qbuf
+//                   (independent of the guiding terms, so every chunk of every block in parallel)
+//   k_filter_chain  one wave per block: segments backward from the block end, chunks backward
+//                   within a segment; all points of a chunk combine in parallel from the chunk
+//                   end's guiding term, lane 0's result is the next chunk's end
+// The last segment of a non-terminal block uses its PPb law with the artificial end
+// observation frozen by set_obs!.
+__global__ void k_filter_mark(const FilterArgs a) {
   const int64_t blk = a.b0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (blk >= a.b1) return;
+  const int g0 = a.gfirst[blk], g1 = a.glast[blk];
+  const bool on = !a.only || a.only[blk];
+  const bool term = a.term[blk] != 0;
+  for (int g = g0; g <= g1; ++g) a.segsel[g] = on ? ((!term && g == g1) ? 2 : 1) : 0;
+}
+
+template <int D>
+__device__ __forceinline__ void filt_law(const FilterArgs& a, int g, int kind, flt::Mat<D>& B,
+                                         double* beta, flt::Mat<D>& At, int& slot) {
+  slot = (kind ? a.selPPB[g] : a.selPP[g]) ^ a.unit;
+  const double* lr = a.law[slot][kind] + (int64_t)g * DMT_LAW_STRIDE;
+#pragma unroll
+  for (int p = 0; p < D; ++p) {
+    beta[p] = lr[DMT_LAW_BETA + p];
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+      B(p, q) = lr[DMT_LAW_BT + p * D + q];
+      const int e = flt::packed_ix(D, p, q);
+      At(p, q) = lr[DMT_LAW_A + e] - lr[DMT_LAW_DA + e];  // ã = a − (a − ã)
+    }
+  }
+}
+
+// chunk j of a segment with np points: steps [lo, lo + cnt), counted from the segment end
+__device__ __forceinline__ void filt_chunk(int np, int j, int& lo, int& cnt) {
+  const int hi = (np - 1) - flt::kFiltChunk * j;
+  lo = hi > flt::kFiltChunk ? hi - flt::kFiltChunk : 0;
+  cnt = hi - lo;
+}
+__device__ __forceinline__ int filt_nchunks(int np) {
+  return (np - 1 + flt::kFiltChunk - 1) / flt::kFiltChunk;
+}
+
+template <int D>
+__device__ __forceinline__ flt::Trans<D> shfl_down_trans(const flt::Trans<D>& x, int k) {
+  flt::Trans<D> r;
+#pragma unroll
+  for (int i = 0; i < D * D; ++i) {
+    r.Phi.a[i] = __shfl_down(x.Phi.a[i], k, 64);
+    r.K.a[i] = __shfl_down(x.K.a[i], k, 64);
+  }
+#pragma unroll
+  for (int i = 0; i < D; ++i) r.mu[i] = __shfl_down(x.mu[i], k, 64);
+  return r;
+}
+
+template <class T, int D>
+__global__ __launch_bounds__(256) void k_filter_scan(const FilterArgs a, int64_t item0,
+                                                     int64_t item1) {
+  const int lane = threadIdx.x & 63;
+  const int64_t item = item0 + (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (item >= item1) return;
+  int lo_g = a.gA, hi_g = a.gB + 1;  // largest g with fchunk_off[g] <= item
+  while (hi_g - lo_g > 1) {
+    const int mid = (lo_g + hi_g) >> 1;
+    if (a.fchunk_off[mid] <= item) lo_g = mid; else hi_g = mid;
+  }
+  const int g = lo_g;
+  const int sel = a.segsel[g];
+  if (!sel) return;
+  flt::Mat<D> B, At;
+  double beta[D];
+  int slot;
+  filt_law<D>(a, g, sel - 1, B, beta, At, slot);
+  int lo, cnt;
+  filt_chunk(a.seg_np[g], (int)(item - a.fchunk_off[g]), lo, cnt);
+  const int64_t r = a.seg_rec[g];
+  const int64_t tq = a.tile_qoff[r / a.tw] + a.seg_q[g];
+  const int rl = (int)(r % a.tw);
+  const T* tt = (const T*)a.t;
+  auto tat = [&](int i) -> double {
+    return a.t_shared ? (double)tt[a.seg_q[g] + i] : (double)tt[(tq + i) * a.tw + rl];
+  };
+  flt::Trans<D> q;
+  if (lane < cnt) {
+    q = flt::step_trans<D>(B, beta, At, tat(lo + lane + 1) - tat(lo + lane));
+  } else {
+    q.Phi = flt::meye<D>();
+    q.K = flt::mzero<D>();
+#pragma unroll
+    for (int i = 0; i < D; ++i) q.mu[i] = 0.0;
+  }
+#pragma unroll
+  for (int k = 1; k < flt::kFiltChunk; k *= 2) {
+    const flt::Trans<D> o = shfl_down_trans<D>(q, k);
+    if (lane + k < cnt) q = flt::compose<D>(q, o);
+  }
+  if (lane < cnt) {
+    const int64_t p = a.pt_off[g] + lo + lane - a.pA;
+    double* Q = a.qbuf + p;
+    int c = 0;
+#pragma unroll
+    for (int i = 0; i < D * D; ++i) Q[(c++) * a.qcap] = q.Phi.a[i];
+#pragma unroll
+    for (int i = 0; i < D; ++i) Q[(c++) * a.qcap] = q.mu[i];
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int j = i; j < D; ++j) Q[(c++) * a.qcap] = q.K(i, j);
+  }
+}
+
+template <class T, int D>
+__global__ __launch_bounds__(64) void k_filter_chain(const FilterArgs a) {
+  const int64_t blk = a.b0 + blockIdx.x;
   if (blk >= a.b1) return;
   if (a.only && !a.only[blk]) return;
   constexpr int d = D, hp = d * (d + 1) / 2;
+  const int lane = threadIdx.x;
   const int g0 = a.gfirst[blk], g1 = a.glast[blk];
   const bool term = a.term[blk] != 0;
   using M = flt::Mat<D>;
+  auto loadq = [&](int g, int j) {
+    flt::Trans<D> q;
+    int lo, cnt;
+    filt_chunk(a.seg_np[g], j, lo, cnt);
+    if (lane < cnt) {
+      const double* Q = a.qbuf + (a.pt_off[g] + lo + lane - a.pA);
+      int c = 0;
+#pragma unroll
+      for (int i = 0; i < D * D; ++i) q.Phi.a[i] = Q[(c++) * a.qcap];
+#pragma unroll
+      for (int i = 0; i < D; ++i) q.mu[i] = Q[(c++) * a.qcap];
+#pragma unroll
+      for (int i = 0; i < D; ++i)
+#pragma unroll
+        for (int j2 = i; j2 < D; ++j2) { const double v = Q[(c++) * a.qcap]; q.K(i, j2) = v; q.K(j2, i) = v; }
+    } else {
+      q.Phi = flt::meye<D>();
+      q.K = flt::mzero<D>();
+#pragma unroll
+      for (int i = 0; i < D; ++i) q.mu[i] = 0.0;
+    }
+    return q;
+  };
+  // prefetch cursor over the block's chunks in processing order (segments backward, chunks
+  // backward in time within a segment): the loads do not depend on the chain
+  int pg = g1, pj = 0;
+  auto norm = [&]() { while (pg >= g0 && pj >= filt_nchunks(a.seg_np[pg])) { --pg; pj = 0; } };
+  norm();
+  flt::Trans<D> qnext;
+  if (pg >= g0) qnext = loadq(pg, pj);
   M Hc = flt::mzero<D>();
   double Fc[D], cc = 0.0;
+#pragma unroll
   for (int p = 0; p < d; ++p) Fc[p] = 0.0;
   for (int g = g1; g >= g0; --g) {
     const int kind = (!term && g == g1) ? 1 : 0;
     const int slot = (kind ? a.selPPB[g] : a.selPP[g]) ^ a.unit;
-    const double* lr = a.law[slot][kind] + (int64_t)g * DMT_LAW_STRIDE;
     // terminal information of the segment: its observation (+ the artificial one of a
     // P_last segment, or + the guiding term at the start of the next segment of the block)
     M HT = flt::mzero<D>();
     double FT[D], cT = a.obsc[g];
+#pragma unroll
     for (int p = 0; p < d; ++p) {
       FT[p] = a.obsF[(int64_t)g * d + p];
+#pragma unroll
       for (int q = 0; q < d; ++q) HT(p, q) = a.obsH[(int64_t)g * hp + flt::packed_ix(d, p, q)];
     }
     if (kind == 1) {
       const double inv = 1.0 / a.art_eps;
       double vv = 0.0;
+#pragma unroll
       for (int p = 0; p < d; ++p) {
         const double v = a.obsv[(int64_t)g * d + p];
         HT(p, p) += inv;
@@ -2017,43 +2163,57 @@ __global__ __launch_bounds__(64) void k_backward_filter(const FilterArgs a) {
       cT += 0.5 * inv * vv + 0.5 * d * (0x1.d67f1c864beb4p+0 + flt::flt_log(a.art_eps));
     } else if (g < g1) {
       HT = flt::madd(HT, Hc);
+#pragma unroll
       for (int p = 0; p < d; ++p) FT[p] += Fc[p];
       cT += cc;
     }
-    M B = flt::mzero<D>(), At = flt::mzero<D>();
-    double beta[D];
-    for (int p = 0; p < d; ++p) {
-      beta[p] = lr[DMT_LAW_BETA + p];
-      for (int q = 0; q < d; ++q) {
-        B(p, q) = lr[DMT_LAW_BT + p * d + q];
-        const int e = flt::packed_ix(d, p, q);
-        At(p, q) = lr[DMT_LAW_A + e] - lr[DMT_LAW_DA + e];  // ã = a − (a − ã)
-      }
-    }
     const int64_t r = a.seg_rec[g];
     const int64_t tq = a.tile_qoff[r / a.tw];
-    const int lane = (int)(r % a.tw);
-    auto ix = [&](int64_t q, int c, int C) -> int64_t { return ((tq + q) * C + c) * a.tw + lane; };
-    const T* tt = (const T*)a.t;
+    const int rl = (int)(r % a.tw);
+    auto ix = [&](int64_t q, int c, int C) -> int64_t { return ((tq + q) * C + c) * a.tw + rl; };
     const int64_t q0 = a.seg_q[g];
     const int np = a.seg_np[g];
-    auto tat = [&](int i) -> double { return a.t_shared ? (double)tt[q0 + i] : (double)tt[ix(q0 + i, 0, 1)]; };
     T* Ht = (T*)a.H[slot][kind];
     T* Ft = (T*)a.F[slot][kind];
     Hc = HT;
+#pragma unroll
     for (int p = 0; p < d; ++p) Fc[p] = FT[p];
     cc = cT;
-    auto store = [&](int i) {
+    auto store = [&](int i, const M& Hs, const double* Fs) {
+#pragma unroll
       for (int p = 0; p < d; ++p)
-        for (int q = p; q < d; ++q) Ht[ix(q0 + i, flt::packed_ix(d, p, q), hp)] = (T)Hc(p, q);
-      for (int p = 0; p < d; ++p) Ft[ix(q0 + i, p, d)] = (T)Fc[p];
+#pragma unroll
+        for (int q = p; q < d; ++q) Ht[ix(q0 + i, flt::packed_ix(d, p, q), hp)] = (T)Hs(p, q);
+#pragma unroll
+      for (int p = 0; p < d; ++p) Ft[ix(q0 + i, p, d)] = (T)Fs[p];
     };
-    store(np - 1);
-    for (int i = np - 2; i >= 0; --i) {
-      if (!flt::filter_step(B, beta, At, tat(i + 1) - tat(i), Hc, Fc, cc)) { *a.fail = 1; return; }
-      store(i);
+    if (lane == 0) store(np - 1, Hc, Fc);
+    const int nch = filt_nchunks(np);
+    for (int j = 0; j < nch; ++j) {
+      const flt::Trans<D> qcur = qnext;
+      ++pj;
+      norm();
+      if (pg >= g0) qnext = loadq(pg, pj);
+      int lo, cnt;
+      filt_chunk(np, j, lo, cnt);
+      M H = Hc;
+      double F[D], c = cc;
+#pragma unroll
+      for (int p = 0; p < d; ++p) F[p] = Fc[p];
+      const bool ok = lane >= cnt || flt::filter_combine<D>(qcur, H, F, c);
+      if (__ballot(!ok) != 0) {
+        if (lane == 0) *a.fail = 1;
+        return;
+      }
+      if (lane < cnt) store(lo + lane, H, F);
+      // lane 0 holds the chunk's first point: the next chunk's end
+#pragma unroll
+      for (int i = 0; i < d * d; ++i) Hc.a[i] = __shfl(H.a[i], 0, 64);
+#pragma unroll
+      for (int p = 0; p < d; ++p) Fc[p] = __shfl(F[p], 0, 64);
+      cc = __shfl(c, 0, 64);
     }
-    a.law[slot][kind][(int64_t)g * DMT_LAW_STRIDE + DMT_LAW_C0] = cc;
+    if (lane == 0) a.law[slot][kind][(int64_t)g * DMT_LAW_STRIDE + DMT_LAW_C0] = cc;
   }
 }
 
@@ -2070,19 +2230,26 @@ __global__ __launch_bounds__(64) void k_backward_filter(const FilterArgs a) {
 // crit[blk] = 1 when a record the backward filter uses for this block (PP, or PPb of a
 // non-terminal block's last segment) has a different auxiliary law (B̃, β̃, ã = a − (a − ã))
 // afterwards.
-__device__ void write_params(const ParamArgs& a, double* r) {
+// r[DMT_LAW_THETA + p] = v with static indices only (r stays in registers)
+__device__ __forceinline__ void put_theta(double* r, int p, double v) {
+#pragma unroll
+  for (int q = 0; q < 12; ++q)
+    if (q == p) r[DMT_LAW_THETA + q] = v;
+}
+
+__device__ __forceinline__ void write_params(const ParamArgs& a, double* r) {
   for (int k = 0; k < a.n; ++k) {
     const int p = a.idx[k];
     const double v = a.val[k];
     if (a.model == DMT_MODEL_FHN) {
       if (p == DMT_PAR_FHN_EPS) { r[DMT_LAW_THETA + 4] = v; r[DMT_LAW_THETA + 0] = 1.0 / v; }
       else if (p == DMT_PAR_FHN_SIGMA) r[DMT_LAW_THETA + 5] = v;
-      else r[DMT_LAW_THETA + p] = v;
+      else put_theta(r, p, v);
     } else if (a.model == DMT_MODEL_LORENZ) {
-      r[DMT_LAW_THETA + p] = v;
+      put_theta(r, p, v);
     } else {
       const int dd = a.d * a.d;
-      r[DMT_LAW_THETA + (p < dd ? p : 9 + (p - dd))] = v;
+      put_theta(r, p < dd ? p : 9 + (p - dd), v);
     }
   }
   if (a.model == DMT_MODEL_FHN) {
@@ -2118,34 +2285,44 @@ __device__ void write_params(const ParamArgs& a, double* r) {
   }
 }
 
-__global__ void k_set_prop_law(const ParamArgs a) {
-  const int64_t blk = a.b0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// one thread per block, or (wg_per_block, for few blocks with many segments) one workgroup per
+// block with its threads over the block's (segment, law kind) records
+__global__ __launch_bounds__(64) void k_set_prop_law(const ParamArgs a, int wg_per_block) {
+  const int64_t blk = wg_per_block ? a.b0 + blockIdx.x : a.b0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (blk >= a.b1) return;
   const int g0 = a.gfirst[blk], g1 = a.glast[blk];
   const bool term = a.term[blk] != 0;
   bool changed = false;
   constexpr int kAux0 = DMT_LAW_A, kAux1 = DMT_LAW_TRACE + 1;  // a, B̃, β̃, a − ã, (c0), trace
-  for (int g = g0; g <= g1; ++g)
-    for (int kind = 0; kind < 2; ++kind) {
-      if (!a.law[0][kind]) continue;
-      const int s = kind ? a.selPPB[g] : a.selPP[g];
-      const double* src = a.law[s][kind] + (int64_t)g * DMT_LAW_STRIDE;
-      double* dst = a.law[s ^ 1][kind] + (int64_t)g * DMT_LAW_STRIDE;
-      double old[kAux1 - kAux0];
+  const int r0 = wg_per_block ? (int)threadIdx.x : 0, st = wg_per_block ? (int)blockDim.x : 1;
+  for (int rr = r0; rr < 2 * (g1 - g0 + 1); rr += st) {
+    const int g = g0 + (rr >> 1), kind = rr & 1;
+    if (!a.law[0][kind]) continue;
+    const int s = kind ? a.selPPB[g] : a.selPP[g];
+    const double* __restrict__ src = a.law[s][kind] + (int64_t)g * DMT_LAW_STRIDE;
+    double* __restrict__ dst = a.law[s ^ 1][kind] + (int64_t)g * DMT_LAW_STRIDE;
+    double old[kAux1 - kAux0], rec[DMT_LAW_STRIDE];
 #pragma unroll
-      for (int i = kAux0; i < kAux1; ++i) old[i - kAux0] = dst[i];
-      const double c0 = dst[DMT_LAW_C0];
-      for (int i = 0; i < DMT_LAW_STRIDE; ++i) dst[i] = src[i];
-      dst[DMT_LAW_C0] = c0;
-      write_params(a, dst);
-      const bool used = kind == ((!term && g == g1) ? 1 : 0);
-      if (used) {
+    for (int i = kAux0; i < kAux1; ++i) old[i - kAux0] = dst[i];
+    const double c0 = dst[DMT_LAW_C0];
 #pragma unroll
-        for (int i = kAux0; i < kAux1; ++i)
-          if (i != DMT_LAW_C0 && __double_as_longlong(old[i - kAux0]) != __double_as_longlong(dst[i]))
-            changed = true;
-      }
+    for (int i = 0; i < DMT_LAW_STRIDE; ++i) rec[i] = src[i];
+    rec[DMT_LAW_C0] = c0;
+    write_params(a, rec);
+#pragma unroll
+    for (int i = 0; i < DMT_LAW_STRIDE; ++i) dst[i] = rec[i];
+    const bool used = kind == ((!term && g == g1) ? 1 : 0);
+    if (used) {
+#pragma unroll
+      for (int i = kAux0; i < kAux1; ++i)
+        if (i != DMT_LAW_C0 && __double_as_longlong(old[i - kAux0]) != __double_as_longlong(rec[i]))
+          changed = true;
     }
+  }
+  if (wg_per_block) {
+    changed = __syncthreads_or(changed ? 1 : 0) != 0;
+    if (threadIdx.x != 0) return;
+  }
   a.crit[blk] = changed ? 1 : 0;
   if (changed) atomicAdd(a.ncrit, 1u);
 }
@@ -2168,12 +2345,22 @@ __global__ void k_set_obs(int tw, int d, const T* X0, const T* X1, const uint8_t
 }
 
 // ---------------------------------------------------------------- small utility kernels
-__global__ void k_flip(uint8_t* sel, const int32_t* gfirst, const int32_t* glast,
-                       const uint8_t* term, int only_nonterm, int64_t b0, int64_t b1) {
-  const int64_t blk = b0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+struct FlipArgs {
+  uint8_t* sel[4];
+  int only_nonterm[4];
+};
+// selector flips of blocks [b0, b1): one thread per block, or (wg_per_block, for few blocks
+// with many segments) one workgroup per block striding over its segments
+__global__ void k_flip(const FlipArgs f, const int32_t* gfirst, const int32_t* glast,
+                       const uint8_t* term, int64_t b0, int64_t b1, int wg_per_block) {
+  const int64_t blk = wg_per_block ? b0 + blockIdx.x : b0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (blk >= b1) return;
-  if (only_nonterm && term[blk]) return;
-  for (int g = gfirst[blk]; g <= glast[blk]; ++g) sel[g] ^= 1;
+  const int gs = wg_per_block ? (int)threadIdx.x : 0, st = wg_per_block ? (int)blockDim.x : 1;
+  const bool tm = term[blk] != 0;
+  for (int g = gfirst[blk] + gs; g <= glast[blk]; g += st)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (f.sel[i] && !(f.only_nonterm[i] && tm)) f.sel[i][g] ^= 1;
 }
 
 __global__ void k_swap_ll(double* ll, double* llp, int64_t b0, int64_t b1) {
@@ -2344,6 +2531,9 @@ __global__ void k_debug_philox(uint64_t seed, const uint32_t* ctr, int64_t n, ui
 
 // ---------------------------------------------------------------- launchers
 static inline unsigned nblk(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
+// block counts up to which the per-block utility kernels run one workgroup per block (the
+// segments of a block in parallel) instead of one thread per block
+constexpr int64_t kFewBlocks = 2048;
 
 thread_local DispatchEvents g_dispatch_events;
 
@@ -2639,8 +2829,16 @@ hipError_t launch_pathll_kernel(const ModelKey& k, int mapping, const void* args
 hipError_t launch_backward_filter(int precision, const FilterArgs& a, hipStream_t s) {
   const int64_t n = a.b1 - a.b0;
   if (n <= 0) return hipSuccess;
-  // one thread per block, 64-thread workgroups: spread the (few) waves over all CUs
-#define DMT_FILTER_LAUNCH(T, D) dlaunch(k_backward_filter<T, D>, dim3(nblk(n, 64)), dim3(64), s, a)
+  hipLaunchKernelGGL(k_filter_mark, dim3(nblk(n, 64)), dim3(64), 0, s, a);
+  // the host copies of fchunk_off bound the scan's work items: passed in via qbuf's batch
+  const int64_t item0 = a.fchunk_off_h0, item1 = a.fchunk_off_h1;
+#define DMT_FILTER_LAUNCH(T, D)                                                                \
+  do {                                                                                         \
+    if (item1 > item0)                                                                         \
+      hipLaunchKernelGGL((k_filter_scan<T, D>), dim3(nblk(item1 - item0, 4)), dim3(256), 0, s, \
+                         a, item0, item1);                                                     \
+    hipLaunchKernelGGL((k_filter_chain<T, D>), dim3(n), dim3(64), 0, s, a);                    \
+  } while (0)
   if (precision == DMT_F64) {
     if (a.d == 1) DMT_FILTER_LAUNCH(double, 1);
     else if (a.d == 2) DMT_FILTER_LAUNCH(double, 2);
@@ -2657,7 +2855,10 @@ hipError_t launch_backward_filter(int precision, const FilterArgs& a, hipStream_
 hipError_t launch_set_prop_law(const ParamArgs& a, hipStream_t s) {
   const int64_t n = a.b1 - a.b0;
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_set_prop_law, dim3(nblk(n, 64)), dim3(64), 0, s, a);
+  if (n <= kFewBlocks)
+    hipLaunchKernelGGL(k_set_prop_law, dim3((unsigned)n), dim3(64), 0, s, a, 1);
+  else
+    hipLaunchKernelGGL(k_set_prop_law, dim3(nblk(n, 64)), dim3(64), 0, s, a, 0);
   return hipGetLastError();
 }
 
@@ -2819,12 +3020,12 @@ hipError_t launch_flip(uint8_t* sel0, uint8_t* sel1, uint8_t* sel2, uint8_t* sel
                        int32_t swap_ppb_nonterm_only, int64_t b0, int64_t b1, hipStream_t s) {
   const int64_t n = b1 - b0;
   if (n <= 0) return hipSuccess;
-  uint8_t* sels[4] = {sel0, sel1, sel2, sel3};
-  for (int i = 0; i < 4; ++i) {
-    if (!sels[i]) continue;
-    const int only_nonterm = (i == 3) ? swap_ppb_nonterm_only : 0;
-    k_flip<<<nblk(n, 256), 256, 0, s>>>(sels[i], gfirst, glast, term, only_nonterm, b0, b1);
-  }
+  FlipArgs f{{sel0, sel1, sel2, sel3}, {0, 0, 0, swap_ppb_nonterm_only}};
+  if (!sel0 && !sel1 && !sel2 && !sel3) return hipSuccess;
+  if (n <= kFewBlocks)
+    k_flip<<<(unsigned)n, 64, 0, s>>>(f, gfirst, glast, term, b0, b1, 1);
+  else
+    k_flip<<<nblk(n, 256), 256, 0, s>>>(f, gfirst, glast, term, b0, b1, 0);
   return hipGetLastError();
 }
 

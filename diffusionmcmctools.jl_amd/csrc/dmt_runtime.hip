@@ -129,6 +129,12 @@ struct dmt_ens {
   double* d_obsc = nullptr;  // [G]
   double* d_obsv = nullptr;  // [G][d] artificial observations of P_last segments
   int* d_fail = nullptr;
+  // chunked device filter (k_filter_*): chunk prefix per segment, segment law marks, scratch
+  std::vector<int64_t> fchunk_off;  // [G + 1]
+  int64_t* d_fchunk_off = nullptr;
+  uint8_t* d_segsel = nullptr;      // [G]
+  double* d_qbuf = nullptr;         // [kFiltNQ(d)][qbuf_cap]
+  int64_t qbuf_cap = 0;
   double art_eps = 1e-11;    // artificial_noise (src/sampling_unit.jl:57)
   // staging
   double* d_stage = nullptr;
@@ -691,7 +697,8 @@ dmt_status dmt_destroy(dmt_ens* h) {
                 h->d_sel[0], h->d_sel[1], h->d_sel[2], h->d_sel[3], h->d_X[0], h->d_X[1],
                 h->d_W[0], h->d_W[1], h->d_t, h->d_stage, h->d_Z, h->d_red, h->d_gather,
                 h->d_red_work, h->d_run, h->d_run_gather, h->d_part, h->d_red_lb, h->d_obsH,
-                h->d_obsF, h->d_obsc, h->d_obsv, h->d_fail};
+                h->d_obsF, h->d_obsc, h->d_obsv, h->d_fail, h->d_fchunk_off, h->d_segsel,
+                h->d_qbuf};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   for (int s = 0; s < 2; ++s)
@@ -1279,6 +1286,15 @@ dmt_status dmt_upload_obs(dmt_ens* h, const double* Hobs, const double* Fobs, co
     DMT_TRY(ens_alloc(h, &h->d_obsv, h->G * h->d));
     DMT_TRY(ens_alloc(h, &h->d_fail, 1));
     HIP_OK(hipMemsetAsync(h->d_obsv, 0, h->G * h->d * 8, h->stream));
+    // chunk offsets of the chunked filter: ceil((npts − 1) / 64) chunks per segment
+    h->fchunk_off.assign(h->G + 1, 0);
+    for (int64_t g = 0; g < h->G; ++g)
+      h->fchunk_off[g + 1] =
+          h->fchunk_off[g] + (h->seg_np[g] - 1 + flt::kFiltChunk - 1) / flt::kFiltChunk;
+    DMT_TRY(ens_alloc(h, &h->d_fchunk_off, h->G + 1));
+    DMT_TRY(ens_alloc(h, &h->d_segsel, h->G));
+    HIP_OK(hipMemcpyAsync(h->d_fchunk_off, h->fchunk_off.data(), (h->G + 1) * 8,
+                          hipMemcpyHostToDevice, h->stream));
   }
   HIP_OK(hipMemcpyAsync(h->d_obsH, Hobs, h->G * h->hp * 8, hipMemcpyHostToDevice, h->stream));
   HIP_OK(hipMemcpyAsync(h->d_obsF, Fobs, h->G * h->d * 8, hipMemcpyHostToDevice, h->stream));
@@ -1343,10 +1359,54 @@ static dmt_status guiding_term_device(dmt_ens* h, Layout* L, int64_t b0, int64_t
   a.art_eps = h->art_eps;
   a.fail = h->d_fail;
   a.only = only;
+  a.pt_off = h->d_pt_off;
+  a.fchunk_off = h->d_fchunk_off;
+  a.segsel = h->d_segsel;
   HIP_OK(hipMemsetAsync(h->d_fail, 0, sizeof(int), h->stream));
-  {
+  // batches of consecutive blocks whose points fit the transition scratch (kFiltBatchPoints,
+  // or one block's points if larger)
+  auto span = [&](int32_t gA, int32_t gB) { return h->pt_off[gB] + h->seg_np[gB] - h->pt_off[gA]; };
+  int64_t need = 0;
+  int32_t gmin = L->gfirst[b0], gmax = L->glast[b0];
+  for (int64_t b = b0; b < b1; ++b) {
+    need = std::max(need, span(L->gfirst[b], L->glast[b]));
+    gmin = std::min(gmin, L->gfirst[b]);
+    gmax = std::max(gmax, L->glast[b]);
+  }
+  const int64_t cap = std::max(need, std::min<int64_t>(span(gmin, gmax), kFiltBatchPoints));
+  if (cap > h->qbuf_cap) {
+    if (h->d_qbuf) {
+      HIP_OK(hipStreamSynchronize(h->stream));
+      HIP_OK(hipFree(h->d_qbuf));
+      h->bytes -= h->qbuf_cap * kFiltNQ(h->d) * 8;
+      h->d_qbuf = nullptr;
+      h->qbuf_cap = 0;
+    }
+    DMT_TRY(ens_alloc(h, &h->d_qbuf, cap * kFiltNQ(h->d)));
+    h->qbuf_cap = cap;
+  }
+  a.qbuf = h->d_qbuf;
+  a.qcap = h->qbuf_cap;
+  for (int64_t bs = b0; bs < b1;) {
+    int32_t gA = L->gfirst[bs], gB = L->glast[bs];
+    int64_t be = bs + 1;
+    for (; be < b1; ++be) {
+      const int32_t nA = std::min(gA, L->gfirst[be]), nB = std::max(gB, L->glast[be]);
+      if (span(nA, nB) > h->qbuf_cap) break;
+      gA = nA;
+      gB = nB;
+    }
+    a.b0 = bs;
+    a.b1 = be;
+    a.gA = gA;
+    a.gB = gB;
+    a.pA = h->pt_off[gA];
+    a.fchunk_off_h0 = h->fchunk_off[gA];
+    a.fchunk_off_h1 = h->fchunk_off[gB + 1];
+    HIP_OK(hipMemsetAsync(h->d_segsel + gA, 0, gB - gA + 1, h->stream));
     TimedScope ts(h, DMT_K_RECOMPUTE);
     HIP_OK(launch_backward_filter(h->key.precision, a, h->stream));
+    bs = be;
   }
   int failed = 0;
   HIP_OK(hipMemcpyAsync(&failed, h->d_fail, sizeof(int), hipMemcpyDeviceToHost, h->stream));
@@ -1576,20 +1636,16 @@ static dmt_status guiding_linear_impl(const double* Bt, const double* beta, cons
   double Fc[D];
   for (int i = 0; i < d; ++i) Fc[i] = FT[i];
   double cc = cT;
-  auto store = [&](int i) {
+  for (int i = 0; i + 1 < npts; ++i)
+    if (!(t[i + 1] - t[i] > 0)) return fail(DMT_ERR_INVALID, "time grid must be strictly increasing");
+  auto store = [&](int i, const flt::Mat<D>& Hs, const double* Fs, double cs) {
     for (int p = 0; p < d; ++p)
-      for (int q = p; q < d; ++q) H[(int64_t)i * hp + dmt_packed(d, p, q)] = Hc(p, q);
-    for (int p = 0; p < d; ++p) F[(int64_t)i * d + p] = Fc[p];
-    c[i] = cc;
+      for (int q = p; q < d; ++q) H[(int64_t)i * hp + dmt_packed(d, p, q)] = Hs(p, q);
+    for (int p = 0; p < d; ++p) F[(int64_t)i * d + p] = Fs[p];
+    c[i] = cs;
   };
-  store(npts - 1);
-  for (int i = npts - 2; i >= 0; --i) {
-    const double hstep = t[i + 1] - t[i];
-    if (!(hstep > 0)) return fail(DMT_ERR_INVALID, "time grid must be strictly increasing");
-    if (!flt::filter_step(B, beta, A, hstep, Hc, Fc, cc))
-      return fail(DMT_ERR_INVALID, "singular I + HK in backward filter");
-    store(i);
-  }
+  if (!flt::filter_segment<D>(B, beta, A, npts, [&](int i) { return t[i]; }, Hc, Fc, cc, store))
+    return fail(DMT_ERR_INVALID, "singular I + HK in backward filter");
   return DMT_OK;
 }
 

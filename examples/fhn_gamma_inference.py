@@ -1,0 +1,186 @@
+"""The reference's "Inference with BiBlocks" tutorial, end to end on libdmt.
+
+Data: docs/src/tutorials/preamble.md:52-66 — FitzHugh–Nagumo θ = (0.1, −0.8, 1.5, 0.0, 0.3),
+Euler–Maruyama on 0:1e-4:10 from y1 = (−0.9, −1.0), the first coordinate observed every 1000
+steps with Σ = 0.01 (100 observations), KnownStartingPt(y1).
+
+Algorithm: docs/src/tutorials/biblock/inference.md:42-75 (``simple_inference``) — one terminal
+BiBlock over all observations, grids ``standard_guid_prop_time_transf`` with dt = 0.001, pCN
+memory ρ, and per iteration
+
+    draw_proposal_path!(bb); accept_reject_proposal_path!(bb, i)
+    θ° = customkernel(θ, ϵ)                      # θ + 2ϵ(U − 0.5)
+    set_proposal_law!(bb, θ°, name_struct, true) # device: law + guiding term + recompute_path!
+    accpt, θ = accept_reject_proposal_param!(bb, i, θ, θ°)
+
+with γ the only updated parameter.  The path draws use the device Philox stream keyed by the
+iteration; the random-walk proposal and the parameter decision's Exp(1) come from a seeded host
+generator.  The reference's dataset comes from Julia's ``Random.seed!(100)`` stream, which is
+not reproducible here; the comparison is statistical (the reference's published chain,
+docs/src/assets/tutorials/biblock/inference_chain.png, wanders over ≈1.45–1.9 around γ = 1.5).
+
+    python examples/fhn_gamma_inference.py [--steps 10000] [--backend device|oracle]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+import diffusionmcmctools_amd as dmt  # noqa: E402
+from diffusionmcmctools_amd import _lib as L  # noqa: E402
+from diffusionmcmctools_amd.models import (FHN, Observation, Recording, guiding_chain,  # noqa: E402
+                                           packed, setup_time_grids)
+
+THETA = (0.1, -0.8, 1.5, 0.0, 0.3)      # ϵ, s, γ, β, σ (preamble.md:53)
+Y1 = (-0.9, -1.0)
+OBS_L = np.array([[1.0, 0.0]])
+OBS_SIGMA = np.array([[0.01]])
+
+
+def simulate_fhn(model, t, x0, rng):
+    """Euler–Maruyama on grid t (``rand(P, tt, y1)``), the noise entering the second coordinate."""
+    n = t.size
+    dW = rng.standard_normal(n - 1) * np.sqrt(np.diff(t))
+    X = np.empty((n, 2))
+    y, v = float(x0[0]), float(x0[1])
+    X[0] = y, v
+    ie, s, g, b, sg = 1.0 / model.eps, model.s, model.gamma, model.beta, model.sg
+    h = np.diff(t)
+    for i in range(n - 1):
+        y, v = (y + (y - y ** 3 - v + s) * ie * h[i],
+                v + (g * y - v + b) * h[i] + sg * dW[i])
+        X[i + 1] = y, v
+    return X
+
+
+def tutorial_data(seed=100, T=10.0, dt=1e-4, every=1000):
+    """The preamble's dataset: (Recording, latent path X, its grid t)."""
+    rng = np.random.default_rng(seed)
+    model = FHN(*THETA)
+    n = int(round(T / dt))
+    t = np.arange(n + 1) * dt
+    X = simulate_fhn(model, t, Y1, rng)
+    noise_sd = math.sqrt(OBS_SIGMA[0, 0])
+    obs = [Observation(float(t[i]), np.array([X[i, 0] + noise_sd * rng.standard_normal()]),
+                       OBS_L, OBS_SIGMA) for i in range(every, n + 1, every)]
+    return Recording(obs, 0.0, np.array(Y1)), X, t
+
+
+def sampling_pair(recording, gamma, dt=1e-3, backend="device", seed=0):
+    """``SamplingPair(FitzHughNagumoAux, recording, tts)`` with tts from
+    ``setup_time_grids(recording, dt, standard_guid_prop_time_transf)`` and γ set to the initial
+    guess (``OBS.set_parameters!``): auxiliary laws linearised at each observation, guiding terms
+    by the host backward filter, observations uploaded for the device's re-derivations, then
+    ``init_paths!`` from the known start point."""
+    th = list(THETA)
+    th[2] = gamma
+    model = FHN(*th)
+    grids = setup_time_grids(recording, dt)
+    auxes = [model.aux(ob.v[0]) for ob in recording.obs]
+    infos = [ob.info() for ob in recording.obs]
+    chain = guiding_chain(auxes, grids, infos)
+    H = np.concatenate([c[0] for c in chain])
+    F = np.concatenate([c[1] for c in chain])
+    laws = np.stack([model.law_record(a, c[2][0]) for a, c in zip(auxes, chain)])
+    n_points = [[len(g) for g in grids]]
+    if backend == "oracle":
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as orc
+        eng = orc.OracleEnsemble(model.kind, model.d, model.m, n_points, prec=L.F64, seed=seed)
+        se = dmt.SamplingEnsemble(model, n_points, _engine=eng)
+    else:
+        se = dmt.SamplingEnsemble(model, n_points, seed=seed)
+    se.upload_grid(np.concatenate(grids))
+    se.set_guiding(H, F, laws)
+    se.set_observations(np.stack([packed(i[0]) for i in infos]),
+                        np.stack([np.asarray(i[1], dtype=np.float64) for i in infos]),
+                        np.array([float(i[2]) for i in infos]))
+    ll0, ok = se.init_paths([recording.x0], iter=0)
+    if not ok.all():
+        raise RuntimeError("init_paths failed")
+    return se
+
+
+def simple_inference(se, gamma0, eps=0.3, rho=0.96, num_steps=10 ** 4, seed=1,
+                     snapshot_every=400, log_every=100, log=None):
+    """``simple_inference`` (biblock/inference.md:42-75) with γ the only variable parameter.
+    Returns a dict with the γ chain (num_steps + 1 values), the per-iteration path and
+    parameter decisions and the accepted log-likelihood per iteration."""
+    rng = np.random.default_rng(seed)
+    nseg = len(se.n_points[0])
+    be = dmt.BlockEnsemble(se, [[range(0, nseg)]], rho=rho, ll_hist_len=num_steps)
+    bb = be.recordings[0].blocks[0]
+    n_snap = num_steps // snapshot_every if snapshot_every else 0
+    if n_snap:
+        se.reserve_snapshots(n_snap)
+    be.loglikhd()
+    theta = np.array([gamma0])
+    chain, a_path, a_par, ll_acc = [theta[0]], [], [], []
+    for i in range(1, num_steps + 1):
+        bb.draw_proposal_path(iter=i)
+        a_path.append(bool(bb.accept_reject_proposal_path(i)[0]))
+        theta_p = theta + 2.0 * eps * (rng.random() - 0.5)          # customkernel(θ, ϵ)
+        bb.set_proposal_law(theta={"gamma": theta_p[0]})
+        acc, theta = bb.accept_reject_proposal_param(i, theta, theta_p,
+                                                      E=rng.exponential(1.0))
+        a_par.append(acc)
+        chain.append(float(theta[0]))
+        ll_acc.append(bb.fetch_ll())
+        if log is not None and i % log_every == 0:
+            log(f"{i}. ll={ll_acc[-1]:.4f}, imp a-r: {np.mean(a_path[-log_every:]):.3f}, "
+                f"updt a-r: {np.mean(a_par[-log_every:]):.3f}, γ={theta[0]:.4f}")
+        if n_snap and i % snapshot_every == 0:
+            se.snapshot_paths(i // snapshot_every - 1, i)
+    return dict(gamma=np.array(chain), accepted_path=np.array(a_path),
+                accepted_param=np.array(a_par), ll=np.array(ll_acc), block=bb)
+
+
+def summarize(res, burn_in):
+    g = res["gamma"][burn_in + 1:]
+    return dict(gamma_mean=float(g.mean()), gamma_sd=float(g.std()),
+                gamma_q05=float(np.quantile(g, 0.05)), gamma_q95=float(np.quantile(g, 0.95)),
+                gamma_min=float(g.min()), gamma_max=float(g.max()),
+                path_accept_rate=float(res["accepted_path"].mean()),
+                param_accept_rate=float(res["accepted_param"].mean()))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=10 ** 4)
+    ap.add_argument("--burn-in", type=int, default=1000)
+    ap.add_argument("--backend", default="device", choices=["device", "oracle"])
+    ap.add_argument("--out", default=None, help="write the summary (and chain) as JSON here")
+    a = ap.parse_args()
+    t0 = time.perf_counter()
+    rec, _, _ = tutorial_data()
+    t1 = time.perf_counter()
+    se = sampling_pair(rec, THETA[2], backend=a.backend)
+    res = simple_inference(se, THETA[2], num_steps=a.steps,
+                           snapshot_every=400 if a.backend == "device" else 0,
+                           log=lambda s: print(s, flush=True))
+    t2 = time.perf_counter()
+    out = dict(tutorial="docs/src/tutorials/biblock/inference.md", backend=a.backend,
+               steps=a.steps, burn_in=a.burn_in, data_seconds=t1 - t0, run_seconds=t2 - t1,
+               n_obs=len(rec.obs), n_points=int(sum(se.n_points[0])),
+               **summarize(res, a.burn_in))
+    print(json.dumps(out))
+    if a.out:
+        out["gamma_chain"] = res["gamma"][::10].tolist()
+        with open(a.out, "w") as f:
+            json.dump(out, f)
+    if a.backend == "device":
+        se.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -763,7 +763,8 @@ void SFX(orc_normals_segment)(uint64_t seed, uint32_t g, uint32_t iter, uint32_t
 #if IS_F64
 /* ---- exact discrete backward filter of a linear auxiliary law (recompute_guiding_term!,
  * SURVEY.md A.5), restating the build's algorithm: Taylor series with scaling and squaring
- * for the transition (Phi, mu, K), Gaussian update with Gauss-Jordan inverse; plain IEEE
+ * for each step's transition (Phi, mu, K), transitions composed within 64-step chunks,
+ * Gaussian update with Gauss-Jordan inverse; plain IEEE
  * operations in the same order, log|det| through rng_log.  Double only. */
 typedef struct { int n; double a[9]; } fm_t;
 static fm_t fm_zero(int n) { fm_t m; m.n = n; for (int i = 0; i < 9; ++i) m.a[i] = 0.0; return m; }
@@ -859,33 +860,51 @@ static void fm_transition(const fm_t* B, const double* beta, const fm_t* At, dou
     for (int i = 0; i < n; ++i)
         for (int j = i + 1; j < n; ++j) { double v = 0.5 * (K->a[i * n + j] + K->a[j * n + i]); K->a[i * n + j] = v; K->a[j * n + i] = v; }
 }
-static int fm_filter_step(const fm_t* B, const double* beta, const fm_t* A, double h, fm_t* Hc,
-                          double* Fc, double* cc) {
-    int d = B->n;
-    fm_t Phi, K; double mu[3];
-    fm_transition(B, beta, A, h, &Phi, mu, &K);
-    fm_t HK = fm_mul(Hc, &K), I = fm_eye(d);
+typedef struct { fm_t Phi; double mu[3]; fm_t K; } ftr_t;
+
+/* transition over f then s: (Phi_s Phi_f, Phi_s mu_f + mu_s, sym(Phi_s K_f Phi_s' + K_s)) */
+static ftr_t ftr_compose(const ftr_t* f, const ftr_t* s) {
+    int n = f->Phi.n;
+    ftr_t r;
+    r.Phi = fm_mul(&s->Phi, &f->Phi);
+    double m[3];
+    fm_vec(&s->Phi, f->mu, m);
+    for (int i = 0; i < n; ++i) r.mu[i] = m[i] + s->mu[i];
+    fm_t PK = fm_mul(&s->Phi, &f->K), PT = fm_T(&s->Phi), PKP = fm_mul(&PK, &PT);
+    r.K = fm_add(&PKP, &s->K);
+    for (int i = 0; i < n; ++i)
+        for (int j = i + 1; j < n; ++j) { double v = 0.5 * (r.K.a[i * n + j] + r.K.a[j * n + i]); r.K.a[i * n + j] = v; r.K.a[j * n + i] = v; }
+    return r;
+}
+
+/* (H, F, c) at the start of transition q from the values at its end (Gaussian integral) */
+static int fm_combine(const ftr_t* q, fm_t* Hc, double* Fc, double* cc) {
+    int d = q->Phi.n;
+    const fm_t* Phi = &q->Phi;
+    const fm_t* K = &q->K;
+    const double* mu = q->mu;
+    fm_t HK = fm_mul(Hc, K), I = fm_eye(d);
     fm_t IHK = fm_add(&I, &HK);
     fm_t S; double lad;
     if (!fm_inv(&IHK, &S, &lad)) return 0;
     fm_t Hh = fm_mul(&S, Hc);
     for (int p = 0; p < d; ++p)
-        for (int q = p + 1; q < d; ++q) { double v = 0.5 * (Hh.a[p * d + q] + Hh.a[q * d + p]); Hh.a[p * d + q] = v; Hh.a[q * d + p] = v; }
+        for (int r = p + 1; r < d; ++r) { double v = 0.5 * (Hh.a[p * d + r] + Hh.a[r * d + p]); Hh.a[p * d + r] = v; Hh.a[r * d + p] = v; }
     double Fh[3], KF[3];
     fm_vec(&S, Fc, Fh);
-    fm_vec(&K, Fc, KF);
+    fm_vec(K, Fc, KF);
     double fkf = 0.0;
     for (int p = 0; p < d; ++p) fkf += Fh[p] * KF[p];
     double ch = *cc + 0.5 * lad - 0.5 * fkf;
     double Hmu[3], g[3], Fn[3];
     fm_vec(&Hh, mu, Hmu);
     for (int p = 0; p < d; ++p) g[p] = Fh[p] - Hmu[p];
-    fm_t PhT = fm_T(&Phi);
+    fm_t PhT = fm_T(Phi);
     fm_vec(&PhT, g, Fn);
     fm_t t1 = fm_mul(&PhT, &Hh);
-    fm_t Hn = fm_mul(&t1, &Phi);
+    fm_t Hn = fm_mul(&t1, Phi);
     for (int p = 0; p < d; ++p)
-        for (int q = p + 1; q < d; ++q) { double v = 0.5 * (Hn.a[p * d + q] + Hn.a[q * d + p]); Hn.a[p * d + q] = v; Hn.a[q * d + p] = v; }
+        for (int r = p + 1; r < d; ++r) { double v = 0.5 * (Hn.a[p * d + r] + Hn.a[r * d + p]); Hn.a[p * d + r] = v; Hn.a[r * d + p] = v; }
     double fmu = 0.0, muHmu = 0.0;
     for (int p = 0; p < d; ++p) { fmu += Fh[p] * mu[p]; muHmu += mu[p] * Hmu[p]; }
     *cc = ch - fmu + 0.5 * muHmu;
@@ -895,7 +914,12 @@ static int fm_filter_step(const fm_t* B, const double* beta, const fm_t* A, doub
 }
 
 /* Backward filter over one segment's grid t[npts] from the terminal information (HT packed,
- * FT, cT): H[npts][hp] packed, F[npts][d], c[npts] (double).  Returns 0 if singular. */
+ * FT, cT): H[npts][hp] packed, F[npts][d], c[npts] (double).  Returns 0 if singular.
+ * Canonical chunked form: chunks of FILT_CHUNK steps counted from the
+ * segment end; per chunk an inclusive Kogge-Stone suffix scan of the step transitions
+ * (stage k: Q_l <- compose(Q_l, Q_{l+k}) if l + k < cnt, previous-stage values), then every
+ * point of the chunk by one combine from the chunk end's (H, F, c). */
+#define FILT_CHUNK 64
 int orc_backward_filter_segment(int d, const double* Bt, const double* beta, const double* at,
                                 int npts, const double* t, const double* HT, const double* FT,
                                 double cT, double* H, double* F, double* c) {
@@ -906,13 +930,34 @@ int orc_backward_filter_segment(int d, const double* Bt, const double* beta, con
         for (int j = 0; j < d; ++j) { A.a[i * d + j] = at[pidx(d, i, j)]; Hc.a[i * d + j] = HT[pidx(d, i, j)]; }
     double Fc[3] = {0, 0, 0}, cc = cT;
     for (int i = 0; i < d; ++i) Fc[i] = FT[i];
-    for (int i = npts - 1; i >= 0; --i) {
-        if (i < npts - 1 && !fm_filter_step(&B, beta, &A, t[i + 1] - t[i], &Hc, Fc, &cc)) return 0;
-        for (int p = 0; p < d; ++p)
-            for (int q = p; q < d; ++q) H[(size_t)i * hp + pidx(d, p, q)] = Hc.a[p * d + q];
-        for (int p = 0; p < d; ++p) F[(size_t)i * d + p] = Fc[p];
-        c[i] = cc;
+#define FILT_STORE(i, Hm, Fv, cv)                                                              \
+    do {                                                                                       \
+        for (int p = 0; p < d; ++p)                                                            \
+            for (int q = p; q < d; ++q) H[(size_t)(i) * hp + pidx(d, p, q)] = (Hm).a[p * d + q]; \
+        for (int p = 0; p < d; ++p) F[(size_t)(i) * d + p] = (Fv)[p];                          \
+        c[i] = (cv);                                                                           \
+    } while (0)
+    FILT_STORE(npts - 1, Hc, Fc, cc);
+    ftr_t Q[FILT_CHUNK], Qn[FILT_CHUNK];
+    for (int hi = npts - 1; hi > 0; hi -= FILT_CHUNK) {
+        int lo = hi > FILT_CHUNK ? hi - FILT_CHUNK : 0, cnt = hi - lo;
+        for (int l = 0; l < cnt; ++l)
+            fm_transition(&B, beta, &A, t[lo + l + 1] - t[lo + l], &Q[l].Phi, Q[l].mu, &Q[l].K);
+        for (int k = 1; k < FILT_CHUNK; k *= 2) {
+            for (int l = 0; l < cnt; ++l) Qn[l] = (l + k < cnt) ? ftr_compose(&Q[l], &Q[l + k]) : Q[l];
+            for (int l = 0; l < cnt; ++l) Q[l] = Qn[l];
+        }
+        fm_t H0 = Hc;
+        double F0[3] = {Fc[0], Fc[1], Fc[2]}, c0 = cc;
+        for (int l = cnt - 1; l >= 0; --l) {
+            fm_t Hl = H0;
+            double Fl[3] = {F0[0], F0[1], F0[2]}, cl = c0;
+            if (!fm_combine(&Q[l], &Hl, Fl, &cl)) return 0;
+            FILT_STORE(lo + l, Hl, Fl, cl);
+            if (l == 0) { Hc = Hl; Fc[0] = Fl[0]; Fc[1] = Fl[1]; Fc[2] = Fl[2]; cc = cl; }
+        }
     }
+#undef FILT_STORE
     return 1;
 }
 /* the canonical log kernel, exposed for the Python container restatement */

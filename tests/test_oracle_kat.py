@@ -253,3 +253,24 @@ def test_oracle_recompute_guiding_term_reproduces_uploaded_tables():
     H1, F1, laws1 = ora.download_law(0, 0)
     assert np.array_equal(H1, H0) and np.array_equal(F1, F0)
     assert np.array_equal(laws1[:, 49], laws0[:, 49])
+
+
+@pytest.mark.parametrize("npts", [1, 2, 64, 65, 66, 129, 300])
+def test_chunked_filter_lengths(dmt, npts):
+    """The chunked filter (64-step chunks from the segment end) at chunk-edge
+    lengths: host == oracle bit for bit, and both agree with the matrix-exponential filter."""
+    from diffusionmcmctools_amd.models import FHN, standard_guid_prop_time_transf
+    aux = FHN(0.1, -0.8, 1.5, 0.0, 0.3).aux(0.4)
+    B, beta, at = aux.Bt, aux.beta, aux.at
+    HT = np.array([[100.0, 0], [0, 0]]); FT = np.array([40.0, 0]); cT = 1.0
+    t = standard_guid_prop_time_transf(0.0, 0.2, 0.2 / max(npts - 1, 1))[:npts] if npts > 1 \
+        else np.array([0.0])
+    H, F, c = dmt.guiding_linear(B, beta, _packed(at), t, _packed(HT), FT, cT)
+    Ho, Fo, co = orc.backward_filter_segment(2, np.asarray(B).ravel(), beta, _packed(at), t,
+                                             _packed(HT), FT, cT)
+    assert np.array_equal(Ho, H) and np.array_equal(Fo, F) and np.array_equal(co, c)
+    He, Fe, ce = npo.backward_filter_expm(B, beta, at, t, HT, FT, cT)
+    Hp = np.stack([_packed(He[i]) for i in range(len(t))])
+    np.testing.assert_allclose(H, Hp, rtol=1e-9, atol=1e-10 * np.abs(Hp).max())
+    np.testing.assert_allclose(F, Fe, rtol=1e-9, atol=1e-10 * np.abs(Fe).max())
+    np.testing.assert_allclose(c, ce, rtol=1e-9, atol=1e-9)

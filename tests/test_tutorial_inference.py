@@ -1,0 +1,87 @@
+"""The reference's "Inference with BiBlocks" tutorial end to end
+(docs/src/tutorials/biblock/inference.md:42-75 on the preamble.md:52-66 dataset, driven by
+examples/fhn_gamma_inference.py): path imputation and the γ random-walk update through
+set_proposal_law! / accept_reject_proposal_param! on one terminal BiBlock over 100 segments.
+
+CPU: the loop runs on the oracle backend.  GPU: the device chain equals the oracle's bit for
+bit over the first iterations (paths, γ chain, decisions, ll), and a longer device chain
+concentrates around the true γ = 1.5 like the reference's published chain
+(docs/src/assets/tutorials/biblock/inference_chain.png: ≈1.45–1.9); the dataset itself is a
+fresh simulation (Julia's seeded stream is not reproducible), so that check is statistical."""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "examples"))
+
+import fhn_gamma_inference as tut  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def recording():
+    rec, X, t = tut.tutorial_data()
+    return rec
+
+
+def test_tutorial_data_shape(recording):
+    assert len(recording.obs) == 100
+    assert [o.t for o in recording.obs[:2]] == [0.1, 0.2] and recording.obs[-1].t == 10.0
+    v = np.array([o.v[0] for o in recording.obs])
+    assert np.all(np.abs(v) < 2.5)          # the FHN relaxation oscillation stays within ±2
+
+
+def test_tutorial_loop_on_oracle(recording):
+    se = tut.sampling_pair(recording, 1.5, backend="oracle")
+    assert sum(se.n_points[0]) == 100 * 101
+    res = tut.simple_inference(se, 1.5, num_steps=20, snapshot_every=0)
+    assert res["gamma"].shape == (21,) and np.all(np.isfinite(res["ll"]))
+    assert 0 < res["accepted_path"].sum() < 20       # ρ = 0.96: most pCN moves accepted
+    assert res["accepted_param"].any()
+    moved = np.diff(res["gamma"]) != 0
+    np.testing.assert_array_equal(moved, res["accepted_param"])
+    bb = res["block"]
+    hist = bb.ll_history[:, 0]
+    assert hist.shape == (20,) and np.all(np.isfinite(hist))
+
+
+@pytest.mark.gpu
+def test_tutorial_device_equals_oracle(recording):
+    """25 iterations of simple_inference on the device and on the oracle from the same state and
+    seeds: identical γ chains, decisions, fetch_ll values and accepted paths."""
+    n = 25
+    out = []
+    for backend in ("device", "oracle"):
+        se = tut.sampling_pair(recording, 1.5, backend=backend)
+        res = tut.simple_inference(se, 1.5, num_steps=n, snapshot_every=0)
+        X = se.ens.download_paths(0, 0)
+        out.append((res, X))
+        if backend == "device":
+            se.close()
+    (rd, Xd), (ro, Xo) = out
+    np.testing.assert_array_equal(rd["gamma"], ro["gamma"])
+    np.testing.assert_array_equal(rd["accepted_path"], ro["accepted_path"])
+    np.testing.assert_array_equal(rd["accepted_param"], ro["accepted_param"])
+    np.testing.assert_array_equal(rd["ll"], ro["ll"])
+    np.testing.assert_array_equal(Xd, Xo)
+
+
+@pytest.mark.gpu
+def test_tutorial_gamma_posterior_on_device(recording):
+    """3000 iterations (the reference runs 10⁴): after 500 burn-in the γ chain sits around the
+    true value, both update kinds mix, and the 400-iteration path snapshots are recorded."""
+    se = tut.sampling_pair(recording, 1.5, backend="device")
+    res = tut.simple_inference(se, 1.5, num_steps=3000, snapshot_every=400)
+    s = tut.summarize(res, 500)
+    assert 1.2 < s["gamma_mean"] < 1.9, s
+    assert s["gamma_q05"] < 1.5 < s["gamma_q95"] + 0.2, s
+    assert 0.2 < s["path_accept_rate"] < 0.95, s
+    assert 0.1 < s["param_accept_rate"] < 0.95, s
+    snap, it = se.snapshot(6)
+    assert it == 2800 and len(snap[0]) == 100 and snap[0][0].shape == (101, 2)
+    np.testing.assert_array_equal(snap[0][0][0], tut.Y1)
+    se.close()
