@@ -203,7 +203,8 @@ hipError_t launch_set_obs(int precision, int tw, int d, const void* X0, const vo
                           const uint8_t* selX,
                           const int64_t* tile_qoff, const int32_t* seg_rec, const int32_t* seg_q,
                           const int32_t* seg_np, const int32_t* glast, const uint8_t* term,
-                          int64_t b0, int64_t b1, double* obsv, hipStream_t s);
+                          int64_t b0, int64_t b1, double* obsv, int model, double* lawb0,
+                          double* lawb1, hipStream_t s);
 hipError_t launch_to_planes(int precision, int tw, const double* src, void* dst0, void* dst1,
                             const uint8_t* sel, int flip, int C, int64_t P, const int64_t* pt_off,
                             int64_t G, const int32_t* seg_rec, const int32_t* seg_q,

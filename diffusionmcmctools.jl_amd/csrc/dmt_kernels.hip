@@ -2237,6 +2237,8 @@ __device__ __forceinline__ void put_theta(double* r, int p, double v) {
     if (q == p) r[DMT_LAW_THETA + q] = v;
 }
 
+__device__ __forceinline__ void derive_law(int model, double* r);
+
 __device__ __forceinline__ void write_params(const ParamArgs& a, double* r) {
   for (int k = 0; k < a.n; ++k) {
     const int p = a.idx[k];
@@ -2252,7 +2254,12 @@ __device__ __forceinline__ void write_params(const ParamArgs& a, double* r) {
       put_theta(r, p < dd ? p : 9 + (p - dd), v);
     }
   }
-  if (a.model == DMT_MODEL_FHN) {
+  derive_law(a.model, r);
+}
+
+// the fields of a law record derived from θ (and, for a linearised auxiliary law, its anchor)
+__device__ __forceinline__ void derive_law(int model, double* r) {
+  if (model == DMT_MODEL_FHN) {
     const double sg = r[DMT_LAW_THETA + 5];
     r[DMT_LAW_SIGMA + 0] = 0.0;
     r[DMT_LAW_SIGMA + 1] = sg;
@@ -2271,7 +2278,7 @@ __device__ __forceinline__ void write_params(const ParamArgs& a, double* r) {
       for (int i = 0; i < 3; ++i) r[DMT_LAW_DA + i] = 0.0;
       r[DMT_LAW_TRACE] = 0.0;
     }
-  } else if (a.model == DMT_MODEL_LORENZ && r[DMT_LAW_AUXLIN] != 0.0) {
+  } else if (model == DMT_MODEL_LORENZ && r[DMT_LAW_AUXLIN] != 0.0) {
     const double s = r[DMT_LAW_THETA + 0], rr = r[DMT_LAW_THETA + 1], b = r[DMT_LAW_THETA + 2];
     const double x0 = r[DMT_LAW_ANCHOR + 0], x1 = r[DMT_LAW_ANCHOR + 1],
                  x2 = r[DMT_LAW_ANCHOR + 2];
@@ -2328,20 +2335,35 @@ __global__ __launch_bounds__(64) void k_set_prop_law(const ParamArgs a, int wg_p
 }
 
 // set_obs!(bb) (src/biblock.jl:273-280): the artificial observation of a non-terminal block's
-// P_last is the end point of its accepted path.
+// P_last is the end point of its accepted path; the P_last laws of b and b° that are
+// linearised at an anchor (FHN y_T, Lorenz x_T) are re-anchored there and re-derived
+// (DESIGN.md §3.5).
 template <class T>
 __global__ void k_set_obs(int tw, int d, const T* X0, const T* X1, const uint8_t* selX,
                           const int64_t* tile_qoff, const int32_t* seg_rec, const int32_t* seg_q,
                           const int32_t* seg_np, const int32_t* glast, const uint8_t* term,
-                          int64_t b0, int64_t b1, double* obsv) {
+                          int64_t b0, int64_t b1, double* obsv, int model, double* lawb0,
+                          double* lawb1) {
   const int64_t blk = b0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (blk >= b1 || term[blk]) return;
   const int g = glast[blk];
   const T* X = selX[g] ? X1 : X0;  // u.XX
   const int64_t r = seg_rec[g];
   const int64_t q = seg_q[g] + seg_np[g] - 1;
-  for (int p = 0; p < d; ++p)
-    obsv[(int64_t)g * d + p] = (double)X[((tile_qoff[r / tw] + q) * d + p) * tw + r % tw];
+  double v[3] = {0.0, 0.0, 0.0};
+  for (int p = 0; p < d; ++p) {
+    v[p] = (double)X[((tile_qoff[r / tw] + q) * d + p) * tw + r % tw];
+    obsv[(int64_t)g * d + p] = v[p];
+  }
+  const int na = model == DMT_MODEL_FHN ? 1 : model == DMT_MODEL_LORENZ ? 3 : 0;
+  if (!na || !lawb0) return;
+  double* recs[2] = {lawb0 + (int64_t)g * DMT_LAW_STRIDE, lawb1 + (int64_t)g * DMT_LAW_STRIDE};
+  for (int u = 0; u < 2; ++u) {
+    double* rec = recs[u];
+    if (rec[DMT_LAW_AUXLIN] == 0.0) continue;
+    for (int i = 0; i < na; ++i) rec[DMT_LAW_ANCHOR + i] = v[i];
+    derive_law(model, rec);
+  }
 }
 
 // ---------------------------------------------------------------- small utility kernels
@@ -2866,17 +2888,17 @@ hipError_t launch_set_obs(int precision, int tw, int d, const void* X0, const vo
                           const uint8_t* selX, const int64_t* tile_qoff, const int32_t* seg_rec,
                           const int32_t* seg_q, const int32_t* seg_np, const int32_t* glast,
                           const uint8_t* term, int64_t b0, int64_t b1, double* obsv,
-                          hipStream_t s) {
+                          int model, double* lawb0, double* lawb1, hipStream_t s) {
   const int64_t n = b1 - b0;
   if (n <= 0) return hipSuccess;
   if (precision == DMT_F64)
     k_set_obs<double><<<nblk(n, 256), 256, 0, s>>>(tw, d, (const double*)X0, (const double*)X1,
                                                    selX, tile_qoff, seg_rec, seg_q, seg_np, glast,
-                                                   term, b0, b1, obsv);
+                                                   term, b0, b1, obsv, model, lawb0, lawb1);
   else
     k_set_obs<float><<<nblk(n, 256), 256, 0, s>>>(tw, d, (const float*)X0, (const float*)X1, selX,
                                                   tile_qoff, seg_rec, seg_q, seg_np, glast, term,
-                                                  b0, b1, obsv);
+                                                  b0, b1, obsv, model, lawb0, lawb1);
   return hipGetLastError();
 }
 

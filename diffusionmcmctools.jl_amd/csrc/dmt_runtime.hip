@@ -1312,7 +1312,8 @@ dmt_status dmt_set_obs(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1) {
   DMT_TRY(check_range(L, b0, b1));
   HIP_OK(launch_set_obs(h->key.precision, h->tw, h->d, h->d_X[0], h->d_X[1], h->d_sel[0],
                         h->d_tile_qoff, h->d_seg_rec, h->d_seg_q, h->d_seg_np, L->d_glast,
-                        L->d_term, b0, b1, h->d_obsv, h->stream));
+                        L->d_term, b0, b1, h->d_obsv, h->key.model, h->d_law[0][1],
+                        h->d_law[1][1], h->stream));
   return DMT_OK;
 }
 

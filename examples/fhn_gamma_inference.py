@@ -38,13 +38,17 @@ if ROOT not in sys.path:
 
 import diffusionmcmctools_amd as dmt  # noqa: E402
 from diffusionmcmctools_amd import _lib as L  # noqa: E402
-from diffusionmcmctools_amd.models import (FHN, Observation, Recording, guiding_chain,  # noqa: E402
-                                           packed, setup_time_grids)
+from diffusionmcmctools_amd.models import (FHN, Observation, Recording,  # noqa: E402
+                                           artificial_obs_info, guiding_chain, packed,
+                                           setup_time_grids)
 
 THETA = (0.1, -0.8, 1.5, 0.0, 0.3)      # ϵ, s, γ, β, σ (preamble.md:53)
 Y1 = (-0.9, -1.0)
 OBS_L = np.array([[1.0, 0.0]])
 OBS_SIGMA = np.array([[0.01]])
+ARTIFICIAL_NOISE = 1e-11                # src/sampling_unit.jl:57
+# the blocking tutorial's two blockings (biblock/inference_with_blocking.md:101), 0-based
+BLOCKINGS = [[range(0, 25), range(25, 75), range(75, 100)], [range(0, 50), range(50, 100)]]
 
 
 def simulate_fhn(model, t, x0, rng):
@@ -76,12 +80,15 @@ def tutorial_data(seed=100, T=10.0, dt=1e-4, every=1000):
     return Recording(obs, 0.0, np.array(Y1)), X, t
 
 
-def sampling_pair(recording, gamma, dt=1e-3, backend="device", seed=0):
+def sampling_pair(recording, gamma, dt=1e-3, backend="device", seed=0, blocking=False):
     """``SamplingPair(FitzHughNagumoAux, recording, tts)`` with tts from
     ``setup_time_grids(recording, dt, standard_guid_prop_time_transf)`` and γ set to the initial
     guess (``OBS.set_parameters!``): auxiliary laws linearised at each observation, guiding terms
     by the host backward filter, observations uploaded for the device's re-derivations, then
-    ``init_paths!`` from the known start point."""
+    ``init_paths!`` from the known start point.  ``blocking``: also the per-segment blocking
+    laws PPb (guid_prop_for_blocking, src/sampling_unit.jl:61-66), set up with an artificial
+    end observation at (v, 0) — ``set_obs!`` + ``recompute_guiding_term!`` replace it by the
+    accepted path's end point before first use."""
     th = list(THETA)
     th[2] = gamma
     model = FHN(*th)
@@ -93,6 +100,15 @@ def sampling_pair(recording, gamma, dt=1e-3, backend="device", seed=0):
     F = np.concatenate([c[1] for c in chain])
     laws = np.stack([model.law_record(a, c[2][0]) for a, c in zip(auxes, chain)])
     n_points = [[len(g) for g in grids]]
+    blaws = {}
+    if blocking:
+        Hb, Fb, lb = [], [], []
+        for k, (a_, ob) in enumerate(zip(auxes, recording.obs)):
+            Ha, Fa, ca = artificial_obs_info(np.array([ob.v[0], 0.0]), ARTIFICIAL_NOISE)
+            Ho, Fo, co = infos[k]
+            (h, f, c), = guiding_chain([a_], [grids[k]], [(Ha + Ho, Fa + Fo, ca + co)])
+            Hb.append(h); Fb.append(f); lb.append(model.law_record(a_, c[0]))
+        blaws = dict(Hb=np.concatenate(Hb), Fb=np.concatenate(Fb), lawsb=np.stack(lb))
     if backend == "oracle":
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle as orc
@@ -101,10 +117,10 @@ def sampling_pair(recording, gamma, dt=1e-3, backend="device", seed=0):
     else:
         se = dmt.SamplingEnsemble(model, n_points, seed=seed)
     se.upload_grid(np.concatenate(grids))
-    se.set_guiding(H, F, laws)
+    se.set_guiding(H, F, laws, **blaws)
     se.set_observations(np.stack([packed(i[0]) for i in infos]),
                         np.stack([np.asarray(i[1], dtype=np.float64) for i in infos]),
-                        np.array([float(i[2]) for i in infos]))
+                        np.array([float(i[2]) for i in infos]), artificial_noise=ARTIFICIAL_NOISE)
     ll0, ok = se.init_paths([recording.x0], iter=0)
     if not ok.all():
         raise RuntimeError("init_paths failed")
@@ -145,6 +161,43 @@ def simple_inference(se, gamma0, eps=0.3, rho=0.96, num_steps=10 ** 4, seed=1,
                 accepted_param=np.array(a_par), ll=np.array(ll_acc), block=bb)
 
 
+def simple_inference_with_blocking(se, gamma0, blockings=BLOCKINGS, eps=0.3, rho=0.96,
+                                   num_steps=10 ** 4, seed=1, log_every=100, log=None):
+    """``simple_inference_with_blocking`` (biblock/inference_with_blocking.md:39-96): per
+    iteration and per blocking, set_obs! → recompute_guiding_term!(b) → find_W_for_X! →
+    loglikhd! → draw_proposal_path! → accept_reject_proposal_path!; then the γ update on the
+    last blocking (set_proposal_law! of every block, recompute_guiding_term!(b°), the MH
+    decision on the summed log-likelihoods).  Blocking k draws with device salt k."""
+    rng = np.random.default_rng(seed)
+    bes = [dmt.BlockEnsemble(se, [b], rho=rho, ll_hist_len=num_steps) for b in blockings]
+    theta = np.array([gamma0])
+    chain, a_path, a_par, ll_acc = [theta[0]], [], [], []
+    for i in range(1, num_steps + 1):
+        acc_i = []
+        for k, be in enumerate(bes):
+            be.set_obs()
+            be.recompute_guiding_term()
+            be.find_W_for_X()
+            be.loglikhd()
+            be.draw_proposal_path(iter=i, salt=k)
+            acc_i.append(be.accept_reject_proposal_path(i, salt=k))
+        a_path.append(np.concatenate(acc_i))
+        theta_p = theta + 2.0 * eps * (rng.random() - 0.5)
+        be = bes[-1]
+        be.set_proposal_law(theta={"gamma": theta_p[0]})
+        be.recompute_guiding_term(unit=L.UPROP)
+        acc, theta = be.accept_reject_proposal_param(i, theta, theta_p, E=rng.exponential(1.0))
+        a_par.append(acc)
+        chain.append(float(theta[0]))
+        ll_acc.append(be.fetch_ll())
+        if log is not None and i % log_every == 0:
+            log(f"{i}. ll={ll_acc[-1]:.4f}, imp a-r: "
+                f"{np.round(np.mean(a_path[-log_every:], axis=0), 2).tolist()}, "
+                f"updt a-r: {np.mean(a_par[-log_every:]):.3f}, γ={theta[0]:.4f}")
+    return dict(gamma=np.array(chain), accepted_path=np.array(a_path),
+                accepted_param=np.array(a_par), ll=np.array(ll_acc), blockings=bes)
+
+
 def summarize(res, burn_in):
     g = res["gamma"][burn_in + 1:]
     return dict(gamma_mean=float(g.mean()), gamma_sd=float(g.std()),
@@ -159,17 +212,25 @@ def main():
     ap.add_argument("--steps", type=int, default=10 ** 4)
     ap.add_argument("--burn-in", type=int, default=1000)
     ap.add_argument("--backend", default="device", choices=["device", "oracle"])
+    ap.add_argument("--blocking", action="store_true",
+                    help="biblock/inference_with_blocking.md instead of biblock/inference.md")
     ap.add_argument("--out", default=None, help="write the summary (and chain) as JSON here")
     a = ap.parse_args()
     t0 = time.perf_counter()
     rec, _, _ = tutorial_data()
     t1 = time.perf_counter()
-    se = sampling_pair(rec, THETA[2], backend=a.backend)
-    res = simple_inference(se, THETA[2], num_steps=a.steps,
-                           snapshot_every=400 if a.backend == "device" else 0,
-                           log=lambda s: print(s, flush=True))
+    se = sampling_pair(rec, THETA[2], backend=a.backend, blocking=a.blocking)
+    if a.blocking:
+        res = simple_inference_with_blocking(se, THETA[2], num_steps=a.steps,
+                                             log=lambda s: print(s, flush=True))
+        tut = "docs/src/tutorials/biblock/inference_with_blocking.md"
+    else:
+        res = simple_inference(se, THETA[2], num_steps=a.steps,
+                               snapshot_every=400 if a.backend == "device" else 0,
+                               log=lambda s: print(s, flush=True))
+        tut = "docs/src/tutorials/biblock/inference.md"
     t2 = time.perf_counter()
-    out = dict(tutorial="docs/src/tutorials/biblock/inference.md", backend=a.backend,
+    out = dict(tutorial=tut, backend=a.backend,
                steps=a.steps, burn_in=a.burn_in, data_seconds=t1 - t0, run_seconds=t2 - t1,
                n_obs=len(rec.obs), n_points=int(sum(se.n_points[0])),
                **summarize(res, a.burn_in))

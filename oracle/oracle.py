@@ -603,10 +603,22 @@ class OracleEnsemble:
         return ok, crit
 
     def set_obs(self, layout, b0, b1):
-        """GP.set_obs!(bb) (src/biblock.jl:273-280): P_last observes the accepted end point."""
+        """GP.set_obs!(bb) (src/biblock.jl:273-280): P_last of b and b° observes the accepted
+        end point; an auxiliary law linearised at its anchor (FHN: y_T, Lorenz: x_T) is
+        re-anchored there and re-derived (set_law_params with no parameter writes), so that
+        b̃ matches b at the exact end point."""
+        na = {1: 1, 2: 3}.get(self.model, 0)
         for bk in self.layouts[layout][b0:b1]:
             if not bk.term:
-                self.obsv[bk.g1] = self.u.XX[bk.g1][-1].astype(np.float64)
+                g = bk.g1
+                self.obsv[g] = self.u.XX[g][-1].astype(np.float64)
+                for unit in (self.u, self.up):
+                    if not unit.PPb or unit.PPb[g] is None or unit.PPb[g].rec is None:
+                        continue
+                    rec = unit.PPb[g].rec
+                    if na and rec[L_AUXLIN] != 0.0:
+                        rec[L_ANCHOR:L_ANCHOR + na] = self.obsv[g, :na]
+                        set_law_params(self.model, self.d, rec, {})
 
     def recompute_guiding_term(self, layout, b0, b1, unit=0):
         """GP.recompute_guiding_term!(b) (src/block.jl:102-110) for `unit`'s laws: segments

@@ -11,4 +11,5 @@ mkdir -p $O
 scripts/gpu_session.sh \
  "timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 240 --timeout-method thread > $O/pytest_gpu.log 2>&1" \
  "timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_tut -o tut --output-format csv -- python examples/fhn_gamma_inference.py --steps 300 --burn-in 100 > $O/prof_tut.log 2>&1" \
- "timeout -k 10 600 python -u examples/fhn_gamma_inference.py --steps $N --out $O/tutorial_device.json > $O/tutorial_device.log 2>&1"
+ "timeout -k 10 600 python -u examples/fhn_gamma_inference.py --steps $N --out $O/tutorial_device.json > $O/tutorial_device.log 2>&1" \
+ "timeout -k 10 900 python -u examples/fhn_gamma_inference.py --blocking --steps $N --out $O/tutorial_blocking_device.json > $O/tutorial_blocking_device.log 2>&1"

@@ -85,3 +85,53 @@ def test_tutorial_gamma_posterior_on_device(recording):
     assert it == 2800 and len(snap[0]) == 100 and snap[0][0].shape == (101, 2)
     np.testing.assert_array_equal(snap[0][0][0], tut.Y1)
     se.close()
+
+
+# ------------------------------------------------------------------ inference with blocking
+def test_set_obs_reanchors_blocking_law(recording):
+    """set_obs! freezes the accepted end point of a non-terminal block as P_last's exact
+    observation; the FHN auxiliary law of P_last (b and b°) is re-linearised at that end point
+    (the host record of the same law built at y_T, bit for bit) so that b̃ = b there."""
+    import diffusionmcmctools_amd as dmt
+    from diffusionmcmctools_amd import _lib as L
+    from diffusionmcmctools_amd.models import FHN
+    se = tut.sampling_pair(recording, 1.5, backend="oracle", blocking=True)
+    be = dmt.BlockEnsemble(se, [tut.BLOCKINGS[0]], rho=0.96, ll_hist_len=2)
+    be.set_obs()
+    X = se.ens.download_paths(L.U, 0)
+    e = se.ens
+    for g in (24, 74):
+        y = X[e.pt_off[g] + e.npts[g] - 1]
+        np.testing.assert_array_equal(e.obsv[g], y)
+        m = FHN(*tut.THETA)
+        want = m.law_record(m.aux(y[0]))
+        for unit in (L.U, L.UPROP):
+            rec = e.download_law(unit, L.LAW_PPB)[2][g]
+            sl = np.r_[0:49, 50:64]            # all but c(t0)
+            assert np.array_equal(rec[sl], want[sl]), (g, unit)
+
+
+def test_blocking_tutorial_loop_on_oracle(recording):
+    se = tut.sampling_pair(recording, 1.5, backend="oracle", blocking=True)
+    res = tut.simple_inference_with_blocking(se, 1.5, num_steps=6)
+    assert res["accepted_path"].shape == (6, 5) and np.all(np.isfinite(res["ll"]))
+    assert res["accepted_path"].mean() > 0.3      # every block moves (exact end points anchored)
+
+
+@pytest.mark.gpu
+def test_blocking_tutorial_device_equals_oracle(recording):
+    """biblock/inference_with_blocking.md's loop (set_obs!, recompute_guiding_term!,
+    find_W_for_X!, loglikhd!, draw, accept per blocking; γ update on the last blocking) for 8
+    iterations: device == oracle bit for bit."""
+    out = []
+    for backend in ("device", "oracle"):
+        se = tut.sampling_pair(recording, 1.5, backend=backend, blocking=True)
+        res = tut.simple_inference_with_blocking(se, 1.5, num_steps=8)
+        out.append((res, se.ens.download_paths(0, 0), se.ens.download_paths(0, 1)))
+        if backend == "device":
+            se.close()
+    (rd, Xd, Wd), (ro, Xo, Wo) = out
+    for k in ("gamma", "accepted_path", "accepted_param", "ll"):
+        np.testing.assert_array_equal(rd[k], ro[k], err_msg=k)
+    np.testing.assert_array_equal(Xd, Xo)
+    np.testing.assert_array_equal(Wd, Wo)
