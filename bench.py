@@ -63,7 +63,11 @@ def measured_traffic(config, kernel_substr):
     (profiles/rNN_traffic_<config>.json, scripts/pmc_traffic.py: separate FETCH_SIZE and
     WRITE_SIZE rocprofv3 passes, calibrated with scripts/calib_stream); None if absent."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_traffic_{config}.json")))
+    # run tags go r01, r01b … r01z, r01aa …: newest = longest tag, then the last in order
+    def tag(p):
+        t = os.path.basename(p).split("_traffic_")[0]
+        return (len(t), t)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_traffic_{config}.json")), key=tag)
     for path in reversed(files):
         with open(path) as f:
             t = json.load(f)

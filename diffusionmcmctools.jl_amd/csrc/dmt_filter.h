@@ -305,7 +305,7 @@ DMT_HD bool filter_combine(const Trans<N>& q, Mat<N>& Hc, double* Fc, double& cc
   return true;
 }
 
-// The canonical chunked filter of one segment.  The steps are cut into chunks
+// The canonical chunked filter of one segment (guiding term).  The steps are cut into chunks
 // of kFiltChunk counted from the segment end; inside a chunk, every step's transition is
 // composed with the rest of the chunk by an inclusive Kogge–Stone suffix scan (stage k: step l
 // takes compose(Q_l, Q_{l+k}) when l + k < cnt, from the previous stage's values), and every

@@ -143,7 +143,7 @@ struct FilterArgs {
   double art_eps;      // its variance (artificial_noise)
   int* fail;           // set to 1 if a filter step is singular
   const uint8_t* only;  // [nblocks] nullable: filter only the blocks flagged here
-  // chunked filter: one batch of blocks [b0, b1) covering segments [gA, gB]
+  // chunked filter (guiding term): one batch of blocks [b0, b1) covering segments [gA, gB]
   const int64_t* pt_off;      // [G] first point of each segment
   const int64_t* fchunk_off;  // [G + 1] prefix of the segments' chunk counts
   uint8_t* segsel;            // [G] 0 skip, 1 PP, 2 PPb (k_filter_mark)
@@ -151,6 +151,7 @@ struct FilterArgs {
   int64_t qcap, pA;
   int32_t gA, gB;
   int64_t fchunk_off_h0, fchunk_off_h1;  // fchunk_off[gA], fchunk_off[gB + 1] (host copies)
+  int fused;  // many blocks: k_filter_fused (a wave per block, no scratch) instead of scan + chain
 };
 constexpr int kFiltNQ(int d) { return d * d + d + d * (d + 1) / 2; }
 
@@ -191,6 +192,9 @@ hipError_t launch_accept(const AcceptArgs& a, hipStream_t s);
 constexpr int kPersistMaxSegments = 64;
 // points per batch of the chunked device filter (its transition scratch: kFiltNQ(d) doubles each)
 constexpr int64_t kFiltBatchPoints = int64_t(1) << 24;
+// block counts from which the device filter runs k_filter_fused (one wave per block) instead of
+// k_filter_scan + k_filter_chain (every chunk in parallel, a short serial chain per block)
+constexpr int64_t kFiltFusedBlocks = 4096;
 constexpr int kResidentMaxSteps = 512;
 hipError_t launch_mcmc_persistent(const ModelKey& k, const void* args, const AcceptArgs& c,
                                   int64_t iter0, int64_t n_iter, double* part, int64_t nwaves,

@@ -726,9 +726,19 @@ __global__ __launch_bounds__(128) void k_block_wave(const BlockArgs<T> a) {
       T xc[D];
 #pragma unroll
       for (int p = 0; p < D; ++p) xc[p] = x[p];
-#pragma unroll 4
+      // the next step's row is read into registers one step ahead, so the LDS latency overlaps
+      // the current step's dependent chain instead of preceding it
+      T nx[NR];
+#pragma unroll
+      for (int i = 0; i < NR; ++i) nx[i] = rw[0][i];
+#pragma unroll 2
       for (int s = 0; s < cnt; ++s) {
-        const T* q = rw[s];
+        T q[NR];
+#pragma unroll
+        for (int i = 0; i < NR; ++i) q[i] = nx[i];
+        const int sn = s + 1 < cnt ? s + 1 : s;
+#pragma unroll
+        for (int i = 0; i < NR; ++i) nx[i] = rw[sn][i];
         T b_[D];
         if (!Mdl::kLinear) Mdl::drift(L.th, x, b_);
         const bool mine = lane == s;
@@ -1978,7 +1988,7 @@ __global__ __launch_bounds__(kAccGroup) void k_accept_reduce_lb(const AcceptArgs
 
 // ---------------------------------------------------------------- guiding term on the device
 // recompute_guiding_term!(b) for linear auxiliary laws (src/block.jl:102-110), in the
-// canonical chunked form of dmt_filter.h (identical to the host
+// canonical chunked form of dmt_filter.h (guiding term; identical to the host
 // dmt_guiding_linear).  Three launches per batch of blocks:
 //   k_filter_mark   which law (PP / PPb of a non-terminal block's last segment) each segment uses
 //   k_filter_scan   one wave per 64-step chunk: the step transitions, their suffix scan → qbuf
@@ -2093,6 +2103,45 @@ __global__ __launch_bounds__(256) void k_filter_scan(const FilterArgs a, int64_t
   }
 }
 
+// lane 0's double, broadcast through v_readfirstlane (no LDS traffic; every lane is active)
+__device__ __forceinline__ double bcast0(double v) {
+  const int lo = __builtin_amdgcn_readfirstlane(__double2loint(v));
+  const int hi = __builtin_amdgcn_readfirstlane(__double2hiint(v));
+  return __hiloint2double(hi, lo);
+}
+
+// per-segment inputs of the chain, all wave-uniform; loaded one segment ahead so that their
+// latency overlaps the current segment's chunks
+template <int D>
+struct FiltSeg {
+  static constexpr int HP = D * (D + 1) / 2;
+  int np, slot, kind;
+  int64_t pt, q0, tq, rl;
+  double oH[HP], oF[D], oc, ov[D];
+};
+
+template <int D>
+__device__ __forceinline__ FiltSeg<D> filt_seg(const FilterArgs& a, int g, int g1, bool term) {
+  FiltSeg<D> m;
+  m.np = a.seg_np[g];
+  m.kind = (!term && g == g1) ? 1 : 0;
+  m.slot = (m.kind ? a.selPPB[g] : a.selPP[g]) ^ a.unit;
+  m.pt = a.pt_off[g];
+  m.q0 = a.seg_q[g];
+  const int64_t r = a.seg_rec[g];
+  m.tq = a.tile_qoff[r / a.tw];
+  m.rl = r % a.tw;
+#pragma unroll
+  for (int c = 0; c < FiltSeg<D>::HP; ++c) m.oH[c] = a.obsH[(int64_t)g * FiltSeg<D>::HP + c];
+#pragma unroll
+  for (int p = 0; p < D; ++p) {
+    m.oF[p] = a.obsF[(int64_t)g * D + p];
+    m.ov[p] = m.kind ? a.obsv[(int64_t)g * D + p] : 0.0;
+  }
+  m.oc = a.obsc[g];
+  return m;
+}
+
 template <class T, int D>
 __global__ __launch_bounds__(64) void k_filter_chain(const FilterArgs a) {
   const int64_t blk = a.b0 + blockIdx.x;
@@ -2103,12 +2152,12 @@ __global__ __launch_bounds__(64) void k_filter_chain(const FilterArgs a) {
   const int g0 = a.gfirst[blk], g1 = a.glast[blk];
   const bool term = a.term[blk] != 0;
   using M = flt::Mat<D>;
-  auto loadq = [&](int g, int j) {
+  auto loadq = [&](int64_t pt, int np, int j) {
     flt::Trans<D> q;
     int lo, cnt;
-    filt_chunk(a.seg_np[g], j, lo, cnt);
+    filt_chunk(np, j, lo, cnt);
     if (lane < cnt) {
-      const double* Q = a.qbuf + (a.pt_off[g] + lo + lane - a.pA);
+      const double* Q = a.qbuf + (pt + lo + lane - a.pA);
       int c = 0;
 #pragma unroll
       for (int i = 0; i < D * D; ++i) q.Phi.a[i] = Q[(c++) * a.qcap];
@@ -2126,36 +2175,32 @@ __global__ __launch_bounds__(64) void k_filter_chain(const FilterArgs a) {
     }
     return q;
   };
-  // prefetch cursor over the block's chunks in processing order (segments backward, chunks
-  // backward in time within a segment): the loads do not depend on the chain
-  int pg = g1, pj = 0;
-  auto norm = [&]() { while (pg >= g0 && pj >= filt_nchunks(a.seg_np[pg])) { --pg; pj = 0; } };
-  norm();
+  FiltSeg<D> cur = filt_seg<D>(a, g1, g1, term);
   flt::Trans<D> qnext;
-  if (pg >= g0) qnext = loadq(pg, pj);
+  bool have_next = cur.np > 1;
+  if (have_next) qnext = loadq(cur.pt, cur.np, 0);
   M Hc = flt::mzero<D>();
   double Fc[D], cc = 0.0;
 #pragma unroll
   for (int p = 0; p < d; ++p) Fc[p] = 0.0;
   for (int g = g1; g >= g0; --g) {
-    const int kind = (!term && g == g1) ? 1 : 0;
-    const int slot = (kind ? a.selPPB[g] : a.selPP[g]) ^ a.unit;
+    const FiltSeg<D> nxt = (g > g0) ? filt_seg<D>(a, g - 1, g1, term) : cur;
     // terminal information of the segment: its observation (+ the artificial one of a
     // P_last segment, or + the guiding term at the start of the next segment of the block)
-    M HT = flt::mzero<D>();
-    double FT[D], cT = a.obsc[g];
+    M HT;
+    double FT[D], cT = cur.oc;
 #pragma unroll
     for (int p = 0; p < d; ++p) {
-      FT[p] = a.obsF[(int64_t)g * d + p];
+      FT[p] = cur.oF[p];
 #pragma unroll
-      for (int q = 0; q < d; ++q) HT(p, q) = a.obsH[(int64_t)g * hp + flt::packed_ix(d, p, q)];
+      for (int q = 0; q < d; ++q) HT(p, q) = cur.oH[flt::packed_ix(d, p, q)];
     }
-    if (kind == 1) {
+    if (cur.kind == 1) {
       const double inv = 1.0 / a.art_eps;
       double vv = 0.0;
 #pragma unroll
       for (int p = 0; p < d; ++p) {
-        const double v = a.obsv[(int64_t)g * d + p];
+        const double v = cur.ov[p];
         HT(p, p) += inv;
         FT[p] += inv * v;
         vv += v * v;
@@ -2167,14 +2212,9 @@ __global__ __launch_bounds__(64) void k_filter_chain(const FilterArgs a) {
       for (int p = 0; p < d; ++p) FT[p] += Fc[p];
       cT += cc;
     }
-    const int64_t r = a.seg_rec[g];
-    const int64_t tq = a.tile_qoff[r / a.tw];
-    const int rl = (int)(r % a.tw);
-    auto ix = [&](int64_t q, int c, int C) -> int64_t { return ((tq + q) * C + c) * a.tw + rl; };
-    const int64_t q0 = a.seg_q[g];
-    const int np = a.seg_np[g];
-    T* Ht = (T*)a.H[slot][kind];
-    T* Ft = (T*)a.F[slot][kind];
+    auto ix = [&](int64_t q, int c, int C) -> int64_t { return ((cur.tq + q) * C + c) * a.tw + cur.rl; };
+    T* Ht = (T*)a.H[cur.slot][cur.kind];
+    T* Ft = (T*)a.F[cur.slot][cur.kind];
     Hc = HT;
 #pragma unroll
     for (int p = 0; p < d; ++p) Fc[p] = FT[p];
@@ -2183,19 +2223,24 @@ __global__ __launch_bounds__(64) void k_filter_chain(const FilterArgs a) {
 #pragma unroll
       for (int p = 0; p < d; ++p)
 #pragma unroll
-        for (int q = p; q < d; ++q) Ht[ix(q0 + i, flt::packed_ix(d, p, q), hp)] = (T)Hs(p, q);
+        for (int q = p; q < d; ++q) Ht[ix(cur.q0 + i, flt::packed_ix(d, p, q), hp)] = (T)Hs(p, q);
 #pragma unroll
-      for (int p = 0; p < d; ++p) Ft[ix(q0 + i, p, d)] = (T)Fs[p];
+      for (int p = 0; p < d; ++p) Ft[ix(cur.q0 + i, p, d)] = (T)Fs[p];
     };
-    if (lane == 0) store(np - 1, Hc, Fc);
-    const int nch = filt_nchunks(np);
+    if (lane == 0) store(cur.np - 1, Hc, Fc);
+    const int nch = filt_nchunks(cur.np);
     for (int j = 0; j < nch; ++j) {
       const flt::Trans<D> qcur = qnext;
-      ++pj;
-      norm();
-      if (pg >= g0) qnext = loadq(pg, pj);
+      // prefetch the next chunk in processing order (this segment's, else the previous
+      // segment's first)
+      if (j + 1 < nch) {
+        qnext = loadq(cur.pt, cur.np, j + 1);
+      } else {
+        have_next = g > g0 && nxt.np > 1;
+        if (have_next) qnext = loadq(nxt.pt, nxt.np, 0);
+      }
       int lo, cnt;
-      filt_chunk(np, j, lo, cnt);
+      filt_chunk(cur.np, j, lo, cnt);
       M H = Hc;
       double F[D], c = cc;
 #pragma unroll
@@ -2208,12 +2253,120 @@ __global__ __launch_bounds__(64) void k_filter_chain(const FilterArgs a) {
       if (lane < cnt) store(lo + lane, H, F);
       // lane 0 holds the chunk's first point: the next chunk's end
 #pragma unroll
-      for (int i = 0; i < d * d; ++i) Hc.a[i] = __shfl(H.a[i], 0, 64);
+      for (int i = 0; i < d * d; ++i) Hc.a[i] = bcast0(H.a[i]);
 #pragma unroll
-      for (int p = 0; p < d; ++p) Fc[p] = __shfl(F[p], 0, 64);
-      cc = __shfl(c, 0, 64);
+      for (int p = 0; p < d; ++p) Fc[p] = bcast0(F[p]);
+      cc = bcast0(c);
     }
-    if (lane == 0) a.law[slot][kind][(int64_t)g * DMT_LAW_STRIDE + DMT_LAW_C0] = cc;
+    if (lane == 0) a.law[cur.slot][cur.kind][(int64_t)g * DMT_LAW_STRIDE + DMT_LAW_C0] = cc;
+    if (nch == 0 && g > g0 && nxt.np > 1) qnext = loadq(nxt.pt, nxt.np, 0);
+    cur = nxt;
+  }
+}
+
+// Many blocks (throughput): one wave per block does everything — the chunk's step
+// transitions (lane-parallel), the suffix scan (shuffles) and the combines — with no scratch
+// round trip; other waves hide the latency.  Same arithmetic as k_filter_scan + k_filter_chain.
+template <class T, int D>
+__global__ __launch_bounds__(256) void k_filter_fused(const FilterArgs a) {
+  const int64_t blk = a.b0 + (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (blk >= a.b1) return;
+  if (a.only && !a.only[blk]) return;
+  constexpr int d = D, hp = d * (d + 1) / 2;
+  const int lane = threadIdx.x & 63;
+  const int g0 = a.gfirst[blk], g1 = a.glast[blk];
+  const bool term = a.term[blk] != 0;
+  using M = flt::Mat<D>;
+  const T* tt = (const T*)a.t;
+  M Hc = flt::mzero<D>();
+  double Fc[D], cc = 0.0;
+#pragma unroll
+  for (int p = 0; p < d; ++p) Fc[p] = 0.0;
+  for (int g = g1; g >= g0; --g) {
+    const FiltSeg<D> cur = filt_seg<D>(a, g, g1, term);
+    M B, At;
+    double beta[D];
+    int slot;
+    filt_law<D>(a, g, cur.kind, B, beta, At, slot);
+    M HT;
+    double FT[D], cT = cur.oc;
+#pragma unroll
+    for (int p = 0; p < d; ++p) {
+      FT[p] = cur.oF[p];
+#pragma unroll
+      for (int q = 0; q < d; ++q) HT(p, q) = cur.oH[flt::packed_ix(d, p, q)];
+    }
+    if (cur.kind == 1) {
+      const double inv = 1.0 / a.art_eps;
+      double vv = 0.0;
+#pragma unroll
+      for (int p = 0; p < d; ++p) {
+        const double v = cur.ov[p];
+        HT(p, p) += inv;
+        FT[p] += inv * v;
+        vv += v * v;
+      }
+      cT += 0.5 * inv * vv + 0.5 * d * (0x1.d67f1c864beb4p+0 + flt::flt_log(a.art_eps));
+    } else if (g < g1) {
+      HT = flt::madd(HT, Hc);
+#pragma unroll
+      for (int p = 0; p < d; ++p) FT[p] += Fc[p];
+      cT += cc;
+    }
+    auto ix = [&](int64_t q, int c, int C) -> int64_t { return ((cur.tq + q) * C + c) * a.tw + cur.rl; };
+    auto tat = [&](int i) -> double {
+      return a.t_shared ? (double)tt[cur.q0 + i] : (double)tt[(cur.tq + cur.q0 + i) * a.tw + cur.rl];
+    };
+    T* Ht = (T*)a.H[cur.slot][cur.kind];
+    T* Ft = (T*)a.F[cur.slot][cur.kind];
+    Hc = HT;
+#pragma unroll
+    for (int p = 0; p < d; ++p) Fc[p] = FT[p];
+    cc = cT;
+    auto store = [&](int i, const M& Hs, const double* Fs) {
+#pragma unroll
+      for (int p = 0; p < d; ++p)
+#pragma unroll
+        for (int q = p; q < d; ++q) Ht[ix(cur.q0 + i, flt::packed_ix(d, p, q), hp)] = (T)Hs(p, q);
+#pragma unroll
+      for (int p = 0; p < d; ++p) Ft[ix(cur.q0 + i, p, d)] = (T)Fs[p];
+    };
+    if (lane == 0) store(cur.np - 1, Hc, Fc);
+    const int nch = filt_nchunks(cur.np);
+    for (int j = 0; j < nch; ++j) {
+      int lo, cnt;
+      filt_chunk(cur.np, j, lo, cnt);
+      flt::Trans<D> q;
+      if (lane < cnt) {
+        q = flt::step_trans<D>(B, beta, At, tat(lo + lane + 1) - tat(lo + lane));
+      } else {
+        q.Phi = flt::meye<D>();
+        q.K = flt::mzero<D>();
+#pragma unroll
+        for (int i = 0; i < D; ++i) q.mu[i] = 0.0;
+      }
+#pragma unroll
+      for (int k = 1; k < flt::kFiltChunk; k *= 2) {
+        const flt::Trans<D> o = shfl_down_trans<D>(q, k);
+        if (lane + k < cnt) q = flt::compose<D>(q, o);
+      }
+      M H = Hc;
+      double F[D], c = cc;
+#pragma unroll
+      for (int p = 0; p < d; ++p) F[p] = Fc[p];
+      const bool ok = lane >= cnt || flt::filter_combine<D>(q, H, F, c);
+      if (__ballot(!ok) != 0) {
+        if (lane == 0) *a.fail = 1;
+        return;
+      }
+      if (lane < cnt) store(lo + lane, H, F);
+#pragma unroll
+      for (int i = 0; i < d * d; ++i) Hc.a[i] = bcast0(H.a[i]);
+#pragma unroll
+      for (int p = 0; p < d; ++p) Fc[p] = bcast0(F[p]);
+      cc = bcast0(c);
+    }
+    if (lane == 0) a.law[cur.slot][cur.kind][(int64_t)g * DMT_LAW_STRIDE + DMT_LAW_C0] = cc;
   }
 }
 
@@ -2337,7 +2490,7 @@ __global__ __launch_bounds__(64) void k_set_prop_law(const ParamArgs a, int wg_p
 // set_obs!(bb) (src/biblock.jl:273-280): the artificial observation of a non-terminal block's
 // P_last is the end point of its accepted path; the P_last laws of b and b° that are
 // linearised at an anchor (FHN y_T, Lorenz x_T) are re-anchored there and re-derived
-// (DESIGN.md §3.5).
+// (set_obs!).
 template <class T>
 __global__ void k_set_obs(int tw, int d, const T* X0, const T* X1, const uint8_t* selX,
                           const int64_t* tile_qoff, const int32_t* seg_rec, const int32_t* seg_q,
@@ -2851,11 +3004,15 @@ hipError_t launch_pathll_kernel(const ModelKey& k, int mapping, const void* args
 hipError_t launch_backward_filter(int precision, const FilterArgs& a, hipStream_t s) {
   const int64_t n = a.b1 - a.b0;
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_filter_mark, dim3(nblk(n, 64)), dim3(64), 0, s, a);
+  if (!a.fused) hipLaunchKernelGGL(k_filter_mark, dim3(nblk(n, 64)), dim3(64), 0, s, a);
   // the host copies of fchunk_off bound the scan's work items: passed in via qbuf's batch
   const int64_t item0 = a.fchunk_off_h0, item1 = a.fchunk_off_h1;
 #define DMT_FILTER_LAUNCH(T, D)                                                                \
   do {                                                                                         \
+    if (a.fused) {                                                                             \
+      hipLaunchKernelGGL((k_filter_fused<T, D>), dim3(nblk(n, 4)), dim3(256), 0, s, a);        \
+      break;                                                                                   \
+    }                                                                                          \
     if (item1 > item0)                                                                         \
       hipLaunchKernelGGL((k_filter_scan<T, D>), dim3(nblk(item1 - item0, 4)), dim3(256), 0, s, \
                          a, item0, item1);                                                     \

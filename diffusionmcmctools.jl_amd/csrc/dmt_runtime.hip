@@ -1364,6 +1364,12 @@ static dmt_status guiding_term_device(dmt_ens* h, Layout* L, int64_t b0, int64_t
   a.fchunk_off = h->d_fchunk_off;
   a.segsel = h->d_segsel;
   HIP_OK(hipMemsetAsync(h->d_fail, 0, sizeof(int), h->stream));
+  if (b1 - b0 >= kFiltFusedBlocks) {
+    // enough blocks to fill the device: one wave per block, no transition scratch
+    a.fused = 1;
+    TimedScope ts(h, DMT_K_RECOMPUTE, false);
+    HIP_OK(launch_backward_filter(h->key.precision, a, h->stream));
+  } else {
   // batches of consecutive blocks whose points fit the transition scratch (kFiltBatchPoints,
   // or one block's points if larger)
   auto span = [&](int32_t gA, int32_t gB) { return h->pt_off[gB] + h->seg_np[gB] - h->pt_off[gA]; };
@@ -1388,6 +1394,9 @@ static dmt_status guiding_term_device(dmt_ens* h, Layout* L, int64_t b0, int64_t
   }
   a.qbuf = h->d_qbuf;
   a.qcap = h->qbuf_cap;
+  // stream events around all batches (three launches each: mark, scan, chain)
+  {
+  TimedScope ts(h, DMT_K_RECOMPUTE, false);
   for (int64_t bs = b0; bs < b1;) {
     int32_t gA = L->gfirst[bs], gB = L->glast[bs];
     int64_t be = bs + 1;
@@ -1405,9 +1414,10 @@ static dmt_status guiding_term_device(dmt_ens* h, Layout* L, int64_t b0, int64_t
     a.fchunk_off_h0 = h->fchunk_off[gA];
     a.fchunk_off_h1 = h->fchunk_off[gB + 1];
     HIP_OK(hipMemsetAsync(h->d_segsel + gA, 0, gB - gA + 1, h->stream));
-    TimedScope ts(h, DMT_K_RECOMPUTE);
     HIP_OK(launch_backward_filter(h->key.precision, a, h->stream));
     bs = be;
+  }
+  }
   }
   int failed = 0;
   HIP_OK(hipMemcpyAsync(&failed, h->d_fail, sizeof(int), hipMemcpyDeviceToHost, h->stream));

@@ -66,9 +66,9 @@ def main():
     ens.upload_obs(Hobs, Fobs, cobs)
     t = timed(L.K_RECOMPUTE, lambda: ens.recompute_guiding_term(lay, 0, nb, L.U))
     byt = s * (hp + w.d) * (steps + nb)
-    out.append(dict(kernel="k_backward_filter (recompute_guiding_term!)", us=t * 1e6, bytes=byt,
+    out.append(dict(kernel="k_filter_scan + k_filter_chain (recompute_guiding_term!)", us=t * 1e6, bytes=byt,
                     GBs=byt / t / 1e9, frac=byt / t / 1e9 / PEAK, points_per_s=(steps + nb) / t,
-                    bound="fp64 VALU (exact transition per point)"))
+                    bound="fp64 VALU (exact transition per step, one combine per point)"))
     for o in out:
         o.update(config=f"C3 FHN {nb} blocks x {a.N} steps fp64")
         print(json.dumps(o))

@@ -522,6 +522,32 @@ def test_device_guiding_term_reproduces_uploaded_tables(mapping):
     assert np.array_equal(laws1[:, L.LAW_C0], laws0[:, L.LAW_C0])
 
 
+@pytest.mark.parametrize("split", [False, True], ids=["fused", "scan_chain"])
+def test_device_filter_many_blocks(split):
+    """4 100 single-segment FHN blocks of 130 steps (3 chunks, a partial one): one call over all
+    of them runs k_filter_fused (a wave per block), calls over halves run k_filter_scan +
+    k_filter_chain; both rebuild the host-made tables (the same chunked filter) bit for bit."""
+    import diffusionmcmctools_amd as d
+    from diffusionmcmctools_amd.models import Observation, packed
+    w = W.c3_fhn(B=4100, N=130, T_burn=0.05)
+    dev = d.Ensemble(w.model.kind, w.d, w.m, w.n_points, precision=w.precision, seed=1,
+                     grid_shared=w.grid_shared)
+    lay = W.fill(dev, w, init_Z=False)
+    H0, F0, laws0 = dev.download_law(L.U, L.LAW_PP)
+    infos = [Observation(0.1, np.array([v]), np.array([[1.0, 0.0]]), 0.01 * np.eye(1)).info()
+             for v in w.meta["v"]]
+    dev.upload_obs(np.stack([packed(i[0]) for i in infos]), np.stack([i[1] for i in infos]),
+                   np.array([float(i[2]) for i in infos]))
+    dev.upload_law(L.U, L.LAW_PP, H=np.zeros_like(H0), F=np.zeros_like(F0))
+    ranges = [(0, 2050), (2050, w.nblocks)] if split else [(0, w.nblocks)]
+    for b0, b1 in ranges:
+        dev.recompute_guiding_term(lay, b0, b1, unit=L.U)
+    H1, F1, laws1 = dev.download_law(L.U, L.LAW_PP)
+    assert np.array_equal(H1, H0) and np.array_equal(F1, F0)
+    assert np.array_equal(laws1[:, L.LAW_C0], laws0[:, L.LAW_C0])
+    dev.close()
+
+
 @pytest.mark.parametrize("mapping", MAPPINGS)
 def test_blocking_loop_bit_exact(mapping):
     """The reference's smoothing-with-blocking iteration (docs/src/tutorials/biblock/

@@ -257,7 +257,7 @@ def test_oracle_recompute_guiding_term_reproduces_uploaded_tables():
 
 @pytest.mark.parametrize("npts", [1, 2, 64, 65, 66, 129, 300])
 def test_chunked_filter_lengths(dmt, npts):
-    """The chunked filter (64-step chunks from the segment end) at chunk-edge
+    """The chunked filter (64-step chunks from the segment end, DESIGN.md §3, guiding term) at chunk-edge
     lengths: host == oracle bit for bit, and both agree with the matrix-exponential filter."""
     from diffusionmcmctools_amd.models import FHN, standard_guid_prop_time_transf
     aux = FHN(0.1, -0.8, 1.5, 0.0, 0.3).aux(0.4)
