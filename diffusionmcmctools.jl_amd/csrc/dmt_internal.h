@@ -152,6 +152,7 @@ struct FilterArgs {
   int32_t gA, gB;
   int64_t fchunk_off_h0, fchunk_off_h1;  // fchunk_off[gA], fchunk_off[gB + 1] (host copies)
   int fused;  // many blocks: k_filter_fused (a wave per block, no scratch) instead of scan + chain
+  double* tbuf;  // [items][hp + d + 1] guiding term at each chunk end (k_filter_chain → _points)
 };
 constexpr int kFiltNQ(int d) { return d * d + d + d * (d + 1) / 2; }
 

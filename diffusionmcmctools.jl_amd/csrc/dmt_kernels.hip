@@ -2116,7 +2116,7 @@ template <int D>
 struct FiltSeg {
   static constexpr int HP = D * (D + 1) / 2;
   int np, slot, kind;
-  int64_t pt, q0, tq, rl;
+  int64_t pt, q0, tq, rl, s;  // s: the segment's first chunk item (fchunk_off)
   double oH[HP], oF[D], oc, ov[D];
 };
 
@@ -2128,6 +2128,7 @@ __device__ __forceinline__ FiltSeg<D> filt_seg(const FilterArgs& a, int g, int g
   m.slot = (m.kind ? a.selPPB[g] : a.selPP[g]) ^ a.unit;
   m.pt = a.pt_off[g];
   m.q0 = a.seg_q[g];
+  m.s = a.fchunk_off ? a.fchunk_off[g] : 0;
   const int64_t r = a.seg_rec[g];
   m.tq = a.tile_qoff[r / a.tw];
   m.rl = r % a.tw;
@@ -2142,6 +2143,42 @@ __device__ __forceinline__ FiltSeg<D> filt_seg(const FilterArgs& a, int g, int g
   return m;
 }
 
+// readlane of a wave-uniform lane index (v_readlane_b32 with an SGPR index: no LDS traffic)
+__device__ __forceinline__ double rl_f64(double v, int l) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ int64_t rl_i64(int64_t v, int l) {
+  const int lo = __builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)v, l);
+  const int hi = __builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l);
+  return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+template <int D>
+__device__ __forceinline__ FiltSeg<D> rl_seg(const FiltSeg<D>& m, int l) {
+  FiltSeg<D> r;
+  r.np = __builtin_amdgcn_readlane(m.np, l);
+  r.slot = __builtin_amdgcn_readlane(m.slot, l);
+  r.kind = __builtin_amdgcn_readlane(m.kind, l);
+  r.pt = rl_i64(m.pt, l);
+  r.q0 = rl_i64(m.q0, l);
+  r.tq = rl_i64(m.tq, l);
+  r.rl = rl_i64(m.rl, l);
+  r.s = rl_i64(m.s, l);
+#pragma unroll
+  for (int c = 0; c < FiltSeg<D>::HP; ++c) r.oH[c] = rl_f64(m.oH[c], l);
+#pragma unroll
+  for (int p = 0; p < D; ++p) { r.oF[p] = rl_f64(m.oF[p], l); r.ov[p] = rl_f64(m.ov[p], l); }
+  r.oc = rl_f64(m.oc, l);
+  return r;
+}
+
+// The serial part of the few-blocks filter: one wave per block walks its chunks (segments
+// backward, chunks backward in time) and carries the guiding term from chunk end to chunk start
+// with one combine per chunk, all lanes computing the same values.  The inputs come in lane
+// windows — lane k holds the k-th chunk's whole-chunk transition (the scan's Q at the chunk's
+// first step) and the k-th segment's observation data — read with v_readlane, so the chain
+// itself issues no memory load.  Every chunk's end value goes to tbuf for k_filter_points.
 template <class T, int D>
 __global__ __launch_bounds__(64) void k_filter_chain(const FilterArgs a) {
   const int64_t blk = a.b0 + blockIdx.x;
@@ -2152,41 +2189,53 @@ __global__ __launch_bounds__(64) void k_filter_chain(const FilterArgs a) {
   const int g0 = a.gfirst[blk], g1 = a.glast[blk];
   const bool term = a.term[blk] != 0;
   using M = flt::Mat<D>;
-  auto loadq = [&](int64_t pt, int np, int j) {
-    flt::Trans<D> q;
-    int lo, cnt;
-    filt_chunk(np, j, lo, cnt);
-    if (lane < cnt) {
-      const double* Q = a.qbuf + (pt + lo + lane - a.pA);
+  const int64_t ilo = a.fchunk_off[g0], ihi = a.fchunk_off[g1 + 1];
+  // chunk window: lane k ↔ item wbase + k
+  int64_t wbase = INT64_MIN / 4;  // nothing loaded yet
+  flt::Trans<D> wq;
+  auto load_window = [&](int64_t base) {
+    wbase = base;
+    const int64_t item = base + lane;
+    if (item >= ilo && item < ihi) {
+      int lo_g = g0, hi_g = g1 + 1;  // largest g with fchunk_off[g] <= item
+      while (hi_g - lo_g > 1) {
+        const int mid = (lo_g + hi_g) >> 1;
+        if (a.fchunk_off[mid] <= item) lo_g = mid; else hi_g = mid;
+      }
+      int lo, cnt;
+      filt_chunk(a.seg_np[lo_g], (int)(item - a.fchunk_off[lo_g]), lo, cnt);
+      const double* Q = a.qbuf + (a.pt_off[lo_g] + lo - a.pA);
       int c = 0;
 #pragma unroll
-      for (int i = 0; i < D * D; ++i) q.Phi.a[i] = Q[(c++) * a.qcap];
+      for (int i = 0; i < D * D; ++i) wq.Phi.a[i] = Q[(c++) * a.qcap];
 #pragma unroll
-      for (int i = 0; i < D; ++i) q.mu[i] = Q[(c++) * a.qcap];
+      for (int i = 0; i < D; ++i) wq.mu[i] = Q[(c++) * a.qcap];
 #pragma unroll
       for (int i = 0; i < D; ++i)
 #pragma unroll
-        for (int j2 = i; j2 < D; ++j2) { const double v = Q[(c++) * a.qcap]; q.K(i, j2) = v; q.K(j2, i) = v; }
+        for (int j2 = i; j2 < D; ++j2) { const double v = Q[(c++) * a.qcap]; wq.K(i, j2) = v; wq.K(j2, i) = v; }
     } else {
-      q.Phi = flt::meye<D>();
-      q.K = flt::mzero<D>();
+      wq.Phi = flt::meye<D>();
+      wq.K = flt::mzero<D>();
 #pragma unroll
-      for (int i = 0; i < D; ++i) q.mu[i] = 0.0;
+      for (int i = 0; i < D; ++i) wq.mu[i] = 0.0;
     }
-    return q;
   };
-  FiltSeg<D> cur = filt_seg<D>(a, g1, g1, term);
-  flt::Trans<D> qnext;
-  bool have_next = cur.np > 1;
-  if (have_next) qnext = loadq(cur.pt, cur.np, 0);
+  // segment window: lane k ↔ segment stop − k
+  int stop = -1;
+  FiltSeg<D> wseg;
+  auto load_segs = [&](int top) {
+    stop = top;
+    const int g = top - lane;
+    wseg = filt_seg<D>(a, g >= g0 ? g : g0, g1, term);
+  };
   M Hc = flt::mzero<D>();
   double Fc[D], cc = 0.0;
 #pragma unroll
   for (int p = 0; p < d; ++p) Fc[p] = 0.0;
   for (int g = g1; g >= g0; --g) {
-    const FiltSeg<D> nxt = (g > g0) ? filt_seg<D>(a, g - 1, g1, term) : cur;
-    // terminal information of the segment: its observation (+ the artificial one of a
-    // P_last segment, or + the guiding term at the start of the next segment of the block)
+    if (g > stop || g <= stop - 64) load_segs(g);
+    const FiltSeg<D> cur = rl_seg<D>(wseg, stop - g);
     M HT;
     double FT[D], cT = cur.oc;
 #pragma unroll
@@ -2212,56 +2261,116 @@ __global__ __launch_bounds__(64) void k_filter_chain(const FilterArgs a) {
       for (int p = 0; p < d; ++p) FT[p] += Fc[p];
       cT += cc;
     }
-    auto ix = [&](int64_t q, int c, int C) -> int64_t { return ((cur.tq + q) * C + c) * a.tw + cur.rl; };
-    T* Ht = (T*)a.H[cur.slot][cur.kind];
-    T* Ft = (T*)a.F[cur.slot][cur.kind];
     Hc = HT;
 #pragma unroll
     for (int p = 0; p < d; ++p) Fc[p] = FT[p];
     cc = cT;
-    auto store = [&](int i, const M& Hs, const double* Fs) {
+    if (lane == 0) {  // the segment's end point
+      T* Ht = (T*)a.H[cur.slot][cur.kind];
+      T* Ft = (T*)a.F[cur.slot][cur.kind];
+      const int64_t q = cur.tq + cur.q0 + cur.np - 1;
 #pragma unroll
       for (int p = 0; p < d; ++p)
 #pragma unroll
-        for (int q = p; q < d; ++q) Ht[ix(cur.q0 + i, flt::packed_ix(d, p, q), hp)] = (T)Hs(p, q);
+        for (int r = p; r < d; ++r) Ht[(q * hp + flt::packed_ix(d, p, r)) * a.tw + cur.rl] = (T)Hc(p, r);
 #pragma unroll
-      for (int p = 0; p < d; ++p) Ft[ix(cur.q0 + i, p, d)] = (T)Fs[p];
-    };
-    if (lane == 0) store(cur.np - 1, Hc, Fc);
+      for (int p = 0; p < d; ++p) Ft[(q * d + p) * a.tw + cur.rl] = (T)Fc[p];
+    }
     const int nch = filt_nchunks(cur.np);
     for (int j = 0; j < nch; ++j) {
-      const flt::Trans<D> qcur = qnext;
-      // prefetch the next chunk in processing order (this segment's, else the previous
-      // segment's first)
-      if (j + 1 < nch) {
-        qnext = loadq(cur.pt, cur.np, j + 1);
-      } else {
-        have_next = g > g0 && nxt.np > 1;
-        if (have_next) qnext = loadq(nxt.pt, nxt.np, 0);
-      }
-      int lo, cnt;
-      filt_chunk(cur.np, j, lo, cnt);
-      M H = Hc;
-      double F[D], c = cc;
+      const int64_t item = cur.s + j;
+      if (item < wbase || item >= wbase + 64)
+        load_window(j == 0 ? max(ilo, item + min(nch, 64) - 64) : item);
+      const int wl = (int)(item - wbase);
+      flt::Trans<D> q;
 #pragma unroll
-      for (int p = 0; p < d; ++p) F[p] = Fc[p];
-      const bool ok = lane >= cnt || flt::filter_combine<D>(qcur, H, F, c);
-      if (__ballot(!ok) != 0) {
+      for (int i = 0; i < D * D; ++i) { q.Phi.a[i] = rl_f64(wq.Phi.a[i], wl); q.K.a[i] = rl_f64(wq.K.a[i], wl); }
+#pragma unroll
+      for (int i = 0; i < D; ++i) q.mu[i] = rl_f64(wq.mu[i], wl);
+      if (lane == 0) {  // the chunk end's guiding term, for k_filter_points
+        double* tb = a.tbuf + (item - a.fchunk_off_h0) * (hp + d + 1);
+        int c = 0;
+#pragma unroll
+        for (int p = 0; p < d; ++p)
+#pragma unroll
+          for (int r = p; r < d; ++r) tb[c++] = Hc(p, r);
+#pragma unroll
+        for (int p = 0; p < d; ++p) tb[c++] = Fc[p];
+        tb[c] = cc;
+      }
+      if (!flt::filter_combine<D>(q, Hc, Fc, cc)) {
         if (lane == 0) *a.fail = 1;
         return;
       }
-      if (lane < cnt) store(lo + lane, H, F);
-      // lane 0 holds the chunk's first point: the next chunk's end
-#pragma unroll
-      for (int i = 0; i < d * d; ++i) Hc.a[i] = bcast0(H.a[i]);
-#pragma unroll
-      for (int p = 0; p < d; ++p) Fc[p] = bcast0(F[p]);
-      cc = bcast0(c);
     }
     if (lane == 0) a.law[cur.slot][cur.kind][(int64_t)g * DMT_LAW_STRIDE + DMT_LAW_C0] = cc;
-    if (nch == 0 && g > g0 && nxt.np > 1) qnext = loadq(nxt.pt, nxt.np, 0);
-    cur = nxt;
   }
+}
+
+// The parallel part of the few-blocks filter: one wave per chunk, every point of the chunk
+// combined from the chunk end's guiding term (tbuf) — the same combine the chain made for the
+// chunk's first point, so that point is written with the chain's own value.
+template <class T, int D>
+__global__ __launch_bounds__(256) void k_filter_points(const FilterArgs a, int64_t item0,
+                                                       int64_t item1) {
+  const int lane = threadIdx.x & 63;
+  const int64_t item = item0 + (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (item >= item1) return;
+  int lo_g = a.gA, hi_g = a.gB + 1;
+  while (hi_g - lo_g > 1) {
+    const int mid = (lo_g + hi_g) >> 1;
+    if (a.fchunk_off[mid] <= item) lo_g = mid; else hi_g = mid;
+  }
+  const int g = lo_g;
+  const int sel = a.segsel[g];
+  if (!sel) return;
+  constexpr int d = D, hp = d * (d + 1) / 2;
+  const int kind = sel - 1;
+  const int slot = (kind ? a.selPPB[g] : a.selPP[g]) ^ a.unit;
+  int lo, cnt;
+  filt_chunk(a.seg_np[g], (int)(item - a.fchunk_off[g]), lo, cnt);
+  if (lane >= cnt) return;
+  const double* tb = a.tbuf + (item - a.fchunk_off_h0) * (hp + d + 1);
+  flt::Mat<D> H;
+  double F[D], c;
+  {
+    int k = 0;
+#pragma unroll
+    for (int p = 0; p < d; ++p)
+#pragma unroll
+      for (int r = p; r < d; ++r) { const double v = tb[k++]; H(p, r) = v; H(r, p) = v; }
+#pragma unroll
+    for (int p = 0; p < d; ++p) F[p] = tb[k++];
+    c = tb[k];
+  }
+  flt::Trans<D> q;
+  {
+    const double* Q = a.qbuf + (a.pt_off[g] + lo + lane - a.pA);
+    int k = 0;
+#pragma unroll
+    for (int i = 0; i < D * D; ++i) q.Phi.a[i] = Q[(k++) * a.qcap];
+#pragma unroll
+    for (int i = 0; i < D; ++i) q.mu[i] = Q[(k++) * a.qcap];
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int j2 = i; j2 < D; ++j2) { const double v = Q[(k++) * a.qcap]; q.K(i, j2) = v; q.K(j2, i) = v; }
+  }
+  if (!flt::filter_combine<D>(q, H, F, c)) {
+    *a.fail = 1;
+    return;
+  }
+  const int64_t r = a.seg_rec[g];
+  const int64_t qq = a.tile_qoff[r / a.tw] + a.seg_q[g] + lo + lane;
+  const int rl = (int)(r % a.tw);
+  T* Ht = (T*)a.H[slot][kind];
+  T* Ft = (T*)a.F[slot][kind];
+#pragma unroll
+  for (int p = 0; p < d; ++p)
+#pragma unroll
+    for (int r2 = p; r2 < d; ++r2) Ht[(qq * hp + flt::packed_ix(d, p, r2)) * a.tw + rl] = (T)H(p, r2);
+#pragma unroll
+  for (int p = 0; p < d; ++p) Ft[(qq * d + p) * a.tw + rl] = (T)F[p];
 }
 
 // Many blocks (throughput): one wave per block does everything — the chunk's step
@@ -3017,6 +3126,9 @@ hipError_t launch_backward_filter(int precision, const FilterArgs& a, hipStream_
       hipLaunchKernelGGL((k_filter_scan<T, D>), dim3(nblk(item1 - item0, 4)), dim3(256), 0, s, \
                          a, item0, item1);                                                     \
     hipLaunchKernelGGL((k_filter_chain<T, D>), dim3(n), dim3(64), 0, s, a);                    \
+    if (item1 > item0)                                                                         \
+      hipLaunchKernelGGL((k_filter_points<T, D>), dim3(nblk(item1 - item0, 4)), dim3(256), 0,  \
+                         s, a, item0, item1);                                                  \
   } while (0)
   if (precision == DMT_F64) {
     if (a.d == 1) DMT_FILTER_LAUNCH(double, 1);

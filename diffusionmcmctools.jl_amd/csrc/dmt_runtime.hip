@@ -135,6 +135,8 @@ struct dmt_ens {
   uint8_t* d_segsel = nullptr;      // [G]
   double* d_qbuf = nullptr;         // [kFiltNQ(d)][qbuf_cap]
   int64_t qbuf_cap = 0;
+  double* d_tbuf = nullptr;         // [tbuf_cap][hp + d + 1] guiding term at chunk ends
+  int64_t tbuf_cap = 0;
   double art_eps = 1e-11;    // artificial_noise (src/sampling_unit.jl:57)
   // staging
   double* d_stage = nullptr;
@@ -698,7 +700,7 @@ dmt_status dmt_destroy(dmt_ens* h) {
                 h->d_W[0], h->d_W[1], h->d_t, h->d_stage, h->d_Z, h->d_red, h->d_gather,
                 h->d_red_work, h->d_run, h->d_run_gather, h->d_part, h->d_red_lb, h->d_obsH,
                 h->d_obsF, h->d_obsc, h->d_obsv, h->d_fail, h->d_fchunk_off, h->d_segsel,
-                h->d_qbuf};
+                h->d_qbuf, h->d_tbuf};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   for (int s = 0; s < 2; ++s)
@@ -1413,6 +1415,19 @@ static dmt_status guiding_term_device(dmt_ens* h, Layout* L, int64_t b0, int64_t
     a.pA = h->pt_off[gA];
     a.fchunk_off_h0 = h->fchunk_off[gA];
     a.fchunk_off_h1 = h->fchunk_off[gB + 1];
+    const int64_t items = a.fchunk_off_h1 - a.fchunk_off_h0;
+    if (items > h->tbuf_cap) {
+      if (h->d_tbuf) {
+        HIP_OK(hipStreamSynchronize(h->stream));
+        HIP_OK(hipFree(h->d_tbuf));
+        h->bytes -= h->tbuf_cap * (h->hp + h->d + 1) * 8;
+        h->d_tbuf = nullptr;
+        h->tbuf_cap = 0;
+      }
+      DMT_TRY(ens_alloc(h, &h->d_tbuf, items * (h->hp + h->d + 1)));
+      h->tbuf_cap = items;
+    }
+    a.tbuf = h->d_tbuf;
     HIP_OK(hipMemsetAsync(h->d_segsel + gA, 0, gB - gA + 1, h->stream));
     HIP_OK(launch_backward_filter(h->key.precision, a, h->stream));
     bs = be;
