@@ -67,17 +67,25 @@ def simulate_fhn(model, t, x0, rng):
     return X
 
 
-def tutorial_data(seed=100, T=10.0, dt=1e-4, every=1000):
-    """The preamble's dataset: (Recording, latent path X, its grid t)."""
+def tutorial_data(seed=100, T=10.0, dt=1e-4, every=1000, num_recs=None):
+    """The preamble's dataset: (Recording, latent path X, its grid t).  With ``num_recs`` the
+    block_ensemble tutorial's data (block_ensemble/inference.md:16-31): that many independent
+    recordings from the same start point, as lists."""
     rng = np.random.default_rng(seed)
     model = FHN(*THETA)
     n = int(round(T / dt))
     t = np.arange(n + 1) * dt
-    X = simulate_fhn(model, t, Y1, rng)
     noise_sd = math.sqrt(OBS_SIGMA[0, 0])
-    obs = [Observation(float(t[i]), np.array([X[i, 0] + noise_sd * rng.standard_normal()]),
-                       OBS_L, OBS_SIGMA) for i in range(every, n + 1, every)]
-    return Recording(obs, 0.0, np.array(Y1)), X, t
+    recs, Xs = [], []
+    for _ in range(1 if num_recs is None else num_recs):
+        X = simulate_fhn(model, t, Y1, rng)
+        obs = [Observation(float(t[i]), np.array([X[i, 0] + noise_sd * rng.standard_normal()]),
+                           OBS_L, OBS_SIGMA) for i in range(every, n + 1, every)]
+        recs.append(Recording(obs, 0.0, np.array(Y1)))
+        Xs.append(X)
+    if num_recs is None:
+        return recs[0], Xs[0], t
+    return recs, Xs, t
 
 
 def sampling_pair(recording, gamma, dt=1e-3, backend="device", seed=0, blocking=False):
@@ -92,23 +100,31 @@ def sampling_pair(recording, gamma, dt=1e-3, backend="device", seed=0, blocking=
     th = list(THETA)
     th[2] = gamma
     model = FHN(*th)
-    grids = setup_time_grids(recording, dt)
-    auxes = [model.aux(ob.v[0]) for ob in recording.obs]
-    infos = [ob.info() for ob in recording.obs]
-    chain = guiding_chain(auxes, grids, infos)
-    H = np.concatenate([c[0] for c in chain])
-    F = np.concatenate([c[1] for c in chain])
-    laws = np.stack([model.law_record(a, c[2][0]) for a, c in zip(auxes, chain)])
-    n_points = [[len(g) for g in grids]]
+    recordings = recording if isinstance(recording, (list, tuple)) else [recording]
+    t_all, H_all, F_all, law_all, n_points, infos_all = [], [], [], [], [], []
+    Hb_all, Fb_all, lb_all = [], [], []
+    for rec in recordings:
+        grids = setup_time_grids(rec, dt)
+        auxes = [model.aux(ob.v[0]) for ob in rec.obs]
+        infos = [ob.info() for ob in rec.obs]
+        chain = guiding_chain(auxes, grids, infos)
+        t_all += grids
+        H_all += [c[0] for c in chain]
+        F_all += [c[1] for c in chain]
+        law_all += [model.law_record(a_, c[2][0]) for a_, c in zip(auxes, chain)]
+        n_points.append([len(g) for g in grids])
+        infos_all += infos
+        if blocking:
+            for k, (a_, ob) in enumerate(zip(auxes, rec.obs)):
+                Ha, Fa, ca = artificial_obs_info(np.array([ob.v[0], 0.0]), ARTIFICIAL_NOISE)
+                Ho, Fo, co = infos[k]
+                (h, f, c), = guiding_chain([a_], [grids[k]], [(Ha + Ho, Fa + Fo, ca + co)])
+                Hb_all.append(h); Fb_all.append(f); lb_all.append(model.law_record(a_, c[0]))
+    H, F, laws = np.concatenate(H_all), np.concatenate(F_all), np.stack(law_all)
+    infos = infos_all
     blaws = {}
     if blocking:
-        Hb, Fb, lb = [], [], []
-        for k, (a_, ob) in enumerate(zip(auxes, recording.obs)):
-            Ha, Fa, ca = artificial_obs_info(np.array([ob.v[0], 0.0]), ARTIFICIAL_NOISE)
-            Ho, Fo, co = infos[k]
-            (h, f, c), = guiding_chain([a_], [grids[k]], [(Ha + Ho, Fa + Fo, ca + co)])
-            Hb.append(h); Fb.append(f); lb.append(model.law_record(a_, c[0]))
-        blaws = dict(Hb=np.concatenate(Hb), Fb=np.concatenate(Fb), lawsb=np.stack(lb))
+        blaws = dict(Hb=np.concatenate(Hb_all), Fb=np.concatenate(Fb_all), lawsb=np.stack(lb_all))
     if backend == "oracle":
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle as orc
@@ -116,12 +132,12 @@ def sampling_pair(recording, gamma, dt=1e-3, backend="device", seed=0, blocking=
         se = dmt.SamplingEnsemble(model, n_points, _engine=eng)
     else:
         se = dmt.SamplingEnsemble(model, n_points, seed=seed)
-    se.upload_grid(np.concatenate(grids))
+    se.upload_grid(np.concatenate(t_all))
     se.set_guiding(H, F, laws, **blaws)
     se.set_observations(np.stack([packed(i[0]) for i in infos]),
                         np.stack([np.asarray(i[1], dtype=np.float64) for i in infos]),
                         np.array([float(i[2]) for i in infos]), artificial_noise=ARTIFICIAL_NOISE)
-    ll0, ok = se.init_paths([recording.x0], iter=0)
+    ll0, ok = se.init_paths([rec.x0 for rec in recordings], iter=0)
     if not ok.all():
         raise RuntimeError("init_paths failed")
     return se
@@ -133,9 +149,11 @@ def simple_inference(se, gamma0, eps=0.3, rho=0.96, num_steps=10 ** 4, seed=1,
     Returns a dict with the γ chain (num_steps + 1 values), the per-iteration path and
     parameter decisions and the accepted log-likelihood per iteration."""
     rng = np.random.default_rng(seed)
-    nseg = len(se.n_points[0])
-    be = dmt.BlockEnsemble(se, [[range(0, nseg)]], rho=rho, ll_hist_len=num_steps)
-    bb = be.recordings[0].blocks[0]
+    be = dmt.BlockEnsemble(se, [[range(0, len(r))] for r in se.n_points], rho=rho,
+                           ll_hist_len=num_steps)
+    # one recording: the BiBlock of biblock/inference.md; several: the whole BlockEnsemble of
+    # block_ensemble/inference.md (one terminal block per recording, γ shared)
+    bb = be.recordings[0].blocks[0] if se.num_recordings() == 1 else be
     n_snap = num_steps // snapshot_every if snapshot_every else 0
     if n_snap:
         se.reserve_snapshots(n_snap)
@@ -144,7 +162,8 @@ def simple_inference(se, gamma0, eps=0.3, rho=0.96, num_steps=10 ** 4, seed=1,
     chain, a_path, a_par, ll_acc = [theta[0]], [], [], []
     for i in range(1, num_steps + 1):
         bb.draw_proposal_path(iter=i)
-        a_path.append(bool(bb.accept_reject_proposal_path(i)[0]))
+        acc_p = np.asarray(bb.accept_reject_proposal_path(i))
+        a_path.append(bool(acc_p[0]) if acc_p.size == 1 else acc_p)
         theta_p = theta + 2.0 * eps * (rng.random() - 0.5)          # customkernel(θ, ϵ)
         bb.set_proposal_law(theta={"gamma": theta_p[0]})
         acc, theta = bb.accept_reject_proposal_param(i, theta, theta_p,
@@ -212,12 +231,16 @@ def main():
     ap.add_argument("--steps", type=int, default=10 ** 4)
     ap.add_argument("--burn-in", type=int, default=1000)
     ap.add_argument("--backend", default="device", choices=["device", "oracle"])
+    ap.add_argument("--recordings", type=int, default=1,
+                    help="> 1: block_ensemble/inference.md (that many recordings sharing γ)")
     ap.add_argument("--blocking", action="store_true",
                     help="biblock/inference_with_blocking.md instead of biblock/inference.md")
     ap.add_argument("--out", default=None, help="write the summary (and chain) as JSON here")
     a = ap.parse_args()
+    if a.blocking and a.recordings != 1:
+        ap.error("--blocking runs the one-recording tutorial (biblock/inference_with_blocking.md)")
     t0 = time.perf_counter()
-    rec, _, _ = tutorial_data()
+    rec, _, _ = tutorial_data(num_recs=a.recordings if a.recordings > 1 else None)
     t1 = time.perf_counter()
     se = sampling_pair(rec, THETA[2], backend=a.backend, blocking=a.blocking)
     if a.blocking:
@@ -228,11 +251,12 @@ def main():
         res = simple_inference(se, THETA[2], num_steps=a.steps,
                                snapshot_every=400 if a.backend == "device" else 0,
                                log=lambda s: print(s, flush=True))
-        tut = "docs/src/tutorials/biblock/inference.md"
+        tut = ("docs/src/tutorials/biblock/inference.md" if a.recordings == 1 else
+               "docs/src/tutorials/block_ensemble/inference.md")
     t2 = time.perf_counter()
     out = dict(tutorial=tut, backend=a.backend,
                steps=a.steps, burn_in=a.burn_in, data_seconds=t1 - t0, run_seconds=t2 - t1,
-               n_obs=len(rec.obs), n_points=int(sum(se.n_points[0])),
+               n_obs=sum(len(r) for r in se.n_points), n_points=int(sum(map(sum, se.n_points))),
                **summarize(res, a.burn_in))
     print(json.dumps(out))
     if a.out:

@@ -135,3 +135,35 @@ def test_blocking_tutorial_device_equals_oracle(recording):
         np.testing.assert_array_equal(rd[k], ro[k], err_msg=k)
     np.testing.assert_array_equal(Xd, Xo)
     np.testing.assert_array_equal(Wd, Wo)
+
+
+# ------------------------------------------------------------------ BlockEnsemble (γ shared)
+@pytest.fixture(scope="module")
+def recordings2():
+    recs, _, _ = tut.tutorial_data(num_recs=2)
+    return recs
+
+
+def test_ensemble_tutorial_loop_on_oracle(recordings2):
+    """block_ensemble/inference.md: two recordings, one terminal block each, the ensemble-level
+    draw / accept / set_proposal_law! / parameter decision on fetch_ll° − fetch_ll."""
+    se = tut.sampling_pair(recordings2, 1.5, backend="oracle")
+    assert se.num_recordings() == 2 and sum(map(sum, se.n_points)) == 2 * 100 * 101
+    res = tut.simple_inference(se, 1.5, num_steps=8, snapshot_every=0)
+    assert res["accepted_path"].shape == (8, 2) and np.all(np.isfinite(res["ll"]))
+    np.testing.assert_array_equal(np.diff(res["gamma"]) != 0, res["accepted_param"])
+
+
+@pytest.mark.gpu
+def test_ensemble_tutorial_device_equals_oracle(recordings2):
+    out = []
+    for backend in ("device", "oracle"):
+        se = tut.sampling_pair(recordings2, 1.5, backend=backend)
+        res = tut.simple_inference(se, 1.5, num_steps=15, snapshot_every=0)
+        out.append((res, se.ens.download_paths(0, 0)))
+        if backend == "device":
+            se.close()
+    (rd, Xd), (ro, Xo) = out
+    for k in ("gamma", "accepted_path", "accepted_param", "ll"):
+        np.testing.assert_array_equal(rd[k], ro[k], err_msg=k)
+    np.testing.assert_array_equal(Xd, Xo)
