@@ -915,7 +915,7 @@ static int fm_combine(const ftr_t* q, fm_t* Hc, double* Fc, double* cc) {
 
 /* Backward filter over one segment's grid t[npts] from the terminal information (HT packed,
  * FT, cT): H[npts][hp] packed, F[npts][d], c[npts] (double).  Returns 0 if singular.
- * Canonical chunked form: chunks of FILT_CHUNK steps counted from the
+ * Canonical chunked form (guiding term): chunks of FILT_CHUNK steps counted from the
  * segment end; per chunk an inclusive Kogge-Stone suffix scan of the step transitions
  * (stage k: Q_l <- compose(Q_l, Q_{l+k}) if l + k < cnt, previous-stage values), then every
  * point of the chunk by one combine from the chunk end's (H, F, c). */

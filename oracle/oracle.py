@@ -606,7 +606,7 @@ class OracleEnsemble:
         """GP.set_obs!(bb) (src/biblock.jl:273-280): P_last of b and b° observes the accepted
         end point; an auxiliary law linearised at its anchor (FHN: y_T, Lorenz: x_T) is
         re-anchored there and re-derived (set_law_params with no parameter writes), so that
-        b̃ matches b at the exact end point."""
+        b̃ matches b at the exact end point (set_obs!)."""
         na = {1: 1, 2: 3}.get(self.model, 0)
         for bk in self.layouts[layout][b0:b1]:
             if not bk.term:
