@@ -109,7 +109,9 @@ DMT_HD double flt_log(double u) {
 }
 
 // inverse and log|det| by Gauss–Jordan with partial pivoting; false if singular.  Row swaps
-// are done with selects over all rows (no dynamic register indexing).
+// are done with selects over all rows (no dynamic register indexing).  The pivot row is scaled
+// by the correctly rounded reciprocal of the pivot, and log|det| is one log of the product of
+// the |pivots| (guiding term).
 template <int N>
 DMT_HD bool minv(const Mat<N>& A, Mat<N>& Inv, double& logabsdet) {
   double w[N][2 * N];
@@ -117,7 +119,7 @@ DMT_HD bool minv(const Mat<N>& A, Mat<N>& Inv, double& logabsdet) {
   for (int i = 0; i < N; ++i)
 #pragma unroll
     for (int j = 0; j < N; ++j) { w[i][j] = A(i, j); w[i][N + j] = (i == j) ? 1.0 : 0.0; }
-  logabsdet = 0.0;
+  double detabs = 1.0;  // |det| as the product of the |pivots| in order; one log at the end
 #pragma unroll
   for (int c = 0; c < N; ++c) {
     int p = c;
@@ -143,9 +145,10 @@ DMT_HD bool minv(const Mat<N>& A, Mat<N>& Inv, double& logabsdet) {
 #pragma unroll
     for (int j = 0; j < 2 * N; ++j) w[c][j] = prow[j];
     const double piv = w[c][c];
-    logabsdet += flt_log(fabs(piv));
+    detabs *= fabs(piv);
+    const double rp = 1.0 / piv;  // one correctly rounded division per pivot row
 #pragma unroll
-    for (int j = 0; j < 2 * N; ++j) w[c][j] /= piv;
+    for (int j = 0; j < 2 * N; ++j) w[c][j] *= rp;
 #pragma unroll
     for (int i = 0; i < N; ++i)
       if (i != c) {
@@ -160,6 +163,7 @@ DMT_HD bool minv(const Mat<N>& A, Mat<N>& Inv, double& logabsdet) {
   for (int i = 0; i < N; ++i)
 #pragma unroll
     for (int j = 0; j < N; ++j) Inv(i, j) = w[i][N + j];
+  logabsdet = flt_log(detabs);
   return true;
 }
 

@@ -797,15 +797,16 @@ static double fm_norm(const fm_t* A) {
 static int fm_inv(const fm_t* A, fm_t* Inv, double* lad) {
     int n = A->n; double w[3][6];
     for (int i = 0; i < n; ++i) for (int j = 0; j < n; ++j) { w[i][j] = A->a[i * n + j]; w[i][n + j] = (i == j) ? 1.0 : 0.0; }
-    *lad = 0.0;
+    double detabs = 1.0;
     for (int c = 0; c < n; ++c) {
         int p = c;
         for (int i = c + 1; i < n; ++i) if (fabs(w[i][c]) > fabs(w[p][c])) p = i;
         if (w[p][c] == 0.0) return 0;
         if (p != c) for (int j = 0; j < 2 * n; ++j) { double t = w[p][j]; w[p][j] = w[c][j]; w[c][j] = t; }
         double piv = w[c][c];
-        *lad += rng_log(fabs(piv));
-        for (int j = 0; j < 2 * n; ++j) w[c][j] /= piv;
+        detabs *= fabs(piv);
+        double rp = 1.0 / piv;
+        for (int j = 0; j < 2 * n; ++j) w[c][j] *= rp;
         for (int i = 0; i < n; ++i) if (i != c) {
             double f = w[i][c];
             if (f != 0.0) for (int j = 0; j < 2 * n; ++j) w[i][j] -= f * w[c][j];
@@ -813,6 +814,7 @@ static int fm_inv(const fm_t* A, fm_t* Inv, double* lad) {
     }
     *Inv = fm_zero(n);
     for (int i = 0; i < n; ++i) for (int j = 0; j < n; ++j) Inv->a[i * n + j] = w[i][n + j];
+    *lad = rng_log(detabs);
     return 1;
 }
 static void fm_transition(const fm_t* B, const double* beta, const fm_t* At, double h,
