@@ -548,6 +548,28 @@ def test_device_filter_many_blocks(split):
     dev.close()
 
 
+@pytest.mark.parametrize("B", [300, 4100], ids=["scan_chain", "fused"])
+def test_device_filter_lorenz_fp32(B):
+    """The device filter for d = 3 on an fp32 ensemble (C5's Lorenz law, full-state
+    observations, grids and tables in float): device == oracle bit for bit, through the
+    few-blocks kernels (300 blocks) and the fused kernel (4 100 blocks)."""
+    from diffusionmcmctools_amd.models import Observation, packed
+    w = W.c5_lorenz(B=B, N=130)
+    dev, ora, lay = cs.both(w, hist_len=1, init_Z=False)
+    infos = [Observation(0.2, v, np.eye(3), 0.1 * np.eye(3)).info() for v in w.meta["v"]]
+    Hobs = np.stack([packed(i[0]) for i in infos])
+    Fobs = np.stack([i[1] for i in infos])
+    cobs = np.array([float(i[2]) for i in infos])
+    for e in (dev, ora):
+        e.upload_obs(Hobs, Fobs, cobs)
+        e.recompute_guiding_term(lay, 0, w.nblocks, unit=L.U)
+    Hd, Fd, ld = dev.download_law(L.U, L.LAW_PP)
+    Ho, Fo, lo = ora.download_law(L.U, L.LAW_PP)
+    assert np.array_equal(Hd, Ho) and np.array_equal(Fd, Fo)
+    assert np.array_equal(ld[:, L.LAW_C0], lo[:, L.LAW_C0])
+    dev.close()
+
+
 @pytest.mark.parametrize("mapping", MAPPINGS)
 def test_blocking_loop_bit_exact(mapping):
     """The reference's smoothing-with-blocking iteration (docs/src/tutorials/biblock/
