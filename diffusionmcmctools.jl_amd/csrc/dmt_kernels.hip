@@ -731,7 +731,10 @@ __global__ __launch_bounds__(128) void k_block_wave(const BlockArgs<T> a) {
       T nx[NR];
 #pragma unroll
       for (int i = 0; i < NR; ++i) nx[i] = rw[0][i];
-#pragma unroll 2
+#ifndef DMT_S_UNROLL
+#define DMT_S_UNROLL 4
+#endif
+#pragma unroll DMT_S_UNROLL
       for (int s = 0; s < cnt; ++s) {
         T q[NR];
 #pragma unroll
