@@ -10,17 +10,19 @@ BlockEnsemble level (src/block_ensemble.jl:50,63-67,140).  Throughput unit: brid
 Euler steps (one grid increment of one segment) per second, whole job.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c5]
-Multi-GPU: launched by torch.distributed.run, one rank per GPU, weak scaling: rank r owns
-recording shard r of a global ensemble of N x B blocks (RNG keyed by global segment ids,
-diffusionmcmctools.jl_amd/shard.py); the only collective is fetch_ll's RCCL all-gather of
-3 doubles per iteration.
+Multi-GPU: one process per GPU, weak scaling: rank r owns recording shard r of a global
+ensemble of N x B blocks (RNG keyed by global segment ids, diffusionmcmctools.jl_amd/shard.py);
+the only collective is fetch_ll's RCCL all-gather of 3 doubles per iteration.  Under
+torch.distributed.run the ranks come from RANK/LOCAL_RANK/WORLD_SIZE; run directly with
+--gpus N > 1 (WORLD_SIZE unset), this process spawns the N ranks itself before touching a GPU.
 """
 from __future__ import annotations
 
 import argparse
 import json
-import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -29,8 +31,9 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-PEAK_HBM_GBS = 8000.0
-EXTRA_ITERS = 5  # untimed iterations after the timed region (accept-kernel event timing)  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md, chip-level parameters)
+EXTRA_ITERS = 5        # untimed iterations after the timed region (accept-kernel event timing)
+CPU_MAX_ITERS = 4000   # bound of the CPU-baseline sample (history slots reserved for it)
 
 WORKLOADS = {
     "c2": ("C2: 2D OU guided bridge, 1024 blocks x 500 Euler steps per GPU, fp64", "f64"),
@@ -58,17 +61,22 @@ def algorithmic_bytes_per_step(w):
     return s * (2 * w.m + 2 * w.d + h)
 
 
+def _newest(pattern):
+    """Committed profile files matching a glob, newest run tag first (tags r01, r01b … r01z,
+    r01aa …, r02a …: ordered by round, then tag length, then name)."""
+    import glob
+
+    def tag(p):
+        t = os.path.basename(p).split("_")[0]
+        return (t[:3], len(t), t)
+    return sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)), key=tag, reverse=True)
+
+
 def measured_traffic(config, kernel_substr):
-    """HBM bytes per launch of the draw kernel from the newest committed PMC summary
+    """HBM bytes per iteration of the draw kernel from the newest committed PMC summary
     (profiles/rNN_traffic_<config>.json, scripts/pmc_traffic.py: separate FETCH_SIZE and
     WRITE_SIZE rocprofv3 passes, calibrated with scripts/calib_stream); None if absent."""
-    import glob
-    # run tags go r01, r01b … r01z, r01aa …: newest = longest tag, then the last in order
-    def tag(p):
-        t = os.path.basename(p).split("_traffic_")[0]
-        return (len(t), t)
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_traffic_{config}.json")), key=tag)
-    for path in reversed(files):
+    for path in _newest(f"r*_traffic_{config}.json"):
         with open(path) as f:
             t = json.load(f)
         if kernel_substr in t.get("kernel", ""):
@@ -76,13 +84,57 @@ def measured_traffic(config, kernel_substr):
     return None, None
 
 
-def cpu_baseline(w, ens, lay, budget_s=12.0):
+def issue_roofline(config, kernel_substr):
+    """VALU issue figures of the dominant kernel from the newest committed SQ-counter summary
+    (profiles/rNN_issue_<config>.json, scripts/sq_summary.py): VALU instructions per step and
+    per wave-iteration, VALU-active fraction of the wave cycles; None if absent."""
+    for path in _newest(f"r*_issue_{config}.json"):
+        with open(path) as f:
+            t = json.load(f)
+        if kernel_substr in t.get("kernel", ""):
+            t = dict(t)
+            t["source"] = os.path.relpath(path, ROOT)
+            return t
+    return None
+
+
+def host_cpu_info():
+    """nproc, the CPUs this process may run on, OMP_NUM_THREADS and the lscpu model name."""
+    model = None
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except Exception:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except Exception:
+        affinity = os.cpu_count()
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return {"nproc": os.cpu_count(), "affinity": affinity,
+            "omp_num_threads": int(omp) if omp and omp.isdigit() else None, "model": model}
+
+
+def cpu_baseline(w, ens, lay, iter0, budget_s=12.0):
     """The oracle's OpenMP restatement (oracle/dmt_oracle.c) timed on this host on a bounded
-    sample: whole MCMC iterations (draw + MH accept) of the same per-GPU workload."""
+    sample of whole MCMC iterations (draw + MH accept) of the same per-GPU workload, from the
+    device's current state and with the device's streams: iteration it draws the normals of
+    key (it, salt 0) and the Exp(1) variables of the same key — exactly what the device's next
+    dmt_mcmc_run(iter0, …) draws.  The CPU leg runs the reference's sequential Euler loop
+    (oracle sequential=True), the device the canonical parallel affine scan (OU) or the same
+    recursion (FHN, Lorenz); the device then runs the same iterations and the per-block MH
+    decisions are compared.  Threads: every CPU this process may use, capped by
+    OMP_NUM_THREADS (the GPU box's CPU share) when that is set."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as orc
     from diffusionmcmctools_amd import _lib as L
-    nthreads = max(1, min(16, os.cpu_count() or 1))
+    info = host_cpu_info()
+    nthreads = info["affinity"] or 1
+    if info["omp_num_threads"]:
+        nthreads = min(nthreads, info["omp_num_threads"])
     B = w.nblocks
     npts = w.n_points[0][0]
     X = ens.download_paths(L.U, 0)
@@ -90,44 +142,86 @@ def cpu_baseline(w, ens, lay, budget_s=12.0):
     Wp = Wc.copy()                                          # the oracle holds increments
     Wp[:, 1:] = Wc[:, 1:] - Wc[:, :-1]
     Wp = Wp.reshape(B * npts, w.m)
-    ens.loglikhd(lay, L.U, 0, B)
     ll = ens.get_block_state(lay, L.BLK_LL, 0, B)
     rho = np.full(B, w.rho)
     prec = w.precision
-    rng = np.random.default_rng(0)
-    res = {}
-    for nt in sorted({1, nthreads}):
-        it = 0
-        acc_n = 0
+
+    def run(nt, max_it, budget, record):
         Xa, Wa, lla = X.copy(), Wp.copy(), ll.copy()
+        decisions = []
+        it, acc_n = 0, 0
         t0 = time.perf_counter()
-        while True:
-            it += 1
+        while it < max_it:
+            key = iter0 + it
             Xo, Wo, llp, _ = orc.draw_terminal_blocks(
                 w.model.kind, w.d, w.m, npts, w.laws, w.t, w.H, w.F, Xa, Wa, rho, Z=None,
-                seed=1234, it=it, salt=0, prec=prec, nthreads=nt, t_shared=True,
+                seed=ens_seed, it=key, salt=0, prec=prec, nthreads=nt, t_shared=True,
                 H_shared=w.H_shared, sequential=True)
-            E = rng.exponential(1.0, B)
+            E = orc.exp1_range(ens_seed, 0, B, key, 0)
             acc = E > -(llp - lla)
             sel = np.repeat(acc, npts)
             Xa = np.where(sel[:, None], Xo, Xa)
             Wa = np.where(sel[:, None], Wo, Wa)
             lla = np.where(acc, llp, lla)
             acc_n += int(acc.sum())
-            el = time.perf_counter() - t0
-            if (el > budget_s / 2 and it >= 2) or it >= 10000:
+            it += 1
+            if record:
+                decisions.append(acc)
+            if time.perf_counter() - t0 > budget and it >= 2:
                 break
-        res[nt] = (w.steps_per_iter * it / el, it, acc_n / (B * it))
-    v, its, ar = res[nthreads]
-    v1 = res[1][0]
+        el = time.perf_counter() - t0
+        return w.steps_per_iter * it / el, it, acc_n / (B * it), decisions
+
+    v1, its1, _, _ = run(1, 3, 0.0, False)  # single-thread rate on a short sample
+    v, its, ar, dec = run(nthreads, CPU_MAX_ITERS, budget_s, True)
+    # the device runs the same iterations from the same state (untimed) and records decisions
+    ens.mcmc_run(lay, 0, B, iter0, its)
+    hist = ens.get_block_state(lay, L.BLK_ACC_HIST, 0, B, hist_len=w.meta["hist_len"])
+    dev = hist[iter0 - 1: iter0 - 1 + its].astype(bool)
+    cpu = np.array(dec)
+    same = dev == cpu
+    first = int(np.argmin(same.all(axis=1))) if not same.all() else None
     return {"value": v, "unit": "steps/s", "cores": nthreads, "kind": "port",
-            "sample": f"{its} full MCMC iterations (draw + MH accept) of the same per-GPU workload "
-                      f"({B} blocks x {npts - 1} steps), step-by-step Euler loop, same "
-                      f"Philox/Box-Muller normals, OpenMP over blocks",
-            "value_1thread": v1, "accept_rate": ar}
+            "sample": f"{its} full MCMC iterations (draw + MH accept) of the same per-GPU "
+                      f"workload ({B} blocks x {npts - 1} steps) from the device's state after "
+                      f"iteration {iter0 - 1}, the device's Philox normal and Exp(1) streams "
+                      f"(keys {iter0}..{iter0 + its - 1}), sequential Euler loop, OpenMP over "
+                      f"blocks",
+            "value_1thread": v1, "iterations_1thread": its1, "accept_rate": ar,
+            "decisions_identical": int(same.sum()), "decisions_total": int(same.size),
+            "first_differing_iteration": None if first is None else iter0 + first,
+            "accept_rate_device_same_iterations": float(dev.mean()),
+            "host": info}
 
 
-def main():
+ens_seed = 0xD1FF
+
+
+def free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch(args, argv):
+    """--gpus N with WORLD_SIZE unset: start N rank processes (one per GPU) with the
+    torch.distributed environment set, before this process touches any GPU; rank 0 prints the
+    result line.  Returns the worst exit code."""
+    port = free_port()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv,
+                                      env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=500)
@@ -137,26 +231,40 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--mapping", default="auto", choices=["auto", "lane", "wave"],
                     help="thread mapping of the Euler recursion (DESIGN.md §2)")
-    args = ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true",
+                    help="rendezvous the ranks and exit before any GPU work (launcher test)")
+    args = ap.parse_args(argv)
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch(args, argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     dist = None
     if world > 1:
-        import torch
         import torch.distributed as dist
         dist.init_process_group("gloo")  # control plane only; the data path is RCCL in libdmt
+        assert dist.get_world_size() == world
+    if args.dry_run:
+        if dist is not None:
+            dist.barrier()
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": world, "ranks": world}))
+        if dist is not None:
+            dist.destroy_process_group()
+        return 0
 
     import diffusionmcmctools_amd as dmt
     from diffusionmcmctools_amd import _lib as L
     from diffusionmcmctools_amd import workloads as W
 
     w = build_workload(args.config, rank)
-    w.meta["hist_len"] = args.warmup + args.steps + EXTRA_ITERS
+    w.meta["hist_len"] = args.warmup + args.steps + EXTRA_ITERS + CPU_MAX_ITERS
     mapping = {"auto": L.MAP_AUTO, "lane": L.MAP_LANE, "wave": L.MAP_WAVE}[args.mapping]
     ens = dmt.Ensemble(w.model.kind, w.d, w.m, w.n_points, precision=w.precision,
-                       seed=0xD1FF, device=local_rank, grid_shared=w.grid_shared,
+                       seed=ens_seed, device=local_rank, grid_shared=w.grid_shared,
                        mapping=mapping)
     # rank r holds recording shard r of the global ensemble: RNG streams keyed by global
     # segment ids (shard.py), so the N-GPU job equals one ensemble of N x B blocks
@@ -167,6 +275,9 @@ def main():
         uid = [dmt.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         ens.comm_init(world, rank, uid[0])
+    rccl_nranks = ens.comm_size()
+    if world > 1 and rccl_nranks != world:
+        raise SystemExit(f"bench.py: RCCL communicator has {rccl_nranks} ranks, expected {world}")
     ens.loglikhd(lay, L.U, 0, B)
 
     # one step = draw_proposal_path!(be); accept_reject_proposal_path!(be, i); fetch_ll(be).
@@ -197,6 +308,8 @@ def main():
         ens.set_timing(True, kernels=[L.K_ACCEPT])
         ens.mcmc_run(lay, 0, B, args.warmup + args.steps + 1, EXTRA_ITERS)
         a_ms, a_n = ens.get_timing(L.K_ACCEPT)
+    else:
+        ens.mcmc_run(lay, 0, B, args.warmup + args.steps + 1, EXTRA_ITERS)
     ens.set_timing(False)
     if dist is not None:
         import torch
@@ -235,11 +348,14 @@ def main():
     traffic, traffic_src = measured_traffic(args.config, kname)  # HBM bytes per iteration
     if traffic is not None:
         traffic *= it_per_launch
+    issue = issue_roofline(args.config, kname)
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(w, ens, lay, budget_s=args.cpu_budget)
+            cpu = cpu_baseline(w, ens, lay, args.warmup + args.steps + EXTRA_ITERS + 1,
+                               budget_s=args.cpu_budget)
         desc, dtype = WORKLOADS[args.config]
+        frac = achieved / PEAK_HBM_GBS
         line = {
             "metric": "bridge-segment Euler steps/sec/GPU; accept-rate vs CPU ref",
             "value": value,
@@ -256,6 +372,7 @@ def main():
             "config": {"workload": desc, "blocks_per_gpu": B,
                        "euler_steps_per_block": w.steps_per_iter // B, "rho": w.rho,
                        "parallelism": f"blockensemble-shard x{world}",
+                       "rccl_nranks": rccl_nranks,
                        "mapping": ("scan-resident" if resident else
                                    "scan-persistent" if persist else
                                    "scan-resident-per-iteration" if kname == "k_block_resident" else
@@ -265,28 +382,35 @@ def main():
             "per_gpu": value / world,
             "accept_rate": accept_rate,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS,
-                         "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
+                         "unit": "GB/s", "frac": frac, "traffic": traffic,
                          "traffic_source": traffic_src,
                          "kernel": kname + (" (draw_proposal_path! + accept_reject_proposal_path! "
-                                            "of every iteration of the launch)" if persist else
+                                            "+ fetch_ll of every iteration of the launch)" if persist else
                                             " (draw_proposal_path!)"),
                          "kernel_avg_us": k_avg_s * 1e6,
                          "kernel_us_per_iteration": k_iter_s * 1e6,
                          "iterations_per_launch": it_per_launch,
                          "algorithmic_bytes_per_launch": bytes_launch,
                          "algorithmic_bytes_per_iteration": bytes_iter,
-                         "bytes_per_step": algorithmic_bytes_per_step(w)},
+                         "bytes_per_step": algorithmic_bytes_per_step(w),
+                         "hbm_frac_from_traffic": (traffic / k_avg_s / 1e9 / PEAK_HBM_GBS
+                                                   if traffic and k_avg_s > 0 else None),
+                         "limiter": (issue or {}).get("limiter"),
+                         "issue": issue},
             "accept_kernel_avg_us": (a_ms / a_n) * 1e3 if a_n else None,
             "cpu_baseline": cpu,
         }
         if cpu is not None:
             line["accept_rate_cpu"] = cpu["accept_rate"]
-        print(json.dumps(line))
+            line["decisions_identical"] = cpu["decisions_identical"]
+            line["decisions_total"] = cpu["decisions_total"]
+        print(json.dumps(line), flush=True)
     ens.close()
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

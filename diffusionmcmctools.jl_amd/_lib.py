@@ -25,6 +25,9 @@ LAW_PP, LAW_PPB = 0, 1
 SWAP_XX, SWAP_WW, SWAP_PP, SWAP_LL = 1, 2, 4, 8
 BLK_LL, BLK_LLPROP, BLK_LL_HIST, BLK_LLPROP_HIST, BLK_ACC_HIST = 0, 1, 2, 3, 4
 K_DRAW, K_ACCEPT, K_PATHLL, K_RECOMPUTE, K_REDUCE = 0, 1, 2, 3, 4
+# device random streams (include/dmt.h): salt = RNG_AUTO draws from the handle's counter
+RNG_AUTO = 0xFFFFFFFF
+SALT_LIMIT = 0x40000000
 LAW_STRIDE = 64
 LAW_THETA, LAW_SIGMA, LAW_A, LAW_BT, LAW_BETA, LAW_DA, LAW_C0, LAW_TRACE = 0, 16, 25, 31, 40, 43, 49, 50
 LAW_SIGINV = 51
@@ -45,6 +48,7 @@ SYMBOLS = [
     "dmt_set_timing", "dmt_get_timing", "dmt_memory_bytes", "dmt_debug_philox",
     "dmt_debug_normals", "dmt_last_error", "dmt_version", "dmt_snapshot_reserve",
     "dmt_snapshot_take", "dmt_snapshot_download", "dmt_snapshot_write", "dmt_set_ll",
+    "dmt_fetch_ll_local", "dmt_comm_size", "dmt_rng_counter", "dmt_set_rng_counter",
 ]
 
 
@@ -126,6 +130,10 @@ _SIGS = {
     "dmt_snapshot_download": [_P, _i32, _i64, _pd, _pi64],
     "dmt_snapshot_write": [_P, C.c_char_p, _i64, _i64],
     "dmt_set_ll": [_P, _i32, _i32, _i64, _i64, _i64, _pd],
+    "dmt_fetch_ll_local": [_P, _i32, _i64, _i64, _i64, _pd, _pd, _pi64],
+    "dmt_comm_size": [_P, _pi32],
+    "dmt_rng_counter": [_P, C.POINTER(_u64)],
+    "dmt_set_rng_counter": [_P, _u64],
 }
 for _name, _args in _SIGS.items():
     _f = getattr(lib, _name)

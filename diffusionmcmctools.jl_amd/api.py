@@ -15,8 +15,12 @@ results: every method is one C-ABI call over the block range the object covers.
 Ranges are 0-based half-open Python ``range``s over a recording's inter-observation segments
 (the reference's ``ranges[i]`` are 1-based ``UnitRange``s of the same segments).  Path
 containers live on the GPU; ``XX``/``WW`` download them in the reference layout.
-Draws: by default the device Philox stream (keyed by ``mcmciter`` / an explicit ``iter``);
-pass ``Z``/``E`` to supply the normals / Exp(1) variables yourself (parity mode).
+Draws: by default each call takes fresh variables from the handle's device stream counter
+(``DMT_RNG_AUTO``), as the reference's calls take them from the global RNG
+(src/biblock.jl:94-99,122): a loop of ``draw_proposal_path()`` / ``accept_reject_proposal_path(i)``
+never reuses normals or Exp(1) variables, and blockings drawn in one iteration are independent.
+An explicit ``iter``/``salt`` selects a reproducible keyed stream instead; ``Z``/``E`` supply the
+normals / Exp(1) variables (parity mode).
 """
 from __future__ import annotations
 
@@ -24,6 +28,13 @@ import numpy as np
 
 from . import _lib as L
 from .engine import Ensemble
+
+def _key(iter, salt):
+    """(iter, salt) of a draw: no key given → the handle's stream counter (RNG_AUTO)."""
+    if iter is None and salt is None:
+        return 0, L.RNG_AUTO
+    return (0 if iter is None else int(iter)), (0 if salt is None else int(salt))
+
 
 __all__ = ["SamplingEnsemble", "SamplingPair", "SamplingUnit", "BlockEnsemble",
            "BlockCollection", "BiBlock"]
@@ -70,7 +81,7 @@ class SamplingEnsemble:
         ``set_obs`` / ``recompute_guiding_term`` on the device."""
         self.ens.upload_obs(Hobs, Fobs, cobs, artificial_noise)
 
-    def init_paths(self, x0, Z=None, iter=0, salt=0xFFFF, x0_prior=None, max_tries=1000):
+    def init_paths(self, x0, Z=None, iter=None, salt=None, x0_prior=None, max_tries=1000):
         """``init_paths!`` (src/sampling_unit.jl:83-87) for every recording, then
         u° ← u (src/sampling_pair.jl:51).  ``x0``: per-recording start points (R × d).
 
@@ -78,14 +89,17 @@ class SamplingEnsemble:
         until it succeeds, a recording whose draw fails is drawn again — with the next device
         normal stream (``iter + k``) and, when ``x0_prior`` (``k -> start point``) is given, a new
         start point — up to ``max_tries`` draws (the reference loops without a bound).
-        Parity-mode normals ``Z`` are fixed inputs: no retry.  Returns (ll, success)."""
+        Parity-mode normals ``Z`` are fixed inputs: no retry.  Without ``iter``/``salt`` every
+        draw takes the next variables of the device stream counter.  Returns (ll, success)."""
         d = self.model.d
         x0 = np.asarray(x0, dtype=np.float64).reshape(-1, d)
         starts = self.ens.pt_off[self.ens.rec_seg0[:-1]]
         X = np.zeros((self.ens.P, d))
         X[starts] = x0
         self.ens.set_paths(L.U, X=X)
-        ll, ok = self.ens.draw_unit(L.U, Z=Z, iter=iter, salt=salt)
+        auto = iter is None and salt is None
+        it0, salt = _key(iter, 0xFFFF if salt is None and not auto else salt)
+        ll, ok = self.ens.draw_unit(L.U, Z=Z, iter=it0, salt=salt)
         ll, ok = np.array(ll), np.array(ok)
         tries = 1
         while Z is None and not ok.all():
@@ -98,7 +112,8 @@ class SamplingEnsemble:
                     X[starts[r]] = np.asarray(x0_prior(tries), dtype=np.float64).reshape(d)
                 self.ens.set_paths(L.U, X=X)
             for r in np.nonzero(~ok)[0]:
-                llr, okr = self.ens.draw_unit(L.U, int(r), int(r) + 1, iter=iter + tries, salt=salt)
+                llr, okr = self.ens.draw_unit(L.U, int(r), int(r) + 1,
+                                              iter=0 if auto else it0 + tries, salt=salt)
                 ll[r], ok[r] = llr[0], okr[0]
             tries += 1
         self.ens.set_paths(L.UPROP, X=self.ens.download_paths(L.U, 0),
@@ -177,10 +192,11 @@ class SamplingUnit:
         """Wiener trajectories (cumulative, as the reference holds them), per segment."""
         return self._split(self.se.ens.download_paths(self.unit, 1))
 
-    def draw_proposal_path(self, Z=None, iter=0, salt=0):
+    def draw_proposal_path(self, Z=None, iter=None, salt=None):
         """``draw_proposal_path!(u::SamplingUnit)`` (src/sampling_unit.jl:118-120): fresh
         Wiener draw and guided solve of the whole recording.  Returns (success, ll)."""
-        ll, ok = self.se.ens.draw_unit(self.unit, self.r, self.r + 1, Z=Z, iter=iter, salt=salt)
+        it, salt = _key(iter, salt)
+        ll, ok = self.se.ens.draw_unit(self.unit, self.r, self.r + 1, Z=Z, iter=it, salt=salt)
         return bool(ok[0]), float(ll[0])
 
 
@@ -205,19 +221,21 @@ class _BlockRange:
         return getattr(self._ens, name)(self._layout, what, self._b0, self._b1, **k)
 
     # ---- imputation (biblock.jl:78-106, block_collection.jl:46, block_ensemble.jl:50)
-    def draw_proposal_path(self, Z=None, iter=None, salt=0):
+    def draw_proposal_path(self, Z=None, iter=None, salt=None):
         """pCN proposal under the accepted law into u°, ll° along the way.  Returns the
-        per-block success flags.  ``iter`` keys the device normals (default 0); ``Z`` (steps
-        × m, whole ensemble) supplies them."""
-        return self._call("draw_proposal", Z=Z, iter=0 if iter is None else iter, salt=salt,
-                          want_success=True)
+        per-block success flags.  Normals: the next ones of the device stream counter, or the
+        stream keyed by an explicit ``iter``/``salt``, or ``Z`` (steps × m, whole ensemble)."""
+        it, salt = _key(iter, salt)
+        return self._call("draw_proposal", Z=Z, iter=it, salt=salt, want_success=True)
 
     # ---- accept / reject (biblock.jl:121-127)
-    def accept_reject_proposal_path(self, mcmciter, E=None, salt=0):
-        """MH decision per block: E > −(ll° − ll), E ~ Exp(1) (device stream keyed by
-        ``mcmciter`` unless ``E`` is given); swap_paths!, set_accepted!, save_ll!, swap_ll!
-        in the reference order.  Returns the per-block decisions."""
-        return self._call("accept_reject", mcmciter, E=E, salt=salt, want_acc=True)
+    def accept_reject_proposal_path(self, mcmciter, E=None, salt=None):
+        """MH decision per block: E > −(ll° − ll), E ~ Exp(1) (the device stream counter —
+        the key of the draw this decision follows —, the stream keyed by (``mcmciter``,
+        ``salt``) when ``salt`` is given, or ``E``); swap_paths!, set_accepted!, save_ll!,
+        swap_ll! in the reference order.  Returns the per-block decisions."""
+        return self._call("accept_reject", mcmciter, E=E,
+                          salt=L.RNG_AUTO if salt is None else int(salt), want_acc=True)
 
     def set_accepted(self, i, v):
         self._call("set_accepted", i, v)
@@ -256,10 +274,19 @@ class _BlockRange:
         non-terminal block as the artificial observation of its P_last law."""
         self._call("set_obs")
 
-    def recompute_guiding_term(self, unit=L.U):
-        """``GP.recompute_guiding_term!(bb.b)`` (``unit=U``) or of ``bb.b°`` (``UPROP``)
-        (src/block.jl:102-110): device backward filter of the blocks' laws."""
-        self._call("recompute_guiding_term", unit=unit)
+    def recompute_guiding_term(self, only=None):
+        """``GP.recompute_guiding_term!`` (device backward filter of the blocks' laws,
+        src/block.jl:102-110): with no flag the guiding terms of both the accepted and the
+        proposal laws, b then b° (src/biblock.jl:288-291, src/block_collection.jl:208-210,
+        src/block_ensemble.jl:199-200); ``only="P_only"`` the accepted laws only
+        (``Val(:P_only)``, i.e. ``recompute_guiding_term!(bb.b)``), ``only="P°_only"`` the
+        proposal laws only (``Val(:P°_only)``, ``recompute_guiding_term!(bb.b°)``;
+        src/block_collection.jl:212-221)."""
+        units = _RGT_ONLY.get(only)
+        if units is None:
+            raise ValueError(f"only must be one of {sorted(k for k in _RGT_ONLY if k)} or None")
+        for unit in units:
+            self._call("recompute_guiding_term", unit=unit)
 
     def find_W_for_X(self):
         """``find_W_for_X!`` (src/block.jl:118-131): u.WW ← the Wiener increments that reproduce
@@ -291,12 +318,16 @@ class _BlockRange:
             self.swap_ll()
         return accepted, (np.array(theta_prop, copy=True) if accepted else np.array(theta, copy=True))
 
+    # BiBlock / BlockCollection sums are this rank's (src/block_collection.jl:144,156);
+    # BlockEnsemble overrides _global: with a communicator its fetch_ll is over every rank
+    _global = False
+
     def fetch_ll(self):
         """Σ ll over the blocks (deterministic pairwise tree)."""
-        return self._call("fetch_ll")[0]
+        return self._call("fetch_ll", local=not self._global)[0]
 
     def fetch_ll_prop(self):
-        return self._call("fetch_ll")[1]
+        return self._call("fetch_ll", local=not self._global)[1]
 
     # ---- state
     @property
@@ -353,17 +384,26 @@ class _BlockRange:
             self._ens.upload_law(L.UPROP, L.LAW_PPB, H=Hb, F=Fb, laws=lawsb, H_shared=H_shared)
         return self.recompute_path(skip=skip)
 
-    def mcmc_step(self, mcmciter, salt=0):
+    def mcmc_step(self, mcmciter, salt=None):
         """``draw_proposal_path!`` + ``accept_reject_proposal_path!(·, mcmciter)`` +
-        ``fetch_ll`` fused into one call (device RNG).  Returns (ll, ll°, n_accepted)."""
-        return self._call("mcmc_step", mcmciter, salt=salt)
+        ``fetch_ll`` fused into one call (device RNG: the stream counter, or the stream keyed
+        by (``mcmciter``, ``salt``)).  Returns (ll, ll°, n_accepted)."""
+        return self._call("mcmc_step", mcmciter, salt=L.RNG_AUTO if salt is None else int(salt))
 
-    def mcmc_run(self, iter0, n_iter, salt=0):
+    def mcmc_run(self, iter0, n_iter, salt=None):
         """``n_iter`` consecutive :meth:`mcmc_step` iterations starting at ``iter0``, queued on
         the device without host round trips; returns an (n_iter, 3) array of (fetch_ll,
         fetch_ll°, accepted count) — the sampling loop of
-        docs/src/tutorials/biblock/smoothing.md:40-44."""
-        return self._call("mcmc_run", iter0, n_iter, salt=salt)
+        docs/src/tutorials/biblock/smoothing.md:40-44.  Without ``salt`` it draws exactly what
+        the loop of counter-keyed :meth:`draw_proposal_path` / :meth:`accept_reject_proposal_path`
+        calls would."""
+        return self._call("mcmc_run", iter0, n_iter,
+                          salt=L.RNG_AUTO if salt is None else int(salt))
+
+
+# recompute_guiding_term! flags (src/block_collection.jl:208-221) → units, in call order
+_RGT_ONLY = {None: (L.U, L.UPROP), "P_only": (L.U,), "P°_only": (L.UPROP,),
+             "Pprop_only": (L.UPROP,)}
 
 
 def _param_indices(ens, theta):
@@ -379,10 +419,54 @@ def _param_indices(ens, theta):
     return out
 
 
-class BiBlock(_BlockRange):
-    """``BiBlock{L}`` (src/biblock.jl:42-63): one block b / b° with pCN memory ρ."""
+def _pair_layout(sp, ranges, rhos, ll_hist_len):
+    """A layout holding only recording ``sp.r``'s blocks ``ranges`` (the last one terminal):
+    the storage of the reference's stand-alone ``BiBlock(sp, …)`` / ``BlockCollection(sp, …)``,
+    whose blocks are views into that pair's containers (src/block.jl:66-72)."""
+    se = sp.se
+    nseg = len(se.n_points[sp.r])
+    rr = [_as_range(x) for x in ranges]
+    for x in rr:
+        if not (0 <= x.start < x.stop <= nseg):
+            raise ValueError(f"block range {x} outside recording {sp.r}'s {nseg} segments")
+    n_blocks = [0] * se.num_recordings()
+    n_blocks[sp.r] = len(rr)
+    last = [1 if i == len(rr) - 1 else 0 for i in range(len(rr))]
+    layout = se.ens.create_layout(n_blocks, [x.start for x in rr], [x.stop - 1 for x in rr],
+                                  last, [float(v) for v in rhos], hist_len=int(ll_hist_len))
+    return layout, rr, last
 
-    def __init__(self, ens, layout, b, hist_len, is_last, rho, segments):
+
+def _as_range(x):
+    return range(x.start, x.stop) if isinstance(x, range) else range(x[0], x[1] + 1)
+
+
+class BiBlock(_BlockRange):
+    """``BiBlock{L}`` (src/biblock.jl:42-63): one block b / b° with pCN memory ρ.
+
+    Reference constructor: ``BiBlock(sp, range, rho=0.0, last_block=False, ll_hist_len=0)``
+    (src/biblock.jl:48-62) — a block over segments ``range`` (0-based, half-open) of the
+    recording of SamplingPair ``sp``.  The BlockEnsemble / BlockCollection constructors make
+    their blocks with the internal form ``BiBlock(engine, layout, b, …)``."""
+
+    def __init__(self, *args, **kw):
+        if args and isinstance(args[0], SamplingPair):
+            self._init_ref(*args, **kw)
+        else:
+            self._init_view(*args, **kw)
+
+    def _init_ref(self, sp, range_, rho=0.0, last_block=False, ll_hist_len=0):
+        if not last_block and len(_as_range(range_)) < 2:
+            raise ValueError("a non-terminal BiBlock needs >= 2 segments (src/block.jl:66,178)")
+        se = sp.se
+        n_blocks = [0] * se.num_recordings()
+        n_blocks[sp.r] = 1
+        x = _as_range(range_)
+        layout = se.ens.create_layout(n_blocks, [x.start], [x.stop - 1], [1 if last_block else 0],
+                                      [float(rho)], hist_len=int(ll_hist_len))
+        self._init_view(se.ens, layout, 0, int(ll_hist_len), last_block, rho, x)
+
+    def _init_view(self, ens, layout, b, hist_len, is_last, rho, segments):
         super().__init__(ens, layout, b, b + 1, hist_len)
         self.is_last, self.rho, self.segments = bool(is_last), float(rho), segments
 
@@ -401,9 +485,29 @@ class BiBlock(_BlockRange):
 
 class BlockCollection(_BlockRange):
     """``BlockCollection`` (src/block_collection.jl:19-38): the blocks of one recording; the
-    last one is terminal (``BiBlock{true}``)."""
+    last one is terminal (``BiBlock{true}``).
 
-    def __init__(self, ens, layout, b0, blocks, hist_len):
+    Reference constructor: ``BlockCollection(sp, ranges, rho=0.0, ll_hist_len=0)``
+    (src/block_collection.jl:22-30): blocks over ``ranges`` (0-based, half-open) of SamplingPair
+    ``sp``'s recording, ``rho`` a scalar or one per block.  ``BlockEnsemble`` makes its
+    collections with the internal form ``BlockCollection(engine, layout, b0, blocks, …)``."""
+
+    def __init__(self, *args, **kw):
+        if args and isinstance(args[0], SamplingPair):
+            self._init_ref(*args, **kw)
+        else:
+            self._init_view(*args, **kw)
+
+    def _init_ref(self, sp, ranges, rho=0.0, ll_hist_len=0):
+        n = len(ranges)
+        rhos = list(rho) if isinstance(rho, (list, tuple, np.ndarray)) else [rho] * n
+        layout, rr, last = _pair_layout(sp, ranges, rhos, ll_hist_len)
+        ens = sp.se.ens
+        blocks = [BiBlock(ens, layout, b, int(ll_hist_len), last[b], rhos[b], rr[b])
+                  for b in range(n)]
+        self._init_view(ens, layout, 0, blocks, int(ll_hist_len))
+
+    def _init_view(self, ens, layout, b0, blocks, hist_len):
         super().__init__(ens, layout, b0, b0 + len(blocks), hist_len)
         self.blocks = blocks
 
@@ -416,6 +520,10 @@ class BlockEnsemble(_BlockRange):
 
     def __init__(self, se: SamplingEnsemble, ranges, rho=0.0, ll_hist_len=0):
         R = se.num_recordings()
+        # ll_hist_len: a scalar or one per recording (_vec_me, src/block_ensemble.jl:27-28);
+        # the device layout keeps one history length, the longest
+        if isinstance(ll_hist_len, (list, tuple, np.ndarray)):
+            ll_hist_len = int(max(ll_hist_len)) if len(ll_hist_len) else 0
         if len(ranges) != R:
             raise ValueError(f"ranges needs one entry per recording ({R})")
         rho_r = rho if isinstance(rho, (list, tuple, np.ndarray)) else [rho] * R
@@ -443,6 +551,7 @@ class BlockEnsemble(_BlockRange):
         layout = ens.create_layout(n_blocks, sf, sl, last, rhos, hist_len=ll_hist_len)
         nb = len(sf)
         super().__init__(ens, layout, 0, nb, ll_hist_len)
+        self._global = True
         self.se = se
         self.recordings = []
         b = 0

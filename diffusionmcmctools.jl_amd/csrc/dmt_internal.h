@@ -103,10 +103,12 @@ struct AcceptArgs {
   double* llp_hist;
   uint8_t* acc_hist;
   int64_t hist_len;
-  int64_t mcmciter;  // 1-based
+  int64_t mcmciter;  // 1-based (history index)
   const double* E;   // [b1-b0] or nullptr
   uint64_t seed;
   uint32_t salt;
+  uint32_t key_iter;  // iteration word of the Exp(1) stream key (= mcmciter unless DMT_RNG_AUTO)
+  int64_t key_delta;  // persistent runs: iteration it draws with key word it + key_delta
   uint32_t seg_base;
   uint8_t* acc_out;  // [b1-b0] or nullptr
 };
@@ -197,11 +199,11 @@ constexpr int64_t kFiltBatchPoints = int64_t(1) << 24;
 // k_filter_scan + k_filter_chain (every chunk in parallel, a short serial chain per block)
 constexpr int64_t kFiltFusedBlocks = 4096;
 constexpr int kResidentMaxSteps = 512;
+// part: [n_iter][3][nwaves] block partials followed by [n_iter][3][ceil(nwaves / WPB)] tree
+// nodes (WPB ≤ 4); out3[n_iter][3]: every iteration's fetch_ll; counter: a zeroed uint32
 hipError_t launch_mcmc_persistent(const ModelKey& k, const void* args, const AcceptArgs& c,
                                   int64_t iter0, int64_t n_iter, double* part, int64_t nwaves,
-                                  int resident, hipStream_t s);
-hipError_t launch_tree_batched(const double* part, int64_t nb, int64_t n_iter, double* out3,
-                               hipStream_t s);
+                                  int resident, double* out3, unsigned* counter, hipStream_t s);
 hipError_t launch_backward_filter(int precision, const FilterArgs& a, hipStream_t s);
 hipError_t launch_set_prop_law(const ParamArgs& a, hipStream_t s);
 hipError_t launch_set_obs(int precision, int tw, int d, const void* X0, const void* X1,

@@ -1320,22 +1320,123 @@ __global__ __launch_bounds__((64 * ScanCfg<Mdl::D, T>::WPB), 1) void k_block_sca
   }
 }
 
+// The fetch_ll trees of every iteration of a persistent run, formed inside the launch (no
+// separate tree launch): (1) each workgroup folds, for every (iteration, component) row of
+// part[n_iter][3][nb], its WPB consecutive leaves (the blocks of its waves) into the node of the
+// canonical tree one log2(WPB) levels up; (2) the last workgroup to finish (device-scope arrival
+// counter) folds every row's nodes — a wave per row, each lane an aligned run of nodes, then the
+// 64-lane adjacent-pair tree.  That is the complete adjacent-pair tree over the zero-padded
+// blocks of launch_block_sum (padding further with zeros changes nothing but
+// the sign of a zero, and the ll sums are canonicalised with + 0.0).
+// Hand-off without a release fence (an agent-scope release writes back the XCD L2's dirty
+// lines — here the run's paths, ≈35 µs per launch measured): the nodes are stored write-through
+// (relaxed agent-scope atomic stores, sc1), every storing wave drains its stores, one lane per
+// workgroup adds to the arrival counter (agent-scope atomic) after a workgroup barrier, and the
+// last arriver — told by the value its add returned — reads the nodes with sc1 loads
+// (MI355X_MICROARCH.md, inter-workgroup visibility: one workgroup per CU, hipMalloc memory).
+template <int WPB>
+__device__ __forceinline__ void persistent_tree_tail(const double* __restrict__ part,
+                                                     double* __restrict__ nodes, int64_t nb,
+                                                     int64_t n_iter, unsigned* __restrict__ counter,
+                                                     double* __restrict__ out3) {
+  __shared__ int s_last;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int64_t ng = (nb + WPB - 1) / WPB, x = blockIdx.x, rows = 3 * n_iter;
+  __syncthreads();  // every wave's part[] stores of the run are done
+  for (int64_t row = tid; row < rows; row += 64 * WPB) {
+    double v[WPB];
+#pragma unroll
+    for (int k = 0; k < WPB; ++k) {
+      const int64_t j = x * WPB + k;
+      v[k] = j < nb ? part[row * nb + j] : 0.0;
+    }
+#pragma unroll
+    for (int w = WPB; w > 1; w >>= 1)
+#pragma unroll
+      for (int k = 0; k < w / 2; ++k) v[k] = v[2 * k] + v[2 * k + 1];
+    __hip_atomic_store(&nodes[row * ng + x], v[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
+  __syncthreads();
+  if (tid == 0)
+    s_last = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                     gridDim.x - 1 ? 1 : 0;
+  __syncthreads();
+  if (!s_last) return;
+  int64_t P = 1;
+  while (P < ng) P <<= 1;
+  const int64_t run = P > 64 ? P / 64 : 1;
+  if (run <= 4) {
+    // ≤ 256 nodes per row: a batch of RB rows' loads in flight per lane, then the folds
+    constexpr int RB = 8;
+    for (int64_t r0 = (int64_t)wv * RB; r0 < rows; r0 += (int64_t)WPB * RB) {
+      double v[RB][4];
+#pragma unroll
+      for (int b = 0; b < RB; ++b)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int64_t row = r0 + b, nd = (int64_t)lane * run + k;
+          v[b][k] = (k < run && row < rows && nd < ng)
+                        ? __hip_atomic_load(&nodes[row * ng + nd], __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT)
+                        : 0.0;
+        }
+#pragma unroll
+      for (int b = 0; b < RB; ++b) {
+        // aligned run of `run` ≤ 4 nodes (the zero slots past it are not part of the fold)
+        double f = run == 1 ? v[b][0]
+                 : run == 2 ? v[b][0] + v[b][1]
+                            : (v[b][0] + v[b][1]) + (v[b][2] + v[b][3]);
+        f = wave_tree_sum<double>(f);
+        const int64_t row = r0 + b;
+        if (lane == 0 && row < rows) out3[row] = (row % 3 == 2) ? f : f + 0.0;
+      }
+    }
+  } else {
+    constexpr int kLv = 24;
+    for (int64_t row = wv; row < rows; row += WPB) {
+      double stk[kLv];
+#pragma unroll
+      for (int l = 0; l < kLv; ++l) stk[l] = 0.0;
+      double acc = 0.0;
+      for (int64_t k = 0; k < run; ++k) {
+        const int64_t nd = (int64_t)lane * run + k;
+        double xv = nd < ng ? __hip_atomic_load(&nodes[row * ng + nd], __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT)
+                            : 0.0;
+        bool carry = true;
+#pragma unroll
+        for (int l = 0; l < kLv; ++l) {
+          const bool bit = (k >> l) & 1;
+          const double y = stk[l] + xv;
+          const bool add = carry && bit;
+          stk[l] = (carry && !bit) ? xv : stk[l];
+          carry = add;
+          xv = add ? y : xv;
+        }
+        acc = xv;
+      }
+      acc = wave_tree_sum<double>(acc);
+      if (lane == 0) out3[row] = (row % 3 == 2) ? acc : acc + 0.0;
+    }
+  }
+  __syncthreads();
+  if (tid == 0)  // ready for the next launch (stream-ordered)
+    __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // dmt_mcmc_run for linear drifts: n_iter path-MCMC iterations in ONE launch.  Blocks are
 // independent across iterations (a block's next proposal depends only on its own accepted
 // state), so each wave loops over the iterations of its block: draw (scan_block, device RNG),
 // then — uniformly, exactly as k_accept — the MH decision, selector flips (bit masks in
 // SGPRs), histories and the ll swap.  Per-iteration (ll, ll°, accepted) go to
-// part[n_iter][3][nb] for the batched fetch_ll tree (k_tree_batched).
+// part[n_iter][3][nb]; persistent_tree_tail forms every iteration's fetch_ll from them.
 template <class Mdl, class T>
-__global__ __launch_bounds__((64 * ScanCfg<Mdl::D, T>::WPB), 1) void k_mcmc_scan(
-    const BlockArgs<T> a, const AcceptArgs c, const int64_t iter0, const int64_t n_iter,
-    double* __restrict__ part) {
-  using Cfg = ScanCfg<Mdl::D, T>;
-  __shared__ ScanLds<Mdl::D, T> lds[Cfg::WPB];
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+__device__ __forceinline__ void mcmc_scan_block(const BlockArgs<T>& a, const AcceptArgs& c,
+                                                const int64_t iter0, const int64_t n_iter,
+                                                double* __restrict__ part, const int64_t blk,
+                                                ScanLds<Mdl::D, T>& L) {
   const int lane = threadIdx.x & 63;
-  const int64_t blk = a.b0 + (int64_t)blockIdx.x * Cfg::WPB + w;
-  if (blk >= a.b1) return;
   const int g0 = ldc(&a.binfo[blk].g0), g1 = ldc(&a.binfo[blk].g1);
   const int nseg = g1 - g0 + 1;  // ≤ kPersistMaxSegments = 64 (host-checked)
   const bool own = lane < nseg;
@@ -1346,10 +1447,10 @@ __global__ __launch_bounds__((64 * ScanCfg<Mdl::D, T>::WPB), 1) void k_mcmc_scan
   const int64_t nb = a.b1 - a.b0, j = blk - a.b0;
   for (int64_t r = 0; r < n_iter; ++r) {
     const int64_t it = iter0 + r;
-    const double E = exp1_draw(c.seed, (uint32_t)g0 + c.seg_base, (uint32_t)it, c.salt);
+    const double E = exp1_draw(c.seed, (uint32_t)g0 + c.seg_base, (uint32_t)(it + c.key_delta), c.salt);
     T lp;
     bool ok;
-    scan_block<Mdl, T, MODE_PCN>(a, blk, (uint32_t)it, sel, lds[w], lp, ok);
+    scan_block<Mdl, T, MODE_PCN>(a, blk, (uint32_t)(it + c.key_delta), sel, L, lp, ok);
     llp = ok ? (double)lp : -INFINITY;
     const bool acc = E > -(llp - ll);
     if (acc) {
@@ -1386,6 +1487,20 @@ __global__ __launch_bounds__((64 * ScanCfg<Mdl::D, T>::WPB), 1) void k_mcmc_scan
     c.llp[blk] = llp;
   }
 }
+
+template <class Mdl, class T>
+__global__ __launch_bounds__((64 * ScanCfg<Mdl::D, T>::WPB), 1) void k_mcmc_scan(
+    const BlockArgs<T> a, const AcceptArgs c, const int64_t iter0, const int64_t n_iter,
+    double* __restrict__ part, double* __restrict__ nodes, unsigned* __restrict__ counter,
+    double* __restrict__ out3) {
+  using Cfg = ScanCfg<Mdl::D, T>;
+  __shared__ ScanLds<Mdl::D, T> lds[Cfg::WPB];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t blk = a.b0 + (int64_t)blockIdx.x * Cfg::WPB + w;
+  if (blk < a.b1) mcmc_scan_block<Mdl, T>(a, c, iter0, n_iter, part, blk, lds[w]);
+  persistent_tree_tail<Cfg::WPB>(part, nodes, a.b1 - a.b0, n_iter, counter, out3);
+}
+
 
 
 // dmt_mcmc_run for linear drifts whose blocks are ONE segment of at most kSChunk steps (e.g.
@@ -1509,7 +1624,7 @@ __device__ __forceinline__ void resident_block(const BlockArgs<T>& a, const Acce
   for (int64_t r0 = 0; r0 < n_iter; ++r0) {
     const int64_t it = iter0 + r0;
     if (MCMC && (r0 & 63) == 0)  // Exp(1) draws of the next 64 iterations, one per lane
-      Ev = exp1_draw(c.seed, (uint32_t)g + c.seg_base, (uint32_t)(it + lane), c.salt);
+      Ev = exp1_draw(c.seed, (uint32_t)g + c.seg_base, (uint32_t)(it + c.key_delta + lane), c.salt);
     const double E = __builtin_bit_cast(
         double, ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(
                      (int)(__builtin_bit_cast(uint64_t, Ev) >> 32), (int)(r0 & 63)) << 32) |
@@ -1528,7 +1643,7 @@ __device__ __forceinline__ void resident_block(const BlockArgs<T>& a, const Acce
           for (int kk = 0; kk < M; ++kk)
             zc[r][kk] = (T)Zg[(int64_t)min(kRun * lane + r, nst - 1) * M + kk];
       } else {
-        draw_z((uint32_t)it, zc);
+        draw_z((uint32_t)(it + c.key_delta), zc);
       }
     }
 #pragma unroll
@@ -1696,12 +1811,15 @@ __global__ __launch_bounds__(256, 1) void k_mcmc_resident(const BlockArgs<T> a,
                                                           const AcceptArgs c,
                                                           const int64_t iter0,
                                                           const int64_t n_iter,
-                                                          double* __restrict__ part) {
+                                                          double* __restrict__ part,
+                                                          double* __restrict__ nodes,
+                                                          unsigned* __restrict__ counter,
+                                                          double* __restrict__ out3) {
   __shared__ ResLds<Mdl::D, Mdl::M, T> lds[4];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t blk = a.b0 + (int64_t)blockIdx.x * 4 + w;
-  if (blk >= a.b1) return;
-  resident_block<Mdl, T, MODE_PCN, true>(a, c, iter0, n_iter, part, blk, lds[w]);
+  if (blk < a.b1) resident_block<Mdl, T, MODE_PCN, true>(a, c, iter0, n_iter, part, blk, lds[w]);
+  persistent_tree_tail<4>(part, nodes, a.b1 - a.b0, n_iter, counter, out3);
 }
 
 // One draw / re-solve (dmt_draw_proposal, dmt_draw_unit, dmt_recompute_path) of single-segment
@@ -1714,54 +1832,6 @@ __global__ __launch_bounds__(256, 1) void k_block_resident(const BlockArgs<T> a)
   const int64_t blk = a.b0 + (int64_t)blockIdx.x * 4 + w;
   if (blk >= a.b1) return;
   resident_block<Mdl, T, MODE, false>(a, AcceptArgs{}, (int64_t)a.iter, 1, nullptr, blk, lds[w]);
-}
-
-// The fetch_ll tree of every iteration of a k_mcmc_scan run: workgroup r reduces row r of
-// part[n_iter][3][nb] with the canonical tree (complete adjacent-pair tree over the blocks,
-// zero-padded; each thread folds an aligned power-of-two run of leaves with the same pairing,
-// then 4 wave trees and a 4-leaf tree), + 0.0 on the two ll sums.
-__global__ __launch_bounds__(256) void k_tree_batched(const double* __restrict__ part, int64_t nb,
-                                                      int64_t run, double* __restrict__ out3) {
-  __shared__ double w0[4], w1[4], w2[4];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int64_t r = blockIdx.x;
-  double v[3];
-  // binary-counter fold of the thread's aligned run of leaves (register stack: selects on the
-  // counter bits, no dynamic indexing, which would go through scratch memory)
-  constexpr int kLv = 24;  // run ≤ 2^24 leaves per thread
-  for (int q = 0; q < 3; ++q) {
-    const double* row = part + (3 * r + q) * nb;
-    double stk[kLv];
-#pragma unroll
-    for (int l = 0; l < kLv; ++l) stk[l] = 0.0;
-    double acc = 0.0;
-    for (int64_t k = 0; k < run; ++k) {
-      const int64_t leaf = (int64_t)tid * run + k;
-      double x = leaf < nb ? row[leaf] : 0.0;
-      bool carry = true;
-#pragma unroll
-      for (int l = 0; l < kLv; ++l) {
-        const bool bit = (k >> l) & 1;
-        const double y = stk[l] + x;
-        const bool add = carry && bit;
-        stk[l] = (carry && !bit) ? x : stk[l];
-        carry = add;
-        x = add ? y : x;
-      }
-      acc = x;
-    }
-    v[q] = acc;
-  }
-  v[0] = wave_tree_sum<double>(v[0]);
-  v[1] = wave_tree_sum<double>(v[1]);
-  v[2] = wave_tree_sum<double>(v[2]);
-  if (lane == 0) { w0[wv] = v[0]; w1[wv] = v[1]; w2[wv] = v[2]; }
-  __syncthreads();
-  if (tid == 0) {
-    out3[3 * r + 0] = ((w0[0] + w0[1]) + (w0[2] + w0[3])) + 0.0;
-    out3[3 * r + 1] = ((w1[0] + w1[1]) + (w1[2] + w1[3])) + 0.0;
-    out3[3 * r + 2] = (w2[0] + w2[1]) + (w2[2] + w2[3]);
-  }
 }
 
 template <class Mdl, class T>
@@ -1824,7 +1894,7 @@ __global__ __launch_bounds__(256) void k_accept(const AcceptArgs a) {
   const int64_t blk = a.b0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (blk >= a.b1) return;
   const double E = a.E ? a.E[blk - a.b0]
-                       : exp1_draw(a.seed, (uint32_t)a.gfirst[blk] + a.seg_base, (uint32_t)a.mcmciter, a.salt);
+                       : exp1_draw(a.seed, (uint32_t)a.gfirst[blk] + a.seg_base, a.key_iter, a.salt);
   const double ll = a.ll[blk], llp = a.llp[blk];
   const bool acc = E > -(llp - ll);
   if (acc) {
@@ -1858,7 +1928,7 @@ __global__ __launch_bounds__(1024) void k_accept_reduce(const AcceptArgs a, doub
   double v0 = 0.0, v1 = 0.0, v2 = 0.0;
   if (blk < a.b1) {
     const double E = a.E ? a.E[blk - a.b0]
-                         : exp1_draw(a.seed, (uint32_t)a.gfirst[blk] + a.seg_base, (uint32_t)a.mcmciter, a.salt);
+                         : exp1_draw(a.seed, (uint32_t)a.gfirst[blk] + a.seg_base, a.key_iter, a.salt);
     double ll = a.ll[blk], llp = a.llp[blk];
     const bool acc = E > -(llp - ll);
     if (acc) {
@@ -1931,7 +2001,7 @@ __global__ __launch_bounds__(kAccGroup) void k_accept_reduce_lb(const AcceptArgs
   double v0 = 0.0, v1 = 0.0, v2 = 0.0;
   if (blk < a.b1) {
     const double E = a.E ? a.E[blk - a.b0]
-                         : exp1_draw(a.seed, (uint32_t)a.gfirst[blk] + a.seg_base, (uint32_t)a.mcmciter, a.salt);
+                         : exp1_draw(a.seed, (uint32_t)a.gfirst[blk] + a.seg_base, a.key_iter, a.salt);
     double ll = a.ll[blk], llp = a.llp[blk];
     const bool acc = E > -(llp - ll);
     if (acc) {
@@ -3067,20 +3137,23 @@ hipError_t launch_block_kernel(const ModelKey& k, int mapping, int mode, const v
 
 template <class Mdl, class T>
 static hipError_t launch_mcmc_t(const void* args, const AcceptArgs& c, int64_t iter0, int64_t n,
-                                double* part, int64_t nwaves, int resident, hipStream_t s) {
+                                double* part, int64_t nwaves, int resident, double* out3,
+                                unsigned* counter, hipStream_t s) {
   if constexpr (Mdl::kLinear) {
     const BlockArgs<T>& a = *static_cast<const BlockArgs<T>*>(args);
     if (nwaves <= 0) return hipSuccess;
+    // part[n][3][nwaves], then the tree nodes [n][3][ceil(nwaves / WPB)] (dmt_mcmc_run sizes it)
+    double* nodes = part + 3 * n * nwaves;
     if constexpr (Mdl::D <= 2) {
       if (resident) {
         dlaunch(k_mcmc_resident<Mdl, T>, dim3((unsigned)((nwaves + 3) / 4)), dim3(256), s, a, c,
-                iter0, n, part);
+                iter0, n, part, nodes, counter, out3);
         return hipGetLastError();
       }
     }
     constexpr int WPB = ScanCfg<Mdl::D, T>::WPB;
     dlaunch(k_mcmc_scan<Mdl, T>, dim3((unsigned)((nwaves + WPB - 1) / WPB)), dim3(64 * WPB), s, a,
-            c, iter0, n, part);
+            c, iter0, n, part, nodes, counter, out3);
     return hipGetLastError();
   } else {
     return hipErrorInvalidValue;
@@ -3089,18 +3162,9 @@ static hipError_t launch_mcmc_t(const void* args, const AcceptArgs& c, int64_t i
 
 hipError_t launch_mcmc_persistent(const ModelKey& k, const void* args, const AcceptArgs& c,
                                   int64_t iter0, int64_t n_iter, double* part, int64_t nwaves,
-                                  int resident, hipStream_t s) {
-  DMT_DISPATCH(k, (launch_mcmc_t<Mdl, T>(args, c, iter0, n_iter, part, nwaves, resident, s)));
-}
-
-hipError_t launch_tree_batched(const double* part, int64_t nb, int64_t n_iter, double* out3,
-                               hipStream_t s) {
-  if (n_iter <= 0) return hipSuccess;
-  int64_t P = 1;
-  while (P < nb) P <<= 1;
-  const int64_t run = P > 256 ? P / 256 : 1;
-  hipLaunchKernelGGL(k_tree_batched, dim3((unsigned)n_iter), dim3(256), 0, s, part, nb, run, out3);
-  return hipGetLastError();
+                                  int resident, double* out3, unsigned* counter, hipStream_t s) {
+  DMT_DISPATCH(k, (launch_mcmc_t<Mdl, T>(args, c, iter0, n_iter, part, nwaves, resident, out3,
+                                         counter, s)));
 }
 
 hipError_t launch_invsolve_kernel(const ModelKey& k, int mapping, const void* args,

@@ -92,6 +92,10 @@ struct dmt_ens {
   int device = 0;
   uint64_t seed = 0;
   uint32_t seg_base = 0;  // dmt_set_shard
+  // DMT_RNG_AUTO stream counter (include/dmt.h): next key, the key of the last auto draw and
+  // whether an auto accept may still take it
+  uint64_t rng_ctr = 0, rng_last_draw = 0;
+  bool rng_pending = false;
   int grid_shared = 0;
   // path snapshots (dmt_snapshot_*): [slots][P][C] doubles in reference layout per kind
   int snap_mask = 0;
@@ -294,6 +298,43 @@ int64_t plane_elems(const dmt_ens* h, int C) { return h->Ptile * C * h->tw; }
 dmt_status check_h(dmt_ens* h) {
   if (!h) return fail(DMT_ERR_INVALID, "null handle");
   if (hipSetDevice(h->device) != hipSuccess) return fail(DMT_ERR_HIP, "hipSetDevice failed");
+  return DMT_OK;
+}
+
+// ---- stream keys (include/dmt.h, "device random streams")
+struct RngKey {
+  uint32_t iter, salt;
+};
+RngKey auto_key(uint64_t k) {
+  return {(uint32_t)k, DMT_SALT_LIMIT + (uint32_t)((k >> 32) & (DMT_SALT_LIMIT - 1))};
+}
+dmt_status check_salt(uint32_t salt) {
+  if (salt != DMT_RNG_AUTO && salt >= DMT_SALT_LIMIT)
+    return fail(DMT_ERR_INVALID, "salt must be < DMT_SALT_LIMIT (larger keys belong to DMT_RNG_AUTO)");
+  return DMT_OK;
+}
+// key of a draw call (draw_proposal: arm = true, the next auto accept reuses it)
+dmt_status draw_key(dmt_ens* h, int64_t iter, uint32_t salt, bool arm, RngKey* k) {
+  DMT_TRY(check_salt(salt));
+  if (salt != DMT_RNG_AUTO) {
+    *k = {(uint32_t)iter, salt};
+    return DMT_OK;
+  }
+  const uint64_t c = h->rng_ctr++;
+  h->rng_last_draw = c;
+  h->rng_pending = arm;
+  *k = auto_key(c);
+  return DMT_OK;
+}
+dmt_status accept_key(dmt_ens* h, int64_t mcmciter, uint32_t salt, RngKey* k) {
+  DMT_TRY(check_salt(salt));
+  if (salt != DMT_RNG_AUTO) {
+    *k = {(uint32_t)mcmciter, salt};
+    return DMT_OK;
+  }
+  const uint64_t c = h->rng_pending ? h->rng_last_draw : h->rng_ctr++;
+  h->rng_pending = false;
+  *k = auto_key(c);
   return DMT_OK;
 }
 
@@ -954,10 +995,12 @@ dmt_status dmt_draw_unit(dmt_ens* h, int32_t unit, int64_t r0, int64_t r1, const
   DMT_TRY(get_layout(h, 0, &L));
   DMT_TRY(check_range(L, r0, r1));
   DMT_TRY(law_ready(h, unit, L, r0, r1));
+  RngKey key;
+  DMT_TRY(draw_key(h, iter, salt, false, &key));
   const double* dZ;
   DMT_TRY(upload_Z(h, Z, &dZ));
   DMT_TRY(run_block_kernel(h, L, MODE_FRESH, DMT_K_DRAW, r0, r1, unit, unit, unit, unit, unit, dZ,
-                           iter, salt, L->d_llp, L->d_success, false));
+                           key.iter, key.salt, L->d_llp, L->d_success, false));
   if (ll_out) HIP_OK(hipMemcpyAsync(ll_out, L->d_llp + r0, (r1 - r0) * 8, hipMemcpyDeviceToHost, h->stream));
   if (success_out) HIP_OK(hipMemcpyAsync(success_out, L->d_success + r0, r1 - r0, hipMemcpyDeviceToHost, h->stream));
   HIP_OK(hipStreamSynchronize(h->stream));
@@ -971,11 +1014,13 @@ dmt_status dmt_draw_proposal(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
   DMT_TRY(get_layout(h, layout, &L));
   DMT_TRY(check_range(L, b0, b1));
   DMT_TRY(law_ready(h, 0, L, b0, b1));
+  RngKey key;
+  DMT_TRY(draw_key(h, iter, salt, true, &key));
   const double* dZ;
   DMT_TRY(upload_Z(h, Z, &dZ));
   // law: accepted u.PP (flip 0); start from u.XX; write u°.XX/u°.WW; read u.WW
-  DMT_TRY(run_block_kernel(h, L, MODE_PCN, DMT_K_DRAW, b0, b1, 0, 0, 1, 0, 1, dZ, iter, salt,
-                           L->d_llp, success_out ? L->d_success : nullptr, false));
+  DMT_TRY(run_block_kernel(h, L, MODE_PCN, DMT_K_DRAW, b0, b1, 0, 0, 1, 0, 1, dZ, key.iter,
+                           key.salt, L->d_llp, success_out ? L->d_success : nullptr, false));
   if (success_out) {
     HIP_OK(hipMemcpyAsync(success_out, L->d_success + b0, b1 - b0, hipMemcpyDeviceToHost, h->stream));
     HIP_OK(hipStreamSynchronize(h->stream));
@@ -986,7 +1031,7 @@ dmt_status dmt_draw_proposal(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
 }
 
 static AcceptArgs accept_args(dmt_ens* h, Layout* L, int64_t b0, int64_t b1, const double* dE,
-                              int64_t mcmciter, uint32_t salt, uint8_t* acc_dev) {
+                              int64_t mcmciter, RngKey key, uint8_t* acc_dev) {
   AcceptArgs a{};
   a.b0 = b0;
   a.b1 = b1;
@@ -1005,7 +1050,9 @@ static AcceptArgs accept_args(dmt_ens* h, Layout* L, int64_t b0, int64_t b1, con
   a.E = dE;
   a.seed = h->seed;
   a.seg_base = h->seg_base;
-  a.salt = salt;
+  a.salt = key.salt;
+  a.key_iter = key.iter;
+  a.key_delta = 0;
   a.acc_out = acc_dev;
   return a;
 }
@@ -1030,8 +1077,8 @@ static dmt_status ensure_red_work(dmt_ens* h, int64_t n) {
 }
 
 // d_red (3 partials of this rank) -> host values, combined over ranks with RCCL
-static dmt_status finish_reduction(dmt_ens* h, double* v) {
-  if (h->comm) {
+static dmt_status finish_reduction(dmt_ens* h, double* v, bool global = true) {
+  if (h->comm && global) {
     if (!h->d_gather) DMT_TRY(ens_alloc(h, &h->d_gather, 3 * h->nranks));
     if (ncclAllGather(h->d_red, h->d_gather, 3, ncclDouble, h->comm, h->stream) != ncclSuccess)
       return fail(DMT_ERR_COMM, "ncclAllGather failed");
@@ -1067,12 +1114,14 @@ dmt_status dmt_mcmc_step(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int
   DMT_TRY(law_ready(h, 0, L, b0, b1));
   if (L->hist_len > 0 && (mcmciter < 1 || mcmciter > L->hist_len))
     return fail(DMT_ERR_INVALID, "mcmciter outside 1:ll_hist_len");
-  DMT_TRY(run_block_kernel(h, L, MODE_PCN, DMT_K_DRAW, b0, b1, 0, 0, 1, 0, 1, nullptr, mcmciter,
-                           salt, L->d_llp, nullptr, false));
+  RngKey key;  // one key for the draw and its decision (disjoint normal / Exp(1) streams)
+  DMT_TRY(draw_key(h, mcmciter, salt, false, &key));
+  DMT_TRY(run_block_kernel(h, L, MODE_PCN, DMT_K_DRAW, b0, b1, 0, 0, 1, 0, 1, nullptr, key.iter,
+                           key.salt, L->d_llp, nullptr, false));
   DMT_TRY(ensure_red_work(h, b1 - b0));
   {
     TimedScope ts(h, DMT_K_ACCEPT);
-    HIP_OK(launch_accept_reduce(accept_args(h, L, b0, b1, nullptr, mcmciter, salt, nullptr),
+    HIP_OK(launch_accept_reduce(accept_args(h, L, b0, b1, nullptr, mcmciter, key, nullptr),
                                 h->d_red_work, h->d_red_lb, h->d_red, h->stream));
   }
   double v[3];
@@ -1083,6 +1132,13 @@ dmt_status dmt_mcmc_step(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int
   return DMT_OK;
 }
 
+// Capacity of dmt_mcmc_run's buffers: grown geometrically with a floor, so that a run of a
+// different length (e.g. a benchmark's warm-up and timed runs) does not free and re-allocate
+// device memory — hipFree synchronises the device.
+static int64_t grown_cap(int64_t need, int64_t cap, int64_t floor_) {
+  return std::max({need, 2 * cap, floor_});
+}
+
 dmt_status dmt_mcmc_run(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int64_t iter0,
                         int64_t n_iter, uint32_t salt, double* out) {
   DMT_TRY(check_h(h));
@@ -1090,10 +1146,24 @@ dmt_status dmt_mcmc_run(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int6
   DMT_TRY(get_layout(h, layout, &L));
   DMT_TRY(check_range(L, b0, b1));
   DMT_TRY(law_ready(h, 0, L, b0, b1));
+  DMT_TRY(check_salt(salt));
   if (n_iter < 0 || iter0 < 1) return fail(DMT_ERR_INVALID, "bad iteration range");
   if (n_iter == 0) return DMT_OK;
   if (L->hist_len > 0 && iter0 + n_iter - 1 > L->hist_len)
     return fail(DMT_ERR_INVALID, "iterations outside 1:ll_hist_len");
+  // stream keys: iteration it draws its normals and its Exp(1) variables with key word
+  // it + key_delta (explicit: the iteration itself; auto: n_iter consecutive counter values,
+  // never straddling a 2^32 boundary so that the salt word is constant over the run)
+  int64_t key_delta = 0;
+  if (salt == DMT_RNG_AUTO) {
+    uint64_t base = h->rng_ctr;
+    if ((base & 0xFFFFFFFFull) + (uint64_t)n_iter > 0x100000000ull)
+      base = (base | 0xFFFFFFFFull) + 1;
+    h->rng_ctr = base + (uint64_t)n_iter;
+    h->rng_pending = false;
+    salt = auto_key(base).salt;
+    key_delta = (int64_t)(uint32_t)base - iter0;
+  }
   const bool multi = h->comm != nullptr;
   if (n_iter > h->run_cap) {
     if (h->d_run) { (void)hipFree(h->d_run); h->bytes -= h->run_cap * 24; h->d_run = nullptr; }
@@ -1102,10 +1172,11 @@ dmt_status dmt_mcmc_run(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int6
       h->bytes -= h->run_cap * 24 * h->nranks;
       h->d_run_gather = nullptr;
     }
+    const int64_t cap = grown_cap(n_iter, h->run_cap, 4096);
     h->run_cap = 0;
-    DMT_TRY(ens_alloc(h, &h->d_run, 3 * n_iter));
-    if (multi) DMT_TRY(ens_alloc(h, &h->d_run_gather, 3 * n_iter * h->nranks));
-    h->run_cap = n_iter;
+    DMT_TRY(ens_alloc(h, &h->d_run, 3 * cap));
+    if (multi) DMT_TRY(ens_alloc(h, &h->d_run_gather, 3 * cap * h->nranks));
+    h->run_cap = cap;
   } else if (multi && !h->d_run_gather) {
     DMT_TRY(ens_alloc(h, &h->d_run_gather, 3 * h->run_cap * h->nranks));
   }
@@ -1118,18 +1189,25 @@ dmt_status dmt_mcmc_run(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int6
   for (int64_t b = b0; b < b1 && resident; ++b)
     resident = L->glast[b] == L->gfirst[b] && h->seg_np[L->gfirst[b]] - 1 <= kResidentMaxSteps;
   if (persist) {
-    // the whole run in one launch per chunk of iterations (k_mcmc_scan), then one batched
-    // fetch_ll tree over all iterations and (multi-GPU) one all-gather
-    const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(n_iter, (int64_t(64) << 20) / (24 * nb)));
-    if (3 * nb * chunk > h->part_cap) {
+    // the whole run in one launch per chunk of iterations (k_mcmc_scan / k_mcmc_resident),
+    // every iteration's fetch_ll tree formed inside the launch
+    const int64_t chunk_max = std::max<int64_t>(1, (int64_t(64) << 20) / (24 * nb));
+    const int64_t chunk = std::min<int64_t>(n_iter, chunk_max);
+    const int64_t ngroups = nb;  // ≥ the tree nodes the kernel folds its blocks into (nb / WPB)
+    const int64_t need = 3 * nb * chunk + 3 * ngroups * chunk + 8;
+    if (need > h->part_cap) {
       if (h->d_part) { (void)hipFree(h->d_part); h->bytes -= h->part_cap * 8; h->d_part = nullptr; }
+      const int64_t cap_it = std::min(chunk_max, std::max<int64_t>(chunk, 256));
+      const int64_t cap = std::max(need, 3 * nb * cap_it + 3 * ngroups * cap_it + 8);
       h->part_cap = 0;
-      DMT_TRY(ens_alloc(h, &h->d_part, 3 * nb * chunk));
-      h->part_cap = 3 * nb * chunk;
+      DMT_TRY(ens_alloc(h, &h->d_part, cap));
+      HIP_OK(hipMemsetAsync(h->d_part, 0, cap * 8, h->stream));  // zero the arrival counter
+      h->part_cap = cap;
     }
     for (int64_t i0 = 0; i0 < n_iter; i0 += chunk) {
       const int64_t n = std::min(chunk, n_iter - i0);
-      const AcceptArgs c = accept_args(h, L, b0, b1, nullptr, iter0 + i0, salt, nullptr);
+      AcceptArgs c = accept_args(h, L, b0, b1, nullptr, iter0 + i0, RngKey{0, salt}, nullptr);
+      c.key_delta = key_delta;
       hipError_t e;
       {
         TimedScope ts(h, DMT_K_DRAW, true, n);
@@ -1143,39 +1221,41 @@ dmt_status dmt_mcmc_run(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int6
           a.wd_flip = 1;
           a.salt = salt;
         };
+        // d_part: [part_cap - 8, part_cap) holds the arrival counter of the in-kernel tree
+        double* counter = h->d_part + h->part_cap - 8;
         if (h->key.precision == DMT_F64) {
           BlockArgs<double> a{};
           fill(a);
-          e = launch_mcmc_persistent(h->key, &a, c, iter0 + i0, n, h->d_part, nb, resident, h->stream);
+          e = launch_mcmc_persistent(h->key, &a, c, iter0 + i0, n, h->d_part, nb, resident,
+                                     h->d_run + 3 * i0, (unsigned*)counter, h->stream);
         } else {
           BlockArgs<float> a{};
           fill(a);
-          e = launch_mcmc_persistent(h->key, &a, c, iter0 + i0, n, h->d_part, nb, resident, h->stream);
+          e = launch_mcmc_persistent(h->key, &a, c, iter0 + i0, n, h->d_part, nb, resident,
+                                     h->d_run + 3 * i0, (unsigned*)counter, h->stream);
         }
       }
       if (e != hipSuccess) return fail(DMT_ERR_HIP, std::string("k_mcmc_scan: ") + hipGetErrorString(e));
-      HIP_OK(launch_tree_batched(h->d_part, nb, n, h->d_run + 3 * i0, h->stream));
     }
-    if (multi && ncclAllGather(h->d_run, h->d_run_gather, 3 * n_iter, ncclDouble, h->comm,
-                               h->stream) != ncclSuccess)
-      return fail(DMT_ERR_COMM, "ncclAllGather failed");
   } else {
     // every iteration is stream-ordered: no host synchronisation until the end
     for (int64_t i = 0; i < n_iter; ++i) {
       const int64_t it = iter0 + i;
-      DMT_TRY(run_block_kernel(h, L, MODE_PCN, DMT_K_DRAW, b0, b1, 0, 0, 1, 0, 1, nullptr, it,
-                               salt, L->d_llp, nullptr, false));
+      const RngKey key{(uint32_t)(it + key_delta), salt};
+      DMT_TRY(run_block_kernel(h, L, MODE_PCN, DMT_K_DRAW, b0, b1, 0, 0, 1, 0, 1, nullptr,
+                               key.iter, key.salt, L->d_llp, nullptr, false));
       {
         TimedScope ts(h, DMT_K_ACCEPT);
-        HIP_OK(launch_accept_reduce(accept_args(h, L, b0, b1, nullptr, it, salt, nullptr),
+        HIP_OK(launch_accept_reduce(accept_args(h, L, b0, b1, nullptr, it, key, nullptr),
                                     h->d_red_work, h->d_red_lb, h->d_run + 3 * i, h->stream));
       }
-      if (multi &&
-          ncclAllGather(h->d_run + 3 * i, h->d_run_gather + 3 * h->nranks * i, 3, ncclDouble,
-                        h->comm, h->stream) != ncclSuccess)
-        return fail(DMT_ERR_COMM, "ncclAllGather failed");
     }
   }
+  // one all-gather of every iteration's three partials, whichever kernel path ran on this
+  // rank (ranks may differ in path eligibility; the collective sequence must not)
+  if (multi && ncclAllGather(h->d_run, h->d_run_gather, 3 * n_iter, ncclDouble, h->comm,
+                             h->stream) != ncclSuccess)
+    return fail(DMT_ERR_COMM, "ncclAllGather failed");
   if (!out) {
     HIP_OK(hipStreamSynchronize(h->stream));
     return DMT_OK;
@@ -1195,8 +1275,7 @@ dmt_status dmt_mcmc_run(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int6
   for (int64_t i = 0; i < n_iter; ++i)
     for (int c = 0; c < 3; ++c) {  // the rank-order tree of finish_reduction
       std::fill(lv.begin(), lv.end(), 0.0);
-      for (int r = 0; r < h->nranks; ++r)
-        lv[r] = persist ? all[(r * n_iter + i) * 3 + c] : all[3 * h->nranks * i + 3 * r + c];
+      for (int r = 0; r < h->nranks; ++r) lv[r] = all[(r * n_iter + i) * 3 + c];
       for (int w = n2; w > 1; w >>= 1)
         for (int j = 0; j < w / 2; ++j) lv[j] = lv[2 * j] + lv[2 * j + 1];
       out[3 * i + c] = lv[0] + 0.0;
@@ -1212,13 +1291,15 @@ dmt_status dmt_accept_reject(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
   DMT_TRY(check_range(L, b0, b1));
   if (L->hist_len > 0 && (mcmciter < 1 || mcmciter > L->hist_len))
     return fail(DMT_ERR_INVALID, "mcmciter outside 1:ll_hist_len");
+  RngKey key;
+  DMT_TRY(accept_key(h, mcmciter, salt, &key));
   const double* dE = nullptr;
   if (E) {
     DMT_TRY(ensure_Z(h, std::max<int64_t>(b1 - b0, 1)));
     HIP_OK(hipMemcpyAsync(h->d_Z, E, (b1 - b0) * 8, hipMemcpyHostToDevice, h->stream));
     dE = h->d_Z;
   }
-  AcceptArgs a = accept_args(h, L, b0, b1, dE, mcmciter, salt, acc_out ? L->d_acc : nullptr);
+  AcceptArgs a = accept_args(h, L, b0, b1, dE, mcmciter, key, acc_out ? L->d_acc : nullptr);
   {
     TimedScope ts(h, DMT_K_ACCEPT);
     HIP_OK(launch_accept(a, h->stream));
@@ -1619,8 +1700,9 @@ dmt_status dmt_set_block_state(dmt_ens* h, int32_t layout, int32_t what, int64_t
   return DMT_OK;
 }
 
-dmt_status dmt_fetch_ll(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int64_t mcmciter,
-                        double* ll, double* ll_prop, int64_t* n_acc) {
+static dmt_status fetch_ll_impl(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
+                                int64_t mcmciter, bool global, double* ll, double* ll_prop,
+                                int64_t* n_acc) {
   DMT_TRY(check_h(h));
   Layout* L;
   DMT_TRY(get_layout(h, layout, &L));
@@ -1637,10 +1719,33 @@ dmt_status dmt_fetch_ll(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int6
                             h->stream));
   }
   double v[3];
-  DMT_TRY(finish_reduction(h, v));
+  DMT_TRY(finish_reduction(h, v, global));
   if (ll) *ll = v[0];
   if (ll_prop) *ll_prop = v[1];
   if (n_acc) *n_acc = (int64_t)v[2];
+  return DMT_OK;
+}
+
+dmt_status dmt_fetch_ll(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int64_t mcmciter,
+                        double* ll, double* ll_prop, int64_t* n_acc) {
+  return fetch_ll_impl(h, layout, b0, b1, mcmciter, true, ll, ll_prop, n_acc);
+}
+
+dmt_status dmt_fetch_ll_local(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
+                              int64_t mcmciter, double* ll, double* ll_prop, int64_t* n_acc) {
+  return fetch_ll_impl(h, layout, b0, b1, mcmciter, false, ll, ll_prop, n_acc);
+}
+
+dmt_status dmt_rng_counter(dmt_ens* h, uint64_t* next) {
+  if (!h || !next) return fail(DMT_ERR_INVALID, "null argument");
+  *next = h->rng_ctr;
+  return DMT_OK;
+}
+
+dmt_status dmt_set_rng_counter(dmt_ens* h, uint64_t next) {
+  if (!h) return fail(DMT_ERR_INVALID, "null handle");
+  h->rng_ctr = next;
+  h->rng_pending = false;
   return DMT_OK;
 }
 
@@ -1712,6 +1817,19 @@ dmt_status dmt_comm_init(dmt_ens* h, int32_t nranks, int32_t rank, const uint8_t
   std::memcpy(&uid, id, 128);
   if (ncclCommInitRank(&h->comm, nranks, uid, rank) != ncclSuccess)
     return fail(DMT_ERR_COMM, "ncclCommInitRank failed");
+  return DMT_OK;
+}
+
+dmt_status dmt_comm_size(dmt_ens* h, int32_t* nranks) {
+  DMT_TRY(check_h(h));
+  if (!nranks) return fail(DMT_ERR_INVALID, "null argument");
+  if (!h->comm) {
+    *nranks = 1;
+    return DMT_OK;
+  }
+  int n = 0;
+  if (ncclCommCount(h->comm, &n) != ncclSuccess) return fail(DMT_ERR_COMM, "ncclCommCount failed");
+  *nranks = n;
   return DMT_OK;
 }
 

@@ -253,10 +253,13 @@ class Ensemble:
         v = np.ascontiguousarray(values, dtype=dt)
         L.call("dmt_set_block_state", self._h, layout, what, b0, b1, v.ctypes.data_as(C.c_void_p))
 
-    def fetch_ll(self, layout, b0, b1, mcmciter=0):
+    def fetch_ll(self, layout, b0, b1, mcmciter=0, local=False):
+        """(Σ ll, Σ ll°, accepted count of ``mcmciter``) over blocks [b0, b1).  With a
+        communicator the sums run over every rank (a collective: BlockEnsemble level) unless
+        ``local`` (BiBlock / BlockCollection level: this rank's blocks only)."""
         a, b, n = C.c_double(), C.c_double(), C.c_int64()
-        L.call("dmt_fetch_ll", self._h, layout, b0, b1, int(mcmciter), C.byref(a), C.byref(b),
-               C.byref(n))
+        L.call("dmt_fetch_ll_local" if local else "dmt_fetch_ll", self._h, layout, b0, b1,
+               int(mcmciter), C.byref(a), C.byref(b), C.byref(n))
         return a.value, b.value, n.value
 
     def mcmc_step(self, layout, b0, b1, mcmciter, salt=0):
@@ -297,6 +300,20 @@ class Ensemble:
         buf = (C.c_uint8 * 128).from_buffer_copy(uid)
         L.call("dmt_comm_init", self._h, int(nranks), int(rank), buf)
 
+    def comm_size(self):
+        """Ranks of the communicator as RCCL reports them (1 without one)."""
+        n = C.c_int32()
+        L.call("dmt_comm_size", self._h, C.byref(n))
+        return n.value
+
+    def rng_counter(self):
+        """Next value of the handle's DMT_RNG_AUTO stream counter."""
+        n = C.c_uint64()
+        L.call("dmt_rng_counter", self._h, C.byref(n))
+        return n.value
+
+    def set_rng_counter(self, value):
+        L.call("dmt_set_rng_counter", self._h, int(value))
 
     def set_shard(self, seg_base):
         """This handle holds a shard whose local segment 0 is global segment ``seg_base``."""

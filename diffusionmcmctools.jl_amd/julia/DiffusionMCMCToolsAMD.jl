@@ -15,7 +15,8 @@ using StaticArrays
 
 import DiffusionMCMCTools: draw_proposal_path!, accept_reject_proposal_path!, loglikhd!,
     loglikhd°!, fetch_ll, fetch_ll°, save_ll!, set_ll!, set_accepted!, swap_paths!, swap_XX!,
-    swap_WW!, swap_PP!, swap_ll!, ll_of_accepted, accpt_rate, recompute_path!, find_W_for_X!
+    swap_WW!, swap_PP!, swap_ll!, ll_of_accepted, accpt_rate, recompute_path!, find_W_for_X!,
+    BiBlock, BlockCollection, BlockEnsemble
 
 export DeviceSamplingEnsemble, DeviceBlockEnsemble, DeviceBlockCollection, DeviceBiBlock,
     mcmc_step!, mcmc_run!, download_XX, download_WW, upload_obs!, set_obs!,
@@ -33,6 +34,12 @@ const DMT_SWAP_XX, DMT_SWAP_WW, DMT_SWAP_PP, DMT_SWAP_LL = Int32(1), Int32(2), I
 const DMT_BLK_LL, DMT_BLK_LLPROP, DMT_BLK_LL_HIST, DMT_BLK_LLPROP_HIST, DMT_BLK_ACC_HIST =
     Int32(0), Int32(1), Int32(2), Int32(3), Int32(4)
 const DMT_LAW_STRIDE = 64
+# draws with no key take the handle's stream counter, as the reference's take the global RNG
+# (src/biblock.jl:94-99,122); explicit salts must stay below DMT_SALT_LIMIT
+const DMT_RNG_AUTO = typemax(UInt32)
+const DMT_SALT_LIMIT = UInt32(0x40000000)
+_key(iter, salt) = (iter === nothing && salt === nothing) ? (0, DMT_RNG_AUTO) :
+    (something(iter, 0), UInt32(something(salt, 0)))
 
 struct dmt_model
     model::Int32
@@ -154,7 +161,9 @@ write_snapshots(se::DeviceSamplingEnsemble, path::AbstractString, s0, s1) =
                 se.h, path, s0, s1))
 
 "draw_proposal_path!(u::SamplingUnit) for recordings r0+1:r1 (src/sampling_unit.jl:118)."
-function draw_unit!(se::DeviceSamplingEnsemble, unit, r0, r1; Z=nothing, iter=0, salt=0)
+function draw_unit!(se::DeviceSamplingEnsemble, unit, r0, r1; Z=nothing, iter=nothing,
+                    salt=nothing)
+    iter, salt = _key(iter, salt)
     ll = Vector{Float64}(undef, r1 - r0)
     ok = Vector{UInt8}(undef, r1 - r0)
     pz = Z === nothing ? Ptr{Float64}(C_NULL) : pointer(Z)
@@ -195,6 +204,19 @@ struct DeviceBiBlock{L} <: DeviceBlocks
 end
 
 """
+    DeviceSamplingPair(se, r)
+
+Recording `r` (1-based) of a device ensemble: the `SamplingPair` argument of the reference's
+`BiBlock(sp, range, ρ, last_block, ll_hist_len)` / `BlockCollection(sp, ranges, ρρ,
+ll_hist_len)` constructors (src/biblock.jl:48-62, src/block_collection.jl:22-30).
+"""
+struct DeviceSamplingPair
+    se::DeviceSamplingEnsemble
+    r::Int
+end
+Base.getindex(se::DeviceSamplingEnsemble, r::Integer) = DeviceSamplingPair(se, r)
+
+"""
     DeviceBlockEnsemble(se, ranges, ρρ=0.0, ll_hist_len=0)
 
 Same arguments as `BlockEnsemble(se, ranges, ρρ, ll_hist_len)` (src/block_ensemble.jl:20):
@@ -203,6 +225,7 @@ or per recording per block.
 """
 function DeviceBlockEnsemble(se::DeviceSamplingEnsemble, ranges, ρρ=0.0, ll_hist_len=0)
     R = length(ranges)
+    ll_hist_len = maximum(ll_hist_len)  # _vec_me (src/block_ensemble.jl:28): one device length
     n_blocks = Int32[length(rr) for rr in ranges]
     sf, sl, islast, rho = Int32[], Int32[], UInt8[], Float64[]
     for r in 1:R
@@ -228,10 +251,43 @@ function DeviceBlockEnsemble(se::DeviceSamplingEnsemble, ranges, ρρ=0.0, ll_hi
     DeviceBlockEnsemble(se, id[], 0, b, ll_hist_len, recs)
 end
 
+# The reference's constructors on device containers (same signatures): unchanged caller code
+# `BlockEnsemble(se, ranges, ρ, n)` / `BlockCollection(sp, ranges, ρ, n)` /
+# `BiBlock(sp, range, ρ, last, n)` builds device blocks when `se` / `sp` live on the GPU.
+BlockEnsemble(se::DeviceSamplingEnsemble, ranges, ρρ=0.0, ll_hist_len=0) =
+    DeviceBlockEnsemble(se, ranges, ρρ, ll_hist_len)
+
+function BlockCollection(sp::DeviceSamplingPair, ranges, ρρ=0.0, ll_hist_len=0)
+    R = length(sp.se.n_points)
+    all_ranges = [r == sp.r ? collect(ranges) : UnitRange{Int}[] for r in 1:R]
+    ρ = [r == sp.r ? ρρ : 0.0 for r in 1:R]
+    DeviceBlockEnsemble(sp.se, all_ranges, ρ, ll_hist_len).recordings[sp.r]
+end
+
+function BiBlock(sp::DeviceSamplingPair, range::UnitRange{Int64}, ρ=0.0, last_block=false,
+                 ll_hist_len=0)
+    R = length(sp.se.n_points)
+    n_blocks = Int32[r == sp.r ? 1 : 0 for r in 1:R]
+    id = Ref{Int32}(0)
+    check(ccall((:dmt_create_layout, libdmt), Int32,
+        (Ptr{Cvoid}, Ptr{Int32}, Ptr{Int32}, Ptr{Int32}, Ptr{UInt8}, Ptr{Float64}, Int64,
+         Ref{Int32}), sp.se.h, n_blocks, Int32[first(range) - 1], Int32[last(range) - 1],
+        UInt8[last_block], Float64[ρ], ll_hist_len, id))
+    DeviceBiBlock{Bool(last_block)}(sp.se, id[], 0, 1, ll_hist_len, ρ)
+end
+
 _n(x::DeviceBlocks) = x.b1 - x.b0
 
 # ---- imputation and MH (src/biblock.jl:78-127, block_collection.jl:46-68, block_ensemble.jl:50-69)
-function draw_proposal_path!(x::DeviceBlocks; Z=nothing, iter=0, salt=0)
+"""
+    draw_proposal_path!(x; Z=nothing, iter=nothing, salt=nothing)
+
+pCN proposal under the accepted law into u°.  With no keyword the normals are the next ones of
+the device stream counter (every call fresh, as the reference's `rand!` on the global RNG);
+`iter`/`salt` select a reproducible keyed stream; `Z` supplies them (parity mode).
+"""
+function draw_proposal_path!(x::DeviceBlocks; Z=nothing, iter=nothing, salt=nothing)
+    iter, salt = _key(iter, salt)
     ok = Vector{UInt8}(undef, _n(x))
     pz = Z === nothing ? Ptr{Float64}(C_NULL) : pointer(Z)
     GC.@preserve Z check(ccall((:dmt_draw_proposal, libdmt), Int32,
@@ -240,7 +296,8 @@ function draw_proposal_path!(x::DeviceBlocks; Z=nothing, iter=0, salt=0)
     x isa DeviceBiBlock ? Bool(ok[1]) : Bool.(ok)
 end
 
-function accept_reject_proposal_path!(x::DeviceBlocks, mcmciter; E=nothing, salt=0)
+function accept_reject_proposal_path!(x::DeviceBlocks, mcmciter; E=nothing, salt=nothing)
+    salt = salt === nothing ? DMT_RNG_AUTO : UInt32(salt)
     acc = Vector{UInt8}(undef, _n(x))
     pe = E === nothing ? Ptr{Float64}(C_NULL) : pointer(E)
     GC.@preserve E check(ccall((:dmt_accept_reject, libdmt), Int32,
@@ -250,7 +307,8 @@ function accept_reject_proposal_path!(x::DeviceBlocks, mcmciter; E=nothing, salt
 end
 
 "draw_proposal_path! + accept_reject_proposal_path!(·, i) + (fetch_ll, fetch_ll°, #accepted)."
-function mcmc_step!(x::DeviceBlocks, mcmciter; salt=0)
+function mcmc_step!(x::DeviceBlocks, mcmciter; salt=nothing)
+    salt = salt === nothing ? DMT_RNG_AUTO : UInt32(salt)
     a, b, n = Ref(0.0), Ref(0.0), Ref{Int64}(0)
     check(ccall((:dmt_mcmc_step, libdmt), Int32,
         (Ptr{Cvoid}, Int32, Int64, Int64, Int64, UInt32, Ref{Float64}, Ref{Float64}, Ref{Int64}),
@@ -259,7 +317,8 @@ function mcmc_step!(x::DeviceBlocks, mcmciter; salt=0)
 end
 
 "n_iter iterations of mcmc_step! from iter0 on, no host round trips; (n_iter, 3) results."
-function mcmc_run!(x::DeviceBlocks, iter0, n_iter; salt=0)
+function mcmc_run!(x::DeviceBlocks, iter0, n_iter; salt=nothing)
+    salt = salt === nothing ? DMT_RNG_AUTO : UInt32(salt)
     out = Matrix{Float64}(undef, 3, n_iter)
     check(ccall((:dmt_mcmc_run, libdmt), Int32,
         (Ptr{Cvoid}, Int32, Int64, Int64, Int64, Int64, UInt32, Ptr{Float64}),
@@ -273,11 +332,19 @@ _ll!(x, unit) = check(ccall((:dmt_loglikhd, libdmt), Int32,
 loglikhd!(x::DeviceBlocks) = _ll!(x, DMT_U)
 loglikhd°!(x::DeviceBlocks) = _ll!(x, DMT_UPROP)
 
+# fetch_ll(be) is the whole (multi-GPU) ensemble's (a collective over ranks); a collection's or
+# a block's is this rank's (src/block_collection.jl:144,156, src/block_ensemble.jl:140,152)
 function _fetch(x::DeviceBlocks)
     a, b, n = Ref(0.0), Ref(0.0), Ref{Int64}(0)
-    check(ccall((:dmt_fetch_ll, libdmt), Int32,
-        (Ptr{Cvoid}, Int32, Int64, Int64, Int64, Ref{Float64}, Ref{Float64}, Ref{Int64}),
-        x.se.h, x.layout, x.b0, x.b1, 0, a, b, n))
+    if x isa DeviceBlockEnsemble
+        check(ccall((:dmt_fetch_ll, libdmt), Int32,
+            (Ptr{Cvoid}, Int32, Int64, Int64, Int64, Ref{Float64}, Ref{Float64}, Ref{Int64}),
+            x.se.h, x.layout, x.b0, x.b1, 0, a, b, n))
+    else
+        check(ccall((:dmt_fetch_ll_local, libdmt), Int32,
+            (Ptr{Cvoid}, Int32, Int64, Int64, Int64, Ref{Float64}, Ref{Float64}, Ref{Int64}),
+            x.se.h, x.layout, x.b0, x.b1, 0, a, b, n))
+    end
     a[], b[]
 end
 fetch_ll(x::DeviceBlocks) = _fetch(x)[1]
@@ -302,10 +369,20 @@ upload_obs!(se::DeviceSamplingEnsemble, Hobs, Fobs, cobs; artificial_noise=1e-11
 set_obs!(x::DeviceBlocks) = check(ccall((:dmt_set_obs, libdmt), Int32,
     (Ptr{Cvoid}, Int32, Int64, Int64), x.se.h, x.layout, x.b0, x.b1))
 
-"GP.recompute_guiding_term!(bb.b) (unit = DMT_U) or of bb.b° (DMT_UPROP) on the device."
-recompute_guiding_term!(x::DeviceBlocks, unit=DMT_U) = check(ccall(
+_rgt!(x::DeviceBlocks, unit) = check(ccall(
     (:dmt_recompute_guiding_term, libdmt), Int32, (Ptr{Cvoid}, Int32, Int64, Int64, Int32),
     x.se.h, x.layout, x.b0, x.b1, unit))
+"""
+    recompute_guiding_term!(x, [::Val{:P_only} | ::Val{:P°_only}])
+
+GP.recompute_guiding_term! on the device: with no flag both the accepted and the proposal laws,
+b then b° (src/biblock.jl:288-291, src/block_collection.jl:208-210); `Val(:P_only)` the
+accepted laws (= `recompute_guiding_term!(bb.b)`), `Val(:P°_only)` the proposal laws
+(src/block_collection.jl:212-221).
+"""
+recompute_guiding_term!(x::DeviceBlocks) = (_rgt!(x, DMT_U); _rgt!(x, DMT_UPROP))
+recompute_guiding_term!(x::DeviceBlocks, ::Val{:P_only}) = _rgt!(x, DMT_U)
+recompute_guiding_term!(x::DeviceBlocks, ::Val{:P°_only}) = _rgt!(x, DMT_UPROP)
 
 """
     set_proposal_law!(x, θ°::AbstractVector, pnames::AbstractVector{Symbol}; skip=0)

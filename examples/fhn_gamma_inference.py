@@ -137,7 +137,7 @@ def sampling_pair(recording, gamma, dt=1e-3, backend="device", seed=0, blocking=
     se.set_observations(np.stack([packed(i[0]) for i in infos]),
                         np.stack([np.asarray(i[1], dtype=np.float64) for i in infos]),
                         np.array([float(i[2]) for i in infos]), artificial_noise=ARTIFICIAL_NOISE)
-    ll0, ok = se.init_paths([rec.x0 for rec in recordings], iter=0)
+    ll0, ok = se.init_paths([rec.x0 for rec in recordings])
     if not ok.all():
         raise RuntimeError("init_paths failed")
     return se
@@ -161,8 +161,8 @@ def simple_inference(se, gamma0, eps=0.3, rho=0.96, num_steps=10 ** 4, seed=1,
     theta = np.array([gamma0])
     chain, a_path, a_par, ll_acc = [theta[0]], [], [], []
     for i in range(1, num_steps + 1):
-        bb.draw_proposal_path(iter=i)
-        acc_p = np.asarray(bb.accept_reject_proposal_path(i))
+        bb.draw_proposal_path()                                      # draw_proposal_path!(bb)
+        acc_p = np.asarray(bb.accept_reject_proposal_path(i))        # (bb, i)
         a_path.append(bool(acc_p[0]) if acc_p.size == 1 else acc_p)
         theta_p = theta + 2.0 * eps * (rng.random() - 0.5)          # customkernel(θ, ϵ)
         bb.set_proposal_law(theta={"gamma": theta_p[0]})
@@ -186,7 +186,8 @@ def simple_inference_with_blocking(se, gamma0, blockings=BLOCKINGS, eps=0.3, rho
     iteration and per blocking, set_obs! → recompute_guiding_term!(b) → find_W_for_X! →
     loglikhd! → draw_proposal_path! → accept_reject_proposal_path!; then the γ update on the
     last blocking (set_proposal_law! of every block, recompute_guiding_term!(b°), the MH
-    decision on the summed log-likelihoods).  Blocking k draws with device salt k."""
+    decision on the summed log-likelihoods).  Draws come from the device stream counter, as the
+    reference's come from the global RNG: every blocking of every iteration gets fresh ones."""
     rng = np.random.default_rng(seed)
     bes = [dmt.BlockEnsemble(se, [b], rho=rho, ll_hist_len=num_steps) for b in blockings]
     theta = np.array([gamma0])
@@ -194,17 +195,17 @@ def simple_inference_with_blocking(se, gamma0, blockings=BLOCKINGS, eps=0.3, rho
     for i in range(1, num_steps + 1):
         acc_i = []
         for k, be in enumerate(bes):
-            be.set_obs()
-            be.recompute_guiding_term()
-            be.find_W_for_X()
-            be.loglikhd()
-            be.draw_proposal_path(iter=i, salt=k)
-            acc_i.append(be.accept_reject_proposal_path(i, salt=k))
+            be.set_obs()                                   # GP.set_obs!.(B)
+            be.recompute_guiding_term(only="P_only")       # (bb->recompute_guiding_term!(bb.b)).(B)
+            be.find_W_for_X()                              # find_W_for_X!.(B)
+            be.loglikhd()                                  # loglikhd!.(B)
+            be.draw_proposal_path()                        # draw_proposal_path!.(B)
+            acc_i.append(be.accept_reject_proposal_path(i))  # accept_reject_proposal_path!.(B, i)
         a_path.append(np.concatenate(acc_i))
         theta_p = theta + 2.0 * eps * (rng.random() - 0.5)
         be = bes[-1]
         be.set_proposal_law(theta={"gamma": theta_p[0]})
-        be.recompute_guiding_term(unit=L.UPROP)
+        be.recompute_guiding_term(only="P°_only")          # (bb->recompute_guiding_term!(bb.b°)).(B)
         acc, theta = be.accept_reject_proposal_param(i, theta, theta_p, E=rng.exponential(1.0))
         a_par.append(acc)
         chain.append(float(theta[0]))

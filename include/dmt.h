@@ -141,6 +141,27 @@ typedef struct {
     int32_t mapping;             /* DMT_MAP_*: thread mapping of the Euler recursion */
 } dmt_config;
 
+/* ---------------- device random streams (perf mode) ----------------
+ * Draw calls take a stream key (iter, salt).  An explicit key (salt < DMT_SALT_LIMIT) selects
+ * a reproducible stream: normals are keyed by (seed, iter, salt, global segment, step), Exp(1)
+ * variables by (seed, mcmciter, salt, global id of the block's first segment).
+ * salt = DMT_RNG_AUTO draws from the handle's own stream counter instead, which is how the
+ * reference consumes randomness: rand! and rand(Exponential(1.0)) read the global RNG and take
+ * no key (src/biblock.jl:94-99,122, src/sampling_unit.jl:119).  Under DMT_RNG_AUTO
+ *   - dmt_draw_proposal, dmt_draw_unit and dmt_mcmc_step take the next counter value k
+ *     (their `iter` argument is ignored);
+ *   - dmt_accept_reject takes the k of the auto draw it follows, once; otherwise the next k
+ *     (`mcmciter` still indexes the histories);
+ *   - dmt_mcmc_run takes n_iter consecutive values, one per iteration, for its draw and its
+ *     decision (so a run equals the loop of auto draw + auto accept calls);
+ * so successive calls never reuse normals or Exp(1) variables, and two blockings drawn in one
+ * iteration get independent streams.  Counter value k maps to the key
+ * (iter = k mod 2^32, salt = DMT_SALT_LIMIT + k div 2^32): auto streams never meet explicit
+ * ones.  The counter starts at 0 on dmt_create; dmt_rng_counter / dmt_set_rng_counter read and
+ * restore it (checkpoint / resume). */
+#define DMT_RNG_AUTO 0xFFFFFFFFu
+#define DMT_SALT_LIMIT 0x40000000u
+
 /* ---------------- lifetime (SamplingEnsemble / SamplingPair containers) ---------------- */
 
 /* Allocates the device containers of a SamplingEnsemble (src/sampling_ensemble.jl:17-41):
@@ -302,6 +323,13 @@ dmt_status dmt_fetch_ll(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
 dmt_status dmt_mcmc_step(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int64_t mcmciter,
                          uint32_t salt, double* ll, double* ll_prop, int64_t* n_acc);
 
+/* fetch_ll over [b0, b1) of THIS rank only (BiBlock / BlockCollection level,
+ * src/biblock.jl:222, src/block_collection.jl:144,156): no collective even when a
+ * communicator is set.  dmt_fetch_ll with a communicator is the BlockEnsemble-level reduction
+ * (src/block_ensemble.jl:140,152) and must be entered by every rank. */
+dmt_status dmt_fetch_ll_local(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
+                              int64_t mcmciter, double* ll, double* ll_prop, int64_t* n_acc);
+
 /* n_iter consecutive dmt_mcmc_step iterations (mcmciter = iter0 … iter0+n_iter-1) queued
  * back to back on the device with no host synchronisation in between: the body of the
  * reference's sampling loop (docs/src/tutorials/biblock/smoothing.md:40-44, which pushes
@@ -324,6 +352,8 @@ dmt_status dmt_guiding_linear(int32_t d, const double* Bt, const double* beta,
 /* ---------------- multi-GPU (RCCL over xGMI) ---------------- */
 dmt_status dmt_comm_unique_id(uint8_t* id_out /*128 bytes*/);
 dmt_status dmt_comm_init(dmt_ens* h, int32_t nranks, int32_t rank, const uint8_t* id);
+/* ranks of the handle's communicator as RCCL reports them (ncclCommCount), 1 without one */
+dmt_status dmt_comm_size(dmt_ens* h, int32_t* nranks);
 /* Declare this handle a shard of a larger SamplingEnsemble: its local segment 0 is global
  * segment seg_base.  Device RNG streams are keyed by global segment ids, so a sharded
  * ensemble draws exactly the normals / Exp(1) variables of the unsharded one (weak-scaling
@@ -359,6 +389,10 @@ dmt_status dmt_snapshot_take(dmt_ens* h, int32_t unit, int64_t slot, int64_t mcm
 dmt_status dmt_snapshot_download(dmt_ens* h, int32_t what, int64_t slot, double* out,
                                  int64_t* mcmciter);
 dmt_status dmt_snapshot_write(dmt_ens* h, const char* path, int64_t s0, int64_t s1);
+
+/* ---------------- random stream counter (DMT_RNG_AUTO) ---------------- */
+dmt_status dmt_rng_counter(dmt_ens* h, uint64_t* next);
+dmt_status dmt_set_rng_counter(dmt_ens* h, uint64_t next);
 
 /* ---------------- misc ---------------- */
 dmt_status dmt_sync(dmt_ens* h);

@@ -739,6 +739,13 @@ double orc_exp1(uint64_t seed, uint32_t blk, uint32_t iter, uint32_t salt) {
     return -rng_log(u);
 }
 
+/* orc_exp1 of blocks whose first segments are g0, g0 + 1, …, g0 + n - 1 (single-segment
+ * blocks: the timed CPU baseline's MH decisions), out[n] */
+void orc_exp1_range(uint64_t seed, uint32_t g0, int64_t n, uint32_t iter, uint32_t salt,
+                    double* out) {
+    for (int64_t i = 0; i < n; ++i) out[i] = orc_exp1(seed, g0 + (uint32_t)i, iter, salt);
+}
+
 /* raw Philox block, for bit-exact checks of the device generator */
 void orc_philox_raw(uint64_t seed, const uint32_t* ctr, uint32_t* out) {
     uint32_t c[4] = {ctr[0], ctr[1], ctr[2], ctr[3]};

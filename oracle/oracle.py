@@ -117,6 +117,8 @@ def _load():
     lib.orc_normal_pair_f64.restype = None
     lib.orc_exp1.argtypes = [u64, u32, u32, u32]
     lib.orc_exp1.restype = d_
+    lib.orc_exp1_range.argtypes = [u64, u32, C.c_int64, u32, u32, C.c_void_p]
+    lib.orc_exp1_range.restype = None
     lib.orc_set_sequential_ou.argtypes = [i_]
     lib.orc_set_sequential_ou.restype = None
     lib.orc_backward_filter_segment.argtypes = [i_, P, P, P, i_, P, P, P, d_, P, P, P]
@@ -245,6 +247,14 @@ def exp1(seed, blk, it, salt):
     return lib.orc_exp1(seed, blk, it & 0xFFFFFFFF, salt)
 
 
+def exp1_range(seed, g0, n, it, salt):
+    """exp1 of the blocks whose first segments are g0 … g0 + n - 1."""
+    out = np.empty(int(n))
+    lib.orc_exp1_range(C.c_uint64(seed), C.c_uint32(g0), C.c_int64(n), C.c_uint32(it & 0xFFFFFFFF),
+                       C.c_uint32(salt), _p(out))
+    return out
+
+
 def philox_raw(seed, ctr):
     ctr = np.ascontiguousarray(ctr, dtype=np.uint32).reshape(-1, 4)
     out = np.empty_like(ctr)
@@ -338,6 +348,17 @@ class _Block:
         self.acc_hist = np.zeros(hist_len, dtype=bool)
 
 
+# Device random stream keys (include/dmt.h, "device random streams"): salt = RNG_AUTO takes the
+# handle's stream counter k instead of the caller's (iter, salt), mapped to
+# (k mod 2^32, SALT_LIMIT + k div 2^32).
+RNG_AUTO = 0xFFFFFFFF
+SALT_LIMIT = 0x40000000
+
+
+def auto_key(k):
+    return k & 0xFFFFFFFF, SALT_LIMIT + ((k >> 32) & (SALT_LIMIT - 1))
+
+
 class OracleEnsemble:
     """Restatement of SamplingEnsemble + BlockEnsemble semantics on reference-layout data.
     Mirrors the libdmt call surface (diffusionmcmctools.jl_amd/engine.py) so tests can drive
@@ -367,6 +388,8 @@ class OracleEnsemble:
             U_.PPb = [None] * self.G
         self.layouts = []
         self.seg_base = 0  # dmt_set_shard
+        # RNG_AUTO counter: next key, the key of the last auto draw, armed for one auto accept
+        self.rng_ctr, self.rng_last, self.rng_pending = 0, 0, False
         # internal layout 0: whole recordings, terminal, rho 0 (draw_proposal_path!(u))
         self.create_layout([1] * self.R, [0] * self.R, [n - 1 for n in self.nseg], [1] * self.R,
                            [0.0] * self.R, 0)
@@ -442,6 +465,37 @@ class OracleEnsemble:
         self.layouts.append(blocks)
         return len(self.layouts) - 1
 
+    # ---- stream keys: the reference's draws take no key (global RNG, src/biblock.jl:94-99,122);
+    # RNG_AUTO restates that with a per-handle counter, exactly as libdmt's draw_key/accept_key
+    def _draw_key(self, it, salt, arm):
+        if salt != RNG_AUTO:
+            if salt >= SALT_LIMIT:
+                raise ValueError("salt must be < SALT_LIMIT")
+            return it, salt
+        k = self.rng_ctr
+        self.rng_ctr += 1
+        self.rng_last, self.rng_pending = k, arm
+        return auto_key(k)
+
+    def _accept_key(self, mcmciter, salt):
+        if salt != RNG_AUTO:
+            if salt >= SALT_LIMIT:
+                raise ValueError("salt must be < SALT_LIMIT")
+            return mcmciter, salt
+        if self.rng_pending:
+            k = self.rng_last
+        else:
+            k = self.rng_ctr
+            self.rng_ctr += 1
+        self.rng_pending = False
+        return auto_key(k)
+
+    def rng_counter(self):
+        return self.rng_ctr
+
+    def set_rng_counter(self, v):
+        self.rng_ctr, self.rng_pending = int(v), False
+
     # ---- the hot path, restated
     def _Zseg(self, Z, g, it, salt):
         n = self.npts[g] - 1
@@ -492,6 +546,7 @@ class OracleEnsemble:
     def draw_unit(self, unit, r0=0, r1=None, Z=None, iter=0, salt=0):
         """draw_proposal_path!(u::SamplingUnit), src/sampling_unit.jl:118-120."""
         r1 = self.R if r1 is None else r1
+        iter, salt = self._draw_key(iter, salt, False)
         lls, oks = [], []
         for r in range(r0, r1):
             bk = self.layouts[0][r]
@@ -503,6 +558,10 @@ class OracleEnsemble:
     def draw_proposal(self, layout, b0, b1, Z=None, iter=0, salt=0, want_success=False):
         """draw_proposal_path!(bb::BiBlock), src/biblock.jl:78-106: proposal drawn under the
         ACCEPTED law bb.b.PP into bb.b°, starting at bb.b.XX[1].x[1]."""
+        iter, salt = self._draw_key(iter, salt, True)
+        return self._draw(layout, b0, b1, Z, iter, salt, want_success)
+
+    def _draw(self, layout, b0, b1, Z, iter, salt, want_success=False):
         oks = []
         for bk in self.layouts[layout][b0:b1]:
             bk.llp, ok = self._solve_block(bk, 0, 0, 0, 1, "pcn", Z, iter, salt)
@@ -511,10 +570,14 @@ class OracleEnsemble:
 
     def accept_reject(self, layout, b0, b1, mcmciter, E=None, salt=0, want_acc=False):
         """accept_reject_proposal_path!(bb, i), src/biblock.jl:121-127."""
+        kit, ksalt = self._accept_key(mcmciter, salt)
+        return self._accept(layout, b0, b1, mcmciter, E, kit, ksalt, want_acc)
+
+    def _accept(self, layout, b0, b1, mcmciter, E, kit, ksalt, want_acc):
         accs = []
         for j, bk in enumerate(self.layouts[layout][b0:b1]):
             e = (float(E[j]) if E is not None
-                 else exp1(self.seed, bk.g0 + self.seg_base, mcmciter, salt))
+                 else exp1(self.seed, bk.g0 + self.seg_base, kit, ksalt))
             acc = e > -(bk.llp - bk.ll)
             if acc:  # swap_paths!: XX and WW element swaps (src/biblock.jl:148-173)
                 for g in range(bk.g0, bk.g1 + 1):
@@ -731,7 +794,34 @@ class OracleEnsemble:
                 h = {2: "ll_hist", 3: "llp_hist", 4: "acc_hist"}[what]
                 getattr(b, h)[...] = v[:, j]
 
-    def fetch_ll(self, layout, b0, b1, mcmciter=0):
+    def mcmc_step(self, layout, b0, b1, mcmciter, salt=0):
+        """dmt_mcmc_step: draw + accept with ONE key (disjoint normal / Exp(1) streams)."""
+        it, ks = self._draw_key(mcmciter, salt, False)
+        self._draw(layout, b0, b1, None, it, ks)
+        self._accept(layout, b0, b1, mcmciter, None, it, ks, False)
+        return self.fetch_ll(layout, b0, b1, mcmciter)
+
+    def mcmc_run(self, layout, b0, b1, iter0, n_iter, salt=0):
+        """dmt_mcmc_run: iteration it keyed by it (explicit) or by n_iter consecutive counter
+        values that do not straddle a 2^32 boundary (RNG_AUTO)."""
+        delta, ks = 0, salt
+        if salt == RNG_AUTO:
+            base = self.rng_ctr
+            if (base & 0xFFFFFFFF) + n_iter > 1 << 32:
+                base = (base | 0xFFFFFFFF) + 1
+            self.rng_ctr, self.rng_pending = base + n_iter, False
+            ks = auto_key(base)[1]
+            delta = (base & 0xFFFFFFFF) - iter0
+        out = np.empty((n_iter, 3))
+        for i in range(n_iter):
+            it = iter0 + i
+            key = (it + delta) & 0xFFFFFFFF
+            self._draw(layout, b0, b1, None, key, ks)
+            self._accept(layout, b0, b1, it, None, key, ks, False)
+            out[i] = self.fetch_ll(layout, b0, b1, it)
+        return out
+
+    def fetch_ll(self, layout, b0, b1, mcmciter=0, local=False):
         bks = self.layouts[layout][b0:b1]
         a = pairwise_tree([b.ll for b in bks])
         p = pairwise_tree([b.llp for b in bks])
