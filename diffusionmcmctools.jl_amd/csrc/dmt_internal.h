@@ -199,8 +199,9 @@ constexpr int64_t kFiltBatchPoints = int64_t(1) << 24;
 // k_filter_scan + k_filter_chain (every chunk in parallel, a short serial chain per block)
 constexpr int64_t kFiltFusedBlocks = 4096;
 constexpr int kResidentMaxSteps = 512;
-// part: [n_iter][3][nwaves] block partials followed by [n_iter][3][ceil(nwaves / WPB)] tree
-// nodes (WPB ≤ 4); out3[n_iter][3]: every iteration's fetch_ll; counter: a zeroed uint32
+// part: [n_iter][3][nwaves] block partials followed by the tree nodes ([3 n_iter][ceil(nwaves /
+// WPB)] then [3 n_iter][ceil(nwaves / (16 WPB))], WPB ≤ 4); out3[n_iter][3]: every iteration's
+// fetch_ll; counter: ceil(nwaves / (16 WPB)) + 1 zeroed uint32 arrival counters (left zero)
 hipError_t launch_mcmc_persistent(const ModelKey& k, const void* args, const AcceptArgs& c,
                                   int64_t iter0, int64_t n_iter, double* part, int64_t nwaves,
                                   int resident, double* out3, unsigned* counter, hipStream_t s);

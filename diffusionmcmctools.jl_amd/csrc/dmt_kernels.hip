@@ -642,11 +642,51 @@ __global__ __launch_bounds__(64) void k_pathll(const BlockArgs<T> a) {
 //   phase B (lane-parallel): lane j evaluates G(t_j, x_j)·dt_j, a 64-lane adjacent-pair
 //            xor-shuffle tree gives the chunk sum (= the canonical chunk tree), and every
 //            lane stores its point: coalesced writes of the path.
+// Cross-lane moves of the adjacent-pair trees: DPP for partners within a 16-lane row (no LDS
+// round trip), ds_swizzle for lane ^ 16, ds_bpermute for lane ^ 32.
+template <int CTRL, class T>
+__device__ __forceinline__ T dpp_mov(T v) {
+  if constexpr (sizeof(T) == 8) {
+    int2 p = __builtin_bit_cast(int2, v);
+    p.x = __builtin_amdgcn_mov_dpp(p.x, CTRL, 0xF, 0xF, false);
+    p.y = __builtin_amdgcn_mov_dpp(p.y, CTRL, 0xF, 0xF, false);
+    return __builtin_bit_cast(T, p);
+  } else {
+    return __builtin_bit_cast(T, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF,
+                                                          0xF, false));
+  }
+}
+template <int PATTERN, class T>
+__device__ __forceinline__ T swizzle_mov(T v) {
+  if constexpr (sizeof(T) == 8) {
+    int2 p = __builtin_bit_cast(int2, v);
+    p.x = __builtin_amdgcn_ds_swizzle(p.x, PATTERN);
+    p.y = __builtin_amdgcn_ds_swizzle(p.y, PATTERN);
+    return __builtin_bit_cast(T, p);
+  } else {
+    return __builtin_bit_cast(T, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, v), PATTERN));
+  }
+}
+// Adjacent-pair tree over every aligned group of G lanes (G = 2 … 64, a power of two), whole
+// wave active: afterwards each lane holds its group's sum, formed exactly as the xor-butterfly
+// v + v[lane ^ off], off = 1, 2, …, G/2 (each level adds a lane's partial to its partner's;
+// IEEE addition is commutative, so every lane's value is the canonical tree's).  Level 4 and 8
+// read the mirrored lane (row_half_mirror, row_mirror): after the lower levels it holds the
+// partner's partial.
+template <int G, class T>
+__device__ __forceinline__ T group_tree_sum(T v) {
+  static_assert(G >= 2 && G <= 64 && (G & (G - 1)) == 0, "G: power of two in [2, 64]");
+  v = v + dpp_mov<0xB1>(v);                                   // quad_perm(1,0,3,2): lane ^ 1
+  if constexpr (G >= 4) v = v + dpp_mov<0x4E>(v);             // quad_perm(2,3,0,1): lane ^ 2
+  if constexpr (G >= 8) v = v + dpp_mov<0x141>(v);            // row_half_mirror
+  if constexpr (G >= 16) v = v + dpp_mov<0x140>(v);           // row_mirror
+  if constexpr (G >= 32) v = v + swizzle_mov<0x401F>(v);      // lane ^ 16 (xor mode)
+  if constexpr (G >= 64) v = v + __shfl_xor(v, 32, 64);       // lane ^ 32
+  return v;
+}
 template <class T>
 __device__ __forceinline__ T wave_tree_sum(T v) {
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) v = v + __shfl_xor(v, off, 64);
-  return v;
+  return group_tree_sum<64, T>(v);
 }
 
 // ---- MAP_WAVE block kernel: a 2-wave workgroup per block, software-pipelined by chunk.
@@ -1275,9 +1315,7 @@ __device__ __forceinline__ void scan_block(const BlockArgs<T>& a, const int64_t 
         gk[k] = v ? G * dt : (T)0;
       }
 #pragma unroll
-      for (int off = 1; off < 64; off <<= 1)
-#pragma unroll
-        for (int k = 0; k < kRun; ++k) gk[k] = gk[k] + __shfl_xor(gk[k], off, 64);
+      for (int k = 0; k < kRun; ++k) gk[k] = wave_tree_sum<T>(gk[k]);
 #pragma unroll
       for (int k = 0; k < kRun; ++k)
         if (64 * k < cnt) seg_acc = seg_acc + (wave_uniform(gk[k]) + (T)0);  // uniform
@@ -1321,29 +1359,60 @@ __global__ __launch_bounds__((64 * ScanCfg<Mdl::D, T>::WPB), 1) void k_block_sca
 }
 
 // The fetch_ll trees of every iteration of a persistent run, formed inside the launch (no
-// separate tree launch): (1) each workgroup folds, for every (iteration, component) row of
-// part[n_iter][3][nb], its WPB consecutive leaves (the blocks of its waves) into the node of the
-// canonical tree one log2(WPB) levels up; (2) the last workgroup to finish (device-scope arrival
-// counter) folds every row's nodes — a wave per row, each lane an aligned run of nodes, then the
-// 64-lane adjacent-pair tree.  That is the complete adjacent-pair tree over the zero-padded
-// blocks of launch_block_sum (padding further with zeros changes nothing but
-// the sign of a zero, and the ll sums are canonicalised with + 0.0).
-// Hand-off without a release fence (an agent-scope release writes back the XCD L2's dirty
-// lines — here the run's paths, ≈35 µs per launch measured): the nodes are stored write-through
-// (relaxed agent-scope atomic stores, sc1), every storing wave drains its stores, one lane per
-// workgroup adds to the arrival counter (agent-scope atomic) after a workgroup barrier, and the
-// last arriver — told by the value its add returned — reads the nodes with sc1 loads
+// separate tree launch), as the complete adjacent-pair tree over the zero-padded blocks of
+// launch_block_sum (padding further with zeros changes nothing but the sign of a zero, and the
+// ll sums are canonicalised with + 0.0), in three levels over the rows (iteration, component)
+// of part[n_iter][3][nb]:
+//   1. every workgroup folds its WPB consecutive leaves (the blocks of its waves) → node1;
+//   2. the last workgroup to finish of each group of kTreeGroup workgroups (an arrival counter
+//      per group) folds the group's node1s → node2 (16-lane DPP trees, all rows at once);
+//   3. the last group to finish (one more counter) folds every row's node2s → out3.
+// Levels 2-3 run on the workgroups that arrive last, so the reads of other CUs' nodes are
+// spread over the groups instead of one CU reading them all.  Hand-offs without a release
+// fence (an agent-scope release writes back the XCD L2's dirty lines — here the run's paths:
+// ≈25 µs per 20-iteration C2 launch measured): nodes are stored write-through (relaxed
+// agent-scope atomic stores, sc1), every storing wave drains its stores, one lane per workgroup
+// adds to the arrival counter (agent-scope atomic) after a workgroup barrier, and the last
+// arriver — told by the value its add returned — reads the nodes with sc1 loads
 // (MI355X_MICROARCH.md, inter-workgroup visibility: one workgroup per CU, hipMalloc memory).
+constexpr int kTreeGroup = 16;
+
+__device__ __forceinline__ double ld_sc1(const double* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// drain this wave's stores, join the workgroup, one lane adds to *cnt; true in every thread of
+// the workgroup whose add completed the count `expect`
+__device__ __forceinline__ bool arrive_last(unsigned* cnt, unsigned expect, int* s_flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    *s_flag = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                      expect - 1 ? 1 : 0;
+  __syncthreads();
+  return *s_flag != 0;
+}
+
+// nodes: node1 [rows][ng] then node2 [rows][ng2]; counters: [ng2] group counters then the top
+// counter, zero on entry and left zero
 template <int WPB>
 __device__ __forceinline__ void persistent_tree_tail(const double* __restrict__ part,
                                                      double* __restrict__ nodes, int64_t nb,
-                                                     int64_t n_iter, unsigned* __restrict__ counter,
+                                                     int64_t n_iter,
+                                                     unsigned* __restrict__ counters,
                                                      double* __restrict__ out3) {
-  __shared__ int s_last;
+  __shared__ int s_flag;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int64_t ng = (nb + WPB - 1) / WPB, x = blockIdx.x, rows = 3 * n_iter;
+  constexpr int NT = 64 * WPB;
+  const int64_t ng = (nb + WPB - 1) / WPB, ng2 = (ng + kTreeGroup - 1) / kTreeGroup;
+  const int64_t x = blockIdx.x, g = x / kTreeGroup, rows = 3 * n_iter;
+  double* node1 = nodes;
+  double* node2 = nodes + rows * ng;
+  // ---- level 1: this workgroup's leaves
   __syncthreads();  // every wave's part[] stores of the run are done
-  for (int64_t row = tid; row < rows; row += 64 * WPB) {
+  for (int64_t row = tid; row < rows; row += NT) {
     double v[WPB];
 #pragma unroll
     for (int k = 0; k < WPB; ++k) {
@@ -1354,45 +1423,55 @@ __device__ __forceinline__ void persistent_tree_tail(const double* __restrict__ 
     for (int w = WPB; w > 1; w >>= 1)
 #pragma unroll
       for (int k = 0; k < w / 2; ++k) v[k] = v[2 * k] + v[2 * k + 1];
-    __hip_atomic_store(&nodes[row * ng + x], v[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    st_sc1(&node1[row * ng + x], v[0]);
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
-  __syncthreads();
-  if (tid == 0)
-    s_last = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                     gridDim.x - 1 ? 1 : 0;
-  __syncthreads();
-  if (!s_last) return;
-  int64_t P = 1;
-  while (P < ng) P <<= 1;
-  const int64_t run = P > 64 ? P / 64 : 1;
-  if (run <= 4) {
-    // ≤ 256 nodes per row: a batch of RB rows' loads in flight per lane, then the folds
-    constexpr int RB = 8;
+  const int64_t gsize = ng - g * kTreeGroup < kTreeGroup ? ng - g * kTreeGroup : kTreeGroup;
+  if (!arrive_last(&counters[g], (unsigned)gsize, &s_flag)) return;
+  // ---- level 2: group g's nodes, 16 lanes per row, NT/16 rows per pass, U passes in flight
+  {
+    constexpr int RPP = NT / kTreeGroup, U = 8;
+    const int k = tid % kTreeGroup;
+    const int64_t col = g * kTreeGroup + k;
+    for (int64_t r0 = 0; r0 < rows; r0 += (int64_t)RPP * U) {
+      double v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t row = r0 + (int64_t)u * RPP + tid / kTreeGroup;
+        v[u] = (row < rows && col < ng) ? ld_sc1(&node1[row * ng + col]) : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        v[u] = group_tree_sum<kTreeGroup, double>(v[u]);
+        const int64_t row = r0 + (int64_t)u * RPP + tid / kTreeGroup;
+        if (k == 0 && row < rows) st_sc1(&node2[row * ng2 + g], v[u]);
+      }
+    }
+  }
+  if (tid == 0) __hip_atomic_store(&counters[g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (!arrive_last(&counters[ng2], (unsigned)ng2, &s_flag)) return;
+  // ---- level 3: every row's group nodes, zero-padded
+  if (ng2 <= 64) {
+    constexpr int RB = 8;  // rows per wave per batch (loads in flight)
     for (int64_t r0 = (int64_t)wv * RB; r0 < rows; r0 += (int64_t)WPB * RB) {
-      double v[RB][4];
-#pragma unroll
-      for (int b = 0; b < RB; ++b)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int64_t row = r0 + b, nd = (int64_t)lane * run + k;
-          v[b][k] = (k < run && row < rows && nd < ng)
-                        ? __hip_atomic_load(&nodes[row * ng + nd], __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_AGENT)
-                        : 0.0;
-        }
+      double v[RB];
 #pragma unroll
       for (int b = 0; b < RB; ++b) {
-        // aligned run of `run` ≤ 4 nodes (the zero slots past it are not part of the fold)
-        double f = run == 1 ? v[b][0]
-                 : run == 2 ? v[b][0] + v[b][1]
-                            : (v[b][0] + v[b][1]) + (v[b][2] + v[b][3]);
-        f = wave_tree_sum<double>(f);
         const int64_t row = r0 + b;
-        if (lane == 0 && row < rows) out3[row] = (row % 3 == 2) ? f : f + 0.0;
+        v[b] = (row < rows && lane < ng2) ? ld_sc1(&node2[row * ng2 + lane]) : 0.0;
+      }
+#pragma unroll
+      for (int b = 0; b < RB; ++b) {
+        const double t = wave_tree_sum<double>(v[b]);
+        const int64_t row = r0 + b;
+        if (lane == 0 && row < rows) out3[row] = (row % 3 == 2) ? t : t + 0.0;
       }
     }
   } else {
+    // very many blocks: each lane folds an aligned run of the padded node2 row (binary
+    // counter), then the 64-lane tree
+    int64_t P = 64;
+    while (P < ng2) P <<= 1;
+    const int64_t run = P / 64;
     constexpr int kLv = 24;
     for (int64_t row = wv; row < rows; row += WPB) {
       double stk[kLv];
@@ -1401,9 +1480,7 @@ __device__ __forceinline__ void persistent_tree_tail(const double* __restrict__ 
       double acc = 0.0;
       for (int64_t k = 0; k < run; ++k) {
         const int64_t nd = (int64_t)lane * run + k;
-        double xv = nd < ng ? __hip_atomic_load(&nodes[row * ng + nd], __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT)
-                            : 0.0;
+        double xv = nd < ng2 ? ld_sc1(&node2[row * ng2 + nd]) : 0.0;
         bool carry = true;
 #pragma unroll
         for (int l = 0; l < kLv; ++l) {
@@ -1422,7 +1499,7 @@ __device__ __forceinline__ void persistent_tree_tail(const double* __restrict__ 
   }
   __syncthreads();
   if (tid == 0)  // ready for the next launch (stream-ordered)
-    __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&counters[ng2], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // dmt_mcmc_run for linear drifts: n_iter path-MCMC iterations in ONE launch.  Blocks are
@@ -1727,9 +1804,7 @@ __device__ __forceinline__ void resident_block(const BlockArgs<T>& a, const Acce
 #pragma unroll
     for (int p = 0; p < D; ++p) xe[p] = lane_read(x[p], 4 * last_lane);
     T tsum = ((gl[0] + gl[1]) + (gl[2] + gl[3])) + ((gl[4] + gl[5]) + (gl[6] + gl[7]));
-    tsum = tsum + __shfl_xor(tsum, 1, 64);
-    tsum = tsum + __shfl_xor(tsum, 2, 64);
-    tsum = tsum + __shfl_xor(tsum, 4, 64);
+    tsum = group_tree_sum<8, T>(tsum);
     T seg_acc = (T)0;
 #pragma unroll
     for (int q = 0; q < 8; ++q)
@@ -1818,8 +1893,13 @@ __global__ __launch_bounds__(256, 1) void k_mcmc_resident(const BlockArgs<T> a,
   __shared__ ResLds<Mdl::D, Mdl::M, T> lds[4];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t blk = a.b0 + (int64_t)blockIdx.x * 4 + w;
+#ifdef DMT_VARIANT_EARLY_RETURN  // measurement variant: no in-kernel trees (out3 not written)
+  if (blk >= a.b1) return;
+  resident_block<Mdl, T, MODE_PCN, true>(a, c, iter0, n_iter, part, blk, lds[w]);
+#else
   if (blk < a.b1) resident_block<Mdl, T, MODE_PCN, true>(a, c, iter0, n_iter, part, blk, lds[w]);
   persistent_tree_tail<4>(part, nodes, a.b1 - a.b0, n_iter, counter, out3);
+#endif
 }
 
 // One draw / re-solve (dmt_draw_proposal, dmt_draw_unit, dmt_recompute_path) of single-segment
@@ -1953,24 +2033,18 @@ __global__ __launch_bounds__(1024) void k_accept_reduce(const AcceptArgs a, doub
     v1 = llp;
     v2 = acc ? 1.0 : 0.0;
   }
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    v0 = v0 + __shfl_xor(v0, off, 64);
-    v1 = v1 + __shfl_xor(v1, off, 64);
-    v2 = v2 + __shfl_xor(v2, off, 64);
-  }
+  v0 = wave_tree_sum<double>(v0);
+  v1 = wave_tree_sum<double>(v1);
+  v2 = wave_tree_sum<double>(v2);
   if (lane == 0) { w0[wv] = v0; w1[wv] = v1; w2[wv] = v2; }
   __syncthreads();
   if (wv == 0) {
     v0 = lane < 16 ? w0[lane] : 0.0;
     v1 = lane < 16 ? w1[lane] : 0.0;
     v2 = lane < 16 ? w2[lane] : 0.0;
-#pragma unroll
-    for (int off = 1; off < 16; off <<= 1) {
-      v0 = v0 + __shfl_xor(v0, off, 64);
-      v1 = v1 + __shfl_xor(v1, off, 64);
-      v2 = v2 + __shfl_xor(v2, off, 64);
-    }
+    v0 = group_tree_sum<16, double>(v0);
+    v1 = group_tree_sum<16, double>(v1);
+    v2 = group_tree_sum<16, double>(v2);
     if (lane == 0) {
       if (nout == 1) {
         out3[0] = v0 + 0.0;
@@ -2841,24 +2915,18 @@ __global__ __launch_bounds__(1024) void k_tree_level(const double* __restrict__ 
       v2 = a0[2 * n + i];
     }
   }
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    v0 = v0 + __shfl_xor(v0, off, 64);
-    v1 = v1 + __shfl_xor(v1, off, 64);
-    v2 = v2 + __shfl_xor(v2, off, 64);
-  }
+  v0 = wave_tree_sum<double>(v0);
+  v1 = wave_tree_sum<double>(v1);
+  v2 = wave_tree_sum<double>(v2);
   if (lane == 0) { w0[wv] = v0; w1[wv] = v1; w2[wv] = v2; }
   __syncthreads();
   if (wv == 0) {
     v0 = lane < 16 ? w0[lane] : 0.0;
     v1 = lane < 16 ? w1[lane] : 0.0;
     v2 = lane < 16 ? w2[lane] : 0.0;
-#pragma unroll
-    for (int off = 1; off < 16; off <<= 1) {
-      v0 = v0 + __shfl_xor(v0, off, 64);
-      v1 = v1 + __shfl_xor(v1, off, 64);
-      v2 = v2 + __shfl_xor(v2, off, 64);
-    }
+    v0 = group_tree_sum<16, double>(v0);
+    v1 = group_tree_sum<16, double>(v1);
+    v2 = group_tree_sum<16, double>(v2);
     if (lane == 0) {
       out[blockIdx.x] = v0;
       out[nout + blockIdx.x] = v1;

@@ -154,6 +154,8 @@ struct dmt_ens {
   double* h_red = nullptr;  // pinned host copy of the 3 reduction results
   double* d_gather = nullptr;
   double* d_run = nullptr;         // dmt_mcmc_run: [n][3] per-iteration reductions
+  double* h_run = nullptr;         // pinned host [run_cap][3]: one rank's results, written by
+                                   // the kernels directly (no device-to-host copy)
   double* d_run_gather = nullptr;  // [n][nranks][3] (persistent path: [nranks][n][3])
   int64_t run_cap = 0;
   double* d_part = nullptr;  // k_mcmc_scan per-iteration block partials [n][3][nb]
@@ -607,6 +609,11 @@ dmt_status dmt_create(dmt_ens** out, const dmt_model* model, const dmt_structure
     return fail(DMT_ERR_HIP, "no HIP device available: libdmt has no CPU fallback");
   if (cfg->device < 0 || cfg->device >= ndev) return fail(DMT_ERR_INVALID, "bad device ordinal");
   HIP_OK(hipSetDevice(cfg->device));
+  // DMT_SYNC_SPIN=1: host threads spin (not sleep) in stream synchronisation — lower wake-up
+  // latency for short calls.  A process-wide device flag, honoured only before the device's
+  // context exists; a failure (context already created) is ignored.
+  if (const char* e = std::getenv("DMT_SYNC_SPIN"); e && e[0] == '1')
+    (void)hipSetDeviceFlags(hipDeviceScheduleSpin);
   auto h = std::make_unique<dmt_ens>();
   h->key = ModelKey{model->model, model->precision, model->d, model->m};
   h->d = model->d;
@@ -754,6 +761,7 @@ dmt_status dmt_destroy(dmt_ens* h) {
     if (h->d_snap[k]) (void)hipFree(h->d_snap[k]);
   if (h->comm) (void)ncclCommDestroy(h->comm);
   if (h->h_red) (void)hipHostFree(h->h_red);
+  if (h->h_run) (void)hipHostFree(h->h_run);
   (void)hipStreamDestroy(h->stream);
   delete h;
   return DMT_OK;
@@ -1167,6 +1175,7 @@ dmt_status dmt_mcmc_run(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int6
   const bool multi = h->comm != nullptr;
   if (n_iter > h->run_cap) {
     if (h->d_run) { (void)hipFree(h->d_run); h->bytes -= h->run_cap * 24; h->d_run = nullptr; }
+    if (h->h_run) { (void)hipHostFree(h->h_run); h->h_run = nullptr; }
     if (h->d_run_gather) {
       (void)hipFree(h->d_run_gather);
       h->bytes -= h->run_cap * 24 * h->nranks;
@@ -1175,12 +1184,21 @@ dmt_status dmt_mcmc_run(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int6
     const int64_t cap = grown_cap(n_iter, h->run_cap, 4096);
     h->run_cap = 0;
     DMT_TRY(ens_alloc(h, &h->d_run, 3 * cap));
+    HIP_OK(hipHostMalloc((void**)&h->h_run, 3 * cap * sizeof(double), hipHostMallocDefault));
     if (multi) DMT_TRY(ens_alloc(h, &h->d_run_gather, 3 * cap * h->nranks));
     h->run_cap = cap;
   } else if (multi && !h->d_run_gather) {
     DMT_TRY(ens_alloc(h, &h->d_run_gather, 3 * h->run_cap * h->nranks));
   }
   DMT_TRY(ensure_red_work(h, b1 - b0));
+  // per-iteration results: one rank → straight into pinned host memory; several → device
+  // memory for the all-gather
+  double* run_out = h->d_run;
+  if (!multi) {
+    void* dp = nullptr;
+    HIP_OK(hipHostGetDevicePointer(&dp, h->h_run, 0));
+    run_out = static_cast<double*>(dp);
+  }
   const int64_t nb = b1 - b0;
   bool persist = h->persist && h->key.model == DMT_MODEL_OU;
   for (int64_t b = b0; b < b1 && persist; ++b)
@@ -1193,12 +1211,15 @@ dmt_status dmt_mcmc_run(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int6
     // every iteration's fetch_ll tree formed inside the launch
     const int64_t chunk_max = std::max<int64_t>(1, (int64_t(64) << 20) / (24 * nb));
     const int64_t chunk = std::min<int64_t>(n_iter, chunk_max);
-    const int64_t ngroups = nb;  // ≥ the tree nodes the kernel folds its blocks into (nb / WPB)
-    const int64_t need = 3 * nb * chunk + 3 * ngroups * chunk + 8;
+    // part [chunk][3][nb], then the tree nodes (node1 [3 chunk][≤ nb], node2 [3 chunk][≤ nb/16 + 1]),
+    // then the arrival counters (≤ nb/16 + 2 uint32) at the end of the buffer
+    const int64_t cnt_words = nb / 2 + 8;  // doubles
+    auto need_for = [&](int64_t it) { return 3 * it * (2 * nb + nb / 16 + 1) + cnt_words; };
+    const int64_t need = need_for(chunk);
     if (need > h->part_cap) {
       if (h->d_part) { (void)hipFree(h->d_part); h->bytes -= h->part_cap * 8; h->d_part = nullptr; }
       const int64_t cap_it = std::min(chunk_max, std::max<int64_t>(chunk, 256));
-      const int64_t cap = std::max(need, 3 * nb * cap_it + 3 * ngroups * cap_it + 8);
+      const int64_t cap = std::max(need, need_for(cap_it));
       h->part_cap = 0;
       DMT_TRY(ens_alloc(h, &h->d_part, cap));
       HIP_OK(hipMemsetAsync(h->d_part, 0, cap * 8, h->stream));  // zero the arrival counter
@@ -1221,18 +1242,18 @@ dmt_status dmt_mcmc_run(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int6
           a.wd_flip = 1;
           a.salt = salt;
         };
-        // d_part: [part_cap - 8, part_cap) holds the arrival counter of the in-kernel tree
-        double* counter = h->d_part + h->part_cap - 8;
+        // the arrival counters of the in-kernel trees: the last cnt_words doubles of d_part
+        double* counter = h->d_part + h->part_cap - cnt_words;
         if (h->key.precision == DMT_F64) {
           BlockArgs<double> a{};
           fill(a);
           e = launch_mcmc_persistent(h->key, &a, c, iter0 + i0, n, h->d_part, nb, resident,
-                                     h->d_run + 3 * i0, (unsigned*)counter, h->stream);
+                                     run_out + 3 * i0, (unsigned*)counter, h->stream);
         } else {
           BlockArgs<float> a{};
           fill(a);
           e = launch_mcmc_persistent(h->key, &a, c, iter0 + i0, n, h->d_part, nb, resident,
-                                     h->d_run + 3 * i0, (unsigned*)counter, h->stream);
+                                     run_out + 3 * i0, (unsigned*)counter, h->stream);
         }
       }
       if (e != hipSuccess) return fail(DMT_ERR_HIP, std::string("k_mcmc_scan: ") + hipGetErrorString(e));
@@ -1247,7 +1268,7 @@ dmt_status dmt_mcmc_run(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int6
       {
         TimedScope ts(h, DMT_K_ACCEPT);
         HIP_OK(launch_accept_reduce(accept_args(h, L, b0, b1, nullptr, it, key, nullptr),
-                                    h->d_red_work, h->d_red_lb, h->d_run + 3 * i, h->stream));
+                                    h->d_red_work, h->d_red_lb, run_out + 3 * i, h->stream));
       }
     }
   }
@@ -1261,8 +1282,8 @@ dmt_status dmt_mcmc_run(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int6
     return DMT_OK;
   }
   if (!multi) {
-    HIP_OK(hipMemcpyAsync(out, h->d_run, 24 * n_iter, hipMemcpyDeviceToHost, h->stream));
     HIP_OK(hipStreamSynchronize(h->stream));
+    std::memcpy(out, h->h_run, 24 * n_iter);
     return DMT_OK;
   }
   std::vector<double> all(3 * h->nranks * n_iter);

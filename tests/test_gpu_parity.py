@@ -222,6 +222,11 @@ def _ragged_ou_build(hist):
     pytest.param(("c2", 100, 60, 6), id="c2-60steps-resident"),
     pytest.param(("c2", 300, 500, 70), id="c2-500steps-resident-70iters"),
     pytest.param(("c2", 40, 1300, 4), id="c2-1300steps-persistent-multichunk"),
+    # the in-kernel fetch_ll tail: several LDS row batches; 8-node lane runs; the direct
+    # (binary-counter) path for many blocks
+    pytest.param(("c2", 1024, 500, 100), id="c2-full-100iters-tail-batches"),
+    pytest.param(("c2", 2048, 80, 12), id="c2-2048blocks-tail-run8"),
+    pytest.param(("c2", 4100, 40, 5), id="c2-4100blocks-tail-direct"),
     pytest.param(("c1", 1, 200, 5), id="c1-resident-d1"),
     pytest.param(("ragged", 0, 0, 5), id="ragged-ou-persistent-multisegment"),
 ])
