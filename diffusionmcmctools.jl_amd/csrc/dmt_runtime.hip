@@ -96,6 +96,7 @@ struct dmt_ens {
   // whether an auto accept may still take it
   uint64_t rng_ctr = 0, rng_last_draw = 0;
   bool rng_pending = false;
+  bool spin_wait = true;  // wait for the stream by polling it (DMT_SPIN_WAIT=0: block in HIP)
   int grid_shared = 0;
   // path snapshots (dmt_snapshot_*): [slots][P][C] doubles in reference layout per kind
   int snap_mask = 0;
@@ -185,6 +186,8 @@ struct dmt_ens {
 };
 
 namespace {
+
+hipError_t stream_wait(dmt_ens* h);
 
 template <class T>
 dmt_status ens_alloc(dmt_ens* h, T** p, int64_t n) {
@@ -301,6 +304,18 @@ dmt_status check_h(dmt_ens* h) {
   if (!h) return fail(DMT_ERR_INVALID, "null handle");
   if (hipSetDevice(h->device) != hipSuccess) return fail(DMT_ERR_HIP, "hipSetDevice failed");
   return DMT_OK;
+}
+
+// Wait for everything queued on the handle's stream by polling it from this thread
+// (DMT_SPIN_WAIT=0: block in hipStreamSynchronize).  On the driver's 20-iteration C2 run the two
+// measured within noise of each other (profiles/r02j); polling keeps the wake-up off the
+// scheduler for short calls.
+hipError_t stream_wait(dmt_ens* h) {
+  if (!h->spin_wait) return hipStreamSynchronize(h->stream);
+  for (;;) {
+    const hipError_t e = hipStreamQuery(h->stream);
+    if (e != hipErrorNotReady) return e;
+  }
 }
 
 // ---- stream keys (include/dmt.h, "device random streams")
@@ -609,12 +624,8 @@ dmt_status dmt_create(dmt_ens** out, const dmt_model* model, const dmt_structure
     return fail(DMT_ERR_HIP, "no HIP device available: libdmt has no CPU fallback");
   if (cfg->device < 0 || cfg->device >= ndev) return fail(DMT_ERR_INVALID, "bad device ordinal");
   HIP_OK(hipSetDevice(cfg->device));
-  // DMT_SYNC_SPIN=1: host threads spin (not sleep) in stream synchronisation — lower wake-up
-  // latency for short calls.  A process-wide device flag, honoured only before the device's
-  // context exists; a failure (context already created) is ignored.
-  if (const char* e = std::getenv("DMT_SYNC_SPIN"); e && e[0] == '1')
-    (void)hipSetDeviceFlags(hipDeviceScheduleSpin);
   auto h = std::make_unique<dmt_ens>();
+  h->spin_wait = !(std::getenv("DMT_SPIN_WAIT") && std::getenv("DMT_SPIN_WAIT")[0] == '0');
   h->key = ModelKey{model->model, model->precision, model->d, model->m};
   h->d = model->d;
   h->m = model->m;
@@ -738,7 +749,7 @@ dmt_status dmt_create(dmt_ens** out, const dmt_model* model, const dmt_structure
 dmt_status dmt_destroy(dmt_ens* h) {
   if (!h) return DMT_OK;
   (void)hipSetDevice(h->device);
-  (void)hipStreamSynchronize(h->stream);
+  (void)stream_wait(h);
   drain_timing(h);
   for (auto e : h->free_events) (void)hipEventDestroy(e);
   for (auto& L : h->layouts)
@@ -788,7 +799,7 @@ dmt_status dmt_upload_grid(dmt_ens* h, const double* t) {
     HIP_OK(launch_to_planes(h->key.precision, h->tw, h->d_stage, h->d_t, h->d_t, nullptr, 0, 1, h->P,
                             h->d_pt_off, h->G, h->d_seg_rec, h->d_seg_q, h->d_tile_qoff, h->stream));
   }
-  HIP_OK(hipStreamSynchronize(h->stream));
+  HIP_OK(stream_wait(h));
   h->have_t = true;
   return DMT_OK;
 }
@@ -886,7 +897,7 @@ dmt_status dmt_upload_law(dmt_ens* h, int32_t unit, int32_t kind, const double* 
       HIP_OK(hipGetLastError());
     }
   }
-  HIP_OK(hipStreamSynchronize(h->stream));
+  HIP_OK(stream_wait(h));
   if (H || F || laws) h->have_law[unit][kind] = true;
   return DMT_OK;
 }
@@ -906,7 +917,7 @@ dmt_status dmt_set_paths(dmt_ens* h, int32_t unit, const double* X, const double
                             h->P, h->d_pt_off, h->G, h->d_seg_rec, h->d_seg_q, h->d_tile_qoff,
                             h->stream, w == 1 ? 1 : 0));
   }
-  HIP_OK(hipStreamSynchronize(h->stream));
+  HIP_OK(stream_wait(h));
   return DMT_OK;
 }
 
@@ -926,7 +937,7 @@ dmt_status dmt_download_paths(dmt_ens* h, int32_t unit, int32_t what, double* ou
                                    unit, C, h->G, h->d_pt_off, h->d_seg_np, h->d_seg_rec, h->d_seg_q,
                                    h->d_tile_qoff, h->stream));
   HIP_OK(hipMemcpyAsync(out, h->d_stage, h->P * C * 8, hipMemcpyDeviceToHost, h->stream));
-  HIP_OK(hipStreamSynchronize(h->stream));
+  HIP_OK(stream_wait(h));
   return DMT_OK;
 }
 
@@ -951,7 +962,7 @@ dmt_status dmt_download_law(dmt_ens* h, int32_t unit, int32_t kind, double* H, d
                                 h->d_tile_qoff, h->stream));
       HIP_OK(hipMemcpyAsync(H, h->d_stage, h->P * h->hp * 8, hipMemcpyDeviceToHost, h->stream));
     }
-    HIP_OK(hipStreamSynchronize(h->stream));
+    HIP_OK(stream_wait(h));
   }
   if (F) {
     DMT_TRY(ensure_stage(h, h->P * h->d));
@@ -959,7 +970,7 @@ dmt_status dmt_download_law(dmt_ens* h, int32_t unit, int32_t kind, double* H, d
                               sel, unit, h->d, h->P, h->d_pt_off, h->G, h->d_seg_rec, h->d_seg_q,
                               h->d_tile_qoff, h->stream));
     HIP_OK(hipMemcpyAsync(F, h->d_stage, h->P * h->d * 8, hipMemcpyDeviceToHost, h->stream));
-    HIP_OK(hipStreamSynchronize(h->stream));
+    HIP_OK(stream_wait(h));
   }
   if (laws) {
     std::vector<double> l0(h->G * DMT_LAW_STRIDE), l1(h->G * DMT_LAW_STRIDE);
@@ -967,7 +978,7 @@ dmt_status dmt_download_law(dmt_ens* h, int32_t unit, int32_t kind, double* H, d
     HIP_OK(hipMemcpyAsync(l0.data(), h->d_law[0][kind], l0.size() * 8, hipMemcpyDeviceToHost, h->stream));
     HIP_OK(hipMemcpyAsync(l1.data(), h->d_law[1][kind], l1.size() * 8, hipMemcpyDeviceToHost, h->stream));
     HIP_OK(hipMemcpyAsync(hs.data(), sel, h->G, hipMemcpyDeviceToHost, h->stream));
-    HIP_OK(hipStreamSynchronize(h->stream));
+    HIP_OK(stream_wait(h));
     for (int64_t g = 0; g < h->G; ++g) {
       const std::vector<double>& src = (hs[g] ^ unit) ? l1 : l0;
       std::memcpy(laws + g * DMT_LAW_STRIDE, src.data() + g * DMT_LAW_STRIDE, DMT_LAW_STRIDE * 8);
@@ -983,7 +994,7 @@ dmt_status dmt_create_layout(dmt_ens* h, const int32_t* n_blocks, const int32_t*
   if (!n_blocks || !seg_first || !seg_last || !last || !rho || !layout_id)
     return fail(DMT_ERR_INVALID, "null argument");
   DMT_TRY(build_layout(h, n_blocks, seg_first, seg_last, last, rho, hist_len, layout_id));
-  HIP_OK(hipStreamSynchronize(h->stream));
+  HIP_OK(stream_wait(h));
   return DMT_OK;
 }
 
@@ -1011,7 +1022,7 @@ dmt_status dmt_draw_unit(dmt_ens* h, int32_t unit, int64_t r0, int64_t r1, const
                            key.iter, key.salt, L->d_llp, L->d_success, false));
   if (ll_out) HIP_OK(hipMemcpyAsync(ll_out, L->d_llp + r0, (r1 - r0) * 8, hipMemcpyDeviceToHost, h->stream));
   if (success_out) HIP_OK(hipMemcpyAsync(success_out, L->d_success + r0, r1 - r0, hipMemcpyDeviceToHost, h->stream));
-  HIP_OK(hipStreamSynchronize(h->stream));
+  HIP_OK(stream_wait(h));
   return DMT_OK;
 }
 
@@ -1031,9 +1042,9 @@ dmt_status dmt_draw_proposal(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
                            key.salt, L->d_llp, success_out ? L->d_success : nullptr, false));
   if (success_out) {
     HIP_OK(hipMemcpyAsync(success_out, L->d_success + b0, b1 - b0, hipMemcpyDeviceToHost, h->stream));
-    HIP_OK(hipStreamSynchronize(h->stream));
+    HIP_OK(stream_wait(h));
   } else if (Z) {
-    HIP_OK(hipStreamSynchronize(h->stream));  // host Z buffer must stay valid until copied
+    HIP_OK(stream_wait(h));  // host Z buffer must stay valid until copied
   }
   return DMT_OK;
 }
@@ -1092,7 +1103,7 @@ static dmt_status finish_reduction(dmt_ens* h, double* v, bool global = true) {
       return fail(DMT_ERR_COMM, "ncclAllGather failed");
     std::vector<double> all(3 * h->nranks);
     HIP_OK(hipMemcpyAsync(all.data(), h->d_gather, 3 * h->nranks * 8, hipMemcpyDeviceToHost, h->stream));
-    HIP_OK(hipStreamSynchronize(h->stream));
+    HIP_OK(stream_wait(h));
     // fixed rank-order adjacent-pair tree, ranks padded to a power of two
     int n2 = 1;
     while (n2 < h->nranks) n2 <<= 1;
@@ -1105,7 +1116,7 @@ static dmt_status finish_reduction(dmt_ens* h, double* v, bool global = true) {
     }
   } else {
     HIP_OK(hipMemcpyAsync(h->h_red, h->d_red, 24, hipMemcpyDeviceToHost, h->stream));
-    HIP_OK(hipStreamSynchronize(h->stream));
+    HIP_OK(stream_wait(h));
     v[0] = h->h_red[0];
     v[1] = h->h_red[1];
     v[2] = h->h_red[2];
@@ -1278,18 +1289,18 @@ dmt_status dmt_mcmc_run(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int6
                              h->stream) != ncclSuccess)
     return fail(DMT_ERR_COMM, "ncclAllGather failed");
   if (!out) {
-    HIP_OK(hipStreamSynchronize(h->stream));
+    HIP_OK(stream_wait(h));
     return DMT_OK;
   }
   if (!multi) {
-    HIP_OK(hipStreamSynchronize(h->stream));
+    HIP_OK(stream_wait(h));
     std::memcpy(out, h->h_run, 24 * n_iter);
     return DMT_OK;
   }
   std::vector<double> all(3 * h->nranks * n_iter);
   HIP_OK(hipMemcpyAsync(all.data(), h->d_run_gather, all.size() * 8, hipMemcpyDeviceToHost,
                         h->stream));
-  HIP_OK(hipStreamSynchronize(h->stream));
+  HIP_OK(stream_wait(h));
   int n2 = 1;
   while (n2 < h->nranks) n2 <<= 1;
   std::vector<double> lv(n2);
@@ -1327,9 +1338,9 @@ dmt_status dmt_accept_reject(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
   }
   if (acc_out) {
     HIP_OK(hipMemcpyAsync(acc_out, L->d_acc, b1 - b0, hipMemcpyDeviceToHost, h->stream));
-    HIP_OK(hipStreamSynchronize(h->stream));
+    HIP_OK(stream_wait(h));
   } else if (E) {
-    HIP_OK(hipStreamSynchronize(h->stream));
+    HIP_OK(stream_wait(h));
   }
   return DMT_OK;
 }
@@ -1361,7 +1372,7 @@ dmt_status dmt_recompute_path(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1
                            0, L->d_llp, success_out ? L->d_success : nullptr, false));
   if (success_out) {
     HIP_OK(hipMemcpyAsync(success_out, L->d_success + b0, b1 - b0, hipMemcpyDeviceToHost, h->stream));
-    HIP_OK(hipStreamSynchronize(h->stream));
+    HIP_OK(stream_wait(h));
   }
   return DMT_OK;
 }
@@ -1404,7 +1415,7 @@ dmt_status dmt_upload_obs(dmt_ens* h, const double* Hobs, const double* Fobs, co
   HIP_OK(hipMemcpyAsync(h->d_obsF, Fobs, h->G * h->d * 8, hipMemcpyHostToDevice, h->stream));
   HIP_OK(hipMemcpyAsync(h->d_obsc, cobs, h->G * 8, hipMemcpyHostToDevice, h->stream));
   h->art_eps = artificial_noise;
-  HIP_OK(hipStreamSynchronize(h->stream));
+  HIP_OK(stream_wait(h));
   return DMT_OK;
 }
 
@@ -1487,7 +1498,7 @@ static dmt_status guiding_term_device(dmt_ens* h, Layout* L, int64_t b0, int64_t
   const int64_t cap = std::max(need, std::min<int64_t>(span(gmin, gmax), kFiltBatchPoints));
   if (cap > h->qbuf_cap) {
     if (h->d_qbuf) {
-      HIP_OK(hipStreamSynchronize(h->stream));
+      HIP_OK(stream_wait(h));
       HIP_OK(hipFree(h->d_qbuf));
       h->bytes -= h->qbuf_cap * kFiltNQ(h->d) * 8;
       h->d_qbuf = nullptr;
@@ -1520,7 +1531,7 @@ static dmt_status guiding_term_device(dmt_ens* h, Layout* L, int64_t b0, int64_t
     const int64_t items = a.fchunk_off_h1 - a.fchunk_off_h0;
     if (items > h->tbuf_cap) {
       if (h->d_tbuf) {
-        HIP_OK(hipStreamSynchronize(h->stream));
+        HIP_OK(stream_wait(h));
         HIP_OK(hipFree(h->d_tbuf));
         h->bytes -= h->tbuf_cap * (h->hp + h->d + 1) * 8;
         h->d_tbuf = nullptr;
@@ -1538,7 +1549,7 @@ static dmt_status guiding_term_device(dmt_ens* h, Layout* L, int64_t b0, int64_t
   }
   int failed = 0;
   HIP_OK(hipMemcpyAsync(&failed, h->d_fail, sizeof(int), hipMemcpyDeviceToHost, h->stream));
-  HIP_OK(hipStreamSynchronize(h->stream));
+  HIP_OK(stream_wait(h));
   if (failed) return fail(DMT_ERR_INVALID, "singular I + HK in the device backward filter");
   return DMT_OK;
 }
@@ -1594,12 +1605,12 @@ dmt_status dmt_set_proposal_law(dmt_ens* h, int32_t layout, int64_t b0, int64_t 
   HIP_OK(launch_set_prop_law(a, h->stream));
   uint32_t ncrit = 0;
   HIP_OK(hipMemcpyAsync(&ncrit, L->d_ncrit, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream));
-  HIP_OK(hipStreamSynchronize(h->stream));
+  HIP_OK(stream_wait(h));
   if (ncrit > 0) DMT_TRY(guiding_term_device(h, L, b0, b1, DMT_UPROP, L->d_crit));
   if (critical_out)
     HIP_OK(hipMemcpyAsync(critical_out, L->d_crit + b0, b1 - b0, hipMemcpyDeviceToHost, h->stream));
   DMT_TRY(dmt_recompute_path(h, layout, b0, b1, 0, success_out));
-  if (critical_out) HIP_OK(hipStreamSynchronize(h->stream));
+  if (critical_out) HIP_OK(stream_wait(h));
   return DMT_OK;
 }
 
@@ -1647,7 +1658,7 @@ dmt_status dmt_set_accepted(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, 
   if (mcmciter < 1 || mcmciter > L->hist_len) return fail(DMT_ERR_INVALID, "mcmciter outside 1:ll_hist_len");
   if (!v) return fail(DMT_ERR_INVALID, "null values");
   HIP_OK(hipMemcpyAsync(L->d_acch + (mcmciter - 1) * L->nblocks + b0, v, b1 - b0, hipMemcpyHostToDevice, h->stream));
-  HIP_OK(hipStreamSynchronize(h->stream));
+  HIP_OK(stream_wait(h));
   return DMT_OK;
 }
 
@@ -1663,7 +1674,7 @@ dmt_status dmt_set_ll(dmt_ens* h, int32_t layout, int32_t unit, int64_t b0, int6
   double* hist = unit == DMT_U ? L->d_llh : L->d_llph;
   HIP_OK(hipMemcpyAsync(hist + (mcmciter - 1) * L->nblocks + b0, v, (b1 - b0) * 8,
                         hipMemcpyHostToDevice, h->stream));
-  HIP_OK(hipStreamSynchronize(h->stream));
+  HIP_OK(stream_wait(h));
   return DMT_OK;
 }
 
@@ -1697,7 +1708,7 @@ dmt_status dmt_get_block_state(dmt_ens* h, int32_t layout, int32_t what, int64_t
                               L->hist_len, hipMemcpyDeviceToHost, h->stream));
     }
   }
-  HIP_OK(hipStreamSynchronize(h->stream));
+  HIP_OK(stream_wait(h));
   return DMT_OK;
 }
 
@@ -1717,7 +1728,7 @@ dmt_status dmt_set_block_state(dmt_ens* h, int32_t layout, int32_t what, int64_t
                               L->hist_len, hipMemcpyHostToDevice, h->stream));
     }
   }
-  HIP_OK(hipStreamSynchronize(h->stream));
+  HIP_OK(stream_wait(h));
   return DMT_OK;
 }
 
@@ -1864,13 +1875,13 @@ dmt_status dmt_set_shard(dmt_ens* h, int64_t seg_base) {
 
 dmt_status dmt_sync(dmt_ens* h) {
   DMT_TRY(check_h(h));
-  HIP_OK(hipStreamSynchronize(h->stream));
+  HIP_OK(stream_wait(h));
   return DMT_OK;
 }
 
 dmt_status dmt_set_timing(dmt_ens* h, int32_t on) {
   DMT_TRY(check_h(h));
-  HIP_OK(hipStreamSynchronize(h->stream));
+  HIP_OK(stream_wait(h));
   drain_timing(h);
   for (int k = 0; k < DMT_K_COUNT; ++k) { h->t_ms[k] = 0; h->t_cnt[k] = 0; }
   h->timing = on < 0 ? 0xFFFFFFFFu : (uint32_t)on;
@@ -1880,7 +1891,7 @@ dmt_status dmt_set_timing(dmt_ens* h, int32_t on) {
 dmt_status dmt_get_timing(dmt_ens* h, int32_t kernel, double* ms, int64_t* count) {
   DMT_TRY(check_h(h));
   if (kernel < 0 || kernel >= DMT_K_COUNT) return fail(DMT_ERR_INVALID, "bad kernel id");
-  HIP_OK(hipStreamSynchronize(h->stream));
+  HIP_OK(stream_wait(h));
   drain_timing(h);
   if (ms) *ms = h->t_ms[kernel];
   if (count) *count = h->t_cnt[kernel];
@@ -1936,7 +1947,7 @@ dmt_status dmt_snapshot_reserve(dmt_ens* h, int32_t what_mask, int64_t n_slots) 
   DMT_TRY(check_h(h));
   if (what_mask < 1 || what_mask > 3 || n_slots < 1)
     return fail(DMT_ERR_INVALID, "what_mask must be 1 (XX), 2 (WW) or 3, n_slots >= 1");
-  HIP_OK(hipStreamSynchronize(h->stream));
+  HIP_OK(stream_wait(h));
   const int C[2] = {h->d, h->m};
   for (int k = 0; k < 2; ++k) {
     if (h->d_snap[k]) {
@@ -1989,7 +2000,7 @@ dmt_status dmt_snapshot_download(dmt_ens* h, int32_t what, int64_t slot, double*
   const int C = what == 0 ? h->d : h->m;
   HIP_OK(hipMemcpyAsync(out, h->d_snap[what] + slot * h->P * C, h->P * C * 8,
                         hipMemcpyDeviceToHost, h->stream));
-  HIP_OK(hipStreamSynchronize(h->stream));
+  HIP_OK(stream_wait(h));
   if (mcmciter) *mcmciter = h->snap_iter[slot];
   return DMT_OK;
 }
@@ -2011,7 +2022,7 @@ dmt_status dmt_snapshot_write(dmt_ens* h, const char* path, int64_t s0, int64_t 
                               1, h->P, h->d_pt_off, h->G, h->d_seg_rec, h->d_seg_q, h->d_tile_qoff,
                               h->stream));
   HIP_OK(hipMemcpyAsync(t.data(), h->d_stage, nt * 8, hipMemcpyDeviceToHost, h->stream));
-  HIP_OK(hipStreamSynchronize(h->stream));
+  HIP_OK(stream_wait(h));
   std::FILE* f = std::fopen(path, "wb");
   if (!f) return fail(DMT_ERR_INVALID, std::string("cannot open ") + path);
   dmt_snapshot_header hd{};
@@ -2086,7 +2097,7 @@ dmt_status dmt_snapshot_write(dmt_ens* h, const char* path, int64_t s0, int64_t 
     }
     if (ok) ok = std::fwrite(pin[b], 8, pieces[k].n, f) == (size_t)pieces[k].n;
   }
-  (void)hipStreamSynchronize(h->stream);
+  (void)stream_wait(h);
   for (int b = 0; b < 2; ++b) {
     if (pin[b]) (void)hipHostFree(pin[b]);
     if (ev[b]) (void)hipEventDestroy(ev[b]);
