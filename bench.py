@@ -303,13 +303,13 @@ def main(argv=None):
     k_ms, k_n = ens.get_timing(L.K_DRAW)  # k_n counts iterations (persistent) or launches
     persist = w.model.kind == L.MODEL_OU and os.environ.get("DMT_MCMC_PERSIST", "1") != "0"
     a_ms = a_n = 0
+    done = args.warmup + args.steps  # iterations run so far
     if not persist:
         # the accept+reduce kernel, timed on a few extra iterations after the timed region
         ens.set_timing(True, kernels=[L.K_ACCEPT])
-        ens.mcmc_run(lay, 0, B, args.warmup + args.steps + 1, EXTRA_ITERS)
+        ens.mcmc_run(lay, 0, B, done + 1, EXTRA_ITERS)
         a_ms, a_n = ens.get_timing(L.K_ACCEPT)
-    else:
-        ens.mcmc_run(lay, 0, B, args.warmup + args.steps + 1, EXTRA_ITERS)
+        done += EXTRA_ITERS
     ens.set_timing(False)
     if dist is not None:
         import torch
@@ -352,8 +352,7 @@ def main(argv=None):
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(w, ens, lay, args.warmup + args.steps + EXTRA_ITERS + 1,
-                               budget_s=args.cpu_budget)
+            cpu = cpu_baseline(w, ens, lay, done + 1, budget_s=args.cpu_budget)
         desc, dtype = WORKLOADS[args.config]
         frac = achieved / PEAK_HBM_GBS
         line = {

@@ -14,6 +14,46 @@ from diffusionmcmctools_amd.models import (FHN, OU, Observation, artificial_obs_
 import oracle as orc
 
 
+_FULL = {}
+
+
+def full_workload(cfg):
+    """BASELINE.json's per-GPU workloads at full size, built once per test session (C3 takes
+    ~40 s of host set-up): C2 1024 × 500, C3 65 536 × 1000 (shorter burn-in of the block
+    starts), C5 32 768 × 2000 fp32.  Callers must not modify the arrays."""
+    if cfg not in _FULL:
+        _FULL[cfg] = {"c2": W.c2_ou2d, "c3": lambda: W.c3_fhn(T_burn=0.2),
+                      "c5": W.c5_lorenz}[cfg]()
+    return _FULL[cfg]
+
+
+def sampled_blocks_reference(w, blocks, seed, it, salt=0):
+    """Oracle restatement, for single-segment terminal blocks `blocks` of workload w, of the
+    fill (init_paths! with w.Z0, ρ = 0) followed by one pCN draw_proposal_path! keyed
+    (seed, it, salt) — each block on its own, with its global segment id's normals.  Returns
+    per block (X°[npts][d], cumulative W°[npts][m], ll°) as the device downloads them."""
+    npts = w.n_points[0][0]
+    d, m, prec = w.d, w.m, w.precision
+    out = []
+    for b in blocks:
+        rows = slice(b * npts, (b + 1) * npts)
+        laws = w.laws[b:b + 1]
+        H = w.H if w.H_shared else w.H[rows]
+        F = w.F[rows]
+        Z0 = w.Z0[b * (npts - 1):(b + 1) * (npts - 1)]
+        X1, W1, _, nf = orc.draw_terminal_blocks(
+            w.model.kind, d, m, npts, laws, w.t, H, F, w.X0[rows], np.zeros((npts, m)),
+            np.zeros(1), Z=Z0, prec=prec, t_shared=True, H_shared=w.H_shared)
+        assert nf == 0
+        Z1 = orc.normals_segment(seed, b, it, salt, npts - 1, m, prec)
+        Xo, Wo, llo, _ = orc.draw_terminal_blocks(
+            w.model.kind, d, m, npts, laws, w.t, H, F, X1, W1, np.full(1, w.rho), Z=Z1,
+            prec=prec, t_shared=True, H_shared=w.H_shared)
+        out.append((Xo.astype(np.float64), orc.w_from_increments(Wo, prec).astype(np.float64),
+                    float(llo[0])))
+    return out
+
+
 def both(w, seed=11, hist_len=0, init_Z=True, mapping=L.MAP_AUTO):
     """Device ensemble + oracle ensemble holding the same workload; returns (dev, ora, layout)."""
     w.meta["hist_len"] = hist_len

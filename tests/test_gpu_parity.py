@@ -386,11 +386,40 @@ def test_first_proposal_auto_accepted_without_loglikhd(mapping):
 
 
 # ---------------------------------------------------------------- full-size properties
+@pytest.mark.parametrize("cfg", ["c3", "c5"])
+def test_full_size_sampled_blocks_bit_exact(cfg):
+    """The full per-GPU shard of C3 (65 536 × 1000, fp64) and C5 (32 768 × 2000, fp32) on the
+    device (MAP_AUTO: the lane mapping): after init_paths! and one pCN draw, 48 blocks drawn at
+    random equal the oracle's restatement of those blocks bit for bit (paths X°, cumulative W°,
+    ll°) — blocks are independent, so the sample pins the whole launch."""
+    import diffusionmcmctools_amd as d
+    w = cs.full_workload(cfg)
+    w.meta["hist_len"] = 0
+    seed = 4
+    dev = d.Ensemble(w.model.kind, w.d, w.m, w.n_points, precision=w.precision, seed=seed,
+                     grid_shared=w.grid_shared)
+    lay = W.fill(dev, w, init_Z=True)
+    nb = w.nblocks
+    ok = dev.draw_proposal(lay, 0, nb, iter=1, salt=0, want_success=True)
+    assert ok.all()
+    X, Wc = dev.download_paths(L.UPROP, 0), dev.download_paths(L.UPROP, 1)
+    llp = dev.get_block_state(lay, L.BLK_LLPROP, 0, nb)
+    dev.close()
+    npts = w.n_points[0][0]
+    blocks = np.sort(np.random.default_rng(7).choice(nb, 48, replace=False))
+    blocks[0], blocks[-1] = 0, nb - 1  # the first and last lane of the first and last tile
+    for b, (Xo, Wo, llo) in zip(blocks, cs.sampled_blocks_reference(w, blocks, seed, 1)):
+        rows = slice(b * npts, (b + 1) * npts)
+        np.testing.assert_array_equal(X[rows], Xo)
+        np.testing.assert_array_equal(Wc[rows], Wo)
+        assert llp[b] == llo
+
+
 @pytest.mark.parametrize("mapping", MAPPINGS)
-@pytest.mark.parametrize("cfg", ["c2", "c3"])
+@pytest.mark.parametrize("cfg", ["c2", "c3", "c5"])
 def test_full_size_properties(cfg, mapping):
     """At BASELINE.json's full sizes (oracle too slow here): size-independent invariants."""
-    w = W.c2_ou2d() if cfg == "c2" else W.c3_fhn(T_burn=0.2)
+    w = cs.full_workload(cfg)
     import diffusionmcmctools_amd as d
     dev = d.Ensemble(w.model.kind, w.d, w.m, w.n_points, precision=w.precision, seed=4,
                      grid_shared=w.grid_shared, mapping=mapping)
@@ -419,6 +448,7 @@ def test_full_size_properties(cfg, mapping):
     assert np.array_equal(dev.download_paths(L.UPROP, 0), dev.download_paths(L.U, 0))
     assert np.array_equal(dev.get_block_state(lay1, L.BLK_LLPROP, 0, nb),
                           dev.get_block_state(lay1, L.BLK_LL, 0, nb))
+    dev.close()
 
 
 @pytest.mark.parametrize("mapping", MAPPINGS)

@@ -116,6 +116,52 @@ def test_gpu_shards_match_unsharded():
 
 
 @pytest.mark.gpu
+def test_gpu_fhn_lane_shards_match_unsharded():
+    """C3's per-rank scale on the lane mapping: two FHN shards of 32 768 blocks × 1000 steps
+    (set_shard: global segment ids key the device streams) against one ensemble of 65 536 —
+    identical paths, ll, decisions and rank-tree fetch_ll over dmt_mcmc_run (the
+    per-iteration kernels k_block / k_block_ps + k_accept_reduce)."""
+    import diffusionmcmctools_amd as dmt
+    from diffusionmcmctools_amd import workloads as W
+    from diffusionmcmctools_amd import shard
+    from diffusionmcmctools_amd import _lib as L
+    world, B, n = 2, 32768, 3
+    ws = [W.c3_fhn(B=B, T_burn=0.05, block_offset=r) for r in range(world)]
+    g = W.concat_workloads(ws)
+    for w in ws + [g]:
+        w.meta["hist_len"] = n
+
+    def make(w, base):
+        e = dmt.Ensemble(w.model.kind, w.d, w.m, w.n_points, precision=w.precision, seed=SEED,
+                         grid_shared=w.grid_shared, mapping=L.MAP_LANE)
+        e.set_shard(base)
+        lay = W.fill(e, w, init_Z=True)
+        e.loglikhd(lay, 0, 0, w.nblocks)
+        return e, lay
+
+    shards = [make(w, r * B) for r, w in enumerate(ws)]
+    full, lay = make(g, 0)
+    res_s = [e.mcmc_run(l, 0, B, 1, n, salt=3) for e, l in shards]
+    res_f = full.mcmc_run(lay, 0, g.nblocks, 1, n, salt=3)
+    for i in range(n):
+        comb = tuple(shard.rank_tree([res_s[r][i][c] for r in range(world)]) for c in range(3))
+        assert comb == tuple(float(x) for x in res_f[i])
+    for what in (L.BLK_LL, L.BLK_LLPROP):
+        np.testing.assert_array_equal(
+            np.concatenate([e.get_block_state(l, what, 0, B) for e, l in shards]),
+            full.get_block_state(lay, what, 0, g.nblocks))
+    np.testing.assert_array_equal(
+        np.concatenate([e.get_block_state(l, L.BLK_ACC_HIST, 0, B, hist_len=n)
+                        for e, l in shards], axis=1),
+        full.get_block_state(lay, L.BLK_ACC_HIST, 0, g.nblocks, hist_len=n))
+    for unit in (L.U, L.UPROP):
+        X = np.concatenate([e.download_paths(unit, 0) for e, _ in shards])
+        np.testing.assert_array_equal(X, full.download_paths(unit, 0))
+    for e, _ in shards + [(full, lay)]:
+        e.close()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("persist", ["1", "0"])
 def test_rccl_allgather_path_single_rank(monkeypatch, persist):
     """The RCCL path of fetch_ll / dmt_mcmc_run (ncclCommInitRank, ncclAllGather, the host
