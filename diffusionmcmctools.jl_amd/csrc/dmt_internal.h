@@ -89,7 +89,6 @@ struct BlockArgs {
                       // steps: one-shot draws on k_block_resident
   int lane_split;     // MAP_LANE draws: producer/consumer waves (k_block_ps); the runtime sets
                       // it only for layouts of single-segment blocks
-  int half_tiles;     // MAP_LANE draws: two waves per tile, 32 slots each (k_block, k_block_ps)
 };
 
 struct AcceptArgs {

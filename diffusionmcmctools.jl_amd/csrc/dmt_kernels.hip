@@ -219,32 +219,6 @@ __device__ __forceinline__ bool map_block(const BlockArgs<T>& a, int64_t& tile, 
   return true;
 }
 
-// Half-tile variant (BlockArgs::half_tiles): two waves per (tile, block index), wave h running
-// the tile's slots 32h … 32h + 31 on its lanes 0-31 (lanes 32-63 idle).  Twice the waves for
-// the same blocks: latency hiding for ensembles with fewer tiles than the chip has SIMDs; every
-// access of a wave stays one 128 B (fp32) / 256 B (fp64) contiguous run per component.
-template <class T>
-__device__ __forceinline__ bool map_block_slot(const BlockArgs<T>& a, int64_t& tile,
-                                               int64_t& blk, int& slot) {
-  const int lane = threadIdx.x & 63;
-  int64_t wave = blockIdx.x;
-  int half = 0;
-  if (a.half_tiles) {
-    half = (int)(wave & 1);
-    wave >>= 1;
-    if (lane >= 32) return false;
-  }
-  slot = a.half_tiles ? lane + 32 * half : lane;
-  tile = a.tile0 + wave / a.MB;
-  const int b = (int)(wave % a.MB);
-  if (tile >= a.tile1) return false;
-  const int64_t r = tile * kLanes + slot;
-  if (r >= a.R) return false;
-  blk = a.blk_off[r] + b;
-  if (blk >= a.blk_off[r + 1] || blk < a.b0 || blk >= a.b1) return false;
-  return true;
-}
-
 // tile-phase repair only while the minority is at most 1/repair_div of the wave
 // (BlockArgs::repair_div; 4 by default, DMT_REPAIR_DIV)
 
@@ -252,8 +226,8 @@ template <class Mdl, class T, int MODE, bool PARITY, int K>
 __global__ __launch_bounds__(64) void k_block(const BlockArgs<T> a) {
   constexpr int D = Mdl::D, M = Mdl::M, HP = D * (D + 1) / 2;
   int64_t tile, blk;
-  int lane;  // the tile slot this lane runs
-  if (!map_block_slot(a, tile, blk, lane)) return;
+  if (!map_block(a, tile, blk)) return;
+  const int lane = threadIdx.x;
   const int64_t tq = a.tile_qoff[tile];
   auto idx = [&](int64_t q, int c, int C) -> int64_t { return ((tq + q) * C + c) * kLanes + lane; };
   const int g0 = a.gfirst[blk], g1 = a.glast[blk];
@@ -358,18 +332,13 @@ __global__ __launch_bounds__(128, DMT_PS_MINW) void k_block_ps(const BlockArgs<T
   __shared__ T s_dt[2][L][64];
   __shared__ T s_dw[2][L][M][64];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;  // LDS column of the (dt, dW°) hand-off
-  // half tiles (BlockArgs::half_tiles): workgroup pair 2·k, 2·k + 1 runs slots 0-31, 32-63 of
-  // (tile, block index) k on lanes 0-31 of its waves
-  const int64_t wg = a.half_tiles ? blockIdx.x >> 1 : blockIdx.x;
-  const int half = a.half_tiles ? (int)(blockIdx.x & 1) : 0;
-  const int64_t tile = a.tile0 + wg / a.MB;
-  const int bidx = (int)(wg % a.MB);
+  const int lane = threadIdx.x & 63;
+  const int64_t tile = a.tile0 + blockIdx.x / a.MB;
+  const int bidx = (int)(blockIdx.x % a.MB);
   if (tile >= a.tile1) return;  // whole workgroup
-  const int slot = a.half_tiles ? (lane & 31) + 32 * half : lane;  // the tile slot this lane runs
-  const int64_t r = tile * kLanes + slot;
+  const int64_t r = tile * kLanes + lane;
   int64_t blk = -1;
-  if (r < a.R && (!a.half_tiles || lane < 32)) {
+  if (r < a.R) {
     blk = a.blk_off[r] + bidx;
     if (blk >= a.blk_off[r + 1] || blk < a.b0 || blk >= a.b1) blk = -1;
   }
@@ -408,11 +377,11 @@ __global__ __launch_bounds__(128, DMT_PS_MINW) void k_block_ps(const BlockArgs<T
       if (sw != pw) { Wcd = a.W[pw ^ a.ws_flip]; nsw = pw; }
     }
   }
-  auto idx = [&](int64_t q, int c, int C) -> int64_t { return ((row + q) * C + c) * kLanes + slot; };
+  auto idx = [&](int64_t q, int c, int C) -> int64_t { return ((row + q) * C + c) * kLanes + lane; };
 
   if (w == 0) {
     // ================= producer =================
-    const T* tb = a.t_shared ? a.t + (act ? a.seg_q[g] : 0) : a.t + row * kLanes + slot;
+    const T* tb = a.t_shared ? a.t + (act ? a.seg_q[g] : 0) : a.t + row * kLanes + lane;
     const int tst = a.t_shared ? 1 : kLanes;
     const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
     const uint32_t seg = (uint32_t)g + a.seg_base, c3 = a.salt << 1;
@@ -485,9 +454,9 @@ __global__ __launch_bounds__(128, DMT_PS_MINW) void k_block_ps(const BlockArgs<T
     Law<Mdl, T> LA;
     const int ls = act ? (a.selPP[g] ^ a.law_flip) : 0;
     LA.load(a.law[ls][0] + (int64_t)g * DMT_LAW_STRIDE);
-    const T* Hb = a.H_shared[ls][0] ? a.H[ls][0] + (act ? a.seg_q[g] : 0) * HP : a.H[ls][0] + row * HP * kLanes + slot;
+    const T* Hb = a.H_shared[ls][0] ? a.H[ls][0] + (act ? a.seg_q[g] : 0) * HP : a.H[ls][0] + row * HP * kLanes + lane;
     const int hst = a.H_shared[ls][0] ? 1 : kLanes;
-    const T* Fb = a.F[ls][0] + row * D * kLanes + slot;
+    const T* Fb = a.F[ls][0] + row * D * kLanes + lane;
     T x[D];
     {
       const T* Xs = a.X[sx ^ a.xs_flip];
@@ -3054,20 +3023,19 @@ static hipError_t launch_block_t(int mapping, int mode, const void* args, int64_
     }
     const dim3 block(64);
     const bool par = a.Z != nullptr;
-    const dim3 lgrid((unsigned)(a.half_tiles ? 2 * nwaves : nwaves));  // half tiles: 2 per wave
     if (mode == MODE_PCN && !par && a.lane_split) {  // producer/consumer waves (k_block_ps)
-      dlaunch(k_block_ps<Mdl, T>, lgrid, dim3(128), s, a);
+      dlaunch(k_block_ps<Mdl, T>, grid, dim3(128), s, a);
       return hipGetLastError();
     }
     switch (mode) {
       case MODE_PCN:
-        if (par) dlaunch(k_block<Mdl, T, MODE_PCN, true, kChunk>, lgrid, block, s, a);
-        else dlaunch(k_block<Mdl, T, MODE_PCN, false, kChunk>, lgrid, block, s, a);
+        if (par) dlaunch(k_block<Mdl, T, MODE_PCN, true, kChunk>, grid, block, s, a);
+        else dlaunch(k_block<Mdl, T, MODE_PCN, false, kChunk>, grid, block, s, a);
         break;
-      case MODE_RECOMPUTE: dlaunch(k_block<Mdl, T, MODE_RECOMPUTE, false, kChunk>, lgrid, block, s, a); break;
+      case MODE_RECOMPUTE: dlaunch(k_block<Mdl, T, MODE_RECOMPUTE, false, kChunk>, grid, block, s, a); break;
       case MODE_FRESH:
-        if (par) dlaunch(k_block<Mdl, T, MODE_FRESH, true, kChunk>, lgrid, block, s, a);
-        else dlaunch(k_block<Mdl, T, MODE_FRESH, false, kChunk>, lgrid, block, s, a);
+        if (par) dlaunch(k_block<Mdl, T, MODE_FRESH, true, kChunk>, grid, block, s, a);
+        else dlaunch(k_block<Mdl, T, MODE_FRESH, false, kChunk>, grid, block, s, a);
         break;
       default: return hipErrorInvalidValue;
     }

@@ -164,7 +164,6 @@ struct dmt_ens {
   bool persist = true;       // dmt_mcmc_run of a linear drift in one launch (DMT_MCMC_PERSIST=0: off)
   bool resident = true;      // ... with register-resident block state when eligible (DMT_MCMC_RESIDENT=0: off)
   int lane_split = -1;       // MAP_LANE draws on producer/consumer waves: 1 on, 0 off, -1 auto
-  int half_tiles = 0;        // MAP_LANE draws on half-tile waves (DMT_HALF_TILES): 1 on, 0 off, -1 auto
                              // (when the draw has fewer waves than the device has SIMDs)
   int64_t n_simd = 1024;
   int repair_div = 4;        // MAP_LANE tile-phase repair threshold (DMT_REPAIR_DIV)
@@ -427,7 +426,6 @@ void fill_common(dmt_ens* h, const Layout* L, BlockArgs<T>& a) {
   a.success = nullptr;
   a.repair_div = h->repair_div;
   a.lane_split = 0;
-  a.half_tiles = 0;
   a.resident1 = 0;
 }
 
@@ -461,10 +459,6 @@ dmt_status run_block_kernel(dmt_ens* h, const Layout* L, int mode, int kind_time
     a.resident1 = h->scan_resident && h->key.model == DMT_MODEL_OU && h->key.d <= 2 &&
                   L->single_seg && L->max_steps <= kResidentMaxSteps;
     a.lane_split = L->single_seg && (h->lane_split == 1 || (h->lane_split < 0 && nwaves < h->n_simd));
-    // half tiles: lane-mapped draws (non-linear models) with fewer waves than 2 per SIMD
-    const int64_t lw = nwaves * (a.lane_split ? 2 : 1);
-    a.half_tiles = op == 0 && h->key.model != DMT_MODEL_OU && h->mapping == MAP_LANE &&
-                   (h->half_tiles == 1 || (h->half_tiles < 0 && lw < 2 * h->n_simd));
   };
   if (h->key.precision == DMT_F64) {
     BlockArgs<double> a{};
@@ -693,7 +687,6 @@ dmt_status dmt_create(dmt_ens** out, const dmt_model* model, const dmt_structure
   if (const char* e = std::getenv("DMT_MCMC_PERSIST")) h->persist = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("DMT_MCMC_RESIDENT")) h->resident = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("DMT_LANE_SPLIT")) h->lane_split = std::atoi(e);
-  if (const char* e = std::getenv("DMT_HALF_TILES")) h->half_tiles = std::atoi(e);
   if (const char* e = std::getenv("DMT_REPAIR_DIV")) h->repair_div = std::max(1, std::atoi(e));
   if (const char* e = std::getenv("DMT_SCAN_RESIDENT")) h->scan_resident = std::strcmp(e, "0") != 0;
   {
