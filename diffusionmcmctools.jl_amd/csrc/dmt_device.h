@@ -542,22 +542,48 @@ __device__ __forceinline__ double exp1_draw(uint64_t seed, uint32_t blk, uint32_
   return -rng_log(u);
 }
 
-// Normal stream of one segment: normal n = step*M + k uses pair n>>1 of Philox block
-// counter (n>>1, segment, iter, salt<<1).
+// Normals per Philox block of the perf-mode stream: fp64 Box–Muller takes 53-bit uniforms,
+// built of the whole 128-bit block, for one pair; fp32 takes 24-bit uniforms, so a block gives
+// two pairs — (z0, z1) of words (x, z), (z2, z3) of words (y, w) (orc_normal_block).
+template <class T>
+struct NormPerBlock {
+  static constexpr int v = 2;
+};
+template <>
+struct NormPerBlock<float> {
+  static constexpr int v = 4;
+};
+__device__ __forceinline__ void normal_block(U4 o, double* z) { normal_pair(o, z[0], z[1]); }
+__device__ __forceinline__ void normal_block(U4 o, float* z) {
+  normal_pair(o, z[0], z[1]);
+  normal_pair(U4{o.y, o.x, o.w, o.z}, z[2], z[3]);
+}
+// entry q of a block's normals without dynamic register indexing
+template <class T, int NPB>
+__device__ __forceinline__ T pick_normal(const T (&zb)[NPB], uint32_t q) {
+  T r = zb[0];
+#pragma unroll
+  for (int e = 1; e < NPB; ++e) r = q == (uint32_t)e ? zb[e] : r;
+  return r;
+}
+
+// Normal stream of one segment: normal n = step*M + k is entry n % NPB of the Philox block
+// with counter (n / NPB, segment, iter, salt<<1).  get() is called with increasing n.
 template <class T>
 struct NormalStream {
-  uint32_t k0, k1, seg, iter, c3;
-  T cached;
+  static constexpr int NPB = NormPerBlock<T>::v;
+  uint32_t k0, k1, seg, iter, c3, have;
+  T zb[NPB];
   __device__ __forceinline__ void init(uint64_t seed, uint32_t g, uint32_t it, uint32_t salt) {
     k0 = (uint32_t)seed; k1 = (uint32_t)(seed >> 32); seg = g; iter = it; c3 = salt << 1;
+    have = 0xFFFFFFFFu;
   }
   __device__ __forceinline__ T get(uint32_t n) {
-    if (n & 1u) return cached;
-    U4 o = philox4x32_10(U4{n >> 1, seg, iter, c3}, k0, k1);
-    T z0, z1;
-    normal_pair(o, z0, z1);
-    cached = z1;
-    return z0;
+    if (n / NPB != have) {
+      have = n / NPB;
+      normal_block(philox4x32_10(U4{have, seg, iter, c3}, k0, k1), zb);
+    }
+    return pick_normal<T, NPB>(zb, n % NPB);
   }
 };
 

@@ -162,15 +162,16 @@ __device__ __forceinline__ bool run_segment(const Law<Mdl, T>& L, const T* __res
     load(0, cur);
     for (int c0 = 0; c0 < nfull; c0 += K) {
       load(c0 + K, nxt);  // prefetch; padded rows keep the last one in bounds
-      if (DRAW && !PARITY) {  // whole Box–Muller pairs of this chunk, straight-line
+      if (DRAW && !PARITY) {  // whole Philox blocks of normals for this chunk, straight-line
+        constexpr int NPB = NormPerBlock<T>::v;
+        static_assert((K * M) % NPB == 0, "chunk must hold whole normal blocks");
 #pragma unroll
-        for (int pp = 0; pp < K * M / 2; ++pp) {
-          const uint32_t pair = (uint32_t)((c0 * M) / 2 + pp);
-          U4 o = philox4x32_10(U4{pair, ns.seg, ns.iter, ns.c3}, ns.k0, ns.k1);
-          T z0, z1;
-          normal_pair(o, z0, z1);
-          cur.Z[(2 * pp) / M][(2 * pp) % M] = z0;
-          cur.Z[(2 * pp + 1) / M][(2 * pp + 1) % M] = z1;
+        for (int bq = 0; bq < K * M / NPB; ++bq) {
+          const uint32_t bc = (uint32_t)((c0 * M) / NPB + bq);
+          T zb[NPB];
+          normal_block(philox4x32_10(U4{bc, ns.seg, ns.iter, ns.c3}, ns.k0, ns.k1), zb);
+#pragma unroll
+          for (int e = 0; e < NPB; ++e) cur.Z[(NPB * bq + e) / M][(NPB * bq + e) % M] = zb[e];
         }
       }
       T gv[K];
@@ -419,14 +420,15 @@ __global__ __launch_bounds__(128, DMT_PS_MINW) void k_block_ps(const BlockArgs<T
         }
         if (cp + 1 < nch) load(cp + 1);
         T z[L][M];
+        constexpr int NPB = NormPerBlock<T>::v;
+        static_assert((L * M) % NPB == 0, "chunk must hold whole normal blocks");
 #pragma unroll
-        for (int pp = 0; pp < L * M / 2; ++pp) {
-          const uint32_t pair = (uint32_t)((cp * L * M) / 2 + pp);
-          U4 o = philox4x32_10(U4{pair, seg, a.iter, c3}, k0, k1);
-          T z0, z1;
-          normal_pair(o, z0, z1);
-          z[(2 * pp) / M][(2 * pp) % M] = z0;
-          z[(2 * pp + 1) / M][(2 * pp + 1) % M] = z1;
+        for (int bq = 0; bq < L * M / NPB; ++bq) {
+          const uint32_t bc = (uint32_t)((cp * L * M) / NPB + bq);
+          T zb[NPB];
+          normal_block(philox4x32_10(U4{bc, seg, a.iter, c3}, k0, k1), zb);
+#pragma unroll
+          for (int e = 0; e < NPB; ++e) z[(NPB * bq + e) / M][(NPB * bq + e) % M] = zb[e];
         }
 #pragma unroll
         for (int j = 0; j < L; ++j) {
@@ -854,8 +856,9 @@ __global__ __launch_bounds__(128) void k_block_wave(const BlockArgs<T> a) {
       for (int kk = 0; kk < M; ++kk) dW[kk] = Wsb[(int64_t)(i + 1) * M + kk];
     } else {
       const double* Zg = a.Z ? a.Z + a.st_off[g] * M : nullptr;
+      constexpr int NPB = NormPerBlock<T>::v;
       uint32_t have = 0xFFFFFFFFu;
-      T z0 = (T)0, z1 = (T)0;
+      T zb[NPB] = {};
       const T sdt = sqrt(dt);
 #pragma unroll
       for (int kk = 0; kk < M; ++kk) {
@@ -864,12 +867,11 @@ __global__ __launch_bounds__(128) void k_block_wave(const BlockArgs<T> a) {
         if (Zg) {
           z = (T)Zg[(int64_t)i * M + kk];
         } else {
-          if ((n >> 1) != have) {
-            U4 o = philox4x32_10(U4{n >> 1, (uint32_t)g + a.seg_base, a.iter, c3}, k0, k1);
-            normal_pair(o, z0, z1);
-            have = n >> 1;
+          if (n / NPB != have) {
+            have = n / NPB;
+            normal_block(philox4x32_10(U4{have, (uint32_t)g + a.seg_base, a.iter, c3}, k0, k1), zb);
           }
-          z = (n & 1u) ? z1 : z0;
+          z = pick_normal<T, NPB>(zb, n % NPB);
         }
         const T w = (MODE == MODE_FRESH) ? (T)0 : Wsb[(int64_t)(i + 1) * M + kk];
         dW[kk] = dfma(rho, w, srho * (sdt * z));
@@ -1180,8 +1182,9 @@ __device__ __forceinline__ void scan_block(const BlockArgs<T>& a, const int64_t 
 #pragma unroll
           for (int kk = 0; kk < M; ++kk) dW[kk] = Wk[k][kk];
         } else {
+          constexpr int NPB = NormPerBlock<T>::v;
           uint32_t have = 0xFFFFFFFFu;
-          T z0 = (T)0, z1 = (T)0;
+          T zb[NPB] = {};
           const T sdt = sqrt(dt);
 #pragma unroll
           for (int kk = 0; kk < M; ++kk) {
@@ -1190,12 +1193,11 @@ __device__ __forceinline__ void scan_block(const BlockArgs<T>& a, const int64_t 
             if (Zg) {
               z = Zk[k][kk];
             } else {
-              if ((n >> 1) != have) {
-                U4 o = philox4x32_10(U4{n >> 1, (uint32_t)g + a.seg_base, iter, c3}, k0, k1);
-                normal_pair(o, z0, z1);
-                have = n >> 1;
+              if (n / NPB != have) {
+                have = n / NPB;
+                normal_block(philox4x32_10(U4{have, (uint32_t)g + a.seg_base, iter, c3}, k0, k1), zb);
               }
-              z = (n & 1u) ? z1 : z0;
+              z = pick_normal<T, NPB>(zb, n % NPB);
             }
             dW[kk] = dfma(rho, Wk[k][kk], srho * (sdt * z));
           }
@@ -1682,15 +1684,18 @@ __device__ __forceinline__ void resident_block(const BlockArgs<T>& a, const Acce
   const int last_lane = (nst - 1) / kRun;
   double Ev = 0.0;
   // the normals of one iteration for this lane's run: normal n = s·M + k of step s = 8·lane + r
-  // is component n & 1 of Philox pair n >> 1; the run's 8M normals are exactly
-  // the pairs 4M·lane … 4M·lane + 4M − 1, so every index below is a compile-time offset
+  // is entry n % NPB of Philox block n / NPB; the run's 8M normals are exactly
+  // the blocks (8M/NPB)·lane … (8M/NPB)·(lane + 1) − 1, so every index below is a compile-time
+  // offset
   auto draw_z = [&](uint32_t itv, T (&z)[kRun][M]) {
-    T zz[2 * 4 * M];
+    constexpr int NPB = NormPerBlock<T>::v, NB = kRun * M / NPB;  // Philox blocks per run
+    static_assert((kRun * M) % NPB == 0, "a run must hold whole normal blocks");
+    T zz[kRun * M];
 #pragma unroll
-    for (int q = 0; q < 4 * M; ++q) {
-      U4 o = philox4x32_10(U4{(uint32_t)(4 * M * lane + q), (uint32_t)g + a.seg_base, itv, c3}, k0, k1);
-      normal_pair(o, zz[2 * q], zz[2 * q + 1]);
-    }
+    for (int q = 0; q < NB; ++q)
+      normal_block(philox4x32_10(U4{(uint32_t)(NB * lane + q), (uint32_t)g + a.seg_base, itv, c3},
+                                 k0, k1),
+                   zz + NPB * q);
 #pragma unroll
     for (int r = 0; r < kRun; ++r)
 #pragma unroll

@@ -458,7 +458,11 @@ dmt_status run_block_kernel(dmt_ens* h, const Layout* L, int mode, int kind_time
     a.success = success;
     a.resident1 = h->scan_resident && h->key.model == DMT_MODEL_OU && h->key.d <= 2 &&
                   L->single_seg && L->max_steps <= kResidentMaxSteps;
-    a.lane_split = L->single_seg && (h->lane_split == 1 || (h->lane_split < 0 && nwaves < h->n_simd));
+    // auto: fp64 only — with fp32's four normals per Philox block the single wave is faster
+    // (C5: 1773 vs 1934 µs per draw, profiles/r02m)
+    a.lane_split = L->single_seg && (h->lane_split == 1 ||
+                                     (h->lane_split < 0 && nwaves < h->n_simd &&
+                                      h->key.precision == DMT_F64));
   };
   if (h->key.precision == DMT_F64) {
     BlockArgs<double> a{};

@@ -500,8 +500,14 @@ void SFX(orc_w_from_increments)(int m, int npts, const REAL* dW, REAL* W) {
  * tests.  Z: [B][npts-1][m] (NULL -> perf-mode Philox stream with seed/iter).
  * Each block may have its own tables (H_stride/F_stride = 0 means shared).
  */
-void SFX(orc_normal_pair)(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
-                          REAL* z0, REAL* z1);
+/* normals per Philox block of the perf-mode stream (orc_normal_block) */
+#if IS_F64
+#define ORC_NPB 2
+#else
+#define ORC_NPB 4
+#endif
+void SFX(orc_normal_block)(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                           REAL* z);
 
 int SFX(orc_draw_terminal_blocks)(int model, int d, int m, int64_t B, int npts,
                                   const double* laws, int64_t law_stride,
@@ -528,7 +534,7 @@ int SFX(orc_draw_terminal_blocks)(int model, int d, int m, int64_t B, int npts,
         REAL rr = (REAL)r, sr = (REAL)sqrt(1.0 - r * r);
         /* pCN (increment form; W arrays hold increments) */
         for (int k = 0; k < m; ++k) Wp[k] = rr * Wa[k];
-        REAL zc = 0; int have = 0;
+        REAL zb[ORC_NPB] = {0};
         for (int q = 0; q < npts - 1; ++q) {
             REAL sdt = SQRT(tb[q + 1] - tb[q]);
             for (int k = 0; k < m; ++k) {
@@ -536,19 +542,15 @@ int SFX(orc_draw_terminal_blocks)(int model, int d, int m, int64_t B, int npts,
                 if (Z) z = Z[((size_t)blk * (npts - 1) + q) * m + k];
                 else {
                     uint32_t n = (uint32_t)(q * m + k);
-                    if (n & 1u) { z = zc; have = 0; }
-                    else {
-                        REAL z0, z1;
-                        SFX(orc_normal_pair)(seed, n >> 1, (uint32_t)blk, (uint32_t)iter,
-                                             salt << 1, &z0, &z1);
-                        z = z0; zc = z1; have = 1;
-                    }
+                    if (n % ORC_NPB == 0)
+                        SFX(orc_normal_block)(seed, n / ORC_NPB, (uint32_t)blk, (uint32_t)iter,
+                                              salt << 1, zb);
+                    z = zb[n % ORC_NPB];
                 }
                 REAL zi = sdt * z;
                 Wp[(size_t)(q + 1) * m + k] = FMA(rr, Wa[(size_t)(q + 1) * m + k], sr * zi);
             }
         }
-        (void)have;
         /* solve + ll (obs term + segment) */
         REAL ll;
         int ok = SFX(orc_solve_segment)(model, d, m, law, npts, tb, Hb, Fb, Wp, Xa, Xp, &ll);
@@ -701,8 +703,43 @@ static inline void rng_sincospif(float x, float* sn, float* cs) {
     *cs = q == 0 ? c0 : q == 1 ? -s0 : q == 2 ? -c0 : s0;
 }
 
-/* Box–Muller normal pair from one Philox block (perf-mode stream).
- * counter = (c0, c1, c2, c3), key = seed. */
+/* Box–Muller normals from one Philox block (perf-mode stream), counter = (c0, c1, c2, c3),
+ * key = seed.  fp64: one pair (z[0], z[1]) from 53-bit uniforms built of the whole block.
+ * fp32: two pairs from 24-bit uniforms — (z[0], z[1]) of words (x, z), (z[2], z[3]) of words
+ * (y, w) — so a block yields ORC_NPB = 4 normals. */
+#if !IS_F64
+static void orc_bm_f32(uint32_t a, uint32_t b, float* z0, float* z1) {
+    float u1 = (float)((a >> 8) + 1u) * 0x1p-24f;
+    float u2 = (float)(b >> 8) * 0x1p-24f;
+    float rad = sqrtf(-2.0f * rng_logf(u1));
+    float sn, cs;
+    rng_sincospif(2.0f * u2, &sn, &cs);
+    *z0 = rad * cs;
+    *z1 = rad * sn;
+}
+#endif
+void SFX(orc_normal_block)(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                           REAL* z) {
+    uint32_t c[4] = {c0, c1, c2, c3};
+    orc_philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+#if IS_F64
+    uint64_t k1 = ((uint64_t)(c[0] >> 5) << 26) | (c[1] >> 6);
+    uint64_t k2 = ((uint64_t)(c[2] >> 5) << 26) | (c[3] >> 6);
+    double u1 = (double)(k1 + 1) * 0x1p-53;
+    double u2 = (double)k2 * 0x1p-53;
+    double rad = sqrt(-2.0 * rng_log(u1));
+    double sn, cs;
+    rng_sincospi(2.0 * u2, &sn, &cs);
+    z[0] = rad * cs;
+    z[1] = rad * sn;
+#else
+    orc_bm_f32(c[0], c[2], &z[0], &z[1]);
+    orc_bm_f32(c[1], c[3], &z[2], &z[3]);
+#endif
+}
+
+/* The first pair of a block (fp64: the whole block) — the Random123-style known-answer
+ * interface of tests/test_gpu_parity.py (dmt_debug_normals). */
 void SFX(orc_normal_pair)(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                           REAL* z0, REAL* z1) {
     uint32_t c[4] = {c0, c1, c2, c3};
@@ -754,16 +791,15 @@ void orc_philox_raw(uint64_t seed, const uint32_t* ctr, uint32_t* out) {
 }
 #endif
 
-/* All perf-mode normals of one segment: Z[i*m + k] for steps i < nsteps
- * (normal n uses pair n>>1 of counter (n>>1, g, iter, salt<<1)). */
+/* All perf-mode normals of one segment: Z[i*m + k] for steps i < nsteps (normal n is
+ * entry n % ORC_NPB of block n / ORC_NPB, counter (n / ORC_NPB, g, iter, salt<<1)). */
 void SFX(orc_normals_segment)(uint64_t seed, uint32_t g, uint32_t iter, uint32_t salt,
                               int nsteps, int m, REAL* Z) {
     int n = nsteps * m;
-    for (int i = 0; i < n; i += 2) {
-        REAL z0, z1;
-        SFX(orc_normal_pair)(seed, (uint32_t)(i >> 1), g, iter, salt << 1, &z0, &z1);
-        Z[i] = z0;
-        if (i + 1 < n) Z[i + 1] = z1;
+    for (int i = 0; i < n; i += ORC_NPB) {
+        REAL zb[ORC_NPB];
+        SFX(orc_normal_block)(seed, (uint32_t)(i / ORC_NPB), g, iter, salt << 1, zb);
+        for (int e = 0; e < ORC_NPB && i + e < n; ++e) Z[i + e] = zb[e];
     }
 }
 
