@@ -404,24 +404,6 @@ __device__ __forceinline__ U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
 #define RNG_P9 0x1.af286bca1af28p-4
 #define RNG_P10 0x1.8618618618618p-4
 #define RNG_P11 0x1.642c8590b2164p-4
-#define RNG_S0 0x1.921fb54442d18p+1
-#define RNG_S1 -0x1.4abbce625be53p+2
-#define RNG_S2 0x1.466bc6775aae2p+1
-#define RNG_S3 -0x1.32d2cce62bd86p-1
-#define RNG_S4 0x1.50783487ee782p-4
-#define RNG_S5 -0x1.e3074fde8871fp-8
-#define RNG_S6 0x1.e8f434d018d63p-12
-#define RNG_S7 -0x1.6fadb9f155744p-16
-#define RNG_S8 0x1.aaec32af93359p-21
-#define RNG_C1 -0x1.3bd3cc9be45dep+2
-#define RNG_C2 0x1.03c1f081b5ac4p+2
-#define RNG_C3 -0x1.55d3c7e3cbffap+0
-#define RNG_C4 0x1.e1f506891babbp-3
-#define RNG_C5 -0x1.a6d1f2a204a8cp-6
-#define RNG_C6 0x1.f9d38a3763cc3p-10
-#define RNG_C7 -0x1.b6e24f44b128fp-14
-#define RNG_C8 0x1.20c62c2f2d7f5p-18
-#define RNG_C9 -0x1.2a0c591af8314p-23
 #define RNGF_SQRT_HALF 0x1.6a09e6p-1f
 #define RNGF_LN2_HI 0x1.62ep-1f
 #define RNGF_LN2_LO 0x1.0bfbe8p-15f
@@ -461,25 +443,6 @@ __device__ __forceinline__ double rng_log(double u) {
     const double de = (double)e;
     return __builtin_fma(de, RNG_LN2_HI, __builtin_fma(de, RNG_LN2_LO, lm));
 }
-/* sin(πx), cos(πx) for x in [0, 2]: n = rint(2x), r = x - n/2 in [-1/4, 1/4] (exact),
- * sin(πr) = r·S(r²), cos(πr) = 1 + r²·C(r²) (Taylor, Horner with fma), quadrant n mod 4. */
-__device__ __forceinline__ void rng_sincospi(double x, double* sn, double* cs) {
-    const double n = __builtin_rint(2.0 * x);
-    const double r = __builtin_fma(-0.5, n, x);
-    const double z = r * r;
-    double sp = RNG_S8;
-    sp = __builtin_fma(sp, z, RNG_S7); sp = __builtin_fma(sp, z, RNG_S6); sp = __builtin_fma(sp, z, RNG_S5);
-    sp = __builtin_fma(sp, z, RNG_S4); sp = __builtin_fma(sp, z, RNG_S3); sp = __builtin_fma(sp, z, RNG_S2);
-    sp = __builtin_fma(sp, z, RNG_S1); sp = __builtin_fma(sp, z, RNG_S0);
-    double cp = RNG_C9;
-    cp = __builtin_fma(cp, z, RNG_C8); cp = __builtin_fma(cp, z, RNG_C7); cp = __builtin_fma(cp, z, RNG_C6);
-    cp = __builtin_fma(cp, z, RNG_C5); cp = __builtin_fma(cp, z, RNG_C4); cp = __builtin_fma(cp, z, RNG_C3);
-    cp = __builtin_fma(cp, z, RNG_C2); cp = __builtin_fma(cp, z, RNG_C1);
-    const double s0 = r * sp, c0 = __builtin_fma(cp, z, 1.0);
-    const int q = (int)n & 3;
-    *sn = q == 0 ? s0 : q == 1 ? c0 : q == 2 ? -s0 : -c0;
-    *cs = q == 0 ? c0 : q == 1 ? -s0 : q == 2 ? -c0 : s0;
-}
 __device__ __forceinline__ float rng_logf(float u) {
     int e;
     float m = __builtin_frexpf(u, &e);
@@ -512,14 +475,61 @@ __device__ __forceinline__ void rng_sincospif(float x, float* sn, float* cs) {
     *cs = q == 0 ? c0 : q == 1 ? -s0 : q == 2 ? -c0 : s0;
 }
 
+// ---- fp64 Box–Muller kernels: table-driven (scripts/gen_bm_tables.py), no division, short
+// dependency chains.  The fp64 normals are the dominant VALU cost of the OU MCMC kernels (C2:
+// Box–Muller ≈ 45 % of k_mcmc_resident_pc's producer wave); the atanh-series rng_log with its
+// division and the degree-17/18 sincospi took ≈ 1.6× the instructions.
+#include "dmt_bm_tables.inc"
+__constant__ double kBmLog[128][2] = DMT_BM_LOG_TABLE;
+__constant__ double kBmSc[65][2] = DMT_BM_SC_TABLE;
+
+/* log(u), u in [2^-53, 1]: u = m·2^e, m in [1, 2), j = top 7 mantissa bits; j < 64:
+ * r = fma(m, c_j, -1), log u = e·ln2 + (L_j + log1p(r)); j >= 64: the same with e + 1 (c_j, L_j
+ * relative to the interval's right end over 2); log1p(r) = fma(r², Q(r), r), Q Horner. */
+__device__ __forceinline__ double bm_log(double u) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, u);
+  const uint32_t hi = (uint32_t)(b >> 32);
+  const int j = (int)((hi >> 13) & 0x7fu);
+  const int e = (int)((hi >> 20) & 0x7ffu) - 1023 + (j >> 6);
+  const double m = __builtin_bit_cast(double, (b & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull);
+  const double cj = kBmLog[j][0], Lj = kBmLog[j][1];
+  const double r = __builtin_fma(m, cj, -1.0);
+  const double r2 = r * r;
+  double q = DMT_BM_Q6;
+  q = __builtin_fma(q, r, DMT_BM_Q5); q = __builtin_fma(q, r, DMT_BM_Q4);
+  q = __builtin_fma(q, r, DMT_BM_Q3); q = __builtin_fma(q, r, DMT_BM_Q2);
+  q = __builtin_fma(q, r, DMT_BM_Q1); q = __builtin_fma(q, r, DMT_BM_Q0);
+  const double lm = Lj + __builtin_fma(r2, q, r);
+  const double de = (double)e;
+  return __builtin_fma(de, RNG_LN2_HI, __builtin_fma(de, RNG_LN2_LO, lm));
+}
+/* sin(πx), cos(πx), x in [0, 2]: n = rint(32x), r = x - n/32 (exact), angle addition with
+ * (S_n, C_n) = (sin, cos)(πn/32) from the table, sin(πr) = r·SP(r²), cos(πr) = fma(r², CP(r²), 1). */
+__device__ __forceinline__ void bm_sincospi(double x, double* sn, double* cs) {
+  const double n = __builtin_rint(32.0 * x);
+  const double r = __builtin_fma(-0x1p-5, n, x);
+  const double z = r * r;
+  double sp = DMT_BM_S4;
+  sp = __builtin_fma(sp, z, DMT_BM_S3); sp = __builtin_fma(sp, z, DMT_BM_S2);
+  sp = __builtin_fma(sp, z, DMT_BM_S1); sp = __builtin_fma(sp, z, DMT_BM_S0);
+  double cp = DMT_BM_C3;
+  cp = __builtin_fma(cp, z, DMT_BM_C2); cp = __builtin_fma(cp, z, DMT_BM_C1);
+  cp = __builtin_fma(cp, z, DMT_BM_C0);
+  const double sr = r * sp, cr = __builtin_fma(cp, z, 1.0);
+  const int k = (int)n;
+  const double Sn = kBmSc[k][0], Cn = kBmSc[k][1];
+  *sn = __builtin_fma(Sn, cr, Cn * sr);
+  *cs = __builtin_fma(Cn, cr, -(Sn * sr));
+}
+
 __device__ __forceinline__ void normal_pair(U4 o, double& z0, double& z1) {
   uint64_t k1 = ((uint64_t)(o.x >> 5) << 26) | (o.y >> 6);
   uint64_t k2 = ((uint64_t)(o.z >> 5) << 26) | (o.w >> 6);
   double u1 = (double)(k1 + 1) * 0x1p-53;
   double u2 = (double)k2 * 0x1p-53;
-  double rad = sqrt(-2.0 * rng_log(u1));
+  double rad = sqrt(-2.0 * bm_log(u1));
   double s, c;
-  rng_sincospi(2.0 * u2, &s, &c);
+  bm_sincospi(2.0 * u2, &s, &c);
   z0 = rad * c;
   z1 = rad * s;
 }

@@ -1398,8 +1398,9 @@ __device__ __forceinline__ bool arrive_last(unsigned* cnt, unsigned expect, int*
 }
 
 // nodes: node1 [rows][ng] then node2 [rows][ng2]; counters: [ng2] group counters then the top
-// counter, zero on entry and left zero
-template <int WPB>
+// counter, zero on entry and left zero.  WPB = blocks (tree leaves) per workgroup, NW = waves
+// per workgroup (every thread of the workgroup calls this)
+template <int WPB, int NW = WPB>
 __device__ __forceinline__ void persistent_tree_tail(const double* __restrict__ part,
                                                      double* __restrict__ nodes, int64_t nb,
                                                      int64_t n_iter,
@@ -1407,7 +1408,7 @@ __device__ __forceinline__ void persistent_tree_tail(const double* __restrict__ 
                                                      double* __restrict__ out3) {
   __shared__ int s_flag;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  constexpr int NT = 64 * WPB;
+  constexpr int NT = 64 * NW;
   const int64_t ng = (nb + WPB - 1) / WPB, ng2 = (ng + kTreeGroup - 1) / kTreeGroup;
   const int64_t x = blockIdx.x, g = x / kTreeGroup, rows = 3 * n_iter;
   double* node1 = nodes;
@@ -1454,7 +1455,7 @@ __device__ __forceinline__ void persistent_tree_tail(const double* __restrict__ 
   // ---- level 3: every row's group nodes, zero-padded
   if (ng2 <= 64) {
     constexpr int RB = 8;  // rows per wave per batch (loads in flight)
-    for (int64_t r0 = (int64_t)wv * RB; r0 < rows; r0 += (int64_t)WPB * RB) {
+    for (int64_t r0 = (int64_t)wv * RB; r0 < rows; r0 += (int64_t)NW * RB) {
       double v[RB];
 #pragma unroll
       for (int b = 0; b < RB; ++b) {
@@ -1475,7 +1476,7 @@ __device__ __forceinline__ void persistent_tree_tail(const double* __restrict__ 
     while (P < ng2) P <<= 1;
     const int64_t run = P / 64;
     constexpr int kLv = 24;
-    for (int64_t row = wv; row < rows; row += WPB) {
+    for (int64_t row = wv; row < rows; row += NW) {
       double stk[kLv];
 #pragma unroll
       for (int l = 0; l < kLv; ++l) stk[l] = 0.0;
@@ -1905,6 +1906,414 @@ __global__ __launch_bounds__(256, 1) void k_mcmc_resident(const BlockArgs<T> a,
   if (blk < a.b1) resident_block<Mdl, T, MODE_PCN, true>(a, c, iter0, n_iter, part, blk, lds[w]);
   persistent_tree_tail<4>(part, nodes, a.b1 - a.b0, n_iter, counter, out3);
 #endif
+}
+
+// ---- k_mcmc_resident split over two waves per block (producer / consumer).
+// One wave per block leaves one wave per SIMD for C2's 1 024 blocks: a lone wave issues a VALU
+// instruction every 4 cycles at best and exposes every LDS / cross-lane latency (SQ counters:
+// VALU active 0.58 of wave cycles).  Here each block has two waves on the same arithmetic:
+//   producer — the normals of the NEXT iteration (Philox4x32-10 + Box–Muller, ≈ 60 % of the
+//              single-wave kernel's VALU), u's Wiener increments (register-resident, updated by
+//              the decision), the pCN increments dW° = fma(ρ, dW, √(1−ρ²)·(√dt·Z)) → LDS (run
+//              order, the consumer's layout), and the coalesced W° stores;
+//   consumer — everything else of resident_block: e maps, run maps, the scan, the points, G and
+//              its trees, the X° stores, the MH decision (→ LDS for the producer).
+// Two workgroup barriers per iteration: B1 (dW° of iteration n ready) and B2 (decision n
+// made).  Between B1 and B2 the producer draws iteration n+1's normals while the consumer runs
+// iteration n, so the two waves of every SIMD issue concurrently.  The operations and their
+// order are resident_block's: bit-identical results (the GPU tests run both).
+#ifndef DMT_PC_DRAW_GROUP
+#define DMT_PC_DRAW_GROUP 1
+#endif
+template <int D, int M, class T>
+struct ResPcLds {
+  ResLds<D, M, T> r;  // pt: X° staging; dw: the dW° hand-off and W° staging; hf: H_i, F_i
+  int acc;            // the consumer's decision of the current iteration
+};
+
+template <class Mdl, class T>
+__device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, const AcceptArgs& c,
+                                                     const int64_t iter0, const int64_t n_iter,
+                                                     double* __restrict__ part, const int64_t blk,
+                                                     const bool valid,
+                                                     ResPcLds<Mdl::D, Mdl::M, T>& P) {
+  constexpr int D = Mdl::D, M = Mdl::M, HP = D * (D + 1) / 2;
+  ResLds<D, M, T>& S = P.r;
+  const int lane = threadIdx.x & 63;
+  const int64_t vb = valid ? blk : a.b0;  // an idle wave reads a valid block's metadata
+  const BlkInfo* bi = a.binfo + vb;
+  const int64_t tq = ldc(&bi->tq);
+  const int g = ldc(&bi->g0);
+  const int q0 = ldc(&bi->q0);
+  const bool term = ldc(&bi->term) != 0;
+  const int nst = ldc(a.seg_np + g) - 1;  // ≤ kSChunk
+  const int64_t row = tq + q0;
+  const int kind = term ? 0 : 1;
+  const int ls = (kind ? ldc(a.selPPB + g) : ldc(a.selPP + g)) ^ a.law_flip;
+  Law<Mdl, T> LA;
+  LA.load(a.law[ls][kind] + (int64_t)g * DMT_LAW_STRIDE);
+  const T* tb = a.t_shared ? a.t + q0 : a.t + row;
+  const T* Hb = a.H_shared[ls][kind] ? a.H[ls][kind] + (int64_t)q0 * HP : a.H[ls][kind] + row * HP;
+  const T* Fb = a.F[ls][kind] + row * D;
+  SelMask sel{(uint64_t)(a.selX[g] & 1), (uint64_t)(a.selW[g] & 1), g};
+  T* const Xd[2] = {a.X[0] + row * D, a.X[1] + row * D};
+  T x0[D], llobs;
+  {
+    const T* Xs = a.X[sel.x(g) ^ a.xs_flip] + row * D;
+    const int lsp = ldc(a.selPP + g) ^ a.law_flip;
+    T H0[HP], F0[D];
+#pragma unroll
+    for (int p = 0; p < D; ++p) x0[p] = Xs[p];
+#pragma unroll
+    for (int cc = 0; cc < HP; ++cc)
+      H0[cc] = a.H_shared[lsp][0] ? a.H[lsp][0][(int64_t)q0 * HP + cc] : a.H[lsp][0][row * HP + cc];
+#pragma unroll
+    for (int cc = 0; cc < D; ++cc) F0[cc] = a.F[lsp][0][row * D + cc];
+    const T c00 = (T)ldc(a.law[lsp][0] + (int64_t)g * DMT_LAW_STRIDE + DMT_LAW_C0);
+    llobs = obs_term<D, T>(H0, F0, x0, c00);
+  }
+  const int nv = max(0, min(kRun, nst - kRun * lane));
+  T Ac[kRun][D * D], dts[kRun];
+#pragma unroll
+  for (int r = 0; r < kRun; ++r) {
+    const int s = min(kRun * lane + r, nst - 1);
+    dts[r] = tb[s + 1] - tb[s];
+    T Hs[HP], Fs[D];
+#pragma unroll
+    for (int cc = 0; cc < HP; ++cc) Hs[cc] = Hb[(int64_t)s * HP + cc];
+#pragma unroll
+    for (int cc = 0; cc < D; ++cc) Fs[cc] = Fb[(int64_t)s * D + cc];
+    T Mg[D * D], cg_unused[D], zero[D] = {}, e_unused[D];
+    guide_coeffs<Mdl, T>(LA, Hs, Fs, Mg, cg_unused);
+#pragma unroll
+    for (int cc = 0; cc < HP; ++cc) S.hf[r][cc][lane] = Hs[cc];
+#pragma unroll
+    for (int cc = 0; cc < D; ++cc) S.hf[r][HP + cc][lane] = Fs[cc];
+    affine_step<D, T>(Mg, cg_unused, dts[r], zero, Ac[r], e_unused);
+  }
+  const uint64_t all = 1;
+  double ll = valid ? c.ll[blk] : 0.0, llp = 0.0;
+  const int64_t nb = a.b1 - a.b0, j = blk - a.b0;
+  const int last_lane = (nst - 1) / kRun;
+  double Ev = 0.0;
+  __syncthreads();  // B1 of iteration 0
+  for (int64_t r0 = 0; r0 < n_iter; ++r0) {
+    const int64_t it = iter0 + r0;
+    if ((r0 & 63) == 0)
+      Ev = exp1_draw(c.seed, (uint32_t)g + c.seg_base, (uint32_t)(it + c.key_delta + lane), c.salt);
+    const double E = __builtin_bit_cast(
+        double, ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(
+                     (int)(__builtin_bit_cast(uint64_t, Ev) >> 32), (int)(r0 & 63)) << 32) |
+                    (uint32_t)__builtin_amdgcn_readlane((int)__builtin_bit_cast(uint64_t, Ev),
+                                                        (int)(r0 & 63)));
+    T* const Xdb = (sel.x(g) ^ a.xd_flip) ? Xd[1] : Xd[0];
+    // the run map of the e maps the producer left in the steps' pt slots
+    T RA[D * D], Re[D];
+#pragma unroll
+    for (int r = 0; r < kRun; ++r) {
+      const int li = lds_ix(kRun * lane + r);
+      T er[D];
+#pragma unroll
+      for (int p = 0; p < D; ++p) er[p] = S.pt[li][p];
+      if (r == 0) {
+#pragma unroll
+        for (int cc = 0; cc < D * D; ++cc) RA[cc] = Ac[0][cc];
+#pragma unroll
+        for (int p = 0; p < D; ++p) Re[p] = er[p];
+      } else {
+        T An[D * D], en[D];
+        affine_compose<D, T>(Ac[r], er, RA, Re, An, en);
+#pragma unroll
+        for (int cc = 0; cc < D * D; ++cc) RA[cc] = An[cc];
+#pragma unroll
+        for (int p = 0; p < D; ++p) Re[p] = en[p];
+      }
+    }
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      T Ap[D * D], ep[D], An[D * D], en[D];
+      const int src = 4 * (lane - o);
+#pragma unroll
+      for (int cc = 0; cc < D * D; ++cc) Ap[cc] = lane_read(RA[cc], src);
+#pragma unroll
+      for (int p = 0; p < D; ++p) ep[p] = lane_read(Re[p], src);
+      affine_compose<D, T>(RA, Re, Ap, ep, An, en);
+      const bool take = lane >= o;
+#pragma unroll
+      for (int cc = 0; cc < D * D; ++cc) RA[cc] = take ? An[cc] : RA[cc];
+#pragma unroll
+      for (int p = 0; p < D; ++p) Re[p] = take ? en[p] : Re[p];
+    }
+    T x[D];
+    {
+      T y[D];
+      affine_apply<D, T>(RA, Re, x0, y);
+#pragma unroll
+      for (int p = 0; p < D; ++p) {
+        const T up = lane_read(y[p], 4 * (lane - 1));
+        x[p] = lane == 0 ? x0[p] : up;
+      }
+    }
+    T gl[kRun];
+#pragma unroll
+    for (int r = 0; r < kRun; ++r) {
+      const int li = lds_ix(kRun * lane + r);
+      const bool v = r < nv;
+      T rr[D], bb[D], Hr[HP], Fr[D], er[D];
+#pragma unroll
+      for (int cc = 0; cc < HP; ++cc) Hr[cc] = S.hf[r][cc][lane];
+#pragma unroll
+      for (int cc = 0; cc < D; ++cc) Fr[cc] = S.hf[r][HP + cc][lane];
+#pragma unroll
+      for (int p = 0; p < D; ++p) er[p] = S.pt[li][p];
+      const T G = g_at<Mdl, T>(LA, Hr, Fr, x, rr, bb);
+      gl[r] = v ? G * dts[r] : (T)0;
+#pragma unroll
+      for (int p = 0; p < D; ++p) S.pt[li][p] = x[p];
+      T xn[D];
+      affine_apply<D, T>(Ac[r], er, x, xn);
+#pragma unroll
+      for (int p = 0; p < D; ++p) x[p] = v ? xn[p] : x[p];
+    }
+    T xe[D];
+#pragma unroll
+    for (int p = 0; p < D; ++p) xe[p] = lane_read(x[p], 4 * last_lane);
+    T tsum = ((gl[0] + gl[1]) + (gl[2] + gl[3])) + ((gl[4] + gl[5]) + (gl[6] + gl[7]));
+    tsum = group_tree_sum<8, T>(tsum);
+    T seg_acc = (T)0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (64 * q < nst) seg_acc = seg_acc + (lane_read(tsum, 4 * 8 * q) + (T)0);
+    wave_lds_sync();
+    if (valid) {
+#pragma unroll
+      for (int k = 0; k < kRun; ++k) {
+        const int s = 64 * k + lane;
+        if (s < nst) {
+          T xv[D];
+#pragma unroll
+          for (int p = 0; p < D; ++p) xv[p] = S.pt[lds_ix(s)][p];
+          store_row<D, T>(Xdb + (int64_t)s * D, xv);
+        }
+      }
+      if (lane == 0) store_row<D, T>(Xdb + (int64_t)nst * D, xe);
+    }
+    bool sok = isfinite(seg_acc);
+#pragma unroll
+    for (int p = 0; p < D; ++p) sok = sok && isfinite(xe[p]);
+    llp = sok ? (double)(llobs + seg_acc) : -INFINITY;
+    const bool acc = valid && E > -(llp - ll);
+    if (acc) {
+      sel.mx ^= all;
+      sel.mw ^= all;
+    }
+    if (lane == 0) {
+      P.acc = acc ? 1 : 0;
+      if (valid) {
+        if (c.hist_len > 0) {
+          const int64_t o = (it - 1) * c.nblocks + blk;
+          c.acc_hist[o] = acc ? 1 : 0;
+          c.ll_hist[o] = ll;
+          c.llp_hist[o] = llp;
+        }
+        part[(3 * r0 + 0) * nb + j] = acc ? llp : ll;
+        part[(3 * r0 + 1) * nb + j] = acc ? ll : llp;
+        part[(3 * r0 + 2) * nb + j] = acc ? 1.0 : 0.0;
+      }
+    }
+    if (acc) {
+      const double t = ll;
+      ll = llp;
+      llp = t;
+    }
+    __syncthreads();  // B2: decision n → producer; pt reads of this iteration done
+    if (r0 + 1 < n_iter) __syncthreads();  // B1: dW° of iteration n + 1 ready
+  }
+  if (valid && lane == 0) {
+    a.selX[g] = (uint8_t)sel.x(g);
+    a.selW[g] = (uint8_t)sel.w(g);
+    c.ll[blk] = ll;
+    c.llp[blk] = llp;
+  }
+}
+
+template <class Mdl, class T>
+__device__ __forceinline__ void resident_pc_producer(const BlockArgs<T>& a, const AcceptArgs& c,
+                                                     const int64_t iter0, const int64_t n_iter,
+                                                     const int64_t blk, const bool valid,
+                                                     ResPcLds<Mdl::D, Mdl::M, T>& P) {
+  constexpr int D = Mdl::D, M = Mdl::M, HP = D * (D + 1) / 2;
+  ResLds<D, M, T>& S = P.r;
+  const int lane = threadIdx.x & 63;
+  const int64_t vb = valid ? blk : a.b0;
+  const BlkInfo* bi = a.binfo + vb;
+  const int64_t tq = ldc(&bi->tq);
+  const int g = ldc(&bi->g0);
+  const int q0 = ldc(&bi->q0);
+  const T rho = (T)ldc(&bi->rho);
+  const T srho = (T)ldc(&bi->srho);
+  const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32), c3 = a.salt << 1;
+  const int nst = ldc(a.seg_np + g) - 1;
+  const int64_t row = tq + q0;
+  const bool term = ldc(&bi->term) != 0;
+  const int kind = term ? 0 : 1;
+  const int ls = (kind ? ldc(a.selPPB + g) : ldc(a.selPP + g)) ^ a.law_flip;
+  Law<Mdl, T> LA;
+  LA.load(a.law[ls][kind] + (int64_t)g * DMT_LAW_STRIDE);
+  const T* tb = a.t_shared ? a.t + q0 : a.t + row;
+  const T* Hb = a.H_shared[ls][kind] ? a.H[ls][kind] + (int64_t)q0 * HP : a.H[ls][kind] + row * HP;
+  const T* Fb = a.F[ls][kind] + row * D;
+  SelMask sel{(uint64_t)(a.selX[g] & 1), (uint64_t)(a.selW[g] & 1), g};
+  T* const Wd[2] = {a.W[0] + row * M, a.W[1] + row * M};
+  T w0[M], dts[kRun], sdts[kRun], wv[kRun][M], cgs[kRun][D];
+  {
+    const T* Ws = a.W[sel.w(g) ^ a.ws_flip] + row * M;
+#pragma unroll
+    for (int k = 0; k < M; ++k) w0[k] = Ws[k];
+#pragma unroll
+    for (int r = 0; r < kRun; ++r) {
+      const int s = min(kRun * lane + r, nst - 1);
+      dts[r] = tb[s + 1] - tb[s];
+      sdts[r] = sqrt(dts[r]);
+#pragma unroll
+      for (int k = 0; k < M; ++k) wv[r][k] = Ws[(int64_t)(s + 1) * M + k];
+      T Hs[HP], Fs[D], Mg_unused[D * D];
+#pragma unroll
+      for (int cc = 0; cc < HP; ++cc) Hs[cc] = Hb[(int64_t)s * HP + cc];
+#pragma unroll
+      for (int cc = 0; cc < D; ++cc) Fs[cc] = Fb[(int64_t)s * D + cc];
+      guide_coeffs<Mdl, T>(LA, Hs, Fs, Mg_unused, cgs[r]);
+    }
+  }
+  const double* Zg = a.Z ? a.Z + ldc(a.st_off + g) * M : nullptr;  // parity-mode normals
+  auto draw_z = [&](uint32_t itv, T (&z)[kRun][M]) {
+    if (Zg) {
+#pragma unroll
+      for (int r = 0; r < kRun; ++r)
+#pragma unroll
+        for (int kk = 0; kk < M; ++kk) z[r][kk] = (T)Zg[(int64_t)min(kRun * lane + r, nst - 1) * M + kk];
+      return;
+    }
+    constexpr int NPB = NormPerBlock<T>::v, NB = kRun * M / NPB;
+    static_assert((kRun * M) % NPB == 0, "a run must hold whole normal blocks");
+    T zz[kRun * M];
+    // the blocks' first counter words are loop-invariant: derived from an opaque copy of the
+    // lane id so that the compiler does not hoist every block's first Philox round (or the
+    // words themselves) out of the iteration loop into spilled registers
+    uint32_t ln = (uint32_t)lane;
+    asm volatile("" : "+v"(ln));
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+#if defined(DMT_PROBE_NO_BM)  // timing probes only (wrong normals): Philox without Box–Muller
+      {
+        const U4 o = philox4x32_10(U4{NB * ln + q, (uint32_t)g + a.seg_base, itv, c3}, k0, k1);
+        zz[NPB * q] = (T)(o.x ^ o.y) * (T)0x1p-32;
+        zz[NPB * q + 1] = (T)(o.z ^ o.w) * (T)0x1p-32;
+      }
+#elif defined(DMT_PROBE_NO_PHILOX)  // Box–Muller without Philox
+      normal_block(U4{NB * ln + q ^ itv, (NB * ln + q) * 0x9E3779B9u ^ itv, itv * 3u + q, c3 ^ ln},
+                   zz + NPB * q);
+#else
+      normal_block(philox4x32_10(U4{NB * ln + q, (uint32_t)g + a.seg_base, itv, c3}, k0, k1),
+                   zz + NPB * q);
+#endif
+      // DMT_PC_DRAW_GROUP Philox blocks + Box–Muller interleaved at a time
+      if ((q + 1) % DMT_PC_DRAW_GROUP == 0) __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int r = 0; r < kRun; ++r)
+#pragma unroll
+      for (int kk = 0; kk < M; ++kk) z[r][kk] = zz[r * M + kk];
+  };
+  T z[kRun][M], w0n[M];
+  // dW° of the iteration whose normals are in z → dw slots, its e maps
+  // e_i = fma(c_i, dt_i, σ·dW°_i) → pt slots (run order), w0n = ρ·W(t0)
+  auto propose = [&]() {
+#pragma unroll
+    for (int r = 0; r < kRun; ++r) {
+      const int li = lds_ix(kRun * lane + r);
+      T dW[M], sdW[D];
+#pragma unroll
+      for (int kk = 0; kk < M; ++kk) {
+        dW[kk] = dfma(rho, wv[r][kk], srho * (sdts[r] * z[r][kk]));
+        S.dw[li][kk] = dW[kk];
+      }
+      sigma_dw<Mdl, T>(LA, dW, sdW);
+#pragma unroll
+      for (int p = 0; p < D; ++p) S.pt[li][p] = dfma(cgs[r][p], dts[r], sdW[p]);
+    }
+#pragma unroll
+    for (int k = 0; k < M; ++k) w0n[k] = rho * w0[k];
+  };
+  // coalesced W° stores of the proposal just handed over (after B1)
+  auto store_w = [&]() {
+    if (!valid) return;
+    T* const Wdb = (sel.w(g) ^ a.wd_flip) ? Wd[1] : Wd[0];
+#pragma unroll
+    for (int k = 0; k < kRun; ++k) {
+      const int s = 64 * k + lane;
+      if (s < nst) {
+        T wd[M];
+#pragma unroll
+        for (int kk = 0; kk < M; ++kk) wd[kk] = S.dw[lds_ix(s)][kk];
+        store_row<M, T>(Wdb + (int64_t)(s + 1) * M, wd);
+      }
+    }
+    if (lane == 0) store_row<M, T>(Wdb, w0n);
+  };
+  draw_z((uint32_t)(iter0 + c.key_delta), z);
+  propose();
+  __syncthreads();  // B1 of iteration 0
+  store_w();
+  for (int64_t r0 = 0; r0 < n_iter; ++r0) {
+    const bool more = r0 + 1 < n_iter;
+    if (more) draw_z((uint32_t)(iter0 + r0 + 1 + c.key_delta), z);
+    __syncthreads();  // B2: decision n
+    if (P.acc) {  // u's increments ← the accepted proposal's, still in the dw slots
+      sel.mx ^= 1;
+      sel.mw ^= 1;
+#pragma unroll
+      for (int r = 0; r < kRun; ++r)
+#pragma unroll
+        for (int k = 0; k < M; ++k) wv[r][k] = S.dw[lds_ix(kRun * lane + r)][k];
+#pragma unroll
+      for (int k = 0; k < M; ++k) w0[k] = w0n[k];
+    }
+    if (more) {
+      propose();
+      __syncthreads();  // B1: dW° of iteration n + 1 ready
+      store_w();
+    }
+  }
+}
+
+template <class Mdl, class T>
+__global__ __launch_bounds__(512, 1) void k_mcmc_resident_pc(const BlockArgs<T> a,
+                                                             const AcceptArgs c,
+                                                             const int64_t iter0,
+                                                             const int64_t n_iter,
+                                                             double* __restrict__ part,
+                                                             double* __restrict__ nodes,
+                                                             unsigned* __restrict__ counter,
+                                                             double* __restrict__ out3) {
+  __shared__ ResPcLds<Mdl::D, Mdl::M, T> lds[4];
+  if (n_iter <= 0) return;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t blk = a.b0 + (int64_t)blockIdx.x * 4 + (w & 3);
+  const bool valid = blk < a.b1;
+#if defined(DMT_PC_STUB_P)  // register-budget probes (scripts/res_usage.sh): one role only
+  if (w < 4) resident_pc_consumer<Mdl, T>(a, c, iter0, n_iter, part, blk, valid, lds[w & 3]);
+  else for (int64_t i = 0; i < 2 * n_iter; ++i) __syncthreads();
+#elif defined(DMT_PC_STUB_C)
+  if (w >= 4) resident_pc_producer<Mdl, T>(a, c, iter0, n_iter, blk, valid, lds[w & 3]);
+  else for (int64_t i = 0; i < 2 * n_iter; ++i) __syncthreads();
+#else
+  if (w < 4)
+    resident_pc_consumer<Mdl, T>(a, c, iter0, n_iter, part, blk, valid, lds[w & 3]);
+  else
+    resident_pc_producer<Mdl, T>(a, c, iter0, n_iter, blk, valid, lds[w & 3]);
+#endif
+  persistent_tree_tail<4, 8>(part, nodes, a.b1 - a.b0, n_iter, counter, out3);
 }
 
 // One draw / re-solve (dmt_draw_proposal, dmt_draw_unit, dmt_recompute_path) of single-segment
@@ -3218,6 +3627,11 @@ static hipError_t launch_mcmc_t(const void* args, const AcceptArgs& c, int64_t i
     // part[n][3][nwaves], then the tree nodes [n][3][ceil(nwaves / WPB)] (dmt_mcmc_run sizes it)
     double* nodes = part + 3 * n * nwaves;
     if constexpr (Mdl::D <= 2) {
+      if (resident == 2) {  // producer / consumer waves (k_mcmc_resident_pc)
+        dlaunch(k_mcmc_resident_pc<Mdl, T>, dim3((unsigned)((nwaves + 3) / 4)), dim3(512), s, a,
+                c, iter0, n, part, nodes, counter, out3);
+        return hipGetLastError();
+      }
       if (resident) {
         dlaunch(k_mcmc_resident<Mdl, T>, dim3((unsigned)((nwaves + 3) / 4)), dim3(256), s, a, c,
                 iter0, n, part, nodes, counter, out3);

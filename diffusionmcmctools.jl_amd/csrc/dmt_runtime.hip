@@ -163,6 +163,7 @@ struct dmt_ens {
   int64_t part_cap = 0;
   bool persist = true;       // dmt_mcmc_run of a linear drift in one launch (DMT_MCMC_PERSIST=0: off)
   bool resident = true;      // ... with register-resident block state when eligible (DMT_MCMC_RESIDENT=0: off)
+  bool resident_pc = true;   // ... split over a producer and a consumer wave per block (DMT_MCMC_PC=0: one wave)
   int lane_split = -1;       // MAP_LANE draws on producer/consumer waves: 1 on, 0 off, -1 auto
                              // (when the draw has fewer waves than the device has SIMDs)
   int64_t n_simd = 1024;
@@ -690,6 +691,7 @@ dmt_status dmt_create(dmt_ens** out, const dmt_model* model, const dmt_structure
   if (model->model == DMT_MODEL_OU) h->mapping = MAP_WAVE;
   if (const char* e = std::getenv("DMT_MCMC_PERSIST")) h->persist = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("DMT_MCMC_RESIDENT")) h->resident = std::strcmp(e, "0") != 0;
+  if (const char* e = std::getenv("DMT_MCMC_PC")) h->resident_pc = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("DMT_LANE_SPLIT")) h->lane_split = std::atoi(e);
   if (const char* e = std::getenv("DMT_REPAIR_DIV")) h->repair_div = std::max(1, std::atoi(e));
   if (const char* e = std::getenv("DMT_SCAN_RESIDENT")) h->scan_resident = std::strcmp(e, "0") != 0;
@@ -1262,12 +1264,14 @@ dmt_status dmt_mcmc_run(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int6
         if (h->key.precision == DMT_F64) {
           BlockArgs<double> a{};
           fill(a);
-          e = launch_mcmc_persistent(h->key, &a, c, iter0 + i0, n, h->d_part, nb, resident,
+          e = launch_mcmc_persistent(h->key, &a, c, iter0 + i0, n, h->d_part, nb,
+                                     resident ? (h->resident_pc ? 2 : 1) : 0,
                                      run_out + 3 * i0, (unsigned*)counter, h->stream);
         } else {
           BlockArgs<float> a{};
           fill(a);
-          e = launch_mcmc_persistent(h->key, &a, c, iter0 + i0, n, h->d_part, nb, resident,
+          e = launch_mcmc_persistent(h->key, &a, c, iter0 + i0, n, h->d_part, nb,
+                                     resident ? (h->resident_pc ? 2 : 1) : 0,
                                      run_out + 3 * i0, (unsigned*)counter, h->stream);
         }
       }

@@ -595,24 +595,6 @@ void orc_philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1);
 #define RNG_P9 0x1.af286bca1af28p-4
 #define RNG_P10 0x1.8618618618618p-4
 #define RNG_P11 0x1.642c8590b2164p-4
-#define RNG_S0 0x1.921fb54442d18p+1
-#define RNG_S1 -0x1.4abbce625be53p+2
-#define RNG_S2 0x1.466bc6775aae2p+1
-#define RNG_S3 -0x1.32d2cce62bd86p-1
-#define RNG_S4 0x1.50783487ee782p-4
-#define RNG_S5 -0x1.e3074fde8871fp-8
-#define RNG_S6 0x1.e8f434d018d63p-12
-#define RNG_S7 -0x1.6fadb9f155744p-16
-#define RNG_S8 0x1.aaec32af93359p-21
-#define RNG_C1 -0x1.3bd3cc9be45dep+2
-#define RNG_C2 0x1.03c1f081b5ac4p+2
-#define RNG_C3 -0x1.55d3c7e3cbffap+0
-#define RNG_C4 0x1.e1f506891babbp-3
-#define RNG_C5 -0x1.a6d1f2a204a8cp-6
-#define RNG_C6 0x1.f9d38a3763cc3p-10
-#define RNG_C7 -0x1.b6e24f44b128fp-14
-#define RNG_C8 0x1.20c62c2f2d7f5p-18
-#define RNG_C9 -0x1.2a0c591af8314p-23
 #define RNGF_SQRT_HALF 0x1.6a09e6p-1f
 #define RNGF_LN2_HI 0x1.62ep-1f
 #define RNGF_LN2_LO 0x1.0bfbe8p-15f
@@ -652,25 +634,6 @@ static inline double rng_log(double u) {
     const double de = (double)e;
     return fma(de, RNG_LN2_HI, fma(de, RNG_LN2_LO, lm));
 }
-/* sin(πx), cos(πx) for x in [0, 2]: n = rint(2x), r = x - n/2 in [-1/4, 1/4] (exact),
- * sin(πr) = r·S(r²), cos(πr) = 1 + r²·C(r²) (Taylor, Horner with fma), quadrant n mod 4. */
-static inline void rng_sincospi(double x, double* sn, double* cs) {
-    const double n = rint(2.0 * x);
-    const double r = fma(-0.5, n, x);
-    const double z = r * r;
-    double sp = RNG_S8;
-    sp = fma(sp, z, RNG_S7); sp = fma(sp, z, RNG_S6); sp = fma(sp, z, RNG_S5);
-    sp = fma(sp, z, RNG_S4); sp = fma(sp, z, RNG_S3); sp = fma(sp, z, RNG_S2);
-    sp = fma(sp, z, RNG_S1); sp = fma(sp, z, RNG_S0);
-    double cp = RNG_C9;
-    cp = fma(cp, z, RNG_C8); cp = fma(cp, z, RNG_C7); cp = fma(cp, z, RNG_C6);
-    cp = fma(cp, z, RNG_C5); cp = fma(cp, z, RNG_C4); cp = fma(cp, z, RNG_C3);
-    cp = fma(cp, z, RNG_C2); cp = fma(cp, z, RNG_C1);
-    const double s0 = r * sp, c0 = fma(cp, z, 1.0);
-    const int q = (int)n & 3;
-    *sn = q == 0 ? s0 : q == 1 ? c0 : q == 2 ? -s0 : -c0;
-    *cs = q == 0 ? c0 : q == 1 ? -s0 : q == 2 ? -c0 : s0;
-}
 static inline float rng_logf(float u) {
     int e;
     float m = frexpf(u, &e);
@@ -703,6 +666,47 @@ static inline void rng_sincospif(float x, float* sn, float* cs) {
     *cs = q == 0 ? c0 : q == 1 ? -s0 : q == 2 ? -c0 : s0;
 }
 
+#if IS_F64
+/* fp64 Box–Muller kernels (libdmt dmt_device.h bm_log / bm_sincospi, DESIGN.md §3 RNG): the
+ * tables and coefficients of scripts/gen_bm_tables.py, the same operations in the same order. */
+#include "bm_tables.inc"
+static const double bm_log_tab[128][2] = DMT_BM_LOG_TABLE;
+static const double bm_sc_tab[65][2] = DMT_BM_SC_TABLE;
+
+static inline double bm_log(double u) {
+    uint64_t b;
+    memcpy(&b, &u, 8);
+    const uint32_t hi = (uint32_t)(b >> 32);
+    const int j = (int)((hi >> 13) & 0x7fu);
+    const int e = (int)((hi >> 20) & 0x7ffu) - 1023 + (j >> 6);
+    const uint64_t mb = (b & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull;
+    double m;
+    memcpy(&m, &mb, 8);
+    const double r = fma(m, bm_log_tab[j][0], -1.0);
+    const double r2 = r * r;
+    double q = DMT_BM_Q6;
+    q = fma(q, r, DMT_BM_Q5); q = fma(q, r, DMT_BM_Q4); q = fma(q, r, DMT_BM_Q3);
+    q = fma(q, r, DMT_BM_Q2); q = fma(q, r, DMT_BM_Q1); q = fma(q, r, DMT_BM_Q0);
+    const double lm = bm_log_tab[j][1] + fma(r2, q, r);
+    const double de = (double)e;
+    return fma(de, RNG_LN2_HI, fma(de, RNG_LN2_LO, lm));
+}
+static inline void bm_sincospi(double x, double* sn, double* cs) {
+    const double n = rint(32.0 * x);
+    const double r = fma(-0x1p-5, n, x);
+    const double z = r * r;
+    double sp = DMT_BM_S4;
+    sp = fma(sp, z, DMT_BM_S3); sp = fma(sp, z, DMT_BM_S2); sp = fma(sp, z, DMT_BM_S1);
+    sp = fma(sp, z, DMT_BM_S0);
+    double cp = DMT_BM_C3;
+    cp = fma(cp, z, DMT_BM_C2); cp = fma(cp, z, DMT_BM_C1); cp = fma(cp, z, DMT_BM_C0);
+    const double sr = r * sp, cr = fma(cp, z, 1.0);
+    const int k = (int)n;
+    *sn = fma(bm_sc_tab[k][0], cr, bm_sc_tab[k][1] * sr);
+    *cs = fma(bm_sc_tab[k][1], cr, -(bm_sc_tab[k][0] * sr));
+}
+#endif
+
 /* Box–Muller normals from one Philox block (perf-mode stream), counter = (c0, c1, c2, c3),
  * key = seed.  fp64: one pair (z[0], z[1]) from 53-bit uniforms built of the whole block.
  * fp32: two pairs from 24-bit uniforms — (z[0], z[1]) of words (x, z), (z[2], z[3]) of words
@@ -727,9 +731,9 @@ void SFX(orc_normal_block)(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2,
     uint64_t k2 = ((uint64_t)(c[2] >> 5) << 26) | (c[3] >> 6);
     double u1 = (double)(k1 + 1) * 0x1p-53;
     double u2 = (double)k2 * 0x1p-53;
-    double rad = sqrt(-2.0 * rng_log(u1));
+    double rad = sqrt(-2.0 * bm_log(u1));
     double sn, cs;
-    rng_sincospi(2.0 * u2, &sn, &cs);
+    bm_sincospi(2.0 * u2, &sn, &cs);
     z[0] = rad * cs;
     z[1] = rad * sn;
 #else
@@ -749,9 +753,9 @@ void SFX(orc_normal_pair)(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2, 
     uint64_t k2 = ((uint64_t)(c[2] >> 5) << 26) | (c[3] >> 6);
     double u1 = (double)(k1 + 1) * 0x1p-53;
     double u2 = (double)k2 * 0x1p-53;
-    double rad = sqrt(-2.0 * rng_log(u1));
+    double rad = sqrt(-2.0 * bm_log(u1));
     double sn, cs;
-    rng_sincospi(2.0 * u2, &sn, &cs);
+    bm_sincospi(2.0 * u2, &sn, &cs);
     *z0 = rad * cs;
     *z1 = rad * sn;
 #else
@@ -1007,4 +1011,5 @@ int orc_backward_filter_segment(int d, const double* Bt, const double* beta, con
 }
 /* the canonical log kernel, exposed for the Python container restatement */
 double orc_rng_log(double u) { return rng_log(u); }
+double orc_bm_log(double u) { return bm_log(u); }
 #endif

@@ -125,6 +125,8 @@ def _load():
     lib.orc_backward_filter_segment.restype = i_
     lib.orc_rng_log.argtypes = [d_]
     lib.orc_rng_log.restype = d_
+    lib.orc_bm_log.argtypes = [d_]
+    lib.orc_bm_log.restype = d_
     lib.orc_philox_raw.argtypes = [u64, P, P]
     lib.orc_philox_raw.restype = None
     return lib

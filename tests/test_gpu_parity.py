@@ -254,6 +254,32 @@ def test_mcmc_run_persistent_paths_equal_step_path(case):
     cs.assert_paths_equal(e0, e1)
 
 
+@pytest.mark.parametrize("case", [
+    pytest.param(("c2", 100, 60, 6), id="c2-60steps"),
+    pytest.param(("c2", 301, 500, 70), id="c2-500steps-ragged-workgroup-70iters"),
+    pytest.param(("c2", 1024, 500, 100), id="c2-full-100iters"),
+    pytest.param(("c1", 1, 200, 5), id="c1-d1"),
+])
+def test_mcmc_run_producer_consumer_equals_one_wave(case):
+    """k_mcmc_resident_pc (a producer and a consumer wave per block, the default) == the
+    one-wave k_mcmc_resident (DMT_MCMC_PC=0), bit for bit, including a partly idle last
+    workgroup (301 blocks) and a continuation run."""
+    kind, B, N, n = case
+    build = _c2_build(B, N, n + 1) if kind == "c2" else _c1_build(n + 1)
+    (e0, lay, nb), (e1, _, _) = _env_ensembles(build, {"DMT_MCMC_PC": "0"})
+    r0 = e0.mcmc_run(lay, 0, nb, 1, n)
+    r1 = e1.mcmc_run(lay, 0, nb, 1, n)
+    assert np.array_equal(r0, r1)
+    cs.assert_paths_equal(e0, e1)
+    for what in (L.BLK_LL, L.BLK_LLPROP):
+        assert np.array_equal(e0.get_block_state(lay, what, 0, nb), e1.get_block_state(lay, what, 0, nb))
+    for what in (L.BLK_ACC_HIST, L.BLK_LL_HIST, L.BLK_LLPROP_HIST):
+        assert np.array_equal(e0.get_block_state(lay, what, 0, nb, n + 1),
+                              e1.get_block_state(lay, what, 0, nb, n + 1))
+    assert np.array_equal(e0.mcmc_run(lay, 0, nb, n + 1, 1), e1.mcmc_run(lay, 0, nb, n + 1, 1))
+    cs.assert_paths_equal(e0, e1)
+
+
 def test_mcmc_run_with_failing_blocks_equals_step_path():
     """Blocks whose proposals overflow (σ = 1e160, so a = σσᵀ = inf) fail every iteration
     (ll° = −Inf, never accepted) inside dmt_mcmc_run's persistent kernel exactly as on the
