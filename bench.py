@@ -335,8 +335,10 @@ def main(argv=None):
     short1 = (w.model.kind == L.MODEL_OU and w.d <= 2
               and all(len(r) == 1 and r[0] - 1 <= 512 for r in w.n_points))
     resident = persist and short1 and os.environ.get("DMT_MCMC_RESIDENT", "1") != "0"
-    if resident:  # linear drift: all K iterations in one k_mcmc_resident launch (dmt_mcmc_run)
-        wave, kname = True, "k_mcmc_resident"
+    if resident:  # linear drift: all K iterations in one k_mcmc_resident(_pc) launch (dmt_mcmc_run)
+        wave = True
+        kname = ("k_mcmc_resident_pc" if os.environ.get("DMT_MCMC_PC", "1") != "0"
+                 else "k_mcmc_resident")
     elif persist:  # linear drift: all K iterations in one k_mcmc_scan launch (dmt_mcmc_run)
         wave, kname = True, "k_mcmc_scan"
     elif short1 and os.environ.get("DMT_SCAN_RESIDENT", "1") != "0":  # one launch per iteration
@@ -380,7 +382,9 @@ def main(argv=None):
                        "rng": "device Philox4x32-10 + Box-Muller (perf mode)"},
             "per_gpu": value / world,
             "accept_rate": accept_rate,
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS,
+            # bound: what the counters show for this kernel (issue summary), HBM otherwise
+            "roofline": {"bound": (issue or {}).get("bound", "hbm"), "achieved": achieved,
+                         "peak": PEAK_HBM_GBS,
                          "unit": "GB/s", "frac": frac, "traffic": traffic,
                          "traffic_source": traffic_src,
                          "kernel": kname + (" (draw_proposal_path! + accept_reject_proposal_path! "

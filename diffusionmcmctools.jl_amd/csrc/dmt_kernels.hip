@@ -2137,12 +2137,18 @@ __device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, cons
   }
 }
 
-template <class Mdl, class T>
+// NP producer waves per block: producer h owns the steps r in [h·RR, (h+1)·RR) of every lane's
+// run (their Philox blocks, u's increments, the pCN and e maps) and the coalesced W° rows
+// k in [h·RR, (h+1)·RR); producer 0 also W(t0).
+template <class Mdl, class T, int NP>
 __device__ __forceinline__ void resident_pc_producer(const BlockArgs<T>& a, const AcceptArgs& c,
                                                      const int64_t iter0, const int64_t n_iter,
                                                      const int64_t blk, const bool valid,
+                                                     const int h,
                                                      ResPcLds<Mdl::D, Mdl::M, T>& P) {
-  constexpr int D = Mdl::D, M = Mdl::M, HP = D * (D + 1) / 2;
+  constexpr int D = Mdl::D, M = Mdl::M, HP = D * (D + 1) / 2, RR = kRun / NP;
+  static_assert(kRun % NP == 0, "whole steps per producer");
+  const int r0h = h * RR;
   ResLds<D, M, T>& S = P.r;
   const int lane = threadIdx.x & 63;
   const int64_t vb = valid ? blk : a.b0;
@@ -2165,14 +2171,14 @@ __device__ __forceinline__ void resident_pc_producer(const BlockArgs<T>& a, cons
   const T* Fb = a.F[ls][kind] + row * D;
   SelMask sel{(uint64_t)(a.selX[g] & 1), (uint64_t)(a.selW[g] & 1), g};
   T* const Wd[2] = {a.W[0] + row * M, a.W[1] + row * M};
-  T w0[M], dts[kRun], sdts[kRun], wv[kRun][M], cgs[kRun][D];
+  T w0[M], dts[RR], sdts[RR], wv[RR][M], cgs[RR][D];
   {
     const T* Ws = a.W[sel.w(g) ^ a.ws_flip] + row * M;
 #pragma unroll
     for (int k = 0; k < M; ++k) w0[k] = Ws[k];
 #pragma unroll
-    for (int r = 0; r < kRun; ++r) {
-      const int s = min(kRun * lane + r, nst - 1);
+    for (int r = 0; r < RR; ++r) {
+      const int s = min(kRun * lane + r0h + r, nst - 1);
       dts[r] = tb[s + 1] - tb[s];
       sdts[r] = sqrt(dts[r]);
 #pragma unroll
@@ -2186,52 +2192,53 @@ __device__ __forceinline__ void resident_pc_producer(const BlockArgs<T>& a, cons
     }
   }
   const double* Zg = a.Z ? a.Z + ldc(a.st_off + g) * M : nullptr;  // parity-mode normals
-  auto draw_z = [&](uint32_t itv, T (&z)[kRun][M]) {
+  auto draw_z = [&](uint32_t itv, T (&z)[RR][M]) {
     if (Zg) {
 #pragma unroll
-      for (int r = 0; r < kRun; ++r)
+      for (int r = 0; r < RR; ++r)
 #pragma unroll
-        for (int kk = 0; kk < M; ++kk) z[r][kk] = (T)Zg[(int64_t)min(kRun * lane + r, nst - 1) * M + kk];
+        for (int kk = 0; kk < M; ++kk)
+          z[r][kk] = (T)Zg[(int64_t)min(kRun * lane + r0h + r, nst - 1) * M + kk];
       return;
     }
-    constexpr int NPB = NormPerBlock<T>::v, NB = kRun * M / NPB;
-    static_assert((kRun * M) % NPB == 0, "a run must hold whole normal blocks");
-    T zz[kRun * M];
+    constexpr int NPB = NormPerBlock<T>::v, NB = RR * M / NPB;  // this producer's blocks
+    static_assert((RR * M) % NPB == 0, "a producer's steps must hold whole normal blocks");
+    T zz[RR * M];
     // the blocks' first counter words are loop-invariant: derived from an opaque copy of the
     // lane id so that the compiler does not hoist every block's first Philox round (or the
     // words themselves) out of the iteration loop into spilled registers
-    uint32_t ln = (uint32_t)lane;
+    uint32_t ln = (uint32_t)(NP * NB * lane + h * NB);  // the run's first block of this producer
     asm volatile("" : "+v"(ln));
 #pragma unroll
     for (int q = 0; q < NB; ++q) {
 #if defined(DMT_PROBE_NO_BM)  // timing probes only (wrong normals): Philox without Box–Muller
       {
-        const U4 o = philox4x32_10(U4{NB * ln + q, (uint32_t)g + a.seg_base, itv, c3}, k0, k1);
+        const U4 o = philox4x32_10(U4{ln + q, (uint32_t)g + a.seg_base, itv, c3}, k0, k1);
         zz[NPB * q] = (T)(o.x ^ o.y) * (T)0x1p-32;
         zz[NPB * q + 1] = (T)(o.z ^ o.w) * (T)0x1p-32;
       }
 #elif defined(DMT_PROBE_NO_PHILOX)  // Box–Muller without Philox
-      normal_block(U4{NB * ln + q ^ itv, (NB * ln + q) * 0x9E3779B9u ^ itv, itv * 3u + q, c3 ^ ln},
+      normal_block(U4{(ln + q) ^ itv, (ln + q) * 0x9E3779B9u ^ itv, itv * 3u + q, c3 ^ ln},
                    zz + NPB * q);
 #else
-      normal_block(philox4x32_10(U4{NB * ln + q, (uint32_t)g + a.seg_base, itv, c3}, k0, k1),
+      normal_block(philox4x32_10(U4{ln + q, (uint32_t)g + a.seg_base, itv, c3}, k0, k1),
                    zz + NPB * q);
 #endif
       // DMT_PC_DRAW_GROUP Philox blocks + Box–Muller interleaved at a time
       if ((q + 1) % DMT_PC_DRAW_GROUP == 0) __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
-    for (int r = 0; r < kRun; ++r)
+    for (int r = 0; r < RR; ++r)
 #pragma unroll
       for (int kk = 0; kk < M; ++kk) z[r][kk] = zz[r * M + kk];
   };
-  T z[kRun][M], w0n[M];
+  T z[RR][M], w0n[M];
   // dW° of the iteration whose normals are in z → dw slots, its e maps
   // e_i = fma(c_i, dt_i, σ·dW°_i) → pt slots (run order), w0n = ρ·W(t0)
   auto propose = [&]() {
 #pragma unroll
-    for (int r = 0; r < kRun; ++r) {
-      const int li = lds_ix(kRun * lane + r);
+    for (int r = 0; r < RR; ++r) {
+      const int li = lds_ix(kRun * lane + r0h + r);
       T dW[M], sdW[D];
 #pragma unroll
       for (int kk = 0; kk < M; ++kk) {
@@ -2250,8 +2257,8 @@ __device__ __forceinline__ void resident_pc_producer(const BlockArgs<T>& a, cons
     if (!valid) return;
     T* const Wdb = (sel.w(g) ^ a.wd_flip) ? Wd[1] : Wd[0];
 #pragma unroll
-    for (int k = 0; k < kRun; ++k) {
-      const int s = 64 * k + lane;
+    for (int k = 0; k < RR; ++k) {
+      const int s = 64 * (r0h + k) + lane;
       if (s < nst) {
         T wd[M];
 #pragma unroll
@@ -2259,7 +2266,7 @@ __device__ __forceinline__ void resident_pc_producer(const BlockArgs<T>& a, cons
         store_row<M, T>(Wdb + (int64_t)(s + 1) * M, wd);
       }
     }
-    if (lane == 0) store_row<M, T>(Wdb, w0n);
+    if (h == 0 && lane == 0) store_row<M, T>(Wdb, w0n);
   };
   draw_z((uint32_t)(iter0 + c.key_delta), z);
   propose();
@@ -2273,9 +2280,9 @@ __device__ __forceinline__ void resident_pc_producer(const BlockArgs<T>& a, cons
       sel.mx ^= 1;
       sel.mw ^= 1;
 #pragma unroll
-      for (int r = 0; r < kRun; ++r)
+      for (int r = 0; r < RR; ++r)
 #pragma unroll
-        for (int k = 0; k < M; ++k) wv[r][k] = S.dw[lds_ix(kRun * lane + r)][k];
+        for (int k = 0; k < M; ++k) wv[r][k] = S.dw[lds_ix(kRun * lane + r0h + r)][k];
 #pragma unroll
       for (int k = 0; k < M; ++k) w0[k] = w0n[k];
     }
@@ -2287,33 +2294,36 @@ __device__ __forceinline__ void resident_pc_producer(const BlockArgs<T>& a, cons
   }
 }
 
-template <class Mdl, class T>
-__global__ __launch_bounds__(512, 1) void k_mcmc_resident_pc(const BlockArgs<T> a,
-                                                             const AcceptArgs c,
-                                                             const int64_t iter0,
-                                                             const int64_t n_iter,
-                                                             double* __restrict__ part,
-                                                             double* __restrict__ nodes,
-                                                             unsigned* __restrict__ counter,
-                                                             double* __restrict__ out3) {
+template <class Mdl, class T, int NP>
+__global__ __launch_bounds__(64 * 4 * (NP + 1), 1) void k_mcmc_resident_pc(const BlockArgs<T> a,
+                                                                      const AcceptArgs c,
+                                                                      const int64_t iter0,
+                                                                      const int64_t n_iter,
+                                                                      double* __restrict__ part,
+                                                                      double* __restrict__ nodes,
+                                                                      unsigned* __restrict__ counter,
+                                                                      double* __restrict__ out3) {
   __shared__ ResPcLds<Mdl::D, Mdl::M, T> lds[4];
   if (n_iter <= 0) return;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t blk = a.b0 + (int64_t)blockIdx.x * 4 + (w & 3);
   const bool valid = blk < a.b1;
-#if defined(DMT_PC_STUB_P)  // register-budget probes (scripts/res_usage.sh): one role only
-  if (w < 4) resident_pc_consumer<Mdl, T>(a, c, iter0, n_iter, part, blk, valid, lds[w & 3]);
+  const int role = w >> 2;  // 0: consumer, 1 + h: producer h
+#if defined(DMT_PC_STUB_P)  // timing probes (scripts/res_usage.sh, gpu_variants.sh): one role only
+  if (role == 0) resident_pc_consumer<Mdl, T>(a, c, iter0, n_iter, part, blk, valid, lds[w & 3]);
   else for (int64_t i = 0; i < 2 * n_iter; ++i) __syncthreads();
 #elif defined(DMT_PC_STUB_C)
-  if (w >= 4) resident_pc_producer<Mdl, T>(a, c, iter0, n_iter, blk, valid, lds[w & 3]);
+  if (role > 0) resident_pc_producer<Mdl, T, NP>(a, c, iter0, n_iter, blk, valid, role - 1, lds[w & 3]);
   else for (int64_t i = 0; i < 2 * n_iter; ++i) __syncthreads();
 #else
-  if (w < 4)
+  if (role == 0)
     resident_pc_consumer<Mdl, T>(a, c, iter0, n_iter, part, blk, valid, lds[w & 3]);
   else
-    resident_pc_producer<Mdl, T>(a, c, iter0, n_iter, blk, valid, lds[w & 3]);
+    resident_pc_producer<Mdl, T, NP>(a, c, iter0, n_iter, blk, valid, role - 1, lds[w & 3]);
 #endif
-  persistent_tree_tail<4, 8>(part, nodes, a.b1 - a.b0, n_iter, counter, out3);
+#ifndef DMT_PC_NO_TAIL  // timing probe: no in-kernel fetch_ll trees
+  persistent_tree_tail<4, 4 * (NP + 1)>(part, nodes, a.b1 - a.b0, n_iter, counter, out3);
+#endif
 }
 
 // One draw / re-solve (dmt_draw_proposal, dmt_draw_unit, dmt_recompute_path) of single-segment
@@ -3627,9 +3637,13 @@ static hipError_t launch_mcmc_t(const void* args, const AcceptArgs& c, int64_t i
     // part[n][3][nwaves], then the tree nodes [n][3][ceil(nwaves / WPB)] (dmt_mcmc_run sizes it)
     double* nodes = part + 3 * n * nwaves;
     if constexpr (Mdl::D <= 2) {
-      if (resident == 2) {  // producer / consumer waves (k_mcmc_resident_pc)
-        dlaunch(k_mcmc_resident_pc<Mdl, T>, dim3((unsigned)((nwaves + 3) / 4)), dim3(512), s, a,
-                c, iter0, n, part, nodes, counter, out3);
+      if (resident >= 2) {  // producer / consumer waves (k_mcmc_resident_pc), resident - 1 producers
+        if (resident == 3)
+          dlaunch(k_mcmc_resident_pc<Mdl, T, 2>, dim3((unsigned)((nwaves + 3) / 4)), dim3(768), s,
+                  a, c, iter0, n, part, nodes, counter, out3);
+        else
+          dlaunch(k_mcmc_resident_pc<Mdl, T, 1>, dim3((unsigned)((nwaves + 3) / 4)), dim3(512), s,
+                  a, c, iter0, n, part, nodes, counter, out3);
         return hipGetLastError();
       }
       if (resident) {

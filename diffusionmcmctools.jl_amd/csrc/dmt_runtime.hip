@@ -163,7 +163,9 @@ struct dmt_ens {
   int64_t part_cap = 0;
   bool persist = true;       // dmt_mcmc_run of a linear drift in one launch (DMT_MCMC_PERSIST=0: off)
   bool resident = true;      // ... with register-resident block state when eligible (DMT_MCMC_RESIDENT=0: off)
-  bool resident_pc = true;   // ... split over a producer and a consumer wave per block (DMT_MCMC_PC=0: one wave)
+  bool dispatch_events = true;  // timing events attached to the dispatch (DMT_DISPATCH_EVENTS=0: recorded around it)
+  int resident_pc = 1;       // ... split over a consumer and this many producer waves per block
+                             // (DMT_MCMC_PC=0: one wave; 1 or 2 producers)
   int lane_split = -1;       // MAP_LANE draws on producer/consumer waves: 1 on, 0 off, -1 auto
                              // (when the draw has fewer waves than the device has SIMDs)
   int64_t n_simd = 1024;
@@ -246,7 +248,7 @@ struct TimedScope {
   int64_t units;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   TimedScope(dmt_ens* h_, int k_, bool dispatch_ = true, int64_t units_ = 1)
-      : h(h_), k(k_), dispatch(dispatch_), units(units_) {
+      : h(h_), k(k_), dispatch(dispatch_ && h_->dispatch_events), units(units_) {
     if (h->timing >> k & 1u) {
       e0 = get_event(h);
       e1 = get_event(h);
@@ -691,7 +693,8 @@ dmt_status dmt_create(dmt_ens** out, const dmt_model* model, const dmt_structure
   if (model->model == DMT_MODEL_OU) h->mapping = MAP_WAVE;
   if (const char* e = std::getenv("DMT_MCMC_PERSIST")) h->persist = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("DMT_MCMC_RESIDENT")) h->resident = std::strcmp(e, "0") != 0;
-  if (const char* e = std::getenv("DMT_MCMC_PC")) h->resident_pc = std::strcmp(e, "0") != 0;
+  if (const char* e = std::getenv("DMT_MCMC_PC")) h->resident_pc = std::max(0, std::min(2, std::atoi(e)));
+  if (const char* e = std::getenv("DMT_DISPATCH_EVENTS")) h->dispatch_events = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("DMT_LANE_SPLIT")) h->lane_split = std::atoi(e);
   if (const char* e = std::getenv("DMT_REPAIR_DIV")) h->repair_div = std::max(1, std::atoi(e));
   if (const char* e = std::getenv("DMT_SCAN_RESIDENT")) h->scan_resident = std::strcmp(e, "0") != 0;
@@ -1265,13 +1268,13 @@ dmt_status dmt_mcmc_run(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int6
           BlockArgs<double> a{};
           fill(a);
           e = launch_mcmc_persistent(h->key, &a, c, iter0 + i0, n, h->d_part, nb,
-                                     resident ? (h->resident_pc ? 2 : 1) : 0,
+                                     resident ? 1 + h->resident_pc : 0,
                                      run_out + 3 * i0, (unsigned*)counter, h->stream);
         } else {
           BlockArgs<float> a{};
           fill(a);
           e = launch_mcmc_persistent(h->key, &a, c, iter0 + i0, n, h->d_part, nb,
-                                     resident ? (h->resident_pc ? 2 : 1) : 0,
+                                     resident ? 1 + h->resident_pc : 0,
                                      run_out + 3 * i0, (unsigned*)counter, h->stream);
         }
       }
