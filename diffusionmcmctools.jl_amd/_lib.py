@@ -49,6 +49,7 @@ SYMBOLS = [
     "dmt_debug_normals", "dmt_last_error", "dmt_version", "dmt_snapshot_reserve",
     "dmt_snapshot_take", "dmt_snapshot_download", "dmt_snapshot_write", "dmt_set_ll",
     "dmt_fetch_ll_local", "dmt_comm_size", "dmt_rng_counter", "dmt_set_rng_counter",
+    "dmt_set_run_snapshots",
 ]
 
 
@@ -127,6 +128,7 @@ _SIGS = {
     "dmt_debug_normals": [_i32, _u64, _pu32, _i64, _pd],
     "dmt_snapshot_reserve": [_P, _i32, _i64],
     "dmt_snapshot_take": [_P, _i32, _i64, _i64],
+    "dmt_set_run_snapshots": [_P, _i64, _i64],
     "dmt_snapshot_download": [_P, _i32, _i64, _pd, _pi64],
     "dmt_snapshot_write": [_P, C.c_char_p, _i64, _i64],
     "dmt_set_ll": [_P, _i32, _i32, _i64, _i64, _i64, _pd],

@@ -142,6 +142,13 @@ class SamplingEnsemble:
             out.append(segs)
         return out, it
 
+    def snapshot_every(self, every, slot0=0):
+        """Snapshots inside later :meth:`BlockEnsemble.mcmc_run` calls: u's paths after every
+        iteration k with k % every == 0 go to slots slot0, slot0 + 1, … (a ring over the
+        reserved slots), with no host round trip — the smoothing loop's `deepcopy(sp.u.XX)`
+        every few iterations (docs/src/tutorials/biblock/smoothing.md:40-44).  0 turns it off."""
+        self.ens.set_run_snapshots(every, slot0)
+
     def write_snapshots(self, path, s0=0, s1=None):
         """Stream slots [s0, s1) to ``path`` (DMTPATH1 format, include/dmt.h); read back with
         :func:`diffusionmcmctools_amd.read_snapshots`."""
@@ -287,6 +294,15 @@ class _BlockRange:
             raise ValueError(f"only must be one of {sorted(k for k in _RGT_ONLY if k)} or None")
         for unit in units:
             self._call("recompute_guiding_term", unit=unit)
+
+    def equalize_obs_params(self):
+        """``GP.equalize_obs_params!(bb)`` (src/biblock.jl:375-387): make u°'s observation
+        parameters those of u.  On the device a recording's observations (``dmt_upload_obs``:
+        the observed values, their noise, the artificial P_last observation) are stored ONCE
+        and read by the laws of both u and u°, so they cannot differ and there is nothing to
+        copy; returns the per-block critical-change flags the reference's call would yield
+        here (all False)."""
+        return np.zeros(self.num_blocks, dtype=bool)
 
     def find_W_for_X(self):
         """``find_W_for_X!`` (src/block.jl:118-131): u.WW ← the Wiener increments that reproduce

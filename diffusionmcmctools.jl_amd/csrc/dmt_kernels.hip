@@ -59,7 +59,7 @@ __device__ __forceinline__ bool run_segment(const Law<Mdl, T>& L, const T* __res
                                             const T* Xcs, T* Xcd, T* Wcd,
                                             NormalStream<T>& ns, const int64_t tq, const int64_t q0,
                                             const int np, const int lane, const T rho,
-                                            const T srho, T* x, T& sl) {
+                                            const T srho, const int ll_skip, T* x, T& sl) {
   constexpr int D = Mdl::D, M = Mdl::M, HP = D * (D + 1) / 2;
   constexpr bool DRAW = MODE != MODE_RECOMPUTE;
   constexpr bool READW = MODE != MODE_FRESH;
@@ -153,7 +153,8 @@ __device__ __forceinline__ bool run_segment(const Law<Mdl, T>& L, const T* __res
 #pragma unroll
     for (int p = 0; p < D; ++p) Xdb[((int64_t)(i + 1) * D + p) * kLanes] = x[p];
     tcur = tn;
-    return G * dt;
+    // recompute_path!(…; skip): the segment's last ll_skip steps add no term
+    return (MODE == MODE_RECOMPUTE && i >= nst - ll_skip) ? (T)0 : G * dt;
   };
 
   const int nfull = nst - nst % K;
@@ -296,7 +297,7 @@ __global__ __launch_bounds__(64) void k_block(const BlockArgs<T> a) {
     T sl;
     const bool sok = run_segment<Mdl, T, MODE, PARITY, K>(
         L, a.t, a.t_shared, a.H[ls][kind], a.H_shared[ls][kind], a.F[ls][kind], Ws, Wd, Xd, Zg,
-        Xcs, Xcd, Wcd, ns, tq, a.seg_q[g], a.seg_np[g], lane, rho, srho, x, sl);
+        Xcs, Xcd, Wcd, ns, tq, a.seg_q[g], a.seg_np[g], lane, rho, srho, a.ll_skip, x, sl);
     if (MODE == MODE_PCN) {
       if (nsx != sx) a.selX[g] = (uint8_t)nsx;
       if (nsw != sw) a.selW[g] = (uint8_t)nsw;
@@ -919,7 +920,8 @@ __global__ __launch_bounds__(128) void k_block_wave(const BlockArgs<T> a) {
 #pragma unroll
     for (int c = 0; c < D; ++c) { Fi[c] = rw[1 + HP + c]; xi[c] = sh.xcap[k & 1][lane][c]; }
     const T G = g_at<Mdl, T>(LB, Hi, Fi, xi, rr, bb);
-    const T csum = wave_tree_sum<T>(valid ? G * rw[0] : (T)0);
+    const bool inll = MODE != MODE_RECOMPUTE || c0 + lane < nst - a.ll_skip;  // skip
+    const T csum = wave_tree_sum<T>((valid && inll) ? G * rw[0] : (T)0);
     seg_acc = seg_acc + (csum + (T)0);
     const bool seg_end = c0 + 64 >= nst;
     if (k <= stop_after) {
@@ -1314,7 +1316,8 @@ __device__ __forceinline__ void scan_block(const BlockArgs<T>& a, const int64_t 
         }
         T rr[D], bb[D];
         const T G = g_at<Mdl, T>(LA, Hi, Fi, xk[k], rr, bb);
-        gk[k] = v ? G * dt : (T)0;
+        const bool inll = MODE != MODE_RECOMPUTE || c0 + s < nst - a.ll_skip;  // skip
+        gk[k] = (v && inll) ? G * dt : (T)0;
       }
 #pragma unroll
       for (int k = 0; k < kRun; ++k) gk[k] = wave_tree_sum<T>(gk[k]);
@@ -1794,7 +1797,7 @@ __device__ __forceinline__ void resident_block(const BlockArgs<T>& a, const Acce
 #pragma unroll
       for (int cc = 0; cc < D; ++cc) Fr[cc] = S.hf[r][HP + cc][lane];
       const T G = g_at<Mdl, T>(LA, Hr, Fr, x, rr, bb);
-      gl[r] = v ? G * dts[r] : (T)0;
+      gl[r] = (v && (MODE != MODE_RECOMPUTE || kRun * lane + r < nst - a.ll_skip)) ? G * dts[r] : (T)0;
       // branch-free: slots of steps past the segment end are written but never read
 #pragma unroll
       for (int p = 0; p < D; ++p) S.pt[li][p] = x[p];

@@ -101,6 +101,8 @@ struct dmt_ens {
   // path snapshots (dmt_snapshot_*): [slots][P][C] doubles in reference layout per kind
   int snap_mask = 0;
   int64_t snap_slots = 0;
+  int64_t run_snap_every = 0;  // dmt_mcmc_run: snapshot u after every iteration k with k % every == 0
+  int64_t run_snap_next = 0;   // ... into this slot next (ring over snap_slots)
   double* d_snap[2] = {nullptr, nullptr};
   std::vector<int64_t> snap_iter, snap_unit;
   int mapping = MAP_LANE;  // thread mapping of the recursion kernels
@@ -435,7 +437,8 @@ void fill_common(dmt_ens* h, const Layout* L, BlockArgs<T>& a) {
 dmt_status run_block_kernel(dmt_ens* h, const Layout* L, int mode, int kind_timer, int64_t b0,
                             int64_t b1, int law_flip, int xs, int xd, int ws, int wd,
                             const double* dZ, int64_t iter, uint32_t salt, double* ll_out,
-                            uint8_t* success, int op /* 0 draw/solve, 1 loglikhd, 2 invsolve */) {
+                            uint8_t* success, int op /* 0 draw/solve, 1 loglikhd, 2 invsolve */,
+                            int ll_skip = 0 /* MODE_RECOMPUTE: recompute_path!(…; skip) */) {
   if (b1 <= b0) return DMT_OK;
   const int64_t r0 = rec_of_block(L, b0), r1 = rec_of_block(L, b1 - 1);
   const int64_t tile0 = r0 / kLanes, tile1 = r1 / kLanes + 1;
@@ -459,6 +462,7 @@ dmt_status run_block_kernel(dmt_ens* h, const Layout* L, int mode, int kind_time
     a.salt = salt;
     a.ll_out = ll_out;
     a.success = success;
+    a.ll_skip = ll_skip;
     a.resident1 = h->scan_resident && h->key.model == DMT_MODEL_OU && h->key.d <= 2 &&
                   L->single_seg && L->max_steps <= kResidentMaxSteps;
     // auto: fp64 only — with fp32's four normals per Philox block the single wave is faster
@@ -1167,6 +1171,16 @@ static int64_t grown_cap(int64_t need, int64_t cap, int64_t floor_) {
   return std::max({need, 2 * cap, floor_});
 }
 
+dmt_status dmt_set_run_snapshots(dmt_ens* h, int64_t every, int64_t slot0) {
+  DMT_TRY(check_h(h));
+  if (every < 0) return fail(DMT_ERR_INVALID, "every must be >= 0");
+  if (every > 0 && !h->snap_mask) return fail(DMT_ERR_STATE, "no snapshot slots (dmt_snapshot_reserve)");
+  if (every > 0 && (slot0 < 0 || slot0 >= h->snap_slots)) return fail(DMT_ERR_INVALID, "slot out of range");
+  h->run_snap_every = every;
+  h->run_snap_next = slot0;
+  return DMT_OK;
+}
+
 dmt_status dmt_mcmc_run(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int64_t iter0,
                         int64_t n_iter, uint32_t salt, double* out) {
   DMT_TRY(check_h(h));
@@ -1179,6 +1193,28 @@ dmt_status dmt_mcmc_run(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int6
   if (n_iter == 0) return DMT_OK;
   if (L->hist_len > 0 && iter0 + n_iter - 1 > L->hist_len)
     return fail(DMT_ERR_INVALID, "iterations outside 1:ll_hist_len");
+  if (h->run_snap_every > 0) {
+    // snapshots inside the run (the smoothing loop's `deepcopy(sp.u.XX)` every k iterations,
+    // docs/src/tutorials/biblock/smoothing.md:40-44): the run is cut after every iteration
+    // k ≡ 0 mod every and u is snapshotted there, stream-ordered (no host round trip); the
+    // pieces take the same stream keys as one run (auto keys: consecutive counter values)
+    const int64_t every = h->run_snap_every;
+    h->run_snap_every = 0;
+    dmt_status st = DMT_OK;
+    for (int64_t done = 0; done < n_iter && st == DMT_OK;) {
+      const int64_t it = iter0 + done;
+      const int64_t k = ((it + every - 1) / every) * every;  // next snapshot iteration >= it
+      const int64_t n = std::min(n_iter - done, k - it + 1);
+      st = dmt_mcmc_run(h, layout, b0, b1, it, n, salt, out ? out + 3 * done : nullptr);
+      done += n;
+      if (st == DMT_OK && (iter0 + done - 1) % every == 0) {
+        st = dmt_snapshot_take(h, DMT_U, h->run_snap_next, iter0 + done - 1);
+        h->run_snap_next = (h->run_snap_next + 1) % h->snap_slots;
+      }
+    }
+    h->run_snap_every = every;
+    return st;
+  }
   // stream keys: iteration it draws its normals and its Exp(1) variables with key word
   // it + key_delta (explicit: the iteration itself; auto: n_iter consecutive counter values,
   // never straddling a 2^32 boundary so that the salt word is constant over the run)
@@ -1371,16 +1407,16 @@ dmt_status dmt_loglikhd(dmt_ens* h, int32_t layout, int32_t unit, int64_t b0, in
 dmt_status dmt_recompute_path(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int32_t skip,
                               uint8_t* success_out) {
   DMT_TRY(check_h(h));
-  if (skip != 0)
-    return fail(DMT_ERR_INVALID, "skip != 0 is not supported (its upstream semantics are not pinned; "
-                                 "every reference call passes skip=0)");
+  if (skip < 0) return fail(DMT_ERR_INVALID, "skip must be >= 0");
   Layout* L;
   DMT_TRY(get_layout(h, layout, &L));
   DMT_TRY(check_range(L, b0, b1));
   DMT_TRY(law_ready(h, 1, L, b0, b1));
   // law u°.PP (flip 1); start from u°.XX; write u°.XX; read u.WW (the accepted W)
+  // skip: the last `skip` Euler steps of every segment add no Girsanov term (GuidedProposals'
+  // solve_and_ll!(…; skip)); the path itself is solved to the end
   DMT_TRY(run_block_kernel(h, L, MODE_RECOMPUTE, DMT_K_RECOMPUTE, b0, b1, 1, 1, 1, 0, 0, nullptr, 0,
-                           0, L->d_llp, success_out ? L->d_success : nullptr, false));
+                           0, L->d_llp, success_out ? L->d_success : nullptr, 0, skip));
   if (success_out) {
     HIP_OK(hipMemcpyAsync(success_out, L->d_success + b0, b1 - b0, hipMemcpyDeviceToHost, h->stream));
     HIP_OK(stream_wait(h));
@@ -1591,8 +1627,7 @@ dmt_status dmt_set_proposal_law(dmt_ens* h, int32_t layout, int64_t b0, int64_t 
                                                       : h->d * h->d + h->d;
   for (int k = 0; k < n; ++k)
     if (idx[k] < 0 || idx[k] >= npar) return fail(DMT_ERR_INVALID, "unknown parameter index");
-  if (skip != 0)
-    return fail(DMT_ERR_INVALID, "skip != 0 is not supported (see dmt_recompute_path)");
+  if (skip < 0) return fail(DMT_ERR_INVALID, "skip must be >= 0");
   DMT_TRY(law_ready(h, 1, L, b0, b1));
   ParamArgs a{};
   a.model = h->key.model;
@@ -1620,7 +1655,7 @@ dmt_status dmt_set_proposal_law(dmt_ens* h, int32_t layout, int64_t b0, int64_t 
   if (ncrit > 0) DMT_TRY(guiding_term_device(h, L, b0, b1, DMT_UPROP, L->d_crit));
   if (critical_out)
     HIP_OK(hipMemcpyAsync(critical_out, L->d_crit + b0, b1 - b0, hipMemcpyDeviceToHost, h->stream));
-  DMT_TRY(dmt_recompute_path(h, layout, b0, b1, 0, success_out));
+  DMT_TRY(dmt_recompute_path(h, layout, b0, b1, skip, success_out));
   if (critical_out) HIP_OK(stream_wait(h));
   return DMT_OK;
 }

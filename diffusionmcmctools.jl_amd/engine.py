@@ -277,6 +277,11 @@ class Ensemble:
                L.f64p(out))
         return out
 
+    def set_run_snapshots(self, every, slot0=0):
+        """Snapshot u inside every later mcmc_run after each iteration k with k % every == 0
+        (slots slot0, slot0 + 1, … of snapshot_reserve, a ring); every = 0: off."""
+        L.call("dmt_set_run_snapshots", self._h, int(every), int(slot0))
+
     # ---------------------------------------------------------------- misc
     def sync(self):
         L.call("dmt_sync", self._h)

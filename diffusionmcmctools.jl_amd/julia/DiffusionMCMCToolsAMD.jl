@@ -20,7 +20,7 @@ import DiffusionMCMCTools: draw_proposal_path!, accept_reject_proposal_path!, lo
 
 export DeviceSamplingEnsemble, DeviceBlockEnsemble, DeviceBlockCollection, DeviceBiBlock,
     mcmc_step!, mcmc_run!, download_XX, download_WW, upload_obs!, set_obs!,
-    recompute_guiding_term!, set_proposal_law!
+    recompute_guiding_term!, set_proposal_law!, snapshot_every!, equalize_obs_params!
 
 const libdmt = get(ENV, "DMT_LIB", joinpath(@__DIR__, "..", "libdmt.so"))
 
@@ -156,6 +156,11 @@ function snapshot(se::DeviceSamplingEnsemble, slot; what=0)
                 (Ptr{Cvoid}, Int32, Int64, Ptr{Float64}, Ref{Int64}), se.h, what, slot, out, it))
     collect(reinterpret(SVector{C,Float64}, out)), it[]
 end
+# snapshots inside mcmc_run!: u after every iteration k with k % every == 0 → slots slot0, …
+# (a ring), no host round trip; every = 0 turns it off
+snapshot_every!(se::DeviceSamplingEnsemble, every; slot0=0) =
+    check(ccall((:dmt_set_run_snapshots, libdmt), Int32, (Ptr{Cvoid}, Int64, Int64),
+                se.h, every, slot0))
 write_snapshots(se::DeviceSamplingEnsemble, path::AbstractString, s0, s1) =
     check(ccall((:dmt_snapshot_write, libdmt), Int32, (Ptr{Cvoid}, Cstring, Int64, Int64),
                 se.h, path, s0, s1))
@@ -358,6 +363,15 @@ function recompute_path!(x::DeviceBlocks; skip=0)
         x.se.h, x.layout, x.b0, x.b1, skip, ok))
     Bool.(ok)
 end
+
+"""
+    GP.equalize_obs_params!(x)
+
+src/biblock.jl:375-387: u°'s observation parameters ← u's.  The device stores a recording's
+observations once for both u and u° (`upload_obs!`), so they never differ: nothing to copy, no
+critical change.
+"""
+equalize_obs_params!(x::DeviceBlocks) = falses(_n(x))
 
 "Observation information at every segment end (packed H, F, c) + artificial noise."
 upload_obs!(se::DeviceSamplingEnsemble, Hobs, Fobs, cobs; artificial_noise=1e-11) =

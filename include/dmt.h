@@ -386,6 +386,12 @@ typedef struct {
 dmt_status dmt_snapshot_reserve(dmt_ens* h, int32_t what_mask, int64_t n_slots);
 /* deepcopy(unit.XX / unit.WW) into slot (after every queued kernel), tagged with mcmciter */
 dmt_status dmt_snapshot_take(dmt_ens* h, int32_t unit, int64_t slot, int64_t mcmciter);
+/* Snapshots inside dmt_mcmc_run: from now on every run snapshots u (dmt_snapshot_take(h, DMT_U,
+ * …)) after each iteration k with k % every == 0, into slots slot0, slot0 + 1, … (a ring over
+ * the reserved slots), without host synchronisation — the reference's smoothing loop keeps
+ * `deepcopy(sp.u.XX)` every few iterations (docs/src/tutorials/biblock/smoothing.md:40-44).
+ * every = 0 turns it off. */
+dmt_status dmt_set_run_snapshots(dmt_ens* h, int64_t every, int64_t slot0);
 dmt_status dmt_snapshot_download(dmt_ens* h, int32_t what, int64_t slot, double* out,
                                  int64_t* mcmciter);
 dmt_status dmt_snapshot_write(dmt_ens* h, const char* path, int64_t s0, int64_t s1);

@@ -253,6 +253,7 @@ static void aff_apply(int d, const REAL* A, const REAL* e, const REAL* x, REAL* 
  * segment start, chunk sums added left to right (psum). */
 #define ORC_RUN 8
 #define ORC_SCHUNK 512
+extern int orc_ll_skip;
 static int solve_segment_scan(int d, int m, const REAL* th, const REAL* sg, const REAL* a,
                               const REAL* Bt, const REAL* beta, const REAL* da, int trace,
                               int npts, const REAL* t, const REAL* H, const REAL* F,
@@ -324,7 +325,7 @@ static int solve_segment_scan(int d, int m, const REAL* th, const REAL* sg, cons
                 if (i > 0) for (int p = 0; p < d; ++p) X[(size_t)i * d + p] = x[p];
                 REAL G = g_at(ORC_OU, d, th, a, Bt, beta, da, trace, H + (size_t)i * h,
                               F + (size_t)i * d, x, rr, b);
-                ps_add(&ps, G * dt);
+                ps_add(&ps, i < n - orc_ll_skip ? G * dt : (REAL)0);
                 REAL xp[3];
                 aff_apply(d, A[s0 + r], e[s0 + r], x, xp);
                 for (int p = 0; p < d; ++p) x[p] = xp[p];
@@ -340,6 +341,17 @@ static int solve_segment_scan(int d, int m, const REAL* th, const REAL* sg, cons
     for (int p = 0; p < d; ++p) ok &= isfinite(xs[p]) ? 1 : 0;
     return ok;
 }
+
+/* recompute_path!(…; skip) (src/block.jl:159-187 → GP.solve_and_ll!(…; skip), GuidedProposals
+ * v0.1.0, not vendored): the last orc_ll_skip Euler steps of a segment add no Girsanov term —
+ * the term is replaced by 0 in the same position of the psum tree; the path is solved to the
+ * end.  Set by oracle.py around recompute_path (0 everywhere else). */
+#if IS_F64
+int orc_ll_skip = 0;
+void orc_set_ll_skip(int k) { orc_ll_skip = k; }
+#else
+extern int orc_ll_skip;
+#endif
 
 /* CPU-baseline switch (bench.py's cpu_baseline only): 1 = evaluate linear-drift segments
  * with the plain step-by-step Euler loop — the natural CPU algorithm, as the reference runs
@@ -372,7 +384,7 @@ int SFX(orc_solve_segment)(int model, int d, int m, const double* law, int npts,
         const REAL* Fi = F + (size_t)i * d;
         REAL r[3] = {0, 0, 0}, b[3] = {0, 0, 0};
         REAL G = g_at(model, d, th, a, Bt, beta, da, trace, Hi, Fi, x, r, b);
-        ps_add(&ps, G * dt);
+        ps_add(&ps, i < npts - 1 - orc_ll_skip ? G * dt : (REAL)0);
         REAL Mg[9], cg[3];
         guide_coeffs(model, d, th, a, Hi, Fi, Mg, cg);
         REAL xn[3];

@@ -121,6 +121,8 @@ def _load():
     lib.orc_exp1_range.restype = None
     lib.orc_set_sequential_ou.argtypes = [i_]
     lib.orc_set_sequential_ou.restype = None
+    lib.orc_set_ll_skip.argtypes = [i_]
+    lib.orc_set_ll_skip.restype = None
     lib.orc_backward_filter_segment.argtypes = [i_, P, P, P, i_, P, P, P, d_, P, P, P]
     lib.orc_backward_filter_segment.restype = i_
     lib.orc_rng_log.argtypes = [d_]
@@ -611,12 +613,17 @@ class OracleEnsemble:
                 bk.llp = float(ll)
 
     def recompute_path(self, layout, b0, b1, skip=0, want_success=False):
-        """recompute_path!(b°, b.WW) (src/block.jl:159-187) under u°.PP."""
-        assert skip == 0
+        """recompute_path!(b°, b.WW; skip) (src/block.jl:159-187) under u°.PP: every
+        segment's solve_and_ll!(…; skip) leaves its last `skip` Girsanov terms out."""
+        assert skip >= 0
         oks = []
-        for bk in self.layouts[layout][b0:b1]:
-            bk.llp, ok = self._solve_block(bk, 1, 1, 0, 1, "given", None, 0, 0)
-            oks.append(ok)
+        lib.orc_set_ll_skip(int(skip))
+        try:
+            for bk in self.layouts[layout][b0:b1]:
+                bk.llp, ok = self._solve_block(bk, 1, 1, 0, 1, "given", None, 0, 0)
+                oks.append(ok)
+        finally:
+            lib.orc_set_ll_skip(0)
         return np.array(oks) if want_success else None
 
     # ---- guiding terms (recompute_guiding_term!, set_obs!)
@@ -642,7 +649,7 @@ class OracleEnsemble:
         (DD.set_parameters!, :360-364), recompute_guiding_term!(b°) for the blocks whose
         auxiliary law changed (:342), recompute_path!(b°, b.WW) (:343).
         Returns (success, critical) per block."""
-        assert skip == 0
+        assert skip >= 0
         crit = np.zeros(b1 - b0, dtype=bool)
         for j, bk in enumerate(self.layouts[layout][b0:b1]):
             for g in range(bk.g0, bk.g1 + 1):
@@ -664,7 +671,7 @@ class OracleEnsemble:
                         crit[j] = True
         for j in np.flatnonzero(crit):
             self.recompute_guiding_term(layout, b0 + j, b0 + j + 1, unit=1)
-        ok = self.recompute_path(layout, b0, b1, want_success=True)
+        ok = self.recompute_path(layout, b0, b1, skip=skip, want_success=True)
         return ok, crit
 
     def set_obs(self, layout, b0, b1):

@@ -269,3 +269,18 @@ def test_api_program_gpu_matches_oracle():
         np.testing.assert_array_equal(bd.ll_history, bo.ll_history)
         np.testing.assert_array_equal(bd.accpt_history, bo.accpt_history)
     se_d.close()
+
+
+def test_equalize_obs_params_is_a_no_op_on_shared_observations():
+    """GP.equalize_obs_params!(bb) (src/biblock.jl:375-387): the observations live once per
+    recording for u and u° (dmt_upload_obs), so the call changes nothing and reports no
+    critical change; the blocks' ll and paths are untouched."""
+    se = _sampling_ensemble(ragged_case(), "oracle")
+    be = dmt.BlockEnsemble(se, RANGES_A, rho=0.5, ll_hist_len=2)
+    be.loglikhd()
+    ll0 = be.ll.copy() if hasattr(be.ll, "copy") else be.ll
+    X0 = se.ens.download_paths(L.U, 0).copy()
+    crit = be.equalize_obs_params()
+    assert crit.dtype == bool and crit.shape == (be.num_blocks,) and not crit.any()
+    assert np.array_equal(se.ens.download_paths(L.U, 0), X0)
+    assert np.array_equal(be.ll, ll0)

@@ -254,6 +254,36 @@ def test_mcmc_run_persistent_paths_equal_step_path(case):
     cs.assert_paths_equal(e0, e1)
 
 
+@pytest.mark.parametrize("mapping", MAPPINGS)
+@pytest.mark.parametrize("kind", ["ragged-fhn", "c2-resident", "c2-scan", "c1"])
+def test_recompute_path_skip_bit_exact(kind, mapping, monkeypatch):
+    """recompute_path!(b°, b.WW; skip) (src/block.jl:159-187): every segment's last `skip`
+    Girsanov terms are left out of ll° (the path is solved to the end) — device == oracle bit
+    for bit on multi-segment FHN blocks with P_last laws (lane and wave kernels), the one-shot
+    resident and general OU scan kernels, and skip larger than a segment."""
+    if kind == "c2-scan":
+        monkeypatch.setenv("DMT_SCAN_RESIDENT", "0")
+    if kind == "ragged-fhn":
+        case, dev, ora, ((A, nA), _) = cs.ragged_pair(mapping=mapping)
+        lawsp = case["laws"].copy()
+        lawsp[:, 2] = 1.7
+        for e in (dev, ora):
+            e.upload_law(L.UPROP, L.LAW_PP, laws=lawsp)
+        lay, nb = A, nA
+    else:
+        w = W.c2_ou2d(B=70, N=300) if kind.startswith("c2") else W.c1_ou1d()
+        dev, ora, lay = cs.both(w, hist_len=2, mapping=mapping)
+        nb = w.nblocks
+    for e in (dev, ora):
+        e.loglikhd(lay, L.U, 0, nb)
+    for skip in (1, 7, 64, 100000):
+        okd = dev.recompute_path(lay, 0, nb, skip=skip, want_success=True)
+        oko = ora.recompute_path(lay, 0, nb, skip=skip, want_success=True)
+        assert np.array_equal(okd, oko)
+        cs.assert_paths_equal(dev, ora)
+        cs.assert_ll_equal(dev, ora, lay, nb)
+
+
 @pytest.mark.parametrize("case", [
     pytest.param(("c2", 100, 60, 6), id="c2-60steps"),
     pytest.param(("c2", 301, 500, 70), id="c2-500steps-ragged-workgroup-70iters"),

@@ -310,3 +310,30 @@ def test_chunked_filter_lengths(dmt, npts):
     np.testing.assert_allclose(H, Hp, rtol=1e-9, atol=1e-10 * np.abs(Hp).max())
     np.testing.assert_allclose(F, Fe, rtol=1e-9, atol=1e-10 * np.abs(Fe).max())
     np.testing.assert_allclose(c, ce, rtol=1e-9, atol=1e-9)
+
+
+def test_recompute_path_skip_semantics():
+    """recompute_path!(b°, b.WW; skip) in the oracle (GP.solve_and_ll!(…; skip), GuidedProposals
+    v0.1.0, not vendored — DESIGN.md §7): the path is solved to the end whatever `skip`; the
+    last `skip` Girsanov terms leave ll°; skip ≥ the segment's steps leaves loglikhd_obs only."""
+    from diffusionmcmctools_amd import _lib as L
+    from diffusionmcmctools_amd import workloads as W
+    w = W.c1_ou1d()
+    w.meta["hist_len"] = 1
+    ora = orc.OracleEnsemble(w.model.kind, w.d, w.m, w.n_points, prec=w.precision, seed=4,
+                             grid_shared=w.grid_shared)
+    lay = W.fill(ora, w)
+    res = {}
+    for skip in (0, 1, 5, 10 ** 6):
+        ora.recompute_path(lay, 0, 1, skip=skip)
+        res[skip] = (ora.download_paths(L.UPROP, 0).copy(),
+                     float(ora.get_block_state(lay, L.BLK_LLPROP, 0, 1)[0]))
+    for skip in (1, 5, 10 ** 6):
+        assert np.array_equal(res[skip][0], res[0][0])
+    ll = [res[k][1] for k in (0, 1, 5, 10 ** 6)]
+    assert all(np.isfinite(ll)) and len(set(ll)) == 4
+    # skip beyond the segment: only the observation term of the block start remains
+    X = res[0][0].reshape(-1, w.d)
+    lw = ora.up.PP[0]
+    obs = orc.obs_term(w.d, lw.rec, lw.H[0], lw.F[0], X[0], w.precision)
+    assert ll[3] == float(obs)

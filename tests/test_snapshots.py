@@ -120,3 +120,45 @@ def test_device_snapshots_and_file_round_trip(tmp_path, cfg):
     for j, k in enumerate(range(1, 4)):
         assert np.array_equal(s["X"][j], ref[k][0]) and np.array_equal(s["W"][j], ref[k][1])
     ens.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", ["c2", "ragged"])
+def test_snapshots_inside_mcmc_run(cfg):
+    """dmt_set_run_snapshots: one mcmc_run of 23 iterations from iteration 3 with every = 5
+    snapshots u after iterations 5, 10, 15, 20, 25 into a 4-slot ring (the 5th wraps to slot
+    0) — the same paths and results as stopping the run there and downloading u, and the same
+    per-iteration fetch_ll values as an unsplit run (auto stream keys)."""
+    import _cases as cs
+    import diffusionmcmctools_amd as d
+
+    def build():
+        if cfg == "c2":
+            w = W.c2_ou2d(B=150, N=90)
+            w.meta["hist_len"] = 40
+            ens = d.Ensemble(w.model.kind, w.d, w.m, w.n_points, precision=w.precision, seed=5,
+                             grid_shared=w.grid_shared)
+            lay = W.fill(ens, w)
+            nb = w.nblocks
+        else:
+            _, ens, _, ((lay, nb), _) = cs.ragged_pair(hist_len=40)
+        ens.loglikhd(lay, L.U, 0, nb)
+        return ens, lay, nb
+    e0, lay, nb = build()
+    e1, _, _ = build()
+    e0.snapshot_reserve(4, what_mask=3)
+    e0.set_run_snapshots(5, slot0=0)
+    r0 = e0.mcmc_run(lay, 0, nb, 3, 23)
+    ref, r1 = {}, []
+    for a, b in ((3, 5), (6, 10), (11, 15), (16, 20), (21, 25)):
+        r1.append(e1.mcmc_run(lay, 0, nb, a, b - a + 1))
+        ref[b] = (e1.download_paths(L.U, 0), e1.download_paths(L.U, 1))
+    assert np.array_equal(r0, np.concatenate(r1[:5]))
+    for slot, it in ((1, 10), (2, 15), (3, 20), (0, 25)):
+        X, got_it = e0.snapshot_download(slot, 0)
+        Wc, _ = e0.snapshot_download(slot, 1)
+        assert got_it == it
+        assert np.array_equal(X, ref[it][0]) and np.array_equal(Wc, ref[it][1])
+    e0.set_run_snapshots(0)
+    e0.close()
+    e1.close()
