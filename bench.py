@@ -138,10 +138,7 @@ def cpu_baseline(w, ens, lay, iter0, budget_s=12.0):
     B = w.nblocks
     npts = w.n_points[0][0]
     X = ens.download_paths(L.U, 0)
-    Wc = ens.download_paths(L.U, 1).reshape(B, npts, w.m)  # cumulative Wiener paths
-    Wp = Wc.copy()                                          # the oracle holds increments
-    Wp[:, 1:] = Wc[:, 1:] - Wc[:, :-1]
-    Wp = Wp.reshape(B * npts, w.m)
+    Wp = ens.download_paths(L.U, 2)  # the Wiener increments exactly as the device holds them
     ll = ens.get_block_state(lay, L.BLK_LL, 0, B)
     rho = np.full(B, w.rho)
     prec = w.precision

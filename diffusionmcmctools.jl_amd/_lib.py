@@ -21,6 +21,7 @@ MODEL_OU, MODEL_FHN, MODEL_LORENZ = 0, 1, 2
 F64, F32 = 0, 1
 MAP_AUTO, MAP_LANE, MAP_WAVE = 0, 1, 2
 U, UPROP = 0, 1
+PATH_X, PATH_W, PATH_DW = 0, 1, 2  # dmt_download_paths `what`
 LAW_PP, LAW_PPB = 0, 1
 SWAP_XX, SWAP_WW, SWAP_PP, SWAP_LL = 1, 2, 4, 8
 BLK_LL, BLK_LLPROP, BLK_LL_HIST, BLK_LLPROP_HIST, BLK_ACC_HIST = 0, 1, 2, 3, 4

@@ -91,6 +91,9 @@ struct Law {
   T da[HP];
   T thmu[D];  // Theta·mu of a linear (OU) drift, canonical order
   bool trace;
+  // non-linear drift with σ exactly the identity (d = m; C5's Lorenz): canonical M = H, c = F,
+  // σ·dW = dW, which the lane kernels take as a wave-uniform fast path
+  bool unit;
   __device__ __forceinline__ void load(const double* L) {
 #pragma unroll
     for (int i = 0; i < Mdl::NTH; ++i) th[i] = (T)ldc(L + DMT_LAW_THETA + i);
@@ -107,6 +110,11 @@ struct Law {
 #pragma unroll
     for (int i = 0; i < HP; ++i) da[i] = (T)ldc(L + DMT_LAW_DA + i);
     trace = ldc(L + DMT_LAW_TRACE) != 0.0;
+    unit = !Mdl::kLinear && D == M;
+#pragma unroll
+    for (int p = 0; p < D; ++p)
+#pragma unroll
+      for (int k = 0; k < M; ++k) unit = unit && sg[p * M + k] == (p == k ? (T)1 : (T)0);
     if (Mdl::kLinear) {
 #pragma unroll
       for (int p = 0; p < D; ++p) {
@@ -138,6 +146,25 @@ __device__ __forceinline__ void guide_coeffs(const Law<Mdl, T>& L, const T* H, c
 #pragma unroll
     for (int c = 1; c < D; ++c) f = dfma(L.a[packed_idx(D, p, c)], F[c], f);
     cg[p] = Mdl::kLinear ? (L.thmu[p] + f) : f;
+  }
+  if constexpr (!Mdl::kLinear) {  // σ = I: M = H, c = F exactly (canonical, per law)
+#pragma unroll
+    for (int p = 0; p < D; ++p) {
+#pragma unroll
+      for (int q = 0; q < D; ++q) Mg[p * D + q] = L.unit ? H[packed_idx(D, p, q)] : Mg[p * D + q];
+      cg[p] = L.unit ? F[p] : cg[p];
+    }
+  }
+}
+// guide_coeffs of a law with L.unit (the caller knows it for the whole wave): no arithmetic
+template <class Mdl, class T>
+__device__ __forceinline__ void guide_coeffs_unit(const T* H, const T* F, T* Mg, T* cg) {
+  constexpr int D = Mdl::D;
+#pragma unroll
+  for (int p = 0; p < D; ++p) {
+#pragma unroll
+    for (int q = 0; q < D; ++q) Mg[p * D + q] = H[packed_idx(D, p, q)];
+    cg[p] = F[p];
   }
 }
 
@@ -189,6 +216,7 @@ __device__ __forceinline__ void sigma_dw(const Law<Mdl, T>& L, const T* dW, T* s
     T v = L.sg[p * M + 0] * dW[0];
 #pragma unroll
     for (int k = 1; k < M; ++k) v = dfma(L.sg[p * M + k], dW[k], v);
+    if constexpr (!Mdl::kLinear && D == M) v = L.unit ? dW[p] : v;  // σ = I: σ·dW = dW exactly
     sdW[p] = v;
   }
 }

@@ -83,6 +83,12 @@ __device__ __forceinline__ bool run_segment(const Law<Mdl, T>& L, const T* __res
 
   // W planes hold increments: row 0 = W(t0), row i+1 = dW_i
   const int nst = np - 1;
+  // wave-uniform: every active lane's law has σ = I (the step's fast path)
+#ifdef DMT_NO_UNIT_FAST  // measurement variant: the generic path (per-lane selects) always
+  const bool all_unit = false;
+#else
+  const bool all_unit = !Mdl::kLinear && __ballot(L.unit) == __ballot(1);
+#endif
   T tcur = tb[0];
   if (cpx) {
 #pragma unroll
@@ -147,8 +153,19 @@ __device__ __forceinline__ bool run_segment(const Law<Mdl, T>& L, const T* __res
     }
     T r[D], b[D], sdW[D], Mg[D * D], cg[D];
     const T G = g_at<Mdl, T>(L, Hi, Fi, x, r, b);
-    sigma_dw<Mdl, T>(L, dW, sdW);
-    guide_coeffs<Mdl, T>(L, Hi, Fi, Mg, cg);
+    bool fast = false;
+    if constexpr (!Mdl::kLinear && D == M) {
+      if (all_unit) {  // every lane's law has σ = I: M = H, c = F, σ·dW = dW (canonical)
+#pragma unroll
+        for (int p = 0; p < D; ++p) sdW[p] = dW[p];
+        guide_coeffs_unit<Mdl, T>(Hi, Fi, Mg, cg);
+        fast = true;
+      }
+    }
+    if (!fast) {
+      sigma_dw<Mdl, T>(L, dW, sdW);
+      guide_coeffs<Mdl, T>(L, Hi, Fi, Mg, cg);
+    }
     euler_step<Mdl, T>(Mg, cg, b, dt, sdW, x);
 #pragma unroll
     for (int p = 0; p < D; ++p) Xdb[((int64_t)(i + 1) * D + p) * kLanes] = x[p];

@@ -936,13 +936,14 @@ dmt_status dmt_set_paths(dmt_ens* h, int32_t unit, const double* X, const double
 
 dmt_status dmt_download_paths(dmt_ens* h, int32_t unit, int32_t what, double* out) {
   DMT_TRY(check_h(h));
-  if ((unit != DMT_U && unit != DMT_UPROP) || (what != 0 && what != 1) || !out)
+  if ((unit != DMT_U && unit != DMT_UPROP) || what < 0 || what > 2 || !out)
     return fail(DMT_ERR_INVALID, "bad unit/what/out");
   const int C = what == 0 ? h->d : h->m;
   DMT_TRY(ensure_stage(h, h->P * C));
   void** src = what == 0 ? h->d_X : h->d_W;
-  if (what == 0)
-    HIP_OK(launch_from_planes(h->key.precision, h->tw, h->d_stage, src[0], src[1], h->d_sel[what], unit,
+  const int sk = what == 0 ? 0 : 1;  // selector kind
+  if (what != 1)  // XX, or the Wiener increments exactly as held (DMT_PATH_DW)
+    HIP_OK(launch_from_planes(h->key.precision, h->tw, h->d_stage, src[0], src[1], h->d_sel[sk], unit,
                               C, h->P, h->d_pt_off, h->G, h->d_seg_rec, h->d_seg_q, h->d_tile_qoff,
                               h->stream));
   else  // increments -> cumulative Wiener path

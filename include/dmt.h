@@ -192,7 +192,11 @@ dmt_status dmt_set_paths(dmt_ens* h, int32_t unit, const double* X, const double
 dmt_status dmt_download_law(dmt_ens* h, int32_t unit, int32_t kind, double* H, double* F,
                             double* laws);
 
-/* Download XX (what=0) / WW (what=1) of a unit, resolving all swaps, reference layout. */
+/* Download XX (what=0) / WW (what=1, the cumulative Wiener path) of a unit, resolving all
+ * swaps, reference layout; what=2 (DMT_PATH_DW): the Wiener increments exactly as the device
+ * holds them (row 0 = W(t0), row i+1 = ΔW_i; cumulating in the working precision and
+ * differencing back is not exact in fp32). */
+#define DMT_PATH_DW 2
 dmt_status dmt_download_paths(dmt_ens* h, int32_t unit, int32_t what, double* out);
 
 /* draw_proposal_path!(u::SamplingUnit) (src/sampling_unit.jl:118-120): rand! with no pCN

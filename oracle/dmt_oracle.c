@@ -190,9 +190,19 @@ static inline REAL g_at(int model, int d, const REAL* th, const REAL* a, const R
     return G;
 }
 
+/* A non-linear drift whose σ is exactly the identity (d = m): the canonical rule M = H, c = F,
+ * σ·dW = dW (libdmt dmt_device.h Law::unit). */
+static inline int law_unit(int model, int d, int m, const REAL* sg) {
+    if (model == ORC_OU || d != m) return 0;
+    for (int p = 0; p < d; ++p)
+        for (int k = 0; k < m; ++k)
+            if (sg[p * m + k] != (p == k ? (REAL)1 : (REAL)0)) return 0;
+    return 1;
+}
+
 /* Per-step guiding coefficients M (d×d row-major) and c (d) of the Euler update. */
 static inline void guide_coeffs(int model, int d, const REAL* th, const REAL* a, const REAL* H,
-                                const REAL* F, REAL* Mg, REAL* cg) {
+                                const REAL* F, REAL* Mg, REAL* cg, int unit) {
     for (int p = 0; p < d; ++p) {
         for (int q = 0; q < d; ++q) {
             REAL v = a[pidx(d, p, 0)] * H[pidx(d, 0, q)];
@@ -209,6 +219,12 @@ static inline void guide_coeffs(int model, int d, const REAL* th, const REAL* a,
             for (int c = 1; c < d; ++c) tm = FMA(th[p * d + c], th[9 + c], tm);
             for (int q = 0; q < d; ++q) Mg[p * d + q] = th[p * d + q] + Mg[p * d + q];
             cg[p] = tm + cg[p];
+        }
+    }
+    if (unit) { /* σ = I: M = H, c = F exactly */
+        for (int p = 0; p < d; ++p) {
+            for (int q = 0; q < d; ++q) Mg[p * d + q] = H[pidx(d, p, q)];
+            cg[p] = F[p];
         }
     }
 }
@@ -273,7 +289,7 @@ static int solve_segment_scan(int d, int m, const REAL* th, const REAL* sg, cons
                 REAL dt = t[i + 1] - t[i];
                 const REAL* dW = W + (size_t)(i + 1) * m;
                 REAL Mg[9], cg[3], sdw[3];
-                guide_coeffs(ORC_OU, d, th, a, H + (size_t)i * h, F + (size_t)i * d, Mg, cg);
+                guide_coeffs(ORC_OU, d, th, a, H + (size_t)i * h, F + (size_t)i * d, Mg, cg, 0);
                 for (int p = 0; p < d; ++p) {
                     REAL v = sg[p * m + 0] * dW[0];
                     for (int k = 1; k < m; ++k) v = FMA(sg[p * m + k], dW[k], v);
@@ -371,6 +387,7 @@ int SFX(orc_solve_segment)(int model, int d, int m, const double* law, int npts,
     int h = d * (d + 1) / 2;
     REAL th[16], sg[9], a[6], Bt[9], beta[3], da[6]; int trace;
     load_law(law, d, m, th, sg, a, Bt, beta, da, &trace);
+    const int unit = law_unit(model, d, m, sg);
     if (model == ORC_OU && !orc_sequential_ou)
         return solve_segment_scan(d, m, th, sg, a, Bt, beta, da, trace, npts, t, H, F, W, y1,
                                   X, ll_out);
@@ -386,7 +403,7 @@ int SFX(orc_solve_segment)(int model, int d, int m, const double* law, int npts,
         REAL G = g_at(model, d, th, a, Bt, beta, da, trace, Hi, Fi, x, r, b);
         ps_add(&ps, i < npts - 1 - orc_ll_skip ? G * dt : (REAL)0);
         REAL Mg[9], cg[3];
-        guide_coeffs(model, d, th, a, Hi, Fi, Mg, cg);
+        guide_coeffs(model, d, th, a, Hi, Fi, Mg, cg, unit);
         REAL xn[3];
         for (int p = 0; p < d; ++p) {
             REAL u = cg[p];
@@ -394,6 +411,7 @@ int SFX(orc_solve_segment)(int model, int d, int m, const double* law, int npts,
             REAL bg = (model == ORC_OU) ? u : (b[p] + u);
             REAL sdw = sg[p * m + 0] * dW[0];
             for (int k = 1; k < m; ++k) sdw = FMA(sg[p * m + k], dW[k], sdw);
+            if (unit) sdw = dW[p];
             xn[p] = FMA(bg, dt, x[p] + sdw);
         }
         for (int p = 0; p < d; ++p) { x[p] = xn[p]; X[(size_t)(i + 1) * d + p] = xn[p]; }
@@ -416,6 +434,7 @@ void SFX(orc_invsolve_segment)(int model, int d, int m, const double* law, int n
     int h = d * (d + 1) / 2;
     REAL th[16], sg[9], a[6], Bt[9], beta[3], da[6]; int trace;
     load_law(law, d, m, th, sg, a, Bt, beta, da, &trace);
+    const int unit = law_unit(model, d, m, sg);
     REAL siginv[9];
     for (int i = 0; i < 9; ++i) siginv[i] = (REAL)law[51 + i];
     for (int k = 0; k < m; ++k) W[k] = (REAL)0;
@@ -424,7 +443,7 @@ void SFX(orc_invsolve_segment)(int model, int d, int m, const double* law, int n
         const REAL* x = X + (size_t)i * d;
         const REAL* xn = X + (size_t)(i + 1) * d;
         REAL Mg[9], cg[3], b[3] = {0, 0, 0}, r[3];
-        guide_coeffs(model, d, th, a, H + (size_t)i * h, F + (size_t)i * d, Mg, cg);
+        guide_coeffs(model, d, th, a, H + (size_t)i * h, F + (size_t)i * d, Mg, cg, unit);
         if (model != ORC_OU) orc_drift(model, d, th, x, b);
         for (int p = 0; p < d; ++p) {
             REAL u = cg[p];

@@ -455,6 +455,8 @@ class OracleEnsemble:
         me = self._unit(unit)
         if what == 0:
             return np.concatenate(me.XX).astype(np.float64)
+        if what == 2:  # DMT_PATH_DW: the increments as held
+            return np.concatenate(me.WW).astype(np.float64)
         return np.concatenate([w_from_increments(w, self.prec) for w in me.WW]).astype(np.float64)
 
     # ---- layouts (BlockEnsemble ranges)

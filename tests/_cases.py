@@ -69,12 +69,12 @@ def both(w, seed=11, hist_len=0, init_Z=True, mapping=L.MAP_AUTO):
 
 def assert_paths_equal(dev, ora, exact=True, rtol=0.0, atol=0.0, equal_nan=False):
     for unit in (L.U, L.UPROP):
-        for what in (0, 1):
+        for what in (0, 1, 2):
             a = dev.download_paths(unit, what)
             b = ora.download_paths(unit, what)
             if exact:
                 assert np.array_equal(a, b, equal_nan=equal_nan), (
-                    f"unit {unit} {'XX' if what == 0 else 'WW'}: max |diff| "
+                    f"unit {unit} {('XX', 'WW', 'dW')[what]}: max |diff| "
                     f"{np.nanmax(np.abs(a - b))} at {np.unravel_index(np.nanargmax(np.abs(a - b)), a.shape)}")
             else:
                 np.testing.assert_allclose(a, b, rtol=rtol, atol=atol)

@@ -80,6 +80,25 @@ def test_c5_lorenz_fp32_reduced_bit_exact(mapping):
 
 
 @pytest.mark.parametrize("mapping", MAPPINGS)
+def test_c5_lorenz_mixed_unit_sigma_bit_exact(mapping):
+    """The canonical σ = I rule (M = H, c = F, σ·dW = dW for a non-linear drift):
+    every third block gets σ = 0.8·I, so lane-mapping waves mix laws with and without the
+    rule (the per-lane selects of the generic path) next to all-σ = I waves (the fast path);
+    device == oracle bit for bit, draws, decisions and find_W_for_X!."""
+    w = W.c5_lorenz(B=200, N=300)
+    laws = w.laws.copy()
+    for b in range(0, 200, 3):
+        for p in range(3):
+            laws[b, L.LAW_SIGMA + 3 * p + p] = 0.8
+        laws[b, L.LAW_A:L.LAW_A + 6] = [0.64, 0.0, 0.0, 0.64, 0.0, 0.64]
+    w.laws = laws
+    dev, ora, lay = run_mcmc_parity(w, iters=3, check_every=False, mapping=mapping)
+    for e in (dev, ora):
+        e.find_W_for_X(lay, 0, w.nblocks)
+    cs.assert_paths_equal(dev, ora)
+
+
+@pytest.mark.parametrize("mapping", MAPPINGS)
 def test_ragged_blocking_layouts_bit_exact(mapping):
     """Multi-segment recordings, non-terminal blocks with P_last laws, two alternating block
     layouts aliasing the same SamplingPair (src/block.jl:66-72), swaps, loglikhd of both units,
