@@ -474,6 +474,8 @@ __global__ __launch_bounds__(128, DMT_PS_MINW) void k_block_ps(const BlockArgs<T
     Law<Mdl, T> LA;
     const int ls = act ? (a.selPP[g] ^ a.law_flip) : 0;
     LA.load(a.law[ls][0] + (int64_t)g * DMT_LAW_STRIDE);
+    // wave-uniform: every active lane's law has σ = I (the step's fast path, as in k_block)
+    const bool all_unit = !Mdl::kLinear && __ballot(!act || LA.unit) == __ballot(1);
     const T* Hb = a.H_shared[ls][0] ? a.H[ls][0] + (act ? a.seg_q[g] : 0) * HP : a.H[ls][0] + row * HP * kLanes + lane;
     const int hst = a.H_shared[ls][0] ? 1 : kLanes;
     const T* Fb = a.F[ls][0] + row * D * kLanes + lane;
@@ -538,8 +540,19 @@ __global__ __launch_bounds__(128, DMT_PS_MINW) void k_block_ps(const BlockArgs<T
             for (int k = 0; k < M; ++k) dW[k] = s_dw[buf][q * K + j][k][lane];
             T rr[D], b[D], sdW[D], Mg[D * D], cg[D];
             const T G = g_at<Mdl, T>(LA, cur.H[j], cur.F[j], x, rr, b);
-            sigma_dw<Mdl, T>(LA, dW, sdW);
-            guide_coeffs<Mdl, T>(LA, cur.H[j], cur.F[j], Mg, cg);
+            bool fast = false;
+            if constexpr (!Mdl::kLinear && D == M) {
+              if (all_unit) {
+#pragma unroll
+                for (int p = 0; p < D; ++p) sdW[p] = dW[p];
+                guide_coeffs_unit<Mdl, T>(cur.H[j], cur.F[j], Mg, cg);
+                fast = true;
+              }
+            }
+            if (!fast) {
+              sigma_dw<Mdl, T>(LA, dW, sdW);
+              guide_coeffs<Mdl, T>(LA, cur.H[j], cur.F[j], Mg, cg);
+            }
             T xn[D];
 #pragma unroll
             for (int p = 0; p < D; ++p) xn[p] = x[p];
