@@ -60,6 +60,79 @@ class SamplingEnsemble:
             device=device, grid_shared=grid_shared, mapping=mapping)
         self.recordings = [SamplingPair(self, r) for r in range(len(self.n_points))]
 
+    @classmethod
+    def from_recordings(cls, model, recordings, tts, aux_laws=None, aux_laws_blocking=None,
+                        artificial_noise=1e-11, blocking=True, precision=L.F64, seed=0,
+                        device=0, mapping=L.MAP_AUTO, init=True, _engine=None):
+        """``SamplingEnsemble(aux_laws, recordings, tts; aux_laws_blocking, artificial_noise)``
+        (src/sampling_ensemble.jl:13-41 → ``SamplingPair`` → ``SamplingUnit``,
+        src/sampling_unit.jl:55-74): the containers built from the recordings and their laws,
+        not from hand-packed tables.
+
+        * ``build_guid_prop`` (:60): per segment k of recording r the auxiliary law
+          ``aux_laws(model, r, k, obs)`` (default ``model.aux_for(obs)``: the law linearised at
+          the observation, as FitzHughNagumoAux / the Lorenz aux of the configs); guiding terms
+          by the exact backward filter over the recording's segments (``models.guiding_chain``,
+          libdmt's host ``dmt_guiding_linear``), law records ``model.law_record(aux, c(t0))``;
+        * ``guid_prop_for_blocking`` (:61-66, ``blocking``): per segment the same law with an
+          extra exact full-state artificial observation of noise ``artificial_noise`` at the
+          segment end — a placeholder (the observed coordinates, zeros elsewhere) until
+          ``set_obs!`` freezes the accepted end point; ``aux_laws_blocking``
+          defaults to ``aux_laws``;
+        * the observations for the device's re-derivations (``set_observations``) and
+          ``init_paths!`` from each recording's ``x0`` (``init``).
+        ``tts[r][k]``: the grid of segment k of recording r (``setup_time_grids``)."""
+        from .models import artificial_obs_info, guiding_chain, packed
+        aux_laws = aux_laws or (lambda mdl, r, k, ob: mdl.aux_for(ob))
+        aux_laws_blocking = aux_laws_blocking or aux_laws
+        d = model.d
+        t_all, H_all, F_all, laws, n_points, infos_all = [], [], [], [], [], []
+        Hb_all, Fb_all, lawsb = [], [], []
+        for r, rec in enumerate(recordings):
+            grids = [np.asarray(g, dtype=np.float64) for g in tts[r]]
+            if len(grids) != len(rec.obs):
+                raise ValueError(f"recording {r}: {len(rec.obs)} observations, {len(grids)} grids")
+            auxes = [aux_laws(model, r, k, ob) for k, ob in enumerate(rec.obs)]
+            infos = [ob.info() for ob in rec.obs]
+            chain = guiding_chain(auxes, grids, infos)
+            t_all += grids
+            H_all += [c[0] for c in chain]
+            F_all += [c[1] for c in chain]
+            laws += [model.law_record(a_, c[2][0]) for a_, c in zip(auxes, chain)]
+            n_points.append([len(g) for g in grids])
+            infos_all += infos
+            if blocking:
+                for k, ob in enumerate(rec.obs):
+                    a_ = aux_laws_blocking(model, r, k, ob)
+                    v = np.zeros(d)
+                    vo = np.atleast_1d(np.asarray(ob.v, dtype=np.float64))
+                    v[:min(d, vo.size)] = vo[:d]
+                    Ha, Fa, ca = artificial_obs_info(v, artificial_noise)
+                    Ho, Fo, co = infos[k]
+                    (h, f, c), = guiding_chain([a_], [grids[k]], [(Ha + Ho, Fa + Fo, ca + co)])
+                    Hb_all.append(h)
+                    Fb_all.append(f)
+                    lawsb.append(model.law_record(a_, c[0]))
+        if callable(_engine):  # test seam: an engine factory of the structure
+            _engine = _engine(n_points)
+        se = cls(model, n_points, precision=precision, seed=seed, device=device,
+                 mapping=mapping, _engine=_engine)
+        se.upload_grid(np.concatenate(t_all))
+        blaws = {}
+        if blocking:
+            blaws = dict(Hb=np.concatenate(Hb_all), Fb=np.concatenate(Fb_all),
+                         lawsb=np.stack(lawsb))
+        se.set_guiding(np.concatenate(H_all), np.concatenate(F_all), np.stack(laws), **blaws)
+        se.set_observations(np.stack([packed(i[0]) for i in infos_all]),
+                            np.stack([np.asarray(i[1], dtype=np.float64) for i in infos_all]),
+                            np.array([float(i[2]) for i in infos_all]),
+                            artificial_noise=artificial_noise)
+        if init:
+            _, ok = se.init_paths([rec.x0 for rec in recordings])
+            if not ok.all():
+                raise RuntimeError("init_paths failed")
+        return se
+
     def num_recordings(self):
         return len(self.recordings)
 

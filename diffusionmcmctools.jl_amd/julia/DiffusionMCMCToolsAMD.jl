@@ -12,6 +12,7 @@ tested.  See INTEGRATION.md for the wiring into the reference package.
 module DiffusionMCMCToolsAMD
 
 using StaticArrays
+using LinearAlgebra: I, det, inv
 
 import DiffusionMCMCTools: draw_proposal_path!, accept_reject_proposal_path!, loglikhd!,
     loglikhd°!, fetch_ll, fetch_ll°, save_ll!, set_ll!, set_accepted!, swap_paths!, swap_XX!,
@@ -20,7 +21,8 @@ import DiffusionMCMCTools: draw_proposal_path!, accept_reject_proposal_path!, lo
 
 export DeviceSamplingEnsemble, DeviceBlockEnsemble, DeviceBlockCollection, DeviceBiBlock,
     mcmc_step!, mcmc_run!, download_XX, download_WW, upload_obs!, set_obs!,
-    recompute_guiding_term!, set_proposal_law!, snapshot_every!, equalize_obs_params!
+    recompute_guiding_term!, set_proposal_law!, snapshot_every!, equalize_obs_params!,
+    law_record, guiding_linear
 
 const libdmt = get(ENV, "DMT_LIB", joinpath(@__DIR__, "..", "libdmt.so"))
 
@@ -176,6 +178,149 @@ function draw_unit!(se::DeviceSamplingEnsemble, unit, r0, r1; Z=nothing, iter=no
         (Ptr{Cvoid}, Int32, Int64, Int64, Ptr{Float64}, Int64, UInt32, Ptr{Float64}, Ptr{UInt8}),
         se.h, unit, r0, r1, pz, iter, salt, ll, ok))
     Bool.(ok), ll
+end
+
+# ============================================================ containers from laws
+# The reference builds its containers from laws: SamplingUnit(aux_laws, recording, tts;
+# aux_laws_blocking, artificial_noise) → build_guid_prop / guid_prop_for_blocking
+# (src/sampling_unit.jl:55-74).  The functions below do the same for the device from the
+# laws' coefficients — the target's parameters and σ, each auxiliary law's (B̃, β̃, σ̃) — with
+# the exact backward filter of dmt_guiding_linear (the Python mirror
+# `SamplingEnsemble.from_recordings`, tests/test_api.py, is the tested twin).
+
+"Upper triangle of a symmetric matrix, row-major (the device's packed H)."
+packed(M::AbstractMatrix) = [M[i, j] for i in 1:size(M, 1) for j in i:size(M, 2)]
+unpacked(p::AbstractVector, d) = (M = zeros(d, d); k = 0;
+    for i in 1:d, j in i:d; k += 1; M[i, j] = M[j, i] = p[k]; end; M)
+
+"""
+    law_record(θrec, σ, B̃, β̃, σ̃, c0; anchor=nothing)
+
+One segment's law record (DMT_LAW_STRIDE doubles, include/dmt.h): θrec = the target's
+parameters in the device order (OU: Θ row-major at 1:d², μ at 10:9+d; FHN: 1/ϵ, s, γ, β, ϵ, σ;
+Lorenz: s, r, β), σ (d×m), the auxiliary law's B̃, β̃, σ̃, c(t₀), and the linearisation point
+of a linearised auxiliary law (FitzHughNagumoAux: y_T; Lorenz: x_T).
+"""
+function law_record(θrec, σ::AbstractMatrix, B̃::AbstractMatrix, β̃, σ̃::AbstractMatrix, c0;
+                    anchor=nothing)
+    d, m = size(σ)
+    hp = d * (d + 1) ÷ 2
+    rec = zeros(DMT_LAW_STRIDE)
+    rec[1:length(θrec)] .= θrec                                    # DMT_LAW_THETA 0
+    rec[17:16+d*m] .= vec(permutedims(σ))                          # DMT_LAW_SIGMA 16
+    a, ã = σ * σ', σ̃ * σ̃'
+    rec[26:25+hp] .= packed(a)                                      # DMT_LAW_A 25
+    rec[32:31+d*d] .= vec(permutedims(B̃))                          # DMT_LAW_BT 31
+    rec[41:40+d] .= β̃                                              # DMT_LAW_BETA 40
+    da = a - ã
+    rec[44:43+hp] .= packed(da)                                     # DMT_LAW_DA 43
+    rec[50] = c0                                                    # DMT_LAW_C0 49
+    rec[51] = any(!iszero, da) ? 1.0 : 0.0                          # DMT_LAW_TRACE 50
+    d == m && (rec[52:51+d*d] .= vec(permutedims(inv(σ))))          # DMT_LAW_SIGINV 51
+    if anchor !== nothing                                           # DMT_LAW_ANCHOR 60
+        rec[61:60+length(anchor)] .= anchor
+        rec[64] = 1.0                                               # DMT_LAW_AUXLIN 63
+    end
+    rec
+end
+
+"""
+    guiding_linear(B̃, β̃, σ̃, t, HT, FT, cT) -> (H, F, c)
+
+The guiding term of a linear auxiliary law on grid `t` from the end information (HT, FT, cT):
+dmt_guiding_linear (the exact discrete filter, DESIGN.md §3).  H: npts × d(d+1)/2 (packed,
+one row per point), F: npts × d, c: npts.
+"""
+function guiding_linear(B̃, β̃, σ̃, t::Vector{Float64}, HT::AbstractMatrix, FT, cT)
+    d, n = length(β̃), length(t)
+    hp = d * (d + 1) ÷ 2
+    Bt, β, at = vec(permutedims(Float64.(B̃))), Float64.(collect(β̃)), packed(σ̃ * σ̃')
+    HTp, FTv = packed(HT), Float64.(collect(FT))
+    H, F, c = Matrix{Float64}(undef, hp, n), Matrix{Float64}(undef, d, n), Vector{Float64}(undef, n)
+    check(ccall((:dmt_guiding_linear, libdmt), Int32,
+        (Int32, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Int32, Ptr{Float64}, Ptr{Float64},
+         Ptr{Float64}, Float64, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}),
+        d, Bt, β, at, n, t, HTp, FTv, cT, H, F, c))
+    permutedims(H), permutedims(F), c
+end
+
+"Information (H, F, c) of an observation v ~ N(L x, Σ) (ObservationSchemes LinearGsnObs)."
+function obs_info(v, L::AbstractMatrix, Σ::AbstractMatrix)
+    Si = inv(Σ)
+    H, F = L' * Si * L, L' * Si * v
+    H, F, 0.5 * v' * Si * v + 0.5 * length(v) * log(2π) + 0.5 * log(det(Σ))
+end
+
+"""
+    DeviceSamplingEnsemble(model, θrec, σ, recordings, tts, aux; artificial_noise=1e-11,
+                           blocking=true, kw...)
+
+`SamplingEnsemble(aux_laws, recordings, tts; artificial_noise)` on the device:
+`recordings[r] = (obs = [(t, v, L, Σ), …], x0 = …)`, `tts[r][k]` the grid of segment k,
+`aux(r, k, obs) -> (B̃, β̃, σ̃, anchor)` the auxiliary law of segment k (e.g. FitzHughNagumoAux
+linearised at the observed y: `(DD.B(t0, P̃), DD.β(t0, P̃), DD.σ(t0, x, P̃), yT)`).  Guiding terms
+through each recording's segments (build_guid_prop), blocking laws with an exact full-state
+artificial end observation (guid_prop_for_blocking; a placeholder until set_obs!), the
+observations for the device's re-derivations, then init_paths! from x0.
+"""
+function DeviceSamplingEnsemble(model::Integer, θrec, σ::AbstractMatrix, recordings, tts, aux;
+                                artificial_noise=1e-11, blocking=true, kw...)
+    d, m = size(σ)
+    t_all, H_all, F_all, laws, infos = Float64[], Matrix{Float64}[], Matrix{Float64}[], Vector{Float64}[], Any[]
+    Hb_all, Fb_all, lawsb = Matrix{Float64}[], Matrix{Float64}[], Vector{Float64}[]
+    n_points = Vector{Int}[]
+    for (r, rec) in enumerate(recordings)
+        K = length(rec.obs)
+        auxes = [aux(r, k, rec.obs[k]) for k in 1:K]
+        info = [obs_info(o.v, o.L, o.Σ) for o in rec.obs]
+        chain = Vector{Any}(undef, K)
+        nxt = nothing
+        for k in K:-1:1                      # segment k ends in obs k, then segment k+1 starts
+            HT, FT, cT = info[k]
+            if nxt !== nothing
+                HT, FT, cT = HT + unpacked(nxt[1], d), FT + nxt[2], cT + nxt[3]
+            end
+            B̃, β̃, σ̃, _ = auxes[k]
+            H, F, c = guiding_linear(B̃, β̃, σ̃, Float64.(tts[r][k]), HT, FT, cT)
+            chain[k] = (H, F, c)
+            nxt = (H[1, :], F[1, :], c[1])
+        end
+        for k in 1:K
+            B̃, β̃, σ̃, an = auxes[k]
+            append!(t_all, tts[r][k]); push!(H_all, chain[k][1]); push!(F_all, chain[k][2])
+            push!(laws, law_record(θrec, σ, B̃, β̃, σ̃, chain[k][3][1]; anchor=an))
+            push!(infos, info[k])
+            if blocking
+                v = zeros(d); vo = collect(rec.obs[k].v); v[1:min(d, length(vo))] .= vo[1:min(d, length(vo))]
+                Ha, Fa, ca = obs_info(v, Matrix(1.0I, d, d), artificial_noise * Matrix(1.0I, d, d))
+                Ho, Fo, co = info[k]
+                H, F, c = guiding_linear(B̃, β̃, σ̃, Float64.(tts[r][k]), Ha + Ho, Fa + Fo, ca + co)
+                push!(Hb_all, H); push!(Fb_all, F)
+                push!(lawsb, law_record(θrec, σ, B̃, β̃, σ̃, c[1]; anchor=an))
+            end
+        end
+        push!(n_points, [length(g) for g in tts[r]])
+    end
+    se = DeviceSamplingEnsemble(model, d, m, n_points; kw...)
+    upload_grid!(se, t_all)
+    flat(Ms) = vec(permutedims(reduce(vcat, Ms)))     # point-major, components contiguous
+    upload_law!(se, DMT_U, DMT_LAW_PP, flat(H_all), flat(F_all), reduce(vcat, laws))
+    blocking && upload_law!(se, DMT_U, DMT_LAW_PPB, flat(Hb_all), flat(Fb_all), reduce(vcat, lawsb))
+    upload_obs!(se, reduce(vcat, [packed(i[1]) for i in infos]),
+                reduce(vcat, [collect(i[2]) for i in infos]), Float64[i[3] for i in infos];
+                artificial_noise=artificial_noise)
+    X = zeros(d, se.P)                                # init_paths!: start points, fresh draws
+    p = 1
+    for (r, rec) in enumerate(recordings)
+        X[:, p] .= rec.x0
+        p += sum(n_points[r])
+    end
+    set_paths!(se, DMT_U, vec(X))
+    ok, _ = draw_unit!(se, DMT_U, 0, length(recordings))
+    all(ok) || error("init_paths!: a recording's first draw failed")
+    flat_paths(A) = collect(reinterpret(Float64, A))
+    set_paths!(se, DMT_UPROP, flat_paths(download_XX(se)), flat_paths(download_WW(se)))
+    se
 end
 
 # ============================================================ blocks

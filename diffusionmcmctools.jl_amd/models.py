@@ -65,6 +65,11 @@ class Model:
     def drift(self, x):
         raise NotImplementedError
 
+    def aux_for(self, obs):
+        """The auxiliary law of a segment ending in observation ``obs`` (the reference's
+        ``AuxLaw(…, obs)`` of build_guid_prop): linearised at the observed value."""
+        raise NotImplementedError
+
     def law_record(self, aux: LinearAux, c0: float = 0.0) -> np.ndarray:
         rec = np.zeros(L.LAW_STRIDE)
         th = self.theta_vec()
@@ -127,6 +132,9 @@ class OU(Model):
     def drift(self, x):
         return -self.Theta @ (np.asarray(x) - self.mu)
 
+    def aux_for(self, obs):
+        return self.aux()
+
     def aux(self, Theta_t=None, mu_t=None, sigma_t=None):
         """OU auxiliary law (Theta_t, mu_t): Bt = -Theta_t, beta = Theta_t mu_t."""
         Th = self.Theta if Theta_t is None else np.atleast_2d(np.asarray(Theta_t, dtype=np.float64))
@@ -157,6 +165,9 @@ class FHN(Model):
         y, v = x
         return np.array([(y - y ** 3 - v + self.s) / self.eps, self.gamma * y - v + self.beta])
 
+    def aux_for(self, obs):
+        return self.aux(np.atleast_1d(obs.v)[0])  # FitzHughNagumoAux at the observed y
+
     def aux(self, yT):
         """FitzHughNagumoAux: linearisation at the observed end value yT (the arithmetic
         order of the device's set_proposal_law! re-derivation)."""
@@ -185,6 +196,9 @@ class Lorenz(Model):
     def drift(self, x):
         x0, x1, x2 = x
         return np.array([self.s_ * (x1 - x0), x0 * (self.r - x2) - x1, x0 * x1 - self.b * x2])
+
+    def aux_for(self, obs):
+        return self.aux(obs.v)  # full-state observation
 
     def aux(self, v):
         """Linearisation of the drift at the point v."""

@@ -39,7 +39,6 @@ if ROOT not in sys.path:
 import diffusionmcmctools_amd as dmt  # noqa: E402
 from diffusionmcmctools_amd import _lib as L  # noqa: E402
 from diffusionmcmctools_amd.models import (FHN, Observation, Recording,  # noqa: E402
-                                           artificial_obs_info, guiding_chain, packed,
                                            setup_time_grids)
 
 THETA = (0.1, -0.8, 1.5, 0.0, 0.3)      # ϵ, s, γ, β, σ (preamble.md:53)
@@ -101,46 +100,16 @@ def sampling_pair(recording, gamma, dt=1e-3, backend="device", seed=0, blocking=
     th[2] = gamma
     model = FHN(*th)
     recordings = recording if isinstance(recording, (list, tuple)) else [recording]
-    t_all, H_all, F_all, law_all, n_points, infos_all = [], [], [], [], [], []
-    Hb_all, Fb_all, lb_all = [], [], []
-    for rec in recordings:
-        grids = setup_time_grids(rec, dt)
-        auxes = [model.aux(ob.v[0]) for ob in rec.obs]
-        infos = [ob.info() for ob in rec.obs]
-        chain = guiding_chain(auxes, grids, infos)
-        t_all += grids
-        H_all += [c[0] for c in chain]
-        F_all += [c[1] for c in chain]
-        law_all += [model.law_record(a_, c[2][0]) for a_, c in zip(auxes, chain)]
-        n_points.append([len(g) for g in grids])
-        infos_all += infos
-        if blocking:
-            for k, (a_, ob) in enumerate(zip(auxes, rec.obs)):
-                Ha, Fa, ca = artificial_obs_info(np.array([ob.v[0], 0.0]), ARTIFICIAL_NOISE)
-                Ho, Fo, co = infos[k]
-                (h, f, c), = guiding_chain([a_], [grids[k]], [(Ha + Ho, Fa + Fo, ca + co)])
-                Hb_all.append(h); Fb_all.append(f); lb_all.append(model.law_record(a_, c[0]))
-    H, F, laws = np.concatenate(H_all), np.concatenate(F_all), np.stack(law_all)
-    infos = infos_all
-    blaws = {}
-    if blocking:
-        blaws = dict(Hb=np.concatenate(Hb_all), Fb=np.concatenate(Fb_all), lawsb=np.stack(lb_all))
+    engine = None
     if backend == "oracle":
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle as orc
-        eng = orc.OracleEnsemble(model.kind, model.d, model.m, n_points, prec=L.F64, seed=seed)
-        se = dmt.SamplingEnsemble(model, n_points, _engine=eng)
-    else:
-        se = dmt.SamplingEnsemble(model, n_points, seed=seed)
-    se.upload_grid(np.concatenate(t_all))
-    se.set_guiding(H, F, laws, **blaws)
-    se.set_observations(np.stack([packed(i[0]) for i in infos]),
-                        np.stack([np.asarray(i[1], dtype=np.float64) for i in infos]),
-                        np.array([float(i[2]) for i in infos]), artificial_noise=ARTIFICIAL_NOISE)
-    ll0, ok = se.init_paths([rec.x0 for rec in recordings])
-    if not ok.all():
-        raise RuntimeError("init_paths failed")
-    return se
+        engine = lambda n_points: orc.OracleEnsemble(model.kind, model.d, model.m, n_points,  # noqa: E731
+                                                     prec=L.F64, seed=seed)
+    # SamplingPair(FitzHughNagumoAux, recording, tts) / SamplingEnsemble(…, recordings, tts)
+    return dmt.SamplingEnsemble.from_recordings(
+        model, recordings, [setup_time_grids(rec, dt) for rec in recordings],
+        artificial_noise=ARTIFICIAL_NOISE, blocking=blocking, seed=seed, _engine=engine)
 
 
 def simple_inference(se, gamma0, eps=0.3, rho=0.96, num_steps=10 ** 4, seed=1,

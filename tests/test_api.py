@@ -284,3 +284,43 @@ def test_equalize_obs_params_is_a_no_op_on_shared_observations():
     assert crit.dtype == bool and crit.shape == (be.num_blocks,) and not crit.any()
     assert np.array_equal(se.ens.download_paths(L.U, 0), X0)
     assert np.array_equal(be.ll, ll0)
+
+
+def test_from_recordings_builds_the_reference_containers():
+    """SamplingEnsemble.from_recordings(model, recordings, tts) — the reference's
+    SamplingEnsemble(aux_laws, recordings, tts; artificial_noise) (src/sampling_unit.jl:55-74):
+    laws linearised at each observation, guiding terms through the recording's segments,
+    blocking laws with the artificial end observation, observations uploaded, init_paths! —
+    equal to the tables built by hand from the same pieces (models.guiding_chain)."""
+    from diffusionmcmctools_amd.models import (FHN, Observation, Recording, guiding_chain,
+                                               setup_time_grids)
+    model = FHN(0.1, -0.8, 1.5, 0.0, 0.3)
+    recs = [Recording(obs=[Observation(0.1 * (k + 1), np.array([y]), np.array([[1.0, 0.0]]),
+                                       np.array([[0.01]])) for k, y in enumerate(ys)],
+                      t0=0.0, x0=np.array([-0.9, -1.0]))
+            for ys in ([-0.5, 0.2, 0.9], [0.1, -0.3])]
+    tts = [setup_time_grids(r, 0.01) for r in recs]
+
+    def engine(n_points):
+        return orc.OracleEnsemble(model.kind, model.d, model.m, n_points, prec=L.F64, seed=3)
+    se = dmt.SamplingEnsemble.from_recordings(model, recs, tts, artificial_noise=1e-11,
+                                              _engine=engine)
+    assert se.n_points == [[len(g) for g in t] for t in tts]
+    H, F, laws = se.ens.download_law(L.U, L.LAW_PP)
+    for r, rec in enumerate(recs):
+        auxes = [model.aux(ob.v[0]) for ob in rec.obs]
+        chain = guiding_chain(auxes, tts[r], [ob.info() for ob in rec.obs])
+        g0 = sum(len(x) for x in recs[:r] for x in [x.obs])
+        p0 = sum(len(g) for t in tts[:r] for g in t)
+        for k, (h, f, c) in enumerate(chain):
+            n = len(tts[r][k])
+            assert np.array_equal(H[p0:p0 + n], h) and np.array_equal(F[p0:p0 + n], f)
+            assert np.array_equal(laws[g0 + k], model.law_record(auxes[k], c[0]))
+            p0 += n
+    Hb, Fb, lawsb = se.ens.download_law(L.U, L.LAW_PPB)
+    assert np.all(np.isfinite(Hb)) and Hb.max() > 1e10   # the 1e-11 artificial observation
+    X = se.ens.download_paths(L.U, 0)
+    assert np.all(np.isfinite(X))
+    be = dmt.BlockEnsemble(se, [[range(0, 3)], [range(0, 2)]], rho=0.5, ll_hist_len=2)
+    be.loglikhd()
+    assert np.isfinite(be.fetch_ll())
