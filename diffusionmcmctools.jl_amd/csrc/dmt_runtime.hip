@@ -157,6 +157,7 @@ struct dmt_ens {
   double* h_red = nullptr;  // pinned host copy of the 3 reduction results
   double* d_gather = nullptr;
   double* d_run = nullptr;         // dmt_mcmc_run: [n][3] per-iteration reductions
+  double* h_run_dev = nullptr;     // h_run's device address (hipHostGetDevicePointer, once)
   double* h_run = nullptr;         // pinned host [run_cap][3]: one rank's results, written by
                                    // the kernels directly (no device-to-host copy)
   double* d_run_gather = nullptr;  // [n][nranks][3] (persistent path: [nranks][n][3])
@@ -1232,7 +1233,7 @@ dmt_status dmt_mcmc_run(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int6
   const bool multi = h->comm != nullptr;
   if (n_iter > h->run_cap) {
     if (h->d_run) { (void)hipFree(h->d_run); h->bytes -= h->run_cap * 24; h->d_run = nullptr; }
-    if (h->h_run) { (void)hipHostFree(h->h_run); h->h_run = nullptr; }
+    if (h->h_run) { (void)hipHostFree(h->h_run); h->h_run = nullptr; h->h_run_dev = nullptr; }
     if (h->d_run_gather) {
       (void)hipFree(h->d_run_gather);
       h->bytes -= h->run_cap * 24 * h->nranks;
@@ -1242,6 +1243,9 @@ dmt_status dmt_mcmc_run(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int6
     h->run_cap = 0;
     DMT_TRY(ens_alloc(h, &h->d_run, 3 * cap));
     HIP_OK(hipHostMalloc((void**)&h->h_run, 3 * cap * sizeof(double), hipHostMallocDefault));
+    void* dp = nullptr;
+    HIP_OK(hipHostGetDevicePointer(&dp, h->h_run, 0));
+    h->h_run_dev = static_cast<double*>(dp);
     if (multi) DMT_TRY(ens_alloc(h, &h->d_run_gather, 3 * cap * h->nranks));
     h->run_cap = cap;
   } else if (multi && !h->d_run_gather) {
@@ -1250,12 +1254,7 @@ dmt_status dmt_mcmc_run(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int6
   DMT_TRY(ensure_red_work(h, b1 - b0));
   // per-iteration results: one rank → straight into pinned host memory; several → device
   // memory for the all-gather
-  double* run_out = h->d_run;
-  if (!multi) {
-    void* dp = nullptr;
-    HIP_OK(hipHostGetDevicePointer(&dp, h->h_run, 0));
-    run_out = static_cast<double*>(dp);
-  }
+  double* run_out = multi ? h->d_run : h->h_run_dev;
   const int64_t nb = b1 - b0;
   bool persist = h->persist && h->key.model == DMT_MODEL_OU;
   for (int64_t b = b0; b < b1 && persist; ++b)

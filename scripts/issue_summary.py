@@ -48,8 +48,9 @@ def main():
         by_id[did].update(v)
     rows = []
     for did, v in by_id.items():
-        if "SQ_WAVES" not in v or "SQ_INSTS_VALU_FMA_F64" not in v:
+        if "SQ_WAVES" not in v:
             continue
+        fma = v.get("SQ_INSTS_VALU_FMA_F64", v.get("SQ_INSTS_VALU_FMA_F32"))
         w, wc, n = v["SQ_WAVES"], v["SQ_WAVE_CYCLES"], a.iters
         wps = w / a.simds
         rows.append({
@@ -58,13 +59,13 @@ def main():
             "valu_insts_per_wave_iteration": v["SQ_INSTS_VALU"] / w / n,
             "valu_insts_per_block_iteration": v["SQ_INSTS_VALU"] / a.blocks / n,
             "valu_insts_per_step": v["SQ_INSTS_VALU"] / a.blocks / n / a.steps_per_block,
-            "fma_f64_per_block_iteration": v["SQ_INSTS_VALU_FMA_F64"] / a.blocks / n,
-            "lds_insts_per_block_iteration": v["SQ_INSTS_LDS"] / a.blocks / n,
+            "fma_per_block_iteration": None if fma is None else fma / a.blocks / n,
+            "lds_insts_per_block_iteration": v["SQ_INSTS_LDS"] / a.blocks / n if "SQ_INSTS_LDS" in v else None,
             "wave_cycles_per_iteration": 4 * wc / w / n,
             "valu_active_frac": v["SQ_ACTIVE_INST_VALU"] / wc,
             "simd_valu_busy": v["SQ_ACTIVE_INST_VALU"] / wc * wps,
             "wait_any_frac": v["SQ_WAIT_ANY"] / wc,
-            "lds_wait_frac": v["SQ_WAIT_INST_LDS"] / wc,
+            "lds_wait_frac": v["SQ_WAIT_INST_LDS"] / wc if "SQ_WAIT_INST_LDS" in v else None,
         })
     if not rows:
         raise SystemExit("no dispatch of that kernel carries both passes")
@@ -72,7 +73,8 @@ def main():
            "source_counters": [os.path.relpath(p) for p in a.csv],
            "command": a.command, "iterations_per_dispatch": a.iters, "dispatches": len(rows)}
     for k in rows[0]:
-        out[k] = statistics.median(r[k] for r in rows)
+        vals = [r[k] for r in rows if r[k] is not None]
+        out[k] = statistics.median(vals) if vals else None
     out["frac"] = out["simd_valu_busy"]
     out["bound"] = a.bound
     out["limiter"] = a.limiter
