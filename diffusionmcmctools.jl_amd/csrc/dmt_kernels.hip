@@ -1956,21 +1956,33 @@ __global__ __launch_bounds__(256, 1) void k_mcmc_resident(const BlockArgs<T> a,
 // iteration n, so the two waves of every SIMD issue concurrently.  The operations and their
 // order are resident_block's: bit-identical results (the GPU tests run both).
 #ifndef DMT_PC_DRAW_GROUP
-#define DMT_PC_DRAW_GROUP 1
+#define DMT_PC_DRAW_GROUP 8
 #endif
+#ifndef DMT_PC_CONS_STEPS
+#define DMT_PC_CONS_STEPS 2
+#endif
+// With one producer, the consumer draws the normals (and forms dW°, e) of the last CR steps of
+// every lane run itself, filling its own latency bubbles and shortening the producer's chain;
+// only when those steps hold whole Philox blocks.
+template <class T, int M, int NP>
+struct PcConsSteps {
+  static constexpr int v = (NP == 1 && (DMT_PC_CONS_STEPS * M) % NormPerBlock<T>::v == 0)
+                               ? DMT_PC_CONS_STEPS : 0;
+};
 template <int D, int M, class T>
 struct ResPcLds {
   ResLds<D, M, T> r;  // pt: X° staging; dw: the dW° hand-off and W° staging; hf: H_i, F_i
   int acc;            // the consumer's decision of the current iteration
 };
 
-template <class Mdl, class T>
+template <class Mdl, class T, int NP>
 __device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, const AcceptArgs& c,
                                                      const int64_t iter0, const int64_t n_iter,
                                                      double* __restrict__ part, const int64_t blk,
                                                      const bool valid,
                                                      ResPcLds<Mdl::D, Mdl::M, T>& P) {
   constexpr int D = Mdl::D, M = Mdl::M, HP = D * (D + 1) / 2;
+  constexpr int CR = PcConsSteps<T, M, NP>::v, RC0 = kRun - CR, CRA = CR > 0 ? CR : 1;
   ResLds<D, M, T>& S = P.r;
   const int lane = threadIdx.x & 63;
   const int64_t vb = valid ? blk : a.b0;  // an idle wave reads a valid block's metadata
@@ -2006,7 +2018,7 @@ __device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, cons
     llobs = obs_term<D, T>(H0, F0, x0, c00);
   }
   const int nv = max(0, min(kRun, nst - kRun * lane));
-  T Ac[kRun][D * D], dts[kRun];
+  T Ac[kRun][D * D], dts[kRun], cgC[CRA][D];
 #pragma unroll
   for (int r = 0; r < kRun; ++r) {
     const int s = min(kRun * lane + r, nst - 1);
@@ -2023,7 +2035,78 @@ __device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, cons
 #pragma unroll
     for (int cc = 0; cc < D; ++cc) S.hf[r][HP + cc][lane] = Fs[cc];
     affine_step<D, T>(Mg, cg_unused, dts[r], zero, Ac[r], e_unused);
+    if (r >= RC0) {
+#pragma unroll
+      for (int p = 0; p < D; ++p) cgC[r >= RC0 ? r - RC0 : 0][p] = cg_unused[p];
+    }
   }
+  // ---- the consumer's own steps r in [RC0, kRun) of every run (PcConsSteps): u's increments,
+  // √dt, the normals of the next iteration, its pCN increments dW° (handed to the producer's
+  // W° stores through the dw slots after B2) and e maps (into its own pt slots)
+  const T rho = (T)ldc(&bi->rho), srho = (T)ldc(&bi->srho);
+  const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32), c3 = a.salt << 1;
+  const double* Zg = a.Z ? a.Z + ldc(a.st_off + g) * M : nullptr;
+  T wvC[CRA][M], sdtC[CRA], zC[CRA][M], dWC[CRA][M];
+  if constexpr (CR > 0) {
+    const T* Ws = a.W[sel.w(g) ^ a.ws_flip] + row * M;
+#pragma unroll
+    for (int r = 0; r < CR; ++r) {
+      const int s = min(kRun * lane + RC0 + r, nst - 1);
+      sdtC[r] = sqrt(dts[RC0 + r]);
+#pragma unroll
+      for (int k = 0; k < M; ++k) wvC[r][k] = Ws[(int64_t)(s + 1) * M + k];
+    }
+  }
+  auto draw_c = [&](uint32_t itv) {
+    if constexpr (CR > 0) {
+      if (Zg) {
+#pragma unroll
+        for (int r = 0; r < CR; ++r)
+#pragma unroll
+          for (int k = 0; k < M; ++k)
+            zC[r][k] = (T)Zg[(int64_t)min(kRun * lane + RC0 + r, nst - 1) * M + k];
+        return;
+      }
+      constexpr int NPB = NormPerBlock<T>::v, NB = CR * M / NPB, NBR = kRun * M / NPB;
+      T zz[CR * M];
+      uint32_t ln = (uint32_t)(NBR * lane + RC0 * M / NPB);  // opaque: no hoisting (producer)
+      asm volatile("" : "+v"(ln));
+#pragma unroll
+      for (int q = 0; q < NB; ++q)
+        normal_block(philox4x32_10(U4{ln + q, (uint32_t)g + a.seg_base, itv, c3}, k0, k1),
+                     zz + NPB * q);
+#pragma unroll
+      for (int r = 0; r < CR; ++r)
+#pragma unroll
+        for (int k = 0; k < M; ++k) zC[r][k] = zz[r * M + k];
+    }
+  };
+  // dW° and e of the consumer's steps for the iteration whose normals are in zC; e → pt slots
+  auto propose_c = [&]() {
+    if constexpr (CR > 0) {
+#pragma unroll
+      for (int r = 0; r < CR; ++r) {
+        T sdW[D];
+#pragma unroll
+        for (int k = 0; k < M; ++k) dWC[r][k] = dfma(rho, wvC[r][k], srho * (sdtC[r] * zC[r][k]));
+        sigma_dw<Mdl, T>(LA, dWC[r], sdW);
+        const int li = lds_ix(kRun * lane + RC0 + r);
+#pragma unroll
+        for (int p = 0; p < D; ++p) S.pt[li][p] = dfma(cgC[r][p], dts[RC0 + r], sdW[p]);
+      }
+    }
+  };
+  auto hand_dw = [&]() {
+    if constexpr (CR > 0) {
+#pragma unroll
+      for (int r = 0; r < CR; ++r)
+#pragma unroll
+        for (int k = 0; k < M; ++k) S.dw[lds_ix(kRun * lane + RC0 + r)][k] = dWC[r][k];
+    }
+  };
+  draw_c((uint32_t)(iter0 + c.key_delta));
+  propose_c();
+  hand_dw();
   const uint64_t all = 1;
   double ll = valid ? c.ll[blk] : 0.0, llp = 0.0;
   const int64_t nb = a.b1 - a.b0, j = blk - a.b0;
@@ -2040,7 +2123,10 @@ __device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, cons
                     (uint32_t)__builtin_amdgcn_readlane((int)__builtin_bit_cast(uint64_t, Ev),
                                                         (int)(r0 & 63)));
     T* const Xdb = (sel.x(g) ^ a.xd_flip) ? Xd[1] : Xd[0];
-    // the run map of the e maps the producer left in the steps' pt slots
+    // the next iteration's normals of the consumer's steps (unconditional: no branch around
+    // them, so they can fill the scan's latency; the last iteration's are never used)
+    draw_c((uint32_t)(it + 1 + c.key_delta));
+    // the run map of the e maps the producer (and, for its steps, the consumer) left in the pt slots
     T RA[D * D], Re[D];
 #pragma unroll
     for (int r = 0; r < kRun; ++r) {
@@ -2159,8 +2245,21 @@ __device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, cons
       ll = llp;
       llp = t;
     }
+    if constexpr (CR > 0) {  // own steps of iteration n + 1: u's increments, then dW° and e
+      if (acc) {
+#pragma unroll
+        for (int r = 0; r < CR; ++r)
+#pragma unroll
+          for (int k = 0; k < M; ++k) wvC[r][k] = dWC[r][k];
+      }
+      wave_lds_sync();  // this wave's pt reads of the X° stores above are done
+      propose_c();
+    }
     __syncthreads();  // B2: decision n → producer; pt reads of this iteration done
-    if (r0 + 1 < n_iter) __syncthreads();  // B1: dW° of iteration n + 1 ready
+    if (r0 + 1 < n_iter) {
+      hand_dw();  // the producer's W° stores of iteration n are done (before its B2)
+      __syncthreads();  // B1: dW° of iteration n + 1 ready
+    }
   }
   if (valid && lane == 0) {
     a.selX[g] = (uint8_t)sel.x(g);
@@ -2179,8 +2278,10 @@ __device__ __forceinline__ void resident_pc_producer(const BlockArgs<T>& a, cons
                                                      const int64_t blk, const bool valid,
                                                      const int h,
                                                      ResPcLds<Mdl::D, Mdl::M, T>& P) {
-  constexpr int D = Mdl::D, M = Mdl::M, HP = D * (D + 1) / 2, RR = kRun / NP;
-  static_assert(kRun % NP == 0, "whole steps per producer");
+  constexpr int D = Mdl::D, M = Mdl::M, HP = D * (D + 1) / 2;
+  constexpr int CR = PcConsSteps<T, M, NP>::v;  // trailing run steps the consumer draws
+  constexpr int RR = (kRun - CR) / NP, RW = kRun / NP;  // steps / W° rows of one producer
+  static_assert((kRun - CR) % NP == 0 && kRun % NP == 0, "whole steps per producer");
   const int r0h = h * RR;
   ResLds<D, M, T>& S = P.r;
   const int lane = threadIdx.x & 63;
@@ -2235,12 +2336,13 @@ __device__ __forceinline__ void resident_pc_producer(const BlockArgs<T>& a, cons
       return;
     }
     constexpr int NPB = NormPerBlock<T>::v, NB = RR * M / NPB;  // this producer's blocks
+    constexpr int NBR = kRun * M / NPB;                          // blocks of a whole run
     static_assert((RR * M) % NPB == 0, "a producer's steps must hold whole normal blocks");
     T zz[RR * M];
     // the blocks' first counter words are loop-invariant: derived from an opaque copy of the
     // lane id so that the compiler does not hoist every block's first Philox round (or the
     // words themselves) out of the iteration loop into spilled registers
-    uint32_t ln = (uint32_t)(NP * NB * lane + h * NB);  // the run's first block of this producer
+    uint32_t ln = (uint32_t)(NBR * lane + h * NB);  // the run's first block of this producer
     asm volatile("" : "+v"(ln));
 #pragma unroll
     for (int q = 0; q < NB; ++q) {
@@ -2290,8 +2392,8 @@ __device__ __forceinline__ void resident_pc_producer(const BlockArgs<T>& a, cons
     if (!valid) return;
     T* const Wdb = (sel.w(g) ^ a.wd_flip) ? Wd[1] : Wd[0];
 #pragma unroll
-    for (int k = 0; k < RR; ++k) {
-      const int s = 64 * (r0h + k) + lane;
+    for (int k = 0; k < RW; ++k) {
+      const int s = 64 * (h * RW + k) + lane;
       if (s < nst) {
         T wd[M];
 #pragma unroll
@@ -2343,14 +2445,14 @@ __global__ __launch_bounds__(64 * 4 * (NP + 1), 1) void k_mcmc_resident_pc(const
   const bool valid = blk < a.b1;
   const int role = w >> 2;  // 0: consumer, 1 + h: producer h
 #if defined(DMT_PC_STUB_P)  // timing probes (scripts/res_usage.sh, gpu_variants.sh): one role only
-  if (role == 0) resident_pc_consumer<Mdl, T>(a, c, iter0, n_iter, part, blk, valid, lds[w & 3]);
+  if (role == 0) resident_pc_consumer<Mdl, T, NP>(a, c, iter0, n_iter, part, blk, valid, lds[w & 3]);
   else for (int64_t i = 0; i < 2 * n_iter; ++i) __syncthreads();
 #elif defined(DMT_PC_STUB_C)
   if (role > 0) resident_pc_producer<Mdl, T, NP>(a, c, iter0, n_iter, blk, valid, role - 1, lds[w & 3]);
   else for (int64_t i = 0; i < 2 * n_iter; ++i) __syncthreads();
 #else
   if (role == 0)
-    resident_pc_consumer<Mdl, T>(a, c, iter0, n_iter, part, blk, valid, lds[w & 3]);
+    resident_pc_consumer<Mdl, T, NP>(a, c, iter0, n_iter, part, blk, valid, lds[w & 3]);
   else
     resident_pc_producer<Mdl, T, NP>(a, c, iter0, n_iter, blk, valid, role - 1, lds[w & 3]);
 #endif
