@@ -1931,6 +1931,13 @@ dmt_status dmt_set_timing(dmt_ens* h, int32_t on) {
   drain_timing(h);
   for (int k = 0; k < DMT_K_COUNT; ++k) { h->t_ms[k] = 0; h->t_cnt[k] = 0; }
   h->timing = on < 0 ? 0xFFFFFFFFu : (uint32_t)on;
+  // the events of the next timed launches are created here, not inside the caller's timed region
+  // (hipEventCreate is a driver call; the bench times its K steps right after this)
+  while (h->timing && h->free_events.size() < 16) {
+    hipEvent_t e;
+    HIP_OK(hipEventCreate(&e));
+    h->free_events.push_back(e);
+  }
   return DMT_OK;
 }
 
