@@ -9,6 +9,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <atomic>
 #include <cmath>
 #include <cstdio>
@@ -166,7 +167,10 @@ struct dmt_ens {
   int64_t part_cap = 0;
   bool persist = true;       // dmt_mcmc_run of a linear drift in one launch (DMT_MCMC_PERSIST=0: off)
   bool resident = true;      // ... with register-resident block state when eligible (DMT_MCMC_RESIDENT=0: off)
-  bool dispatch_events = true;  // timing events attached to the dispatch (DMT_DISPATCH_EVENTS=0: recorded around it)
+  // timing events recorded on the stream around the timed launch (default), or attached to its
+  // dispatch packet (DMT_DISPATCH_EVENTS=1: hipExtLaunchKernel with events — the kernel's own
+  // execution interval, but ≈ 10 µs more host time in the launch call, profiles/r02zo)
+  bool dispatch_events = false;
   int resident_pc = 1;       // ... split over a consumer and this many producer waves per block
                              // (DMT_MCMC_PC=0: one wave; 1 or 2 producers)
   int lane_split = -1;       // MAP_LANE draws on producer/consumer waves: 1 on, 0 off, -1 auto
@@ -241,9 +245,11 @@ void drain_timing(dmt_ens* h) {
   }
 }
 
-// Times the kernel launched inside the scope.  dispatch = true: the events ride on that
-// kernel's dispatch packet (the launcher uses hipExtLaunchKernel; the time is the kernel's
-// execution, as rocprofv3 reports it); otherwise they are recorded on the stream around it.
+// Times the kernel launched inside the scope.  dispatch = true (DMT_DISPATCH_EVENTS=1): the
+// events ride on that kernel's dispatch packet (the launcher uses hipExtLaunchKernel; the time is
+// the kernel's execution, as rocprofv3 reports it); otherwise (default) they are recorded on the
+// stream around it: the interval also holds the dispatch itself (≈ 2 µs on a 138 µs C2 launch
+// against rocprofv3's 138.2), and the launch call stays ≈ 10 µs cheaper on the host.
 struct TimedScope {
   dmt_ens* h;
   int k;
@@ -1183,8 +1189,15 @@ dmt_status dmt_set_run_snapshots(dmt_ens* h, int64_t every, int64_t slot0) {
   return DMT_OK;
 }
 
+static double hp_now() {
+  return std::chrono::duration<double, std::micro>(
+             std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+static const bool g_host_prof = std::getenv("DMT_HOST_PROFILE") != nullptr;
+static double g_hp[6];
 dmt_status dmt_mcmc_run(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int64_t iter0,
                         int64_t n_iter, uint32_t salt, double* out) {
+  if (g_host_prof) g_hp[0] = hp_now();
   DMT_TRY(check_h(h));
   Layout* L;
   DMT_TRY(get_layout(h, layout, &L));
@@ -1300,6 +1313,7 @@ dmt_status dmt_mcmc_run(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int6
         };
         // the arrival counters of the in-kernel trees: the last cnt_words doubles of d_part
         double* counter = h->d_part + h->part_cap - cnt_words;
+        if (g_host_prof) g_hp[1] = hp_now();
         if (h->key.precision == DMT_F64) {
           BlockArgs<double> a{};
           fill(a);
@@ -1314,6 +1328,7 @@ dmt_status dmt_mcmc_run(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int6
                                      run_out + 3 * i0, (unsigned*)counter, h->stream);
         }
       }
+      if (g_host_prof) g_hp[2] = hp_now();
       if (e != hipSuccess) return fail(DMT_ERR_HIP, std::string("k_mcmc_scan: ") + hipGetErrorString(e));
     }
   } else {
@@ -1340,8 +1355,14 @@ dmt_status dmt_mcmc_run(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int6
     return DMT_OK;
   }
   if (!multi) {
+    if (g_host_prof) g_hp[3] = hp_now();
     HIP_OK(stream_wait(h));
+    if (g_host_prof) g_hp[4] = hp_now();
     std::memcpy(out, h->h_run, 24 * n_iter);
+    if (g_host_prof)
+      std::fprintf(stderr, "hostprof n=%lld pre=%.1f launch=%.1f post=%.1f wait=%.1f tail=%.1f\n",
+                   (long long)n_iter, g_hp[1] - g_hp[0], g_hp[2] - g_hp[1], g_hp[3] - g_hp[2],
+                   g_hp[4] - g_hp[3], hp_now() - g_hp[4]);
     return DMT_OK;
   }
   std::vector<double> all(3 * h->nranks * n_iter);
