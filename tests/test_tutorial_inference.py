@@ -5,9 +5,10 @@ set_proposal_law! / accept_reject_proposal_param! on one terminal BiBlock over 1
 
 CPU: the loop runs on the oracle backend.  GPU: the device chain equals the oracle's bit for
 bit over the first iterations (paths, γ chain, decisions, ll), and a longer device chain
-concentrates around the true γ = 1.5 like the reference's published chain
-(docs/src/assets/tutorials/biblock/inference_chain.png: ≈1.45–1.9); the dataset itself is a
-fresh simulation (Julia's seeded stream is not reproducible), so that check is statistical."""
+covers the true γ = 1.5 within its 5–95 % range.  The dataset is a fresh simulation (Julia's
+seeded stream is not reproducible), so the chain is not comparable with the reference's
+published one (docs/src/assets/tutorials/biblock/inference_chain.png) and is not checked
+against it."""
 from __future__ import annotations
 
 import os
@@ -109,6 +110,27 @@ def test_set_obs_reanchors_blocking_law(recording):
             rec = e.download_law(unit, L.LAW_PPB)[2][g]
             sl = np.r_[0:49, 50:64]            # all but c(t0)
             assert np.array_equal(rec[sl], want[sl]), (g, unit)
+
+
+def test_set_obs_reanchoring_is_local_to_p_last(recording):
+    """Localises the unpinned re-anchoring reading of set_obs! (GuidedProposals'
+    set_obs! is not vendored): it rewrites only the P_last law records of the non-terminal
+    blocks' last segments (b and b°).  Every PP record, H/F table and terminal block is untouched,
+    so a reading without the re-anchoring can differ only in those blocks' guiding terms."""
+    import diffusionmcmctools_amd as dmt
+    from diffusionmcmctools_amd import _lib as L
+    se = tut.sampling_pair(recording, 1.5, backend="oracle", blocking=True)
+    be = dmt.BlockEnsemble(se, [tut.BLOCKINGS[0]], rho=0.96, ll_hist_len=2)
+    e = se.ens
+    kinds = (L.LAW_PP, L.LAW_PPB)
+    before = {(u, k): [np.array(a, copy=True) for a in e.download_law(u, k)]
+              for u in (L.U, L.UPROP) for k in kinds}
+    be.set_obs()
+    for (u, k), (H0, F0, R0) in before.items():
+        H1, F1, R1 = e.download_law(u, k)
+        assert np.array_equal(H1, H0) and np.array_equal(F1, F0), (u, k)
+        changed = sorted(set(np.nonzero(np.any(R1 != R0, axis=1))[0].tolist()))
+        assert changed == ([] if k == L.LAW_PP else [24, 74]), (u, k, changed)
 
 
 def test_blocking_tutorial_loop_on_oracle(recording):
