@@ -35,8 +35,9 @@ LAW_SIGINV = 51
 LAW_ANCHOR = 60
 LAW_AUXLIN = 63
 # set_proposal_law! parameter names (include/dmt.h DMT_PAR_*)
-PAR_FHN = {"eps": 0, "s": 1, "gamma": 2, "beta": 3, "sigma": 4}
-PAR_LORENZ = {"s": 0, "r": 1, "beta": 2}
+# (ASCII and DiffusionDefinition's own symbols, e.g. :γ)
+PAR_FHN = {"eps": 0, "s": 1, "gamma": 2, "beta": 3, "sigma": 4, "ϵ": 0, "γ": 2, "β": 3, "σ": 4}
+PAR_LORENZ = {"s": 0, "r": 1, "beta": 2, "β": 2}
 
 # exported symbols (checked against include/dmt.h by tests/test_abi.py)
 SYMBOLS = [
@@ -50,7 +51,7 @@ SYMBOLS = [
     "dmt_debug_normals", "dmt_last_error", "dmt_version", "dmt_snapshot_reserve",
     "dmt_snapshot_take", "dmt_snapshot_download", "dmt_snapshot_write", "dmt_set_ll",
     "dmt_fetch_ll_local", "dmt_comm_size", "dmt_rng_counter", "dmt_set_rng_counter",
-    "dmt_set_run_snapshots",
+    "dmt_set_run_snapshots", "dmt_mcmc_step_local", "dmt_mcmc_run_local",
 ]
 
 
@@ -120,6 +121,8 @@ _SIGS = {
     "dmt_comm_unique_id": [_pu8],
     "dmt_comm_init": [_P, _i32, _i32, _pu8],
     "dmt_mcmc_run": [_P, _i32, _i64, _i64, _i64, _i64, _u32, _pd],
+    "dmt_mcmc_step_local": [_P, _i32, _i64, _i64, _i64, _u32, _pd, _pd, _pi64],
+    "dmt_mcmc_run_local": [_P, _i32, _i64, _i64, _i64, _i64, _u32, _pd],
     "dmt_set_shard": [_P, _i64],
     "dmt_sync": [_P],
     "dmt_set_timing": [_P, _i32],

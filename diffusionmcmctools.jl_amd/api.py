@@ -37,7 +37,51 @@ def _key(iter, salt):
 
 
 __all__ = ["SamplingEnsemble", "SamplingPair", "SamplingUnit", "BlockEnsemble",
-           "BlockCollection", "BiBlock"]
+           "BlockCollection", "BiBlock", "Block"]
+
+
+# Test seam: an engine factory (model, n_points, precision, seed) -> engine that the
+# reference-form constructors use instead of the HIP library (tests run the same caller code
+# on the CPU oracle with it).  None (always, outside tests): the HIP library.
+_ENGINE_FACTORY = None
+
+
+class engine_override:
+    """``with engine_override(factory): …`` — test infrastructure only (see _ENGINE_FACTORY)."""
+
+    def __init__(self, factory):
+        self.factory = factory
+
+    def __enter__(self):
+        global _ENGINE_FACTORY
+        self.prev, _ENGINE_FACTORY = _ENGINE_FACTORY, self.factory
+        return self
+
+    def __exit__(self, *exc):
+        global _ENGINE_FACTORY
+        _ENGINE_FACTORY = self.prev
+        return False
+
+
+def _is_model(x):
+    from .models import Model
+    return isinstance(x, Model)
+
+
+def _aux_callable(AuxLaw):
+    """The reference's ``aux_laws`` argument (src/sampling_unit.jl:55-60) as the
+    ``aux_laws(model, r, k, obs)`` of :meth:`SamplingEnsemble.from_recordings`: an auxiliary-law
+    constructor ``AuxLaw(P, obs)`` (e.g. ``models.FitzHughNagumoAux``: the target linearised at
+    the segment's observation), a fixed ``LinearAux`` for every segment, or one such per
+    segment (a list)."""
+    from .models import LinearAux
+    if AuxLaw is None:
+        return None
+    if isinstance(AuxLaw, LinearAux):
+        return lambda mdl, r, k, ob: AuxLaw
+    if isinstance(AuxLaw, (list, tuple)):
+        return lambda mdl, r, k, ob: (AuxLaw[k](mdl, ob) if callable(AuxLaw[k]) else AuxLaw[k])
+    return lambda mdl, r, k, ob: AuxLaw(mdl, ob)
 
 
 # ============================================================================ sampling units
@@ -49,8 +93,39 @@ class SamplingEnsemble:
     size of segment k of recording r.  Guiding terms, laws and the grid are uploaded with
     :meth:`set_guiding` / :meth:`upload_grid` (host filter: ``models.guiding_chain``)."""
 
-    def __init__(self, model, n_points, precision=L.F64, seed=0, device=0, grid_shared=False,
-                 mapping=L.MAP_AUTO, _engine=None):
+    def __new__(cls, *args, **kw):
+        if args and not _is_model(args[0]):
+            # the reference's SamplingEnsemble(aux_laws, recordings, tts; aux_laws_blocking,
+            # artificial_noise) (src/sampling_ensemble.jl:20-40): each recording's target law
+            # is its ``P`` (models.build_recording)
+            return cls._from_reference_args(*args, **kw)
+        return super().__new__(cls)
+
+    @classmethod
+    def _from_reference_args(cls, aux_laws, recordings, tts, aux_laws_blocking=None,
+                             artificial_noise=1e-11, **kw):
+        recordings = list(recordings)
+        models = [getattr(rec, "P", None) for rec in recordings]
+        if any(m is None for m in models):
+            raise ValueError("SamplingEnsemble(aux_laws, recordings, tts): every recording needs "
+                             "its target law P (models.build_recording(P, data, t0, x0))")
+        if any(type(m) is not type(models[0]) for m in models):
+            raise ValueError("all recordings of one ensemble must share the model family")
+        # per-recording target parameters enter the law records (recording r's P)
+        aux = _aux_callable(aux_laws)
+        auxb = _aux_callable(aux_laws_blocking) or aux
+        se = cls.from_recordings(models[0], recordings, tts,
+                                 aux_laws=lambda mdl, r, k, ob: aux(models[r], r, k, ob),
+                                 aux_laws_blocking=lambda mdl, r, k, ob: auxb(models[r], r, k, ob),
+                                 artificial_noise=artificial_noise,
+                                 record_models=models, **kw)
+        se._ref_built = True
+        return se
+
+    def __init__(self, model, n_points=None, precision=L.F64, seed=0, device=0,
+                 grid_shared=False, mapping=L.MAP_AUTO, _engine=None, **_):
+        if getattr(self, "_ref_built", False):
+            return  # built by the reference-form __new__ (Python re-enters __init__)
         self.model = model
         self.n_points = [list(r) for r in n_points]
         # _engine: test seam for driving the host logic on another backend; the product
@@ -63,7 +138,8 @@ class SamplingEnsemble:
     @classmethod
     def from_recordings(cls, model, recordings, tts, aux_laws=None, aux_laws_blocking=None,
                         artificial_noise=1e-11, blocking=True, precision=L.F64, seed=0,
-                        device=0, mapping=L.MAP_AUTO, init=True, _engine=None):
+                        device=0, mapping=L.MAP_AUTO, init=True, _engine=None,
+                        record_models=None):
         """``SamplingEnsemble(aux_laws, recordings, tts; aux_laws_blocking, artificial_noise)``
         (src/sampling_ensemble.jl:13-41 → ``SamplingPair`` → ``SamplingUnit``,
         src/sampling_unit.jl:55-74): the containers built from the recordings and their laws,
@@ -81,7 +157,9 @@ class SamplingEnsemble:
           defaults to ``aux_laws``;
         * the observations for the device's re-derivations (``set_observations``) and
           ``init_paths!`` from each recording's ``x0`` (``init``).
-        ``tts[r][k]``: the grid of segment k of recording r (``setup_time_grids``)."""
+        ``tts[r][k]``: the grid of segment k of recording r (``setup_time_grids``);
+        ``record_models[r]``: recording r's own target law (its parameters go into its law
+        records; default ``model`` for all)."""
         from .models import artificial_obs_info, guiding_chain, packed
         aux_laws = aux_laws or (lambda mdl, r, k, ob: mdl.aux_for(ob))
         aux_laws_blocking = aux_laws_blocking or aux_laws
@@ -98,7 +176,8 @@ class SamplingEnsemble:
             t_all += grids
             H_all += [c[0] for c in chain]
             F_all += [c[1] for c in chain]
-            laws += [model.law_record(a_, c[2][0]) for a_, c in zip(auxes, chain)]
+            mdl_r = record_models[r] if record_models is not None else model
+            laws += [mdl_r.law_record(a_, c[2][0]) for a_, c in zip(auxes, chain)]
             n_points.append([len(g) for g in grids])
             infos_all += infos
             if blocking:
@@ -112,11 +191,16 @@ class SamplingEnsemble:
                     (h, f, c), = guiding_chain([a_], [grids[k]], [(Ha + Ho, Fa + Fo, ca + co)])
                     Hb_all.append(h)
                     Fb_all.append(f)
-                    lawsb.append(model.law_record(a_, c[0]))
+                    lawsb.append(mdl_r.law_record(a_, c[0]))
+        if _engine is None and _ENGINE_FACTORY is not None:
+            fac = _ENGINE_FACTORY
+            _engine = lambda n_points: fac(model, n_points, precision, seed)  # noqa: E731
         if callable(_engine):  # test seam: an engine factory of the structure
             _engine = _engine(n_points)
-        se = cls(model, n_points, precision=precision, seed=seed, device=device,
-                 mapping=mapping, _engine=_engine)
+        se = object.__new__(cls)
+        se.__init__(model, n_points, precision=precision, seed=seed, device=device,
+                    mapping=mapping, _engine=_engine)
+        se._record_models = list(record_models) if record_models is not None else None
         se.upload_grid(np.concatenate(t_all))
         blaws = {}
         if blocking:
@@ -135,6 +219,11 @@ class SamplingEnsemble:
 
     def num_recordings(self):
         return len(self.recordings)
+
+    def record_model(self, r):
+        """Recording r's target law (its own parameters when built from recordings)."""
+        rm = getattr(self, "_record_models", None)
+        return rm[r] if rm is not None else self.model
 
     def upload_grid(self, t):
         self.ens.upload_grid(t)
@@ -235,13 +324,31 @@ class SamplingEnsemble:
 
 
 class SamplingPair:
-    """``SamplingPair`` (src/sampling_pair.jl:33-57): ``u`` (accepted) and ``u°`` of one
-    recording."""
+    """``SamplingPair`` (src/sampling_pair.jl:33-57): ``u`` (accepted) and ``u°`` (``u_prop``)
+    of one recording.
 
-    def __init__(self, se: SamplingEnsemble, r: int):
+    Reference constructor: ``SamplingPair(aux_laws, recording, tts; aux_laws_blocking,
+    artificial_noise)`` (src/sampling_pair.jl:40-54) — the containers of ONE recording (its own
+    one-recording ensemble on the GPU, ``sp.se``), u° = deepcopy(u).  ``recording`` carries its
+    target law ``P`` (``models.build_recording``); ``aux_laws`` is an auxiliary-law constructor
+    ``AuxLaw(P, obs)`` such as ``models.FitzHughNagumoAux``.  The ensemble form
+    ``SamplingPair(se, r)`` is the r-th recording of a :class:`SamplingEnsemble`."""
+
+    def __init__(self, *args, **kw):
+        if args and isinstance(args[0], SamplingEnsemble):
+            self._init_view(*args)
+            return
+        se = SamplingEnsemble._from_reference_args(args[0], [args[1]], [args[2]], *args[3:], **kw)
+        self._init_view(se, 0)
+        se.recordings[0] = self
+
+    def _init_view(self, se, r):
         self.se, self.r = se, r
         self.u = SamplingUnit(se, r, L.U)
         self.u_prop = SamplingUnit(se, r, L.UPROP)
+
+    def close(self):
+        self.se.close()
 
 
 class SamplingUnit:
@@ -278,6 +385,23 @@ class SamplingUnit:
         it, salt = _key(iter, salt)
         ll, ok = self.se.ens.draw_unit(self.unit, self.r, self.r + 1, Z=Z, iter=it, salt=salt)
         return bool(ok[0]), float(ll[0])
+
+    # The unit's methods run on the handle's internal layout 0 (one terminal block per
+    # recording over all its segments, ρ = 0 — the unit seen as one block).
+    def recompute_guiding_term(self):
+        """``GP.recompute_guiding_term!(u::SamplingUnit)`` (src/sampling_unit.jl:100-102): the
+        guiding terms of ``u.PP`` over the whole recording, backward from its last
+        observation (device filter)."""
+        self.se.ens.recompute_guiding_term(0, self.r, self.r + 1, unit=self.unit)
+
+    def loglikhd(self):
+        """``GP.loglikhd(u::SamplingUnit)`` (src/sampling_unit.jl:109): the log-likelihood
+        ``loglikhd(u.PP, u.XX)`` of the stored path (``loglikhd_obs`` at the start plus every
+        segment's Girsanov sum) — a value; the unit is not modified."""
+        e = self.se.ens
+        e.loglikhd(0, self.unit, self.r, self.r + 1)
+        what = L.BLK_LL if self.unit == L.U else L.BLK_LLPROP
+        return float(e.get_block_state(0, what, self.r, self.r + 1)[0])
 
 
 # ============================================================================ blocks
@@ -477,7 +601,8 @@ class _BlockRange:
         """``draw_proposal_path!`` + ``accept_reject_proposal_path!(·, mcmciter)`` +
         ``fetch_ll`` fused into one call (device RNG: the stream counter, or the stream keyed
         by (``mcmciter``, ``salt``)).  Returns (ll, ll°, n_accepted)."""
-        return self._call("mcmc_step", mcmciter, salt=L.RNG_AUTO if salt is None else int(salt))
+        return self._call("mcmc_step", mcmciter, salt=L.RNG_AUTO if salt is None else int(salt),
+                          local=not self._global)
 
     def mcmc_run(self, iter0, n_iter, salt=None):
         """``n_iter`` consecutive :meth:`mcmc_step` iterations starting at ``iter0``, queued on
@@ -487,7 +612,7 @@ class _BlockRange:
         the loop of counter-keyed :meth:`draw_proposal_path` / :meth:`accept_reject_proposal_path`
         calls would."""
         return self._call("mcmc_run", iter0, n_iter,
-                          salt=L.RNG_AUTO if salt is None else int(salt))
+                          salt=L.RNG_AUTO if salt is None else int(salt), local=not self._global)
 
 
 # recompute_guiding_term! flags (src/block_collection.jl:208-221) → units, in call order
@@ -530,6 +655,58 @@ def _as_range(x):
     return range(x.start, x.stop) if isinstance(x, range) else range(x[0], x[1] + 1)
 
 
+class Block:
+    """``Block{L}`` (src/block.jl:49-79): the view ``bb.b`` (unit u, the accepted path and
+    laws) or ``bb.b°`` (``bb.b_prop``, unit u°) of a :class:`BiBlock` onto the segments of its
+    recording.  ``ll`` reads and assigns the block's log-likelihood (``bb.b°.ll - bb.b.ll`` in
+    the reference's parameter step, docs/src/tutorials/biblock/inference.md:44), ``ll_history``
+    its history, ``XX`` / ``WW`` download the block's segments (reference layout, resolving
+    swaps; src/block.jl:71-72), ``is_last`` is the type parameter L."""
+
+    def __init__(self, bb, unit):
+        self.bb, self.unit = bb, unit
+
+    @property
+    def is_last(self):
+        return self.bb.is_last
+
+    def _state(self, hist=False):
+        u = self.unit == L.U
+        return (L.BLK_LL_HIST if u else L.BLK_LLPROP_HIST) if hist else (L.BLK_LL if u else L.BLK_LLPROP)
+
+    @property
+    def ll(self):
+        bb = self.bb
+        return float(bb._ens.get_block_state(bb._layout, self._state(), bb._b0, bb._b1)[0])
+
+    @ll.setter
+    def ll(self, v):
+        bb = self.bb
+        bb._ens.set_block_state(bb._layout, self._state(), bb._b0, bb._b1,
+                                np.array([float(v)]))
+
+    @property
+    def ll_history(self):
+        bb = self.bb
+        return bb._ens.get_block_state(bb._layout, self._state(True), bb._b0, bb._b1,
+                                       hist_len=bb.ll_hist_len)[:, 0]
+
+    def _segments(self, what):
+        bb, e = self.bb, self.bb._ens
+        A = e.download_paths(self.unit, what)
+        g0 = int(e.rec_seg0[bb.rec])
+        return [A[e.pt_off[g]:e.pt_off[g] + e.npts[g]]
+                for g in range(g0 + bb.segments.start, g0 + bb.segments.stop)]
+
+    @property
+    def XX(self):
+        return self._segments(0)
+
+    @property
+    def WW(self):
+        return self._segments(1)
+
+
 class BiBlock(_BlockRange):
     """``BiBlock{L}`` (src/biblock.jl:42-63): one block b / b° with pCN memory ρ.
 
@@ -553,11 +730,16 @@ class BiBlock(_BlockRange):
         x = _as_range(range_)
         layout = se.ens.create_layout(n_blocks, [x.start], [x.stop - 1], [1 if last_block else 0],
                                       [float(rho)], hist_len=int(ll_hist_len))
-        self._init_view(se.ens, layout, 0, int(ll_hist_len), last_block, rho, x)
+        self._init_view(se.ens, layout, 0, int(ll_hist_len), last_block, rho, x, sp.r,
+                        se.record_model(sp.r))
 
-    def _init_view(self, ens, layout, b, hist_len, is_last, rho, segments):
+    def _init_view(self, ens, layout, b, hist_len, is_last, rho, segments, rec=0, model=None):
         super().__init__(ens, layout, b, b + 1, hist_len)
         self.is_last, self.rho, self.segments = bool(is_last), float(rho), segments
+        self.rec, self.model = int(rec), model
+        # bb.b / bb.b° (src/biblock.jl:43-46): the accepted and the proposal Block views
+        self.b = Block(self, L.U)
+        self.b_prop = Block(self, L.UPROP)
 
     def fetch_ll(self):
         return float(self.ll[0])
@@ -592,8 +774,8 @@ class BlockCollection(_BlockRange):
         rhos = list(rho) if isinstance(rho, (list, tuple, np.ndarray)) else [rho] * n
         layout, rr, last = _pair_layout(sp, ranges, rhos, ll_hist_len)
         ens = sp.se.ens
-        blocks = [BiBlock(ens, layout, b, int(ll_hist_len), last[b], rhos[b], rr[b])
-                  for b in range(n)]
+        blocks = [BiBlock(ens, layout, b, int(ll_hist_len), last[b], rhos[b], rr[b], sp.r,
+                          sp.se.record_model(sp.r)) for b in range(n)]
         self._init_view(ens, layout, 0, blocks, int(ll_hist_len))
 
     def _init_view(self, ens, layout, b0, blocks, hist_len):
@@ -648,7 +830,7 @@ class BlockEnsemble(_BlockRange):
             blocks = []
             for _ in range(n_blocks[r]):
                 blocks.append(BiBlock(ens, layout, b, ll_hist_len, last[b], rhos[b],
-                                      range(sf[b], sl[b] + 1)))
+                                      range(sf[b], sl[b] + 1), r, se.record_model(r)))
                 b += 1
             self.recordings.append(BlockCollection(ens, layout, b - len(blocks), blocks,
                                                    ll_hist_len))

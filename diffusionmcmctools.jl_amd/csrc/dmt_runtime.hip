@@ -1145,8 +1145,9 @@ static dmt_status finish_reduction(dmt_ens* h, double* v, bool global = true) {
   return DMT_OK;
 }
 
-dmt_status dmt_mcmc_step(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int64_t mcmciter,
-                         uint32_t salt, double* ll, double* ll_prop, int64_t* n_acc) {
+static dmt_status mcmc_step_impl(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
+                                 int64_t mcmciter, uint32_t salt, double* ll, double* ll_prop,
+                                 int64_t* n_acc, bool global) {
   DMT_TRY(check_h(h));
   Layout* L;
   DMT_TRY(get_layout(h, layout, &L));
@@ -1165,11 +1166,22 @@ dmt_status dmt_mcmc_step(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int
                                 h->d_red_work, h->d_red_lb, h->d_red, h->stream));
   }
   double v[3];
-  DMT_TRY(finish_reduction(h, v));
+  DMT_TRY(finish_reduction(h, v, global));
   if (ll) *ll = v[0];
   if (ll_prop) *ll_prop = v[1];
   if (n_acc) *n_acc = (int64_t)v[2];
   return DMT_OK;
+}
+
+dmt_status dmt_mcmc_step(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int64_t mcmciter,
+                         uint32_t salt, double* ll, double* ll_prop, int64_t* n_acc) {
+  return mcmc_step_impl(h, layout, b0, b1, mcmciter, salt, ll, ll_prop, n_acc, true);
+}
+
+dmt_status dmt_mcmc_step_local(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
+                               int64_t mcmciter, uint32_t salt, double* ll, double* ll_prop,
+                               int64_t* n_acc) {
+  return mcmc_step_impl(h, layout, b0, b1, mcmciter, salt, ll, ll_prop, n_acc, false);
 }
 
 // Capacity of dmt_mcmc_run's buffers: grown geometrically with a floor, so that a run of a
@@ -1195,8 +1207,9 @@ static double hp_now() {
 }
 static const bool g_host_prof = std::getenv("DMT_HOST_PROFILE") != nullptr;
 static double g_hp[6];
-dmt_status dmt_mcmc_run(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int64_t iter0,
-                        int64_t n_iter, uint32_t salt, double* out) {
+static dmt_status mcmc_run_impl(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
+                                int64_t iter0, int64_t n_iter, uint32_t salt, double* out,
+                                bool global) {
   if (g_host_prof) g_hp[0] = hp_now();
   DMT_TRY(check_h(h));
   Layout* L;
@@ -1220,7 +1233,7 @@ dmt_status dmt_mcmc_run(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int6
       const int64_t it = iter0 + done;
       const int64_t k = ((it + every - 1) / every) * every;  // next snapshot iteration >= it
       const int64_t n = std::min(n_iter - done, k - it + 1);
-      st = dmt_mcmc_run(h, layout, b0, b1, it, n, salt, out ? out + 3 * done : nullptr);
+      st = mcmc_run_impl(h, layout, b0, b1, it, n, salt, out ? out + 3 * done : nullptr, global);
       done += n;
       if (st == DMT_OK && (iter0 + done - 1) % every == 0) {
         st = dmt_snapshot_take(h, DMT_U, h->run_snap_next, iter0 + done - 1);
@@ -1243,7 +1256,9 @@ dmt_status dmt_mcmc_run(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int6
     salt = auto_key(base).salt;
     key_delta = (int64_t)(uint32_t)base - iter0;
   }
-  const bool multi = h->comm != nullptr;
+  // BlockEnsemble level (global): the partials of every rank; BiBlock / BlockCollection
+  // level: this rank's blocks only, no collective (src/block_collection.jl:144,156)
+  const bool multi = h->comm != nullptr && global;
   if (n_iter > h->run_cap) {
     if (h->d_run) { (void)hipFree(h->d_run); h->bytes -= h->run_cap * 24; h->d_run = nullptr; }
     if (h->h_run) { (void)hipHostFree(h->h_run); h->h_run = nullptr; h->h_run_dev = nullptr; }
@@ -1381,6 +1396,16 @@ dmt_status dmt_mcmc_run(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int6
       out[3 * i + c] = lv[0] + 0.0;
     }
   return DMT_OK;
+}
+
+dmt_status dmt_mcmc_run(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int64_t iter0,
+                        int64_t n_iter, uint32_t salt, double* out) {
+  return mcmc_run_impl(h, layout, b0, b1, iter0, n_iter, salt, out, true);
+}
+
+dmt_status dmt_mcmc_run_local(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int64_t iter0,
+                              int64_t n_iter, uint32_t salt, double* out) {
+  return mcmc_run_impl(h, layout, b0, b1, iter0, n_iter, salt, out, false);
 }
 
 dmt_status dmt_accept_reject(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, const double* E,

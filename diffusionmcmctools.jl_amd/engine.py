@@ -262,18 +262,20 @@ class Ensemble:
                int(mcmciter), C.byref(a), C.byref(b), C.byref(n))
         return a.value, b.value, n.value
 
-    def mcmc_step(self, layout, b0, b1, mcmciter, salt=0):
-        """draw_proposal (device RNG) + accept_reject + fetch_ll in one call."""
+    def mcmc_step(self, layout, b0, b1, mcmciter, salt=0, local=False):
+        """draw_proposal (device RNG) + accept_reject + fetch_ll in one call; ``local``: this
+        rank's sums only (BiBlock / BlockCollection level, no collective)."""
         a, b, n = C.c_double(), C.c_double(), C.c_int64()
-        L.call("dmt_mcmc_step", self._h, layout, b0, b1, int(mcmciter), int(salt), C.byref(a),
+        L.call("dmt_mcmc_step_local" if local else "dmt_mcmc_step", self._h, layout, b0, b1, int(mcmciter), int(salt), C.byref(a),
                C.byref(b), C.byref(n))
         return a.value, b.value, n.value
 
-    def mcmc_run(self, layout, b0, b1, iter0, n_iter, salt=0):
+    def mcmc_run(self, layout, b0, b1, iter0, n_iter, salt=0, local=False):
         """n_iter mcmc_step iterations without host synchronisation in between; returns
-        (n_iter, 3): fetch_ll, fetch_ll°, accepted count per iteration."""
+        (n_iter, 3): fetch_ll, fetch_ll°, accepted count per iteration (``local``: this rank's
+        sums, no collective)."""
         out = np.empty((int(n_iter), 3), dtype=np.float64)
-        L.call("dmt_mcmc_run", self._h, layout, b0, b1, int(iter0), int(n_iter), int(salt),
+        L.call("dmt_mcmc_run_local" if local else "dmt_mcmc_run", self._h, layout, b0, b1, int(iter0), int(n_iter), int(salt),
                L.f64p(out))
         return out
 

@@ -1,28 +1,43 @@
 #= DiffusionMCMCToolsAMD — Julia binding of libdmt (include/dmt.h) for DiffusionMCMCTools.jl.
 
-Device-resident counterparts of SamplingEnsemble / BlockEnsemble / BlockCollection / BiBlock
-whose methods carry the reference's names and argument meaning, each one `ccall` over a block
-range.  The host arrays passed in are the reference's own containers reinterpreted
-(Vector{SVector{d,Float64}} == double[npts][d]).
+Loading this module next to DiffusionMCMCTools makes the reference's unchanged caller code run
+on the GPU: the reference's own constructors (`SamplingPair(AuxLaw, recording, tts)`,
+`SamplingEnsemble(AuxLaw, recordings, tts)`, `BiBlock(sp, …)`, `BlockCollection(sp, …)`,
+`BlockEnsemble(se, …)`) build device containers, and every function the tutorials call is a
+METHOD of the reference's generic function (imported from DiffusionMCMCTools, or GuidedProposals'
+`GP.set_obs!`, `GP.recompute_guiding_term!`, `GP.loglikhd`, `GP.equalize_obs_params!`) on the
+device types, with the reference's field accesses (`bb.b.ll`, `bb.b°.ll`, `bb.b.XX`, `sp.u.XX`,
+`se.recordings`).  Each method is one `ccall` over a block range; host arrays are the
+reference's own containers reinterpreted (Vector{SVector{d,Float64}} == double[npts][d]).
+`use_device!(false)` restores the reference's CPU constructors.
 
-No Julia toolchain exists in the build image, so this file is shipped as source and is not
-exercised by the test suite; the Python mirror (../api.py) calls the same entry points and is
-tested.  See INTEGRATION.md for the wiring into the reference package.
+No Julia toolchain exists in the build image, so this file is shipped as source and is not run
+by the test suite; tests/test_julia_binding.py checks every `ccall` type tuple against the
+prototypes of include/dmt.h and that every name the reference's tutorials call is defined here
+as a method of the reference's (or GuidedProposals') generic function.  The Python mirror
+(../api.py, ../functions.py) calls the same entry points and is tested end to end, including
+the tutorial loops verbatim (examples/reference_tutorials.py).  See INTEGRATION.md.
 =#
 module DiffusionMCMCToolsAMD
 
 using StaticArrays
 using LinearAlgebra: I, det, inv
 
+import GuidedProposals
+const GP = GuidedProposals
+import DiffusionDefinition
+const DD = DiffusionDefinition
+import DiffusionMCMCTools
 import DiffusionMCMCTools: draw_proposal_path!, accept_reject_proposal_path!, loglikhd!,
     loglikhd°!, fetch_ll, fetch_ll°, save_ll!, set_ll!, set_accepted!, swap_paths!, swap_XX!,
     swap_WW!, swap_PP!, swap_ll!, ll_of_accepted, accpt_rate, recompute_path!, find_W_for_X!,
-    BiBlock, BlockCollection, BlockEnsemble
+    set_proposal_law!, SamplingPair, SamplingEnsemble, BiBlock, BlockCollection, BlockEnsemble,
+    ParamNamesRecording, ParamNamesAllObs
 
-export DeviceSamplingEnsemble, DeviceBlockEnsemble, DeviceBlockCollection, DeviceBiBlock,
-    mcmc_step!, mcmc_run!, download_XX, download_WW, upload_obs!, set_obs!,
-    recompute_guiding_term!, set_proposal_law!, snapshot_every!, equalize_obs_params!,
-    law_record, guiding_linear
+# device-only names (everything the reference's callers use is a method of its own functions)
+export DeviceSamplingEnsemble, DeviceSamplingPair, DeviceSamplingUnit, DeviceBlockEnsemble,
+    DeviceBlockCollection, DeviceBiBlock, DeviceBlock, use_device!, mcmc_step!, mcmc_run!,
+    download_XX, download_WW, upload_obs!, snapshot_every!, law_record, guiding_linear
 
 const libdmt = get(ENV, "DMT_LIB", joinpath(@__DIR__, "..", "libdmt.so"))
 
@@ -69,6 +84,13 @@ function check(st::Int32)
     error("libdmt error $st: $msg")
 end
 
+# `using DiffusionMCMCToolsAMD` sends the reference's SamplingPair / SamplingEnsemble
+# constructors to the device; use_device!(false) gives the CPU ones back
+const DEVICE = Ref(true)
+const DEVICE_OPTS = Ref{Any}((device=0, seed=0))
+use_device!(on::Bool=true; device::Integer=0, seed::Integer=0) =
+    (DEVICE[] = on; DEVICE_OPTS[] = (device=device, seed=seed); on)
+
 # ============================================================ SamplingEnsemble (device)
 """
     DeviceSamplingEnsemble(model, d, m, n_points; precision, seed, device, grid_shared)
@@ -83,6 +105,7 @@ mutable struct DeviceSamplingEnsemble
     m::Int
     n_points::Vector{Vector{Int}}
     P::Int
+    t::Vector{Float64}       # host copy of the time grids (trajectory views)
     function DeviceSamplingEnsemble(model::Integer, d::Integer, m::Integer, n_points;
                                     precision=DMT_F64, seed::Integer=0, device::Integer=0,
                                     grid_shared::Bool=false, mapping=DMT_MAP_AUTO)
@@ -97,7 +120,8 @@ mutable struct DeviceSamplingEnsemble
                         (Ref{Ptr{Cvoid}}, Ref{dmt_model}, Ref{dmt_structure}, Ref{dmt_config}),
                         h, mdl, st, cfg))
         end
-        se = new(h[], Int32(model), d, m, [collect(Int, r) for r in n_points], sum(npts))
+        se = new(h[], Int32(model), d, m, [collect(Int, r) for r in n_points], sum(npts),
+                 Float64[])
         finalizer(se) do x
             x.h == C_NULL || ccall((:dmt_destroy, libdmt), Int32, (Ptr{Cvoid},), x.h)
             x.h = C_NULL
@@ -109,8 +133,11 @@ end
 "Concatenate per-segment trajectories (Vector{SVector}) recording-major into one flat buffer."
 flatten_paths(segs) = reduce(vcat, (collect(reinterpret(Float64, s)) for s in segs))
 
-upload_grid!(se::DeviceSamplingEnsemble, t::Vector{Float64}) =
+function upload_grid!(se::DeviceSamplingEnsemble, t::Vector{Float64})
     check(ccall((:dmt_upload_grid, libdmt), Int32, (Ptr{Cvoid}, Ptr{Float64}), se.h, t))
+    se.t = copy(t)
+    nothing
+end
 
 """
     upload_law!(se, unit, kind, H, F, laws; H_shared=false)
@@ -141,6 +168,20 @@ function _download(se::DeviceSamplingEnsemble, unit, what, C)
 end
 download_XX(se::DeviceSamplingEnsemble, unit=DMT_U) = _download(se, unit, 0, se.d)
 download_WW(se::DeviceSamplingEnsemble, unit=DMT_U) = _download(se, unit, 1, se.m)
+
+# flat point offsets of the segments, recording-major
+_pt_off(se::DeviceSamplingEnsemble) = cumsum([0; [n for r in se.n_points for n in r]])
+_seg0(se::DeviceSamplingEnsemble, r) = sum(length.(se.n_points[1:r-1]); init=0)
+
+"Per-segment trajectories (t, x) of segments `segs` (1-based, global) from a flat download."
+function _trajectories(se::DeviceSamplingEnsemble, A, segs)
+    off = _pt_off(se)
+    map(segs) do g
+        rows = off[g]+1:off[g+1]
+        # DiffusionDefinition's trajectory(t, x): the type sp.u.XX holds in the reference
+        DD.trajectory(se.t[rows], A[rows])
+    end
+end
 
 # ---- path snapshots: `append!(paths, [deepcopy(bb.b.XX)])` (docs/src/tutorials/biblock/
 # smoothing.md:55) without leaving the GPU; slots are 0-based, what_mask 1 = XX, 2 = WW, 3 = both
@@ -258,14 +299,16 @@ end
 `SamplingEnsemble(aux_laws, recordings, tts; artificial_noise)` on the device:
 `recordings[r] = (obs = [(t, v, L, Σ), …], x0 = …)`, `tts[r][k]` the grid of segment k,
 `aux(r, k, obs) -> (B̃, β̃, σ̃, anchor)` the auxiliary law of segment k (e.g. FitzHughNagumoAux
-linearised at the observed y: `(DD.B(t0, P̃), DD.β(t0, P̃), DD.σ(t0, x, P̃), yT)`).  Guiding terms
-through each recording's segments (build_guid_prop), blocking laws with an exact full-state
-artificial end observation (guid_prop_for_blocking; a placeholder until set_obs!), the
-observations for the device's re-derivations, then init_paths! from x0.
+linearised at the observed y: `(DD.B(t0, P̃), DD.β(t0, P̃), DD.σ(t0, x, P̃), yT)`).  `θrec` is one
+law-parameter vector for all recordings or a function `r -> θrec` (each recording's own target
+law).  Guiding terms through each recording's segments (build_guid_prop), blocking laws with an
+exact full-state artificial end observation (guid_prop_for_blocking; a placeholder until
+set_obs!), the observations for the device's re-derivations, then init_paths! from x0.
 """
 function DeviceSamplingEnsemble(model::Integer, θrec, σ::AbstractMatrix, recordings, tts, aux;
                                 artificial_noise=1e-11, blocking=true, kw...)
     d, m = size(σ)
+    θof = θrec isa Function ? θrec : (r -> θrec)
     t_all, H_all, F_all, laws, infos = Float64[], Matrix{Float64}[], Matrix{Float64}[], Vector{Float64}[], Any[]
     Hb_all, Fb_all, lawsb = Matrix{Float64}[], Matrix{Float64}[], Vector{Float64}[]
     n_points = Vector{Int}[]
@@ -288,7 +331,7 @@ function DeviceSamplingEnsemble(model::Integer, θrec, σ::AbstractMatrix, recor
         for k in 1:K
             B̃, β̃, σ̃, an = auxes[k]
             append!(t_all, tts[r][k]); push!(H_all, chain[k][1]); push!(F_all, chain[k][2])
-            push!(laws, law_record(θrec, σ, B̃, β̃, σ̃, chain[k][3][1]; anchor=an))
+            push!(laws, law_record(θof(r), σ, B̃, β̃, σ̃, chain[k][3][1]; anchor=an))
             push!(infos, info[k])
             if blocking
                 v = zeros(d); vo = collect(rec.obs[k].v); v[1:min(d, length(vo))] .= vo[1:min(d, length(vo))]
@@ -296,7 +339,7 @@ function DeviceSamplingEnsemble(model::Integer, θrec, σ::AbstractMatrix, recor
                 Ho, Fo, co = info[k]
                 H, F, c = guiding_linear(B̃, β̃, σ̃, Float64.(tts[r][k]), Ha + Ho, Fa + Fo, ca + co)
                 push!(Hb_all, H); push!(Fb_all, F)
-                push!(lawsb, law_record(θrec, σ, B̃, β̃, σ̃, c[1]; anchor=an))
+                push!(lawsb, law_record(θof(r), σ, B̃, β̃, σ̃, c[1]; anchor=an))
             end
         end
         push!(n_points, [length(g) for g in tts[r]])
@@ -321,6 +364,133 @@ function DeviceSamplingEnsemble(model::Integer, θrec, σ::AbstractMatrix, recor
     flat_paths(A) = collect(reinterpret(Float64, A))
     set_paths!(se, DMT_UPROP, flat_paths(download_XX(se)), flat_paths(download_WW(se)))
     se
+end
+
+# ---- the reference's (aux_laws, recording(s), tts) constructors on the device
+# The target law of a recording is `recording.P` (ObservationSchemes recordings are
+# (P, obs, t0, x0_prior), docs/src/get_started/overview.md:18-20); its observations are
+# LinearGsnObs with fields t, obs, L, Σ (docs/src/tutorials/preamble.md:80-86).  Models are
+# recognised by their DiffusionDefinition names; extend `device_model` for others.
+"""
+    device_model(P) -> (kind, θrec, σ)
+
+The device model of a DiffusionDefinition target law: FitzHughNagumo (θ = ϵ, s, γ, β, σ —
+positional, `FitzHughNagumo(θ...)` at docs/src/tutorials/preamble.md:78) and Lorenz.
+"""
+function device_model(P)
+    name = nameof(typeof(P))
+    if name === :FitzHughNagumo
+        ϵ, s, γ, β, σ = (getfield(P, i) for i in 1:5)
+        return DMT_MODEL_FHN, [1 / ϵ, s, γ, β, ϵ, σ], reshape([0.0, σ], 2, 1)
+    elseif name === :Lorenz || name === :Lorenz63
+        s, r, β = (getfield(P, i) for i in 1:3)
+        σ = nfields(P) >= 6 ? [getfield(P, 4), getfield(P, 5), getfield(P, 6)] : [1.0, 1.0, 1.0]
+        return DMT_MODEL_LORENZ, [s, r, β], Matrix{Float64}(LinearAlgebra_diag(σ))
+    end
+    error("DiffusionMCMCToolsAMD: no device model for $(name); extend device_model")
+end
+LinearAlgebra_diag(v) = [i == j ? v[i] : 0.0 for i in 1:length(v), j in 1:length(v)]
+
+"""
+    device_aux(kind, θrec, σ, o) -> (B̃, β̃, σ̃, anchor)
+
+The auxiliary law of a segment ending in observation `o`, linearised at the observed value
+(FitzHughNagumoAux; the Lorenz aux of config C5), in the arithmetic order of the device's
+re-derivation in set_proposal_law! (DESIGN.md §3), so host and device laws agree bit for bit.
+"""
+function device_aux(kind, θrec, σ, o)
+    if kind == DMT_MODEL_FHN
+        e, s, γ, β = θrec[5], θrec[2], θrec[3], θrec[4]
+        y = Float64(o.v[1])
+        B̃ = [(1.0 - 3.0 * (y * y)) / e  -1.0 / e; γ  -1.0]
+        β̃ = [(s + 2.0 * (y * y * y)) / e, β]
+        return B̃, β̃, σ, [y]
+    else
+        s, r, b = θrec[1], θrec[2], θrec[3]
+        x0, x1, x2 = Float64.(o.v[1:3])
+        J = [-s s 0.0; r-x2 -1.0 -x0; x1 x0 -b]
+        f = [s * (x1 - x0), x0 * (r - x2) - x1, x0 * x1 - b * x2]
+        β̃ = [f[i] - ((J[i, 1] * x0 + J[i, 2] * x1) + J[i, 3] * x2) for i in 1:3]
+        return J, β̃, σ, [x0, x1, x2]
+    end
+end
+
+_obs(o) = (t = o.t, v = collect(Float64, o.obs), L = Matrix{Float64}(o.L), Σ = Matrix{Float64}(o.Σ))
+
+function _device_ensemble(aux_laws, recordings, tts; artificial_noise=1e-11, kw...)
+    kinds = [device_model(rec.P) for rec in recordings]
+    kind, _, σ = kinds[1]
+    all(k -> k[1] == kind, kinds) || error("one device ensemble holds one model family")
+    recs = [(obs = [_obs(o) for o in rec.obs], x0 = rand(rec.x0_prior)) for rec in recordings]
+    aux(r, k, o) = device_aux(kind, kinds[r][2], σ, o)
+    opts = DEVICE_OPTS[]
+    DeviceSamplingEnsemble(kind, r -> kinds[r][2], σ, recs, tts, aux;
+                           artificial_noise=artificial_noise, device=opts.device, seed=opts.seed)
+end
+
+# ============================================================ views (the reference's fields)
+"""
+    DeviceSamplingPair(se, r)
+
+Recording `r` (1-based) of a device ensemble, with the reference's fields `u` / `u°`
+(`DeviceSamplingUnit` views, src/sampling_pair.jl:36-38): the `SamplingPair` argument of the
+reference's `BiBlock(sp, range, ρ, last_block, ll_hist_len)` / `BlockCollection(sp, ranges, ρρ,
+ll_hist_len)` constructors (src/biblock.jl:48-62, src/block_collection.jl:22-30).
+"""
+struct DeviceSamplingPair
+    se::DeviceSamplingEnsemble
+    r::Int
+end
+Base.getindex(se::DeviceSamplingEnsemble, r::Integer) = DeviceSamplingPair(se, r)
+
+"`sp.u` / `sp.u°` of a device SamplingPair (src/sampling_unit.jl:48-53): XX, WW per segment."
+struct DeviceSamplingUnit
+    se::DeviceSamplingEnsemble
+    r::Int
+    unit::Int32
+end
+
+function Base.getproperty(sp::DeviceSamplingPair, s::Symbol)
+    s === :u && return DeviceSamplingUnit(getfield(sp, :se), getfield(sp, :r), DMT_U)
+    s === :u° && return DeviceSamplingUnit(getfield(sp, :se), getfield(sp, :r), DMT_UPROP)
+    getfield(sp, s)
+end
+
+_segs(se::DeviceSamplingEnsemble, r) = (_seg0(se, r) + 1):(_seg0(se, r) + length(se.n_points[r]))
+
+function Base.getproperty(u::DeviceSamplingUnit, s::Symbol)
+    se = getfield(u, :se)
+    if s === :XX
+        return _trajectories(se, download_XX(se, getfield(u, :unit)), _segs(se, getfield(u, :r)))
+    elseif s === :WW
+        return _trajectories(se, download_WW(se, getfield(u, :unit)), _segs(se, getfield(u, :r)))
+    end
+    getfield(u, s)
+end
+
+function Base.getproperty(se::DeviceSamplingEnsemble, s::Symbol)
+    # se.recordings: one SamplingPair per recording (src/sampling_ensemble.jl:17-18)
+    s === :recordings && return [DeviceSamplingPair(se, r) for r in 1:length(getfield(se, :n_points))]
+    getfield(se, s)
+end
+
+# the reference's constructors: device containers while use_device!(true) (the default after
+# `using DiffusionMCMCToolsAMD`), the reference's CPU ones otherwise
+function SamplingPair(aux_laws::Type, recording, tts, args...; kw...)
+    DEVICE[] || return invoke(SamplingPair, Tuple{Any,Any,Any,Vararg{Any}}, aux_laws,
+                              recording, tts, args...; kw...)
+    kws = Dict(kw)
+    se = _device_ensemble(aux_laws, [recording], [tts];
+                          artificial_noise=get(kws, :artificial_noise, 1e-11))
+    DeviceSamplingPair(se, 1)
+end
+
+function SamplingEnsemble(aux_laws::Type, recordings, tts, args...; kw...)
+    DEVICE[] || return invoke(SamplingEnsemble, Tuple{Any,Any,Any,Vararg{Any}}, aux_laws,
+                              recordings, tts, args...; kw...)
+    kws = Dict(kw)
+    _device_ensemble(aux_laws, collect(recordings), collect(tts);
+                     artificial_noise=get(kws, :artificial_noise, 1e-11))
 end
 
 # ============================================================ blocks
@@ -351,20 +521,52 @@ struct DeviceBiBlock{L} <: DeviceBlocks
     b1::Int64
     hist_len::Int64
     ρ::Float64
+    segs::UnitRange{Int}     # the block's segments, 1-based, global over the ensemble
 end
 
 """
-    DeviceSamplingPair(se, r)
+    DeviceBlock
 
-Recording `r` (1-based) of a device ensemble: the `SamplingPair` argument of the reference's
-`BiBlock(sp, range, ρ, last_block, ll_hist_len)` / `BlockCollection(sp, ranges, ρρ,
-ll_hist_len)` constructors (src/biblock.jl:48-62, src/block_collection.jl:22-30).
+`bb.b` / `bb.b°` of a device BiBlock (the reference's `Block{L}` views, src/block.jl:49-79):
+`ll` (read and assigned), `ll_history`, `XX`, `WW` of the block's segments.
 """
-struct DeviceSamplingPair
-    se::DeviceSamplingEnsemble
-    r::Int
+struct DeviceBlock
+    bb::DeviceBiBlock
+    unit::Int32
 end
-Base.getindex(se::DeviceSamplingEnsemble, r::Integer) = DeviceSamplingPair(se, r)
+
+function Base.getproperty(bb::DeviceBiBlock, s::Symbol)
+    s === :b && return DeviceBlock(bb, DMT_U)
+    s === :b° && return DeviceBlock(bb, DMT_UPROP)
+    getfield(bb, s)
+end
+
+_llsel(b::DeviceBlock) = getfield(b, :unit) == DMT_U ? DMT_BLK_LL : DMT_BLK_LLPROP
+_histsel(b::DeviceBlock) = getfield(b, :unit) == DMT_U ? DMT_BLK_LL_HIST : DMT_BLK_LLPROP_HIST
+
+function Base.getproperty(b::DeviceBlock, s::Symbol)
+    bb, unit = getfield(b, :bb), getfield(b, :unit)
+    if s === :ll
+        return _state(bb, _llsel(b), Float64, 1)[1]
+    elseif s === :ll_history
+        return vec(_hist(bb, _histsel(b), Float64))
+    elseif s === :XX
+        return _trajectories(bb.se, download_XX(bb.se, unit), bb.segs)
+    elseif s === :WW
+        return _trajectories(bb.se, download_WW(bb.se, unit), bb.segs)
+    end
+    getfield(b, s)
+end
+
+function Base.setproperty!(b::DeviceBlock, s::Symbol, v)
+    s === :ll || error("DeviceBlock: only ll can be assigned")
+    bb = getfield(b, :bb)
+    vals = Float64[v]
+    check(ccall((:dmt_set_block_state, libdmt), Int32,
+        (Ptr{Cvoid}, Int32, Int32, Int64, Int64, Ptr{Cvoid}),
+        bb.se.h, bb.layout, _llsel(b), bb.b0, bb.b1, vals))
+    v
+end
 
 """
     DeviceBlockEnsemble(se, ranges, ρρ=0.0, ll_hist_len=0)
@@ -393,8 +595,10 @@ function DeviceBlockEnsemble(se::DeviceSamplingEnsemble, ranges, ρρ=0.0, ll_hi
     recs = Any[]
     b = 0
     for r in 1:R
+        g0 = _seg0(se, r)
         blocks = Any[DeviceBiBlock{Bool(islast[b+i])}(se, id[], b + i - 1, b + i, ll_hist_len,
-                                                     rho[b+i]) for i in 1:n_blocks[r]]
+                                                     rho[b+i], (g0 + sf[b+i] + 1):(g0 + sl[b+i] + 1))
+                     for i in 1:n_blocks[r]]
         push!(recs, DeviceBlockCollection(se, id[], b, b + n_blocks[r], ll_hist_len, blocks))
         b += n_blocks[r]
     end
@@ -414,7 +618,7 @@ function BlockCollection(sp::DeviceSamplingPair, ranges, ρρ=0.0, ll_hist_len=0
     DeviceBlockEnsemble(sp.se, all_ranges, ρ, ll_hist_len).recordings[sp.r]
 end
 
-function BiBlock(sp::DeviceSamplingPair, range::UnitRange{Int64}, ρ=0.0, last_block=false,
+function BiBlock(sp::DeviceSamplingPair, range::UnitRange{<:Integer}, ρ=0.0, last_block=false,
                  ll_hist_len=0)
     R = length(sp.se.n_points)
     n_blocks = Int32[r == sp.r ? 1 : 0 for r in 1:R]
@@ -423,7 +627,9 @@ function BiBlock(sp::DeviceSamplingPair, range::UnitRange{Int64}, ρ=0.0, last_b
         (Ptr{Cvoid}, Ptr{Int32}, Ptr{Int32}, Ptr{Int32}, Ptr{UInt8}, Ptr{Float64}, Int64,
          Ref{Int32}), sp.se.h, n_blocks, Int32[first(range) - 1], Int32[last(range) - 1],
         UInt8[last_block], Float64[ρ], ll_hist_len, id))
-    DeviceBiBlock{Bool(last_block)}(sp.se, id[], 0, 1, ll_hist_len, ρ)
+    g0 = _seg0(sp.se, sp.r)
+    DeviceBiBlock{Bool(last_block)}(sp.se, id[], 0, 1, ll_hist_len, ρ,
+                                    (g0 + first(range)):(g0 + last(range)))
 end
 
 _n(x::DeviceBlocks) = x.b1 - x.b0
@@ -446,6 +652,12 @@ function draw_proposal_path!(x::DeviceBlocks; Z=nothing, iter=nothing, salt=noth
     x isa DeviceBiBlock ? Bool(ok[1]) : Bool.(ok)
 end
 
+"draw_proposal_path!(u::SamplingUnit) (src/sampling_unit.jl:118-120): (success, ll)."
+function draw_proposal_path!(u::DeviceSamplingUnit)
+    ok, ll = draw_unit!(u.se, u.unit, u.r - 1, u.r)
+    ok[1], ll[1]
+end
+
 function accept_reject_proposal_path!(x::DeviceBlocks, mcmciter; E=nothing, salt=nothing)
     salt = salt === nothing ? DMT_RNG_AUTO : UInt32(salt)
     acc = Vector{UInt8}(undef, _n(x))
@@ -456,13 +668,21 @@ function accept_reject_proposal_path!(x::DeviceBlocks, mcmciter; E=nothing, salt
     nothing
 end
 
+# fused iterations: a BlockEnsemble's sums are over every rank (collective); a collection's or
+# a block's are this rank's (the _local entry points: no collective)
 "draw_proposal_path! + accept_reject_proposal_path!(·, i) + (fetch_ll, fetch_ll°, #accepted)."
 function mcmc_step!(x::DeviceBlocks, mcmciter; salt=nothing)
     salt = salt === nothing ? DMT_RNG_AUTO : UInt32(salt)
     a, b, n = Ref(0.0), Ref(0.0), Ref{Int64}(0)
-    check(ccall((:dmt_mcmc_step, libdmt), Int32,
-        (Ptr{Cvoid}, Int32, Int64, Int64, Int64, UInt32, Ref{Float64}, Ref{Float64}, Ref{Int64}),
-        x.se.h, x.layout, x.b0, x.b1, mcmciter, salt, a, b, n))
+    if x isa DeviceBlockEnsemble
+        check(ccall((:dmt_mcmc_step, libdmt), Int32,
+            (Ptr{Cvoid}, Int32, Int64, Int64, Int64, UInt32, Ref{Float64}, Ref{Float64}, Ref{Int64}),
+            x.se.h, x.layout, x.b0, x.b1, mcmciter, salt, a, b, n))
+    else
+        check(ccall((:dmt_mcmc_step_local, libdmt), Int32,
+            (Ptr{Cvoid}, Int32, Int64, Int64, Int64, UInt32, Ref{Float64}, Ref{Float64}, Ref{Int64}),
+            x.se.h, x.layout, x.b0, x.b1, mcmciter, salt, a, b, n))
+    end
     a[], b[], n[]
 end
 
@@ -470,9 +690,15 @@ end
 function mcmc_run!(x::DeviceBlocks, iter0, n_iter; salt=nothing)
     salt = salt === nothing ? DMT_RNG_AUTO : UInt32(salt)
     out = Matrix{Float64}(undef, 3, n_iter)
-    check(ccall((:dmt_mcmc_run, libdmt), Int32,
-        (Ptr{Cvoid}, Int32, Int64, Int64, Int64, Int64, UInt32, Ptr{Float64}),
-        x.se.h, x.layout, x.b0, x.b1, iter0, n_iter, salt, out))
+    if x isa DeviceBlockEnsemble
+        check(ccall((:dmt_mcmc_run, libdmt), Int32,
+            (Ptr{Cvoid}, Int32, Int64, Int64, Int64, Int64, UInt32, Ptr{Float64}),
+            x.se.h, x.layout, x.b0, x.b1, iter0, n_iter, salt, out))
+    else
+        check(ccall((:dmt_mcmc_run_local, libdmt), Int32,
+            (Ptr{Cvoid}, Int32, Int64, Int64, Int64, Int64, UInt32, Ptr{Float64}),
+            x.se.h, x.layout, x.b0, x.b1, iter0, n_iter, salt, out))
+    end
     permutedims(out)
 end
 
@@ -481,6 +707,19 @@ _ll!(x, unit) = check(ccall((:dmt_loglikhd, libdmt), Int32,
     (Ptr{Cvoid}, Int32, Int32, Int64, Int64), x.se.h, x.layout, unit, x.b0, x.b1))
 loglikhd!(x::DeviceBlocks) = _ll!(x, DMT_U)
 loglikhd°!(x::DeviceBlocks) = _ll!(x, DMT_UPROP)
+loglikhd!(b::DeviceBlock) = _ll!(getfield(b, :bb), getfield(b, :unit))
+
+"GP.loglikhd(u::SamplingUnit) (src/sampling_unit.jl:109): the stored path's log-likelihood."
+function GP.loglikhd(u::DeviceSamplingUnit)
+    # the handle's internal layout 0 holds one terminal block per recording over all segments
+    check(ccall((:dmt_loglikhd, libdmt), Int32, (Ptr{Cvoid}, Int32, Int32, Int64, Int64),
+                u.se.h, 0, u.unit, u.r - 1, u.r))
+    out = Vector{Float64}(undef, 1)
+    check(ccall((:dmt_get_block_state, libdmt), Int32,
+        (Ptr{Cvoid}, Int32, Int32, Int64, Int64, Ptr{Cvoid}),
+        u.se.h, 0, u.unit == DMT_U ? DMT_BLK_LL : DMT_BLK_LLPROP, u.r - 1, u.r, out))
+    out[1]
+end
 
 # fetch_ll(be) is the whole (multi-GPU) ensemble's (a collective over ranks); a collection's or
 # a block's is this rank's (src/block_collection.jl:144,156, src/block_ensemble.jl:140,152)
@@ -508,6 +747,13 @@ function recompute_path!(x::DeviceBlocks; skip=0)
         x.se.h, x.layout, x.b0, x.b1, skip, ok))
     Bool.(ok)
 end
+# the reference's own call form, recompute_path!(bb.b°, bb.b.WW; skip) (src/biblock.jl:343):
+# the device re-solves b° with b's Wiener path, the only one the reference passes
+function recompute_path!(b::DeviceBlock, WW; skip=0)
+    getfield(b, :unit) == DMT_UPROP ||
+        error("recompute_path!: the device re-solves the proposal bb.b° with bb.b.WW")
+    recompute_path!(getfield(b, :bb); skip=skip)
+end
 
 """
     GP.equalize_obs_params!(x)
@@ -516,7 +762,7 @@ src/biblock.jl:375-387: u°'s observation parameters ← u's.  The device stores
 observations once for both u and u° (`upload_obs!`), so they never differ: nothing to copy, no
 critical change.
 """
-equalize_obs_params!(x::DeviceBlocks) = falses(_n(x))
+GP.equalize_obs_params!(x::DeviceBlocks) = false
 
 "Observation information at every segment end (packed H, F, c) + artificial noise."
 upload_obs!(se::DeviceSamplingEnsemble, Hobs, Fobs, cobs; artificial_noise=1e-11) =
@@ -524,51 +770,114 @@ upload_obs!(se::DeviceSamplingEnsemble, Hobs, Fobs, cobs; artificial_noise=1e-11
         (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Float64),
         se.h, Hobs, Fobs, cobs, artificial_noise))
 
-"GP.set_obs!(bb) (src/biblock.jl:273-280) over the blocks."
-set_obs!(x::DeviceBlocks) = check(ccall((:dmt_set_obs, libdmt), Int32,
+"GP.set_obs!(bb) (src/biblock.jl:273-280, broadcasts src/block_collection.jl:198, src/block_ensemble.jl:192)."
+GP.set_obs!(x::DeviceBlocks) = check(ccall((:dmt_set_obs, libdmt), Int32,
     (Ptr{Cvoid}, Int32, Int64, Int64), x.se.h, x.layout, x.b0, x.b1))
 
 _rgt!(x::DeviceBlocks, unit) = check(ccall(
     (:dmt_recompute_guiding_term, libdmt), Int32, (Ptr{Cvoid}, Int32, Int64, Int64, Int32),
     x.se.h, x.layout, x.b0, x.b1, unit))
 """
-    recompute_guiding_term!(x, [::Val{:P_only} | ::Val{:P°_only}])
+    GP.recompute_guiding_term!(x, [::Val{:P_only} | ::Val{:P°_only}])
 
-GP.recompute_guiding_term! on the device: with no flag both the accepted and the proposal laws,
-b then b° (src/biblock.jl:288-291, src/block_collection.jl:208-210); `Val(:P_only)` the
-accepted laws (= `recompute_guiding_term!(bb.b)`), `Val(:P°_only)` the proposal laws
-(src/block_collection.jl:212-221).
+GP.recompute_guiding_term! on the device: of a BiBlock / collection / ensemble with no flag both
+the accepted and the proposal laws, b then b° (src/biblock.jl:288-291,
+src/block_collection.jl:208-210); `Val(:P_only)` the accepted laws, `Val(:P°_only)` the proposal
+laws (src/block_collection.jl:212-221); of a block view `bb.b` / `bb.b°` its own laws
+(src/block.jl:102-110, as `(bb->recompute_guiding_term!(bb.b)).(B)` in
+docs/src/tutorials/biblock/smoothing_with_blocking.md:38); of a SamplingUnit its PP over the
+whole recording (src/sampling_unit.jl:100-102).
 """
-recompute_guiding_term!(x::DeviceBlocks) = (_rgt!(x, DMT_U); _rgt!(x, DMT_UPROP))
-recompute_guiding_term!(x::DeviceBlocks, ::Val{:P_only}) = _rgt!(x, DMT_U)
-recompute_guiding_term!(x::DeviceBlocks, ::Val{:P°_only}) = _rgt!(x, DMT_UPROP)
+GP.recompute_guiding_term!(x::DeviceBlocks) = (_rgt!(x, DMT_U); _rgt!(x, DMT_UPROP))
+GP.recompute_guiding_term!(x::DeviceBlocks, ::Val{:P_only}) = _rgt!(x, DMT_U)
+GP.recompute_guiding_term!(x::DeviceBlocks, ::Val{:P°_only}) = _rgt!(x, DMT_UPROP)
+GP.recompute_guiding_term!(b::DeviceBlock) = _rgt!(getfield(b, :bb), getfield(b, :unit))
+GP.recompute_guiding_term!(u::DeviceSamplingUnit) = check(ccall(
+    (:dmt_recompute_guiding_term, libdmt), Int32, (Ptr{Cvoid}, Int32, Int64, Int64, Int32),
+    u.se.h, 0, u.r - 1, u.r, u.unit))
 
-"""
-    set_proposal_law!(x, θ°::AbstractVector, pnames::AbstractVector{Symbol}; skip=0)
+# ---- parameter names (src/param_names_collections.jl) for device blocks: only the θ° → name
+# maps `updt` are needed (the device re-derives the auxiliary laws from θ itself)
+_pn_unit(θnames, pdep) = (var = (), var_aux = [],
+    updt = Tuple(findfirst(==(p[1]), θnames) => p[2] for p in pdep if p[1] in θnames),
+    updt_aux = [], updt_obs = [])
+_pn_block(θnames, pdep) = (PP = _pn_unit(θnames, pdep), P_last = _pn_unit(θnames, pdep),
+    P_excl = _pn_unit(θnames, pdep), Pb_excl = _pn_unit(θnames, pdep))
+"ParamNamesRecording(bc, θnames, pdep, odeps) of a device BlockCollection (src/param_names_collections.jl:249-257)."
+ParamNamesRecording(bc::DeviceBlockCollection, θnames, pdep, odeps) =
+    (blocks = [_pn_block(θnames, pdep) for _ in bc.blocks],)
+"ParamNamesAllObs(be, θnames, all_obs) of a device BlockEnsemble (src/param_names_collections.jl:274-288)."
+ParamNamesAllObs(be::DeviceBlockEnsemble, θnames, all_obs) =
+    (recordings = [ParamNamesRecording(be.recordings[i], θnames, all_obs.param_depend_rev[i],
+                                       all_obs.obs_depend_rev[i]) for i in 1:length(be.recordings)],)
 
-set_proposal_law! (src/biblock.jl:334-345) on the device: u°'s laws ← u's with the named
-parameters set to θ° (names as DiffusionDefinition's: FHN `:ϵ, :s, :γ, :β, :σ`, Lorenz
-`:s, :r, :β`), the guiding term recomputed where the auxiliary law changed, then
-recompute_path!(b°, b.WW).  Returns (success, critical) per block.
-"""
 const _PAR_NAMES = Dict(
     DMT_MODEL_FHN => Dict(:ϵ => 0, :s => 1, :γ => 2, :β => 3, :σ => 4),
     DMT_MODEL_LORENZ => Dict(:s => 0, :r => 1, :β => 2))
-function set_proposal_law!(x::DeviceBlocks, θ°::AbstractVector, pnames::AbstractVector; skip=0)
-    names = get(_PAR_NAMES, x.se.model, Dict{Symbol,Int}())
-    idx = Int32[p isa Symbol ? names[p] : Int32(p) for p in pnames]
-    val = Float64.(θ°)
-    ok = Vector{UInt8}(undef, x.b1 - x.b0)
-    crit = Vector{UInt8}(undef, x.b1 - x.b0)
+
+"The θ° entry → device parameter index map of one block's pnames (all four law collections)."
+function _param_map(se::DeviceSamplingEnsemble, pnames_block)
+    names = get(_PAR_NAMES, se.model, Dict{Symbol,Int}())
+    m = Dict{Int32,Int}()
+    for coll in (:PP, :P_last, :P_excl, :Pb_excl)
+        u = getproperty(pnames_block, coll)
+        pairs = collect(u.updt)
+        for ua in u.updt_aux
+            append!(pairs, collect(ua))
+        end
+        for (idx, name) in pairs
+            k = Int32(name isa Symbol ? names[name] : name)
+            get(m, k, idx) == idx || error("parameter $name updated from two entries of θ°")
+            m[k] = idx
+        end
+    end
+    m
+end
+
+function _set_law!(x::DeviceBlocks, θ°, pmap; skip=0)
+    idx = collect(keys(pmap))
+    val = Float64[θ°[pmap[k]] for k in idx]
+    ok = Vector{UInt8}(undef, _n(x))
+    crit = Vector{UInt8}(undef, _n(x))
     check(ccall((:dmt_set_proposal_law, libdmt), Int32,
         (Ptr{Cvoid}, Int32, Int64, Int64, Int32, Ptr{Int32}, Ptr{Float64}, Int32, Ptr{UInt8},
          Ptr{UInt8}), x.se.h, x.layout, x.b0, x.b1, length(idx), idx, val, skip, ok, crit))
-    Bool.(ok), Bool.(crit)
+    Bool.(ok)
 end
+
+"""
+    set_proposal_law!(x, θ°, pnames, critical_change=true; skip=0)
+
+The reference's `set_proposal_law!` (src/biblock.jl:334-344, src/block_collection.jl:264-276,
+src/block_ensemble.jl:242-255) on device blocks: `pnames` as the reference's (a BiBlock's
+NamedTuple / ParamNamesBlock of `PP, P_last, P_excl, Pb_excl` with `updt` pairs `idx => name`;
+`pnames.blocks[i]` of a collection; `pnames.recordings[r].blocks[i]` of an ensemble).  u°'s laws
+← u's with the named parameters set from θ°, the guiding term of b° recomputed where the law
+changed (what any correct `critical_change` requests; an unchanged law's recomputation
+reproduces its guiding term bit for bit), then recompute_path!(b°, b.WW; skip).  One ccall over
+all blocks whose maps agree.
+"""
+function set_proposal_law!(bb::DeviceBiBlock, θ°, pnames, critical_change=true; skip=0)
+    _set_law!(bb, θ°, _param_map(bb.se, pnames); skip=skip)
+end
+
+function _set_law_blocks!(x, blocks, pblocks, θ°; skip=0)
+    maps = [_param_map(x.se, pb) for pb in pblocks]
+    all(==(maps[1]), maps) && return _set_law!(x, θ°, maps[1]; skip=skip)
+    reduce(vcat, [_set_law!(bb, θ°, m; skip=skip) for (bb, m) in zip(blocks, maps)])
+end
+
+set_proposal_law!(bc::DeviceBlockCollection, θ°, pnames, critical_change=true; skip=0) =
+    _set_law_blocks!(bc, bc.blocks, pnames.blocks, θ°; skip=skip)
+
+set_proposal_law!(be::DeviceBlockEnsemble, θ°, pnames, critical_change=true; skip=0) =
+    _set_law_blocks!(be, [bb for bc in be.recordings for bb in bc.blocks],
+                     [pb for pr in pnames.recordings for pb in pr.blocks], θ°; skip=skip)
 
 "find_W_for_X!(b) (src/block.jl:118-131): u.WW from u.XX under the accepted laws."
 find_W_for_X!(x::DeviceBlocks) = check(ccall((:dmt_find_W_for_X, libdmt), Int32,
     (Ptr{Cvoid}, Int32, Int64, Int64), x.se.h, x.layout, x.b0, x.b1))
+find_W_for_X!(b::DeviceBlock) = find_W_for_X!(getfield(b, :bb))
 
 # ---- swaps, histories (src/biblock.jl:135-259)
 _swap!(x, what) = check(ccall((:dmt_swap, libdmt), Int32,
@@ -579,19 +888,22 @@ swap_WW!(x::DeviceBlocks) = _swap!(x, DMT_SWAP_WW)
 swap_PP!(x::DeviceBlocks) = _swap!(x, DMT_SWAP_PP)
 swap_ll!(x::DeviceBlocks) = _swap!(x, DMT_SWAP_LL)
 
-save_ll!(x::DeviceBlocks, i::Int) = check(ccall((:dmt_save_ll, libdmt), Int32,
+save_ll!(x::DeviceBlocks, i::Integer) = check(ccall((:dmt_save_ll, libdmt), Int32,
     (Ptr{Cvoid}, Int32, Int64, Int64, Int64), x.se.h, x.layout, x.b0, x.b1, i))
+"save_ll!(b, i) of a block view (src/block.jl:94): ll_history[i] = ll."
+save_ll!(b::DeviceBlock, i::Integer) = set_ll!(b, i, b.ll)
 
 "set_ll!(b, i, v) (src/block.jl:82-86): ll_history[i] of bb.b (unit DMT_U) or bb.b°."
-function set_ll!(x::DeviceBlocks, i::Int, v; unit=DMT_U)
+function set_ll!(x::DeviceBlocks, i::Integer, v; unit=DMT_U)
     vals = Vector{Float64}(undef, x.b1 - x.b0)
     vals .= v
     check(ccall((:dmt_set_ll, libdmt), Int32,
                 (Ptr{Cvoid}, Int32, Int32, Int64, Int64, Int64, Ptr{Float64}),
                 x.se.h, x.layout, unit, x.b0, x.b1, i, vals))
 end
+set_ll!(b::DeviceBlock, i::Integer, v) = set_ll!(getfield(b, :bb), i, v; unit=getfield(b, :unit))
 
-function set_accepted!(x::DeviceBlocks, i::Int, v)
+function set_accepted!(x::DeviceBlocks, i::Integer, v)
     vv = fill(UInt8(v), _n(x))
     check(ccall((:dmt_set_accepted, libdmt), Int32,
         (Ptr{Cvoid}, Int32, Int64, Int64, Int64, Ptr{UInt8}), x.se.h, x.layout, x.b0, x.b1, i, vv))

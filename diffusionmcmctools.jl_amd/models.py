@@ -51,10 +51,39 @@ class LinearAux:
         return s @ s.T
 
 
+# parameter-name aliases: DiffusionDefinition's symbols (:ϵ, :γ, …) and ASCII spellings
+_ALIASES = {"eps": "ϵ", "epsilon": "ϵ", "ε": "ϵ", "gamma": "γ", "beta": "β", "sigma": "σ"}
+
+
+def canonical_name(name):
+    name = str(name).lstrip(":")
+    return _ALIASES.get(name, name)
+
+
 class Model:
     kind: int
     d: int
     m: int
+    # DiffusionDefinition's parameter names in θ order (set_parameters!, set_proposal_law!)
+    param_names: tuple = ()
+    # DD.var_parameter_names(P) (src/param_names_collections.jl:141-164): the parameters an MCMC
+    # update may change; the tutorials restrict it per type, e.g.
+    # ``FHN.var_parameter_names = ("γ",)`` for ``DD.var_parameter_names(::FitzHughNagumo) = (:γ,)``
+    var_parameter_names: tuple = None
+
+    def variable_names(self):
+        v = type(self).var_parameter_names
+        return tuple(self.param_names if v is None else (canonical_name(n) for n in v))
+
+    def _attr(self, name):
+        raise KeyError(name)
+
+    def get_param(self, name):
+        return getattr(self, self._attr(canonical_name(name)))
+
+    def set_param(self, name, value):
+        """``DD.set_parameters!``-style update of one named parameter in place."""
+        setattr(self, self._attr(canonical_name(name)), float(value))
 
     def theta_vec(self) -> np.ndarray:
         raise NotImplementedError
@@ -150,6 +179,11 @@ class FHN(Model):
 
     kind = L.MODEL_FHN
     d, m = 2, 1
+    param_names = ("ϵ", "s", "γ", "β", "σ")
+    _ATTRS = {"ϵ": "eps", "s": "s", "γ": "gamma", "β": "beta", "σ": "sg"}
+
+    def _attr(self, name):
+        return self._ATTRS[name]
 
     def __init__(self, eps, s, gamma, beta, sigma):
         self.eps, self.s, self.gamma, self.beta, self.sg = map(float, (eps, s, gamma, beta, sigma))
@@ -182,6 +216,11 @@ class Lorenz(Model):
 
     kind = L.MODEL_LORENZ
     d, m = 3, 3
+    param_names = ("s", "r", "β")
+    _ATTRS = {"s": "s_", "r": "r", "β": "b"}
+
+    def _attr(self, name):
+        return self._ATTRS[name]
 
     def __init__(self, s=10.0, r=28.0, beta=8.0 / 3.0, sigma=(1.0, 1.0, 1.0)):
         self.s_, self.r, self.b = float(s), float(r), float(beta)
@@ -234,11 +273,58 @@ class Observation:
 @dataclass
 class Recording:
     """(P, obs, t0, x0) of ObservationSchemes (docs/src/get_started/overview.md:18-20);
-    KnownStartingPt x0."""
+    KnownStartingPt x0.  ``P`` is the recording's target law (a :class:`Model`), which the
+    reference-form constructors ``SamplingPair(AuxLaw, recording, tts)`` read."""
     obs: list
     t0: float
     x0: np.ndarray
     extra: dict = field(default_factory=dict)
+    P: Model | None = None
+
+    @property
+    def x0_prior(self):
+        return self.x0
+
+
+def build_recording(P, data, t0, x0):
+    """``build_recording(P, data, t0, KnownStartingPt(y1))`` (docs/src/tutorials/preamble.md:87):
+    a recording of the observations ``data`` (a list of :class:`Observation`) of a path of the
+    target law ``P`` started at the known point ``x0``.  ``P`` is copied: ``set_parameters``
+    changes the recording's own law."""
+    import copy
+    return Recording(list(data), float(t0), np.asarray(x0, dtype=np.float64), P=copy.deepcopy(P))
+
+
+def set_parameters(target, theta):
+    """``OBS.set_parameters!(recording, θ)`` / ``OBS.set_parameters!(all_obs, θ)``
+    (docs/src/tutorials/biblock/inference.md:58): the named parameters of the target law(s).
+    ``theta``: a mapping name → value; a name is a law parameter (``"γ"``), a per-recording name
+    ``"REC<k>_<p>"`` or a shared name declared with ``AllObservations.add_dependency``."""
+    from .param_names import AllObservations
+    if isinstance(target, AllObservations):
+        target.set_parameters(theta)
+        return
+    for name, v in dict(theta).items():
+        nm = canonical_name(name)
+        if nm.startswith("REC") and "_" in nm:
+            nm = canonical_name(nm.split("_", 1)[1])
+        target.P.set_param(nm, v)
+
+
+class FitzHughNagumoAux:
+    """``FitzHughNagumoAux`` (DiffusionDefinition, docs/src/tutorials/preamble.md:28) as the
+    ``aux_laws`` of the reference-form constructors: for the segment ending in observation
+    ``obs``, the target law ``P`` linearised at the observed ``y`` (``FHN.aux``)."""
+
+    def __new__(cls, P, obs):
+        return P.aux_for(obs)
+
+
+class LorenzAux:
+    """The Lorenz-63 auxiliary law of config C5: the drift linearised at the observed state."""
+
+    def __new__(cls, P, obs):
+        return P.aux_for(obs)
 
 
 def standard_guid_prop_time_transf(t0, T, dt):
@@ -252,8 +338,11 @@ def standard_guid_prop_time_transf(t0, T, dt):
     return tau
 
 
-def setup_time_grids(recording: Recording, dt: float, transf=standard_guid_prop_time_transf):
-    """One grid per inter-observation interval (OBS.setup_time_grids)."""
+def setup_time_grids(recording, dt: float, transf=standard_guid_prop_time_transf):
+    """One grid per inter-observation interval (OBS.setup_time_grids); of an
+    ``AllObservations``, one such list per recording."""
+    if hasattr(recording, "recordings"):
+        return [setup_time_grids(rec, dt, transf) for rec in recording.recordings]
     grids, t0 = [], recording.t0
     for ob in recording.obs:
         grids.append(transf(t0, ob.t, dt))

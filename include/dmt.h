@@ -334,6 +334,14 @@ dmt_status dmt_mcmc_step(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int
 dmt_status dmt_fetch_ll_local(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
                               int64_t mcmciter, double* ll, double* ll_prop, int64_t* n_acc);
 
+/* dmt_mcmc_step over [b0, b1) of THIS rank only: the fused iteration of a BiBlock or a
+ * BlockCollection (src/biblock.jl:78-127, src/block_collection.jl:46,60-64,144,156), whose
+ * fetch_ll is rank-local; no collective even when a communicator is set, so one rank may call
+ * it alone.  dmt_mcmc_step with a communicator is the BlockEnsemble-level call (every rank). */
+dmt_status dmt_mcmc_step_local(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
+                               int64_t mcmciter, uint32_t salt, double* ll, double* ll_prop,
+                               int64_t* n_acc);
+
 /* n_iter consecutive dmt_mcmc_step iterations (mcmciter = iter0 … iter0+n_iter-1) queued
  * back to back on the device with no host synchronisation in between: the body of the
  * reference's sampling loop (docs/src/tutorials/biblock/smoothing.md:40-44, which pushes
@@ -341,6 +349,10 @@ dmt_status dmt_fetch_ll_local(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1
  * accepted count) of every iteration, identical to what the single-step calls return. */
 dmt_status dmt_mcmc_run(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int64_t iter0,
                         int64_t n_iter, uint32_t salt, double* out);
+/* dmt_mcmc_run with rank-local sums (BiBlock / BlockCollection level, as dmt_mcmc_step_local):
+ * no collective. */
+dmt_status dmt_mcmc_run_local(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int64_t iter0,
+                              int64_t n_iter, uint32_t salt, double* out);
 
 /* ---------------- guiding term (host set-up, GP.build_guid_prop) ---------------- */
 

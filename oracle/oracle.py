@@ -805,14 +805,14 @@ class OracleEnsemble:
                 h = {2: "ll_hist", 3: "llp_hist", 4: "acc_hist"}[what]
                 getattr(b, h)[...] = v[:, j]
 
-    def mcmc_step(self, layout, b0, b1, mcmciter, salt=0):
+    def mcmc_step(self, layout, b0, b1, mcmciter, salt=0, local=False):
         """dmt_mcmc_step: draw + accept with ONE key (disjoint normal / Exp(1) streams)."""
         it, ks = self._draw_key(mcmciter, salt, False)
         self._draw(layout, b0, b1, None, it, ks)
         self._accept(layout, b0, b1, mcmciter, None, it, ks, False)
         return self.fetch_ll(layout, b0, b1, mcmciter)
 
-    def mcmc_run(self, layout, b0, b1, iter0, n_iter, salt=0):
+    def mcmc_run(self, layout, b0, b1, iter0, n_iter, salt=0, local=False):
         """dmt_mcmc_run: iteration it keyed by it (explicit) or by n_iter consecutive counter
         values that do not straddle a 2^32 boundary (RNG_AUTO)."""
         delta, ks = 0, salt
