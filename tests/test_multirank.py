@@ -189,3 +189,50 @@ def test_rccl_allgather_path_single_rank(monkeypatch, persist):
     for e in ens:
         e.close()
 
+
+
+def test_collection_level_calls_are_rank_local():
+    """A BiBlock's or BlockCollection's fused mcmc_step / mcmc_run and fetch_ll are this
+    rank's (src/block_collection.jl:144,156): they reach libdmt as the *_local entry points
+    (no collective, so one rank may call them alone); only the BlockEnsemble's are global."""
+    import oracle as orc
+    import diffusionmcmctools_amd as dmt
+    from diffusionmcmctools_amd import workloads as W
+    w = W.c2_ou2d(B=4, N=20)
+    w.meta["hist_len"] = 6
+    calls = []
+
+    class Recorder(orc.OracleEnsemble):
+        depth = 0
+
+        def _rec(self, name, local, fn, *a, **k):
+            if Recorder.depth == 0:  # the API's calls, not the oracle's own nested ones
+                calls.append((name, local))
+            Recorder.depth += 1
+            try:
+                return fn(*a, local=local, **k)
+            finally:
+                Recorder.depth -= 1
+
+        def mcmc_run(self, *a, local=False, **k):
+            return self._rec("run", local, super().mcmc_run, *a, **k)
+
+        def mcmc_step(self, *a, local=False, **k):
+            return self._rec("step", local, super().mcmc_step, *a, **k)
+
+        def fetch_ll(self, *a, local=False, **k):
+            return self._rec("fetch", local, super().fetch_ll, *a, **k)
+
+    eng = Recorder(w.model.kind, w.d, w.m, w.n_points, prec=w.precision, seed=1,
+                   grid_shared=w.grid_shared)
+    se = dmt.SamplingEnsemble(w.model, w.n_points, _engine=eng)
+    W.fill(eng, w, init_Z=True)
+    be = dmt.BlockEnsemble(se, [[range(0, 1)]] * 4, rho=0.5, ll_hist_len=6)
+    for x, local in ((be.recordings[1], True), (be.recordings[2].blocks[0], True), (be, False)):
+        calls.clear()
+        x.mcmc_run(1, 2)
+        x.mcmc_step(3)
+        x.fetch_ll()
+        assert calls[:2] == [("run", local), ("step", local)], calls
+        if not isinstance(x, dmt.BiBlock):  # a BiBlock reads its ll directly
+            assert ("fetch", local) in calls[2:], calls
