@@ -89,6 +89,7 @@ struct BlockArgs {
                       // steps: one-shot draws on k_block_resident
   int lane_split;     // MAP_LANE draws: producer/consumer waves (k_block_ps); the runtime sets
                       // it only for layouts of single-segment blocks
+  int lane_pair;      // MAP_LANE device-RNG draws: two lanes per recording (k_block_pair)
   int ll_skip;        // MODE_RECOMPUTE: the last ll_skip steps of every segment add no Girsanov
                       // term (recompute_path!(…; skip), GP.solve_and_ll!(…; skip))
 };

@@ -51,7 +51,34 @@ __device__ __forceinline__ T tree_sum(T* v) {
 // come in whole Box–Muller pairs (K·M even); the chunk's K Girsanov terms are summed as an
 // aligned subtree and inserted into the 64-step pairwise counter.  A tail of < K steps
 // runs through the single-step path.
-template <class Mdl, class T, int MODE, bool PARITY, int K>
+#ifndef DMT_KCHUNK_PAIR_BASE
+#define DMT_KCHUNK_PAIR_BASE 4  // pair-kernel chunk (doubled when it would hold an odd number of
+                                // Philox blocks: Lorenz fp32, 3 normals per step → 8 steps)
+#endif
+// Two lanes of one wave (l and l + 32) holding the same recording (the pair mapping,
+// k_block_pair): role 0 draws the even Philox blocks of a chunk, role 1 the odd ones, and
+// v_permlane32_swap hands each half's normals to the other — both roles then run the same
+// recursion on the same values (bit-identical to one lane drawing them all).
+template <class T>
+__device__ __forceinline__ void pair_exchange(T v, T& lo, T& hi);
+template <>
+__device__ __forceinline__ void pair_exchange<float>(float v, float& lo, float& hi) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false,
+                                                  false);
+  lo = __uint_as_float(r[0]);  // role 0's value in every lane
+  hi = __uint_as_float(r[1]);  // role 1's value in every lane
+}
+template <>
+__device__ __forceinline__ void pair_exchange<double>(double v, double& lo, double& hi) {
+  const uint64_t b = (uint64_t)__double_as_longlong(v);
+  const auto l = __builtin_amdgcn_permlane32_swap((uint32_t)b, (uint32_t)b, false, false);
+  const auto h = __builtin_amdgcn_permlane32_swap((uint32_t)(b >> 32), (uint32_t)(b >> 32),
+                                                  false, false);
+  lo = __longlong_as_double((long long)(((uint64_t)h[0] << 32) | l[0]));
+  hi = __longlong_as_double((long long)(((uint64_t)h[1] << 32) | l[1]));
+}
+
+template <class Mdl, class T, int MODE, bool PARITY, int K, bool PAIR = false>
 __device__ __forceinline__ bool run_segment(const Law<Mdl, T>& L, const T* __restrict__ tpl,
                                             const int t_sh, const T* __restrict__ Ht,
                                             const int H_sh, const T* __restrict__ Ft,
@@ -59,7 +86,8 @@ __device__ __forceinline__ bool run_segment(const Law<Mdl, T>& L, const T* __res
                                             const T* Xcs, T* Xcd, T* Wcd,
                                             NormalStream<T>& ns, const int64_t tq, const int64_t q0,
                                             const int np, const int lane, const T rho,
-                                            const T srho, const int ll_skip, T* x, T& sl) {
+                                            const T srho, const int ll_skip, T* x, T& sl,
+                                            const int role = 0) {
   constexpr int D = Mdl::D, M = Mdl::M, HP = D * (D + 1) / 2;
   constexpr bool DRAW = MODE != MODE_RECOMPUTE;
   constexpr bool READW = MODE != MODE_FRESH;
@@ -183,13 +211,31 @@ __device__ __forceinline__ bool run_segment(const Law<Mdl, T>& L, const T* __res
       if (DRAW && !PARITY) {  // whole Philox blocks of normals for this chunk, straight-line
         constexpr int NPB = NormPerBlock<T>::v;
         static_assert((K * M) % NPB == 0, "chunk must hold whole normal blocks");
+        if constexpr (PAIR) {  // role r draws blocks 2j + r; the pair swaps halves
+          static_assert((K * M / NPB) % 2 == 0, "a pair chunk holds an even number of blocks");
 #pragma unroll
-        for (int bq = 0; bq < K * M / NPB; ++bq) {
-          const uint32_t bc = (uint32_t)((c0 * M) / NPB + bq);
-          T zb[NPB];
-          normal_block(philox4x32_10(U4{bc, ns.seg, ns.iter, ns.c3}, ns.k0, ns.k1), zb);
+          for (int j = 0; j < K * M / NPB / 2; ++j) {
+            const uint32_t bc = (uint32_t)((c0 * M) / NPB + 2 * j + role);
+            T zb[NPB];
+            normal_block(philox4x32_10(U4{bc, ns.seg, ns.iter, ns.c3}, ns.k0, ns.k1), zb);
 #pragma unroll
-          for (int e = 0; e < NPB; ++e) cur.Z[(NPB * bq + e) / M][(NPB * bq + e) % M] = zb[e];
+            for (int e = 0; e < NPB; ++e) {
+              T lo, hi;
+              pair_exchange<T>(zb[e], lo, hi);
+              const int n0 = NPB * (2 * j) + e, n1 = NPB * (2 * j + 1) + e;
+              cur.Z[n0 / M][n0 % M] = lo;
+              cur.Z[n1 / M][n1 % M] = hi;
+            }
+          }
+        } else {
+#pragma unroll
+          for (int bq = 0; bq < K * M / NPB; ++bq) {
+            const uint32_t bc = (uint32_t)((c0 * M) / NPB + bq);
+            T zb[NPB];
+            normal_block(philox4x32_10(U4{bc, ns.seg, ns.iter, ns.c3}, ns.k0, ns.k1), zb);
+#pragma unroll
+            for (int e = 0; e < NPB; ++e) cur.Z[(NPB * bq + e) / M][(NPB * bq + e) % M] = zb[e];
+          }
         }
       }
       T gv[K];
@@ -241,12 +287,12 @@ __device__ __forceinline__ bool map_block(const BlockArgs<T>& a, int64_t& tile, 
 // tile-phase repair only while the minority is at most 1/repair_div of the wave
 // (BlockArgs::repair_div; 4 by default, DMT_REPAIR_DIV)
 
-template <class Mdl, class T, int MODE, bool PARITY, int K>
-__global__ __launch_bounds__(64) void k_block(const BlockArgs<T> a) {
+// The lane kernel's body for block blk of recording tile `tile`, recording slot `lane` of the
+// tile (the lane-interleaved layout's column); PAIR: two lanes (roles) per recording.
+template <class Mdl, class T, int MODE, bool PARITY, int K, bool PAIR>
+__device__ __forceinline__ void lane_block(const BlockArgs<T>& a, const int64_t tile,
+                                           const int64_t blk, const int lane, const int role) {
   constexpr int D = Mdl::D, M = Mdl::M, HP = D * (D + 1) / 2;
-  int64_t tile, blk;
-  if (!map_block(a, tile, blk)) return;
-  const int lane = threadIdx.x;
   const int64_t tq = a.tile_qoff[tile];
   auto idx = [&](int64_t q, int c, int C) -> int64_t { return ((tq + q) * C + c) * kLanes + lane; };
   const int g0 = a.gfirst[blk], g1 = a.glast[blk];
@@ -312,9 +358,9 @@ __global__ __launch_bounds__(64) void k_block(const BlockArgs<T> a) {
       }
     }
     T sl;
-    const bool sok = run_segment<Mdl, T, MODE, PARITY, K>(
+    const bool sok = run_segment<Mdl, T, MODE, PARITY, K, PAIR>(
         L, a.t, a.t_shared, a.H[ls][kind], a.H_shared[ls][kind], a.F[ls][kind], Ws, Wd, Xd, Zg,
-        Xcs, Xcd, Wcd, ns, tq, a.seg_q[g], a.seg_np[g], lane, rho, srho, a.ll_skip, x, sl);
+        Xcs, Xcd, Wcd, ns, tq, a.seg_q[g], a.seg_np[g], lane, rho, srho, a.ll_skip, x, sl, role);
     if (MODE == MODE_PCN) {
       if (nsx != sx) a.selX[g] = (uint8_t)nsx;
       if (nsw != sw) a.selW[g] = (uint8_t)nsw;
@@ -322,9 +368,48 @@ __global__ __launch_bounds__(64) void k_block(const BlockArgs<T> a) {
     if (!sok) { ok = false; break; }
     ll = ll + sl;
   }
-  a.ll_out[blk] = ok ? (double)ll : -INFINITY;
-  if (a.success) a.success[blk] = ok ? 1 : 0;
+  if (role == 0) {
+    a.ll_out[blk] = ok ? (double)ll : -INFINITY;
+    if (a.success) a.success[blk] = ok ? 1 : 0;
+  }
 }
+
+template <class Mdl, class T, int MODE, bool PARITY, int K>
+__global__ __launch_bounds__(64) void k_block(const BlockArgs<T> a) {
+  int64_t tile, blk;
+  if (!map_block(a, tile, blk)) return;
+  lane_block<Mdl, T, MODE, PARITY, K, false>(a, tile, blk, threadIdx.x, 0);
+}
+
+// ---- MAP_LANE, pair mapping: two waves per (recording tile, block index), each
+// holding 32 recordings of the tile on lane pairs (l, l + 32).  The pair draws a chunk's normals
+// half each (pair_exchange) and runs the recursion redundantly, so an ensemble with fewer
+// tiles than the device has SIMDs (C5: 512 tiles, 1 024 SIMDs) fills the chip with waves whose
+// per-step instruction stream is the recursion plus HALF the random-number work.  Same
+// operations on the same values per recording: bit-identical to k_block.
+template <class Mdl, class T>
+struct PairChunk {  // steps per chunk: an even number of whole Philox blocks of normals
+  static constexpr int NPB = NormPerBlock<T>::v;
+  static constexpr int v = ((DMT_KCHUNK_PAIR_BASE * Mdl::M) % (2 * NPB) == 0)
+                               ? DMT_KCHUNK_PAIR_BASE : 2 * DMT_KCHUNK_PAIR_BASE;
+};
+
+template <class Mdl, class T, int MODE>
+__global__ __launch_bounds__(64) void k_block_pair(const BlockArgs<T> a) {
+  const int lane = threadIdx.x, role = lane >> 5;
+  const int64_t wave = blockIdx.x, w2 = wave >> 1;
+  const int slot = (int)(wave & 1) * 32 + (lane & 31);
+  const int64_t tile = a.tile0 + w2 / a.MB;
+  const int b = (int)(w2 % a.MB);
+  if (tile >= a.tile1) return;
+  const int64_t r = tile * kLanes + slot;
+  if (r >= a.R) return;
+  const int64_t blk = a.blk_off[r] + b;
+  if (blk >= a.blk_off[r + 1] || blk < a.b0 || blk >= a.b1) return;
+  lane_block<Mdl, T, MODE, false, PairChunk<Mdl, T>::v, true>(a, tile, blk, slot, role);
+}
+
+
 
 // ---- MAP_LANE, split into a producer and a consumer wave.  For draws
 // (MODE_PCN, device RNG) over single-segment blocks.  One workgroup of two waves per
@@ -3582,6 +3667,12 @@ static hipError_t launch_block_t(int mapping, int mode, const void* args, int64_
     }
     const dim3 block(64);
     const bool par = a.Z != nullptr;
+    if (!par && a.lane_pair && (mode == MODE_PCN || mode == MODE_FRESH)) {  // lane pairs
+      const dim3 pgrid((unsigned)(2 * nwaves));
+      if (mode == MODE_PCN) dlaunch(k_block_pair<Mdl, T, MODE_PCN>, pgrid, block, s, a);
+      else dlaunch(k_block_pair<Mdl, T, MODE_FRESH>, pgrid, block, s, a);
+      return hipGetLastError();
+    }
     if (mode == MODE_PCN && !par && a.lane_split) {  // producer/consumer waves (k_block_ps)
       dlaunch(k_block_ps<Mdl, T>, grid, dim3(128), s, a);
       return hipGetLastError();

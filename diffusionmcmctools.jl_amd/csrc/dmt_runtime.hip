@@ -174,6 +174,7 @@ struct dmt_ens {
   int resident_pc = 1;       // ... split over a consumer and this many producer waves per block
                              // (DMT_MCMC_PC=0: one wave; 1 or 2 producers)
   int lane_split = -1;       // MAP_LANE draws on producer/consumer waves: 1 on, 0 off, -1 auto
+  int lane_pair = -1;        // MAP_LANE device-RNG draws on lane pairs: 1 on, 0 off, -1 auto
                              // (when the draw has fewer waves than the device has SIMDs)
   int64_t n_simd = 1024;
   int repair_div = 4;        // MAP_LANE tile-phase repair threshold (DMT_REPAIR_DIV)
@@ -438,6 +439,7 @@ void fill_common(dmt_ens* h, const Layout* L, BlockArgs<T>& a) {
   a.success = nullptr;
   a.repair_div = h->repair_div;
   a.lane_split = 0;
+  a.lane_pair = 0;
   a.resident1 = 0;
 }
 
@@ -474,9 +476,13 @@ dmt_status run_block_kernel(dmt_ens* h, const Layout* L, int mode, int kind_time
                   L->single_seg && L->max_steps <= kResidentMaxSteps;
     // auto: fp64 only — with fp32's four normals per Philox block the single wave is faster
     // (C5: 1773 vs 1934 µs per draw, profiles/r02m)
-    a.lane_split = L->single_seg && (h->lane_split == 1 ||
-                                     (h->lane_split < 0 && nwaves < h->n_simd &&
-                                      h->key.precision == DMT_F64));
+    // lane pairs (k_block_pair): on request only — bit-identical, but measured no faster on C5
+    // (1 862 / 1 925 vs 1 829 µs per draw) and slower on C3 (1 821 vs 1 301 µs):
+    // profiles/r03d, DESIGN.md §6
+    a.lane_pair = h->lane_pair == 1;
+    a.lane_split = !a.lane_pair && L->single_seg &&
+                   (h->lane_split == 1 || (h->lane_split < 0 && nwaves < h->n_simd &&
+                                           h->key.precision == DMT_F64));
   };
   if (h->key.precision == DMT_F64) {
     BlockArgs<double> a{};
@@ -707,6 +713,7 @@ dmt_status dmt_create(dmt_ens** out, const dmt_model* model, const dmt_structure
   if (const char* e = std::getenv("DMT_MCMC_PC")) h->resident_pc = std::max(0, std::min(2, std::atoi(e)));
   if (const char* e = std::getenv("DMT_DISPATCH_EVENTS")) h->dispatch_events = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("DMT_LANE_SPLIT")) h->lane_split = std::atoi(e);
+  if (const char* e = std::getenv("DMT_LANE_PAIR")) h->lane_pair = std::atoi(e);
   if (const char* e = std::getenv("DMT_REPAIR_DIV")) h->repair_div = std::max(1, std::atoi(e));
   if (const char* e = std::getenv("DMT_SCAN_RESIDENT")) h->scan_resident = std::strcmp(e, "0") != 0;
   {

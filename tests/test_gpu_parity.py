@@ -430,6 +430,40 @@ def test_device_rng_mode_bit_exact_c5_fp32(mapping):
     run_device_rng_parity(W.c5_lorenz(B=40, N=300), iters=2, mapping=mapping)
 
 
+@pytest.mark.parametrize("variant", [
+    pytest.param({"DMT_LANE_PAIR": "0", "DMT_LANE_SPLIT": "0"}, id="single-lane"),
+    pytest.param({"DMT_LANE_PAIR": "1"}, id="lane-pair"),
+    pytest.param({"DMT_LANE_PAIR": "0", "DMT_LANE_SPLIT": "1"}, id="producer-consumer"),
+])
+@pytest.mark.parametrize("cfg", ["c3", "c5"])
+def test_device_rng_lane_kernels_bit_exact(cfg, variant, monkeypatch):
+    """The three lane-mapping draw kernels (k_block one lane per recording, k_block_pair two
+    lanes per recording sharing the normals, k_block_ps producer/consumer waves) draw the same
+    device streams and give the oracle's paths, ll and decisions bit for bit — on a ragged
+    last tile (70 / 40 recordings) and through two MCMC iterations."""
+    for k, v in variant.items():
+        monkeypatch.setenv(k, v)
+    w = (W.c3_fhn(B=70, N=300, T_burn=0.1) if cfg == "c3" else W.c5_lorenz(B=40, N=300))
+    run_device_rng_parity(w, iters=2, mapping=L.MAP_LANE, seed=13)
+
+
+@pytest.mark.parametrize("pair", ["0", "1"])
+def test_device_rng_lane_pair_multisegment_bit_exact(pair, monkeypatch):
+    """k_block_pair on multi-segment blocks with P_last laws (two blocking layouts)."""
+    monkeypatch.setenv("DMT_LANE_PAIR", pair)
+    _, dev, ora, ((A, nA), (Bl, nB)) = cs.ragged_pair(hist_len=3, mapping=L.MAP_LANE)
+    for lay, nb in ((A, nA), (Bl, nB)):
+        for e in (dev, ora):
+            e.loglikhd(lay, L.U, 0, nb)
+        for i in (1, 2):
+            for e in (dev, ora):
+                e.draw_proposal(lay, 0, nb, iter=i, salt=3)
+            assert np.array_equal(dev.accept_reject(lay, 0, nb, i, salt=3, want_acc=True),
+                                  ora.accept_reject(lay, 0, nb, i, salt=3, want_acc=True))
+            cs.assert_paths_equal(dev, ora)
+            cs.assert_ll_equal(dev, ora, lay, nb)
+
+
 @pytest.mark.parametrize("mapping", MAPPINGS)
 def test_failure_gives_minus_inf_and_rejects(mapping):
     w = W.c1_ou1d()
