@@ -143,7 +143,7 @@ def cpu_baseline(w, ens, lay, iter0, budget_s=12.0):
     rho = np.full(B, w.rho)
     prec = w.precision
 
-    def run(nt, max_it, budget, record):
+    def run(nt, max_it, budget, record, max_it_min=2):
         Xa, Wa, lla = X.copy(), Wp.copy(), ll.copy()
         decisions = []
         it, acc_n = 0, 0
@@ -164,12 +164,12 @@ def cpu_baseline(w, ens, lay, iter0, budget_s=12.0):
             it += 1
             if record:
                 decisions.append(acc)
-            if time.perf_counter() - t0 > budget and it >= 2:
+            if time.perf_counter() - t0 > budget and it >= max_it_min:
                 break
         el = time.perf_counter() - t0
         return w.steps_per_iter * it / el, it, acc_n / (B * it), decisions
 
-    v1, its1, _, _ = run(1, 3, 0.0, False)  # single-thread rate on a short sample
+    v1, its1, _, _ = run(1, 5, 0.0, False, 5)  # single-thread rate: 5 whole iterations
     v, its, ar, dec = run(nthreads, CPU_MAX_ITERS, budget_s, True)
     # the device runs the same iterations from the same state (untimed) and records decisions
     ens.mcmc_run(lay, 0, B, iter0, its)
@@ -192,6 +192,51 @@ def cpu_baseline(w, ens, lay, iter0, budget_s=12.0):
 
 
 ens_seed = 0xD1FF
+
+
+def separate_calls(ens, lay, B, iter0, n, global_, python=True):
+    """The reference's unchanged caller loop, every call separate — draw_proposal_path!(be);
+    accept_reject_proposal_path!(be, i); fetch_ll(be); fetch_ll°(be) — issued as C-ABI calls
+    from C (csrc/dmt_callbench.c: what a Julia caller's ccalls cost) and, for comparison, from
+    Python through ctypes (the Python mirror).  Returns µs per iteration of both loops and the
+    C loop's per-iteration (fetch_ll, fetch_ll°, accepted count)."""
+    import ctypes as C
+    from diffusionmcmctools_amd import _lib as L
+    lib = C.CDLL(os.path.join(ROOT, "diffusionmcmctools.jl_amd", "libdmt_callbench.so"))
+    out = np.empty((n, 3))
+    sec = C.c_double()
+    st = lib.dmt_callbench_loop(ens.handle, C.c_int32(lay), C.c_int64(0), C.c_int64(B),
+                                C.c_int64(iter0), C.c_int64(n), C.c_int32(1 if global_ else 0),
+                                out.ctypes.data_as(C.POINTER(C.c_double)), C.byref(sec))
+    if st != 0:
+        raise RuntimeError(f"dmt_callbench_loop failed at step {st}: {L.lib.dmt_last_error()}")
+    c_us = sec.value / n * 1e6
+    if not python:
+        return c_us, None, out
+    t0 = time.perf_counter()
+    for i in range(iter0 + n, iter0 + 2 * n):
+        ens.draw_proposal(lay, 0, B, salt=L.RNG_AUTO, want_success="lazy")
+        ens.accept_reject(lay, 0, B, i, salt=L.RNG_AUTO)
+        ens.fetch_ll(lay, 0, B, i, local=not global_)
+        ens.fetch_ll(lay, 0, B, 0, local=not global_)
+    py_us = (time.perf_counter() - t0) / n * 1e6
+    return c_us, py_us, out
+
+
+def rank_diagnostics(dist, world, k_ms, allgather_us, rccl_nranks):
+    """Per-rank timing spread of an N-GPU run (rank 0 prints it): the slowest and fastest rank's
+    draw-kernel time over the timed region, the RCCL all-gather's cost per fetch_ll call and
+    the communicator size, so that a scaling loss shows whether it is skew or the collective.
+    Gathered over the gloo control plane (also in --dry-run, with null values)."""
+    vals = [None] * world
+    dist.all_gather_object(vals, {"kernel_ms": k_ms, "allgather_us": allgather_us})
+    ks = [v["kernel_ms"] for v in vals if v["kernel_ms"] is not None]
+    ag = [v["allgather_us"] for v in vals if v["allgather_us"] is not None]
+    return {"ranks": world, "rccl_nranks": rccl_nranks,
+            "kernel_ms_max": max(ks) if ks else None, "kernel_ms_min": min(ks) if ks else None,
+            "kernel_skew": (max(ks) / min(ks) if ks and min(ks) > 0 else None),
+            "allgather_us_per_call_max": max(ag) if ag else None,
+            "per_rank": vals}
 
 
 def free_port():
@@ -230,6 +275,14 @@ def main(argv=None):
                     help="thread mapping of the Euler recursion (DESIGN.md §2)")
     ap.add_argument("--dry-run", action="store_true",
                     help="rendezvous the ranks and exit before any GPU work (launcher test)")
+    ap.add_argument("--repeats", type=int, default=5,
+                    help="extra timed runs of the same K steps after the timed region: their "
+                         "median and mean ms/step are reported beside the headline")
+    ap.add_argument("--api", default="run", choices=["run", "calls"],
+                    help="run: the K steps as one dmt_mcmc_run call (headline); calls: the "
+                         "caller's loop of separate draw / accept / fetch_ll C calls as value")
+    ap.add_argument("--calls-iters", type=int, default=200,
+                    help="iterations of the separate-call loop measured beside the headline")
     args = ap.parse_args(argv)
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -245,10 +298,13 @@ def main(argv=None):
         dist.init_process_group("gloo")  # control plane only; the data path is RCCL in libdmt
         assert dist.get_world_size() == world
     if args.dry_run:
+        diag = None
         if dist is not None:
             dist.barrier()
+            diag = rank_diagnostics(dist, world, None, None, None)
         if rank == 0:
-            print(json.dumps({"dry_run": True, "n_gpus": world, "ranks": world}))
+            print(json.dumps({"dry_run": True, "n_gpus": world, "ranks": world,
+                              "rank_diagnostics": diag}))
         if dist is not None:
             dist.destroy_process_group()
         return 0
@@ -258,7 +314,8 @@ def main(argv=None):
     from diffusionmcmctools_amd import workloads as W
 
     w = build_workload(args.config, rank)
-    w.meta["hist_len"] = args.warmup + args.steps + EXTRA_ITERS + CPU_MAX_ITERS
+    w.meta["hist_len"] = (args.warmup + args.steps * (2 + max(args.repeats, 0)) + EXTRA_ITERS +
+                          CPU_MAX_ITERS + 2 * args.calls_iters)
     mapping = {"auto": L.MAP_AUTO, "lane": L.MAP_LANE, "wave": L.MAP_WAVE}[args.mapping]
     ens = dmt.Ensemble(w.model.kind, w.d, w.m, w.n_points, precision=w.precision,
                        seed=ens_seed, device=local_rank, grid_shared=w.grid_shared,
@@ -293,7 +350,14 @@ def main(argv=None):
     ens.set_timing(True, kernels=[L.K_DRAW])
     barrier()
     t0 = time.perf_counter()
-    res = ens.mcmc_run(lay, 0, B, args.warmup + 1, args.steps)
+    if args.api == "calls":
+        # the caller's loop of separate C calls (deferred draw fused with its accept, fetch_ll
+        # from the fused tree), timed by the same clock as the headline; the untimed Python
+        # comparison loop of separate_calls runs after it
+        _, _, res = separate_calls(ens, lay, B, args.warmup + 1, args.steps, world > 1,
+                                   python=False)
+    else:
+        res = ens.mcmc_run(lay, 0, B, args.warmup + 1, args.steps)
     barrier()
     el = time.perf_counter() - t0
     n_acc = float(res[:, 2].sum())
@@ -314,11 +378,47 @@ def main(argv=None):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
 
+    # repeats of the same K steps (median and mean beside the headline)
+    rep_ms = []
+    for _ in range(max(args.repeats, 0)):
+        barrier()
+        t1 = time.perf_counter()
+        ens.mcmc_run(lay, 0, B, done + 1, args.steps)
+        barrier()
+        rep_ms.append((time.perf_counter() - t1) / args.steps * 1e3)
+        done += args.steps
+    # the caller's separate-call loop beside the fused headline
+    calls = None
+    if args.calls_iters > 0 and args.api == "run":
+        c_us, py_us, _ = separate_calls(ens, lay, B, done + 1, args.calls_iters, world > 1)
+        done += 2 * args.calls_iters
+        calls = {"loop": "draw_proposal_path!(be); accept_reject_proposal_path!(be, i); "
+                         "fetch_ll(be); fetch_ll°(be) as separate C-ABI calls",
+                 "us_per_iteration_c": c_us, "us_per_iteration_python_ctypes": py_us,
+                 "steps_per_s_c": w.steps_per_iter / (c_us * 1e-6),
+                 "iterations": args.calls_iters,
+                 "fused_launch_per_iteration": os.environ.get("DMT_DEFER", "1") != "0"}
+    diag = None
+    if dist is not None:
+        # all-gather cost per call: global (collective) minus local fetch_ll, 20 calls each
+        ens.sync()
+        t1 = time.perf_counter()
+        for _ in range(20):
+            ens.fetch_ll(lay, 0, B, 0, local=True)
+        loc = time.perf_counter() - t1
+        dist.barrier()
+        t1 = time.perf_counter()
+        for _ in range(20):
+            ens.fetch_ll(lay, 0, B, 0)
+        glob = time.perf_counter() - t1
+        diag = rank_diagnostics(dist, world, k_ms, (glob - loc) / 20 * 1e6, rccl_nranks)
+
     steps_total = w.steps_per_iter * args.steps * world
     value = steps_total / el
     # launches of the dominant kernel in the timed region: one per iteration, or (persistent,
     # dmt_mcmc_run) one per chunk of iterations (dmt_runtime.hip: ≤ 64 MiB of partials)
-    it_per_launch = min(args.steps, max(1, (64 << 20) // (24 * B))) if persist else 1
+    it_per_launch = (min(args.steps, max(1, (64 << 20) // (24 * B)))
+                     if persist and args.api == "run" else 1)
     launches = -(-args.steps // it_per_launch)
     k_avg_s = (k_ms / launches) * 1e-3          # average launch duration
     k_iter_s = (k_ms / max(args.steps, 1)) * 1e-3
@@ -398,6 +498,14 @@ def main(argv=None):
                          "limiter": (issue or {}).get("limiter"),
                          "issue": issue},
             "accept_kernel_avg_us": (a_ms / a_n) * 1e3 if a_n else None,
+            "api": args.api,
+            "repeats": {"n": len(rep_ms),
+                        "ms_per_step_median": float(np.median(rep_ms)) if rep_ms else None,
+                        "ms_per_step_mean": float(np.mean(rep_ms)) if rep_ms else None,
+                        "value_median": (w.steps_per_iter * world / (np.median(rep_ms) * 1e-3)
+                                         if rep_ms else None)},
+            "separate_calls": calls,
+            "rank_diagnostics": diag,
             "cpu_baseline": cpu,
         }
         if cpu is not None:

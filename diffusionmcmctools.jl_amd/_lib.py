@@ -51,7 +51,8 @@ SYMBOLS = [
     "dmt_debug_normals", "dmt_last_error", "dmt_version", "dmt_snapshot_reserve",
     "dmt_snapshot_take", "dmt_snapshot_download", "dmt_snapshot_write", "dmt_set_ll",
     "dmt_fetch_ll_local", "dmt_comm_size", "dmt_rng_counter", "dmt_set_rng_counter",
-    "dmt_set_run_snapshots", "dmt_mcmc_step_local", "dmt_mcmc_run_local",
+    "dmt_set_run_snapshots", "dmt_mcmc_step_local", "dmt_mcmc_run_local", "dmt_draw_success",
+    "dmt_rng_state", "dmt_set_rng_state",
 ]
 
 
@@ -140,6 +141,9 @@ _SIGS = {
     "dmt_comm_size": [_P, _pi32],
     "dmt_rng_counter": [_P, C.POINTER(_u64)],
     "dmt_set_rng_counter": [_P, _u64],
+    "dmt_draw_success": [_P, _i32, _i64, _i64, _pu8],
+    "dmt_rng_state": [_P, C.POINTER(_u64), C.POINTER(_u64), _pu8],
+    "dmt_set_rng_state": [_P, _u64, _u64, C.c_uint8],
 }
 for _name, _args in _SIGS.items():
     _f = getattr(lib, _name)

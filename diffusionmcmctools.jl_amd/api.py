@@ -430,7 +430,9 @@ class _BlockRange:
         per-block success flags.  Normals: the next ones of the device stream counter, or the
         stream keyed by an explicit ``iter``/``salt``, or ``Z`` (steps × m, whole ensemble)."""
         it, salt = _key(iter, salt)
-        return self._call("draw_proposal", Z=Z, iter=it, salt=salt, want_success=True)
+        # the flags are read only if used: the draw may wait for (and fuse with) the
+        # accept_reject that follows (include/dmt.h, deferred draws)
+        return self._call("draw_proposal", Z=Z, iter=it, salt=salt, want_success="lazy")
 
     # ---- accept / reject (biblock.jl:121-127)
     def accept_reject_proposal_path(self, mcmciter, E=None, salt=None):

@@ -44,6 +44,32 @@ __device__ __forceinline__ T tree_sum(T* v) {
   return v[0];
 }
 
+// Streamed path / table accesses of the lane kernels.  DMT_LANE_NT_LOADS / DMT_LANE_NT_STORES
+// (measurement variants): non-temporal hints for data a draw touches once per launch (C3 / C5
+// stream 4.7 GB per draw, ≫ L2 and MALL).  Cache hints only: the values are the same.
+#ifndef DMT_LANE_NT_LOADS
+#define DMT_LANE_NT_LOADS 0
+#endif
+#ifndef DMT_LANE_NT_STORES
+#define DMT_LANE_NT_STORES 0
+#endif
+template <class T>
+__device__ __forceinline__ T lane_ld(const T* p) {
+#if DMT_LANE_NT_LOADS
+  return __builtin_nontemporal_load(p);
+#else
+  return *p;
+#endif
+}
+template <class T>
+__device__ __forceinline__ void lane_st(T* p, T v) {
+#if DMT_LANE_NT_STORES
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+
 // One lane integrates one segment.  Main loop: full chunks of K steps, branch-free, with the
 // next chunk's inputs (t, H, F, accepted W, and Z in parity mode) loaded into registers
 // before the current chunk is integrated (prefetch distance K; no memory operation sits in
@@ -120,16 +146,16 @@ __device__ __forceinline__ bool run_segment(const Law<Mdl, T>& L, const T* __res
   T tcur = tb[0];
   if (cpx) {
 #pragma unroll
-    for (int p = 0; p < D; ++p) Xcdb[p * kLanes] = Xcsb[p * kLanes];
+    for (int p = 0; p < D; ++p) lane_st(&Xcdb[p * kLanes], lane_ld(&Xcsb[p * kLanes]));
   }
 #pragma unroll
-  for (int p = 0; p < D; ++p) Xdb[p * kLanes] = x[p];
+  for (int p = 0; p < D; ++p) lane_st(&Xdb[p * kLanes], x[p]);
   if (DRAW) {
 #pragma unroll
     for (int k = 0; k < M; ++k) {
-      const T w0 = READW ? Wsb[k * kLanes] : (T)0;
-      if (cpw) Wcdb[k * kLanes] = w0;
-      Wdb[k * kLanes] = rho * w0;
+      const T w0 = READW ? lane_ld(&Wsb[k * kLanes]) : (T)0;
+      if (cpw) lane_st(&Wcdb[k * kLanes], w0);
+      lane_st(&Wdb[k * kLanes], rho * w0);
     }
   }
   PSum<T> ps;
@@ -144,17 +170,17 @@ __device__ __forceinline__ bool run_segment(const Law<Mdl, T>& L, const T* __res
       const int64_t i = c0 + j;
       c.t[j] = tb[(i + 1) * tst];
 #pragma unroll
-      for (int e = 0; e < HP; ++e) c.H[j][e] = Hb[(i * HP + e) * hst];
+      for (int e = 0; e < HP; ++e) c.H[j][e] = lane_ld(&Hb[(i * HP + e) * hst]);
 #pragma unroll
-      for (int e = 0; e < D; ++e) c.F[j][e] = Fb[(i * D + e) * kLanes];
+      for (int e = 0; e < D; ++e) c.F[j][e] = lane_ld(&Fb[(i * D + e) * kLanes]);
 #pragma unroll
       for (int k = 0; k < M; ++k) {
-        c.W[j][k] = READW ? Wsb[((i + 1) * M + k) * kLanes] : (T)0;
+        c.W[j][k] = READW ? lane_ld(&Wsb[((i + 1) * M + k) * kLanes]) : (T)0;
         c.Z[j][k] = (PARITY && DRAW) ? (T)Zg[i * M + k] : (T)0;
       }
       if (cpx) {  // u.X of the points this chunk overwrites (read before they are)
 #pragma unroll
-        for (int e = 0; e < D; ++e) c.Xu[j][e] = Xcsb[((i + 1) * D + e) * kLanes];
+        for (int e = 0; e < D; ++e) c.Xu[j][e] = lane_ld(&Xcsb[((i + 1) * D + e) * kLanes]);
       }
     }
   };
@@ -165,7 +191,7 @@ __device__ __forceinline__ bool run_segment(const Law<Mdl, T>& L, const T* __res
     T dW[M];
     if (cpx) {
 #pragma unroll
-      for (int e = 0; e < D; ++e) Xcdb[((int64_t)(i + 1) * D + e) * kLanes] = Xui[e];
+      for (int e = 0; e < D; ++e) lane_st(&Xcdb[((int64_t)(i + 1) * D + e) * kLanes], Xui[e]);
     }
     if (!DRAW) {
 #pragma unroll
@@ -174,9 +200,9 @@ __device__ __forceinline__ bool run_segment(const Law<Mdl, T>& L, const T* __res
       const T sdt = sqrt(dt);
 #pragma unroll
       for (int k = 0; k < M; ++k) {
-        if (cpw) Wcdb[((int64_t)(i + 1) * M + k) * kLanes] = Wi[k];
+        if (cpw) lane_st(&Wcdb[((int64_t)(i + 1) * M + k) * kLanes], Wi[k]);
         dW[k] = dfma(rho, Wi[k], srho * (sdt * Zi[k]));
-        Wdb[((int64_t)(i + 1) * M + k) * kLanes] = dW[k];
+        lane_st(&Wdb[((int64_t)(i + 1) * M + k) * kLanes], dW[k]);
       }
     }
     T r[D], b[D], sdW[D], Mg[D * D], cg[D];
@@ -196,7 +222,7 @@ __device__ __forceinline__ bool run_segment(const Law<Mdl, T>& L, const T* __res
     }
     euler_step<Mdl, T>(Mg, cg, b, dt, sdW, x);
 #pragma unroll
-    for (int p = 0; p < D; ++p) Xdb[((int64_t)(i + 1) * D + p) * kLanes] = x[p];
+    for (int p = 0; p < D; ++p) lane_st(&Xdb[((int64_t)(i + 1) * D + p) * kLanes], x[p]);
     tcur = tn;
     // recompute_path!(…; skip): the segment's last ll_skip steps add no term
     return (MODE == MODE_RECOMPUTE && i >= nst - ll_skip) ? (T)0 : G * dt;
@@ -250,14 +276,14 @@ __device__ __forceinline__ bool run_segment(const Law<Mdl, T>& L, const T* __res
     const int64_t q = i;
     T Hi[HP], Fi[D], Wi[M], Zi[M], Xui[D];
 #pragma unroll
-    for (int e = 0; e < D; ++e) Xui[e] = cpx ? Xcsb[((q + 1) * D + e) * kLanes] : (T)0;
+    for (int e = 0; e < D; ++e) Xui[e] = cpx ? lane_ld(&Xcsb[((q + 1) * D + e) * kLanes]) : (T)0;
 #pragma unroll
-    for (int e = 0; e < HP; ++e) Hi[e] = Hb[(q * HP + e) * hst];
+    for (int e = 0; e < HP; ++e) Hi[e] = lane_ld(&Hb[(q * HP + e) * hst]);
 #pragma unroll
-    for (int e = 0; e < D; ++e) Fi[e] = Fb[(q * D + e) * kLanes];
+    for (int e = 0; e < D; ++e) Fi[e] = lane_ld(&Fb[(q * D + e) * kLanes]);
 #pragma unroll
     for (int k = 0; k < M; ++k) {
-      Wi[k] = READW ? Wsb[((q + 1) * M + k) * kLanes] : (T)0;
+      Wi[k] = READW ? lane_ld(&Wsb[((q + 1) * M + k) * kLanes]) : (T)0;
       Zi[k] = DRAW ? (PARITY ? (T)Zg[q * M + k] : ns.get((uint32_t)(i * M + k))) : (T)0;
     }
     ps.add(step(i, tb[(q + 1) * tst], Hi, Fi, Wi, Zi, Xui));
@@ -1969,6 +1995,7 @@ __device__ __forceinline__ void resident_block(const BlockArgs<T>& a, const Acce
     }
     // ---- MH decision (k_accept's order), selectors, histories, partials
     llp = sok ? (double)(llobs + seg_acc) : -INFINITY;
+    if (lane == 0 && a.success) a.success[blk] = sok ? 1 : 0;  // the run's last draw's flag
     const bool acc = E > -(llp - ll);
     if (acc) {
       sel.mx ^= all;
@@ -2306,6 +2333,7 @@ __device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, cons
 #pragma unroll
     for (int p = 0; p < D; ++p) sok = sok && isfinite(xe[p]);
     llp = sok ? (double)(llobs + seg_acc) : -INFINITY;
+    if (lane == 0 && valid && a.success) a.success[blk] = sok ? 1 : 0;  // last draw's flag
     const bool acc = valid && E > -(llp - ll);
     if (acc) {
       sel.mx ^= all;

@@ -98,6 +98,24 @@ struct dmt_ens {
   uint64_t rng_ctr = 0, rng_last_draw = 0;
   bool rng_pending = false;
   bool spin_wait = true;  // wait for the stream by polling it (DMT_SPIN_WAIT=0: block in HIP)
+  // Deferred draws (include/dmt.h): a device-RNG dmt_draw_proposal over a range the
+  // register-resident kernel serves is not launched at once; the dmt_accept_reject that follows
+  // on the same range runs draw + decision + fetch_ll tree as ONE launch of that kernel, whose
+  // fetch_ll values (pinned h_run[0..2]) the next dmt_fetch_ll of the range returns without a
+  // launch.  Any other call launches the deferred draw first (flush_deferred), so every call
+  // sees exactly the state the launch-per-call order gives.  DMT_DEFER=0: off.
+  struct {
+    bool on = false;
+    int32_t layout = 0;
+    int64_t b0 = 0, b1 = 0;
+    uint32_t iter = 0, salt = 0;
+  } def;
+  struct {
+    bool on = false;
+    int32_t layout = 0;
+    int64_t b0 = 0, b1 = 0, mcmciter = 0;
+  } fused;
+  bool defer = true;
   int grid_shared = 0;
   // path snapshots (dmt_snapshot_*): [slots][P][C] doubles in reference layout per kind
   int snap_mask = 0;
@@ -325,9 +343,16 @@ dmt_status check_h(dmt_ens* h) {
 // scheduler for short calls.
 hipError_t stream_wait(dmt_ens* h) {
   if (!h->spin_wait) return hipStreamSynchronize(h->stream);
+  // poll for at most kSpinUs, then block in HIP: short waits (the hot path's per-call results)
+  // stay off the scheduler, long ones (filters, snapshot writes, destroy) do not burn a core
+  constexpr double kSpinUs = 200.0;
+  const auto t0 = std::chrono::steady_clock::now();
   for (;;) {
     const hipError_t e = hipStreamQuery(h->stream);
     if (e != hipErrorNotReady) return e;
+    if (std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() >
+        kSpinUs)
+      return hipStreamSynchronize(h->stream);
   }
 }
 
@@ -499,6 +524,33 @@ dmt_status run_block_kernel(dmt_ens* h, const Layout* L, int mode, int kind_time
   }
   if (e != hipSuccess) return fail(DMT_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(e));
   return DMT_OK;
+}
+
+// Launch a deferred draw (if any): the kernel launch dmt_draw_proposal would have made, with
+// the stream key it took.  The fused results stay valid (the draw is ordered after them).
+dmt_status flush_deferred(dmt_ens* h) {
+  if (!h->def.on) return DMT_OK;
+  h->def.on = false;
+  Layout* L;
+  DMT_TRY(get_layout(h, h->def.layout, &L));
+  return run_block_kernel(h, L, MODE_PCN, DMT_K_DRAW, h->def.b0, h->def.b1, 0, 0, 1, 0, 1,
+                          nullptr, h->def.iter, h->def.salt, L->d_llp, L->d_success, false);
+}
+
+// Entry of every call that reads or changes state: the deferred draw is launched first and the
+// fused fetch_ll values are dropped.
+dmt_status enter(dmt_ens* h) {
+  DMT_TRY(check_h(h));
+  DMT_TRY(flush_deferred(h));
+  h->fused.on = false;
+  return DMT_OK;
+}
+
+// The register-resident MCMC kernel serves the range: single-segment blocks of <= 512 steps of
+// a linear drift with d <= 2 (dmt_mcmc_run's own condition, layout-wide)
+bool resident_range(const dmt_ens* h, const Layout* L) {
+  return h->persist && h->resident && h->key.model == DMT_MODEL_OU && h->key.d <= 2 &&
+         L->single_seg && L->max_steps <= kResidentMaxSteps;
 }
 
 dmt_status upload_Z(dmt_ens* h, const double* Z, const double** dZ) {
@@ -714,6 +766,7 @@ dmt_status dmt_create(dmt_ens** out, const dmt_model* model, const dmt_structure
   if (const char* e = std::getenv("DMT_DISPATCH_EVENTS")) h->dispatch_events = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("DMT_LANE_SPLIT")) h->lane_split = std::atoi(e);
   if (const char* e = std::getenv("DMT_LANE_PAIR")) h->lane_pair = std::atoi(e);
+  if (const char* e = std::getenv("DMT_DEFER")) h->defer = std::atoi(e) != 0;
   if (const char* e = std::getenv("DMT_REPAIR_DIV")) h->repair_div = std::max(1, std::atoi(e));
   if (const char* e = std::getenv("DMT_SCAN_RESIDENT")) h->scan_resident = std::strcmp(e, "0") != 0;
   {
@@ -806,7 +859,7 @@ dmt_status dmt_destroy(dmt_ens* h) {
 }
 
 dmt_status dmt_upload_grid(dmt_ens* h, const double* t) {
-  DMT_TRY(check_h(h));
+  DMT_TRY(enter(h));
   if (!t) return fail(DMT_ERR_INVALID, "null grid");
   if (h->grid_shared) {
     if (!h->d_t) {
@@ -847,7 +900,7 @@ extern "C" {
 
 dmt_status dmt_upload_law(dmt_ens* h, int32_t unit, int32_t kind, const double* H,
                           int32_t H_shared, const double* F, const double* laws) {
-  DMT_TRY(check_h(h));
+  DMT_TRY(enter(h));
   if ((unit != DMT_U && unit != DMT_UPROP) || (kind != DMT_LAW_PP && kind != DMT_LAW_PPB))
     return fail(DMT_ERR_INVALID, "bad unit/kind");
   uint8_t* sel = h->d_sel[2 + kind];
@@ -930,7 +983,7 @@ dmt_status dmt_upload_law(dmt_ens* h, int32_t unit, int32_t kind, const double* 
 }
 
 dmt_status dmt_set_paths(dmt_ens* h, int32_t unit, const double* X, const double* W) {
-  DMT_TRY(check_h(h));
+  DMT_TRY(enter(h));
   if (unit != DMT_U && unit != DMT_UPROP) return fail(DMT_ERR_INVALID, "bad unit");
   const double* src[2] = {X, W};
   const int C[2] = {h->d, h->m};
@@ -949,7 +1002,7 @@ dmt_status dmt_set_paths(dmt_ens* h, int32_t unit, const double* X, const double
 }
 
 dmt_status dmt_download_paths(dmt_ens* h, int32_t unit, int32_t what, double* out) {
-  DMT_TRY(check_h(h));
+  DMT_TRY(enter(h));
   if ((unit != DMT_U && unit != DMT_UPROP) || what < 0 || what > 2 || !out)
     return fail(DMT_ERR_INVALID, "bad unit/what/out");
   const int C = what == 0 ? h->d : h->m;
@@ -971,7 +1024,7 @@ dmt_status dmt_download_paths(dmt_ens* h, int32_t unit, int32_t what, double* ou
 
 dmt_status dmt_download_law(dmt_ens* h, int32_t unit, int32_t kind, double* H, double* F,
                             double* laws) {
-  DMT_TRY(check_h(h));
+  DMT_TRY(enter(h));
   if ((unit != DMT_U && unit != DMT_UPROP) || (kind != DMT_LAW_PP && kind != DMT_LAW_PPB))
     return fail(DMT_ERR_INVALID, "bad unit/kind");
   if (!h->have_law[0][kind] && !h->have_law[1][kind]) return fail(DMT_ERR_STATE, "law not uploaded");
@@ -1018,7 +1071,7 @@ dmt_status dmt_download_law(dmt_ens* h, int32_t unit, int32_t kind, double* H, d
 dmt_status dmt_create_layout(dmt_ens* h, const int32_t* n_blocks, const int32_t* seg_first,
                              const int32_t* seg_last, const uint8_t* last, const double* rho,
                              int64_t hist_len, int32_t* layout_id) {
-  DMT_TRY(check_h(h));
+  DMT_TRY(enter(h));
   if (!n_blocks || !seg_first || !seg_last || !last || !rho || !layout_id)
     return fail(DMT_ERR_INVALID, "null argument");
   DMT_TRY(build_layout(h, n_blocks, seg_first, seg_last, last, rho, hist_len, layout_id));
@@ -1027,7 +1080,7 @@ dmt_status dmt_create_layout(dmt_ens* h, const int32_t* n_blocks, const int32_t*
 }
 
 dmt_status dmt_layout_size(dmt_ens* h, int32_t layout, int64_t* n) {
-  DMT_TRY(check_h(h));
+  DMT_TRY(enter(h));
   Layout* L;
   DMT_TRY(get_layout(h, layout, &L));
   *n = L->nblocks;
@@ -1036,7 +1089,7 @@ dmt_status dmt_layout_size(dmt_ens* h, int32_t layout, int64_t* n) {
 
 dmt_status dmt_draw_unit(dmt_ens* h, int32_t unit, int64_t r0, int64_t r1, const double* Z,
                          int64_t iter, uint32_t salt, double* ll_out, uint8_t* success_out) {
-  DMT_TRY(check_h(h));
+  DMT_TRY(enter(h));
   if (unit != DMT_U && unit != DMT_UPROP) return fail(DMT_ERR_INVALID, "bad unit");
   Layout* L;
   DMT_TRY(get_layout(h, 0, &L));
@@ -1056,18 +1109,29 @@ dmt_status dmt_draw_unit(dmt_ens* h, int32_t unit, int64_t r0, int64_t r1, const
 
 dmt_status dmt_draw_proposal(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, const double* Z,
                              int64_t iter, uint32_t salt, uint8_t* success_out) {
-  DMT_TRY(check_h(h));
+  DMT_TRY(enter(h));
   Layout* L;
   DMT_TRY(get_layout(h, layout, &L));
   DMT_TRY(check_range(L, b0, b1));
   DMT_TRY(law_ready(h, 0, L, b0, b1));
   RngKey key;
   DMT_TRY(draw_key(h, iter, salt, true, &key));
+  if (!Z && !success_out && h->defer && resident_range(h, L)) {
+    // deferred: launched with the accept_reject that follows (one fused launch), or by the
+    // next call that needs it (flush_deferred)
+    h->def.on = true;
+    h->def.layout = layout;
+    h->def.b0 = b0;
+    h->def.b1 = b1;
+    h->def.iter = key.iter;
+    h->def.salt = key.salt;
+    return DMT_OK;
+  }
   const double* dZ;
   DMT_TRY(upload_Z(h, Z, &dZ));
   // law: accepted u.PP (flip 0); start from u.XX; write u°.XX/u°.WW; read u.WW
   DMT_TRY(run_block_kernel(h, L, MODE_PCN, DMT_K_DRAW, b0, b1, 0, 0, 1, 0, 1, dZ, key.iter,
-                           key.salt, L->d_llp, success_out ? L->d_success : nullptr, false));
+                           key.salt, L->d_llp, L->d_success, false));
   if (success_out) {
     HIP_OK(hipMemcpyAsync(success_out, L->d_success + b0, b1 - b0, hipMemcpyDeviceToHost, h->stream));
     HIP_OK(stream_wait(h));
@@ -1155,7 +1219,7 @@ static dmt_status finish_reduction(dmt_ens* h, double* v, bool global = true) {
 static dmt_status mcmc_step_impl(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
                                  int64_t mcmciter, uint32_t salt, double* ll, double* ll_prop,
                                  int64_t* n_acc, bool global) {
-  DMT_TRY(check_h(h));
+  DMT_TRY(enter(h));
   Layout* L;
   DMT_TRY(get_layout(h, layout, &L));
   DMT_TRY(check_range(L, b0, b1));
@@ -1199,7 +1263,7 @@ static int64_t grown_cap(int64_t need, int64_t cap, int64_t floor_) {
 }
 
 dmt_status dmt_set_run_snapshots(dmt_ens* h, int64_t every, int64_t slot0) {
-  DMT_TRY(check_h(h));
+  DMT_TRY(enter(h));
   if (every < 0) return fail(DMT_ERR_INVALID, "every must be >= 0");
   if (every > 0 && !h->snap_mask) return fail(DMT_ERR_STATE, "no snapshot slots (dmt_snapshot_reserve)");
   if (every > 0 && (slot0 < 0 || slot0 >= h->snap_slots)) return fail(DMT_ERR_INVALID, "slot out of range");
@@ -1214,11 +1278,15 @@ static double hp_now() {
 }
 static const bool g_host_prof = std::getenv("DMT_HOST_PROFILE") != nullptr;
 static double g_hp[6];
+static dmt_status mcmc_run_launch(dmt_ens* h, Layout* L, int64_t b0, int64_t b1, int64_t iter0,
+                                  int64_t n_iter, uint32_t salt, int64_t key_delta, bool multi);
+static dmt_status mcmc_run_collect(dmt_ens* h, int64_t n_iter, double* out, bool multi);
+
 static dmt_status mcmc_run_impl(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
                                 int64_t iter0, int64_t n_iter, uint32_t salt, double* out,
                                 bool global) {
   if (g_host_prof) g_hp[0] = hp_now();
-  DMT_TRY(check_h(h));
+  DMT_TRY(enter(h));
   Layout* L;
   DMT_TRY(get_layout(h, layout, &L));
   DMT_TRY(check_range(L, b0, b1));
@@ -1266,6 +1334,15 @@ static dmt_status mcmc_run_impl(dmt_ens* h, int32_t layout, int64_t b0, int64_t 
   // BlockEnsemble level (global): the partials of every rank; BiBlock / BlockCollection
   // level: this rank's blocks only, no collective (src/block_collection.jl:144,156)
   const bool multi = h->comm != nullptr && global;
+  DMT_TRY(mcmc_run_launch(h, L, b0, b1, iter0, n_iter, salt, key_delta, multi));
+  return mcmc_run_collect(h, n_iter, out, multi);
+}
+
+// Queue n_iter MCMC iterations (iteration it keyed by it + key_delta, salt) on the stream; the
+// per-iteration (fetch_ll, fetch_ll°, accepted count) go to pinned h_run (one rank) or d_run
+// (multi: for the all-gather, which is queued too).  No host synchronisation.
+static dmt_status mcmc_run_launch(dmt_ens* h, Layout* L, int64_t b0, int64_t b1, int64_t iter0,
+                                  int64_t n_iter, uint32_t salt, int64_t key_delta, bool multi) {
   if (n_iter > h->run_cap) {
     if (h->d_run) { (void)hipFree(h->d_run); h->bytes -= h->run_cap * 24; h->d_run = nullptr; }
     if (h->h_run) { (void)hipHostFree(h->h_run); h->h_run = nullptr; h->h_run_dev = nullptr; }
@@ -1277,7 +1354,9 @@ static dmt_status mcmc_run_impl(dmt_ens* h, int32_t layout, int64_t b0, int64_t 
     const int64_t cap = grown_cap(n_iter, h->run_cap, 4096);
     h->run_cap = 0;
     DMT_TRY(ens_alloc(h, &h->d_run, 3 * cap));
-    HIP_OK(hipHostMalloc((void**)&h->h_run, 3 * cap * sizeof(double), hipHostMallocDefault));
+    // coherent and mapped: the kernels write the per-iteration results straight into it
+    HIP_OK(hipHostMalloc((void**)&h->h_run, 3 * cap * sizeof(double),
+                         hipHostMallocMapped | hipHostMallocCoherent));
     void* dp = nullptr;
     HIP_OK(hipHostGetDevicePointer(&dp, h->h_run, 0));
     h->h_run_dev = static_cast<double*>(dp);
@@ -1325,6 +1404,7 @@ static dmt_status mcmc_run_impl(dmt_ens* h, int32_t layout, int64_t b0, int64_t 
         TimedScope ts(h, DMT_K_DRAW, true, n);
         auto fill = [&](auto& a) {
           fill_common(h, L, a);
+          a.success = L->d_success;  // the last iteration's draw flags (dmt_draw_success)
           a.b0 = b0;
           a.b1 = b1;
           a.tile0 = 0;
@@ -1359,7 +1439,7 @@ static dmt_status mcmc_run_impl(dmt_ens* h, int32_t layout, int64_t b0, int64_t 
       const int64_t it = iter0 + i;
       const RngKey key{(uint32_t)(it + key_delta), salt};
       DMT_TRY(run_block_kernel(h, L, MODE_PCN, DMT_K_DRAW, b0, b1, 0, 0, 1, 0, 1, nullptr,
-                               key.iter, key.salt, L->d_llp, nullptr, false));
+                               key.iter, key.salt, L->d_llp, L->d_success, false));
       {
         TimedScope ts(h, DMT_K_ACCEPT);
         HIP_OK(launch_accept_reduce(accept_args(h, L, b0, b1, nullptr, it, key, nullptr),
@@ -1372,6 +1452,11 @@ static dmt_status mcmc_run_impl(dmt_ens* h, int32_t layout, int64_t b0, int64_t 
   if (multi && ncclAllGather(h->d_run, h->d_run_gather, 3 * n_iter, ncclDouble, h->comm,
                              h->stream) != ncclSuccess)
     return fail(DMT_ERR_COMM, "ncclAllGather failed");
+  return DMT_OK;
+}
+
+// Wait for a queued run and return its per-iteration results (rank-order tree over ranks).
+static dmt_status mcmc_run_collect(dmt_ens* h, int64_t n_iter, double* out, bool multi) {
   if (!out) {
     HIP_OK(stream_wait(h));
     return DMT_OK;
@@ -1423,8 +1508,27 @@ dmt_status dmt_accept_reject(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
   DMT_TRY(check_range(L, b0, b1));
   if (L->hist_len > 0 && (mcmciter < 1 || mcmciter > L->hist_len))
     return fail(DMT_ERR_INVALID, "mcmciter outside 1:ll_hist_len");
+  const bool fuse = h->def.on && h->def.layout == layout && h->def.b0 == b0 &&
+                    h->def.b1 == b1 && !E && !acc_out && mcmciter >= 1;
+  h->fused.on = false;
+  if (!fuse) DMT_TRY(flush_deferred(h));
   RngKey key;
   DMT_TRY(accept_key(h, mcmciter, salt, &key));
+  if (fuse && key.iter == h->def.iter && key.salt == h->def.salt) {
+    // the deferred draw and this decision with ONE stream key: one launch of the resident MCMC
+    // kernel (draw, decision, histories, fetch_ll tree) — the launch dmt_mcmc_step makes
+    h->def.on = false;
+    DMT_TRY(ensure_red_work(h, b1 - b0));
+    DMT_TRY(mcmc_run_launch(h, L, b0, b1, mcmciter, 1, key.salt,
+                            (int64_t)key.iter - mcmciter, false));
+    h->fused.on = true;
+    h->fused.layout = layout;
+    h->fused.b0 = b0;
+    h->fused.b1 = b1;
+    h->fused.mcmciter = mcmciter;
+    return DMT_OK;
+  }
+  DMT_TRY(flush_deferred(h));  // a different key: the draw's own launch first
   const double* dE = nullptr;
   if (E) {
     DMT_TRY(ensure_Z(h, std::max<int64_t>(b1 - b0, 1)));
@@ -1446,7 +1550,7 @@ dmt_status dmt_accept_reject(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
 }
 
 dmt_status dmt_loglikhd(dmt_ens* h, int32_t layout, int32_t unit, int64_t b0, int64_t b1) {
-  DMT_TRY(check_h(h));
+  DMT_TRY(enter(h));
   if (unit != DMT_U && unit != DMT_UPROP) return fail(DMT_ERR_INVALID, "bad unit");
   Layout* L;
   DMT_TRY(get_layout(h, layout, &L));
@@ -1459,7 +1563,7 @@ dmt_status dmt_loglikhd(dmt_ens* h, int32_t layout, int32_t unit, int64_t b0, in
 
 dmt_status dmt_recompute_path(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int32_t skip,
                               uint8_t* success_out) {
-  DMT_TRY(check_h(h));
+  DMT_TRY(enter(h));
   if (skip < 0) return fail(DMT_ERR_INVALID, "skip must be >= 0");
   Layout* L;
   DMT_TRY(get_layout(h, layout, &L));
@@ -1478,7 +1582,7 @@ dmt_status dmt_recompute_path(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1
 }
 
 dmt_status dmt_find_W_for_X(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1) {
-  DMT_TRY(check_h(h));
+  DMT_TRY(enter(h));
   Layout* L;
   DMT_TRY(get_layout(h, layout, &L));
   DMT_TRY(check_range(L, b0, b1));
@@ -1491,7 +1595,7 @@ dmt_status dmt_find_W_for_X(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1) 
 
 dmt_status dmt_upload_obs(dmt_ens* h, const double* Hobs, const double* Fobs, const double* cobs,
                           double artificial_noise) {
-  DMT_TRY(check_h(h));
+  DMT_TRY(enter(h));
   if (!Hobs || !Fobs || !cobs || !(artificial_noise > 0.0))
     return fail(DMT_ERR_INVALID, "bad arguments to dmt_upload_obs");
   if (!h->d_obsH) {
@@ -1520,7 +1624,7 @@ dmt_status dmt_upload_obs(dmt_ens* h, const double* Hobs, const double* Fobs, co
 }
 
 dmt_status dmt_set_obs(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1) {
-  DMT_TRY(check_h(h));
+  DMT_TRY(enter(h));
   if (!h->d_obsv) return fail(DMT_ERR_STATE, "dmt_upload_obs first");
   Layout* L;
   DMT_TRY(get_layout(h, layout, &L));
@@ -1658,7 +1762,7 @@ extern "C" {
 
 dmt_status dmt_recompute_guiding_term(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
                                       int32_t unit) {
-  DMT_TRY(check_h(h));
+  DMT_TRY(enter(h));
   if (unit != DMT_U && unit != DMT_UPROP) return fail(DMT_ERR_INVALID, "bad unit");
   Layout* L;
   DMT_TRY(get_layout(h, layout, &L));
@@ -1669,7 +1773,7 @@ dmt_status dmt_recompute_guiding_term(dmt_ens* h, int32_t layout, int64_t b0, in
 dmt_status dmt_set_proposal_law(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int32_t n,
                                 const int32_t* idx, const double* val, int32_t skip,
                                 uint8_t* success_out, uint8_t* critical_out) {
-  DMT_TRY(check_h(h));
+  DMT_TRY(enter(h));
   Layout* L;
   DMT_TRY(get_layout(h, layout, &L));
   DMT_TRY(check_range(L, b0, b1));
@@ -1714,7 +1818,7 @@ dmt_status dmt_set_proposal_law(dmt_ens* h, int32_t layout, int64_t b0, int64_t 
 }
 
 dmt_status dmt_swap(dmt_ens* h, int32_t layout, int32_t what, int64_t b0, int64_t b1) {
-  DMT_TRY(check_h(h));
+  DMT_TRY(enter(h));
   Layout* L;
   DMT_TRY(get_layout(h, layout, &L));
   DMT_TRY(check_range(L, b0, b1));
@@ -1739,7 +1843,7 @@ dmt_status dmt_swap(dmt_ens* h, int32_t layout, int32_t what, int64_t b0, int64_
 }
 
 dmt_status dmt_save_ll(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int64_t mcmciter) {
-  DMT_TRY(check_h(h));
+  DMT_TRY(enter(h));
   Layout* L;
   DMT_TRY(get_layout(h, layout, &L));
   DMT_TRY(check_range(L, b0, b1));
@@ -1750,7 +1854,7 @@ dmt_status dmt_save_ll(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int64
 
 dmt_status dmt_set_accepted(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int64_t mcmciter,
                             const uint8_t* v) {
-  DMT_TRY(check_h(h));
+  DMT_TRY(enter(h));
   Layout* L;
   DMT_TRY(get_layout(h, layout, &L));
   DMT_TRY(check_range(L, b0, b1));
@@ -1763,7 +1867,7 @@ dmt_status dmt_set_accepted(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, 
 
 dmt_status dmt_set_ll(dmt_ens* h, int32_t layout, int32_t unit, int64_t b0, int64_t b1,
                       int64_t mcmciter, const double* v) {
-  DMT_TRY(check_h(h));
+  DMT_TRY(enter(h));
   Layout* L;
   DMT_TRY(get_layout(h, layout, &L));
   DMT_TRY(check_range(L, b0, b1));
@@ -1793,7 +1897,7 @@ static dmt_status block_state_ptr(Layout* L, int32_t what, void** p, size_t* esz
 
 dmt_status dmt_get_block_state(dmt_ens* h, int32_t layout, int32_t what, int64_t b0, int64_t b1,
                                void* out) {
-  DMT_TRY(check_h(h));
+  DMT_TRY(enter(h));
   Layout* L;
   DMT_TRY(get_layout(h, layout, &L));
   DMT_TRY(check_range(L, b0, b1));
@@ -1813,7 +1917,7 @@ dmt_status dmt_get_block_state(dmt_ens* h, int32_t layout, int32_t what, int64_t
 
 dmt_status dmt_set_block_state(dmt_ens* h, int32_t layout, int32_t what, int64_t b0, int64_t b1,
                                const void* in) {
-  DMT_TRY(check_h(h));
+  DMT_TRY(enter(h));
   Layout* L;
   DMT_TRY(get_layout(h, layout, &L));
   DMT_TRY(check_range(L, b0, b1));
@@ -1838,6 +1942,17 @@ static dmt_status fetch_ll_impl(dmt_ens* h, int32_t layout, int64_t b0, int64_t 
   Layout* L;
   DMT_TRY(get_layout(h, layout, &L));
   DMT_TRY(check_range(L, b0, b1));
+  if (h->fused.on && h->fused.layout == layout && h->fused.b0 == b0 && h->fused.b1 == b1 &&
+      (mcmciter == 0 || mcmciter == h->fused.mcmciter) && !(h->comm && global)) {
+    // the fused draw + accept of this range formed this very tree in its launch (same order,
+    // same values): wait for it, no launch
+    HIP_OK(stream_wait(h));
+    if (ll) *ll = h->h_run[0];
+    if (ll_prop) *ll_prop = h->h_run[1];
+    if (n_acc) *n_acc = mcmciter > 0 ? (int64_t)h->h_run[2] : 0;
+    return DMT_OK;
+  }
+  DMT_TRY(enter(h));
   const uint8_t* acc = nullptr;
   if (mcmciter > 0) {
     if (mcmciter > L->hist_len) return fail(DMT_ERR_INVALID, "mcmciter outside 1:ll_hist_len");
@@ -1854,6 +1969,19 @@ static dmt_status fetch_ll_impl(dmt_ens* h, int32_t layout, int64_t b0, int64_t 
   if (ll) *ll = v[0];
   if (ll_prop) *ll_prop = v[1];
   if (n_acc) *n_acc = (int64_t)v[2];
+  return DMT_OK;
+}
+
+dmt_status dmt_draw_success(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
+                            uint8_t* success_out) {
+  DMT_TRY(check_h(h));
+  Layout* L;
+  DMT_TRY(get_layout(h, layout, &L));
+  DMT_TRY(check_range(L, b0, b1));
+  if (!success_out) return fail(DMT_ERR_INVALID, "null output");
+  DMT_TRY(flush_deferred(h));  // reading flags changes nothing: fused results stay valid
+  HIP_OK(hipMemcpyAsync(success_out, L->d_success + b0, b1 - b0, hipMemcpyDeviceToHost, h->stream));
+  HIP_OK(stream_wait(h));
   return DMT_OK;
 }
 
@@ -1877,6 +2005,22 @@ dmt_status dmt_set_rng_counter(dmt_ens* h, uint64_t next) {
   if (!h) return fail(DMT_ERR_INVALID, "null handle");
   h->rng_ctr = next;
   h->rng_pending = false;
+  return DMT_OK;
+}
+
+dmt_status dmt_rng_state(dmt_ens* h, uint64_t* next, uint64_t* last_draw, uint8_t* pending) {
+  if (!h || !next || !last_draw || !pending) return fail(DMT_ERR_INVALID, "null argument");
+  *next = h->rng_ctr;
+  *last_draw = h->rng_last_draw;
+  *pending = h->rng_pending ? 1 : 0;
+  return DMT_OK;
+}
+
+dmt_status dmt_set_rng_state(dmt_ens* h, uint64_t next, uint64_t last_draw, uint8_t pending) {
+  if (!h) return fail(DMT_ERR_INVALID, "null handle");
+  h->rng_ctr = next;
+  h->rng_last_draw = last_draw;
+  h->rng_pending = pending != 0;
   return DMT_OK;
 }
 
@@ -1933,7 +2077,7 @@ dmt_status dmt_comm_unique_id(uint8_t* id_out) {
 }
 
 dmt_status dmt_comm_init(dmt_ens* h, int32_t nranks, int32_t rank, const uint8_t* id) {
-  DMT_TRY(check_h(h));
+  DMT_TRY(enter(h));
   if (nranks < 1 || rank < 0 || rank >= nranks || !id) return fail(DMT_ERR_INVALID, "bad comm args");
   if (h->comm) {
     (void)ncclCommDestroy(h->comm);
@@ -1952,7 +2096,7 @@ dmt_status dmt_comm_init(dmt_ens* h, int32_t nranks, int32_t rank, const uint8_t
 }
 
 dmt_status dmt_comm_size(dmt_ens* h, int32_t* nranks) {
-  DMT_TRY(check_h(h));
+  DMT_TRY(enter(h));
   if (!nranks) return fail(DMT_ERR_INVALID, "null argument");
   if (!h->comm) {
     *nranks = 1;
@@ -1965,7 +2109,7 @@ dmt_status dmt_comm_size(dmt_ens* h, int32_t* nranks) {
 }
 
 dmt_status dmt_set_shard(dmt_ens* h, int64_t seg_base) {
-  DMT_TRY(check_h(h));
+  DMT_TRY(enter(h));
   if (seg_base < 0 || seg_base + h->G > (int64_t)UINT32_MAX)
     return fail(DMT_ERR_INVALID, "seg_base out of range");
   h->seg_base = (uint32_t)seg_base;
@@ -1973,13 +2117,13 @@ dmt_status dmt_set_shard(dmt_ens* h, int64_t seg_base) {
 }
 
 dmt_status dmt_sync(dmt_ens* h) {
-  DMT_TRY(check_h(h));
+  DMT_TRY(enter(h));
   HIP_OK(stream_wait(h));
   return DMT_OK;
 }
 
 dmt_status dmt_set_timing(dmt_ens* h, int32_t on) {
-  DMT_TRY(check_h(h));
+  DMT_TRY(enter(h));
   HIP_OK(stream_wait(h));
   drain_timing(h);
   for (int k = 0; k < DMT_K_COUNT; ++k) { h->t_ms[k] = 0; h->t_cnt[k] = 0; }
@@ -1995,7 +2139,7 @@ dmt_status dmt_set_timing(dmt_ens* h, int32_t on) {
 }
 
 dmt_status dmt_get_timing(dmt_ens* h, int32_t kernel, double* ms, int64_t* count) {
-  DMT_TRY(check_h(h));
+  DMT_TRY(enter(h));
   if (kernel < 0 || kernel >= DMT_K_COUNT) return fail(DMT_ERR_INVALID, "bad kernel id");
   HIP_OK(stream_wait(h));
   drain_timing(h);
@@ -2050,7 +2194,7 @@ dmt_status dmt_debug_normals(int32_t device, uint64_t seed, const uint32_t* ctr,
 // stream without a host round trip, and are written to disk in one pass when wanted.
 
 dmt_status dmt_snapshot_reserve(dmt_ens* h, int32_t what_mask, int64_t n_slots) {
-  DMT_TRY(check_h(h));
+  DMT_TRY(enter(h));
   if (what_mask < 1 || what_mask > 3 || n_slots < 1)
     return fail(DMT_ERR_INVALID, "what_mask must be 1 (XX), 2 (WW) or 3, n_slots >= 1");
   HIP_OK(stream_wait(h));
@@ -2074,7 +2218,7 @@ dmt_status dmt_snapshot_reserve(dmt_ens* h, int32_t what_mask, int64_t n_slots) 
 }
 
 dmt_status dmt_snapshot_take(dmt_ens* h, int32_t unit, int64_t slot, int64_t mcmciter) {
-  DMT_TRY(check_h(h));
+  DMT_TRY(enter(h));
   if (unit != DMT_U && unit != DMT_UPROP) return fail(DMT_ERR_INVALID, "bad unit");
   if (!h->snap_mask) return fail(DMT_ERR_STATE, "no snapshot slots (dmt_snapshot_reserve)");
   if (slot < 0 || slot >= h->snap_slots) return fail(DMT_ERR_INVALID, "slot out of range");
@@ -2099,7 +2243,7 @@ dmt_status dmt_snapshot_take(dmt_ens* h, int32_t unit, int64_t slot, int64_t mcm
 
 dmt_status dmt_snapshot_download(dmt_ens* h, int32_t what, int64_t slot, double* out,
                                  int64_t* mcmciter) {
-  DMT_TRY(check_h(h));
+  DMT_TRY(enter(h));
   if ((what != 0 && what != 1) || !out) return fail(DMT_ERR_INVALID, "bad what/out");
   if (!(h->snap_mask >> what & 1)) return fail(DMT_ERR_STATE, "that path kind is not snapshotted");
   if (slot < 0 || slot >= h->snap_slots) return fail(DMT_ERR_INVALID, "slot out of range");
@@ -2112,7 +2256,7 @@ dmt_status dmt_snapshot_download(dmt_ens* h, int32_t what, int64_t slot, double*
 }
 
 dmt_status dmt_snapshot_write(dmt_ens* h, const char* path, int64_t s0, int64_t s1) {
-  DMT_TRY(check_h(h));
+  DMT_TRY(enter(h));
   if (!path) return fail(DMT_ERR_INVALID, "null path");
   if (!h->snap_mask) return fail(DMT_ERR_STATE, "no snapshot slots (dmt_snapshot_reserve)");
   if (s0 < 0 || s1 > h->snap_slots || s0 > s1) return fail(DMT_ERR_INVALID, "bad slot range");

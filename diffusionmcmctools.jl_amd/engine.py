@@ -34,6 +34,7 @@ class Ensemble:
         self.grid_shared = bool(grid_shared)
         self.Q0 = int(self.npts[: self.nseg[0]].sum())
         self._h = C.c_void_p()
+        self._hist_len = {0: 0}  # history length of each layout (dmt_get_block_state fills all)
         mdl = L.dmt_model(self.model, self.precision, self.d, self.m)
         st = L.dmt_structure(self.R, L.i32p(self.nseg), L.i32p(self.npts))
         cfg = L.dmt_config(int(seed) & (2**64 - 1), int(device), 1 if grid_shared else 0,
@@ -148,6 +149,7 @@ class Ensemble:
         lid = C.c_int32()
         L.call("dmt_create_layout", self._h, L.i32p(nb), L.i32p(sf), L.i32p(sl), L.u8p(lt),
                L.f64p(rh), int(hist_len), C.byref(lid))
+        self._hist_len[lid.value] = int(hist_len)
         return lid.value
 
     def layout_size(self, layout):
@@ -156,11 +158,23 @@ class Ensemble:
         return n.value
 
     def draw_proposal(self, layout, b0, b1, Z=None, iter=0, salt=0, want_success=False):
-        ok = np.empty(b1 - b0, dtype=np.uint8) if want_success else None
+        """``want_success``: True → the flags (the draw runs now); "lazy" → a LazyFlags that
+        reads them (dmt_draw_success) only when used, so the draw may be deferred and fused
+        with the accept_reject that follows (include/dmt.h, deferred draws)."""
+        eager = want_success is True
+        ok = np.empty(b1 - b0, dtype=np.uint8) if eager else None
         Z = self._Z(Z)
         L.call("dmt_draw_proposal", self._h, layout, b0, b1, L.f64p(Z), int(iter), int(salt),
                L.u8p(ok))
+        if want_success == "lazy":
+            return LazyFlags(self, layout, b0, b1)
         return None if ok is None else ok.astype(bool)
+
+    def draw_success(self, layout, b0, b1):
+        """Success flags of the last draw over blocks [b0, b1)."""
+        ok = np.empty(b1 - b0, dtype=np.uint8)
+        L.call("dmt_draw_success", self._h, layout, b0, b1, L.u8p(ok))
+        return ok.astype(bool)
 
     def accept_reject(self, layout, b0, b1, mcmciter, E=None, salt=0, want_acc=False):
         acc = np.empty(b1 - b0, dtype=np.uint8) if want_acc else None
@@ -236,8 +250,11 @@ class Ensemble:
         if what in (L.BLK_LL, L.BLK_LLPROP):
             out = np.empty(b1 - b0, dtype=np.float64)
         else:
+            have = self._hist_len.get(layout)
             if hist_len is None:
-                raise ValueError("hist_len needed for histories")
+                hist_len = have
+            if hist_len is None or (have is not None and hist_len != have):
+                raise ValueError(f"layout {layout} holds {have} history rows, not {hist_len}")
             dt = np.uint8 if what == L.BLK_ACC_HIST else np.float64
             out = np.empty((hist_len, b1 - b0), dtype=dt)
         L.call("dmt_get_block_state", self._h, layout, what, b0, b1, out.ctypes.data_as(C.c_void_p))
@@ -322,9 +339,58 @@ class Ensemble:
     def set_rng_counter(self, value):
         L.call("dmt_set_rng_counter", self._h, int(value))
 
+    def rng_state(self):
+        """(next counter value, key of the last auto draw, accept pending) — checkpoint."""
+        n, last, pend = C.c_uint64(), C.c_uint64(), C.c_uint8()
+        L.call("dmt_rng_state", self._h, C.byref(n), C.byref(last), C.byref(pend))
+        return n.value, last.value, bool(pend.value)
+
+    def set_rng_state(self, state):
+        n, last, pend = state
+        L.call("dmt_set_rng_state", self._h, int(n), int(last), 1 if pend else 0)
+
     def set_shard(self, seg_base):
         """This handle holds a shard whose local segment 0 is global segment ``seg_base``."""
         L.call("dmt_set_shard", self._h, int(seg_base))
+
+
+class LazyFlags:
+    """The success flags a draw returns, read from the device only when used (bool(), indexing,
+    iteration, numpy conversion): the draw itself may still be deferred (include/dmt.h)."""
+
+    def __init__(self, ens, layout, b0, b1):
+        self._args, self._v = (ens, layout, b0, b1), None
+
+    def _get(self):
+        if self._v is None:
+            ens, layout, b0, b1 = self._args
+            self._v = ens.draw_success(layout, b0, b1)
+        return self._v
+
+    def __array__(self, dtype=None, copy=None):
+        v = self._get()
+        return v if dtype is None else v.astype(dtype)
+
+    def __len__(self):
+        return len(self._get())
+
+    def __iter__(self):
+        return iter(self._get())
+
+    def __getitem__(self, k):
+        return self._get()[k]
+
+    def __bool__(self):
+        return bool(self._get().all())
+
+    def all(self):
+        return bool(self._get().all())
+
+    def __eq__(self, other):
+        return self._get() == other
+
+    def __repr__(self):
+        return f"LazyFlags({self._get()!r})"
 
 
 def comm_unique_id() -> bytes:

@@ -644,13 +644,38 @@ the device stream counter (every call fresh, as the reference's `rand!` on the g
 """
 function draw_proposal_path!(x::DeviceBlocks; Z=nothing, iter=nothing, salt=nothing)
     iter, salt = _key(iter, salt)
-    ok = Vector{UInt8}(undef, _n(x))
     pz = Z === nothing ? Ptr{Float64}(C_NULL) : pointer(Z)
+    # no success buffer: the draw may be deferred and fused with the accept_reject_proposal_path!
+    # that follows (include/dmt.h, deferred draws); the flags are read only if used
     GC.@preserve Z check(ccall((:dmt_draw_proposal, libdmt), Int32,
         (Ptr{Cvoid}, Int32, Int64, Int64, Ptr{Float64}, Int64, UInt32, Ptr{UInt8}),
-        x.se.h, x.layout, x.b0, x.b1, pz, iter, salt, ok))
-    x isa DeviceBiBlock ? Bool(ok[1]) : Bool.(ok)
+        x.se.h, x.layout, x.b0, x.b1, pz, iter, salt, Ptr{UInt8}(C_NULL)))
+    DrawSuccess(x)
 end
+
+"""
+    DrawSuccess
+
+What `draw_proposal_path!` returns (the reference returns the success flag(s),
+src/biblock.jl:78-92): read from the device (dmt_draw_success) only when used — `Bool(s)`,
+`s[i]`, `collect(s)`, `all(s)`, `s == v` — so an unused return value costs nothing.
+"""
+struct DrawSuccess{X}
+    x::X
+end
+function _flags(s::DrawSuccess)
+    x = s.x
+    ok = Vector{UInt8}(undef, _n(x))
+    check(ccall((:dmt_draw_success, libdmt), Int32, (Ptr{Cvoid}, Int32, Int64, Int64, Ptr{UInt8}),
+                x.se.h, x.layout, x.b0, x.b1, ok))
+    Bool.(ok)
+end
+Base.Bool(s::DrawSuccess) = all(_flags(s))
+Base.convert(::Type{Bool}, s::DrawSuccess) = Bool(s)
+Base.collect(s::DrawSuccess) = _flags(s)
+Base.getindex(s::DrawSuccess, i...) = _flags(s)[i...]
+Base.all(s::DrawSuccess) = all(_flags(s))
+Base.:(==)(s::DrawSuccess, v) = (s.x isa DeviceBiBlock ? Bool(s) : _flags(s)) == v
 
 "draw_proposal_path!(u::SamplingUnit) (src/sampling_unit.jl:118-120): (success, ll)."
 function draw_proposal_path!(u::DeviceSamplingUnit)

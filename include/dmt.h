@@ -229,6 +229,21 @@ dmt_status dmt_draw_proposal(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
                              const double* Z, int64_t iter, uint32_t salt,
                              uint8_t* success_out);
 
+/* Success flags of the last draw over blocks [b0, b1) (the value draw_proposal_path! returns,
+ * src/biblock.jl:78-92): a caller that passes success_out = NULL to dmt_draw_proposal reads them
+ * here, when (and only if) it needs them.
+ *
+ * Deferred draws.  dmt_draw_proposal with Z = NULL and success_out = NULL over a layout of
+ * single-segment linear-drift blocks (the register-resident kernel's range, e.g. C2) only
+ * records the draw and its stream key.  The dmt_accept_reject that follows on the same range,
+ * E = NULL, acc_out = NULL and the same stream key (the auto key of the draw, or an explicit key
+ * equal to the draw's), runs draw, decision, histories and the fetch_ll tree as ONE kernel
+ * launch; the next dmt_fetch_ll / dmt_fetch_ll_local of that range (mcmciter 0 or the same)
+ * returns the tree's values without a launch.  Any other call first launches the deferred draw,
+ * so every result is exactly that of launching each call at once (DMT_DEFER=0). */
+dmt_status dmt_draw_success(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
+                            uint8_t* success_out);
+
 /* accept_reject_proposal_path!(·, mcmciter) (src/biblock.jl:121-127): E > -(ll° - ll),
  * swap XX/WW, set_accepted!, save_ll! (both), swap ll.  E: double[b1-b0] (parity) or NULL
  * (device Exp(1) stream keyed by (seed, mcmciter, salt, global id of the block's first
@@ -415,6 +430,12 @@ dmt_status dmt_snapshot_write(dmt_ens* h, const char* path, int64_t s0, int64_t 
 /* ---------------- random stream counter (DMT_RNG_AUTO) ---------------- */
 dmt_status dmt_rng_counter(dmt_ens* h, uint64_t* next);
 dmt_status dmt_set_rng_counter(dmt_ens* h, uint64_t next);
+/* The whole auto-stream state for checkpoint / resume: the next counter value, the key of the
+ * last auto draw and whether the next auto accept still takes it (an accept pending after a
+ * draw).  Restoring all three resumes bit for bit even between a draw and its accept
+ * (dmt_set_rng_counter alone clears the pending draw). */
+dmt_status dmt_rng_state(dmt_ens* h, uint64_t* next, uint64_t* last_draw, uint8_t* pending);
+dmt_status dmt_set_rng_state(dmt_ens* h, uint64_t next, uint64_t last_draw, uint8_t pending);
 
 /* ---------------- misc ---------------- */
 dmt_status dmt_sync(dmt_ens* h);

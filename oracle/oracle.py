@@ -502,6 +502,12 @@ class OracleEnsemble:
     def set_rng_counter(self, v):
         self.rng_ctr, self.rng_pending = int(v), False
 
+    def rng_state(self):
+        return self.rng_ctr, self.rng_last, self.rng_pending
+
+    def set_rng_state(self, st):
+        self.rng_ctr, self.rng_last, self.rng_pending = int(st[0]), int(st[1]), bool(st[2])
+
     # ---- the hot path, restated
     def _Zseg(self, Z, g, it, salt):
         n = self.npts[g] - 1

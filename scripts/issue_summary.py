@@ -50,7 +50,10 @@ def main():
     for did, v in by_id.items():
         if "SQ_WAVES" not in v:
             continue
-        fma = v.get("SQ_INSTS_VALU_FMA_F64", v.get("SQ_INSTS_VALU_FMA_F32"))
+        # the FMA counter of the kernel's own precision, None when that pass did not collect it
+        # (an F32 count of an fp64 kernel is not its FMA count)
+        fp32 = "float" in a.kernel or "IfE" in a.kernel
+        fma = v.get("SQ_INSTS_VALU_FMA_F32" if fp32 else "SQ_INSTS_VALU_FMA_F64")
         w, wc, n = v["SQ_WAVES"], v["SQ_WAVE_CYCLES"], a.iters
         wps = w / a.simds
         rows.append({

@@ -27,6 +27,13 @@ def test_launcher_spawns_ranks():
     assert len(lines) == 1, p.stdout          # rank 0 only
     out = json.loads(lines[0])
     assert out["dry_run"] and out["n_gpus"] == 2 and out["ranks"] == 2
+    # the N-GPU line's self-diagnosis (rank_diagnostics): gathered from every rank over gloo
+    diag = out["rank_diagnostics"]
+    for k in ("ranks", "rccl_nranks", "kernel_ms_max", "kernel_ms_min", "kernel_skew",
+              "allgather_us_per_call_max", "per_rank"):
+        assert k in diag, k
+    assert diag["ranks"] == 2 and len(diag["per_rank"]) == 2
+    assert all(set(r) == {"kernel_ms", "allgather_us"} for r in diag["per_rank"])
 
 
 def test_world_size_must_match_gpus():
