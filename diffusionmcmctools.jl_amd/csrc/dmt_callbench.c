@@ -29,3 +29,22 @@ int dmt_callbench_loop(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int64
   *seconds = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
   return 0;
 }
+
+/* The same loop, the duration of every iteration in lat[i] (seconds): the latency spread. */
+int dmt_callbench_lat(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int64_t iter0,
+                      int64_t n, double* lat) {
+  for (int64_t i = 0; i < n; ++i) {
+    struct timespec t0, t1;
+    const int64_t it = iter0 + i;
+    double ll = 0, llp = 0;
+    int64_t na = 0;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    if (dmt_draw_proposal(h, layout, b0, b1, 0, 0, DMT_RNG_AUTO, 0)) return 1;
+    if (dmt_accept_reject(h, layout, b0, b1, 0, it, DMT_RNG_AUTO, 0)) return 2;
+    if (dmt_fetch_ll_local(h, layout, b0, b1, it, &ll, &llp, &na)) return 3;
+    if (dmt_fetch_ll_local(h, layout, b0, b1, 0, &ll, &llp, &na)) return 4;
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    lat[i] = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+  }
+  return 0;
+}

@@ -116,6 +116,22 @@ struct AcceptArgs {
   uint8_t* acc_out;  // [b1-b0] or nullptr
 };
 
+// The resident MCMC service (include/dmt.h "deferred draws"): a launch of the
+// register-resident producer/consumer kernel that runs the iterations the host posts one at a
+// time, keeping every block's state in registers between the caller's separate calls.
+struct SvcArgs {
+  const uint64_t* posted;  // host memory: iterations posted so far (written by the host)
+  const uint32_t* stop;    // host memory: 1 = leave at the next gate
+  uint64_t* rec;           // host memory: [2][grid][4] 16-byte records (sum bits, iteration + 1)
+                           //   of every workgroup's (ll, ll°, accepted) sums, by iteration parity
+  uint64_t* go;            // device: workgroup 0's answers to the other workgroups' gates —
+  uint64_t* quit;          //   go / quit = base + r + 1 at gate r (zeroed before every launch)
+  uint64_t idle_ticks;     // wall-clock ticks a waiting launch stays without a command
+  uint64_t* probe;         // DMT_SVC_PROBE builds only: [capacity][8] wall-clock stamps
+  uint64_t base;           // the launch's iteration r is the service's iteration base + r (a
+                           // launch that left idle is re-launched from where it stopped)
+};
+
 // Timing events attached to the next kernel dispatch (hipExtLaunchKernel): armed by the
 // runtime for a timed launch, consumed (and cleared) by that kernel's launcher.
 struct DispatchEvents {
@@ -205,6 +221,10 @@ constexpr int kResidentMaxSteps = 512;
 // part: [n_iter][3][nwaves] block partials followed by the tree nodes ([3 n_iter][ceil(nwaves /
 // WPB)] then [3 n_iter][ceil(nwaves / (16 WPB))], WPB ≤ 4); out3[n_iter][3]: every iteration's
 // fetch_ll; counter: ceil(nwaves / (16 WPB)) + 1 zeroed uint32 arrival counters (left zero)
+hipError_t launch_mcmc_service(const ModelKey& k, const void* args, const AcceptArgs& c,
+                               int64_t iter0, int64_t capacity, double* part, int64_t nwaves,
+                               int producers, int n_cu, const SvcArgs& sv, hipStream_t s);
+bool mcmc_service_fits(const ModelKey& k, int64_t nwaves, int producers, int n_cu);
 hipError_t launch_mcmc_persistent(const ModelKey& k, const void* args, const AcceptArgs& c,
                                   int64_t iter0, int64_t n_iter, double* part, int64_t nwaves,
                                   int resident, double* out3, unsigned* counter, hipStream_t s);

@@ -26,6 +26,12 @@
 #include "dmt_internal.h"
 #include "dmt_filter.h"
 
+// gfx950 only: no other target is built or validated (the persistent kernels' inter-workgroup
+// hand-offs use gfx950's write-through agent-scope stores).
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "dmt_kernels.hip targets gfx950 (MI355X) only"
+#endif
+
 namespace dmt {
 
 template <int K>
@@ -44,14 +50,17 @@ __device__ __forceinline__ T tree_sum(T* v) {
   return v[0];
 }
 
-// Streamed path / table accesses of the lane kernels.  DMT_LANE_NT_LOADS / DMT_LANE_NT_STORES
-// (measurement variants): non-temporal hints for data a draw touches once per launch (C3 / C5
-// stream 4.7 GB per draw, ≫ L2 and MALL).  Cache hints only: the values are the same.
+// Streamed path / table accesses of the lane kernels: non-temporal hints for data a draw
+// touches once per launch (C3 / C5 stream 4.7 GB per draw, ≫ L2 and MALL).  Cache hints only:
+// the values are the same.  Measured (profiles/r03f, one box): non-temporal X°/W° stores take
+// C3 (fp64) from 1 239 to 1 144 µs per draw, but C5 (fp32, whose mixed-selector stores write
+// partial lines) from 1 878 to 1 957 µs; non-temporal loads slow both (1 414, 2 291 µs).  So:
+// NT stores for fp64 (DMT_LANE_NT_STORES=1 also for fp32, 0 for none), normal loads.
 #ifndef DMT_LANE_NT_LOADS
 #define DMT_LANE_NT_LOADS 0
 #endif
 #ifndef DMT_LANE_NT_STORES
-#define DMT_LANE_NT_STORES 0
+#define DMT_LANE_NT_STORES 2  // 2: fp64 only, 1: all, 0: none
 #endif
 template <class T>
 __device__ __forceinline__ T lane_ld(const T* p) {
@@ -63,11 +72,10 @@ __device__ __forceinline__ T lane_ld(const T* p) {
 }
 template <class T>
 __device__ __forceinline__ void lane_st(T* p, T v) {
-#if DMT_LANE_NT_STORES
-  __builtin_nontemporal_store(v, p);
-#else
-  *p = v;
-#endif
+  if constexpr (DMT_LANE_NT_STORES == 1 || (DMT_LANE_NT_STORES == 2 && sizeof(T) == 8))
+    __builtin_nontemporal_store(v, p);
+  else
+    *p = v;
 }
 
 // One lane integrates one segment.  Main loop: full chunks of K steps, branch-free, with the
@@ -2087,12 +2095,94 @@ struct ResPcLds {
   int acc;            // the consumer's decision of the current iteration
 };
 
-template <class Mdl, class T, int NP>
+// ---- the resident MCMC service (SvcArgs): iterations posted by the host one at a time.
+struct SvcLds {
+  int go;             // the gate's answer
+  double row[3][4];   // the iteration's (ll, ll°, accepted) of the workgroup's 4 blocks
+};
+// Gate of iteration r (in place of its B1 barrier).  Workgroup 0's thread 0 is the launch's one
+// reader of host memory: it waits until the host has posted iteration r, asked the launch to
+// stop, or stayed silent for idle_ticks, and publishes the answer in device memory — go word
+// = base + r + 1, or exit word = base + r + 1 — which the other workgroups' thread 0 wait for
+// (agent scope: no PCIe traffic from 256 pollers; one decision, so every workgroup leaves at
+// the same gate and the launch's state is exactly that of its first r iterations).  The grid
+// is co-resident (launch_mcmc_service checks), so the reader always reaches the gate.  The
+// barrier hands the answer to every wave.  Nothing global is written for an iteration before
+// its gate opens.
+__device__ __forceinline__ bool svc_gate(const SvcArgs& sv, int64_t r, SvcLds* sl) {
+  if (threadIdx.x == 0) {
+    const uint64_t want = sv.base + (uint64_t)r + 1;
+    int go = 0;
+    if (blockIdx.x == 0) {
+      const uint64_t t0 = (uint64_t)wall_clock64();
+      for (;;) {
+        if (__hip_atomic_load(sv.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) break;
+        if (__hip_atomic_load(sv.posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= want) {
+          go = 1;
+          break;
+        }
+        if ((uint64_t)wall_clock64() - t0 > sv.idle_ticks) break;
+        __builtin_amdgcn_s_sleep(4);
+      }
+      __hip_atomic_store(go ? sv.go : sv.quit, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#ifdef DMT_SVC_PROBE
+      if (go) sv.probe[8 * (want - 1) + 0] = (uint64_t)wall_clock64();
+#endif
+    } else {
+      for (;;) {
+        if (__hip_atomic_load(sv.go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want) {
+          go = 1;
+          break;
+        }
+        if (__hip_atomic_load(sv.quit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == want) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+    sl->go = go;
+#ifdef DMT_SVC_PROBE
+    if (go) __hip_atomic_fetch_max(&sv.probe[8 * (want - 1) + 1], (uint64_t)wall_clock64(),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
+  }
+  __syncthreads();
+  return sl->go != 0;
+}
+
+// Iteration r's gate has opened: the workgroup's 4 consumer waves left their blocks' (ll, ll°,
+// accepted) in row[c][0..3] before it (0.0 for a block past b1).  Lanes 0..2 of wave 0 fold them — the
+// aligned 4-leaf subtree ((x0 + x1) + (x2 + x3)) of the canonical fetch_ll tree — and send each
+// sum with the iteration's tag to the host as ONE 16-byte store (value bits, tag): the host
+// reads a record once its three tags show the iteration and folds the workgroups' sums in the
+// canonical order (svc_fold in dmt_runtime.hip).  No counter, no wait: the workgroup goes on.
+// Records alternate between two sets by the iteration's parity; the host reads set s & 1 of
+// iteration s before it posts s + 1, so set s & 1 is free again when iteration s + 2 writes it.
+__device__ __forceinline__ void svc_record(const SvcArgs& sv, const SvcLds* sl, int64_t r) {
+  const int lane = threadIdx.x & 63;
+  if (lane < 3) {
+    const double v = (sl->row[lane][0] + sl->row[lane][1]) + (sl->row[lane][2] + sl->row[lane][3]);
+    const uint64_t slot = sv.base + (uint64_t)r;
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const uint64_t vb = __builtin_bit_cast(uint64_t, v), tag = slot + 1;
+    const u32x4 rec = {(uint32_t)vb, (uint32_t)(vb >> 32), (uint32_t)tag, (uint32_t)(tag >> 32)};
+    uint64_t* dst = sv.rec + (((slot & 1) * gridDim.x + blockIdx.x) * 4 + lane) * 2;
+    // one 16-byte vector store, system-coherent (sc0 sc1: written through to host memory now,
+    // not held in L2 until the launch ends)
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" : : "v"(dst), "v"(rec) : "memory");
+  }
+#ifdef DMT_SVC_PROBE
+  if (lane == 0)
+    __hip_atomic_fetch_max(&sv.probe[8 * (sv.base + r) + 2], (uint64_t)wall_clock64(),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
+}
+
+template <class Mdl, class T, int NP, bool SVC>
 __device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, const AcceptArgs& c,
                                                      const int64_t iter0, const int64_t n_iter,
                                                      double* __restrict__ part, const int64_t blk,
                                                      const bool valid,
-                                                     ResPcLds<Mdl::D, Mdl::M, T>& P) {
+                                                     ResPcLds<Mdl::D, Mdl::M, T>& P,
+                                                     const SvcArgs& sv, SvcLds* sl) {
   constexpr int D = Mdl::D, M = Mdl::M, HP = D * (D + 1) / 2;
   constexpr int CR = PcConsSteps<T, M, NP>::v, RC0 = kRun - CR, CRA = CR > 0 ? CR : 1;
   ResLds<D, M, T>& S = P.r;
@@ -2236,8 +2326,10 @@ __device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, cons
                                                         (int)(r0 & 63)));
     T* const Xdb = (sel.x(g) ^ a.xd_flip) ? Xd[1] : Xd[0];
     // the next iteration's normals of the consumer's steps (unconditional: no branch around
-    // them, so they can fill the scan's latency; the last iteration's are never used)
-    draw_c((uint32_t)(it + 1 + c.key_delta));
+    // them, so they can fill the scan's latency; the last iteration's are never used).  The
+    // service draws them after B2 instead: there the iteration's latency is what the caller
+    // waits for, and the host's round trip to the next post hides them.
+    if constexpr (!SVC) draw_c((uint32_t)(it + 1 + c.key_delta));
     // the run map of the e maps the producer (and, for its steps, the consumer) left in the pt slots
     T RA[D * D], Re[D];
 #pragma unroll
@@ -2315,6 +2407,25 @@ __device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, cons
 #pragma unroll
     for (int q = 0; q < 8; ++q)
       if (64 * q < nst) seg_acc = seg_acc + (lane_read(tsum, 4 * 8 * q) + (T)0);
+    // the service computes an iteration ahead of its post (registers and LDS only) and
+    // publishes it — stores, flags, selectors, the decision — once the host has posted it.  The
+    // block's fetch_ll leaves go to LDS before the gate, and the workgroup's records to the host
+    // as soon as it opens, ahead of the path stores
+    if constexpr (SVC) {
+      if (lane == 0) {
+        bool ok = isfinite(seg_acc);
+#pragma unroll
+        for (int p = 0; p < D; ++p) ok = ok && isfinite(xe[p]);
+        const double lp = ok ? (double)(llobs + seg_acc) : -INFINITY;
+        const bool ac = valid && E > -(lp - ll);
+        const int w4 = (int)(threadIdx.x >> 6) & 3;
+        sl->row[0][w4] = valid ? (ac ? lp : ll) : 0.0;
+        sl->row[1][w4] = valid ? (ac ? ll : lp) : 0.0;
+        sl->row[2][w4] = ac ? 1.0 : 0.0;
+      }
+      if (!svc_gate(sv, r0, sl)) break;
+      if (threadIdx.x < 64) svc_record(sv, sl, r0);  // the workgroup's fetch_ll sums → host
+    }
     wave_lds_sync();
     if (valid) {
 #pragma unroll
@@ -2348,9 +2459,11 @@ __device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, cons
           c.ll_hist[o] = ll;
           c.llp_hist[o] = llp;
         }
-        part[(3 * r0 + 0) * nb + j] = acc ? llp : ll;
-        part[(3 * r0 + 1) * nb + j] = acc ? ll : llp;
-        part[(3 * r0 + 2) * nb + j] = acc ? 1.0 : 0.0;
+        if constexpr (!SVC) {
+          part[(3 * r0 + 0) * nb + j] = acc ? llp : ll;
+          part[(3 * r0 + 1) * nb + j] = acc ? ll : llp;
+          part[(3 * r0 + 2) * nb + j] = acc ? 1.0 : 0.0;
+        }
       }
     }
     if (acc) {
@@ -2365,10 +2478,18 @@ __device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, cons
 #pragma unroll
           for (int k = 0; k < M; ++k) wvC[r][k] = dWC[r][k];
       }
-      wave_lds_sync();  // this wave's pt reads of the X° stores above are done
-      propose_c();
+      if constexpr (!SVC) {
+        wave_lds_sync();  // this wave's pt reads of the X° stores above are done
+        propose_c();
+      }
     }
     __syncthreads();  // B2: decision n → producer; pt reads of this iteration done
+    if constexpr (SVC) {
+      if constexpr (CR > 0) {
+        draw_c((uint32_t)(it + 1 + c.key_delta));
+        propose_c();
+      }
+    }
     if (r0 + 1 < n_iter) {
       hand_dw();  // the producer's W° stores of iteration n are done (before its B2)
       __syncthreads();  // B1: dW° of iteration n + 1 ready
@@ -2385,12 +2506,13 @@ __device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, cons
 // NP producer waves per block: producer h owns the steps r in [h·RR, (h+1)·RR) of every lane's
 // run (their Philox blocks, u's increments, the pCN and e maps) and the coalesced W° rows
 // k in [h·RR, (h+1)·RR); producer 0 also W(t0).
-template <class Mdl, class T, int NP>
+template <class Mdl, class T, int NP, bool SVC>
 __device__ __forceinline__ void resident_pc_producer(const BlockArgs<T>& a, const AcceptArgs& c,
                                                      const int64_t iter0, const int64_t n_iter,
                                                      const int64_t blk, const bool valid,
                                                      const int h,
-                                                     ResPcLds<Mdl::D, Mdl::M, T>& P) {
+                                                     ResPcLds<Mdl::D, Mdl::M, T>& P,
+                                                     const SvcArgs& sv, SvcLds* sl) {
   constexpr int D = Mdl::D, M = Mdl::M, HP = D * (D + 1) / 2;
   constexpr int CR = PcConsSteps<T, M, NP>::v;  // trailing run steps the consumer draws
   constexpr int RR = (kRun - CR) / NP, RW = kRun / NP;  // steps / W° rows of one producer
@@ -2519,10 +2641,16 @@ __device__ __forceinline__ void resident_pc_producer(const BlockArgs<T>& a, cons
   draw_z((uint32_t)(iter0 + c.key_delta), z);
   propose();
   __syncthreads();  // B1 of iteration 0
-  store_w();
+  if constexpr (!SVC) store_w();
   for (int64_t r0 = 0; r0 < n_iter; ++r0) {
     const bool more = r0 + 1 < n_iter;
+    // the next iteration's normals (they depend on the stream key alone), while the consumer
+    // runs this one
     if (more) draw_z((uint32_t)(iter0 + r0 + 1 + c.key_delta), z);
+    if constexpr (SVC) {  // the service: W° of iteration n once the host has posted it
+      if (!svc_gate(sv, r0, sl)) break;
+      store_w();
+    }
     __syncthreads();  // B2: decision n
     if (P.acc) {  // u's increments ← the accepted proposal's, still in the dw slots
       sel.mx ^= 1;
@@ -2537,12 +2665,12 @@ __device__ __forceinline__ void resident_pc_producer(const BlockArgs<T>& a, cons
     if (more) {
       propose();
       __syncthreads();  // B1: dW° of iteration n + 1 ready
-      store_w();
+      if constexpr (!SVC) store_w();
     }
   }
 }
 
-template <class Mdl, class T, int NP>
+template <class Mdl, class T, int NP, bool SVC = false>
 __global__ __launch_bounds__(64 * 4 * (NP + 1), 1) void k_mcmc_resident_pc(const BlockArgs<T> a,
                                                                       const AcceptArgs c,
                                                                       const int64_t iter0,
@@ -2550,27 +2678,34 @@ __global__ __launch_bounds__(64 * 4 * (NP + 1), 1) void k_mcmc_resident_pc(const
                                                                       double* __restrict__ part,
                                                                       double* __restrict__ nodes,
                                                                       unsigned* __restrict__ counter,
-                                                                      double* __restrict__ out3) {
+                                                                      double* __restrict__ out3,
+                                                                      const SvcArgs sv) {
   __shared__ ResPcLds<Mdl::D, Mdl::M, T> lds[4];
+  __shared__ SvcLds s_svc;
   if (n_iter <= 0) return;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t blk = a.b0 + (int64_t)blockIdx.x * 4 + (w & 3);
   const bool valid = blk < a.b1;
   const int role = w >> 2;  // 0: consumer, 1 + h: producer h
 #if defined(DMT_PC_STUB_P)  // timing probes (scripts/res_usage.sh, gpu_variants.sh): one role only
-  if (role == 0) resident_pc_consumer<Mdl, T, NP>(a, c, iter0, n_iter, part, blk, valid, lds[w & 3]);
+  if (role == 0)
+    resident_pc_consumer<Mdl, T, NP, SVC>(a, c, iter0, n_iter, part, blk, valid, lds[w & 3], sv, &s_svc);
   else for (int64_t i = 0; i < 2 * n_iter; ++i) __syncthreads();
 #elif defined(DMT_PC_STUB_C)
-  if (role > 0) resident_pc_producer<Mdl, T, NP>(a, c, iter0, n_iter, blk, valid, role - 1, lds[w & 3]);
+  if (role > 0)
+    resident_pc_producer<Mdl, T, NP, SVC>(a, c, iter0, n_iter, blk, valid, role - 1, lds[w & 3], sv, &s_svc);
   else for (int64_t i = 0; i < 2 * n_iter; ++i) __syncthreads();
 #else
   if (role == 0)
-    resident_pc_consumer<Mdl, T, NP>(a, c, iter0, n_iter, part, blk, valid, lds[w & 3]);
+    resident_pc_consumer<Mdl, T, NP, SVC>(a, c, iter0, n_iter, part, blk, valid, lds[w & 3], sv,
+                                          &s_svc);
   else
-    resident_pc_producer<Mdl, T, NP>(a, c, iter0, n_iter, blk, valid, role - 1, lds[w & 3]);
+    resident_pc_producer<Mdl, T, NP, SVC>(a, c, iter0, n_iter, blk, valid, role - 1, lds[w & 3],
+                                          sv, &s_svc);
 #endif
 #ifndef DMT_PC_NO_TAIL  // timing probe: no in-kernel fetch_ll trees
-  persistent_tree_tail<4, 4 * (NP + 1)>(part, nodes, a.b1 - a.b0, n_iter, counter, out3);
+  if constexpr (!SVC)  // the service forms each iteration's tree as the iteration ends
+    persistent_tree_tail<4, 4 * (NP + 1)>(part, nodes, a.b1 - a.b0, n_iter, counter, out3);
 #endif
 }
 
@@ -3892,12 +4027,13 @@ static hipError_t launch_mcmc_t(const void* args, const AcceptArgs& c, int64_t i
     double* nodes = part + 3 * n * nwaves;
     if constexpr (Mdl::D <= 2) {
       if (resident >= 2) {  // producer / consumer waves (k_mcmc_resident_pc), resident - 1 producers
+        const SvcArgs none{};
         if (resident == 3)
           dlaunch(k_mcmc_resident_pc<Mdl, T, 2>, dim3((unsigned)((nwaves + 3) / 4)), dim3(768), s,
-                  a, c, iter0, n, part, nodes, counter, out3);
+                  a, c, iter0, n, part, nodes, counter, out3, none);
         else
           dlaunch(k_mcmc_resident_pc<Mdl, T, 1>, dim3((unsigned)((nwaves + 3) / 4)), dim3(512), s,
-                  a, c, iter0, n, part, nodes, counter, out3);
+                  a, c, iter0, n, part, nodes, counter, out3, none);
         return hipGetLastError();
       }
       if (resident) {
@@ -3913,6 +4049,61 @@ static hipError_t launch_mcmc_t(const void* args, const AcceptArgs& c, int64_t i
   } else {
     return hipErrorInvalidValue;
   }
+}
+
+// The service's workgroups wait on one another through the host (an iteration is posted once
+// every block has finished the previous one): the whole grid must be resident at once.
+template <class Mdl, class T>
+static bool svc_fits_t(int64_t nwaves, int producers, int n_cu) {
+  if constexpr (Mdl::kLinear && Mdl::D <= 2) {
+    int per_cu = 0;
+    const hipError_t e =
+        producers == 2
+            ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                  &per_cu, reinterpret_cast<const void*>(k_mcmc_resident_pc<Mdl, T, 2, true>), 768, 0)
+            : hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                  &per_cu, reinterpret_cast<const void*>(k_mcmc_resident_pc<Mdl, T, 1, true>), 512, 0);
+    return e == hipSuccess && (nwaves + 3) / 4 <= (int64_t)per_cu * n_cu;
+  } else {
+    return false;
+  }
+}
+
+template <class Mdl, class T>
+static hipError_t launch_svc_t(const void* args, const AcceptArgs& c, int64_t iter0, int64_t cap,
+                               double* part, int64_t nwaves, int producers, int n_cu,
+                               const SvcArgs& sv, hipStream_t s) {
+  if constexpr (Mdl::kLinear && Mdl::D <= 2) {
+    const BlockArgs<T>& a = *static_cast<const BlockArgs<T>*>(args);
+    if (nwaves <= 0) return hipSuccess;
+    const dim3 grid((unsigned)((nwaves + 3) / 4));
+    if (!svc_fits_t<Mdl, T>(nwaves, producers, n_cu)) return hipErrorCooperativeLaunchTooLarge;
+    if (producers == 2)
+      dlaunch(k_mcmc_resident_pc<Mdl, T, 2, true>, grid, dim3(768), s, a, c, iter0, cap, part,
+              nullptr, nullptr, nullptr, sv);
+    else
+      dlaunch(k_mcmc_resident_pc<Mdl, T, 1, true>, grid, dim3(512), s, a, c, iter0, cap, part,
+              nullptr, nullptr, nullptr, sv);
+    return hipGetLastError();
+  } else {
+    return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_mcmc_service(const ModelKey& k, const void* args, const AcceptArgs& c,
+                               int64_t iter0, int64_t capacity, double* part, int64_t nwaves,
+                               int producers, int n_cu, const SvcArgs& sv, hipStream_t s) {
+  DMT_DISPATCH(k, (launch_svc_t<Mdl, T>(args, c, iter0, capacity, part, nwaves, producers, n_cu,
+                                        sv, s)));
+}
+
+static hipError_t svc_fits_err(const ModelKey& k, int64_t nwaves, int producers, int n_cu) {
+  DMT_DISPATCH(k, (svc_fits_t<Mdl, T>(nwaves, producers, n_cu) ? hipSuccess
+                                                                 : hipErrorCooperativeLaunchTooLarge));
+}
+
+bool mcmc_service_fits(const ModelKey& k, int64_t nwaves, int producers, int n_cu) {
+  return svc_fits_err(k, nwaves, producers, n_cu) == hipSuccess;
 }
 
 hipError_t launch_mcmc_persistent(const ModelKey& k, const void* args, const AcceptArgs& c,

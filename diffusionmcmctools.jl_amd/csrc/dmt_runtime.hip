@@ -114,8 +114,38 @@ struct dmt_ens {
     bool on = false;
     int32_t layout = 0;
     int64_t b0 = 0, b1 = 0, mcmciter = 0;
+    int64_t slot = -1;  // >= 0: the values are the service's iteration `slot` (its records)
+    double vals[3];     // slot -1: h_run; -2: these (folded when the service stopped)
   } fused;
   bool defer = true;
+  // The resident MCMC service (SvcArgs, dmt_kernels.hip): the fused draw + accept iterations
+  // of consecutive stream keys and mcmciters on one range run in ONE launch of the resident
+  // producer/consumer kernel, which keeps the blocks' state in registers and waits for the
+  // host to post each iteration; fetch_ll reads the iteration's tree from pinned memory.  The
+  // launch stops (the host asks, and waits) before any other call touches the stream, and
+  // leaves on its own after DMT_SVC_IDLE_MS (2 ms) without a command.  DMT_SERVICE=0: off.
+  struct {
+    bool on = false;
+    int32_t layout = 0;
+    int64_t b0 = 0, b1 = 0, iter0 = 0, cap = 0;
+    uint32_t key0 = 0, salt = 0;
+    uint64_t posted = 0;
+    uint64_t done = 0;    // iterations whose records the host has seen complete
+    int64_t nwg = 0;      // workgroups of the launch (records per iteration)
+    std::chrono::steady_clock::time_point t_last;
+  } svc;
+  bool service = true;
+  double svc_idle_ms = 2.0;   // DMT_SVC_IDLE_MS: a launch idles this long for a post, then leaves
+  int64_t svc_fit_nb = -1;    // the range size whose co-residency svc_fit holds
+  bool svc_fit = false;
+  struct { uint64_t starts = 0, relaunches = 0, posts = 0, waits = 0; } svc_stats;  // DMT_SVC_STATS
+  char* svc_host = nullptr;     // pinned: posted @0, stop @64 (separate lines)
+  uint64_t* svc_rec = nullptr;  // pinned: [2][svc_rec_nwg][8] records (SvcArgs::rec)
+  int64_t svc_rec_nwg = 0;
+  uint64_t* d_svc_words = nullptr;  // device: go @0, quit @128 bytes
+  uint64_t* d_svc_probe = nullptr;  // DMT_SVC_PROBE builds
+  std::vector<double> svc_host_seen, svc_host_post, svc_host_code;  // DMT_SVC_PROBE: host stamps (µs)
+  uint64_t wall_khz = 100000;   // device wall clock (hipDeviceAttributeWallClockRate)
   int grid_shared = 0;
   // path snapshots (dmt_snapshot_*): [slots][P][C] doubles in reference layout per kind
   int snap_mask = 0;
@@ -526,10 +556,104 @@ dmt_status run_block_kernel(dmt_ens* h, const Layout* L, int mode, int kind_time
   return DMT_OK;
 }
 
+// ---- the resident MCMC service
+constexpr int64_t kSvcCap = 4096;       // iterations per service launch
+dmt_status svc_relaunch(dmt_ens* h, uint64_t base);  // svc_launch (below)
+inline volatile uint64_t* svc_posted(dmt_ens* h) { return (volatile uint64_t*)(h->svc_host); }
+inline volatile uint32_t* svc_stopw(dmt_ens* h) { return (volatile uint32_t*)(h->svc_host + 64); }
+
+// Iteration `slot`'s records are all in: every workgroup's three 16-byte (sum, tag) stores
+// carry tag slot + 1 (each store lands whole, so a tag vouches for the value beside it)
+bool svc_slot_ready(const dmt_ens* h, uint64_t slot) {
+  const volatile uint64_t* r = h->svc_rec + (slot & 1) * h->svc.nwg * 8;
+  for (int64_t w = h->svc.nwg - 1; w >= 0; --w)
+    for (int c = 0; c < 3; ++c)
+      if (r[8 * w + 2 * c + 1] != slot + 1) return false;
+  return true;
+}
+
+// fetch_ll, fetch_ll° and the accepted count of iteration `slot` from its records: the
+// workgroups' 4-block sums folded by the canonical adjacent-pair tree (padded with zeros to a
+// power of two >= 64 leaves, + 0.0 on the two sums — the tree of dmt_fetch_ll)
+void svc_fold(const dmt_ens* h, uint64_t slot, double* out3) {
+  const volatile uint64_t* r = h->svc_rec + (slot & 1) * h->svc.nwg * 8;
+  const int64_t n = h->svc.nwg;
+  int64_t P = 64;
+  while (P < n) P <<= 1;
+  std::vector<double> v(P);
+  for (int c = 0; c < 3; ++c) {
+    for (int64_t w = 0; w < P; ++w) {
+      uint64_t bits = w < n ? r[8 * w + 2 * c] : 0;
+      double x;
+      std::memcpy(&x, &bits, 8);
+      v[w] = w < n ? x : 0.0;
+    }
+    for (int64_t m = P; m > 1; m >>= 1)
+      for (int64_t k = 0; k < m / 2; ++k) v[k] = v[2 * k] + v[2 * k + 1];
+    out3[c] = c == 2 ? v[0] : v[0] + 0.0;
+  }
+}
+
+// Wait until the service has finished n iterations (spin: the caller waits for this very
+// result).  A launch that left idle before an iteration was posted to it (the host was away
+// longer than the idle window) is launched again from the first iteration it did not run; a
+// launch that failed is an error, never a hang.
+dmt_status svc_wait_done(dmt_ens* h, uint64_t n) {
+  auto& v = h->svc;
+  auto t0 = std::chrono::steady_clock::now();
+  bool waited = false;
+  while (v.done < n) {
+    if (svc_slot_ready(h, v.done)) {
+      ++v.done;
+      continue;
+    }
+    waited = true;
+    const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    if (us > 100.0) {
+      const hipError_t e = hipStreamQuery(h->stream);
+      if (e == hipSuccess) {  // the launch has ended: everything it wrote is visible
+        if (svc_slot_ready(h, v.done)) continue;
+        ++h->svc_stats.relaunches;
+        DMT_TRY(svc_relaunch(h, v.done));
+        t0 = std::chrono::steady_clock::now();
+      } else if (e != hipErrorNotReady) {
+        return fail(DMT_ERR_HIP, std::string("resident service: ") + hipGetErrorString(e));
+      } else if (us > 10e6) {
+        return fail(DMT_ERR_HIP, "resident service: no result in 10 s");
+      }
+    }
+  }
+  if (waited) ++h->svc_stats.waits;
+  return DMT_OK;
+}
+
+// Stop a running service: every posted iteration finished, then the stop word, then the launch
+// drains (its waves leave at their next gate); the words are re-armed for the next launch.  The
+// values of a fused iteration of the service are folded first (they stay fetch_ll's answer).
+dmt_status svc_stop(dmt_ens* h) {
+  if (!h->svc.on) return DMT_OK;
+  h->svc.on = false;
+  dmt_status st = svc_wait_done(h, h->svc.posted);
+  if (st == DMT_OK && h->fused.on && h->fused.slot >= 0) {
+    svc_fold(h, (uint64_t)h->fused.slot, h->fused.vals);
+    h->fused.slot = -2;
+  }
+  __atomic_store_n(svc_stopw(h), 1u, __ATOMIC_RELEASE);
+  const hipError_t e = stream_wait(h);
+  __atomic_store_n(svc_stopw(h), 0u, __ATOMIC_RELEASE);
+  __atomic_store_n(svc_posted(h), (uint64_t)0, __ATOMIC_RELEASE);
+  h->svc.posted = 0;
+  h->svc.done = 0;
+  if (st != DMT_OK) return st;
+  if (e != hipSuccess) return fail(DMT_ERR_HIP, std::string("resident service: ") + hipGetErrorString(e));
+  return DMT_OK;
+}
+
 // Launch a deferred draw (if any): the kernel launch dmt_draw_proposal would have made, with
 // the stream key it took.  The fused results stay valid (the draw is ordered after them).
 dmt_status flush_deferred(dmt_ens* h) {
   if (!h->def.on) return DMT_OK;
+  DMT_TRY(svc_stop(h));
   h->def.on = false;
   Layout* L;
   DMT_TRY(get_layout(h, h->def.layout, &L));
@@ -541,6 +665,7 @@ dmt_status flush_deferred(dmt_ens* h) {
 // fused fetch_ll values are dropped.
 dmt_status enter(dmt_ens* h) {
   DMT_TRY(check_h(h));
+  DMT_TRY(svc_stop(h));
   DMT_TRY(flush_deferred(h));
   h->fused.on = false;
   return DMT_OK;
@@ -767,12 +892,29 @@ dmt_status dmt_create(dmt_ens** out, const dmt_model* model, const dmt_structure
   if (const char* e = std::getenv("DMT_LANE_SPLIT")) h->lane_split = std::atoi(e);
   if (const char* e = std::getenv("DMT_LANE_PAIR")) h->lane_pair = std::atoi(e);
   if (const char* e = std::getenv("DMT_DEFER")) h->defer = std::atoi(e) != 0;
+  if (const char* e = std::getenv("DMT_SERVICE")) h->service = std::atoi(e) != 0;
+  if (const char* e = std::getenv("DMT_SVC_IDLE_MS")) h->svc_idle_ms = std::max(0.1, std::atof(e));
+  {
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, cfg->device) == hipSuccess &&
+        khz > 0)
+      h->wall_khz = (uint64_t)khz;
+  }
   if (const char* e = std::getenv("DMT_REPAIR_DIV")) h->repair_div = std::max(1, std::atoi(e));
   if (const char* e = std::getenv("DMT_SCAN_RESIDENT")) h->scan_resident = std::strcmp(e, "0") != 0;
   {
     hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, h->device) == hipSuccess)
-      h->n_simd = 4 * (int64_t)prop.multiProcessorCount;
+    if (hipGetDeviceProperties(&prop, h->device) != hipSuccess)
+      return fail(DMT_ERR_HIP, "hipGetDeviceProperties failed");
+    // The kernels are built for gfx950 only, and the in-kernel fetch_ll hand-offs rely on its
+    // write-through (sc1) agent-scope stores being performed at vmcnt(0): refuse
+    // any other architecture rather than run unvalidated ordering assumptions.
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+      const std::string arch = prop.gcnArchName;
+      return fail(DMT_ERR_HIP, "libdmt is built and validated for gfx950 (MI355X) only; device " +
+                                   std::to_string(cfg->device) + " is " + arch);
+    }
+    h->n_simd = 4 * (int64_t)prop.multiProcessorCount;
   }
   h->tw = h->mapping == MAP_WAVE ? 1 : kLanes;
   h->ntiles = (h->R + h->tw - 1) / h->tw;
@@ -829,6 +971,42 @@ dmt_status dmt_create(dmt_ens** out, const dmt_model* model, const dmt_structure
 dmt_status dmt_destroy(dmt_ens* h) {
   if (!h) return DMT_OK;
   (void)hipSetDevice(h->device);
+  (void)svc_stop(h);
+#ifdef DMT_SVC_PROBE
+  if (h->d_svc_probe) {  // median stage durations (µs) of the first service's iterations
+    std::vector<uint64_t> pr(8 * kSvcCap);
+    (void)hipMemcpy(pr.data(), h->d_svc_probe, pr.size() * 8, hipMemcpyDeviceToHost);
+    const double tick_us = 1e3 / (double)h->wall_khz;
+    std::vector<double> d[3];
+    for (int64_t r = 1; r + 1 < kSvcCap && pr[8 * (r + 1)]; ++r) {
+      const uint64_t* p = &pr[8 * r];
+      d[0].push_back((p[1] - p[0]) * tick_us);   // poller saw the post -> last workgroup's gate
+      d[1].push_back((p[2] - p[1]) * tick_us);   // -> last workgroup's records sent (publish, B2)
+      d[2].push_back((pr[8 * (r + 1)] - p[2]) * tick_us);  // -> the next post seen (PCIe, host)
+    }
+    for (int64_t r = 1; r < (int64_t)std::min(h->svc_host_post.size(), h->svc_host_seen.size()); ++r)
+      if (h->svc_host_post[r] > 0 && h->svc_host_seen[r - 1] > 0)
+        h->svc_host_code.push_back(h->svc_host_post[r] - h->svc_host_seen[r - 1]);
+    if (!h->svc_host_code.empty()) {
+      auto& v = h->svc_host_code;
+      std::sort(v.begin(), v.end());
+      std::fprintf(stderr, "svc probe host code (result seen -> next post) median %.2f us  p10 %.2f  p90 %.2f\n",
+                   v[v.size() / 2], v[v.size() / 10], v[v.size() * 9 / 10]);
+    }
+    const char* nm[3] = {"gate", "publish", "return"};
+    for (int k = 0; k < 3; ++k) {
+      if (d[k].empty()) continue;
+      std::sort(d[k].begin(), d[k].end());
+      std::fprintf(stderr, "svc probe %-9s median %.2f us  p10 %.2f  p90 %.2f  (n=%zu)\n", nm[k],
+                   d[k][d[k].size() / 2], d[k][d[k].size() / 10], d[k][d[k].size() * 9 / 10],
+                   d[k].size());
+    }
+  }
+#endif
+  if (std::getenv("DMT_SVC_STATS"))
+    std::fprintf(stderr, "dmt service: %llu starts, %llu relaunches, %llu posts, %llu waits\n",
+                 (unsigned long long)h->svc_stats.starts, (unsigned long long)h->svc_stats.relaunches,
+                 (unsigned long long)h->svc_stats.posts, (unsigned long long)h->svc_stats.waits);
   (void)stream_wait(h);
   drain_timing(h);
   for (auto e : h->free_events) (void)hipEventDestroy(e);
@@ -853,6 +1031,10 @@ dmt_status dmt_destroy(dmt_ens* h) {
   if (h->comm) (void)ncclCommDestroy(h->comm);
   if (h->h_red) (void)hipHostFree(h->h_red);
   if (h->h_run) (void)hipHostFree(h->h_run);
+  if (h->svc_host) (void)hipHostFree(h->svc_host);
+  if (h->svc_rec) (void)hipHostFree(h->svc_rec);
+  if (h->d_svc_words) (void)hipFree(h->d_svc_words);
+  if (h->d_svc_probe) (void)hipFree(h->d_svc_probe);
   (void)hipStreamDestroy(h->stream);
   delete h;
   return DMT_OK;
@@ -1109,7 +1291,14 @@ dmt_status dmt_draw_unit(dmt_ens* h, int32_t unit, int64_t r0, int64_t r1, const
 
 dmt_status dmt_draw_proposal(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, const double* Z,
                              int64_t iter, uint32_t salt, uint8_t* success_out) {
-  DMT_TRY(enter(h));
+  DMT_TRY(check_h(h));
+  {  // a draw the next accept may fuse with leaves a running service alone
+    Layout* Lq;
+    DMT_TRY(get_layout(h, layout, &Lq));
+    if (!(!Z && !success_out && h->defer && resident_range(h, Lq))) DMT_TRY(enter(h));
+    DMT_TRY(flush_deferred(h));  // an earlier deferred draw: launched first
+    h->fused.on = false;         // fetch_ll° now sees this proposal
+  }
   Layout* L;
   DMT_TRY(get_layout(h, layout, &L));
   DMT_TRY(check_range(L, b0, b1));
@@ -1500,6 +1689,102 @@ dmt_status dmt_mcmc_run_local(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1
   return mcmc_run_impl(h, layout, b0, b1, iter0, n_iter, salt, out, false);
 }
 
+// (Re-)launch the service's kernel from its iteration `base` (0: a new service).  The launch
+// runs at most cap − base iterations, each once the host has posted it.
+static dmt_status svc_launch(dmt_ens* h, uint64_t base) {
+  auto& v = h->svc;
+  Layout* L;
+  DMT_TRY(get_layout(h, v.layout, &L));
+  const int64_t nb = v.b1 - v.b0;
+  SvcArgs sv{};
+  void* dp = nullptr;
+  HIP_OK(hipHostGetDevicePointer(&dp, h->svc_host, 0));
+  sv.posted = (const uint64_t*)dp;
+  sv.stop = (const uint32_t*)((char*)dp + 64);
+  HIP_OK(hipHostGetDevicePointer(&dp, h->svc_rec, 0));
+  sv.rec = (uint64_t*)dp;
+  sv.go = h->d_svc_words;        // separate 128-byte lines
+  sv.quit = h->d_svc_words + 16;
+  HIP_OK(hipMemsetAsync(h->d_svc_words, 0, 32 * sizeof(uint64_t), h->stream));
+  sv.idle_ticks = (uint64_t)(h->wall_khz * h->svc_idle_ms);
+  sv.base = base;
+#ifdef DMT_SVC_PROBE
+  if (!h->d_svc_probe) {
+    DMT_TRY(ens_alloc(h, &h->d_svc_probe, 8 * kSvcCap));
+    HIP_OK(hipMemsetAsync(h->d_svc_probe, 0, 8 * kSvcCap * 8, h->stream));
+  }
+  sv.probe = h->d_svc_probe;
+#endif
+  AcceptArgs c = accept_args(h, L, v.b0, v.b1, nullptr, v.iter0 + (int64_t)base,
+                             RngKey{0, v.salt}, nullptr);
+  c.key_delta = (int64_t)v.key0 - v.iter0;
+  auto fill = [&](auto& a) {
+    fill_common(h, L, a);
+    a.success = L->d_success;
+    a.b0 = v.b0;
+    a.b1 = v.b1;
+    a.xd_flip = 1;  // MODE_PCN: start u, write u°, read u.W, write u°.W
+    a.wd_flip = 1;
+    a.salt = v.salt;
+  };
+  hipError_t e;
+  if (h->key.precision == DMT_F64) {
+    BlockArgs<double> a{};
+    fill(a);
+    e = launch_mcmc_service(h->key, &a, c, v.iter0 + (int64_t)base, v.cap - (int64_t)base,
+                            nullptr, nb, h->resident_pc, (int)(h->n_simd / 4), sv,
+                            h->stream);
+  } else {
+    BlockArgs<float> a{};
+    fill(a);
+    e = launch_mcmc_service(h->key, &a, c, v.iter0 + (int64_t)base, v.cap - (int64_t)base,
+                            nullptr, nb, h->resident_pc, (int)(h->n_simd / 4), sv,
+                            h->stream);
+  }
+  if (e != hipSuccess) return fail(DMT_ERR_HIP, std::string("resident service: ") + hipGetErrorString(e));
+  return DMT_OK;
+}
+
+namespace {
+dmt_status svc_relaunch(dmt_ens* h, uint64_t base) { return svc_launch(h, base); }
+}  // namespace
+
+// A new service on (layout, b0:b1) whose first iteration is mcmciter with stream key `key`
+static dmt_status svc_start(dmt_ens* h, Layout* L, int32_t layout, int64_t b0, int64_t b1,
+                            int64_t mcmciter, RngKey key) {
+  const int64_t nb = b1 - b0;
+  if (!h->svc_host) {
+    HIP_OK(hipHostMalloc((void**)&h->svc_host, 256, hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(h->svc_host, 0, 256);
+    DMT_TRY(ens_alloc(h, &h->d_svc_words, 32));
+  }
+  const int64_t nwg = (nb + 3) / 4;  // the launch's workgroups (4 blocks each)
+  if (nwg > h->svc_rec_nwg) {
+    if (h->svc_rec) { (void)hipHostFree(h->svc_rec); h->svc_rec = nullptr; }
+    h->svc_rec_nwg = 0;
+    HIP_OK(hipHostMalloc((void**)&h->svc_rec, 2 * nwg * 64, hipHostMallocMapped | hipHostMallocCoherent));
+    h->svc_rec_nwg = nwg;
+  }
+  std::memset(h->svc_rec, 0, 2 * nwg * 64);  // no tag of an earlier service can match
+  auto& v = h->svc;
+  v.nwg = nwg;
+  v.done = 0;
+  v.layout = layout;
+  v.b0 = b0;
+  v.b1 = b1;
+  v.iter0 = mcmciter;
+  v.key0 = key.iter;
+  v.salt = key.salt;
+  v.cap = L->hist_len > 0 ? std::min<int64_t>(kSvcCap, L->hist_len - mcmciter + 1) : kSvcCap;
+  v.posted = 0;
+  __atomic_store_n(svc_posted(h), (uint64_t)0, __ATOMIC_RELEASE);
+  __atomic_store_n(svc_stopw(h), 0u, __ATOMIC_RELEASE);
+  DMT_TRY(svc_launch(h, 0));
+  ++h->svc_stats.starts;
+  v.on = true;
+  return DMT_OK;
+}
+
 dmt_status dmt_accept_reject(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, const double* E,
                              int64_t mcmciter, uint32_t salt, uint8_t* acc_out) {
   DMT_TRY(check_h(h));
@@ -1511,13 +1796,62 @@ dmt_status dmt_accept_reject(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
   const bool fuse = h->def.on && h->def.layout == layout && h->def.b0 == b0 &&
                     h->def.b1 == b1 && !E && !acc_out && mcmciter >= 1;
   h->fused.on = false;
-  if (!fuse) DMT_TRY(flush_deferred(h));
+  if (!fuse) {
+    DMT_TRY(svc_stop(h));
+    DMT_TRY(flush_deferred(h));
+  }
   RngKey key;
   DMT_TRY(accept_key(h, mcmciter, salt, &key));
   if (fuse && key.iter == h->def.iter && key.salt == h->def.salt) {
     // the deferred draw and this decision with ONE stream key: one launch of the resident MCMC
-    // kernel (draw, decision, histories, fetch_ll tree) — the launch dmt_mcmc_step makes
+    // kernel (draw, decision, histories, fetch_ll tree) — the launch dmt_mcmc_step makes — or
+    // the next iteration of the running resident service
     h->def.on = false;
+    if (h->service && h->resident_pc >= 1 && !h->comm && h->svc_fit_nb != b1 - b0) {
+      h->svc_fit_nb = b1 - b0;
+      h->svc_fit = mcmc_service_fits(h->key, b1 - b0, h->resident_pc, (int)(h->n_simd / 4));
+    }
+    if (h->service && h->resident_pc >= 1 && !h->comm && h->svc_fit) {
+      const auto now = std::chrono::steady_clock::now();
+      auto& v = h->svc;
+      const bool cont =
+          v.on && v.layout == layout && v.b0 == b0 && v.b1 == b1 && v.salt == key.salt &&
+          key.iter == (uint32_t)(v.key0 + v.posted) && mcmciter == v.iter0 + (int64_t)v.posted &&
+          (int64_t)v.posted < v.cap;
+      if (!cont) {
+        DMT_TRY(svc_stop(h));
+        DMT_TRY(svc_start(h, L, layout, b0, b1, mcmciter, key));
+      }
+      const uint64_t slot = v.posted;
+      // the records alternate between two sets: every earlier iteration is seen complete before
+      // this one is posted, so that it never overwrites records not yet read (immediate when the
+      // caller fetched the previous iteration)
+      DMT_TRY(svc_wait_done(h, slot));
+      if (cont && std::chrono::duration<double, std::milli>(now - v.t_last).count() >
+                      0.5 * h->svc_idle_ms &&
+          hipStreamQuery(h->stream) == hipSuccess) {
+        // the host was away long enough for the launch to leave idle: launch it again from
+        // this iteration at once (instead of finding out in svc_wait_done)
+        ++h->svc_stats.relaunches;
+        DMT_TRY(svc_relaunch(h, slot));
+      }
+      v.posted = slot + 1;
+      ++h->svc_stats.posts;
+#ifdef DMT_SVC_PROBE
+      if (h->svc_host_post.size() < (size_t)kSvcCap) h->svc_host_post.resize(kSvcCap, 0.0);
+      if (h->svc_stats.starts == 1) h->svc_host_post[slot] = hp_now();
+#endif
+      v.t_last = now;
+      __atomic_store_n(svc_posted(h), v.posted, __ATOMIC_RELEASE);
+      h->fused.on = true;
+      h->fused.layout = layout;
+      h->fused.b0 = b0;
+      h->fused.b1 = b1;
+      h->fused.mcmciter = mcmciter;
+      h->fused.slot = (int64_t)slot;
+      return DMT_OK;
+    }
+    DMT_TRY(svc_stop(h));
     DMT_TRY(ensure_red_work(h, b1 - b0));
     DMT_TRY(mcmc_run_launch(h, L, b0, b1, mcmciter, 1, key.salt,
                             (int64_t)key.iter - mcmciter, false));
@@ -1526,6 +1860,7 @@ dmt_status dmt_accept_reject(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
     h->fused.b0 = b0;
     h->fused.b1 = b1;
     h->fused.mcmciter = mcmciter;
+    h->fused.slot = -1;
     return DMT_OK;
   }
   DMT_TRY(flush_deferred(h));  // a different key: the draw's own launch first
@@ -1946,10 +2281,24 @@ static dmt_status fetch_ll_impl(dmt_ens* h, int32_t layout, int64_t b0, int64_t 
       (mcmciter == 0 || mcmciter == h->fused.mcmciter) && !(h->comm && global)) {
     // the fused draw + accept of this range formed this very tree in its launch (same order,
     // same values): wait for it, no launch
-    HIP_OK(stream_wait(h));
-    if (ll) *ll = h->h_run[0];
-    if (ll_prop) *ll_prop = h->h_run[1];
-    if (n_acc) *n_acc = mcmciter > 0 ? (int64_t)h->h_run[2] : 0;
+    const double* r3 = h->h_run;
+    double sv3[3];
+    if (h->fused.slot >= 0) {
+      DMT_TRY(svc_wait_done(h, (uint64_t)h->fused.slot + 1));
+#ifdef DMT_SVC_PROBE
+      if (h->svc_host_seen.size() < (size_t)kSvcCap) h->svc_host_seen.resize(kSvcCap, 0.0);
+      if (h->svc_host_seen[h->fused.slot] == 0.0) h->svc_host_seen[h->fused.slot] = hp_now();
+#endif
+      svc_fold(h, (uint64_t)h->fused.slot, sv3);
+      r3 = sv3;
+    } else if (h->fused.slot == -2) {
+      r3 = h->fused.vals;
+    } else {
+      HIP_OK(stream_wait(h));
+    }
+    if (ll) *ll = r3[0];
+    if (ll_prop) *ll_prop = r3[1];
+    if (n_acc) *n_acc = mcmciter > 0 ? (int64_t)r3[2] : 0;
     return DMT_OK;
   }
   DMT_TRY(enter(h));
@@ -1979,7 +2328,8 @@ dmt_status dmt_draw_success(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
   DMT_TRY(get_layout(h, layout, &L));
   DMT_TRY(check_range(L, b0, b1));
   if (!success_out) return fail(DMT_ERR_INVALID, "null output");
-  DMT_TRY(flush_deferred(h));  // reading flags changes nothing: fused results stay valid
+  DMT_TRY(svc_stop(h));        // reading flags changes nothing: fused results stay valid
+  DMT_TRY(flush_deferred(h));
   HIP_OK(hipMemcpyAsync(success_out, L->d_success + b0, b1 - b0, hipMemcpyDeviceToHost, h->stream));
   HIP_OK(stream_wait(h));
   return DMT_OK;

@@ -240,7 +240,19 @@ dmt_status dmt_draw_proposal(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
  * equal to the draw's), runs draw, decision, histories and the fetch_ll tree as ONE kernel
  * launch; the next dmt_fetch_ll / dmt_fetch_ll_local of that range (mcmciter 0 or the same)
  * returns the tree's values without a launch.  Any other call first launches the deferred draw,
- * so every result is exactly that of launching each call at once (DMT_DEFER=0). */
+ * so every result is exactly that of launching each call at once (DMT_DEFER=0).
+ *
+ * Resident service (DMT_SERVICE, default on; one process, no communicator, the launch's
+ * workgroups co-resident).  Consecutive fused iterations of one range — stream keys and
+ * mcmciters advancing by one — run in ONE launch of the register-resident kernel that stays on
+ * the device between the caller's calls: it computes each iteration ahead, publishes it when
+ * dmt_accept_reject posts it (a word in pinned memory), and sends the iteration's fetch_ll sums
+ * to pinned memory, which dmt_fetch_ll folds in the canonical order.  Results are bit-identical
+ * to the one-launch-per-iteration path (DMT_SERVICE=0).  Any other libdmt call on the handle
+ * stops the launch first (and waits for it); a launch with no post for DMT_SVC_IDLE_MS (2 ms)
+ * leaves by itself and is launched again when the next iteration is posted.  While it waits,
+ * the launch occupies the device: call dmt_sync (or any libdmt call) before a device-wide
+ * synchronisation from outside libdmt, or that synchronisation waits up to DMT_SVC_IDLE_MS. */
 dmt_status dmt_draw_success(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
                             uint8_t* success_out);
 

@@ -21,22 +21,28 @@ from diffusionmcmctools_amd import _lib as L  # noqa: E402
 from diffusionmcmctools_amd import workloads as W  # noqa: E402
 
 
-def _ensembles(defer_values, B=96, N=300, hist=12, with_oracle=True):
+def _ensembles(defer_values, B=96, N=300, hist=12, with_oracle=True, service=None):
+    """One device ensemble per DMT_DEFER value (DMT_SERVICE: `service`, one per ensemble, or
+    the library's default), then the oracle's."""
     import oracle as orc
     w = W.c2_ou2d(B=B, N=N)
     w.meta["hist_len"] = hist
     out = []
-    for dv in defer_values:
-        saved = os.environ.get("DMT_DEFER")
-        os.environ["DMT_DEFER"] = dv
+    for k, dv in enumerate(defer_values):
+        env = {"DMT_DEFER": dv}
+        if service is not None:
+            env["DMT_SERVICE"] = service[k]
+        saved = {n: os.environ.get(n) for n in env}
+        os.environ.update(env)
         try:
             e = dmt.Ensemble(w.model.kind, w.d, w.m, w.n_points, precision=w.precision, seed=5,
                              grid_shared=w.grid_shared)
         finally:
-            if saved is None:
-                os.environ.pop("DMT_DEFER")
-            else:
-                os.environ["DMT_DEFER"] = saved
+            for n, v in saved.items():
+                if v is None:
+                    os.environ.pop(n)
+                else:
+                    os.environ[n] = v
         out.append(e)
     if with_oracle:
         out.append(orc.OracleEnsemble(w.model.kind, w.d, w.m, w.n_points, prec=w.precision,
@@ -157,3 +163,77 @@ def test_rng_state_checkpoint_between_draw_and_accept():
     acc = [e.accept_reject(lay, 0, nb, 1, salt=L.RNG_AUTO, want_acc=True) for e in (a, b)]
     assert np.array_equal(acc[0], acc[1])
     _same_state(a, b, lay, nb, 12)
+
+
+# ------------------------------------------------------------------ the resident service
+@pytest.mark.gpu
+def test_service_equals_fused_launches_and_oracle():
+    """DMT_SERVICE=1 (iterations posted to one resident launch) vs DMT_SERVICE=0 (one fused
+    launch per iteration) vs DMT_DEFER=0 vs the oracle: every fetch_ll value, path, flag and
+    history bit-identical, over more iterations than one auto-key Exp(1) row (64)."""
+    (svc, fused, imm, ora), lay, nb = _ensembles(["1", "1", "0"], hist=80,
+                                                 service=["1", "0", "0"])
+    r = [_loop(e, lay, nb, 70, _nothing) for e in (svc, fused, imm, ora)]
+    for k in (1, 2, 3):
+        assert np.array_equal(r[0], r[k]), k
+    for e in (fused, imm, ora):
+        _same_state(svc, e, lay, nb, 80)
+    for e in (svc, fused, imm):
+        e.close()
+
+
+def _loop_gaps(e, lay, nb, iters, fetch_every, sleep_at=(), sleep_s=0.0):
+    import time
+    e.loglikhd(lay, L.U, 0, nb)
+    res = []
+    for i in range(1, iters + 1):
+        e.draw_proposal(lay, 0, nb, salt=L.RNG_AUTO, want_success="lazy")
+        if i in sleep_at:
+            time.sleep(sleep_s)      # longer than the launch's idle window (2 ms)
+        e.accept_reject(lay, 0, nb, i, salt=L.RNG_AUTO)
+        if i % fetch_every == 0:
+            res.append(e.fetch_ll(lay, 0, nb, i))
+    res.append(e.fetch_ll(lay, 0, nb, 0))
+    return np.array(res)
+
+
+@pytest.mark.gpu
+def test_service_unfetched_iterations_and_idle_relaunch():
+    """Iterations posted without their fetch_ll in between (the launch's one row set is reused:
+    the host waits for the previous tree before posting) and host pauses longer than the
+    launch's idle window (the launch leaves; the waiter launches it again from the first
+    iteration it did not run): same results as one launch per call."""
+    (svc, imm, ora), lay, nb = _ensembles(["1", "0"], hist=40, service=["1", "0"])
+    kw = dict(fetch_every=3, sleep_at=(5, 6, 17), sleep_s=0.05)
+    r = [_loop_gaps(e, lay, nb, 30, **kw) for e in (svc, imm, ora)]
+    assert np.array_equal(r[0], r[1])
+    assert np.array_equal(r[0], r[2])
+    _same_state(svc, imm, lay, nb, 40)
+    _same_state(svc, ora, lay, nb, 40)
+    assert np.array_equal(svc.draw_success(lay, 0, nb), imm.draw_success(lay, 0, nb))
+    for e in (svc, imm):
+        e.close()
+
+
+@pytest.mark.gpu
+def test_service_explicit_keys_ranges_and_capacity():
+    """Explicit keys, a change of range in the middle (the service stops and a new one starts),
+    a sub-range, and a run to the end of the history (the launch's capacity): same results."""
+    (svc, imm, ora), lay, nb = _ensembles(["1", "0"], hist=24, service=["1", "0"])
+    h = nb // 2
+    out = []
+    for e in (svc, imm, ora):
+        e.loglikhd(lay, L.U, 0, nb)
+        res = []
+        for i in range(1, 25):
+            b0, b1 = (0, nb) if i <= 10 or i > 16 else (0, h)
+            e.draw_proposal(lay, b0, b1, iter=i, salt=7)
+            e.accept_reject(lay, b0, b1, i, salt=7)
+            res.append(e.fetch_ll(lay, b0, b1, i))
+        out.append(np.array(res))
+    assert np.array_equal(out[0], out[1])
+    assert np.array_equal(out[0], out[2])
+    _same_state(svc, imm, lay, nb, 24)
+    _same_state(svc, ora, lay, nb, 24)
+    for e in (svc, imm):
+        e.close()

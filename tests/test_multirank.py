@@ -236,3 +236,61 @@ def test_collection_level_calls_are_rank_local():
         assert calls[:2] == [("run", local), ("step", local)], calls
         if not isinstance(x, dmt.BiBlock):  # a BiBlock reads its ll directly
             assert ("fetch", local) in calls[2:], calls
+
+
+def _gpu_worker(rank, world, port, out_dir, B):
+    """One rank process: its libdmt shard on device 0 (both ranks share the one GPU of the
+    box), fetch_ll partials combined over gloo with the rank-order tree (shard.rank_tree)."""
+    import sys
+    for p in (ROOT, os.path.join(ROOT, "tests")):
+        sys.path.insert(0, p)
+    import torch.distributed as dist
+    import diffusionmcmctools_amd as dmt
+    from diffusionmcmctools_amd import workloads as W
+    from diffusionmcmctools_amd import shard
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    w = W.c3_fhn(B=B, N=200, T_burn=0.05, block_offset=rank)
+    w.meta["hist_len"] = ITERS
+    e = dmt.Ensemble(w.model.kind, w.d, w.m, w.n_points, precision=w.precision, seed=SEED,
+                     grid_shared=w.grid_shared)
+    e.set_shard(rank * B)
+    lay = W.fill(e, w, init_Z=True)
+    e.loglikhd(lay, 0, 0, B)
+    res = e.mcmc_run(lay, 0, B, 1, ITERS, salt=3, local=True)   # this rank's partials
+    allres = [None] * world
+    dist.all_gather_object(allres, res.tolist())
+    comb = [[shard.rank_tree([allres[r][i][c] for r in range(world)]) for c in range(3)]
+            for i in range(ITERS)]
+    np.save(os.path.join(out_dir, f"X{rank}.npy"), e.download_paths(0, 0))
+    if rank == 0:
+        np.save(os.path.join(out_dir, "comb.npy"), np.array(comb))
+    e.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_gpu_two_rank_processes_match_unsharded(tmp_path):
+    """Two rank PROCESSES (gloo control plane, world size 2), each with its own libdmt handle
+    on the box's one GPU holding one recording shard: paths and the rank-tree fetch_ll of every
+    iteration equal one process's unsharded ensemble bit for bit — the multi-process form of
+    the N-GPU job on real hardware (the RCCL all-gather itself needs one GPU per rank)."""
+    import torch.multiprocessing as mp
+    import diffusionmcmctools_amd as dmt
+    from diffusionmcmctools_amd import workloads as W
+    world, B = 2, 256  # power-of-two blocks per rank: the rank tree is a subtree split
+    mp.start_processes(_gpu_worker, args=(world, _free_port(), str(tmp_path), B), nprocs=world,
+                       join=True, start_method="spawn")
+    g = W.concat_workloads([W.c3_fhn(B=B, N=200, T_burn=0.05, block_offset=r)
+                            for r in range(world)])
+    g.meta["hist_len"] = ITERS
+    e = dmt.Ensemble(g.model.kind, g.d, g.m, g.n_points, precision=g.precision, seed=SEED,
+                     grid_shared=g.grid_shared)
+    lay = W.fill(e, g, init_Z=True)
+    e.loglikhd(lay, 0, 0, g.nblocks)
+    full = e.mcmc_run(lay, 0, g.nblocks, 1, ITERS, salt=3)
+    np.testing.assert_array_equal(np.load(tmp_path / "comb.npy"), full)
+    X = np.concatenate([np.load(tmp_path / f"X{r}.npy") for r in range(world)])
+    np.testing.assert_array_equal(X, e.download_paths(0, 0))
+    e.close()
