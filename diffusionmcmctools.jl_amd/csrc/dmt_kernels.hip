@@ -1182,6 +1182,11 @@ __device__ __forceinline__ float lane_read(float v, int addr) {
 // Store one point's N components (16-byte stores when N is even and T is double).
 template <int N, class T>
 __device__ __forceinline__ void store_row(T* p, const T* v) {
+#if defined(DMT_PATH_STORE_WT)  // experiment: write-through path stores
+#pragma unroll
+  for (int c = 0; c < N; ++c) __hip_atomic_store(p + c, v[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return;
+#endif
   if constexpr (std::is_same<T, double>::value && N % 2 == 0) {
 #pragma unroll
     for (int c = 0; c < N; c += 2) *reinterpret_cast<double2*>(p + c) = make_double2(v[c], v[c + 1]);

@@ -37,7 +37,7 @@ import DiffusionMCMCTools: draw_proposal_path!, accept_reject_proposal_path!, lo
 # device-only names (everything the reference's callers use is a method of its own functions)
 export DeviceSamplingEnsemble, DeviceSamplingPair, DeviceSamplingUnit, DeviceBlockEnsemble,
     DeviceBlockCollection, DeviceBiBlock, DeviceBlock, use_device!, mcmc_step!, mcmc_run!,
-    download_XX, download_WW, upload_obs!, snapshot_every!, law_record, guiding_linear
+    download_XX, download_WW, upload_obs!, snapshot_every!, law_record, guiding_linear, sync
 
 const libdmt = get(ENV, "DMT_LIB", joinpath(@__DIR__, "..", "libdmt.so"))
 
@@ -129,6 +129,14 @@ mutable struct DeviceSamplingEnsemble
         se
     end
 end
+
+"""
+    sync(x)
+
+Wait for the ensemble's queued device work and stop a resident service launch (include/dmt.h,
+"Resident service"): call it before a device-wide synchronisation issued outside libdmt.
+"""
+sync(se::DeviceSamplingEnsemble) = check(ccall((:dmt_sync, libdmt), Int32, (Ptr{Cvoid},), se.h))
 
 "Concatenate per-segment trajectories (Vector{SVector}) recording-major into one flat buffer."
 flatten_paths(segs) = reduce(vcat, (collect(reinterpret(Float64, s)) for s in segs))
@@ -635,6 +643,8 @@ end
 _n(x::DeviceBlocks) = x.b1 - x.b0
 
 # ---- imputation and MH (src/biblock.jl:78-127, block_collection.jl:46-68, block_ensemble.jl:50-69)
+sync(x::DeviceBlocks) = sync(x.se)
+
 """
     draw_proposal_path!(x; Z=nothing, iter=nothing, salt=nothing)
 
