@@ -30,6 +30,7 @@ K_DRAW, K_ACCEPT, K_PATHLL, K_RECOMPUTE, K_REDUCE = 0, 1, 2, 3, 4
 RNG_AUTO = 0xFFFFFFFF
 SALT_LIMIT = 0x40000000
 LAW_STRIDE = 64
+LAW_AUXTD = 15  # DMT_LAW_AUXTD: time-dependent auxiliary law (dmt_upload_aux)
 LAW_THETA, LAW_SIGMA, LAW_A, LAW_BT, LAW_BETA, LAW_DA, LAW_C0, LAW_TRACE = 0, 16, 25, 31, 40, 43, 49, 50
 LAW_SIGINV = 51
 LAW_ANCHOR = 60
@@ -46,7 +47,7 @@ SYMBOLS = [
     "dmt_draw_proposal", "dmt_accept_reject", "dmt_loglikhd", "dmt_recompute_path", "dmt_find_W_for_X", "dmt_upload_obs", "dmt_set_obs",
     "dmt_recompute_guiding_term", "dmt_set_proposal_law", "dmt_download_law", "dmt_swap",
     "dmt_save_ll", "dmt_set_accepted", "dmt_get_block_state", "dmt_set_block_state",
-    "dmt_fetch_ll", "dmt_mcmc_step", "dmt_mcmc_run", "dmt_guiding_linear", "dmt_comm_unique_id", "dmt_comm_init", "dmt_set_shard", "dmt_sync",
+    "dmt_fetch_ll", "dmt_mcmc_step", "dmt_mcmc_run", "dmt_guiding_linear", "dmt_guiding_linear_td", "dmt_upload_aux", "dmt_comm_unique_id", "dmt_comm_init", "dmt_set_shard", "dmt_sync",
     "dmt_set_timing", "dmt_get_timing", "dmt_memory_bytes", "dmt_debug_philox",
     "dmt_debug_normals", "dmt_last_error", "dmt_version", "dmt_snapshot_reserve",
     "dmt_snapshot_take", "dmt_snapshot_download", "dmt_snapshot_write", "dmt_set_ll",
@@ -119,6 +120,8 @@ _SIGS = {
     "dmt_fetch_ll": [_P, _i32, _i64, _i64, _i64, _pd, _pd, _pi64],
     "dmt_mcmc_step": [_P, _i32, _i64, _i64, _i64, _u32, _pd, _pd, _pi64],
     "dmt_guiding_linear": [_i32, _pd, _pd, _pd, _i32, _pd, _pd, _pd, C.c_double, _pd, _pd, _pd],
+    "dmt_guiding_linear_td": [_i32, _pd, _pd, _i32, _pd, _pd, _pd, C.c_double, _pd, _pd, _pd],
+    "dmt_upload_aux": [_P, _i32, _pd],
     "dmt_comm_unique_id": [_pu8],
     "dmt_comm_init": [_P, _i32, _i32, _pu8],
     "dmt_mcmc_run": [_P, _i32, _i64, _i64, _i64, _i64, _u32, _pd],

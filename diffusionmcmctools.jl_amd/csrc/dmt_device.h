@@ -91,6 +91,7 @@ struct Law {
   T da[HP];
   T thmu[D];  // Theta·mu of a linear (OU) drift, canonical order
   bool trace;
+  bool auxtd;  // DMT_LAW_AUXTD: B̃, β̃ per step from the per-point table (dmt_upload_aux)
   // non-linear drift with σ exactly the identity (d = m; C5's Lorenz): canonical M = H, c = F,
   // σ·dW = dW, which the lane kernels take as a wave-uniform fast path
   bool unit;
@@ -110,6 +111,7 @@ struct Law {
 #pragma unroll
     for (int i = 0; i < HP; ++i) da[i] = (T)ldc(L + DMT_LAW_DA + i);
     trace = ldc(L + DMT_LAW_TRACE) != 0.0;
+    auxtd = !Mdl::kLinear && ldc(L + DMT_LAW_AUXTD) != 0.0;
     unit = !Mdl::kLinear && D == M;
 #pragma unroll
     for (int p = 0; p < D; ++p)
@@ -168,10 +170,11 @@ __device__ __forceinline__ void guide_coeffs_unit(const T* H, const T* F, T* Mg,
   }
 }
 
-// G(t_i, x_i) of the Girsanov weight; returns G, writes r = F - Hx and the drift b.
+// G(t_i, x_i) of the Girsanov weight with the auxiliary drift B̃x + β̃ given (a time-dependent
+// auxiliary law: step i's B̃(t_i), β̃(t_i)); returns G, writes r = F - Hx and the drift b.
 template <class Mdl, class T>
-__device__ __forceinline__ T g_at(const Law<Mdl, T>& L, const T* H, const T* F, const T* x, T* r,
-                                  T* b) {
+__device__ __forceinline__ T g_at_aux(const Law<Mdl, T>& L, const T* H, const T* F, const T* x,
+                                      T* r, T* b, const T* Bt, const T* beta) {
   constexpr int D = Mdl::D;
 #pragma unroll
   for (int p = 0; p < D; ++p) {
@@ -184,9 +187,9 @@ __device__ __forceinline__ T g_at(const Law<Mdl, T>& L, const T* H, const T* F, 
   T db[D];
 #pragma unroll
   for (int p = 0; p < D; ++p) {
-    T bt = L.beta[p];
+    T bt = beta[p];
 #pragma unroll
-    for (int q = 0; q < D; ++q) bt = dfma(L.Bt[p * D + q], x[q], bt);
+    for (int q = 0; q < D; ++q) bt = dfma(Bt[p * D + q], x[q], bt);
     db[p] = b[p] - bt;
   }
   T G = db[0] * r[0];
@@ -205,6 +208,29 @@ __device__ __forceinline__ T g_at(const Law<Mdl, T>& L, const T* H, const T* F, 
     G = dfma((T)-0.5, tr, G);
   }
   return G;
+}
+// G with the law's own (time-homogeneous) auxiliary drift
+template <class Mdl, class T>
+__device__ __forceinline__ T g_at(const Law<Mdl, T>& L, const T* H, const T* F, const T* x, T* r,
+                                  T* b) {
+  return g_at_aux<Mdl, T>(L, H, F, x, r, b, L.Bt, L.beta);
+}
+// The auxiliary drift of one step: the law's B̃, β̃, or — where the lane's law is time-dependent
+// (DMT_LAW_AUXTD) — the step's row of the per-point table, component c at row[c * cstride]
+template <class Mdl, class T, class Ld>
+__device__ __forceinline__ void aux_step(const Law<Mdl, T>& L, const T* row, int64_t cstride,
+                                         T* Bt, T* beta, Ld ld) {
+  constexpr int D = Mdl::D;
+#pragma unroll
+  for (int c = 0; c < D * D; ++c) {
+    const T v = ld(&row[c * cstride]);
+    Bt[c] = L.auxtd ? v : L.Bt[c];
+  }
+#pragma unroll
+  for (int p = 0; p < D; ++p) {
+    const T v = ld(&row[(D * D + p) * cstride]);
+    beta[p] = L.auxtd ? v : L.beta[p];
+  }
 }
 
 // sigma·dW of one step (canonical: sdW_a = s_a0 dW_0, then fma over k)

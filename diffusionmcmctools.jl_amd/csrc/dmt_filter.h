@@ -318,14 +318,21 @@ DMT_HD bool filter_combine(const Trans<N>& q, Mat<N>& Hc, double* Fc, double& cc
 // (k_filter_scan / k_filter_chain); this is the serial host statement of the same arithmetic.
 constexpr int kFiltChunk = 64;
 
-template <int N, class TimeAt, class Store>
-inline bool filter_segment(const Mat<N>& B, const double* beta, const Mat<N>& A, int npts,
-                           TimeAt tat, Mat<N>& Hc, double* Fc, double& cc, Store store) {
+// Coef(i, B, beta): the auxiliary drift of step i (constant, or a time-dependent law's
+// coefficients at the step's left point t_i).
+template <int N, class TimeAt, class Coef, class Store>
+inline bool filter_segment(Coef coef, const Mat<N>& A, int npts, TimeAt tat, Mat<N>& Hc,
+                           double* Fc, double& cc, Store store) {
   store(npts - 1, Hc, Fc, cc);
   Trans<N> Q[kFiltChunk], Qn[kFiltChunk];
   for (int hi = npts - 1; hi > 0; hi -= kFiltChunk) {
     const int lo = hi > kFiltChunk ? hi - kFiltChunk : 0, cnt = hi - lo;
-    for (int l = 0; l < cnt; ++l) Q[l] = step_trans(B, beta, A, tat(lo + l + 1) - tat(lo + l));
+    for (int l = 0; l < cnt; ++l) {
+      Mat<N> B;
+      double beta[N];
+      coef(lo + l, B, beta);
+      Q[l] = step_trans(B, beta, A, tat(lo + l + 1) - tat(lo + l));
+    }
     for (int k = 1; k < kFiltChunk; k *= 2) {
       for (int l = 0; l < cnt; ++l) Qn[l] = (l + k < cnt) ? compose(Q[l], Q[l + k]) : Q[l];
       for (int l = 0; l < cnt; ++l) Q[l] = Qn[l];

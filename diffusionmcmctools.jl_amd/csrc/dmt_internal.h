@@ -65,6 +65,7 @@ struct BlockArgs {
   int H_shared[2][2];
   const T* F[2][2];
   const double* law[2][2];
+  const T* aux[2];  // [kind] per-point B̃(t_i), β̃(t_i) (dmt_upload_aux), nullptr: none
   // layout
   const int64_t* blk_off;  // [R + 1]
   const int32_t* blk_rec;  // [nblocks] recording of each block
@@ -157,6 +158,7 @@ struct FilterArgs {
   double* law[2][2];
   const void* t;  // grid (T)
   int t_shared;
+  const void* aux[2];  // [kind] per-point B̃(t_i), β̃(t_i) (T), nullptr: none
   const double* obsH;  // [G][hp] information of the observation at each segment's end
   const double* obsF;  // [G][d]
   const double* obsc;  // [G]

@@ -112,10 +112,11 @@ __device__ __forceinline__ void pair_exchange<double>(double v, double& lo, doub
   hi = __longlong_as_double((long long)(((uint64_t)h[1] << 32) | l[1]));
 }
 
-template <class Mdl, class T, int MODE, bool PARITY, int K, bool PAIR = false>
+template <class Mdl, class T, int MODE, bool PARITY, int K, bool PAIR = false, bool TD = false>
 __device__ __forceinline__ bool run_segment(const Law<Mdl, T>& L, const T* __restrict__ tpl,
                                             const int t_sh, const T* __restrict__ Ht,
                                             const int H_sh, const T* __restrict__ Ft,
+                                            const T* __restrict__ At,
                                             const T* Ws, T* Wd, T* Xd, const double* __restrict__ Zg,
                                             const T* Xcs, T* Xcd, T* Wcd,
                                             NormalStream<T>& ns, const int64_t tq, const int64_t q0,
@@ -135,6 +136,13 @@ __device__ __forceinline__ bool run_segment(const Law<Mdl, T>& L, const T* __res
   const T* Wsb = Ws + row * M * kLanes + lane;
   T* Wdb = Wd + row * M * kLanes + lane;
   T* Xdb = Xd + row * D * kLanes + lane;
+  // time-dependent auxiliary law (DMT_LAW_AUXTD): step i's B̃(t_i), β̃(t_i) from the per-point
+  // table; wave-uniform, so a time-homogeneous ensemble takes the branch-free path
+  // (TD: the ensemble has a per-point table; a separate instantiation, so that a
+  // time-homogeneous ensemble runs the kernel without it)
+  constexpr int CA = D * D + D;
+  const T* Ab = (TD && At) ? At + row * CA * kLanes + lane : nullptr;
+  const bool td = TD && Ab != nullptr && __ballot(L.auxtd) != 0;
   // tile-phase repair: a lane whose u lives in the "wrong" buffer copies u.X
   // (Xcs -> Xcd) and u.W (-> Wcd) to the tile's u buffer while its proposal goes to the
   // tile's proposal buffer; nullptr = nothing to copy
@@ -214,7 +222,19 @@ __device__ __forceinline__ bool run_segment(const Law<Mdl, T>& L, const T* __res
       }
     }
     T r[D], b[D], sdW[D], Mg[D * D], cg[D];
-    const T G = g_at<Mdl, T>(L, Hi, Fi, x, r, b);
+    T G;
+    if constexpr (TD) {
+      if (td) {
+        T Bq[D * D], bq[D];
+        aux_step<Mdl, T>(L, Ab + (int64_t)i * CA * kLanes, kLanes, Bq, bq,
+                         [](const T* p) { return lane_ld(p); });
+        G = g_at_aux<Mdl, T>(L, Hi, Fi, x, r, b, Bq, bq);
+      } else {
+        G = g_at<Mdl, T>(L, Hi, Fi, x, r, b);
+      }
+    } else {
+      G = g_at<Mdl, T>(L, Hi, Fi, x, r, b);
+    }
     bool fast = false;
     if constexpr (!Mdl::kLinear && D == M) {
       if (all_unit) {  // every lane's law has σ = I: M = H, c = F, σ·dW = dW (canonical)
@@ -323,7 +343,7 @@ __device__ __forceinline__ bool map_block(const BlockArgs<T>& a, int64_t& tile, 
 
 // The lane kernel's body for block blk of recording tile `tile`, recording slot `lane` of the
 // tile (the lane-interleaved layout's column); PAIR: two lanes (roles) per recording.
-template <class Mdl, class T, int MODE, bool PARITY, int K, bool PAIR>
+template <class Mdl, class T, int MODE, bool PARITY, int K, bool PAIR, bool TD = false>
 __device__ __forceinline__ void lane_block(const BlockArgs<T>& a, const int64_t tile,
                                            const int64_t blk, const int lane, const int role) {
   constexpr int D = Mdl::D, M = Mdl::M, HP = D * (D + 1) / 2;
@@ -392,8 +412,9 @@ __device__ __forceinline__ void lane_block(const BlockArgs<T>& a, const int64_t 
       }
     }
     T sl;
-    const bool sok = run_segment<Mdl, T, MODE, PARITY, K, PAIR>(
-        L, a.t, a.t_shared, a.H[ls][kind], a.H_shared[ls][kind], a.F[ls][kind], Ws, Wd, Xd, Zg,
+    const bool sok = run_segment<Mdl, T, MODE, PARITY, K, PAIR, TD>(
+        L, a.t, a.t_shared, a.H[ls][kind], a.H_shared[ls][kind], a.F[ls][kind], a.aux[kind], Ws,
+        Wd, Xd, Zg,
         Xcs, Xcd, Wcd, ns, tq, a.seg_q[g], a.seg_np[g], lane, rho, srho, a.ll_skip, x, sl, role);
     if (MODE == MODE_PCN) {
       if (nsx != sx) a.selX[g] = (uint8_t)nsx;
@@ -408,11 +429,11 @@ __device__ __forceinline__ void lane_block(const BlockArgs<T>& a, const int64_t 
   }
 }
 
-template <class Mdl, class T, int MODE, bool PARITY, int K>
+template <class Mdl, class T, int MODE, bool PARITY, int K, bool TD = false>
 __global__ __launch_bounds__(64) void k_block(const BlockArgs<T> a) {
   int64_t tile, blk;
   if (!map_block(a, tile, blk)) return;
-  lane_block<Mdl, T, MODE, PARITY, K, false>(a, tile, blk, threadIdx.x, 0);
+  lane_block<Mdl, T, MODE, PARITY, K, false, TD>(a, tile, blk, threadIdx.x, 0);
 }
 
 // ---- MAP_LANE, pair mapping: two waves per (recording tile, block index), each
@@ -715,7 +736,7 @@ __global__ __launch_bounds__(128, DMT_PS_MINW) void k_block_ps(const BlockArgs<T
 }
 
 // Girsanov log-weight of a stored path (loglikhd!), same summation order as k_block.
-template <class Mdl, class T, int K>
+template <class Mdl, class T, int K, bool TD = false>
 __global__ __launch_bounds__(64) void k_pathll(const BlockArgs<T> a) {
   constexpr int D = Mdl::D, HP = D * (D + 1) / 2;
   int64_t tile, blk;
@@ -753,6 +774,9 @@ __global__ __launch_bounds__(64) void k_pathll(const BlockArgs<T> a) {
     const T* __restrict__ Xs = a.X[a.selX[g] ^ a.xs_flip];
     const int64_t q0 = a.seg_q[g];
     const int nst = a.seg_np[g] - 1;
+    constexpr int CA = D * D + D;  // time-dependent auxiliary law (run_segment)
+    const T* At = TD ? a.aux[kind] : nullptr;
+    const bool td = TD && At != nullptr && __ballot(L.auxtd) != 0;
     PSum<T> ps;
     ps.init();
     T tcur = tload(q0);
@@ -774,7 +798,19 @@ __global__ __launch_bounds__(64) void k_pathll(const BlockArgs<T> a) {
         if (c0 + j < nst) {
           const T dt = vt[j] - tcur;
           T r[D], b[D];
-          const T G = g_at<Mdl, T>(L, vH[j], vF[j], vX[j], r, b);
+          T G;
+          if constexpr (TD) {
+            if (td) {
+              T Bq[D * D], bq[D];
+              aux_step<Mdl, T>(L, At + idx(q0 + c0 + j, 0, CA), kLanes, Bq, bq,
+                               [](const T* p) { return *p; });
+              G = g_at_aux<Mdl, T>(L, vH[j], vF[j], vX[j], r, b, Bq, bq);
+            } else {
+              G = g_at<Mdl, T>(L, vH[j], vF[j], vX[j], r, b);
+            }
+          } else {
+            G = g_at<Mdl, T>(L, vH[j], vF[j], vX[j], r, b);
+          }
           ps.add(G * dt);
           tcur = vt[j];
         }
@@ -1068,7 +1104,17 @@ __global__ __launch_bounds__(128) void k_block_wave(const BlockArgs<T> a) {
     for (int c = 0; c < HP; ++c) Hi[c] = rw[1 + c];
 #pragma unroll
     for (int c = 0; c < D; ++c) { Fi[c] = rw[1 + HP + c]; xi[c] = sh.xcap[k & 1][lane][c]; }
-    const T G = g_at<Mdl, T>(LB, Hi, Fi, xi, rr, bb);
+    T G;
+    if (a.aux[kind] && LB.auxtd) {  // time-dependent auxiliary law: step i's B̃(t_i), β̃(t_i)
+      constexpr int CA = D * D + D;
+      const int i = c0 + (valid ? lane : cnt - 1);
+      T Bq[D * D], bq[D];
+      aux_step<Mdl, T>(LB, a.aux[kind] + (tq + a.seg_q[g] + i) * CA, 1, Bq, bq,
+                       [](const T* p) { return *p; });
+      G = g_at_aux<Mdl, T>(LB, Hi, Fi, xi, rr, bb, Bq, bq);
+    } else {
+      G = g_at<Mdl, T>(LB, Hi, Fi, xi, rr, bb);
+    }
     const bool inll = MODE != MODE_RECOMPUTE || c0 + lane < nst - a.ll_skip;  // skip
     const T csum = wave_tree_sum<T>((valid && inll) ? G * rw[0] : (T)0);
     seg_acc = seg_acc + (csum + (T)0);
@@ -2772,7 +2818,15 @@ __global__ __launch_bounds__(64) void k_pathll_wave(const BlockArgs<T> a) {
       for (int c = 0; c < HP; ++c) Hi[c] = Hb[(int64_t)i * HP + c];
 #pragma unroll
       for (int c = 0; c < D; ++c) { Fi[c] = Fb[(int64_t)i * D + c]; xi[c] = Xb[(int64_t)i * D + c]; }
-      const T G = g_at<Mdl, T>(L, Hi, Fi, xi, rr, bb);
+      T G;
+      if (a.aux[kind] && L.auxtd) {  // time-dependent auxiliary law (k_block_wave)
+        constexpr int CA = D * D + D;
+        T Bq[D * D], bq[D];
+        aux_step<Mdl, T>(L, a.aux[kind] + (row + i) * CA, 1, Bq, bq, [](const T* p) { return *p; });
+        G = g_at_aux<Mdl, T>(L, Hi, Fi, xi, rr, bb, Bq, bq);
+      } else {
+        G = g_at<Mdl, T>(L, Hi, Fi, xi, rr, bb);
+      }
       const T csum = wave_tree_sum<T>(valid ? G * dt : (T)0);
       acc = acc + (csum + (T)0);
     }
@@ -2968,9 +3022,10 @@ __global__ void k_filter_mark(const FilterArgs a) {
 
 template <int D>
 __device__ __forceinline__ void filt_law(const FilterArgs& a, int g, int kind, flt::Mat<D>& B,
-                                         double* beta, flt::Mat<D>& At, int& slot) {
+                                         double* beta, flt::Mat<D>& At, int& slot, bool& td) {
   slot = (kind ? a.selPPB[g] : a.selPP[g]) ^ a.unit;
   const double* lr = a.law[slot][kind] + (int64_t)g * DMT_LAW_STRIDE;
+  td = a.aux[kind] != nullptr && lr[DMT_LAW_AUXTD] != 0.0;
 #pragma unroll
   for (int p = 0; p < D; ++p) {
     beta[p] = lr[DMT_LAW_BETA + p];
@@ -2981,6 +3036,17 @@ __device__ __forceinline__ void filt_law(const FilterArgs& a, int g, int kind, f
       At(p, q) = lr[DMT_LAW_A + e] - lr[DMT_LAW_DA + e];  // ã = a − (a − ã)
     }
   }
+}
+
+// A time-dependent auxiliary law's B̃(t_i), β̃(t_i) (the per-point table, element c of point q
+// at tab[ix(q, c)]) as the filter's doubles
+template <int D, class T, class Ix>
+__device__ __forceinline__ void filt_aux_step(const T* tab, Ix ix, int64_t q, flt::Mat<D>& B,
+                                              double* beta) {
+#pragma unroll
+  for (int c = 0; c < D * D; ++c) B.a[c] = (double)tab[ix(q, c)];
+#pragma unroll
+  for (int p = 0; p < D; ++p) beta[p] = (double)tab[ix(q, D * D + p)];
 }
 
 // chunk j of a segment with np points: steps [lo, lo + cnt), counted from the segment end
@@ -3023,7 +3089,8 @@ __global__ __launch_bounds__(256) void k_filter_scan(const FilterArgs a, int64_t
   flt::Mat<D> B, At;
   double beta[D];
   int slot;
-  filt_law<D>(a, g, sel - 1, B, beta, At, slot);
+  bool td;
+  filt_law<D>(a, g, sel - 1, B, beta, At, slot, td);
   int lo, cnt;
   filt_chunk(a.seg_np[g], (int)(item - a.fchunk_off[g]), lo, cnt);
   const int64_t r = a.seg_rec[g];
@@ -3035,6 +3102,12 @@ __global__ __launch_bounds__(256) void k_filter_scan(const FilterArgs a, int64_t
   };
   flt::Trans<D> q;
   if (lane < cnt) {
+    if (td) {
+      constexpr int CA = D * D + D;
+      filt_aux_step<D>((const T*)a.aux[sel - 1],
+                       [&](int64_t qq, int c) { return ((tq + qq) * CA + c) * a.tw + rl; },
+                       lo + lane, B, beta);
+    }
     q = flt::step_trans<D>(B, beta, At, tat(lo + lane + 1) - tat(lo + lane));
   } else {
     q.Phi = flt::meye<D>();
@@ -3355,7 +3428,8 @@ __global__ __launch_bounds__(256) void k_filter_fused(const FilterArgs a) {
     M B, At;
     double beta[D];
     int slot;
-    filt_law<D>(a, g, cur.kind, B, beta, At, slot);
+    bool td;
+    filt_law<D>(a, g, cur.kind, B, beta, At, slot, td);
     M HT;
     double FT[D], cT = cur.oc;
 #pragma unroll
@@ -3406,7 +3480,17 @@ __global__ __launch_bounds__(256) void k_filter_fused(const FilterArgs a) {
       filt_chunk(cur.np, j, lo, cnt);
       flt::Trans<D> q;
       if (lane < cnt) {
-        q = flt::step_trans<D>(B, beta, At, tat(lo + lane + 1) - tat(lo + lane));
+        M Bq = B;
+        double bq[D];
+#pragma unroll
+        for (int p = 0; p < d; ++p) bq[p] = beta[p];
+        if (td) {
+          constexpr int CA = D * D + D;
+          filt_aux_step<D>((const T*)a.aux[cur.kind],
+                           [&](int64_t qq, int c) { return ix(cur.q0 + qq, c, CA); }, lo + lane, Bq,
+                           bq);
+        }
+        q = flt::step_trans<D>(Bq, bq, At, tat(lo + lane + 1) - tat(lo + lane));
       } else {
         q.Phi = flt::meye<D>();
         q.K = flt::mzero<D>();
@@ -3835,6 +3919,23 @@ static hipError_t launch_block_t(int mapping, int mode, const void* args, int64_
     }
     const dim3 block(64);
     const bool par = a.Z != nullptr;
+    if (a.aux[0] || a.aux[1]) {  // time-dependent auxiliary laws: the TD instantiation
+      switch (mode) {
+        case MODE_PCN:
+          if (par) dlaunch(k_block<Mdl, T, MODE_PCN, true, kChunk, true>, grid, block, s, a);
+          else dlaunch(k_block<Mdl, T, MODE_PCN, false, kChunk, true>, grid, block, s, a);
+          break;
+        case MODE_RECOMPUTE:
+          dlaunch(k_block<Mdl, T, MODE_RECOMPUTE, false, kChunk, true>, grid, block, s, a);
+          break;
+        case MODE_FRESH:
+          if (par) dlaunch(k_block<Mdl, T, MODE_FRESH, true, kChunk, true>, grid, block, s, a);
+          else dlaunch(k_block<Mdl, T, MODE_FRESH, false, kChunk, true>, grid, block, s, a);
+          break;
+        default: return hipErrorInvalidValue;
+      }
+      return hipGetLastError();
+    }
     if (!par && a.lane_pair && (mode == MODE_PCN || mode == MODE_FRESH)) {  // lane pairs
       const dim3 pgrid((unsigned)(2 * nwaves));
       if (mode == MODE_PCN) dlaunch(k_block_pair<Mdl, T, MODE_PCN>, pgrid, block, s, a);
@@ -3981,8 +4082,12 @@ static hipError_t launch_pathll_t(int mapping, const void* args, int64_t nwaves,
   if (nwaves <= 0) return hipSuccess;
   if (Mdl::kLinear || mapping == MAP_WAVE)
     dlaunch(k_pathll_wave<Mdl, T>, dim3((unsigned)nwaves), dim3(64), s, a);
-  else if constexpr (!Mdl::kLinear)
-    dlaunch(k_pathll<Mdl, T, kChunk>, dim3((unsigned)nwaves), dim3(64), s, a);
+  else if constexpr (!Mdl::kLinear) {
+    if (a.aux[0] || a.aux[1])  // time-dependent auxiliary laws: the TD instantiation
+      dlaunch(k_pathll<Mdl, T, kChunk, true>, dim3((unsigned)nwaves), dim3(64), s, a);
+    else
+      dlaunch(k_pathll<Mdl, T, kChunk>, dim3((unsigned)nwaves), dim3(64), s, a);
+  }
   return hipGetLastError();
 }
 

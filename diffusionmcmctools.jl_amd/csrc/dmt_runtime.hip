@@ -177,6 +177,7 @@ struct dmt_ens {
   void* d_H[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};  // [slot][kind]
   int H_shared[2] = {0, 0};                                     // per kind
   void* d_F[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+  void* d_aux[2] = {nullptr, nullptr};  // [kind] per-point B̃(t_i), β̃(t_i) (dmt_upload_aux)
   double* d_law[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
   bool have_law[2][2] = {{false, false}, {false, false}};  // [unit][kind] uploaded at least once
   // observation information for the device backward filter (dmt_upload_obs / dmt_set_obs)
@@ -479,6 +480,8 @@ void fill_common(dmt_ens* h, const Layout* L, BlockArgs<T>& a) {
   }
   a.t = (const T*)h->d_t;
   a.t_shared = h->grid_shared;
+  a.aux[0] = (const T*)h->d_aux[0];
+  a.aux[1] = (const T*)h->d_aux[1];
   a.blk_off = L->d_blk_off;
   a.blk_rec = L->d_blk_rec;
   a.binfo = L->d_binfo;
@@ -1024,6 +1027,7 @@ dmt_status dmt_destroy(dmt_ens* h) {
     for (int k = 0; k < 2; ++k) {
       if (h->d_H[s][k] && !(s == 1 && h->d_H[1][k] == h->d_H[0][k])) (void)hipFree(h->d_H[s][k]);
       if (h->d_F[s][k]) (void)hipFree(h->d_F[s][k]);
+      if (s == 0 && h->d_aux[k]) (void)hipFree(h->d_aux[k]);
       if (h->d_law[s][k]) (void)hipFree(h->d_law[s][k]);
     }
   for (int k = 0; k < 2; ++k)
@@ -1161,6 +1165,36 @@ dmt_status dmt_upload_law(dmt_ens* h, int32_t unit, int32_t kind, const double* 
   }
   HIP_OK(stream_wait(h));
   if (H || F || laws) h->have_law[unit][kind] = true;
+  return DMT_OK;
+}
+
+dmt_status dmt_upload_aux(dmt_ens* h, int32_t kind, const double* aux) {
+  DMT_TRY(enter(h));
+  if (kind != DMT_LAW_PP && kind != DMT_LAW_PPB) return fail(DMT_ERR_INVALID, "bad kind");
+  if (h->key.model == DMT_MODEL_OU)
+    return fail(DMT_ERR_INVALID, "time-dependent auxiliary laws: non-linear drifts only (the OU "
+                                 "kernels' affine scan takes the auxiliary drift per segment)");
+  if (!aux) {
+    if (h->d_aux[kind]) {
+      HIP_OK(stream_wait(h));
+      (void)hipFree(h->d_aux[kind]);
+      h->bytes -= plane_elems(h, h->d * h->d + h->d) * (int64_t)h->esz;
+      h->d_aux[kind] = nullptr;
+    }
+    return DMT_OK;
+  }
+  const int C = (int)(h->d * h->d + h->d);
+  if (!h->d_aux[kind]) {
+    DMT_TRY(ens_alloc_bytes(h, &h->d_aux[kind], plane_elems(h, C) * h->esz));
+    HIP_OK(hipMemsetAsync(h->d_aux[kind], 0, plane_elems(h, C) * h->esz, h->stream));
+  }
+  DMT_TRY(ensure_stage(h, h->P * C));
+  HIP_OK(hipMemcpyAsync(h->d_stage, aux, h->P * C * 8, hipMemcpyHostToDevice, h->stream));
+  // one table for u and u°: both destinations of the per-segment copy are the table itself
+  HIP_OK(launch_to_planes(h->key.precision, h->tw, h->d_stage, h->d_aux[kind], h->d_aux[kind],
+                          h->d_sel[2 + kind], 0, C, h->P, h->d_pt_off, h->G, h->d_seg_rec,
+                          h->d_seg_q, h->d_tile_qoff, h->stream));
+  HIP_OK(stream_wait(h));  // the host buffer is the caller's
   return DMT_OK;
 }
 
@@ -2007,6 +2041,8 @@ static dmt_status guiding_term_device(dmt_ens* h, Layout* L, int64_t b0, int64_t
     }
   a.t = h->d_t;
   a.t_shared = h->grid_shared;
+  a.aux[0] = h->d_aux[0];
+  a.aux[1] = h->d_aux[1];
   a.obsH = h->d_obsH;
   a.obsF = h->d_obsF;
   a.obsc = h->d_obsc;
@@ -2377,13 +2413,13 @@ dmt_status dmt_set_rng_state(dmt_ens* h, uint64_t next, uint64_t last_draw, uint
 }  // extern "C"
 
 template <int D>
-static dmt_status guiding_linear_impl(const double* Bt, const double* beta, const double* at,
-                                      int32_t npts, const double* t, const double* HT,
-                                      const double* FT, double cT, double* H, double* F,
-                                      double* c) {
+// aux: nullptr (B̃ = Bt, β̃ = beta throughout) or [npts][d·d + d] per-point coefficients
+static dmt_status guiding_linear_impl(const double* Bt, const double* beta, const double* aux,
+                                      const double* at, int32_t npts, const double* t,
+                                      const double* HT, const double* FT, double cT, double* H,
+                                      double* F, double* c) {
   constexpr int d = D, hp = d * (d + 1) / 2;
-  flt::Mat<D> B = flt::mzero<D>(), A = flt::mzero<D>(), Hc = flt::mzero<D>();
-  for (int i = 0; i < d * d; ++i) B.a[i] = Bt[i];
+  flt::Mat<D> A = flt::mzero<D>(), Hc = flt::mzero<D>();
   for (int i = 0; i < d; ++i)
     for (int j = 0; j < d; ++j) {
       A(i, j) = at[dmt_packed(d, i, j)];
@@ -2400,7 +2436,13 @@ static dmt_status guiding_linear_impl(const double* Bt, const double* beta, cons
     for (int p = 0; p < d; ++p) F[(int64_t)i * d + p] = Fs[p];
     c[i] = cs;
   };
-  if (!flt::filter_segment<D>(B, beta, A, npts, [&](int i) { return t[i]; }, Hc, Fc, cc, store))
+  auto coef = [&](int i, flt::Mat<D>& B, double* be) {
+    const double* bs = aux ? aux + (int64_t)i * (d * d + d) : Bt;
+    const double* bb = aux ? bs + d * d : beta;
+    for (int k = 0; k < d * d; ++k) B.a[k] = bs[k];
+    for (int p = 0; p < d; ++p) be[p] = bb[p];
+  };
+  if (!flt::filter_segment<D>(coef, A, npts, [&](int i) { return t[i]; }, Hc, Fc, cc, store))
     return fail(DMT_ERR_INVALID, "singular I + HK in backward filter");
   return DMT_OK;
 }
@@ -2412,9 +2454,19 @@ dmt_status dmt_guiding_linear(int32_t d, const double* Bt, const double* beta, c
                               double cT, double* H, double* F, double* c) {
   if (d < 1 || d > 3 || npts < 1 || !Bt || !beta || !at || !t || !HT || !FT || !H || !F || !c)
     return fail(DMT_ERR_INVALID, "bad arguments to dmt_guiding_linear");
-  if (d == 1) return guiding_linear_impl<1>(Bt, beta, at, npts, t, HT, FT, cT, H, F, c);
-  if (d == 2) return guiding_linear_impl<2>(Bt, beta, at, npts, t, HT, FT, cT, H, F, c);
-  return guiding_linear_impl<3>(Bt, beta, at, npts, t, HT, FT, cT, H, F, c);
+  if (d == 1) return guiding_linear_impl<1>(Bt, beta, nullptr, at, npts, t, HT, FT, cT, H, F, c);
+  if (d == 2) return guiding_linear_impl<2>(Bt, beta, nullptr, at, npts, t, HT, FT, cT, H, F, c);
+  return guiding_linear_impl<3>(Bt, beta, nullptr, at, npts, t, HT, FT, cT, H, F, c);
+}
+
+dmt_status dmt_guiding_linear_td(int32_t d, const double* aux, const double* at, int32_t npts,
+                                 const double* t, const double* HT, const double* FT, double cT,
+                                 double* H, double* F, double* c) {
+  if (d < 1 || d > 3 || npts < 1 || !aux || !at || !t || !HT || !FT || !H || !F || !c)
+    return fail(DMT_ERR_INVALID, "bad arguments to dmt_guiding_linear_td");
+  if (d == 1) return guiding_linear_impl<1>(nullptr, nullptr, aux, at, npts, t, HT, FT, cT, H, F, c);
+  if (d == 2) return guiding_linear_impl<2>(nullptr, nullptr, aux, at, npts, t, HT, FT, cT, H, F, c);
+  return guiding_linear_impl<3>(nullptr, nullptr, aux, at, npts, t, HT, FT, cT, H, F, c);
 }
 
 dmt_status dmt_comm_unique_id(uint8_t* id_out) {

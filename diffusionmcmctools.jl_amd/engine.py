@@ -81,6 +81,14 @@ class Ensemble:
         L.call("dmt_upload_law", self._h, unit, kind, L.f64p(H), 1 if H_shared else 0,
                L.f64p(F), L.f64p(laws))
 
+    def upload_aux(self, kind, aux):
+        """dmt_upload_aux: per-point B̃(t_i), β̃(t_i) ([P][d·d + d]) of the laws of `kind` (u and
+        u° alike) for segments whose record has LAW_AUXTD set; None removes the table."""
+        aux = None if aux is None else np.ascontiguousarray(aux, dtype=np.float64)
+        if aux is not None and aux.size != self.P * (self.d * self.d + self.d):
+            raise ValueError("aux needs P·(d·d + d) values")
+        L.call("dmt_upload_aux", self._h, int(kind), L.f64p(aux))
+
     def set_paths(self, unit, X=None, W=None):
         X = None if X is None else np.ascontiguousarray(X, dtype=np.float64)
         W = None if W is None else np.ascontiguousarray(W, dtype=np.float64)
@@ -410,6 +418,25 @@ def guiding_linear(Bt, beta, at_packed, t, HT_packed, FT, cT):
     c = np.empty(n)
     L.call("dmt_guiding_linear", d, L.f64p(np.ascontiguousarray(Bt, dtype=np.float64).ravel()),
            L.f64p(np.ascontiguousarray(beta, dtype=np.float64)),
+           L.f64p(np.ascontiguousarray(at_packed, dtype=np.float64)), n, L.f64p(t),
+           L.f64p(np.ascontiguousarray(HT_packed, dtype=np.float64)),
+           L.f64p(np.ascontiguousarray(FT, dtype=np.float64)), float(cT), L.f64p(H), L.f64p(F),
+           L.f64p(c))
+    return H, F, c
+
+
+def guiding_linear_td(aux, at_packed, t, HT_packed, FT, cT):
+    """The host filter of a time-dependent auxiliary drift (dmt_guiding_linear_td):
+    aux[npts][d·d + d] = B̃(t_i), β̃(t_i), step i taking its left point's row."""
+    t = np.ascontiguousarray(t, dtype=np.float64)
+    n = t.size
+    aux = np.ascontiguousarray(aux, dtype=np.float64).reshape(n, -1)
+    d = {2: 1, 6: 2, 12: 3}[aux.shape[1]]
+    hp = d * (d + 1) // 2
+    H = np.empty((n, hp))
+    F = np.empty((n, d))
+    c = np.empty(n)
+    L.call("dmt_guiding_linear_td", d, L.f64p(aux),
            L.f64p(np.ascontiguousarray(at_packed, dtype=np.float64)), n, L.f64p(t),
            L.f64p(np.ascontiguousarray(HT_packed, dtype=np.float64)),
            L.f64p(np.ascontiguousarray(FT, dtype=np.float64)), float(cT), L.f64p(H), L.f64p(F),

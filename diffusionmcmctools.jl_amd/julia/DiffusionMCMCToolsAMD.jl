@@ -37,7 +37,8 @@ import DiffusionMCMCTools: draw_proposal_path!, accept_reject_proposal_path!, lo
 # device-only names (everything the reference's callers use is a method of its own functions)
 export DeviceSamplingEnsemble, DeviceSamplingPair, DeviceSamplingUnit, DeviceBlockEnsemble,
     DeviceBlockCollection, DeviceBiBlock, DeviceBlock, use_device!, mcmc_step!, mcmc_run!,
-    download_XX, download_WW, upload_obs!, snapshot_every!, law_record, guiding_linear, sync
+    download_XX, download_WW, upload_obs!, snapshot_every!, law_record, guiding_linear, sync,
+    upload_aux!
 
 const libdmt = get(ENV, "DMT_LIB", joinpath(@__DIR__, "..", "libdmt.so"))
 
@@ -243,15 +244,16 @@ unpacked(p::AbstractVector, d) = (M = zeros(d, d); k = 0;
     for i in 1:d, j in i:d; k += 1; M[i, j] = M[j, i] = p[k]; end; M)
 
 """
-    law_record(θrec, σ, B̃, β̃, σ̃, c0; anchor=nothing)
+    law_record(θrec, σ, B̃, β̃, σ̃, c0; anchor=nothing, time_dependent=false)
 
 One segment's law record (DMT_LAW_STRIDE doubles, include/dmt.h): θrec = the target's
 parameters in the device order (OU: Θ row-major at 1:d², μ at 10:9+d; FHN: 1/ϵ, s, γ, β, ϵ, σ;
 Lorenz: s, r, β), σ (d×m), the auxiliary law's B̃, β̃, σ̃, c(t₀), and the linearisation point
-of a linearised auxiliary law (FitzHughNagumoAux: y_T; Lorenz: x_T).
+of a linearised auxiliary law (FitzHughNagumoAux: y_T; Lorenz: x_T).  `time_dependent=true`:
+B̃(t), β̃(t) vary within the segment and come from `upload_aux!` (B̃, β̃ here: any one value).
 """
 function law_record(θrec, σ::AbstractMatrix, B̃::AbstractMatrix, β̃, σ̃::AbstractMatrix, c0;
-                    anchor=nothing)
+                    anchor=nothing, time_dependent=false)
     d, m = size(σ)
     hp = d * (d + 1) ÷ 2
     rec = zeros(DMT_LAW_STRIDE)
@@ -270,7 +272,22 @@ function law_record(θrec, σ::AbstractMatrix, B̃::AbstractMatrix, β̃, σ̃::
         rec[61:60+length(anchor)] .= anchor
         rec[64] = 1.0                                               # DMT_LAW_AUXLIN 63
     end
+    time_dependent && (rec[16] = 1.0)                               # DMT_LAW_AUXTD 15
     rec
+end
+
+"""
+    upload_aux!(se, kind, aux)
+
+Time-dependent auxiliary laws (dmt_upload_aux): `aux` is (d² + d) × P — column i holds
+B̃(t_i) (row-major) then β̃(t_i) at grid point i of every segment — for the laws of `kind`
+(0: PP, 1: PPb) of u and u°; `nothing` removes it.  Used by the segments whose law record has
+`time_dependent=true`.  Non-linear drifts only.
+"""
+function upload_aux!(se::DeviceSamplingEnsemble, kind, aux)
+    p(x) = x === nothing ? Ptr{Float64}(C_NULL) : pointer(x)
+    GC.@preserve aux check(ccall((:dmt_upload_aux, libdmt), Int32,
+        (Ptr{Cvoid}, Int32, Ptr{Float64}), se.h, kind, p(aux)))
 end
 
 """
@@ -290,6 +307,29 @@ function guiding_linear(B̃, β̃, σ̃, t::Vector{Float64}, HT::AbstractMatrix,
         (Int32, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Int32, Ptr{Float64}, Ptr{Float64},
          Ptr{Float64}, Float64, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}),
         d, Bt, β, at, n, t, HTp, FTv, cT, H, F, c))
+    permutedims(H), permutedims(F), c
+end
+
+"""
+    guiding_linear(B̃::Function, β̃::Function, σ̃, t, HT, FT, cT) -> (H, F, c)
+
+The guiding term of a time-dependent linear auxiliary law dX = (B̃(t)X + β̃(t))dt + σ̃dW:
+dmt_guiding_linear_td, each step's exact transition taking B̃, β̃ at its left point.
+"""
+function guiding_linear(B̃::Function, β̃::Function, σ̃, t::Vector{Float64}, HT::AbstractMatrix, FT, cT)
+    d, n = length(β̃(t[1])), length(t)
+    hp = d * (d + 1) ÷ 2
+    aux = Matrix{Float64}(undef, d * d + d, n)
+    for i in 1:n
+        aux[1:d*d, i] .= vec(permutedims(Float64.(B̃(t[i]))))
+        aux[d*d+1:end, i] .= Float64.(collect(β̃(t[i])))
+    end
+    at, HTp, FTv = packed(σ̃ * σ̃'), packed(HT), Float64.(collect(FT))
+    H, F, c = Matrix{Float64}(undef, hp, n), Matrix{Float64}(undef, d, n), Vector{Float64}(undef, n)
+    check(ccall((:dmt_guiding_linear_td, libdmt), Int32,
+        (Int32, Ptr{Float64}, Ptr{Float64}, Int32, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
+         Float64, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}),
+        d, aux, at, n, t, HTp, FTv, cT, H, F, c))
     permutedims(H), permutedims(F), c
 end
 

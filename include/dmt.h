@@ -80,11 +80,13 @@ enum { DMT_K_DRAW = 0, DMT_K_ACCEPT = 1, DMT_K_PATHLL = 2, DMT_K_RECOMPUTE = 3,
  * Law record: one per segment per (unit, kind), DMT_LAW_STRIDE doubles.
  * It carries the target-law parameters θ and the auxiliary (linear) law used
  * by the Girsanov weight.  Offsets:
- *   [0,16)  theta  model parameters
+ *   [0,15)  theta  model parameters
  *             OU:     Theta (d×d row-major) at 0, mu at 9
  *             FHN:    1/eps, s, gamma, beta, then the raw eps, σ at 4, 5
  *                     (σ also goes in sigma)
  *             Lorenz: s, r, beta
+ *   15      auxtd  1.0: the auxiliary drift varies within the segment — step i uses
+ *                  B̃(t_i), β̃(t_i) of the per-point table of dmt_upload_aux (Bt/beta unused)
  *   [16,25) sigma  d×m row-major (constant diffusion coefficient)
  *   [25,31) a      packed upper-triangular σσᵀ (row-major upper: 00,01,(02),11,(12),22)
  *   [31,40) Bt     auxiliary drift matrix B̃ (d×d row-major)
@@ -111,6 +113,7 @@ enum { DMT_K_DRAW = 0, DMT_K_ACCEPT = 1, DMT_K_PATHLL = 2, DMT_K_RECOMPUTE = 3,
 #define DMT_LAW_SIGINV 51
 #define DMT_LAW_ANCHOR 60
 #define DMT_LAW_AUXLIN 63
+#define DMT_LAW_AUXTD 15
 
 /* Parameter names of dmt_set_proposal_law (DiffusionDefinition's parameter order):
  *   FHN    (eps, s, gamma, beta, sigma), docs/src/tutorials/preamble.md:77
@@ -181,6 +184,17 @@ dmt_status dmt_upload_grid(dmt_ens* h, const double* t);
  *   F[P][d], laws[G][DMT_LAW_STRIDE].  Any of H/F/laws may be NULL to keep the previous one. */
 dmt_status dmt_upload_law(dmt_ens* h, int32_t unit, int32_t kind, const double* H,
                           int32_t H_shared, const double* F, const double* laws);
+
+/* Time-dependent linear auxiliary laws within a segment: the reference takes any linear
+ * auxiliary law of GuidedProposals (aux_laws, src/sampling_unit.jl:55-66), whose B̃(t), β̃(t)
+ * may vary in t.  aux[P][d·d + d] holds B̃(t_i) (row-major) then β̃(t_i) at every grid point
+ * of every segment (layout of dmt_upload_law's F) for the laws of kind PP or PPB, u and u° alike
+ * (the auxiliary law does not depend on θ).  A segment whose law record has DMT_LAW_AUXTD = 1.0
+ * takes step i's auxiliary drift B̃(t_i)x + β̃(t_i) (left point, frozen over [t_i, t_{i+1}]) in
+ * the Girsanov term G and in the backward filter's exact step transition
+ * (dmt_recompute_guiding_term); ã stays the record's (σ̃ constant per segment).  aux = NULL
+ * removes the table.  Non-linear drifts (FHN, Lorenz) only: DMT_ERR_INVALID for OU. */
+dmt_status dmt_upload_aux(dmt_ens* h, int32_t kind, const double* aux);
 
 /* Paths of unit u / u°: X[P][d], W[P][m]; NULL keeps the current one.  Used by
  * init_paths! (src/sampling_unit.jl:83-87) and find_W_for_X! (src/block.jl:118-131). */
@@ -391,6 +405,11 @@ dmt_status dmt_guiding_linear(int32_t d, const double* Bt, const double* beta,
                               const double* at, int32_t npts, const double* t,
                               const double* HT, const double* FT, double cT,
                               double* H, double* F, double* c);
+/* The same filter for a time-dependent auxiliary drift: aux[npts][d·d + d] = B̃(t_i), β̃(t_i);
+ * step i's exact transition takes the coefficients of its left point t_i (dmt_upload_aux). */
+dmt_status dmt_guiding_linear_td(int32_t d, const double* aux, const double* at, int32_t npts,
+                                 const double* t, const double* HT, const double* FT, double cT,
+                                 double* H, double* F, double* c);
 
 /* ---------------- multi-GPU (RCCL over xGMI) ---------------- */
 dmt_status dmt_comm_unique_id(uint8_t* id_out /*128 bytes*/);

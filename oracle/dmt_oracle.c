@@ -91,6 +91,7 @@
 #define L_DA 43
 #define L_C0 49
 #define L_TRACE 50
+#define L_AUXTD 15
 
 enum { ORC_OU = 0, ORC_FHN = 1, ORC_LORENZ = 2 };
 
@@ -369,6 +370,26 @@ void orc_set_ll_skip(int k) { orc_ll_skip = k; }
 extern int orc_ll_skip;
 #endif
 
+/* Time-dependent auxiliary law of the segment being solved (libdmt dmt_upload_aux; set by
+ * oracle.py around a segment call, NULL otherwise): rows [npts][d*d + d] = B~(t_i), beta~(t_i),
+ * used at step i (left point) in place of the record's Bt, beta when the record's auxtd
+ * (offset 15) is set.  Non-linear drifts only. */
+#if IS_F64
+const double* orc_aux = 0;
+void orc_set_aux(const double* p) { orc_aux = p; }
+#else
+extern const double* orc_aux;
+#endif
+static inline const REAL* aux_coeffs(const double* law, int model, int d, int i, const REAL* Bt,
+                                     const REAL* beta, REAL* Bq, REAL* bq, const REAL** bo) {
+    if (model == ORC_OU || !orc_aux || law[L_AUXTD] == 0.0) { *bo = beta; return Bt; }
+    const double* row = orc_aux + (size_t)i * (d * d + d);
+    for (int k = 0; k < d * d; ++k) Bq[k] = (REAL)row[k];
+    for (int p = 0; p < d; ++p) bq[p] = (REAL)row[d * d + p];
+    *bo = bq;
+    return Bq;
+}
+
 /* CPU-baseline switch (bench.py's cpu_baseline only): 1 = evaluate linear-drift segments
  * with the plain step-by-step Euler loop — the natural CPU algorithm, as the reference runs
  * it — instead of the canonical chunked scan (equal up to rounding; not used for parity). */
@@ -400,7 +421,10 @@ int SFX(orc_solve_segment)(int model, int d, int m, const double* law, int npts,
         const REAL* Hi = H + (size_t)i * h;
         const REAL* Fi = F + (size_t)i * d;
         REAL r[3] = {0, 0, 0}, b[3] = {0, 0, 0};
-        REAL G = g_at(model, d, th, a, Bt, beta, da, trace, Hi, Fi, x, r, b);
+        REAL Bq[9], bq[3];
+        const REAL* bu;
+        const REAL* Bu = aux_coeffs(law, model, d, i, Bt, beta, Bq, bq, &bu);
+        REAL G = g_at(model, d, th, a, Bu, bu, da, trace, Hi, Fi, x, r, b);
         ps_add(&ps, i < npts - 1 - orc_ll_skip ? G * dt : (REAL)0);
         REAL Mg[9], cg[3];
         guide_coeffs(model, d, th, a, Hi, Fi, Mg, cg, unit);
@@ -474,7 +498,10 @@ REAL SFX(orc_path_ll_segment)(int model, int d, int m, const double* law, int np
     for (int i = 0; i < npts - 1; ++i) {
         REAL dt = t[i + 1] - t[i];
         REAL r[3] = {0, 0, 0}, b[3] = {0, 0, 0};
-        REAL G = g_at(model, d, th, a, Bt, beta, da, trace, H + (size_t)i * h,
+        REAL Bq[9], bq[3];
+        const REAL* bu;
+        const REAL* Bu = aux_coeffs(law, model, d, i, Bt, beta, Bq, bq, &bu);
+        REAL G = g_at(model, d, th, a, Bu, bu, da, trace, H + (size_t)i * h,
                       F + (size_t)i * d, X + (size_t)i * d, r, b);
         ps_add(&ps, G * dt);
     }
@@ -1000,12 +1027,14 @@ static int fm_combine(const ftr_t* q, fm_t* Hc, double* Fc, double* cc) {
  * (stage k: Q_l <- compose(Q_l, Q_{l+k}) if l + k < cnt, previous-stage values), then every
  * point of the chunk by one combine from the chunk end's (H, F, c). */
 #define FILT_CHUNK 64
-int orc_backward_filter_segment(int d, const double* Bt, const double* beta, const double* at,
-                                int npts, const double* t, const double* HT, const double* FT,
-                                double cT, double* H, double* F, double* c) {
+/* aux: NULL (B~ = Bt, beta~ = beta on every step) or [npts][d*d + d] per-point coefficients
+ * of a time-dependent auxiliary law, step i taking row i (left point). */
+static int backward_filter(int d, const double* Bt, const double* beta, const double* aux,
+                           const double* at, int npts, const double* t, const double* HT,
+                           const double* FT, double cT, double* H, double* F, double* c) {
     int hp = d * (d + 1) / 2;
     fm_t B = fm_zero(d), A = fm_zero(d), Hc = fm_zero(d);
-    for (int i = 0; i < d * d; ++i) B.a[i] = Bt[i];
+    if (!aux) for (int i = 0; i < d * d; ++i) B.a[i] = Bt[i];
     for (int i = 0; i < d; ++i)
         for (int j = 0; j < d; ++j) { A.a[i * d + j] = at[pidx(d, i, j)]; Hc.a[i * d + j] = HT[pidx(d, i, j)]; }
     double Fc[3] = {0, 0, 0}, cc = cT;
@@ -1021,8 +1050,15 @@ int orc_backward_filter_segment(int d, const double* Bt, const double* beta, con
     ftr_t Q[FILT_CHUNK], Qn[FILT_CHUNK];
     for (int hi = npts - 1; hi > 0; hi -= FILT_CHUNK) {
         int lo = hi > FILT_CHUNK ? hi - FILT_CHUNK : 0, cnt = hi - lo;
-        for (int l = 0; l < cnt; ++l)
-            fm_transition(&B, beta, &A, t[lo + l + 1] - t[lo + l], &Q[l].Phi, Q[l].mu, &Q[l].K);
+        for (int l = 0; l < cnt; ++l) {
+            const double* bl = beta;
+            if (aux) {
+                const double* row = aux + (size_t)(lo + l) * (d * d + d);
+                for (int i = 0; i < d * d; ++i) B.a[i] = row[i];
+                bl = row + d * d;
+            }
+            fm_transition(&B, bl, &A, t[lo + l + 1] - t[lo + l], &Q[l].Phi, Q[l].mu, &Q[l].K);
+        }
         for (int k = 1; k < FILT_CHUNK; k *= 2) {
             for (int l = 0; l < cnt; ++l) Qn[l] = (l + k < cnt) ? ftr_compose(&Q[l], &Q[l + k]) : Q[l];
             for (int l = 0; l < cnt; ++l) Q[l] = Qn[l];
@@ -1039,6 +1075,16 @@ int orc_backward_filter_segment(int d, const double* Bt, const double* beta, con
     }
 #undef FILT_STORE
     return 1;
+}
+int orc_backward_filter_segment(int d, const double* Bt, const double* beta, const double* at,
+                                int npts, const double* t, const double* HT, const double* FT,
+                                double cT, double* H, double* F, double* c) {
+    return backward_filter(d, Bt, beta, 0, at, npts, t, HT, FT, cT, H, F, c);
+}
+int orc_backward_filter_segment_td(int d, const double* aux, const double* at, int npts,
+                                   const double* t, const double* HT, const double* FT,
+                                   double cT, double* H, double* F, double* c) {
+    return backward_filter(d, 0, 0, aux, at, npts, t, HT, FT, cT, H, F, c);
 }
 /* the canonical log kernel, exposed for the Python container restatement */
 double orc_rng_log(double u) { return rng_log(u); }

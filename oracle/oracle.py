@@ -35,6 +35,8 @@ LIB = os.path.join(HERE, "liboracle.so")
 LAW_STRIDE = 64
 L_C0 = 49
 L_BT, L_TRACE, L_A, L_SIGMA, L_ANCHOR, L_AUXLIN = 31, 50, 25, 16, 60, 63
+L_AUXTD = 15   # time-dependent auxiliary law flag (include/dmt.h DMT_LAW_AUXTD)
+MODEL_OU = 0
 
 
 def set_law_params(model, d, rec, params):
@@ -125,6 +127,10 @@ def _load():
     lib.orc_set_ll_skip.restype = None
     lib.orc_backward_filter_segment.argtypes = [i_, P, P, P, i_, P, P, P, d_, P, P, P]
     lib.orc_backward_filter_segment.restype = i_
+    lib.orc_backward_filter_segment_td.argtypes = [i_, P, P, i_, P, P, P, d_, P, P, P]
+    lib.orc_backward_filter_segment_td.restype = i_
+    lib.orc_set_aux.argtypes = [P]
+    lib.orc_set_aux.restype = None
     lib.orc_rng_log.argtypes = [d_]
     lib.orc_rng_log.restype = d_
     lib.orc_bm_log.argtypes = [d_]
@@ -150,7 +156,23 @@ def _sfx(prec):
 
 
 # ------------------------------------------------------------------ per-segment numerics
-def solve_segment(model, d, m, law, t, H, F, W, y1, prec=0):
+class _aux_rows:
+    """The segment's time-dependent auxiliary coefficients (rows [npts][d·d + d], doubles) for
+    the C calls inside the block (orc_set_aux), or nothing."""
+
+    def __init__(self, aux):
+        self.aux = None if aux is None else np.ascontiguousarray(aux, dtype=np.float64)
+
+    def __enter__(self):
+        if self.aux is not None:
+            lib.orc_set_aux(_p(self.aux))
+
+    def __exit__(self, *exc):
+        if self.aux is not None:
+            lib.orc_set_aux(None)
+
+
+def solve_segment(model, d, m, law, t, H, F, W, y1, prec=0, aux=None):
     dt = _dt(prec)
     t, H, F, W = (np.ascontiguousarray(a, dtype=dt) for a in (t, H, F, W))
     y1 = np.ascontiguousarray(y1, dtype=dt)
@@ -158,8 +180,9 @@ def solve_segment(model, d, m, law, t, H, F, W, y1, prec=0):
     n = t.size
     X = np.empty((n, d), dtype=dt)
     ll = np.zeros(1, dtype=dt)
-    ok = getattr(lib, f"orc_solve_segment_{_sfx(prec)}")(model, d, m, _p(law), n, _p(t), _p(H),
-                                                          _p(F), _p(W), _p(y1), _p(X), _p(ll))
+    with _aux_rows(aux):
+        ok = getattr(lib, f"orc_solve_segment_{_sfx(prec)}")(model, d, m, _p(law), n, _p(t), _p(H),
+                                                              _p(F), _p(W), _p(y1), _p(X), _p(ll))
     return X, dt(ll[0]), bool(ok)
 
 
@@ -181,6 +204,22 @@ def backward_filter_segment(d, Bt, beta, at_packed, t, HT_packed, FT, cT):
     return H, F, c
 
 
+def backward_filter_segment_td(d, aux, at_packed, t, HT_packed, FT, cT):
+    """The same filter for a time-dependent auxiliary drift: aux[npts][d·d + d] = B̃(t_i), β̃(t_i),
+    step i taking its left point's row (dmt_guiding_linear_td, dmt_upload_aux)."""
+    t = np.ascontiguousarray(t, dtype=np.float64)
+    n = t.size
+    hp = d * (d + 1) // 2
+    H = np.empty((n, hp)); F = np.empty((n, d)); c = np.empty(n)
+    args = [np.ascontiguousarray(a, dtype=np.float64) for a in (aux, at_packed, HT_packed, FT)]
+    assert args[0].shape == (n, d * d + d)
+    ok = lib.orc_backward_filter_segment_td(d, _p(args[0]), _p(args[1]), n, _p(t), _p(args[2]),
+                                            _p(args[3]), float(cT), _p(H), _p(F), _p(c))
+    if not ok:
+        raise FloatingPointError("singular I + HK in the backward filter")
+    return H, F, c
+
+
 def invsolve_segment(model, d, m, law, t, H, F, X, prec=0):
     """DD.invsolve!: Wiener increments (row 0 = W(t0) = 0) reproducing X under the law."""
     dt = _dt(prec)
@@ -192,12 +231,13 @@ def invsolve_segment(model, d, m, law, t, H, F, X, prec=0):
     return W
 
 
-def path_ll_segment(model, d, m, law, t, H, F, X, prec=0):
+def path_ll_segment(model, d, m, law, t, H, F, X, prec=0, aux=None):
     dt = _dt(prec)
     t, H, F, X = (np.ascontiguousarray(a, dtype=dt) for a in (t, H, F, X))
     law = np.ascontiguousarray(law, dtype=np.float64)
-    return dt(getattr(lib, f"orc_path_ll_segment_{_sfx(prec)}")(model, d, m, _p(law), t.size,
-                                                                 _p(t), _p(H), _p(F), _p(X)))
+    with _aux_rows(aux):
+        return dt(getattr(lib, f"orc_path_ll_segment_{_sfx(prec)}")(model, d, m, _p(law), t.size,
+                                                                     _p(t), _p(H), _p(F), _p(X)))
 
 
 def obs_term(d, law, H0, F0, x, prec=0):
@@ -391,6 +431,7 @@ class OracleEnsemble:
             U_.PP = [None] * self.G
             U_.PPb = [None] * self.G
         self.layouts = []
+        self.aux = [None, None]  # [kind] time-dependent auxiliary coefficients (upload_aux)
         self.seg_base = 0  # dmt_set_shard
         # RNG_AUTO counter: next key, the key of the last auto draw, armed for one auto accept
         self.rng_ctr, self.rng_last, self.rng_pending = 0, 0, False
@@ -441,6 +482,26 @@ class OracleEnsemble:
         if first:  # u° = deepcopy(u) (src/sampling_pair.jl:51)
             for g in range(self.G):
                 otab[g] = copy.deepcopy(tab[g])
+
+    def upload_aux(self, kind, aux):
+        """dmt_upload_aux: per-point B̃(t_i), β̃(t_i) ([P][d·d + d]) of the laws of `kind`, u and u°
+        alike, held in the working precision (as the device holds them) for the segments whose
+        record has auxtd set; None removes them.  Non-linear drifts only."""
+        if self.model == MODEL_OU:
+            raise ValueError("time-dependent auxiliary laws: non-linear drifts only")
+        C_ = self.d * self.d + self.d
+        self.aux[kind] = (None if aux is None else
+                          np.asarray(aux, dtype=np.float64).reshape(self.P, C_)
+                          .astype(self.dt).astype(np.float64))
+
+    def _aux_seg(self, bk, g):
+        """The segment's rows of its law kind's table when its record is time-dependent."""
+        kind = 1 if (not bk.term and g == bk.g1) else 0
+        tab = self.aux[kind]
+        lw = self._law(0, bk, g)
+        if tab is None or lw.rec is None or lw.rec[L_AUXTD] == 0.0:
+            return None
+        return tab[self.pt_off[g]: self.pt_off[g] + self.npts[g]]
 
     def set_paths(self, unit, X=None, W=None):
         """Host W is cumulative (the reference's Wiener trajectories); held as increments."""
@@ -545,8 +606,9 @@ class OracleEnsemble:
                     Wuse = pcn_segment(self.m, t, win.WW[g], Zg, dt(bk.rho), dt(bk.srho),
                                        self.prec)
                 out.WW[g][...] = Wuse
+            aux = self._aux_seg(bk, g) if lw.rec[L_AUXTD] != 0.0 else None
             X, sl, ok = solve_segment(self.model, self.d, self.m, lw.rec, t, lw.H, lw.F, Wuse, x,
-                                      self.prec)
+                                      self.prec, aux=aux)
             out.XX[g][...] = X
             if not ok:
                 ok_all = False
@@ -613,8 +675,9 @@ class OracleEnsemble:
             ll = obs_term(self.d, law0.rec, law0.H[0], law0.F[0], me.XX[bk.g0][0], self.prec)
             for g in range(bk.g0, bk.g1 + 1):
                 lw = self._law(unit, bk, g)
+                aux = self._aux_seg(bk, g) if lw.rec[L_AUXTD] != 0.0 else None
                 ll = dt(ll + path_ll_segment(self.model, self.d, self.m, lw.rec, self.t[g], lw.H,
-                                             lw.F, me.XX[g], self.prec))
+                                             lw.F, me.XX[g], self.prec, aux=aux))
             if unit == 0:
                 bk.ll = float(ll)
             else:
@@ -731,8 +794,14 @@ class OracleEnsemble:
                 Bt = rec[31:31 + d * d]
                 beta = rec[40:40 + d]
                 at = rec[25:25 + hp] - rec[43:43 + hp]
-                H, F, c = backward_filter_segment(d, Bt, beta, at, self.t[g].astype(np.float64),
-                                                  packed_sym(HT), FT, cT)
+                kind = 1 if last_b else 0
+                if rec[L_AUXTD] != 0.0 and self.aux[kind] is not None:
+                    rows = self.aux[kind][self.pt_off[g]: self.pt_off[g] + self.npts[g]]
+                    H, F, c = backward_filter_segment_td(d, rows, at, self.t[g].astype(np.float64),
+                                                         packed_sym(HT), FT, cT)
+                else:
+                    H, F, c = backward_filter_segment(d, Bt, beta, at, self.t[g].astype(np.float64),
+                                                      packed_sym(HT), FT, cT)
                 lw.H = H.astype(self.dt)
                 lw.F = F.astype(self.dt)
                 lw.rec[L_C0] = c[0]

@@ -1,0 +1,287 @@
+"""Time-dependent linear auxiliary laws within a segment (include/dmt.h dmt_upload_aux,
+DMT_LAW_AUXTD).  The reference takes any linear auxiliary law of
+GuidedProposals (aux_laws, /root/reference/src/sampling_unit.jl:55-66), whose B̃(t), β̃(t) may
+vary in t; step i of a segment takes the coefficients of its left point t_i, frozen over
+[t_i, t_{i+1}], in the Girsanov term G and in the backward filter's exact step transition.
+
+CPU: the oracle's and libdmt's host filters agree bit for bit; a constant table reproduces the
+time-homogeneous law bit for bit (filter and oracle ensemble); the frozen-coefficient filter
+converges (first order) as the grid is refined — the guiding term of the ODEs of SURVEY.md A.5.
+GPU: device == oracle bit for bit on the ragged FHN ensemble with a varying table on part of
+the segments, through the blocking loop (set_obs!, recompute_guiding_term!, find_W_for_X!,
+loglikhd!, draws with caller and device normals, accept, recompute_path!), lane and wave
+mappings, fp64 and fp32.
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import oracle as orc  # noqa: E402
+import _cases as cs  # noqa: E402
+import diffusionmcmctools_amd as dmt  # noqa: E402
+from diffusionmcmctools_amd import _lib as L  # noqa: E402
+
+MAPPINGS = [L.MAP_LANE, L.MAP_WAVE]
+
+
+def _law2():
+    """A 2-D linear auxiliary law with time-varying coefficients and noise on coordinate 2."""
+    B0 = np.array([[-1.0, -0.5], [1.5, -1.0]])
+    B1 = np.array([[0.4, 0.0], [-0.3, 0.2]])
+    B = lambda t: B0 + np.sin(3.0 * t) * B1  # noqa: E731
+    beta = lambda t: np.array([0.3 + 0.5 * t, -0.2 * np.cos(2.0 * t)])  # noqa: E731
+    at = np.array([0.0, 0.0, 0.09])  # packed σ̃σ̃ᵀ, σ̃ = (0, 0.3)
+    return B, beta, at
+
+
+def _table(B, beta, t):
+    return np.stack([np.concatenate([B(x).ravel(), beta(x)]) for x in t])
+
+
+def _end_info():
+    HT = np.array([[25.0, 0.0], [0.0, 0.0]])
+    return orc.packed_sym(HT), np.array([12.5, 0.0]), 3.1
+
+
+def test_td_filter_host_equals_oracle_and_constant_equals_homogeneous():
+    B, beta, at = _law2()
+    t = np.sort(np.concatenate([[0.0, 1.0], np.random.default_rng(3).uniform(0, 1, 150)]))
+    HT, FT, cT = _end_info()
+    aux = _table(B, beta, t)
+    h = dmt.guiding_linear_td(aux, at, t, HT, FT, cT)
+    o = orc.backward_filter_segment_td(2, aux, at, t, HT, FT, cT)
+    for a, b in zip(h, o):
+        assert np.array_equal(a, b)
+    # a constant table is the time-homogeneous law, bit for bit (host and oracle)
+    const = np.tile(np.concatenate([B(0.4).ravel(), beta(0.4)]), (t.size, 1))
+    hc = dmt.guiding_linear_td(const, at, t, HT, FT, cT)
+    hh = dmt.guiding_linear(B(0.4), beta(0.4), at, t, HT, FT, cT)
+    oc = orc.backward_filter_segment_td(2, const, at, t, HT, FT, cT)
+    for a, b, c in zip(hc, hh, oc):
+        assert np.array_equal(a, b) and np.array_equal(a, c)
+    # and the varying table really is used
+    assert not np.array_equal(h[0], hh[0])
+
+
+def test_td_filter_converges_as_the_grid_is_refined():
+    """Left-point frozen coefficients are a first-order scheme for the filter of the
+    time-dependent law (SURVEY.md A.5's ODEs): the guiding term at t0 on grids of n, 2n, … steps
+    converges, each halving of the step roughly halving the error against the finest grid."""
+    B, beta, at = _law2()
+    HT, FT, cT = _end_info()
+
+    def at_t0(n):
+        t = np.linspace(0.0, 1.0, n + 1)
+        H, F, c = dmt.guiding_linear_td(_table(B, beta, t), at, t, HT, FT, cT)
+        return np.concatenate([H[0], F[0], [c[0]]])
+
+    ref = at_t0(4096)
+    errs = [np.max(np.abs(at_t0(n) - ref)) for n in (32, 64, 128, 256)]
+    for e0, e1 in zip(errs, errs[1:]):
+        assert 1.6 < e0 / e1 < 2.6, errs
+    assert errs[-1] < 2e-3 * np.max(np.abs(ref))
+
+
+def _flag_segments(ens, kinds, segs):
+    """Set DMT_LAW_AUXTD in the law records of `segs` (both units, the given kinds)."""
+    for unit in (L.U, L.UPROP):
+        for kind in kinds:
+            laws = ens.download_law(unit, kind)[2].copy()
+            laws[segs, L.LAW_AUXTD] = 1.0
+            ens.upload_law(unit, kind, laws=laws)
+
+
+def _tables(case, ens, vary=True):
+    """Per-point aux tables of both kinds: each segment's record B̃, β̃, plus (vary) a
+    time-varying perturbation — for the PPb laws a different one."""
+    t = case["t"]
+    out = []
+    for kind, laws in ((L.LAW_PP, case["laws"]), (L.LAW_PPB, case["lawsb"])):
+        rows = []
+        for g, n in enumerate(np.concatenate(case["n_points"])):
+            rec = laws[g]
+            Bt = rec[L.LAW_BT:L.LAW_BT + 4].reshape(2, 2)
+            be = rec[L.LAW_BETA:L.LAW_BETA + 2]
+            off = int(np.sum(np.concatenate(case["n_points"])[:g]))
+            for tt in t[off:off + n]:
+                if vary:
+                    s = np.sin(7.0 * tt + g + kind)
+                    Bq = Bt + s * np.array([[0.3, -0.1], [0.2, 0.0]])
+                    bq = be + np.array([0.4 * np.cos(5.0 * tt), 0.1 * s])
+                else:
+                    Bq, bq = Bt, be
+                rows.append(np.concatenate([Bq.ravel(), bq]))
+        out.append(np.array(rows))
+    return out
+
+
+def _td_pair(mapping, prec, vary=True, segs=None, oracle_only=False):
+    case = cs.ragged_case(prec=prec)
+    m = case["model"]
+    ens = []
+    if not oracle_only:
+        ens.append(dmt.Ensemble(m.kind, m.d, m.m, case["n_points"], precision=prec, seed=11,
+                                mapping=mapping))
+    ens.append(orc.OracleEnsemble(m.kind, m.d, m.m, case["n_points"], prec=prec, seed=11))
+    G = int(sum(case["nsegs"]))
+    segs = np.arange(0, G, 2) if segs is None else segs
+    tabs = _tables(case, ens[0], vary)
+    for e in ens:
+        cs.load_ragged(e, case)
+        e.upload_obs(case["Hobs"], case["Fobs"], case["cobs"])
+        _flag_segments(e, (L.LAW_PP, L.LAW_PPB), segs)
+        e.upload_aux(L.LAW_PP, tabs[0])
+        e.upload_aux(L.LAW_PPB, tabs[1])
+    layA = dict(n_blocks=[2, 3, 2], seg_first=[0, 2, 0, 2, 4, 0, 3], seg_last=[1, 3, 1, 3, 5, 2, 4],
+                last=[0, 1, 0, 0, 1, 0, 1])
+    layB = dict(n_blocks=[1, 2, 2], seg_first=[0, 0, 3, 0, 2], seg_last=[3, 2, 5, 1, 4],
+                last=[1, 0, 1, 0, 1])
+    ids = []
+    for lay, rho in ((layA, 0.7), (layB, 0.3)):
+        nb = int(sum(lay["n_blocks"]))
+        ids_ = [e.create_layout(lay["n_blocks"], lay["seg_first"], lay["seg_last"], lay["last"],
+                                np.full(nb, rho), 6) for e in ens]
+        assert len(set(ids_)) == 1
+        ids.append((ids_[0], nb))
+    return case, ens, ids
+
+
+def _blocking_loop(ens, ids, S, iters, rng, device_rng=False):
+    out = []
+    for i in range(1, iters + 1):
+        lid, nb = ids[(i - 1) % 2]
+        Z = rng.standard_normal((S, 1))
+        E = rng.exponential(1.0, nb)
+        for e in ens:
+            e.set_obs(lid, 0, nb)
+            e.recompute_guiding_term(lid, 0, nb, unit=L.U)
+            e.find_W_for_X(lid, 0, nb)
+            e.loglikhd(lid, L.U, 0, nb)
+            if device_rng:
+                e.draw_proposal(lid, 0, nb, iter=i, salt=3)
+            else:
+                e.draw_proposal(lid, 0, nb, Z=Z, iter=i)
+        out.append([e.accept_reject(lid, 0, nb, i, E=E, want_acc=True) for e in ens])
+    return out
+
+
+def _fixed_aux(ens):
+    """Auxiliary laws that set_obs! does not re-linearise (DMT_LAW_AUXLIN = 0): a
+    time-dependent record takes B̃, β̃ from its table, so only a fixed law compares with it."""
+    for unit in (L.U, L.UPROP):
+        for kind in (L.LAW_PP, L.LAW_PPB):
+            laws = ens.download_law(unit, kind)[2].copy()
+            laws[:, L.LAW_AUXLIN] = 0.0
+            ens.upload_law(unit, kind, laws=laws)
+
+
+def test_oracle_constant_table_equals_homogeneous_law():
+    """The oracle with every segment flagged time-dependent and a table holding each record's
+    own B̃, β̃ runs the blocking loop bit-identically to the plain oracle (fixed laws)."""
+    case, (td,), ids = _td_pair(None, L.F64, vary=False, oracle_only=True,
+                                segs=np.arange(sum(cs.ragged_case()["nsegs"])))
+    m = case["model"]
+    plain = orc.OracleEnsemble(m.kind, m.d, m.m, case["n_points"], prec=L.F64, seed=11)
+    cs.load_ragged(plain, case)
+    plain.upload_obs(case["Hobs"], case["Fobs"], case["cobs"])
+    for e in (td, plain):
+        _fixed_aux(e)
+    for lay in (dict(n_blocks=[2, 3, 2], seg_first=[0, 2, 0, 2, 4, 0, 3],
+                     seg_last=[1, 3, 1, 3, 5, 2, 4], last=[0, 1, 0, 0, 1, 0, 1], rho=0.7),
+                dict(n_blocks=[1, 2, 2], seg_first=[0, 0, 3, 0, 2], seg_last=[3, 2, 5, 1, 4],
+                     last=[1, 0, 1, 0, 1], rho=0.3)):
+        nb = int(sum(lay["n_blocks"]))
+        plain.create_layout(lay["n_blocks"], lay["seg_first"], lay["seg_last"], lay["last"],
+                            np.full(nb, lay["rho"]), 6)
+    S = td.S
+    a = _blocking_loop([td], ids, S, 4, np.random.default_rng(2))
+    b = _blocking_loop([plain], ids, S, 4, np.random.default_rng(2))
+    for x, y in zip(a, b):
+        assert np.array_equal(x[0], y[0])
+    cs.assert_paths_equal(td, plain)
+    for lid, nb in ids:
+        cs.assert_ll_equal(td, plain, lid, nb)
+
+
+def test_upload_aux_rejected_for_ou_oracle():
+    o = orc.OracleEnsemble(0, 2, 1, [[11]], prec=0, seed=1)
+    with pytest.raises(ValueError):
+        o.upload_aux(L.LAW_PP, np.zeros((11, 6)))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("prec", [L.F64, L.F32], ids=["f64", "f32"])
+@pytest.mark.parametrize("mapping", MAPPINGS, ids=["lane", "wave"])
+def test_td_aux_blocking_loop_device_equals_oracle(mapping, prec):
+    case, (dev, ora), ids = _td_pair(mapping, prec)
+    rng = np.random.default_rng(8)
+    res = _blocking_loop([dev, ora], ids, dev.S, 6, rng)
+    for i, (ad, ao) in enumerate(res):
+        assert np.array_equal(ad, ao), f"iteration {i + 1}"
+    for kind in (L.LAW_PP, L.LAW_PPB):
+        for unit in (L.U, L.UPROP):
+            for a_, b_ in zip(dev.download_law(unit, kind), ora.download_law(unit, kind)):
+                assert np.array_equal(a_, b_), (unit, kind)
+    cs.assert_paths_equal(dev, ora)
+    for lid, nb in ids:
+        cs.assert_ll_equal(dev, ora, lid, nb)
+    # device normals, then recompute_path! under u°'s law
+    res = _blocking_loop([dev, ora], ids, dev.S, 2, rng, device_rng=True)
+    for ad, ao in res:
+        assert np.array_equal(ad, ao)
+    for lid, nb in ids:
+        for e in (dev, ora):
+            e.recompute_path(lid, 0, nb)
+        cs.assert_paths_equal(dev, ora)
+        cs.assert_ll_equal(dev, ora, lid, nb)
+    dev.close()
+
+
+@pytest.mark.gpu
+def test_td_aux_removed_table_is_homogeneous_again():
+    """upload_aux(kind, None) drops the table: the flagged segments fall back to the record's
+    B̃, β̃ (the time-homogeneous kernels run again), device == oracle."""
+    case, (dev, ora), ids = _td_pair(L.MAP_LANE, L.F64)
+    for e in (dev, ora):
+        e.upload_aux(L.LAW_PP, None)
+        e.upload_aux(L.LAW_PPB, None)
+    res = _blocking_loop([dev, ora], ids, dev.S, 2, np.random.default_rng(4))
+    for ad, ao in res:
+        assert np.array_equal(ad, ao)
+    cs.assert_paths_equal(dev, ora)
+    dev.close()
+
+
+@pytest.mark.gpu
+def test_td_aux_rejected_for_ou():
+    w = __import__("diffusionmcmctools_amd.workloads", fromlist=["c2_ou2d"]).c2_ou2d(B=4, N=20)
+    e = dmt.Ensemble(w.model.kind, w.d, w.m, w.n_points, precision=w.precision, seed=1,
+                     grid_shared=w.grid_shared)
+    with pytest.raises(dmt.DMTError):
+        e.upload_aux(L.LAW_PP, np.zeros((e.P, 6)))
+    e.close()
+
+
+def test_oracle_varying_table_enters_girsanov_and_filter():
+    """The table is what the flagged segments use: with the guiding tables left as uploaded,
+    loglikhd! (G only) already differs from the constant table's, and so do the guiding tables
+    recompute_guiding_term! builds."""
+    case, (var,), ids = _td_pair(None, L.F64, vary=True, oracle_only=True)
+    _, (con,), _ = _td_pair(None, L.F64, vary=False, oracle_only=True)
+    lid, nb = ids[0]
+    for e in (var, con):
+        e.loglikhd(lid, L.U, 0, nb)
+    assert not np.array_equal(var.get_block_state(lid, L.BLK_LL, 0, nb),
+                              con.get_block_state(lid, L.BLK_LL, 0, nb))
+    for e in (var, con):
+        e.recompute_guiding_term(lid, 0, nb, unit=L.U)
+    Hv, Hc = var.download_law(L.U, L.LAW_PP)[0], con.download_law(L.U, L.LAW_PP)[0]
+    assert not np.array_equal(Hv, Hc)
