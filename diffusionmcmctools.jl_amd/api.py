@@ -72,12 +72,12 @@ def _aux_callable(AuxLaw):
     """The reference's ``aux_laws`` argument (src/sampling_unit.jl:55-60) as the
     ``aux_laws(model, r, k, obs)`` of :meth:`SamplingEnsemble.from_recordings`: an auxiliary-law
     constructor ``AuxLaw(P, obs)`` (e.g. ``models.FitzHughNagumoAux``: the target linearised at
-    the segment's observation), a fixed ``LinearAux`` for every segment, or one such per
-    segment (a list)."""
-    from .models import LinearAux
+    the segment's observation), a fixed ``LinearAux`` or ``TimeDependentLinearAux`` (B̃(t), β̃(t))
+    for every segment, or one such per segment (a list)."""
+    from .models import LinearAux, TimeDependentLinearAux
     if AuxLaw is None:
         return None
-    if isinstance(AuxLaw, LinearAux):
+    if isinstance(AuxLaw, (LinearAux, TimeDependentLinearAux)):
         return lambda mdl, r, k, ob: AuxLaw
     if isinstance(AuxLaw, (list, tuple)):
         return lambda mdl, r, k, ob: (AuxLaw[k](mdl, ob) if callable(AuxLaw[k]) else AuxLaw[k])
@@ -160,17 +160,25 @@ class SamplingEnsemble:
         ``tts[r][k]``: the grid of segment k of recording r (``setup_time_grids``);
         ``record_models[r]``: recording r's own target law (its parameters go into its law
         records; default ``model`` for all)."""
-        from .models import artificial_obs_info, guiding_chain, packed
+        from .models import artificial_obs_info, guiding_chain, is_time_dependent, packed
         aux_laws = aux_laws or (lambda mdl, r, k, ob: mdl.aux_for(ob))
         aux_laws_blocking = aux_laws_blocking or aux_laws
         d = model.d
         t_all, H_all, F_all, laws, n_points, infos_all = [], [], [], [], [], []
         Hb_all, Fb_all, lawsb = [], [], []
+        # time-dependent auxiliary laws (models.TimeDependentLinearAux): per-point tables of
+        # both kinds, zero rows for time-homogeneous segments (unused there)
+        tab_pp, tab_b, any_td = [], [], False
+        C_ = d * d + d
         for r, rec in enumerate(recordings):
             grids = [np.asarray(g, dtype=np.float64) for g in tts[r]]
             if len(grids) != len(rec.obs):
                 raise ValueError(f"recording {r}: {len(rec.obs)} observations, {len(grids)} grids")
             auxes = [aux_laws(model, r, k, ob) for k, ob in enumerate(rec.obs)]
+            for a_, g_ in zip(auxes, grids):
+                td = is_time_dependent(a_)
+                any_td |= td
+                tab_pp.append(a_.table(g_) if td else np.zeros((len(g_), C_)))
             infos = [ob.info() for ob in rec.obs]
             chain = guiding_chain(auxes, grids, infos)
             t_all += grids
@@ -183,6 +191,9 @@ class SamplingEnsemble:
             if blocking:
                 for k, ob in enumerate(rec.obs):
                     a_ = aux_laws_blocking(model, r, k, ob)
+                    td = is_time_dependent(a_)
+                    any_td |= td
+                    tab_b.append(a_.table(grids[k]) if td else np.zeros((len(grids[k]), C_)))
                     v = np.zeros(d)
                     vo = np.atleast_1d(np.asarray(ob.v, dtype=np.float64))
                     v[:min(d, vo.size)] = vo[:d]
@@ -207,6 +218,10 @@ class SamplingEnsemble:
             blaws = dict(Hb=np.concatenate(Hb_all), Fb=np.concatenate(Fb_all),
                          lawsb=np.stack(lawsb))
         se.set_guiding(np.concatenate(H_all), np.concatenate(F_all), np.stack(laws), **blaws)
+        if any_td:
+            se.ens.upload_aux(L.LAW_PP, np.concatenate(tab_pp))
+            if blocking:
+                se.ens.upload_aux(L.LAW_PPB, np.concatenate(tab_b))
         se.set_observations(np.stack([packed(i[0]) for i in infos_all]),
                             np.stack([np.asarray(i[1], dtype=np.float64) for i in infos_all]),
                             np.array([float(i[2]) for i in infos_all]),

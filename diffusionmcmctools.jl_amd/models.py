@@ -14,7 +14,7 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from . import _lib as L
-from .engine import guiding_linear
+from .engine import guiding_linear, guiding_linear_td
 
 
 def packed(M):
@@ -49,6 +49,33 @@ class LinearAux:
     def at(self):
         s = np.asarray(self.sigma_t, dtype=np.float64)
         return s @ s.T
+
+
+@dataclass
+class TimeDependentLinearAux:
+    """Auxiliary law dX = (B̃(t) X + β̃(t)) dt + σ̃ dW whose drift varies within a segment (any
+    linear law of GuidedProposals, the reference's aux_laws, src/sampling_unit.jl:55-66).
+    ``Bt(t)``, ``beta(t)``: callables; on the device, step i takes its left point's values
+    (include/dmt.h dmt_upload_aux).  Non-linear drifts only."""
+    Bt: object
+    beta: object
+    sigma_t: np.ndarray  # d×m
+    anchor = None  # never re-linearised: the law is given as functions of t
+
+    @property
+    def at(self):
+        s = np.asarray(self.sigma_t, dtype=np.float64)
+        return s @ s.T
+
+    def table(self, t):
+        """Per-point rows B̃(t_i) (row-major), β̃(t_i) on grid ``t``."""
+        return np.stack([np.concatenate([np.asarray(self.Bt(x), dtype=np.float64).ravel(),
+                                         np.asarray(self.beta(x), dtype=np.float64).ravel()])
+                         for x in np.asarray(t, dtype=np.float64)])
+
+
+def is_time_dependent(aux):
+    return isinstance(aux, TimeDependentLinearAux)
 
 
 # parameter-name aliases: DiffusionDefinition's symbols (:ϵ, :γ, …) and ASCII spellings
@@ -108,8 +135,11 @@ class Model:
         a = sg @ sg.T
         hp = self.d * (self.d + 1) // 2
         rec[L.LAW_A:L.LAW_A + hp] = packed(a)
-        rec[L.LAW_BT:L.LAW_BT + self.d * self.d] = np.asarray(aux.Bt, dtype=np.float64).ravel()
-        rec[L.LAW_BETA:L.LAW_BETA + self.d] = np.asarray(aux.beta, dtype=np.float64)
+        if is_time_dependent(aux):  # B̃, β̃ come from the per-point table (dmt_upload_aux)
+            rec[L.LAW_AUXTD] = 1.0
+        else:
+            rec[L.LAW_BT:L.LAW_BT + self.d * self.d] = np.asarray(aux.Bt, dtype=np.float64).ravel()
+            rec[L.LAW_BETA:L.LAW_BETA + self.d] = np.asarray(aux.beta, dtype=np.float64)
         da = a - aux.at
         rec[L.LAW_DA:L.LAW_DA + hp] = packed(da)
         rec[L.LAW_C0] = c0
@@ -367,7 +397,7 @@ def guiding_chain(auxes, grids, infos, H_in=None):
     out = [None] * K
     nxt = None
     for k in range(K - 1, -1, -1):
-        d = len(auxes[k].beta)
+        d = np.asarray(auxes[k].sigma_t).shape[0]
         HT, FT, cT = infos[k]
         HT = np.array(HT, dtype=np.float64).reshape(d, d)
         FT = np.array(FT, dtype=np.float64).reshape(d)
@@ -376,8 +406,12 @@ def guiding_chain(auxes, grids, infos, H_in=None):
             HT = HT + unpacked(Hn, d)
             FT = FT + Fn
             cT = cT + cn
-        H, F, c = guiding_linear(auxes[k].Bt, auxes[k].beta, packed(auxes[k].at), grids[k],
-                                 packed(HT), FT, cT)
+        if is_time_dependent(auxes[k]):
+            H, F, c = guiding_linear_td(auxes[k].table(grids[k]), packed(auxes[k].at), grids[k],
+                                        packed(HT), FT, cT)
+        else:
+            H, F, c = guiding_linear(auxes[k].Bt, auxes[k].beta, packed(auxes[k].at), grids[k],
+                                     packed(HT), FT, cT)
         out[k] = (H, F, c)
         nxt = (H[0], F[0], c[0])
     return out
