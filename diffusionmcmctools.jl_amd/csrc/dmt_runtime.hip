@@ -58,6 +58,7 @@ struct Layout {
   std::vector<uint8_t> term;
   bool single_seg = false;  // every block is one segment (the lane kernels' producer/consumer split)
   int32_t max_steps = 0;    // longest segment of any block (single-segment layouts)
+  bool all_term = false;    // every block is terminal (no PPb law needed: law_ready)
   int64_t* d_blk_off = nullptr;
   BlkInfo* d_binfo = nullptr;
   int32_t* d_blk_rec = nullptr;
@@ -446,8 +447,8 @@ int64_t rec_of_block(const Layout* L, int64_t blk) {
 
 dmt_status law_ready(dmt_ens* h, int unit_needed_flip, const Layout* L, int64_t b0, int64_t b1) {
   // the PP law is always needed; PPB only for non-terminal blocks
-  bool need_ppb = false;
-  for (int64_t b = b0; b < b1 && !need_ppb; ++b) need_ppb = !L->term[b];
+  bool need_ppb = false;  // (per call: a host loop over the range unless the layout says)
+  for (int64_t b = b0; b < b1 && !need_ppb && !L->all_term; ++b) need_ppb = !L->term[b];
   if (!h->have_t) return fail(DMT_ERR_STATE, "time grid not uploaded (dmt_upload_grid)");
   if (!h->d_law[0][0] || !h->d_law[1][0] || !h->d_H[0][0] || !h->d_F[0][0])
     return fail(DMT_ERR_STATE, "PP law not uploaded (dmt_upload_law)");
@@ -730,6 +731,8 @@ dmt_status build_layout(dmt_ens* h, const int32_t* n_blocks, const int32_t* seg_
   L->max_steps = 0;
   for (int64_t b = 0; b < L->nblocks && L->single_seg; ++b)
     L->max_steps = std::max(L->max_steps, h->seg_np[L->gfirst[b]] - 1);
+  L->all_term = true;
+  for (int64_t b = 0; b < L->nblocks && L->all_term; ++b) L->all_term = L->term[b] != 0;
   const int64_t nb = L->nblocks;
   DMT_TRY(ens_alloc(h, &L->d_blk_off, h->R + 1));
   DMT_TRY(ens_alloc(h, &L->d_gfirst, nb));
@@ -1593,11 +1596,14 @@ static dmt_status mcmc_run_launch(dmt_ens* h, Layout* L, int64_t b0, int64_t b1,
   // memory for the all-gather
   double* run_out = multi ? h->d_run : h->h_run_dev;
   const int64_t nb = b1 - b0;
+  // kernel eligibility of the range: from the layout's flags when they decide it (no host
+  // loop over the blocks per call), else block by block
+  const bool lay_res = L->single_seg && L->max_steps <= kResidentMaxSteps;
   bool persist = h->persist && h->key.model == DMT_MODEL_OU;
-  for (int64_t b = b0; b < b1 && persist; ++b)
+  for (int64_t b = b0; b < b1 && persist && !L->single_seg; ++b)
     persist = L->glast[b] - L->gfirst[b] + 1 <= kPersistMaxSegments;
   bool resident = persist && h->key.d <= 2 && h->resident;
-  for (int64_t b = b0; b < b1 && resident; ++b)
+  for (int64_t b = b0; b < b1 && resident && !lay_res; ++b)
     resident = L->glast[b] == L->gfirst[b] && h->seg_np[L->gfirst[b]] - 1 <= kResidentMaxSteps;
   if (persist) {
     // the whole run in one launch per chunk of iterations (k_mcmc_scan / k_mcmc_resident),
