@@ -237,3 +237,25 @@ def test_service_explicit_keys_ranges_and_capacity():
     _same_state(svc, ora, lay, nb, 24)
     for e in (svc, imm):
         e.close()
+
+
+@pytest.mark.gpu
+def test_two_services_on_one_device_interleaved():
+    """Two handles on one device, their caller loops interleaved call by call: each resident
+    service waits for the device while the other holds it (its launch leaves idle and is
+    launched again), and every result equals the one-launch-per-iteration path's."""
+    (a, b, a0, b0), lay, nb = _ensembles(["1", "1", "0", "0"], hist=12, with_oracle=False,
+                                         service=["1", "1", "0", "0"])
+    for e in (a, b, a0, b0):
+        e.loglikhd(lay, L.U, 0, nb)
+    res = {id(e): [] for e in (a, b, a0, b0)}
+    for i in range(1, 6):
+        for e in (a, b, a0, b0):
+            e.draw_proposal(lay, 0, nb, salt=L.RNG_AUTO, want_success="lazy")
+            e.accept_reject(lay, 0, nb, i, salt=L.RNG_AUTO)
+            res[id(e)].append(e.fetch_ll(lay, 0, nb, i))
+    assert res[id(a)] == res[id(a0)] and res[id(b)] == res[id(b0)]
+    _same_state(a, a0, lay, nb, 12)
+    _same_state(b, b0, lay, nb, 12)
+    for e in (a, b, a0, b0):
+        e.close()
