@@ -19,6 +19,22 @@ enum Mode : int {
   MODE_FRESH = 2,      // draw_proposal_path!(u::SamplingUnit): fresh W (ρ = 0), in place
 };
 
+// Path selectors (selX, selW; one byte per segment): bits 0-1 = the physical buffer holding
+// u.XX[g] (u.WW[g]), bits 2-3 = the buffer holding u°'s.  A swap exchanges the two fields.
+// Ensembles with two buffers keep u° = u ^ 1 (sel_two); MAP_LANE ensembles of non-linear models
+// hold a third, and a draw writes every proposal of a wave to a buffer that holds none of the
+// wave's u paths ("path buffers").  Law selectors (selPP, selPPB) stay 0/1 with
+// the other slot implied.
+__host__ __device__ __forceinline__ int sel_u(unsigned s) { return (int)(s & 3u); }
+__host__ __device__ __forceinline__ int sel_p(unsigned s) { return (int)((s >> 2) & 3u); }
+__host__ __device__ __forceinline__ int sel_buf(unsigned s, int flip) {  // flip: 0 u, 1 u°
+  return flip ? sel_p(s) : sel_u(s);
+}
+__host__ __device__ __forceinline__ uint8_t sel_make(int u, int p) { return (uint8_t)(u | (p << 2)); }
+__host__ __device__ __forceinline__ uint8_t sel_swap(unsigned s) { return sel_make(sel_p(s), sel_u(s)); }
+__host__ __device__ __forceinline__ uint8_t sel_two(int u) { return sel_make(u, u ^ 1); }
+constexpr uint8_t kSelInit = 4;  // sel_two(0): u in buffer 0, u° in buffer 1
+
 // Thread mappings of the recursion (chosen per ensemble at dmt_create):
 //   MAP_LANE: one lane per (recording, block); tile width tw = 64 recordings
 //   MAP_WAVE: one wavefront per block, 64 consecutive steps per chunk; tw = 1
@@ -52,13 +68,14 @@ struct BlockArgs {
   const int32_t* seg_q;      // [G] first point of the segment within its recording
   const int32_t* seg_np;     // [G] points of the segment
   const int64_t* st_off;     // [G] first step of the segment in reference (Z) order
-  uint8_t* selX;             // [G] physical buffer holding u.XX[g]; u° holds the other
-                             // (the lane kernel re-points them when it moves a path)
+  uint8_t* selX;             // [G] path selectors (sel_u / sel_p above; the lane kernel
+                             // re-points them when it moves a path or picks u°'s buffer)
   uint8_t* selW;
   const uint8_t* selPP;
   const uint8_t* selPPB;
-  T* X[2];
-  T* W[2];
+  T* X[3];                   // X[2], W[2]: the third path buffers (nullptr: two-buffer ensemble)
+  T* W[3];
+  int nbuf;                  // path buffers per container (2 or 3)
   const T* t;
   int t_shared;
   const T* H[2][2];  // [slot][kind]
@@ -85,7 +102,8 @@ struct BlockArgs {
   uint32_t seg_base;  // global id of local segment 0 (RNG streams; dmt_set_shard)
   double* ll_out;     // [nblocks]
   uint8_t* success;   // [nblocks] or nullptr
-  int repair_div;     // MAP_LANE tile-phase repair while the minority is <= 1/repair_div
+  int repair_div;     // MAP_LANE draws: consolidate a wave's u paths while the lanes outside the
+  int repair_min;     // majority's buffer are <= 1/repair_div of it and >= repair_min (path_plan)
   int resident1;      // linear drift, layout of single-segment blocks of <= kResidentMaxSteps
                       // steps: one-shot draws on k_block_resident
   int lane_split;     // MAP_LANE draws: producer/consumer waves (k_block_ps); the runtime sets
@@ -233,7 +251,7 @@ hipError_t launch_mcmc_persistent(const ModelKey& k, const void* args, const Acc
 hipError_t launch_backward_filter(int precision, const FilterArgs& a, hipStream_t s);
 hipError_t launch_set_prop_law(const ParamArgs& a, hipStream_t s);
 hipError_t launch_set_obs(int precision, int tw, int d, const void* X0, const void* X1,
-                          const uint8_t* selX,
+                          const void* X2, const uint8_t* selX,
                           const int64_t* tile_qoff, const int32_t* seg_rec, const int32_t* seg_q,
                           const int32_t* seg_np, const int32_t* glast, const uint8_t* term,
                           int64_t b0, int64_t b1, double* obsv, int model, double* lawb0,
@@ -241,16 +259,19 @@ hipError_t launch_set_obs(int precision, int tw, int d, const void* X0, const vo
 hipError_t launch_to_planes(int precision, int tw, const double* src, void* dst0, void* dst1,
                             const uint8_t* sel, int flip, int C, int64_t P, const int64_t* pt_off,
                             int64_t G, const int32_t* seg_rec, const int32_t* seg_q,
-                            const int64_t* tile_qoff, hipStream_t s, int incr = 0);
+                            const int64_t* tile_qoff, hipStream_t s, int incr = 0,
+                            void* dst2 = nullptr, int enc = 0);
 hipError_t launch_from_planes_incr(int precision, int tw, double* dst, const void* src0,
                                    const void* src1, const uint8_t* sel, int flip, int C,
                                    int64_t G, const int64_t* pt_off, const int32_t* seg_np,
                                    const int32_t* seg_rec, const int32_t* seg_q,
-                                   const int64_t* tile_qoff, hipStream_t s);
+                                   const int64_t* tile_qoff, hipStream_t s,
+                                   const void* src2 = nullptr, int enc = 0);
 hipError_t launch_from_planes(int precision, int tw, double* dst, const void* src0,
                               const void* src1, const uint8_t* sel, int flip, int C, int64_t P,
                               const int64_t* pt_off, int64_t G, const int32_t* seg_rec,
-                              const int32_t* seg_q, const int64_t* tile_qoff, hipStream_t s);
+                              const int32_t* seg_q, const int64_t* tile_qoff, hipStream_t s,
+                              const void* src2 = nullptr, int enc = 0);
 hipError_t launch_cast(int precision, const double* src, void* dst, int64_t n, hipStream_t s);
 hipError_t launch_cast_back(int precision, const void* src, double* dst, int64_t n, hipStream_t s);
 hipError_t launch_block_sum(const double* ll, const double* llp, const uint8_t* acc, int64_t n,

@@ -176,6 +176,12 @@ __device__ __forceinline__ bool run_segment(const Law<Mdl, T>& L, const T* __res
   }
   PSum<T> ps;
   ps.init();
+#ifdef DMT_PROBE_PKT  // timing probe only: a chunk's X°/W° rows as per-lane K-step packets
+  constexpr bool PKT = MODE == MODE_PCN && !PAIR;
+#else
+  constexpr bool PKT = false;
+#endif
+  T pkx[K][D], pkw[K][M];
 
   struct Chunk {
     T t[K], H[K][HP], F[K][D], W[K][M], Z[K][M], Xu[K][D];
@@ -202,7 +208,7 @@ __device__ __forceinline__ bool run_segment(const Law<Mdl, T>& L, const T* __res
   };
   // one Euler step from registers; returns the Girsanov term G·dt
   auto step = [&](int i, T tn, const T* Hi, const T* Fi, const T* Wi, const T* Zi,
-                  const T* Xui) -> T {
+                  const T* Xui, const int pj) -> T {
     const T dt = tn - tcur;
     T dW[M];
     if (cpx) {
@@ -218,7 +224,8 @@ __device__ __forceinline__ bool run_segment(const Law<Mdl, T>& L, const T* __res
       for (int k = 0; k < M; ++k) {
         if (cpw) lane_st(&Wcdb[((int64_t)(i + 1) * M + k) * kLanes], Wi[k]);
         dW[k] = dfma(rho, Wi[k], srho * (sdt * Zi[k]));
-        lane_st(&Wdb[((int64_t)(i + 1) * M + k) * kLanes], dW[k]);
+        if (PKT && pj >= 0) pkw[pj][k] = dW[k];
+        else lane_st(&Wdb[((int64_t)(i + 1) * M + k) * kLanes], dW[k]);
       }
     }
     T r[D], b[D], sdW[D], Mg[D * D], cg[D];
@@ -250,7 +257,10 @@ __device__ __forceinline__ bool run_segment(const Law<Mdl, T>& L, const T* __res
     }
     euler_step<Mdl, T>(Mg, cg, b, dt, sdW, x);
 #pragma unroll
-    for (int p = 0; p < D; ++p) lane_st(&Xdb[((int64_t)(i + 1) * D + p) * kLanes], x[p]);
+    for (int p = 0; p < D; ++p) {
+      if (PKT && pj >= 0) pkx[pj][p] = x[p];
+      else lane_st(&Xdb[((int64_t)(i + 1) * D + p) * kLanes], x[p]);
+    }
     tcur = tn;
     // recompute_path!(…; skip): the segment's last ll_skip steps add no term
     return (MODE == MODE_RECOMPUTE && i >= nst - ll_skip) ? (T)0 : G * dt;
@@ -295,8 +305,35 @@ __device__ __forceinline__ bool run_segment(const Law<Mdl, T>& L, const T* __res
       T gv[K];
 #pragma unroll
       for (int j = 0; j < K; ++j)
-        gv[j] = step(c0 + j, cur.t[j], cur.H[j], cur.F[j], cur.W[j], cur.Z[j], cur.Xu[j]);
+        gv[j] = step(c0 + j, cur.t[j], cur.H[j], cur.F[j], cur.W[j], cur.Z[j], cur.Xu[j], j);
       ps.template add_subtree<Log2<K>::v>(tree_sum<T, K>(gv));
+      if constexpr (PKT) {
+        static_assert(K * sizeof(T) % 16 == 0, "packets of whole 16-byte pieces");
+        typedef T v16 __attribute__((ext_vector_type(16 / sizeof(T))));
+        constexpr int NV = 16 / sizeof(T);
+#pragma unroll
+        for (int p = 0; p < D; ++p) {
+          T* q = Xd + (row + c0 + 1) * D * kLanes + ((int64_t)p * kLanes + lane) * K;
+#pragma unroll
+          for (int h = 0; h < K / NV; ++h) {
+            v16 v;
+#pragma unroll
+            for (int e = 0; e < NV; ++e) v[e] = pkx[h * NV + e][p];
+            __builtin_nontemporal_store(v, (v16*)(q + h * NV));
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < M; ++k) {
+          T* q = Wd + (row + c0 + 1) * M * kLanes + ((int64_t)k * kLanes + lane) * K;
+#pragma unroll
+          for (int h = 0; h < K / NV; ++h) {
+            v16 v;
+#pragma unroll
+            for (int e = 0; e < NV; ++e) v[e] = pkw[h * NV + e][k];
+            __builtin_nontemporal_store(v, (v16*)(q + h * NV));
+          }
+        }
+      }
       cur = nxt;
     }
   }
@@ -314,7 +351,7 @@ __device__ __forceinline__ bool run_segment(const Law<Mdl, T>& L, const T* __res
       Wi[k] = READW ? lane_ld(&Wsb[((q + 1) * M + k) * kLanes]) : (T)0;
       Zi[k] = DRAW ? (PARITY ? (T)Zg[q * M + k] : ns.get((uint32_t)(i * M + k))) : (T)0;
     }
-    ps.add(step(i, tb[(q + 1) * tst], Hi, Fi, Wi, Zi, Xui));
+    ps.add(step(i, tb[(q + 1) * tst], Hi, Fi, Wi, Zi, Xui, -1));
   }
   sl = ps.finish();
   bool ok = isfinite(sl);
@@ -338,8 +375,51 @@ __device__ __forceinline__ bool map_block(const BlockArgs<T>& a, int64_t& tile, 
   return true;
 }
 
-// tile-phase repair only while the minority is at most 1/repair_div of the wave
-// (BlockArgs::repair_div; 4 by default, DMT_REPAIR_DIV)
+
+// Path buffers of one container (X or W) in a MAP_LANE draw (MODE_PCN: reads u, writes u°),
+// decided per wave over its active lanes from how many lanes hold their u in each buffer
+// ("path buffers").  A partial line costs far more than its bytes: a wave's
+// proposal stores should all go to ONE buffer.  M = the buffer holding most lanes' u.
+//  * a buffer holds no active lane's u and M holds >= 3/4 of them (high acceptance: a wave's
+//    lanes mostly move together): every proposal goes there, nothing is copied;
+//  * three buffers all in use by <= 1/16 stragglers outside M: no copy, the smallest group's
+//    lanes write to M, the rest to the smallest group's buffer;
+//  * otherwise (while the off-M lanes are <= 1/repair_div of the wave and >= repair_min lanes):
+//    consolidate — every lane outside M moves its u to M during the sweep (read before
+//    overwritten) and every proposal goes to buffer 0 or 1 other than M (the tile-phase repair
+//    of two buffers; a wave of a low-acceptance chain stays on two buffers);
+//  * else each lane writes to a buffer other than its own u (mixed).
+// Measured per draw (profiles/r03rep, r03pbuf2; draw + accept loops): C3 (acceptance 0.99) two
+// buffers with the repair 1 137-1 164 µs, with up to 3 mixed lanes per wave 1 351, three buffers
+// without copies 1 037, all lanes flipping together 1 010; C5 (0.54) two buffers mixed 1 899,
+// consolidated 1 818, three buffers in use 2 264-2 284.
+struct PathPlan {
+  int p, src, dst;  // this lane's proposal buffer; its u moves src -> dst (src < 0: stays)
+};
+__device__ __forceinline__ PathPlan path_plan(const bool act, const int u, const int nbuf,
+                                              const int repair_div, const int repair_min) {
+  const int nact = __popcll(__ballot(act));
+  const int c0 = __popcll(__ballot(act && u == 0)), c1 = __popcll(__ballot(act && u == 1));
+  const int c2 = nact - c0 - c1;  // 0 with two buffers
+  int m = c1 > c0 ? 1 : 0, cm = c1 > c0 ? c1 : c0;
+  if (nbuf == 3 && c2 > cm) { m = 2; cm = c2; }
+  const int fr = c0 == 0 ? 0 : (c1 == 0 ? 1 : (nbuf == 3 && c2 == 0 ? 2 : -1));  // a free buffer
+  const int off = nact - cm;
+  const int other = m == 0 ? 1 : 0;  // the proposal buffer of a consolidated wave
+  PathPlan r{u == m ? other : m, -1, -1};  // mixed
+  if (fr >= 0 && 4 * cm >= 3 * nact) {
+    r.p = fr;
+  } else if (nbuf == 3 && fr < 0 && 16 * off <= nact) {
+    const int o1 = m == 0 ? 1 : 0, o2 = m == 2 ? 1 : 2;  // the two buffers other than m
+    const int co1 = o1 == 0 ? c0 : c1, co2 = o2 == 1 ? c1 : c2;
+    const int sm = co1 <= co2 ? o1 : o2;
+    r.p = u == sm ? m : sm;
+  } else if (repair_div * off <= nact && off >= repair_min) {
+    r.p = other;
+    if (u != m) { r.src = u; r.dst = m; }
+  }
+  return r;
+}
 
 // The lane kernel's body for block blk of recording tile `tile`, recording slot `lane` of the
 // tile (the lane-interleaved layout's column); PAIR: two lanes (roles) per recording.
@@ -354,7 +434,7 @@ __device__ __forceinline__ void lane_block(const BlockArgs<T>& a, const int64_t 
 
   T x[D];
   {
-    const T* Xs = a.X[a.selX[g0] ^ a.xs_flip];
+    const T* Xs = a.X[sel_buf(a.selX[g0], a.xs_flip)];
     const int64_t q = a.seg_q[g0];
 #pragma unroll
     for (int p = 0; p < D; ++p) x[p] = Xs[idx(q, p, D)];
@@ -385,31 +465,21 @@ __device__ __forceinline__ void lane_block(const BlockArgs<T>& a, const int64_t 
     ns.init(a.seed, (uint32_t)g + a.seg_base, a.iter, a.salt);
     const double* Zg = a.Z ? a.Z + a.st_off[g] * M : nullptr;
     const int sx = a.selX[g], sw = a.selW[g];
-    T* Xd = a.X[sx ^ a.xd_flip];
-    const T* Ws = a.W[sw ^ a.ws_flip];
-    T* Wd = a.W[sw ^ a.wd_flip];
+    T* Xd = a.X[sel_buf(sx, a.xd_flip)];
+    const T* Ws = a.W[sel_buf(sw, a.ws_flip)];
+    T* Wd = a.W[sel_buf(sw, a.wd_flip)];
     const T* Xcs = nullptr;
     T *Xcd = nullptr, *Wcd = nullptr;
     int nsx = sx, nsw = sw;
-    if (MODE == MODE_PCN) {
-      // Tile-phase repair: proposals of all active lanes go to the buffer opposite the
-      // majority's u; a minority lane first moves its u there (copy during the sweep) and
-      // re-points its selector, so the wave's stores stay full-line.
-      // Only worth it while the minority is small: a copied lane costs its path once more
-      // (read u.X, write u.X and u.W), mixed lanes cost partial lines for the whole wave.
-      const uint64_t act = __ballot(1);
-      const int nact = __popcll(act);
-      const int ox = __popcll(__ballot(sx != 0)), ow = __popcll(__ballot(sw != 0));
-      const int px = 2 * ox > nact ? 1 : 0, pw = 2 * ow > nact ? 1 : 0;
-      const int mx = px ? nact - ox : ox, mw = pw ? nact - ow : ow;  // minority sizes
-      if (a.repair_div * mx <= nact) {
-        Xd = a.X[px ^ a.xd_flip];
-        if (sx != px) { Xcs = a.X[sx ^ a.xs_flip]; Xcd = a.X[px ^ a.xs_flip]; nsx = px; }
-      }
-      if (a.repair_div * mw <= nact) {
-        Wd = a.W[pw ^ a.wd_flip];
-        if (sw != pw) { Wcd = a.W[pw ^ a.ws_flip]; nsw = pw; }
-      }
+    if (MODE == MODE_PCN) {  // one proposal buffer per wave (path_plan)
+      const PathPlan px = path_plan(true, sel_u(sx), a.nbuf, a.repair_div, a.repair_min);
+      const PathPlan pw = path_plan(true, sel_u(sw), a.nbuf, a.repair_div, a.repair_min);
+      Xd = a.X[px.p];
+      Wd = a.W[pw.p];
+      if (px.src >= 0) { Xcs = a.X[px.src]; Xcd = a.X[px.dst]; }
+      if (pw.src >= 0) Wcd = a.W[pw.dst];
+      nsx = sel_make(px.src >= 0 ? px.dst : sel_u(sx), px.p);
+      nsw = sel_make(pw.src >= 0 ? pw.dst : sel_u(sw), pw.p);
     }
     T sl;
     const bool sok = run_segment<Mdl, T, MODE, PARITY, K, PAIR, TD>(
@@ -514,28 +584,19 @@ __global__ __launch_bounds__(128, DMT_PS_MINW) void k_block_ps(const BlockArgs<T
   const T rho = act ? (T)a.rho[blk] : (T)0;
   const T srho = act ? (T)a.srho[blk] : (T)1;
   // selectors and the tile-phase repair decision (k_block), identical in both waves
-  const int sx = act ? a.selX[g] : 0, sw = act ? a.selW[g] : 0;
-  T* Xd = a.X[sx ^ a.xd_flip];
-  const T* Ws = a.W[sw ^ a.ws_flip];
-  T* Wd = a.W[sw ^ a.wd_flip];
+  const int sx = act ? a.selX[g] : kSelInit, sw = act ? a.selW[g] : kSelInit;
+  const T* Ws = a.W[sel_buf(sw, a.ws_flip)];
   const T *Xcs = nullptr;
   T *Xcd = nullptr, *Wcd = nullptr;
-  int nsx = sx, nsw = sw;
-  {
-    const uint64_t am = __ballot(act);
-    const int nact = __popcll(am);
-    const int ox = __popcll(__ballot(act && sx != 0)), ow = __popcll(__ballot(act && sw != 0));
-    const int px = 2 * ox > nact ? 1 : 0, pw = 2 * ow > nact ? 1 : 0;
-    const int mx = px ? nact - ox : ox, mw = pw ? nact - ow : ow;
-    if (a.repair_div * mx <= nact) {
-      Xd = a.X[px ^ a.xd_flip];
-      if (sx != px) { Xcs = a.X[sx ^ a.xs_flip]; Xcd = a.X[px ^ a.xs_flip]; nsx = px; }
-    }
-    if (a.repair_div * mw <= nact) {
-      Wd = a.W[pw ^ a.wd_flip];
-      if (sw != pw) { Wcd = a.W[pw ^ a.ws_flip]; nsw = pw; }
-    }
-  }
+  // one proposal buffer per wave (path_plan; MODE_PCN)
+  const PathPlan px = path_plan(act, sel_u(sx), a.nbuf, a.repair_div, a.repair_min);
+  const PathPlan pw = path_plan(act, sel_u(sw), a.nbuf, a.repair_div, a.repair_min);
+  T* Xd = a.X[px.p];
+  T* Wd = a.W[pw.p];
+  if (px.src >= 0) { Xcs = a.X[px.src]; Xcd = a.X[px.dst]; }
+  if (pw.src >= 0) Wcd = a.W[pw.dst];
+  const int nsx = sel_make(px.src >= 0 ? px.dst : sel_u(sx), px.p);
+  const int nsw = sel_make(pw.src >= 0 ? pw.dst : sel_u(sw), pw.p);
   auto idx = [&](int64_t q, int c, int C) -> int64_t { return ((row + q) * C + c) * kLanes + lane; };
 
   if (w == 0) {
@@ -621,7 +682,7 @@ __global__ __launch_bounds__(128, DMT_PS_MINW) void k_block_ps(const BlockArgs<T
     const T* Fb = a.F[ls][0] + row * D * kLanes + lane;
     T x[D];
     {
-      const T* Xs = a.X[sx ^ a.xs_flip];
+      const T* Xs = a.X[sel_buf(sx, a.xs_flip)];
 #pragma unroll
       for (int p = 0; p < D; ++p) x[p] = Xs[idx(0, p, D)];
     }
@@ -751,7 +812,7 @@ __global__ __launch_bounds__(64) void k_pathll(const BlockArgs<T> a) {
   {
     const int ls = a.selPP[g0] ^ a.law_flip;
     const double* Lr = a.law[ls][0] + (int64_t)g0 * DMT_LAW_STRIDE;
-    const T* Xs = a.X[a.selX[g0] ^ a.xs_flip];
+    const T* Xs = a.X[sel_buf(a.selX[g0], a.xs_flip)];
     const int64_t q = a.seg_q[g0];
     T H0[HP], F0[D], x0[D];
 #pragma unroll
@@ -771,7 +832,7 @@ __global__ __launch_bounds__(64) void k_pathll(const BlockArgs<T> a) {
     const T* __restrict__ Ht = a.H[ls][kind];
     const T* __restrict__ Ft = a.F[ls][kind];
     const int Hsh = a.H_shared[ls][kind];
-    const T* __restrict__ Xs = a.X[a.selX[g] ^ a.xs_flip];
+    const T* __restrict__ Xs = a.X[sel_buf(a.selX[g], a.xs_flip)];
     const int64_t q0 = a.seg_q[g];
     const int nst = a.seg_np[g] - 1;
     constexpr int CA = D * D + D;  // time-dependent auxiliary law (run_segment)
@@ -930,7 +991,7 @@ __global__ __launch_bounds__(128) void k_block_wave(const BlockArgs<T> a) {
   };
   T x[D];
   {
-    const T* Xs = a.X[a.selX[g0] ^ a.xs_flip];
+    const T* Xs = a.X[sel_buf(a.selX[g0], a.xs_flip)];
     const int64_t q = a.seg_q[g0];
 #pragma unroll
     for (int p = 0; p < D; ++p) x[p] = Xs[(tq + q) * D + p];
@@ -1027,7 +1088,7 @@ __global__ __launch_bounds__(128) void k_block_wave(const BlockArgs<T> a) {
     const T* tb = a.t_shared ? a.t + q0 : a.t + row;
     const T* Hb = a.H_shared[ls][kind] ? a.H[ls][kind] + q0 * HP : a.H[ls][kind] + row * HP;
     const T* Fb = a.F[ls][kind] + row * D;
-    const T* Wsb = a.W[a.selW[g] ^ a.ws_flip] + row * M;
+    const T* Wsb = a.W[sel_buf(a.selW[g], a.ws_flip)] + row * M;
     const int cnt = min(64, nst - c0);
     const bool valid = lane < cnt;
     const int i = c0 + (valid ? lane : cnt - 1);
@@ -1121,8 +1182,8 @@ __global__ __launch_bounds__(128) void k_block_wave(const BlockArgs<T> a) {
     const bool seg_end = c0 + 64 >= nst;
     if (k <= stop_after) {
       const int64_t row = tq + a.seg_q[g];
-      T* Xdb = a.X[a.selX[g] ^ a.xd_flip] + row * D;
-      T* Wdb = a.W[a.selW[g] ^ a.wd_flip] + row * M;
+      T* Xdb = a.X[sel_buf(a.selX[g], a.xd_flip)] + row * D;
+      T* Wdb = a.W[sel_buf(a.selW[g], a.wd_flip)] + row * M;
       if (valid) {
         const int i = c0 + lane;
 #pragma unroll
@@ -1248,8 +1309,9 @@ __device__ __forceinline__ void store_row(T* p, const T* v) {
 struct SelGlobal {
   const uint8_t* sx;
   const uint8_t* sw;
-  __device__ __forceinline__ int x(int g) const { return ldc(sx + g); }
-  __device__ __forceinline__ int w(int g) const { return ldc(sw + g); }
+  // u's buffer (0/1: linear models keep two path buffers, u° = u ^ 1)
+  __device__ __forceinline__ int x(int g) const { return sel_u(ldc(sx + g)); }
+  __device__ __forceinline__ int w(int g) const { return sel_u(ldc(sw + g)); }
 };
 struct SelMask {
   uint64_t mx, mw;
@@ -1723,8 +1785,8 @@ __device__ __forceinline__ void mcmc_scan_block(const BlockArgs<T>& a, const Acc
   const int g0 = ldc(&a.binfo[blk].g0), g1 = ldc(&a.binfo[blk].g1);
   const int nseg = g1 - g0 + 1;  // ≤ kPersistMaxSegments = 64 (host-checked)
   const bool own = lane < nseg;
-  SelMask sel{__ballot(own && a.selX[g0 + (own ? lane : 0)] != 0),
-              __ballot(own && a.selW[g0 + (own ? lane : 0)] != 0), g0};
+  SelMask sel{__ballot(own && sel_u(a.selX[g0 + (own ? lane : 0)]) != 0),
+              __ballot(own && sel_u(a.selW[g0 + (own ? lane : 0)]) != 0), g0};
   const uint64_t all = nseg >= 64 ? ~(uint64_t)0 : (((uint64_t)1 << nseg) - 1);
   double ll = wave_uniform(c.ll[blk]), llp = 0.0;
   const int64_t nb = a.b1 - a.b0, j = blk - a.b0;
@@ -1762,8 +1824,8 @@ __device__ __forceinline__ void mcmc_scan_block(const BlockArgs<T>& a, const Acc
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   }
   if (own) {
-    a.selX[g0 + lane] = (uint8_t)sel.x(g0 + lane);
-    a.selW[g0 + lane] = (uint8_t)sel.w(g0 + lane);
+    a.selX[g0 + lane] = sel_two(sel.x(g0 + lane));
+    a.selW[g0 + lane] = sel_two(sel.w(g0 + lane));
   }
   if (lane == 0) {
     c.ll[blk] = ll;
@@ -1834,7 +1896,7 @@ __device__ __forceinline__ void resident_block(const BlockArgs<T>& a, const Acce
   const T* tb = a.t_shared ? a.t + q0 : a.t + row;
   const T* Hb = a.H_shared[ls][kind] ? a.H[ls][kind] + (int64_t)q0 * HP : a.H[ls][kind] + row * HP;
   const T* Fb = a.F[ls][kind] + row * D;
-  SelMask sel{(uint64_t)(a.selX[g] & 1), (uint64_t)(a.selW[g] & 1), g};
+  SelMask sel{(uint64_t)sel_u(a.selX[g]), (uint64_t)sel_u(a.selW[g]), g};
   T* const Xd[2] = {a.X[0] + row * D, a.X[1] + row * D};
   T* const Wd[2] = {a.W[0] + row * M, a.W[1] + row * M};
   // ---- per-launch state: start point, loglikhd_obs, per-step constants (run order)
@@ -2084,8 +2146,8 @@ __device__ __forceinline__ void resident_block(const BlockArgs<T>& a, const Acce
     }
   }
   if (MCMC && lane == 0) {
-    a.selX[g] = (uint8_t)sel.x(g);
-    a.selW[g] = (uint8_t)sel.w(g);
+    a.selX[g] = sel_two(sel.x(g));
+    a.selW[g] = sel_two(sel.w(g));
     c.ll[blk] = ll;
     c.llp[blk] = llp;
   }
@@ -2253,7 +2315,7 @@ __device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, cons
   const T* tb = a.t_shared ? a.t + q0 : a.t + row;
   const T* Hb = a.H_shared[ls][kind] ? a.H[ls][kind] + (int64_t)q0 * HP : a.H[ls][kind] + row * HP;
   const T* Fb = a.F[ls][kind] + row * D;
-  SelMask sel{(uint64_t)(a.selX[g] & 1), (uint64_t)(a.selW[g] & 1), g};
+  SelMask sel{(uint64_t)sel_u(a.selX[g]), (uint64_t)sel_u(a.selW[g]), g};
   T* const Xd[2] = {a.X[0] + row * D, a.X[1] + row * D};
   T x0[D], llobs;
   {
@@ -2547,8 +2609,8 @@ __device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, cons
     }
   }
   if (valid && lane == 0) {
-    a.selX[g] = (uint8_t)sel.x(g);
-    a.selW[g] = (uint8_t)sel.w(g);
+    a.selX[g] = sel_two(sel.x(g));
+    a.selW[g] = sel_two(sel.w(g));
     c.ll[blk] = ll;
     c.llp[blk] = llp;
   }
@@ -2589,7 +2651,7 @@ __device__ __forceinline__ void resident_pc_producer(const BlockArgs<T>& a, cons
   const T* tb = a.t_shared ? a.t + q0 : a.t + row;
   const T* Hb = a.H_shared[ls][kind] ? a.H[ls][kind] + (int64_t)q0 * HP : a.H[ls][kind] + row * HP;
   const T* Fb = a.F[ls][kind] + row * D;
-  SelMask sel{(uint64_t)(a.selX[g] & 1), (uint64_t)(a.selW[g] & 1), g};
+  SelMask sel{(uint64_t)sel_u(a.selX[g]), (uint64_t)sel_u(a.selW[g]), g};
   T* const Wd[2] = {a.W[0] + row * M, a.W[1] + row * M};
   T w0[M], dts[RR], sdts[RR], wv[RR][M], cgs[RR][D];
   {
@@ -2786,7 +2848,7 @@ __global__ __launch_bounds__(64) void k_pathll_wave(const BlockArgs<T> a) {
   {
     const int ls = a.selPP[g0] ^ a.law_flip;
     const double* Lr = a.law[ls][0] + (int64_t)g0 * DMT_LAW_STRIDE;
-    const T* Xs = a.X[a.selX[g0] ^ a.xs_flip];
+    const T* Xs = a.X[sel_buf(a.selX[g0], a.xs_flip)];
     const int64_t q = a.seg_q[g0];
     T H0[HP], F0[D], x0[D];
 #pragma unroll
@@ -2805,7 +2867,7 @@ __global__ __launch_bounds__(64) void k_pathll_wave(const BlockArgs<T> a) {
     const T* tb = a.t_shared ? a.t + q0 : a.t + row;
     const T* Hb = a.H_shared[ls][kind] ? a.H[ls][kind] + q0 * HP : a.H[ls][kind] + row * HP;
     const T* Fb = a.F[ls][kind] + row * D;
-    const T* Xb = a.X[a.selX[g] ^ a.xs_flip] + row * D;
+    const T* Xb = a.X[sel_buf(a.selX[g], a.xs_flip)] + row * D;
     const int nst = a.seg_np[g] - 1;
     T acc = (T)0;
     for (int c0 = 0; c0 < nst; c0 += 64) {
@@ -2845,8 +2907,8 @@ __global__ __launch_bounds__(256) void k_accept(const AcceptArgs a) {
   const bool acc = E > -(llp - ll);
   if (acc) {
     for (int g = a.gfirst[blk]; g <= a.glast[blk]; ++g) {
-      a.selX[g] ^= 1;
-      a.selW[g] ^= 1;
+      a.selX[g] = sel_swap(a.selX[g]);
+      a.selW[g] = sel_swap(a.selW[g]);
     }
   }
   if (a.hist_len > 0) {
@@ -2879,8 +2941,8 @@ __global__ __launch_bounds__(1024) void k_accept_reduce(const AcceptArgs a, doub
     const bool acc = E > -(llp - ll);
     if (acc) {
       for (int g = a.gfirst[blk]; g <= a.glast[blk]; ++g) {
-        a.selX[g] ^= 1;
-        a.selW[g] ^= 1;
+        a.selX[g] = sel_swap(a.selX[g]);
+        a.selW[g] = sel_swap(a.selW[g]);
       }
     }
     if (a.hist_len > 0) {
@@ -2946,8 +3008,8 @@ __global__ __launch_bounds__(kAccGroup) void k_accept_reduce_lb(const AcceptArgs
     const bool acc = E > -(llp - ll);
     if (acc) {
       for (int g = a.gfirst[blk]; g <= a.glast[blk]; ++g) {
-        a.selX[g] ^= 1;
-        a.selW[g] ^= 1;
+        a.selX[g] = sel_swap(a.selX[g]);
+        a.selW[g] = sel_swap(a.selW[g]);
       }
     }
     if (a.hist_len > 0) {
@@ -3644,7 +3706,8 @@ __global__ __launch_bounds__(64) void k_set_prop_law(const ParamArgs a, int wg_p
 // linearised at an anchor (FHN y_T, Lorenz x_T) are re-anchored there and re-derived
 // (set_obs!).
 template <class T>
-__global__ void k_set_obs(int tw, int d, const T* X0, const T* X1, const uint8_t* selX,
+__global__ void k_set_obs(int tw, int d, const T* X0, const T* X1, const T* X2,
+                          const uint8_t* selX,
                           const int64_t* tile_qoff, const int32_t* seg_rec, const int32_t* seg_q,
                           const int32_t* seg_np, const int32_t* glast, const uint8_t* term,
                           int64_t b0, int64_t b1, double* obsv, int model, double* lawb0,
@@ -3652,7 +3715,8 @@ __global__ void k_set_obs(int tw, int d, const T* X0, const T* X1, const uint8_t
   const int64_t blk = b0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (blk >= b1 || term[blk]) return;
   const int g = glast[blk];
-  const T* X = selX[g] ? X1 : X0;  // u.XX
+  const int xb = sel_u(selX[g]);
+  const T* X = xb == 0 ? X0 : xb == 1 ? X1 : X2;  // u.XX
   const int64_t r = seg_rec[g];
   const int64_t q = seg_q[g] + seg_np[g] - 1;
   double v[3] = {0.0, 0.0, 0.0};
@@ -3687,7 +3751,8 @@ __global__ void k_flip(const FlipArgs f, const int32_t* gfirst, const int32_t* g
   for (int g = gfirst[blk] + gs; g <= glast[blk]; g += st)
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      if (f.sel[i] && !(f.only_nonterm[i] && tm)) f.sel[i][g] ^= 1;
+      if (f.sel[i] && !(f.only_nonterm[i] && tm))
+        f.sel[i][g] = i < 2 ? sel_swap(f.sel[i][g]) : (uint8_t)(f.sel[i][g] ^ 1);  // paths: swap u/u°
 }
 
 __global__ void k_swap_ll(double* ll, double* llp, int64_t b0, int64_t b1) {
@@ -3715,11 +3780,19 @@ __device__ __forceinline__ int64_t find_seg(const int64_t* pt_off, int64_t G, in
   return lo;
 }
 
+// Physical buffer of segment g: path selectors (enc = 1: sel_buf) or law / 0-1 selectors
+// (the other slot implied); no selector: buffer 0.
+__device__ __forceinline__ int plane_slot(const uint8_t* sel, int enc, int64_t g, int flip) {
+  if (!sel) return 0;
+  return enc ? sel_buf(sel[g], flip) : ((sel[g] ^ flip) & 1);
+}
+
 // Reference layout -> planes.  incr: the source is a cumulative Wiener path; the planes get
 // row 0 = W(t0) and row i+1 = W(t_{i+1}) - W(t_i), computed in the working precision.
 template <class T>
 __global__ void k_to_planes(const int tw, const double* __restrict__ src, T* dst0, T* dst1,
-                            const uint8_t* __restrict__ sel, int flip, int C, int64_t P,
+                            T* dst2, const uint8_t* __restrict__ sel, int enc, int flip, int C,
+                            int64_t P,
                             const int64_t* __restrict__ pt_off, int64_t G,
                             const int32_t* __restrict__ seg_rec, const int32_t* __restrict__ seg_q,
                             const int64_t* __restrict__ tile_qoff, int incr) {
@@ -3731,16 +3804,17 @@ __global__ void k_to_planes(const int tw, const double* __restrict__ src, T* dst
   const int64_t r = seg_rec[g];
   const int64_t q = seg_q[g] + (p - pt_off[g]);
   const int64_t o = ((tile_qoff[r / tw] + q) * C + c) * tw + (r % tw);
-  const int slot = sel ? ((sel[g] ^ flip) & 1) : 0;
+  const int slot = plane_slot(sel, enc, g, flip);
   T v = (T)src[e];
   if (incr && p > pt_off[g]) v = v - (T)src[e - C];
-  (slot ? dst1 : dst0)[o] = v;
+  (slot == 0 ? dst0 : slot == 1 ? dst1 : dst2)[o] = v;
 }
 
 // planes (increments) -> cumulative reference layout: one thread per (segment, component)
 template <class T>
 __global__ void k_from_planes_incr(const int tw, double* __restrict__ dst, const T* src0,
-                                   const T* src1, const uint8_t* __restrict__ sel, int flip, int C,
+                                   const T* src1, const T* src2, const uint8_t* __restrict__ sel,
+                                   int enc, int flip, int C,
                                    int64_t G, const int64_t* __restrict__ pt_off,
                                    const int32_t* __restrict__ seg_np,
                                    const int32_t* __restrict__ seg_rec,
@@ -3751,8 +3825,8 @@ __global__ void k_from_planes_incr(const int tw, double* __restrict__ dst, const
   const int64_t g = e / C;
   const int c = (int)(e % C);
   const int64_t r = seg_rec[g];
-  const int slot = sel ? ((sel[g] ^ flip) & 1) : 0;
-  const T* src = slot ? src1 : src0;
+  const int slot = plane_slot(sel, enc, g, flip);
+  const T* src = slot == 0 ? src0 : slot == 1 ? src1 : src2;
   T acc = (T)0;
   for (int i = 0; i < seg_np[g]; ++i) {
     const int64_t o = ((tile_qoff[r / tw] + seg_q[g] + i) * C + c) * tw + (r % tw);
@@ -3763,7 +3837,8 @@ __global__ void k_from_planes_incr(const int tw, double* __restrict__ dst, const
 
 template <class T>
 __global__ void k_from_planes(const int tw, double* __restrict__ dst, const T* src0, const T* src1,
-                              const uint8_t* __restrict__ sel, int flip, int C, int64_t P,
+                              const T* src2, const uint8_t* __restrict__ sel, int enc, int flip,
+                              int C, int64_t P,
                               const int64_t* __restrict__ pt_off, int64_t G,
                               const int32_t* __restrict__ seg_rec,
                               const int32_t* __restrict__ seg_q,
@@ -3776,8 +3851,8 @@ __global__ void k_from_planes(const int tw, double* __restrict__ dst, const T* s
   const int64_t r = seg_rec[g];
   const int64_t q = seg_q[g] + (p - pt_off[g]);
   const int64_t o = ((tile_qoff[r / tw] + q) * C + c) * tw + (r % tw);
-  const int slot = sel ? ((sel[g] ^ flip) & 1) : 0;
-  dst[e] = (double)(slot ? src1 : src0)[o];
+  const int slot = plane_slot(sel, enc, g, flip);
+  dst[e] = (double)(slot == 0 ? src0 : slot == 1 ? src1 : src2)[o];
 }
 
 template <class T>
@@ -3986,8 +4061,8 @@ __global__ __launch_bounds__(64) void k_invsolve(const BlockArgs<T> a) {
     const T* Ht = a.H[ls][kind];
     const T* Ft = a.F[ls][kind];
     const int Hsh = a.H_shared[ls][kind];
-    const T* Xs = a.X[a.selX[g] ^ a.xs_flip];
-    T* Wd = a.W[a.selW[g] ^ a.wd_flip];
+    const T* Xs = a.X[sel_buf(a.selX[g], a.xs_flip)];
+    T* Wd = a.W[sel_buf(a.selW[g], a.wd_flip)];
     const int64_t q0 = a.seg_q[g];
     const int nst = a.seg_np[g] - 1;
 #pragma unroll
@@ -4038,8 +4113,8 @@ __global__ __launch_bounds__(64) void k_invsolve_wave(const BlockArgs<T> a) {
     const T* tb = a.t_shared ? a.t + q0 : a.t + row;
     const T* Hb = a.H_shared[ls][kind] ? a.H[ls][kind] + q0 * HP : a.H[ls][kind] + row * HP;
     const T* Fb = a.F[ls][kind] + row * D;
-    const T* Xb = a.X[a.selX[g] ^ a.xs_flip] + row * D;
-    T* Wb = a.W[a.selW[g] ^ a.wd_flip] + row * M;
+    const T* Xb = a.X[sel_buf(a.selX[g], a.xs_flip)] + row * D;
+    T* Wb = a.W[sel_buf(a.selW[g], a.wd_flip)] + row * M;
     const int nst = a.seg_np[g] - 1;
     if (lane == 0) {
 #pragma unroll
@@ -4277,7 +4352,7 @@ hipError_t launch_set_prop_law(const ParamArgs& a, hipStream_t s) {
 }
 
 hipError_t launch_set_obs(int precision, int tw, int d, const void* X0, const void* X1,
-                          const uint8_t* selX, const int64_t* tile_qoff, const int32_t* seg_rec,
+                          const void* X2, const uint8_t* selX, const int64_t* tile_qoff, const int32_t* seg_rec,
                           const int32_t* seg_q, const int32_t* seg_np, const int32_t* glast,
                           const uint8_t* term, int64_t b0, int64_t b1, double* obsv,
                           int model, double* lawb0, double* lawb1, hipStream_t s) {
@@ -4285,10 +4360,11 @@ hipError_t launch_set_obs(int precision, int tw, int d, const void* X0, const vo
   if (n <= 0) return hipSuccess;
   if (precision == DMT_F64)
     k_set_obs<double><<<nblk(n, 256), 256, 0, s>>>(tw, d, (const double*)X0, (const double*)X1,
-                                                   selX, tile_qoff, seg_rec, seg_q, seg_np, glast,
+                                                   (const double*)X2, selX, tile_qoff, seg_rec, seg_q, seg_np, glast,
                                                    term, b0, b1, obsv, model, lawb0, lawb1);
   else
-    k_set_obs<float><<<nblk(n, 256), 256, 0, s>>>(tw, d, (const float*)X0, (const float*)X1, selX,
+    k_set_obs<float><<<nblk(n, 256), 256, 0, s>>>(tw, d, (const float*)X0, (const float*)X1,
+                                                  (const float*)X2, selX,
                                                   tile_qoff, seg_rec, seg_q, seg_np, glast, term,
                                                   b0, b1, obsv, model, lawb0, lawb1);
   return hipGetLastError();
@@ -4304,15 +4380,18 @@ hipError_t launch_accept(const AcceptArgs& a, hipStream_t s) {
 hipError_t launch_to_planes(int precision, int tw, const double* src, void* dst0, void* dst1,
                             const uint8_t* sel, int flip, int C, int64_t P, const int64_t* pt_off,
                             int64_t G, const int32_t* seg_rec, const int32_t* seg_q,
-                            const int64_t* tile_qoff, hipStream_t s, int incr) {
+                            const int64_t* tile_qoff, hipStream_t s, int incr, void* dst2,
+                            int enc) {
   const int64_t n = P * C;
   if (n <= 0) return hipSuccess;
   if (precision == DMT_F64)
-    k_to_planes<double><<<nblk(n, 256), 256, 0, s>>>(tw, src, (double*)dst0, (double*)dst1, sel, flip,
-                                                      C, P, pt_off, G, seg_rec, seg_q, tile_qoff, incr);
+    k_to_planes<double><<<nblk(n, 256), 256, 0, s>>>(tw, src, (double*)dst0, (double*)dst1,
+                                                      (double*)dst2, sel, enc, flip, C, P, pt_off,
+                                                      G, seg_rec, seg_q, tile_qoff, incr);
   else
-    k_to_planes<float><<<nblk(n, 256), 256, 0, s>>>(tw, src, (float*)dst0, (float*)dst1, sel, flip, C,
-                                                     P, pt_off, G, seg_rec, seg_q, tile_qoff, incr);
+    k_to_planes<float><<<nblk(n, 256), 256, 0, s>>>(tw, src, (float*)dst0, (float*)dst1,
+                                                     (float*)dst2, sel, enc, flip, C, P, pt_off, G,
+                                                     seg_rec, seg_q, tile_qoff, incr);
   return hipGetLastError();
 }
 
@@ -4320,16 +4399,19 @@ hipError_t launch_from_planes_incr(int precision, int tw, double* dst, const voi
                                    const void* src1, const uint8_t* sel, int flip, int C,
                                    int64_t G, const int64_t* pt_off, const int32_t* seg_np,
                                    const int32_t* seg_rec, const int32_t* seg_q,
-                                   const int64_t* tile_qoff, hipStream_t s) {
+                                   const int64_t* tile_qoff, hipStream_t s, const void* src2,
+                                   int enc) {
   const int64_t n = G * C;
   if (n <= 0) return hipSuccess;
   if (precision == DMT_F64)
     k_from_planes_incr<double><<<nblk(n, 64), 64, 0, s>>>(tw, dst, (const double*)src0,
-                                                          (const double*)src1, sel, flip, C, G,
+                                                          (const double*)src1, (const double*)src2,
+                                                          sel, enc, flip, C, G,
                                                           pt_off, seg_np, seg_rec, seg_q, tile_qoff);
   else
     k_from_planes_incr<float><<<nblk(n, 64), 64, 0, s>>>(tw, dst, (const float*)src0,
-                                                         (const float*)src1, sel, flip, C, G,
+                                                         (const float*)src1, (const float*)src2,
+                                                         sel, enc, flip, C, G,
                                                          pt_off, seg_np, seg_rec, seg_q, tile_qoff);
   return hipGetLastError();
 }
@@ -4337,16 +4419,19 @@ hipError_t launch_from_planes_incr(int precision, int tw, double* dst, const voi
 hipError_t launch_from_planes(int precision, int tw, double* dst, const void* src0, const void* src1,
                               const uint8_t* sel, int flip, int C, int64_t P,
                               const int64_t* pt_off, int64_t G, const int32_t* seg_rec,
-                              const int32_t* seg_q, const int64_t* tile_qoff, hipStream_t s) {
+                              const int32_t* seg_q, const int64_t* tile_qoff, hipStream_t s,
+                              const void* src2, int enc) {
   const int64_t n = P * C;
   if (n <= 0) return hipSuccess;
   if (precision == DMT_F64)
     k_from_planes<double><<<nblk(n, 256), 256, 0, s>>>(tw, dst, (const double*)src0,
-                                                        (const double*)src1, sel, flip, C, P,
+                                                        (const double*)src1, (const double*)src2,
+                                                        sel, enc, flip, C, P,
                                                         pt_off, G, seg_rec, seg_q, tile_qoff);
   else
     k_from_planes<float><<<nblk(n, 256), 256, 0, s>>>(tw, dst, (const float*)src0, (const float*)src1,
-                                                       sel, flip, C, P, pt_off, G, seg_rec, seg_q,
+                                                       (const float*)src2, sel, enc, flip, C, P,
+                                                       pt_off, G, seg_rec, seg_q,
                                                        tile_qoff);
   return hipGetLastError();
 }

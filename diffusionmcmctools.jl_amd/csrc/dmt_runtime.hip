@@ -171,8 +171,9 @@ struct dmt_ens {
   int32_t* d_seg_np = nullptr;
   uint8_t* d_sel[4] = {nullptr, nullptr, nullptr, nullptr};  // X, W, PP, PPB
   std::vector<uint8_t> h_selPP, h_selPPB;                     // host mirrors (laws swap only by dmt_swap)
-  void* d_X[2] = {nullptr, nullptr};
-  void* d_W[2] = {nullptr, nullptr};
+  void* d_X[3] = {nullptr, nullptr, nullptr};  // path buffers; [2]: MAP_LANE only (nbuf = 3)
+  void* d_W[3] = {nullptr, nullptr, nullptr};
+  int nbuf = 2;  // path buffers per container (DESIGN.md §2 "path buffers"; DMT_PATH_BUFS)
   void* d_t = nullptr;
   bool have_t = false;
   void* d_H[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};  // [slot][kind]
@@ -227,7 +228,8 @@ struct dmt_ens {
   int lane_pair = -1;        // MAP_LANE device-RNG draws on lane pairs: 1 on, 0 off, -1 auto
                              // (when the draw has fewer waves than the device has SIMDs)
   int64_t n_simd = 1024;
-  int repair_div = 4;        // MAP_LANE tile-phase repair threshold (DMT_REPAIR_DIV)
+  int repair_div = 1;        // MAP_LANE path consolidation threshold (DMT_REPAIR_DIV; path_plan)
+  int repair_min = 1;        // … and minimum minority (DMT_REPAIR_MIN)
   bool scan_resident = true; // one-shot OU draws on k_block_resident when eligible (DMT_SCAN_RESIDENT=0: off)
   std::vector<std::unique_ptr<Layout>> layouts;  // layouts[0] = internal "unit" layout
   // timing
@@ -469,9 +471,12 @@ void fill_common(dmt_ens* h, const Layout* L, BlockArgs<T>& a) {
   a.selW = h->d_sel[1];
   a.selPP = h->d_sel[2];
   a.selPPB = h->d_sel[3];
-  for (int s = 0; s < 2; ++s) {
+  a.nbuf = h->nbuf;
+  for (int s = 0; s < 3; ++s) {
     a.X[s] = (T*)h->d_X[s];
     a.W[s] = (T*)h->d_W[s];
+  }
+  for (int s = 0; s < 2; ++s) {
     for (int k = 0; k < 2; ++k) {
       a.H[s][k] = (const T*)h->d_H[s][k];
       a.H_shared[s][k] = h->H_shared[k];
@@ -497,6 +502,7 @@ void fill_common(dmt_ens* h, const Layout* L, BlockArgs<T>& a) {
   a.Z = nullptr;
   a.success = nullptr;
   a.repair_div = h->repair_div;
+  a.repair_min = h->repair_min;
   a.lane_split = 0;
   a.lane_pair = 0;
   a.resident1 = 0;
@@ -907,6 +913,7 @@ dmt_status dmt_create(dmt_ens** out, const dmt_model* model, const dmt_structure
       h->wall_khz = (uint64_t)khz;
   }
   if (const char* e = std::getenv("DMT_REPAIR_DIV")) h->repair_div = std::max(1, std::atoi(e));
+  if (const char* e = std::getenv("DMT_REPAIR_MIN")) h->repair_min = std::max(1, std::atoi(e));
   if (const char* e = std::getenv("DMT_SCAN_RESIDENT")) h->scan_resident = std::strcmp(e, "0") != 0;
   {
     hipDeviceProp_t prop;
@@ -945,13 +952,17 @@ dmt_status dmt_create(dmt_ens** out, const dmt_model* model, const dmt_structure
   HIP_OK(hipMemcpy(hp->d_seg_rec, hp->seg_rec.data(), hp->G * 4, hipMemcpyHostToDevice));
   HIP_OK(hipMemcpy(hp->d_seg_q, hp->seg_q.data(), hp->G * 4, hipMemcpyHostToDevice));
   HIP_OK(hipMemcpy(hp->d_seg_np, hp->seg_np.data(), hp->G * 4, hipMemcpyHostToDevice));
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < 4; ++i) {  // paths: u in buffer 0, u° in 1 (kSelInit); laws: slot 0
     DMT_TRY(ens_alloc(hp, &hp->d_sel[i], hp->G));
-    HIP_OK(hipMemset(hp->d_sel[i], 0, hp->G));
+    HIP_OK(hipMemset(hp->d_sel[i], i < 2 ? kSelInit : 0, hp->G));
   }
   hp->h_selPP.assign(hp->G, 0);
   hp->h_selPPB.assign(hp->G, 0);
-  for (int s = 0; s < 2; ++s) {
+  // MAP_LANE: a third path buffer per container, so that a wave's proposals can go to a buffer
+  // none of its lanes' u occupies (DESIGN.md §2 "path buffers"; DMT_PATH_BUFS=2: two)
+  hp->nbuf = hp->mapping == MAP_LANE ? 3 : 2;
+  if (const char* e = std::getenv("DMT_PATH_BUFS")) hp->nbuf = std::atoi(e) == 2 ? 2 : hp->nbuf;
+  for (int s = 0; s < hp->nbuf; ++s) {
     DMT_TRY(ens_alloc_bytes(hp, &hp->d_X[s], plane_elems(hp, hp->d) * hp->esz));
     DMT_TRY(ens_alloc_bytes(hp, &hp->d_W[s], plane_elems(hp, hp->m) * hp->esz));
     HIP_OK(hipMemset(hp->d_X[s], 0, plane_elems(hp, hp->d) * hp->esz));
@@ -1020,7 +1031,7 @@ dmt_status dmt_destroy(dmt_ens* h) {
     if (L) L->release();
   void* ps[] = {h->d_pt_off, h->d_st_off, h->d_tile_qoff, h->d_seg_rec, h->d_seg_q, h->d_seg_np,
                 h->d_sel[0], h->d_sel[1], h->d_sel[2], h->d_sel[3], h->d_X[0], h->d_X[1],
-                h->d_W[0], h->d_W[1], h->d_t, h->d_stage, h->d_Z, h->d_red, h->d_gather,
+                h->d_X[2], h->d_W[0], h->d_W[1], h->d_W[2], h->d_t, h->d_stage, h->d_Z, h->d_red, h->d_gather,
                 h->d_red_work, h->d_run, h->d_run_gather, h->d_part, h->d_red_lb, h->d_obsH,
                 h->d_obsF, h->d_obsc, h->d_obsv, h->d_fail, h->d_fchunk_off, h->d_segsel,
                 h->d_qbuf, h->d_tbuf};
@@ -1214,7 +1225,7 @@ dmt_status dmt_set_paths(dmt_ens* h, int32_t unit, const double* X, const double
     // Wiener paths are held as increments on the device
     HIP_OK(launch_to_planes(h->key.precision, h->tw, h->d_stage, dst[0], dst[1], h->d_sel[w], unit, C[w],
                             h->P, h->d_pt_off, h->G, h->d_seg_rec, h->d_seg_q, h->d_tile_qoff,
-                            h->stream, w == 1 ? 1 : 0));
+                            h->stream, w == 1 ? 1 : 0, dst[2], 1));
   }
   HIP_OK(stream_wait(h));
   return DMT_OK;
@@ -1231,11 +1242,11 @@ dmt_status dmt_download_paths(dmt_ens* h, int32_t unit, int32_t what, double* ou
   if (what != 1)  // XX, or the Wiener increments exactly as held (DMT_PATH_DW)
     HIP_OK(launch_from_planes(h->key.precision, h->tw, h->d_stage, src[0], src[1], h->d_sel[sk], unit,
                               C, h->P, h->d_pt_off, h->G, h->d_seg_rec, h->d_seg_q, h->d_tile_qoff,
-                              h->stream));
+                              h->stream, src[2], 1));
   else  // increments -> cumulative Wiener path
     HIP_OK(launch_from_planes_incr(h->key.precision, h->tw, h->d_stage, src[0], src[1], h->d_sel[what],
                                    unit, C, h->G, h->d_pt_off, h->d_seg_np, h->d_seg_rec, h->d_seg_q,
-                                   h->d_tile_qoff, h->stream));
+                                   h->d_tile_qoff, h->stream, src[2], 1));
   HIP_OK(hipMemcpyAsync(out, h->d_stage, h->P * C * 8, hipMemcpyDeviceToHost, h->stream));
   HIP_OK(stream_wait(h));
   return DMT_OK;
@@ -2004,7 +2015,7 @@ dmt_status dmt_set_obs(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1) {
   Layout* L;
   DMT_TRY(get_layout(h, layout, &L));
   DMT_TRY(check_range(L, b0, b1));
-  HIP_OK(launch_set_obs(h->key.precision, h->tw, h->d, h->d_X[0], h->d_X[1], h->d_sel[0],
+  HIP_OK(launch_set_obs(h->key.precision, h->tw, h->d, h->d_X[0], h->d_X[1], h->d_X[2], h->d_sel[0],
                         h->d_tile_qoff, h->d_seg_rec, h->d_seg_q, h->d_seg_np, L->d_glast,
                         L->d_term, b0, b1, h->d_obsv, h->key.model, h->d_law[0][1],
                         h->d_law[1][1], h->stream));
@@ -2638,11 +2649,11 @@ dmt_status dmt_snapshot_take(dmt_ens* h, int32_t unit, int64_t slot, int64_t mcm
     if (k == 0)
       HIP_OK(launch_from_planes(h->key.precision, h->tw, dst, src[0], src[1], h->d_sel[0], unit, C,
                                 h->P, h->d_pt_off, h->G, h->d_seg_rec, h->d_seg_q, h->d_tile_qoff,
-                                h->stream));
+                                h->stream, src[2], 1));
     else  // increments -> cumulative Wiener path, as dmt_download_paths
       HIP_OK(launch_from_planes_incr(h->key.precision, h->tw, dst, src[0], src[1], h->d_sel[1], unit,
                                      C, h->G, h->d_pt_off, h->d_seg_np, h->d_seg_rec, h->d_seg_q,
-                                     h->d_tile_qoff, h->stream));
+                                     h->d_tile_qoff, h->stream, src[2], 1));
   }
   h->snap_iter[slot] = mcmciter;
   h->snap_unit[slot] = unit;

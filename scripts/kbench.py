@@ -16,6 +16,8 @@ ap.add_argument("--accept", action="store_true", help="accept_reject after every
 ap.add_argument("--step", action="store_true", help="use dmt_mcmc_step")
 ap.add_argument("--accept-all", action="store_true", help="accept_reject with E = +inf (all accept)")
 ap.add_argument("--sync", action="store_true", help="synchronise after every call")
+ap.add_argument("--mix", type=float, default=0.0,
+                help="before timing, accept a random fraction of the blocks (mixed selectors)")
 a = ap.parse_args()
 kw = {"B": a.B} if a.B else {}
 w = {"c2": W.c2_ou2d, "c3": W.c3_fhn, "c5": W.c5_lorenz, "c1": W.c1_ou1d}[a.config](**kw)
@@ -27,6 +29,9 @@ lay = W.fill(ens, w, init_Z=False)
 B = w.nblocks
 Z = np.random.default_rng(0).standard_normal((w.steps_per_iter, w.m)) if a.parity else None
 ens.draw_proposal(lay, 0, B, Z=Z, iter=1)
+if a.mix > 0:
+    acc = np.random.default_rng(1).random(B) < a.mix
+    ens.accept_reject(lay, 0, B, 1, E=np.where(acc, np.inf, -np.inf))
 ens.sync()
 ens.set_timing(True)
 t0 = time.perf_counter()
