@@ -76,6 +76,7 @@ struct BlockArgs {
   T* X[3];                   // X[2], W[2]: the third path buffers (nullptr: two-buffer ensemble)
   T* W[3];
   int nbuf;                  // path buffers per container (2 or 3)
+  int full_copy;             // consolidation rewrites every lane's u (whole lines; DMT_FULL_COPY)
   const T* t;
   int t_shared;
   const T* H[2][2];  // [slot][kind]

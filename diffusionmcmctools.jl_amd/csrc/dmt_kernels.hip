@@ -397,7 +397,8 @@ struct PathPlan {
   int p, src, dst;  // this lane's proposal buffer; its u moves src -> dst (src < 0: stays)
 };
 __device__ __forceinline__ PathPlan path_plan(const bool act, const int u, const int nbuf,
-                                              const int repair_div, const int repair_min) {
+                                              const int repair_div, const int repair_min,
+                                              const int full = 0) {
   const int nact = __popcll(__ballot(act));
   const int c0 = __popcll(__ballot(act && u == 0)), c1 = __popcll(__ballot(act && u == 1));
   const int c2 = nact - c0 - c1;  // 0 with two buffers
@@ -416,7 +417,7 @@ __device__ __forceinline__ PathPlan path_plan(const bool act, const int u, const
     r.p = u == sm ? m : sm;
   } else if (repair_div * off <= nact && off >= repair_min) {
     r.p = other;
-    if (u != m) { r.src = u; r.dst = m; }
+    if (u != m || full) { r.src = u; r.dst = m; }  // full: the majority rewrites its own u too
   }
   return r;
 }
@@ -472,8 +473,8 @@ __device__ __forceinline__ void lane_block(const BlockArgs<T>& a, const int64_t 
     T *Xcd = nullptr, *Wcd = nullptr;
     int nsx = sx, nsw = sw;
     if (MODE == MODE_PCN) {  // one proposal buffer per wave (path_plan)
-      const PathPlan px = path_plan(true, sel_u(sx), a.nbuf, a.repair_div, a.repair_min);
-      const PathPlan pw = path_plan(true, sel_u(sw), a.nbuf, a.repair_div, a.repair_min);
+      const PathPlan px = path_plan(true, sel_u(sx), a.nbuf, a.repair_div, a.repair_min, a.full_copy);
+      const PathPlan pw = path_plan(true, sel_u(sw), a.nbuf, a.repair_div, a.repair_min, a.full_copy);
       Xd = a.X[px.p];
       Wd = a.W[pw.p];
       if (px.src >= 0) { Xcs = a.X[px.src]; Xcd = a.X[px.dst]; }
@@ -589,8 +590,8 @@ __global__ __launch_bounds__(128, DMT_PS_MINW) void k_block_ps(const BlockArgs<T
   const T *Xcs = nullptr;
   T *Xcd = nullptr, *Wcd = nullptr;
   // one proposal buffer per wave (path_plan; MODE_PCN)
-  const PathPlan px = path_plan(act, sel_u(sx), a.nbuf, a.repair_div, a.repair_min);
-  const PathPlan pw = path_plan(act, sel_u(sw), a.nbuf, a.repair_div, a.repair_min);
+  const PathPlan px = path_plan(act, sel_u(sx), a.nbuf, a.repair_div, a.repair_min, a.full_copy);
+  const PathPlan pw = path_plan(act, sel_u(sw), a.nbuf, a.repair_div, a.repair_min, a.full_copy);
   T* Xd = a.X[px.p];
   T* Wd = a.W[pw.p];
   if (px.src >= 0) { Xcs = a.X[px.src]; Xcd = a.X[px.dst]; }

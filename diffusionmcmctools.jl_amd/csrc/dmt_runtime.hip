@@ -173,6 +173,7 @@ struct dmt_ens {
   std::vector<uint8_t> h_selPP, h_selPPB;                     // host mirrors (laws swap only by dmt_swap)
   void* d_X[3] = {nullptr, nullptr, nullptr};  // path buffers; [2]: MAP_LANE only (nbuf = 3)
   void* d_W[3] = {nullptr, nullptr, nullptr};
+  int full_copy = 0;  // DMT_FULL_COPY
   int nbuf = 2;  // path buffers per container (DESIGN.md §2 "path buffers"; DMT_PATH_BUFS)
   void* d_t = nullptr;
   bool have_t = false;
@@ -472,6 +473,7 @@ void fill_common(dmt_ens* h, const Layout* L, BlockArgs<T>& a) {
   a.selPP = h->d_sel[2];
   a.selPPB = h->d_sel[3];
   a.nbuf = h->nbuf;
+  a.full_copy = h->full_copy;
   for (int s = 0; s < 3; ++s) {
     a.X[s] = (T*)h->d_X[s];
     a.W[s] = (T*)h->d_W[s];
@@ -962,6 +964,7 @@ dmt_status dmt_create(dmt_ens** out, const dmt_model* model, const dmt_structure
   // none of its lanes' u occupies (DESIGN.md §2 "path buffers"; DMT_PATH_BUFS=2: two)
   hp->nbuf = hp->mapping == MAP_LANE ? 3 : 2;
   if (const char* e = std::getenv("DMT_PATH_BUFS")) hp->nbuf = std::atoi(e) == 2 ? 2 : hp->nbuf;
+  if (const char* e = std::getenv("DMT_FULL_COPY")) hp->full_copy = std::atoi(e) != 0;
   for (int s = 0; s < hp->nbuf; ++s) {
     DMT_TRY(ens_alloc_bytes(hp, &hp->d_X[s], plane_elems(hp, hp->d) * hp->esz));
     DMT_TRY(ens_alloc_bytes(hp, &hp->d_W[s], plane_elems(hp, hp->m) * hp->esz));

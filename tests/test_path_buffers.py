@@ -7,7 +7,7 @@ consolidation of every u into the majority's buffer (copied during the sweep), o
 per-lane destinations.  Which buffer holds what is bookkeeping only: paths, ll, decisions and
 fetch_ll must equal the oracle's bit for bit whatever the acceptance pattern, with three
 buffers and with two (DMT_PATH_BUFS=2), with consolidation and without it (DMT_REPAIR_DIV
-large: mixed), in every lane draw kernel.  Forced decisions (E = ±inf per block) drive the
+large: mixed), consolidating whole lines (DMT_FULL_COPY=1), in every lane draw kernel.  Forced decisions (E = ±inf per block) drive the
 buffer states through every branch: nearly all accepted, half, few accepted.
 """
 import numpy as np
@@ -23,6 +23,7 @@ pytestmark = pytest.mark.gpu
 def _set_bufs(monkeypatch, bufs):
     monkeypatch.setenv("DMT_PATH_BUFS", bufs[0])
     monkeypatch.setenv("DMT_REPAIR_DIV", "100000" if bufs.endswith("mixed") else "1")
+    monkeypatch.setenv("DMT_FULL_COPY", "1" if bufs.endswith("full") else "0")
 
 
 def _workload(cfg):
@@ -32,7 +33,7 @@ def _workload(cfg):
 
 @pytest.mark.parametrize("split", ["0", "1"], ids=["k_block", "k_block_ps"])
 @pytest.mark.parametrize("p_acc", [0.97, 0.5, 0.15])
-@pytest.mark.parametrize("bufs", ["3", "3-mixed", "2", "2-mixed"])
+@pytest.mark.parametrize("bufs", ["3", "3-mixed", "3-full", "2", "2-mixed"])
 @pytest.mark.parametrize("cfg", ["c5", "c3"])
 def test_forced_decisions_bit_exact(cfg, bufs, p_acc, split, monkeypatch):
     _set_bufs(monkeypatch, bufs)
