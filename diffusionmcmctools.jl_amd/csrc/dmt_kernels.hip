@@ -2784,8 +2784,10 @@ __device__ __forceinline__ void resident_pc_producer(const BlockArgs<T>& a, cons
   }
 }
 
-template <class Mdl, class T, int NP, bool SVC = false>
-__global__ __launch_bounds__(64 * 4 * (NP + 1), 1) void k_mcmc_resident_pc(const BlockArgs<T> a,
+// BPW blocks per workgroup (4; 1: every block's waves synchronise only with each other, four
+// workgroups per CU — DMT_PC_BPW=1, the service keeps 4)
+template <class Mdl, class T, int NP, bool SVC = false, int BPW = 4>
+__global__ __launch_bounds__(64 * BPW * (NP + 1), BPW == 4 ? 1 : 2) void k_mcmc_resident_pc(const BlockArgs<T> a,
                                                                       const AcceptArgs c,
                                                                       const int64_t iter0,
                                                                       const int64_t n_iter,
@@ -2794,13 +2796,13 @@ __global__ __launch_bounds__(64 * 4 * (NP + 1), 1) void k_mcmc_resident_pc(const
                                                                       unsigned* __restrict__ counter,
                                                                       double* __restrict__ out3,
                                                                       const SvcArgs sv) {
-  __shared__ ResPcLds<Mdl::D, Mdl::M, T> lds[4];
+  __shared__ ResPcLds<Mdl::D, Mdl::M, T> lds[BPW];
   __shared__ SvcLds s_svc;
   if (n_iter <= 0) return;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t blk = a.b0 + (int64_t)blockIdx.x * 4 + (w & 3);
+  const int64_t blk = a.b0 + (int64_t)blockIdx.x * BPW + (w % BPW);
   const bool valid = blk < a.b1;
-  const int role = w >> 2;  // 0: consumer, 1 + h: producer h
+  const int role = w / BPW;  // 0: consumer, 1 + h: producer h
 #if defined(DMT_PC_STUB_P)  // timing probes (scripts/res_usage.sh, gpu_variants.sh): one role only
   if (role == 0)
     resident_pc_consumer<Mdl, T, NP, SVC>(a, c, iter0, n_iter, part, blk, valid, lds[w & 3], sv, &s_svc);
@@ -2811,15 +2813,15 @@ __global__ __launch_bounds__(64 * 4 * (NP + 1), 1) void k_mcmc_resident_pc(const
   else for (int64_t i = 0; i < 2 * n_iter; ++i) __syncthreads();
 #else
   if (role == 0)
-    resident_pc_consumer<Mdl, T, NP, SVC>(a, c, iter0, n_iter, part, blk, valid, lds[w & 3], sv,
+    resident_pc_consumer<Mdl, T, NP, SVC>(a, c, iter0, n_iter, part, blk, valid, lds[w % BPW], sv,
                                           &s_svc);
   else
-    resident_pc_producer<Mdl, T, NP, SVC>(a, c, iter0, n_iter, blk, valid, role - 1, lds[w & 3],
+    resident_pc_producer<Mdl, T, NP, SVC>(a, c, iter0, n_iter, blk, valid, role - 1, lds[w % BPW],
                                           sv, &s_svc);
 #endif
 #ifndef DMT_PC_NO_TAIL  // timing probe: no in-kernel fetch_ll trees
   if constexpr (!SVC)  // the service forms each iteration's tree as the iteration ends
-    persistent_tree_tail<4, 4 * (NP + 1)>(part, nodes, a.b1 - a.b0, n_iter, counter, out3);
+    persistent_tree_tail<BPW, BPW * (NP + 1)>(part, nodes, a.b1 - a.b0, n_iter, counter, out3);
 #endif
 }
 
@@ -4216,6 +4218,9 @@ static hipError_t launch_mcmc_t(const void* args, const AcceptArgs& c, int64_t i
         const SvcArgs none{};
         if (resident == 3)
           dlaunch(k_mcmc_resident_pc<Mdl, T, 2>, dim3((unsigned)((nwaves + 3) / 4)), dim3(768), s,
+                  a, c, iter0, n, part, nodes, counter, out3, none);
+        else if (resident == 4)  // one block per workgroup
+          dlaunch(k_mcmc_resident_pc<Mdl, T, 1, false, 1>, dim3((unsigned)nwaves), dim3(128), s,
                   a, c, iter0, n, part, nodes, counter, out3, none);
         else
           dlaunch(k_mcmc_resident_pc<Mdl, T, 1>, dim3((unsigned)((nwaves + 3) / 4)), dim3(512), s,

@@ -224,6 +224,7 @@ struct dmt_ens {
   // execution interval, but ≈ 10 µs more host time in the launch call, profiles/r02zo)
   bool dispatch_events = false;
   int resident_pc = 1;       // ... split over a consumer and this many producer waves per block
+  bool pc_bpw1 = false;      // ... one block per workgroup (DMT_PC_BPW=1)
                              // (DMT_MCMC_PC=0: one wave; 1 or 2 producers)
   int lane_split = -1;       // MAP_LANE draws on producer/consumer waves: 1 on, 0 off, -1 auto
   int lane_pair = -1;        // MAP_LANE device-RNG draws on lane pairs: 1 on, 0 off, -1 auto
@@ -902,6 +903,7 @@ dmt_status dmt_create(dmt_ens** out, const dmt_model* model, const dmt_structure
   if (const char* e = std::getenv("DMT_MCMC_PERSIST")) h->persist = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("DMT_MCMC_RESIDENT")) h->resident = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("DMT_MCMC_PC")) h->resident_pc = std::max(0, std::min(2, std::atoi(e)));
+  if (const char* e = std::getenv("DMT_PC_BPW")) h->pc_bpw1 = std::atoi(e) == 1;
   if (const char* e = std::getenv("DMT_DISPATCH_EVENTS")) h->dispatch_events = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("DMT_LANE_SPLIT")) h->lane_split = std::atoi(e);
   if (const char* e = std::getenv("DMT_LANE_PAIR")) h->lane_pair = std::atoi(e);
@@ -1663,13 +1665,13 @@ static dmt_status mcmc_run_launch(dmt_ens* h, Layout* L, int64_t b0, int64_t b1,
           BlockArgs<double> a{};
           fill(a);
           e = launch_mcmc_persistent(h->key, &a, c, iter0 + i0, n, h->d_part, nb,
-                                     resident ? 1 + h->resident_pc : 0,
+                                     !resident ? 0 : (h->pc_bpw1 && h->resident_pc == 1) ? 4 : 1 + h->resident_pc,
                                      run_out + 3 * i0, (unsigned*)counter, h->stream);
         } else {
           BlockArgs<float> a{};
           fill(a);
           e = launch_mcmc_persistent(h->key, &a, c, iter0 + i0, n, h->d_part, nb,
-                                     resident ? 1 + h->resident_pc : 0,
+                                     !resident ? 0 : (h->pc_bpw1 && h->resident_pc == 1) ? 4 : 1 + h->resident_pc,
                                      run_out + 3 * i0, (unsigned*)counter, h->stream);
         }
       }
