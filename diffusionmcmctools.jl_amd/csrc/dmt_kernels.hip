@@ -1663,6 +1663,9 @@ __device__ __forceinline__ bool arrive_last(unsigned* cnt, unsigned expect, int*
   return *s_flag != 0;
 }
 
+#ifndef DMT_TREE_ONEHOP
+#define DMT_TREE_ONEHOP 1  // persistent_tree_tail: one arrival hop for <= 256 workgroups
+#endif
 // nodes: node1 [rows][ng] then node2 [rows][ng2]; counters: [ng2] group counters then the top
 // counter, zero on entry and left zero.  WPB = blocks (tree leaves) per workgroup, NW = waves
 // per workgroup (every thread of the workgroup calls this)
@@ -1694,6 +1697,35 @@ __device__ __forceinline__ void persistent_tree_tail(const double* __restrict__ 
       for (int k = 0; k < w / 2; ++k) v[k] = v[2 * k] + v[2 * k + 1];
     st_sc1(&node1[row * ng + x], v[0]);
   }
+#if DMT_TREE_ONEHOP
+  if (ng <= 256 && rows * ng <= 32768) {
+    // few workgroups and rows (C2 at the driver's 20 iterations: 256 x 60): one arrival over all of them, then each row's tree over its ng
+    // level-1 nodes as 64 lanes x 4 adjacent leaves (zero-padded to 256) — the same complete
+    // adjacent-pair tree as the two-hop form below, whose 16 x 16 grouping it skips
+    if (!arrive_last(&counters[ng2], (unsigned)ng, &s_flag)) return;
+    constexpr int RB = 8;  // rows per wave per batch (4 RB loads per lane in flight)
+    for (int64_t r0 = (int64_t)wv * RB; r0 < rows; r0 += (int64_t)NW * RB) {
+      double v[RB][4];
+#pragma unroll
+      for (int b = 0; b < RB; ++b)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int64_t row = r0 + b, nd = 4 * lane + k;
+          v[b][k] = (row < rows && nd < ng) ? ld_sc1(&node1[row * ng + nd]) : 0.0;
+        }
+#pragma unroll
+      for (int b = 0; b < RB; ++b) {
+        const double t = wave_tree_sum<double>((v[b][0] + v[b][1]) + (v[b][2] + v[b][3]));
+        const int64_t row = r0 + b;
+        if (lane == 0 && row < rows) out3[row] = (row % 3 == 2) ? t : t + 0.0;
+      }
+    }
+    __syncthreads();
+    if (tid == 0)  // ready for the next launch (stream-ordered)
+      __hip_atomic_store(&counters[ng2], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+#endif
   const int64_t gsize = ng - g * kTreeGroup < kTreeGroup ? ng - g * kTreeGroup : kTreeGroup;
   if (!arrive_last(&counters[g], (unsigned)gsize, &s_flag)) return;
   // ---- level 2: group g's nodes, 16 lanes per row, NT/16 rows per pass, U passes in flight
