@@ -1663,8 +1663,8 @@ __device__ __forceinline__ bool arrive_last(unsigned* cnt, unsigned expect, int*
   return *s_flag != 0;
 }
 
-#ifndef DMT_TREE_ONEHOP
-#define DMT_TREE_ONEHOP 1  // persistent_tree_tail: one arrival hop for <= 256 workgroups
+#ifndef DMT_TREE_ONEHOP  // persistent_tree_tail: one arrival hop for <= 256 workgroups (1) —
+#define DMT_TREE_ONEHOP 0  // measured 2 µs slower per C2 launch than the two hops (profiles/r03end)
 #endif
 // nodes: node1 [rows][ng] then node2 [rows][ng2]; counters: [ng2] group counters then the top
 // counter, zero on entry and left zero.  WPB = blocks (tree leaves) per workgroup, NW = waves
