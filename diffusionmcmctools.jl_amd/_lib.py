@@ -53,7 +53,7 @@ SYMBOLS = [
     "dmt_snapshot_take", "dmt_snapshot_download", "dmt_snapshot_write", "dmt_set_ll",
     "dmt_fetch_ll_local", "dmt_comm_size", "dmt_rng_counter", "dmt_set_rng_counter",
     "dmt_set_run_snapshots", "dmt_mcmc_step_local", "dmt_mcmc_run_local", "dmt_draw_success",
-    "dmt_rng_state", "dmt_set_rng_state",
+    "dmt_rng_state", "dmt_set_rng_state", "dmt_combine_rank_partials",
 ]
 
 
@@ -147,6 +147,7 @@ _SIGS = {
     "dmt_draw_success": [_P, _i32, _i64, _i64, _pu8],
     "dmt_rng_state": [_P, C.POINTER(_u64), C.POINTER(_u64), _pu8],
     "dmt_set_rng_state": [_P, _u64, _u64, C.c_uint8],
+    "dmt_combine_rank_partials": [_pd, _i32, _i64, _pd],
 }
 for _name, _args in _SIGS.items():
     _f = getattr(lib, _name)

@@ -1429,6 +1429,23 @@ static dmt_status ensure_red_work(dmt_ens* h, int64_t n) {
   return DMT_OK;
 }
 
+// The rank-order combination of all-gathered partials (dmt_combine_rank_partials):
+// all[(r·n_iter + i)·3 + c] → out[i·3 + c], complete adjacent-pair tree over ranks padded with
+// zeros to a power of two, + 0.0.
+static void combine_rank_partials(const double* all, int nranks, int64_t n_iter, double* out) {
+  int n2 = 1;
+  while (n2 < nranks) n2 <<= 1;
+  std::vector<double> lv(n2);
+  for (int64_t i = 0; i < n_iter; ++i)
+    for (int c = 0; c < 3; ++c) {
+      std::fill(lv.begin(), lv.end(), 0.0);
+      for (int r = 0; r < nranks; ++r) lv[r] = all[(r * n_iter + i) * 3 + c];
+      for (int w = n2; w > 1; w >>= 1)
+        for (int j = 0; j < w / 2; ++j) lv[j] = lv[2 * j] + lv[2 * j + 1];
+      out[3 * i + c] = lv[0] + 0.0;
+    }
+}
+
 // d_red (3 partials of this rank) -> host values, combined over ranks with RCCL
 static dmt_status finish_reduction(dmt_ens* h, double* v, bool global = true) {
   if (h->comm && global) {
@@ -1438,16 +1455,7 @@ static dmt_status finish_reduction(dmt_ens* h, double* v, bool global = true) {
     std::vector<double> all(3 * h->nranks);
     HIP_OK(hipMemcpyAsync(all.data(), h->d_gather, 3 * h->nranks * 8, hipMemcpyDeviceToHost, h->stream));
     HIP_OK(stream_wait(h));
-    // fixed rank-order adjacent-pair tree, ranks padded to a power of two
-    int n2 = 1;
-    while (n2 < h->nranks) n2 <<= 1;
-    for (int c = 0; c < 3; ++c) {
-      std::vector<double> lv(n2, 0.0);
-      for (int r = 0; r < h->nranks; ++r) lv[r] = all[3 * r + c];
-      for (int w = n2; w > 1; w >>= 1)
-        for (int j = 0; j < w / 2; ++j) lv[j] = lv[2 * j] + lv[2 * j + 1];
-      v[c] = lv[0] + 0.0;
-    }
+    combine_rank_partials(all.data(), h->nranks, 1, v);  // fixed rank-order tree
   } else {
     HIP_OK(hipMemcpyAsync(h->h_red, h->d_red, 24, hipMemcpyDeviceToHost, h->stream));
     HIP_OK(stream_wait(h));
@@ -1721,17 +1729,7 @@ static dmt_status mcmc_run_collect(dmt_ens* h, int64_t n_iter, double* out, bool
   HIP_OK(hipMemcpyAsync(all.data(), h->d_run_gather, all.size() * 8, hipMemcpyDeviceToHost,
                         h->stream));
   HIP_OK(stream_wait(h));
-  int n2 = 1;
-  while (n2 < h->nranks) n2 <<= 1;
-  std::vector<double> lv(n2);
-  for (int64_t i = 0; i < n_iter; ++i)
-    for (int c = 0; c < 3; ++c) {  // the rank-order tree of finish_reduction
-      std::fill(lv.begin(), lv.end(), 0.0);
-      for (int r = 0; r < h->nranks; ++r) lv[r] = all[(r * n_iter + i) * 3 + c];
-      for (int w = n2; w > 1; w >>= 1)
-        for (int j = 0; j < w / 2; ++j) lv[j] = lv[2 * j] + lv[2 * j + 1];
-      out[3 * i + c] = lv[0] + 0.0;
-    }
+  combine_rank_partials(all.data(), h->nranks, n_iter, out);  // the tree of finish_reduction
   return DMT_OK;
 }
 
@@ -2529,6 +2527,14 @@ dmt_status dmt_comm_size(dmt_ens* h, int32_t* nranks) {
   int n = 0;
   if (ncclCommCount(h->comm, &n) != ncclSuccess) return fail(DMT_ERR_COMM, "ncclCommCount failed");
   *nranks = n;
+  return DMT_OK;
+}
+
+dmt_status dmt_combine_rank_partials(const double* all, int32_t nranks, int64_t n_iter,
+                                     double* out) {
+  if (!all || !out) return fail(DMT_ERR_INVALID, "null argument");
+  if (nranks < 1 || n_iter < 0) return fail(DMT_ERR_INVALID, "nranks < 1 or n_iter < 0");
+  combine_rank_partials(all, nranks, n_iter, out);
   return DMT_OK;
 }
 

@@ -407,6 +407,19 @@ def comm_unique_id() -> bytes:
     return bytes(buf)
 
 
+def combine_rank_partials(all_partials):
+    """The host step of the multi-rank fetch_ll / dmt_mcmc_run (dmt_combine_rank_partials):
+    ``all_partials[r][i][c]`` = rank r's partial c of iteration i, as the RCCL all-gather leaves
+    them; returns ``[n_iter][3]``, the rank-order tree of ``shard.rank_tree`` per entry."""
+    a = np.ascontiguousarray(all_partials, dtype=np.float64)
+    if a.ndim == 2:
+        a = a[:, None, :]
+    nranks, n_iter = a.shape[0], a.shape[1]
+    out = np.empty((n_iter, 3))
+    L.call("dmt_combine_rank_partials", L.f64p(a.reshape(-1)), nranks, n_iter, L.f64p(out))
+    return out
+
+
 def guiding_linear(Bt, beta, at_packed, t, HT_packed, FT, cT):
     """Exact discrete backward filter on one segment (host; dmt_guiding_linear)."""
     d = len(beta)

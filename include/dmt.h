@@ -422,6 +422,15 @@ dmt_status dmt_comm_size(dmt_ens* h, int32_t* nranks);
  * shards are bit-identical to the corresponding blocks of one big ensemble).  Default 0.
  * No reference counterpart (the reference is single-process). */
 dmt_status dmt_set_shard(dmt_ens* h, int64_t seg_base);
+/* The host step of the multi-rank fetch_ll / dmt_mcmc_run: combine every rank's all-gathered
+ * partials in rank order.  all[(r·n_iter + i)·3 + c] = rank r's partial c (ll, ll°, accepted
+ * count) of iteration i, as ncclAllGather of each rank's [n_iter][3] leaves them;
+ * out[i·3 + c] = the complete adjacent-pair tree over ranks 0..nranks−1, padded with zeros to a
+ * power of two, + 0.0.  Host-only (no device needed); the code the RCCL
+ * paths run after their all-gather.  Replaces the cross-recording part of fetch_ll's
+ * mapreduce (src/block_ensemble.jl:140,152), which the single-process reference never splits. */
+dmt_status dmt_combine_rank_partials(const double* all, int32_t nranks, int64_t n_iter,
+                                     double* out);
 
 /* ---------------- path snapshots ----------------
  * The reference's callers keep every k-th accepted path, `append!(paths, [deepcopy(bb.b.XX)])`

@@ -1,0 +1,276 @@
+// c5_layout_probe.hip — timing probe (not product code): the C5 lane draw's memory pattern under
+// different path-plane layouts, with the real per-step arithmetic (Philox4x32-10 + Box–Muller
+// normals, the Lorenz guided Euler step with σ = I, its Girsanov term) so that issue and memory
+// interact as in k_block<Lorenz<float>>.
+//
+// Per step and lane: read t (shared), H (6) and F (3) rows of a read-only table, u's W increment
+// (3) from the lane's u buffer; write X° (3) and W° (3) to the lane's proposal buffer.
+// Layouts of the path planes (X, W; H/F keep the row layout):
+//   P = 1   row layout of today: ((q·C + c)·64 + lane)            — a wave's row is 256 B
+//   P = 8/16/32  lane packets: a lane's P consecutive points of one component contiguous,
+//           row q at position q + P − 1 so that chunk rows c0+1 … c0+4 are one aligned float4
+// Selectors: uniform (every lane reads buffer 0, writes buffer 1), mixed (lane u ∈ {0,1} at
+// random, writes 1 − u), consolidated (row layout only: mixed, the minority copies its u.X/u.W
+// to the majority's buffer during the sweep and every proposal goes to the other buffer — what
+// path_plan does for C5 today).
+//
+// build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off scripts/c5_layout_probe.hip \
+//          -o scripts/c5_layout_probe
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <vector>
+#include <random>
+
+#include "../diffusionmcmctools.jl_amd/csrc/dmt_device.h"
+
+using namespace dmt;
+typedef float T;
+typedef Lorenz<T> Mdl;
+constexpr int D = 3, M = 3, HP = 6, K = 4;
+
+#define CHECK(x)                                                                        \
+  do {                                                                                  \
+    hipError_t e_ = (x);                                                                \
+    if (e_ != hipSuccess) {                                                             \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_));        \
+      exit(2);                                                                          \
+    }                                                                                   \
+  } while (0)
+
+struct Args {
+  const T* t;  // shared grid [rows]
+  const T* H;  // row layout, per tile [rows][HP][64]
+  const T* F;  // [rows][D][64]
+  T* X[2];
+  T* W[2];
+  const uint8_t* u;  // [R] lane's u buffer
+  int64_t rows;      // padded point rows per tile (path planes and tables alike)
+  int nst;           // steps per segment
+  double* ll;        // [R]
+  uint32_t iter;
+};
+
+template <int P>
+__device__ __forceinline__ int64_t ppos(int64_t q, int c, int C, int lane) {
+  if constexpr (P == 1) {
+    return (q * C + c) * 64 + lane;
+  } else {
+    const int64_t p = q + P - 1;
+    return ((p / P) * C + c) * 64 * P + (int64_t)lane * P + (p % P);
+  }
+}
+
+// SEL: 0 uniform, 1 mixed, 2 consolidated (P = 1 only)
+template <int P, int SEL>
+__global__ __launch_bounds__(64) void k_probe(const Args a) {
+  const int lane = threadIdx.x;
+  const int64_t tile = blockIdx.x;
+  const int64_t r = tile * 64 + lane;
+  const int64_t tb = tile * a.rows;  // first row of the tile
+  const int64_t pbD = tb * D * 64, pbM = tb * M * 64;
+  int u = SEL == 0 ? 0 : a.u[r];
+  int pbuf = 1 - u;
+  bool copy = false;
+  if (SEL == 2) {  // consolidate: the majority's buffer m; minority copies, proposals to 1 − m
+    const int c1 = __popcll(__ballot(u == 1));
+    const int m = c1 > 32 ? 1 : 0;
+    copy = u != m;
+    pbuf = 1 - m;
+  }
+  const T* Ws = a.W[u] + pbM;
+  T* Wd = a.W[pbuf] + pbM;
+  T* Xd = a.X[pbuf] + pbD;
+  T* Xcd = a.X[1 - pbuf] + pbD;  // consolidation target (= the majority's buffer)
+  const T* Xcs = a.X[u] + pbD;
+  T* Wcd = a.W[1 - pbuf] + pbM;
+  const T* Hb = a.H + tb * HP * 64 + lane;
+  const T* Fb = a.F + tb * D * 64 + lane;
+
+  Law<Mdl, T> L;
+  L.th[0] = 10; L.th[1] = 28; L.th[2] = 8.0f / 3;
+  for (int i = 0; i < D * D; ++i) L.Bt[i] = (i % 4 == 0) ? -1.0f : 0.1f;
+  for (int i = 0; i < D; ++i) L.beta[i] = 0.5f;
+  for (int i = 0; i < HP; ++i) L.da[i] = 0;
+  L.trace = false;
+  L.unit = true;
+  L.auxtd = false;
+
+  T x[D] = {1.0f, 1.0f, 20.0f};
+  T tcur = a.t[0];
+  T ll = 0;
+  const T rho = 0.9f, srho = sqrtf(1 - 0.81f);
+  const uint32_t seg = (uint32_t)r;
+  struct Chunk {
+    T t[K], H[K][HP], F[K][D], W[K][M];
+  };
+  auto load = [&](int c0, Chunk& c) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const int64_t i = c0 + j;
+      c.t[j] = a.t[i + 1];
+#pragma unroll
+      for (int e = 0; e < HP; ++e) c.H[j][e] = Hb[(i * HP + e) * 64];
+#pragma unroll
+      for (int e = 0; e < D; ++e) c.F[j][e] = Fb[(i * D + e) * 64];
+    }
+    if constexpr (P == 1) {
+#pragma unroll
+      for (int j = 0; j < K; ++j)
+#pragma unroll
+        for (int k = 0; k < M; ++k) c.W[j][k] = Ws[ppos<P>(c0 + j + 1, k, M, lane)];
+    } else {
+#pragma unroll
+      for (int k = 0; k < M; ++k) {
+        const float4 v = *(const float4*)&Ws[ppos<P>(c0 + 1, k, M, lane)];
+        c.W[0][k] = v.x; c.W[1][k] = v.y; c.W[2][k] = v.z; c.W[3][k] = v.w;
+      }
+    }
+  };
+  const int nfull = a.nst - a.nst % K;
+  Chunk cur, nxt;
+  load(0, cur);
+  for (int c0 = 0; c0 < nfull; c0 += K) {
+    load(c0 + K, nxt);
+    T Z[K][M];
+#pragma unroll
+    for (int bq = 0; bq < K * M / 4; ++bq) {
+      T zb[4];
+      normal_block(philox4x32_10(U4{(uint32_t)(c0 * M / 4 + bq), seg, a.iter, 0u}, 0x1234u, 0x5678u),
+                   zb);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) Z[(4 * bq + e) / M][(4 * bq + e) % M] = zb[e];
+    }
+    T ox[K][D], ow[K][M], cx[K][D];
+    T g[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const T dt = cur.t[j] - tcur;
+      const T sdt = sqrtf(dt);
+      T dW[M];
+#pragma unroll
+      for (int k = 0; k < M; ++k) dW[k] = dfma(rho, cur.W[j][k], srho * (sdt * Z[j][k]));
+      T rr[D], b[D], Mg[D * D], cg[D];
+      const T G = g_at<Mdl, T>(L, cur.H[j], cur.F[j], x, rr, b);
+      guide_coeffs_unit<Mdl, T>(cur.H[j], cur.F[j], Mg, cg);
+      euler_step<Mdl, T>(Mg, cg, b, dt, dW, x);
+      tcur = cur.t[j];
+      g[j] = G * dt;
+#pragma unroll
+      for (int p = 0; p < D; ++p) ox[j][p] = x[p];
+#pragma unroll
+      for (int k = 0; k < M; ++k) ow[j][k] = dW[k];
+    }
+    ll += (g[0] + g[1]) + (g[2] + g[3]);
+    if constexpr (SEL == 2) {  // the minority's u.X of these rows (read before overwritten)
+      if (copy) {
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+#pragma unroll
+          for (int p = 0; p < D; ++p) cx[j][p] = Xcs[ppos<P>(c0 + j + 1, p, D, lane)];
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+#pragma unroll
+          for (int p = 0; p < D; ++p) Xcd[ppos<P>(c0 + j + 1, p, D, lane)] = cx[j][p];
+#pragma unroll
+          for (int k = 0; k < M; ++k) Wcd[ppos<P>(c0 + j + 1, k, M, lane)] = cur.W[j][k];
+        }
+      }
+    }
+    if constexpr (P == 1) {
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+#pragma unroll
+        for (int p = 0; p < D; ++p) Xd[ppos<P>(c0 + j + 1, p, D, lane)] = ox[j][p];
+#pragma unroll
+        for (int k = 0; k < M; ++k) Wd[ppos<P>(c0 + j + 1, k, M, lane)] = ow[j][k];
+      }
+    } else {
+#pragma unroll
+      for (int p = 0; p < D; ++p)
+        *(float4*)&Xd[ppos<P>(c0 + 1, p, D, lane)] = make_float4(ox[0][p], ox[1][p], ox[2][p], ox[3][p]);
+#pragma unroll
+      for (int k = 0; k < M; ++k)
+        *(float4*)&Wd[ppos<P>(c0 + 1, k, M, lane)] = make_float4(ow[0][k], ow[1][k], ow[2][k], ow[3][k]);
+    }
+    cur = nxt;
+  }
+  a.ll[r] = (double)ll + (double)x[0];
+}
+
+template <int P, int SEL>
+static double run(const Args& a, int ntiles, int reps, const char* name) {
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  k_probe<P, SEL><<<ntiles, 64>>>(a);  // warm-up
+  CHECK(hipGetLastError());
+  CHECK(hipDeviceSynchronize());
+  CHECK(hipEventRecord(e0));
+  for (int i = 0; i < reps; ++i) k_probe<P, SEL><<<ntiles, 64>>>(a);
+  CHECK(hipEventRecord(e1));
+  CHECK(hipEventSynchronize(e1));
+  float ms;
+  CHECK(hipEventElapsedTime(&ms, e0, e1));
+  const double us = ms * 1e3 / reps;
+  const double steps = (double)ntiles * 64 * a.nst;
+  printf("{\"variant\": \"%s\", \"P\": %d, \"sel\": %d, \"us_per_draw\": %.1f, \"frac_72B\": %.3f}\n",
+         name, P, SEL, us, steps * 72 / (us * 1e-6) / 8e12);
+  fflush(stdout);
+  return us;
+}
+
+int main(int argc, char** argv) {
+  const int ntiles = argc > 1 ? atoi(argv[1]) : 512;
+  const int nst = 2000;
+  const int reps = argc > 2 ? atoi(argv[2]) : 10;
+  const char* only = argc > 3 ? argv[3] : nullptr;
+  const int64_t rows = ((nst + 1 + 2 * K + 32 + 31) / 32) * 32 + 32;  // room for prefetch + packet shift
+  const int64_t R = (int64_t)ntiles * 64;
+  Args a{};
+  a.rows = rows;
+  a.nst = nst;
+  a.iter = 1;
+  std::vector<T> th(rows);
+  for (int64_t i = 0; i < rows; ++i) th[i] = (T)i * 1e-3f;
+  T* dt;
+  CHECK(hipMalloc(&dt, rows * sizeof(T)));
+  CHECK(hipMemcpy(dt, th.data(), rows * sizeof(T), hipMemcpyHostToDevice));
+  a.t = dt;
+  auto alloc = [&](int C, float v) {
+    T* p;
+    const size_t n = (size_t)ntiles * rows * C * 64;
+    CHECK(hipMalloc(&p, n * sizeof(T)));
+    std::vector<T> h(n, v);
+    CHECK(hipMemcpy(p, h.data(), n * sizeof(T), hipMemcpyHostToDevice));
+    return p;
+  };
+  a.H = alloc(HP, 0.01f);
+  a.F = alloc(D, 0.02f);
+  for (int b = 0; b < 2; ++b) {
+    a.X[b] = alloc(D, 0.0f);
+    a.W[b] = alloc(M, 0.001f);
+  }
+  std::vector<uint8_t> hu(R);
+  std::mt19937 g(7);
+  for (auto& v : hu) v = (uint8_t)(g() & 1);
+  uint8_t* du;
+  CHECK(hipMalloc(&du, R));
+  CHECK(hipMemcpy(du, hu.data(), R, hipMemcpyHostToDevice));
+  a.u = du;
+  CHECK(hipMalloc(&a.ll, R * sizeof(double)));
+  auto want = [&](const char* n) { return !only || strstr(n, only) != nullptr; };
+  for (int rep = 0; rep < 2; ++rep) {  // two interleaved passes
+    if (want("row_uniform")) run<1, 0>(a, ntiles, reps, "row_uniform");
+    if (want("row_mixed")) run<1, 1>(a, ntiles, reps, "row_mixed");
+    if (want("row_consolidated")) run<1, 2>(a, ntiles, reps, "row_consolidated");
+    if (want("pk8_uniform")) run<8, 0>(a, ntiles, reps, "pk8_uniform");
+    if (want("pk8_mixed")) run<8, 1>(a, ntiles, reps, "pk8_mixed");
+    if (want("pk16_uniform")) run<16, 0>(a, ntiles, reps, "pk16_uniform");
+    if (want("pk16_mixed")) run<16, 1>(a, ntiles, reps, "pk16_mixed");
+    if (want("pk32_uniform")) run<32, 0>(a, ntiles, reps, "pk32_uniform");
+    if (want("pk32_mixed")) run<32, 1>(a, ntiles, reps, "pk32_mixed");
+  }
+  return 0;
+}

@@ -63,6 +63,51 @@ def test_shard_helpers():
     assert shard.rank_tree([1.0, 2.0, 3.0]) == (1.0 + 2.0) + (3.0 + 0.0)
 
 
+@pytest.mark.parametrize("nranks", [1, 2, 3, 6, 8])
+def test_rank_combine_host_path_matches_rank_tree(dmt, nranks):
+    """libdmt's host combination of all-gathered partials (dmt_combine_rank_partials: the code
+    finish_reduction and mcmc_run_collect run after ncclAllGather) against shard.rank_tree,
+    bit for bit, for every iteration and component: synthetic partials of mixed magnitudes and
+    signs (so that any other summation order would round differently), -inf and 0."""
+    from diffusionmcmctools_amd import shard
+    rng = np.random.default_rng(nranks)
+    n_iter = 7
+    allp = rng.standard_normal((nranks, n_iter, 3)) * 10.0 ** rng.integers(-8, 9, (nranks, n_iter, 3))
+    allp[:, :, 2] = rng.integers(0, 1 << 20, (nranks, n_iter))  # accepted counts
+    allp[0, 3, 1] = -np.inf
+    allp[-1, 4, 0] = 0.0
+    out = dmt.combine_rank_partials(allp)
+    assert out.shape == (n_iter, 3)
+    for i in range(n_iter):
+        for c in range(3):
+            want = shard.rank_tree(allp[:, i, c])
+            got = out[i, c]
+            assert (got == want) or (np.isnan(got) and np.isnan(want)), (nranks, i, c, got, want)
+            assert np.signbit(got) == np.signbit(want)
+
+
+@pytest.mark.parametrize("nranks", [2, 4, 8])
+def test_rank_combine_of_power_of_two_shards_is_the_global_tree(dmt, orc, nranks):
+    """Power-of-two blocks per rank: each rank's fetch_ll subtree, combined by libdmt's host
+    step, equals the single-ensemble tree over all blocks — the property that
+    makes an N-GPU job bit-identical to one ensemble.  Block values from a real oracle run."""
+    from diffusionmcmctools_amd import workloads as W
+    B = 16
+    g = W.concat_workloads([W.c2_ou2d(B=B, N=30, block_offset=r) for r in range(nranks)])
+    g.meta["hist_len"] = 2
+    ens = orc.OracleEnsemble(g.model.kind, g.d, g.m, g.n_points, prec=g.precision, seed=SEED,
+                             grid_shared=g.grid_shared)
+    lay = W.fill(ens, g, init_Z=True)
+    nb = g.nblocks
+    ens.loglikhd(lay, 0, 0, nb)
+    ens.draw_proposal(lay, 0, nb, Z=None, iter=1)
+    ens.accept_reject(lay, 0, nb, 1)
+    want = ens.fetch_ll(lay, 0, nb, 1)
+    per_rank = np.array([ens.fetch_ll(lay, r * B, (r + 1) * B, 1) for r in range(nranks)])
+    got = dmt.combine_rank_partials(per_rank)[0]
+    np.testing.assert_array_equal(got, np.asarray(want, dtype=np.float64))
+
+
 def test_two_rank_shards_match_unsharded(tmp_path):
     import torch.multiprocessing as mp
     import oracle as orc
