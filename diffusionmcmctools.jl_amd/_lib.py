@@ -54,6 +54,7 @@ SYMBOLS = [
     "dmt_fetch_ll_local", "dmt_comm_size", "dmt_rng_counter", "dmt_set_rng_counter",
     "dmt_set_run_snapshots", "dmt_mcmc_step_local", "dmt_mcmc_run_local", "dmt_draw_success",
     "dmt_rng_state", "dmt_set_rng_state", "dmt_combine_rank_partials",
+    "dmt_set_service", "dmt_service_stats", "dmt_set_proposal_law_cc",
 ]
 
 
@@ -148,6 +149,9 @@ _SIGS = {
     "dmt_rng_state": [_P, C.POINTER(_u64), C.POINTER(_u64), _pu8],
     "dmt_set_rng_state": [_P, _u64, _u64, C.c_uint8],
     "dmt_combine_rank_partials": [_pd, _i32, _i64, _pd],
+    "dmt_set_service": [_P, _i32, C.c_double],
+    "dmt_set_proposal_law_cc": [_P, _i32, _i64, _i64, _i32, _P, _P, _i32, _i32, _P, _P],
+    "dmt_service_stats": [_P, C.POINTER(_u64)],
 }
 for _name, _args in _SIGS.items():
     _f = getattr(lib, _name)

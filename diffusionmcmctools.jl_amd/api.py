@@ -597,17 +597,20 @@ class _BlockRange:
 
     # ---- parameter updates (biblock.jl:334-375, block_collection.jl:306-334)
     def set_proposal_law(self, theta=None, H=None, F=None, laws=None, Hb=None, Fb=None,
-                         lawsb=None, H_shared=False, skip=0):
-        """``set_proposal_law!(bb, θ°, pnames; skip)``.
+                         lawsb=None, H_shared=False, skip=0, critical_change=None):
+        """``set_proposal_law!(bb, θ°, pnames, critical_change; skip)``.
 
         With ``theta`` ({parameter name or DMT_PAR_* index: value}; names as in
         ``_lib.PAR_FHN`` / ``PAR_LORENZ``, OU indices Θ[i][j] = i·d + j, μ[i] = d² + i) it runs
         on the device: u°'s laws ← u's with θ° set and the auxiliary law re-derived,
         ``recompute_guiding_term!(b°)`` where that changed, then ``recompute_path!(b°, b.WW)``;
         returns (success, critical) per block.  Without ``theta`` it installs host-made tables
-        in u° (ensemble-wide upload) and re-solves; returns the success flags."""
+        in u° (ensemble-wide upload) and re-solves; returns the success flags.
+        ``critical_change=False`` keeps u°'s guiding term unless equalizing u°'s law with u's
+        changed its auxiliary law (src/biblock.jl:340-342)."""
         if theta is not None:
-            return self._call("set_proposal_law", _param_indices(self._ens, theta), skip=skip)
+            return self._call("set_proposal_law", _param_indices(self._ens, theta), skip=skip,
+                              critical_change=critical_change)
         if H is not None or F is not None or laws is not None:
             self._ens.upload_law(L.UPROP, L.LAW_PP, H=H, F=F, laws=laws, H_shared=H_shared)
         if Hb is not None or Fb is not None or lawsb is not None:

@@ -142,7 +142,8 @@ struct AcceptArgs {
 struct SvcArgs {
   const uint64_t* posted;  // host memory: iterations posted so far (written by the host)
   const uint32_t* stop;    // host memory: 1 = leave at the next gate
-  uint64_t* rec;           // host memory: [2][grid][4] 16-byte records (sum bits, iteration + 1)
+  uint64_t* rec;           // host memory: [2][grid][4] 16-byte records (sum bits, sum bits ^
+                           //   svc_mix(iteration + 1))
                            //   of every workgroup's (ll, ll°, accepted) sums, by iteration parity
   uint64_t* go;            // device: workgroup 0's answers to the other workgroups' gates —
   uint64_t* quit;          //   go / quit = base + r + 1 at gate r (zeroed before every launch)
@@ -151,6 +152,18 @@ struct SvcArgs {
   uint64_t base;           // the launch's iteration r is the service's iteration base + r (a
                            // launch that left idle is re-launched from where it stopped)
 };
+
+// Check word of a service record (svc_record / svc_slot_ready): a record is (value bits,
+// value bits ^ svc_mix(tag)).  The host accepts a record only when its two words agree for the
+// tag it waits for, so a read that sees one word of the 16-byte store and not the other (no
+// API promises that a 16-byte write to host memory is seen whole) is rejected and read again;
+// a record of an older iteration never agrees with a newer tag.  splitmix64's finaliser.
+__host__ __device__ __forceinline__ uint64_t svc_mix(uint64_t tag) {
+  uint64_t z = tag + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
 
 // Timing events attached to the next kernel dispatch (hipExtLaunchKernel): armed by the
 // runtime for a timed launch, consumed (and cleared) by that kernel's launcher.
@@ -213,6 +226,9 @@ struct ParamArgs {
   int64_t b0, b1;
   uint8_t* crit;    // [nblocks] 1 if the block's auxiliary law (as the filter uses it) changed
   uint32_t* ncrit;  // count of such blocks
+  int cc_mode;      // critical_change (src/biblock.jl:340-342): -1 a block is critical when its
+                    // auxiliary law changed; 0 (false) only when equalizing u°'s law with u's
+                    // changed it; 1 (true) every block
 };
 
 // Model/precision dispatch keys.

@@ -2297,9 +2297,10 @@ __device__ __forceinline__ bool svc_gate(const SvcArgs& sv, int64_t r, SvcLds* s
 // Iteration r's gate has opened: the workgroup's 4 consumer waves left their blocks' (ll, ll°,
 // accepted) in row[c][0..3] before it (0.0 for a block past b1).  Lanes 0..2 of wave 0 fold them — the
 // aligned 4-leaf subtree ((x0 + x1) + (x2 + x3)) of the canonical fetch_ll tree — and send each
-// sum with the iteration's tag to the host as ONE 16-byte store (value bits, tag): the host
-// reads a record once its three tags show the iteration and folds the workgroups' sums in the
-// canonical order (svc_fold in dmt_runtime.hip).  No counter, no wait: the workgroup goes on.
+// sum to the host as ONE 16-byte store (value bits, value bits ^ svc_mix(iteration + 1)): the
+// host takes a record once its two words agree for the iteration it waits for (a torn read does
+// not, dmt_internal.h) and folds the workgroups' sums in the canonical order (svc_fold in
+// dmt_runtime.hip).  No counter, no wait: the workgroup goes on.
 // Records alternate between two sets by the iteration's parity; the host reads set s & 1 of
 // iteration s before it posts s + 1, so set s & 1 is free again when iteration s + 2 writes it.
 __device__ __forceinline__ void svc_record(const SvcArgs& sv, const SvcLds* sl, int64_t r) {
@@ -2308,8 +2309,8 @@ __device__ __forceinline__ void svc_record(const SvcArgs& sv, const SvcLds* sl, 
     const double v = (sl->row[lane][0] + sl->row[lane][1]) + (sl->row[lane][2] + sl->row[lane][3]);
     const uint64_t slot = sv.base + (uint64_t)r;
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    const uint64_t vb = __builtin_bit_cast(uint64_t, v), tag = slot + 1;
-    const u32x4 rec = {(uint32_t)vb, (uint32_t)(vb >> 32), (uint32_t)tag, (uint32_t)(tag >> 32)};
+    const uint64_t vb = __builtin_bit_cast(uint64_t, v), chk = vb ^ svc_mix(slot + 1);
+    const u32x4 rec = {(uint32_t)vb, (uint32_t)(vb >> 32), (uint32_t)chk, (uint32_t)(chk >> 32)};
     uint64_t* dst = sv.rec + (((slot & 1) * gridDim.x + blockIdx.x) * 4 + lane) * 2;
     // one 16-byte vector store, system-coherent (sc0 sc1: written through to host memory now,
     // not held in L2 until the launch ends)
@@ -3717,11 +3718,24 @@ __global__ __launch_bounds__(64) void k_set_prop_law(const ParamArgs a, int wg_p
 #pragma unroll
     for (int i = 0; i < DMT_LAW_STRIDE; ++i) rec[i] = src[i];
     rec[DMT_LAW_C0] = c0;
+    // critical_change = false: only GP.equalize_law_params! (u°'s law ← u's) can make the update
+    // critical (src/biblock.jl:361-362) — compare u°'s auxiliary law before with u's
+    bool eq_changed = false;
+    if (a.cc_mode == 0) {
+#pragma unroll
+      for (int i = kAux0; i < kAux1; ++i)
+        if (i != DMT_LAW_C0 && __double_as_longlong(old[i - kAux0]) != __double_as_longlong(rec[i]))
+          eq_changed = true;
+    }
     write_params(a, rec);
 #pragma unroll
     for (int i = 0; i < DMT_LAW_STRIDE; ++i) dst[i] = rec[i];
     const bool used = kind == ((!term && g == g1) ? 1 : 0);
-    if (used) {
+    if (used && a.cc_mode == 1) {
+      changed = true;
+    } else if (used && a.cc_mode == 0) {
+      changed = changed || eq_changed;
+    } else if (used) {
 #pragma unroll
       for (int i = kAux0; i < kAux1; ++i)
         if (i != DMT_LAW_C0 && __double_as_longlong(old[i - kAux0]) != __double_as_longlong(rec[i]))

@@ -139,7 +139,7 @@ struct dmt_ens {
   double svc_idle_ms = 2.0;   // DMT_SVC_IDLE_MS: a launch idles this long for a post, then leaves
   int64_t svc_fit_nb = -1;    // the range size whose co-residency svc_fit holds
   bool svc_fit = false;
-  struct { uint64_t starts = 0, relaunches = 0, posts = 0, waits = 0; } svc_stats;  // DMT_SVC_STATS
+  struct { uint64_t starts = 0, relaunches = 0, posts = 0, waits = 0, off = 0; } svc_stats;  // DMT_SVC_STATS
   char* svc_host = nullptr;     // pinned: posted @0, stop @64 (separate lines)
   uint64_t* svc_rec = nullptr;  // pinned: [2][svc_rec_nwg][8] records (SvcArgs::rec)
   int64_t svc_rec_nwg = 0;
@@ -575,13 +575,21 @@ dmt_status svc_relaunch(dmt_ens* h, uint64_t base);  // svc_launch (below)
 inline volatile uint64_t* svc_posted(dmt_ens* h) { return (volatile uint64_t*)(h->svc_host); }
 inline volatile uint32_t* svc_stopw(dmt_ens* h) { return (volatile uint32_t*)(h->svc_host + 64); }
 
-// Iteration `slot`'s records are all in: every workgroup's three 16-byte (sum, tag) stores
-// carry tag slot + 1 (each store lands whole, so a tag vouches for the value beside it)
+// Iteration `slot`'s records are all in: every workgroup's three 16-byte (sum, check) records
+// agree for tag slot + 1 (check = sum bits ^ svc_mix(slot + 1), dmt_internal.h).  The two words
+// are read separately, and nothing promises that the device's 16-byte store reaches host memory
+// as one piece; a record read half old, half new fails the check and is read again.  A check
+// reads the value word last, so the value that passed is the one svc_fold reads (records of
+// `slot` are not rewritten before the host has posted slot + 2).
 bool svc_slot_ready(const dmt_ens* h, uint64_t slot) {
   const volatile uint64_t* r = h->svc_rec + (slot & 1) * h->svc.nwg * 8;
+  const uint64_t mix = svc_mix(slot + 1);
   for (int64_t w = h->svc.nwg - 1; w >= 0; --w)
-    for (int c = 0; c < 3; ++c)
-      if (r[8 * w + 2 * c + 1] != slot + 1) return false;
+    for (int c = 0; c < 3; ++c) {
+      const uint64_t chk = r[8 * w + 2 * c + 1];
+      std::atomic_thread_fence(std::memory_order_acquire);
+      if (chk != (r[8 * w + 2 * c] ^ mix)) return false;
+    }
   return true;
 }
 
@@ -607,6 +615,17 @@ void svc_fold(const dmt_ens* h, uint64_t slot, double* out3) {
   }
 }
 
+// A service whose launches keep leaving idle before their iteration was posted (other work
+// holding the CUs the grid needs: the non-resident workgroups start only after workgroup 0's
+// idle exit) is turned off for the handle; the fused iterations then run one launch each.
+void svc_check_degraded(dmt_ens* h) {
+  const auto& st = h->svc_stats;
+  if (h->service && st.posts >= 16 && 4 * st.relaunches > st.posts) {
+    h->service = false;
+    h->svc_stats.off = 1;
+  }
+}
+
 // Wait until the service has finished n iterations (spin: the caller waits for this very
 // result).  A launch that left idle before an iteration was posted to it (the host was away
 // longer than the idle window) is launched again from the first iteration it did not run; a
@@ -627,6 +646,7 @@ dmt_status svc_wait_done(dmt_ens* h, uint64_t n) {
       if (e == hipSuccess) {  // the launch has ended: everything it wrote is visible
         if (svc_slot_ready(h, v.done)) continue;
         ++h->svc_stats.relaunches;
+        svc_check_degraded(h);
         DMT_TRY(svc_relaunch(h, v.done));
         t0 = std::chrono::steady_clock::now();
       } else if (e != hipErrorNotReady) {
@@ -1888,6 +1908,7 @@ dmt_status dmt_accept_reject(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
         // this iteration at once (instead of finding out in svc_wait_done)
         ++h->svc_stats.relaunches;
         DMT_TRY(svc_relaunch(h, slot));
+        svc_check_degraded(h);
       }
       v.posted = slot + 1;
       ++h->svc_stats.posts;
@@ -2164,6 +2185,14 @@ dmt_status dmt_recompute_guiding_term(dmt_ens* h, int32_t layout, int64_t b0, in
 dmt_status dmt_set_proposal_law(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int32_t n,
                                 const int32_t* idx, const double* val, int32_t skip,
                                 uint8_t* success_out, uint8_t* critical_out) {
+  return dmt_set_proposal_law_cc(h, layout, b0, b1, n, idx, val, skip, -1, success_out,
+                                 critical_out);
+}
+
+dmt_status dmt_set_proposal_law_cc(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int32_t n,
+                                   const int32_t* idx, const double* val, int32_t skip,
+                                   int32_t critical_change, uint8_t* success_out,
+                                   uint8_t* critical_out) {
   DMT_TRY(enter(h));
   Layout* L;
   DMT_TRY(get_layout(h, layout, &L));
@@ -2176,8 +2205,11 @@ dmt_status dmt_set_proposal_law(dmt_ens* h, int32_t layout, int64_t b0, int64_t 
   for (int k = 0; k < n; ++k)
     if (idx[k] < 0 || idx[k] >= npar) return fail(DMT_ERR_INVALID, "unknown parameter index");
   if (skip < 0) return fail(DMT_ERR_INVALID, "skip must be >= 0");
+  if (critical_change < -1 || critical_change > 1)
+    return fail(DMT_ERR_INVALID, "critical_change must be -1, 0 or 1");
   DMT_TRY(law_ready(h, 1, L, b0, b1));
   ParamArgs a{};
+  a.cc_mode = critical_change;
   a.model = h->key.model;
   a.d = h->d;
   a.m = h->m;
@@ -2527,6 +2559,27 @@ dmt_status dmt_comm_size(dmt_ens* h, int32_t* nranks) {
   int n = 0;
   if (ncclCommCount(h->comm, &n) != ncclSuccess) return fail(DMT_ERR_COMM, "ncclCommCount failed");
   *nranks = n;
+  return DMT_OK;
+}
+
+dmt_status dmt_set_service(dmt_ens* h, int32_t enable, double idle_ms) {
+  DMT_TRY(check_h(h));
+  if (!(idle_ms >= 0.0) || idle_ms > 60000.0) return fail(DMT_ERR_INVALID, "idle_ms outside [0, 60000]");
+  DMT_TRY(svc_stop(h));
+  h->service = enable != 0 && idle_ms > 0.0;
+  if (idle_ms > 0.0) h->svc_idle_ms = idle_ms;
+  h->svc_stats.off = 0;
+  return DMT_OK;
+}
+
+dmt_status dmt_service_stats(dmt_ens* h, uint64_t* stats) {
+  DMT_TRY(check_h(h));
+  if (!stats) return fail(DMT_ERR_INVALID, "null argument");
+  stats[0] = h->svc_stats.starts;
+  stats[1] = h->svc_stats.relaunches;
+  stats[2] = h->svc_stats.posts;
+  stats[3] = h->svc_stats.waits;
+  stats[4] = h->svc_stats.off;
   return DMT_OK;
 }
 

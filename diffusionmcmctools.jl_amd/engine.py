@@ -232,15 +232,18 @@ class Ensemble:
     def recompute_guiding_term(self, layout, b0, b1, unit=L.U):
         L.call("dmt_recompute_guiding_term", self._h, layout, b0, b1, unit)
 
-    def set_proposal_law(self, layout, b0, b1, params, skip=0):
-        """set_proposal_law!(bb, θ°, pnames; skip) on the device: params is {name index: value}
-        (DMT_PAR_*).  Returns (success[b1-b0], critical[b1-b0])."""
+    def set_proposal_law(self, layout, b0, b1, params, skip=0, critical_change=None):
+        """set_proposal_law!(bb, θ°, pnames, critical_change; skip) on the device: params is
+        {name index: value} (DMT_PAR_*); critical_change None: recompute the guiding term where
+        the auxiliary law changed, True: everywhere, False: only where equalizing u°'s law with
+        u's changed it (dmt_set_proposal_law_cc).  Returns (success[b1-b0], critical[b1-b0])."""
         idx = np.ascontiguousarray(np.fromiter(params.keys(), dtype=np.int32, count=len(params)))
         val = np.ascontiguousarray(np.fromiter(params.values(), dtype=np.float64, count=len(params)))
         ok = np.empty(b1 - b0, dtype=np.uint8)
         crit = np.empty(b1 - b0, dtype=np.uint8)
-        L.call("dmt_set_proposal_law", self._h, layout, b0, b1, len(params),
-               idx.ctypes.data_as(C.c_void_p), val.ctypes.data_as(C.c_void_p), int(skip),
+        cc = -1 if critical_change is None else (1 if critical_change else 0)
+        L.call("dmt_set_proposal_law_cc", self._h, layout, b0, b1, len(params),
+               idx.ctypes.data_as(C.c_void_p), val.ctypes.data_as(C.c_void_p), int(skip), cc,
                ok.ctypes.data_as(C.c_void_p), crit.ctypes.data_as(C.c_void_p))
         return ok.astype(bool), crit.astype(bool)
 
@@ -312,6 +315,17 @@ class Ensemble:
     # ---------------------------------------------------------------- misc
     def sync(self):
         L.call("dmt_sync", self._h)
+
+    def set_service(self, enable=True, idle_ms=2.0):
+        """The resident MCMC service's switch and idle window (dmt_set_service); idle_ms = 0
+        or enable = False: off — no launch waits on the device between calls."""
+        L.call("dmt_set_service", self._h, 1 if enable else 0, float(idle_ms))
+
+    def service_stats(self):
+        """(starts, relaunches, posts, waits, off) of the resident service (dmt_service_stats)."""
+        st = (C.c_uint64 * 5)()
+        L.call("dmt_service_stats", self._h, st)
+        return dict(zip(("starts", "relaunches", "posts", "waits", "off"), map(int, st)))
 
     def set_timing(self, on=True, kernels=None):
         """Event timing of kernel classes ``kernels`` (iterable of K_*; default all)."""

@@ -179,6 +179,11 @@ def _pairs(pn_block):
     out = {}
     for coll in ("PP", "P_last", "P_excl", "Pb_excl"):
         u = _get(pn_block, coll)
+        obs = _get(u, "updt_obs") if (isinstance(u, dict) and "updt_obs" in u) or hasattr(u, "updt_obs") else ()
+        if any(len(list(o)) for o in obs):
+            raise NotImplementedError(
+                "set_proposal_law: observation parameters (updt_obs) are not updated on the "
+                "device; the observations are uploaded once (dmt_upload_obs)")
         pairs = list(_get(u, "updt"))
         for ua in _get(u, "updt_aux"):
             pairs += list(ua)
@@ -195,7 +200,7 @@ def _theta_map(pn_block, θ):
     return {name: float(θ[idx - 1]) for name, idx in _pairs(pn_block).items()}
 
 
-def set_proposal_law(x, θ_prop, pnames, critical_change=True, skip=0):
+def set_proposal_law(x, θ_prop, pnames, critical_change=None, skip=0):
     """``set_proposal_law!(x, θ°, pnames, critical_change; skip)`` (src/biblock.jl:334-344,
     src/block_collection.jl:264-276, src/block_ensemble.jl:242-255): u°'s laws ← u's with the
     parameters ``pnames`` names set from θ° (``pnames``: a ParamNamesBlock, or the tutorials'
@@ -203,11 +208,16 @@ def set_proposal_law(x, θ_prop, pnames, critical_change=True, skip=0):
     BiBlock; ``pnames.blocks[i]`` for a BlockCollection; ``pnames.recordings[r].blocks[i]`` for a
     BlockEnsemble), the guiding term of b° recomputed, then ``recompute_path!(b°, b.WW; skip)``.
 
-    ``critical_change`` (Bool / per block / per recording per block) is accepted for the
-    reference's signature; the device recomputes the guiding term of exactly the blocks whose
-    law record changed — what any correct ``critical_change`` asks for (a recomputation of an
-    unchanged law reproduces its guiding term bit for bit).  One device call covers all blocks
-    whose θ° → name maps agree (every tutorial: a single call).  Returns per-block success."""
+    ``critical_change`` (Bool / per block / per recording per block, as the reference
+    broadcasts it): omitted — the reference's default GP.is_critical_update — recomputes the
+    guiding term of the blocks whose auxiliary law changed (a recomputation of an unchanged law
+    reproduces its guiding term bit for bit); True recomputes every block's; False keeps b°'s
+    guiding term unless equalizing b°'s law with b's changed the auxiliary law
+    (src/biblock.jl:340-342, 361-362).  Observation parameters
+    (``updt_obs``, DD.set_parameters!(PP, θ°, updt, updt_aux, updt_obs), :373-375) are not
+    device state here — a non-empty ``updt_obs`` raises.  One device call covers all blocks
+    whose θ° → name maps and flags agree (every tutorial: a single call).  Returns per-block
+    success."""
     if isinstance(x, BiBlock):
         groups = [(x, _theta_map(pnames, θ_prop))]
     elif isinstance(x, BlockCollection):
@@ -218,10 +228,28 @@ def set_proposal_law(x, θ_prop, pnames, critical_change=True, skip=0):
                   for bb, pb in zip(bc.blocks, _get(pr, "blocks"))]
     else:
         raise TypeError("set_proposal_law: expected a BiBlock, BlockCollection or BlockEnsemble")
-    if all(m == groups[0][1] for _, m in groups):
-        ok, _ = x.set_proposal_law(theta=groups[0][1], skip=skip)
+    ccs = [None] * len(groups) if critical_change is None else _flags(critical_change, len(groups))
+    if all(m == groups[0][1] for _, m in groups) and all(c == ccs[0] for c in ccs):
+        ok, _ = x.set_proposal_law(theta=groups[0][1], skip=skip, critical_change=ccs[0])
         return ok
-    return np.concatenate([bb.set_proposal_law(theta=m, skip=skip)[0] for bb, m in groups])
+    return np.concatenate([bb.set_proposal_law(theta=m, skip=skip, critical_change=c)[0]
+                           for (bb, m), c in zip(groups, ccs)])
+
+
+def _flags(cc, n):
+    """critical_change as one Bool per block: a Bool, a per-block vector, or per recording
+    a per-block vector (the reference's BlockCollection / BlockEnsemble broadcasts)."""
+    if isinstance(cc, (bool, np.bool_)):
+        return [bool(cc)] * n
+    flat = []
+    for v in cc:
+        if isinstance(v, (bool, np.bool_, int, np.integer)):
+            flat.append(bool(v))
+        else:
+            flat += [bool(u) for u in v]
+    if len(flat) != n:
+        raise ValueError(f"critical_change: {len(flat)} flags for {n} blocks")
+    return flat
 
 
 # ------------------------------------------------------------------ GuidedProposals' methods

@@ -270,6 +270,19 @@ dmt_status dmt_draw_proposal(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
 dmt_status dmt_draw_success(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1,
                             uint8_t* success_out);
 
+/* The resident service's switch and idle window, per handle (the environment's DMT_SERVICE /
+ * DMT_SVC_IDLE_MS give the defaults).  enable = 0, or idle_ms = 0, turns it off: every fused
+ * iteration is its own launch and no launch waits on the device between calls (for callers
+ * that share the device with other work or synchronise it from outside libdmt).  A running
+ * service is stopped first.  The service also turns itself off for the handle when launches
+ * keep leaving idle before their iteration is posted — more than one relaunch per four posts
+ * after 16 posts, e.g. because other work holds CUs the grid needs (co-residency is checked
+ * on an empty device only); dmt_service_stats reports it. */
+dmt_status dmt_set_service(dmt_ens* h, int32_t enable, double idle_ms);
+/* stats[5]: launches started, relaunches, iterations posted, host waits, 1 if the service
+ * turned itself off (see above). */
+dmt_status dmt_service_stats(dmt_ens* h, uint64_t* stats);
+
 /* accept_reject_proposal_path!(·, mcmciter) (src/biblock.jl:121-127): E > -(ll° - ll),
  * swap XX/WW, set_accepted!, save_ll! (both), swap ll.  E: double[b1-b0] (parity) or NULL
  * (device Exp(1) stream keyed by (seed, mcmciter, salt, global id of the block's first
@@ -329,6 +342,18 @@ dmt_status dmt_recompute_guiding_term(dmt_ens* h, int32_t layout, int64_t b0, in
 dmt_status dmt_set_proposal_law(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int32_t n,
                                 const int32_t* idx, const double* val, int32_t skip,
                                 uint8_t* success_out, uint8_t* critical_out);
+/* set_proposal_law!(bb, θ°, pnames, critical_change; skip) with the reference's explicit
+ * critical_change (src/biblock.jl:334-344): 1 (true) recomputes u°'s guiding term for every
+ * block; 0 (false) only for the blocks where equalizing u°'s law with u's changed the auxiliary
+ * law (GP.equalize_law_params!, :361-362), keeping u°'s guiding term elsewhere even if θ°
+ * touched it, as the reference does for a caller that passes false; -1 (the default,
+ * GP.is_critical_update's role; dmt_set_proposal_law) for the blocks whose auxiliary law
+ * changed — the same bits as 1 whenever u°'s guiding term matches its law, since an unchanged
+ * law reproduces its guiding term.  critical_out reports the blocks recomputed. */
+dmt_status dmt_set_proposal_law_cc(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1, int32_t n,
+                                   const int32_t* idx, const double* val, int32_t skip,
+                                   int32_t critical_change, uint8_t* success_out,
+                                   uint8_t* critical_out);
 
 /* swap_XX!/swap_WW!/swap_PP!/swap_ll! (src/biblock.jl:148-209), what = DMT_SWAP_* mask. */
 dmt_status dmt_swap(dmt_ens* h, int32_t layout, int32_t what, int64_t b0, int64_t b1);

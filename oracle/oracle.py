@@ -714,11 +714,13 @@ class OracleEnsemble:
         laws = np.stack([lw.rec for lw in tab])
         return H, F, laws
 
-    def set_proposal_law(self, layout, b0, b1, params, skip=0):
-        """set_proposal_law!(bb, θ°, pnames; skip) (src/biblock.jl:334-345): u°'s law records ←
-        u's except c(t0) (equalize_law_params!, :390-431), the named parameters ← θ°
-        (DD.set_parameters!, :360-364), recompute_guiding_term!(b°) for the blocks whose
-        auxiliary law changed (:342), recompute_path!(b°, b.WW) (:343).
+    def set_proposal_law(self, layout, b0, b1, params, skip=0, critical_change=None):
+        """set_proposal_law!(bb, θ°, pnames, critical_change; skip) (src/biblock.jl:334-345):
+        u°'s law records ← u's except c(t0) (equalize_law_params!, :390-431), the named
+        parameters ← θ° (DD.set_parameters!, :360-364), recompute_guiding_term!(b°) for the
+        blocks whose auxiliary law changed (:342) — with critical_change = True for every block,
+        with False only where the equalization itself changed it (:361-362) —
+        recompute_path!(b°, b.WW) (:343).
         Returns (success, critical) per block."""
         assert skip >= 0
         crit = np.zeros(b1 - b0, dtype=bool)
@@ -734,11 +736,15 @@ class OracleEnsemble:
                     c0 = dst[L_C0]
                     dst[:] = tab_u[g].rec
                     dst[L_C0] = c0
+                    eq = dst[L_A:L_TRACE + 1].copy()  # after equalize_law_params!, before θ°
                     set_law_params(self.model, self.d, dst, params)
                     used = kind == (1 if (not bk.term and g == bk.g1) else 0)
                     new = dst[L_A:L_TRACE + 1].copy()
+                    if critical_change is not None and not critical_change:
+                        new = eq
                     new[L_C0 - L_A] = old[L_C0 - L_A]
-                    if used and old.view(np.uint64).tolist() != new.view(np.uint64).tolist():
+                    if used and (critical_change is True or
+                                 old.view(np.uint64).tolist() != new.view(np.uint64).tolist()):
                         crit[j] = True
         for j in np.flatnonzero(crit):
             self.recompute_guiding_term(layout, b0 + j, b0 + j + 1, unit=1)

@@ -259,3 +259,33 @@ def test_two_services_on_one_device_interleaved():
     _same_state(b, b0, lay, nb, 12)
     for e in (a, b, a0, b0):
         e.close()
+
+
+@pytest.mark.gpu
+def test_service_switch_from_the_api_and_self_disable():
+    """dmt_set_service: off (enable 0, or an idle window of 0) runs one fused launch per
+    iteration and starts no service; a window so short that every launch leaves before its
+    iteration is posted makes the service turn itself off after 16 posts (more than one relaunch
+    per four posts: the fallback for a grid that other work keeps from being co-resident).
+    Every result equals the default service's and the oracle's."""
+    (svc, off, idle0, short, ora), lay, nb = _ensembles(["1", "1", "1", "1"], hist=40,
+                                                        service=["1", "1", "1", "1"])
+    off.set_service(False)
+    idle0.set_service(True, 0.0)
+    short.set_service(True, 0.001)
+    r = [_loop_gaps(e, lay, nb, 30, fetch_every=1) for e in (svc, off, idle0, ora)]
+    # the host away 0.5 ms before every post: each launch has left (1 µs window) by then
+    r.insert(3, _loop_gaps(short, lay, nb, 30, fetch_every=1, sleep_at=range(1, 31),
+                           sleep_s=0.0005))
+    for k in range(1, 5):
+        assert np.array_equal(r[0], r[k]), k
+    for e in (off, idle0, short, ora):
+        _same_state(svc, e, lay, nb, 40)
+    assert svc.service_stats()["starts"] >= 1 and svc.service_stats()["off"] == 0
+    assert off.service_stats()["starts"] == 0 and idle0.service_stats()["starts"] == 0
+    st = short.service_stats()
+    assert st["off"] == 1 and st["posts"] < 30, st
+    with pytest.raises(Exception):
+        svc.set_service(True, -1.0)
+    for e in (svc, off, idle0, short):
+        e.close()

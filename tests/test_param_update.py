@@ -90,6 +90,47 @@ def test_oracle_unchanged_theta_is_not_critical():
     assert crit.all()
 
 
+def test_oracle_critical_change_false_keeps_the_guiding_term():
+    """critical_change = false (src/biblock.jl:340-342): with u°'s law equal to u's, a θ° that
+    moves the auxiliary law still leaves u°'s guiding term (H, F, c(t0)) as it was — only the
+    records and the path change; after a swap made u°'s law differ from u's, the equalization
+    alone makes the update critical again (:361-362)."""
+    case = cs.ragged_case()
+    m = case["model"]
+    ora = orc.OracleEnsemble(m.kind, m.d, m.m, case["n_points"], prec=case["prec"], seed=1)
+    cs.load_ragged(ora, case)
+    ora.upload_obs(case["Hobs"], case["Fobs"], case["cobs"])
+    lay, R = _whole_recording_layout(ora, case)
+    H0, F0, laws0 = ora.download_law(L.UPROP, L.LAW_PP)
+    ok, crit = ora.set_proposal_law(lay, 0, R, _fhn_params(THETA1), critical_change=False)
+    assert ok.all() and not crit.any()
+    H1, F1, laws1 = ora.download_law(L.UPROP, L.LAW_PP)
+    assert np.array_equal(H1, H0) and np.array_equal(F1, F0)
+    assert not np.array_equal(laws1, laws0)  # θ° written, the auxiliary law re-derived
+    ok, crit = ora.set_proposal_law(lay, 0, R, _fhn_params(THETA1), critical_change=True)
+    assert crit.all()
+    ora.swap(lay, L.SWAP_PP, 0, R)  # u° now holds THETA0's law, u THETA1's
+    ok, crit = ora.set_proposal_law(lay, 0, R, _fhn_params(THETA1), critical_change=False)
+    assert crit.all()
+
+
+def test_updt_obs_is_refused():
+    """Observation parameters (updt_obs) are not device state: a ParamNamesBlock that would
+    update them raises instead of being silently ignored."""
+    from diffusionmcmctools_amd import functions as fn
+    unit = {"updt": ((1, "γ"),), "updt_aux": [((1, "γ"),)], "updt_obs": [((2, 1),)]}
+    empty = {"updt": (), "updt_aux": [], "updt_obs": []}
+    pn = {"PP": unit, "P_last": empty, "P_excl": empty, "Pb_excl": empty}
+    with pytest.raises(NotImplementedError):
+        fn._pairs(pn)
+    pn["PP"] = dict(unit, updt_obs=[()])
+    assert list(fn._pairs(pn).values()) == [1]
+    assert fn._flags(False, 3) == [False] * 3
+    assert fn._flags([[True, False], [True]], 3) == [True, False, True]
+    with pytest.raises(ValueError):
+        fn._flags([True], 2)
+
+
 def test_api_set_proposal_law_by_name():
     """BlockEnsemble.set_proposal_law(theta={name: value}) maps DD parameter names and runs the
     device operation (here through the oracle seam)."""
@@ -148,6 +189,35 @@ def test_parameter_mh_loop_bit_exact(mapping):
             for e in (dev, ora):
                 e.swap(lid, L.SWAP_XX | L.SWAP_PP | L.SWAP_LL, 0, nb)
         cs.assert_paths_equal(dev, ora)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mapping", MAPPINGS)
+def test_critical_change_false_bit_exact(mapping):
+    """set_proposal_law!(bb, θ°, pnames, false): device == oracle bit for bit — u°'s guiding
+    term kept where only θ° moved the auxiliary law, recomputed where the equalization with u's
+    law changed it (after a parameter swap)."""
+    case, dev, ora, ids = cs.ragged_pair(mapping=mapping, hist_len=4)
+    for e in (dev, ora):
+        e.upload_obs(case["Hobs"], case["Fobs"], case["cobs"])
+    lid, nb = ids[0]
+    for e in (dev, ora):
+        e.recompute_guiding_term(lid, 0, nb, unit=L.U)
+        e.loglikhd(lid, L.U, 0, nb)
+    for step, cc in enumerate((False, True, "swap", False)):
+        if cc == "swap":
+            for e in (dev, ora):
+                e.swap(lid, L.SWAP_XX | L.SWAP_PP | L.SWAP_LL, 0, nb)
+            continue
+        th = THETA1 if step < 2 else THETA0
+        okd, crd = dev.set_proposal_law(lid, 0, nb, _fhn_params(th), critical_change=cc)
+        oko, cro = ora.set_proposal_law(lid, 0, nb, _fhn_params(th), critical_change=cc)
+        assert np.array_equal(okd, oko) and np.array_equal(crd, cro), step
+        for kind in (L.LAW_PP, L.LAW_PPB):
+            for a_, b_ in zip(dev.download_law(L.UPROP, kind), ora.download_law(L.UPROP, kind)):
+                assert np.array_equal(a_, b_), (step, kind)
+        cs.assert_paths_equal(dev, ora)
+        cs.assert_ll_equal(dev, ora, lid, nb)
 
 
 @pytest.mark.gpu
