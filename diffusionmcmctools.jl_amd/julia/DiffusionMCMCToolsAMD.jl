@@ -523,19 +523,41 @@ function Base.getproperty(se::DeviceSamplingEnsemble, s::Symbol)
 end
 
 # the reference's constructors: device containers while use_device!(true) (the default after
-# `using DiffusionMCMCToolsAMD`), the reference's CPU ones otherwise
-function SamplingPair(aux_laws::Type, recording, tts, args...; kw...)
-    DEVICE[] || return invoke(SamplingPair, Tuple{Any,Any,Any,Vararg{Any}}, aux_laws,
-                              recording, tts, args...; kw...)
+# `using DiffusionMCMCToolsAMD`), the reference's CPU ones otherwise.  The reference's inner
+# constructors take (aux_laws, recording(s), tts) or (…, args) (src/sampling_pair.jl:40-44,
+# src/sampling_ensemble.jl:20-24): methods of arity 3 and 4.  These methods add the same two
+# arities for aux_laws::Type (the tutorials pass the auxiliary law's type), strictly more
+# specific than the reference's, so there is no ambiguity; the CPU fallback `invoke`s the
+# reference's method of the same arity.  (Extending the reference's own constructor for its
+# own argument types is type piracy, deliberately: it is what lets the tutorials' code run
+# unchanged — INTEGRATION.md §2 names the explicit alternative, DeviceSamplingPair.)
+function SamplingPair(aux_laws::Type, recording, tts; kw...)
+    DEVICE[] || return invoke(SamplingPair, Tuple{Any,Any,Any}, aux_laws, recording, tts; kw...)
+    _device_pair(aux_laws, recording, tts; kw...)
+end
+function SamplingPair(aux_laws::Type, recording, tts, args; kw...)
+    DEVICE[] || return invoke(SamplingPair, Tuple{Any,Any,Any,Any}, aux_laws, recording, tts,
+                              args; kw...)
+    _device_pair(aux_laws, recording, tts; kw...)
+end
+function _device_pair(aux_laws, recording, tts; kw...)
     kws = Dict(kw)
     se = _device_ensemble(aux_laws, [recording], [tts];
                           artificial_noise=get(kws, :artificial_noise, 1e-11))
     DeviceSamplingPair(se, 1)
 end
 
-function SamplingEnsemble(aux_laws::Type, recordings, tts, args...; kw...)
-    DEVICE[] || return invoke(SamplingEnsemble, Tuple{Any,Any,Any,Vararg{Any}}, aux_laws,
-                              recordings, tts, args...; kw...)
+function SamplingEnsemble(aux_laws::Type, recordings, tts; kw...)
+    DEVICE[] || return invoke(SamplingEnsemble, Tuple{Any,Any,Any}, aux_laws, recordings, tts;
+                              kw...)
+    _device_ensemble_kw(aux_laws, recordings, tts; kw...)
+end
+function SamplingEnsemble(aux_laws::Type, recordings, tts, args; kw...)
+    DEVICE[] || return invoke(SamplingEnsemble, Tuple{Any,Any,Any,Any}, aux_laws, recordings,
+                              tts, args; kw...)
+    _device_ensemble_kw(aux_laws, recordings, tts; kw...)
+end
+function _device_ensemble_kw(aux_laws, recordings, tts; kw...)
     kws = Dict(kw)
     _device_ensemble(aux_laws, collect(recordings), collect(tts);
                      artificial_noise=get(kws, :artificial_noise, 1e-11))
@@ -896,6 +918,10 @@ function _param_map(se::DeviceSamplingEnsemble, pnames_block)
     m = Dict{Int32,Int}()
     for coll in (:PP, :P_last, :P_excl, :Pb_excl)
         u = getproperty(pnames_block, coll)
+        # observation parameters (DD.set_parameters!(PP, θ°, updt, updt_aux, updt_obs),
+        # src/biblock.jl:373-375) are not device state: refuse instead of dropping them
+        hasproperty(u, :updt_obs) && any(!isempty, u.updt_obs) &&
+            error("set_proposal_law!: observation parameters (updt_obs) are not updated on the device")
         pairs = collect(u.updt)
         for ua in u.updt_aux
             append!(pairs, collect(ua))
@@ -909,45 +935,58 @@ function _param_map(se::DeviceSamplingEnsemble, pnames_block)
     m
 end
 
-function _set_law!(x::DeviceBlocks, θ°, pmap; skip=0)
+# critical_change: nothing (the reference's default, GP.is_critical_update) → -1, recompute the
+# guiding term where the auxiliary law changed; true → 1, every block; false → 0, only where
+# equalizing u°'s law with u's changed it (dmt_set_proposal_law_cc, include/dmt.h)
+_cc(c) = c === nothing ? Int32(-1) : (c ? Int32(1) : Int32(0))
+
+function _set_law!(x::DeviceBlocks, θ°, pmap, cc::Int32; skip=0)
     idx = collect(keys(pmap))
     val = Float64[θ°[pmap[k]] for k in idx]
     ok = Vector{UInt8}(undef, _n(x))
     crit = Vector{UInt8}(undef, _n(x))
-    check(ccall((:dmt_set_proposal_law, libdmt), Int32,
-        (Ptr{Cvoid}, Int32, Int64, Int64, Int32, Ptr{Int32}, Ptr{Float64}, Int32, Ptr{UInt8},
-         Ptr{UInt8}), x.se.h, x.layout, x.b0, x.b1, length(idx), idx, val, skip, ok, crit))
+    check(ccall((:dmt_set_proposal_law_cc, libdmt), Int32,
+        (Ptr{Cvoid}, Int32, Int64, Int64, Int32, Ptr{Int32}, Ptr{Float64}, Int32, Int32,
+         Ptr{UInt8}, Ptr{UInt8}), x.se.h, x.layout, x.b0, x.b1, length(idx), idx, val, skip, cc,
+        ok, crit))
     Bool.(ok)
 end
 
 """
-    set_proposal_law!(x, θ°, pnames, critical_change=true; skip=0)
+    set_proposal_law!(x, θ°, pnames, critical_change=nothing; skip=0)
 
 The reference's `set_proposal_law!` (src/biblock.jl:334-344, src/block_collection.jl:264-276,
 src/block_ensemble.jl:242-255) on device blocks: `pnames` as the reference's (a BiBlock's
 NamedTuple / ParamNamesBlock of `PP, P_last, P_excl, Pb_excl` with `updt` pairs `idx => name`;
 `pnames.blocks[i]` of a collection; `pnames.recordings[r].blocks[i]` of an ensemble).  u°'s laws
-← u's with the named parameters set from θ°, the guiding term of b° recomputed where the law
-changed (what any correct `critical_change` requests; an unchanged law's recomputation
-reproduces its guiding term bit for bit), then recompute_path!(b°, b.WW; skip).  One ccall over
-all blocks whose maps agree.
+← u's with the named parameters set from θ°, the guiding term of b° recomputed — omitted
+(the reference's default GP.is_critical_update): where the auxiliary law changed (an unchanged
+law's recomputation reproduces its guiding term bit for bit); `true`: every block; `false`: only
+where equalizing b°'s law with b's changed it (:340-342, 361-362); a collection / ensemble also
+takes one Bool per block (per recording a vector) — then recompute_path!(b°, b.WW; skip).  One
+ccall over all blocks whose maps and flags agree.
 """
-function set_proposal_law!(bb::DeviceBiBlock, θ°, pnames, critical_change=true; skip=0)
-    _set_law!(bb, θ°, _param_map(bb.se, pnames); skip=skip)
+function set_proposal_law!(bb::DeviceBiBlock, θ°, pnames, critical_change=nothing; skip=0)
+    _set_law!(bb, θ°, _param_map(bb.se, pnames), _cc(critical_change); skip=skip)
 end
 
-function _set_law_blocks!(x, blocks, pblocks, θ°; skip=0)
+function _set_law_blocks!(x, blocks, pblocks, θ°, critical_change; skip=0)
     maps = [_param_map(x.se, pb) for pb in pblocks]
-    all(==(maps[1]), maps) && return _set_law!(x, θ°, maps[1]; skip=skip)
-    reduce(vcat, [_set_law!(bb, θ°, m; skip=skip) for (bb, m) in zip(blocks, maps)])
+    ccs = critical_change isa AbstractArray ?
+        Int32[_cc(c) for c in Iterators.flatten(critical_change)] :
+        fill(_cc(critical_change), length(blocks))
+    length(ccs) == length(blocks) || error("critical_change: $(length(ccs)) flags for $(length(blocks)) blocks")
+    all(==(maps[1]), maps) && all(==(ccs[1]), ccs) && return _set_law!(x, θ°, maps[1], ccs[1]; skip=skip)
+    reduce(vcat, [_set_law!(bb, θ°, m, c; skip=skip) for (bb, m, c) in zip(blocks, maps, ccs)])
 end
 
-set_proposal_law!(bc::DeviceBlockCollection, θ°, pnames, critical_change=true; skip=0) =
-    _set_law_blocks!(bc, bc.blocks, pnames.blocks, θ°; skip=skip)
+set_proposal_law!(bc::DeviceBlockCollection, θ°, pnames, critical_change=nothing; skip=0) =
+    _set_law_blocks!(bc, bc.blocks, pnames.blocks, θ°, critical_change; skip=skip)
 
-set_proposal_law!(be::DeviceBlockEnsemble, θ°, pnames, critical_change=true; skip=0) =
+set_proposal_law!(be::DeviceBlockEnsemble, θ°, pnames, critical_change=nothing; skip=0) =
     _set_law_blocks!(be, [bb for bc in be.recordings for bb in bc.blocks],
-                     [pb for pr in pnames.recordings for pb in pr.blocks], θ°; skip=skip)
+                     [pb for pr in pnames.recordings for pb in pr.blocks], θ°, critical_change;
+                     skip=skip)
 
 "find_W_for_X!(b) (src/block.jl:118-131): u.WW from u.XX under the accepted laws."
 find_W_for_X!(x::DeviceBlocks) = check(ccall((:dmt_find_W_for_X, libdmt), Int32,

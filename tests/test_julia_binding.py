@@ -24,6 +24,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 JL = os.path.join(ROOT, "diffusionmcmctools.jl_amd", "julia", "DiffusionMCMCToolsAMD.jl")
+REF = "/root/reference"  # read as text by CPU tests only, when present (never on the GPU box)
 HDR = os.path.join(ROOT, "include", "dmt.h")
 
 # C parameter type → the Julia ccall types that pass it
@@ -172,7 +173,7 @@ def test_every_ccall_matches_the_header():
     # the hot path and the tutorial surface all go through the binding
     for must in ("dmt_create", "dmt_draw_proposal", "dmt_accept_reject", "dmt_loglikhd",
                  "dmt_fetch_ll", "dmt_fetch_ll_local", "dmt_mcmc_step_local", "dmt_mcmc_run_local",
-                 "dmt_set_proposal_law", "dmt_set_obs", "dmt_recompute_guiding_term",
+                 "dmt_set_proposal_law_cc", "dmt_set_obs", "dmt_recompute_guiding_term",
                  "dmt_find_W_for_X", "dmt_get_block_state", "dmt_set_block_state"):
         assert must in seen, must
 
@@ -205,8 +206,46 @@ def test_tutorial_calls_are_methods_of_the_reference_functions():
     assert re.search(r"GP\.recompute_guiding_term!\(b::DeviceBlock\)", src)
     # set_proposal_law!(bb, θ°, pnames, critical_change; skip) — the reference's signature
     for T in ("DeviceBiBlock", "DeviceBlockCollection", "DeviceBlockEnsemble"):
-        assert re.search(r"set_proposal_law!\(\w+::" + T + r", θ°, pnames, critical_change=true;"
+        assert re.search(r"set_proposal_law!\(\w+::" + T + r", θ°, pnames, critical_change=nothing;"
                          r" skip=0\)", src), T
+    assert "dmt_set_proposal_law_cc" in src
+
+
+def _reference_constructor_arities(path, name):
+    """Positional arities of the reference's inner constructor `name(a, b, c, args=tuple(); …)`:
+    the required count and each optional one added."""
+    src = open(path).read()
+    m = re.search(r"function " + name + r"\(\s*(.*?)\)\s*\n", src, re.S)
+    pos = m.group(1).split(";")[0]
+    params = [p.strip() for p in pos.split(",") if p.strip()]
+    req = sum(1 for p in params if "=" not in p)
+    return set(range(req, len(params) + 1))
+
+
+def test_cpu_fallback_invokes_defined_reference_arities():
+    """use_device!(false) falls back to the reference's own constructors with `invoke`: every
+    invoke signature must name a positional arity the reference's inner constructor defines
+    (src/sampling_pair.jl:40-44, src/sampling_ensemble.jl:20-24 — 3 or 4; a Vararg signature
+    matches no single method), and each device method must be an arity-fixed method on
+    aux_laws::Type (strictly more specific than the reference's, so no ambiguity)."""
+    src = _strip_comments(open(JL).read())
+    ref = {"SamplingPair": os.path.join(REF, "src", "sampling_pair.jl"),
+           "SamplingEnsemble": os.path.join(REF, "src", "sampling_ensemble.jl")}
+    for name, path in ref.items():
+        arities = (_reference_constructor_arities(path, name) if os.path.exists(path)
+                   else {3, 4})  # the reference is not on the GPU box
+        inv = re.findall(r"invoke\(" + name + r", Tuple\{([^}]*)\}", src)
+        assert inv, name
+        seen = set()
+        for sig in inv:
+            assert "Vararg" not in sig, (name, sig)
+            n = len([t for t in sig.split(",") if t.strip()])
+            assert n in arities, (name, sig, arities)
+            seen.add(n)
+        assert seen == arities, (name, seen, arities)
+        defs = re.findall(r"function " + name + r"\((aux_laws::Type[^;)]*)[;)]", src)
+        assert sorted(len(d.split(",")) for d in defs) == sorted(arities), (name, defs)
+        assert all("..." not in d for d in defs), defs
 
 
 def test_tutorial_field_accesses_are_served():
