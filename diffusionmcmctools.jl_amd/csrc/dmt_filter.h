@@ -319,7 +319,7 @@ DMT_HD bool filter_combine(const Trans<N>& q, Mat<N>& Hc, double* Fc, double& cc
 constexpr int kFiltChunk = 64;
 
 // Coef(i, B, beta): the auxiliary drift of step i (constant, or a time-dependent law's
-// coefficients at the step's left point t_i).
+// trapezoidal average over [t_i, t_i+1]: second order).
 template <int N, class TimeAt, class Coef, class Store>
 inline bool filter_segment(Coef coef, const Mat<N>& A, int npts, TimeAt tat, Mat<N>& Hc,
                            double* Fc, double& cc, Store store) {

@@ -3136,15 +3136,18 @@ __device__ __forceinline__ void filt_law(const FilterArgs& a, int g, int kind, f
   }
 }
 
-// A time-dependent auxiliary law's B̃(t_i), β̃(t_i) (the per-point table, element c of point q
-// at tab[ix(q, c)]) as the filter's doubles
+// A time-dependent auxiliary law's coefficients of the filter's step q → q + 1 (the per-point
+// table, element c of point q at tab[ix(q, c)]), as doubles: the trapezoidal averages
+// (v(t_q) + v(t_q+1))·0.5 of B̃ and β̃, which make the exact step transition a second-order
+// scheme for the filter ODEs (a constant table gives the table's value exactly)
 template <int D, class T, class Ix>
 __device__ __forceinline__ void filt_aux_step(const T* tab, Ix ix, int64_t q, flt::Mat<D>& B,
                                               double* beta) {
 #pragma unroll
-  for (int c = 0; c < D * D; ++c) B.a[c] = (double)tab[ix(q, c)];
+  for (int c = 0; c < D * D; ++c) B.a[c] = ((double)tab[ix(q, c)] + (double)tab[ix(q + 1, c)]) * 0.5;
 #pragma unroll
-  for (int p = 0; p < D; ++p) beta[p] = (double)tab[ix(q, D * D + p)];
+  for (int p = 0; p < D; ++p)
+    beta[p] = ((double)tab[ix(q, D * D + p)] + (double)tab[ix(q + 1, D * D + p)]) * 0.5;
 }
 
 // chunk j of a segment with np points: steps [lo, lo + cnt), counted from the segment end

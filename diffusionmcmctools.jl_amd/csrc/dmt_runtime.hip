@@ -2466,6 +2466,7 @@ dmt_status dmt_set_rng_state(dmt_ens* h, uint64_t next, uint64_t last_draw, uint
 
 template <int D>
 // aux: nullptr (B̃ = Bt, β̃ = beta throughout) or [npts][d·d + d] per-point coefficients
+// (step i: the trapezoidal average of rows i and i + 1)
 static dmt_status guiding_linear_impl(const double* Bt, const double* beta, const double* aux,
                                       const double* at, int32_t npts, const double* t,
                                       const double* HT, const double* FT, double cT, double* H,
@@ -2488,11 +2489,18 @@ static dmt_status guiding_linear_impl(const double* Bt, const double* beta, cons
     for (int p = 0; p < d; ++p) F[(int64_t)i * d + p] = Fs[p];
     c[i] = cs;
   };
+  // step i's auxiliary drift: the law's, or the trapezoidal average of a time-dependent law's
+  // coefficients at t_i and t_i+1 (second order; DESIGN.md §3, filt_aux_step on the device)
   auto coef = [&](int i, flt::Mat<D>& B, double* be) {
-    const double* bs = aux ? aux + (int64_t)i * (d * d + d) : Bt;
-    const double* bb = aux ? bs + d * d : beta;
-    for (int k = 0; k < d * d; ++k) B.a[k] = bs[k];
-    for (int p = 0; p < d; ++p) be[p] = bb[p];
+    if (!aux) {
+      for (int k = 0; k < d * d; ++k) B.a[k] = Bt[k];
+      for (int p = 0; p < d; ++p) be[p] = beta[p];
+      return;
+    }
+    const double* r0 = aux + (int64_t)i * (d * d + d);
+    const double* r1 = r0 + (d * d + d);
+    for (int k = 0; k < d * d; ++k) B.a[k] = (r0[k] + r1[k]) * 0.5;
+    for (int p = 0; p < d; ++p) be[p] = (r0[d * d + p] + r1[d * d + p]) * 0.5;
   };
   if (!flt::filter_segment<D>(coef, A, npts, [&](int i) { return t[i]; }, Hc, Fc, cc, store))
     return fail(DMT_ERR_INVALID, "singular I + HK in backward filter");

@@ -1028,7 +1028,9 @@ static int fm_combine(const ftr_t* q, fm_t* Hc, double* Fc, double* cc) {
  * point of the chunk by one combine from the chunk end's (H, F, c). */
 #define FILT_CHUNK 64
 /* aux: NULL (B~ = Bt, beta~ = beta on every step) or [npts][d*d + d] per-point coefficients
- * of a time-dependent auxiliary law, step i taking row i (left point). */
+ * of a time-dependent auxiliary law; step i's exact transition takes the trapezoidal average
+ * (row i + row i+1) * 0.5 — a second-order scheme for the filter ODEs (libdmt filt_aux_step,
+ * dmt_guiding_linear_td). */
 static int backward_filter(int d, const double* Bt, const double* beta, const double* aux,
                            const double* at, int npts, const double* t, const double* HT,
                            const double* FT, double cT, double* H, double* F, double* c) {
@@ -1052,10 +1054,13 @@ static int backward_filter(int d, const double* Bt, const double* beta, const do
         int lo = hi > FILT_CHUNK ? hi - FILT_CHUNK : 0, cnt = hi - lo;
         for (int l = 0; l < cnt; ++l) {
             const double* bl = beta;
-            if (aux) {
-                const double* row = aux + (size_t)(lo + l) * (d * d + d);
-                for (int i = 0; i < d * d; ++i) B.a[i] = row[i];
-                bl = row + d * d;
+            double bavg[3];
+            if (aux) {  /* step lo + l: trapezoidal average of rows lo + l and lo + l + 1 */
+                const double* r0 = aux + (size_t)(lo + l) * (d * d + d);
+                const double* r1 = r0 + (d * d + d);
+                for (int i = 0; i < d * d; ++i) B.a[i] = (r0[i] + r1[i]) * 0.5;
+                for (int i = 0; i < d; ++i) bavg[i] = (r0[d * d + i] + r1[d * d + i]) * 0.5;
+                bl = bavg;
             }
             fm_transition(&B, bl, &A, t[lo + l + 1] - t[lo + l], &Q[l].Phi, Q[l].mu, &Q[l].K);
         }

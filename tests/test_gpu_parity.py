@@ -743,3 +743,49 @@ def test_blocking_loop_bit_exact(mapping):
         assert np.array_equal(ad, ao), f"iteration {i}"
         cs.assert_paths_equal(dev, ora)
         cs.assert_ll_equal(dev, ora, lid, nb)
+
+
+@pytest.mark.parametrize("n_iter", [5])
+def test_headline_mcmc_run_full_c2_bit_exact(n_iter):
+    """The bench's headline kernel itself — dmt_mcmc_run on the full C2 shard (1 024 blocks ×
+    500 steps, fp64, device RNG), i.e. k_mcmc_resident_pc: draw, MH decision, histories and
+    every iteration's fetch_ll tree in one launch — against the oracle's restatement of the same
+    iterations (src/biblock.jl:80-127: pCN draw, E > -(ll° - ll), swaps), ALL blocks, bit for
+    bit: every iteration's decisions, fetch_ll, fetch_ll° and accepted count, and the final
+    paths X, W and ll of u.  The oracle runs the canonical arithmetic on the
+    device's own Philox normal and Exp(1) streams (key (iteration, salt 0))."""
+    import diffusionmcmctools_amd as d
+    w = cs.full_workload("c2")
+    w.meta["hist_len"] = n_iter
+    seed = 0xD1FF
+    dev = d.Ensemble(w.model.kind, w.d, w.m, w.n_points, precision=w.precision, seed=seed,
+                     grid_shared=w.grid_shared)
+    lay = W.fill(dev, w, init_Z=False)
+    B, npts = w.nblocks, w.n_points[0][0]
+    dev.loglikhd(lay, L.U, 0, B)
+    X, Wd = dev.download_paths(L.U, 0), dev.download_paths(L.U, 2)
+    ll = dev.get_block_state(lay, L.BLK_LL, 0, B)
+    out = dev.mcmc_run(lay, 0, B, 1, n_iter)          # one k_mcmc_resident_pc launch
+    acc_dev = dev.get_block_state(lay, L.BLK_ACC_HIST, 0, B, hist_len=n_iter).astype(bool)
+    Xd, Wdd = dev.download_paths(L.U, 0), dev.download_paths(L.U, 2)
+    lld = dev.get_block_state(lay, L.BLK_LL, 0, B)
+    dev.close()
+    rho = np.full(B, w.rho)
+    for it in range(1, n_iter + 1):
+        Xo, Wo, llp, nf = orc.draw_terminal_blocks(
+            w.model.kind, w.d, w.m, npts, w.laws, w.t, w.H, w.F, X, Wd, rho, Z=None, seed=seed,
+            it=it, salt=0, prec=w.precision, nthreads=8, t_shared=True, H_shared=w.H_shared)
+        assert nf == 0
+        E = orc.exp1_range(seed, 0, B, it, 0)
+        acc = E > -(llp - ll)
+        np.testing.assert_array_equal(acc_dev[it - 1], acc, err_msg=f"decisions, iteration {it}")
+        llprop_after = np.where(acc, ll, llp)         # swap_ll! on acceptance
+        ll = np.where(acc, llp, ll)
+        sel = np.repeat(acc, npts)[:, None]
+        X, Wd = np.where(sel, Xo, X), np.where(sel, Wo, Wd)
+        want = (orc.pairwise_tree(ll), orc.pairwise_tree(llprop_after), float(acc.sum()))
+        assert tuple(out[it - 1]) == want, (it, tuple(out[it - 1]), want)
+    assert 0.3 < acc_dev.mean() < 1.0
+    np.testing.assert_array_equal(Xd, X)
+    np.testing.assert_array_equal(Wdd, Wd)
+    np.testing.assert_array_equal(lld, ll)
