@@ -1653,12 +1653,32 @@ __device__ __forceinline__ void st_sc1(double* p, double v) {
 }
 // drain this wave's stores, join the workgroup, one lane adds to *cnt; true in every thread of
 // the workgroup whose add completed the count `expect`
+// The form is the guide's measured one (MI355X_MICROARCH.md, inter-workgroup visibility,
+// "Hand-offs measured with sc1 loads", row 1: sc1 stores drained by every storing wave, one
+// lane per workgroup adds to one unsharded counter after a barrier, the last adder — told by
+// its add's return — loads with sc1; hipMalloc memory, one workgroup per CU), not an API
+// guarantee.  DMT_TREE_FENCES=1 (measurement build) adds the API's agent-scope release before
+// the add and acquire after it (their price per C2 launch).
+#ifndef DMT_TREE_FENCES
+#define DMT_TREE_FENCES 0
+#endif
 __device__ __forceinline__ bool arrive_last(unsigned* cnt, unsigned expect, int* s_flag) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0)
+  if (threadIdx.x == 0) {
+#if DMT_TREE_FENCES
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
     *s_flag = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
                       expect - 1 ? 1 : 0;
+#if DMT_TREE_FENCES
+    if (*s_flag) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+#endif
+  }
   __syncthreads();
   return *s_flag != 0;
 }

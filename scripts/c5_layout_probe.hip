@@ -43,8 +43,8 @@ struct Args {
   const T* t;  // shared grid [rows]
   const T* H;  // row layout, per tile [rows][HP][64]
   const T* F;  // [rows][D][64]
-  T* X[2];
-  T* W[2];
+  T* X[3];
+  T* W[3];
   const uint8_t* u;  // [R] lane's u buffer
   int64_t rows;      // padded point rows per tile (path planes and tables alike)
   int nst;           // steps per segment
@@ -62,7 +62,8 @@ __device__ __forceinline__ int64_t ppos(int64_t q, int c, int C, int lane) {
   }
 }
 
-// SEL: 0 uniform, 1 mixed, 2 consolidated (P = 1 only)
+// SEL: 0 uniform, 1 mixed, 2 consolidated (P = 1 only), 3 reads mixed (buffer u) / writes
+// uniform (buffer 2), 4 reads uniform (buffer 0) / writes mixed (buffer 1 + u)
 template <int P, int SEL>
 __global__ __launch_bounds__(64) void k_probe(const Args a) {
   const int lane = threadIdx.x;
@@ -79,7 +80,9 @@ __global__ __launch_bounds__(64) void k_probe(const Args a) {
     copy = u != m;
     pbuf = 1 - m;
   }
-  const T* Ws = a.W[u] + pbM;
+  const T* Ws = a.W[SEL == 4 ? 0 : u] + pbM;
+  if (SEL == 3) pbuf = 2;
+  if (SEL == 4) pbuf = 1 + u;
   T* Wd = a.W[pbuf] + pbM;
   T* Xd = a.X[pbuf] + pbD;
   T* Xcd = a.X[1 - pbuf] + pbD;  // consolidation target (= the majority's buffer)
@@ -199,6 +202,155 @@ __global__ __launch_bounds__(64) void k_probe(const Args a) {
   a.ll[r] = (double)ll + (double)x[0];
 }
 
+// Full lane packets: the path planes' row q at position q + P − 1 of the lane's P-point packets
+// (P·4 B each: 32 B for P = 8, 64 B for P = 16); per packet of P steps, the lane loads its u.W
+// packet (P/4 float4 per component, back to back, one packet ahead) and stores its X°/W°
+// packets whole at the packet's end — every access a whole 32/64-byte piece of ONE lane, so a
+// lane's buffer never shares a piece with another lane's.  SEL: 0 uniform, 1 mixed.
+template <int P, int SEL>
+__global__ __launch_bounds__(64) void k_probe_pk(const Args a) {
+  const int lane = threadIdx.x;
+  const int64_t tile = blockIdx.x;
+  const int64_t r = tile * 64 + lane;
+  const int64_t tb = tile * a.rows;
+  const int64_t pbD = tb * D * 64, pbM = tb * M * 64;
+  const int u = SEL == 0 ? 0 : a.u[r];
+  const int pbuf = 1 - u;
+  const T* Ws = a.W[u] + pbM;
+  T* Wd = a.W[pbuf] + pbM;
+  T* Xd = a.X[pbuf] + pbD;
+  const T* Hb = a.H + tb * HP * 64 + lane;
+  const T* Fb = a.F + tb * D * 64 + lane;
+  Law<Mdl, T> L;
+  L.th[0] = 10; L.th[1] = 28; L.th[2] = 8.0f / 3;
+  for (int i = 0; i < D * D; ++i) L.Bt[i] = (i % 4 == 0) ? -1.0f : 0.1f;
+  for (int i = 0; i < D; ++i) L.beta[i] = 0.5f;
+  for (int i = 0; i < HP; ++i) L.da[i] = 0;
+  L.trace = false;
+  L.unit = true;
+  L.auxtd = false;
+  T x[D] = {1.0f, 1.0f, 20.0f};
+  T tcur = a.t[0];
+  T ll = 0;
+  const T rho = 0.9f, srho = sqrtf(1 - 0.81f);
+  const uint32_t seg = (uint32_t)r;
+  constexpr int NV = P / 4;
+  // packet j (rows jP+1 … jP+P) of component c: lane's float4 pieces
+  auto pk = [&](const T* base, int64_t j, int c, int C) -> const float4* {
+    return (const float4*)&base[(((j + 1) * C + c) * 64 + lane) * P];
+  };
+  auto pkw = [&](T* base, int64_t j, int c, int C) -> float4* {
+    return (float4*)&base[(((j + 1) * C + c) * 64 + lane) * P];
+  };
+  float4 wcur[M][NV], wnxt[M][NV];
+  auto loadw = [&](int64_t j, float4 (&w)[M][NV]) {
+#pragma unroll
+    for (int k = 0; k < M; ++k)
+#pragma unroll
+      for (int v = 0; v < NV; ++v) w[k][v] = pk(Ws, j, k, M)[v];
+  };
+  struct Chunk {
+    T t[K], H[K][HP], F[K][D];
+  };
+  auto load = [&](int c0, Chunk& c) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const int64_t i = c0 + j;
+      c.t[j] = a.t[i + 1];
+#pragma unroll
+      for (int e = 0; e < HP; ++e) c.H[j][e] = Hb[(i * HP + e) * 64];
+#pragma unroll
+      for (int e = 0; e < D; ++e) c.F[j][e] = Fb[(i * D + e) * 64];
+    }
+  };
+  const int npk = a.nst / P;
+  Chunk cur, nxt;
+  load(0, cur);
+  loadw(0, wcur);
+  for (int j = 0; j < npk; ++j) {
+    loadw(j + 1, wnxt);  // padded rows keep the last packet's prefetch in bounds
+    float4 ox[D][NV], ow[M][NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int c0 = j * P + 4 * v;
+      load(c0 + K, nxt);
+      T Z[K][M];
+#pragma unroll
+      for (int bq = 0; bq < K * M / 4; ++bq) {
+        T zb[4];
+        normal_block(philox4x32_10(U4{(uint32_t)(c0 * M / 4 + bq), seg, a.iter, 0u}, 0x1234u, 0x5678u),
+                     zb);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) Z[(4 * bq + e) / M][(4 * bq + e) % M] = zb[e];
+      }
+      T g[K], oxs[K][D], ows[K][M];
+#pragma unroll
+      for (int q = 0; q < K; ++q) {
+        const T dt = cur.t[q] - tcur;
+        const T sdt = sqrtf(dt);
+        T dW[M];
+#pragma unroll
+        for (int k = 0; k < M; ++k) {
+          const float4 w4 = wcur[k][v];
+          const T wu = q == 0 ? w4.x : q == 1 ? w4.y : q == 2 ? w4.z : w4.w;
+          dW[k] = dfma(rho, wu, srho * (sdt * Z[q][k]));
+        }
+        T rr[D], b[D], Mg[D * D], cg[D];
+        const T G = g_at<Mdl, T>(L, cur.H[q], cur.F[q], x, rr, b);
+        guide_coeffs_unit<Mdl, T>(cur.H[q], cur.F[q], Mg, cg);
+        euler_step<Mdl, T>(Mg, cg, b, dt, dW, x);
+        tcur = cur.t[q];
+        g[q] = G * dt;
+#pragma unroll
+        for (int p = 0; p < D; ++p) oxs[q][p] = x[p];
+#pragma unroll
+        for (int k = 0; k < M; ++k) ows[q][k] = dW[k];
+      }
+      ll += (g[0] + g[1]) + (g[2] + g[3]);
+#pragma unroll
+      for (int p = 0; p < D; ++p) ox[p][v] = make_float4(oxs[0][p], oxs[1][p], oxs[2][p], oxs[3][p]);
+#pragma unroll
+      for (int k = 0; k < M; ++k) ow[k][v] = make_float4(ows[0][k], ows[1][k], ows[2][k], ows[3][k]);
+      cur = nxt;
+    }
+#pragma unroll
+    for (int p = 0; p < D; ++p)
+#pragma unroll
+      for (int v = 0; v < NV; ++v) pkw(Xd, j, p, D)[v] = ox[p][v];
+#pragma unroll
+    for (int k = 0; k < M; ++k)
+#pragma unroll
+      for (int v = 0; v < NV; ++v) pkw(Wd, j, k, M)[v] = ow[k][v];
+#pragma unroll
+    for (int k = 0; k < M; ++k)
+#pragma unroll
+      for (int v = 0; v < NV; ++v) wcur[k][v] = wnxt[k][v];
+  }
+  a.ll[r] = (double)ll + (double)x[0];
+}
+
+template <int P, int SEL>
+static double run_pk(const Args& a, int ntiles, int reps, const char* name) {
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  k_probe_pk<P, SEL><<<ntiles, 64>>>(a);
+  CHECK(hipGetLastError());
+  CHECK(hipDeviceSynchronize());
+  CHECK(hipEventRecord(e0));
+  for (int i = 0; i < reps; ++i) k_probe_pk<P, SEL><<<ntiles, 64>>>(a);
+  CHECK(hipEventRecord(e1));
+  CHECK(hipEventSynchronize(e1));
+  float ms;
+  CHECK(hipEventElapsedTime(&ms, e0, e1));
+  const double us = ms * 1e3 / reps;
+  const double steps = (double)ntiles * 64 * (a.nst / P) * P;
+  printf("{\"variant\": \"%s\", \"P\": %d, \"sel\": %d, \"us_per_draw\": %.1f, \"frac_72B\": %.3f}\n",
+         name, P, SEL, us, steps * 72 / (us * 1e-6) / 8e12);
+  fflush(stdout);
+  return us;
+}
+
 template <int P, int SEL>
 static double run(const Args& a, int ntiles, int reps, const char* name) {
   hipEvent_t e0, e1;
@@ -226,7 +378,7 @@ int main(int argc, char** argv) {
   const int nst = 2000;
   const int reps = argc > 2 ? atoi(argv[2]) : 10;
   const char* only = argc > 3 ? argv[3] : nullptr;
-  const int64_t rows = ((nst + 1 + 2 * K + 32 + 31) / 32) * 32 + 32;  // room for prefetch + packet shift
+  const int64_t rows = ((nst + 1 + 2 * K + 32 + 31) / 32) * 32 + 96;  // room for prefetch + packet shift
   const int64_t R = (int64_t)ntiles * 64;
   Args a{};
   a.rows = rows;
@@ -248,7 +400,7 @@ int main(int argc, char** argv) {
   };
   a.H = alloc(HP, 0.01f);
   a.F = alloc(D, 0.02f);
-  for (int b = 0; b < 2; ++b) {
+  for (int b = 0; b < 3; ++b) {
     a.X[b] = alloc(D, 0.0f);
     a.W[b] = alloc(M, 0.001f);
   }
@@ -265,12 +417,12 @@ int main(int argc, char** argv) {
     if (want("row_uniform")) run<1, 0>(a, ntiles, reps, "row_uniform");
     if (want("row_mixed")) run<1, 1>(a, ntiles, reps, "row_mixed");
     if (want("row_consolidated")) run<1, 2>(a, ntiles, reps, "row_consolidated");
-    if (want("pk8_uniform")) run<8, 0>(a, ntiles, reps, "pk8_uniform");
-    if (want("pk8_mixed")) run<8, 1>(a, ntiles, reps, "pk8_mixed");
-    if (want("pk16_uniform")) run<16, 0>(a, ntiles, reps, "pk16_uniform");
-    if (want("pk16_mixed")) run<16, 1>(a, ntiles, reps, "pk16_mixed");
-    if (want("pk32_uniform")) run<32, 0>(a, ntiles, reps, "pk32_uniform");
-    if (want("pk32_mixed")) run<32, 1>(a, ntiles, reps, "pk32_mixed");
+    if (want("row_mixread")) run<1, 3>(a, ntiles, reps, "row_mixread");
+    if (want("row_mixwrite")) run<1, 4>(a, ntiles, reps, "row_mixwrite");
+    if (want("pk8f_uniform")) run_pk<8, 0>(a, ntiles, reps, "pk8f_uniform");
+    if (want("pk8f_mixed")) run_pk<8, 1>(a, ntiles, reps, "pk8f_mixed");
+    if (want("pk16f_uniform")) run_pk<16, 0>(a, ntiles, reps, "pk16f_uniform");
+    if (want("pk16f_mixed")) run_pk<16, 1>(a, ntiles, reps, "pk16f_mixed");
   }
   return 0;
 }
