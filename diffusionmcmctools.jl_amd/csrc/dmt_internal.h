@@ -35,6 +35,23 @@ __host__ __device__ __forceinline__ uint8_t sel_swap(unsigned s) { return sel_ma
 __host__ __device__ __forceinline__ uint8_t sel_two(int u) { return sel_make(u, u ^ 1); }
 constexpr uint8_t kSelInit = 4;  // sel_two(0): u in buffer 0, u° in buffer 1
 
+// Element index in a plane of tile width tw: component c of C of plane row `row` (= the tile's
+// first row tile_qoff + the point's row q within its recording) for tile slot `slot`.
+//   pk = 0: the row layout ((row·C + c)·tw + slot) — a wave's 64 lanes touch 64 consecutive
+//           elements per component;
+//   pk > 0 (a power of two; the path planes X, W of an fp32 MAP_LANE ensemble, DESIGN.md §2
+//           "lane packets"): each slot's pk consecutive rows of one component are contiguous —
+//           64-byte pieces, so a lane's path never shares a piece of memory with another lane's
+//           and per-lane MH decisions (each lane's u in its own buffer) cost no partial writes.
+__host__ __device__ __forceinline__ int64_t plane_ix(int64_t row, int c, int C, int tw, int slot,
+                                                      int pk) {
+  if (pk == 0) return (row * C + c) * tw + slot;
+  const int lg = __builtin_ctz((unsigned)pk);
+  return (((row >> lg) * C + c) * tw + slot) * pk + (row & (pk - 1));
+}
+// lane-packet length of the path planes of an fp32 MAP_LANE ensemble (16 points = 64 bytes)
+constexpr int kPathPacket = 16;
+
 // Thread mappings of the recursion (chosen per ensemble at dmt_create):
 //   MAP_LANE: one lane per (recording, block); tile width tw = 64 recordings
 //   MAP_WAVE: one wavefront per block, 64 consecutive steps per chunk; tw = 1
@@ -76,6 +93,7 @@ struct BlockArgs {
   T* X[3];                   // X[2], W[2]: the third path buffers (nullptr: two-buffer ensemble)
   T* W[3];
   int nbuf;                  // path buffers per container (2 or 3)
+  int pk;                    // path planes in lane packets of pk points (0: row layout; plane_ix)
   int full_copy;             // consolidation rewrites every lane's u (whole lines; DMT_FULL_COPY)
   const T* t;
   int t_shared;
@@ -267,7 +285,7 @@ hipError_t launch_mcmc_persistent(const ModelKey& k, const void* args, const Acc
                                   int resident, double* out3, unsigned* counter, hipStream_t s);
 hipError_t launch_backward_filter(int precision, const FilterArgs& a, hipStream_t s);
 hipError_t launch_set_prop_law(const ParamArgs& a, hipStream_t s);
-hipError_t launch_set_obs(int precision, int tw, int d, const void* X0, const void* X1,
+hipError_t launch_set_obs(int precision, int tw, int pk, int d, const void* X0, const void* X1,
                           const void* X2, const uint8_t* selX,
                           const int64_t* tile_qoff, const int32_t* seg_rec, const int32_t* seg_q,
                           const int32_t* seg_np, const int32_t* glast, const uint8_t* term,
@@ -277,18 +295,18 @@ hipError_t launch_to_planes(int precision, int tw, const double* src, void* dst0
                             const uint8_t* sel, int flip, int C, int64_t P, const int64_t* pt_off,
                             int64_t G, const int32_t* seg_rec, const int32_t* seg_q,
                             const int64_t* tile_qoff, hipStream_t s, int incr = 0,
-                            void* dst2 = nullptr, int enc = 0);
+                            void* dst2 = nullptr, int enc = 0, int pk = 0);
 hipError_t launch_from_planes_incr(int precision, int tw, double* dst, const void* src0,
                                    const void* src1, const uint8_t* sel, int flip, int C,
                                    int64_t G, const int64_t* pt_off, const int32_t* seg_np,
                                    const int32_t* seg_rec, const int32_t* seg_q,
                                    const int64_t* tile_qoff, hipStream_t s,
-                                   const void* src2 = nullptr, int enc = 0);
+                                   const void* src2 = nullptr, int enc = 0, int pk = 0);
 hipError_t launch_from_planes(int precision, int tw, double* dst, const void* src0,
                               const void* src1, const uint8_t* sel, int flip, int C, int64_t P,
                               const int64_t* pt_off, int64_t G, const int32_t* seg_rec,
                               const int32_t* seg_q, const int64_t* tile_qoff, hipStream_t s,
-                              const void* src2 = nullptr, int enc = 0);
+                              const void* src2 = nullptr, int enc = 0, int pk = 0);
 hipError_t launch_cast(int precision, const double* src, void* dst, int64_t n, hipStream_t s);
 hipError_t launch_cast_back(int precision, const void* src, double* dst, int64_t n, hipStream_t s);
 hipError_t launch_block_sum(const double* ll, const double* llp, const uint8_t* acc, int64_t n,

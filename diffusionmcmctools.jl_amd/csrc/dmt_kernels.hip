@@ -507,6 +507,329 @@ __global__ __launch_bounds__(64) void k_block(const BlockArgs<T> a) {
   lane_block<Mdl, T, MODE, PARITY, K, false, TD>(a, tile, blk, threadIdx.x, 0);
 }
 
+// ---- MAP_LANE with lane packets (fp32 ensembles, BlockArgs::pk = kPathPacket).
+// The path planes X, W hold each lane's PK consecutive points of a component as one 64-byte
+// piece (plane_ix), so the per-lane buffers of u and u° (two, selected per segment exactly as
+// the reference swaps its containers) never share a piece of memory: a wave whose lanes hold u
+// in different buffers reads and writes whole pieces of its own, with no partial lines, no
+// consolidation copies and no third buffer (the row layout's path_plan).  FAST (every active
+// lane's segment starts at point ≡ PK − 1 of a packet, which dmt_create arranges for the first
+// segment of every recording): per packet of PK steps the lane loads u.W's packet one packet
+// ahead (NV 16-byte pieces per component, back to back) and stores the packet's X°, W° whole at
+// its end; the remaining steps (and segments not so aligned) go point by point through
+// plane_ix.  The arithmetic, its order and the Girsanov summation tree (K-step subtrees from
+// the segment start, single steps for the last nst % K) are run_segment's, so the results are
+// bit-identical to the row layout's and to the oracle's.
+template <class Mdl, class T, int MODE, bool PARITY, int K, bool TD, int PK, bool FAST>
+__device__ __forceinline__ bool run_segment_pk(const Law<Mdl, T>& L, const T* __restrict__ tpl,
+                                               const int t_sh, const T* __restrict__ Ht,
+                                               const int H_sh, const T* __restrict__ Ft,
+                                               const T* __restrict__ At, const T* Ws, T* Wd,
+                                               T* Xd, const double* __restrict__ Zg,
+                                               NormalStream<T>& ns, const int64_t tq,
+                                               const int64_t q0, const int np, const int lane,
+                                               const T rho, const T srho, const int ll_skip,
+                                               T* x, T& sl) {
+  constexpr int D = Mdl::D, M = Mdl::M, HP = D * (D + 1) / 2;
+  constexpr bool DRAW = MODE != MODE_RECOMPUTE;
+  constexpr bool READW = MODE != MODE_FRESH;
+  constexpr int VE = 16 / (int)sizeof(T);  // elements per 16-byte piece
+  constexpr int NV = PK / VE;              // pieces per packet
+  static_assert(PK % K == 0 && (K * M) % 2 == 0 && 64 % K == 0, "packets of whole chunks");
+  typedef T v16 __attribute__((ext_vector_type(VE)));
+  const int64_t row = tq + q0;
+  const T* tb = t_sh ? tpl + q0 : tpl + row * kLanes + lane;
+  const int tst = t_sh ? 1 : kLanes;
+  const T* Hb = H_sh ? Ht + q0 * HP : Ht + row * HP * kLanes + lane;
+  const int hst = H_sh ? 1 : kLanes;
+  const T* Fb = Ft + row * D * kLanes + lane;
+  auto pix = [&](int64_t i, int c, int C) -> int64_t {  // point i of the segment, component c
+    return plane_ix(row + i, c, C, kLanes, lane, PK);
+  };
+  constexpr int CA = D * D + D;
+  const T* Ab = (TD && At) ? At + row * CA * kLanes + lane : nullptr;
+  const bool td = TD && Ab != nullptr && __ballot(L.auxtd) != 0;
+  const int nst = np - 1;
+#ifdef DMT_NO_UNIT_FAST
+  const bool all_unit = false;
+#else
+  const bool all_unit = !Mdl::kLinear && __ballot(L.unit) == __ballot(1);
+#endif
+  T tcur = tb[0];
+#pragma unroll
+  for (int p = 0; p < D; ++p) Xd[pix(0, p, D)] = x[p];
+  if (DRAW) {
+#pragma unroll
+    for (int k = 0; k < M; ++k) {
+      const T w0 = READW ? Ws[pix(0, k, M)] : (T)0;
+      Wd[pix(0, k, M)] = rho * w0;
+    }
+  }
+  PSum<T> ps;
+  ps.init();
+  // one Euler step from registers (run_segment's step): dW (in: u's increment, out: the
+  // proposal's), x advanced; returns the Girsanov term G·dt
+  auto step = [&](int i, T tn, const T* Hi, const T* Fi, T* dW, const T* Zi) -> T {
+    const T dt = tn - tcur;
+    if (DRAW) {
+      const T sdt = sqrt(dt);
+#pragma unroll
+      for (int k = 0; k < M; ++k) dW[k] = dfma(rho, dW[k], srho * (sdt * Zi[k]));
+    }
+    T r[D], b[D], sdW[D], Mg[D * D], cg[D];
+    T G;
+    if constexpr (TD) {
+      if (td) {
+        T Bq[D * D], bq[D];
+        aux_step<Mdl, T>(L, Ab + (int64_t)i * CA * kLanes, kLanes, Bq, bq,
+                         [](const T* p) { return lane_ld(p); });
+        G = g_at_aux<Mdl, T>(L, Hi, Fi, x, r, b, Bq, bq);
+      } else {
+        G = g_at<Mdl, T>(L, Hi, Fi, x, r, b);
+      }
+    } else {
+      G = g_at<Mdl, T>(L, Hi, Fi, x, r, b);
+    }
+    bool fast = false;
+    if constexpr (!Mdl::kLinear && D == M) {
+      if (all_unit) {
+#pragma unroll
+        for (int p = 0; p < D; ++p) sdW[p] = dW[p];
+        guide_coeffs_unit<Mdl, T>(Hi, Fi, Mg, cg);
+        fast = true;
+      }
+    }
+    if (!fast) {
+      sigma_dw<Mdl, T>(L, dW, sdW);
+      guide_coeffs<Mdl, T>(L, Hi, Fi, Mg, cg);
+    }
+    euler_step<Mdl, T>(Mg, cg, b, dt, sdW, x);
+    tcur = tn;
+    return (MODE == MODE_RECOMPUTE && i >= nst - ll_skip) ? (T)0 : G * dt;
+  };
+  struct Chunk {
+    T t[K], H[K][HP], F[K][D], Z[K][M];
+  };
+  auto load = [&](int c0, Chunk& c) {  // the chunk's grid, guiding term, caller normals
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const int64_t i = c0 + j;
+      c.t[j] = tb[(i + 1) * tst];
+#pragma unroll
+      for (int e = 0; e < HP; ++e) c.H[j][e] = lane_ld(&Hb[(i * HP + e) * hst]);
+#pragma unroll
+      for (int e = 0; e < D; ++e) c.F[j][e] = lane_ld(&Fb[(i * D + e) * kLanes]);
+#pragma unroll
+      for (int k = 0; k < M; ++k) c.Z[j][k] = (PARITY && DRAW) ? (T)Zg[i * M + k] : (T)0;
+    }
+  };
+  auto normals = [&](int c0, Chunk& c) {  // whole Philox blocks of the chunk, straight-line
+    if (DRAW && !PARITY) {
+      constexpr int NPB = NormPerBlock<T>::v;
+      static_assert((K * M) % NPB == 0, "chunk must hold whole normal blocks");
+#pragma unroll
+      for (int bq = 0; bq < K * M / NPB; ++bq) {
+        const uint32_t bc = (uint32_t)((c0 * M) / NPB + bq);
+        T zb[NPB];
+        normal_block(philox4x32_10(U4{bc, ns.seg, ns.iter, ns.c3}, ns.k0, ns.k1), zb);
+#pragma unroll
+        for (int e = 0; e < NPB; ++e) c.Z[(NPB * bq + e) / M][(NPB * bq + e) % M] = zb[e];
+      }
+    }
+  };
+  int i0 = 0;  // steps done by the packet loop
+  if constexpr (FAST) {
+    const int npk = nst / PK;
+    if (npk > 0) {
+      // packet j of a component: the segment's points j·PK + 1 … j·PK + PK, NV pieces
+      auto wpk = [&](int j, int k) -> const v16* { return (const v16*)&Ws[pix((int64_t)j * PK + 1, k, M)]; };
+      v16 wc[M][NV], wn[M][NV];
+      if (READW) {
+#pragma unroll
+        for (int k = 0; k < M; ++k)
+#pragma unroll
+          for (int v = 0; v < NV; ++v) wc[k][v] = wpk(0, k)[v];
+      }
+      Chunk cur, nxt;
+      load(0, cur);
+      for (int j = 0; j < npk; ++j) {
+        if (READW) {  // next packet (the tile's spare rows keep the last one in bounds)
+#pragma unroll
+          for (int k = 0; k < M; ++k)
+#pragma unroll
+            for (int v = 0; v < NV; ++v) wn[k][v] = wpk(j + 1, k)[v];
+        }
+        v16 ox[D][NV], ow[M][NV];
+#pragma unroll
+        for (int v = 0; v < PK / K; ++v) {
+          const int c0 = j * PK + v * K;
+          load(c0 + K, nxt);
+          normals(c0, cur);
+          T gv[K];
+#pragma unroll
+          for (int q = 0; q < K; ++q) {
+            const int e = v * K + q;  // element of the packet
+            T dW[M];
+#pragma unroll
+            for (int k = 0; k < M; ++k) dW[k] = READW ? wc[k][e / VE][e % VE] : (T)0;
+            gv[q] = step(c0 + q, cur.t[q], cur.H[q], cur.F[q], dW, cur.Z[q]);
+#pragma unroll
+            for (int p = 0; p < D; ++p) ox[p][e / VE][e % VE] = x[p];
+#pragma unroll
+            for (int k = 0; k < M; ++k) ow[k][e / VE][e % VE] = dW[k];
+          }
+          ps.template add_subtree<Log2<K>::v>(tree_sum<T, K>(gv));
+          cur = nxt;
+        }
+#pragma unroll
+        for (int p = 0; p < D; ++p) {
+          v16* dst = (v16*)&Xd[pix((int64_t)j * PK + 1, p, D)];
+#pragma unroll
+          for (int v = 0; v < NV; ++v) dst[v] = ox[p][v];
+        }
+        if (DRAW) {
+#pragma unroll
+          for (int k = 0; k < M; ++k) {
+            v16* dst = (v16*)&Wd[pix((int64_t)j * PK + 1, k, M)];
+#pragma unroll
+            for (int v = 0; v < NV; ++v) dst[v] = ow[k][v];
+          }
+        }
+        if (READW) {
+#pragma unroll
+          for (int k = 0; k < M; ++k)
+#pragma unroll
+            for (int v = 0; v < NV; ++v) wc[k][v] = wn[k][v];
+        }
+      }
+      i0 = npk * PK;
+    }
+  }
+  // the remaining whole chunks, point by point (FAST: < PK steps; else every chunk)
+  const int nfull = nst - nst % K;
+  if (i0 < nfull) {
+    Chunk cur, nxt;
+    load(i0, cur);
+    for (int c0 = i0; c0 < nfull; c0 += K) {
+      load(c0 + K, nxt);
+      T wu[K][M];
+#pragma unroll
+      for (int q = 0; q < K; ++q)
+#pragma unroll
+        for (int k = 0; k < M; ++k) wu[q][k] = READW ? Ws[pix(c0 + q + 1, k, M)] : (T)0;
+      normals(c0, cur);
+      T gv[K];
+#pragma unroll
+      for (int q = 0; q < K; ++q) {
+        gv[q] = step(c0 + q, cur.t[q], cur.H[q], cur.F[q], wu[q], cur.Z[q]);
+#pragma unroll
+        for (int p = 0; p < D; ++p) Xd[pix(c0 + q + 1, p, D)] = x[p];
+        if (DRAW) {
+#pragma unroll
+          for (int k = 0; k < M; ++k) Wd[pix(c0 + q + 1, k, M)] = wu[q][k];
+        }
+      }
+      ps.template add_subtree<Log2<K>::v>(tree_sum<T, K>(gv));
+      cur = nxt;
+    }
+  }
+  for (int i = nfull; i < nst; ++i) {  // tail (< K steps): single steps
+    const int64_t q = i;
+    T Hi[HP], Fi[D], dW[M], Zi[M];
+#pragma unroll
+    for (int e = 0; e < HP; ++e) Hi[e] = lane_ld(&Hb[(q * HP + e) * hst]);
+#pragma unroll
+    for (int e = 0; e < D; ++e) Fi[e] = lane_ld(&Fb[(q * D + e) * kLanes]);
+#pragma unroll
+    for (int k = 0; k < M; ++k) {
+      dW[k] = READW ? Ws[pix(q + 1, k, M)] : (T)0;
+      Zi[k] = DRAW ? (PARITY ? (T)Zg[q * M + k] : ns.get((uint32_t)(i * M + k))) : (T)0;
+    }
+    ps.add(step(i, tb[(q + 1) * tst], Hi, Fi, dW, Zi));
+#pragma unroll
+    for (int p = 0; p < D; ++p) Xd[pix(q + 1, p, D)] = x[p];
+    if (DRAW) {
+#pragma unroll
+      for (int k = 0; k < M; ++k) Wd[pix(q + 1, k, M)] = dW[k];
+    }
+  }
+  sl = ps.finish();
+  bool ok = isfinite(sl);
+#pragma unroll
+  for (int p = 0; p < D; ++p) ok = ok && isfinite(x[p]);
+  return ok;
+}
+
+template <class Mdl, class T, int MODE, bool PARITY, int K, bool TD>
+__device__ __forceinline__ void lane_block_pk(const BlockArgs<T>& a, const int64_t tile,
+                                              const int64_t blk, const int lane) {
+  constexpr int D = Mdl::D, HP = D * (D + 1) / 2, PK = kPathPacket;
+  const int64_t tq = a.tile_qoff[tile];
+  auto idx = [&](int64_t q, int c, int C) -> int64_t { return ((tq + q) * C + c) * kLanes + lane; };
+  const int g0 = a.gfirst[blk], g1 = a.glast[blk];
+  const bool term = a.term[blk] != 0;
+  T x[D];
+  {
+    const T* Xs = a.X[sel_buf(a.selX[g0], a.xs_flip)];
+    const int64_t q = a.seg_q[g0];
+#pragma unroll
+    for (int p = 0; p < D; ++p) x[p] = Xs[plane_ix(tq + q, p, D, kLanes, lane, PK)];
+  }
+  T ll;
+  {
+    const int ls = a.selPP[g0] ^ a.law_flip;
+    const double* Lr = a.law[ls][0] + (int64_t)g0 * DMT_LAW_STRIDE;
+    const T* Ht = a.H[ls][0];
+    const T* Ft = a.F[ls][0];
+    const int64_t q = a.seg_q[g0];
+    T H0[HP], F0[D];
+#pragma unroll
+    for (int c = 0; c < HP; ++c) H0[c] = a.H_shared[ls][0] ? Ht[q * HP + c] : Ht[idx(q, c, HP)];
+#pragma unroll
+    for (int c = 0; c < D; ++c) F0[c] = Ft[idx(q, c, D)];
+    ll = obs_term<D, T>(H0, F0, x, (T)Lr[DMT_LAW_C0]);
+  }
+  bool ok = true;
+  const T rho = (MODE == MODE_FRESH) ? (T)0 : (T)a.rho[blk];
+  const T srho = (MODE == MODE_FRESH) ? (T)1 : (T)a.srho[blk];
+  for (int g = g0; g <= g1; ++g) {
+    const int kind = (!term && g == g1) ? 1 : 0;
+    const int ls = (kind ? a.selPPB[g] : a.selPP[g]) ^ a.law_flip;
+    Law<Mdl, T> L;
+    L.load(a.law[ls][kind] + (int64_t)g * DMT_LAW_STRIDE);
+    NormalStream<T> ns;
+    ns.init(a.seed, (uint32_t)g + a.seg_base, a.iter, a.salt);
+    const double* Zg = a.Z ? a.Z + a.st_off[g] * Mdl::M : nullptr;
+    const int sx = a.selX[g], sw = a.selW[g];
+    T* Xd = a.X[sel_buf(sx, a.xd_flip)];
+    const T* Ws = a.W[sel_buf(sw, a.ws_flip)];
+    T* Wd = a.W[sel_buf(sw, a.wd_flip)];
+    const int64_t q0 = a.seg_q[g];
+    const bool aligned = __ballot(((tq + q0 + 1) & (PK - 1)) != 0) == 0;
+    T sl;
+    const bool sok =
+        aligned ? run_segment_pk<Mdl, T, MODE, PARITY, K, TD, PK, true>(
+                      L, a.t, a.t_shared, a.H[ls][kind], a.H_shared[ls][kind], a.F[ls][kind],
+                      a.aux[kind], Ws, Wd, Xd, Zg, ns, tq, q0, a.seg_np[g], lane, rho, srho,
+                      a.ll_skip, x, sl)
+                : run_segment_pk<Mdl, T, MODE, PARITY, K, TD, PK, false>(
+                      L, a.t, a.t_shared, a.H[ls][kind], a.H_shared[ls][kind], a.F[ls][kind],
+                      a.aux[kind], Ws, Wd, Xd, Zg, ns, tq, q0, a.seg_np[g], lane, rho, srho,
+                      a.ll_skip, x, sl);
+    if (!sok) { ok = false; break; }
+    ll = ll + sl;
+  }
+  a.ll_out[blk] = ok ? (double)ll : -INFINITY;
+  if (a.success) a.success[blk] = ok ? 1 : 0;
+}
+
+template <class Mdl, class T, int MODE, bool PARITY, int K, bool TD = false>
+__global__ __launch_bounds__(64) void k_block_pk(const BlockArgs<T> a) {
+  int64_t tile, blk;
+  if (!map_block(a, tile, blk)) return;
+  lane_block_pk<Mdl, T, MODE, PARITY, K, TD>(a, tile, blk, threadIdx.x);
+}
+
 // ---- MAP_LANE, pair mapping: two waves per (recording tile, block index), each
 // holding 32 recordings of the tile on lane pairs (l, l + 32).  The pair draws a chunk's normals
 // half each (pair_exchange) and runs the recursion redundantly, so an ensemble with fewer
@@ -806,6 +1129,8 @@ __global__ __launch_bounds__(64) void k_pathll(const BlockArgs<T> a) {
   const int lane = threadIdx.x;
   const int64_t tq = a.tile_qoff[tile];
   auto idx = [&](int64_t q, int c, int C) -> int64_t { return ((tq + q) * C + c) * kLanes + lane; };
+  // the path planes (X): row layout or lane packets (plane_ix)
+  auto pidx = [&](int64_t q, int c, int C) -> int64_t { return plane_ix(tq + q, c, C, kLanes, lane, a.pk); };
   auto tload = [&](int64_t q) -> T { return a.t_shared ? a.t[q] : a.t[idx(q, 0, 1)]; };
   const int g0 = a.gfirst[blk], g1 = a.glast[blk];
   const bool term = a.term[blk] != 0;
@@ -822,7 +1147,7 @@ __global__ __launch_bounds__(64) void k_pathll(const BlockArgs<T> a) {
 #pragma unroll
     for (int c = 0; c < D; ++c) F0[c] = a.F[ls][0][idx(q, c, D)];
 #pragma unroll
-    for (int c = 0; c < D; ++c) x0[c] = Xs[idx(q, c, D)];
+    for (int c = 0; c < D; ++c) x0[c] = Xs[pidx(q, c, D)];
     ll = obs_term<D, T>(H0, F0, x0, (T)Lr[DMT_LAW_C0]);
   }
   for (int g = g0; g <= g1; ++g) {
@@ -853,7 +1178,7 @@ __global__ __launch_bounds__(64) void k_pathll(const BlockArgs<T> a) {
 #pragma unroll
         for (int c = 0; c < HP; ++c) vH[j][c] = Hsh ? Ht[q * HP + c] : Ht[idx(q, c, HP)];
 #pragma unroll
-        for (int c = 0; c < D; ++c) { vF[j][c] = Ft[idx(q, c, D)]; vX[j][c] = Xs[idx(q, c, D)]; }
+        for (int c = 0; c < D; ++c) { vF[j][c] = Ft[idx(q, c, D)]; vX[j][c] = Xs[pidx(q, c, D)]; }
       }
 #pragma unroll
       for (int j = 0; j < K; ++j) {
@@ -3778,7 +4103,7 @@ __global__ __launch_bounds__(64) void k_set_prop_law(const ParamArgs a, int wg_p
 // linearised at an anchor (FHN y_T, Lorenz x_T) are re-anchored there and re-derived
 // (set_obs!).
 template <class T>
-__global__ void k_set_obs(int tw, int d, const T* X0, const T* X1, const T* X2,
+__global__ void k_set_obs(int tw, int pk, int d, const T* X0, const T* X1, const T* X2,
                           const uint8_t* selX,
                           const int64_t* tile_qoff, const int32_t* seg_rec, const int32_t* seg_q,
                           const int32_t* seg_np, const int32_t* glast, const uint8_t* term,
@@ -3793,7 +4118,7 @@ __global__ void k_set_obs(int tw, int d, const T* X0, const T* X1, const T* X2,
   const int64_t q = seg_q[g] + seg_np[g] - 1;
   double v[3] = {0.0, 0.0, 0.0};
   for (int p = 0; p < d; ++p) {
-    v[p] = (double)X[((tile_qoff[r / tw] + q) * d + p) * tw + r % tw];
+    v[p] = (double)X[plane_ix(tile_qoff[r / tw] + q, p, d, tw, (int)(r % tw), pk)];
     obsv[(int64_t)g * d + p] = v[p];
   }
   const int na = model == DMT_MODEL_FHN ? 1 : model == DMT_MODEL_LORENZ ? 3 : 0;
@@ -3867,7 +4192,7 @@ __global__ void k_to_planes(const int tw, const double* __restrict__ src, T* dst
                             int64_t P,
                             const int64_t* __restrict__ pt_off, int64_t G,
                             const int32_t* __restrict__ seg_rec, const int32_t* __restrict__ seg_q,
-                            const int64_t* __restrict__ tile_qoff, int incr) {
+                            const int64_t* __restrict__ tile_qoff, int incr, int pk) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= P * C) return;
   const int64_t p = e / C;
@@ -3875,7 +4200,7 @@ __global__ void k_to_planes(const int tw, const double* __restrict__ src, T* dst
   const int64_t g = find_seg(pt_off, G, p);
   const int64_t r = seg_rec[g];
   const int64_t q = seg_q[g] + (p - pt_off[g]);
-  const int64_t o = ((tile_qoff[r / tw] + q) * C + c) * tw + (r % tw);
+  const int64_t o = plane_ix(tile_qoff[r / tw] + q, c, C, tw, (int)(r % tw), pk);
   const int slot = plane_slot(sel, enc, g, flip);
   T v = (T)src[e];
   if (incr && p > pt_off[g]) v = v - (T)src[e - C];
@@ -3891,7 +4216,7 @@ __global__ void k_from_planes_incr(const int tw, double* __restrict__ dst, const
                                    const int32_t* __restrict__ seg_np,
                                    const int32_t* __restrict__ seg_rec,
                                    const int32_t* __restrict__ seg_q,
-                                   const int64_t* __restrict__ tile_qoff) {
+                                   const int64_t* __restrict__ tile_qoff, int pk) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= G * C) return;
   const int64_t g = e / C;
@@ -3901,7 +4226,7 @@ __global__ void k_from_planes_incr(const int tw, double* __restrict__ dst, const
   const T* src = slot == 0 ? src0 : slot == 1 ? src1 : src2;
   T acc = (T)0;
   for (int i = 0; i < seg_np[g]; ++i) {
-    const int64_t o = ((tile_qoff[r / tw] + seg_q[g] + i) * C + c) * tw + (r % tw);
+    const int64_t o = plane_ix(tile_qoff[r / tw] + seg_q[g] + i, c, C, tw, (int)(r % tw), pk);
     acc = i == 0 ? src[o] : acc + src[o];
     dst[(pt_off[g] + i) * C + c] = (double)acc;
   }
@@ -3914,7 +4239,7 @@ __global__ void k_from_planes(const int tw, double* __restrict__ dst, const T* s
                               const int64_t* __restrict__ pt_off, int64_t G,
                               const int32_t* __restrict__ seg_rec,
                               const int32_t* __restrict__ seg_q,
-                              const int64_t* __restrict__ tile_qoff) {
+                              const int64_t* __restrict__ tile_qoff, int pk) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= P * C) return;
   const int64_t p = e / C;
@@ -3922,7 +4247,7 @@ __global__ void k_from_planes(const int tw, double* __restrict__ dst, const T* s
   const int64_t g = find_seg(pt_off, G, p);
   const int64_t r = seg_rec[g];
   const int64_t q = seg_q[g] + (p - pt_off[g]);
-  const int64_t o = ((tile_qoff[r / tw] + q) * C + c) * tw + (r % tw);
+  const int64_t o = plane_ix(tile_qoff[r / tw] + q, c, C, tw, (int)(r % tw), pk);
   const int slot = plane_slot(sel, enc, g, flip);
   dst[e] = (double)(slot == 0 ? src0 : slot == 1 ? src1 : src2)[o];
 }
@@ -4066,6 +4391,39 @@ static hipError_t launch_block_t(int mapping, int mode, const void* args, int64_
     }
     const dim3 block(64);
     const bool par = a.Z != nullptr;
+    if (a.pk) {  // lane packets (fp32 ensembles): k_block_pk, every mode (no pair / split forms)
+      if constexpr (sizeof(T) == 4) {
+        const bool td = a.aux[0] || a.aux[1];
+        switch (mode) {
+          case MODE_PCN:
+            if (td) {
+              if (par) dlaunch(k_block_pk<Mdl, T, MODE_PCN, true, kChunk, true>, grid, block, s, a);
+              else dlaunch(k_block_pk<Mdl, T, MODE_PCN, false, kChunk, true>, grid, block, s, a);
+            } else {
+              if (par) dlaunch(k_block_pk<Mdl, T, MODE_PCN, true, kChunk>, grid, block, s, a);
+              else dlaunch(k_block_pk<Mdl, T, MODE_PCN, false, kChunk>, grid, block, s, a);
+            }
+            break;
+          case MODE_RECOMPUTE:
+            if (td) dlaunch(k_block_pk<Mdl, T, MODE_RECOMPUTE, false, kChunk, true>, grid, block, s, a);
+            else dlaunch(k_block_pk<Mdl, T, MODE_RECOMPUTE, false, kChunk>, grid, block, s, a);
+            break;
+          case MODE_FRESH:
+            if (td) {
+              if (par) dlaunch(k_block_pk<Mdl, T, MODE_FRESH, true, kChunk, true>, grid, block, s, a);
+              else dlaunch(k_block_pk<Mdl, T, MODE_FRESH, false, kChunk, true>, grid, block, s, a);
+            } else {
+              if (par) dlaunch(k_block_pk<Mdl, T, MODE_FRESH, true, kChunk>, grid, block, s, a);
+              else dlaunch(k_block_pk<Mdl, T, MODE_FRESH, false, kChunk>, grid, block, s, a);
+            }
+            break;
+          default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+      } else {
+        return hipErrorInvalidValue;  // lane packets are an fp32 layout (dmt_create)
+      }
+    }
     if (a.aux[0] || a.aux[1]) {  // time-dependent auxiliary laws: the TD instantiation
       switch (mode) {
         case MODE_PCN:
@@ -4118,6 +4476,7 @@ __global__ __launch_bounds__(64) void k_invsolve(const BlockArgs<T> a) {
   const int lane = threadIdx.x;
   const int64_t tq = a.tile_qoff[tile];
   auto idx = [&](int64_t q, int c, int C) -> int64_t { return ((tq + q) * C + c) * kLanes + lane; };
+  auto pidx = [&](int64_t q, int c, int C) -> int64_t { return plane_ix(tq + q, c, C, kLanes, lane, a.pk); };
   auto tload = [&](int64_t q) -> T { return a.t_shared ? a.t[q] : a.t[idx(q, 0, 1)]; };
   const int g0 = a.gfirst[blk], g1 = a.glast[blk];
   const bool term = a.term[blk] != 0;
@@ -4138,10 +4497,10 @@ __global__ __launch_bounds__(64) void k_invsolve(const BlockArgs<T> a) {
     const int64_t q0 = a.seg_q[g];
     const int nst = a.seg_np[g] - 1;
 #pragma unroll
-    for (int k = 0; k < M; ++k) Wd[idx(q0, k, M)] = (T)0;  // W(t0) = 0
+    for (int k = 0; k < M; ++k) Wd[pidx(q0, k, M)] = (T)0;  // W(t0) = 0
     T x[D];
 #pragma unroll
-    for (int c = 0; c < D; ++c) x[c] = Xs[idx(q0, c, D)];
+    for (int c = 0; c < D; ++c) x[c] = Xs[pidx(q0, c, D)];
     T tcur = tload(q0);
     for (int i = 0; i < nst; ++i) {
       const int64_t q = q0 + i;
@@ -4149,11 +4508,11 @@ __global__ __launch_bounds__(64) void k_invsolve(const BlockArgs<T> a) {
 #pragma unroll
       for (int c = 0; c < HP; ++c) Hi[c] = Hsh ? Ht[q * HP + c] : Ht[idx(q, c, HP)];
 #pragma unroll
-      for (int c = 0; c < D; ++c) { Fi[c] = Ft[idx(q, c, D)]; xn[c] = Xs[idx(q + 1, c, D)]; }
+      for (int c = 0; c < D; ++c) { Fi[c] = Ft[idx(q, c, D)]; xn[c] = Xs[pidx(q + 1, c, D)]; }
       const T tn = tload(q + 1);
       inv_step<Mdl, T>(L, siginv, Hi, Fi, tn - tcur, x, xn, dW);
 #pragma unroll
-      for (int k = 0; k < M; ++k) Wd[idx(q + 1, k, M)] = dW[k];
+      for (int k = 0; k < M; ++k) Wd[pidx(q + 1, k, M)] = dW[k];
 #pragma unroll
       for (int c = 0; c < D; ++c) x[c] = xn[c];
       tcur = tn;
@@ -4426,7 +4785,7 @@ hipError_t launch_set_prop_law(const ParamArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_set_obs(int precision, int tw, int d, const void* X0, const void* X1,
+hipError_t launch_set_obs(int precision, int tw, int pk, int d, const void* X0, const void* X1,
                           const void* X2, const uint8_t* selX, const int64_t* tile_qoff, const int32_t* seg_rec,
                           const int32_t* seg_q, const int32_t* seg_np, const int32_t* glast,
                           const uint8_t* term, int64_t b0, int64_t b1, double* obsv,
@@ -4434,11 +4793,11 @@ hipError_t launch_set_obs(int precision, int tw, int d, const void* X0, const vo
   const int64_t n = b1 - b0;
   if (n <= 0) return hipSuccess;
   if (precision == DMT_F64)
-    k_set_obs<double><<<nblk(n, 256), 256, 0, s>>>(tw, d, (const double*)X0, (const double*)X1,
+    k_set_obs<double><<<nblk(n, 256), 256, 0, s>>>(tw, pk, d, (const double*)X0, (const double*)X1,
                                                    (const double*)X2, selX, tile_qoff, seg_rec, seg_q, seg_np, glast,
                                                    term, b0, b1, obsv, model, lawb0, lawb1);
   else
-    k_set_obs<float><<<nblk(n, 256), 256, 0, s>>>(tw, d, (const float*)X0, (const float*)X1,
+    k_set_obs<float><<<nblk(n, 256), 256, 0, s>>>(tw, pk, d, (const float*)X0, (const float*)X1,
                                                   (const float*)X2, selX,
                                                   tile_qoff, seg_rec, seg_q, seg_np, glast, term,
                                                   b0, b1, obsv, model, lawb0, lawb1);
@@ -4456,17 +4815,17 @@ hipError_t launch_to_planes(int precision, int tw, const double* src, void* dst0
                             const uint8_t* sel, int flip, int C, int64_t P, const int64_t* pt_off,
                             int64_t G, const int32_t* seg_rec, const int32_t* seg_q,
                             const int64_t* tile_qoff, hipStream_t s, int incr, void* dst2,
-                            int enc) {
+                            int enc, int pk) {
   const int64_t n = P * C;
   if (n <= 0) return hipSuccess;
   if (precision == DMT_F64)
     k_to_planes<double><<<nblk(n, 256), 256, 0, s>>>(tw, src, (double*)dst0, (double*)dst1,
                                                       (double*)dst2, sel, enc, flip, C, P, pt_off,
-                                                      G, seg_rec, seg_q, tile_qoff, incr);
+                                                      G, seg_rec, seg_q, tile_qoff, incr, pk);
   else
     k_to_planes<float><<<nblk(n, 256), 256, 0, s>>>(tw, src, (float*)dst0, (float*)dst1,
                                                      (float*)dst2, sel, enc, flip, C, P, pt_off, G,
-                                                     seg_rec, seg_q, tile_qoff, incr);
+                                                     seg_rec, seg_q, tile_qoff, incr, pk);
   return hipGetLastError();
 }
 
@@ -4475,19 +4834,19 @@ hipError_t launch_from_planes_incr(int precision, int tw, double* dst, const voi
                                    int64_t G, const int64_t* pt_off, const int32_t* seg_np,
                                    const int32_t* seg_rec, const int32_t* seg_q,
                                    const int64_t* tile_qoff, hipStream_t s, const void* src2,
-                                   int enc) {
+                                   int enc, int pk) {
   const int64_t n = G * C;
   if (n <= 0) return hipSuccess;
   if (precision == DMT_F64)
     k_from_planes_incr<double><<<nblk(n, 64), 64, 0, s>>>(tw, dst, (const double*)src0,
                                                           (const double*)src1, (const double*)src2,
                                                           sel, enc, flip, C, G,
-                                                          pt_off, seg_np, seg_rec, seg_q, tile_qoff);
+                                                          pt_off, seg_np, seg_rec, seg_q, tile_qoff, pk);
   else
     k_from_planes_incr<float><<<nblk(n, 64), 64, 0, s>>>(tw, dst, (const float*)src0,
                                                          (const float*)src1, (const float*)src2,
                                                          sel, enc, flip, C, G,
-                                                         pt_off, seg_np, seg_rec, seg_q, tile_qoff);
+                                                         pt_off, seg_np, seg_rec, seg_q, tile_qoff, pk);
   return hipGetLastError();
 }
 
@@ -4495,19 +4854,19 @@ hipError_t launch_from_planes(int precision, int tw, double* dst, const void* sr
                               const uint8_t* sel, int flip, int C, int64_t P,
                               const int64_t* pt_off, int64_t G, const int32_t* seg_rec,
                               const int32_t* seg_q, const int64_t* tile_qoff, hipStream_t s,
-                              const void* src2, int enc) {
+                              const void* src2, int enc, int pk) {
   const int64_t n = P * C;
   if (n <= 0) return hipSuccess;
   if (precision == DMT_F64)
     k_from_planes<double><<<nblk(n, 256), 256, 0, s>>>(tw, dst, (const double*)src0,
                                                         (const double*)src1, (const double*)src2,
                                                         sel, enc, flip, C, P,
-                                                        pt_off, G, seg_rec, seg_q, tile_qoff);
+                                                        pt_off, G, seg_rec, seg_q, tile_qoff, pk);
   else
     k_from_planes<float><<<nblk(n, 256), 256, 0, s>>>(tw, dst, (const float*)src0, (const float*)src1,
                                                        (const float*)src2, sel, enc, flip, C, P,
                                                        pt_off, G, seg_rec, seg_q,
-                                                       tile_qoff);
+                                                       tile_qoff, pk);
   return hipGetLastError();
 }
 

@@ -175,6 +175,7 @@ struct dmt_ens {
   void* d_W[3] = {nullptr, nullptr, nullptr};
   int full_copy = 0;  // DMT_FULL_COPY
   int nbuf = 2;  // path buffers per container (DESIGN.md §2 "path buffers"; DMT_PATH_BUFS)
+  int pk = 0;    // path planes in lane packets of pk points (fp32 MAP_LANE; DMT_PATH_PACKETS)
   void* d_t = nullptr;
   bool have_t = false;
   void* d_H[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};  // [slot][kind]
@@ -474,6 +475,7 @@ void fill_common(dmt_ens* h, const Layout* L, BlockArgs<T>& a) {
   a.selPP = h->d_sel[2];
   a.selPPB = h->d_sel[3];
   a.nbuf = h->nbuf;
+  a.pk = h->pk;
   a.full_copy = h->full_copy;
   for (int s = 0; s < 3; ++s) {
     a.X[s] = (T*)h->d_X[s];
@@ -547,8 +549,8 @@ dmt_status run_block_kernel(dmt_ens* h, const Layout* L, int mode, int kind_time
     // lane pairs (k_block_pair): on request only — bit-identical, but measured no faster on C5
     // (1 862 / 1 925 vs 1 829 µs per draw) and slower on C3 (1 821 vs 1 301 µs):
     // profiles/r03d, DESIGN.md §6
-    a.lane_pair = h->lane_pair == 1;
-    a.lane_split = !a.lane_pair && L->single_seg &&
+    a.lane_pair = h->lane_pair == 1 && !h->pk;
+    a.lane_split = !a.lane_pair && !h->pk && L->single_seg &&
                    (h->lane_split == 1 || (h->lane_split < 0 && nwaves < h->n_simd &&
                                            h->key.precision == DMT_F64));
   };
@@ -954,12 +956,26 @@ dmt_status dmt_create(dmt_ens** out, const dmt_model* model, const dmt_structure
     h->n_simd = 4 * (int64_t)prop.multiProcessorCount;
   }
   h->tw = h->mapping == MAP_WAVE ? 1 : kLanes;
+  // lane packets: the path planes of an fp32 lane-mapped ensemble (non-linear
+  // drift; OU ensembles are wave-mapped) in 16-point pieces per lane; DMT_PATH_PACKETS=0: rows
+  h->pk = (h->mapping == MAP_LANE && model->precision == DMT_F32) ? kPathPacket : 0;
+  if (const char* e = std::getenv("DMT_PATH_PACKETS")) h->pk = std::atoi(e) == 0 ? 0 : h->pk;
   h->ntiles = (h->R + h->tw - 1) / h->tw;
   h->tile_qoff.assign(h->ntiles + 1, 0);
-  for (int64_t t = 0; t < h->ntiles; ++t) {
-    int64_t mx = 0;
-    for (int64_t r = t * h->tw; r < std::min<int64_t>(h->R, (t + 1) * h->tw); ++r) mx = std::max(mx, recQ[r]);
-    h->tile_qoff[t + 1] = h->tile_qoff[t] + mx + kPadPoints;
+  {
+    // with packets every tile starts at row ≡ pk − 1 (mod pk): a recording's first segment then
+    // starts one point before a packet boundary, so its steps' points fill whole packets
+    // (run_segment_pk's fast path); the planes end on a packet boundary
+    const int64_t pk = h->pk;
+    auto up = [&](int64_t v) { return pk ? (v + pk - 1) / pk * pk : v; };
+    int64_t end = 0;
+    for (int64_t t = 0; t < h->ntiles; ++t) {
+      int64_t mx = 0;
+      for (int64_t r = t * h->tw; r < std::min<int64_t>(h->R, (t + 1) * h->tw); ++r) mx = std::max(mx, recQ[r]);
+      h->tile_qoff[t] = pk ? up(end) + pk - 1 : end;
+      end = h->tile_qoff[t] + mx + kPadPoints;
+    }
+    h->tile_qoff[h->ntiles] = up(end);
   }
   h->Ptile = h->tile_qoff[h->ntiles];
   HIP_OK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
@@ -986,6 +1002,7 @@ dmt_status dmt_create(dmt_ens** out, const dmt_model* model, const dmt_structure
   // none of its lanes' u occupies (DESIGN.md §2 "path buffers"; DMT_PATH_BUFS=2: two)
   hp->nbuf = hp->mapping == MAP_LANE ? 3 : 2;
   if (const char* e = std::getenv("DMT_PATH_BUFS")) hp->nbuf = std::atoi(e) == 2 ? 2 : hp->nbuf;
+  if (hp->pk) hp->nbuf = 2;  // lane packets: per-lane buffers cost nothing
   if (const char* e = std::getenv("DMT_FULL_COPY")) hp->full_copy = std::atoi(e) != 0;
   for (int s = 0; s < hp->nbuf; ++s) {
     DMT_TRY(ens_alloc_bytes(hp, &hp->d_X[s], plane_elems(hp, hp->d) * hp->esz));
@@ -1250,7 +1267,7 @@ dmt_status dmt_set_paths(dmt_ens* h, int32_t unit, const double* X, const double
     // Wiener paths are held as increments on the device
     HIP_OK(launch_to_planes(h->key.precision, h->tw, h->d_stage, dst[0], dst[1], h->d_sel[w], unit, C[w],
                             h->P, h->d_pt_off, h->G, h->d_seg_rec, h->d_seg_q, h->d_tile_qoff,
-                            h->stream, w == 1 ? 1 : 0, dst[2], 1));
+                            h->stream, w == 1 ? 1 : 0, dst[2], 1, h->pk));
   }
   HIP_OK(stream_wait(h));
   return DMT_OK;
@@ -1267,11 +1284,11 @@ dmt_status dmt_download_paths(dmt_ens* h, int32_t unit, int32_t what, double* ou
   if (what != 1)  // XX, or the Wiener increments exactly as held (DMT_PATH_DW)
     HIP_OK(launch_from_planes(h->key.precision, h->tw, h->d_stage, src[0], src[1], h->d_sel[sk], unit,
                               C, h->P, h->d_pt_off, h->G, h->d_seg_rec, h->d_seg_q, h->d_tile_qoff,
-                              h->stream, src[2], 1));
+                              h->stream, src[2], 1, h->pk));
   else  // increments -> cumulative Wiener path
     HIP_OK(launch_from_planes_incr(h->key.precision, h->tw, h->d_stage, src[0], src[1], h->d_sel[what],
                                    unit, C, h->G, h->d_pt_off, h->d_seg_np, h->d_seg_rec, h->d_seg_q,
-                                   h->d_tile_qoff, h->stream, src[2], 1));
+                                   h->d_tile_qoff, h->stream, src[2], 1, h->pk));
   HIP_OK(hipMemcpyAsync(out, h->d_stage, h->P * C * 8, hipMemcpyDeviceToHost, h->stream));
   HIP_OK(stream_wait(h));
   return DMT_OK;
@@ -2039,7 +2056,7 @@ dmt_status dmt_set_obs(dmt_ens* h, int32_t layout, int64_t b0, int64_t b1) {
   Layout* L;
   DMT_TRY(get_layout(h, layout, &L));
   DMT_TRY(check_range(L, b0, b1));
-  HIP_OK(launch_set_obs(h->key.precision, h->tw, h->d, h->d_X[0], h->d_X[1], h->d_X[2], h->d_sel[0],
+  HIP_OK(launch_set_obs(h->key.precision, h->tw, h->pk, h->d, h->d_X[0], h->d_X[1], h->d_X[2], h->d_sel[0],
                         h->d_tile_qoff, h->d_seg_rec, h->d_seg_q, h->d_seg_np, L->d_glast,
                         L->d_term, b0, b1, h->d_obsv, h->key.model, h->d_law[0][1],
                         h->d_law[1][1], h->stream));
@@ -2721,11 +2738,11 @@ dmt_status dmt_snapshot_take(dmt_ens* h, int32_t unit, int64_t slot, int64_t mcm
     if (k == 0)
       HIP_OK(launch_from_planes(h->key.precision, h->tw, dst, src[0], src[1], h->d_sel[0], unit, C,
                                 h->P, h->d_pt_off, h->G, h->d_seg_rec, h->d_seg_q, h->d_tile_qoff,
-                                h->stream, src[2], 1));
+                                h->stream, src[2], 1, h->pk));
     else  // increments -> cumulative Wiener path, as dmt_download_paths
       HIP_OK(launch_from_planes_incr(h->key.precision, h->tw, dst, src[0], src[1], h->d_sel[1], unit,
                                      C, h->G, h->d_pt_off, h->d_seg_np, h->d_seg_rec, h->d_seg_q,
-                                     h->d_tile_qoff, h->stream, src[2], 1));
+                                     h->d_tile_qoff, h->stream, src[2], 1, h->pk));
   }
   h->snap_iter[slot] = mcmciter;
   h->snap_unit[slot] = unit;
