@@ -520,6 +520,9 @@ __global__ __launch_bounds__(64) void k_block(const BlockArgs<T> a) {
 // plane_ix.  The arithmetic, its order and the Girsanov summation tree (K-step subtrees from
 // the segment start, single steps for the last nst % K) are run_segment's, so the results are
 // bit-identical to the row layout's and to the oracle's.
+#ifndef DMT_PK_ROLL  // 1: u.W's next packet loaded piece by piece into the registers just consumed
+#define DMT_PK_ROLL 1   // 0: the whole next packet in a second register set
+#endif
 template <class Mdl, class T, int MODE, bool PARITY, int K, bool TD, int PK, bool FAST>
 __device__ __forceinline__ bool run_segment_pk(const Law<Mdl, T>& L, const T* __restrict__ tpl,
                                                const int t_sh, const T* __restrict__ Ht,
@@ -535,7 +538,8 @@ __device__ __forceinline__ bool run_segment_pk(const Law<Mdl, T>& L, const T* __
   constexpr bool READW = MODE != MODE_FRESH;
   constexpr int VE = 16 / (int)sizeof(T);  // elements per 16-byte piece
   constexpr int NV = PK / VE;              // pieces per packet
-  static_assert(PK % K == 0 && (K * M) % 2 == 0 && 64 % K == 0, "packets of whole chunks");
+  static_assert(PK % K == 0 && K % VE == 0 && (K * M) % 2 == 0 && 64 % K == 0,
+                "packets of whole chunks, chunks of whole 16-byte pieces");
   typedef T v16 __attribute__((ext_vector_type(VE)));
   const int64_t row = tq + q0;
   const T* tb = t_sh ? tpl + q0 : tpl + row * kLanes + lane;
@@ -643,7 +647,10 @@ __device__ __forceinline__ bool run_segment_pk(const Law<Mdl, T>& L, const T* __
     if (npk > 0) {
       // packet j of a component: the segment's points j·PK + 1 … j·PK + PK, NV pieces
       auto wpk = [&](int j, int k) -> const v16* { return (const v16*)&Ws[pix((int64_t)j * PK + 1, k, M)]; };
-      v16 wc[M][NV], wn[M][NV];
+      v16 wc[M][NV];
+#if !DMT_PK_ROLL
+      v16 wn[M][NV];
+#endif
       if (READW) {
 #pragma unroll
         for (int k = 0; k < M; ++k)
@@ -653,12 +660,14 @@ __device__ __forceinline__ bool run_segment_pk(const Law<Mdl, T>& L, const T* __
       Chunk cur, nxt;
       load(0, cur);
       for (int j = 0; j < npk; ++j) {
+#if !DMT_PK_ROLL
         if (READW) {  // next packet (the tile's spare rows keep the last one in bounds)
 #pragma unroll
           for (int k = 0; k < M; ++k)
 #pragma unroll
             for (int v = 0; v < NV; ++v) wn[k][v] = wpk(j + 1, k)[v];
         }
+#endif
         v16 ox[D][NV], ow[M][NV];
 #pragma unroll
         for (int v = 0; v < PK / K; ++v) {
@@ -678,6 +687,17 @@ __device__ __forceinline__ bool run_segment_pk(const Law<Mdl, T>& L, const T* __
 #pragma unroll
             for (int k = 0; k < M; ++k) ow[k][e / VE][e % VE] = dW[k];
           }
+#if DMT_PK_ROLL
+          // the piece of u.W this chunk consumed is refilled with the next packet's: a prefetch
+          // distance of one packet in the registers of one (the tile's spare rows keep the
+          // last packet's in bounds)
+          if (READW) {
+#pragma unroll
+            for (int k = 0; k < M; ++k)
+#pragma unroll
+              for (int pc = v * K / VE; pc < (v + 1) * K / VE; ++pc) wc[k][pc] = wpk(j + 1, k)[pc];
+          }
+#endif
           ps.template add_subtree<Log2<K>::v>(tree_sum<T, K>(gv));
           cur = nxt;
         }
@@ -695,12 +715,14 @@ __device__ __forceinline__ bool run_segment_pk(const Law<Mdl, T>& L, const T* __
             for (int v = 0; v < NV; ++v) dst[v] = ow[k][v];
           }
         }
+#if !DMT_PK_ROLL
         if (READW) {
 #pragma unroll
           for (int k = 0; k < M; ++k)
 #pragma unroll
             for (int v = 0; v < NV; ++v) wc[k][v] = wn[k][v];
         }
+#endif
       }
       i0 = npk * PK;
     }
