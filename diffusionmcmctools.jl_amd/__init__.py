@@ -12,7 +12,7 @@ contains a dot).
 """
 from . import _lib  # noqa: F401  (raises ImportError if libdmt.so is missing)
 from ._lib import DMTError, version  # noqa: F401
-from .engine import Ensemble, comm_unique_id, combine_rank_partials, guiding_linear, guiding_linear_td, read_snapshots  # noqa: F401
+from .engine import Ensemble, comm_unique_id, combine_rank_partials, guiding_linear, guiding_linear_td, guiding_linear_tda, read_snapshots  # noqa: F401
 from .api import (BiBlock, Block, BlockCollection, BlockEnsemble,  # noqa: F401
                   SamplingEnsemble, SamplingPair, SamplingUnit)
 from .functions import *  # noqa: F401,F403  (the reference's generic functions)
@@ -20,7 +20,7 @@ from .functions import __all__ as _fn_all
 from .param_names import (AllObservations, ParamNamesAllObs, ParamNamesBlock,  # noqa: F401
                           ParamNamesRecording, ParamNamesUnit)
 
-__all__ = ["Ensemble", "DMTError", "version", "comm_unique_id", "combine_rank_partials", "guiding_linear", "guiding_linear_td", "read_snapshots",
+__all__ = ["Ensemble", "DMTError", "version", "comm_unique_id", "combine_rank_partials", "guiding_linear", "guiding_linear_td", "guiding_linear_tda", "read_snapshots",
            "SamplingEnsemble", "SamplingPair", "SamplingUnit", "BlockEnsemble",
            "BlockCollection", "BiBlock", "Block", "AllObservations", "ParamNamesUnit",
            "ParamNamesBlock", "ParamNamesRecording", "ParamNamesAllObs"] + list(_fn_all)

@@ -54,7 +54,8 @@ SYMBOLS = [
     "dmt_fetch_ll_local", "dmt_comm_size", "dmt_rng_counter", "dmt_set_rng_counter",
     "dmt_set_run_snapshots", "dmt_mcmc_step_local", "dmt_mcmc_run_local", "dmt_draw_success",
     "dmt_rng_state", "dmt_set_rng_state", "dmt_combine_rank_partials",
-    "dmt_set_service", "dmt_service_stats", "dmt_set_proposal_law_cc",
+    "dmt_set_service", "dmt_service_stats", "dmt_set_proposal_law_cc", "dmt_upload_aux_a",
+    "dmt_guiding_linear_tda",
 ]
 
 
@@ -123,6 +124,8 @@ _SIGS = {
     "dmt_guiding_linear": [_i32, _pd, _pd, _pd, _i32, _pd, _pd, _pd, C.c_double, _pd, _pd, _pd],
     "dmt_guiding_linear_td": [_i32, _pd, _pd, _i32, _pd, _pd, _pd, C.c_double, _pd, _pd, _pd],
     "dmt_upload_aux": [_P, _i32, _pd],
+    "dmt_upload_aux_a": [_P, _i32, _pd, _i32],
+    "dmt_guiding_linear_tda": [_i32, _pd, _i32, _pd, _pd, _pd, C.c_double, _pd, _pd, _pd],
     "dmt_comm_unique_id": [_pu8],
     "dmt_comm_init": [_P, _i32, _i32, _pu8],
     "dmt_mcmc_run": [_P, _i32, _i64, _i64, _i64, _i64, _u32, _pd],

@@ -92,6 +92,7 @@ struct Law {
   T thmu[D];  // Theta·mu of a linear (OU) drift, canonical order
   bool trace;
   bool auxtd;  // DMT_LAW_AUXTD: B̃, β̃ per step from the per-point table (dmt_upload_aux)
+  bool auxa;   // DMT_LAW_AUXTD = 2: ã = σ̃σ̃ᵀ per step from the table too (dmt_upload_aux_a)
   // non-linear drift with σ exactly the identity (d = m; C5's Lorenz): canonical M = H, c = F,
   // σ·dW = dW, which the lane kernels take as a wave-uniform fast path
   bool unit;
@@ -112,6 +113,7 @@ struct Law {
     for (int i = 0; i < HP; ++i) da[i] = (T)ldc(L + DMT_LAW_DA + i);
     trace = ldc(L + DMT_LAW_TRACE) != 0.0;
     auxtd = !Mdl::kLinear && ldc(L + DMT_LAW_AUXTD) != 0.0;
+    auxa = !Mdl::kLinear && ldc(L + DMT_LAW_AUXTD) == 2.0;
     unit = !Mdl::kLinear && D == M;
 #pragma unroll
     for (int p = 0; p < D; ++p)
@@ -170,11 +172,13 @@ __device__ __forceinline__ void guide_coeffs_unit(const T* H, const T* F, T* Mg,
   }
 }
 
-// G(t_i, x_i) of the Girsanov weight with the auxiliary drift B̃x + β̃ given (a time-dependent
-// auxiliary law: step i's B̃(t_i), β̃(t_i)); returns G, writes r = F - Hx and the drift b.
+// G(t_i, x_i) of the Girsanov weight with the auxiliary drift B̃x + β̃ and the trace weights
+// a − ã given (a time-dependent auxiliary law: step i's B̃(t_i), β̃(t_i), a − ã(t_i)); trace: the
+// −½ tr((a − ã)(H − rrᵀ)) term is taken; returns G, writes r = F - Hx and the drift b.
 template <class Mdl, class T>
 __device__ __forceinline__ T g_at_aux(const Law<Mdl, T>& L, const T* H, const T* F, const T* x,
-                                      T* r, T* b, const T* Bt, const T* beta) {
+                                      T* r, T* b, const T* Bt, const T* beta, const T* da,
+                                      bool trace) {
   constexpr int D = Mdl::D;
 #pragma unroll
   for (int p = 0; p < D; ++p) {
@@ -195,14 +199,14 @@ __device__ __forceinline__ T g_at_aux(const Law<Mdl, T>& L, const T* H, const T*
   T G = db[0] * r[0];
 #pragma unroll
   for (int p = 1; p < D; ++p) G = dfma(db[p], r[p], G);
-  if (L.trace) {
+  if (trace) {
     T tr = (T)0;
 #pragma unroll
     for (int p = 0; p < D; ++p)
 #pragma unroll
       for (int q = 0; q < D; ++q) {
         T tmp = dfma(-r[p], r[q], H[packed_idx(D, p, q)]);
-        T w = L.da[packed_idx(D, p, q)];
+        T w = da[packed_idx(D, p, q)];
         tr = (p == 0 && q == 0) ? (w * tmp) : dfma(w, tmp, tr);
       }
     G = dfma((T)-0.5, tr, G);
@@ -213,14 +217,19 @@ __device__ __forceinline__ T g_at_aux(const Law<Mdl, T>& L, const T* H, const T*
 template <class Mdl, class T>
 __device__ __forceinline__ T g_at(const Law<Mdl, T>& L, const T* H, const T* F, const T* x, T* r,
                                   T* b) {
-  return g_at_aux<Mdl, T>(L, H, F, x, r, b, L.Bt, L.beta);
+  return g_at_aux<Mdl, T>(L, H, F, x, r, b, L.Bt, L.beta, L.da, L.trace);
 }
-// The auxiliary drift of one step: the law's B̃, β̃, or — where the lane's law is time-dependent
-// (DMT_LAW_AUXTD) — the step's row of the per-point table, component c at row[c * cstride]
+// Columns of a per-point auxiliary-law table (dmt_upload_aux): B̃ (d·d), β̃ (d), ã packed (hp)
+template <int D>
+constexpr int kAuxCols = D * D + D + D * (D + 1) / 2;
+// The auxiliary law of one step: the law's B̃, β̃, a − ã, or — where the lane's law is
+// time-dependent (DMT_LAW_AUXTD) — the step's row of the per-point table, component c at
+// row[c * cstride]: B̃, β̃, and with DMT_LAW_AUXTD = 2 also a − ã(t_i) = a − row's ã (in T);
+// trace: whether G takes the trace term (the law's flag, or a table ã)
 template <class Mdl, class T, class Ld>
 __device__ __forceinline__ void aux_step(const Law<Mdl, T>& L, const T* row, int64_t cstride,
-                                         T* Bt, T* beta, Ld ld) {
-  constexpr int D = Mdl::D;
+                                         T* Bt, T* beta, T* da, bool& trace, Ld ld) {
+  constexpr int D = Mdl::D, HP = D * (D + 1) / 2;
 #pragma unroll
   for (int c = 0; c < D * D; ++c) {
     const T v = ld(&row[c * cstride]);
@@ -231,6 +240,12 @@ __device__ __forceinline__ void aux_step(const Law<Mdl, T>& L, const T* row, int
     const T v = ld(&row[(D * D + p) * cstride]);
     beta[p] = L.auxtd ? v : L.beta[p];
   }
+#pragma unroll
+  for (int e = 0; e < HP; ++e) {
+    const T v = ld(&row[(D * D + D + e) * cstride]);
+    da[e] = L.auxa ? L.a[e] - v : L.da[e];
+  }
+  trace = L.trace || L.auxa;
 }
 
 // sigma·dW of one step (canonical: sdW_a = s_a0 dW_0, then fma over k)

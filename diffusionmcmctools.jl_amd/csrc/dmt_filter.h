@@ -318,8 +318,9 @@ DMT_HD bool filter_combine(const Trans<N>& q, Mat<N>& Hc, double* Fc, double& cc
 // (k_filter_scan / k_filter_chain); this is the serial host statement of the same arithmetic.
 constexpr int kFiltChunk = 64;
 
-// Coef(i, B, beta): the auxiliary drift of step i (constant, or a time-dependent law's
-// trapezoidal average over [t_i, t_i+1]: second order).
+// Coef(i, B, beta, A): the auxiliary law of step i — drift B, beta and, where ã is
+// time-dependent, A (in: the segment's ã) — constant, or a time-dependent law's trapezoidal
+// average over [t_i, t_i+1] (second order).
 template <int N, class TimeAt, class Coef, class Store>
 inline bool filter_segment(Coef coef, const Mat<N>& A, int npts, TimeAt tat, Mat<N>& Hc,
                            double* Fc, double& cc, Store store) {
@@ -328,10 +329,10 @@ inline bool filter_segment(Coef coef, const Mat<N>& A, int npts, TimeAt tat, Mat
   for (int hi = npts - 1; hi > 0; hi -= kFiltChunk) {
     const int lo = hi > kFiltChunk ? hi - kFiltChunk : 0, cnt = hi - lo;
     for (int l = 0; l < cnt; ++l) {
-      Mat<N> B;
+      Mat<N> B, As = A;
       double beta[N];
-      coef(lo + l, B, beta);
-      Q[l] = step_trans(B, beta, A, tat(lo + l + 1) - tat(lo + l));
+      coef(lo + l, B, beta, As);
+      Q[l] = step_trans(B, beta, As, tat(lo + l + 1) - tat(lo + l));
     }
     for (int k = 1; k < kFiltChunk; k *= 2) {
       for (int l = 0; l < cnt; ++l) Qn[l] = (l + k < cnt) ? compose(Q[l], Q[l + k]) : Q[l];

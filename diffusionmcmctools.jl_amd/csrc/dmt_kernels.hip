@@ -140,7 +140,7 @@ __device__ __forceinline__ bool run_segment(const Law<Mdl, T>& L, const T* __res
   // table; wave-uniform, so a time-homogeneous ensemble takes the branch-free path
   // (TD: the ensemble has a per-point table; a separate instantiation, so that a
   // time-homogeneous ensemble runs the kernel without it)
-  constexpr int CA = D * D + D;
+  constexpr int CA = kAuxCols<D>;
   const T* Ab = (TD && At) ? At + row * CA * kLanes + lane : nullptr;
   const bool td = TD && Ab != nullptr && __ballot(L.auxtd) != 0;
   // tile-phase repair: a lane whose u lives in the "wrong" buffer copies u.X
@@ -232,10 +232,11 @@ __device__ __forceinline__ bool run_segment(const Law<Mdl, T>& L, const T* __res
     T G;
     if constexpr (TD) {
       if (td) {
-        T Bq[D * D], bq[D];
-        aux_step<Mdl, T>(L, Ab + (int64_t)i * CA * kLanes, kLanes, Bq, bq,
+        T Bq[D * D], bq[D], dq[D * (D + 1) / 2];
+        bool trq;
+        aux_step<Mdl, T>(L, Ab + (int64_t)i * CA * kLanes, kLanes, Bq, bq, dq, trq,
                          [](const T* p) { return lane_ld(p); });
-        G = g_at_aux<Mdl, T>(L, Hi, Fi, x, r, b, Bq, bq);
+        G = g_at_aux<Mdl, T>(L, Hi, Fi, x, r, b, Bq, bq, dq, trq);
       } else {
         G = g_at<Mdl, T>(L, Hi, Fi, x, r, b);
       }
@@ -532,7 +533,7 @@ __device__ __forceinline__ bool run_segment_pk(const Law<Mdl, T>& L, const T* __
                                                NormalStream<T>& ns, const int64_t tq,
                                                const int64_t q0, const int np, const int lane,
                                                const T rho, const T srho, const int ll_skip,
-                                               T* x, T& sl) {
+                                               T* x, T& sl, T* stg) {
   constexpr int D = Mdl::D, M = Mdl::M, HP = D * (D + 1) / 2;
   constexpr bool DRAW = MODE != MODE_RECOMPUTE;
   constexpr bool READW = MODE != MODE_FRESH;
@@ -550,7 +551,7 @@ __device__ __forceinline__ bool run_segment_pk(const Law<Mdl, T>& L, const T* __
   auto pix = [&](int64_t i, int c, int C) -> int64_t {  // point i of the segment, component c
     return plane_ix(row + i, c, C, kLanes, lane, PK);
   };
-  constexpr int CA = D * D + D;
+  constexpr int CA = kAuxCols<D>;
   const T* Ab = (TD && At) ? At + row * CA * kLanes + lane : nullptr;
   const bool td = TD && Ab != nullptr && __ballot(L.auxtd) != 0;
   const int nst = np - 1;
@@ -584,10 +585,11 @@ __device__ __forceinline__ bool run_segment_pk(const Law<Mdl, T>& L, const T* __
     T G;
     if constexpr (TD) {
       if (td) {
-        T Bq[D * D], bq[D];
-        aux_step<Mdl, T>(L, Ab + (int64_t)i * CA * kLanes, kLanes, Bq, bq,
+        T Bq[D * D], bq[D], dq[D * (D + 1) / 2];
+        bool trq;
+        aux_step<Mdl, T>(L, Ab + (int64_t)i * CA * kLanes, kLanes, Bq, bq, dq, trq,
                          [](const T* p) { return lane_ld(p); });
-        G = g_at_aux<Mdl, T>(L, Hi, Fi, x, r, b, Bq, bq);
+        G = g_at_aux<Mdl, T>(L, Hi, Fi, x, r, b, Bq, bq, dq, trq);
       } else {
         G = g_at<Mdl, T>(L, Hi, Fi, x, r, b);
       }
@@ -668,7 +670,10 @@ __device__ __forceinline__ bool run_segment_pk(const Law<Mdl, T>& L, const T* __
             for (int v = 0; v < NV; ++v) wn[k][v] = wpk(j + 1, k)[v];
         }
 #endif
-        v16 ox[D][NV], ow[M][NV];
+        // the packet's X°, W° go to the lane's LDS rows step by step (stg[c][e][lane], a
+        // 65-element row pitch) and leave as whole 16-byte pieces at the packet's end:
+        // register-staged packets measured slower (AGPR moves; 1 378 vs 1 288 µs in the probe)
+        auto st = [&](int c, int e) -> T& { return stg[(c * PK + e) * 65 + lane]; };
 #pragma unroll
         for (int v = 0; v < PK / K; ++v) {
           const int c0 = j * PK + v * K;
@@ -683,9 +688,11 @@ __device__ __forceinline__ bool run_segment_pk(const Law<Mdl, T>& L, const T* __
             for (int k = 0; k < M; ++k) dW[k] = READW ? wc[k][e / VE][e % VE] : (T)0;
             gv[q] = step(c0 + q, cur.t[q], cur.H[q], cur.F[q], dW, cur.Z[q]);
 #pragma unroll
-            for (int p = 0; p < D; ++p) ox[p][e / VE][e % VE] = x[p];
+            for (int p = 0; p < D; ++p) st(p, e) = x[p];
+            if (DRAW) {
 #pragma unroll
-            for (int k = 0; k < M; ++k) ow[k][e / VE][e % VE] = dW[k];
+              for (int k = 0; k < M; ++k) st(D + k, e) = dW[k];
+            }
           }
 #if DMT_PK_ROLL
           // the piece of u.W this chunk consumed is refilled with the next packet's: a prefetch
@@ -701,18 +708,24 @@ __device__ __forceinline__ bool run_segment_pk(const Law<Mdl, T>& L, const T* __
           ps.template add_subtree<Log2<K>::v>(tree_sum<T, K>(gv));
           cur = nxt;
         }
+        auto piece = [&](int c, int v) -> v16 {
+          v16 o;
+#pragma unroll
+          for (int u = 0; u < VE; ++u) o[u] = st(c, v * VE + u);
+          return o;
+        };
 #pragma unroll
         for (int p = 0; p < D; ++p) {
           v16* dst = (v16*)&Xd[pix((int64_t)j * PK + 1, p, D)];
 #pragma unroll
-          for (int v = 0; v < NV; ++v) dst[v] = ox[p][v];
+          for (int v = 0; v < NV; ++v) dst[v] = piece(p, v);
         }
         if (DRAW) {
 #pragma unroll
           for (int k = 0; k < M; ++k) {
             v16* dst = (v16*)&Wd[pix((int64_t)j * PK + 1, k, M)];
 #pragma unroll
-            for (int v = 0; v < NV; ++v) dst[v] = ow[k][v];
+            for (int v = 0; v < NV; ++v) dst[v] = piece(D + k, v);
           }
         }
 #if !DMT_PK_ROLL
@@ -784,7 +797,7 @@ __device__ __forceinline__ bool run_segment_pk(const Law<Mdl, T>& L, const T* __
 
 template <class Mdl, class T, int MODE, bool PARITY, int K, bool TD>
 __device__ __forceinline__ void lane_block_pk(const BlockArgs<T>& a, const int64_t tile,
-                                              const int64_t blk, const int lane) {
+                                              const int64_t blk, const int lane, T* stg) {
   constexpr int D = Mdl::D, HP = D * (D + 1) / 2, PK = kPathPacket;
   const int64_t tq = a.tile_qoff[tile];
   auto idx = [&](int64_t q, int c, int C) -> int64_t { return ((tq + q) * C + c) * kLanes + lane; };
@@ -833,11 +846,11 @@ __device__ __forceinline__ void lane_block_pk(const BlockArgs<T>& a, const int64
         aligned ? run_segment_pk<Mdl, T, MODE, PARITY, K, TD, PK, true>(
                       L, a.t, a.t_shared, a.H[ls][kind], a.H_shared[ls][kind], a.F[ls][kind],
                       a.aux[kind], Ws, Wd, Xd, Zg, ns, tq, q0, a.seg_np[g], lane, rho, srho,
-                      a.ll_skip, x, sl)
+                      a.ll_skip, x, sl, stg)
                 : run_segment_pk<Mdl, T, MODE, PARITY, K, TD, PK, false>(
                       L, a.t, a.t_shared, a.H[ls][kind], a.H_shared[ls][kind], a.F[ls][kind],
                       a.aux[kind], Ws, Wd, Xd, Zg, ns, tq, q0, a.seg_np[g], lane, rho, srho,
-                      a.ll_skip, x, sl);
+                      a.ll_skip, x, sl, stg);
     if (!sok) { ok = false; break; }
     ll = ll + sl;
   }
@@ -847,9 +860,10 @@ __device__ __forceinline__ void lane_block_pk(const BlockArgs<T>& a, const int64
 
 template <class Mdl, class T, int MODE, bool PARITY, int K, bool TD = false>
 __global__ __launch_bounds__(64) void k_block_pk(const BlockArgs<T> a) {
+  __shared__ T stg[(Mdl::D + Mdl::M) * kPathPacket * 65];  // the packet's X°, W° (run_segment_pk)
   int64_t tile, blk;
   if (!map_block(a, tile, blk)) return;
-  lane_block_pk<Mdl, T, MODE, PARITY, K, TD>(a, tile, blk, threadIdx.x);
+  lane_block_pk<Mdl, T, MODE, PARITY, K, TD>(a, tile, blk, threadIdx.x, stg);
 }
 
 // ---- MAP_LANE, pair mapping: two waves per (recording tile, block index), each
@@ -1183,7 +1197,7 @@ __global__ __launch_bounds__(64) void k_pathll(const BlockArgs<T> a) {
     const T* __restrict__ Xs = a.X[sel_buf(a.selX[g], a.xs_flip)];
     const int64_t q0 = a.seg_q[g];
     const int nst = a.seg_np[g] - 1;
-    constexpr int CA = D * D + D;  // time-dependent auxiliary law (run_segment)
+    constexpr int CA = kAuxCols<D>;  // time-dependent auxiliary law (run_segment)
     const T* At = TD ? a.aux[kind] : nullptr;
     const bool td = TD && At != nullptr && __ballot(L.auxtd) != 0;
     PSum<T> ps;
@@ -1210,10 +1224,11 @@ __global__ __launch_bounds__(64) void k_pathll(const BlockArgs<T> a) {
           T G;
           if constexpr (TD) {
             if (td) {
-              T Bq[D * D], bq[D];
-              aux_step<Mdl, T>(L, At + idx(q0 + c0 + j, 0, CA), kLanes, Bq, bq,
+              T Bq[D * D], bq[D], dq[HP];
+              bool trq;
+              aux_step<Mdl, T>(L, At + idx(q0 + c0 + j, 0, CA), kLanes, Bq, bq, dq, trq,
                                [](const T* p) { return *p; });
-              G = g_at_aux<Mdl, T>(L, vH[j], vF[j], vX[j], r, b, Bq, bq);
+              G = g_at_aux<Mdl, T>(L, vH[j], vF[j], vX[j], r, b, Bq, bq, dq, trq);
             } else {
               G = g_at<Mdl, T>(L, vH[j], vF[j], vX[j], r, b);
             }
@@ -1515,12 +1530,13 @@ __global__ __launch_bounds__(128) void k_block_wave(const BlockArgs<T> a) {
     for (int c = 0; c < D; ++c) { Fi[c] = rw[1 + HP + c]; xi[c] = sh.xcap[k & 1][lane][c]; }
     T G;
     if (a.aux[kind] && LB.auxtd) {  // time-dependent auxiliary law: step i's B̃(t_i), β̃(t_i)
-      constexpr int CA = D * D + D;
+      constexpr int CA = kAuxCols<D>;
       const int i = c0 + (valid ? lane : cnt - 1);
-      T Bq[D * D], bq[D];
-      aux_step<Mdl, T>(LB, a.aux[kind] + (tq + a.seg_q[g] + i) * CA, 1, Bq, bq,
+      T Bq[D * D], bq[D], dq[HP];
+      bool trq;
+      aux_step<Mdl, T>(LB, a.aux[kind] + (tq + a.seg_q[g] + i) * CA, 1, Bq, bq, dq, trq,
                        [](const T* p) { return *p; });
-      G = g_at_aux<Mdl, T>(LB, Hi, Fi, xi, rr, bb, Bq, bq);
+      G = g_at_aux<Mdl, T>(LB, Hi, Fi, xi, rr, bb, Bq, bq, dq, trq);
     } else {
       G = g_at<Mdl, T>(LB, Hi, Fi, xi, rr, bb);
     }
@@ -3285,10 +3301,12 @@ __global__ __launch_bounds__(64) void k_pathll_wave(const BlockArgs<T> a) {
       for (int c = 0; c < D; ++c) { Fi[c] = Fb[(int64_t)i * D + c]; xi[c] = Xb[(int64_t)i * D + c]; }
       T G;
       if (a.aux[kind] && L.auxtd) {  // time-dependent auxiliary law (k_block_wave)
-        constexpr int CA = D * D + D;
-        T Bq[D * D], bq[D];
-        aux_step<Mdl, T>(L, a.aux[kind] + (row + i) * CA, 1, Bq, bq, [](const T* p) { return *p; });
-        G = g_at_aux<Mdl, T>(L, Hi, Fi, xi, rr, bb, Bq, bq);
+        constexpr int CA = kAuxCols<D>;
+        T Bq[D * D], bq[D], dq[HP];
+        bool trq;
+        aux_step<Mdl, T>(L, a.aux[kind] + (row + i) * CA, 1, Bq, bq, dq, trq,
+                         [](const T* p) { return *p; });
+        G = g_at_aux<Mdl, T>(L, Hi, Fi, xi, rr, bb, Bq, bq, dq, trq);
       } else {
         G = g_at<Mdl, T>(L, Hi, Fi, xi, rr, bb);
       }
@@ -3487,10 +3505,12 @@ __global__ void k_filter_mark(const FilterArgs a) {
 
 template <int D>
 __device__ __forceinline__ void filt_law(const FilterArgs& a, int g, int kind, flt::Mat<D>& B,
-                                         double* beta, flt::Mat<D>& At, int& slot, bool& td) {
+                                         double* beta, flt::Mat<D>& At, int& slot, bool& td,
+                                         bool& tda) {
   slot = (kind ? a.selPPB[g] : a.selPP[g]) ^ a.unit;
   const double* lr = a.law[slot][kind] + (int64_t)g * DMT_LAW_STRIDE;
   td = a.aux[kind] != nullptr && lr[DMT_LAW_AUXTD] != 0.0;
+  tda = a.aux[kind] != nullptr && lr[DMT_LAW_AUXTD] == 2.0;
 #pragma unroll
   for (int p = 0; p < D; ++p) {
     beta[p] = lr[DMT_LAW_BETA + p];
@@ -3509,12 +3529,21 @@ __device__ __forceinline__ void filt_law(const FilterArgs& a, int g, int kind, f
 // scheme for the filter ODEs (a constant table gives the table's value exactly)
 template <int D, class T, class Ix>
 __device__ __forceinline__ void filt_aux_step(const T* tab, Ix ix, int64_t q, flt::Mat<D>& B,
-                                              double* beta) {
+                                              double* beta, flt::Mat<D>& A, bool tda) {
 #pragma unroll
   for (int c = 0; c < D * D; ++c) B.a[c] = ((double)tab[ix(q, c)] + (double)tab[ix(q + 1, c)]) * 0.5;
 #pragma unroll
   for (int p = 0; p < D; ++p)
     beta[p] = ((double)tab[ix(q, D * D + p)] + (double)tab[ix(q + 1, D * D + p)]) * 0.5;
+  if (tda) {  // ã(t) from the table as well (DMT_LAW_AUXTD = 2), its trapezoidal average
+#pragma unroll
+    for (int p = 0; p < D; ++p)
+#pragma unroll
+      for (int r = 0; r < D; ++r) {
+        const int c = D * D + D + flt::packed_ix(D, p, r);
+        A(p, r) = ((double)tab[ix(q, c)] + (double)tab[ix(q + 1, c)]) * 0.5;
+      }
+  }
 }
 
 // chunk j of a segment with np points: steps [lo, lo + cnt), counted from the segment end
@@ -3557,8 +3586,8 @@ __global__ __launch_bounds__(256) void k_filter_scan(const FilterArgs a, int64_t
   flt::Mat<D> B, At;
   double beta[D];
   int slot;
-  bool td;
-  filt_law<D>(a, g, sel - 1, B, beta, At, slot, td);
+  bool td, tda;
+  filt_law<D>(a, g, sel - 1, B, beta, At, slot, td, tda);
   int lo, cnt;
   filt_chunk(a.seg_np[g], (int)(item - a.fchunk_off[g]), lo, cnt);
   const int64_t r = a.seg_rec[g];
@@ -3571,10 +3600,10 @@ __global__ __launch_bounds__(256) void k_filter_scan(const FilterArgs a, int64_t
   flt::Trans<D> q;
   if (lane < cnt) {
     if (td) {
-      constexpr int CA = D * D + D;
+      constexpr int CA = kAuxCols<D>;
       filt_aux_step<D>((const T*)a.aux[sel - 1],
                        [&](int64_t qq, int c) { return ((tq + qq) * CA + c) * a.tw + rl; },
-                       lo + lane, B, beta);
+                       lo + lane, B, beta, At, tda);
     }
     q = flt::step_trans<D>(B, beta, At, tat(lo + lane + 1) - tat(lo + lane));
   } else {
@@ -3896,8 +3925,8 @@ __global__ __launch_bounds__(256) void k_filter_fused(const FilterArgs a) {
     M B, At;
     double beta[D];
     int slot;
-    bool td;
-    filt_law<D>(a, g, cur.kind, B, beta, At, slot, td);
+    bool td, tda;
+    filt_law<D>(a, g, cur.kind, B, beta, At, slot, td, tda);
     M HT;
     double FT[D], cT = cur.oc;
 #pragma unroll
@@ -3948,17 +3977,17 @@ __global__ __launch_bounds__(256) void k_filter_fused(const FilterArgs a) {
       filt_chunk(cur.np, j, lo, cnt);
       flt::Trans<D> q;
       if (lane < cnt) {
-        M Bq = B;
+        M Bq = B, Aq = At;
         double bq[D];
 #pragma unroll
         for (int p = 0; p < d; ++p) bq[p] = beta[p];
         if (td) {
-          constexpr int CA = D * D + D;
+          constexpr int CA = kAuxCols<D>;
           filt_aux_step<D>((const T*)a.aux[cur.kind],
                            [&](int64_t qq, int c) { return ix(cur.q0 + qq, c, CA); }, lo + lane, Bq,
-                           bq);
+                           bq, Aq, tda);
         }
-        q = flt::step_trans<D>(Bq, bq, At, tat(lo + lane + 1) - tat(lo + lane));
+        q = flt::step_trans<D>(Bq, bq, Aq, tat(lo + lane + 1) - tat(lo + lane));
       } else {
         q.Phi = flt::meye<D>();
         q.K = flt::mzero<D>();

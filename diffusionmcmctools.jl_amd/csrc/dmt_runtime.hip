@@ -1225,8 +1225,15 @@ dmt_status dmt_upload_law(dmt_ens* h, int32_t unit, int32_t kind, const double* 
 }
 
 dmt_status dmt_upload_aux(dmt_ens* h, int32_t kind, const double* aux) {
+  return dmt_upload_aux_a(h, kind, aux, (int32_t)(h ? h->d * h->d + h->d : 0));
+}
+
+dmt_status dmt_upload_aux_a(dmt_ens* h, int32_t kind, const double* aux, int32_t ncols) {
   DMT_TRY(enter(h));
   if (kind != DMT_LAW_PP && kind != DMT_LAW_PPB) return fail(DMT_ERR_INVALID, "bad kind");
+  const int nb = (int)(h->d * h->d + h->d), na = nb + (int)h->hp;  // table columns (kAuxCols)
+  if (aux && ncols != nb && ncols != na)
+    return fail(DMT_ERR_INVALID, "aux table: d*d + d or d*d + d + d(d+1)/2 columns per point");
   if (h->key.model == DMT_MODEL_OU)
     return fail(DMT_ERR_INVALID, "time-dependent auxiliary laws: non-linear drifts only (the OU "
                                  "kernels' affine scan takes the auxiliary drift per segment)");
@@ -1234,18 +1241,26 @@ dmt_status dmt_upload_aux(dmt_ens* h, int32_t kind, const double* aux) {
     if (h->d_aux[kind]) {
       HIP_OK(stream_wait(h));
       (void)hipFree(h->d_aux[kind]);
-      h->bytes -= plane_elems(h, h->d * h->d + h->d) * (int64_t)h->esz;
+      h->bytes -= plane_elems(h, na) * (int64_t)h->esz;
       h->d_aux[kind] = nullptr;
     }
     return DMT_OK;
   }
-  const int C = (int)(h->d * h->d + h->d);
+  const int C = na;  // the device table always holds the ã columns (zero when not given)
   if (!h->d_aux[kind]) {
     DMT_TRY(ens_alloc_bytes(h, &h->d_aux[kind], plane_elems(h, C) * h->esz));
     HIP_OK(hipMemsetAsync(h->d_aux[kind], 0, plane_elems(h, C) * h->esz, h->stream));
   }
   DMT_TRY(ensure_stage(h, h->P * C));
-  HIP_OK(hipMemcpyAsync(h->d_stage, aux, h->P * C * 8, hipMemcpyHostToDevice, h->stream));
+  if (ncols == na) {
+    HIP_OK(hipMemcpyAsync(h->d_stage, aux, h->P * C * 8, hipMemcpyHostToDevice, h->stream));
+  } else {  // B̃, β̃ only: pad each row with zero ã columns
+    std::vector<double> full((size_t)h->P * C, 0.0);
+    for (int64_t p = 0; p < h->P; ++p)
+      std::memcpy(&full[(size_t)p * C], aux + (size_t)p * nb, nb * 8);
+    HIP_OK(hipMemcpyAsync(h->d_stage, full.data(), h->P * C * 8, hipMemcpyHostToDevice, h->stream));
+    HIP_OK(stream_wait(h));
+  }
   // one table for u and u°: both destinations of the per-segment copy are the table itself
   HIP_OK(launch_to_planes(h->key.precision, h->tw, h->d_stage, h->d_aux[kind], h->d_aux[kind],
                           h->d_sel[2 + kind], 0, C, h->P, h->d_pt_off, h->G, h->d_seg_rec,
@@ -2482,17 +2497,19 @@ dmt_status dmt_set_rng_state(dmt_ens* h, uint64_t next, uint64_t last_draw, uint
 }  // extern "C"
 
 template <int D>
-// aux: nullptr (B̃ = Bt, β̃ = beta throughout) or [npts][d·d + d] per-point coefficients
-// (step i: the trapezoidal average of rows i and i + 1)
+// aux: nullptr (B̃ = Bt, β̃ = beta throughout) or [npts][ncols] per-point coefficients — B̃, β̃
+// (ncols = d·d + d; ã = at throughout) or B̃, β̃, ã packed (ncols = d·d + d + hp; at unused) —
+// step i taking the trapezoidal average of rows i and i + 1
 static dmt_status guiding_linear_impl(const double* Bt, const double* beta, const double* aux,
                                       const double* at, int32_t npts, const double* t,
                                       const double* HT, const double* FT, double cT, double* H,
-                                      double* F, double* c) {
+                                      double* F, double* c, int ncols = D * D + D) {
   constexpr int d = D, hp = d * (d + 1) / 2;
+  const bool tda = aux && ncols == d * d + d + hp;
   flt::Mat<D> A = flt::mzero<D>(), Hc = flt::mzero<D>();
   for (int i = 0; i < d; ++i)
     for (int j = 0; j < d; ++j) {
-      A(i, j) = at[dmt_packed(d, i, j)];
+      A(i, j) = tda ? 0.0 : at[dmt_packed(d, i, j)];
       Hc(i, j) = HT[dmt_packed(d, i, j)];
     }
   double Fc[D];
@@ -2508,16 +2525,22 @@ static dmt_status guiding_linear_impl(const double* Bt, const double* beta, cons
   };
   // step i's auxiliary drift: the law's, or the trapezoidal average of a time-dependent law's
   // coefficients at t_i and t_i+1 (second order; DESIGN.md §3, filt_aux_step on the device)
-  auto coef = [&](int i, flt::Mat<D>& B, double* be) {
+  auto coef = [&](int i, flt::Mat<D>& B, double* be, flt::Mat<D>& As) {
     if (!aux) {
       for (int k = 0; k < d * d; ++k) B.a[k] = Bt[k];
       for (int p = 0; p < d; ++p) be[p] = beta[p];
       return;
     }
-    const double* r0 = aux + (int64_t)i * (d * d + d);
-    const double* r1 = r0 + (d * d + d);
+    const double* r0 = aux + (int64_t)i * ncols;
+    const double* r1 = r0 + ncols;
     for (int k = 0; k < d * d; ++k) B.a[k] = (r0[k] + r1[k]) * 0.5;
     for (int p = 0; p < d; ++p) be[p] = (r0[d * d + p] + r1[d * d + p]) * 0.5;
+    if (tda)
+      for (int p = 0; p < d; ++p)
+        for (int q = 0; q < d; ++q) {
+          const int e = d * d + d + dmt_packed(d, p, q);
+          As(p, q) = (r0[e] + r1[e]) * 0.5;
+        }
   };
   if (!flt::filter_segment<D>(coef, A, npts, [&](int i) { return t[i]; }, Hc, Fc, cc, store))
     return fail(DMT_ERR_INVALID, "singular I + HK in backward filter");
@@ -2544,6 +2567,17 @@ dmt_status dmt_guiding_linear_td(int32_t d, const double* aux, const double* at,
   if (d == 1) return guiding_linear_impl<1>(nullptr, nullptr, aux, at, npts, t, HT, FT, cT, H, F, c);
   if (d == 2) return guiding_linear_impl<2>(nullptr, nullptr, aux, at, npts, t, HT, FT, cT, H, F, c);
   return guiding_linear_impl<3>(nullptr, nullptr, aux, at, npts, t, HT, FT, cT, H, F, c);
+}
+
+dmt_status dmt_guiding_linear_tda(int32_t d, const double* aux, int32_t npts, const double* t,
+                                  const double* HT, const double* FT, double cT, double* H,
+                                  double* F, double* c) {
+  if (d < 1 || d > 3 || npts < 1 || !aux || !t || !HT || !FT || !H || !F || !c)
+    return fail(DMT_ERR_INVALID, "bad arguments to dmt_guiding_linear_tda");
+  const int nc = d * d + d + d * (d + 1) / 2;
+  if (d == 1) return guiding_linear_impl<1>(nullptr, nullptr, aux, nullptr, npts, t, HT, FT, cT, H, F, c, nc);
+  if (d == 2) return guiding_linear_impl<2>(nullptr, nullptr, aux, nullptr, npts, t, HT, FT, cT, H, F, c, nc);
+  return guiding_linear_impl<3>(nullptr, nullptr, aux, nullptr, npts, t, HT, FT, cT, H, F, c, nc);
 }
 
 dmt_status dmt_comm_unique_id(uint8_t* id_out) {

@@ -82,12 +82,18 @@ class Ensemble:
                L.f64p(F), L.f64p(laws))
 
     def upload_aux(self, kind, aux):
-        """dmt_upload_aux: per-point B̃(t_i), β̃(t_i) ([P][d·d + d]) of the laws of `kind` (u and
-        u° alike) for segments whose record has LAW_AUXTD set; None removes the table."""
-        aux = None if aux is None else np.ascontiguousarray(aux, dtype=np.float64)
-        if aux is not None and aux.size != self.P * (self.d * self.d + self.d):
-            raise ValueError("aux needs P·(d·d + d) values")
-        L.call("dmt_upload_aux", self._h, int(kind), L.f64p(aux))
+        """dmt_upload_aux(_a): per-point B̃(t_i), β̃(t_i) ([P][d·d + d]) — or B̃, β̃, ã(t_i) packed
+        ([P][d·d + d + d(d+1)/2]) — of the laws of `kind` (u and u° alike) for segments whose
+        record has LAW_AUXTD set (2: ã from the table too); None removes the table."""
+        if aux is None:
+            L.call("dmt_upload_aux", self._h, int(kind), None)
+            return
+        aux = np.ascontiguousarray(aux, dtype=np.float64)
+        nb = self.d * self.d + self.d
+        na = nb + self.d * (self.d + 1) // 2
+        if aux.size not in (self.P * nb, self.P * na):
+            raise ValueError("aux needs P·(d·d + d) or P·(d·d + d + d(d+1)/2) values")
+        L.call("dmt_upload_aux_a", self._h, int(kind), L.f64p(aux), aux.size // self.P)
 
     def set_paths(self, unit, X=None, W=None):
         X = None if X is None else np.ascontiguousarray(X, dtype=np.float64)
@@ -465,6 +471,24 @@ def guiding_linear_td(aux, at_packed, t, HT_packed, FT, cT):
     c = np.empty(n)
     L.call("dmt_guiding_linear_td", d, L.f64p(aux),
            L.f64p(np.ascontiguousarray(at_packed, dtype=np.float64)), n, L.f64p(t),
+           L.f64p(np.ascontiguousarray(HT_packed, dtype=np.float64)),
+           L.f64p(np.ascontiguousarray(FT, dtype=np.float64)), float(cT), L.f64p(H), L.f64p(F),
+           L.f64p(c))
+    return H, F, c
+
+
+def guiding_linear_tda(aux, t, HT_packed, FT, cT):
+    """The host filter of a time-dependent auxiliary law with time-dependent ã too
+    (dmt_guiding_linear_tda): aux[npts][d·d + d + d(d+1)/2] = B̃, β̃, ã packed."""
+    t = np.ascontiguousarray(t, dtype=np.float64)
+    n = t.size
+    aux = np.ascontiguousarray(aux, dtype=np.float64).reshape(n, -1)
+    d = {3: 1, 9: 2, 18: 3}[aux.shape[1]]
+    hp = d * (d + 1) // 2
+    H = np.empty((n, hp))
+    F = np.empty((n, d))
+    c = np.empty(n)
+    L.call("dmt_guiding_linear_tda", d, L.f64p(aux), n, L.f64p(t),
            L.f64p(np.ascontiguousarray(HT_packed, dtype=np.float64)),
            L.f64p(np.ascontiguousarray(FT, dtype=np.float64)), float(cT), L.f64p(H), L.f64p(F),
            L.f64p(c))

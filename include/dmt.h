@@ -195,6 +195,13 @@ dmt_status dmt_upload_law(dmt_ens* h, int32_t unit, int32_t kind, const double* 
  * (dmt_recompute_guiding_term); ã stays the record's (σ̃ constant per segment).  aux = NULL
  * removes the table.  Non-linear drifts (FHN, Lorenz) only: DMT_ERR_INVALID for OU. */
 dmt_status dmt_upload_aux(dmt_ens* h, int32_t kind, const double* aux);
+/* The same with a time-dependent ã(t) = σ̃σ̃ᵀ(t) too: aux[P][ncols], ncols = d·d + d (as
+ * dmt_upload_aux) or d·d + d + d(d+1)/2 — B̃, β̃ and ã packed (upper triangle, row-major) per
+ * point.  A segment whose law record has DMT_LAW_AUXTD = 2 takes step i's a − ã(t_i) in G's trace
+ * term (a − ã computed in the working precision; the term is taken whatever the record's trace
+ * flag) and the trapezoidal average of ã over [t_i, t_i+1] in the filter's step transition
+ * (DESIGN.md §7); DMT_LAW_AUXTD = 1 keeps the record's ã. */
+dmt_status dmt_upload_aux_a(dmt_ens* h, int32_t kind, const double* aux, int32_t ncols);
 
 /* Paths of unit u / u°: X[P][d], W[P][m]; NULL keeps the current one.  Used by
  * init_paths! (src/sampling_unit.jl:83-87) and find_W_for_X! (src/block.jl:118-131). */
@@ -435,6 +442,11 @@ dmt_status dmt_guiding_linear(int32_t d, const double* Bt, const double* beta,
 dmt_status dmt_guiding_linear_td(int32_t d, const double* aux, const double* at, int32_t npts,
                                  const double* t, const double* HT, const double* FT, double cT,
                                  double* H, double* F, double* c);
+/* ... and with a time-dependent ã too: aux[npts][d·d + d + d(d+1)/2] = B̃, β̃, ã packed; step
+ * i's transition takes the trapezoidal averages of rows i and i + 1 (dmt_upload_aux_a). */
+dmt_status dmt_guiding_linear_tda(int32_t d, const double* aux, int32_t npts, const double* t,
+                                  const double* HT, const double* FT, double cT, double* H,
+                                  double* F, double* c);
 
 /* ---------------- multi-GPU (RCCL over xGMI) ---------------- */
 dmt_status dmt_comm_unique_id(uint8_t* id_out /*128 bytes*/);

@@ -370,10 +370,13 @@ void orc_set_ll_skip(int k) { orc_ll_skip = k; }
 extern int orc_ll_skip;
 #endif
 
-/* Time-dependent auxiliary law of the segment being solved (libdmt dmt_upload_aux; set by
- * oracle.py around a segment call, NULL otherwise): rows [npts][d*d + d] = B~(t_i), beta~(t_i),
- * used at step i (left point) in place of the record's Bt, beta when the record's auxtd
- * (offset 15) is set.  Non-linear drifts only. */
+/* Time-dependent auxiliary law of the segment being solved (libdmt dmt_upload_aux(_a); set by
+ * oracle.py around a segment call, NULL otherwise): rows [npts][d*d + d + d(d+1)/2] =
+ * B~(t_i), beta~(t_i), a~(t_i) packed (zeros where not given), used at step i (left point) in
+ * place of the record's Bt, beta when the record's auxtd (offset 15) is set, and — auxtd = 2 —
+ * a − a~(t_i) (in the working precision) in place of the record's a − a~ in G's trace term,
+ * which is then taken whatever the record's trace flag (libdmt aux_step).  Non-linear drifts
+ * only. */
 #if IS_F64
 const double* orc_aux = 0;
 void orc_set_aux(const double* p) { orc_aux = p; }
@@ -381,11 +384,21 @@ void orc_set_aux(const double* p) { orc_aux = p; }
 extern const double* orc_aux;
 #endif
 static inline const REAL* aux_coeffs(const double* law, int model, int d, int i, const REAL* Bt,
-                                     const REAL* beta, REAL* Bq, REAL* bq, const REAL** bo) {
+                                     const REAL* beta, REAL* Bq, REAL* bq, const REAL** bo,
+                                     const REAL* a, const REAL* da, int trace, REAL* dq,
+                                     const REAL** dao, int* tro) {
+    *dao = da;
+    *tro = trace;
     if (model == ORC_OU || !orc_aux || law[L_AUXTD] == 0.0) { *bo = beta; return Bt; }
-    const double* row = orc_aux + (size_t)i * (d * d + d);
+    const int hp = d * (d + 1) / 2;
+    const double* row = orc_aux + (size_t)i * (d * d + d + hp);
     for (int k = 0; k < d * d; ++k) Bq[k] = (REAL)row[k];
     for (int p = 0; p < d; ++p) bq[p] = (REAL)row[d * d + p];
+    if (law[L_AUXTD] == 2.0) {
+        for (int e = 0; e < hp; ++e) dq[e] = a[e] - (REAL)row[d * d + d + e];
+        *dao = dq;
+        *tro = 1;
+    }
     *bo = bq;
     return Bq;
 }
@@ -421,10 +434,11 @@ int SFX(orc_solve_segment)(int model, int d, int m, const double* law, int npts,
         const REAL* Hi = H + (size_t)i * h;
         const REAL* Fi = F + (size_t)i * d;
         REAL r[3] = {0, 0, 0}, b[3] = {0, 0, 0};
-        REAL Bq[9], bq[3];
-        const REAL* bu;
-        const REAL* Bu = aux_coeffs(law, model, d, i, Bt, beta, Bq, bq, &bu);
-        REAL G = g_at(model, d, th, a, Bu, bu, da, trace, Hi, Fi, x, r, b);
+        REAL Bq[9], bq[3], dq[6];
+        const REAL *bu, *du;
+        int tu;
+        const REAL* Bu = aux_coeffs(law, model, d, i, Bt, beta, Bq, bq, &bu, a, da, trace, dq, &du, &tu);
+        REAL G = g_at(model, d, th, a, Bu, bu, du, tu, Hi, Fi, x, r, b);
         ps_add(&ps, i < npts - 1 - orc_ll_skip ? G * dt : (REAL)0);
         REAL Mg[9], cg[3];
         guide_coeffs(model, d, th, a, Hi, Fi, Mg, cg, unit);
@@ -498,10 +512,11 @@ REAL SFX(orc_path_ll_segment)(int model, int d, int m, const double* law, int np
     for (int i = 0; i < npts - 1; ++i) {
         REAL dt = t[i + 1] - t[i];
         REAL r[3] = {0, 0, 0}, b[3] = {0, 0, 0};
-        REAL Bq[9], bq[3];
-        const REAL* bu;
-        const REAL* Bu = aux_coeffs(law, model, d, i, Bt, beta, Bq, bq, &bu);
-        REAL G = g_at(model, d, th, a, Bu, bu, da, trace, H + (size_t)i * h,
+        REAL Bq[9], bq[3], dq[6];
+        const REAL *bu, *du;
+        int tu;
+        const REAL* Bu = aux_coeffs(law, model, d, i, Bt, beta, Bq, bq, &bu, a, da, trace, dq, &du, &tu);
+        REAL G = g_at(model, d, th, a, Bu, bu, du, tu, H + (size_t)i * h,
                       F + (size_t)i * d, X + (size_t)i * d, r, b);
         ps_add(&ps, G * dt);
     }
@@ -1027,18 +1042,24 @@ static int fm_combine(const ftr_t* q, fm_t* Hc, double* Fc, double* cc) {
  * (stage k: Q_l <- compose(Q_l, Q_{l+k}) if l + k < cnt, previous-stage values), then every
  * point of the chunk by one combine from the chunk end's (H, F, c). */
 #define FILT_CHUNK 64
-/* aux: NULL (B~ = Bt, beta~ = beta on every step) or [npts][d*d + d] per-point coefficients
- * of a time-dependent auxiliary law; step i's exact transition takes the trapezoidal average
- * (row i + row i+1) * 0.5 — a second-order scheme for the filter ODEs (libdmt filt_aux_step,
- * dmt_guiding_linear_td). */
+/* aux: NULL (B~ = Bt, beta~ = beta on every step) or [npts][ncols] per-point coefficients of
+ * a time-dependent auxiliary law — B~, beta~ (ncols = d*d + d; a~ = at) or B~, beta~, a~
+ * packed (ncols = d*d + d + hp; at unused); step i's exact transition takes the trapezoidal
+ * averages (row i + row i+1) * 0.5 — a second-order scheme for the filter ODEs (libdmt
+ * filt_aux_step, dmt_guiding_linear_td(a)). */
 static int backward_filter(int d, const double* Bt, const double* beta, const double* aux,
-                           const double* at, int npts, const double* t, const double* HT,
-                           const double* FT, double cT, double* H, double* F, double* c) {
+                           int ncols, const double* at, int npts, const double* t,
+                           const double* HT, const double* FT, double cT, double* H, double* F,
+                           double* c) {
     int hp = d * (d + 1) / 2;
+    const int tda = aux && ncols == d * d + d + hp;
     fm_t B = fm_zero(d), A = fm_zero(d), Hc = fm_zero(d);
     if (!aux) for (int i = 0; i < d * d; ++i) B.a[i] = Bt[i];
     for (int i = 0; i < d; ++i)
-        for (int j = 0; j < d; ++j) { A.a[i * d + j] = at[pidx(d, i, j)]; Hc.a[i * d + j] = HT[pidx(d, i, j)]; }
+        for (int j = 0; j < d; ++j) {
+            A.a[i * d + j] = tda ? 0.0 : at[pidx(d, i, j)];
+            Hc.a[i * d + j] = HT[pidx(d, i, j)];
+        }
     double Fc[3] = {0, 0, 0}, cc = cT;
     for (int i = 0; i < d; ++i) Fc[i] = FT[i];
 #define FILT_STORE(i, Hm, Fv, cv)                                                              \
@@ -1056,11 +1077,17 @@ static int backward_filter(int d, const double* Bt, const double* beta, const do
             const double* bl = beta;
             double bavg[3];
             if (aux) {  /* step lo + l: trapezoidal average of rows lo + l and lo + l + 1 */
-                const double* r0 = aux + (size_t)(lo + l) * (d * d + d);
-                const double* r1 = r0 + (d * d + d);
+                const double* r0 = aux + (size_t)(lo + l) * ncols;
+                const double* r1 = r0 + ncols;
                 for (int i = 0; i < d * d; ++i) B.a[i] = (r0[i] + r1[i]) * 0.5;
                 for (int i = 0; i < d; ++i) bavg[i] = (r0[d * d + i] + r1[d * d + i]) * 0.5;
                 bl = bavg;
+                if (tda)
+                    for (int i = 0; i < d; ++i)
+                        for (int j = 0; j < d; ++j) {
+                            const int e = d * d + d + pidx(d, i, j);
+                            A.a[i * d + j] = (r0[e] + r1[e]) * 0.5;
+                        }
             }
             fm_transition(&B, bl, &A, t[lo + l + 1] - t[lo + l], &Q[l].Phi, Q[l].mu, &Q[l].K);
         }
@@ -1084,12 +1111,19 @@ static int backward_filter(int d, const double* Bt, const double* beta, const do
 int orc_backward_filter_segment(int d, const double* Bt, const double* beta, const double* at,
                                 int npts, const double* t, const double* HT, const double* FT,
                                 double cT, double* H, double* F, double* c) {
-    return backward_filter(d, Bt, beta, 0, at, npts, t, HT, FT, cT, H, F, c);
+    return backward_filter(d, Bt, beta, 0, 0, at, npts, t, HT, FT, cT, H, F, c);
 }
 int orc_backward_filter_segment_td(int d, const double* aux, const double* at, int npts,
                                    const double* t, const double* HT, const double* FT,
                                    double cT, double* H, double* F, double* c) {
-    return backward_filter(d, 0, 0, aux, at, npts, t, HT, FT, cT, H, F, c);
+    return backward_filter(d, 0, 0, aux, d * d + d, at, npts, t, HT, FT, cT, H, F, c);
+}
+
+int orc_backward_filter_segment_tda(int d, const double* aux, int npts, const double* t,
+                                    const double* HT, const double* FT, double cT, double* H,
+                                    double* F, double* c) {
+    return backward_filter(d, 0, 0, aux, d * d + d + d * (d + 1) / 2, 0, npts, t, HT, FT, cT,
+                           H, F, c);
 }
 /* the canonical log kernel, exposed for the Python container restatement */
 double orc_rng_log(double u) { return rng_log(u); }

@@ -129,6 +129,8 @@ def _load():
     lib.orc_backward_filter_segment.restype = i_
     lib.orc_backward_filter_segment_td.argtypes = [i_, P, P, i_, P, P, P, d_, P, P, P]
     lib.orc_backward_filter_segment_td.restype = i_
+    lib.orc_backward_filter_segment_tda.argtypes = [i_, P, i_, P, P, P, d_, P, P, P]
+    lib.orc_backward_filter_segment_tda.restype = i_
     lib.orc_set_aux.argtypes = [P]
     lib.orc_set_aux.restype = None
     lib.orc_rng_log.argtypes = [d_]
@@ -157,8 +159,8 @@ def _sfx(prec):
 
 # ------------------------------------------------------------------ per-segment numerics
 class _aux_rows:
-    """The segment's time-dependent auxiliary coefficients (rows [npts][d·d + d], doubles) for
-    the C calls inside the block (orc_set_aux), or nothing."""
+    """The segment's time-dependent auxiliary coefficients (rows [npts][d·d + d + d(d+1)/2] =
+    B̃, β̃, ã packed, doubles) for the C calls inside the block (orc_set_aux), or nothing."""
 
     def __init__(self, aux):
         self.aux = None if aux is None else np.ascontiguousarray(aux, dtype=np.float64)
@@ -215,6 +217,22 @@ def backward_filter_segment_td(d, aux, at_packed, t, HT_packed, FT, cT):
     assert args[0].shape == (n, d * d + d)
     ok = lib.orc_backward_filter_segment_td(d, _p(args[0]), _p(args[1]), n, _p(t), _p(args[2]),
                                             _p(args[3]), float(cT), _p(H), _p(F), _p(c))
+    if not ok:
+        raise FloatingPointError("singular I + HK in the backward filter")
+    return H, F, c
+
+
+def backward_filter_segment_tda(d, aux, t, HT_packed, FT, cT):
+    """The filter with a time-dependent ã too: aux[npts][d·d + d + d(d+1)/2] = B̃, β̃, ã packed,
+    step i taking the trapezoidal averages of rows i and i + 1 (dmt_guiding_linear_tda)."""
+    t = np.ascontiguousarray(t, dtype=np.float64)
+    n = t.size
+    hp = d * (d + 1) // 2
+    H = np.empty((n, hp)); F = np.empty((n, d)); c = np.empty(n)
+    args = [np.ascontiguousarray(a, dtype=np.float64) for a in (aux, HT_packed, FT)]
+    assert args[0].shape == (n, d * d + d + hp)
+    ok = lib.orc_backward_filter_segment_tda(d, _p(args[0]), n, _p(t), _p(args[1]), _p(args[2]),
+                                             float(cT), _p(H), _p(F), _p(c))
     if not ok:
         raise FloatingPointError("singular I + HK in the backward filter")
     return H, F, c
@@ -484,15 +502,24 @@ class OracleEnsemble:
                 otab[g] = copy.deepcopy(tab[g])
 
     def upload_aux(self, kind, aux):
-        """dmt_upload_aux: per-point B̃(t_i), β̃(t_i) ([P][d·d + d]) of the laws of `kind`, u and u°
-        alike, held in the working precision (as the device holds them) for the segments whose
-        record has auxtd set; None removes them.  Non-linear drifts only."""
+        """dmt_upload_aux(_a): per-point B̃(t_i), β̃(t_i) ([P][d·d + d]) — or B̃, β̃, ã(t_i) packed
+        ([P][d·d + d + d(d+1)/2]) — of the laws of `kind`, u and u° alike, held in the working
+        precision (as the device holds them; ã zero where not given) for the segments whose
+        record has auxtd set (2: ã from the table too); None removes them.  Non-linear drifts
+        only."""
         if self.model == MODEL_OU:
             raise ValueError("time-dependent auxiliary laws: non-linear drifts only")
-        C_ = self.d * self.d + self.d
-        self.aux[kind] = (None if aux is None else
-                          np.asarray(aux, dtype=np.float64).reshape(self.P, C_)
-                          .astype(self.dt).astype(np.float64))
+        if aux is None:
+            self.aux[kind] = None
+            return
+        nb = self.d * self.d + self.d
+        na = nb + self.d * (self.d + 1) // 2
+        a = np.asarray(aux, dtype=np.float64).reshape(self.P, -1)
+        if a.shape[1] not in (nb, na):
+            raise ValueError("aux needs d·d + d or d·d + d + d(d+1)/2 columns")
+        full = np.zeros((self.P, na))
+        full[:, :a.shape[1]] = a
+        self.aux[kind] = full.astype(self.dt).astype(np.float64)
 
     def _aux_seg(self, bk, g):
         """The segment's rows of its law kind's table when its record is time-dependent."""
@@ -801,8 +828,12 @@ class OracleEnsemble:
                 beta = rec[40:40 + d]
                 at = rec[25:25 + hp] - rec[43:43 + hp]
                 kind = 1 if last_b else 0
-                if rec[L_AUXTD] != 0.0 and self.aux[kind] is not None:
+                if rec[L_AUXTD] == 2.0 and self.aux[kind] is not None:
                     rows = self.aux[kind][self.pt_off[g]: self.pt_off[g] + self.npts[g]]
+                    H, F, c = backward_filter_segment_tda(d, rows, self.t[g].astype(np.float64),
+                                                          packed_sym(HT), FT, cT)
+                elif rec[L_AUXTD] != 0.0 and self.aux[kind] is not None:
+                    rows = self.aux[kind][self.pt_off[g]: self.pt_off[g] + self.npts[g], :d * d + d]
                     H, F, c = backward_filter_segment_td(d, rows, at, self.t[g].astype(np.float64),
                                                          packed_sym(HT), FT, cT)
                 else:

@@ -329,6 +329,144 @@ __global__ __launch_bounds__(64) void k_probe_pk(const Args a) {
   a.ll[r] = (double)ll + (double)x[0];
 }
 
+// Full lane packets with the outputs staged in LDS (k_probe_lds): per packet of P steps each
+// lane writes its X°/W° values to its own LDS rows step by step and, at the packet's end, reads
+// them back as 16-byte pieces and stores whole packets (P·4 B per component: 128 B for P = 32,
+// one lane per 128-byte line); u.W's next packet is loaded piece by piece into the registers
+// just consumed (one packet ahead).  SEL: 0 uniform, 1 mixed.
+template <int P, int SEL>
+__global__ __launch_bounds__(64) void k_probe_lds(const Args a) {
+  constexpr int NV = P / 4, C6 = D + M;
+  __shared__ float stage[C6][P][65];  // [component][step][lane] (+1: conflict-free)
+  const int lane = threadIdx.x;
+  const int64_t tile = blockIdx.x;
+  const int64_t r = tile * 64 + lane;
+  const int64_t tb = tile * a.rows;
+  const int64_t pbD = tb * D * 64, pbM = tb * M * 64;
+  const int u = SEL == 0 ? 0 : a.u[r];
+  const int pbuf = 1 - u;
+  const T* Ws = a.W[u] + pbM;
+  T* Wd = a.W[pbuf] + pbM;
+  T* Xd = a.X[pbuf] + pbD;
+  const T* Hb = a.H + tb * HP * 64 + lane;
+  const T* Fb = a.F + tb * D * 64 + lane;
+  Law<Mdl, T> L;
+  L.th[0] = 10; L.th[1] = 28; L.th[2] = 8.0f / 3;
+  for (int i = 0; i < D * D; ++i) L.Bt[i] = (i % 4 == 0) ? -1.0f : 0.1f;
+  for (int i = 0; i < D; ++i) L.beta[i] = 0.5f;
+  for (int i = 0; i < HP; ++i) L.da[i] = 0;
+  L.trace = false;
+  L.unit = true;
+  L.auxtd = false;
+  T x[D] = {1.0f, 1.0f, 20.0f};
+  T tcur = a.t[0];
+  T ll = 0;
+  const T rho = 0.9f, srho = sqrtf(1 - 0.81f);
+  const uint32_t seg = (uint32_t)r;
+  auto pk = [&](const T* base, int64_t j, int c, int C) -> const float4* {
+    return (const float4*)&base[(((j + 1) * C + c) * 64 + lane) * P];
+  };
+  auto pkw = [&](T* base, int64_t j, int c, int C) -> float4* {
+    return (float4*)&base[(((j + 1) * C + c) * 64 + lane) * P];
+  };
+  float4 wc[M][NV];
+#pragma unroll
+  for (int k = 0; k < M; ++k)
+#pragma unroll
+    for (int v = 0; v < NV; ++v) wc[k][v] = pk(Ws, 0, k, M)[v];
+  struct Chunk {
+    T t[K], H[K][HP], F[K][D];
+  };
+  auto load = [&](int c0, Chunk& c) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const int64_t i = c0 + j;
+      c.t[j] = a.t[i + 1];
+#pragma unroll
+      for (int e = 0; e < HP; ++e) c.H[j][e] = Hb[(i * HP + e) * 64];
+#pragma unroll
+      for (int e = 0; e < D; ++e) c.F[j][e] = Fb[(i * D + e) * 64];
+    }
+  };
+  const int npk = a.nst / P;
+  Chunk cur, nxt;
+  load(0, cur);
+  for (int j = 0; j < npk; ++j) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int c0 = j * P + 4 * v;
+      load(c0 + K, nxt);
+      T Z[K][M];
+#pragma unroll
+      for (int bq = 0; bq < K * M / 4; ++bq) {
+        T zb[4];
+        normal_block(philox4x32_10(U4{(uint32_t)(c0 * M / 4 + bq), seg, a.iter, 0u}, 0x1234u, 0x5678u),
+                     zb);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) Z[(4 * bq + e) / M][(4 * bq + e) % M] = zb[e];
+      }
+      T g[K];
+#pragma unroll
+      for (int q = 0; q < K; ++q) {
+        const T dt = cur.t[q] - tcur;
+        const T sdt = sqrtf(dt);
+        T dW[M];
+#pragma unroll
+        for (int k = 0; k < M; ++k) {
+          const float4 w4 = wc[k][v];
+          const T wu = q == 0 ? w4.x : q == 1 ? w4.y : q == 2 ? w4.z : w4.w;
+          dW[k] = dfma(rho, wu, srho * (sdt * Z[q][k]));
+        }
+        T rr[D], b[D], Mg[D * D], cg[D];
+        const T G = g_at<Mdl, T>(L, cur.H[q], cur.F[q], x, rr, b);
+        guide_coeffs_unit<Mdl, T>(cur.H[q], cur.F[q], Mg, cg);
+        euler_step<Mdl, T>(Mg, cg, b, dt, dW, x);
+        tcur = cur.t[q];
+        g[q] = G * dt;
+#pragma unroll
+        for (int p = 0; p < D; ++p) stage[p][4 * v + q][lane] = x[p];
+#pragma unroll
+        for (int k = 0; k < M; ++k) stage[D + k][4 * v + q][lane] = dW[k];
+      }
+      ll += (g[0] + g[1]) + (g[2] + g[3]);
+#pragma unroll
+      for (int k = 0; k < M; ++k) wc[k][v] = pk(Ws, j + 1, k, M)[v];  // next packet's piece
+      cur = nxt;
+    }
+#pragma unroll
+    for (int c = 0; c < C6; ++c) {
+      float4* dst = c < D ? pkw(Xd, j, c, D) : pkw(Wd, j, c - D, M);
+#pragma unroll
+      for (int v = 0; v < NV; ++v)
+        dst[v] = make_float4(stage[c][4 * v][lane], stage[c][4 * v + 1][lane],
+                             stage[c][4 * v + 2][lane], stage[c][4 * v + 3][lane]);
+    }
+  }
+  a.ll[r] = (double)ll + (double)x[0];
+}
+
+template <int P, int SEL>
+static double run_lds(const Args& a, int ntiles, int reps, const char* name) {
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  k_probe_lds<P, SEL><<<ntiles, 64>>>(a);
+  CHECK(hipGetLastError());
+  CHECK(hipDeviceSynchronize());
+  CHECK(hipEventRecord(e0));
+  for (int i = 0; i < reps; ++i) k_probe_lds<P, SEL><<<ntiles, 64>>>(a);
+  CHECK(hipEventRecord(e1));
+  CHECK(hipEventSynchronize(e1));
+  float ms;
+  CHECK(hipEventElapsedTime(&ms, e0, e1));
+  const double us = ms * 1e3 / reps;
+  const double steps = (double)ntiles * 64 * (a.nst / P) * P;
+  printf("{\"variant\": \"%s\", \"P\": %d, \"sel\": %d, \"us_per_draw\": %.1f, \"frac_72B\": %.3f}\n",
+         name, P, SEL, us, steps * 72 / (us * 1e-6) / 8e12);
+  fflush(stdout);
+  return us;
+}
+
 template <int P, int SEL>
 static double run_pk(const Args& a, int ntiles, int reps, const char* name) {
   hipEvent_t e0, e1;
@@ -423,6 +561,10 @@ int main(int argc, char** argv) {
     if (want("pk8f_mixed")) run_pk<8, 1>(a, ntiles, reps, "pk8f_mixed");
     if (want("pk16f_uniform")) run_pk<16, 0>(a, ntiles, reps, "pk16f_uniform");
     if (want("pk16f_mixed")) run_pk<16, 1>(a, ntiles, reps, "pk16f_mixed");
+    if (want("pk16l_uniform")) run_lds<16, 0>(a, ntiles, reps, "pk16l_uniform");
+    if (want("pk16l_mixed")) run_lds<16, 1>(a, ntiles, reps, "pk16l_mixed");
+    if (want("pk32l_uniform")) run_lds<32, 0>(a, ntiles, reps, "pk32l_uniform");
+    if (want("pk32l_mixed")) run_lds<32, 1>(a, ntiles, reps, "pk32l_mixed");
   }
   return 0;
 }

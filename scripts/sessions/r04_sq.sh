@@ -10,7 +10,11 @@ P1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_
 P2="SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VALU_FMA_F64"
 B5="python bench.py --config c5 --steps 4 --warmup 2 --no-cpu-baseline --calls-iters 0 --repeats 0"
 B3="python bench.py --config c3 --steps 4 --warmup 2 --no-cpu-baseline --calls-iters 0 --repeats 0"
+P=scripts/c5_layout_probe
 scripts/gpu_session.sh \
+ "timeout -k 10 90 $P 512 10 pk > $O/probe.jsonl 2> $O/probe.err" \
+ "timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_pfetch -o f --output-format csv -- $P 512 2 pk > $O/pmc_pfetch.log 2>&1" \
+ "timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_pwrite -o w --output-format csv -- $P 512 2 pk > $O/pmc_pwrite.log 2>&1" \
  "timeout -k 10 150 $K --config c5 --accept > $O/c5_roll.json 2> $O/c5_roll.err" \
  "DMT_LIB_PATH=build_variants/libdmt_noroll.so timeout -k 10 150 $K --config c5 --accept > $O/c5_noroll.json 2> $O/c5_noroll.err" \
  "timeout -k 10 150 $K --config c5 --accept > $O/c5_roll2.json 2> $O/c5_roll2.err" \

@@ -121,18 +121,20 @@ def test_td_filter_matches_an_independent_ode_solution():
     assert np.max(np.abs(F[0] - F0)) < 1e-5 * max(1.0, np.max(np.abs(F0)))
 
 
-def _flag_segments(ens, kinds, segs):
-    """Set DMT_LAW_AUXTD in the law records of `segs` (both units, the given kinds)."""
+def _flag_segments(ens, kinds, segs, value=1.0):
+    """Set DMT_LAW_AUXTD (1: B̃, β̃ from the table; 2: ã too) in the law records of `segs`
+    (both units, the given kinds)."""
     for unit in (L.U, L.UPROP):
         for kind in kinds:
             laws = ens.download_law(unit, kind)[2].copy()
-            laws[segs, L.LAW_AUXTD] = 1.0
+            laws[segs, L.LAW_AUXTD] = value
             ens.upload_law(unit, kind, laws=laws)
 
 
-def _tables(case, ens, vary=True):
-    """Per-point aux tables of both kinds: each segment's record B̃, β̃, plus (vary) a
-    time-varying perturbation — for the PPb laws a different one."""
+def _tables(case, ens, vary=True, with_a=False):
+    """Per-point aux tables of both kinds: each segment's record B̃, β̃ (and with_a: ã = a − (a −
+    ã) of the record, packed), plus (vary) a time-varying perturbation — for the PPb laws a
+    different one; ã's varies the noise coordinate's variance."""
     t = case["t"]
     out = []
     for kind, laws in ((L.LAW_PP, case["laws"]), (L.LAW_PPB, case["lawsb"])):
@@ -141,20 +143,22 @@ def _tables(case, ens, vary=True):
             rec = laws[g]
             Bt = rec[L.LAW_BT:L.LAW_BT + 4].reshape(2, 2)
             be = rec[L.LAW_BETA:L.LAW_BETA + 2]
+            at = rec[L.LAW_A:L.LAW_A + 3] - rec[L.LAW_DA:L.LAW_DA + 3]
             off = int(np.sum(np.concatenate(case["n_points"])[:g]))
             for tt in t[off:off + n]:
                 if vary:
                     s = np.sin(7.0 * tt + g + kind)
                     Bq = Bt + s * np.array([[0.3, -0.1], [0.2, 0.0]])
                     bq = be + np.array([0.4 * np.cos(5.0 * tt), 0.1 * s])
+                    aq = at * np.array([1.0, 1.0, 1.0 + 0.3 * np.cos(3.0 * tt + g)])
                 else:
-                    Bq, bq = Bt, be
-                rows.append(np.concatenate([Bq.ravel(), bq]))
+                    Bq, bq, aq = Bt, be, at
+                rows.append(np.concatenate([Bq.ravel(), bq] + ([aq] if with_a else [])))
         out.append(np.array(rows))
     return out
 
 
-def _td_pair(mapping, prec, vary=True, segs=None, oracle_only=False):
+def _td_pair(mapping, prec, vary=True, segs=None, oracle_only=False, with_a=False):
     case = cs.ragged_case(prec=prec)
     m = case["model"]
     ens = []
@@ -164,11 +168,11 @@ def _td_pair(mapping, prec, vary=True, segs=None, oracle_only=False):
     ens.append(orc.OracleEnsemble(m.kind, m.d, m.m, case["n_points"], prec=prec, seed=11))
     G = int(sum(case["nsegs"]))
     segs = np.arange(0, G, 2) if segs is None else segs
-    tabs = _tables(case, ens[0], vary)
+    tabs = _tables(case, ens[0], vary, with_a)
     for e in ens:
         cs.load_ragged(e, case)
         e.upload_obs(case["Hobs"], case["Fobs"], case["cobs"])
-        _flag_segments(e, (L.LAW_PP, L.LAW_PPB), segs)
+        _flag_segments(e, (L.LAW_PP, L.LAW_PPB), segs, 2.0 if with_a else 1.0)
         e.upload_aux(L.LAW_PP, tabs[0])
         e.upload_aux(L.LAW_PPB, tabs[1])
     layA = dict(n_blocks=[2, 3, 2], seg_first=[0, 2, 0, 2, 4, 0, 3], seg_last=[1, 3, 1, 3, 5, 2, 4],
@@ -248,11 +252,105 @@ def test_upload_aux_rejected_for_ou_oracle():
         o.upload_aux(L.LAW_PP, np.zeros((11, 6)))
 
 
+def _law2a():
+    """_law2 with a time-dependent ã(t) = σ̃σ̃ᵀ(t) too (σ̃ = (0, 0.3(1 + 0.4 sin 2t)))."""
+    B, beta, _ = _law2()
+    at = lambda t: np.array([0.0, 0.0, (0.3 * (1.0 + 0.4 * np.sin(2.0 * t))) ** 2])  # noqa: E731
+    return B, beta, at
+
+
+def _table_a(B, beta, at, t):
+    return np.stack([np.concatenate([B(x).ravel(), beta(x), at(x)]) for x in t])
+
+
+def test_tda_filter_host_equals_oracle_and_constant_equals_td():
+    B, beta, at = _law2a()
+    t = np.sort(np.concatenate([[0.0, 1.0], np.random.default_rng(5).uniform(0, 1, 150)]))
+    HT, FT, cT = _end_info()
+    h = dmt.guiding_linear_tda(_table_a(B, beta, at, t), t, HT, FT, cT)
+    o = orc.backward_filter_segment_tda(2, _table_a(B, beta, at, t), t, HT, FT, cT)
+    for a_, b_ in zip(h, o):
+        assert np.array_equal(a_, b_)
+    # a constant ã column is the ã of dmt_guiding_linear_td, bit for bit
+    a0 = at(0.0)
+    hc = dmt.guiding_linear_tda(_table_a(B, beta, lambda x: a0, t), t, HT, FT, cT)
+    ht = dmt.guiding_linear_td(_table(B, beta, t), a0, t, HT, FT, cT)
+    for a_, b_ in zip(hc, ht):
+        assert np.array_equal(a_, b_)
+    assert not np.array_equal(h[0], ht[0])
+
+
+def test_tda_filter_converges_to_the_ode_at_second_order():
+    """With ã(t) time-dependent as well, the trapezoidal step transition still converges at
+    second order to SURVEY.md A.5's backward ODEs (here integrated independently with
+    solve_ivp, ã(t) in the Riccati term)."""
+    from scipy.integrate import solve_ivp
+    B, beta, at = _law2a()
+    HT, FT, cT = _end_info()
+
+    def rhs(t, y):
+        H = y[:4].reshape(2, 2)
+        F = y[4:6]
+        Bt, bt, A = B(t), beta(t), orc.unpacked(at(t), 2)
+        dH = -Bt.T @ H - H @ Bt + H @ A @ H
+        dF = -Bt.T @ F + H @ A @ F + H @ bt
+        dc = bt @ F + 0.5 * F @ A @ F - 0.5 * np.trace(A @ H)
+        return np.concatenate([dH.ravel(), dF, [dc]])
+
+    sol = solve_ivp(rhs, (1.0, 0.0), np.concatenate([orc.unpacked(HT, 2).ravel(), FT, [cT]]),
+                    rtol=1e-12, atol=1e-12)
+    ref = np.concatenate([orc.packed_sym(sol.y[:4, -1].reshape(2, 2)), sol.y[4:6, -1]])
+
+    def at_t0(n):
+        t = np.linspace(0.0, 1.0, n + 1)
+        H, F, _ = dmt.guiding_linear_tda(_table_a(B, beta, at, t), t, HT, FT, cT)
+        return np.concatenate([H[0], F[0]])
+
+    errs = [np.max(np.abs(at_t0(n) - ref)) for n in (32, 64, 128, 256)]
+    for e0, e1 in zip(errs, errs[1:]):
+        assert 3.3 < e0 / e1 < 4.8, errs
+
+
+def test_oracle_tda_with_the_records_a_equals_td():
+    """An ã column equal to each record's own ã (FHN: ã = a, so a − ã(t_i) = 0 exactly and the
+    trace term adds fma(−½, 0, G) = G) runs the blocking loop bit-identically to the B̃, β̃-only
+    table (DMT_LAW_AUXTD 2 vs 1) on the oracle."""
+    segs = np.arange(sum(cs.ragged_case()["nsegs"]))
+    _, (ta,), ids = _td_pair(None, L.F64, vary=False, oracle_only=True, segs=segs, with_a=True)
+    _, (t1,), _ = _td_pair(None, L.F64, vary=False, oracle_only=True, segs=segs)
+    for e in (ta, t1):
+        _fixed_aux(e)
+    a = _blocking_loop([ta], ids, ta.S, 4, np.random.default_rng(2))
+    b = _blocking_loop([t1], ids, t1.S, 4, np.random.default_rng(2))
+    for x, y in zip(a, b):
+        assert np.array_equal(x[0], y[0])
+    cs.assert_paths_equal(ta, t1)
+    for lid, nb in ids:
+        cs.assert_ll_equal(ta, t1, lid, nb)
+
+
+def test_oracle_varying_a_enters_girsanov_and_filter():
+    """A varying ã(t) changes both the guiding term and the Girsanov weights (oracle)."""
+    segs = np.arange(sum(cs.ragged_case()["nsegs"]))
+    _, (ta,), ids = _td_pair(None, L.F64, vary=True, oracle_only=True, segs=segs, with_a=True)
+    _, (t1,), _ = _td_pair(None, L.F64, vary=True, oracle_only=True, segs=segs)
+    lid, nb = ids[0]
+    for e in (ta, t1):
+        e.set_obs(lid, 0, nb)
+        e.recompute_guiding_term(lid, 0, nb, unit=L.U)
+    assert not np.array_equal(ta.download_law(L.U, L.LAW_PP)[0], t1.download_law(L.U, L.LAW_PP)[0])
+    for e in (ta, t1):
+        e.upload_law(L.U, L.LAW_PP, H=t1.download_law(L.U, L.LAW_PP)[0])
+        e.loglikhd(lid, L.U, 0, nb)
+    assert not np.array_equal(ta.block_ll(lid, 0, nb)[0], t1.block_ll(lid, 0, nb)[0])
+
+
 @pytest.mark.gpu
+@pytest.mark.parametrize("with_a", [False, True], ids=["Bbeta", "Bbeta_a"])
 @pytest.mark.parametrize("prec", [L.F64, L.F32], ids=["f64", "f32"])
 @pytest.mark.parametrize("mapping", MAPPINGS, ids=["lane", "wave"])
-def test_td_aux_blocking_loop_device_equals_oracle(mapping, prec):
-    case, (dev, ora), ids = _td_pair(mapping, prec)
+def test_td_aux_blocking_loop_device_equals_oracle(mapping, prec, with_a):
+    case, (dev, ora), ids = _td_pair(mapping, prec, with_a=with_a)
     rng = np.random.default_rng(8)
     res = _blocking_loop([dev, ora], ids, dev.S, 6, rng)
     for i, (ad, ao) in enumerate(res):
