@@ -508,6 +508,13 @@ __global__ __launch_bounds__(64) void k_block(const BlockArgs<T> a) {
   lane_block<Mdl, T, MODE, PARITY, K, false, TD>(a, tile, blk, threadIdx.x, 0);
 }
 
+template <class Mdl, class T>
+struct PairChunk {  // steps per chunk: an even number of whole Philox blocks of normals
+  static constexpr int NPB = NormPerBlock<T>::v;
+  static constexpr int v = ((DMT_KCHUNK_PAIR_BASE * Mdl::M) % (2 * NPB) == 0)
+                               ? DMT_KCHUNK_PAIR_BASE : 2 * DMT_KCHUNK_PAIR_BASE;
+};
+
 // ---- MAP_LANE with lane packets (fp32 ensembles, BlockArgs::pk = kPathPacket).
 // The path planes X, W hold each lane's PK consecutive points of a component as one 64-byte
 // piece (plane_ix), so the per-lane buffers of u and u° (two, selected per segment exactly as
@@ -524,7 +531,13 @@ __global__ __launch_bounds__(64) void k_block(const BlockArgs<T> a) {
 #ifndef DMT_PK_ROLL  // 1: u.W's next packet loaded piece by piece into the registers just consumed
 #define DMT_PK_ROLL 1   // 0: the whole next packet in a second register set
 #endif
-template <class Mdl, class T, int MODE, bool PARITY, int K, bool TD, int PK, bool FAST>
+// PAIR (k_block_pk_pair): two lanes (roles) of a wave per recording, l and l + 32 — each draws
+// every other Philox block of a chunk and the pair swaps halves (pair_exchange), both run the
+// recursion on the same values; role 0 stores X°, role 1 W° (every load is the same address
+// for both, one request).  Fills the chip with twice the waves when the ensemble has fewer
+// recording tiles than SIMDs (C5: 512 tiles, 1 024 SIMDs).  Bit-identical.
+template <class Mdl, class T, int MODE, bool PARITY, int K, bool TD, int PK, bool FAST,
+          bool PAIR = false>
 __device__ __forceinline__ bool run_segment_pk(const Law<Mdl, T>& L, const T* __restrict__ tpl,
                                                const int t_sh, const T* __restrict__ Ht,
                                                const int H_sh, const T* __restrict__ Ft,
@@ -533,10 +546,11 @@ __device__ __forceinline__ bool run_segment_pk(const Law<Mdl, T>& L, const T* __
                                                NormalStream<T>& ns, const int64_t tq,
                                                const int64_t q0, const int np, const int lane,
                                                const T rho, const T srho, const int ll_skip,
-                                               T* x, T& sl, T* stg) {
+                                               T* x, T& sl, T* stg, const int role = 0) {
   constexpr int D = Mdl::D, M = Mdl::M, HP = D * (D + 1) / 2;
   constexpr bool DRAW = MODE != MODE_RECOMPUTE;
   constexpr bool READW = MODE != MODE_FRESH;
+  const bool stx = !PAIR || role == 0, stw = DRAW && (!PAIR || role == 1);  // who stores what
   constexpr int VE = 16 / (int)sizeof(T);  // elements per 16-byte piece
   constexpr int NV = PK / VE;              // pieces per packet
   static_assert(PK % K == 0 && K % VE == 0 && (K * M) % 2 == 0 && 64 % K == 0,
@@ -561,9 +575,11 @@ __device__ __forceinline__ bool run_segment_pk(const Law<Mdl, T>& L, const T* __
   const bool all_unit = !Mdl::kLinear && __ballot(L.unit) == __ballot(1);
 #endif
   T tcur = tb[0];
+  if (stx) {
 #pragma unroll
-  for (int p = 0; p < D; ++p) Xd[pix(0, p, D)] = x[p];
-  if (DRAW) {
+    for (int p = 0; p < D; ++p) Xd[pix(0, p, D)] = x[p];
+  }
+  if (stw) {
 #pragma unroll
     for (int k = 0; k < M; ++k) {
       const T w0 = READW ? Ws[pix(0, k, M)] : (T)0;
@@ -633,13 +649,31 @@ __device__ __forceinline__ bool run_segment_pk(const Law<Mdl, T>& L, const T* __
     if (DRAW && !PARITY) {
       constexpr int NPB = NormPerBlock<T>::v;
       static_assert((K * M) % NPB == 0, "chunk must hold whole normal blocks");
+      if constexpr (PAIR) {  // role r draws blocks 2j + r; the pair swaps halves
+        static_assert((K * M / NPB) % 2 == 0, "a pair chunk holds an even number of blocks");
 #pragma unroll
-      for (int bq = 0; bq < K * M / NPB; ++bq) {
-        const uint32_t bc = (uint32_t)((c0 * M) / NPB + bq);
-        T zb[NPB];
-        normal_block(philox4x32_10(U4{bc, ns.seg, ns.iter, ns.c3}, ns.k0, ns.k1), zb);
+        for (int j = 0; j < K * M / NPB / 2; ++j) {
+          const uint32_t bc = (uint32_t)((c0 * M) / NPB + 2 * j + role);
+          T zb[NPB];
+          normal_block(philox4x32_10(U4{bc, ns.seg, ns.iter, ns.c3}, ns.k0, ns.k1), zb);
 #pragma unroll
-        for (int e = 0; e < NPB; ++e) c.Z[(NPB * bq + e) / M][(NPB * bq + e) % M] = zb[e];
+          for (int e = 0; e < NPB; ++e) {
+            T lo, hi;
+            pair_exchange<T>(zb[e], lo, hi);
+            const int n0 = NPB * (2 * j) + e, n1 = NPB * (2 * j + 1) + e;
+            c.Z[n0 / M][n0 % M] = lo;
+            c.Z[n1 / M][n1 % M] = hi;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int bq = 0; bq < K * M / NPB; ++bq) {
+          const uint32_t bc = (uint32_t)((c0 * M) / NPB + bq);
+          T zb[NPB];
+          normal_block(philox4x32_10(U4{bc, ns.seg, ns.iter, ns.c3}, ns.k0, ns.k1), zb);
+#pragma unroll
+          for (int e = 0; e < NPB; ++e) c.Z[(NPB * bq + e) / M][(NPB * bq + e) % M] = zb[e];
+        }
       }
     }
   };
@@ -687,9 +721,11 @@ __device__ __forceinline__ bool run_segment_pk(const Law<Mdl, T>& L, const T* __
 #pragma unroll
             for (int k = 0; k < M; ++k) dW[k] = READW ? wc[k][e / VE][e % VE] : (T)0;
             gv[q] = step(c0 + q, cur.t[q], cur.H[q], cur.F[q], dW, cur.Z[q]);
+            if (stx) {
 #pragma unroll
-            for (int p = 0; p < D; ++p) st(p, e) = x[p];
-            if (DRAW) {
+              for (int p = 0; p < D; ++p) st(p, e) = x[p];
+            }
+            if (stw) {
 #pragma unroll
               for (int k = 0; k < M; ++k) st(D + k, e) = dW[k];
             }
@@ -714,13 +750,15 @@ __device__ __forceinline__ bool run_segment_pk(const Law<Mdl, T>& L, const T* __
           for (int u = 0; u < VE; ++u) o[u] = st(c, v * VE + u);
           return o;
         };
+        if (stx) {
 #pragma unroll
-        for (int p = 0; p < D; ++p) {
-          v16* dst = (v16*)&Xd[pix((int64_t)j * PK + 1, p, D)];
+          for (int p = 0; p < D; ++p) {
+            v16* dst = (v16*)&Xd[pix((int64_t)j * PK + 1, p, D)];
 #pragma unroll
-          for (int v = 0; v < NV; ++v) dst[v] = piece(p, v);
+            for (int v = 0; v < NV; ++v) dst[v] = piece(p, v);
+          }
         }
-        if (DRAW) {
+        if (stw) {
 #pragma unroll
           for (int k = 0; k < M; ++k) {
             v16* dst = (v16*)&Wd[pix((int64_t)j * PK + 1, k, M)];
@@ -757,9 +795,11 @@ __device__ __forceinline__ bool run_segment_pk(const Law<Mdl, T>& L, const T* __
 #pragma unroll
       for (int q = 0; q < K; ++q) {
         gv[q] = step(c0 + q, cur.t[q], cur.H[q], cur.F[q], wu[q], cur.Z[q]);
+        if (stx) {
 #pragma unroll
-        for (int p = 0; p < D; ++p) Xd[pix(c0 + q + 1, p, D)] = x[p];
-        if (DRAW) {
+          for (int p = 0; p < D; ++p) Xd[pix(c0 + q + 1, p, D)] = x[p];
+        }
+        if (stw) {
 #pragma unroll
           for (int k = 0; k < M; ++k) Wd[pix(c0 + q + 1, k, M)] = wu[q][k];
         }
@@ -781,9 +821,11 @@ __device__ __forceinline__ bool run_segment_pk(const Law<Mdl, T>& L, const T* __
       Zi[k] = DRAW ? (PARITY ? (T)Zg[q * M + k] : ns.get((uint32_t)(i * M + k))) : (T)0;
     }
     ps.add(step(i, tb[(q + 1) * tst], Hi, Fi, dW, Zi));
+    if (stx) {
 #pragma unroll
-    for (int p = 0; p < D; ++p) Xd[pix(q + 1, p, D)] = x[p];
-    if (DRAW) {
+      for (int p = 0; p < D; ++p) Xd[pix(q + 1, p, D)] = x[p];
+    }
+    if (stw) {
 #pragma unroll
       for (int k = 0; k < M; ++k) Wd[pix(q + 1, k, M)] = dW[k];
     }
@@ -795,9 +837,10 @@ __device__ __forceinline__ bool run_segment_pk(const Law<Mdl, T>& L, const T* __
   return ok;
 }
 
-template <class Mdl, class T, int MODE, bool PARITY, int K, bool TD>
+template <class Mdl, class T, int MODE, bool PARITY, int K, bool TD, bool PAIR = false>
 __device__ __forceinline__ void lane_block_pk(const BlockArgs<T>& a, const int64_t tile,
-                                              const int64_t blk, const int lane, T* stg) {
+                                              const int64_t blk, const int lane, T* stg,
+                                              const int role = 0) {
   constexpr int D = Mdl::D, HP = D * (D + 1) / 2, PK = kPathPacket;
   const int64_t tq = a.tile_qoff[tile];
   auto idx = [&](int64_t q, int c, int C) -> int64_t { return ((tq + q) * C + c) * kLanes + lane; };
@@ -843,19 +886,21 @@ __device__ __forceinline__ void lane_block_pk(const BlockArgs<T>& a, const int64
     const bool aligned = __ballot(((tq + q0 + 1) & (PK - 1)) != 0) == 0;
     T sl;
     const bool sok =
-        aligned ? run_segment_pk<Mdl, T, MODE, PARITY, K, TD, PK, true>(
+        aligned ? run_segment_pk<Mdl, T, MODE, PARITY, K, TD, PK, true, PAIR>(
                       L, a.t, a.t_shared, a.H[ls][kind], a.H_shared[ls][kind], a.F[ls][kind],
                       a.aux[kind], Ws, Wd, Xd, Zg, ns, tq, q0, a.seg_np[g], lane, rho, srho,
-                      a.ll_skip, x, sl, stg)
-                : run_segment_pk<Mdl, T, MODE, PARITY, K, TD, PK, false>(
+                      a.ll_skip, x, sl, stg, role)
+                : run_segment_pk<Mdl, T, MODE, PARITY, K, TD, PK, false, PAIR>(
                       L, a.t, a.t_shared, a.H[ls][kind], a.H_shared[ls][kind], a.F[ls][kind],
                       a.aux[kind], Ws, Wd, Xd, Zg, ns, tq, q0, a.seg_np[g], lane, rho, srho,
-                      a.ll_skip, x, sl, stg);
+                      a.ll_skip, x, sl, stg, role);
     if (!sok) { ok = false; break; }
     ll = ll + sl;
   }
-  a.ll_out[blk] = ok ? (double)ll : -INFINITY;
-  if (a.success) a.success[blk] = ok ? 1 : 0;
+  if (role == 0) {
+    a.ll_out[blk] = ok ? (double)ll : -INFINITY;
+    if (a.success) a.success[blk] = ok ? 1 : 0;
+  }
 }
 
 template <class Mdl, class T, int MODE, bool PARITY, int K, bool TD = false>
@@ -866,18 +911,31 @@ __global__ __launch_bounds__(64) void k_block_pk(const BlockArgs<T> a) {
   lane_block_pk<Mdl, T, MODE, PARITY, K, TD>(a, tile, blk, threadIdx.x, stg);
 }
 
+// lane pairs on the packet layout (device-RNG draws): two waves per (recording tile, block
+// index), 32 recordings each on lanes (l, l + 32) — the mapping of k_block_pair
+template <class Mdl, class T, int MODE, bool TD = false>
+__global__ __launch_bounds__(64) void k_block_pk_pair(const BlockArgs<T> a) {
+  __shared__ T stg[(Mdl::D + Mdl::M) * kPathPacket * 65];
+  const int lane = threadIdx.x, role = lane >> 5;
+  const int64_t wave = blockIdx.x, w2 = wave >> 1;
+  const int slot = (int)(wave & 1) * 32 + (lane & 31);
+  const int64_t tile = a.tile0 + w2 / a.MB;
+  const int b = (int)(w2 % a.MB);
+  if (tile >= a.tile1) return;
+  const int64_t r = tile * kLanes + slot;
+  if (r >= a.R) return;
+  const int64_t blk = a.blk_off[r] + b;
+  if (blk >= a.blk_off[r + 1] || blk < a.b0 || blk >= a.b1) return;
+  lane_block_pk<Mdl, T, MODE, false, PairChunk<Mdl, T>::v, TD, true>(a, tile, blk, slot, stg, role);
+}
+
 // ---- MAP_LANE, pair mapping: two waves per (recording tile, block index), each
 // holding 32 recordings of the tile on lane pairs (l, l + 32).  The pair draws a chunk's normals
 // half each (pair_exchange) and runs the recursion redundantly, so an ensemble with fewer
 // tiles than the device has SIMDs (C5: 512 tiles, 1 024 SIMDs) fills the chip with waves whose
 // per-step instruction stream is the recursion plus HALF the random-number work.  Same
 // operations on the same values per recording: bit-identical to k_block.
-template <class Mdl, class T>
-struct PairChunk {  // steps per chunk: an even number of whole Philox blocks of normals
-  static constexpr int NPB = NormPerBlock<T>::v;
-  static constexpr int v = ((DMT_KCHUNK_PAIR_BASE * Mdl::M) % (2 * NPB) == 0)
-                               ? DMT_KCHUNK_PAIR_BASE : 2 * DMT_KCHUNK_PAIR_BASE;
-};
+
 
 template <class Mdl, class T, int MODE>
 __global__ __launch_bounds__(64) void k_block_pair(const BlockArgs<T> a) {
@@ -4442,9 +4500,20 @@ static hipError_t launch_block_t(int mapping, int mode, const void* args, int64_
     }
     const dim3 block(64);
     const bool par = a.Z != nullptr;
-    if (a.pk) {  // lane packets (fp32 ensembles): k_block_pk, every mode (no pair / split forms)
+    if (a.pk) {  // lane packets (fp32 ensembles): k_block_pk, every mode; lane pairs for draws
       if constexpr (sizeof(T) == 4) {
         const bool td = a.aux[0] || a.aux[1];
+        if (!par && a.lane_pair && (mode == MODE_PCN || mode == MODE_FRESH)) {
+          const dim3 pgrid((unsigned)(2 * nwaves));
+          if (mode == MODE_PCN) {
+            if (td) dlaunch(k_block_pk_pair<Mdl, T, MODE_PCN, true>, pgrid, block, s, a);
+            else dlaunch(k_block_pk_pair<Mdl, T, MODE_PCN>, pgrid, block, s, a);
+          } else {
+            if (td) dlaunch(k_block_pk_pair<Mdl, T, MODE_FRESH, true>, pgrid, block, s, a);
+            else dlaunch(k_block_pk_pair<Mdl, T, MODE_FRESH>, pgrid, block, s, a);
+          }
+          return hipGetLastError();
+        }
         switch (mode) {
           case MODE_PCN:
             if (td) {

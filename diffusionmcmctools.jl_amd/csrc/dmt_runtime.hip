@@ -549,7 +549,11 @@ dmt_status run_block_kernel(dmt_ens* h, const Layout* L, int mode, int kind_time
     // lane pairs (k_block_pair): on request only — bit-identical, but measured no faster on C5
     // (1 862 / 1 925 vs 1 829 µs per draw) and slower on C3 (1 821 vs 1 301 µs):
     // profiles/r03d, DESIGN.md §6
-    a.lane_pair = h->lane_pair == 1 && !h->pk;
+    // lane pairs: on request on the row layout (measured no faster there: profiles/r03d); on
+    // the packet layout (fp32) automatically when the draw has fewer waves than the device has
+    // SIMDs (C5), DMT_LANE_PAIR=0/1 to force (lane packets)
+    a.lane_pair = h->pk ? (h->lane_pair == 1 || (h->lane_pair < 0 && 2 * nwaves <= h->n_simd))
+                        : h->lane_pair == 1;
     a.lane_split = !a.lane_pair && !h->pk && L->single_seg &&
                    (h->lane_split == 1 || (h->lane_split < 0 && nwaves < h->n_simd &&
                                            h->key.precision == DMT_F64));
