@@ -112,8 +112,8 @@ struct Law {
 #pragma unroll
     for (int i = 0; i < HP; ++i) da[i] = (T)ldc(L + DMT_LAW_DA + i);
     trace = ldc(L + DMT_LAW_TRACE) != 0.0;
-    auxtd = !Mdl::kLinear && ldc(L + DMT_LAW_AUXTD) != 0.0;
-    auxa = !Mdl::kLinear && ldc(L + DMT_LAW_AUXTD) == 2.0;
+    auxtd = ldc(L + DMT_LAW_AUXTD) != 0.0;
+    auxa = ldc(L + DMT_LAW_AUXTD) == 2.0;
     unit = !Mdl::kLinear && D == M;
 #pragma unroll
     for (int p = 0; p < D; ++p)

@@ -531,6 +531,9 @@ struct PairChunk {  // steps per chunk: an even number of whole Philox blocks of
 #ifndef DMT_PK_ROLL  // 1: u.W's next packet loaded piece by piece into the registers just consumed
 #define DMT_PK_ROLL 1   // 0: the whole next packet in a second register set
 #endif
+#ifndef DMT_PK_LDS  // 1: the packet's X°, W° staged in the lane's LDS rows
+#define DMT_PK_LDS 0   // 0: staged in registers (measured faster in the kernel: 1 455 vs 1 574 µs, C5)
+#endif
 // PAIR (k_block_pk_pair): two lanes (roles) of a wave per recording, l and l + 32 — each draws
 // every other Philox block of a chunk and the pair swaps halves (pair_exchange), both run the
 // recursion on the same values; role 0 stores X°, role 1 W° (every load is the same address
@@ -704,10 +707,19 @@ __device__ __forceinline__ bool run_segment_pk(const Law<Mdl, T>& L, const T* __
             for (int v = 0; v < NV; ++v) wn[k][v] = wpk(j + 1, k)[v];
         }
 #endif
-        // the packet's X°, W° go to the lane's LDS rows step by step (stg[c][e][lane], a
-        // 65-element row pitch) and leave as whole 16-byte pieces at the packet's end:
-        // register-staged packets measured slower (AGPR moves; 1 378 vs 1 288 µs in the probe)
+        // the packet's X°, W° are collected step by step and leave as whole 16-byte pieces at
+        // the packet's end: in registers (default), or in the lane's LDS rows (stg[c][e][lane],
+        // a 65-element row pitch; DMT_PK_LDS=1 — faster in the layout probe, slower in the kernel)
+        // (a pair's roles each store one of the two, so they share NS staging rows: X° rows for
+        // role 0, W° rows for role 1)
+        constexpr int NS = PAIR ? (D > M ? D : M) : D + M, WR = PAIR ? 0 : D;
+#if DMT_PK_LDS
         auto st = [&](int c, int e) -> T& { return stg[(c * PK + e) * 65 + lane]; };
+        auto put = [&](int c, int e, T v) { st(c, e) = v; };
+#else
+        v16 ob[NS][NV];
+        auto put = [&](int c, int e, T v) { ob[c][e / VE][e % VE] = v; };
+#endif
 #pragma unroll
         for (int v = 0; v < PK / K; ++v) {
           const int c0 = j * PK + v * K;
@@ -721,13 +733,17 @@ __device__ __forceinline__ bool run_segment_pk(const Law<Mdl, T>& L, const T* __
 #pragma unroll
             for (int k = 0; k < M; ++k) dW[k] = READW ? wc[k][e / VE][e % VE] : (T)0;
             gv[q] = step(c0 + q, cur.t[q], cur.H[q], cur.F[q], dW, cur.Z[q]);
-            if (stx) {
+            if constexpr (PAIR) {
 #pragma unroll
-              for (int p = 0; p < D; ++p) st(p, e) = x[p];
-            }
-            if (stw) {
+              for (int c = 0; c < NS; ++c)
+                put(c, e, stx ? (c < D ? x[c] : (T)0) : (c < M ? dW[c] : (T)0));
+            } else {
 #pragma unroll
-              for (int k = 0; k < M; ++k) st(D + k, e) = dW[k];
+              for (int p = 0; p < D; ++p) put(p, e, x[p]);
+              if (DRAW) {
+#pragma unroll
+                for (int k = 0; k < M; ++k) put(D + k, e, dW[k]);
+              }
             }
           }
 #if DMT_PK_ROLL
@@ -745,10 +761,14 @@ __device__ __forceinline__ bool run_segment_pk(const Law<Mdl, T>& L, const T* __
           cur = nxt;
         }
         auto piece = [&](int c, int v) -> v16 {
+#if DMT_PK_LDS
           v16 o;
 #pragma unroll
           for (int u = 0; u < VE; ++u) o[u] = st(c, v * VE + u);
           return o;
+#else
+          return ob[c][v];
+#endif
         };
         if (stx) {
 #pragma unroll
@@ -763,7 +783,7 @@ __device__ __forceinline__ bool run_segment_pk(const Law<Mdl, T>& L, const T* __
           for (int k = 0; k < M; ++k) {
             v16* dst = (v16*)&Wd[pix((int64_t)j * PK + 1, k, M)];
 #pragma unroll
-            for (int v = 0; v < NV; ++v) dst[v] = piece(D + k, v);
+            for (int v = 0; v < NV; ++v) dst[v] = piece(WR + k, v);
           }
         }
 #if !DMT_PK_ROLL
@@ -905,7 +925,7 @@ __device__ __forceinline__ void lane_block_pk(const BlockArgs<T>& a, const int64
 
 template <class Mdl, class T, int MODE, bool PARITY, int K, bool TD = false>
 __global__ __launch_bounds__(64) void k_block_pk(const BlockArgs<T> a) {
-  __shared__ T stg[(Mdl::D + Mdl::M) * kPathPacket * 65];  // the packet's X°, W° (run_segment_pk)
+  __shared__ T stg[DMT_PK_LDS ? (Mdl::D + Mdl::M) * kPathPacket * 65 : 1];  // X°, W° (DMT_PK_LDS)
   int64_t tile, blk;
   if (!map_block(a, tile, blk)) return;
   lane_block_pk<Mdl, T, MODE, PARITY, K, TD>(a, tile, blk, threadIdx.x, stg);
@@ -915,7 +935,7 @@ __global__ __launch_bounds__(64) void k_block_pk(const BlockArgs<T> a) {
 // index), 32 recordings each on lanes (l, l + 32) — the mapping of k_block_pair
 template <class Mdl, class T, int MODE, bool TD = false>
 __global__ __launch_bounds__(64) void k_block_pk_pair(const BlockArgs<T> a) {
-  __shared__ T stg[(Mdl::D + Mdl::M) * kPathPacket * 65];
+  __shared__ T stg[DMT_PK_LDS ? (Mdl::D + Mdl::M) * kPathPacket * 65 : 1];
   const int lane = threadIdx.x, role = lane >> 5;
   const int64_t wave = blockIdx.x, w2 = wave >> 1;
   const int slot = (int)(wave & 1) * 32 + (lane & 31);
@@ -1773,7 +1793,10 @@ __device__ __forceinline__ void wave_lds_sync() {
 }
 
 // One block's draw / re-solve by one wave; every lane returns the block's ll and success.
-template <class Mdl, class T, int MODE, class Sel>
+// TD: time-dependent auxiliary laws (an aux table is present) — the recursion is the target
+// law's and does not change; phase 3 takes step i's B̃(t_i), β̃(t_i) (and a − ã(t_i)) in G where
+// the segment's law record says so (DMT_LAW_AUXTD).
+template <class Mdl, class T, int MODE, class Sel, bool TD = false>
 __device__ __forceinline__ void scan_block(const BlockArgs<T>& a, const int64_t blk,
                                            const uint32_t iter, const Sel& sel,
                                            ScanLds<Mdl::D, T>& S, T& ll_res, bool& ok_res) {
@@ -1999,7 +2022,22 @@ __device__ __forceinline__ void scan_block(const BlockArgs<T>& a, const int64_t 
           for (int c = 0; c < D; ++c) Fi[c] = Fb[(int64_t)i * D + c];
         }
         T rr[D], bb[D];
-        const T G = g_at<Mdl, T>(LA, Hi, Fi, xk[k], rr, bb);
+        T G;
+        if constexpr (TD) {
+          if (LA.auxtd) {  // uniform: the segment's law
+            constexpr int CA = kAuxCols<D>;
+            const int i = c0 + (v ? s : cnt - 1);
+            T Bq[D * D], bq[D], dq[HP];
+            bool trq;
+            aux_step<Mdl, T>(LA, a.aux[kind] + (row + i) * CA, 1, Bq, bq, dq, trq,
+                             [](const T* p) { return *p; });
+            G = g_at_aux<Mdl, T>(LA, Hi, Fi, xk[k], rr, bb, Bq, bq, dq, trq);
+          } else {
+            G = g_at<Mdl, T>(LA, Hi, Fi, xk[k], rr, bb);
+          }
+        } else {
+          G = g_at<Mdl, T>(LA, Hi, Fi, xk[k], rr, bb);
+        }
         const bool inll = MODE != MODE_RECOMPUTE || c0 + s < nst - a.ll_skip;  // skip
         gk[k] = (v && inll) ? G * dt : (T)0;
       }
@@ -2031,7 +2069,7 @@ __device__ __forceinline__ void scan_block(const BlockArgs<T>& a, const int64_t 
   ok_res = ok;
 }
 
-template <class Mdl, class T, int MODE>
+template <class Mdl, class T, int MODE, bool TD = false>
 __global__ __launch_bounds__((64 * ScanCfg<Mdl::D, T>::WPB), 1) void k_block_scan(const BlockArgs<T> a) {
   using Cfg = ScanCfg<Mdl::D, T>;
   __shared__ ScanLds<Mdl::D, T> lds[Cfg::WPB];
@@ -2040,7 +2078,7 @@ __global__ __launch_bounds__((64 * ScanCfg<Mdl::D, T>::WPB), 1) void k_block_sca
   if (blk >= a.b1) return;  // whole wave: the waves of a workgroup never synchronise
   T ll;
   bool ok;
-  scan_block<Mdl, T, MODE>(a, blk, a.iter, SelGlobal{a.selX, a.selW}, lds[w], ll, ok);
+  scan_block<Mdl, T, MODE, SelGlobal, TD>(a, blk, a.iter, SelGlobal{a.selX, a.selW}, lds[w], ll, ok);
   if ((threadIdx.x & 63) == 0) {
     a.ll_out[blk] = ok ? (double)ll : -INFINITY;
     if (a.success) a.success[blk] = ok ? 1 : 0;
@@ -2250,7 +2288,7 @@ __device__ __forceinline__ void persistent_tree_tail(const double* __restrict__ 
 // then — uniformly, exactly as k_accept — the MH decision, selector flips (bit masks in
 // SGPRs), histories and the ll swap.  Per-iteration (ll, ll°, accepted) go to
 // part[n_iter][3][nb]; persistent_tree_tail forms every iteration's fetch_ll from them.
-template <class Mdl, class T>
+template <class Mdl, class T, bool TD = false>
 __device__ __forceinline__ void mcmc_scan_block(const BlockArgs<T>& a, const AcceptArgs& c,
                                                 const int64_t iter0, const int64_t n_iter,
                                                 double* __restrict__ part, const int64_t blk,
@@ -2269,7 +2307,7 @@ __device__ __forceinline__ void mcmc_scan_block(const BlockArgs<T>& a, const Acc
     const double E = exp1_draw(c.seed, (uint32_t)g0 + c.seg_base, (uint32_t)(it + c.key_delta), c.salt);
     T lp;
     bool ok;
-    scan_block<Mdl, T, MODE_PCN>(a, blk, (uint32_t)(it + c.key_delta), sel, L, lp, ok);
+    scan_block<Mdl, T, MODE_PCN, SelMask, TD>(a, blk, (uint32_t)(it + c.key_delta), sel, L, lp, ok);
     llp = ok ? (double)lp : -INFINITY;
     const bool acc = E > -(llp - ll);
     if (acc) {
@@ -2307,7 +2345,7 @@ __device__ __forceinline__ void mcmc_scan_block(const BlockArgs<T>& a, const Acc
   }
 }
 
-template <class Mdl, class T>
+template <class Mdl, class T, bool TD = false>
 __global__ __launch_bounds__((64 * ScanCfg<Mdl::D, T>::WPB), 1) void k_mcmc_scan(
     const BlockArgs<T> a, const AcceptArgs c, const int64_t iter0, const int64_t n_iter,
     double* __restrict__ part, double* __restrict__ nodes, unsigned* __restrict__ counter,
@@ -2316,7 +2354,7 @@ __global__ __launch_bounds__((64 * ScanCfg<Mdl::D, T>::WPB), 1) void k_mcmc_scan
   __shared__ ScanLds<Mdl::D, T> lds[Cfg::WPB];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t blk = a.b0 + (int64_t)blockIdx.x * Cfg::WPB + w;
-  if (blk < a.b1) mcmc_scan_block<Mdl, T>(a, c, iter0, n_iter, part, blk, lds[w]);
+  if (blk < a.b1) mcmc_scan_block<Mdl, T, TD>(a, c, iter0, n_iter, part, blk, lds[w]);
   persistent_tree_tail<Cfg::WPB>(part, nodes, a.b1 - a.b0, n_iter, counter, out3);
 }
 
@@ -2662,6 +2700,24 @@ __global__ __launch_bounds__(256, 1) void k_mcmc_resident(const BlockArgs<T> a,
 // made).  Between B1 and B2 the producer draws iteration n+1's normals while the consumer runs
 // iteration n, so the two waves of every SIMD issue concurrently.  The operations and their
 // order are resident_block's: bit-identical results (the GPU tests run both).
+// Measurement build only (-DDMT_PC_STAMPS, scripts/pc_stamps.py): device wall-clock stamps of
+// one k_mcmc_resident_pc launch per workgroup — entry, the consumer's and the producer's set-up
+// done, B1 of iteration 0 passed, the loop's end, the tail's end (dmt_probe_pc_stamps).
+#ifdef DMT_PC_STAMPS
+__device__ uint64_t g_pc_stamps[8192 * 8];
+#define PC_STAMP(TID, K)                                                                  \
+  do {                                                                                    \
+    if (threadIdx.x == (TID) && blockIdx.x < 8192)                                        \
+      g_pc_stamps[blockIdx.x * 8 + (K)] = (uint64_t)wall_clock64();                        \
+  } while (0)
+extern "C" int dmt_probe_pc_stamps(uint64_t* out, int64_t n) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pc_stamps), (size_t)std::min<int64_t>(n, 8192 * 8) * 8);
+}
+#else
+#define PC_STAMP(TID, K) \
+  do {                   \
+  } while (0)
+#endif
 #ifndef DMT_PC_DRAW_GROUP
 #define DMT_PC_DRAW_GROUP 8
 #endif
@@ -2902,7 +2958,9 @@ __device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, cons
   const int64_t nb = a.b1 - a.b0, j = blk - a.b0;
   const int last_lane = (nst - 1) / kRun;
   double Ev = 0.0;
+  PC_STAMP(0, 1);
   __syncthreads();  // B1 of iteration 0
+  PC_STAMP(0, 3);
   for (int64_t r0 = 0; r0 < n_iter; ++r0) {
     const int64_t it = iter0 + r0;
     if ((r0 & 63) == 0)
@@ -3083,6 +3141,7 @@ __device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, cons
       __syncthreads();  // B1: dW° of iteration n + 1 ready
     }
   }
+  PC_STAMP(0, 4);
   if (valid && lane == 0) {
     a.selX[g] = sel_two(sel.x(g));
     a.selW[g] = sel_two(sel.w(g));
@@ -3228,6 +3287,7 @@ __device__ __forceinline__ void resident_pc_producer(const BlockArgs<T>& a, cons
   };
   draw_z((uint32_t)(iter0 + c.key_delta), z);
   propose();
+  PC_STAMP(256, 2);  // producer 0 of workgroup block 0 (BPW = 4)
   __syncthreads();  // B1 of iteration 0
   if constexpr (!SVC) store_w();
   for (int64_t r0 = 0; r0 < n_iter; ++r0) {
@@ -3273,6 +3333,7 @@ __global__ __launch_bounds__(64 * BPW * (NP + 1), BPW == 4 ? 1 : 2) void k_mcmc_
   __shared__ ResPcLds<Mdl::D, Mdl::M, T> lds[BPW];
   __shared__ SvcLds s_svc;
   if (n_iter <= 0) return;
+  PC_STAMP(0, 0);
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t blk = a.b0 + (int64_t)blockIdx.x * BPW + (w % BPW);
   const bool valid = blk < a.b1;
@@ -3297,6 +3358,7 @@ __global__ __launch_bounds__(64 * BPW * (NP + 1), BPW == 4 ? 1 : 2) void k_mcmc_
   if constexpr (!SVC)  // the service forms each iteration's tree as the iteration ends
     persistent_tree_tail<BPW, BPW * (NP + 1)>(part, nodes, a.b1 - a.b0, n_iter, counter, out3);
 #endif
+  PC_STAMP(0, 5);
 }
 
 // One draw / re-solve (dmt_draw_proposal, dmt_draw_unit, dmt_recompute_path) of single-segment
@@ -4466,8 +4528,9 @@ static hipError_t launch_block_t(int mapping, int mode, const void* args, int64_
   if (nwaves <= 0) return hipSuccess;
   const dim3 grid((unsigned)nwaves);
   if constexpr (Mdl::kLinear) {  // one wave per block, always
+    const bool td = a.aux[0] || a.aux[1];  // time-dependent auxiliary laws: scan kernels only
     if constexpr (Mdl::D <= 2) {
-      if (a.resident1) {  // single-segment blocks of <= kSChunk steps: run-order kernel
+      if (a.resident1 && !td) {  // single-segment blocks of <= kSChunk steps: run-order kernel
         const dim3 rgrid((unsigned)((nwaves + 3) / 4)), rblock(256);
         switch (mode) {
           case MODE_PCN: dlaunch(k_block_resident<Mdl, T, MODE_PCN>, rgrid, rblock, s, a); break;
@@ -4480,10 +4543,13 @@ static hipError_t launch_block_t(int mapping, int mode, const void* args, int64_
     }
     constexpr int WPB = ScanCfg<Mdl::D, T>::WPB;
     const dim3 grid((unsigned)((nwaves + WPB - 1) / WPB)), sblock(64 * WPB);
-    switch (mode) {
-      case MODE_PCN: dlaunch(k_block_scan<Mdl, T, MODE_PCN>, grid, sblock, s, a); break;
-      case MODE_RECOMPUTE: dlaunch(k_block_scan<Mdl, T, MODE_RECOMPUTE>, grid, sblock, s, a); break;
-      case MODE_FRESH: dlaunch(k_block_scan<Mdl, T, MODE_FRESH>, grid, sblock, s, a); break;
+    switch (mode * 2 + (td ? 1 : 0)) {
+      case 2 * MODE_PCN: dlaunch(k_block_scan<Mdl, T, MODE_PCN>, grid, sblock, s, a); break;
+      case 2 * MODE_RECOMPUTE: dlaunch(k_block_scan<Mdl, T, MODE_RECOMPUTE>, grid, sblock, s, a); break;
+      case 2 * MODE_FRESH: dlaunch(k_block_scan<Mdl, T, MODE_FRESH>, grid, sblock, s, a); break;
+      case 2 * MODE_PCN + 1: dlaunch(k_block_scan<Mdl, T, MODE_PCN, true>, grid, sblock, s, a); break;
+      case 2 * MODE_RECOMPUTE + 1: dlaunch(k_block_scan<Mdl, T, MODE_RECOMPUTE, true>, grid, sblock, s, a); break;
+      case 2 * MODE_FRESH + 1: dlaunch(k_block_scan<Mdl, T, MODE_FRESH, true>, grid, sblock, s, a); break;
       default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -4761,7 +4827,9 @@ static hipError_t launch_mcmc_t(const void* args, const AcceptArgs& c, int64_t i
     if (nwaves <= 0) return hipSuccess;
     // part[n][3][nwaves], then the tree nodes [n][3][ceil(nwaves / WPB)] (dmt_mcmc_run sizes it)
     double* nodes = part + 3 * n * nwaves;
+    const bool td = a.aux[0] || a.aux[1];  // time-dependent auxiliary laws: k_mcmc_scan only
     if constexpr (Mdl::D <= 2) {
+      if (td) resident = 0;
       if (resident >= 2) {  // producer / consumer waves (k_mcmc_resident_pc), resident - 1 producers
         const SvcArgs none{};
         if (resident == 3)
@@ -4782,8 +4850,12 @@ static hipError_t launch_mcmc_t(const void* args, const AcceptArgs& c, int64_t i
       }
     }
     constexpr int WPB = ScanCfg<Mdl::D, T>::WPB;
-    dlaunch(k_mcmc_scan<Mdl, T>, dim3((unsigned)((nwaves + WPB - 1) / WPB)), dim3(64 * WPB), s, a,
-            c, iter0, n, part, nodes, counter, out3);
+    if (td)
+      dlaunch(k_mcmc_scan<Mdl, T, true>, dim3((unsigned)((nwaves + WPB - 1) / WPB)), dim3(64 * WPB),
+              s, a, c, iter0, n, part, nodes, counter, out3);
+    else
+      dlaunch(k_mcmc_scan<Mdl, T>, dim3((unsigned)((nwaves + WPB - 1) / WPB)), dim3(64 * WPB), s, a,
+              c, iter0, n, part, nodes, counter, out3);
     return hipGetLastError();
   } else {
     return hipErrorInvalidValue;

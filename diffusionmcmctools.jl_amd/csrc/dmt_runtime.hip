@@ -513,6 +513,10 @@ void fill_common(dmt_ens* h, const Layout* L, BlockArgs<T>& a) {
   a.resident1 = 0;
 }
 
+// A time-dependent auxiliary law's table is present: linear drifts then run on the scan
+// kernels only (the register-resident ones take the law's own B̃, β̃)
+static bool has_aux_table(const dmt_ens* h) { return h->d_aux[0] || h->d_aux[1]; }
+
 dmt_status run_block_kernel(dmt_ens* h, const Layout* L, int mode, int kind_timer, int64_t b0,
                             int64_t b1, int law_flip, int xs, int xd, int ws, int wd,
                             const double* dZ, int64_t iter, uint32_t salt, double* ll_out,
@@ -543,7 +547,7 @@ dmt_status run_block_kernel(dmt_ens* h, const Layout* L, int mode, int kind_time
     a.success = success;
     a.ll_skip = ll_skip;
     a.resident1 = h->scan_resident && h->key.model == DMT_MODEL_OU && h->key.d <= 2 &&
-                  L->single_seg && L->max_steps <= kResidentMaxSteps;
+                  !has_aux_table(h) && L->single_seg && L->max_steps <= kResidentMaxSteps;
     // auto: fp64 only — with fp32's four normals per Philox block the single wave is faster
     // (C5: 1773 vs 1934 µs per draw, profiles/r02m)
     // lane pairs (k_block_pair): on request only — bit-identical, but measured no faster on C5
@@ -714,7 +718,7 @@ dmt_status enter(dmt_ens* h) {
 // a linear drift with d <= 2 (dmt_mcmc_run's own condition, layout-wide)
 bool resident_range(const dmt_ens* h, const Layout* L) {
   return h->persist && h->resident && h->key.model == DMT_MODEL_OU && h->key.d <= 2 &&
-         L->single_seg && L->max_steps <= kResidentMaxSteps;
+         !has_aux_table(h) && L->single_seg && L->max_steps <= kResidentMaxSteps;
 }
 
 dmt_status upload_Z(dmt_ens* h, const double* Z, const double** dZ) {
@@ -1238,9 +1242,6 @@ dmt_status dmt_upload_aux_a(dmt_ens* h, int32_t kind, const double* aux, int32_t
   const int nb = (int)(h->d * h->d + h->d), na = nb + (int)h->hp;  // table columns (kAuxCols)
   if (aux && ncols != nb && ncols != na)
     return fail(DMT_ERR_INVALID, "aux table: d*d + d or d*d + d + d(d+1)/2 columns per point");
-  if (h->key.model == DMT_MODEL_OU)
-    return fail(DMT_ERR_INVALID, "time-dependent auxiliary laws: non-linear drifts only (the OU "
-                                 "kernels' affine scan takes the auxiliary drift per segment)");
   if (!aux) {
     if (h->d_aux[kind]) {
       HIP_OK(stream_wait(h));
@@ -1682,7 +1683,7 @@ static dmt_status mcmc_run_launch(dmt_ens* h, Layout* L, int64_t b0, int64_t b1,
   bool persist = h->persist && h->key.model == DMT_MODEL_OU;
   for (int64_t b = b0; b < b1 && persist && !L->single_seg; ++b)
     persist = L->glast[b] - L->gfirst[b] + 1 <= kPersistMaxSegments;
-  bool resident = persist && h->key.d <= 2 && h->resident;
+  bool resident = persist && h->key.d <= 2 && h->resident && !has_aux_table(h);
   for (int64_t b = b0; b < b1 && resident && !lay_res; ++b)
     resident = L->glast[b] == L->gfirst[b] && h->seg_np[L->gfirst[b]] - 1 <= kResidentMaxSteps;
   if (persist) {

@@ -190,10 +190,12 @@ dmt_status dmt_upload_law(dmt_ens* h, int32_t unit, int32_t kind, const double* 
  * may vary in t.  aux[P][d·d + d] holds B̃(t_i) (row-major) then β̃(t_i) at every grid point
  * of every segment (layout of dmt_upload_law's F) for the laws of kind PP or PPB, u and u° alike
  * (the auxiliary law does not depend on θ).  A segment whose law record has DMT_LAW_AUXTD = 1.0
- * takes step i's auxiliary drift B̃(t_i)x + β̃(t_i) (left point, frozen over [t_i, t_{i+1}]) in
- * the Girsanov term G and in the backward filter's exact step transition
+ * takes step i's auxiliary drift B̃(t_i)x + β̃(t_i) (left point) in the Girsanov term G and the
+ * trapezoidal average of B̃, β̃ over [t_i, t_{i+1}] in the backward filter's step transition
  * (dmt_recompute_guiding_term); ã stays the record's (σ̃ constant per segment).  aux = NULL
- * removes the table.  Non-linear drifts (FHN, Lorenz) only: DMT_ERR_INVALID for OU. */
+ * removes the table.  Every model: a linear drift (OU) takes the table in G and the filter only
+ * (its recursion is the target law's), on the scan kernels (the register-resident kernels are not
+ * used while a table is present). */
 dmt_status dmt_upload_aux(dmt_ens* h, int32_t kind, const double* aux);
 /* The same with a time-dependent ã(t) = σ̃σ̃ᵀ(t) too: aux[P][ncols], ncols = d·d + d (as
  * dmt_upload_aux) or d·d + d + d(d+1)/2 — B̃, β̃ and ã packed (upper triangle, row-major) per

@@ -271,8 +271,13 @@ static void aff_apply(int d, const REAL* A, const REAL* e, const REAL* x, REAL* 
 #define ORC_RUN 8
 #define ORC_SCHUNK 512
 extern int orc_ll_skip;
-static int solve_segment_scan(int d, int m, const REAL* th, const REAL* sg, const REAL* a,
-                              const REAL* Bt, const REAL* beta, const REAL* da, int trace,
+static inline const REAL* aux_coeffs(const double* law, int model, int d, int i, const REAL* Bt,
+                                     const REAL* beta, REAL* Bq, REAL* bq, const REAL** bo,
+                                     const REAL* a, const REAL* da, int trace, REAL* dq,
+                                     const REAL** dao, int* tro);
+static int solve_segment_scan(const double* law, int d, int m, const REAL* th, const REAL* sg,
+                              const REAL* a, const REAL* Bt, const REAL* beta, const REAL* da,
+                              int trace,
                               int npts, const REAL* t, const REAL* H, const REAL* F,
                               const REAL* W, const REAL* y1, REAL* X, REAL* ll_out) {
     int h = d * (d + 1) / 2;
@@ -340,7 +345,12 @@ static int solve_segment_scan(int d, int m, const REAL* th, const REAL* sg, cons
                 REAL dt = t[i + 1] - t[i];
                 REAL rr[3] = {0, 0, 0}, b[3] = {0, 0, 0};
                 if (i > 0) for (int p = 0; p < d; ++p) X[(size_t)i * d + p] = x[p];
-                REAL G = g_at(ORC_OU, d, th, a, Bt, beta, da, trace, H + (size_t)i * h,
+                REAL Bq[9], bq[3], dq[6];
+                const REAL *bu, *du;
+                int tu;
+                const REAL* Bu = aux_coeffs(law, ORC_OU, d, i, Bt, beta, Bq, bq, &bu, a, da, trace,
+                                            dq, &du, &tu);
+                REAL G = g_at(ORC_OU, d, th, a, Bu, bu, du, tu, H + (size_t)i * h,
                               F + (size_t)i * d, x, rr, b);
                 ps_add(&ps, i < n - orc_ll_skip ? G * dt : (REAL)0);
                 REAL xp[3];
@@ -375,8 +385,8 @@ extern int orc_ll_skip;
  * B~(t_i), beta~(t_i), a~(t_i) packed (zeros where not given), used at step i (left point) in
  * place of the record's Bt, beta when the record's auxtd (offset 15) is set, and — auxtd = 2 —
  * a − a~(t_i) (in the working precision) in place of the record's a − a~ in G's trace term,
- * which is then taken whatever the record's trace flag (libdmt aux_step).  Non-linear drifts
- * only. */
+ * which is then taken whatever the record's trace flag (libdmt aux_step).  A linear drift's
+ * scan (solve_segment_scan) takes it in G only: the recursion is the target law's. */
 #if IS_F64
 const double* orc_aux = 0;
 void orc_set_aux(const double* p) { orc_aux = p; }
@@ -389,7 +399,7 @@ static inline const REAL* aux_coeffs(const double* law, int model, int d, int i,
                                      const REAL** dao, int* tro) {
     *dao = da;
     *tro = trace;
-    if (model == ORC_OU || !orc_aux || law[L_AUXTD] == 0.0) { *bo = beta; return Bt; }
+    if (!orc_aux || law[L_AUXTD] == 0.0) { *bo = beta; return Bt; }
     const int hp = d * (d + 1) / 2;
     const double* row = orc_aux + (size_t)i * (d * d + d + hp);
     for (int k = 0; k < d * d; ++k) Bq[k] = (REAL)row[k];
@@ -423,7 +433,7 @@ int SFX(orc_solve_segment)(int model, int d, int m, const double* law, int npts,
     load_law(law, d, m, th, sg, a, Bt, beta, da, &trace);
     const int unit = law_unit(model, d, m, sg);
     if (model == ORC_OU && !orc_sequential_ou)
-        return solve_segment_scan(d, m, th, sg, a, Bt, beta, da, trace, npts, t, H, F, W, y1,
+        return solve_segment_scan(law, d, m, th, sg, a, Bt, beta, da, trace, npts, t, H, F, W, y1,
                                   X, ll_out);
     REAL x[3];
     for (int p = 0; p < d; ++p) { x[p] = y1[p]; X[p] = x[p]; }

@@ -505,10 +505,8 @@ class OracleEnsemble:
         """dmt_upload_aux(_a): per-point B̃(t_i), β̃(t_i) ([P][d·d + d]) — or B̃, β̃, ã(t_i) packed
         ([P][d·d + d + d(d+1)/2]) — of the laws of `kind`, u and u° alike, held in the working
         precision (as the device holds them; ã zero where not given) for the segments whose
-        record has auxtd set (2: ã from the table too); None removes them.  Non-linear drifts
-        only."""
-        if self.model == MODEL_OU:
-            raise ValueError("time-dependent auxiliary laws: non-linear drifts only")
+        record has auxtd set (2: ã from the table too); None removes them.  A linear drift (OU)
+        takes them in G only (its recursion is the target law's)."""
         if aux is None:
             self.aux[kind] = None
             return

@@ -10,7 +10,8 @@ converges (first order) as the grid is refined — the guiding term of the ODEs 
 GPU: device == oracle bit for bit on the ragged FHN ensemble with a varying table on part of
 the segments, through the blocking loop (set_obs!, recompute_guiding_term!, find_W_for_X!,
 loglikhd!, draws with caller and device normals, accept, recompute_path!), lane and wave
-mappings, fp64 and fp32.
+mappings, fp64 and fp32; and on the ragged OU ensemble (scan kernels; dmt_mcmc_run's
+k_mcmc_scan too).
 """
 from __future__ import annotations
 
@@ -158,8 +159,9 @@ def _tables(case, ens, vary=True, with_a=False):
     return out
 
 
-def _td_pair(mapping, prec, vary=True, segs=None, oracle_only=False, with_a=False):
-    case = cs.ragged_case(prec=prec)
+def _td_pair(mapping, prec, vary=True, segs=None, oracle_only=False, with_a=False, model=None,
+             hist_len=6):
+    case = cs.ragged_case(prec=prec, model=model)
     m = case["model"]
     ens = []
     if not oracle_only:
@@ -183,7 +185,7 @@ def _td_pair(mapping, prec, vary=True, segs=None, oracle_only=False, with_a=Fals
     for lay, rho in ((layA, 0.7), (layB, 0.3)):
         nb = int(sum(lay["n_blocks"]))
         ids_ = [e.create_layout(lay["n_blocks"], lay["seg_first"], lay["seg_last"], lay["last"],
-                                np.full(nb, rho), 6) for e in ens]
+                                np.full(nb, rho), hist_len) for e in ens]
         assert len(set(ids_)) == 1
         ids.append((ids_[0], nb))
     return case, ens, ids
@@ -246,10 +248,65 @@ def test_oracle_constant_table_equals_homogeneous_law():
         cs.assert_ll_equal(td, plain, lid, nb)
 
 
-def test_upload_aux_rejected_for_ou_oracle():
-    o = orc.OracleEnsemble(0, 2, 1, [[11]], prec=0, seed=1)
-    with pytest.raises(ValueError):
-        o.upload_aux(L.LAW_PP, np.zeros((11, 6)))
+# ------------------------------------------------------------------ linear drifts (OU)
+# A linear drift's recursion is the target law's affine step map (the scan kernels): the
+# auxiliary law enters G and the backward filter only, so a time-dependent one takes step i's
+# B̃(t_i), β̃(t_i) (and a − ã(t_i)) in phase 3's G of the scan and in the filter.
+def _ou_loop(ens, ids, S, iters, rng, device_rng=False):
+    """The OU blocking loop: set_obs!, recompute_guiding_term!, loglikhd!, draws (caller or
+    device normals), accept."""
+    out = []
+    for i in range(1, iters + 1):
+        lid, nb = ids[(i - 1) % 2]
+        Z = rng.standard_normal((S, 1))
+        E = rng.exponential(1.0, nb)
+        for e in ens:
+            e.set_obs(lid, 0, nb)
+            e.recompute_guiding_term(lid, 0, nb, unit=L.U)
+            e.loglikhd(lid, L.U, 0, nb)
+            if device_rng:
+                e.draw_proposal(lid, 0, nb, iter=i, salt=3)
+            else:
+                e.draw_proposal(lid, 0, nb, Z=Z, iter=i)
+        out.append([e.accept_reject(lid, 0, nb, i, E=E, want_acc=True) for e in ens])
+    return out
+
+
+def test_oracle_ou_constant_table_equals_homogeneous_law():
+    """OU: every segment flagged time-dependent with a table holding each record's own B̃, β̃
+    runs the blocking loop bit-identically to the plain oracle; a varying table changes the
+    Girsanov weights and the guiding term."""
+    model = cs.ou_ragged_model()
+    G = sum(cs.ragged_case()["nsegs"])
+    case, (td,), ids = _td_pair(None, L.F64, vary=False, oracle_only=True, segs=np.arange(G),
+                                model=model)
+    plain = orc.OracleEnsemble(model.kind, model.d, model.m, case["n_points"], prec=L.F64, seed=11)
+    cs.load_ragged(plain, case)
+    plain.upload_obs(case["Hobs"], case["Fobs"], case["cobs"])
+    for lay in (dict(n_blocks=[2, 3, 2], seg_first=[0, 2, 0, 2, 4, 0, 3],
+                     seg_last=[1, 3, 1, 3, 5, 2, 4], last=[0, 1, 0, 0, 1, 0, 1], rho=0.7),
+                dict(n_blocks=[1, 2, 2], seg_first=[0, 0, 3, 0, 2], seg_last=[3, 2, 5, 1, 4],
+                     last=[1, 0, 1, 0, 1], rho=0.3)):
+        nb = int(sum(lay["n_blocks"]))
+        plain.create_layout(lay["n_blocks"], lay["seg_first"], lay["seg_last"], lay["last"],
+                            np.full(nb, lay["rho"]), 6)
+    a = _ou_loop([td], ids, td.S, 4, np.random.default_rng(2))
+    b = _ou_loop([plain], ids, td.S, 4, np.random.default_rng(2))
+    for x, y in zip(a, b):
+        assert np.array_equal(x[0], y[0])
+    cs.assert_paths_equal(td, plain)
+    for lid, nb in ids:
+        cs.assert_ll_equal(td, plain, lid, nb)
+    _, (var,), ids = _td_pair(None, L.F64, vary=True, oracle_only=True, segs=np.arange(G),
+                              model=model)
+    lid, nb = ids[0]
+    for e in (var, td):
+        e.loglikhd(lid, L.U, 0, nb)
+    assert not np.array_equal(var.get_block_state(lid, L.BLK_LL, 0, nb),
+                              td.get_block_state(lid, L.BLK_LL, 0, nb))
+    for e in (var, td):
+        e.recompute_guiding_term(lid, 0, nb, unit=L.U)
+    assert not np.array_equal(var.download_law(L.U, L.LAW_PP)[0], td.download_law(L.U, L.LAW_PP)[0])
 
 
 def _law2a():
@@ -390,13 +447,48 @@ def test_td_aux_removed_table_is_homogeneous_again():
 
 
 @pytest.mark.gpu
-def test_td_aux_rejected_for_ou():
-    w = __import__("diffusionmcmctools_amd.workloads", fromlist=["c2_ou2d"]).c2_ou2d(B=4, N=20)
-    e = dmt.Ensemble(w.model.kind, w.d, w.m, w.n_points, precision=w.precision, seed=1,
-                     grid_shared=w.grid_shared)
-    with pytest.raises(dmt.DMTError):
-        e.upload_aux(L.LAW_PP, np.zeros((e.P, 6)))
-    e.close()
+@pytest.mark.parametrize("with_a", [False, True], ids=["Bbeta", "Bbeta_a"])
+@pytest.mark.parametrize("prec", [L.F64, L.F32], ids=["f64", "f32"])
+def test_ou_td_aux_blocking_loop_device_equals_oracle(prec, with_a):
+    """OU (scan kernels, multi-segment blocks, P_last laws) with time-dependent auxiliary laws
+    on half the segments: device == oracle bit for bit through set_obs!, the filter, loglikhd!,
+    draws with caller and device normals, accept and recompute_path!."""
+    case, (dev, ora), ids = _td_pair(L.MAP_AUTO, prec, with_a=with_a, model=cs.ou_ragged_model())
+    rng = np.random.default_rng(8)
+    for ad, ao in _ou_loop([dev, ora], ids, dev.S, 4, rng):
+        assert np.array_equal(ad, ao)
+    for kind in (L.LAW_PP, L.LAW_PPB):
+        for a_, b_ in zip(dev.download_law(L.U, kind), ora.download_law(L.U, kind)):
+            assert np.array_equal(a_, b_), kind
+    cs.assert_paths_equal(dev, ora)
+    for ad, ao in _ou_loop([dev, ora], ids, dev.S, 2, rng, device_rng=True):
+        assert np.array_equal(ad, ao)
+    for lid, nb in ids:
+        cs.assert_ll_equal(dev, ora, lid, nb)
+        for e in (dev, ora):
+            e.recompute_path(lid, 0, nb)
+        cs.assert_paths_equal(dev, ora)
+        cs.assert_ll_equal(dev, ora, lid, nb)
+    dev.close()
+
+
+@pytest.mark.gpu
+def test_ou_td_aux_mcmc_run_device_equals_oracle():
+    """dmt_mcmc_run on an OU ensemble with time-dependent auxiliary laws (k_mcmc_scan's TD
+    instantiation; the register-resident kernels are not eligible): fetch_ll results, paths,
+    ll and histories equal the oracle's, bit for bit."""
+    case, (dev, ora), ids = _td_pair(L.MAP_AUTO, L.F64, model=cs.ou_ragged_model(), hist_len=7)
+    lid, nb = ids[0]
+    for e in (dev, ora):
+        e.loglikhd(lid, L.U, 0, nb)
+    assert np.array_equal(dev.mcmc_run(lid, 0, nb, 1, 6, salt=7), ora.mcmc_run(lid, 0, nb, 1, 6, salt=7))
+    cs.assert_paths_equal(dev, ora)
+    for what in (L.BLK_LL, L.BLK_LLPROP):
+        assert np.array_equal(dev.get_block_state(lid, what, 0, nb), ora.get_block_state(lid, what, 0, nb))
+    for what in (L.BLK_ACC_HIST, L.BLK_LL_HIST, L.BLK_LLPROP_HIST):
+        assert np.array_equal(dev.get_block_state(lid, what, 0, nb, 7),
+                              ora.get_block_state(lid, what, 0, nb, 7))
+    dev.close()
 
 
 def test_oracle_varying_table_enters_girsanov_and_filter():
