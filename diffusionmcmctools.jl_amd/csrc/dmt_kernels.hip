@@ -1728,6 +1728,87 @@ __device__ __forceinline__ float lane_read(float v, int addr) {
   return __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(addr, __builtin_bit_cast(int, v)));
 }
 
+// DPP moves (VALU, no LDS round trip): lane l receives lane src(l) of the pattern CTRL in the
+// rows ROWMASK enables; the other lanes keep their own value (bound_ctrl off, old = v).
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ double dpp_mov(double v) {
+  const int2 p = __builtin_bit_cast(int2, v);
+  int2 r;
+  r.x = __builtin_amdgcn_update_dpp(p.x, p.x, CTRL, ROWMASK, 0xF, false);
+  r.y = __builtin_amdgcn_update_dpp(p.y, p.y, CTRL, ROWMASK, 0xF, false);
+  return __builtin_bit_cast(double, r);
+}
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ float dpp_mov(float v) {
+  const int p = __builtin_bit_cast(int, v);
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(p, p, CTRL, ROWMASK, 0xF, false));
+}
+constexpr int kDppRowShr = 0x110;    // row_shr:n = kDppRowShr + n (within rows of 16 lanes)
+constexpr int kDppRowBcast15 = 0x142;  // lane 15 of a row → the next row
+constexpr int kDppRowBcast31 = 0x143;  // lane 31 → rows 2 and 3
+constexpr int kDppWaveShr1 = 0x138;    // lane l − 1 → lane l
+
+// One level of the wave's inclusive scan of affine maps: lanes with `take` compose their map
+// after the map DPP pattern CTRL brings them (An = own ∘ received, affine_compose's order).
+template <int CTRL, int ROWMASK, int D, class T>
+__device__ __forceinline__ void affine_scan_level(T* RA, T* Re, const bool take) {
+  T Ap[D * D], ep[D], An[D * D], en[D];
+#pragma unroll
+  for (int c = 0; c < D * D; ++c) Ap[c] = dpp_mov<CTRL, ROWMASK>(RA[c]);
+#pragma unroll
+  for (int c = 0; c < D; ++c) ep[c] = dpp_mov<CTRL, ROWMASK>(Re[c]);
+  affine_compose<D, T>(RA, Re, Ap, ep, An, en);
+#pragma unroll
+  for (int c = 0; c < D * D; ++c) RA[c] = take ? An[c] : RA[c];
+#pragma unroll
+  for (int c = 0; c < D; ++c) Re[c] = take ? en[c] : Re[c];
+}
+// Inclusive scan of the 64 lanes' maps (lane j ← map_j ∘ … ∘ map_0).  DMT_SCAN_DPP = 1: the DPP
+// tree the oracle restates with ORC_SCAN_DPP = 1 (dmt_oracle.c wave_scan_dpp) — Kogge–Stone
+// within each row of 16 lanes (shifts 1, 2, 4, 8), then rows 1 and 3 compose after lane 15 /
+// lane 47 (row_bcast:15), then rows 2 and 3 after lane 31 (row_bcast:31); every level is VALU
+// work, no ds_bpermute round trip on the chain.  0: the 64-lane Kogge–Stone over ds_bpermute.
+#ifndef DMT_SCAN_DPP  // 0: the 64-lane Kogge–Stone over ds_bpermute (oracle ORC_SCAN_DPP = 0)
+#define DMT_SCAN_DPP 0
+#endif
+template <int D, class T>
+__device__ __forceinline__ void wave_affine_scan(T* RA, T* Re, const int lane) {
+#if !DMT_SCAN_DPP
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    T Ap[D * D], ep[D], An[D * D], en[D];
+    const int src = 4 * (lane - o);  // lanes < o read garbage and keep their own map
+#pragma unroll
+    for (int c = 0; c < D * D; ++c) Ap[c] = lane_read(RA[c], src);
+#pragma unroll
+    for (int c = 0; c < D; ++c) ep[c] = lane_read(Re[c], src);
+    affine_compose<D, T>(RA, Re, Ap, ep, An, en);
+    const bool take = lane >= o;
+#pragma unroll
+    for (int c = 0; c < D * D; ++c) RA[c] = take ? An[c] : RA[c];
+#pragma unroll
+    for (int c = 0; c < D; ++c) Re[c] = take ? en[c] : Re[c];
+  }
+  return;
+#endif
+  const int rl = lane & 15;
+  affine_scan_level<kDppRowShr + 1, 0xF, D, T>(RA, Re, rl >= 1);
+  affine_scan_level<kDppRowShr + 2, 0xF, D, T>(RA, Re, rl >= 2);
+  affine_scan_level<kDppRowShr + 4, 0xF, D, T>(RA, Re, rl >= 4);
+  affine_scan_level<kDppRowShr + 8, 0xF, D, T>(RA, Re, rl >= 8);
+  affine_scan_level<kDppRowBcast15, 0xA, D, T>(RA, Re, (lane & 16) != 0);
+  affine_scan_level<kDppRowBcast31, 0xC, D, T>(RA, Re, lane >= 32);
+}
+// The exclusive form's start points: lane l receives lane l − 1's value (lane 0: its own)
+template <class T>
+__device__ __forceinline__ T wave_shr1(T v) {
+#if DMT_SCAN_DPP
+  return dpp_mov<kDppWaveShr1, 0xF>(v);
+#else
+  return lane_read(v, 4 * ((int)(threadIdx.x & 63) - 1));
+#endif
+}
+
 // Store one point's N components (16-byte stores when N is even and T is double).
 template <int N, class T>
 __device__ __forceinline__ void store_row(T* p, const T* v) {
@@ -1951,22 +2032,8 @@ __device__ __forceinline__ void scan_block(const BlockArgs<T>& a, const int64_t 
 #pragma unroll
         for (int c = 0; c < D; ++c) Re[c] = en[c];
       }
-      // inclusive Kogge–Stone scan over the lanes: lane j ← run_j ∘ … ∘ run_0
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        T Ap[D * D], ep[D], An[D * D], en[D];
-        const int src = 4 * (lane - o);  // lanes < o read garbage and keep their own map
-#pragma unroll
-        for (int c = 0; c < D * D; ++c) Ap[c] = lane_read(RA[c], src);
-#pragma unroll
-        for (int c = 0; c < D; ++c) ep[c] = lane_read(Re[c], src);
-        affine_compose<D, T>(RA, Re, Ap, ep, An, en);
-        const bool take = lane >= o;
-#pragma unroll
-        for (int c = 0; c < D * D; ++c) RA[c] = take ? An[c] : RA[c];
-#pragma unroll
-        for (int c = 0; c < D; ++c) Re[c] = take ? en[c] : Re[c];
-      }
+      // inclusive scan over the lanes: lane j ← run_j ∘ … ∘ run_0
+      wave_affine_scan<D, T>(RA, Re, lane);
       // start of run j = prefix_{j-1} applied to the chunk start (lane 0: the chunk start)
       T x[D];
       {
@@ -1974,7 +2041,7 @@ __device__ __forceinline__ void scan_block(const BlockArgs<T>& a, const int64_t 
         affine_apply<D, T>(RA, Re, xc, y);
 #pragma unroll
         for (int p = 0; p < D; ++p) {
-          const T up = lane_read(y[p], 4 * (lane - 1));
+          const T up = wave_shr1<T>(y[p]);
           x[p] = lane == 0 ? xc[p] : up;
         }
       }
@@ -2533,28 +2600,14 @@ __device__ __forceinline__ void resident_block(const BlockArgs<T>& a, const Acce
 #pragma unroll
       for (int p = 0; p < D; ++p) Re[p] = en[p];
     }
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      T Ap[D * D], ep[D], An[D * D], en[D];
-      const int src = 4 * (lane - o);
-#pragma unroll
-      for (int cc = 0; cc < D * D; ++cc) Ap[cc] = lane_read(RA[cc], src);
-#pragma unroll
-      for (int p = 0; p < D; ++p) ep[p] = lane_read(Re[p], src);
-      affine_compose<D, T>(RA, Re, Ap, ep, An, en);
-      const bool take = lane >= o;
-#pragma unroll
-      for (int cc = 0; cc < D * D; ++cc) RA[cc] = take ? An[cc] : RA[cc];
-#pragma unroll
-      for (int p = 0; p < D; ++p) Re[p] = take ? en[p] : Re[p];
-    }
+    wave_affine_scan<D, T>(RA, Re, lane);
     T x[D];
     {
       T y[D];
       affine_apply<D, T>(RA, Re, x0, y);
 #pragma unroll
       for (int p = 0; p < D; ++p) {
-        const T up = lane_read(y[p], 4 * (lane - 1));
+        const T up = wave_shr1<T>(y[p]);
         x[p] = lane == 0 ? x0[p] : up;
       }
     }
@@ -2998,28 +3051,14 @@ __device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, cons
         for (int p = 0; p < D; ++p) Re[p] = en[p];
       }
     }
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      T Ap[D * D], ep[D], An[D * D], en[D];
-      const int src = 4 * (lane - o);
-#pragma unroll
-      for (int cc = 0; cc < D * D; ++cc) Ap[cc] = lane_read(RA[cc], src);
-#pragma unroll
-      for (int p = 0; p < D; ++p) ep[p] = lane_read(Re[p], src);
-      affine_compose<D, T>(RA, Re, Ap, ep, An, en);
-      const bool take = lane >= o;
-#pragma unroll
-      for (int cc = 0; cc < D * D; ++cc) RA[cc] = take ? An[cc] : RA[cc];
-#pragma unroll
-      for (int p = 0; p < D; ++p) Re[p] = take ? en[p] : Re[p];
-    }
+    wave_affine_scan<D, T>(RA, Re, lane);
     T x[D];
     {
       T y[D];
       affine_apply<D, T>(RA, Re, x0, y);
 #pragma unroll
       for (int p = 0; p < D; ++p) {
-        const T up = lane_read(y[p], 4 * (lane - 1));
+        const T up = wave_shr1<T>(y[p]);
         x[p] = lane == 0 ? x0[p] : up;
       }
     }

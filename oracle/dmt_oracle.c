@@ -271,6 +271,33 @@ static void aff_apply(int d, const REAL* A, const REAL* e, const REAL* x, REAL* 
 #define ORC_RUN 8
 #define ORC_SCHUNK 512
 extern int orc_ll_skip;
+/* The kernels' inclusive scan of the 64 lanes' run maps (libdmt wave_affine_scan, DPP):
+ * Kogge–Stone within each row of 16 lanes (lane j composes after lane j − o when j mod 16 >= o,
+ * o = 1, 2, 4, 8), then rows 1 and 3 after lane 15 / 47 (row_bcast:15), then rows 2 and 3 after
+ * lane 31 (row_bcast:31); every level reads the previous level's maps. */
+#ifndef ORC_SCAN_DPP  /* the tree libdmt is built with (DMT_SCAN_DPP) */
+#define ORC_SCAN_DPP 0
+#endif
+#if ORC_SCAN_DPP
+static int dpp_src(int level, int j) {
+    if (level < 4) { int o = 1 << level; return (j & 15) >= o ? j - o : -1; }
+    if (level == 4) return (j & 16) ? (j & ~15) - 1 : -1;
+    return j >= 32 ? 31 : -1;
+}
+static void wave_scan_dpp(int d, REAL RA[64][9], REAL Re[64][3], REAL An[64][9], REAL en[64][3]) {
+    for (int level = 0; level < 6; ++level) {
+        for (int j = 0; j < 64; ++j) {
+            int src = dpp_src(level, j);
+            if (src >= 0) aff_compose(d, RA[j], Re[j], RA[src], Re[src], An[j], en[j]);
+        }
+        for (int j = 0; j < 64; ++j) {
+            if (dpp_src(level, j) < 0) continue;
+            memcpy(RA[j], An[j], sizeof(REAL) * d * d);
+            memcpy(Re[j], en[j], sizeof(REAL) * d);
+        }
+    }
+}
+#endif
 static inline const REAL* aux_coeffs(const double* law, int model, int d, int i, const REAL* Bt,
                                      const REAL* beta, REAL* Bq, REAL* bq, const REAL** bo,
                                      const REAL* a, const REAL* da, int trace, REAL* dq,
@@ -326,6 +353,9 @@ static int solve_segment_scan(const double* law, int d, int m, const REAL* th, c
                 memcpy(Re[j], te, sizeof(REAL) * d);
             }
         }
+#if ORC_SCAN_DPP
+        wave_scan_dpp(d, RA, Re, An, en);
+#else
         for (int o = 1; o < 64; o <<= 1) {
             for (int j = o; j < 64; ++j) aff_compose(d, RA[j], Re[j], RA[j - o], Re[j - o], An[j], en[j]);
             for (int j = o; j < 64; ++j) {
@@ -333,6 +363,7 @@ static int solve_segment_scan(const double* law, int d, int m, const REAL* th, c
                 memcpy(Re[j], en[j], sizeof(REAL) * d);
             }
         }
+#endif
         REAL xend[3];
         for (int j = 0; j < 64 && ORC_RUN * j < cnt; ++j) {
             REAL x[3];

@@ -30,7 +30,7 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(HERE, "liboracle.so")
+LIB = os.environ.get("DMT_ORACLE_LIB") or os.path.join(HERE, "liboracle.so")  # measurement variants
 
 LAW_STRIDE = 64
 L_C0 = 49
