@@ -80,8 +80,25 @@ def measured_traffic(config, kernel_substr):
         with open(path) as f:
             t = json.load(f)
         if kernel_substr in t.get("kernel", ""):
-            return t["traffic_bytes_per_launch"], os.path.relpath(path, ROOT)
+            per_unit = t.get("traffic_bytes_per_unit")
+            if per_unit is None:  # summaries of one unit per launch written before the field
+                per_unit = t["traffic_bytes_per_launch"] / max(1, t.get("units_per_launch", 1))
+            return per_unit, os.path.relpath(path, ROOT)
     return None, None
+
+
+def rocprof_kernel(config, kernel_substr):
+    """The dominant kernel's average dispatch duration from the newest committed rocprofv3
+    kernel-trace summary of this config (profiles/rNN_kstats_<config>.json,
+    scripts/kstats_summary.py); None if absent."""
+    for path in _newest(f"r*_kstats_{config}.json"):
+        with open(path) as f:
+            t = json.load(f)
+        if kernel_substr in t.get("kernel", "") or t.get("kernel", "") in kernel_substr:
+            t = dict(t)
+            t["summary"] = os.path.relpath(path, ROOT)
+            return t
+    return None
 
 
 def issue_roofline(config, kernel_substr):
@@ -452,6 +469,10 @@ def main(argv=None):
     if traffic is not None:
         traffic *= it_per_launch
     issue = issue_roofline(args.config, kname)
+    rp = rocprof_kernel(args.config, kname)
+    rp_us = None
+    if rp is not None and rp.get("units_per_launch", 1) == it_per_launch:  # same launch shape
+        rp_us = rp["avg_us"]
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
@@ -492,6 +513,12 @@ def main(argv=None):
                                             "+ fetch_ll of every iteration of the launch)" if persist else
                                             " (draw_proposal_path!)"),
                          "kernel_avg_us": k_avg_s * 1e6,
+                         # the same kernel's average dispatch in the committed rocprofv3 trace of
+                         # this config (the profiler's clock; the line's own figure is HIP events)
+                         "kernel_avg_us_rocprof": rp_us,
+                         "frac_rocprof": (bytes_launch / (rp_us * 1e-6) / 1e9 / PEAK_HBM_GBS
+                                          if rp_us else None),
+                         "rocprof_source": (rp or {}).get("summary"),
                          "kernel_us_per_iteration": k_iter_s * 1e6,
                          "iterations_per_launch": it_per_launch,
                          "algorithmic_bytes_per_launch": bytes_launch,

@@ -2355,7 +2355,7 @@ __device__ __forceinline__ void persistent_tree_tail(const double* __restrict__ 
 // then — uniformly, exactly as k_accept — the MH decision, selector flips (bit masks in
 // SGPRs), histories and the ll swap.  Per-iteration (ll, ll°, accepted) go to
 // part[n_iter][3][nb]; persistent_tree_tail forms every iteration's fetch_ll from them.
-template <class Mdl, class T, bool TD = false>
+template <class Mdl, class T>
 __device__ __forceinline__ void mcmc_scan_block(const BlockArgs<T>& a, const AcceptArgs& c,
                                                 const int64_t iter0, const int64_t n_iter,
                                                 double* __restrict__ part, const int64_t blk,
@@ -2374,7 +2374,7 @@ __device__ __forceinline__ void mcmc_scan_block(const BlockArgs<T>& a, const Acc
     const double E = exp1_draw(c.seed, (uint32_t)g0 + c.seg_base, (uint32_t)(it + c.key_delta), c.salt);
     T lp;
     bool ok;
-    scan_block<Mdl, T, MODE_PCN, SelMask, TD>(a, blk, (uint32_t)(it + c.key_delta), sel, L, lp, ok);
+    scan_block<Mdl, T, MODE_PCN>(a, blk, (uint32_t)(it + c.key_delta), sel, L, lp, ok);
     llp = ok ? (double)lp : -INFINITY;
     const bool acc = E > -(llp - ll);
     if (acc) {
@@ -2412,7 +2412,7 @@ __device__ __forceinline__ void mcmc_scan_block(const BlockArgs<T>& a, const Acc
   }
 }
 
-template <class Mdl, class T, bool TD = false>
+template <class Mdl, class T>
 __global__ __launch_bounds__((64 * ScanCfg<Mdl::D, T>::WPB), 1) void k_mcmc_scan(
     const BlockArgs<T> a, const AcceptArgs c, const int64_t iter0, const int64_t n_iter,
     double* __restrict__ part, double* __restrict__ nodes, unsigned* __restrict__ counter,
@@ -2421,7 +2421,7 @@ __global__ __launch_bounds__((64 * ScanCfg<Mdl::D, T>::WPB), 1) void k_mcmc_scan
   __shared__ ScanLds<Mdl::D, T> lds[Cfg::WPB];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t blk = a.b0 + (int64_t)blockIdx.x * Cfg::WPB + w;
-  if (blk < a.b1) mcmc_scan_block<Mdl, T, TD>(a, c, iter0, n_iter, part, blk, lds[w]);
+  if (blk < a.b1) mcmc_scan_block<Mdl, T>(a, c, iter0, n_iter, part, blk, lds[w]);
   persistent_tree_tail<Cfg::WPB>(part, nodes, a.b1 - a.b0, n_iter, counter, out3);
 }
 
@@ -2916,6 +2916,7 @@ __device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, cons
     const T c00 = (T)ldc(a.law[lsp][0] + (int64_t)g * DMT_LAW_STRIDE + DMT_LAW_C0);
     llobs = obs_term<D, T>(H0, F0, x0, c00);
   }
+  PC_STAMP(0, 6);
   const int nv = max(0, min(kRun, nst - kRun * lane));
   T Ac[kRun][D * D], dts[kRun], cgC[CRA][D];
 #pragma unroll
@@ -3003,6 +3004,7 @@ __device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, cons
         for (int k = 0; k < M; ++k) S.dw[lds_ix(kRun * lane + RC0 + r)][k] = dWC[r][k];
     }
   };
+  PC_STAMP(0, 7);
   draw_c((uint32_t)(iter0 + c.key_delta));
   propose_c();
   hand_dw();
@@ -4866,9 +4868,9 @@ static hipError_t launch_mcmc_t(const void* args, const AcceptArgs& c, int64_t i
     if (nwaves <= 0) return hipSuccess;
     // part[n][3][nwaves], then the tree nodes [n][3][ceil(nwaves / WPB)] (dmt_mcmc_run sizes it)
     double* nodes = part + 3 * n * nwaves;
-    const bool td = a.aux[0] || a.aux[1];  // time-dependent auxiliary laws: k_mcmc_scan only
+    // time-dependent auxiliary laws run the per-iteration kernels (dmt_mcmc_run's choice)
+    if (a.aux[0] || a.aux[1]) return hipErrorInvalidValue;
     if constexpr (Mdl::D <= 2) {
-      if (td) resident = 0;
       if (resident >= 2) {  // producer / consumer waves (k_mcmc_resident_pc), resident - 1 producers
         const SvcArgs none{};
         if (resident == 3)
@@ -4889,12 +4891,8 @@ static hipError_t launch_mcmc_t(const void* args, const AcceptArgs& c, int64_t i
       }
     }
     constexpr int WPB = ScanCfg<Mdl::D, T>::WPB;
-    if (td)
-      dlaunch(k_mcmc_scan<Mdl, T, true>, dim3((unsigned)((nwaves + WPB - 1) / WPB)), dim3(64 * WPB),
-              s, a, c, iter0, n, part, nodes, counter, out3);
-    else
-      dlaunch(k_mcmc_scan<Mdl, T>, dim3((unsigned)((nwaves + WPB - 1) / WPB)), dim3(64 * WPB), s, a,
-              c, iter0, n, part, nodes, counter, out3);
+    dlaunch(k_mcmc_scan<Mdl, T>, dim3((unsigned)((nwaves + WPB - 1) / WPB)), dim3(64 * WPB), s, a,
+            c, iter0, n, part, nodes, counter, out3);
     return hipGetLastError();
   } else {
     return hipErrorInvalidValue;

@@ -553,11 +553,10 @@ dmt_status run_block_kernel(dmt_ens* h, const Layout* L, int mode, int kind_time
     // lane pairs (k_block_pair): on request only — bit-identical, but measured no faster on C5
     // (1 862 / 1 925 vs 1 829 µs per draw) and slower on C3 (1 821 vs 1 301 µs):
     // profiles/r03d, DESIGN.md §6
-    // lane pairs: on request on the row layout (measured no faster there: profiles/r03d); on
-    // the packet layout (fp32) automatically when the draw has fewer waves than the device has
-    // SIMDs (C5), DMT_LANE_PAIR=0/1 to force (lane packets)
-    a.lane_pair = h->pk ? (h->lane_pair == 1 || (h->lane_pair < 0 && 2 * nwaves <= h->n_simd))
-                        : h->lane_pair == 1;
+    // lane pairs: on request only (DMT_LANE_PAIR=1) — bit-identical, but no faster on the row
+    // layout (profiles/r03d) and slower on the packet layout: C5 1 753–1 789 vs 1 455–1 463 µs
+    // per draw with register-staged packets (profiles/r04g)
+    a.lane_pair = h->lane_pair == 1;
     a.lane_split = !a.lane_pair && !h->pk && L->single_seg &&
                    (h->lane_split == 1 || (h->lane_split < 0 && nwaves < h->n_simd &&
                                            h->key.precision == DMT_F64));
@@ -1680,10 +1679,12 @@ static dmt_status mcmc_run_launch(dmt_ens* h, Layout* L, int64_t b0, int64_t b1,
   // kernel eligibility of the range: from the layout's flags when they decide it (no host
   // loop over the blocks per call), else block by block
   const bool lay_res = L->single_seg && L->max_steps <= kResidentMaxSteps;
-  bool persist = h->persist && h->key.model == DMT_MODEL_OU;
+  // (an ensemble with a time-dependent auxiliary table runs the per-iteration kernels: the
+  // persistent ones take the law's own B̃, β̃)
+  bool persist = h->persist && h->key.model == DMT_MODEL_OU && !has_aux_table(h);
   for (int64_t b = b0; b < b1 && persist && !L->single_seg; ++b)
     persist = L->glast[b] - L->gfirst[b] + 1 <= kPersistMaxSegments;
-  bool resident = persist && h->key.d <= 2 && h->resident && !has_aux_table(h);
+  bool resident = persist && h->key.d <= 2 && h->resident;
   for (int64_t b = b0; b < b1 && resident && !lay_res; ++b)
     resident = L->glast[b] == L->gfirst[b] && h->seg_np[L->gfirst[b]] - 1 <= kResidentMaxSteps;
   if (persist) {

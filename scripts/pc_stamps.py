@@ -2,7 +2,8 @@
 """Where the fixed time of one C2 k_mcmc_resident_pc launch goes: device wall-clock stamps
 (100 MHz) per workgroup from a -DDMT_PC_STAMPS build (DMT_LIB_PATH=build_variants/
 libdmt_stamps.so): entry (0), consumer set-up done (1), producer first draw + propose done (2),
-B1 of iteration 0 passed (3), loop end (4), tree tail end (5).  Prints the spread over the
+B1 of iteration 0 passed (3), loop end (4), tree tail end (5), consumer: law record and
+loglikhd_obs done (6), per-step constants loaded (7) (before its own normals).  Prints the spread over the
 workgroups of each stage relative to the launch's first entry, for a few launches of
 --iters iterations, beside the HIP-event kernel time."""
 import argparse
@@ -48,11 +49,11 @@ for k in range(a.launches):
     assert fn(st.ctypes.data, st.size) == 0
     s = st[:nwg * 8].reshape(nwg, 8).astype(np.int64)
     t0 = s[:, 0].min()
-    rel = (s[:, :6] - t0) * 0.01  # µs
+    rel = (s[:, :8] - t0) * 0.01  # µs
     row = {"launch": k, "event_kernel_us": round(ms * 1e3, 2),  # one launch (n counts iterations)
            "span_us": float((s[:, 5].max() - t0) * 0.01)}
     for j, name in enumerate(["entry", "cons_setup", "prod_first_draw", "b1_iter0", "loop_end",
-                              "tail_end"]):
+                              "tail_end", "cons_law_obs", "cons_step_consts"]):
         v = rel[:, j]
         row[name] = {"min": round(float(v.min()), 2), "med": round(float(np.median(v)), 2),
                      "max": round(float(v.max()), 2)}

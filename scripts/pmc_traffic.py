@@ -7,7 +7,8 @@
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch (rocprofv3 counter_collection.csv).  Each is
 corrected by a factor measured with scripts/calib_stream (a known 1 GiB read + 1 GiB write at
 the same access width, fp64 8 B/lane or fp32 4 B/lane), as MI355X_MICROARCH.md prescribes for
-widths it does not calibrate.  Output: median corrected bytes per launch of the matching kernel.
+widths it does not calibrate.  Output: median corrected bytes per dispatch of the matching kernel,
+per launch and per unit (--units-per-launch: the iterations one persistent dispatch runs).
 """
 import argparse
 import csv
@@ -54,9 +55,12 @@ def main():
                  "fetch_kib_raw": statistics.median(cfv), "write_kib_raw": statistics.median(cwv)}
     f_b = statistics.median(fk) * 1024.0 * cf / a.units_per_launch
     w_b = statistics.median(wk) * 1024.0 * cw / a.units_per_launch
+    # per unit (an iteration of a persistent launch; 1 unit per launch otherwise) and per launch
     out = {"config": a.config, "kernel": a.kernel, "dispatches": [len(fk), len(wk)],
            "units_per_launch": a.units_per_launch,
-           "fetch_bytes": f_b, "write_bytes": w_b, "traffic_bytes_per_launch": f_b + w_b,
+           "fetch_bytes_per_unit": f_b, "write_bytes_per_unit": w_b,
+           "traffic_bytes_per_unit": f_b + w_b,
+           "traffic_bytes_per_launch": (f_b + w_b) * a.units_per_launch,
            "fetch_kib_raw_median": statistics.median(fk),
            "write_kib_raw_median": statistics.median(wk), "calibration": calib}
     with open(a.out, "w") as f:

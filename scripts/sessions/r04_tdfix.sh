@@ -1,0 +1,16 @@
+#!/bin/bash
+# Round 4: OU time-dependent dmt_mcmc_run on the per-iteration kernels (isolated first, launches
+# synchronous so that a fault names its call), the time-dependent tests, C2 launch stamps
+# (consumer set-up split), and the GPU suite.  Stops at the first failing step.
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/${TAG:-r04h}
+mkdir -p $O
+PT="python -u -m pytest -x -q -p no:cacheprovider --timeout 200 --timeout-method thread"
+HIP_LAUNCH_BLOCKING=1 timeout -k 10 200 $PT tests/test_td_aux.py -k ou_td_aux_mcmc_run > $O/pytest_ou_mcmc.log 2>&1 &&
+timeout -k 10 300 $PT tests/test_td_aux.py > $O/pytest_td.log 2>&1 &&
+DMT_LIB_PATH=build_variants/libdmt_stamps.so timeout -k 10 120 python scripts/pc_stamps.py > $O/c2_stamps.jsonl 2> $O/c2_stamps.err &&
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
+rc=$?
+echo "session rc=$rc"
+exit $rc

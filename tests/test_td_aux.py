@@ -10,8 +10,8 @@ converges (first order) as the grid is refined — the guiding term of the ODEs 
 GPU: device == oracle bit for bit on the ragged FHN ensemble with a varying table on part of
 the segments, through the blocking loop (set_obs!, recompute_guiding_term!, find_W_for_X!,
 loglikhd!, draws with caller and device normals, accept, recompute_path!), lane and wave
-mappings, fp64 and fp32; and on the ragged OU ensemble (scan kernels; dmt_mcmc_run's
-k_mcmc_scan too).
+mappings, fp64 and fp32; and on the ragged OU ensemble (scan kernels, through the blocking
+loop and dmt_mcmc_run).
 """
 from __future__ import annotations
 
@@ -474,9 +474,10 @@ def test_ou_td_aux_blocking_loop_device_equals_oracle(prec, with_a):
 
 @pytest.mark.gpu
 def test_ou_td_aux_mcmc_run_device_equals_oracle():
-    """dmt_mcmc_run on an OU ensemble with time-dependent auxiliary laws (k_mcmc_scan's TD
-    instantiation; the register-resident kernels are not eligible): fetch_ll results, paths,
-    ll and histories equal the oracle's, bit for bit."""
+    """dmt_mcmc_run on an OU ensemble with time-dependent auxiliary laws (the per-iteration
+    scan and accept kernels: the persistent and register-resident ones are not eligible while a
+    table is present): fetch_ll results, paths, ll and histories equal the oracle's, bit for
+    bit."""
     case, (dev, ora), ids = _td_pair(L.MAP_AUTO, L.F64, model=cs.ou_ragged_model(), hist_len=7)
     lid, nb = ids[0]
     for e in (dev, ora):
