@@ -2766,13 +2766,31 @@ __device__ uint64_t g_pc_stamps[8192 * 8];
 extern "C" int dmt_probe_pc_stamps(uint64_t* out, int64_t n) {
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pc_stamps), (size_t)std::min<int64_t>(n, 8192 * 8) * 8);
 }
+// per iteration r < 64 of workgroup 0: consumer after B1 (0), its decision made (1), at B2 (2),
+// after B2 (3); producer after B1 (4), at B2 with the next normals drawn (5), after B2 (6), at
+// B1 with the next proposal handed over (7)
+__device__ uint64_t g_pc_it[64 * 8];
+#define PC_ITSTAMP(TID, R, K)                                                             \
+  do {                                                                                    \
+    if (threadIdx.x == (TID) && blockIdx.x == 0 && (R) < 64)                              \
+      g_pc_it[(R) * 8 + (K)] = (uint64_t)wall_clock64();                                   \
+  } while (0)
+extern "C" int dmt_probe_pc_iter_stamps(uint64_t* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pc_it), 64 * 8 * 8);
+}
 #else
 #define PC_STAMP(TID, K) \
   do {                   \
   } while (0)
+#define PC_ITSTAMP(TID, R, K) \
+  do {                        \
+  } while (0)
 #endif
 #ifndef DMT_PC_DRAW_GROUP
 #define DMT_PC_DRAW_GROUP 8
+#endif
+#ifndef DMT_PC_SETUP_OVERLAP  // set-up loads in flight while the first normals are drawn
+#define DMT_PC_SETUP_OVERLAP 1
 #endif
 #ifndef DMT_PC_CONS_STEPS
 #define DMT_PC_CONS_STEPS 2
@@ -2891,6 +2909,39 @@ __device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, cons
   const int q0 = ldc(&bi->q0);
   const bool term = ldc(&bi->term) != 0;
   const int nst = ldc(a.seg_np + g) - 1;  // ≤ kSChunk
+  const T rho = (T)ldc(&bi->rho), srho = (T)ldc(&bi->srho);
+  const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32), c3 = a.salt << 1;
+  const double* Zg = a.Z ? a.Z + ldc(a.st_off + g) * M : nullptr;
+  T wvC[CRA][M], sdtC[CRA], zC[CRA][M], dWC[CRA][M];
+  auto draw_c = [&](uint32_t itv) {
+    if constexpr (CR > 0) {
+      if (Zg) {
+#pragma unroll
+        for (int r = 0; r < CR; ++r)
+#pragma unroll
+          for (int k = 0; k < M; ++k)
+            zC[r][k] = (T)Zg[(int64_t)min(kRun * lane + RC0 + r, nst - 1) * M + k];
+        return;
+      }
+      constexpr int NPB = NormPerBlock<T>::v, NB = CR * M / NPB, NBR = kRun * M / NPB;
+      T zz[CR * M];
+      uint32_t ln = (uint32_t)(NBR * lane + RC0 * M / NPB);  // opaque: no hoisting (producer)
+      asm volatile("" : "+v"(ln));
+#pragma unroll
+      for (int q = 0; q < NB; ++q)
+        normal_block(philox4x32_10(U4{ln + q, (uint32_t)g + a.seg_base, itv, c3}, k0, k1),
+                     zz + NPB * q);
+#pragma unroll
+      for (int r = 0; r < CR; ++r)
+#pragma unroll
+        for (int k = 0; k < M; ++k) zC[r][k] = zz[r * M + k];
+    }
+  };
+#if DMT_PC_SETUP_OVERLAP
+  // the first iteration's normals of the consumer's steps: they need the block's segment
+  // only, so their arithmetic runs while the metadata and per-step loads below are in flight
+  draw_c((uint32_t)(iter0 + c.key_delta));
+#endif
   const int64_t row = tq + q0;
   const int kind = term ? 0 : 1;
   const int ls = (kind ? ldc(a.selPPB + g) : ldc(a.selPP + g)) ^ a.law_flip;
@@ -2918,69 +2969,50 @@ __device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, cons
   }
   PC_STAMP(0, 6);
   const int nv = max(0, min(kRun, nst - kRun * lane));
-  T Ac[kRun][D * D], dts[kRun], cgC[CRA][D];
+  // ---- the consumer's own steps r in [RC0, kRun) of every run (PcConsSteps): u's increments,
+  // √dt, the normals of the next iteration, its pCN increments dW° (handed to the producer's
+  // W° stores through the dw slots after B2) and e maps (into its own pt slots)
+  // set-up: the run's per-step inputs, loaded before any of them is used
+  T tl[kRun], tr[kRun], Hs[kRun][HP], Fs[kRun][D];
 #pragma unroll
   for (int r = 0; r < kRun; ++r) {
     const int s = min(kRun * lane + r, nst - 1);
-    dts[r] = tb[s + 1] - tb[s];
-    T Hs[HP], Fs[D];
+    tl[r] = tb[s];
+    tr[r] = tb[s + 1];
 #pragma unroll
-    for (int cc = 0; cc < HP; ++cc) Hs[cc] = Hb[(int64_t)s * HP + cc];
+    for (int cc = 0; cc < HP; ++cc) Hs[r][cc] = Hb[(int64_t)s * HP + cc];
 #pragma unroll
-    for (int cc = 0; cc < D; ++cc) Fs[cc] = Fb[(int64_t)s * D + cc];
+    for (int cc = 0; cc < D; ++cc) Fs[r][cc] = Fb[(int64_t)s * D + cc];
+  }
+  if constexpr (CR > 0) {
+    const T* Ws = a.W[sel.w(g) ^ a.ws_flip] + row * M;
+#pragma unroll
+    for (int r = 0; r < CR; ++r) {
+      const int s = min(kRun * lane + RC0 + r, nst - 1);
+#pragma unroll
+      for (int k = 0; k < M; ++k) wvC[r][k] = Ws[(int64_t)(s + 1) * M + k];
+    }
+  }
+  T Ac[kRun][D * D], dts[kRun], cgC[CRA][D];
+#pragma unroll
+  for (int r = 0; r < kRun; ++r) {
+    dts[r] = tr[r] - tl[r];
     T Mg[D * D], cg_unused[D], zero[D] = {}, e_unused[D];
-    guide_coeffs<Mdl, T>(LA, Hs, Fs, Mg, cg_unused);
+    guide_coeffs<Mdl, T>(LA, Hs[r], Fs[r], Mg, cg_unused);
 #pragma unroll
-    for (int cc = 0; cc < HP; ++cc) S.hf[r][cc][lane] = Hs[cc];
+    for (int cc = 0; cc < HP; ++cc) S.hf[r][cc][lane] = Hs[r][cc];
 #pragma unroll
-    for (int cc = 0; cc < D; ++cc) S.hf[r][HP + cc][lane] = Fs[cc];
+    for (int cc = 0; cc < D; ++cc) S.hf[r][HP + cc][lane] = Fs[r][cc];
     affine_step<D, T>(Mg, cg_unused, dts[r], zero, Ac[r], e_unused);
     if (r >= RC0) {
 #pragma unroll
       for (int p = 0; p < D; ++p) cgC[r >= RC0 ? r - RC0 : 0][p] = cg_unused[p];
     }
   }
-  // ---- the consumer's own steps r in [RC0, kRun) of every run (PcConsSteps): u's increments,
-  // √dt, the normals of the next iteration, its pCN increments dW° (handed to the producer's
-  // W° stores through the dw slots after B2) and e maps (into its own pt slots)
-  const T rho = (T)ldc(&bi->rho), srho = (T)ldc(&bi->srho);
-  const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32), c3 = a.salt << 1;
-  const double* Zg = a.Z ? a.Z + ldc(a.st_off + g) * M : nullptr;
-  T wvC[CRA][M], sdtC[CRA], zC[CRA][M], dWC[CRA][M];
   if constexpr (CR > 0) {
-    const T* Ws = a.W[sel.w(g) ^ a.ws_flip] + row * M;
 #pragma unroll
-    for (int r = 0; r < CR; ++r) {
-      const int s = min(kRun * lane + RC0 + r, nst - 1);
-      sdtC[r] = sqrt(dts[RC0 + r]);
-#pragma unroll
-      for (int k = 0; k < M; ++k) wvC[r][k] = Ws[(int64_t)(s + 1) * M + k];
-    }
+    for (int r = 0; r < CR; ++r) sdtC[r] = sqrt(dts[RC0 + r]);
   }
-  auto draw_c = [&](uint32_t itv) {
-    if constexpr (CR > 0) {
-      if (Zg) {
-#pragma unroll
-        for (int r = 0; r < CR; ++r)
-#pragma unroll
-          for (int k = 0; k < M; ++k)
-            zC[r][k] = (T)Zg[(int64_t)min(kRun * lane + RC0 + r, nst - 1) * M + k];
-        return;
-      }
-      constexpr int NPB = NormPerBlock<T>::v, NB = CR * M / NPB, NBR = kRun * M / NPB;
-      T zz[CR * M];
-      uint32_t ln = (uint32_t)(NBR * lane + RC0 * M / NPB);  // opaque: no hoisting (producer)
-      asm volatile("" : "+v"(ln));
-#pragma unroll
-      for (int q = 0; q < NB; ++q)
-        normal_block(philox4x32_10(U4{ln + q, (uint32_t)g + a.seg_base, itv, c3}, k0, k1),
-                     zz + NPB * q);
-#pragma unroll
-      for (int r = 0; r < CR; ++r)
-#pragma unroll
-        for (int k = 0; k < M; ++k) zC[r][k] = zz[r * M + k];
-    }
-  };
   // dW° and e of the consumer's steps for the iteration whose normals are in zC; e → pt slots
   auto propose_c = [&]() {
     if constexpr (CR > 0) {
@@ -3005,7 +3037,9 @@ __device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, cons
     }
   };
   PC_STAMP(0, 7);
+#if !DMT_PC_SETUP_OVERLAP
   draw_c((uint32_t)(iter0 + c.key_delta));
+#endif
   propose_c();
   hand_dw();
   const uint64_t all = 1;
@@ -3030,6 +3064,7 @@ __device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, cons
     // them, so they can fill the scan's latency; the last iteration's are never used).  The
     // service draws them after B2 instead: there the iteration's latency is what the caller
     // waits for, and the host's round trip to the next post hides them.
+    PC_ITSTAMP(0, r0, 0);
     if constexpr (!SVC) draw_c((uint32_t)(it + 1 + c.key_delta));
     // the run map of the e maps the producer (and, for its steps, the consumer) left in the pt slots
     T RA[D * D], Re[D];
@@ -3137,6 +3172,7 @@ __device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, cons
       sel.mx ^= all;
       sel.mw ^= all;
     }
+    PC_ITSTAMP(0, r0, 1);
     if (lane == 0) {
       P.acc = acc ? 1 : 0;
       if (valid) {
@@ -3170,7 +3206,9 @@ __device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, cons
         propose_c();
       }
     }
+    PC_ITSTAMP(0, r0, 2);
     __syncthreads();  // B2: decision n → producer; pt reads of this iteration done
+    PC_ITSTAMP(0, r0, 3);
     if constexpr (SVC) {
       if constexpr (CR > 0) {
         draw_c((uint32_t)(it + 1 + c.key_delta));
@@ -3217,37 +3255,6 @@ __device__ __forceinline__ void resident_pc_producer(const BlockArgs<T>& a, cons
   const T srho = (T)ldc(&bi->srho);
   const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32), c3 = a.salt << 1;
   const int nst = ldc(a.seg_np + g) - 1;
-  const int64_t row = tq + q0;
-  const bool term = ldc(&bi->term) != 0;
-  const int kind = term ? 0 : 1;
-  const int ls = (kind ? ldc(a.selPPB + g) : ldc(a.selPP + g)) ^ a.law_flip;
-  Law<Mdl, T> LA;
-  LA.load(a.law[ls][kind] + (int64_t)g * DMT_LAW_STRIDE);
-  const T* tb = a.t_shared ? a.t + q0 : a.t + row;
-  const T* Hb = a.H_shared[ls][kind] ? a.H[ls][kind] + (int64_t)q0 * HP : a.H[ls][kind] + row * HP;
-  const T* Fb = a.F[ls][kind] + row * D;
-  SelMask sel{(uint64_t)sel_u(a.selX[g]), (uint64_t)sel_u(a.selW[g]), g};
-  T* const Wd[2] = {a.W[0] + row * M, a.W[1] + row * M};
-  T w0[M], dts[RR], sdts[RR], wv[RR][M], cgs[RR][D];
-  {
-    const T* Ws = a.W[sel.w(g) ^ a.ws_flip] + row * M;
-#pragma unroll
-    for (int k = 0; k < M; ++k) w0[k] = Ws[k];
-#pragma unroll
-    for (int r = 0; r < RR; ++r) {
-      const int s = min(kRun * lane + r0h + r, nst - 1);
-      dts[r] = tb[s + 1] - tb[s];
-      sdts[r] = sqrt(dts[r]);
-#pragma unroll
-      for (int k = 0; k < M; ++k) wv[r][k] = Ws[(int64_t)(s + 1) * M + k];
-      T Hs[HP], Fs[D], Mg_unused[D * D];
-#pragma unroll
-      for (int cc = 0; cc < HP; ++cc) Hs[cc] = Hb[(int64_t)s * HP + cc];
-#pragma unroll
-      for (int cc = 0; cc < D; ++cc) Fs[cc] = Fb[(int64_t)s * D + cc];
-      guide_coeffs<Mdl, T>(LA, Hs, Fs, Mg_unused, cgs[r]);
-    }
-  }
   const double* Zg = a.Z ? a.Z + ldc(a.st_off + g) * M : nullptr;  // parity-mode normals
   auto draw_z = [&](uint32_t itv, T (&z)[RR][M]) {
     if (Zg) {
@@ -3291,6 +3298,49 @@ __device__ __forceinline__ void resident_pc_producer(const BlockArgs<T>& a, cons
       for (int kk = 0; kk < M; ++kk) z[r][kk] = zz[r * M + kk];
   };
   T z[RR][M], w0n[M];
+#if DMT_PC_SETUP_OVERLAP
+  // the first iteration's normals: they need the block's segment only, so their arithmetic
+  // runs while the metadata and per-step loads below are in flight (bit-identical)
+  draw_z((uint32_t)(iter0 + c.key_delta), z);
+#endif
+  const int64_t row = tq + q0;
+  const bool term = ldc(&bi->term) != 0;
+  const int kind = term ? 0 : 1;
+  const int ls = (kind ? ldc(a.selPPB + g) : ldc(a.selPP + g)) ^ a.law_flip;
+  Law<Mdl, T> LA;
+  LA.load(a.law[ls][kind] + (int64_t)g * DMT_LAW_STRIDE);
+  const T* tb = a.t_shared ? a.t + q0 : a.t + row;
+  const T* Hb = a.H_shared[ls][kind] ? a.H[ls][kind] + (int64_t)q0 * HP : a.H[ls][kind] + row * HP;
+  const T* Fb = a.F[ls][kind] + row * D;
+  SelMask sel{(uint64_t)sel_u(a.selX[g]), (uint64_t)sel_u(a.selW[g]), g};
+  T* const Wd[2] = {a.W[0] + row * M, a.W[1] + row * M};
+  T w0[M], dts[RR], sdts[RR], wv[RR][M], cgs[RR][D];
+  {
+    // the per-step inputs, loaded before any of them is used
+    const T* Ws = a.W[sel.w(g) ^ a.ws_flip] + row * M;
+#pragma unroll
+    for (int k = 0; k < M; ++k) w0[k] = Ws[k];
+    T tl[RR], tr[RR], Hs[RR][HP], Fs[RR][D];
+#pragma unroll
+    for (int r = 0; r < RR; ++r) {
+      const int s = min(kRun * lane + r0h + r, nst - 1);
+      tl[r] = tb[s];
+      tr[r] = tb[s + 1];
+#pragma unroll
+      for (int k = 0; k < M; ++k) wv[r][k] = Ws[(int64_t)(s + 1) * M + k];
+#pragma unroll
+      for (int cc = 0; cc < HP; ++cc) Hs[r][cc] = Hb[(int64_t)s * HP + cc];
+#pragma unroll
+      for (int cc = 0; cc < D; ++cc) Fs[r][cc] = Fb[(int64_t)s * D + cc];
+    }
+#pragma unroll
+    for (int r = 0; r < RR; ++r) {
+      dts[r] = tr[r] - tl[r];
+      sdts[r] = sqrt(dts[r]);
+      T Mg_unused[D * D];
+      guide_coeffs<Mdl, T>(LA, Hs[r], Fs[r], Mg_unused, cgs[r]);
+    }
+  }
   // dW° of the iteration whose normals are in z → dw slots, its e maps
   // e_i = fma(c_i, dt_i, σ·dW°_i) → pt slots (run order), w0n = ρ·W(t0)
   auto propose = [&]() {
@@ -3326,13 +3376,16 @@ __device__ __forceinline__ void resident_pc_producer(const BlockArgs<T>& a, cons
     }
     if (h == 0 && lane == 0) store_row<M, T>(Wdb, w0n);
   };
+#if !DMT_PC_SETUP_OVERLAP
   draw_z((uint32_t)(iter0 + c.key_delta), z);
+#endif
   propose();
   PC_STAMP(256, 2);  // producer 0 of workgroup block 0 (BPW = 4)
   __syncthreads();  // B1 of iteration 0
   if constexpr (!SVC) store_w();
   for (int64_t r0 = 0; r0 < n_iter; ++r0) {
     const bool more = r0 + 1 < n_iter;
+    PC_ITSTAMP(256, r0, 4);
     // the next iteration's normals (they depend on the stream key alone), while the consumer
     // runs this one
     if (more) draw_z((uint32_t)(iter0 + r0 + 1 + c.key_delta), z);
@@ -3340,7 +3393,9 @@ __device__ __forceinline__ void resident_pc_producer(const BlockArgs<T>& a, cons
       if (!svc_gate(sv, r0, sl)) break;
       store_w();
     }
+    PC_ITSTAMP(256, r0, 5);
     __syncthreads();  // B2: decision n
+    PC_ITSTAMP(256, r0, 6);
     if (P.acc) {  // u's increments ← the accepted proposal's, still in the dw slots
       sel.mx ^= 1;
       sel.mw ^= 1;
@@ -3353,6 +3408,7 @@ __device__ __forceinline__ void resident_pc_producer(const BlockArgs<T>& a, cons
     }
     if (more) {
       propose();
+      PC_ITSTAMP(256, r0, 7);
       __syncthreads();  // B1: dW° of iteration n + 1 ready
       if constexpr (!SVC) store_w();
     }

@@ -61,3 +61,20 @@ for k in range(a.launches):
     row["per_iter_us_med"] = round(row["loop_us_med"] / a.iters, 3)
     out.append(row)
     print(json.dumps(row), flush=True)
+
+# per-iteration stamps of workgroup 0 (the last launch): durations in µs per iteration
+fi = L.lib.dmt_probe_pc_iter_stamps
+fi.argtypes = [C.c_void_p]
+it = np.zeros(64 * 8, dtype=np.uint64)
+assert fi(it.ctypes.data) == 0
+t = it.reshape(64, 8).astype(np.int64)[:a.iters]
+d = lambda i, j: np.median((t[:, j] - t[:, i]) * 0.01)  # noqa: E731
+cyc = np.median(np.diff(t[:, 0]) * 0.01)
+print(json.dumps({"wg0_iteration_us": round(float(cyc), 3),
+                  "cons_B1_to_decision": round(float(d(0, 1)), 3),
+                  "cons_decision_to_B2_arrive": round(float(d(1, 2)), 3),
+                  "cons_B2_wait": round(float(d(2, 3)), 3),
+                  "prod_B1_to_B2_arrive (W stores + draw)": round(float(d(4, 5)), 3),
+                  "prod_B2_wait": round(float(d(5, 6)), 3),
+                  "prod_B2_to_B1_arrive (propose)": round(float(d(6, 7)), 3),
+                  "cons_B2_to_next_B1_pass": round(float(np.median((t[1:, 0] - t[:-1, 3]) * 0.01)), 3)}))
