@@ -2789,6 +2789,12 @@ extern "C" int dmt_probe_pc_iter_stamps(uint64_t* out) {
 #ifndef DMT_PC_DRAW_GROUP
 #define DMT_PC_DRAW_GROUP 8
 #endif
+#ifndef DMT_PC_LATE_C  // the consumer forms its own steps' next proposal after B2
+#define DMT_PC_LATE_C 1
+#endif
+#ifndef DMT_PC_SPEC  // the producer forms both candidates of the next proposal before B2
+#define DMT_PC_SPEC 1
+#endif
 #ifndef DMT_PC_SETUP_OVERLAP  // set-up loads in flight while the first normals are drawn
 #define DMT_PC_SETUP_OVERLAP 1
 #endif
@@ -3201,7 +3207,7 @@ __device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, cons
 #pragma unroll
           for (int k = 0; k < M; ++k) wvC[r][k] = dWC[r][k];
       }
-      if constexpr (!SVC) {
+      if constexpr (!SVC && !DMT_PC_LATE_C) {
         wave_lds_sync();  // this wave's pt reads of the X° stores above are done
         propose_c();
       }
@@ -3209,6 +3215,9 @@ __device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, cons
     PC_ITSTAMP(0, r0, 2);
     __syncthreads();  // B2: decision n → producer; pt reads of this iteration done
     PC_ITSTAMP(0, r0, 3);
+    // (DMT_PC_LATE_C: the consumer's own steps of iteration n + 1 after B2, beside the producer's
+    // proposal — the consumer, not the producer, is the one late at B2)
+    if constexpr (!SVC && DMT_PC_LATE_C && CR > 0) propose_c();
     if constexpr (SVC) {
       if constexpr (CR > 0) {
         draw_c((uint32_t)(it + 1 + c.key_delta));
@@ -3343,22 +3352,32 @@ __device__ __forceinline__ void resident_pc_producer(const BlockArgs<T>& a, cons
   }
   // dW° of the iteration whose normals are in z → dw slots, its e maps
   // e_i = fma(c_i, dt_i, σ·dW°_i) → pt slots (run order), w0n = ρ·W(t0)
-  auto propose = [&]() {
+  // (dWp keeps this producer's dW° in registers: u's increments after an acceptance)
+  T dWp[RR][M];
+  auto propose_from = [&](const T (&dWs)[RR][M]) {
 #pragma unroll
     for (int r = 0; r < RR; ++r) {
       const int li = lds_ix(kRun * lane + r0h + r);
-      T dW[M], sdW[D];
+      T sdW[D];
 #pragma unroll
       for (int kk = 0; kk < M; ++kk) {
-        dW[kk] = dfma(rho, wv[r][kk], srho * (sdts[r] * z[r][kk]));
-        S.dw[li][kk] = dW[kk];
+        S.dw[li][kk] = dWs[r][kk];
+        dWp[r][kk] = dWs[r][kk];
       }
-      sigma_dw<Mdl, T>(LA, dW, sdW);
+      sigma_dw<Mdl, T>(LA, dWs[r], sdW);
 #pragma unroll
       for (int p = 0; p < D; ++p) S.pt[li][p] = dfma(cgs[r][p], dts[r], sdW[p]);
     }
 #pragma unroll
     for (int k = 0; k < M; ++k) w0n[k] = rho * w0[k];
+  };
+  auto propose = [&]() {
+    T dW[RR][M];
+#pragma unroll
+    for (int r = 0; r < RR; ++r)
+#pragma unroll
+      for (int kk = 0; kk < M; ++kk) dW[r][kk] = dfma(rho, wv[r][kk], srho * (sdts[r] * z[r][kk]));
+    propose_from(dW);
   };
   // coalesced W° stores of the proposal just handed over (after B1)
   auto store_w = [&]() {
@@ -3387,8 +3406,23 @@ __device__ __forceinline__ void resident_pc_producer(const BlockArgs<T>& a, cons
     const bool more = r0 + 1 < n_iter;
     PC_ITSTAMP(256, r0, 4);
     // the next iteration's normals (they depend on the stream key alone), while the consumer
-    // runs this one
-    if (more) draw_z((uint32_t)(iter0 + r0 + 1 + c.key_delta), z);
+    // runs this one, and both candidates of its pCN increments — u's increments are the
+    // current proposal's if the consumer accepts it, else they stay — so that after B2 only a
+    // selection, σ·dW° and the e maps stand between the decision and B1 (DMT_PC_SPEC)
+    T dWa[RR][M], dWr[RR][M];
+    if (more) {
+      draw_z((uint32_t)(iter0 + r0 + 1 + c.key_delta), z);
+#if DMT_PC_SPEC
+#pragma unroll
+      for (int r = 0; r < RR; ++r)
+#pragma unroll
+        for (int kk = 0; kk < M; ++kk) {
+          const T q = srho * (sdts[r] * z[r][kk]);
+          dWa[r][kk] = dfma(rho, dWp[r][kk], q);
+          dWr[r][kk] = dfma(rho, wv[r][kk], q);
+        }
+#endif
+    }
     if constexpr (SVC) {  // the service: W° of iteration n once the host has posted it
       if (!svc_gate(sv, r0, sl)) break;
       store_w();
@@ -3396,18 +3430,28 @@ __device__ __forceinline__ void resident_pc_producer(const BlockArgs<T>& a, cons
     PC_ITSTAMP(256, r0, 5);
     __syncthreads();  // B2: decision n
     PC_ITSTAMP(256, r0, 6);
-    if (P.acc) {  // u's increments ← the accepted proposal's, still in the dw slots
+    const bool acc = P.acc != 0;
+    if (acc) {  // u's increments ← the accepted proposal's
       sel.mx ^= 1;
       sel.mw ^= 1;
 #pragma unroll
-      for (int r = 0; r < RR; ++r)
-#pragma unroll
-        for (int k = 0; k < M; ++k) wv[r][k] = S.dw[lds_ix(kRun * lane + r0h + r)][k];
-#pragma unroll
       for (int k = 0; k < M; ++k) w0[k] = w0n[k];
     }
+#pragma unroll
+    for (int r = 0; r < RR; ++r)
+#pragma unroll
+      for (int k = 0; k < M; ++k) wv[r][k] = acc ? dWp[r][k] : wv[r][k];
     if (more) {
+#if DMT_PC_SPEC
+      T dWn[RR][M];
+#pragma unroll
+      for (int r = 0; r < RR; ++r)
+#pragma unroll
+        for (int k = 0; k < M; ++k) dWn[r][k] = acc ? dWa[r][k] : dWr[r][k];
+      propose_from(dWn);
+#else
       propose();
+#endif
       PC_ITSTAMP(256, r0, 7);
       __syncthreads();  // B1: dW° of iteration n + 1 ready
       if constexpr (!SVC) store_w();
