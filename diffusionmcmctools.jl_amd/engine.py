@@ -34,6 +34,7 @@ class Ensemble:
         self.grid_shared = bool(grid_shared)
         self.Q0 = int(self.npts[: self.nseg[0]].sum())
         self._h = C.c_void_p()
+        self._run_out = {}  # dmt_mcmc_run result buffers by run length (mcmc_run)
         self._hist_len = {0: 0}  # history length of each layout (dmt_get_block_state fills all)
         mdl = L.dmt_model(self.model, self.precision, self.d, self.m)
         st = L.dmt_structure(self.R, L.i32p(self.nseg), L.i32p(self.npts))
@@ -308,10 +309,16 @@ class Ensemble:
         """n_iter mcmc_step iterations without host synchronisation in between; returns
         (n_iter, 3): fetch_ll, fetch_ll°, accepted count per iteration (``local``: this rank's
         sums, no collective)."""
-        out = np.empty((int(n_iter), 3), dtype=np.float64)
-        L.call("dmt_mcmc_run_local" if local else "dmt_mcmc_run", self._h, layout, b0, b1, int(iter0), int(n_iter), int(salt),
-               L.f64p(out))
-        return out
+        n = int(n_iter)
+        buf = self._run_out.get(n)
+        if buf is None:  # one result buffer per run length, its address taken once
+            arr = np.empty((n, 3), dtype=np.float64)
+            buf = self._run_out[n] = (arr, arr.ctypes.data)
+        st = L.fast["dmt_mcmc_run_local" if local else "dmt_mcmc_run"](
+            self._h, layout, b0, b1, iter0, n, salt, buf[1])
+        if st:
+            L.check(st)
+        return buf[0].copy()
 
     def set_run_snapshots(self, every, slot0=0):
         """Snapshot u inside every later mcmc_run after each iteration k with k % every == 0
@@ -320,7 +327,9 @@ class Ensemble:
 
     # ---------------------------------------------------------------- misc
     def sync(self):
-        L.call("dmt_sync", self._h)
+        st = L.fast["dmt_sync"](self._h)
+        if st:
+            L.check(st)
 
     def set_service(self, enable=True, idle_ms=2.0):
         """The resident MCMC service's switch and idle window (dmt_set_service); idle_ms = 0
