@@ -1809,6 +1809,19 @@ __device__ __forceinline__ T wave_shr1(T v) {
 #endif
 }
 
+// store_row with nontemporal stores (the path stores of the resident MCMC kernels: written
+// once per iteration, read by no later iteration of the launch, DMT_PC_NT_STORES)
+template <int N, class T>
+__device__ __forceinline__ void store_row_nt(T* p, const T* v) {
+  if constexpr (std::is_same<T, double>::value && N % 2 == 0) {
+    typedef double d2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int c = 0; c < N; c += 2) __builtin_nontemporal_store(d2{v[c], v[c + 1]}, (d2*)(p + c));
+  } else {
+#pragma unroll
+    for (int c = 0; c < N; ++c) __builtin_nontemporal_store(v[c], p + c);
+  }
+}
 // Store one point's N components (16-byte stores when N is even and T is double).
 template <int N, class T>
 __device__ __forceinline__ void store_row(T* p, const T* v) {
@@ -1824,6 +1837,18 @@ __device__ __forceinline__ void store_row(T* p, const T* v) {
 #pragma unroll
     for (int c = 0; c < N; ++c) p[c] = v[c];
   }
+}
+
+#ifndef DMT_PC_NT_STORES
+#define DMT_PC_NT_STORES 1
+#endif
+template <int N, class T>
+__device__ __forceinline__ void store_row_pc(T* p, const T* v) {
+#if DMT_PC_NT_STORES
+  store_row_nt<N, T>(p, v);
+#else
+  store_row<N, T>(p, v);
+#endif
 }
 
 // Path selectors of the scan kernels: read from the ensemble arrays (one launch per call;
@@ -3163,10 +3188,10 @@ __device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, cons
           T xv[D];
 #pragma unroll
           for (int p = 0; p < D; ++p) xv[p] = S.pt[lds_ix(s)][p];
-          store_row<D, T>(Xdb + (int64_t)s * D, xv);
+          store_row_pc<D, T>(Xdb + (int64_t)s * D, xv);
         }
       }
-      if (lane == 0) store_row<D, T>(Xdb + (int64_t)nst * D, xe);
+      if (lane == 0) store_row_pc<D, T>(Xdb + (int64_t)nst * D, xe);
     }
     bool sok = isfinite(seg_acc);
 #pragma unroll
@@ -3390,10 +3415,10 @@ __device__ __forceinline__ void resident_pc_producer(const BlockArgs<T>& a, cons
         T wd[M];
 #pragma unroll
         for (int kk = 0; kk < M; ++kk) wd[kk] = S.dw[lds_ix(s)][kk];
-        store_row<M, T>(Wdb + (int64_t)(s + 1) * M, wd);
+        store_row_pc<M, T>(Wdb + (int64_t)(s + 1) * M, wd);
       }
     }
-    if (h == 0 && lane == 0) store_row<M, T>(Wdb, w0n);
+    if (h == 0 && lane == 0) store_row_pc<M, T>(Wdb, w0n);
   };
 #if !DMT_PC_SETUP_OVERLAP
   draw_z((uint32_t)(iter0 + c.key_delta), z);
