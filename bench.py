@@ -463,8 +463,11 @@ def main(argv=None):
         wave, kname = True, "k_block_resident"
     elif w.model.kind == L.MODEL_OU:  # linear drift: the affine-scan kernel per iteration
         wave, kname = True, "k_block_scan"
-    else:
-        kname = "k_block_wave" if wave else "k_block<"
+    elif wave:
+        kname = "k_block_wave"
+    else:  # lane mapping: fp32 ensembles on lane packets (dmt_create; DMT_PATH_PACKETS=0: rows)
+        kname = ("k_block_pk<" if w.precision == L.F32 and os.environ.get("DMT_PATH_PACKETS", "1") != "0"
+                 else "k_block<")
     traffic, traffic_src = measured_traffic(args.config, kname)  # HBM bytes per iteration
     if traffic is not None:
         traffic *= it_per_launch
@@ -500,7 +503,8 @@ def main(argv=None):
                                    "scan-persistent" if persist else
                                    "scan-resident-per-iteration" if kname == "k_block_resident" else
                                    "scan" if kname == "k_block_scan" else
-                                   "wave" if wave else "lane"),
+                                   "wave" if wave else
+                                   "lane-packets" if kname == "k_block_pk<" else "lane"),
                        "rng": "device Philox4x32-10 + Box-Muller (perf mode)"},
             "per_gpu": value / world,
             "accept_rate": accept_rate,
