@@ -3153,13 +3153,13 @@ __device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, cons
     }
     T xe[D];
 #pragma unroll
-    for (int p = 0; p < D; ++p) xe[p] = lane_read(x[p], 4 * last_lane);
+    for (int p = 0; p < D; ++p) xe[p] = lane_value(x[p], last_lane);  // uniform: v_readlane
     T tsum = ((gl[0] + gl[1]) + (gl[2] + gl[3])) + ((gl[4] + gl[5]) + (gl[6] + gl[7]));
     tsum = group_tree_sum<8, T>(tsum);
     T seg_acc = (T)0;
 #pragma unroll
     for (int q = 0; q < 8; ++q)
-      if (64 * q < nst) seg_acc = seg_acc + (lane_read(tsum, 4 * 8 * q) + (T)0);
+      if (64 * q < nst) seg_acc = seg_acc + (lane_value(tsum, 8 * q) + (T)0);
     // the service computes an iteration ahead of its post (registers and LDS only) and
     // publishes it — stores, flags, selectors, the decision — once the host has posted it.  The
     // block's fetch_ll leaves go to LDS before the gate, and the workgroup's records to the host
