@@ -224,6 +224,9 @@ struct dmt_ens {
   // dispatch packet (DMT_DISPATCH_EVENTS=1: hipExtLaunchKernel with events — the kernel's own
   // execution interval, but ≈ 10 µs more host time in the launch call, profiles/r02zo)
   bool dispatch_events = false;
+  // flags of the timing events (DMT_EVENT_FLAGS): they only measure, so a system-scope fence
+  // (cache writeback and invalidation when the event is recorded) buys nothing
+  unsigned event_flags = hipEventDefault;
   int resident_pc = 1;       // ... split over a consumer and this many producer waves per block
   bool pc_bpw1 = false;      // ... one block per workgroup (DMT_PC_BPW=1)
                              // (DMT_MCMC_PC=0: one wave; 1 or 2 producers)
@@ -281,7 +284,7 @@ hipEvent_t get_event(dmt_ens* h) {
     return e;
   }
   hipEvent_t e;
-  (void)hipEventCreate(&e);
+  (void)hipEventCreateWithFlags(&e, h->event_flags);
   return e;
 }
 
@@ -934,6 +937,7 @@ dmt_status dmt_create(dmt_ens** out, const dmt_model* model, const dmt_structure
   if (const char* e = std::getenv("DMT_MCMC_PC")) h->resident_pc = std::max(0, std::min(2, std::atoi(e)));
   if (const char* e = std::getenv("DMT_PC_BPW")) h->pc_bpw1 = std::atoi(e) == 1;
   if (const char* e = std::getenv("DMT_DISPATCH_EVENTS")) h->dispatch_events = std::strcmp(e, "0") != 0;
+  if (const char* e = std::getenv("DMT_EVENT_FLAGS")) h->event_flags = (unsigned)std::strtoul(e, nullptr, 0);
   if (const char* e = std::getenv("DMT_LANE_SPLIT")) h->lane_split = std::atoi(e);
   if (const char* e = std::getenv("DMT_LANE_PAIR")) h->lane_pair = std::atoi(e);
   if (const char* e = std::getenv("DMT_DEFER")) h->defer = std::atoi(e) != 0;
@@ -2680,7 +2684,7 @@ dmt_status dmt_set_timing(dmt_ens* h, int32_t on) {
   // (hipEventCreate is a driver call; the bench times its K steps right after this)
   while (h->timing && h->free_events.size() < 16) {
     hipEvent_t e;
-    HIP_OK(hipEventCreate(&e));
+    HIP_OK(hipEventCreateWithFlags(&e, h->event_flags));
     h->free_events.push_back(e);
   }
   return DMT_OK;
