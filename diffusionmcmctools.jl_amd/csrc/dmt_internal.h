@@ -97,6 +97,7 @@ struct BlockArgs {
   int full_copy;             // consolidation rewrites every lane's u (whole lines; DMT_FULL_COPY)
   const T* t;
   int t_shared;
+  const T* sdt;  // shared grid: sqrt(t[q+1] − t[q]) per point in T (dmt_upload_grid), else nullptr
   const T* H[2][2];  // [slot][kind]
   int H_shared[2][2];
   const T* F[2][2];

@@ -531,6 +531,9 @@ struct PairChunk {  // steps per chunk: an even number of whole Philox blocks of
 #ifndef DMT_PK_ROLL  // 1: u.W's next packet loaded piece by piece into the registers just consumed
 #define DMT_PK_ROLL 1   // 0: the whole next packet in a second register set
 #endif
+#ifndef DMT_PK_SDT_TABLE  // shared grids: the packet kernel reads √dt from a per-point table
+#define DMT_PK_SDT_TABLE 1
+#endif
 #ifndef DMT_PK_LDS  // 1: the packet's X°, W° staged in the lane's LDS rows
 #define DMT_PK_LDS 0   // 0: staged in registers (measured faster in the kernel: 1 455 vs 1 574 µs, C5)
 #endif
@@ -539,8 +542,9 @@ struct PairChunk {  // steps per chunk: an even number of whole Philox blocks of
 // recursion on the same values; role 0 stores X°, role 1 W° (every load is the same address
 // for both, one request).  Fills the chip with twice the waves when the ensemble has fewer
 // recording tiles than SIMDs (C5: 512 tiles, 1 024 SIMDs).  Bit-identical.
+// SDT: a shared grid's √dt table (BlockArgs::sdt) read per step in place of the square root
 template <class Mdl, class T, int MODE, bool PARITY, int K, bool TD, int PK, bool FAST,
-          bool PAIR = false>
+          bool PAIR = false, bool SDT = false>
 __device__ __forceinline__ bool run_segment_pk(const Law<Mdl, T>& L, const T* __restrict__ tpl,
                                                const int t_sh, const T* __restrict__ Ht,
                                                const int H_sh, const T* __restrict__ Ft,
@@ -549,7 +553,8 @@ __device__ __forceinline__ bool run_segment_pk(const Law<Mdl, T>& L, const T* __
                                                NormalStream<T>& ns, const int64_t tq,
                                                const int64_t q0, const int np, const int lane,
                                                const T rho, const T srho, const int ll_skip,
-                                               T* x, T& sl, T* stg, const int role = 0) {
+                                               T* x, T& sl, T* stg, const int role = 0,
+                                               const T* __restrict__ sdtab = nullptr) {
   constexpr int D = Mdl::D, M = Mdl::M, HP = D * (D + 1) / 2;
   constexpr bool DRAW = MODE != MODE_RECOMPUTE;
   constexpr bool READW = MODE != MODE_FRESH;
@@ -593,10 +598,11 @@ __device__ __forceinline__ bool run_segment_pk(const Law<Mdl, T>& L, const T* __
   ps.init();
   // one Euler step from registers (run_segment's step): dW (in: u's increment, out: the
   // proposal's), x advanced; returns the Girsanov term G·dt
-  auto step = [&](int i, T tn, const T* Hi, const T* Fi, T* dW, const T* Zi) -> T {
+  const T* sdb = SDT ? sdtab + q0 : nullptr;  // step i's √dt at sdb[i] (shared grid)
+  auto step = [&](int i, T tn, const T* Hi, const T* Fi, T* dW, const T* Zi, T sdt_i) -> T {
     const T dt = tn - tcur;
     if (DRAW) {
-      const T sdt = sqrt(dt);
+      const T sdt = SDT ? sdt_i : sqrt(dt);
 #pragma unroll
       for (int k = 0; k < M; ++k) dW[k] = dfma(rho, dW[k], srho * (sdt * Zi[k]));
     }
@@ -633,13 +639,14 @@ __device__ __forceinline__ bool run_segment_pk(const Law<Mdl, T>& L, const T* __
     return (MODE == MODE_RECOMPUTE && i >= nst - ll_skip) ? (T)0 : G * dt;
   };
   struct Chunk {
-    T t[K], H[K][HP], F[K][D], Z[K][M];
+    T t[K], s[K], H[K][HP], F[K][D], Z[K][M];
   };
   auto load = [&](int c0, Chunk& c) {  // the chunk's grid, guiding term, caller normals
 #pragma unroll
     for (int j = 0; j < K; ++j) {
       const int64_t i = c0 + j;
       c.t[j] = tb[(i + 1) * tst];
+      c.s[j] = (SDT && DRAW) ? sdb[i] : (T)0;
 #pragma unroll
       for (int e = 0; e < HP; ++e) c.H[j][e] = lane_ld(&Hb[(i * HP + e) * hst]);
 #pragma unroll
@@ -732,7 +739,7 @@ __device__ __forceinline__ bool run_segment_pk(const Law<Mdl, T>& L, const T* __
             T dW[M];
 #pragma unroll
             for (int k = 0; k < M; ++k) dW[k] = READW ? wc[k][e / VE][e % VE] : (T)0;
-            gv[q] = step(c0 + q, cur.t[q], cur.H[q], cur.F[q], dW, cur.Z[q]);
+            gv[q] = step(c0 + q, cur.t[q], cur.H[q], cur.F[q], dW, cur.Z[q], cur.s[q]);
             if constexpr (PAIR) {
 #pragma unroll
               for (int c = 0; c < NS; ++c)
@@ -814,7 +821,7 @@ __device__ __forceinline__ bool run_segment_pk(const Law<Mdl, T>& L, const T* __
       T gv[K];
 #pragma unroll
       for (int q = 0; q < K; ++q) {
-        gv[q] = step(c0 + q, cur.t[q], cur.H[q], cur.F[q], wu[q], cur.Z[q]);
+        gv[q] = step(c0 + q, cur.t[q], cur.H[q], cur.F[q], wu[q], cur.Z[q], cur.s[q]);
         if (stx) {
 #pragma unroll
           for (int p = 0; p < D; ++p) Xd[pix(c0 + q + 1, p, D)] = x[p];
@@ -840,7 +847,7 @@ __device__ __forceinline__ bool run_segment_pk(const Law<Mdl, T>& L, const T* __
       dW[k] = READW ? Ws[pix(q + 1, k, M)] : (T)0;
       Zi[k] = DRAW ? (PARITY ? (T)Zg[q * M + k] : ns.get((uint32_t)(i * M + k))) : (T)0;
     }
-    ps.add(step(i, tb[(q + 1) * tst], Hi, Fi, dW, Zi));
+    ps.add(step(i, tb[(q + 1) * tst], Hi, Fi, dW, Zi, (SDT && DRAW) ? sdb[q] : (T)0));
     if (stx) {
 #pragma unroll
       for (int p = 0; p < D; ++p) Xd[pix(q + 1, p, D)] = x[p];
@@ -857,7 +864,8 @@ __device__ __forceinline__ bool run_segment_pk(const Law<Mdl, T>& L, const T* __
   return ok;
 }
 
-template <class Mdl, class T, int MODE, bool PARITY, int K, bool TD, bool PAIR = false>
+template <class Mdl, class T, int MODE, bool PARITY, int K, bool TD, bool PAIR = false,
+          bool SDT = false>
 __device__ __forceinline__ void lane_block_pk(const BlockArgs<T>& a, const int64_t tile,
                                               const int64_t blk, const int lane, T* stg,
                                               const int role = 0) {
@@ -905,11 +913,12 @@ __device__ __forceinline__ void lane_block_pk(const BlockArgs<T>& a, const int64
     const int64_t q0 = a.seg_q[g];
     const bool aligned = __ballot(((tq + q0 + 1) & (PK - 1)) != 0) == 0;
     T sl;
+    // SDT (a shared grid with its √dt table, launch-time choice): the aligned segments read √dt
     const bool sok =
-        aligned ? run_segment_pk<Mdl, T, MODE, PARITY, K, TD, PK, true, PAIR>(
+        aligned ? run_segment_pk<Mdl, T, MODE, PARITY, K, TD, PK, true, PAIR, SDT>(
                       L, a.t, a.t_shared, a.H[ls][kind], a.H_shared[ls][kind], a.F[ls][kind],
                       a.aux[kind], Ws, Wd, Xd, Zg, ns, tq, q0, a.seg_np[g], lane, rho, srho,
-                      a.ll_skip, x, sl, stg, role)
+                      a.ll_skip, x, sl, stg, role, SDT ? a.sdt : nullptr)
                 : run_segment_pk<Mdl, T, MODE, PARITY, K, TD, PK, false, PAIR>(
                       L, a.t, a.t_shared, a.H[ls][kind], a.H_shared[ls][kind], a.F[ls][kind],
                       a.aux[kind], Ws, Wd, Xd, Zg, ns, tq, q0, a.seg_np[g], lane, rho, srho,
@@ -923,12 +932,12 @@ __device__ __forceinline__ void lane_block_pk(const BlockArgs<T>& a, const int64
   }
 }
 
-template <class Mdl, class T, int MODE, bool PARITY, int K, bool TD = false>
+template <class Mdl, class T, int MODE, bool PARITY, int K, bool TD = false, bool SDT = false>
 __global__ __launch_bounds__(64) void k_block_pk(const BlockArgs<T> a) {
   __shared__ T stg[DMT_PK_LDS ? (Mdl::D + Mdl::M) * kPathPacket * 65 : 1];  // X°, W° (DMT_PK_LDS)
   int64_t tile, blk;
   if (!map_block(a, tile, blk)) return;
-  lane_block_pk<Mdl, T, MODE, PARITY, K, TD>(a, tile, blk, threadIdx.x, stg);
+  lane_block_pk<Mdl, T, MODE, PARITY, K, TD, false, SDT>(a, tile, blk, threadIdx.x, stg);
 }
 
 // lane pairs on the packet layout (device-RNG draws): two waves per (recording tile, block
@@ -4753,6 +4762,8 @@ static hipError_t launch_block_t(int mapping, int mode, const void* args, int64_
               else dlaunch(k_block_pk<Mdl, T, MODE_PCN, false, kChunk, true>, grid, block, s, a);
             } else {
               if (par) dlaunch(k_block_pk<Mdl, T, MODE_PCN, true, kChunk>, grid, block, s, a);
+              else if (DMT_PK_SDT_TABLE && a.t_shared && a.sdt)  // shared grid: √dt table
+                dlaunch(k_block_pk<Mdl, T, MODE_PCN, false, kChunk, false, true>, grid, block, s, a);
               else dlaunch(k_block_pk<Mdl, T, MODE_PCN, false, kChunk>, grid, block, s, a);
             }
             break;
@@ -4766,6 +4777,8 @@ static hipError_t launch_block_t(int mapping, int mode, const void* args, int64_
               else dlaunch(k_block_pk<Mdl, T, MODE_FRESH, false, kChunk, true>, grid, block, s, a);
             } else {
               if (par) dlaunch(k_block_pk<Mdl, T, MODE_FRESH, true, kChunk>, grid, block, s, a);
+              else if (DMT_PK_SDT_TABLE && a.t_shared && a.sdt)
+                dlaunch(k_block_pk<Mdl, T, MODE_FRESH, false, kChunk, false, true>, grid, block, s, a);
               else dlaunch(k_block_pk<Mdl, T, MODE_FRESH, false, kChunk>, grid, block, s, a);
             }
             break;

@@ -177,6 +177,7 @@ struct dmt_ens {
   int nbuf = 2;  // path buffers per container (DESIGN.md §2 "path buffers"; DMT_PATH_BUFS)
   int pk = 0;    // path planes in lane packets of pk points (fp32 MAP_LANE; DMT_PATH_PACKETS)
   void* d_t = nullptr;
+  void* d_sdt = nullptr;  // shared grid: √dt per point in the working precision (lane kernels)
   bool have_t = false;
   void* d_H[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};  // [slot][kind]
   int H_shared[2] = {0, 0};                                     // per kind
@@ -493,6 +494,7 @@ void fill_common(dmt_ens* h, const Layout* L, BlockArgs<T>& a) {
     }
   }
   a.t = (const T*)h->d_t;
+  a.sdt = h->grid_shared ? (const T*)h->d_sdt : nullptr;
   a.t_shared = h->grid_shared;
   a.aux[0] = (const T*)h->d_aux[0];
   a.aux[1] = (const T*)h->d_aux[1];
@@ -1084,7 +1086,7 @@ dmt_status dmt_destroy(dmt_ens* h) {
     if (L) L->release();
   void* ps[] = {h->d_pt_off, h->d_st_off, h->d_tile_qoff, h->d_seg_rec, h->d_seg_q, h->d_seg_np,
                 h->d_sel[0], h->d_sel[1], h->d_sel[2], h->d_sel[3], h->d_X[0], h->d_X[1],
-                h->d_X[2], h->d_W[0], h->d_W[1], h->d_W[2], h->d_t, h->d_stage, h->d_Z, h->d_red, h->d_gather,
+                h->d_X[2], h->d_W[0], h->d_W[1], h->d_W[2], h->d_t, h->d_sdt, h->d_stage, h->d_Z, h->d_red, h->d_gather,
                 h->d_red_work, h->d_run, h->d_run_gather, h->d_part, h->d_red_lb, h->d_obsH,
                 h->d_obsF, h->d_obsc, h->d_obsv, h->d_fail, h->d_fchunk_off, h->d_segsel,
                 h->d_qbuf, h->d_tbuf};
@@ -1122,6 +1124,22 @@ dmt_status dmt_upload_grid(dmt_ens* h, const double* t) {
     DMT_TRY(ensure_stage(h, h->Q0));
     HIP_OK(hipMemcpyAsync(h->d_stage, t, h->Q0 * 8, hipMemcpyHostToDevice, h->stream));
     HIP_OK(launch_cast(h->key.precision, h->d_stage, h->d_t, h->Q0, h->stream));
+    // √dt per point for the lane kernels' draws: the value their step computes, sqrt(t[q+1] −
+    // t[q]) in the working precision (IEEE subtraction and correctly rounded square root on
+    // both sides), so a table read replaces a per-step square root bit for bit
+    if (!h->d_sdt) DMT_TRY(ens_alloc_bytes(h, &h->d_sdt, (h->Q0 + kPadPoints) * h->esz));
+    const int64_t ns = h->Q0 + kPadPoints;
+    if (h->key.precision == DMT_F64) {
+      std::vector<double> v(ns, 0.0);
+      for (int64_t q = 0; q + 1 < h->Q0; ++q) v[q] = std::sqrt(t[q + 1] - t[q]);
+      HIP_OK(hipMemcpyAsync(h->d_sdt, v.data(), ns * 8, hipMemcpyHostToDevice, h->stream));
+      HIP_OK(stream_wait(h));
+    } else {
+      std::vector<float> v(ns, 0.0f);
+      for (int64_t q = 0; q + 1 < h->Q0; ++q) v[q] = std::sqrt((float)t[q + 1] - (float)t[q]);
+      HIP_OK(hipMemcpyAsync(h->d_sdt, v.data(), ns * 4, hipMemcpyHostToDevice, h->stream));
+      HIP_OK(stream_wait(h));
+    }
   } else {
     if (!h->d_t) {
       DMT_TRY(ens_alloc_bytes(h, &h->d_t, plane_elems(h, 1) * h->esz));
