@@ -72,47 +72,38 @@ def _newest(pattern):
     return sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)), key=tag, reverse=True)
 
 
-def measured_traffic(config, kernel_substr):
-    """HBM bytes per iteration of the draw kernel from the newest committed PMC summary
-    (profiles/rNN_traffic_<config>.json, scripts/pmc_traffic.py: separate FETCH_SIZE and
-    WRITE_SIZE rocprofv3 passes, calibrated with scripts/calib_stream); None if absent."""
-    for path in _newest(f"r*_traffic_{config}.json"):
+_TREE = None
+
+
+def tree_digest():
+    """Digest of the library sources this bench runs from (scripts/provenance.py)."""
+    global _TREE
+    if _TREE is None:
+        sys.path.insert(0, os.path.join(ROOT, "scripts"))
+        import provenance
+        _TREE = provenance.csrc_digest(ROOT)
+    return _TREE
+
+
+def committed_summary(kind, config, kernel_substr):
+    """The newest committed profile summary of `kind` (traffic: scripts/pmc_traffic.py, kstats:
+    scripts/kstats_summary.py, issue: scripts/issue_summary.py) for this config and kernel,
+    used only if it measured THIS source tree (its csrc_sha16 equals tree_digest()).  Returns
+    (summary with "source" set, None), or (None, the newest matching file's name) when that
+    file measured another tree, or (None, None) when there is none."""
+    for path in _newest(f"r*_{kind}_{config}.json"):
         with open(path) as f:
             t = json.load(f)
-        if kernel_substr in t.get("kernel", ""):
-            per_unit = t.get("traffic_bytes_per_unit")
-            if per_unit is None:  # summaries of one unit per launch written before the field
-                per_unit = t["traffic_bytes_per_launch"] / max(1, t.get("units_per_launch", 1))
-            return per_unit, os.path.relpath(path, ROOT)
+        k = t.get("kernel", "")
+        if not k or kernel_substr not in k and k not in kernel_substr:
+            continue
+        rel = os.path.relpath(path, ROOT)
+        if t.get("csrc_sha16") != tree_digest():
+            return None, rel
+        t = dict(t)
+        t["source"] = rel
+        return t, None
     return None, None
-
-
-def rocprof_kernel(config, kernel_substr):
-    """The dominant kernel's average dispatch duration from the newest committed rocprofv3
-    kernel-trace summary of this config (profiles/rNN_kstats_<config>.json,
-    scripts/kstats_summary.py); None if absent."""
-    for path in _newest(f"r*_kstats_{config}.json"):
-        with open(path) as f:
-            t = json.load(f)
-        if kernel_substr in t.get("kernel", "") or t.get("kernel", "") in kernel_substr:
-            t = dict(t)
-            t["summary"] = os.path.relpath(path, ROOT)
-            return t
-    return None
-
-
-def issue_roofline(config, kernel_substr):
-    """VALU issue figures of the dominant kernel from the newest committed SQ-counter summary
-    (profiles/rNN_issue_<config>.json, scripts/sq_summary.py): VALU instructions per step and
-    per wave-iteration, VALU-active fraction of the wave cycles; None if absent."""
-    for path in _newest(f"r*_issue_{config}.json"):
-        with open(path) as f:
-            t = json.load(f)
-        if kernel_substr in t.get("kernel", ""):
-            t = dict(t)
-            t["source"] = os.path.relpath(path, ROOT)
-            return t
-    return None
 
 
 def host_cpu_info():
@@ -331,7 +322,7 @@ def main(argv=None):
     from diffusionmcmctools_amd import workloads as W
 
     w = build_workload(args.config, rank)
-    w.meta["hist_len"] = (args.warmup + args.steps * (2 + max(args.repeats, 0)) + EXTRA_ITERS +
+    w.meta["hist_len"] = (args.warmup + args.steps * (3 + max(args.repeats, 0)) + EXTRA_ITERS +
                           CPU_MAX_ITERS + 2 * args.calls_iters)
     mapping = {"auto": L.MAP_AUTO, "lane": L.MAP_LANE, "wave": L.MAP_WAVE}[args.mapping]
     ens = dmt.Ensemble(w.model.kind, w.d, w.m, w.n_points, precision=w.precision,
@@ -361,15 +352,11 @@ def main(argv=None):
             dist.barrier()
 
     if args.warmup:
-        # the warm-up takes the timed path too (HIP events around the launch), so that the
-        # timed call is not the first to record them
-        ens.set_timing(True, kernels=[L.K_DRAW])
         ens.mcmc_run(lay, 0, B, 1, args.warmup)
     barrier()
-    # HIP events around the dominant (draw) kernel over the timed region, on libdmt's stream
-    # (set_timing drops what the warm-up recorded)
-    ens.set_timing(True, kernels=[L.K_DRAW])
-    barrier()
+    # The timed region holds the K steps and nothing else: no timing events (they cost ≈ 10 µs
+    # of event completion per call); the kernel's own duration comes from the
+    # same K steps re-run with HIP events right after it (below) and from rocprofv3.
     t0 = time.perf_counter()
     if args.api == "calls":
         # the caller's loop of separate C calls (deferred draw fused with its accept, fetch_ll
@@ -382,12 +369,24 @@ def main(argv=None):
     barrier()
     el = time.perf_counter() - t0
     n_acc = float(res[:, 2].sum())
+    done = args.warmup + args.steps  # iterations run so far
+    # The dominant kernel's launch duration: HIP events recorded on libdmt's stream around the
+    # launches of the same K steps, run twice right after the timed region (same launch shape,
+    # same state; the first event-recording call is not the one averaged alone).
+    ens.set_timing(True, kernels=[L.K_DRAW])
+    for _ in range(2):
+        if args.api == "calls":
+            separate_calls(ens, lay, B, done + 1, args.steps, world > 1, python=False)
+        else:
+            ens.mcmc_run(lay, 0, B, done + 1, args.steps)
+        done += args.steps
+    ens.sync()
     k_ms, k_n = ens.get_timing(L.K_DRAW)  # k_n counts iterations (persistent) or launches
+    k_ms /= 2.0  # per K steps
     persist = w.model.kind == L.MODEL_OU and os.environ.get("DMT_MCMC_PERSIST", "1") != "0"
     a_ms = a_n = 0
-    done = args.warmup + args.steps  # iterations run so far
     if not persist:
-        # the accept+reduce kernel, timed on a few extra iterations after the timed region
+        # the accept+reduce kernel, timed on a few extra iterations
         ens.set_timing(True, kernels=[L.K_ACCEPT])
         ens.mcmc_run(lay, 0, B, done + 1, EXTRA_ITERS)
         a_ms, a_n = ens.get_timing(L.K_ACCEPT)
@@ -468,11 +467,12 @@ def main(argv=None):
     else:  # lane mapping: fp32 ensembles on lane packets (dmt_create; DMT_PATH_PACKETS=0: rows)
         kname = ("k_block_pk<" if w.precision == L.F32 and os.environ.get("DMT_PATH_PACKETS", "1") != "0"
                  else "k_block<")
-    traffic, traffic_src = measured_traffic(args.config, kname)  # HBM bytes per iteration
-    if traffic is not None:
-        traffic *= it_per_launch
-    issue = issue_roofline(args.config, kname)
-    rp = rocprof_kernel(args.config, kname)
+    # committed profile summaries of THIS source tree only (scripts/provenance.py)
+    tr, traffic_stale = committed_summary("traffic", args.config, kname)
+    traffic = tr["traffic_bytes_per_unit"] * it_per_launch if tr else None  # per launch
+    traffic_src = tr["source"] if tr else None
+    issue, issue_stale = committed_summary("issue", args.config, kname)
+    rp, rp_stale = committed_summary("kstats", args.config, kname)
     rp_us = None
     if rp is not None and rp.get("units_per_launch", 1) == it_per_launch:  # same launch shape
         rp_us = rp["avg_us"]
@@ -522,7 +522,14 @@ def main(argv=None):
                          "kernel_avg_us_rocprof": rp_us,
                          "frac_rocprof": (bytes_launch / (rp_us * 1e-6) / 1e9 / PEAK_HBM_GBS
                                           if rp_us else None),
-                         "rocprof_source": (rp or {}).get("summary"),
+                         "rocprof_source": (rp or {}).get("source"),
+                         "kernel_timing": ("HIP events on libdmt's stream around the same K "
+                                           "steps, re-run twice right after the timed region"),
+                         "source_tree": tree_digest(),
+                         # newest committed summaries that measured another tree (not quoted)
+                         "stale_summaries": {k: v for k, v in (("traffic", traffic_stale),
+                                                               ("issue", issue_stale),
+                                                               ("kstats", rp_stale)) if v},
                          "kernel_us_per_iteration": k_iter_s * 1e6,
                          "iterations_per_launch": it_per_launch,
                          "algorithmic_bytes_per_launch": bytes_launch,

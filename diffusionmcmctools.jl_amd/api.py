@@ -75,8 +75,8 @@ def _aux_callable(AuxLaw):
     the segment's observation), a fixed ``LinearAux`` or ``TimeDependentLinearAux`` (B̃(t), β̃(t))
     for every segment, or one such per segment (a list)."""
     from .models import LinearAux, TimeDependentLinearAux
-    if AuxLaw is None:
-        return None
+    if AuxLaw is None:  # the target's own auxiliary law at the observation (Model.aux_for)
+        return lambda mdl, r, k, ob: mdl.aux_for(ob)
     if isinstance(AuxLaw, (LinearAux, TimeDependentLinearAux)):
         return lambda mdl, r, k, ob: AuxLaw
     if isinstance(AuxLaw, (list, tuple)):
@@ -102,8 +102,18 @@ class SamplingEnsemble:
         return super().__new__(cls)
 
     @classmethod
-    def _from_reference_args(cls, aux_laws, recordings, tts, aux_laws_blocking=None,
-                             artificial_noise=1e-11, **kw):
+    def _from_reference_args(cls, aux_laws, recordings, tts, args=(), aux_laws_blocking=None,
+                             artificial_noise=1e-11, solver_choice_blocking=None, _pair=False,
+                             **kw):
+        """The reference's ``SamplingEnsemble(aux_laws, recordings, tts, args=tuple();
+        aux_laws_blocking=aux_laws, artificial_noise=1e-11, solver_choice_blocking=args)``
+        (src/sampling_ensemble.jl:20-40; ``_pair``: ``SamplingPair(…)`` of one recording,
+        src/sampling_pair.jl:40-50).  As there (``_vec_me``), a list ``aux_laws`` /
+        ``aux_laws_blocking`` / ``artificial_noise`` of the ensemble form holds one entry per
+        recording; each entry (and the pair form's argument) may itself be a list per segment
+        (``_aux_callable``).  ``args`` / ``solver_choice_blocking`` choose GuidedProposals' ODE
+        solver of the guiding term: the device's guiding term is the exact discrete filter
+        (DESIGN.md §7), so they are accepted and have no effect."""
         recordings = list(recordings)
         models = [getattr(rec, "P", None) for rec in recordings]
         if any(m is None for m in models):
@@ -111,12 +121,25 @@ class SamplingEnsemble:
                              "its target law P (models.build_recording(P, data, t0, x0))")
         if any(type(m) is not type(models[0]) for m in models):
             raise ValueError("all recordings of one ensemble must share the model family")
+        R = len(recordings)
+
+        def per_rec(v):  # _vec_me (src/sampling_ensemble.jl:44)
+            if not _pair and isinstance(v, (list, tuple)):
+                if len(v) != R:
+                    raise ValueError(f"a per-recording argument needs {R} entries, got {len(v)}")
+                return list(v)
+            return [v] * R
+        noise = per_rec(artificial_noise)
+        if any(x != noise[0] for x in noise):
+            raise ValueError("one artificial_noise per device ensemble (the device stores one)")
+        artificial_noise = float(noise[0])
         # per-recording target parameters enter the law records (recording r's P)
-        aux = _aux_callable(aux_laws)
-        auxb = _aux_callable(aux_laws_blocking) or aux
+        aux = [_aux_callable(a) for a in per_rec(aux_laws)]
+        auxb = ([_aux_callable(a) for a in per_rec(aux_laws_blocking)]
+                if aux_laws_blocking is not None else aux)
         se = cls.from_recordings(models[0], recordings, tts,
-                                 aux_laws=lambda mdl, r, k, ob: aux(models[r], r, k, ob),
-                                 aux_laws_blocking=lambda mdl, r, k, ob: auxb(models[r], r, k, ob),
+                                 aux_laws=lambda mdl, r, k, ob: aux[r](models[r], r, k, ob),
+                                 aux_laws_blocking=lambda mdl, r, k, ob: auxb[r](models[r], r, k, ob),
                                  artificial_noise=artificial_noise,
                                  record_models=models, **kw)
         se._ref_built = True
@@ -353,7 +376,8 @@ class SamplingPair:
         if args and isinstance(args[0], SamplingEnsemble):
             self._init_view(*args)
             return
-        se = SamplingEnsemble._from_reference_args(args[0], [args[1]], [args[2]], *args[3:], **kw)
+        se = SamplingEnsemble._from_reference_args(args[0], [args[1]], [args[2]], *args[3:],
+                                                   _pair=True, **kw)
         self._init_view(se, 0)
         se.recordings[0] = self
 

@@ -103,6 +103,7 @@ struct BlockArgs {
   const T* F[2][2];
   const double* law[2][2];
   const T* aux[2];  // [kind] per-point B̃(t_i), β̃(t_i) (dmt_upload_aux), nullptr: none
+  int64_t aux_n;    // elements of each aux table (the bounds the DMT_AUX_CHECK build checks)
   // layout
   const int64_t* blk_off;  // [R + 1]
   const int32_t* blk_rec;  // [nblocks] recording of each block

@@ -34,6 +34,16 @@
 
 namespace dmt {
 
+#ifndef DMT_SPLIT  // 1: one translation unit of the split build (Makefile; see DMT_DISPATCH)
+#define DMT_SPLIT 0
+#endif
+#ifndef DMT_TU_GROUP
+#define DMT_TU_GROUP -1
+#endif
+// the model-independent kernels and launchers: the monolithic build, or the split build's
+// common unit
+#define DMT_TU_COMMON (!DMT_SPLIT || DMT_TU_GROUP < 0)
+
 template <int K>
 struct Log2 { static constexpr int v = K == 1 ? 0 : 1 + Log2<(K > 1 ? K / 2 : 1)>::v; };
 template <>
@@ -1907,6 +1917,26 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+#ifndef DMT_AUX_CHECK
+#define DMT_AUX_CHECK 0
+#endif
+#if DMT_AUX_CHECK
+// Measurement build (DMT_AUX_CHECK=1): an aux-table read outside the table is not made; the
+// first kAuxDbg such reads are recorded (dmt_debug_aux_check).
+constexpr int kAuxDbg = 16;
+static __device__ unsigned long long g_aux_dbg[1 + 8 * kAuxDbg];
+__device__ __forceinline__ void aux_check_record(int64_t blk, int g, int kind, int64_t row,
+                                                 int64_t i, int c0, int cnt, int64_t nonnull) {
+  const unsigned long long n = atomicAdd(&g_aux_dbg[0], 1ull);
+  if (n < kAuxDbg) {
+    unsigned long long* r = &g_aux_dbg[1 + 8 * n];
+    r[0] = (unsigned long long)blk; r[1] = (unsigned long long)g; r[2] = (unsigned long long)kind;
+    r[3] = (unsigned long long)row; r[4] = (unsigned long long)i; r[5] = (unsigned long long)c0;
+    r[6] = (unsigned long long)cnt; r[7] = (unsigned long long)nonnull;
+  }
+}
+#endif
+
 // One block's draw / re-solve by one wave; every lane returns the block's ll and success.
 // TD: time-dependent auxiliary laws (an aux table is present) — the recursion is the target
 // law's and does not change; phase 3 takes step i's B̃(t_i), β̃(t_i) (and a − ã(t_i)) in G where
@@ -2130,9 +2160,18 @@ __device__ __forceinline__ void scan_block(const BlockArgs<T>& a, const int64_t 
             const int i = c0 + (v ? s : cnt - 1);
             T Bq[D * D], bq[D], dq[HP];
             bool trq;
+#if DMT_AUX_CHECK
+            const int64_t ix = (row + i) * CA;
+            if (a.aux[kind] == nullptr || ix < 0 || ix + CA > a.aux_n) {
+              aux_check_record(blk, g, kind, row, i, c0, cnt, (int64_t)(a.aux[kind] != nullptr));
+              G = g_at<Mdl, T>(LA, Hi, Fi, xk[k], rr, bb);
+            } else
+#endif
+            {
             aux_step<Mdl, T>(LA, a.aux[kind] + (row + i) * CA, 1, Bq, bq, dq, trq,
                              [](const T* p) { return *p; });
             G = g_at_aux<Mdl, T>(LA, Hi, Fi, xk[k], rr, bb, Bq, bq, dq, trq);
+            }
           } else {
             G = g_at<Mdl, T>(LA, Hi, Fi, xk[k], rr, bb);
           }
@@ -2389,7 +2428,7 @@ __device__ __forceinline__ void persistent_tree_tail(const double* __restrict__ 
 // then — uniformly, exactly as k_accept — the MH decision, selector flips (bit masks in
 // SGPRs), histories and the ll swap.  Per-iteration (ll, ll°, accepted) go to
 // part[n_iter][3][nb]; persistent_tree_tail forms every iteration's fetch_ll from them.
-template <class Mdl, class T>
+template <class Mdl, class T, bool TD = false>
 __device__ __forceinline__ void mcmc_scan_block(const BlockArgs<T>& a, const AcceptArgs& c,
                                                 const int64_t iter0, const int64_t n_iter,
                                                 double* __restrict__ part, const int64_t blk,
@@ -2408,7 +2447,7 @@ __device__ __forceinline__ void mcmc_scan_block(const BlockArgs<T>& a, const Acc
     const double E = exp1_draw(c.seed, (uint32_t)g0 + c.seg_base, (uint32_t)(it + c.key_delta), c.salt);
     T lp;
     bool ok;
-    scan_block<Mdl, T, MODE_PCN>(a, blk, (uint32_t)(it + c.key_delta), sel, L, lp, ok);
+    scan_block<Mdl, T, MODE_PCN, SelMask, TD>(a, blk, (uint32_t)(it + c.key_delta), sel, L, lp, ok);
     llp = ok ? (double)lp : -INFINITY;
     const bool acc = E > -(llp - ll);
     if (acc) {
@@ -2446,7 +2485,7 @@ __device__ __forceinline__ void mcmc_scan_block(const BlockArgs<T>& a, const Acc
   }
 }
 
-template <class Mdl, class T>
+template <class Mdl, class T, bool TD = false>
 __global__ __launch_bounds__((64 * ScanCfg<Mdl::D, T>::WPB), 1) void k_mcmc_scan(
     const BlockArgs<T> a, const AcceptArgs c, const int64_t iter0, const int64_t n_iter,
     double* __restrict__ part, double* __restrict__ nodes, unsigned* __restrict__ counter,
@@ -2455,7 +2494,7 @@ __global__ __launch_bounds__((64 * ScanCfg<Mdl::D, T>::WPB), 1) void k_mcmc_scan
   __shared__ ScanLds<Mdl::D, T> lds[Cfg::WPB];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t blk = a.b0 + (int64_t)blockIdx.x * Cfg::WPB + w;
-  if (blk < a.b1) mcmc_scan_block<Mdl, T>(a, c, iter0, n_iter, part, blk, lds[w]);
+  if (blk < a.b1) mcmc_scan_block<Mdl, T, TD>(a, c, iter0, n_iter, part, blk, lds[w]);
   persistent_tree_tail<Cfg::WPB>(part, nodes, a.b1 - a.b0, n_iter, counter, out3);
 }
 
@@ -3614,6 +3653,7 @@ __global__ __launch_bounds__(64) void k_pathll_wave(const BlockArgs<T> a) {
 }
 
 // ---------------------------------------------------------------- accept / reject
+#if DMT_TU_COMMON
 __global__ __launch_bounds__(256) void k_accept(const AcceptArgs a) {
   const int64_t blk = a.b0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (blk >= a.b1) return;
@@ -3639,11 +3679,13 @@ __global__ __launch_bounds__(256) void k_accept(const AcceptArgs a) {
   }
   if (a.acc_out) a.acc_out[blk - a.b0] = acc ? 1 : 0;
 }
+#endif  // DMT_TU_COMMON
 
 // accept_reject + the first level of the fetch_ll tree in one pass: each thread decides its
 // block (as k_accept), then the 1024-block group reduces (ll, ll°, accepted) exactly as
 // k_tree_level<true> does on the post-decision values.  With one group the final
 // canonicalised result is written directly.
+#if DMT_TU_COMMON
 __global__ __launch_bounds__(1024) void k_accept_reduce(const AcceptArgs a, double* __restrict__ out,
                                                         int64_t nout, double* __restrict__ out3) {
   __shared__ double w0[16], w1[16], w2[16];
@@ -3702,12 +3744,14 @@ __global__ __launch_bounds__(1024) void k_accept_reduce(const AcceptArgs a, doub
     }
   }
 }
+#endif  // DMT_TU_COMMON
 
 // Single-launch form for up to 256 groups of 256 blocks: every workgroup decides its 256
 // blocks and reduces them (4 wave trees + one 4-leaf tree = the aligned 256-leaf subtree of
 // the fetch_ll tree); the last workgroup to finish (device-scope counter) reduces the group
 // partials in group order with the same tree and writes the canonicalised result.
 constexpr int kAccGroup = 256;
+#if DMT_TU_COMMON
 __global__ __launch_bounds__(kAccGroup) void k_accept_reduce_lb(const AcceptArgs a,
                                                                 double* __restrict__ part,
                                                                 unsigned* __restrict__ counter,
@@ -3776,6 +3820,7 @@ __global__ __launch_bounds__(kAccGroup) void k_accept_reduce_lb(const AcceptArgs
     *counter = 0u;  // ready for the next launch (stream-ordered)
   }
 }
+#endif  // DMT_TU_COMMON
 
 // ---------------------------------------------------------------- guiding term on the device
 // recompute_guiding_term!(b) for linear auxiliary laws (src/block.jl:102-110), in the
@@ -3789,6 +3834,7 @@ __global__ __launch_bounds__(kAccGroup) void k_accept_reduce_lb(const AcceptArgs
 //                   end's guiding term, lane 0's result is the next chunk's end
 // The last segment of a non-terminal block uses its PPb law with the artificial end
 // observation frozen by set_obs!.
+#if DMT_TU_COMMON
 __global__ void k_filter_mark(const FilterArgs a) {
   const int64_t blk = a.b0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (blk >= a.b1) return;
@@ -3797,6 +3843,7 @@ __global__ void k_filter_mark(const FilterArgs a) {
   const bool term = a.term[blk] != 0;
   for (int g = g0; g <= g1; ++g) a.segsel[g] = on ? ((!term && g == g1) ? 2 : 1) : 0;
 }
+#endif  // DMT_TU_COMMON
 
 template <int D>
 __device__ __forceinline__ void filt_law(const FilterArgs& a, int g, int kind, flt::Mat<D>& B,
@@ -4391,6 +4438,7 @@ __device__ __forceinline__ void derive_law(int model, double* r) {
 
 // one thread per block, or (wg_per_block, for few blocks with many segments) one workgroup per
 // block with its threads over the block's (segment, law kind) records
+#if DMT_TU_COMMON
 __global__ __launch_bounds__(64) void k_set_prop_law(const ParamArgs a, int wg_per_block) {
   const int64_t blk = wg_per_block ? a.b0 + blockIdx.x : a.b0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (blk >= a.b1) return;
@@ -4443,6 +4491,7 @@ __global__ __launch_bounds__(64) void k_set_prop_law(const ParamArgs a, int wg_p
   a.crit[blk] = changed ? 1 : 0;
   if (changed) atomicAdd(a.ncrit, 1u);
 }
+#endif  // DMT_TU_COMMON
 
 // set_obs!(bb) (src/biblock.jl:273-280): the artificial observation of a non-terminal block's
 // P_last is the end point of its accepted path; the P_last laws of b and b° that are
@@ -4485,6 +4534,7 @@ struct FlipArgs {
 };
 // selector flips of blocks [b0, b1): one thread per block, or (wg_per_block, for few blocks
 // with many segments) one workgroup per block striding over its segments
+#if DMT_TU_COMMON
 __global__ void k_flip(const FlipArgs f, const int32_t* gfirst, const int32_t* glast,
                        const uint8_t* term, int64_t b0, int64_t b1, int wg_per_block) {
   const int64_t blk = wg_per_block ? b0 + blockIdx.x : b0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -4497,7 +4547,9 @@ __global__ void k_flip(const FlipArgs f, const int32_t* gfirst, const int32_t* g
       if (f.sel[i] && !(f.only_nonterm[i] && tm))
         f.sel[i][g] = i < 2 ? sel_swap(f.sel[i][g]) : (uint8_t)(f.sel[i][g] ^ 1);  // paths: swap u/u°
 }
+#endif  // DMT_TU_COMMON
 
+#if DMT_TU_COMMON
 __global__ void k_swap_ll(double* ll, double* llp, int64_t b0, int64_t b1) {
   const int64_t blk = b0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (blk >= b1) return;
@@ -4505,7 +4557,9 @@ __global__ void k_swap_ll(double* ll, double* llp, int64_t b0, int64_t b1) {
   ll[blk] = llp[blk];
   llp[blk] = v;
 }
+#endif  // DMT_TU_COMMON
 
+#if DMT_TU_COMMON
 __global__ void k_save_ll(const double* ll, const double* llp, double* llh, double* llph,
                           int64_t nblocks, int64_t it0, int64_t b0, int64_t b1) {
   const int64_t blk = b0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -4513,6 +4567,7 @@ __global__ void k_save_ll(const double* ll, const double* llp, double* llh, doub
   llh[it0 * nblocks + blk] = ll[blk];
   llph[it0 * nblocks + blk] = llp[blk];
 }
+#endif  // DMT_TU_COMMON
 
 __device__ __forceinline__ int64_t find_seg(const int64_t* pt_off, int64_t G, int64_t p) {
   int64_t lo = 0, hi = G;  // largest g with pt_off[g] <= p
@@ -4649,12 +4704,15 @@ __global__ __launch_bounds__(1024) void k_tree_level(const double* __restrict__ 
   }
 }
 
+#if DMT_TU_COMMON
 __global__ void k_tree_final(const double* __restrict__ in, int64_t nout, double* __restrict__ out3) {
   out3[0] = in[0] + 0.0;
   out3[1] = in[nout] + 0.0;
   out3[2] = in[2 * nout];
 }
+#endif  // DMT_TU_COMMON
 
+#if DMT_TU_COMMON
 __global__ void k_debug_philox(uint64_t seed, const uint32_t* ctr, int64_t n, uint32_t* out,
                                double* normals) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -4667,6 +4725,7 @@ __global__ void k_debug_philox(uint64_t seed, const uint32_t* ctr, int64_t n, ui
   normals[2 * i] = z0;
   normals[2 * i + 1] = z1;
 }
+#endif  // DMT_TU_COMMON
 
 // ---------------------------------------------------------------- launchers
 static inline unsigned nblk(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
@@ -4674,7 +4733,9 @@ static inline unsigned nblk(int64_t n, int bs) { return (unsigned)((n + bs - 1) 
 // segments of a block in parallel) instead of one thread per block
 constexpr int64_t kFewBlocks = 2048;
 
+#if DMT_TU_COMMON
 thread_local DispatchEvents g_dispatch_events;
+#endif
 
 // Launch; when the runtime has armed dispatch events (timed launch), they are attached to
 // the kernel's own dispatch packet (hipExtLaunchKernel), so the measured time is the
@@ -4962,37 +5023,89 @@ static hipError_t launch_pathll_t(int mapping, const void* args, int64_t nwaves,
   return hipGetLastError();
 }
 
+// Model dispatch.  One monolithic translation unit by default; the Makefile's split build
+// compiles this file seven times in parallel (DMT_TU_GROUP = 0..5: one (precision, model)
+// group's kernels and entry points, named <entry>_g<group>; DMT_TU_GROUP = -1 with
+// DMT_SPLIT: the model-independent kernels and launchers plus the dispatchers below), so a
+// change to one model's kernels rebuilds in a fraction of the time.  Groups: 3·(precision) +
+// model — 0 f64 OU, 1 f64 FHN, 2 f64 Lorenz, 3 f32 OU, 4 f32 FHN, 5 f32 Lorenz.
+#define DMT_CAT_(a, b) a##b
+#define DMT_CAT(a, b) DMT_CAT_(a, b)
+#if DMT_TU_GROUP >= 0
+#define DMT_ENTRY(name) DMT_CAT(name, DMT_CAT(_g, DMT_TU_GROUP))
+#else
+#define DMT_ENTRY(name) name
+#endif
+#define DMT_GROUP_ON(g) (!DMT_SPLIT || DMT_TU_GROUP == (g))
+#if DMT_GROUP_ON(0)
+#define DMT_CASE_0(KEY, CALL)                                                          \
+  if ((KEY).precision == DMT_F64 && (KEY).model == DMT_MODEL_OU) {                     \
+    using T = double;                                                                  \
+    if ((KEY).d == 1 && (KEY).m == 1) { using Mdl = OU<T, 1, 1>; return CALL; }        \
+    if ((KEY).d == 2 && (KEY).m == 2) { using Mdl = OU<T, 2, 2>; return CALL; }        \
+    if ((KEY).d == 2 && (KEY).m == 1) { using Mdl = OU<T, 2, 1>; return CALL; }        \
+    if ((KEY).d == 3 && (KEY).m == 3) { using Mdl = OU<T, 3, 3>; return CALL; }        \
+  }
+#else
+#define DMT_CASE_0(KEY, CALL)
+#endif
+#if DMT_GROUP_ON(1)
+#define DMT_CASE_1(KEY, CALL)                                                          \
+  if ((KEY).precision == DMT_F64 && (KEY).model == DMT_MODEL_FHN) {                    \
+    using T = double; using Mdl = FHN<T>; return CALL;                                 \
+  }
+#else
+#define DMT_CASE_1(KEY, CALL)
+#endif
+#if DMT_GROUP_ON(2)
+#define DMT_CASE_2(KEY, CALL)                                                          \
+  if ((KEY).precision == DMT_F64 && (KEY).model == DMT_MODEL_LORENZ) {                 \
+    using T = double; using Mdl = Lorenz<T>; return CALL;                              \
+  }
+#else
+#define DMT_CASE_2(KEY, CALL)
+#endif
+#if DMT_GROUP_ON(3)
+#define DMT_CASE_3(KEY, CALL)                                                          \
+  if ((KEY).precision != DMT_F64 && (KEY).model == DMT_MODEL_OU) {                     \
+    using T = float;                                                                   \
+    if ((KEY).d == 1 && (KEY).m == 1) { using Mdl = OU<T, 1, 1>; return CALL; }        \
+    if ((KEY).d == 2 && (KEY).m == 2) { using Mdl = OU<T, 2, 2>; return CALL; }        \
+    if ((KEY).d == 2 && (KEY).m == 1) { using Mdl = OU<T, 2, 1>; return CALL; }        \
+    if ((KEY).d == 3 && (KEY).m == 3) { using Mdl = OU<T, 3, 3>; return CALL; }        \
+  }
+#else
+#define DMT_CASE_3(KEY, CALL)
+#endif
+#if DMT_GROUP_ON(4)
+#define DMT_CASE_4(KEY, CALL)                                                          \
+  if ((KEY).precision != DMT_F64 && (KEY).model == DMT_MODEL_FHN) {                    \
+    using T = float; using Mdl = FHN<T>; return CALL;                                  \
+  }
+#else
+#define DMT_CASE_4(KEY, CALL)
+#endif
+#if DMT_GROUP_ON(5)
+#define DMT_CASE_5(KEY, CALL)                                                          \
+  if ((KEY).precision != DMT_F64 && (KEY).model == DMT_MODEL_LORENZ) {                 \
+    using T = float; using Mdl = Lorenz<T>; return CALL;                               \
+  }
+#else
+#define DMT_CASE_5(KEY, CALL)
+#endif
 #define DMT_DISPATCH(KEY, CALL)                                                        \
   do {                                                                                 \
-    if ((KEY).precision == DMT_F64) {                                                  \
-      using T = double;                                                                \
-      if ((KEY).model == DMT_MODEL_OU) {                                               \
-        if ((KEY).d == 1 && (KEY).m == 1) { using Mdl = OU<T, 1, 1>; return CALL; }    \
-        if ((KEY).d == 2 && (KEY).m == 2) { using Mdl = OU<T, 2, 2>; return CALL; }    \
-        if ((KEY).d == 2 && (KEY).m == 1) { using Mdl = OU<T, 2, 1>; return CALL; }    \
-        if ((KEY).d == 3 && (KEY).m == 3) { using Mdl = OU<T, 3, 3>; return CALL; }    \
-      } else if ((KEY).model == DMT_MODEL_FHN) {                                       \
-        using Mdl = FHN<T>; return CALL;                                               \
-      } else if ((KEY).model == DMT_MODEL_LORENZ) {                                    \
-        using Mdl = Lorenz<T>; return CALL;                                            \
-      }                                                                                \
-    } else {                                                                           \
-      using T = float;                                                                 \
-      if ((KEY).model == DMT_MODEL_OU) {                                               \
-        if ((KEY).d == 1 && (KEY).m == 1) { using Mdl = OU<T, 1, 1>; return CALL; }    \
-        if ((KEY).d == 2 && (KEY).m == 2) { using Mdl = OU<T, 2, 2>; return CALL; }    \
-        if ((KEY).d == 2 && (KEY).m == 1) { using Mdl = OU<T, 2, 1>; return CALL; }    \
-        if ((KEY).d == 3 && (KEY).m == 3) { using Mdl = OU<T, 3, 3>; return CALL; }    \
-      } else if ((KEY).model == DMT_MODEL_FHN) {                                       \
-        using Mdl = FHN<T>; return CALL;                                               \
-      } else if ((KEY).model == DMT_MODEL_LORENZ) {                                    \
-        using Mdl = Lorenz<T>; return CALL;                                            \
-      }                                                                                \
-    }                                                                                  \
+    DMT_CASE_0(KEY, CALL)                                                              \
+    DMT_CASE_1(KEY, CALL)                                                              \
+    DMT_CASE_2(KEY, CALL)                                                              \
+    DMT_CASE_3(KEY, CALL)                                                              \
+    DMT_CASE_4(KEY, CALL)                                                              \
+    DMT_CASE_5(KEY, CALL)                                                              \
     return hipErrorInvalidValue;                                                       \
   } while (0)
 
-hipError_t launch_block_kernel(const ModelKey& k, int mapping, int mode, const void* args,
+#if !DMT_SPLIT || DMT_TU_GROUP >= 0
+hipError_t DMT_ENTRY(launch_block_kernel)(const ModelKey& k, int mapping, int mode, const void* args,
                                int64_t nwaves, hipStream_t s) {
   DMT_DISPATCH(k, (launch_block_t<Mdl, T>(mapping, mode, args, nwaves, s)));
 }
@@ -5006,8 +5119,10 @@ static hipError_t launch_mcmc_t(const void* args, const AcceptArgs& c, int64_t i
     if (nwaves <= 0) return hipSuccess;
     // part[n][3][nwaves], then the tree nodes [n][3][ceil(nwaves / WPB)] (dmt_mcmc_run sizes it)
     double* nodes = part + 3 * n * nwaves;
-    // time-dependent auxiliary laws run the per-iteration kernels (dmt_mcmc_run's choice)
-    if (a.aux[0] || a.aux[1]) return hipErrorInvalidValue;
+    // time-dependent auxiliary laws: k_mcmc_scan's TD instantiation only (the register-resident
+    // kernels take the law's own B̃, β̃; dmt_mcmc_run does not pick them while a table is present)
+    const bool td = a.aux[0] || a.aux[1];
+    if (td && resident) return hipErrorInvalidValue;
     if constexpr (Mdl::D <= 2) {
       if (resident >= 2) {  // producer / consumer waves (k_mcmc_resident_pc), resident - 1 producers
         const SvcArgs none{};
@@ -5029,8 +5144,12 @@ static hipError_t launch_mcmc_t(const void* args, const AcceptArgs& c, int64_t i
       }
     }
     constexpr int WPB = ScanCfg<Mdl::D, T>::WPB;
-    dlaunch(k_mcmc_scan<Mdl, T>, dim3((unsigned)((nwaves + WPB - 1) / WPB)), dim3(64 * WPB), s, a,
-            c, iter0, n, part, nodes, counter, out3);
+    if (td)
+      dlaunch(k_mcmc_scan<Mdl, T, true>, dim3((unsigned)((nwaves + WPB - 1) / WPB)), dim3(64 * WPB),
+              s, a, c, iter0, n, part, nodes, counter, out3);
+    else
+      dlaunch(k_mcmc_scan<Mdl, T>, dim3((unsigned)((nwaves + WPB - 1) / WPB)), dim3(64 * WPB), s, a,
+              c, iter0, n, part, nodes, counter, out3);
     return hipGetLastError();
   } else {
     return hipErrorInvalidValue;
@@ -5076,39 +5195,104 @@ static hipError_t launch_svc_t(const void* args, const AcceptArgs& c, int64_t it
   }
 }
 
-hipError_t launch_mcmc_service(const ModelKey& k, const void* args, const AcceptArgs& c,
+hipError_t DMT_ENTRY(launch_mcmc_service)(const ModelKey& k, const void* args, const AcceptArgs& c,
                                int64_t iter0, int64_t capacity, double* part, int64_t nwaves,
                                int producers, int n_cu, const SvcArgs& sv, hipStream_t s) {
   DMT_DISPATCH(k, (launch_svc_t<Mdl, T>(args, c, iter0, capacity, part, nwaves, producers, n_cu,
                                         sv, s)));
 }
 
-static hipError_t svc_fits_err(const ModelKey& k, int64_t nwaves, int producers, int n_cu) {
+static hipError_t DMT_ENTRY(svc_fits_err)(const ModelKey& k, int64_t nwaves, int producers, int n_cu) {
   DMT_DISPATCH(k, (svc_fits_t<Mdl, T>(nwaves, producers, n_cu) ? hipSuccess
                                                                  : hipErrorCooperativeLaunchTooLarge));
 }
 
-bool mcmc_service_fits(const ModelKey& k, int64_t nwaves, int producers, int n_cu) {
-  return svc_fits_err(k, nwaves, producers, n_cu) == hipSuccess;
+bool DMT_ENTRY(mcmc_service_fits)(const ModelKey& k, int64_t nwaves, int producers, int n_cu) {
+  return DMT_ENTRY(svc_fits_err)(k, nwaves, producers, n_cu) == hipSuccess;
 }
 
-hipError_t launch_mcmc_persistent(const ModelKey& k, const void* args, const AcceptArgs& c,
+hipError_t DMT_ENTRY(launch_mcmc_persistent)(const ModelKey& k, const void* args, const AcceptArgs& c,
                                   int64_t iter0, int64_t n_iter, double* part, int64_t nwaves,
                                   int resident, double* out3, unsigned* counter, hipStream_t s) {
   DMT_DISPATCH(k, (launch_mcmc_t<Mdl, T>(args, c, iter0, n_iter, part, nwaves, resident, out3,
                                          counter, s)));
 }
 
-hipError_t launch_invsolve_kernel(const ModelKey& k, int mapping, const void* args,
+hipError_t DMT_ENTRY(launch_invsolve_kernel)(const ModelKey& k, int mapping, const void* args,
                                   int64_t nwaves, hipStream_t s) {
   DMT_DISPATCH(k, (launch_invsolve_t<Mdl, T>(mapping, args, nwaves, s)));
 }
 
-hipError_t launch_pathll_kernel(const ModelKey& k, int mapping, const void* args, int64_t nwaves,
+hipError_t DMT_ENTRY(launch_pathll_kernel)(const ModelKey& k, int mapping, const void* args, int64_t nwaves,
                                 hipStream_t s) {
   DMT_DISPATCH(k, (launch_pathll_t<Mdl, T>(mapping, args, nwaves, s)));
 }
 
+#endif  // !DMT_SPLIT || DMT_TU_GROUP >= 0
+
+#if DMT_SPLIT && DMT_TU_GROUP < 0
+// the split build's dispatchers: the (precision, model) group's translation unit
+#define DMT_DECL_GROUP(G)                                                                        \
+  hipError_t launch_block_kernel_g##G(const ModelKey&, int, int, const void*, int64_t, hipStream_t); \
+  hipError_t launch_mcmc_service_g##G(const ModelKey&, const void*, const AcceptArgs&, int64_t,    \
+                                      int64_t, double*, int64_t, int, int, const SvcArgs&,         \
+                                      hipStream_t);                                                \
+  bool mcmc_service_fits_g##G(const ModelKey&, int64_t, int, int);                                 \
+  hipError_t launch_mcmc_persistent_g##G(const ModelKey&, const void*, const AcceptArgs&, int64_t, \
+                                         int64_t, double*, int64_t, int, double*, unsigned*,       \
+                                         hipStream_t);                                             \
+  hipError_t launch_invsolve_kernel_g##G(const ModelKey&, int, const void*, int64_t, hipStream_t); \
+  hipError_t launch_pathll_kernel_g##G(const ModelKey&, int, const void*, int64_t, hipStream_t);
+DMT_DECL_GROUP(0)
+DMT_DECL_GROUP(1)
+DMT_DECL_GROUP(2)
+DMT_DECL_GROUP(3)
+DMT_DECL_GROUP(4)
+DMT_DECL_GROUP(5)
+static int model_group(const ModelKey& k) {
+  if (k.model < DMT_MODEL_OU || k.model > DMT_MODEL_LORENZ) return -1;
+  return (k.precision == DMT_F64 ? 0 : 3) + k.model;
+}
+#define DMT_FORWARD(RET, FN, ...)                      \
+  switch (model_group(k)) {                            \
+    case 0: return FN##_g0(__VA_ARGS__);               \
+    case 1: return FN##_g1(__VA_ARGS__);               \
+    case 2: return FN##_g2(__VA_ARGS__);               \
+    case 3: return FN##_g3(__VA_ARGS__);               \
+    case 4: return FN##_g4(__VA_ARGS__);               \
+    case 5: return FN##_g5(__VA_ARGS__);               \
+    default: return RET;                               \
+  }
+hipError_t launch_block_kernel(const ModelKey& k, int mapping, int mode, const void* args,
+                               int64_t nwaves, hipStream_t s) {
+  DMT_FORWARD(hipErrorInvalidValue, launch_block_kernel, k, mapping, mode, args, nwaves, s);
+}
+hipError_t launch_mcmc_service(const ModelKey& k, const void* args, const AcceptArgs& c,
+                               int64_t iter0, int64_t capacity, double* part, int64_t nwaves,
+                               int producers, int n_cu, const SvcArgs& sv, hipStream_t s) {
+  DMT_FORWARD(hipErrorInvalidValue, launch_mcmc_service, k, args, c, iter0, capacity, part, nwaves,
+              producers, n_cu, sv, s);
+}
+bool mcmc_service_fits(const ModelKey& k, int64_t nwaves, int producers, int n_cu) {
+  DMT_FORWARD(false, mcmc_service_fits, k, nwaves, producers, n_cu);
+}
+hipError_t launch_mcmc_persistent(const ModelKey& k, const void* args, const AcceptArgs& c,
+                                  int64_t iter0, int64_t n_iter, double* part, int64_t nwaves,
+                                  int resident, double* out3, unsigned* counter, hipStream_t s) {
+  DMT_FORWARD(hipErrorInvalidValue, launch_mcmc_persistent, k, args, c, iter0, n_iter, part, nwaves,
+              resident, out3, counter, s);
+}
+hipError_t launch_invsolve_kernel(const ModelKey& k, int mapping, const void* args,
+                                  int64_t nwaves, hipStream_t s) {
+  DMT_FORWARD(hipErrorInvalidValue, launch_invsolve_kernel, k, mapping, args, nwaves, s);
+}
+hipError_t launch_pathll_kernel(const ModelKey& k, int mapping, const void* args, int64_t nwaves,
+                                hipStream_t s) {
+  DMT_FORWARD(hipErrorInvalidValue, launch_pathll_kernel, k, mapping, args, nwaves, s);
+}
+#endif  // DMT_SPLIT && DMT_TU_GROUP < 0
+
+#if DMT_TU_COMMON
 hipError_t launch_backward_filter(int precision, const FilterArgs& a, hipStream_t s) {
   const int64_t n = a.b1 - a.b0;
   if (n <= 0) return hipSuccess;
@@ -5351,4 +5535,18 @@ hipError_t launch_debug_philox(uint64_t seed, const uint32_t* ctr, int64_t n, ui
   return hipGetLastError();
 }
 
+#endif  // DMT_TU_COMMON
 }  // namespace dmt
+
+#if DMT_AUX_CHECK && !DMT_SPLIT
+extern "C" int dmt_debug_aux_check(unsigned long long* out, int n) {
+  // out[0] = count of out-of-table aux reads, then up to kAuxDbg records of 8 words
+  // (block, segment, kind, row, step, chunk start, chunk count, table present); resets them
+  if (n < 1 + 8 * dmt::kAuxDbg) return -1;
+  if (hipDeviceSynchronize() != hipSuccess) return -2;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(dmt::g_aux_dbg), sizeof(dmt::g_aux_dbg)) != hipSuccess) return -3;
+  static const unsigned long long zero[1 + 8 * dmt::kAuxDbg] = {};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(dmt::g_aux_dbg), zero, sizeof(zero)) != hipSuccess) return -4;
+  return 0;
+}
+#endif

@@ -498,6 +498,7 @@ void fill_common(dmt_ens* h, const Layout* L, BlockArgs<T>& a) {
   a.t_shared = h->grid_shared;
   a.aux[0] = (const T*)h->d_aux[0];
   a.aux[1] = (const T*)h->d_aux[1];
+  a.aux_n = plane_elems(h, (int)(h->d * h->d + h->d + h->hp));
   a.blk_off = L->d_blk_off;
   a.blk_rec = L->d_blk_rec;
   a.binfo = L->d_binfo;
@@ -1666,6 +1667,9 @@ static dmt_status mcmc_run_impl(dmt_ens* h, int32_t layout, int64_t b0, int64_t 
   return mcmc_run_collect(h, n_iter, out, multi);
 }
 
+#ifndef DMT_MCMC_SCAN_TD  // 0: an ensemble with an aux table runs dmt_mcmc_run per iteration
+#define DMT_MCMC_SCAN_TD 0
+#endif
 // Queue n_iter MCMC iterations (iteration it keyed by it + key_delta, salt) on the stream; the
 // per-iteration (fetch_ll, fetch_ll°, accepted count) go to pinned h_run (one rank) or d_run
 // (multi: for the all-gather, which is queued too).  No host synchronisation.
@@ -1701,12 +1705,13 @@ static dmt_status mcmc_run_launch(dmt_ens* h, Layout* L, int64_t b0, int64_t b1,
   // kernel eligibility of the range: from the layout's flags when they decide it (no host
   // loop over the blocks per call), else block by block
   const bool lay_res = L->single_seg && L->max_steps <= kResidentMaxSteps;
-  // (an ensemble with a time-dependent auxiliary table runs the per-iteration kernels: the
-  // persistent ones take the law's own B̃, β̃)
-  bool persist = h->persist && h->key.model == DMT_MODEL_OU && !has_aux_table(h);
+  // (an ensemble with a time-dependent auxiliary table runs k_mcmc_scan's TD instantiation;
+  // the register-resident kernels take the law's own B̃, β̃ and are not eligible)
+  bool persist = h->persist && h->key.model == DMT_MODEL_OU &&
+                 (DMT_MCMC_SCAN_TD || !has_aux_table(h));
   for (int64_t b = b0; b < b1 && persist && !L->single_seg; ++b)
     persist = L->glast[b] - L->gfirst[b] + 1 <= kPersistMaxSegments;
-  bool resident = persist && h->key.d <= 2 && h->resident;
+  bool resident = persist && h->key.d <= 2 && h->resident && !has_aux_table(h);
   for (int64_t b = b0; b < b1 && resident && !lay_res; ++b)
     resident = L->glast[b] == L->gfirst[b] && h->seg_np[L->gfirst[b]] - 1 <= kResidentMaxSteps;
   if (persist) {

@@ -38,7 +38,7 @@ import DiffusionMCMCTools: draw_proposal_path!, accept_reject_proposal_path!, lo
 export DeviceSamplingEnsemble, DeviceSamplingPair, DeviceSamplingUnit, DeviceBlockEnsemble,
     DeviceBlockCollection, DeviceBiBlock, DeviceBlock, use_device!, mcmc_step!, mcmc_run!,
     download_XX, download_WW, upload_obs!, snapshot_every!, law_record, guiding_linear, sync,
-    upload_aux!
+    upload_aux!, upload_aux_a!, device_model, device_aux
 
 const libdmt = get(ENV, "DMT_LIB", joinpath(@__DIR__, "..", "libdmt.so"))
 
@@ -291,6 +291,18 @@ function upload_aux!(se::DeviceSamplingEnsemble, kind, aux)
 end
 
 """
+    upload_aux_a!(se, kind, aux, ncols)
+
+dmt_upload_aux_a: `aux` is ncols × P with ncols = d² + d (as `upload_aux!`) or d² + d + d(d+1)/2
+— B̃(t_i), β̃(t_i) and ã(t_i) packed — for segments whose record has DMT_LAW_AUXTD = 2 (ã(t) from
+the table) or 1 (the record's ã).
+"""
+function upload_aux_a!(se::DeviceSamplingEnsemble, kind, aux, ncols::Integer)
+    GC.@preserve aux check(ccall((:dmt_upload_aux_a, libdmt), Int32,
+        (Ptr{Cvoid}, Int32, Ptr{Float64}, Int32), se.h, kind, pointer(aux), ncols))
+end
+
+"""
     guiding_linear(B̃, β̃, σ̃, t, HT, FT, cT) -> (H, F, c)
 
 The guiding term of a linear auxiliary law on grid `t` from the end information (HT, FT, cT):
@@ -341,24 +353,29 @@ function obs_info(v, L::AbstractMatrix, Σ::AbstractMatrix)
 end
 
 """
-    DeviceSamplingEnsemble(model, θrec, σ, recordings, tts, aux; artificial_noise=1e-11,
-                           blocking=true, kw...)
+    DeviceSamplingEnsemble(model, θrec, σ, recordings, tts, aux; aux_blocking=aux,
+                           artificial_noise=1e-11, blocking=true, kw...)
 
-`SamplingEnsemble(aux_laws, recordings, tts; artificial_noise)` on the device:
-`recordings[r] = (obs = [(t, v, L, Σ), …], x0 = …)`, `tts[r][k]` the grid of segment k,
-`aux(r, k, obs) -> (B̃, β̃, σ̃, anchor)` the auxiliary law of segment k (e.g. FitzHughNagumoAux
-linearised at the observed y: `(DD.B(t0, P̃), DD.β(t0, P̃), DD.σ(t0, x, P̃), yT)`).  `θrec` is one
-law-parameter vector for all recordings or a function `r -> θrec` (each recording's own target
-law).  Guiding terms through each recording's segments (build_guid_prop), blocking laws with an
-exact full-state artificial end observation (guid_prop_for_blocking; a placeholder until
-set_obs!), the observations for the device's re-derivations, then init_paths! from x0.
+`SamplingEnsemble(aux_laws, recordings, tts; aux_laws_blocking, artificial_noise)` on the device
+(src/sampling_ensemble.jl:20-40 → src/sampling_unit.jl:55-66): `recordings[r] = (obs = [(t, v,
+L, Σ), …], x0 = …)`, `tts[r][k]` the grid of segment k, `aux(r, k, obs) -> (B̃, β̃, σ̃, anchor)`
+the auxiliary law of segment k (build_guid_prop), `aux_blocking` the same for the blocking laws
+(guid_prop_for_blocking).  B̃ and β̃ may be functions of t (a time-dependent linear law: the
+segment's law record is flagged and its per-point table goes up with `upload_aux!`), and so may
+σ̃ (then ã(t) = σ̃σ̃ᵀ(t) is tabled too: `upload_aux_a!`).  `θrec` is one law-parameter vector for
+all recordings or a function `r -> θrec` (each recording's own target law).  Guiding terms
+through each recording's segments, blocking laws with an exact full-state artificial end
+observation (a placeholder until set_obs!), the observations for the device's re-derivations,
+then init_paths! from x0.  The Python twin is `SamplingEnsemble.from_recordings` (api.py).
 """
 function DeviceSamplingEnsemble(model::Integer, θrec, σ::AbstractMatrix, recordings, tts, aux;
-                                artificial_noise=1e-11, blocking=true, kw...)
+                                aux_blocking=aux, artificial_noise=1e-11, blocking=true, kw...)
     d, m = size(σ)
     θof = θrec isa Function ? θrec : (r -> θrec)
     t_all, H_all, F_all, laws, infos = Float64[], Matrix{Float64}[], Matrix{Float64}[], Vector{Float64}[], Any[]
     Hb_all, Fb_all, lawsb = Matrix{Float64}[], Matrix{Float64}[], Vector{Float64}[]
+    tab_pp, tab_b = Matrix{Float64}[], Matrix{Float64}[]   # per-point aux tables (na × npts)
+    any_td, any_tda = false, false
     n_points = Vector{Int}[]
     for (r, rec) in enumerate(recordings)
         K = length(rec.obs)
@@ -371,23 +388,26 @@ function DeviceSamplingEnsemble(model::Integer, θrec, σ::AbstractMatrix, recor
             if nxt !== nothing
                 HT, FT, cT = HT + unpacked(nxt[1], d), FT + nxt[2], cT + nxt[3]
             end
-            B̃, β̃, σ̃, _ = auxes[k]
-            H, F, c = guiding_linear(B̃, β̃, σ̃, Float64.(tts[r][k]), HT, FT, cT)
-            chain[k] = (H, F, c)
-            nxt = (H[1, :], F[1, :], c[1])
+            chain[k] = _guiding(auxes[k], Float64.(tts[r][k]), HT, FT, cT)
+            nxt = (chain[k][1][1, :], chain[k][2][1, :], chain[k][3][1])
         end
         for k in 1:K
-            B̃, β̃, σ̃, an = auxes[k]
+            g = Float64.(tts[r][k])
             append!(t_all, tts[r][k]); push!(H_all, chain[k][1]); push!(F_all, chain[k][2])
-            push!(laws, law_record(θof(r), σ, B̃, β̃, σ̃, chain[k][3][1]; anchor=an))
+            push!(laws, _law_record(θof(r), σ, auxes[k], chain[k][3][1]))
+            push!(tab_pp, aux_table(auxes[k], g, d))
+            any_td |= is_time_dependent(auxes[k]); any_tda |= is_time_dependent_a(auxes[k])
             push!(infos, info[k])
             if blocking
+                ab = aux_blocking(r, k, rec.obs[k])
                 v = zeros(d); vo = collect(rec.obs[k].v); v[1:min(d, length(vo))] .= vo[1:min(d, length(vo))]
                 Ha, Fa, ca = obs_info(v, Matrix(1.0I, d, d), artificial_noise * Matrix(1.0I, d, d))
                 Ho, Fo, co = info[k]
-                H, F, c = guiding_linear(B̃, β̃, σ̃, Float64.(tts[r][k]), Ha + Ho, Fa + Fo, ca + co)
+                H, F, c = _guiding(ab, g, Ha + Ho, Fa + Fo, ca + co)
                 push!(Hb_all, H); push!(Fb_all, F)
-                push!(lawsb, law_record(θof(r), σ, B̃, β̃, σ̃, c[1]; anchor=an))
+                push!(lawsb, _law_record(θof(r), σ, ab, c[1]))
+                push!(tab_b, aux_table(ab, g, d))
+                any_td |= is_time_dependent(ab); any_tda |= is_time_dependent_a(ab)
             end
         end
         push!(n_points, [length(g) for g in tts[r]])
@@ -397,6 +417,11 @@ function DeviceSamplingEnsemble(model::Integer, θrec, σ::AbstractMatrix, recor
     flat(Ms) = vec(permutedims(reduce(vcat, Ms)))     # point-major, components contiguous
     upload_law!(se, DMT_U, DMT_LAW_PP, flat(H_all), flat(F_all), reduce(vcat, laws))
     blocking && upload_law!(se, DMT_U, DMT_LAW_PPB, flat(Hb_all), flat(Fb_all), reduce(vcat, lawsb))
+    if any_td   # per-point tables of both kinds (zero rows on time-homogeneous segments, unused)
+        nc = any_tda ? d * d + d + d * (d + 1) ÷ 2 : d * d + d
+        upload_aux_a!(se, DMT_LAW_PP, vec(reduce(hcat, tab_pp)[1:nc, :]), nc)
+        blocking && upload_aux_a!(se, DMT_LAW_PPB, vec(reduce(hcat, tab_b)[1:nc, :]), nc)
+    end
     upload_obs!(se, reduce(vcat, [packed(i[1]) for i in infos]),
                 reduce(vcat, [collect(i[2]) for i in infos]), Float64[i[3] for i in infos];
                 artificial_noise=artificial_noise)
@@ -414,16 +439,80 @@ function DeviceSamplingEnsemble(model::Integer, θrec, σ::AbstractMatrix, recor
     se
 end
 
+# ---- auxiliary laws: (B̃, β̃, σ̃, anchor); B̃, β̃ (and σ̃) may be functions of t
+is_time_dependent(a) = a[1] isa Function || a[2] isa Function || a[3] isa Function
+is_time_dependent_a(a) = a[3] isa Function
+_at(σ̃, t) = (S = σ̃ isa Function ? Matrix{Float64}(σ̃(t)) : Matrix{Float64}(σ̃); S * S')
+_val(f, t) = f isa Function ? f(t) : f
+
+"Guiding term (H, F, c) of auxiliary law `a` on grid `g` from the end information."
+function _guiding(a, g, HT, FT, cT)
+    B̃, β̃, σ̃, _ = a
+    d = size(HT, 1)
+    if is_time_dependent_a(a)
+        tab = aux_table(a, g, d)
+        hp = d * (d + 1) ÷ 2
+        H, F, c = Matrix{Float64}(undef, hp, length(g)), Matrix{Float64}(undef, d, length(g)),
+                  Vector{Float64}(undef, length(g))
+        check(ccall((:dmt_guiding_linear_tda, libdmt), Int32,
+            (Int32, Ptr{Float64}, Int32, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Float64,
+             Ptr{Float64}, Ptr{Float64}, Ptr{Float64}),
+            d, tab, length(g), g, packed(HT), Float64.(collect(FT)), cT, H, F, c))
+        return permutedims(H), permutedims(F), c
+    elseif is_time_dependent(a)
+        return guiding_linear(t -> _val(B̃, t), t -> _val(β̃, t), σ̃, g, HT, FT, cT)
+    end
+    guiding_linear(B̃, β̃, σ̃, g, HT, FT, cT)
+end
+
+"""
+    aux_table(a, g, d) -> Matrix (d² + d + d(d+1)/2) × length(g)
+
+Per-point rows of a time-dependent auxiliary law on grid `g` (dmt_upload_aux_a layout: B̃(t_i)
+row-major, β̃(t_i), ã(t_i) packed); zeros for a time-homogeneous law (its rows are unused).
+"""
+function aux_table(a, g, d)
+    hp = d * (d + 1) ÷ 2
+    T = zeros(d * d + d + hp, length(g))
+    is_time_dependent(a) || return T
+    B̃, β̃, σ̃, _ = a
+    for (i, t) in enumerate(g)
+        T[1:d*d, i] .= vec(permutedims(Float64.(_val(B̃, t))))
+        T[d*d+1:d*d+d, i] .= Float64.(collect(_val(β̃, t)))
+        T[d*d+d+1:end, i] .= packed(_at(σ̃, t))
+    end
+    T
+end
+
+"Law record of a segment with auxiliary law `a` (time-dependent laws flagged, DMT_LAW_AUXTD)."
+function _law_record(θrec, σ, a, c0)
+    B̃, β̃, σ̃, an = a
+    d = size(σ, 1)
+    if is_time_dependent(a)
+        rec = law_record(θrec, σ, zeros(d, d), zeros(d), σ̃ isa Function ? σ : σ̃, c0;
+                         time_dependent=true)
+        is_time_dependent_a(a) && (rec[16] = 2.0)   # DMT_LAW_AUXTD = 2: ã(t) from the table
+        return rec
+    end
+    law_record(θrec, σ, B̃, β̃, σ̃, c0; anchor=an)
+end
+
 # ---- the reference's (aux_laws, recording(s), tts) constructors on the device
 # The target law of a recording is `recording.P` (ObservationSchemes recordings are
 # (P, obs, t0, x0_prior), docs/src/get_started/overview.md:18-20); its observations are
 # LinearGsnObs with fields t, obs, L, Σ (docs/src/tutorials/preamble.md:80-86).  Models are
-# recognised by their DiffusionDefinition names; extend `device_model` for others.
+# recognised by their DiffusionDefinition names or fields; extend `device_model` for others.
+# Every DMT_MODEL_* of include/dmt.h has a branch (tests/test_julia_binding.py checks it).
 """
     device_model(P) -> (kind, θrec, σ)
 
-The device model of a DiffusionDefinition target law: FitzHughNagumo (θ = ϵ, s, γ, β, σ —
-positional, `FitzHughNagumo(θ...)` at docs/src/tutorials/preamble.md:78) and Lorenz.
+The device model of a DiffusionDefinition target law:
+* DMT_MODEL_OU — an Ornstein–Uhlenbeck law dX = −Θ(X − μ)dt + σdW: DiffusionDefinition's
+  `OrnsteinUhlenbeck(θ, μ, σ)` (scalar, d = 1) or any law with fields `Θ` (or `θ`), `μ`, `σ`
+  (d ≤ 3; matrices, vectors or scalars) — the north star's 2-D OU bridge;
+* DMT_MODEL_FHN — FitzHughNagumo (θ = ϵ, s, γ, β, σ — positional, `FitzHughNagumo(θ...)` at
+  docs/src/tutorials/preamble.md:78);
+* DMT_MODEL_LORENZ — Lorenz / Lorenz63 (s, r, β[, σ₁, σ₂, σ₃]).
 """
 function device_model(P)
     name = nameof(typeof(P))
@@ -434,6 +523,22 @@ function device_model(P)
         s, r, β = (getfield(P, i) for i in 1:3)
         σ = nfields(P) >= 6 ? [getfield(P, 4), getfield(P, 5), getfield(P, 6)] : [1.0, 1.0, 1.0]
         return DMT_MODEL_LORENZ, [s, r, β], Matrix{Float64}(LinearAlgebra_diag(σ))
+    elseif name === :OrnsteinUhlenbeck || name === :OU || name === :OrnsteinUhlenbeck2D ||
+           (hasproperty(P, :μ) && hasproperty(P, :σ) && (hasproperty(P, :Θ) || hasproperty(P, :θ)))
+        Θ = hasproperty(P, :Θ) ? getproperty(P, :Θ) :
+            hasproperty(P, :θ) ? getproperty(P, :θ) : getfield(P, 1)
+        μ = hasproperty(P, :μ) ? getproperty(P, :μ) : getfield(P, 2)
+        σ = hasproperty(P, :σ) ? getproperty(P, :σ) : getfield(P, 3)
+        μv = μ isa Number ? [Float64(μ)] : Float64.(collect(μ))
+        d = length(μv)
+        Θm = Θ isa Number ? Float64(Θ) * Matrix(1.0I, d, d) : Matrix{Float64}(reshape(collect(Θ), d, d))
+        σm = σ isa Number ? Float64(σ) * Matrix(1.0I, d, d) :
+             σ isa AbstractVector ? Matrix{Float64}(LinearAlgebra_diag(Float64.(σ))) : Matrix{Float64}(σ)
+        d <= 3 || error("DiffusionMCMCToolsAMD: OU of dimension $d (the device holds d ≤ 3)")
+        θrec = zeros(12)
+        θrec[1:d*d] .= vec(permutedims(Θm))            # Θ row-major (DMT_LAW_THETA 0)
+        θrec[10:9+d] .= μv                               # μ at 9
+        return DMT_MODEL_OU, θrec, σm
     end
     error("DiffusionMCMCToolsAMD: no device model for $(name); extend device_model")
 end
@@ -442,9 +547,12 @@ LinearAlgebra_diag(v) = [i == j ? v[i] : 0.0 for i in 1:length(v), j in 1:length
 """
     device_aux(kind, θrec, σ, o) -> (B̃, β̃, σ̃, anchor)
 
-The auxiliary law of a segment ending in observation `o`, linearised at the observed value
-(FitzHughNagumoAux; the Lorenz aux of config C5), in the arithmetic order of the device's
-re-derivation in set_proposal_law! (DESIGN.md §3), so host and device laws agree bit for bit.
+The auxiliary law of a segment ending in observation `o` that an auxiliary-law TYPE stands for
+(the tutorials pass `FitzHughNagumoAux`): the target linearised at the observed value
+(FitzHughNagumoAux; the Lorenz aux of config C5) or, for a linear target (OU), the target law
+itself (B̃ = −Θ, β̃ = Θμ, σ̃ = σ: the guided proposal is then exact).  In the arithmetic order of
+the device's re-derivation in set_proposal_law! and of the Python twin (models.py), so host and
+device laws agree bit for bit.
 """
 function device_aux(kind, θrec, σ, o)
     if kind == DMT_MODEL_FHN
@@ -453,6 +561,12 @@ function device_aux(kind, θrec, σ, o)
         B̃ = [(1.0 - 3.0 * (y * y)) / e  -1.0 / e; γ  -1.0]
         β̃ = [(s + 2.0 * (y * y * y)) / e, β]
         return B̃, β̃, σ, [y]
+    elseif kind == DMT_MODEL_OU
+        d = size(σ, 1)
+        Θ = permutedims(reshape(θrec[1:d*d], d, d))
+        μ = θrec[10:9+d]
+        β̃ = [sum(Θ[i, j] * μ[j] for j in 1:d) for i in 1:d]   # left to right, no fma
+        return -Θ, β̃, σ, nothing
     else
         s, r, b = θrec[1], θrec[2], θrec[3]
         x0, x1, x2 = Float64.(o.v[1:3])
@@ -465,14 +579,75 @@ end
 
 _obs(o) = (t = o.t, v = collect(Float64, o.obs), L = Matrix{Float64}(o.L), Σ = Matrix{Float64}(o.Σ))
 
-function _device_ensemble(aux_laws, recordings, tts; artificial_noise=1e-11, kw...)
+"""
+    _as_aux(a, σ) -> (B̃, β̃, σ̃, anchor)
+
+One auxiliary law given by the caller: a tuple (B̃, β̃[, σ̃[, anchor]]) or a NamedTuple with
+fields B̃ (or B), β̃ (or β), optionally σ̃ (or σ) and anchor — B̃, β̃, σ̃ constants or functions of
+t (a time-dependent linear law, GuidedProposals' `aux_laws` varying in t).  σ̃ defaults to the
+target's σ.
+"""
+function _as_aux(a, σ)
+    if a isa NamedTuple
+        B̃ = haskey(a, :B̃) ? a.B̃ : a.B
+        β̃ = haskey(a, :β̃) ? a.β̃ : a.β
+        σ̃ = haskey(a, :σ̃) ? a.σ̃ : haskey(a, :σ) ? a.σ : σ
+        return B̃, β̃, σ̃, get(a, :anchor, nothing)
+    end
+    length(a) >= 2 || error("an auxiliary law is (B̃, β̃[, σ̃[, anchor]])")
+    (a[1], a[2], length(a) >= 3 ? a[3] : σ, length(a) >= 4 ? a[4] : nothing)
+end
+
+"""
+    aux_function(aux_laws, kind, θof, σ, Ps) -> (r, k, o) -> (B̃, β̃, σ̃, anchor)
+
+The reference's `aux_laws` argument (src/sampling_unit.jl:55-60), as the Python twin
+`api._aux_callable` reads it: `nothing` or an auxiliary-law TYPE (`FitzHughNagumoAux`) — the
+law `device_aux` derives for the target at the segment's observation; a function
+`(P, obs) -> law` of recording r's target `Ps[r]`; one law (tuple / NamedTuple, `_as_aux`) for
+every segment; or a vector of those per segment k.
+"""
+function aux_function(aux_laws, kind, θof, σ, Ps)
+    (aux_laws === nothing || aux_laws isa Type) &&
+        return (r, k, o) -> device_aux(kind, θof(r), σ, o)
+    if aux_laws isa AbstractVector
+        return function (r, k, o)
+            a = aux_laws[k]
+            a isa Type ? device_aux(kind, θof(r), σ, o) :
+            a isa Function ? _as_aux(a(Ps[r], o), σ) : _as_aux(a, σ)
+        end
+    end
+    aux_laws isa Function && return (r, k, o) -> _as_aux(aux_laws(Ps[r], o), σ)
+    return (r, k, o) -> _as_aux(aux_laws, σ)
+end
+
+"""
+    _device_ensemble(aux_laws, recordings, tts; aux_laws_blocking, artificial_noise,
+                     solver_choice, solver_choice_blocking, args...)
+
+The reference's `SamplingEnsemble(aux_laws, recordings, tts[, args]; aux_laws_blocking,
+artificial_noise, solver_choice_blocking)` / `SamplingPair(…)` on the device
+(src/sampling_ensemble.jl:20-40, src/sampling_pair.jl:40-50, src/sampling_unit.jl:55-66):
+every keyword of those signatures is read.  `aux_laws` and `aux_laws_blocking` (default
+`aux_laws`) give the laws of PP and PPb (`aux_function`), `artificial_noise` the blocking
+laws' artificial observation.  `args` and the `solver_choice*` keywords select GuidedProposals'
+ODE solver for the guiding term; the device's guiding term is the exact discrete filter that
+every convergent solver approaches (DESIGN.md §7), so they are accepted and have no effect.
+"""
+function _device_ensemble(aux_laws, recordings, tts; aux_laws_blocking=nothing,
+                          artificial_noise=1e-11, solver_choice=nothing,
+                          solver_choice_blocking=nothing, args=nothing, kw...)
+    isempty(kw) || error("DiffusionMCMCToolsAMD: unknown keyword(s) $(collect(keys(kw)))")
     kinds = [device_model(rec.P) for rec in recordings]
     kind, _, σ = kinds[1]
     all(k -> k[1] == kind, kinds) || error("one device ensemble holds one model family")
+    Ps = [rec.P for rec in recordings]
+    θof = r -> kinds[r][2]
     recs = [(obs = [_obs(o) for o in rec.obs], x0 = rand(rec.x0_prior)) for rec in recordings]
-    aux(r, k, o) = device_aux(kind, kinds[r][2], σ, o)
+    aux = aux_function(aux_laws, kind, θof, σ, Ps)
+    auxb = aux_laws_blocking === nothing ? aux : aux_function(aux_laws_blocking, kind, θof, σ, Ps)
     opts = DEVICE_OPTS[]
-    DeviceSamplingEnsemble(kind, r -> kinds[r][2], σ, recs, tts, aux;
+    DeviceSamplingEnsemble(kind, θof, σ, recs, tts, aux; aux_blocking=auxb,
                            artificial_noise=artificial_noise, device=opts.device, seed=opts.seed)
 end
 
@@ -538,30 +713,32 @@ end
 function SamplingPair(aux_laws::Type, recording, tts, args; kw...)
     DEVICE[] || return invoke(SamplingPair, Tuple{Any,Any,Any,Any}, aux_laws, recording, tts,
                               args; kw...)
-    _device_pair(aux_laws, recording, tts; kw...)
+    _device_pair(aux_laws, recording, tts; args=args, kw...)
 end
+# aux_laws given as laws rather than a type (a function (P, obs) -> law, one law, or a vector
+# per segment; time-dependent laws included): DeviceSamplingPair / DeviceSamplingEnsemble by
+# name (a method of the reference's constructor for these argument types would capture its
+# CPU calls too)
+DeviceSamplingPair(aux_laws, recording, tts, args...; kw...) =
+    _device_pair(aux_laws, recording, tts; (isempty(args) ? () : (args=args[1],))..., kw...)
 function _device_pair(aux_laws, recording, tts; kw...)
-    kws = Dict(kw)
-    se = _device_ensemble(aux_laws, [recording], [tts];
-                          artificial_noise=get(kws, :artificial_noise, 1e-11))
+    se = _device_ensemble(aux_laws, [recording], [tts]; kw...)
     DeviceSamplingPair(se, 1)
 end
 
 function SamplingEnsemble(aux_laws::Type, recordings, tts; kw...)
     DEVICE[] || return invoke(SamplingEnsemble, Tuple{Any,Any,Any}, aux_laws, recordings, tts;
                               kw...)
-    _device_ensemble_kw(aux_laws, recordings, tts; kw...)
+    _device_ensemble(aux_laws, collect(recordings), collect(tts); kw...)
 end
 function SamplingEnsemble(aux_laws::Type, recordings, tts, args; kw...)
     DEVICE[] || return invoke(SamplingEnsemble, Tuple{Any,Any,Any,Any}, aux_laws, recordings,
                               tts, args; kw...)
-    _device_ensemble_kw(aux_laws, recordings, tts; kw...)
+    _device_ensemble(aux_laws, collect(recordings), collect(tts); args=args, kw...)
 end
-function _device_ensemble_kw(aux_laws, recordings, tts; kw...)
-    kws = Dict(kw)
+DeviceSamplingEnsemble(aux_laws, recordings::AbstractVector, tts::AbstractVector, args...; kw...) =
     _device_ensemble(aux_laws, collect(recordings), collect(tts);
-                     artificial_noise=get(kws, :artificial_noise, 1e-11))
-end
+                     (isempty(args) ? () : (args=args[1],))..., kw...)
 
 # ============================================================ blocks
 abstract type DeviceBlocks end

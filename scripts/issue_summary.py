@@ -20,6 +20,10 @@ import collections
 import csv
 import json
 import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import provenance  # noqa: E402
 import statistics
 
 
@@ -83,6 +87,7 @@ def main():
     out["limiter"] = a.limiter
     out["note"] = ("issue roofline: frac = share of SIMD cycles in which a VALU instruction "
                    "issues (1.0 = the SIMD's VALU never idle)")
+    provenance.stamp(out)  # the source tree this profile measured
     with open(a.out, "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out))

@@ -13,6 +13,11 @@ the --stats kernel_stats.csv average (every dispatch) when no trace is given.
 import argparse
 import csv
 import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import provenance  # noqa: E402
 import statistics
 
 
@@ -54,6 +59,7 @@ def main():
     else:
         raise SystemExit("--trace or --stats")
     out["avg_us_per_unit"] = out["avg_us"] / a.units_per_launch
+    provenance.stamp(out)  # the source tree this profile measured
     with open(a.out, "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out))

@@ -13,6 +13,11 @@ per launch and per unit (--units-per-launch: the iterations one persistent dispa
 import argparse
 import csv
 import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import provenance  # noqa: E402
 import statistics
 
 
@@ -63,6 +68,7 @@ def main():
            "traffic_bytes_per_launch": (f_b + w_b) * a.units_per_launch,
            "fetch_kib_raw_median": statistics.median(fk),
            "write_kib_raw_median": statistics.median(wk), "calibration": calib}
+    provenance.stamp(out)  # the source tree this profile measured
     with open(a.out, "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out))
