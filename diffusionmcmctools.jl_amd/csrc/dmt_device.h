@@ -442,12 +442,14 @@ struct PSum {
 struct U4 { uint32_t x, y, z, w; };
 
 __device__ __forceinline__ U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
+  k0 = __builtin_amdgcn_readfirstlane(k0);  // the key is the ensemble's seed: wave-uniform
+  k1 = __builtin_amdgcn_readfirstlane(k1);
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
     // full 64-bit products: one v_mad_u64_u32 each instead of a mul_lo + mul_hi pair
     const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
-    U4 n = {(uint32_t)(p1 >> 32) ^ c.y ^ k0, (uint32_t)p1, (uint32_t)(p0 >> 32) ^ c.w ^ k1,
-            (uint32_t)p0};
+    U4 n = {(uint32_t)(p1 >> 32) ^ c.y ^ k0, (uint32_t)p1,
+            (uint32_t)(p0 >> 32) ^ c.w ^ k1, (uint32_t)p0};
     c = n;
     k0 += 0x9E3779B9u;
     k1 += 0xBB67AE85u;
@@ -540,8 +542,14 @@ __device__ __forceinline__ void rng_sincospif(float x, float* sn, float* cs) {
     cp = __builtin_fmaf(cp, z, RNGF_C1);
     const float s0 = r * sp, c0 = __builtin_fmaf(cp, z, 1.0f);
     const int q = (int)n & 3;
-    *sn = q == 0 ? s0 : q == 1 ? c0 : q == 2 ? -s0 : -c0;
-    *cs = q == 0 ? c0 : q == 1 ? -s0 : q == 2 ? -c0 : s0;
+    // quadrant q: (sin, cos) = (s0, c0), (c0, −s0), (−s0, −c0), (−c0, s0) — a swap on odd q and
+    // sign flips (exact) on the sign bit, branch-free (the chained selects became divergent
+    // branches)
+    const bool sw = (q & 1) != 0;
+    const uint32_t sa = __builtin_bit_cast(uint32_t, sw ? c0 : s0);
+    const uint32_t ca = __builtin_bit_cast(uint32_t, sw ? s0 : c0);
+    *sn = __builtin_bit_cast(float, sa ^ ((uint32_t)(q & 2) << 30));
+    *cs = __builtin_bit_cast(float, ca ^ ((uint32_t)((q + 1) & 2) << 30));
 }
 
 // ---- fp64 Box–Muller kernels: table-driven (scripts/gen_bm_tables.py), no division, short

@@ -544,6 +544,10 @@ struct PairChunk {  // steps per chunk: an even number of whole Philox blocks of
 #ifndef DMT_PK_SDT_TABLE  // shared grids: the packet kernel reads √dt from a per-point table
 #define DMT_PK_SDT_TABLE 1
 #endif
+#ifndef DMT_PK_CHUNK_STORE  // 1: X°, W° pieces stored at the end of the chunk that completes them
+#define DMT_PK_CHUNK_STORE 0   // (measured slower: C5 1 906-1 925 vs 1 432-1 449 µs per draw,
+                               // profiles/r05b) 0: the whole packet staged in registers, stored at its end
+#endif
 #ifndef DMT_PK_LDS  // 1: the packet's X°, W° staged in the lane's LDS rows
 #define DMT_PK_LDS 0   // 0: staged in registers (measured faster in the kernel: 1 455 vs 1 574 µs, C5)
 #endif
@@ -733,6 +737,12 @@ __device__ __forceinline__ bool run_segment_pk(const Law<Mdl, T>& L, const T* __
 #if DMT_PK_LDS
         auto st = [&](int c, int e) -> T& { return stg[(c * PK + e) * 65 + lane]; };
         auto put = [&](int c, int e, T v) { st(c, e) = v; };
+#elif DMT_PK_CHUNK_STORE
+        // a chunk of K steps completes K / VE whole pieces of every component: they leave at
+        // the chunk's end (the registers of one chunk's pieces instead of a whole packet's)
+        constexpr int CP = K / VE;
+        v16 ob[NS][CP];
+        auto put = [&](int c, int e, T v) { ob[c][(e % K) / VE][e % VE] = v; };
 #else
         v16 ob[NS][NV];
         auto put = [&](int c, int e, T v) { ob[c][e / VE][e % VE] = v; };
@@ -763,6 +773,24 @@ __device__ __forceinline__ bool run_segment_pk(const Law<Mdl, T>& L, const T* __
               }
             }
           }
+#if !DMT_PK_LDS && DMT_PK_CHUNK_STORE
+          if (stx) {
+#pragma unroll
+            for (int p = 0; p < D; ++p) {
+              v16* dst = (v16*)&Xd[pix((int64_t)j * PK + 1, p, D)];
+#pragma unroll
+              for (int u = 0; u < CP; ++u) dst[v * CP + u] = ob[p][u];
+            }
+          }
+          if (stw) {
+#pragma unroll
+            for (int k = 0; k < M; ++k) {
+              v16* dst = (v16*)&Wd[pix((int64_t)j * PK + 1, k, M)];
+#pragma unroll
+              for (int u = 0; u < CP; ++u) dst[v * CP + u] = ob[WR + k][u];
+            }
+          }
+#endif
 #if DMT_PK_ROLL
           // the piece of u.W this chunk consumed is refilled with the next packet's: a prefetch
           // distance of one packet in the registers of one (the tile's spare rows keep the
@@ -777,6 +805,7 @@ __device__ __forceinline__ bool run_segment_pk(const Law<Mdl, T>& L, const T* __
           ps.template add_subtree<Log2<K>::v>(tree_sum<T, K>(gv));
           cur = nxt;
         }
+#if DMT_PK_LDS || !DMT_PK_CHUNK_STORE
         auto piece = [&](int c, int v) -> v16 {
 #if DMT_PK_LDS
           v16 o;
@@ -803,6 +832,7 @@ __device__ __forceinline__ bool run_segment_pk(const Law<Mdl, T>& L, const T* __
             for (int v = 0; v < NV; ++v) dst[v] = piece(WR + k, v);
           }
         }
+#endif
 #if !DMT_PK_ROLL
         if (READW) {
 #pragma unroll
@@ -2209,6 +2239,22 @@ __device__ __forceinline__ void scan_block(const BlockArgs<T>& a, const int64_t 
   ok_res = ok;
 }
 
+// The persistent kernel's time-dependent iterations call scan_block out of line (DESIGN.md §7,
+// "the round-4 k_mcmc_scan<TD> fault"): inlined into k_mcmc_scan's iteration loop, the TD body
+// (256 VGPRs + ~100 AGPRs, ~150 SGPRs spilled to VGPR lanes) gave wrong Girsanov terms from the
+// third iteration on, or an illegal address, depending on the build; out of line it is
+// bit-identical to the per-iteration kernels and the oracle.  0: inline (for that record).
+#ifndef DMT_TD_NOINLINE
+#define DMT_TD_NOINLINE 1
+#endif
+template <class Mdl, class T, int MODE, class Sel, bool TD>
+__device__ __attribute__((noinline)) void scan_block_ni(const BlockArgs<T>& a, const int64_t blk,
+                                                       const uint32_t iter, const Sel& sel,
+                                                       ScanLds<Mdl::D, T>& S, T& ll_res,
+                                                       bool& ok_res) {
+  scan_block<Mdl, T, MODE, Sel, TD>(a, blk, iter, sel, S, ll_res, ok_res);
+}
+
 template <class Mdl, class T, int MODE, bool TD = false>
 __global__ __launch_bounds__((64 * ScanCfg<Mdl::D, T>::WPB), 1) void k_block_scan(const BlockArgs<T> a) {
   using Cfg = ScanCfg<Mdl::D, T>;
@@ -2447,6 +2493,11 @@ __device__ __forceinline__ void mcmc_scan_block(const BlockArgs<T>& a, const Acc
     const double E = exp1_draw(c.seed, (uint32_t)g0 + c.seg_base, (uint32_t)(it + c.key_delta), c.salt);
     T lp;
     bool ok;
+#if DMT_TD_NOINLINE
+    if constexpr (TD)
+      scan_block_ni<Mdl, T, MODE_PCN, SelMask, TD>(a, blk, (uint32_t)(it + c.key_delta), sel, L, lp, ok);
+    else
+#endif
     scan_block<Mdl, T, MODE_PCN, SelMask, TD>(a, blk, (uint32_t)(it + c.key_delta), sel, L, lp, ok);
     llp = ok ? (double)lp : -INFINITY;
     const bool acc = E > -(llp - ll);

@@ -1668,7 +1668,7 @@ static dmt_status mcmc_run_impl(dmt_ens* h, int32_t layout, int64_t b0, int64_t 
 }
 
 #ifndef DMT_MCMC_SCAN_TD  // 0: an ensemble with an aux table runs dmt_mcmc_run per iteration
-#define DMT_MCMC_SCAN_TD 0
+#define DMT_MCMC_SCAN_TD 1
 #endif
 // Queue n_iter MCMC iterations (iteration it keyed by it + key_delta, salt) on the stream; the
 // per-iteration (fetch_ll, fetch_ll°, accepted count) go to pinned h_run (one rank) or d_run

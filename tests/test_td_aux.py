@@ -474,10 +474,10 @@ def test_ou_td_aux_blocking_loop_device_equals_oracle(prec, with_a):
 
 @pytest.mark.gpu
 def test_ou_td_aux_mcmc_run_device_equals_oracle():
-    """dmt_mcmc_run on an OU ensemble with time-dependent auxiliary laws (the per-iteration
-    scan and accept kernels: the persistent and register-resident ones are not eligible while a
-    table is present): fetch_ll results, paths, ll and histories equal the oracle's, bit for
-    bit."""
+    """dmt_mcmc_run on an OU ensemble with time-dependent auxiliary laws (k_mcmc_scan's TD
+    instantiation, its scan body out of line — DESIGN.md §7, the round-4 fault; the
+    register-resident kernels are not eligible while a table is present): fetch_ll results,
+    paths, ll and histories equal the oracle's, bit for bit."""
     case, (dev, ora), ids = _td_pair(L.MAP_AUTO, L.F64, model=cs.ou_ragged_model(), hist_len=7)
     lid, nb = ids[0]
     for e in (dev, ora):
@@ -572,3 +572,42 @@ def test_reference_form_td_aux_tutorial_device_equals_oracle():
     assert d[2]["bb"].ll == o[2]["bb"].ll
     np.testing.assert_array_equal(np.concatenate(d[2]["sp"].u.XX), np.concatenate(o[2]["sp"].u.XX))
     d[2]["sp"].close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_iter", [6, 25])
+def test_ou_td_aux_persistent_equals_per_iteration(n_iter):
+    """The round-4 fault's shape (gpurun_out/r04g/pytest.log:31): one multi-iteration
+    dmt_mcmc_run launch of k_mcmc_scan<…, TD> against the per-iteration scan + accept kernels
+    (DMT_MCMC_PERSIST=0) on the same ensemble — every iteration's per-block ll° (the first
+    wrong one was the third, profiles/r05a) and decisions, the fetch_ll results and the paths,
+    bit for bit."""
+    ens = []
+    for env in ({}, {"DMT_MCMC_PERSIST": "0"}):
+        saved = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
+        try:
+            _, (dev,), ids = _td_pair_dev_only(n_iter + 1)
+        finally:
+            for k, v in saved.items():
+                os.environ.pop(k) if v is None else os.environ.__setitem__(k, v)
+        ens.append(dev)
+    lid, nb = ids[0]
+    for e in ens:
+        e.loglikhd(lid, L.U, 0, nb)
+    r = [e.mcmc_run(lid, 0, nb, 1, n_iter, salt=7) for e in ens]
+    assert np.array_equal(r[0], r[1])
+    for what in (L.BLK_LLPROP_HIST, L.BLK_ACC_HIST, L.BLK_LL_HIST):
+        assert np.array_equal(ens[0].get_block_state(lid, what, 0, nb, n_iter + 1),
+                              ens[1].get_block_state(lid, what, 0, nb, n_iter + 1))
+    cs.assert_paths_equal(ens[0], ens[1])
+    for e in ens:
+        e.close()
+
+
+def _td_pair_dev_only(hist_len):
+    """The device ensemble of _td_pair (ragged OU, varying tables on every other segment)."""
+    case, (dev, _), ids = _td_pair(L.MAP_AUTO, L.F64, model=cs.ou_ragged_model(),
+                                   hist_len=hist_len)
+    return case, (dev,), ids
+
