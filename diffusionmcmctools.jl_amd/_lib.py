@@ -31,6 +31,7 @@ RNG_AUTO = 0xFFFFFFFF
 SALT_LIMIT = 0x40000000
 LAW_STRIDE = 64
 LAW_AUXTD = 15  # DMT_LAW_AUXTD: time-dependent auxiliary law (dmt_upload_aux)
+LAW_GSTALE = 14  # DMT_LAW_GSTALE: u°'s guiding term left stale by critical_change = false
 LAW_THETA, LAW_SIGMA, LAW_A, LAW_BT, LAW_BETA, LAW_DA, LAW_C0, LAW_TRACE = 0, 16, 25, 31, 40, 43, 49, 50
 LAW_SIGINV = 51
 LAW_ANCHOR = 60

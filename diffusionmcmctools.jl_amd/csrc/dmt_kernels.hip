@@ -4508,6 +4508,7 @@ __global__ __launch_bounds__(64) void k_set_prop_law(const ParamArgs a, int wg_p
 #pragma unroll
     for (int i = kAux0; i < kAux1; ++i) old[i - kAux0] = dst[i];
     const double c0 = dst[DMT_LAW_C0];
+    const bool old_stale = dst[DMT_LAW_GSTALE] != 0.0;
 #pragma unroll
     for (int i = 0; i < DMT_LAW_STRIDE; ++i) rec[i] = src[i];
     rec[DMT_LAW_C0] = c0;
@@ -4521,19 +4522,29 @@ __global__ __launch_bounds__(64) void k_set_prop_law(const ParamArgs a, int wg_p
           eq_changed = true;
     }
     write_params(a, rec);
+    bool aux_changed = false;  // u°'s auxiliary law, before vs after the update
 #pragma unroll
-    for (int i = 0; i < DMT_LAW_STRIDE; ++i) dst[i] = rec[i];
+    for (int i = kAux0; i < kAux1; ++i)
+      if (i != DMT_LAW_C0 && __double_as_longlong(old[i - kAux0]) != __double_as_longlong(rec[i]))
+        aux_changed = true;
     const bool used = kind == ((!term && g == g1) ? 1 : 0);
+    // the stale-guiding-term bit of u°'s record: false keeps a guiding term whose
+    // auxiliary law changed — marked, so that the default treats the record as critical later;
+    // a recomputed (or unchanged) guiding term clears it; a record the block does not use keeps it
     if (used && a.cc_mode == 1) {
       changed = true;
+      rec[DMT_LAW_GSTALE] = 0.0;
     } else if (used && a.cc_mode == 0) {
       changed = changed || eq_changed;
+      rec[DMT_LAW_GSTALE] = ((old_stale || aux_changed) && !eq_changed) ? 1.0 : 0.0;
     } else if (used) {
-#pragma unroll
-      for (int i = kAux0; i < kAux1; ++i)
-        if (i != DMT_LAW_C0 && __double_as_longlong(old[i - kAux0]) != __double_as_longlong(rec[i]))
-          changed = true;
+      changed = changed || aux_changed || old_stale;
+      rec[DMT_LAW_GSTALE] = 0.0;
+    } else {
+      rec[DMT_LAW_GSTALE] = old_stale ? 1.0 : 0.0;
     }
+#pragma unroll
+    for (int i = 0; i < DMT_LAW_STRIDE; ++i) dst[i] = rec[i];
   }
   if (wg_per_block) {
     changed = __syncthreads_or(changed ? 1 : 0) != 0;

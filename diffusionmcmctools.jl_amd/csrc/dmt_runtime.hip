@@ -139,7 +139,10 @@ struct dmt_ens {
   double svc_idle_ms = 2.0;   // DMT_SVC_IDLE_MS: a launch idles this long for a post, then leaves
   int64_t svc_fit_nb = -1;    // the range size whose co-residency svc_fit holds
   bool svc_fit = false;
-  struct { uint64_t starts = 0, relaunches = 0, posts = 0, waits = 0, off = 0; } svc_stats;  // DMT_SVC_STATS
+  // DMT_SVC_STATS; posts0 / relaunches0: the counts when the service was last enabled (the
+  // self-disable rule looks at the counts since then)
+  struct { uint64_t starts = 0, relaunches = 0, posts = 0, waits = 0, off = 0, posts0 = 0,
+           relaunches0 = 0; } svc_stats;
   char* svc_host = nullptr;     // pinned: posted @0, stop @64 (separate lines)
   uint64_t* svc_rec = nullptr;  // pinned: [2][svc_rec_nwg][8] records (SvcArgs::rec)
   int64_t svc_rec_nwg = 0;
@@ -185,6 +188,10 @@ struct dmt_ens {
   void* d_aux[2] = {nullptr, nullptr};  // [kind] per-point B̃(t_i), β̃(t_i) (dmt_upload_aux)
   double* d_law[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
   bool have_law[2][2] = {{false, false}, {false, false}};  // [unit][kind] uploaded at least once
+  // [unit][kind]: an uploaded law record asks for ã(t) from the table (DMT_LAW_AUXTD = 2) /
+  // [kind]: the aux table holds ã columns (dmt_upload_aux_a with d·d + d + d(d+1)/2 columns)
+  bool law_auxtd2[2][2] = {{false, false}, {false, false}};
+  bool aux_has_a[2] = {false, false};
   // observation information for the device backward filter (dmt_upload_obs / dmt_set_obs)
   double* d_obsH = nullptr;  // [G][hp]
   double* d_obsF = nullptr;  // [G][d]
@@ -463,6 +470,10 @@ dmt_status law_ready(dmt_ens* h, int unit_needed_flip, const Layout* L, int64_t 
     return fail(DMT_ERR_STATE, "PP law not uploaded (dmt_upload_law)");
   if (need_ppb && (!h->d_law[0][1] || !h->d_H[0][1] || !h->d_F[0][1]))
     return fail(DMT_ERR_STATE, "PPb (blocking) law not uploaded but a non-terminal block is used");
+  for (int k = 0; k < 2; ++k)
+    if ((h->law_auxtd2[0][k] || h->law_auxtd2[1][k]) && !(h->d_aux[k] && h->aux_has_a[k]))
+      return fail(DMT_ERR_STATE, "a law record with DMT_LAW_AUXTD = 2 needs an aux table with ã "
+                                 "columns (dmt_upload_aux_a)");
   (void)unit_needed_flip;
   return DMT_OK;
 }
@@ -630,12 +641,17 @@ void svc_fold(const dmt_ens* h, uint64_t slot, double* out3) {
   }
 }
 
-// A service whose launches keep leaving idle before their iteration was posted (other work
-// holding the CUs the grid needs: the non-resident workgroups start only after workgroup 0's
-// idle exit) is turned off for the handle; the fused iterations then run one launch each.
+// A service whose launches keep leaving idle before their iteration is posted is turned off for
+// the handle; the fused iterations then run one launch each.  Two causes, both counted: other
+// work holding the CUs the grid needs (the non-resident workgroups start only after workgroup
+// 0's idle exit: found in svc_wait_done), and a host that is away longer than half the idle
+// window between its iterations (relaunched at the post) — then every iteration pays a launch
+// anyway and the resident launch buys nothing.  The rule looks at the posts and relaunches
+// since the service was last enabled (dmt_set_service), so re-enabling it starts afresh.
 void svc_check_degraded(dmt_ens* h) {
   const auto& st = h->svc_stats;
-  if (h->service && st.posts >= 16 && 4 * st.relaunches > st.posts) {
+  const uint64_t posts = st.posts - st.posts0, rel = st.relaunches - st.relaunches0;
+  if (h->service && posts >= 16 && 4 * rel > posts) {
     h->service = false;
     h->svc_stats.off = 1;
   }
@@ -1235,6 +1251,13 @@ dmt_status dmt_upload_law(dmt_ens* h, int32_t unit, int32_t kind, const double* 
                               h->d_tile_qoff, h->stream));
   }
   if (laws) {
+    bool td2 = false;
+    for (int64_t g = 0; g < h->G && !td2; ++g) td2 = laws[g * DMT_LAW_STRIDE + DMT_LAW_AUXTD] == 2.0;
+    if (td2 && h->d_aux[kind] && !h->aux_has_a[kind])
+      return fail(DMT_ERR_INVALID, "a law record with DMT_LAW_AUXTD = 2 needs the aux table's ã "
+                                   "columns (dmt_upload_aux_a with d*d + d + d(d+1)/2 columns)");
+    h->law_auxtd2[unit][kind] = td2;
+    if (!seeded) h->law_auxtd2[unit ^ 1][kind] = td2;
     for (int s = 0; s < 2; ++s)
       if (!h->d_law[s][kind]) {
         DMT_TRY(ens_alloc(h, &h->d_law[s][kind], h->G * DMT_LAW_STRIDE));
@@ -1271,8 +1294,13 @@ dmt_status dmt_upload_aux_a(dmt_ens* h, int32_t kind, const double* aux, int32_t
       h->bytes -= plane_elems(h, na) * (int64_t)h->esz;
       h->d_aux[kind] = nullptr;
     }
+    h->aux_has_a[kind] = false;
     return DMT_OK;
   }
+  if (ncols == nb && (h->law_auxtd2[0][kind] || h->law_auxtd2[1][kind]))
+    return fail(DMT_ERR_INVALID, "a law record with DMT_LAW_AUXTD = 2 needs the aux table's ã "
+                                 "columns (d*d + d + d(d+1)/2 per point)");
+  h->aux_has_a[kind] = ncols == na;
   const int C = na;  // the device table always holds the ã columns (zero when not given)
   if (!h->d_aux[kind]) {
     DMT_TRY(ens_alloc_bytes(h, &h->d_aux[kind], plane_elems(h, C) * h->esz));
@@ -2661,6 +2689,8 @@ dmt_status dmt_set_service(dmt_ens* h, int32_t enable, double idle_ms) {
   h->service = enable != 0 && idle_ms > 0.0;
   if (idle_ms > 0.0) h->svc_idle_ms = idle_ms;
   h->svc_stats.off = 0;
+  h->svc_stats.posts0 = h->svc_stats.posts;  // the self-disable rule counts from here
+  h->svc_stats.relaunches0 = h->svc_stats.relaunches;
   return DMT_OK;
 }
 

@@ -311,14 +311,22 @@ class Ensemble:
         sums, no collective)."""
         n = int(n_iter)
         buf = self._run_out.get(n)
-        if buf is None:  # one result buffer per run length, its address taken once
-            arr = np.empty((n, 3), dtype=np.float64)
-            buf = self._run_out[n] = (arr, arr.ctypes.data)
+        if buf is None:
+            buf = self.prepare_run(n)
         st = L.fast["dmt_mcmc_run_local" if local else "dmt_mcmc_run"](
             self._h, layout, b0, b1, iter0, n, salt, buf[1])
         if st:
             L.check(st)
         return buf[0].copy()
+
+    def prepare_run(self, n_iter):
+        """The result buffer of mcmc_run calls of n_iter iterations (one per run length, its
+        address taken once), created ahead of a timed call."""
+        n = int(n_iter)
+        if n not in self._run_out:
+            arr = np.empty((n, 3), dtype=np.float64)
+            self._run_out[n] = (arr, arr.ctypes.data)
+        return self._run_out[n]
 
     def set_run_snapshots(self, every, slot0=0):
         """Snapshot u inside every later mcmc_run after each iteration k with k % every == 0

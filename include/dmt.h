@@ -85,6 +85,8 @@ enum { DMT_K_DRAW = 0, DMT_K_ACCEPT = 1, DMT_K_PATHLL = 2, DMT_K_RECOMPUTE = 3,
  *             FHN:    1/eps, s, gamma, beta, then the raw eps, σ at 4, 5
  *                     (σ also goes in sigma)
  *             Lorenz: s, r, beta
+ *   14      gstale 1.0: u°'s guiding term no longer matches the record's auxiliary law
+ *                  (set_proposal_law with critical_change = false; see DMT_LAW_GSTALE)
  *   15      auxtd  1.0: the auxiliary drift varies within the segment — step i uses
  *                  B̃(t_i), β̃(t_i) of the per-point table of dmt_upload_aux (Bt/beta unused)
  *   [16,25) sigma  d×m row-major (constant diffusion coefficient)
@@ -114,6 +116,10 @@ enum { DMT_K_DRAW = 0, DMT_K_ACCEPT = 1, DMT_K_PATHLL = 2, DMT_K_RECOMPUTE = 3,
 #define DMT_LAW_ANCHOR 60
 #define DMT_LAW_AUXLIN 63
 #define DMT_LAW_AUXTD 15
+/* 1.0: u°'s guiding term of this record is stale — set_proposal_law!(…, false) left it although
+ * the record's auxiliary law changed; the default (critical_change omitted) treats the record as
+ * critical until the guiding term is recomputed.  Kept by libdmt; uploads write 0. */
+#define DMT_LAW_GSTALE 14
 
 /* Parameter names of dmt_set_proposal_law (DiffusionDefinition's parameter order):
  *   FHN    (eps, s, gamma, beta, sigma), docs/src/tutorials/preamble.md:77

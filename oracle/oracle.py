@@ -36,6 +36,7 @@ LAW_STRIDE = 64
 L_C0 = 49
 L_BT, L_TRACE, L_A, L_SIGMA, L_ANCHOR, L_AUXLIN = 31, 50, 25, 16, 60, 63
 L_AUXTD = 15   # time-dependent auxiliary law flag (include/dmt.h DMT_LAW_AUXTD)
+L_GSTALE = 14  # u°'s guiding term left stale by critical_change = false (DMT_LAW_GSTALE)
 MODEL_OU = 0
 
 
@@ -137,6 +138,8 @@ def _load():
     lib.orc_rng_log.restype = d_
     lib.orc_bm_log.argtypes = [d_]
     lib.orc_bm_log.restype = d_
+    lib.orc_bm_logf.argtypes = [C.c_float]
+    lib.orc_bm_logf.restype = C.c_float
     lib.orc_philox_raw.argtypes = [u64, P, P]
     lib.orc_philox_raw.restype = None
     return lib
@@ -759,18 +762,29 @@ class OracleEnsemble:
                     dst = tab_p[g].rec
                     old = dst[L_A:L_TRACE + 1].copy()
                     c0 = dst[L_C0]
+                    old_stale = dst[L_GSTALE] != 0.0
                     dst[:] = tab_u[g].rec
                     dst[L_C0] = c0
                     eq = dst[L_A:L_TRACE + 1].copy()  # after equalize_law_params!, before θ°
                     set_law_params(self.model, self.d, dst, params)
                     used = kind == (1 if (not bk.term and g == bk.g1) else 0)
                     new = dst[L_A:L_TRACE + 1].copy()
-                    if critical_change is not None and not critical_change:
-                        new = eq
                     new[L_C0 - L_A] = old[L_C0 - L_A]
-                    if used and (critical_change is True or
-                                 old.view(np.uint64).tolist() != new.view(np.uint64).tolist()):
+                    eq[L_C0 - L_A] = old[L_C0 - L_A]
+                    same = lambda x, y: x.view(np.uint64).tolist() == y.view(np.uint64).tolist()  # noqa: E731
+                    aux_changed, eq_changed = not same(old, new), not same(old, eq)
+                    # u°'s stale-guiding-term bit (libdmt DMT_LAW_GSTALE, k_set_prop_law)
+                    if used and critical_change is True:
                         crit[j] = True
+                        dst[L_GSTALE] = 0.0
+                    elif used and critical_change is not None and not critical_change:
+                        crit[j] |= eq_changed
+                        dst[L_GSTALE] = 1.0 if (old_stale or aux_changed) and not eq_changed else 0.0
+                    elif used:
+                        crit[j] |= aux_changed or old_stale
+                        dst[L_GSTALE] = 0.0
+                    else:
+                        dst[L_GSTALE] = 1.0 if old_stale else 0.0
         for j in np.flatnonzero(crit):
             self.recompute_guiding_term(layout, b0 + j, b0 + j + 1, unit=1)
         ok = self.recompute_path(layout, b0, b1, skip=skip, want_success=True)

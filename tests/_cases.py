@@ -165,8 +165,8 @@ def ou_ragged_model():
     return _OU([[1.0, 0.3], [-0.3, 0.8]], [0.1, -0.2], [[0.2], [0.5]])
 
 
-def ragged_pair(seed=11, hist_len=8, mapping=L.MAP_AUTO, model=None):
-    case = ragged_case(model=model)
+def ragged_pair(seed=11, hist_len=8, mapping=L.MAP_AUTO, model=None, prec=L.F64):
+    case = ragged_case(model=model, prec=prec)
     m = case["model"]
     dev = dmt.Ensemble(m.kind, m.d, m.m, case["n_points"], precision=case["prec"], seed=seed,
                        mapping=mapping)

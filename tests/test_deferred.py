@@ -285,7 +285,25 @@ def test_service_switch_from_the_api_and_self_disable():
     assert off.service_stats()["starts"] == 0 and idle0.service_stats()["starts"] == 0
     st = short.service_stats()
     assert st["off"] == 1 and st["posts"] < 30, st
+    # re-enabled from the API, the service starts again (the self-disable rule counts from the
+    # enable): iterations 31-40 without host pauses, equal to the default service's
+    short.set_service(True, 2.0)
+    r2 = [_loop_from(e, lay, nb, 31, 10) for e in (svc, short)]
+    assert np.array_equal(r2[0], r2[1])
+    _same_state(svc, short, lay, nb, 40)
+    st2 = short.service_stats()
+    assert st2["off"] == 0 and st2["starts"] > st["starts"] and st2["posts"] > st["posts"], (st, st2)
     with pytest.raises(Exception):
         svc.set_service(True, -1.0)
     for e in (svc, off, idle0, short):
         e.close()
+
+
+def _loop_from(e, lay, nb, i0, iters):
+    """_loop_gaps continued: iterations i0 … i0 + iters - 1, each fetched, no pauses."""
+    res = []
+    for i in range(i0, i0 + iters):
+        e.draw_proposal(lay, 0, nb, salt=L.RNG_AUTO, want_success="lazy")
+        e.accept_reject(lay, 0, nb, i, salt=L.RNG_AUTO)
+        res.append(e.fetch_ll(lay, 0, nb, i))
+    return np.array(res)

@@ -98,12 +98,18 @@ def test_c5_lorenz_mixed_unit_sigma_bit_exact(mapping):
     cs.assert_paths_equal(dev, ora)
 
 
-@pytest.mark.parametrize("mapping", MAPPINGS)
-def test_ragged_blocking_layouts_bit_exact(mapping):
+# fp32 on the lane mapping: the lane-packet path planes on multi-segment,
+# unaligned recordings (the FAST=false packet paths, set_obs, find_W_for_X)
+RAGGED_CASES = [pytest.param(L.MAP_LANE, L.F64, id="lane"), pytest.param(L.MAP_WAVE, L.F64, id="wave"),
+                pytest.param(L.MAP_LANE, L.F32, id="lane-f32")]
+
+
+@pytest.mark.parametrize("mapping,prec", RAGGED_CASES)
+def test_ragged_blocking_layouts_bit_exact(mapping, prec):
     """Multi-segment recordings, non-terminal blocks with P_last laws, two alternating block
     layouts aliasing the same SamplingPair (src/block.jl:66-72), swaps, loglikhd of both units,
     a proposal law and recompute_path! (src/biblock.jl:334-344)."""
-    case, dev, ora, ((A, nA), (B, nB)) = cs.ragged_pair(mapping=mapping)
+    case, dev, ora, ((A, nA), (B, nB)) = cs.ragged_pair(mapping=mapping, prec=prec)
     rng = np.random.default_rng(9)
     S = case["t"].size - sum(case["nsegs"])
     for e in (dev, ora):
@@ -634,15 +640,54 @@ def test_find_W_for_X_bit_exact(cfg, mapping):
     cs.assert_ll_equal(dev, ora, lay, nb)
 
 
-@pytest.mark.parametrize("mapping", MAPPINGS)
-def test_find_W_for_X_blocking_layouts(mapping):
+@pytest.mark.parametrize("mapping,prec", RAGGED_CASES)
+def test_find_W_for_X_blocking_layouts(mapping, prec):
     """Ragged multi-segment FHN with P_last laws: invsolve uses PPb on the last segment of
-    non-terminal blocks (src/block.jl:118-124)."""
-    case, dev, ora, ids = cs.ragged_pair(mapping=mapping)
+    non-terminal blocks (src/block.jl:118-124); set_obs! before it (fp32 lane packets too)."""
+    case, dev, ora, ids = cs.ragged_pair(mapping=mapping, prec=prec)
+    for e in (dev, ora):
+        e.upload_obs(case["Hobs"], case["Fobs"], case["cobs"])
     for lid, nb in ids:
         for e in (dev, ora):
+            e.set_obs(lid, 0, nb)
             e.find_W_for_X(lid, 0, nb)
         cs.assert_paths_equal(dev, ora)
+        for kind in (L.LAW_PP, L.LAW_PPB):
+            for a_, b_ in zip(dev.download_law(L.U, kind), ora.download_law(L.U, kind)):
+                assert np.array_equal(a_, b_)
+
+
+@pytest.mark.parametrize("env", [{"DMT_PATH_PACKETS": "0"}, {"DMT_LANE_PAIR": "1"}],
+                         ids=["rows", "lane-pairs"])
+def test_fp32_lane_variants_bit_identical(env):
+    """fp32 lane ensembles: the row layout (DMT_PATH_PACKETS=0) and the lane-pair packet kernel
+    (DMT_LANE_PAIR=1, k_block_pk_pair) against the default packet kernel on the ragged
+    multi-segment case — device-RNG draws, accepts, loglikhd and the downloaded paths, bit for
+    bit."""
+    import diffusionmcmctools_amd as d
+
+    def build():
+        case = cs.ragged_case(prec=L.F32)
+        m = case["model"]
+        e = d.Ensemble(m.kind, m.d, m.m, case["n_points"], precision=L.F32, seed=4,
+                       mapping=L.MAP_LANE)
+        cs.load_ragged(e, case)
+        lay = e.create_layout([2, 3, 2], [0, 2, 0, 2, 4, 0, 3], [1, 3, 1, 3, 5, 2, 4],
+                              [0, 1, 0, 0, 1, 0, 1], np.full(7, 0.6), 6)
+        return e, lay, 7
+    (e0, lay, nb), (e1, _, _) = _env_ensembles(build, env)
+    for e in (e0, e1):
+        e.loglikhd(lay, L.U, 0, nb)
+    for i in range(1, 6):
+        acc = []
+        for e in (e0, e1):
+            e.draw_proposal(lay, 0, nb, iter=i, salt=2)
+            acc.append(e.accept_reject(lay, 0, nb, i, salt=2, want_acc=True))
+        assert np.array_equal(acc[0], acc[1]), i
+        cs.assert_paths_equal(e0, e1)
+        cs.assert_ll_equal(e0, e1, lay, nb)
+    for e in (e0, e1):
+        e.close()
 
 
 @pytest.mark.parametrize("mapping", MAPPINGS)

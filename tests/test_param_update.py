@@ -114,6 +114,33 @@ def test_oracle_critical_change_false_keeps_the_guiding_term():
     assert crit.all()
 
 
+def test_oracle_false_then_default_recomputes_the_stale_guiding_term():
+    """critical_change = false leaves u°'s guiding term stale where θ° moved the
+    auxiliary law; a later call with the default and an unchanged θ° must still treat those
+    blocks as critical (DMT_LAW_GSTALE), after which u°'s guiding term is the one a `true` call
+    gives — and the bit is clear again."""
+    case = cs.ragged_case()
+    m = case["model"]
+    made = []
+    for seq in ((False, None), (True,)):
+        ora = orc.OracleEnsemble(m.kind, m.d, m.m, case["n_points"], prec=case["prec"], seed=1)
+        cs.load_ragged(ora, case)
+        ora.upload_obs(case["Hobs"], case["Fobs"], case["cobs"])
+        lay, R = _whole_recording_layout(ora, case)
+        for k, cc in enumerate(seq):
+            ok, crit = ora.set_proposal_law(lay, 0, R, _fhn_params(THETA1), critical_change=cc)
+            if seq[0] is False:
+                laws = ora.download_law(L.UPROP, L.LAW_PP)[2]
+                if k == 0:
+                    assert not crit.any() and (laws[:, L.LAW_GSTALE] == 1.0).any()
+                else:
+                    assert crit.all() and (laws[:, L.LAW_GSTALE] == 0.0).all()
+        made.append([ora.download_law(L.UPROP, kind) for kind in (L.LAW_PP, L.LAW_PPB)])
+    for a_, b_ in zip(made[0], made[1]):
+        for x, y in zip(a_, b_):
+            assert np.array_equal(x, y)
+
+
 def test_updt_obs_is_refused():
     """Observation parameters (updt_obs) are not device state: a ParamNamesBlock that would
     update them raises instead of being silently ignored."""
@@ -204,12 +231,14 @@ def test_critical_change_false_bit_exact(mapping):
     for e in (dev, ora):
         e.recompute_guiding_term(lid, 0, nb, unit=L.U)
         e.loglikhd(lid, L.U, 0, nb)
-    for step, cc in enumerate((False, True, "swap", False)):
+    # False, then the default with θ° unchanged (the stale-guiding-term bit), True,
+    # a parameter swap, False again
+    for step, cc in enumerate((False, None, True, "swap", False)):
         if cc == "swap":
             for e in (dev, ora):
                 e.swap(lid, L.SWAP_XX | L.SWAP_PP | L.SWAP_LL, 0, nb)
             continue
-        th = THETA1 if step < 2 else THETA0
+        th = THETA1 if step < 3 else THETA0
         okd, crd = dev.set_proposal_law(lid, 0, nb, _fhn_params(th), critical_change=cc)
         oko, cro = ora.set_proposal_law(lid, 0, nb, _fhn_params(th), critical_change=cc)
         assert np.array_equal(okd, oko) and np.array_equal(crd, cro), step

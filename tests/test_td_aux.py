@@ -611,3 +611,37 @@ def _td_pair_dev_only(hist_len):
                                    hist_len=hist_len)
     return case, (dev,), ids
 
+
+
+@pytest.mark.gpu
+def test_auxtd2_needs_the_a_columns():
+    """a law record with DMT_LAW_AUXTD = 2 (ã(t) from the table) and a table given
+    with only the B̃, β̃ columns is refused — at the table upload, at the law upload, and at the
+    first draw when no table was given at all — instead of running with ã(t) = 0."""
+    case = cs.ragged_case(model=cs.ou_ragged_model())
+    m = case["model"]
+    nb_cols = m.d * m.d + m.d
+    G = int(sum(case["nsegs"]))
+
+    def fresh():
+        e = dmt.Ensemble(m.kind, m.d, m.m, case["n_points"], precision=L.F64, seed=11)
+        cs.load_ragged(e, case)
+        e.upload_obs(case["Hobs"], case["Fobs"], case["cobs"])
+        return e
+    e = fresh()
+    _flag_segments(e, (L.LAW_PP,), np.arange(0, G, 2), 2.0)
+    with pytest.raises(dmt.DMTError):
+        e.upload_aux(L.LAW_PP, np.zeros((e.P, nb_cols)))
+    e.close()
+    e = fresh()
+    e.upload_aux(L.LAW_PP, np.zeros((e.P, nb_cols)))
+    with pytest.raises(dmt.DMTError):
+        _flag_segments(e, (L.LAW_PP,), np.arange(0, G, 2), 2.0)
+    e.close()
+    e = fresh()
+    _flag_segments(e, (L.LAW_PP,), np.arange(0, G, 2), 2.0)
+    lay = e.create_layout([2, 3, 2], [0, 2, 0, 2, 4, 0, 3], [1, 3, 1, 3, 5, 2, 4],
+                          [0, 1, 0, 0, 1, 0, 1], np.full(7, 0.5), 2)
+    with pytest.raises(dmt.DMTError):
+        e.draw_proposal(lay, 0, 7, iter=1, salt=3)
+    e.close()
