@@ -56,13 +56,22 @@ struct FHN {
   static constexpr int D = 2, M = 1, NTH = 4;
   static constexpr bool kLinear = false;
   static constexpr int kNoiseCoord = 1;  // hypoelliptic: the noise enters coordinate 1 only
-  // theta: 1/eps, s, gamma, beta
+  // theta: 1/eps, s, gamma, beta.  Canonical (round 5): t0 = fma(−y², y, y) +
+  // (s − v), b0 = t0·ε⁻¹ — four dependent operations from y instead of six — and the Euler step's
+  // guided drift bg0 = fma(t0, ε⁻¹, u0) (guided()), one more fused: the serial recursion's
+  // chain is y² → fma → + (s − v) → fma(t0, ε⁻¹, u0) → fma(bg0, dt, x0 + σdW0)
+  __device__ __forceinline__ static T t0(const T* th, const T* x) {
+    const T y = x[0], v = x[1];
+    return dfma(-(y * y), y, y) + (th[1] - v);
+  }
   __device__ __forceinline__ static void drift(const T* th, const T* x, T* b) {
-    T y = x[0], v = x[1];
-    T y3 = (y * y) * y;
-    T t0 = ((y - y3) - v) + th[1];
-    b[0] = t0 * th[0];
+    const T y = x[0], v = x[1];
+    b[0] = t0(th, x) * th[0];
     b[1] = dfma(th[2], y, th[3] - v);
+  }
+  // b_p + u_p of the Euler step (b from drift())
+  __device__ __forceinline__ static T guided(const T* th, const T* x, const T* b, T u, int p) {
+    return p == 0 ? dfma(t0(th, x), th[0], u) : b[p] + u;
   }
 };
 
@@ -76,6 +85,9 @@ struct Lorenz {
     b[0] = th[0] * (x[1] - x[0]);
     b[1] = dfma(x[0], th[1] - x[2], -x[1]);
     b[2] = dfma(x[0], x[1], -(th[2] * x[2]));
+  }
+  __device__ __forceinline__ static T guided(const T*, const T*, const T* b, T u, int p) {
+    return b[p] + u;
   }
 };
 
@@ -272,8 +284,8 @@ __device__ __forceinline__ void sigma_dw(const Law<Mdl, T>& L, const T* dW, T* s
 //   u_a = c_a - Σ_b M_ab x_b ;  bg = u (linear drift) or b(x) + u ;  x'_a = fma(bg_a, dt, x_a + sdW_a)
 // b is the model drift at x (ignored for a linear drift, which M, c already contain).
 template <class Mdl, class T>
-__device__ __forceinline__ void euler_step(const T* Mg, const T* cg, const T* b, T dt,
-                                           const T* sdW, T* x) {
+__device__ __forceinline__ void euler_step(const T* th, const T* Mg, const T* cg, const T* b,
+                                           T dt, const T* sdW, T* x) {
   constexpr int D = Mdl::D;
   T xn[D];
 #pragma unroll
@@ -281,7 +293,9 @@ __device__ __forceinline__ void euler_step(const T* Mg, const T* cg, const T* b,
     T u = cg[p];
 #pragma unroll
     for (int q = 0; q < D; ++q) u = dfma(-Mg[p * D + q], x[q], u);
-    const T bg = Mdl::kLinear ? u : (b[p] + u);
+    T bg;
+    if constexpr (Mdl::kLinear) bg = u;
+    else bg = Mdl::guided(th, x, b, u, p);
     xn[p] = dfma(bg, dt, x[p] + sdW[p]);
   }
 #pragma unroll
@@ -353,7 +367,9 @@ __device__ __forceinline__ void inv_step(const Law<Mdl, T>& L, const T* siginv, 
     T u = cg[p];
 #pragma unroll
     for (int q = 0; q < D; ++q) u = dfma(-Mg[p * D + q], x[q], u);
-    const T bg = Mdl::kLinear ? u : (b[p] + u);
+    T bg;
+    if constexpr (Mdl::kLinear) bg = u;
+    else bg = Mdl::guided(L.th, x, b, u, p);
     r[p] = dfma(-bg, dt, xn[p] - x[p]);
   }
   if constexpr (Mdl::kNoiseCoord >= 0) {

@@ -266,7 +266,7 @@ __device__ __forceinline__ bool run_segment(const Law<Mdl, T>& L, const T* __res
       sigma_dw<Mdl, T>(L, dW, sdW);
       guide_coeffs<Mdl, T>(L, Hi, Fi, Mg, cg);
     }
-    euler_step<Mdl, T>(Mg, cg, b, dt, sdW, x);
+    euler_step<Mdl, T>(L.th, Mg, cg, b, dt, sdW, x);
 #pragma unroll
     for (int p = 0; p < D; ++p) {
       if (PKT && pj >= 0) pkx[pj][p] = x[p];
@@ -648,7 +648,7 @@ __device__ __forceinline__ bool run_segment_pk(const Law<Mdl, T>& L, const T* __
       sigma_dw<Mdl, T>(L, dW, sdW);
       guide_coeffs<Mdl, T>(L, Hi, Fi, Mg, cg);
     }
-    euler_step<Mdl, T>(Mg, cg, b, dt, sdW, x);
+    euler_step<Mdl, T>(L.th, Mg, cg, b, dt, sdW, x);
     tcur = tn;
     return (MODE == MODE_RECOMPUTE && i >= nst - ll_skip) ? (T)0 : G * dt;
   };
@@ -1244,7 +1244,7 @@ __global__ __launch_bounds__(128, DMT_PS_MINW) void k_block_ps(const BlockArgs<T
             T xn[D];
 #pragma unroll
             for (int p = 0; p < D; ++p) xn[p] = x[p];
-            euler_step<Mdl, T>(Mg, cg, b, dt, sdW, xn);
+            euler_step<Mdl, T>(LA.th, Mg, cg, b, dt, sdW, xn);
             if (v) {
               if (Xcd) {
 #pragma unroll
@@ -1526,7 +1526,7 @@ __global__ __launch_bounds__(128) void k_block_wave(const BlockArgs<T> a) {
         const bool mine = lane == s;
 #pragma unroll
         for (int p = 0; p < D; ++p) xc[p] = mine ? x[p] : xc[p];
-        euler_step<Mdl, T>(q + 1 + D, q + 1 + D + D * D, b_, q[0], q + 1, x);
+        euler_step<Mdl, T>(L.th, q + 1 + D, q + 1 + D + D * D, b_, q[0], q + 1, x);
       }
 #pragma unroll
       for (int p = 0; p < D; ++p) sh.xcap[k & 1][lane][p] = xc[p];

@@ -42,7 +42,8 @@
  *       with (Theta mu)_a = Theta_a0*mu_0 ; fma(Theta_ac, mu_c, .)
  *     otherwise:                              M_ab = aH_ab ; c_a = aF_a
  *   u_a     = c_a ; u_a = fma(-M_ab, x_b, u_a)       for b = 0..d-1
- *   bg_a    = u_a (linear drift)  or  b_a + u_a      (= b + a(F - Hx) in exact arithmetic)
+ *   bg_a    = u_a (linear drift)  or  b_a + u_a      (= b + a(F - Hx) in exact arithmetic);
+ *             FHN's bg_0 = fma(t0, 1/eps, u_0) with b_0 = t0·(1/eps) (orc_guided)
  *   bt_a    = Bt_a-row · x + beta_a  (bt_a = beta_a ; fma(Bt_ab, x_b, bt_a))
  *   db_a    = b_a - bt_a
  *   G       = db_0*r_0 ; G = fma(db_a, r_a, G)
@@ -101,6 +102,20 @@ static inline int pidx(int d, int a, int b) {
     return a * d - (a * (a - 1)) / 2 + (b - a);
 }
 
+/* FHN's t0 = fma(-y², y, y) + (s - v) (libdmt dmt_device.h FHN::t0). */
+static inline REAL fhn_t0(const REAL* th, const REAL* x) {
+    const REAL y = x[0], v = x[1];
+    return FMA(-(y * y), y, y) + (th[1] - v);
+}
+/* b_p + u_p of the Euler step (libdmt FHN/Lorenz::guided): FHN's first coordinate fuses its
+ * 1/eps scaling, bg0 = fma(t0, 1/eps, u0); every other coordinate b_p + u_p; OU: u_p. */
+static inline REAL orc_guided(int model, const REAL* th, const REAL* x, const REAL* b, REAL u,
+                              int p) {
+    if (model == ORC_OU) return u;
+    if (model == ORC_FHN && p == 0) return FMA(fhn_t0(th, x), th[0], u);
+    return b[p] + u;
+}
+
 /* Model drifts (DiffusionDefinition models). */
 static void orc_drift(int model, int d, const REAL* th, const REAL* x, REAL* b) {
     if (model == ORC_OU) {
@@ -113,11 +128,10 @@ static void orc_drift(int model, int d, const REAL* th, const REAL* x, REAL* b) 
             b[a] = acc;
         }
     } else if (model == ORC_FHN) {
-        /* theta: 1/eps, s, gamma, beta.  dY = (Y - Y^3 - X + s)/eps, dX = (gamma Y - X + beta) */
+        /* theta: 1/eps, s, gamma, beta.  dY = (Y - Y^3 - X + s)/eps, dX = (gamma Y - X + beta);
+         * canonical (round 5): t0 = fma(-y², y, y) + (s - v), b0 = t0·(1/eps) */
         REAL y = x[0], v = x[1];
-        REAL y3 = (y * y) * y;
-        REAL t0 = ((y - y3) - v) + th[1];
-        b[0] = t0 * th[0];
+        b[0] = fhn_t0(th, x) * th[0];
         b[1] = FMA(th[2], y, th[3] - v);
     } else { /* Lorenz-63: theta: s, r, beta */
         b[0] = th[0] * (x[1] - x[0]);
@@ -487,7 +501,7 @@ int SFX(orc_solve_segment)(int model, int d, int m, const double* law, int npts,
         for (int p = 0; p < d; ++p) {
             REAL u = cg[p];
             for (int q = 0; q < d; ++q) u = FMA(-Mg[p * d + q], x[q], u);
-            REAL bg = (model == ORC_OU) ? u : (b[p] + u);
+            REAL bg = orc_guided(model, th, x, b, u, p);
             REAL sdw = sg[p * m + 0] * dW[0];
             for (int k = 1; k < m; ++k) sdw = FMA(sg[p * m + k], dW[k], sdw);
             if (unit) sdw = dW[p];
@@ -527,7 +541,7 @@ void SFX(orc_invsolve_segment)(int model, int d, int m, const double* law, int n
         for (int p = 0; p < d; ++p) {
             REAL u = cg[p];
             for (int q = 0; q < d; ++q) u = FMA(-Mg[p * d + q], x[q], u);
-            REAL bg = (model == ORC_OU) ? u : (b[p] + u);
+            REAL bg = orc_guided(model, th, x, b, u, p);
             r[p] = FMA(-bg, dt, xn[p] - x[p]);
         }
         REAL* dW = W + (size_t)(i + 1) * m;

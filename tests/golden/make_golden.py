@@ -14,7 +14,8 @@ fixtures pin instead:
                        final paths).
 The last two freeze the canonical arithmetic: any later change to the kernels or
 the oracle that alters a bit shows up against them.  Inputs are stored in full, so tests never
-regenerate them."""
+regenerate them.  Round 5 changed the FHN drift's canonical order: the ragged
+trace's outputs were refreshed from its stored inputs (``--refresh-ragged-outputs``)."""
 from __future__ import annotations
 
 import math
@@ -139,6 +140,55 @@ def ragged_trace():
         arrays[f"lay{k}_rho"] = np.array(lay["rho"])
     np.savez_compressed(os.path.join(OUT, "ragged_trace.npz"), **arrays)
 
+
+def refresh_ragged_outputs():
+    """Round 5 (FHN drift reassociated): keep ragged_trace.npz's stored INPUTS and
+    recompute its outputs (decisions, ll, ll°, fetch_ll, final paths) with the current oracle —
+    the replay of test_golden.replay_ragged, recording instead of asserting."""
+    import oracle as orc
+    from diffusionmcmctools_amd import _lib as L
+    path = os.path.join(OUT, "ragged_trace.npz")
+    g = dict(np.load(path))
+    npts, nested, i = g["n_points"], [], 0
+    for K in g["nsegs"]:
+        nested.append([int(x) for x in npts[i:i + K]])
+        i += K
+    ens = orc.OracleEnsemble(1, 2, 1, nested, prec=0, seed=11)
+    ens.upload_grid(g["t"])
+    ens.upload_law(L.U, L.LAW_PP, H=g["H"], F=g["F"], laws=g["laws"])
+    ens.upload_law(L.U, L.LAW_PPB, H=g["Hb"], F=g["Fb"], laws=g["lawsb"])
+    ens.set_paths(L.U, X=g["X0"])
+    ens.draw_unit(L.U, Z=g["Z0"], iter=0, salt=1)
+    ens.set_paths(L.UPROP, X=ens.download_paths(L.U, 0), W=ens.download_paths(L.U, 1))
+    iters = g["Zs"].shape[0]
+    ids = []
+    for k in ("A", "B"):
+        nb = int(g[f"lay{k}_n_blocks"].sum())
+        ids.append((ens.create_layout(g[f"lay{k}_n_blocks"], g[f"lay{k}_seg_first"],
+                                      g[f"lay{k}_seg_last"], g[f"lay{k}_last"],
+                                      np.full(nb, float(g[f"lay{k}_rho"])), iters), nb))
+    for lid, nb in ids:
+        ens.loglikhd(lid, L.U, 0, nb)
+    acc, ll, llp, fetch = [], [], [], []
+    for it in range(1, iters + 1):
+        lid, nb = ids[(it - 1) % 2]
+        ens.draw_proposal(lid, 0, nb, Z=g["Zs"][it - 1], iter=it)
+        a = ens.accept_reject(lid, 0, nb, it, E=g["Es"][it - 1, :nb], want_acc=True)
+        pad = lambda v: np.concatenate([v, np.full(7 - nb, np.nan)])  # noqa: E731
+        acc.append(np.concatenate([a, np.zeros(7 - nb, bool)]))
+        ll.append(pad(ens.get_block_state(lid, L.BLK_LL, 0, nb)))
+        llp.append(pad(ens.get_block_state(lid, L.BLK_LLPROP, 0, nb)))
+        fetch.append(ens.fetch_ll(lid, 0, nb, it))
+    g.update(acc=np.array(acc), ll=np.array(ll), llp=np.array(llp),
+             fetch=np.array(fetch, dtype=np.float64),
+             X_final=ens.download_paths(L.U, 0), W_final=ens.download_paths(L.U, 1),
+             Xp_final=ens.download_paths(L.UPROP, 0), Wp_final=ens.download_paths(L.UPROP, 1))
+    np.savez_compressed(path, **g)
+
+
+if __name__ == "__main__" and "--refresh-ragged-outputs" in sys.argv:
+    refresh_ragged_outputs()
+    sys.exit(0)
 
 if __name__ == "__main__":
     philox_kat()
