@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--limiter", default="")
     ap.add_argument("--csv", nargs="+", required=True)
     ap.add_argument("--out", required=True)
+    ap.add_argument("--tree", help="tree.txt of the GPU session (the digest of the tree it ran)")
     a = ap.parse_args()
     disp = collections.defaultdict(dict)
     for f in a.csv:
@@ -87,7 +88,7 @@ def main():
     out["limiter"] = a.limiter
     out["note"] = ("issue roofline: frac = share of SIMD cycles in which a VALU instruction "
                    "issues (1.0 = the SIMD's VALU never idle)")
-    provenance.stamp(out)  # the source tree this profile measured
+    provenance.stamp(out, digest=provenance.read_digest(a.tree) if a.tree else None)  # the tree measured
     with open(a.out, "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out))

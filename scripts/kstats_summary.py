@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--units-per-launch", type=int, default=1)
     ap.add_argument("--command", default="")
     ap.add_argument("--out", required=True)
+    ap.add_argument("--tree", help="tree.txt of the GPU session (the digest of the tree it ran)")
     a = ap.parse_args()
     out = {"config": a.config, "kernel": a.kernel, "units_per_launch": a.units_per_launch,
            "command": a.command}
@@ -59,7 +60,7 @@ def main():
     else:
         raise SystemExit("--trace or --stats")
     out["avg_us_per_unit"] = out["avg_us"] / a.units_per_launch
-    provenance.stamp(out)  # the source tree this profile measured
+    provenance.stamp(out, digest=provenance.read_digest(a.tree) if a.tree else None)  # the tree measured
     with open(a.out, "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out))

@@ -43,6 +43,7 @@ def main():
                     help="iterations one dispatch runs (k_mcmc_scan: --steps of the bench); "
                          "bytes are reported per iteration, like bench.py's roofline")
     ap.add_argument("--out", required=True)
+    ap.add_argument("--tree", help="tree.txt of the GPU session (the digest of the tree it ran)")
     a = ap.parse_args()
     fk = per_kernel(a.fetch, "FETCH_SIZE", a.kernel)
     wk = per_kernel(a.write, "WRITE_SIZE", a.kernel)
@@ -68,7 +69,7 @@ def main():
            "traffic_bytes_per_launch": (f_b + w_b) * a.units_per_launch,
            "fetch_kib_raw_median": statistics.median(fk),
            "write_kib_raw_median": statistics.median(wk), "calibration": calib}
-    provenance.stamp(out)  # the source tree this profile measured
+    provenance.stamp(out, digest=provenance.read_digest(a.tree) if a.tree else None)  # the tree measured
     with open(a.out, "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out))

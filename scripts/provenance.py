@@ -39,8 +39,19 @@ def git_commit(root=ROOT):
         return None
 
 
-def stamp(out, root=ROOT):
-    """Add the provenance fields to a summary dict (in place) and return it."""
-    out["csrc_sha16"] = csrc_digest(root)
+def stamp(out, root=ROOT, digest=None):
+    """Add the provenance fields to a summary dict (in place) and return it.  `digest`: the
+    digest the GPU session recorded for the tree it ran (its tree.txt); default: this tree's."""
+    out["csrc_sha16"] = digest or csrc_digest(root)
     out["git_commit"] = git_commit(root)
     return out
+
+
+def read_digest(path):
+    """The digest a GPU session wrote with `python scripts/provenance.py > <dir>/tree.txt`."""
+    with open(path) as f:
+        return f.read().split()[0]
+
+
+if __name__ == "__main__":
+    print(csrc_digest())
