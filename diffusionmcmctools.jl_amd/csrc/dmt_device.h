@@ -536,6 +536,25 @@ __device__ __forceinline__ double rng_log(double u) {
     const double de = (double)e;
     return __builtin_fma(de, RNG_LN2_HI, __builtin_fma(de, RNG_LN2_LO, lm));
 }
+__device__ __forceinline__ float rng_logf(float u) {
+    int e;
+    float m = __builtin_frexpf(u, &e);
+    const int lo = m < RNGF_SQRT_HALF;
+    m = lo ? m * 2.0f : m;
+    e = lo ? e - 1 : e;
+    const float f = m - 1.0f;
+    const float s = f / (2.0f + f);
+    const float z = s * s;
+    float p = RNGF_P5;
+    p = __builtin_fmaf(p, z, RNGF_P4); p = __builtin_fmaf(p, z, RNGF_P3); p = __builtin_fmaf(p, z, RNGF_P2);
+    p = __builtin_fmaf(p, z, RNGF_P1);
+    const float lm = __builtin_fmaf(s, z * p, 2.0f * s);
+    const float de = (float)e;
+    return __builtin_fmaf(de, RNGF_LN2_HI, __builtin_fmaf(de, RNGF_LN2_LO, lm));
+}
+// (round 5: a table-driven, division-free binary32 log in bm_log's form measured 17 % slower in
+// the C5 packet kernel — 1 682–1 710 vs 1 437–1 442 µs per draw, profiles/r05e: the per-lane
+// table reads are memory operations in a kernel that waits on its loads — and was not kept)
 __device__ __forceinline__ void rng_sincospif(float x, float* sn, float* cs) {
     const float n = __builtin_rintf(2.0f * x);
     const float r = __builtin_fmaf(-0.5f, n, x);
@@ -565,7 +584,6 @@ __device__ __forceinline__ void rng_sincospif(float x, float* sn, float* cs) {
 #include "dmt_bm_tables.inc"
 __constant__ double kBmLog[128][2] = DMT_BM_LOG_TABLE;
 __constant__ double kBmSc[65][2] = DMT_BM_SC_TABLE;
-__constant__ float kBmLogF[128][2] = DMT_BM_LOGF_TABLE;
 
 /* log(u), u in [2^-53, 1]: u = m·2^e, m in [1, 2), j = top 7 mantissa bits; j < 64:
  * r = fma(m, c_j, -1), log u = e·ln2 + (L_j + log1p(r)); j >= 64: the same with e + 1 (c_j, L_j
@@ -586,25 +604,6 @@ __device__ __forceinline__ double bm_log(double u) {
   const double lm = Lj + __builtin_fma(r2, q, r);
   const double de = (double)e;
   return __builtin_fma(de, RNG_LN2_HI, __builtin_fma(de, RNG_LN2_LO, lm));
-}
-/* fp32 log(u), u in [2^-24, 1] (round 5; replaces rng_logf's atanh form, whose correctly
- * rounded division was ≈ a third of the fp32 Box–Muller): bm_log's split in binary32 —
- * j = the top 7 mantissa bits, r = fma(m, c_j, -1) (|r| < 2^-7), log u = e'·ln2 + (L_j +
- * log1p(r)), log1p(r) = r + r²·(-1/2 + r·(1/3 - r/4)) (truncation < 2^-28 relative); no
- * division, no frexp.  Restated in oracle/dmt_oracle.c (bm_logf), tables of
- * scripts/gen_bm_tables.py. */
-__device__ __forceinline__ float bm_logf(float u) {
-  const uint32_t b = __builtin_bit_cast(uint32_t, u);
-  const int j = (int)((b >> 16) & 0x7fu);
-  const int e = (int)((b >> 23) & 0xffu) - 127 + (j >> 6);
-  const float m = __builtin_bit_cast(float, (b & 0x007FFFFFu) | 0x3F800000u);
-  const float cj = kBmLogF[j][0], Lj = kBmLogF[j][1];
-  const float r = __builtin_fmaf(m, cj, -1.0f);
-  float q = __builtin_fmaf(DMT_BM_QF2, r, DMT_BM_QF1);
-  q = __builtin_fmaf(q, r, DMT_BM_QF0);
-  const float lm = Lj + __builtin_fmaf(r * r, q, r);
-  const float de = (float)e;
-  return __builtin_fmaf(de, RNGF_LN2_HI, __builtin_fmaf(de, RNGF_LN2_LO, lm));
 }
 /* sin(πx), cos(πx), x in [0, 2]: n = rint(32x), r = x - n/32 (exact), angle addition with
  * (S_n, C_n) = (sin, cos)(πn/32) from the table, sin(πr) = r·SP(r²), cos(πr) = fma(r², CP(r²), 1). */
@@ -639,7 +638,7 @@ __device__ __forceinline__ void normal_pair(U4 o, double& z0, double& z1) {
 __device__ __forceinline__ void normal_pair(U4 o, float& z0, float& z1) {
   float u1 = (float)((o.x >> 8) + 1u) * 0x1p-24f;
   float u2 = (float)(o.z >> 8) * 0x1p-24f;
-  float rad = sqrtf(-2.0f * bm_logf(u1));
+  float rad = sqrtf(-2.0f * rng_logf(u1));
   float s, c;
   rng_sincospif(2.0f * u2, &s, &c);
   z0 = rad * c;

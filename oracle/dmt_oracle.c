@@ -762,6 +762,22 @@ static inline double rng_log(double u) {
     const double de = (double)e;
     return fma(de, RNG_LN2_HI, fma(de, RNG_LN2_LO, lm));
 }
+static inline float rng_logf(float u) {
+    int e;
+    float m = frexpf(u, &e);
+    const int lo = m < RNGF_SQRT_HALF;
+    m = lo ? m * 2.0f : m;
+    e = lo ? e - 1 : e;
+    const float f = m - 1.0f;
+    const float s = f / (2.0f + f);
+    const float z = s * s;
+    float p = RNGF_P5;
+    p = fmaf(p, z, RNGF_P4); p = fmaf(p, z, RNGF_P3); p = fmaf(p, z, RNGF_P2);
+    p = fmaf(p, z, RNGF_P1);
+    const float lm = fmaf(s, z * p, 2.0f * s);
+    const float de = (float)e;
+    return fmaf(de, RNGF_LN2_HI, fmaf(de, RNGF_LN2_LO, lm));
+}
 static inline void rng_sincospif(float x, float* sn, float* cs) {
     const float n = rintf(2.0f * x);
     const float r = fmaf(-0.5f, n, x);
@@ -779,27 +795,6 @@ static inline void rng_sincospif(float x, float* sn, float* cs) {
 }
 
 #include "bm_tables.inc"
-#if !IS_F64
-/* fp32 Box–Muller log (libdmt dmt_device.h bm_logf, DESIGN.md §3 RNG; round 5): bm_log's split
- * in binary32 with the float table of scripts/gen_bm_tables.py, the same operations in the same
- * order (no division). */
-static const float bm_logf_tab[128][2] = DMT_BM_LOGF_TABLE;
-static inline float bm_logf(float u) {
-    uint32_t b;
-    memcpy(&b, &u, 4);
-    const int j = (int)((b >> 16) & 0x7fu);
-    const int e = (int)((b >> 23) & 0xffu) - 127 + (j >> 6);
-    const uint32_t mb = (b & 0x007FFFFFu) | 0x3F800000u;
-    float m;
-    memcpy(&m, &mb, 4);
-    const float r = fmaf(m, bm_logf_tab[j][0], -1.0f);
-    float q = fmaf(DMT_BM_QF2, r, DMT_BM_QF1);
-    q = fmaf(q, r, DMT_BM_QF0);
-    const float lm = bm_logf_tab[j][1] + fmaf(r * r, q, r);
-    const float de = (float)e;
-    return fmaf(de, RNGF_LN2_HI, fmaf(de, RNGF_LN2_LO, lm));
-}
-#endif
 #if IS_F64
 /* fp64 Box–Muller kernels (libdmt dmt_device.h bm_log / bm_sincospi, DESIGN.md §3 RNG): the
  * tables and coefficients of scripts/gen_bm_tables.py, the same operations in the same order. */
@@ -848,7 +843,7 @@ static inline void bm_sincospi(double x, double* sn, double* cs) {
 static void orc_bm_f32(uint32_t a, uint32_t b, float* z0, float* z1) {
     float u1 = (float)((a >> 8) + 1u) * 0x1p-24f;
     float u2 = (float)(b >> 8) * 0x1p-24f;
-    float rad = sqrtf(-2.0f * bm_logf(u1));
+    float rad = sqrtf(-2.0f * rng_logf(u1));
     float sn, cs;
     rng_sincospif(2.0f * u2, &sn, &cs);
     *z0 = rad * cs;
@@ -894,7 +889,7 @@ void SFX(orc_normal_pair)(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2, 
 #else
     float u1 = (float)((c[0] >> 8) + 1u) * 0x1p-24f;
     float u2 = (float)(c[2] >> 8) * 0x1p-24f;
-    float rad = sqrtf(-2.0f * bm_logf(u1));
+    float rad = sqrtf(-2.0f * rng_logf(u1));
     float sn, cs;
     rng_sincospif(2.0f * u2, &sn, &cs);
     *z0 = rad * cs;
@@ -1188,6 +1183,4 @@ int orc_backward_filter_segment_tda(int d, const double* aux, int npts, const do
 /* the canonical log kernel, exposed for the Python container restatement */
 double orc_rng_log(double u) { return rng_log(u); }
 double orc_bm_log(double u) { return bm_log(u); }
-#else
-float orc_bm_logf(float u) { return bm_logf(u); }
 #endif

@@ -138,8 +138,6 @@ def _load():
     lib.orc_rng_log.restype = d_
     lib.orc_bm_log.argtypes = [d_]
     lib.orc_bm_log.restype = d_
-    lib.orc_bm_logf.argtypes = [C.c_float]
-    lib.orc_bm_logf.restype = C.c_float
     lib.orc_philox_raw.argtypes = [u64, P, P]
     lib.orc_philox_raw.restype = None
     return lib

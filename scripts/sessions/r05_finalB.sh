@@ -11,6 +11,10 @@ P2="SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR S
 B5="python bench.py --config c5 --steps 4 --warmup 2 --no-cpu-baseline --calls-iters 0 --repeats 0"
 B3="python bench.py --config c3 --steps 4 --warmup 2 --no-cpu-baseline --calls-iters 0 --repeats 0"
 scripts/gpu_session.sh \
+ "DMT_LIB_PATH=$PWD/build_variants/libdmt_base.so timeout -k 10 120 python scripts/kbench.py --config c5 --mapping lane --accept --iters 20 > $O/c5_base1.json 2> $O/c5_base1.err" \
+ "timeout -k 10 120 python scripts/kbench.py --config c5 --mapping lane --accept --iters 20 > $O/c5_new1.json 2> $O/c5_new1.err" \
+ "DMT_LIB_PATH=$PWD/build_variants/libdmt_base.so timeout -k 10 120 python scripts/kbench.py --config c5 --mapping lane --accept --iters 20 > $O/c5_base2.json 2> $O/c5_base2.err" \
+ "timeout -k 10 120 python scripts/kbench.py --config c5 --mapping lane --accept --iters 20 > $O/c5_new2.json 2> $O/c5_new2.err" \
  "timeout -k 10 300 python bench.py --config c5 --steps 20 --warmup 3 > $O/bench_c5.json 2> $O/bench_c5.err" \
  "timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_c5 -o c5 --output-format csv -- python bench.py --config c5 --steps 20 --warmup 3 --no-cpu-baseline --calls-iters 0 --repeats 0 > $O/prof_c5.json 2> $O/prof_c5.log" \
  "timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_c5_fetch -o f --output-format csv -- $B5 > $O/pmc_c5_fetch.log 2>&1" \

@@ -73,24 +73,6 @@ def test_fp64_normals_match_libm_box_muller():
         assert v < 0 and abs(v - math.log(u)) <= 2 ** -52 * abs(math.log(u))
 
 
-def test_fp32_log_table_accuracy():
-    """bm_logf (the division-free fp32 Box–Muller log): within 2 ulp of the
-    float32 rounding of log(u) on every 24-bit uniform class it sees — all j of the table, the
-    small end 2^-24 and u → 1⁻ (where it stays ≤ 0 and exact at 1)."""
-    f = orc.lib.orc_bm_logf
-    assert f(1.0) == 0.0
-    rng = np.random.default_rng(3)
-    us = np.concatenate([(np.arange(1, 2 ** 12) * 2.0 ** -24),
-                         (rng.integers(1, 2 ** 24, 40000) * 2.0 ** -24),
-                         1.0 - np.arange(1, 4000) * 2.0 ** -24]).astype(np.float32)
-    for u in us:
-        v = np.float32(f(float(u)))
-        want = np.float32(math.log(float(u)))
-        assert v <= 0.0
-        ulp = np.spacing(np.abs(want)) if want != 0 else np.float32(2.0 ** -149)
-        assert abs(float(v) - float(want)) <= 2 * float(ulp), (u, v, want)
-
-
 # ---------------------------------------------------------------- guiding term
 def test_guiding_ou1d_closed_form(dmt):
     theta, mu, sigma, T, v, Sig = 0.5, 0.2, 0.7, 1.0, 0.3, 0.01
