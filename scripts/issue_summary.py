@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--limiter", default="")
     ap.add_argument("--csv", nargs="+", required=True)
     ap.add_argument("--out", required=True)
+    ap.add_argument("--skip", type=int, default=0, help="drop the kernel's first N dispatches")
     ap.add_argument("--tree", help="tree.txt of the GPU session (the digest of the tree it ran)")
     a = ap.parse_args()
     disp = collections.defaultdict(dict)
@@ -51,6 +52,8 @@ def main():
     by_id = collections.defaultdict(dict)
     for (f, did), v in disp.items():
         by_id[did].update(v)
+    for did in sorted(by_id, key=int)[:a.skip]:  # warm-up dispatches of another shape
+        del by_id[did]
     rows = []
     for did, v in by_id.items():
         if "SQ_WAVES" not in v:

@@ -21,13 +21,15 @@ import provenance  # noqa: E402
 import statistics
 
 
-def per_kernel(path, counter, substr):
+def per_kernel(path, counter, substr, skip=0):
+    """The counter's value per dispatch of the kernel, in dispatch order, the first `skip`
+    dispatches dropped (a bench's warm-up launches of a different iteration count)."""
     vals = []
     with open(path, newline="") as f:
         for row in csv.DictReader(f):
             if row["Counter_Name"] == counter and substr in row["Kernel_Name"]:
-                vals.append(float(row["Counter_Value"]))
-    return vals
+                vals.append((int(row["Dispatch_Id"]), float(row["Counter_Value"])))
+    return [v for _, v in sorted(vals)[skip:]]
 
 
 def main():
@@ -43,10 +45,11 @@ def main():
                     help="iterations one dispatch runs (k_mcmc_scan: --steps of the bench); "
                          "bytes are reported per iteration, like bench.py's roofline")
     ap.add_argument("--out", required=True)
+    ap.add_argument("--skip", type=int, default=0, help="drop the kernel's first N dispatches")
     ap.add_argument("--tree", help="tree.txt of the GPU session (the digest of the tree it ran)")
     a = ap.parse_args()
-    fk = per_kernel(a.fetch, "FETCH_SIZE", a.kernel)
-    wk = per_kernel(a.write, "WRITE_SIZE", a.kernel)
+    fk = per_kernel(a.fetch, "FETCH_SIZE", a.kernel, a.skip)
+    wk = per_kernel(a.write, "WRITE_SIZE", a.kernel, a.skip)
     if not fk or not wk:
         raise SystemExit(f"no dispatches of {a.kernel!r} in the PMC files")
     cf = cw = 1.0
@@ -63,6 +66,7 @@ def main():
     w_b = statistics.median(wk) * 1024.0 * cw / a.units_per_launch
     # per unit (an iteration of a persistent launch; 1 unit per launch otherwise) and per launch
     out = {"config": a.config, "kernel": a.kernel, "dispatches": [len(fk), len(wk)],
+           "skipped": a.skip,
            "units_per_launch": a.units_per_launch,
            "fetch_bytes_per_unit": f_b, "write_bytes_per_unit": w_b,
            "traffic_bytes_per_unit": f_b + w_b,
