@@ -1455,9 +1455,6 @@ struct ChunkIt {  // (segment, first step) iterator over a block's chunks of 64 
   }
 };
 
-#ifndef DMT_S_PREFETCH  // wave S: rows in registers ahead of the recursion (1: one step ahead)
-#define DMT_S_PREFETCH 4
-#endif
 // DIAG (timing diagnostics only, never selected in production): bit 0 = S skips its
 // recursion, bit 1 = P skips phase A, bit 2 = P skips phase B.
 template <class Mdl, class T, int MODE, int DIAG = 0>
@@ -1508,38 +1505,6 @@ __global__ __launch_bounds__(128) void k_block_wave(const BlockArgs<T> a) {
       T xc[D];
 #pragma unroll
       for (int p = 0; p < D; ++p) xc[p] = x[p];
-#if DMT_S_PREFETCH > 1
-      // the rows of the next DMT_S_PREFETCH steps are in registers (a ring refilled as each is
-      // consumed), so the LDS latency of a row is spread over that many steps' dependent chains
-      // (one step ahead, round 1–4, left the recursion waiting on LDS: ≈ 78 ns per step whatever
-      // its arithmetic)
-      constexpr int PF = DMT_S_PREFETCH;
-      T ring[PF][NR];
-#pragma unroll
-      for (int k = 0; k < PF; ++k)
-#pragma unroll
-        for (int i = 0; i < NR; ++i) ring[k][i] = rw[k < cnt ? k : (cnt > 0 ? cnt - 1 : 0)][i];
-      for (int s0 = 0; s0 < cnt; s0 += PF) {
-#pragma unroll
-        for (int j = 0; j < PF; ++j) {
-          const int s = s0 + j;
-          if (s < cnt) {
-            T q[NR];
-#pragma unroll
-            for (int i = 0; i < NR; ++i) q[i] = ring[j][i];
-            const int sn = s + PF < cnt ? s + PF : cnt - 1;
-#pragma unroll
-            for (int i = 0; i < NR; ++i) ring[j][i] = rw[sn][i];
-            T b_[D];
-            if (!Mdl::kLinear) Mdl::drift(L.th, x, b_);
-            const bool mine = lane == s;
-#pragma unroll
-            for (int p = 0; p < D; ++p) xc[p] = mine ? x[p] : xc[p];
-            euler_step<Mdl, T>(L.th, q + 1 + D, q + 1 + D + D * D, b_, q[0], q + 1, x);
-          }
-        }
-      }
-#else
       // the next step's row is read into registers one step ahead, so the LDS latency overlaps
       // the current step's dependent chain instead of preceding it
       T nx[NR];
@@ -1563,7 +1528,6 @@ __global__ __launch_bounds__(128) void k_block_wave(const BlockArgs<T> a) {
         for (int p = 0; p < D; ++p) xc[p] = mine ? x[p] : xc[p];
         euler_step<Mdl, T>(L.th, q + 1 + D, q + 1 + D + D * D, b_, q[0], q + 1, x);
       }
-#endif
 #pragma unroll
       for (int p = 0; p < D; ++p) sh.xcap[k & 1][lane][p] = xc[p];
       const bool seg_end = it.c0 + 64 >= it.nst;

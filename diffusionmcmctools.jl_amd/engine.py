@@ -305,10 +305,11 @@ class Ensemble:
                C.byref(b), C.byref(n))
         return a.value, b.value, n.value
 
-    def mcmc_run(self, layout, b0, b1, iter0, n_iter, salt=0, local=False):
+    def mcmc_run(self, layout, b0, b1, iter0, n_iter, salt=0, local=False, copy=True):
         """n_iter mcmc_step iterations without host synchronisation in between; returns
         (n_iter, 3): fetch_ll, fetch_ll°, accepted count per iteration (``local``: this rank's
-        sums, no collective)."""
+        sums, no collective).  ``copy=False`` returns the handle's result buffer for this run
+        length itself (valid until the next run of the same length)."""
         n = int(n_iter)
         buf = self._run_out.get(n)
         if buf is None:
@@ -317,7 +318,7 @@ class Ensemble:
             self._h, layout, b0, b1, iter0, n, salt, buf[1])
         if st:
             L.check(st)
-        return buf[0].copy()
+        return buf[0].copy() if copy else buf[0]
 
     def prepare_run(self, n_iter):
         """The result buffer of mcmc_run calls of n_iter iterations (one per run length, its
