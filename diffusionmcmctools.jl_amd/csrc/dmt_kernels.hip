@@ -95,6 +95,9 @@ __device__ __forceinline__ void lane_st(T* p, T v) {
 // come in whole Box–Muller pairs (K·M even); the chunk's K Girsanov terms are summed as an
 // aligned subtree and inserted into the 64-step pairwise counter.  A tail of < K steps
 // runs through the single-step path.
+#ifndef DMT_LANE_AHEAD  // lane kernels (row layout): chunks of K steps loaded ahead (1 or 2;
+#define DMT_LANE_AHEAD 0  // 0: two when a chunk's inputs fit in 40 registers per lane, e.g. FHN)
+#endif
 #ifndef DMT_KCHUNK_PAIR_BASE
 #define DMT_KCHUNK_PAIR_BASE 4  // pair-kernel chunk (doubled when it would hold an odd number of
                                 // Philox blocks: Lorenz fp32, 3 normals per step → 8 steps)
@@ -278,73 +281,104 @@ __device__ __forceinline__ bool run_segment(const Law<Mdl, T>& L, const T* __res
   };
 
   const int nfull = nst - nst % K;
-  if (nfull > 0) {
+  // one chunk of K steps from registers: its normals, the steps, the chunk's subtree
+  auto run_chunk = [&](const int c0, Chunk& cur) {
+    if (DRAW && !PARITY) {  // whole Philox blocks of normals for this chunk, straight-line
+      constexpr int NPB = NormPerBlock<T>::v;
+      static_assert((K * M) % NPB == 0, "chunk must hold whole normal blocks");
+      if constexpr (PAIR) {  // role r draws blocks 2j + r; the pair swaps halves
+        static_assert((K * M / NPB) % 2 == 0, "a pair chunk holds an even number of blocks");
+#pragma unroll
+        for (int j = 0; j < K * M / NPB / 2; ++j) {
+          const uint32_t bc = (uint32_t)((c0 * M) / NPB + 2 * j + role);
+          T zb[NPB];
+          normal_block(philox4x32_10(U4{bc, ns.seg, ns.iter, ns.c3}, ns.k0, ns.k1), zb);
+#pragma unroll
+          for (int e = 0; e < NPB; ++e) {
+            T lo, hi;
+            pair_exchange<T>(zb[e], lo, hi);
+            const int n0 = NPB * (2 * j) + e, n1 = NPB * (2 * j + 1) + e;
+            cur.Z[n0 / M][n0 % M] = lo;
+            cur.Z[n1 / M][n1 % M] = hi;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int bq = 0; bq < K * M / NPB; ++bq) {
+          const uint32_t bc = (uint32_t)((c0 * M) / NPB + bq);
+          T zb[NPB];
+          normal_block(philox4x32_10(U4{bc, ns.seg, ns.iter, ns.c3}, ns.k0, ns.k1), zb);
+#pragma unroll
+          for (int e = 0; e < NPB; ++e) cur.Z[(NPB * bq + e) / M][(NPB * bq + e) % M] = zb[e];
+        }
+      }
+    }
+    T gv[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+      gv[j] = step(c0 + j, cur.t[j], cur.H[j], cur.F[j], cur.W[j], cur.Z[j], cur.Xu[j], j);
+    ps.template add_subtree<Log2<K>::v>(tree_sum<T, K>(gv));
+    if constexpr (PKT) {
+      static_assert(K * sizeof(T) % 16 == 0, "packets of whole 16-byte pieces");
+      typedef T v16 __attribute__((ext_vector_type(16 / sizeof(T))));
+      constexpr int NV = 16 / sizeof(T);
+#pragma unroll
+      for (int p = 0; p < D; ++p) {
+        T* q = Xd + (row + c0 + 1) * D * kLanes + ((int64_t)p * kLanes + lane) * K;
+#pragma unroll
+        for (int h = 0; h < K / NV; ++h) {
+          v16 v;
+#pragma unroll
+          for (int e = 0; e < NV; ++e) v[e] = pkx[h * NV + e][p];
+          __builtin_nontemporal_store(v, (v16*)(q + h * NV));
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < M; ++k) {
+        T* q = Wd + (row + c0 + 1) * M * kLanes + ((int64_t)k * kLanes + lane) * K;
+#pragma unroll
+        for (int h = 0; h < K / NV; ++h) {
+          v16 v;
+#pragma unroll
+          for (int e = 0; e < NV; ++e) v[e] = pkw[h * NV + e][k];
+          __builtin_nontemporal_store(v, (v16*)(q + h * NV));
+        }
+      }
+    }
+  };
+  // chunks in flight: one, or two where a chunk's inputs (t, H, F, W, Z, u.X: one value each)
+  // take few registers — C3 (FHN, fp64): 1 061-1 070 -> 1 011-1 013 µs per draw; Lorenz's
+  // lane kernels spill with two (profiles/r05h)
+  constexpr int kChunkVals = K * (1 + HP + D + 2 * M + D);
+  constexpr int AHEAD = DMT_LANE_AHEAD ? DMT_LANE_AHEAD : (kChunkVals <= 40 ? 2 : 1);
+  if (nfull > 0 && AHEAD == 2) {
+    // a ring of three register sets, unrolled by three so that no set is copied (a copy would
+    // wait for the loads just issued); the tile's kPadPoints spare rows keep the prefetch 2K
+    // points past the segment in bounds
+    static_assert(2 * K <= kPadPoints, "prefetch distance exceeds the tile's spare rows");
+    Chunk c_a, c_b, c_c;
+    load(0, c_a);
+    load(K, c_b);
+    for (int c0 = 0;;) {
+      if (c0 >= nfull) break;
+      load(c0 + 2 * K, c_c);
+      run_chunk(c0, c_a);
+      c0 += K;
+      if (c0 >= nfull) break;
+      load(c0 + 2 * K, c_a);
+      run_chunk(c0, c_b);
+      c0 += K;
+      if (c0 >= nfull) break;
+      load(c0 + 2 * K, c_b);
+      run_chunk(c0, c_c);
+      c0 += K;
+    }
+  } else if (nfull > 0) {
     Chunk cur, nxt;
     load(0, cur);
     for (int c0 = 0; c0 < nfull; c0 += K) {
       load(c0 + K, nxt);  // prefetch; padded rows keep the last one in bounds
-      if (DRAW && !PARITY) {  // whole Philox blocks of normals for this chunk, straight-line
-        constexpr int NPB = NormPerBlock<T>::v;
-        static_assert((K * M) % NPB == 0, "chunk must hold whole normal blocks");
-        if constexpr (PAIR) {  // role r draws blocks 2j + r; the pair swaps halves
-          static_assert((K * M / NPB) % 2 == 0, "a pair chunk holds an even number of blocks");
-#pragma unroll
-          for (int j = 0; j < K * M / NPB / 2; ++j) {
-            const uint32_t bc = (uint32_t)((c0 * M) / NPB + 2 * j + role);
-            T zb[NPB];
-            normal_block(philox4x32_10(U4{bc, ns.seg, ns.iter, ns.c3}, ns.k0, ns.k1), zb);
-#pragma unroll
-            for (int e = 0; e < NPB; ++e) {
-              T lo, hi;
-              pair_exchange<T>(zb[e], lo, hi);
-              const int n0 = NPB * (2 * j) + e, n1 = NPB * (2 * j + 1) + e;
-              cur.Z[n0 / M][n0 % M] = lo;
-              cur.Z[n1 / M][n1 % M] = hi;
-            }
-          }
-        } else {
-#pragma unroll
-          for (int bq = 0; bq < K * M / NPB; ++bq) {
-            const uint32_t bc = (uint32_t)((c0 * M) / NPB + bq);
-            T zb[NPB];
-            normal_block(philox4x32_10(U4{bc, ns.seg, ns.iter, ns.c3}, ns.k0, ns.k1), zb);
-#pragma unroll
-            for (int e = 0; e < NPB; ++e) cur.Z[(NPB * bq + e) / M][(NPB * bq + e) % M] = zb[e];
-          }
-        }
-      }
-      T gv[K];
-#pragma unroll
-      for (int j = 0; j < K; ++j)
-        gv[j] = step(c0 + j, cur.t[j], cur.H[j], cur.F[j], cur.W[j], cur.Z[j], cur.Xu[j], j);
-      ps.template add_subtree<Log2<K>::v>(tree_sum<T, K>(gv));
-      if constexpr (PKT) {
-        static_assert(K * sizeof(T) % 16 == 0, "packets of whole 16-byte pieces");
-        typedef T v16 __attribute__((ext_vector_type(16 / sizeof(T))));
-        constexpr int NV = 16 / sizeof(T);
-#pragma unroll
-        for (int p = 0; p < D; ++p) {
-          T* q = Xd + (row + c0 + 1) * D * kLanes + ((int64_t)p * kLanes + lane) * K;
-#pragma unroll
-          for (int h = 0; h < K / NV; ++h) {
-            v16 v;
-#pragma unroll
-            for (int e = 0; e < NV; ++e) v[e] = pkx[h * NV + e][p];
-            __builtin_nontemporal_store(v, (v16*)(q + h * NV));
-          }
-        }
-#pragma unroll
-        for (int k = 0; k < M; ++k) {
-          T* q = Wd + (row + c0 + 1) * M * kLanes + ((int64_t)k * kLanes + lane) * K;
-#pragma unroll
-          for (int h = 0; h < K / NV; ++h) {
-            v16 v;
-#pragma unroll
-            for (int e = 0; e < NV; ++e) v[e] = pkw[h * NV + e][k];
-            __builtin_nontemporal_store(v, (v16*)(q + h * NV));
-          }
-        }
-      }
+      run_chunk(c0, cur);
       cur = nxt;
     }
   }
@@ -4818,6 +4852,11 @@ static void dlaunch(void (*k)(KArgs...), dim3 grid, dim3 block, hipStream_t s, A
 #endif
 constexpr int kChunk = DMT_KCHUNK;  // lane-kernel steps per prefetch chunk
 static_assert(2 * kChunk <= kPadPoints, "prefetch reads up to 2 chunks past a segment end");
+#ifndef DMT_PK_KCHUNK  // the packet kernels' chunk (their guiding-term prefetch distance)
+#define DMT_PK_KCHUNK DMT_KCHUNK
+#endif
+constexpr int kPkChunk = DMT_PK_KCHUNK;
+static_assert(2 * kPkChunk <= kPadPoints, "prefetch reads up to 2 chunks past a segment end");
 
 template <class Mdl, class T>
 static hipError_t launch_block_t(int mapping, int mode, const void* args, int64_t nwaves,
@@ -4881,28 +4920,28 @@ static hipError_t launch_block_t(int mapping, int mode, const void* args, int64_
         switch (mode) {
           case MODE_PCN:
             if (td) {
-              if (par) dlaunch(k_block_pk<Mdl, T, MODE_PCN, true, kChunk, true>, grid, block, s, a);
-              else dlaunch(k_block_pk<Mdl, T, MODE_PCN, false, kChunk, true>, grid, block, s, a);
+              if (par) dlaunch(k_block_pk<Mdl, T, MODE_PCN, true, kPkChunk, true>, grid, block, s, a);
+              else dlaunch(k_block_pk<Mdl, T, MODE_PCN, false, kPkChunk, true>, grid, block, s, a);
             } else {
-              if (par) dlaunch(k_block_pk<Mdl, T, MODE_PCN, true, kChunk>, grid, block, s, a);
+              if (par) dlaunch(k_block_pk<Mdl, T, MODE_PCN, true, kPkChunk>, grid, block, s, a);
               else if (DMT_PK_SDT_TABLE && a.t_shared && a.sdt)  // shared grid: √dt table
-                dlaunch(k_block_pk<Mdl, T, MODE_PCN, false, kChunk, false, true>, grid, block, s, a);
-              else dlaunch(k_block_pk<Mdl, T, MODE_PCN, false, kChunk>, grid, block, s, a);
+                dlaunch(k_block_pk<Mdl, T, MODE_PCN, false, kPkChunk, false, true>, grid, block, s, a);
+              else dlaunch(k_block_pk<Mdl, T, MODE_PCN, false, kPkChunk>, grid, block, s, a);
             }
             break;
           case MODE_RECOMPUTE:
-            if (td) dlaunch(k_block_pk<Mdl, T, MODE_RECOMPUTE, false, kChunk, true>, grid, block, s, a);
-            else dlaunch(k_block_pk<Mdl, T, MODE_RECOMPUTE, false, kChunk>, grid, block, s, a);
+            if (td) dlaunch(k_block_pk<Mdl, T, MODE_RECOMPUTE, false, kPkChunk, true>, grid, block, s, a);
+            else dlaunch(k_block_pk<Mdl, T, MODE_RECOMPUTE, false, kPkChunk>, grid, block, s, a);
             break;
           case MODE_FRESH:
             if (td) {
-              if (par) dlaunch(k_block_pk<Mdl, T, MODE_FRESH, true, kChunk, true>, grid, block, s, a);
-              else dlaunch(k_block_pk<Mdl, T, MODE_FRESH, false, kChunk, true>, grid, block, s, a);
+              if (par) dlaunch(k_block_pk<Mdl, T, MODE_FRESH, true, kPkChunk, true>, grid, block, s, a);
+              else dlaunch(k_block_pk<Mdl, T, MODE_FRESH, false, kPkChunk, true>, grid, block, s, a);
             } else {
-              if (par) dlaunch(k_block_pk<Mdl, T, MODE_FRESH, true, kChunk>, grid, block, s, a);
+              if (par) dlaunch(k_block_pk<Mdl, T, MODE_FRESH, true, kPkChunk>, grid, block, s, a);
               else if (DMT_PK_SDT_TABLE && a.t_shared && a.sdt)
-                dlaunch(k_block_pk<Mdl, T, MODE_FRESH, false, kChunk, false, true>, grid, block, s, a);
-              else dlaunch(k_block_pk<Mdl, T, MODE_FRESH, false, kChunk>, grid, block, s, a);
+                dlaunch(k_block_pk<Mdl, T, MODE_FRESH, false, kPkChunk, false, true>, grid, block, s, a);
+              else dlaunch(k_block_pk<Mdl, T, MODE_FRESH, false, kPkChunk>, grid, block, s, a);
             }
             break;
           default: return hipErrorInvalidValue;
