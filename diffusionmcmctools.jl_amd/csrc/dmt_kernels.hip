@@ -1260,6 +1260,12 @@ __global__ __launch_bounds__(128, DMT_PS_MINW) void k_block_ps(const BlockArgs<T
             T dW[M];
 #pragma unroll
             for (int k = 0; k < M; ++k) dW[k] = s_dw[buf][q * K + j][k][lane];
+            T xn[D];
+#if DMT_PSPK_STUB == 1  // timing stub: the producer alone (no recursion; wrong results)
+            const T G = cur.H[j][0] + cur.F[j][0];
+#pragma unroll
+            for (int p = 0; p < D; ++p) xn[p] = x[p] + dW[p % M] * dt;
+#else
             T rr[D], b[D], sdW[D], Mg[D * D], cg[D];
             const T G = g_at<Mdl, T>(LA, cur.H[j], cur.F[j], x, rr, b);
             bool fast = false;
@@ -1275,10 +1281,10 @@ __global__ __launch_bounds__(128, DMT_PS_MINW) void k_block_ps(const BlockArgs<T
               sigma_dw<Mdl, T>(LA, dW, sdW);
               guide_coeffs<Mdl, T>(LA, cur.H[j], cur.F[j], Mg, cg);
             }
-            T xn[D];
 #pragma unroll
             for (int p = 0; p < D; ++p) xn[p] = x[p];
             euler_step<Mdl, T>(LA.th, Mg, cg, b, dt, sdW, xn);
+#endif
             if (v) {
               if (Xcd) {
 #pragma unroll
@@ -1311,6 +1317,303 @@ __global__ __launch_bounds__(128, DMT_PS_MINW) void k_block_ps(const BlockArgs<T
       for (int p = 0; p < D; ++p) ok = ok && isfinite(x[p]);
       if (nsx != sx) a.selX[g] = (uint8_t)nsx;
       if (nsw != sw) a.selW[g] = (uint8_t)nsw;
+      a.ll_out[blk] = ok ? (double)(ll + sl) : -INFINITY;
+      if (a.success) a.success[blk] = ok ? 1 : 0;
+    }
+  }
+}
+
+// ---- MAP_LANE packets, split into a producer and a consumer wave: k_block_ps's division of
+// work on the lane-packet layout (fp32 ensembles).  For draws (MODE_PCN, device
+// RNG, no per-point auxiliary table) over single-segment blocks whose segments start on a packet
+// boundary (the first segment of every recording does).  One workgroup of two waves per
+// (recording tile, block index), one packet of PK steps per hand-off (double-buffered LDS, one
+// barrier per packet): the PRODUCER reads u.W's packets, draws the packet's normals (whole
+// Philox blocks), forms dW° = fma(ρ, dW, √(1−ρ²)·(√dt·Z)), stores W°'s packet and hands (dt,
+// dW°) over; the CONSUMER loads H, F one chunk of K steps ahead, runs the guided recursion and
+// the Girsanov terms and stores X°'s packet.  The operations, their order, the normal numbering
+// and the summation tree are run_segment_pk's (K-step subtrees for every whole chunk, single
+// steps after), so the results are bit-identical to k_block_pk's.  A wave whose segments are
+// not aligned runs lane_block_pk on the consumer wave alone.
+#ifndef DMT_PSPK_STUB
+#define DMT_PSPK_STUB 0
+#endif
+#ifndef DMT_PSPK_RING  // the consumer's H, F register ring (chunks of K steps; 2 = one ahead)
+#define DMT_PSPK_RING 4
+#endif
+template <class Mdl, class T, int K, bool SDT>
+__global__ __launch_bounds__(128, 1) void k_block_ps_pk(const BlockArgs<T> a) {
+  constexpr int D = Mdl::D, M = Mdl::M, HP = D * (D + 1) / 2, PK = kPathPacket;
+  constexpr int VE = 16 / (int)sizeof(T), NV = PK / VE;
+  constexpr int NPB = NormPerBlock<T>::v;
+  static_assert(PK % K == 0 && (PK * M) % NPB == 0 && (K * M) % 2 == 0, "whole chunks, blocks");
+  typedef T v16 __attribute__((ext_vector_type(VE)));
+  __shared__ T s_dt[2][PK][64];
+  __shared__ T s_dw[2][PK][M][64];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int64_t tile = a.tile0 + blockIdx.x / a.MB;
+  const int bidx = (int)(blockIdx.x % a.MB);
+  if (tile >= a.tile1) return;  // whole workgroup
+  const int64_t r = tile * kLanes + lane;
+  int64_t blk = -1;
+  if (r < a.R) {
+    blk = a.blk_off[r] + bidx;
+    if (blk >= a.blk_off[r + 1] || blk < a.b0 || blk >= a.b1) blk = -1;
+  }
+  const bool act = blk >= 0;
+  const int64_t tq = a.tile_qoff[tile];
+  const int g = act ? a.gfirst[blk] : 0;  // the block's only segment (host-checked)
+  const int64_t q0 = act ? a.seg_q[g] : 0;
+  const int64_t row = tq + q0;
+  // both waves take the same branch (same lanes, same values)
+  if (__ballot(act && ((row + 1) & (PK - 1)) != 0) != 0) {
+    if (w == 1 && act) lane_block_pk<Mdl, T, MODE_PCN, false, K, false, false, SDT>(a, tile, blk, lane, nullptr);
+    return;
+  }
+  const int nst = act ? a.seg_np[g] - 1 : 0;
+  int nmax = nst;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) nmax = max(nmax, __shfl_xor(nmax, o, 64));
+  const int nch = (__builtin_amdgcn_readfirstlane(nmax) + PK - 1) / PK;  // packets
+  const int sx = act ? a.selX[g] : kSelInit, sw = act ? a.selW[g] : kSelInit;
+  auto pix = [&](int64_t i, int c, int C) -> int64_t { return plane_ix(row + i, c, C, kLanes, lane, PK); };
+
+  if (w == 0) {
+    // ================= producer =================
+    const T rho = act ? (T)a.rho[blk] : (T)0;
+    const T srho = act ? (T)a.srho[blk] : (T)1;
+    NormalStream<T> ns;
+    ns.init(a.seed, (uint32_t)g + a.seg_base, a.iter, a.salt);
+    const T* Ws = a.W[sel_buf(sw, a.ws_flip)];
+    T* Wd = a.W[sel_buf(sw, a.wd_flip)];
+    const T* tb = a.t_shared ? a.t + q0 : a.t + row * kLanes + lane;
+    const int tst = a.t_shared ? 1 : kLanes;
+    const T* sdb = SDT ? a.sdt + q0 : nullptr;
+    const int ilast = max(nst - 1, 0);  // per-step tables are read clamped to the segment
+    T tcur = tb[0];
+    if (act) {
+#pragma unroll
+      for (int k = 0; k < M; ++k) Wd[pix(0, k, M)] = rho * Ws[pix(0, k, M)];
+    }
+    // packet p of a component: points p·PK + 1 … p·PK + PK (the tile's spare rows keep the last
+    // packet's whole pieces in bounds); the next packet's pieces and grid prefetched
+    auto wpk = [&](int p, int k) -> const v16* { return (const v16*)&Ws[pix((int64_t)p * PK + 1, k, M)]; };
+    v16 wn[M][NV];
+    T tn_[PK], sn_[PK];
+    auto load = [&](int p) {
+#pragma unroll
+      for (int k = 0; k < M; ++k)
+#pragma unroll
+        for (int v = 0; v < NV; ++v) wn[k][v] = wpk(p, k)[v];
+#pragma unroll
+      for (int e = 0; e < PK; ++e) {
+        const int64_t i = min((int64_t)p * PK + e, (int64_t)ilast);
+        tn_[e] = tb[(i + 1) * tst];
+        sn_[e] = SDT ? sdb[i] : (T)0;
+      }
+    };
+    load(0);
+    for (int c = -1; c < nch; ++c) {
+      if (c + 1 < nch) {
+        const int p = c + 1, buf = p & 1;
+        v16 wc[M][NV];
+        T tc[PK], sc[PK];
+#pragma unroll
+        for (int k = 0; k < M; ++k)
+#pragma unroll
+          for (int v = 0; v < NV; ++v) wc[k][v] = wn[k][v];
+#pragma unroll
+        for (int e = 0; e < PK; ++e) { tc[e] = tn_[e]; sc[e] = sn_[e]; }
+        if (p + 1 < nch) load(p + 1);
+        T z[PK][M];
+#pragma unroll
+        for (int bq = 0; bq < PK * M / NPB; ++bq) {
+          const uint32_t bc = (uint32_t)((p * PK * M) / NPB + bq);
+          T zb[NPB];
+#if DMT_PSPK_STUB == 2  // timing stub: the consumer alone (no normals drawn; wrong results)
+#pragma unroll
+          for (int e = 0; e < NPB; ++e) zb[e] = (T)(bc & 7) * (T)0.125;
+#else
+          normal_block(philox4x32_10(U4{bc, ns.seg, ns.iter, ns.c3}, ns.k0, ns.k1), zb);
+#endif
+#pragma unroll
+          for (int e = 0; e < NPB; ++e) z[(NPB * bq + e) / M][(NPB * bq + e) % M] = zb[e];
+        }
+        v16 ob[M][NV];
+#pragma unroll
+        for (int e = 0; e < PK; ++e) {
+          const bool v = act && p * PK + e < nst;
+          const T dt = tc[e] - tcur;
+          const T sdt = SDT ? sc[e] : sqrt(dt);
+          s_dt[buf][e][lane] = dt;
+#pragma unroll
+          for (int k = 0; k < M; ++k) {
+            const T dw = dfma(rho, wc[k][e / VE][e % VE], srho * (sdt * z[e][k]));
+            s_dw[buf][e][k][lane] = dw;
+            ob[k][e / VE][e % VE] = dw;
+          }
+          tcur = v ? tc[e] : tcur;
+        }
+        if (act) {
+          if ((p + 1) * PK <= nst) {  // a whole packet: its pieces
+#pragma unroll
+            for (int k = 0; k < M; ++k) {
+              v16* dst = (v16*)&Wd[pix((int64_t)p * PK + 1, k, M)];
+#pragma unroll
+              for (int v = 0; v < NV; ++v) dst[v] = ob[k][v];
+            }
+          } else {
+#pragma unroll
+            for (int e = 0; e < PK; ++e)
+              if (p * PK + e < nst)
+#pragma unroll
+                for (int k = 0; k < M; ++k) Wd[pix((int64_t)p * PK + e + 1, k, M)] = ob[k][e / VE][e % VE];
+          }
+        }
+      }
+      __syncthreads();
+    }
+  } else {
+    // ================= consumer =================
+    const bool term = act ? a.term[blk] != 0 : true;
+    const int kind = term ? 0 : 1;  // a non-terminal block's segment takes the blocking law
+    const int ls = act ? ((kind ? a.selPPB[g] : a.selPP[g]) ^ a.law_flip) : 0;
+    Law<Mdl, T> LA;
+    LA.load(a.law[ls][kind] + (int64_t)g * DMT_LAW_STRIDE);
+    const bool all_unit = !Mdl::kLinear && __ballot(!act || LA.unit) == __ballot(1);
+    const T* Ht = a.H[ls][kind];
+    const int hsh = a.H_shared[ls][kind];
+    const T* Hb = hsh ? Ht + q0 * HP : Ht + row * HP * kLanes + lane;
+    const int hst = hsh ? 1 : kLanes;
+    const T* Fb = a.F[ls][kind] + row * D * kLanes + lane;
+    T x[D];
+    {
+      const T* Xs = a.X[sel_buf(sx, a.xs_flip)];
+#pragma unroll
+      for (int p = 0; p < D; ++p) x[p] = Xs[pix(0, p, D)];
+    }
+    T ll;
+    {  // the block's observation term: u's terminal-kind law of its first segment (lane_block_pk)
+      const int l0 = act ? (a.selPP[g] ^ a.law_flip) : 0;
+      const T* H0t = a.H[l0][0];
+      T H0[HP], F0[D];
+#pragma unroll
+      for (int e = 0; e < HP; ++e) H0[e] = a.H_shared[l0][0] ? H0t[q0 * HP + e] : H0t[(row * HP + e) * kLanes + lane];
+#pragma unroll
+      for (int e = 0; e < D; ++e) F0[e] = a.F[l0][0][(row * D + e) * kLanes + lane];
+      ll = obs_term<D, T>(H0, F0, x, (T)a.law[l0][0][(int64_t)g * DMT_LAW_STRIDE + DMT_LAW_C0]);
+    }
+    T* Xd = a.X[sel_buf(sx, a.xd_flip)];
+    if (act) {
+#pragma unroll
+      for (int p = 0; p < D; ++p) Xd[pix(0, p, D)] = x[p];
+    }
+    const int ilast = max(nst - 1, 0);
+    PSum<T> ps;
+    ps.init();
+    const int nfull = nst - nst % K;
+    struct Sub { T H[K][HP], F[K][D]; };
+    auto load = [&](int64_t i0, Sub& s) {
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        const int64_t i = min<int64_t>(i0 + j, ilast);
+#pragma unroll
+        for (int e = 0; e < HP; ++e) s.H[j][e] = lane_ld(&Hb[(i * HP + e) * hst]);
+#pragma unroll
+        for (int e = 0; e < D; ++e) s.F[j][e] = lane_ld(&Fb[(i * D + e) * kLanes]);
+      }
+    };
+    // H, F chunks in flight: a ring of NR register sets, NR - 1 chunks ahead; NR divides the
+    // packet's chunks, so the unrolled packet loop indexes the ring with constants (the consumer
+    // has little arithmetic per step to cover the loads' latency with)
+    constexpr int NR = DMT_PSPK_RING;
+    static_assert((PK / K) % NR == 0 && (NR - 1) * K <= kPadPoints, "ring of whole packets");
+    Sub sb[NR];
+#pragma unroll
+    for (int u = 0; u < NR - 1; ++u) load((int64_t)u * K, sb[u]);
+    for (int c = -1; c < nch; ++c) {
+      if (c >= 0) {
+        const int buf = c & 1;
+        v16 ob[D][NV];
+#pragma unroll
+        for (int q = 0; q < PK / K; ++q) {
+          const int64_t i0 = (int64_t)c * PK + q * K;
+          load(i0 + (NR - 1) * K, sb[(q + NR - 1) % NR]);  // prefetch NR - 1 chunks ahead
+          Sub& cur = sb[q % NR];
+          T gv[K];
+#pragma unroll
+          for (int j = 0; j < K; ++j) {
+            const int e = q * K + j;
+            const bool v = act && i0 + j < nst;
+            const T dt = s_dt[buf][e][lane];
+            T dW[M];
+#pragma unroll
+            for (int k = 0; k < M; ++k) dW[k] = s_dw[buf][e][k][lane];
+            T xn[D];
+#if DMT_PSPK_STUB == 1  // timing stub: the producer alone (no recursion; wrong results)
+            const T G = cur.H[j][0] + cur.F[j][0];
+#pragma unroll
+            for (int p = 0; p < D; ++p) xn[p] = x[p] + dW[p % M] * dt;
+#else
+            T rr[D], b[D], sdW[D], Mg[D * D], cg[D];
+            const T G = g_at<Mdl, T>(LA, cur.H[j], cur.F[j], x, rr, b);
+            bool fast = false;
+            if constexpr (!Mdl::kLinear && D == M) {
+              if (all_unit) {
+#pragma unroll
+                for (int p = 0; p < D; ++p) sdW[p] = dW[p];
+                guide_coeffs_unit<Mdl, T>(cur.H[j], cur.F[j], Mg, cg);
+                fast = true;
+              }
+            }
+            if (!fast) {
+              sigma_dw<Mdl, T>(LA, dW, sdW);
+              guide_coeffs<Mdl, T>(LA, cur.H[j], cur.F[j], Mg, cg);
+            }
+#pragma unroll
+            for (int p = 0; p < D; ++p) xn[p] = x[p];
+            euler_step<Mdl, T>(LA.th, Mg, cg, b, dt, sdW, xn);
+#endif
+#pragma unroll
+            for (int p = 0; p < D; ++p) {
+              x[p] = v ? xn[p] : x[p];
+              ob[p][e / VE][e % VE] = xn[p];
+            }
+            gv[j] = G * dt;
+          }
+          if (i0 + K <= nfull) {
+            ps.template add_subtree<Log2<K>::v>(tree_sum<T, K>(gv));
+          } else {
+#pragma unroll
+            for (int j = 0; j < K; ++j)
+              if (i0 + j < nst) ps.add(gv[j]);
+          }
+        }
+        if (act) {
+          if ((int64_t)(c + 1) * PK <= nst) {  // a whole packet: its pieces
+#pragma unroll
+            for (int p = 0; p < D; ++p) {
+              v16* dst = (v16*)&Xd[pix((int64_t)c * PK + 1, p, D)];
+#pragma unroll
+              for (int v = 0; v < NV; ++v) dst[v] = ob[p][v];
+            }
+          } else {
+#pragma unroll
+            for (int e = 0; e < PK; ++e)
+              if ((int64_t)c * PK + e < nst)
+#pragma unroll
+                for (int p = 0; p < D; ++p) Xd[pix((int64_t)c * PK + e + 1, p, D)] = ob[p][e / VE][e % VE];
+          }
+        }
+      }
+      __syncthreads();
+    }
+    if (act) {
+      const T sl = ps.finish();
+      bool ok = isfinite(sl);
+#pragma unroll
+      for (int p = 0; p < D; ++p) ok = ok && isfinite(x[p]);
       a.ll_out[blk] = ok ? (double)(ll + sl) : -INFINITY;
       if (a.success) a.success[blk] = ok ? 1 : 0;
     }
@@ -4915,6 +5218,13 @@ static hipError_t launch_block_t(int mapping, int mode, const void* args, int64_
             if (td) dlaunch(k_block_pk_pair<Mdl, T, MODE_FRESH, true>, pgrid, block, s, a);
             else dlaunch(k_block_pk_pair<Mdl, T, MODE_FRESH>, pgrid, block, s, a);
           }
+          return hipGetLastError();
+        }
+        if (mode == MODE_PCN && !par && !td && a.lane_split) {  // producer/consumer waves
+          if (DMT_PK_SDT_TABLE && a.t_shared && a.sdt)
+            dlaunch(k_block_ps_pk<Mdl, T, kPkChunk, true>, grid, dim3(128), s, a);
+          else
+            dlaunch(k_block_ps_pk<Mdl, T, kPkChunk, false>, grid, dim3(128), s, a);
           return hipGetLastError();
         }
         switch (mode) {

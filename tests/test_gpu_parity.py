@@ -444,7 +444,8 @@ def test_device_rng_mode_bit_exact_c5_fp32(mapping):
 @pytest.mark.parametrize("cfg", ["c3", "c5"])
 def test_device_rng_lane_kernels_bit_exact(cfg, variant, monkeypatch):
     """The three lane-mapping draw kernels (k_block one lane per recording, k_block_pair two
-    lanes per recording sharing the normals, k_block_ps producer/consumer waves) draw the same
+    lanes per recording sharing the normals, k_block_ps producer/consumer waves — on C5's fp32
+    lane packets k_block_pk, k_block_pk_pair, k_block_ps_pk) draw the same
     device streams and give the oracle's paths, ll and decisions bit for bit — on a ragged
     last tile (70 / 40 recordings) and through two MCMC iterations."""
     for k, v in variant.items():
@@ -683,6 +684,41 @@ def test_fp32_lane_variants_bit_identical(env):
         for e in (e0, e1):
             e.draw_proposal(lay, 0, nb, iter=i, salt=2)
             acc.append(e.accept_reject(lay, 0, nb, i, salt=2, want_acc=True))
+        assert np.array_equal(acc[0], acc[1]), i
+        cs.assert_paths_equal(e0, e1)
+        for what in (L.BLK_LL, L.BLK_LLPROP):
+            assert np.array_equal(e0.get_block_state(lay, what, 0, nb),
+                                  e1.get_block_state(lay, what, 0, nb)), (i, what)
+    for e in (e0, e1):
+        e.close()
+
+
+def test_fp32_split_packets_single_segment_blocks_bit_identical():
+    """The packet layout's producer/consumer kernel (DMT_LANE_SPLIT=1, k_block_ps_pk) against the
+    default packet kernel on one-segment blocks of the ragged case (terminal: a non-terminal
+    block needs two segments): block index 0 holds every recording's first segment
+    (packet-aligned), the later block indices segments that start inside a packet (the kernel's
+    fallback to lane_block_pk) —
+    device-RNG draws, accepts, loglikhd and the downloaded paths, bit for bit."""
+    import diffusionmcmctools_amd as d
+
+    def build():
+        case = cs.ragged_case(prec=L.F32)
+        m = case["model"]
+        e = d.Ensemble(m.kind, m.d, m.m, case["n_points"], precision=L.F32, seed=6,
+                       mapping=L.MAP_LANE)
+        cs.load_ragged(e, case)
+        segs = [0, 1, 2, 3, 0, 1, 2, 3, 4, 5, 0, 1, 2, 3, 4]
+        lay = e.create_layout([4, 6, 5], segs, segs, [1] * 15, np.full(15, 0.5), 6)
+        return e, lay, 15
+    (e0, lay, nb), (e1, _, _) = _env_ensembles(build, {"DMT_LANE_SPLIT": "1"})
+    for e in (e0, e1):
+        e.loglikhd(lay, L.U, 0, nb)
+    for i in range(1, 5):
+        acc = []
+        for e in (e0, e1):
+            e.draw_proposal(lay, 0, nb, iter=i, salt=5)
+            acc.append(e.accept_reject(lay, 0, nb, i, salt=5, want_acc=True))
         assert np.array_equal(acc[0], acc[1]), i
         cs.assert_paths_equal(e0, e1)
         for what in (L.BLK_LL, L.BLK_LLPROP):
