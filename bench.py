@@ -467,9 +467,12 @@ def main(argv=None):
         wave, kname = True, "k_block_scan"
     elif wave:
         kname = "k_block_wave"
-    else:  # lane mapping: fp32 ensembles on lane packets (dmt_create; DMT_PATH_PACKETS=0: rows)
-        kname = ("k_block_pk<" if w.precision == L.F32 and os.environ.get("DMT_PATH_PACKETS", "1") != "0"
-                 else "k_block<")
+    else:  # lane mapping: fp32 ensembles on lane packets (dmt_create; DMT_PATH_PACKETS=0: rows),
+        # with fewer recording tiles than SIMDs on producer/consumer waves (DMT_LANE_SPLIT=0: one)
+        pk = w.precision == L.F32 and os.environ.get("DMT_PATH_PACKETS", "1") != "0"
+        split = (os.environ.get("DMT_LANE_SPLIT", "-1") != "0"
+                 and all(len(r) == 1 for r in w.n_points) and B // 64 < 1024)
+        kname = ("k_block_ps_pk<" if pk and split else "k_block_pk<" if pk else "k_block<")
     # committed profile summaries of THIS source tree only (scripts/provenance.py)
     tr, traffic_stale = committed_summary("traffic", args.config, kname)
     traffic = tr["traffic_bytes_per_unit"] * it_per_launch if tr else None  # per launch
@@ -507,7 +510,8 @@ def main(argv=None):
                                    "scan-resident-per-iteration" if kname == "k_block_resident" else
                                    "scan" if kname == "k_block_scan" else
                                    "wave" if wave else
-                                   "lane-packets" if kname == "k_block_pk<" else "lane"),
+                                   "lane-packets" if kname in ("k_block_pk<", "k_block_ps_pk<")
+                                   else "lane"),
                        "rng": "device Philox4x32-10 + Box-Muller (perf mode)"},
             "per_gpu": value / world,
             "accept_rate": accept_rate,

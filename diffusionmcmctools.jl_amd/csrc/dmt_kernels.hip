@@ -1260,12 +1260,6 @@ __global__ __launch_bounds__(128, DMT_PS_MINW) void k_block_ps(const BlockArgs<T
             T dW[M];
 #pragma unroll
             for (int k = 0; k < M; ++k) dW[k] = s_dw[buf][q * K + j][k][lane];
-            T xn[D];
-#if DMT_PSPK_STUB == 1  // timing stub: the producer alone (no recursion; wrong results)
-            const T G = cur.H[j][0] + cur.F[j][0];
-#pragma unroll
-            for (int p = 0; p < D; ++p) xn[p] = x[p] + dW[p % M] * dt;
-#else
             T rr[D], b[D], sdW[D], Mg[D * D], cg[D];
             const T G = g_at<Mdl, T>(LA, cur.H[j], cur.F[j], x, rr, b);
             bool fast = false;
@@ -1281,10 +1275,10 @@ __global__ __launch_bounds__(128, DMT_PS_MINW) void k_block_ps(const BlockArgs<T
               sigma_dw<Mdl, T>(LA, dW, sdW);
               guide_coeffs<Mdl, T>(LA, cur.H[j], cur.F[j], Mg, cg);
             }
+            T xn[D];
 #pragma unroll
             for (int p = 0; p < D; ++p) xn[p] = x[p];
             euler_step<Mdl, T>(LA.th, Mg, cg, b, dt, sdW, xn);
-#endif
             if (v) {
               if (Xcd) {
 #pragma unroll
@@ -1338,8 +1332,8 @@ __global__ __launch_bounds__(128, DMT_PS_MINW) void k_block_ps(const BlockArgs<T
 #ifndef DMT_PSPK_STUB
 #define DMT_PSPK_STUB 0
 #endif
-#ifndef DMT_PSPK_RING  // the consumer's H, F register ring (chunks of K steps; 2 = one ahead)
-#define DMT_PSPK_RING 4
+#ifndef DMT_PSPK_RING  // the consumer's H, F register ring (chunks of K steps; 2 = one ahead;
+#define DMT_PSPK_RING 2   // 4, three ahead, measured the same: 1 350 vs 1 341-1 343 µs, r05l)
 #endif
 template <class Mdl, class T, int K, bool SDT>
 __global__ __launch_bounds__(128, 1) void k_block_ps_pk(const BlockArgs<T> a) {
@@ -1431,7 +1425,7 @@ __global__ __launch_bounds__(128, 1) void k_block_ps_pk(const BlockArgs<T> a) {
         for (int bq = 0; bq < PK * M / NPB; ++bq) {
           const uint32_t bc = (uint32_t)((p * PK * M) / NPB + bq);
           T zb[NPB];
-#if DMT_PSPK_STUB == 2  // timing stub: the consumer alone (no normals drawn; wrong results)
+#if DMT_PSPK_STUB & 2  // timing stub: the consumer alone (no normals drawn; wrong results)
 #pragma unroll
           for (int e = 0; e < NPB; ++e) zb[e] = (T)(bc & 7) * (T)0.125;
 #else
@@ -1518,10 +1512,17 @@ __global__ __launch_bounds__(128, 1) void k_block_ps_pk(const BlockArgs<T> a) {
 #pragma unroll
       for (int j = 0; j < K; ++j) {
         const int64_t i = min<int64_t>(i0 + j, ilast);
+#if DMT_PSPK_STUB & 8  // timing stub: no H, F loads (wrong results)
+#pragma unroll
+        for (int e = 0; e < HP; ++e) s.H[j][e] = (T)(i & 3) * (T)0.01;
+#pragma unroll
+        for (int e = 0; e < D; ++e) s.F[j][e] = (T)(i & 7) * (T)0.01;
+#else
 #pragma unroll
         for (int e = 0; e < HP; ++e) s.H[j][e] = lane_ld(&Hb[(i * HP + e) * hst]);
 #pragma unroll
         for (int e = 0; e < D; ++e) s.F[j][e] = lane_ld(&Fb[(i * D + e) * kLanes]);
+#endif
       }
     };
     // H, F chunks in flight: a ring of NR register sets, NR - 1 chunks ahead; NR divides the
@@ -1551,7 +1552,7 @@ __global__ __launch_bounds__(128, 1) void k_block_ps_pk(const BlockArgs<T> a) {
 #pragma unroll
             for (int k = 0; k < M; ++k) dW[k] = s_dw[buf][e][k][lane];
             T xn[D];
-#if DMT_PSPK_STUB == 1  // timing stub: the producer alone (no recursion; wrong results)
+#if DMT_PSPK_STUB & 1  // timing stub: the producer alone (no recursion; wrong results)
             const T G = cur.H[j][0] + cur.F[j][0];
 #pragma unroll
             for (int p = 0; p < D; ++p) xn[p] = x[p] + dW[p % M] * dt;
@@ -1590,7 +1591,7 @@ __global__ __launch_bounds__(128, 1) void k_block_ps_pk(const BlockArgs<T> a) {
               if (i0 + j < nst) ps.add(gv[j]);
           }
         }
-        if (act) {
+        if (act && !(DMT_PSPK_STUB & 4)) {  // (timing stub 4: no X° stores)
           if ((int64_t)(c + 1) * PK <= nst) {  // a whole packet: its pieces
 #pragma unroll
             for (int p = 0; p < D; ++p) {

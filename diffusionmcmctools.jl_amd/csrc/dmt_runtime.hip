@@ -574,10 +574,11 @@ dmt_status run_block_kernel(dmt_ens* h, const Layout* L, int mode, int kind_time
     // layout (profiles/r03d) and slower on the packet layout: C5 1 753–1 789 vs 1 455–1 463 µs
     // per draw with register-staged packets (profiles/r04g)
     a.lane_pair = h->lane_pair == 1;
-    // the packet layout's split (k_block_ps_pk): on request (DMT_LANE_SPLIT=1) until measured
+    // the packet layout's split (k_block_ps_pk; fp32 lane packets): C5 1 343-1 355 vs
+    // 1 445-1 461 µs per draw (profiles/r05j)
     a.lane_split = !a.lane_pair && L->single_seg &&
                    (h->lane_split == 1 || (h->lane_split < 0 && nwaves < h->n_simd &&
-                                           h->key.precision == DMT_F64 && !h->pk));
+                                           (h->key.precision == DMT_F64 || h->pk)));
   };
   if (h->key.precision == DMT_F64) {
     BlockArgs<double> a{};
