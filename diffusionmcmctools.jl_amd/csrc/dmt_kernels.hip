@@ -1509,26 +1509,6 @@ __global__ __launch_bounds__(128, 1) void k_block_ps_pk(const BlockArgs<T> a) {
     const int nfull = nst - nst % K;
     struct Sub { T H[K][HP], F[K][D]; };
     auto load = [&](int64_t i0, Sub& s) {
-#if DMT_PSPK_STUB & 16  // timing stub: the chunk's H, F bytes as 16-byte loads (wrong lanes)
-      {
-        typedef T v4 __attribute__((ext_vector_type(4)));
-        const v4* hq = (const v4*)(Ht + (row + i0) * HP * kLanes);
-        const v4* fq = (const v4*)(a.F[ls][kind] + (row + i0) * D * kLanes);
-#pragma unroll
-        for (int u = 0; u < K * HP / 4; ++u) {
-          const v4 v = hq[u * kLanes + lane];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) s.H[(4 * u + e) / HP][(4 * u + e) % HP] = v[e];
-        }
-#pragma unroll
-        for (int u = 0; u < K * D / 4; ++u) {
-          const v4 v = fq[u * kLanes + lane];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) s.F[(4 * u + e) / D][(4 * u + e) % D] = v[e];
-        }
-        return;
-      }
-#endif
 #pragma unroll
       for (int j = 0; j < K; ++j) {
         const int64_t i = min<int64_t>(i0 + j, ilast);
