@@ -2672,7 +2672,7 @@ __device__ __forceinline__ bool arrive_last(unsigned* cnt, unsigned expect, int*
 // nodes: node1 [rows][ng] then node2 [rows][ng2]; counters: [ng2] group counters then the top
 // counter, zero on entry and left zero.  WPB = blocks (tree leaves) per workgroup, NW = waves
 // per workgroup (every thread of the workgroup calls this)
-template <int WPB, int NW = WPB>
+template <int WPB, int NW = WPB, bool L1 = false>
 __device__ __forceinline__ void persistent_tree_tail(const double* __restrict__ part,
                                                      double* __restrict__ nodes, int64_t nb,
                                                      int64_t n_iter,
@@ -2685,9 +2685,10 @@ __device__ __forceinline__ void persistent_tree_tail(const double* __restrict__ 
   const int64_t x = blockIdx.x, g = x / kTreeGroup, rows = 3 * n_iter;
   double* node1 = nodes;
   double* node2 = nodes + rows * ng;
-  // ---- level 1: this workgroup's leaves
-  __syncthreads();  // every wave's part[] stores of the run are done
-  for (int64_t row = tid; row < rows; row += NT) {
+  // ---- level 1: this workgroup's leaves (L1: formed and stored iteration by iteration during
+  // the run — the stores are drained by arrive_last)
+  if (!L1) __syncthreads();  // every wave's part[] stores of the run are done
+  for (int64_t row = tid; row < (L1 ? 0 : rows); row += NT) {
     double v[WPB];
 #pragma unroll
     for (int k = 0; k < WPB; ++k) {
@@ -3359,13 +3360,18 @@ __device__ __forceinline__ void svc_record(const SvcArgs& sv, const SvcLds* sl, 
 #endif
 }
 
-template <class Mdl, class T, int NP, bool SVC>
+#ifndef DMT_PC_L1_LOOP  // 1: level 1 of the fetch_ll trees formed during the run (after B2);
+                        // 0: read back from part[] by persistent_tree_tail
+#define DMT_PC_L1_LOOP 1
+#endif
+template <class Mdl, class T, int NP, bool SVC, int BPW = 4>
 __device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, const AcceptArgs& c,
                                                      const int64_t iter0, const int64_t n_iter,
                                                      double* __restrict__ part, const int64_t blk,
                                                      const bool valid,
                                                      ResPcLds<Mdl::D, Mdl::M, T>& P,
-                                                     const SvcArgs& sv, SvcLds* sl) {
+                                                     const SvcArgs& sv, SvcLds* sl,
+                                                     double* __restrict__ nodes = nullptr) {
   constexpr int D = Mdl::D, M = Mdl::M, HP = D * (D + 1) / 2;
   constexpr int CR = PcConsSteps<T, M, NP>::v, RC0 = kRun - CR, CRA = CR > 0 ? CR : 1;
   ResLds<D, M, T>& S = P.r;
@@ -3650,11 +3656,17 @@ __device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, cons
           c.ll_hist[o] = ll;
           c.llp_hist[o] = llp;
         }
-        if constexpr (!SVC) {
+        if constexpr (!SVC && !DMT_PC_L1_LOOP) {
           part[(3 * r0 + 0) * nb + j] = acc ? llp : ll;
           part[(3 * r0 + 1) * nb + j] = acc ? ll : llp;
           part[(3 * r0 + 2) * nb + j] = acc ? 1.0 : 0.0;
         }
+      }
+      if constexpr (!SVC && DMT_PC_L1_LOOP) {  // the workgroup's fetch_ll leaves (0: no block)
+        const int wi = (int)(threadIdx.x >> 6) % BPW;
+        sl->row[0][wi] = valid ? (acc ? llp : ll) : 0.0;
+        sl->row[1][wi] = valid ? (acc ? ll : llp) : 0.0;
+        sl->row[2][wi] = acc ? 1.0 : 0.0;
       }
     }
     if (acc) {
@@ -3677,6 +3689,21 @@ __device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, cons
     PC_ITSTAMP(0, r0, 2);
     __syncthreads();  // B2: decision n → producer; pt reads of this iteration done
     PC_ITSTAMP(0, r0, 3);
+    if constexpr (!SVC && DMT_PC_L1_LOOP) {
+      // level 1 of iteration n's fetch_ll trees (persistent_tree_tail): the workgroup's BPW
+      // leaves, adjacent pairs, stored write-through now instead of read back after the run
+      if (threadIdx.x < 3) {
+        double v[BPW];
+#pragma unroll
+        for (int k = 0; k < BPW; ++k) v[k] = sl->row[threadIdx.x][k];
+#pragma unroll
+        for (int w = BPW; w > 1; w >>= 1)
+#pragma unroll
+          for (int k = 0; k < w / 2; ++k) v[k] = v[2 * k] + v[2 * k + 1];
+        const int64_t ng = (a.b1 - a.b0 + BPW - 1) / BPW;
+        st_sc1(&nodes[(3 * r0 + threadIdx.x) * ng + blockIdx.x], v[0]);
+      }
+    }
     // (DMT_PC_LATE_C: the consumer's own steps of iteration n + 1 after B2, beside the producer's
     // proposal — the consumer, not the producer, is the one late at B2)
     if constexpr (!SVC && DMT_PC_LATE_C && CR > 0) propose_c();
@@ -3951,15 +3978,16 @@ __global__ __launch_bounds__(64 * BPW * (NP + 1), BPW == 4 ? 1 : 2) void k_mcmc_
   else for (int64_t i = 0; i < 2 * n_iter; ++i) __syncthreads();
 #else
   if (role == 0)
-    resident_pc_consumer<Mdl, T, NP, SVC>(a, c, iter0, n_iter, part, blk, valid, lds[w % BPW], sv,
-                                          &s_svc);
+    resident_pc_consumer<Mdl, T, NP, SVC, BPW>(a, c, iter0, n_iter, part, blk, valid, lds[w % BPW],
+                                               sv, &s_svc, nodes);
   else
     resident_pc_producer<Mdl, T, NP, SVC>(a, c, iter0, n_iter, blk, valid, role - 1, lds[w % BPW],
                                           sv, &s_svc);
 #endif
 #ifndef DMT_PC_NO_TAIL  // timing probe: no in-kernel fetch_ll trees
   if constexpr (!SVC)  // the service forms each iteration's tree as the iteration ends
-    persistent_tree_tail<BPW, BPW * (NP + 1)>(part, nodes, a.b1 - a.b0, n_iter, counter, out3);
+    persistent_tree_tail<BPW, BPW * (NP + 1), DMT_PC_L1_LOOP != 0>(part, nodes, a.b1 - a.b0,
+                                                                    n_iter, counter, out3);
 #endif
   PC_STAMP(0, 5);
 }

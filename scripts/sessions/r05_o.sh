@@ -1,0 +1,27 @@
+#!/bin/bash
+# round 5: C2 resident kernel with level 1 of the fetch_ll trees formed during the run
+# (DMT_PC_L1_LOOP=1, default) against the read-back tail (l1off); GPU suite first
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/r05o; mkdir -p $O
+python scripts/provenance.py > $O/tree.txt
+S=("timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread > $O/pytest.log 2>&1")
+for r in 1 2; do
+  for v in def l1off; do
+    if [ $v = def ]; then LP=$PWD/diffusionmcmctools.jl_amd/libdmt.so; else LP=$PWD/build_variants/libdmt_$v.so; fi
+    S+=("DMT_LIB_PATH=$LP timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --calls-iters 0 --repeats 20 > $O/c2_${v}_$r.json 2> $O/c2_${v}_$r.err")
+  done
+done
+for v in def l1off; do
+  if [ $v = def ]; then LP=$PWD/diffusionmcmctools.jl_amd/libdmt.so; else LP=$PWD/build_variants/libdmt_$v.so; fi
+  S+=("DMT_LIB_PATH=$LP timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_$v -o c2 --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline --calls-iters 0 --repeats 20 > $O/prof_$v.json 2> $O/prof_$v.log")
+done
+scripts/gpu_session.sh "${S[@]}"
+tail -2 $O/pytest.log
+for f in $O/c2_*.json; do python -c "import json;d=json.load(open('$f'));print('$f', round(d['value']/1e10,4), round(d['repeats']['value_median']/1e10,4), round(d['roofline']['kernel_avg_us'],2))"; done
+for v in def l1off; do python -c "
+import csv,glob,statistics
+f=glob.glob('$O/prof_$v/*kernel_trace.csv')[0]
+d=[(int(r['End_Timestamp'])-int(r['Start_Timestamp']))/1e3 for r in csv.DictReader(open(f)) if 'k_mcmc_resident_pc' in r['Kernel_Name']]
+d=d[5:]
+print('$v', len(d), round(statistics.median(d),2), round(min(d),2))"; done
