@@ -3283,6 +3283,9 @@ struct SvcLds {
   int go;             // the gate's answer
   double row[3][4];   // the iteration's (ll, ll°, accepted) of the workgroup's 4 blocks
 };
+#ifndef DMT_SVC_PEEK  // the gate's host words read ahead (svc_peek): 1 after the iteration's
+#define DMT_SVC_PEEK 1   // points, 2 after its scan; 0: at the gate only
+#endif
 // Gate of iteration r (in place of its B1 barrier).  Workgroup 0's thread 0 is the launch's one
 // reader of host memory: it waits until the host has posted iteration r, asked the launch to
 // stop, or stayed silent for idle_ticks, and publishes the answer in device memory — go word
@@ -3292,13 +3295,32 @@ struct SvcLds {
 // is co-resident (launch_mcmc_service checks), so the reader always reaches the gate.  The
 // barrier hands the answer to every wave.  Nothing global is written for an iteration before
 // its gate opens.
-__device__ __forceinline__ bool svc_gate(const SvcArgs& sv, int64_t r, SvcLds* sl) {
+// spec_stop, spec_posted: workgroup 0's thread 0 read the two host words once already, late in
+// the iteration's arithmetic (svc_peek); a post seen there opens the gate without another PCIe
+// round trip (the loop below reads them again otherwise)
+struct SvcPeek {
+  uint32_t stop = 1u;
+  uint64_t posted = 0;
+};
+__device__ __forceinline__ SvcPeek svc_peek(const SvcArgs& sv) {
+  SvcPeek p;
+#if DMT_SVC_PEEK
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    p.stop = __hip_atomic_load(sv.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    p.posted = __hip_atomic_load(sv.posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+#endif
+  return p;
+}
+__device__ __forceinline__ bool svc_gate(const SvcArgs& sv, int64_t r, SvcLds* sl,
+                                         const SvcPeek pk = SvcPeek{}) {
   if (threadIdx.x == 0) {
     const uint64_t want = sv.base + (uint64_t)r + 1;
     int go = 0;
     if (blockIdx.x == 0) {
       const uint64_t t0 = (uint64_t)wall_clock64();
-      for (;;) {
+      if (pk.stop == 0u && pk.posted >= want) go = 1;
+      for (; !go;) {
         if (__hip_atomic_load(sv.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) break;
         if (__hip_atomic_load(sv.posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= want) {
           go = 1;
@@ -3563,6 +3585,8 @@ __device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, cons
       }
     }
     wave_affine_scan<D, T>(RA, Re, lane);
+    SvcPeek peek;  // (the service: the gate's host words, requested ahead — svc_peek)
+    if constexpr (SVC && DMT_SVC_PEEK == 2) peek = svc_peek(sv);
     T x[D];
     {
       T y[D];
@@ -3594,6 +3618,8 @@ __device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, cons
 #pragma unroll
       for (int p = 0; p < D; ++p) x[p] = v ? xn[p] : x[p];
     }
+    // (the service: the gate's host words requested now, answered while the trees finish)
+    if constexpr (SVC && DMT_SVC_PEEK == 1) peek = svc_peek(sv);
     T xe[D];
 #pragma unroll
     for (int p = 0; p < D; ++p) xe[p] = lane_value(x[p], last_lane);  // uniform: v_readlane
@@ -3619,7 +3645,7 @@ __device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, cons
         sl->row[1][w4] = valid ? (ac ? ll : lp) : 0.0;
         sl->row[2][w4] = ac ? 1.0 : 0.0;
       }
-      if (!svc_gate(sv, r0, sl)) break;
+      if (!svc_gate(sv, r0, sl, peek)) break;
       if (threadIdx.x < 64) svc_record(sv, sl, r0);  // the workgroup's fetch_ll sums → host
     }
     wave_lds_sync();
