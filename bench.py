@@ -21,6 +21,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import re
 import socket
 import subprocess
 import sys
@@ -83,6 +84,26 @@ def tree_digest():
         import provenance
         _TREE = provenance.csrc_digest(ROOT)
     return _TREE
+
+
+# the draw kernels a timed call can dispatch, as committed summaries name them (lane kernels with
+# their template bracket so that k_block< does not match k_block_pk<)
+DRAW_KERNELS = ("k_mcmc_resident_pc", "k_mcmc_resident", "k_mcmc_scan", "k_block_resident",
+                "k_block_scan", "k_block_wave", "k_block_ps_pk<", "k_block_pk<", "k_block<")
+
+
+def dispatched_kernel(recent):
+    """The family of the most recent draw kernel among libdmt's recently launched kernels
+    (demangled names, most recent first), or None."""
+    for name in recent:
+        m = re.search(r"\bdmt::(k_\w+)<", name)
+        if not m:
+            continue
+        base = m.group(1)
+        for fam in DRAW_KERNELS:
+            if fam.rstrip("<") == base:
+                return fam
+    return None
 
 
 def committed_summary(kind, config, kernel_substr):
@@ -371,6 +392,7 @@ def main(argv=None):
         res = ens.mcmc_run(lay, 0, B, args.warmup + 1, args.steps, copy=False)
     barrier()
     el = time.perf_counter() - t0
+    recent = L.recent_kernels()  # the kernels the timed call dispatched (dmt_recent_kernels)
     n_acc = float(res[:, 2].sum())  # read before any later run of this length reuses the buffer
     done = args.warmup + args.steps  # iterations run so far
     # The dominant kernel's launch duration: HIP events recorded on libdmt's stream around the
@@ -473,6 +495,9 @@ def main(argv=None):
         split = (os.environ.get("DMT_LANE_SPLIT", "-1") != "0"
                  and all(len(r) == 1 for r in w.n_points) and B // 64 < 1024)
         kname = ("k_block_ps_pk<" if pk and split else "k_block_pk<" if pk else "k_block<")
+    # the draw kernel the library actually dispatched in the timed call, when it reports one
+    # (the restatement above is the fallback for a library without dmt_recent_kernels)
+    kname = dispatched_kernel(recent) or kname
     # committed profile summaries of THIS source tree only (scripts/provenance.py)
     tr, traffic_stale = committed_summary("traffic", args.config, kname)
     traffic = tr["traffic_bytes_per_unit"] * it_per_launch if tr else None  # per launch

@@ -49,7 +49,7 @@ SYMBOLS = [
     "dmt_recompute_guiding_term", "dmt_set_proposal_law", "dmt_download_law", "dmt_swap",
     "dmt_save_ll", "dmt_set_accepted", "dmt_get_block_state", "dmt_set_block_state",
     "dmt_fetch_ll", "dmt_mcmc_step", "dmt_mcmc_run", "dmt_guiding_linear", "dmt_guiding_linear_td", "dmt_upload_aux", "dmt_comm_unique_id", "dmt_comm_init", "dmt_set_shard", "dmt_sync",
-    "dmt_set_timing", "dmt_get_timing", "dmt_memory_bytes", "dmt_debug_philox",
+    "dmt_set_timing", "dmt_get_timing", "dmt_memory_bytes", "dmt_debug_philox", "dmt_recent_kernels",
     "dmt_debug_normals", "dmt_last_error", "dmt_version", "dmt_snapshot_reserve",
     "dmt_snapshot_take", "dmt_snapshot_download", "dmt_snapshot_write", "dmt_set_ll",
     "dmt_fetch_ll_local", "dmt_comm_size", "dmt_rng_counter", "dmt_set_rng_counter",
@@ -156,6 +156,7 @@ _SIGS = {
     "dmt_set_service": [_P, _i32, C.c_double],
     "dmt_set_proposal_law_cc": [_P, _i32, _i64, _i64, _i32, _P, _P, _i32, _i32, _P, _P],
     "dmt_service_stats": [_P, C.POINTER(_u64)],
+    "dmt_recent_kernels": [C.c_char_p, _i64],
 }
 for _name, _args in _SIGS.items():
     _f = getattr(lib, _name)
@@ -179,6 +180,14 @@ _FAST = {
 fast = {}
 for _name, _args in _FAST.items():
     fast[_name] = C.CFUNCTYPE(C.c_int32, *_args)((_name, lib))
+
+
+def recent_kernels() -> list:
+    """Demangled names of the last (≤ 8) kernels this thread launched through libdmt, most
+    recent first (dmt_recent_kernels)."""
+    buf = C.create_string_buffer(8192)
+    check(lib.dmt_recent_kernels(buf, len(buf)))
+    return [n for n in buf.value.decode(errors="replace").split("\n") if n]
 
 
 def check(status: int) -> None:

@@ -109,6 +109,7 @@ struct Law {
   // σ·dW = dW, which the lane kernels take as a wave-uniform fast path
   bool unit;
   __device__ __forceinline__ void load(const double* L) {
+    static_assert(DMT_LAW_THETA + Mdl::NTH <= DMT_LAW_GSTALE, "theta would overwrite the gstale slot");
 #pragma unroll
     for (int i = 0; i < Mdl::NTH; ++i) th[i] = (T)ldc(L + DMT_LAW_THETA + i);
 #pragma unroll

@@ -191,6 +191,12 @@ struct DispatchEvents {
   hipEvent_t start = nullptr, stop = nullptr;
 };
 extern thread_local DispatchEvents g_dispatch_events;
+// the host stubs of the last kRecentKernels kernels this thread launched (dlaunch), most recent
+// at g_recent_n - 1 (mod kRecentKernels): dmt_recent_kernels names them, so a caller (bench.py)
+// can tell which kernel a call dispatched instead of restating the runtime's choice
+constexpr int kRecentKernels = 8;
+extern thread_local const void* g_recent_k[kRecentKernels];
+extern thread_local unsigned g_recent_n;
 
 // recompute_guiding_term! on the device (k_backward_filter): one thread per block.
 struct FilterArgs {

@@ -1344,6 +1344,8 @@ __global__ __launch_bounds__(128, 1) void k_block_ps_pk(const BlockArgs<T> a) {
   typedef T v16 __attribute__((ext_vector_type(VE)));
   __shared__ T s_dt[2][PK][64];
   __shared__ T s_dw[2][PK][M][64];
+  // the one-wave fallback's X°, W° staging (DMT_PK_LDS builds; one element otherwise)
+  __shared__ T stg[DMT_PK_LDS ? (Mdl::D + Mdl::M) * kPathPacket * 65 : 1];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int64_t tile = a.tile0 + blockIdx.x / a.MB;
@@ -1362,7 +1364,7 @@ __global__ __launch_bounds__(128, 1) void k_block_ps_pk(const BlockArgs<T> a) {
   const int64_t row = tq + q0;
   // both waves take the same branch (same lanes, same values)
   if (__ballot(act && ((row + 1) & (PK - 1)) != 0) != 0) {
-    if (w == 1 && act) lane_block_pk<Mdl, T, MODE_PCN, false, K, false, false, SDT>(a, tile, blk, lane, nullptr);
+    if (w == 1 && act) lane_block_pk<Mdl, T, MODE_PCN, false, K, false, false, SDT>(a, tile, blk, lane, stg);
     return;
   }
   const int nst = act ? a.seg_np[g] - 1 : 0;
@@ -2133,7 +2135,7 @@ __device__ __forceinline__ float dpp_mov(float v) {
 constexpr int kDppRowShr = 0x110;    // row_shr:n = kDppRowShr + n (within rows of 16 lanes)
 constexpr int kDppRowBcast15 = 0x142;  // lane 15 of a row → the next row
 constexpr int kDppRowBcast31 = 0x143;  // lane 31 → rows 2 and 3
-constexpr int kDppWaveShr1 = 0x138;    // lane l − 1 → lane l
+[[maybe_unused]] constexpr int kDppWaveShr1 = 0x138;    // lane l − 1 → lane l
 
 // One level of the wave's inclusive scan of affine maps: lanes with `take` compose their map
 // after the map DPP pattern CTRL brings them (An = own ∘ received, affine_compose's order).
@@ -2364,6 +2366,9 @@ __device__ __forceinline__ void scan_block(const BlockArgs<T>& a, const int64_t 
     T* const Xdb = a.X[sel.x(g) ^ a.xd_flip] + row * D;
     T* const Wdb = a.W[sel.w(g) ^ a.wd_flip] + row * M;
     const double* Zg = a.Z ? a.Z + ldc(a.st_off + g) * M : nullptr;
+    // the segment's aux-table rows (TD): one uniform base per segment, not a kernel-argument
+    // slot chosen by `kind` and re-read inside the chunk loop
+    const T* const auxb = (TD && LA.auxtd) ? a.aux[kind] + row * kAuxCols<D> : nullptr;
     if (MODE != MODE_RECOMPUTE && lane == 0) {  // W°(t0) = ρ·W(t0)
       T w0v[M];
 #pragma unroll
@@ -2536,7 +2541,7 @@ __device__ __forceinline__ void scan_block(const BlockArgs<T>& a, const int64_t 
             } else
 #endif
             {
-            aux_step<Mdl, T>(LA, a.aux[kind] + (row + i) * CA, 1, Bq, bq, dq, trq,
+            aux_step<Mdl, T>(LA, auxb + (int64_t)i * CA, 1, Bq, bq, dq, trq,
                              [](const T* p) { return *p; });
             G = g_at_aux<Mdl, T>(LA, Hi, Fi, xk[k], rr, bb, Bq, bq, dq, trq);
             }
@@ -2578,13 +2583,11 @@ __device__ __forceinline__ void scan_block(const BlockArgs<T>& a, const int64_t 
 }
 
 // The persistent kernel's time-dependent iterations call scan_block out of line (DESIGN.md §7,
-// "the round-4 k_mcmc_scan<TD> fault"): inlined into k_mcmc_scan's iteration loop, the TD body
-// (256 VGPRs + ~100 AGPRs, ~150 SGPRs spilled to VGPR lanes) gave wrong Girsanov terms from the
-// third iteration on, or an illegal address, depending on the build; out of line it is
-// bit-identical to the per-iteration kernels and the oracle.  0: inline (for that record).
-#ifndef DMT_TD_NOINLINE
-#define DMT_TD_NOINLINE 1
-#endif
+// "the round-4 k_mcmc_scan<TD> fault"): inlined into k_mcmc_scan's iteration loop, the round-4/5
+// TD body gave wrong Girsanov terms from the third iteration on, or an illegal address,
+// depending on the build; the cause was not found (its SGPR spill lanes are consistent,
+// scripts/spill_flow.py), so the inline form is no longer built and dmt_mcmc_run with an aux
+// table runs the per-iteration kernels unless DMT_MCMC_SCAN_TD=1 (dmt_runtime.hip).
 template <class Mdl, class T, int MODE, class Sel, bool TD>
 __device__ __attribute__((noinline)) void scan_block_ni(const BlockArgs<T>& a, const int64_t blk,
                                                        const uint32_t iter, const Sel& sel,
@@ -2832,12 +2835,10 @@ __device__ __forceinline__ void mcmc_scan_block(const BlockArgs<T>& a, const Acc
     const double E = exp1_draw(c.seed, (uint32_t)g0 + c.seg_base, (uint32_t)(it + c.key_delta), c.salt);
     T lp;
     bool ok;
-#if DMT_TD_NOINLINE
     if constexpr (TD)
       scan_block_ni<Mdl, T, MODE_PCN, SelMask, TD>(a, blk, (uint32_t)(it + c.key_delta), sel, L, lp, ok);
     else
-#endif
-    scan_block<Mdl, T, MODE_PCN, SelMask, TD>(a, blk, (uint32_t)(it + c.key_delta), sel, L, lp, ok);
+      scan_block<Mdl, T, MODE_PCN, SelMask, TD>(a, blk, (uint32_t)(it + c.key_delta), sel, L, lp, ok);
     llp = ok ? (double)lp : -INFINITY;
     const bool acc = E > -(llp - ll);
     if (acc) {
@@ -3261,6 +3262,12 @@ extern "C" int dmt_probe_pc_iter_stamps(uint64_t* out) {
 #ifndef DMT_PC_SETUP_OVERLAP  // set-up loads in flight while the first normals are drawn
 #define DMT_PC_SETUP_OVERLAP 1
 #endif
+#ifndef DMT_PC_NST_OPAQUE  // the consumer's valid-row tests recomputed per iteration (1) or
+#define DMT_PC_NST_OPAQUE 1  // hoisted by the compiler as lane masks (0)
+#endif
+#ifndef DMT_PC_HIST_LDS  // histories through an LDS ring stored once per 64 iterations, the success
+#define DMT_PC_HIST_LDS 1  // flag after the loop (1); lane 0's global stores every iteration (0)
+#endif
 #ifndef DMT_PC_CONS_STEPS
 #define DMT_PC_CONS_STEPS 2
 #endif
@@ -3276,6 +3283,10 @@ template <int D, int M, class T>
 struct ResPcLds {
   ResLds<D, M, T> r;  // pt: X° staging; dw: the dW° hand-off and W° staging; hf: H_i, F_i
   int acc;            // the consumer's decision of the current iteration
+  // the block's histories of up to 64 iterations (ll, ll°, accepted), stored to memory once per
+  // 64 iterations and at the loop's end (resident_pc_consumer)
+  double hll[64], hllp[64];
+  uint8_t hacc[64];
 };
 
 // ---- the resident MCMC service (SvcArgs): iterations posted by the host one at a time.
@@ -3543,11 +3554,36 @@ __device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, cons
   const int64_t nb = a.b1 - a.b0, j = blk - a.b0;
   const int last_lane = (nst - 1) / kRun;
   double Ev = 0.0;
+  // histories (accpt_history, ll_history) of up to 64 iterations held in LDS (P.hll, P.hllp,
+  // P.hacc; iteration hb0 + l in slot l) and stored by the wave's lanes once per 64 iterations
+  // and at the loop's end, instead of by lane 0 every iteration (three global stores per
+  // iteration and their pointers, which spilled to VGPR lanes; registers for them in every lane
+  // would push the consumer past its 256 VGPRs)
+  int h_n = 0;          // (uniform) iterations held
+  int64_t hb0 = iter0;  // the first of them
+  auto hist_flush = [&]() {
+    wave_lds_sync();
+    if (valid && c.hist_len > 0 && lane < h_n) {
+      const int64_t o = (hb0 + lane - 1) * c.nblocks + blk;
+      c.acc_hist[o] = P.hacc[lane];
+      c.ll_hist[o] = P.hll[lane];
+      c.llp_hist[o] = P.hllp[lane];
+    }
+  };
+  bool s_ok = true;  // the last completed draw's success flag (stored after the loop)
+  int64_t n_done = 0;
   PC_STAMP(0, 1);
   __syncthreads();  // B1 of iteration 0
   PC_STAMP(0, 3);
   for (int64_t r0 = 0; r0 < n_iter; ++r0) {
     const int64_t it = iter0 + r0;
+    // the step count, opaque per iteration: the valid-row tests below are recomputed from it
+    // (one compare each) instead of hoisted out of the loop as sixteen 64-bit lane masks, which
+    // spilled to VGPR lanes and cost two v_readlane per test per iteration
+    int nsti = nst;
+#if DMT_PC_NST_OPAQUE
+    asm volatile("" : "+s"(nsti));
+#endif
     if ((r0 & 63) == 0)
       Ev = exp1_draw(c.seed, (uint32_t)g + c.seg_base, (uint32_t)(it + c.key_delta + lane), c.salt);
     const double E = __builtin_bit_cast(
@@ -3628,7 +3664,7 @@ __device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, cons
     T seg_acc = (T)0;
 #pragma unroll
     for (int q = 0; q < 8; ++q)
-      if (64 * q < nst) seg_acc = seg_acc + (lane_value(tsum, 8 * q) + (T)0);
+      if (64 * q < nsti) seg_acc = seg_acc + (lane_value(tsum, 8 * q) + (T)0);
     // the service computes an iteration ahead of its post (registers and LDS only) and
     // publishes it — stores, flags, selectors, the decision — once the host has posted it.  The
     // block's fetch_ll leaves go to LDS before the gate, and the workgroup's records to the host
@@ -3653,7 +3689,7 @@ __device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, cons
 #pragma unroll
       for (int k = 0; k < kRun; ++k) {
         const int s = 64 * k + lane;
-        if (s < nst) {
+        if (s < nsti) {
           T xv[D];
 #pragma unroll
           for (int p = 0; p < D; ++p) xv[p] = S.pt[lds_ix(s)][p];
@@ -3666,22 +3702,41 @@ __device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, cons
 #pragma unroll
     for (int p = 0; p < D; ++p) sok = sok && isfinite(xe[p]);
     llp = sok ? (double)(llobs + seg_acc) : -INFINITY;
+#if DMT_PC_HIST_LDS
+    s_ok = sok;
+    n_done = r0 + 1;
+#else
     if (lane == 0 && valid && a.success) a.success[blk] = sok ? 1 : 0;  // last draw's flag
+#endif
     const bool acc = valid && E > -(llp - ll);
     if (acc) {
       sel.mx ^= all;
       sel.mw ^= all;
     }
     PC_ITSTAMP(0, r0, 1);
+#if DMT_PC_HIST_LDS
+    if (lane == 0) {
+      P.hacc[h_n] = acc ? 1 : 0;
+      P.hll[h_n] = ll;
+      P.hllp[h_n] = llp;
+    }
+    if (++h_n == 64) {
+      hist_flush();
+      h_n = 0;
+      hb0 = it + 1;
+    }
+#endif
     if (lane == 0) {
       P.acc = acc ? 1 : 0;
       if (valid) {
+#if !DMT_PC_HIST_LDS
         if (c.hist_len > 0) {
           const int64_t o = (it - 1) * c.nblocks + blk;
           c.acc_hist[o] = acc ? 1 : 0;
           c.ll_hist[o] = ll;
           c.llp_hist[o] = llp;
         }
+#endif
         if constexpr (!SVC && !DMT_PC_L1_LOOP) {
           part[(3 * r0 + 0) * nb + j] = acc ? llp : ll;
           part[(3 * r0 + 1) * nb + j] = acc ? ll : llp;
@@ -3745,6 +3800,10 @@ __device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, cons
     }
   }
   PC_STAMP(0, 4);
+#if DMT_PC_HIST_LDS
+  hist_flush();
+  if (valid && lane == 0 && a.success && n_done > 0) a.success[blk] = s_ok ? 1 : 0;  // last draw's flag
+#endif
   if (valid && lane == 0) {
     a.selX[g] = sel_two(sel.x(g));
     a.selW[g] = sel_two(sel.w(g));
@@ -4193,7 +4252,7 @@ __global__ __launch_bounds__(1024) void k_accept_reduce(const AcceptArgs a, doub
 // blocks and reduces them (4 wave trees + one 4-leaf tree = the aligned 256-leaf subtree of
 // the fetch_ll tree); the last workgroup to finish (device-scope counter) reduces the group
 // partials in group order with the same tree and writes the canonicalised result.
-constexpr int kAccGroup = 256;
+[[maybe_unused]] constexpr int kAccGroup = 256;
 #if DMT_TU_COMMON
 __global__ __launch_bounds__(kAccGroup) void k_accept_reduce_lb(const AcceptArgs a,
                                                                 double* __restrict__ part,
@@ -5182,13 +5241,15 @@ __global__ void k_debug_philox(uint64_t seed, const uint32_t* ctr, int64_t n, ui
 #endif  // DMT_TU_COMMON
 
 // ---------------------------------------------------------------- launchers
-static inline unsigned nblk(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
+[[maybe_unused]] static inline unsigned nblk(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
 // block counts up to which the per-block utility kernels run one workgroup per block (the
 // segments of a block in parallel) instead of one thread per block
-constexpr int64_t kFewBlocks = 2048;
+[[maybe_unused]] constexpr int64_t kFewBlocks = 2048;
 
 #if DMT_TU_COMMON
 thread_local DispatchEvents g_dispatch_events;
+thread_local const void* g_recent_k[kRecentKernels];
+thread_local unsigned g_recent_n;
 #endif
 
 // Launch; when the runtime has armed dispatch events (timed launch), they are attached to
@@ -5196,6 +5257,7 @@ thread_local DispatchEvents g_dispatch_events;
 // kernel's execution as the profiler sees it, without the stream's event-packet overheads.
 template <class... KArgs, class... Args>
 static void dlaunch(void (*k)(KArgs...), dim3 grid, dim3 block, hipStream_t s, Args... args) {
+  g_recent_k[g_recent_n++ % kRecentKernels] = reinterpret_cast<const void*>(k);
   if (g_dispatch_events.start) {
     const DispatchEvents ev = g_dispatch_events;
     g_dispatch_events = DispatchEvents{};

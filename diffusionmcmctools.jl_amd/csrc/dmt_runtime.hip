@@ -7,6 +7,8 @@
 // SamplingPair vectors (src/block.jl:66-72), so selectors live per segment.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <cxxabi.h>
+#include <dlfcn.h>
 
 #include <algorithm>
 #include <chrono>
@@ -228,6 +230,10 @@ struct dmt_ens {
   int64_t part_cap = 0;
   bool persist = true;       // dmt_mcmc_run of a linear drift in one launch (DMT_MCMC_PERSIST=0: off)
   bool resident = true;      // ... with register-resident block state when eligible (DMT_MCMC_RESIDENT=0: off)
+  // ... also with a time-dependent aux table, through k_mcmc_scan<…, TD> (DMT_MCMC_SCAN_TD=1:
+  // opt-in; off by default since the round-4/5 fault of that kernel was not root-caused,
+  // DESIGN.md §7 — the per-iteration kernels run such ensembles)
+  bool persist_td = false;
   // timing events recorded on the stream around the timed launch (default), or attached to its
   // dispatch packet (DMT_DISPATCH_EVENTS=1: hipExtLaunchKernel with events — the kernel's own
   // execution interval, but ≈ 10 µs more host time in the launch call, profiles/r02zo)
@@ -955,6 +961,7 @@ dmt_status dmt_create(dmt_ens** out, const dmt_model* model, const dmt_structure
   if (model->model == DMT_MODEL_OU) h->mapping = MAP_WAVE;
   if (const char* e = std::getenv("DMT_MCMC_PERSIST")) h->persist = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("DMT_MCMC_RESIDENT")) h->resident = std::strcmp(e, "0") != 0;
+  if (const char* e = std::getenv("DMT_MCMC_SCAN_TD")) h->persist_td = std::strcmp(e, "1") == 0;
   if (const char* e = std::getenv("DMT_MCMC_PC")) h->resident_pc = std::max(0, std::min(2, std::atoi(e)));
   if (const char* e = std::getenv("DMT_PC_BPW")) h->pc_bpw1 = std::atoi(e) == 1;
   if (const char* e = std::getenv("DMT_DISPATCH_EVENTS")) h->dispatch_events = std::strcmp(e, "0") != 0;
@@ -1697,9 +1704,6 @@ static dmt_status mcmc_run_impl(dmt_ens* h, int32_t layout, int64_t b0, int64_t 
   return mcmc_run_collect(h, n_iter, out, multi);
 }
 
-#ifndef DMT_MCMC_SCAN_TD  // 0: an ensemble with an aux table runs dmt_mcmc_run per iteration
-#define DMT_MCMC_SCAN_TD 1
-#endif
 // Queue n_iter MCMC iterations (iteration it keyed by it + key_delta, salt) on the stream; the
 // per-iteration (fetch_ll, fetch_ll°, accepted count) go to pinned h_run (one rank) or d_run
 // (multi: for the all-gather, which is queued too).  No host synchronisation.
@@ -1735,10 +1739,11 @@ static dmt_status mcmc_run_launch(dmt_ens* h, Layout* L, int64_t b0, int64_t b1,
   // kernel eligibility of the range: from the layout's flags when they decide it (no host
   // loop over the blocks per call), else block by block
   const bool lay_res = L->single_seg && L->max_steps <= kResidentMaxSteps;
-  // (an ensemble with a time-dependent auxiliary table runs k_mcmc_scan's TD instantiation;
-  // the register-resident kernels take the law's own B̃, β̃ and are not eligible)
+  // (an ensemble with a time-dependent auxiliary table runs the per-iteration kernels, or with
+  // DMT_MCMC_SCAN_TD=1 k_mcmc_scan's TD instantiation; the register-resident kernels take the
+  // law's own B̃, β̃ and are not eligible)
   bool persist = h->persist && h->key.model == DMT_MODEL_OU &&
-                 (DMT_MCMC_SCAN_TD || !has_aux_table(h));
+                 (h->persist_td || !has_aux_table(h));
   for (int64_t b = b0; b < b1 && persist && !L->single_seg; ++b)
     persist = L->glast[b] - L->gfirst[b] + 1 <= kPersistMaxSegments;
   bool resident = persist && h->key.d <= 2 && h->resident && !has_aux_table(h);
@@ -2758,6 +2763,30 @@ dmt_status dmt_get_timing(dmt_ens* h, int32_t kernel, double* ms, int64_t* count
 dmt_status dmt_memory_bytes(dmt_ens* h, int64_t* bytes) {
   if (!h || !bytes) return fail(DMT_ERR_INVALID, "null argument");
   *bytes = h->bytes;
+  return DMT_OK;
+}
+
+dmt_status dmt_recent_kernels(char* buf, int64_t n) {
+  if (!buf || n <= 0) return fail(DMT_ERR_INVALID, "null buffer");
+  std::string out;
+  const unsigned cnt = std::min<unsigned>(g_recent_n, kRecentKernels);
+  for (unsigned i = 0; i < cnt; ++i) {
+    const void* k = g_recent_k[(g_recent_n - 1 - i) % kRecentKernels];
+    Dl_info info{};
+    std::string name = "?";
+    // a kernel's host stub carries the kernel's mangled name (exported from libdmt.so)
+    if (dladdr(k, &info) && info.dli_sname) {
+      int st = 0;
+      char* dm = abi::__cxa_demangle(info.dli_sname, nullptr, nullptr, &st);
+      name = (st == 0 && dm) ? dm : info.dli_sname;
+      std::free(dm);
+    }
+    out += name;
+    out += '\n';
+  }
+  const size_t m = std::min<size_t>(out.size(), (size_t)n - 1);
+  std::memcpy(buf, out.data(), m);
+  buf[m] = '\0';
   return DMT_OK;
 }
 

@@ -31,8 +31,8 @@ import DiffusionMCMCTools
 import DiffusionMCMCTools: draw_proposal_path!, accept_reject_proposal_path!, loglikhd!,
     loglikhd°!, fetch_ll, fetch_ll°, save_ll!, set_ll!, set_accepted!, swap_paths!, swap_XX!,
     swap_WW!, swap_PP!, swap_ll!, ll_of_accepted, accpt_rate, recompute_path!, find_W_for_X!,
-    set_proposal_law!, SamplingPair, SamplingEnsemble, BiBlock, BlockCollection, BlockEnsemble,
-    ParamNamesRecording, ParamNamesAllObs
+    set_proposal_law!, SamplingUnit, SamplingPair, SamplingEnsemble, Block, BiBlock,
+    BlockCollection, BlockEnsemble, ParamNamesBlock, ParamNamesRecording, ParamNamesAllObs
 
 # device-only names (everything the reference's callers use is a method of its own functions)
 export DeviceSamplingEnsemble, DeviceSamplingPair, DeviceSamplingUnit, DeviceBlockEnsemble,
@@ -636,20 +636,37 @@ every convergent solver approaches (DESIGN.md §7), so they are accepted and hav
 """
 function _device_ensemble(aux_laws, recordings, tts; aux_laws_blocking=nothing,
                           artificial_noise=1e-11, solver_choice=nothing,
-                          solver_choice_blocking=nothing, args=nothing, kw...)
+                          solver_choice_blocking=nothing, args=nothing, pair=false, kw...)
     isempty(kw) || error("DiffusionMCMCToolsAMD: unknown keyword(s) $(collect(keys(kw)))")
     kinds = [device_model(rec.P) for rec in recordings]
     kind, _, σ = kinds[1]
     all(k -> k[1] == kind, kinds) || error("one device ensemble holds one model family")
     Ps = [rec.P for rec in recordings]
     θof = r -> kinds[r][2]
+    R = length(recordings)
     recs = [(obs = [_obs(o) for o in rec.obs], x0 = rand(rec.x0_prior)) for rec in recordings]
-    aux = aux_function(aux_laws, kind, θof, σ, Ps)
-    auxb = aux_laws_blocking === nothing ? aux : aux_function(aux_laws_blocking, kind, θof, σ, Ps)
+    # the ensemble form reads a vector aux_laws / aux_laws_blocking / artificial_noise as one
+    # entry per RECORDING (_vec_me, src/sampling_ensemble.jl:26-30, 44), each entry (and the pair
+    # form's argument, src/sampling_pair.jl:40-50) possibly a vector per segment (aux_function);
+    # the Python twin api.SamplingEnsemble._from_reference_args reads them the same way
+    per_rec(v) = pair ? fill(v, R) : _vec_me(v, R)
+    auxr = [aux_function(a, kind, θof, σ, Ps) for a in per_rec(aux_laws)]
+    length(auxr) == R || error("aux_laws: one entry per recording ($R), got $(length(auxr))")
+    aux = (r, k, o) -> auxr[r](r, k, o)
+    auxb = aux
+    if aux_laws_blocking !== nothing
+        auxbr = [aux_function(a, kind, θof, σ, Ps) for a in per_rec(aux_laws_blocking)]
+        length(auxbr) == R || error("aux_laws_blocking: one entry per recording ($R)")
+        auxb = (r, k, o) -> auxbr[r](r, k, o)
+    end
+    noise = per_rec(artificial_noise)
+    length(noise) == R && all(==(noise[1]), noise) ||
+        error("artificial_noise: one value per device ensemble (the device stores one)")
     opts = DEVICE_OPTS[]
     DeviceSamplingEnsemble(kind, θof, σ, recs, tts, aux; aux_blocking=auxb,
-                           artificial_noise=artificial_noise, device=opts.device, seed=opts.seed)
+                           artificial_noise=Float64(noise[1]), device=opts.device, seed=opts.seed)
 end
+_vec_me(val, N) = val isa AbstractArray ? val : fill(val, N)  # src/sampling_ensemble.jl:44
 
 # ============================================================ views (the reference's fields)
 """
@@ -722,8 +739,24 @@ end
 DeviceSamplingPair(aux_laws, recording, tts, args...; kw...) =
     _device_pair(aux_laws, recording, tts; (isempty(args) ? () : (args=args[1],))..., kw...)
 function _device_pair(aux_laws, recording, tts; kw...)
-    se = _device_ensemble(aux_laws, [recording], [tts]; kw...)
+    se = _device_ensemble(aux_laws, [recording], [tts]; pair=true, kw...)
     DeviceSamplingPair(se, 1)
+end
+
+# The reference's standalone `SamplingUnit(aux_laws, recording, tts, args=tuple(); kw…)`
+# (src/sampling_unit.jl:55-74): the unit `u` of a device pair built from the same arguments —
+# on the device a unit is a view of its recording's paths and laws (DeviceSamplingUnit), and
+# the pair's u° is held beside it unused.  Same arities and CPU fallback as SamplingPair.
+# (Laws given as values rather than a type: DeviceSamplingPair(aux_laws, …).u — a method of
+# DeviceSamplingUnit's own name would shadow its field constructor.)
+function SamplingUnit(aux_laws::Type, recording, tts; kw...)
+    DEVICE[] || return invoke(SamplingUnit, Tuple{Any,Any,Any}, aux_laws, recording, tts; kw...)
+    _device_pair(aux_laws, recording, tts; kw...).u
+end
+function SamplingUnit(aux_laws::Type, recording, tts, args; kw...)
+    DEVICE[] || return invoke(SamplingUnit, Tuple{Any,Any,Any,Any}, aux_laws, recording, tts,
+                              args; kw...)
+    _device_pair(aux_laws, recording, tts; args=args, kw...).u
 end
 
 function SamplingEnsemble(aux_laws::Type, recordings, tts; kw...)
@@ -877,6 +910,22 @@ function BiBlock(sp::DeviceSamplingPair, range::UnitRange{<:Integer}, ρ=0.0, la
     g0 = _seg0(sp.se, sp.r)
     DeviceBiBlock{Bool(last_block)}(sp.se, id[], 0, 1, ll_hist_len, ρ,
                                     (g0 + first(range)):(g0 + last(range)))
+end
+
+"""
+    Block(u::DeviceSamplingUnit, range, last_block=false, ll_hist_len=0)
+
+The reference's standalone `Block(u, range, last_block, ll_hist_len)` (src/block.jl:60-79): the
+window `range` (1-based segments of u's recording) of one unit.  On the device a block's state
+lives in a layout of the pair (its ll, history, and the views of u's and u°'s paths and laws),
+so this is the `b` (u) or `b°` (u°) view of a one-block device BiBlock over `range` with ρ = 0:
+`ll` starts at −Inf (src/block.jl:75), and `loglikhd!`, `recompute_path!(b, WW)`,
+`find_W_for_X!`, `set_ll!` / `save_ll!` act on that unit only.
+"""
+function Block(u::DeviceSamplingUnit, range::UnitRange{<:Integer}, last_block=false,
+               ll_hist_len=0)
+    bb = BiBlock(DeviceSamplingPair(u.se, u.r), range, 0.0, last_block, ll_hist_len)
+    DeviceBlock(bb, u.unit)
 end
 
 _n(x::DeviceBlocks) = x.b1 - x.b0
@@ -1077,6 +1126,8 @@ _pn_unit(θnames, pdep) = (var = (), var_aux = [],
     updt_aux = [], updt_obs = [])
 _pn_block(θnames, pdep) = (PP = _pn_unit(θnames, pdep), P_last = _pn_unit(θnames, pdep),
     P_excl = _pn_unit(θnames, pdep), Pb_excl = _pn_unit(θnames, pdep))
+"ParamNamesBlock(b, θnames, pdep, odeps) of a device block view (src/param_names_collections.jl:204-225)."
+ParamNamesBlock(b::DeviceBlock, θnames, pdep, odeps) = _pn_block(θnames, pdep)
 "ParamNamesRecording(bc, θnames, pdep, odeps) of a device BlockCollection (src/param_names_collections.jl:249-257)."
 ParamNamesRecording(bc::DeviceBlockCollection, θnames, pdep, odeps) =
     (blocks = [_pn_block(θnames, pdep) for _ in bc.blocks],)

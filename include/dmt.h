@@ -80,7 +80,7 @@ enum { DMT_K_DRAW = 0, DMT_K_ACCEPT = 1, DMT_K_PATHLL = 2, DMT_K_RECOMPUTE = 3,
  * Law record: one per segment per (unit, kind), DMT_LAW_STRIDE doubles.
  * It carries the target-law parameters θ and the auxiliary (linear) law used
  * by the Girsanov weight.  Offsets:
- *   [0,15)  theta  model parameters
+ *   [0,14)  theta  model parameters (at most 14: slot 14 is gstale; Law::load asserts it)
  *             OU:     Theta (d×d row-major) at 0, mu at 9
  *             FHN:    1/eps, s, gamma, beta, then the raw eps, σ at 4, 5
  *                     (σ also goes in sigma)
@@ -537,6 +537,10 @@ dmt_status dmt_debug_philox(int32_t device, uint64_t seed, const uint32_t* ctr, 
 /* Debug: device normal pairs (double) for n counters. */
 dmt_status dmt_debug_normals(int32_t device, uint64_t seed, const uint32_t* ctr, int64_t n,
                              double* out);
+/* Names (demangled) of the last kernels (up to 8) the calling thread launched through libdmt,
+ * most recent first, one per line, into buf[n] (truncated, NUL-terminated): which kernel a call
+ * dispatched (e.g. k_block_ps_pk or k_block_pk for a C5 draw), as the runtime chose it. */
+dmt_status dmt_recent_kernels(char* buf, int64_t n);
 const char* dmt_last_error(void);
 const char* dmt_version(void);
 

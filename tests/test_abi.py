@@ -54,3 +54,24 @@ def test_host_only_entry_points_work_without_gpu(dmt):
     assert H.shape == (11, 1) and np.all(np.isfinite(H)) and H[0, 0] < H[-1, 0]
     with pytest.raises(dmt.DMTError):
         dmt.guiding_linear([[-1.0]], [0.0], [1.0], np.array([0.0, 0.0]), [1.0], [1.0], 0.0)
+
+
+def test_recent_kernels_names_launches_without_gpu(dmt):
+    """dmt_recent_kernels (no device work): empty before any launch on this thread, and the
+    bench's family match reads demangled kernel names (bench.dispatched_kernel)."""
+    from diffusionmcmctools_amd import _lib
+    from conftest import gpu_available
+    if not gpu_available():
+        assert _lib.recent_kernels() == []
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    names = ["void dmt::k_accept_reduce_lb(dmt::AcceptArgs, double*, double*, unsigned int*)",
+             "void dmt::k_block_ps_pk<dmt::Lorenz<float>, float, 4, true>(dmt::BlockArgs<float>)"]
+    assert bench.dispatched_kernel(names) == "k_block_ps_pk<"
+    assert bench.dispatched_kernel(
+        ["void dmt::k_block<dmt::FHN<double>, double, 0, false, 4, false>(dmt::BlockArgs<double>)"]
+    ) == "k_block<"
+    assert bench.dispatched_kernel(["void dmt::k_mcmc_resident_pc<dmt::OU<double, 2, 2>, double, 1,"
+                                    " false, 4>(dmt::BlockArgs<double>)"]) == "k_mcmc_resident_pc"
+    assert bench.dispatched_kernel(["?"]) is None

@@ -230,7 +230,8 @@ def test_cpu_fallback_invokes_defined_reference_arities():
     aux_laws::Type (strictly more specific than the reference's, so no ambiguity)."""
     src = _strip_comments(open(JL).read())
     ref = {"SamplingPair": os.path.join(REF, "src", "sampling_pair.jl"),
-           "SamplingEnsemble": os.path.join(REF, "src", "sampling_ensemble.jl")}
+           "SamplingEnsemble": os.path.join(REF, "src", "sampling_ensemble.jl"),
+           "SamplingUnit": os.path.join(REF, "src", "sampling_unit.jl")}
     for name, path in ref.items():
         arities = (_reference_constructor_arities(path, name) if os.path.exists(path)
                    else {3, 4})  # the reference is not on the GPU box
@@ -314,10 +315,74 @@ def test_constructors_read_every_reference_keyword():
     for kw in want | {"args"}:
         assert re.search(r"\b" + kw + r"\s*=", sig), f"_device_ensemble lacks keyword {kw}"
     # the laws of both kinds come from the caller's aux_laws / aux_laws_blocking
-    assert "aux_function(aux_laws," in body and "aux_function(aux_laws_blocking," in body
-    assert "artificial_noise=artificial_noise" in body
+    assert re.search(r"aux_function\(a, kind, θof, σ, Ps\) for a in per_rec\(aux_laws\)", body)
+    assert re.search(r"aux_function\(a, kind, θof, σ, Ps\) for a in per_rec\(aux_laws_blocking\)",
+                     body)
+    assert "per_rec(artificial_noise)" in body and "artificial_noise=Float64(noise[1])" in body
     # the 4-argument constructors pass `args` on; every constructor forwards its keywords
     for name in ("SamplingPair", "SamplingEnsemble"):
         four = re.search(r"function " + name + r"\(aux_laws::Type, \w+, tts, args; kw\.\.\.\)(.*?)\nend",
                          src, re.S)
         assert four and "args=args" in four.group(1) and "kw..." in four.group(1), name
+
+
+# The reference's exported constructors (src/DiffusionMCMCTools.jl:28-60) and what serves each
+# on the device: a device method (signature regex on the shim's source) or the documented
+# reason there is none.
+EXPORTED_CONSTRUCTORS = {
+    "SamplingUnit": r"function SamplingUnit\(aux_laws::Type, recording, tts",
+    "SamplingPair": r"function SamplingPair\(aux_laws::Type, recording, tts",
+    "SamplingEnsemble": r"function SamplingEnsemble\(aux_laws::Type, recordings, tts",
+    "Block": r"function Block\(u::DeviceSamplingUnit, range::UnitRange\{<:Integer\}, last_block=false,",
+    "BiBlock": r"function BiBlock\(sp::DeviceSamplingPair, range::UnitRange\{<:Integer\}, ρ=0\.0, last_block=false,",
+    "BlockCollection": r"function BlockCollection\(sp::DeviceSamplingPair, ranges, ρρ=0\.0, ll_hist_len=0\)",
+    "BlockEnsemble": r"BlockEnsemble\(se::DeviceSamplingEnsemble, ranges, ρρ=0\.0, ll_hist_len=0\) =",
+    "ParamNamesBlock": r"ParamNamesBlock\(b::DeviceBlock, θnames, pdep, odeps\) =",
+    "ParamNamesRecording": r"ParamNamesRecording\(bc::DeviceBlockCollection, θnames, pdep, odeps\) =",
+    "ParamNamesAllObs": r"ParamNamesAllObs\(be::DeviceBlockEnsemble, θnames, all_obs\) =",
+}
+NO_DEVICE_METHOD = {
+    # src/param_names_collections.jl:56-61: its first argument is a vector of GuidedProposals
+    # GuidProp laws, which no device container holds (the device keeps law records and
+    # re-derives the auxiliary laws from θ itself); device blocks get their
+    # names from ParamNamesBlock / ParamNamesRecording / ParamNamesAllObs above
+    "ParamNamesUnit": "takes GuidProp law vectors; device names come from ParamNamesBlock",
+}
+
+
+def test_every_exported_constructor_has_a_device_method_or_a_reason():
+    """each constructor the reference exports (src/DiffusionMCMCTools.jl:28-60)
+    has a device method in the shim — the standalone SamplingUnit (src/sampling_unit.jl:55-74)
+    and Block (src/block.jl:60-79) included — or a documented reason it has none; the names are
+    imported from DiffusionMCMCTools, so the methods extend the reference's constructors."""
+    src, imported, exported = _imports_exports()
+    ctors = {n for n in REFERENCE_EXPORTS if n[0].isupper()}
+    assert ctors == set(EXPORTED_CONSTRUCTORS) | set(NO_DEVICE_METHOD)
+    for name, pat in EXPORTED_CONSTRUCTORS.items():
+        assert re.search(pat, src), f"no device method of {name}"
+        assert name in imported and name not in exported, name
+    path = os.path.join(REF, "src", "DiffusionMCMCTools.jl")
+    if os.path.exists(path):  # the reference's export list itself
+        ref_exports = set(re.findall(r"export\s+(.*)", open(path).read()))
+        names = {n.strip() for line in ref_exports for n in line.split(",")}
+        assert {n for n in names if n[:1].isupper()} == ctors
+
+
+def test_ensemble_form_expands_vector_arguments_per_recording():
+    """the ensemble form reads a vector aux_laws / aux_laws_blocking /
+    artificial_noise as one entry per recording (_vec_me, src/sampling_ensemble.jl:26-30, 44), as
+    the Python twin does (api.SamplingEnsemble._from_reference_args: per_rec); the pair form
+    keeps the per-segment reading of a vector aux_laws (aux_function)."""
+    src = _strip_comments(open(JL).read())
+    m = re.search(r"function _device_ensemble\((.*?)\)\n(.*?)\nend", src, re.S)
+    sig, body = m.group(1), m.group(2)
+    assert "pair=false" in sig
+    assert re.search(r"per_rec\(v\) = pair \? fill\(v, R\) : _vec_me\(v, R\)", body)
+    for arg in ("aux_laws", "aux_laws_blocking", "artificial_noise"):
+        assert f"per_rec({arg})" in body, arg
+    assert re.search(r"_vec_me\(val, N\) = val isa AbstractArray \? val : fill\(val, N\)", src)
+    pair = re.search(r"function _device_pair\(.*?\)\n(.*?)\nend", src, re.S).group(1)
+    assert "pair=true" in pair
+    # aux_function keeps the per-segment vector reading inside one recording's entry
+    af = re.search(r"function aux_function\(.*?\)\n(.*?)\nend", src, re.S).group(1)
+    assert "aux_laws[k]" in af

@@ -474,10 +474,10 @@ def test_ou_td_aux_blocking_loop_device_equals_oracle(prec, with_a):
 
 @pytest.mark.gpu
 def test_ou_td_aux_mcmc_run_device_equals_oracle():
-    """dmt_mcmc_run on an OU ensemble with time-dependent auxiliary laws (k_mcmc_scan's TD
-    instantiation, its scan body out of line — DESIGN.md §7, the round-4 fault; the
-    register-resident kernels are not eligible while a table is present): fetch_ll results,
-    paths, ll and histories equal the oracle's, bit for bit."""
+    """dmt_mcmc_run on an OU ensemble with time-dependent auxiliary laws (by default the
+    per-iteration scan + accept kernels — DESIGN.md §7, the round-4 fault of the persistent TD
+    kernel; the register-resident kernels are not eligible while a table is present): fetch_ll
+    results, paths, ll and histories equal the oracle's, bit for bit."""
     case, (dev, ora), ids = _td_pair(L.MAP_AUTO, L.F64, model=cs.ou_ragged_model(), hist_len=7)
     lid, nb = ids[0]
     for e in (dev, ora):
@@ -578,12 +578,12 @@ def test_reference_form_td_aux_tutorial_device_equals_oracle():
 @pytest.mark.parametrize("n_iter", [6, 25])
 def test_ou_td_aux_persistent_equals_per_iteration(n_iter):
     """The round-4 fault's shape (gpurun_out/r04g/pytest.log:31): one multi-iteration
-    dmt_mcmc_run launch of k_mcmc_scan<…, TD> against the per-iteration scan + accept kernels
-    (DMT_MCMC_PERSIST=0) on the same ensemble — every iteration's per-block ll° (the first
-    wrong one was the third, profiles/r05a) and decisions, the fetch_ll results and the paths,
-    bit for bit."""
+    dmt_mcmc_run launch of k_mcmc_scan<…, TD> (opt-in, DMT_MCMC_SCAN_TD=1) against the default
+    per-iteration scan + accept kernels on the same ensemble — every iteration's per-block ll°
+    (the first wrong one was the third, profiles/r05a) and decisions, the fetch_ll results and
+    the paths, bit for bit."""
     ens = []
-    for env in ({}, {"DMT_MCMC_PERSIST": "0"}):
+    for env in ({"DMT_MCMC_SCAN_TD": "1"}, {"DMT_MCMC_SCAN_TD": "0"}):
         saved = {k: os.environ.get(k) for k in env}
         os.environ.update(env)
         try:
