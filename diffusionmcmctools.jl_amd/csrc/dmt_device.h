@@ -35,6 +35,7 @@ template <class T, int D_, int M_>
 struct OU {
   static constexpr int D = D_, M = M_, NTH = 12;
   static constexpr bool kLinear = true;  // drift folded into the guiding coefficients
+  static constexpr bool kAffineStep = false;
   static constexpr int kNoiseCoord = -1;  // σ invertible (d = m)
   // theta: Theta (d×d row-major) at 0, mu at 9
   __device__ __forceinline__ static void drift(const T* th, const T* x, T* b) {
@@ -56,10 +57,41 @@ struct FHN {
   static constexpr int D = 2, M = 1, NTH = 4;
   static constexpr bool kLinear = false;
   static constexpr int kNoiseCoord = 1;  // hypoelliptic: the noise enters coordinate 1 only
+  // The guided Euler step as a per-step affine map plus the cubic term (round 6):
+  // the drift's linear part (ε⁻¹(y − v + s), γy − v + β) and the guiding term's u = c − Mx are
+  // folded into x' = A x + e, and only −ε⁻¹·dt·y³ depends on x non-linearly:
+  //   ed = ε⁻¹·dt;  A00 = fma(−M00, dt, 1) + ed;  A01 = fma(−M01, dt, −ed);
+  //   A10 = fma(−M10, dt, γ·dt);  A11 = fma(−M11, dt, 1 − dt);
+  //   e0 = fma(c0, dt, fma(s, ed, σdW0));  e1 = fma(c1, dt, fma(β, dt, σdW1));  r = (−ed)·(y·y)
+  //   y' = fma(r, y, fma(A00, y, fma(A01, v, e0)));   v' = fma(A10, y, fma(A11, v, e1))
+  // The map {A, e, −ed} does not depend on x (computed lane-parallel ahead of a serial
+  // recursion); the recursion's dependent chain per step is y·y → r → y' (three operations,
+  // seven fp64 instructions per step in all), against five (sixteen) for the round-5 form.
+  static constexpr bool kAffineStep = true;
+  static constexpr int NS = 7;  // step-map values: A00, A01, A10, A11, e0, e1, −ed
+  __device__ __forceinline__ static void step_map(const T* th, const T* Mg, const T* cg, T dt,
+                                                  const T* sdW, T* sm) {
+    const T ed = th[0] * dt;
+    sm[0] = dfma(-Mg[0], dt, (T)1) + ed;
+    sm[1] = dfma(-Mg[1], dt, -ed);
+    sm[2] = dfma(-Mg[2], dt, th[2] * dt);
+    sm[3] = dfma(-Mg[3], dt, (T)1 - dt);
+    sm[4] = dfma(cg[0], dt, dfma(th[1], ed, sdW[0]));
+    sm[5] = dfma(cg[1], dt, dfma(th[3], dt, sdW[1]));
+    sm[6] = -ed;
+  }
+  __device__ __forceinline__ static void step_apply(const T* sm, T* x) {
+    const T y = x[0], v = x[1];
+    const T r = sm[6] * (y * y);
+    const T y1 = dfma(r, y, dfma(sm[0], y, dfma(sm[1], v, sm[4])));
+    const T v1 = dfma(sm[2], y, dfma(sm[3], v, sm[5]));
+    x[0] = y1;
+    x[1] = v1;
+  }
   // theta: 1/eps, s, gamma, beta.  Canonical (round 5): t0 = fma(−y², y, y) +
-  // (s − v), b0 = t0·ε⁻¹ — four dependent operations from y instead of six — and the Euler step's
-  // guided drift bg0 = fma(t0, ε⁻¹, u0) (guided()), one more fused: the serial recursion's
-  // chain is y² → fma → + (s − v) → fma(t0, ε⁻¹, u0) → fma(bg0, dt, x0 + σdW0)
+  // (s − v), b0 = t0·ε⁻¹ (the drift of the Girsanov term) and the guided drift
+  // bg0 = fma(t0, ε⁻¹, u0) (guided(): find_W_for_X!'s increment); the forward Euler step is the
+  // step map above
   __device__ __forceinline__ static T t0(const T* th, const T* x) {
     const T y = x[0], v = x[1];
     return dfma(-(y * y), y, y) + (th[1] - v);
@@ -79,6 +111,7 @@ template <class T>
 struct Lorenz {
   static constexpr int D = 3, M = 3, NTH = 3;
   static constexpr bool kLinear = false;
+  static constexpr bool kAffineStep = false;
   static constexpr int kNoiseCoord = -1;
   // theta: s, r, beta
   __device__ __forceinline__ static void drift(const T* th, const T* x, T* b) {
@@ -288,6 +321,12 @@ template <class Mdl, class T>
 __device__ __forceinline__ void euler_step(const T* th, const T* Mg, const T* cg, const T* b,
                                            T dt, const T* sdW, T* x) {
   constexpr int D = Mdl::D;
+  if constexpr (Mdl::kAffineStep) {  // FHN: the step map, then the recursion's step (b unused)
+    T sm[Mdl::NS];
+    Mdl::step_map(th, Mg, cg, dt, sdW, sm);
+    Mdl::step_apply(sm, x);
+    return;
+  }
   T xn[D];
 #pragma unroll
   for (int p = 0; p < D; ++p) {

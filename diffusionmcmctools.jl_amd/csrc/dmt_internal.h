@@ -49,8 +49,18 @@ __host__ __device__ __forceinline__ int64_t plane_ix(int64_t row, int c, int C, 
   const int lg = __builtin_ctz((unsigned)pk);
   return (((row >> lg) * C + c) * tw + slot) * pk + (row & (pk - 1));
 }
-// lane-packet length of the path planes of an fp32 MAP_LANE ensemble (16 points = 64 bytes)
-constexpr int kPathPacket = 16;
+// lane-packet length of the path planes of an fp32 MAP_LANE ensemble: 32 points = 128 bytes, a
+// whole cache line per lane and component, so a lane's stores never share a line with another
+// lane's (round 6; 16 points = 64-byte pieces left every line shared by a lane pair, whose
+// per-lane buffers differ after their MH decisions: partial lines, read-modify-write FETCH)
+#ifndef DMT_PATH_PACKET
+#define DMT_PATH_PACKET 32
+#endif
+constexpr int kPathPacket = DMT_PATH_PACKET;
+// points a packet kernel stages in registers at a time (one 64-byte piece per component): the
+// processing unit of k_block_pk / k_block_ps_pk, a divisor of kPathPacket
+constexpr int kPkChunkPts = 16;
+static_assert(kPathPacket % kPkChunkPts == 0, "whole register-staged pieces per lane packet");
 
 // Thread mappings of the recursion (chosen per ensemble at dmt_create):
 //   MAP_LANE: one lane per (recording, block); tile width tw = 64 recordings

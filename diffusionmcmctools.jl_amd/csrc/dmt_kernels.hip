@@ -618,8 +618,11 @@ __device__ __forceinline__ bool run_segment_pk(const Law<Mdl, T>& L, const T* __
   const T* Hb = H_sh ? Ht + q0 * HP : Ht + row * HP * kLanes + lane;
   const int hst = H_sh ? 1 : kLanes;
   const T* Fb = Ft + row * D * kLanes + lane;
-  auto pix = [&](int64_t i, int c, int C) -> int64_t {  // point i of the segment, component c
-    return plane_ix(row + i, c, C, kLanes, lane, PK);
+  // point i of the segment, component c, in the layout's lane packets (kPathPacket points); the
+  // loop below stages PK-point pieces of them (PK divides kPathPacket)
+  static_assert(kPathPacket % PK == 0, "whole pieces per layout packet");
+  auto pix = [&](int64_t i, int c, int C) -> int64_t {
+    return plane_ix(row + i, c, C, kLanes, lane, kPathPacket);
   };
   constexpr int CA = kAuxCols<D>;
   const T* Ab = (TD && At) ? At + row * CA * kLanes + lane : nullptr;
@@ -943,7 +946,7 @@ template <class Mdl, class T, int MODE, bool PARITY, int K, bool TD, bool PAIR =
 __device__ __forceinline__ void lane_block_pk(const BlockArgs<T>& a, const int64_t tile,
                                               const int64_t blk, const int lane, T* stg,
                                               const int role = 0) {
-  constexpr int D = Mdl::D, HP = D * (D + 1) / 2, PK = kPathPacket;
+  constexpr int D = Mdl::D, HP = D * (D + 1) / 2, PK = kPkChunkPts;  // staged piece (points)
   const int64_t tq = a.tile_qoff[tile];
   auto idx = [&](int64_t q, int c, int C) -> int64_t { return ((tq + q) * C + c) * kLanes + lane; };
   const int g0 = a.gfirst[blk], g1 = a.glast[blk];
@@ -953,7 +956,7 @@ __device__ __forceinline__ void lane_block_pk(const BlockArgs<T>& a, const int64
     const T* Xs = a.X[sel_buf(a.selX[g0], a.xs_flip)];
     const int64_t q = a.seg_q[g0];
 #pragma unroll
-    for (int p = 0; p < D; ++p) x[p] = Xs[plane_ix(tq + q, p, D, kLanes, lane, PK)];
+    for (int p = 0; p < D; ++p) x[p] = Xs[plane_ix(tq + q, p, D, kLanes, lane, kPathPacket)];
   }
   T ll;
   {
@@ -1008,7 +1011,7 @@ __device__ __forceinline__ void lane_block_pk(const BlockArgs<T>& a, const int64
 
 template <class Mdl, class T, int MODE, bool PARITY, int K, bool TD = false, bool SDT = false>
 __global__ __launch_bounds__(64) void k_block_pk(const BlockArgs<T> a) {
-  __shared__ T stg[DMT_PK_LDS ? (Mdl::D + Mdl::M) * kPathPacket * 65 : 1];  // X°, W° (DMT_PK_LDS)
+  __shared__ T stg[DMT_PK_LDS ? (Mdl::D + Mdl::M) * kPkChunkPts * 65 : 1];  // X°, W° (DMT_PK_LDS)
   int64_t tile, blk;
   if (!map_block(a, tile, blk)) return;
   lane_block_pk<Mdl, T, MODE, PARITY, K, TD, false, SDT>(a, tile, blk, threadIdx.x, stg);
@@ -1018,7 +1021,7 @@ __global__ __launch_bounds__(64) void k_block_pk(const BlockArgs<T> a) {
 // index), 32 recordings each on lanes (l, l + 32) — the mapping of k_block_pair
 template <class Mdl, class T, int MODE, bool TD = false>
 __global__ __launch_bounds__(64) void k_block_pk_pair(const BlockArgs<T> a) {
-  __shared__ T stg[DMT_PK_LDS ? (Mdl::D + Mdl::M) * kPathPacket * 65 : 1];
+  __shared__ T stg[DMT_PK_LDS ? (Mdl::D + Mdl::M) * kPkChunkPts * 65 : 1];
   const int lane = threadIdx.x, role = lane >> 5;
   const int64_t wave = blockIdx.x, w2 = wave >> 1;
   const int slot = (int)(wave & 1) * 32 + (lane & 31);
@@ -1337,7 +1340,7 @@ __global__ __launch_bounds__(128, DMT_PS_MINW) void k_block_ps(const BlockArgs<T
 #endif
 template <class Mdl, class T, int K, bool SDT>
 __global__ __launch_bounds__(128, 1) void k_block_ps_pk(const BlockArgs<T> a) {
-  constexpr int D = Mdl::D, M = Mdl::M, HP = D * (D + 1) / 2, PK = kPathPacket;
+  constexpr int D = Mdl::D, M = Mdl::M, HP = D * (D + 1) / 2, PK = kPkChunkPts;  // staged piece
   constexpr int VE = 16 / (int)sizeof(T), NV = PK / VE;
   constexpr int NPB = NormPerBlock<T>::v;
   static_assert(PK % K == 0 && (PK * M) % NPB == 0 && (K * M) % 2 == 0, "whole chunks, blocks");
@@ -1345,7 +1348,7 @@ __global__ __launch_bounds__(128, 1) void k_block_ps_pk(const BlockArgs<T> a) {
   __shared__ T s_dt[2][PK][64];
   __shared__ T s_dw[2][PK][M][64];
   // the one-wave fallback's X°, W° staging (DMT_PK_LDS builds; one element otherwise)
-  __shared__ T stg[DMT_PK_LDS ? (Mdl::D + Mdl::M) * kPathPacket * 65 : 1];
+  __shared__ T stg[DMT_PK_LDS ? (Mdl::D + Mdl::M) * kPkChunkPts * 65 : 1];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int64_t tile = a.tile0 + blockIdx.x / a.MB;
@@ -1373,7 +1376,9 @@ __global__ __launch_bounds__(128, 1) void k_block_ps_pk(const BlockArgs<T> a) {
   for (int o = 1; o < 64; o <<= 1) nmax = max(nmax, __shfl_xor(nmax, o, 64));
   const int nch = (__builtin_amdgcn_readfirstlane(nmax) + PK - 1) / PK;  // packets
   const int sx = act ? a.selX[g] : kSelInit, sw = act ? a.selW[g] : kSelInit;
-  auto pix = [&](int64_t i, int c, int C) -> int64_t { return plane_ix(row + i, c, C, kLanes, lane, PK); };
+  auto pix = [&](int64_t i, int c, int C) -> int64_t {  // the layout's lane packets
+    return plane_ix(row + i, c, C, kLanes, lane, kPathPacket);
+  };
 
   if (w == 0) {
     // ================= producer =================
@@ -1775,13 +1780,20 @@ __device__ __forceinline__ T wave_tree_sum(T v) {
 // the chunk, the per-segment success test) and then prepares chunk k+1 (loads, Philox /
 // Box–Muller normals, the increment-form pCN dW° = fma(ρ, dW, √(1-ρ²)·√dt·Z), σ·dW°) — all
 // lane-parallel.  One __syncthreads per period.  Canonical arithmetic.
-template <class T, int D, int M, int HP>
+// wave S's row per step: {dt, σdW[D], M[D·D], c[D]}, or a model's step map (FHN: {A, e, −ε⁻¹dt},
+// Mdl::step_map), padded to an even count
+template <class Mdl>
+constexpr int wave_row_len() {
+  if constexpr (Mdl::kAffineStep) return (Mdl::NS + 1) & ~1;
+  else return ((1 + Mdl::D + Mdl::D * Mdl::D + Mdl::D) + 1) & ~1;
+}
+template <class T, int D, int M, int HP, int NRR>
 struct WaveLds {
-  static constexpr int NR = ((1 + D + D * D + D) + 1) & ~1;  // dt, sdW[D], M[D*D], c[D]
+  static constexpr int NR = NRR;
   static constexpr int NB = 1 + HP + D;                      // dt, H[HP], F[D] (phase B)
   T rows[2][64][NR];
   T rowsB[2][64][NB];
-  T xcap[2][64][D];
+  alignas(16) T xcap[2][64][D];
   T wcap[2][64][M];  // dW° of each step (stored to W° by phase B)
   T xend[2][D];
   T w0[2][M];
@@ -1795,12 +1807,24 @@ struct ChunkIt {  // (segment, first step) iterator over a block's chunks of 64 
   }
 };
 
+#ifndef DMT_S_UNROLL
+#define DMT_S_UNROLL 4
+#endif
+#ifndef DMT_S_LDS_CAPTURE  // wave S captures x_s through an LDS store of lane 0 (1) or a
+#define DMT_S_LDS_CAPTURE 1  // register select in lane s (0)
+#endif
+#ifndef DMT_S_FULL_UNROLL  // whole 64-step chunks straight-line (1) or the DMT_S_UNROLL loop (0)
+#define DMT_S_FULL_UNROLL 1
+#endif
+#ifndef DMT_S_AHEAD  // rows read this many steps ahead in the straight-line chunk
+#define DMT_S_AHEAD 2
+#endif
 // DIAG (timing diagnostics only, never selected in production): bit 0 = S skips its
 // recursion, bit 1 = P skips phase A, bit 2 = P skips phase B.
 template <class Mdl, class T, int MODE, int DIAG = 0>
 __global__ __launch_bounds__(128) void k_block_wave(const BlockArgs<T> a) {
   constexpr int D = Mdl::D, M = Mdl::M, HP = D * (D + 1) / 2;
-  using Lds = WaveLds<T, D, M, HP>;
+  using Lds = WaveLds<T, D, M, HP, wave_row_len<Mdl>()>;
   constexpr int NR = Lds::NR;
   __shared__ Lds sh;
   const int lane = threadIdx.x & 63;
@@ -1842,34 +1866,90 @@ __global__ __launch_bounds__(128) void k_block_wave(const BlockArgs<T> a) {
       }
       const int cnt = (DIAG & 1) ? 0 : min(64, it.nst - it.c0);
       const T(*rw)[NR] = sh.rows[k & 1];
+      T(*const xw)[D] = sh.xcap[k & 1];
+#if DMT_S_LDS_CAPTURE
+      // lanes past the chunk's last step keep the chunk's start point (as the register capture)
+      if (lane >= cnt) {
+#pragma unroll
+        for (int p = 0; p < D; ++p) xw[lane][p] = x[p];
+      }
+#else
       T xc[D];
 #pragma unroll
       for (int p = 0; p < D; ++p) xc[p] = x[p];
+#endif
       // the next step's row is read into registers one step ahead, so the LDS latency overlaps
       // the current step's dependent chain instead of preceding it
       T nx[NR];
 #pragma unroll
       for (int i = 0; i < NR; ++i) nx[i] = rw[0][i];
-#ifndef DMT_S_UNROLL
-#define DMT_S_UNROLL 4
-#endif
-#pragma unroll DMT_S_UNROLL
-      for (int s = 0; s < cnt; ++s) {
-        T q[NR];
+      // step s of the chunk from its row q.  x_s is captured for phase B: lane 0 writes it to
+      // the LDS row s (DMT_S_LDS_CAPTURE; an exec-masked store, no VALU), or lane s keeps it in
+      // a register (four v_cndmask and a compare per step, on the serial chain's wave)
+      auto body = [&](const int s, const T* q) {
+#if DMT_S_LDS_CAPTURE
+        if (lane == 0) {
+          if constexpr (D == 2) {  // one 16/8-byte store at an immediate offset
+            typedef T t2 __attribute__((ext_vector_type(2)));
+            *reinterpret_cast<t2*>(&xw[s][0]) = t2{x[0], x[1]};
+          } else {
 #pragma unroll
-        for (int i = 0; i < NR; ++i) q[i] = nx[i];
-        const int sn = s + 1 < cnt ? s + 1 : s;
-#pragma unroll
-        for (int i = 0; i < NR; ++i) nx[i] = rw[sn][i];
-        T b_[D];
-        if (!Mdl::kLinear) Mdl::drift(L.th, x, b_);
+            for (int p = 0; p < D; ++p) xw[s][p] = x[p];
+          }
+        }
+#else
         const bool mine = lane == s;
 #pragma unroll
         for (int p = 0; p < D; ++p) xc[p] = mine ? x[p] : xc[p];
-        euler_step<Mdl, T>(L.th, q + 1 + D, q + 1 + D + D * D, b_, q[0], q + 1, x);
-      }
+#endif
+        if constexpr (Mdl::kAffineStep) {
+          Mdl::step_apply(q, x);  // the row is the step's map (Mdl::step_map, phase A)
+        } else {
+          T b_[D];
+          if (!Mdl::kLinear) Mdl::drift(L.th, x, b_);
+          euler_step<Mdl, T>(L.th, q + 1 + D, q + 1 + D + D * D, b_, q[0], q + 1, x);
+        }
+      };
+#if DMT_S_FULL_UNROLL
+      if (cnt == 64) {
+        // a whole chunk (all but a segment's last): straight-line, no loop control, the rows
+        // read DMT_S_AHEAD steps ahead into a register ring indexed by constants
+        constexpr int AH = DMT_S_AHEAD;
+        T rb[AH][NR];
 #pragma unroll
-      for (int p = 0; p < D; ++p) sh.xcap[k & 1][lane][p] = xc[p];
+        for (int i = 0; i < NR; ++i) rb[0][i] = nx[i];
+#pragma unroll
+        for (int a = 1; a < AH; ++a)
+#pragma unroll
+          for (int i = 0; i < NR; ++i) rb[a][i] = rw[a][i];
+#pragma unroll
+        for (int s = 0; s < 64; ++s) {
+          T q[NR];
+#pragma unroll
+          for (int i = 0; i < NR; ++i) q[i] = rb[s % AH][i];
+          const int sn = s + AH < 64 ? s + AH : 63;
+#pragma unroll
+          for (int i = 0; i < NR; ++i) rb[s % AH][i] = rw[sn][i];
+          body(s, q);
+        }
+      } else
+#endif
+      {
+#pragma unroll DMT_S_UNROLL
+        for (int s = 0; s < cnt; ++s) {  // the row read one step ahead
+          T q[NR];
+#pragma unroll
+          for (int i = 0; i < NR; ++i) q[i] = nx[i];
+          const int sn = s + 1 < cnt ? s + 1 : s;
+#pragma unroll
+          for (int i = 0; i < NR; ++i) nx[i] = rw[sn][i];
+          body(s, q);
+        }
+      }
+#if !DMT_S_LDS_CAPTURE
+#pragma unroll
+      for (int p = 0; p < D; ++p) xw[lane][p] = xc[p];
+#endif
       const bool seg_end = it.c0 + 64 >= it.nst;
       if (seg_end && lane == 0) {
 #pragma unroll
@@ -1962,13 +2042,20 @@ __global__ __launch_bounds__(128) void k_block_wave(const BlockArgs<T> a) {
     sigma_dw<Mdl, T>(LA, dW, sdW);
     guide_coeffs<Mdl, T>(LA, Hi, Fi, Mg, cg);
     T* rw = sh.rows[k & 1][lane];
-    rw[0] = dt;
+    if constexpr (Mdl::kAffineStep) {  // the step's map, as euler_step forms it
+      T sm[Mdl::NS];
+      Mdl::step_map(LA.th, Mg, cg, dt, sdW, sm);
 #pragma unroll
-    for (int p = 0; p < D; ++p) rw[1 + p] = sdW[p];
+      for (int e = 0; e < Mdl::NS; ++e) rw[e] = sm[e];
+    } else {
+      rw[0] = dt;
 #pragma unroll
-    for (int e = 0; e < D * D; ++e) rw[1 + D + e] = Mg[e];
+      for (int p = 0; p < D; ++p) rw[1 + p] = sdW[p];
 #pragma unroll
-    for (int p = 0; p < D; ++p) rw[1 + D + D * D + p] = cg[p];
+      for (int e = 0; e < D * D; ++e) rw[1 + D + e] = Mg[e];
+#pragma unroll
+      for (int p = 0; p < D; ++p) rw[1 + D + D * D + p] = cg[p];
+    }
     T* rb = sh.rowsB[k & 1][lane];
     rb[0] = dt;
 #pragma unroll
@@ -3262,12 +3349,6 @@ extern "C" int dmt_probe_pc_iter_stamps(uint64_t* out) {
 #ifndef DMT_PC_SETUP_OVERLAP  // set-up loads in flight while the first normals are drawn
 #define DMT_PC_SETUP_OVERLAP 1
 #endif
-#ifndef DMT_PC_NST_OPAQUE  // the consumer's valid-row tests recomputed per iteration (1) or
-#define DMT_PC_NST_OPAQUE 1  // hoisted by the compiler as lane masks (0)
-#endif
-#ifndef DMT_PC_HIST_LDS  // histories through an LDS ring stored once per 64 iterations, the success
-#define DMT_PC_HIST_LDS 1  // flag after the loop (1); lane 0's global stores every iteration (0)
-#endif
 #ifndef DMT_PC_CONS_STEPS
 #define DMT_PC_CONS_STEPS 2
 #endif
@@ -3283,10 +3364,6 @@ template <int D, int M, class T>
 struct ResPcLds {
   ResLds<D, M, T> r;  // pt: X° staging; dw: the dW° hand-off and W° staging; hf: H_i, F_i
   int acc;            // the consumer's decision of the current iteration
-  // the block's histories of up to 64 iterations (ll, ll°, accepted), stored to memory once per
-  // 64 iterations and at the loop's end (resident_pc_consumer)
-  double hll[64], hllp[64];
-  uint8_t hacc[64];
 };
 
 // ---- the resident MCMC service (SvcArgs): iterations posted by the host one at a time.
@@ -3554,36 +3631,11 @@ __device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, cons
   const int64_t nb = a.b1 - a.b0, j = blk - a.b0;
   const int last_lane = (nst - 1) / kRun;
   double Ev = 0.0;
-  // histories (accpt_history, ll_history) of up to 64 iterations held in LDS (P.hll, P.hllp,
-  // P.hacc; iteration hb0 + l in slot l) and stored by the wave's lanes once per 64 iterations
-  // and at the loop's end, instead of by lane 0 every iteration (three global stores per
-  // iteration and their pointers, which spilled to VGPR lanes; registers for them in every lane
-  // would push the consumer past its 256 VGPRs)
-  int h_n = 0;          // (uniform) iterations held
-  int64_t hb0 = iter0;  // the first of them
-  auto hist_flush = [&]() {
-    wave_lds_sync();
-    if (valid && c.hist_len > 0 && lane < h_n) {
-      const int64_t o = (hb0 + lane - 1) * c.nblocks + blk;
-      c.acc_hist[o] = P.hacc[lane];
-      c.ll_hist[o] = P.hll[lane];
-      c.llp_hist[o] = P.hllp[lane];
-    }
-  };
-  bool s_ok = true;  // the last completed draw's success flag (stored after the loop)
-  int64_t n_done = 0;
   PC_STAMP(0, 1);
   __syncthreads();  // B1 of iteration 0
   PC_STAMP(0, 3);
   for (int64_t r0 = 0; r0 < n_iter; ++r0) {
     const int64_t it = iter0 + r0;
-    // the step count, opaque per iteration: the valid-row tests below are recomputed from it
-    // (one compare each) instead of hoisted out of the loop as sixteen 64-bit lane masks, which
-    // spilled to VGPR lanes and cost two v_readlane per test per iteration
-    int nsti = nst;
-#if DMT_PC_NST_OPAQUE
-    asm volatile("" : "+s"(nsti));
-#endif
     if ((r0 & 63) == 0)
       Ev = exp1_draw(c.seed, (uint32_t)g + c.seg_base, (uint32_t)(it + c.key_delta + lane), c.salt);
     const double E = __builtin_bit_cast(
@@ -3664,7 +3716,7 @@ __device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, cons
     T seg_acc = (T)0;
 #pragma unroll
     for (int q = 0; q < 8; ++q)
-      if (64 * q < nsti) seg_acc = seg_acc + (lane_value(tsum, 8 * q) + (T)0);
+      if (64 * q < nst) seg_acc = seg_acc + (lane_value(tsum, 8 * q) + (T)0);
     // the service computes an iteration ahead of its post (registers and LDS only) and
     // publishes it — stores, flags, selectors, the decision — once the host has posted it.  The
     // block's fetch_ll leaves go to LDS before the gate, and the workgroup's records to the host
@@ -3689,7 +3741,7 @@ __device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, cons
 #pragma unroll
       for (int k = 0; k < kRun; ++k) {
         const int s = 64 * k + lane;
-        if (s < nsti) {
+        if (s < nst) {
           T xv[D];
 #pragma unroll
           for (int p = 0; p < D; ++p) xv[p] = S.pt[lds_ix(s)][p];
@@ -3702,41 +3754,22 @@ __device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, cons
 #pragma unroll
     for (int p = 0; p < D; ++p) sok = sok && isfinite(xe[p]);
     llp = sok ? (double)(llobs + seg_acc) : -INFINITY;
-#if DMT_PC_HIST_LDS
-    s_ok = sok;
-    n_done = r0 + 1;
-#else
     if (lane == 0 && valid && a.success) a.success[blk] = sok ? 1 : 0;  // last draw's flag
-#endif
     const bool acc = valid && E > -(llp - ll);
     if (acc) {
       sel.mx ^= all;
       sel.mw ^= all;
     }
     PC_ITSTAMP(0, r0, 1);
-#if DMT_PC_HIST_LDS
-    if (lane == 0) {
-      P.hacc[h_n] = acc ? 1 : 0;
-      P.hll[h_n] = ll;
-      P.hllp[h_n] = llp;
-    }
-    if (++h_n == 64) {
-      hist_flush();
-      h_n = 0;
-      hb0 = it + 1;
-    }
-#endif
     if (lane == 0) {
       P.acc = acc ? 1 : 0;
       if (valid) {
-#if !DMT_PC_HIST_LDS
         if (c.hist_len > 0) {
           const int64_t o = (it - 1) * c.nblocks + blk;
           c.acc_hist[o] = acc ? 1 : 0;
           c.ll_hist[o] = ll;
           c.llp_hist[o] = llp;
         }
-#endif
         if constexpr (!SVC && !DMT_PC_L1_LOOP) {
           part[(3 * r0 + 0) * nb + j] = acc ? llp : ll;
           part[(3 * r0 + 1) * nb + j] = acc ? ll : llp;
@@ -3800,10 +3833,6 @@ __device__ __forceinline__ void resident_pc_consumer(const BlockArgs<T>& a, cons
     }
   }
   PC_STAMP(0, 4);
-#if DMT_PC_HIST_LDS
-  hist_flush();
-  if (valid && lane == 0 && a.success && n_done > 0) a.success[blk] = s_ok ? 1 : 0;  // last draw's flag
-#endif
   if (valid && lane == 0) {
     a.selX[g] = sel_two(sel.x(g));
     a.selW[g] = sel_two(sel.w(g));

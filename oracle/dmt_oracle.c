@@ -56,7 +56,10 @@
  *   LINEAR DRIFT (OU): the step is affine, x' = A x + e with A_ab = fma(-M_ab, dt, δ_ab),
  *   e_a = fma(c_a, dt, sdW_a), and the segment is evaluated as chunked Kogge–Stone prefix
  *   scans of these maps (solve_segment_scan below) — this REPLACES the last line above
- *   for OU models.  FHN / Lorenz use the step-by-step form.
+ *   for OU models.  Lorenz uses the step-by-step form.
+ *   FHN (round 6): the step is the affine map of the drift's linear part and u plus the cubic
+ *   term (fhn_step) — this REPLACES the bg/x' lines above for FHN's forward step; bg_0 (with
+ *   the fused scaling) remains the find_W_for_X! increment's (orc_invsolve_segment).
  *
  *   Log-weight summation: within a segment the g's are summed in chunks of 64
  *   consecutive steps by the adjacent-pair binary tree ((g0+g1)+(g2+g3))+…
@@ -106,6 +109,27 @@ static inline int pidx(int d, int a, int b) {
 static inline REAL fhn_t0(const REAL* th, const REAL* x) {
     const REAL y = x[0], v = x[1];
     return FMA(-(y * y), y, y) + (th[1] - v);
+}
+/* FHN's guided Euler step as a per-step affine map plus the cubic term (round 6; libdmt
+ * dmt_device.h FHN::step_map / step_apply):
+ *   ed = (1/eps)·dt; A00 = fma(-M00, dt, 1) + ed; A01 = fma(-M01, dt, -ed);
+ *   A10 = fma(-M10, dt, gamma·dt); A11 = fma(-M11, dt, 1 - dt);
+ *   e0 = fma(c0, dt, fma(s, ed, sdW0)); e1 = fma(c1, dt, fma(beta, dt, sdW1)); r = (-ed)·(y·y)
+ *   y' = fma(r, y, fma(A00, y, fma(A01, v, e0)));  v' = fma(A10, y, fma(A11, v, e1)) */
+static inline void fhn_step(const REAL* th, const REAL* Mg, const REAL* cg, REAL dt,
+                            const REAL* sdw, REAL* x) {
+    const REAL ed = th[0] * dt;
+    const REAL A00 = FMA(-Mg[0], dt, (REAL)1) + ed;
+    const REAL A01 = FMA(-Mg[1], dt, -ed);
+    const REAL A10 = FMA(-Mg[2], dt, th[2] * dt);
+    const REAL A11 = FMA(-Mg[3], dt, (REAL)1 - dt);
+    const REAL e0 = FMA(cg[0], dt, FMA(th[1], ed, sdw[0]));
+    const REAL e1 = FMA(cg[1], dt, FMA(th[3], dt, sdw[1]));
+    const REAL ned = -ed;
+    const REAL y = x[0], v = x[1];
+    const REAL r = ned * (y * y);
+    x[0] = FMA(r, y, FMA(A00, y, FMA(A01, v, e0)));
+    x[1] = FMA(A10, y, FMA(A11, v, e1));
 }
 /* b_p + u_p of the Euler step (libdmt FHN/Lorenz::guided): FHN's first coordinate fuses its
  * 1/eps scaling, bg0 = fma(t0, 1/eps, u0); every other coordinate b_p + u_p; OU: u_p. */
@@ -498,7 +522,12 @@ int SFX(orc_solve_segment)(int model, int d, int m, const double* law, int npts,
         REAL Mg[9], cg[3];
         guide_coeffs(model, d, th, a, Hi, Fi, Mg, cg, unit);
         REAL xn[3];
-        for (int p = 0; p < d; ++p) {
+        if (model == ORC_FHN) {  /* the step map (fhn_step) */
+            REAL sdw[2];
+            for (int p = 0; p < 2; ++p) sdw[p] = sg[p * m + 0] * dW[0];
+            xn[0] = x[0]; xn[1] = x[1];
+            fhn_step(th, Mg, cg, dt, sdw, xn);
+        } else for (int p = 0; p < d; ++p) {
             REAL u = cg[p];
             for (int q = 0; q < d; ++q) u = FMA(-Mg[p * d + q], x[q], u);
             REAL bg = orc_guided(model, th, x, b, u, p);

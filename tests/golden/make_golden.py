@@ -14,7 +14,7 @@ fixtures pin instead:
                        final paths).
 The last two freeze the canonical arithmetic: any later change to the kernels or
 the oracle that alters a bit shows up against them.  Inputs are stored in full, so tests never
-regenerate them.  Round 5 changed the FHN drift's canonical order: the ragged
+regenerate them.  Rounds 5 and 6 changed FHN's canonical order: the ragged
 trace's outputs were refreshed from its stored inputs (``--refresh-ragged-outputs``)."""
 from __future__ import annotations
 
@@ -142,7 +142,7 @@ def ragged_trace():
 
 
 def refresh_ragged_outputs():
-    """Round 5 (FHN drift reassociated): keep ragged_trace.npz's stored INPUTS and
+    """Rounds 5 and 6 (FHN drift reassociated; the FHN step map): keep ragged_trace.npz's stored INPUTS and
     recompute its outputs (decisions, ll, ll°, fetch_ll, final paths) with the current oracle —
     the replay of test_golden.replay_ragged, recording instead of asserting."""
     import oracle as orc
