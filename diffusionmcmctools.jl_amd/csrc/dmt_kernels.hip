@@ -1335,6 +1335,25 @@ __global__ __launch_bounds__(128, DMT_PS_MINW) void k_block_ps(const BlockArgs<T
 #ifndef DMT_PSPK_STUB
 #define DMT_PSPK_STUB 0
 #endif
+#ifndef DMT_PSPK_GLDS  // the consumer's H, F chunks by LDS-DMA (global_load_lds_dwordx4), ring of
+#define DMT_PSPK_GLDS 0   // DMT_PSPK_GLDS_SLOTS slots, one fewer chunks in flight (0: register ring)
+#endif
+#ifndef DMT_PSPK_GLDS_SLOTS
+#define DMT_PSPK_GLDS_SLOTS 4
+#endif
+// One LDS-DMA wave-instruction: each lane's 16 bytes at gsrc land at the wave-uniform LDS byte
+// address lds_dst + 16·lane (M0 holds the base; saved and restored in the same statement, the
+// recipe of cdna_hip_programming.md §5.7).  hipcc does not count it: the caller waits with its
+// own s_waitcnt vmcnt before reading the bytes.
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
+}
+#ifndef DMT_PSPK_PAIR  // whole 128-byte lines per lane: a packet's first piece waits in LDS
+#define DMT_PSPK_PAIR 0
+#endif
 #ifndef DMT_PSPK_RING  // the consumer's H, F register ring (chunks of K steps; 2 = one ahead;
 #define DMT_PSPK_RING 2   // 4, three ahead, measured the same: 1 350 vs 1 341-1 343 µs, r05l)
 #endif
@@ -1349,6 +1368,18 @@ __global__ __launch_bounds__(128, 1) void k_block_ps_pk(const BlockArgs<T> a) {
   __shared__ T s_dw[2][PK][M][64];
   // the one-wave fallback's X°, W° staging (DMT_PK_LDS builds; one element otherwise)
   __shared__ T stg[DMT_PK_LDS ? (Mdl::D + Mdl::M) * kPkChunkPts * 65 : 1];
+  // whole-line stores (DMT_PSPK_PAIR): a layout packet is kPathPacket / PK pieces; the first
+  // piece of each waits in LDS (each lane its own slots) until the second completes the lane's
+  // 128-byte line, which then leaves in one run of stores — a half line written ≈ 16 steps
+  // before its other half was often evicted in between: a partial write, read back (FETCH)
+  constexpr bool PAIRW = DMT_PSPK_PAIR && kPathPacket == 2 * PK;
+  __shared__ v16 stW[PAIRW ? M : 1][PAIRW ? NV : 1][64];  // producer: W° first halves
+  __shared__ v16 stX[PAIRW ? D : 1][PAIRW ? NV : 1][64];  // consumer: X° first halves
+  // the consumer's H, F chunks of K steps by LDS-DMA (DMT_PSPK_GLDS): slot image = the tile's
+  // rows as they lie in memory, H [K][HP][64] then F [K][D][64]
+  constexpr int GCH = K * HP * 64, GCF = K * D * 64;  // elements per chunk
+  constexpr int NGS = DMT_PSPK_GLDS ? DMT_PSPK_GLDS_SLOTS : 1;
+  __shared__ T hfr[NGS][DMT_PSPK_GLDS ? GCH + GCF : 1];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int64_t tile = a.tile0 + blockIdx.x / a.MB;
@@ -1365,8 +1396,15 @@ __global__ __launch_bounds__(128, 1) void k_block_ps_pk(const BlockArgs<T> a) {
   const int g = act ? a.gfirst[blk] : 0;  // the block's only segment (host-checked)
   const int64_t q0 = act ? a.seg_q[g] : 0;
   const int64_t row = tq + q0;
-  // both waves take the same branch (same lanes, same values)
-  if (__ballot(act && ((row + 1) & (PK - 1)) != 0) != 0) {
+  // both waves take the same branch (same lanes, same values).  The LDS-DMA consumer
+  // (DMT_PSPK_GLDS) also needs every lane's segment at the tile's first row and per-point H
+  bool glds_off = false;
+  if constexpr (DMT_PSPK_GLDS) {
+    const int lsu = act ? ((a.term[blk] != 0 ? a.selPP[g] : a.selPPB[g]) ^ a.law_flip) : 0;
+    const int kdu = act && a.term[blk] == 0 ? 1 : 0;
+    glds_off = __ballot(act && (q0 != 0 || a.H_shared[lsu][kdu] != 0)) != 0;
+  }
+  if (glds_off || __ballot(act && ((row + 1) & (PK - 1)) != 0) != 0) {
     if (w == 1 && act) lane_block_pk<Mdl, T, MODE_PCN, false, K, false, false, SDT>(a, tile, blk, lane, stg);
     return;
   }
@@ -1376,6 +1414,9 @@ __global__ __launch_bounds__(128, 1) void k_block_ps_pk(const BlockArgs<T> a) {
   for (int o = 1; o < 64; o <<= 1) nmax = max(nmax, __shfl_xor(nmax, o, 64));
   const int nch = (__builtin_amdgcn_readfirstlane(nmax) + PK - 1) / PK;  // packets
   const int sx = act ? a.selX[g] : kSelInit, sw = act ? a.selW[g] : kSelInit;
+  // every lane's segment starts a layout packet: piece p is the first half of its packet for
+  // even p (uniform; the first segment of every recording, dmt_create's tile alignment)
+  const bool pair = PAIRW && __ballot(act && ((row + 1) & (kPathPacket - 1)) != 0) == 0;
   auto pix = [&](int64_t i, int c, int C) -> int64_t {  // the layout's lane packets
     return plane_ix(row + i, c, C, kLanes, lane, kPathPacket);
   };
@@ -1457,12 +1498,28 @@ __global__ __launch_bounds__(128, 1) void k_block_ps_pk(const BlockArgs<T> a) {
           tcur = v ? tc[e] : tcur;
         }
         if (act) {
-          if ((p + 1) * PK <= nst) {  // a whole packet: its pieces
+          if ((p + 1) * PK <= nst) {  // a whole piece
+            if (pair && (p & 1) == 0 && (p + 2) * PK <= nst) {  // first half: wait in LDS
 #pragma unroll
-            for (int k = 0; k < M; ++k) {
-              v16* dst = (v16*)&Wd[pix((int64_t)p * PK + 1, k, M)];
+              for (int k = 0; k < M; ++k)
 #pragma unroll
-              for (int v = 0; v < NV; ++v) dst[v] = ob[k][v];
+                for (int v = 0; v < NV; ++v) stW[k][v][lane] = ob[k][v];
+            } else if (pair && (p & 1) == 1) {  // second half: the lane's whole line
+#pragma unroll
+              for (int k = 0; k < M; ++k) {
+                v16* dst = (v16*)&Wd[pix((int64_t)(p - 1) * PK + 1, k, M)];
+#pragma unroll
+                for (int v = 0; v < NV; ++v) dst[v] = stW[k][v][lane];
+#pragma unroll
+                for (int v = 0; v < NV; ++v) dst[NV + v] = ob[k][v];
+              }
+            } else {
+#pragma unroll
+              for (int k = 0; k < M; ++k) {
+                v16* dst = (v16*)&Wd[pix((int64_t)p * PK + 1, k, M)];
+#pragma unroll
+                for (int v = 0; v < NV; ++v) dst[v] = ob[k][v];
+              }
             }
           } else {
 #pragma unroll
@@ -1532,14 +1589,53 @@ __global__ __launch_bounds__(128, 1) void k_block_ps_pk(const BlockArgs<T> a) {
 #endif
       }
     };
+#if DMT_PSPK_GLDS
+    // LDS-DMA ring (every lane's segment at the tile's first row — the first segment of every
+    // recording, C5 — and per-point tables: a chunk of the tile's H, F rows is then one
+    // contiguous block, copied by 1 KB wave-instructions without registers, the loads of
+    // NGS - 1 chunks in flight).  The chunk's rows are read unclamped: a lane past its own
+    // segment end only evaluates steps it never adds or applies (the tile's spare rows keep
+    // every read inside the tile)
+    constexpr int NIH = GCH * (int)sizeof(T) / 1024, NIF = GCF * (int)sizeof(T) / 1024;
+    static_assert(GCH * sizeof(T) % 1024 == 0 && GCF * sizeof(T) % 1024 == 0, "whole 1 KB copies");
+    static_assert((NGS - 1) * K + K <= kPadPoints && (NGS - 1) * (NIH + NIF) <= 63, "ring depth");
+    const T* Ft = a.F[ls][kind];
+    auto gissue = [&](int64_t i0, int slot) {  // chunk of steps [i0, i0 + K) → slot
+      const T* hs = Ht + (tq + i0) * HP * kLanes + lane * (16 / (int)sizeof(T));
+      const T* fs = Ft + (tq + i0) * D * kLanes + lane * (16 / (int)sizeof(T));
+      const uint32_t l0 = (uint32_t)(uintptr_t)&hfr[slot][0];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot's last reads retired (WAR)
+#pragma unroll
+      for (int j = 0; j < NIH; ++j)
+        glds16(hs + j * (1024 / (int)sizeof(T)), __builtin_amdgcn_readfirstlane(l0 + 1024u * j));
+#pragma unroll
+      for (int j = 0; j < NIF; ++j)
+        glds16(fs + j * (1024 / (int)sizeof(T)),
+               __builtin_amdgcn_readfirstlane(l0 + (uint32_t)(GCH * sizeof(T)) + 1024u * j));
+    };
+    auto gread = [&](int slot, Sub& s) {
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+#pragma unroll
+        for (int e = 0; e < HP; ++e) s.H[j][e] = hfr[slot][(j * HP + e) * 64 + lane];
+#pragma unroll
+        for (int e = 0; e < D; ++e) s.F[j][e] = hfr[slot][GCH + (j * D + e) * 64 + lane];
+      }
+    };
+#endif
     // H, F chunks in flight: a ring of NR register sets, NR - 1 chunks ahead; NR divides the
     // packet's chunks, so the unrolled packet loop indexes the ring with constants (the consumer
     // has little arithmetic per step to cover the loads' latency with)
     constexpr int NR = DMT_PSPK_RING;
     static_assert((PK / K) % NR == 0 && (NR - 1) * K <= kPadPoints, "ring of whole packets");
+#if DMT_PSPK_GLDS
+#pragma unroll
+    for (int u = 0; u < NGS - 1; ++u) gissue((int64_t)u * K, u);
+#else
     Sub sb[NR];
 #pragma unroll
     for (int u = 0; u < NR - 1; ++u) load((int64_t)u * K, sb[u]);
+#endif
     for (int c = -1; c < nch; ++c) {
       if (c >= 0) {
         const int buf = c & 1;
@@ -1547,8 +1643,18 @@ __global__ __launch_bounds__(128, 1) void k_block_ps_pk(const BlockArgs<T> a) {
 #pragma unroll
         for (int q = 0; q < PK / K; ++q) {
           const int64_t i0 = (int64_t)c * PK + q * K;
+#if DMT_PSPK_GLDS
+          // chunk jj + NGS - 1 into the slot chunk jj - 1 was read from; chunk jj's copies are
+          // the oldest loads outstanding but the (NGS - 1)(NIH + NIF) issued after them
+          const int jj = c * (PK / K) + q;
+          gissue(i0 + (NGS - 1) * K, (jj + NGS - 1) % NGS);
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NGS - 1) * (NIH + NIF)) : "memory");
+          Sub cur;
+          gread(jj % NGS, cur);
+#else
           load(i0 + (NR - 1) * K, sb[(q + NR - 1) % NR]);  // prefetch NR - 1 chunks ahead
           Sub& cur = sb[q % NR];
+#endif
           T gv[K];
 #pragma unroll
           for (int j = 0; j < K; ++j) {
@@ -1599,12 +1705,28 @@ __global__ __launch_bounds__(128, 1) void k_block_ps_pk(const BlockArgs<T> a) {
           }
         }
         if (act && !(DMT_PSPK_STUB & 4)) {  // (timing stub 4: no X° stores)
-          if ((int64_t)(c + 1) * PK <= nst) {  // a whole packet: its pieces
+          if ((int64_t)(c + 1) * PK <= nst) {  // a whole piece
+            if (pair && (c & 1) == 0 && (int64_t)(c + 2) * PK <= nst) {  // first half: LDS
 #pragma unroll
-            for (int p = 0; p < D; ++p) {
-              v16* dst = (v16*)&Xd[pix((int64_t)c * PK + 1, p, D)];
+              for (int p = 0; p < D; ++p)
 #pragma unroll
-              for (int v = 0; v < NV; ++v) dst[v] = ob[p][v];
+                for (int v = 0; v < NV; ++v) stX[p][v][lane] = ob[p][v];
+            } else if (pair && (c & 1) == 1) {  // second half: the lane's whole line
+#pragma unroll
+              for (int p = 0; p < D; ++p) {
+                v16* dst = (v16*)&Xd[pix((int64_t)(c - 1) * PK + 1, p, D)];
+#pragma unroll
+                for (int v = 0; v < NV; ++v) dst[v] = stX[p][v][lane];
+#pragma unroll
+                for (int v = 0; v < NV; ++v) dst[NV + v] = ob[p][v];
+              }
+            } else {
+#pragma unroll
+              for (int p = 0; p < D; ++p) {
+                v16* dst = (v16*)&Xd[pix((int64_t)c * PK + 1, p, D)];
+#pragma unroll
+                for (int v = 0; v < NV; ++v) dst[v] = ob[p][v];
+              }
             }
           } else {
 #pragma unroll
