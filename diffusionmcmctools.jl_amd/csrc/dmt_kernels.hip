@@ -1336,8 +1336,8 @@ __global__ __launch_bounds__(128, DMT_PS_MINW) void k_block_ps(const BlockArgs<T
 #define DMT_PSPK_STUB 0
 #endif
 #ifndef DMT_PSPK_GLDS  // the consumer's H, F chunks by LDS-DMA (global_load_lds_dwordx4), ring of
-#define DMT_PSPK_GLDS 0   // DMT_PSPK_GLDS_SLOTS slots, one fewer chunks in flight (0: register ring)
-#endif
+#define DMT_PSPK_GLDS 0   // DMT_PSPK_GLDS_SLOTS slots, one fewer chunks in flight (0: register ring);
+#endif                    // C5 1 282 (4 slots), 1 293 (5) vs 1 278 µs per draw (profiles/r06e)
 #ifndef DMT_PSPK_GLDS_SLOTS
 #define DMT_PSPK_GLDS_SLOTS 4
 #endif
@@ -1351,8 +1351,8 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
                "s_mov_b32 m0, %0"
                : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
 }
-#ifndef DMT_PSPK_PAIR  // whole 128-byte lines per lane: a packet's first piece waits in LDS
-#define DMT_PSPK_PAIR 0
+#ifndef DMT_PSPK_PAIR  // whole 128-byte lines per lane: a packet's first piece waits in LDS;
+#define DMT_PSPK_PAIR 1   // C5 1 152 vs 1 278 µs per draw without (profiles/r06e)
 #endif
 #ifndef DMT_PSPK_RING  // the consumer's H, F register ring (chunks of K steps; 2 = one ahead;
 #define DMT_PSPK_RING 2   // 4, three ahead, measured the same: 1 350 vs 1 341-1 343 µs, r05l)
