@@ -1354,11 +1354,14 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
 #ifndef DMT_PSPK_PAIR  // whole 128-byte lines per lane: a packet's first piece waits in LDS;
 #define DMT_PSPK_PAIR 1   // C5 1 152 vs 1 278 µs per draw without (profiles/r06e)
 #endif
+#ifndef DMT_PSPK_HELPER  // a third wave per tile draws half of the producer's normals
+#define DMT_PSPK_HELPER 0
+#endif
 #ifndef DMT_PSPK_RING  // the consumer's H, F register ring (chunks of K steps; 2 = one ahead;
 #define DMT_PSPK_RING 2   // 4, three ahead, measured the same: 1 350 vs 1 341-1 343 µs, r05l)
 #endif
 template <class Mdl, class T, int K, bool SDT>
-__global__ __launch_bounds__(128, 1) void k_block_ps_pk(const BlockArgs<T> a) {
+__global__ __launch_bounds__(DMT_PSPK_HELPER ? 192 : 128, 1) void k_block_ps_pk(const BlockArgs<T> a) {
   constexpr int D = Mdl::D, M = Mdl::M, HP = D * (D + 1) / 2, PK = kPkChunkPts;  // staged piece
   constexpr int VE = 16 / (int)sizeof(T), NV = PK / VE;
   constexpr int NPB = NormPerBlock<T>::v;
@@ -1366,6 +1369,11 @@ __global__ __launch_bounds__(128, 1) void k_block_ps_pk(const BlockArgs<T> a) {
   typedef T v16 __attribute__((ext_vector_type(VE)));
   __shared__ T s_dt[2][PK][64];
   __shared__ T s_dw[2][PK][M][64];
+  // DMT_PSPK_HELPER: a third wave draws the odd Philox blocks of every packet one packet ahead
+  // of the producer, which draws the even ones and reads the odd ones' normals from here
+  constexpr int NBQ = PK * M / NPB, HELP = DMT_PSPK_HELPER;
+  static_assert(!HELP || NBQ % 2 == 0, "the helper draws half of a packet's normal blocks");
+  __shared__ T s_zh[HELP ? 2 : 1][HELP ? NBQ / 2 : 1][NPB][64];
   // the one-wave fallback's X°, W° staging (DMT_PK_LDS builds; one element otherwise)
   __shared__ T stg[DMT_PK_LDS ? (Mdl::D + Mdl::M) * kPkChunkPts * 65 : 1];
   // whole-line stores (DMT_PSPK_PAIR): a layout packet is kPathPacket / PK pieces; the first
@@ -1420,6 +1428,31 @@ __global__ __launch_bounds__(128, 1) void k_block_ps_pk(const BlockArgs<T> a) {
   auto pix = [&](int64_t i, int c, int C) -> int64_t {  // the layout's lane packets
     return plane_ix(row + i, c, C, kLanes, lane, kPathPacket);
   };
+  // the helper's draw for packet p (its odd blocks) into slot p & 1
+  auto help_draw = [&](NormalStream<T>& ns, int p) {
+#pragma unroll
+    for (int h = 0; h < NBQ / 2; ++h) {
+      const uint32_t bc = (uint32_t)((p * PK * M) / NPB + 2 * h + 1);
+      T zb[NPB];
+      normal_block(philox4x32_10(U4{bc, ns.seg, ns.iter, ns.c3}, ns.k0, ns.k1), zb);
+#pragma unroll
+      for (int e = 0; e < NPB; ++e) s_zh[p & 1][h][e][lane] = zb[e];
+    }
+  };
+  if constexpr (HELP) {
+    if (w == 2) {  // ================= helper =================
+      NormalStream<T> ns;
+      ns.init(a.seed, (uint32_t)g + a.seg_base, a.iter, a.salt);
+      help_draw(ns, 0);
+      __syncthreads();
+      for (int c = -1; c < nch; ++c) {
+        if (c + 2 < nch) help_draw(ns, c + 2);
+        __syncthreads();
+      }
+      return;
+    }
+    __syncthreads();  // packet 0's odd blocks
+  }
 
   if (w == 0) {
     // ================= producer =================
@@ -1477,7 +1510,22 @@ __global__ __launch_bounds__(128, 1) void k_block_ps_pk(const BlockArgs<T> a) {
 #pragma unroll
           for (int e = 0; e < NPB; ++e) zb[e] = (T)(bc & 7) * (T)0.125;
 #else
-          normal_block(philox4x32_10(U4{bc, ns.seg, ns.iter, ns.c3}, ns.k0, ns.k1), zb);
+          if (HELP && (bq & 1)) {  // the helper's block
+#pragma unroll
+            for (int e = 0; e < NPB; ++e) zb[e] = s_zh[p & 1][bq >> 1][e][lane];
+          } else {
+            normal_block(philox4x32_10(U4{bc, ns.seg, ns.iter, ns.c3}, ns.k0, ns.k1), zb);
+          }
+#endif
+#if DMT_PSPK_STUB & 16  // timing probe (results unchanged): every normal block drawn twice
+          {
+            uint32_t bc2 = bc;
+            asm volatile("" : "+v"(bc2));
+            T zb2[NPB];
+            normal_block(philox4x32_10(U4{bc2, ns.seg, ns.iter, ns.c3}, ns.k0, ns.k1), zb2);
+#pragma unroll
+            for (int e = 0; e < NPB; ++e) asm volatile("" ::"v"(zb2[e]));
+          }
 #endif
 #pragma unroll
           for (int e = 0; e < NPB; ++e) z[(NPB * bq + e) / M][(NPB * bq + e) % M] = zb[e];
@@ -1688,6 +1736,23 @@ __global__ __launch_bounds__(128, 1) void k_block_ps_pk(const BlockArgs<T> a) {
 #pragma unroll
             for (int p = 0; p < D; ++p) xn[p] = x[p];
             euler_step<Mdl, T>(LA.th, Mg, cg, b, dt, sdW, xn);
+#if DMT_PSPK_STUB & 32  // timing probe (results unchanged): every step's arithmetic twice
+            {
+              T x2[D], r2[D], b2[D], M2[D * D], c2[D], H2[HP], F2[D];
+#pragma unroll
+              for (int p = 0; p < D; ++p) { x2[p] = x[p]; asm volatile("" : "+v"(x2[p])); }
+#pragma unroll
+              for (int e2 = 0; e2 < HP; ++e2) { H2[e2] = cur.H[j][e2]; asm volatile("" : "+v"(H2[e2])); }
+#pragma unroll
+              for (int e2 = 0; e2 < D; ++e2) { F2[e2] = cur.F[j][e2]; asm volatile("" : "+v"(F2[e2])); }
+              const T G2 = g_at<Mdl, T>(LA, H2, F2, x2, r2, b2);
+              guide_coeffs<Mdl, T>(LA, H2, F2, M2, c2);
+              euler_step<Mdl, T>(LA.th, M2, c2, b2, dt, sdW, x2);
+              asm volatile("" ::"v"(G2));
+#pragma unroll
+              for (int p = 0; p < D; ++p) asm volatile("" ::"v"(x2[p]));
+            }
+#endif
 #endif
 #pragma unroll
             for (int p = 0; p < D; ++p) {
@@ -5490,9 +5555,9 @@ static hipError_t launch_block_t(int mapping, int mode, const void* args, int64_
         }
         if (mode == MODE_PCN && !par && !td && a.lane_split) {  // producer/consumer waves
           if (DMT_PK_SDT_TABLE && a.t_shared && a.sdt)
-            dlaunch(k_block_ps_pk<Mdl, T, kPkChunk, true>, grid, dim3(128), s, a);
+            dlaunch(k_block_ps_pk<Mdl, T, kPkChunk, true>, grid, dim3(DMT_PSPK_HELPER ? 192 : 128), s, a);
           else
-            dlaunch(k_block_ps_pk<Mdl, T, kPkChunk, false>, grid, dim3(128), s, a);
+            dlaunch(k_block_ps_pk<Mdl, T, kPkChunk, false>, grid, dim3(DMT_PSPK_HELPER ? 192 : 128), s, a);
           return hipGetLastError();
         }
         switch (mode) {
