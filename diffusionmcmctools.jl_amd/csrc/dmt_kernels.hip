@@ -1354,14 +1354,11 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
 #ifndef DMT_PSPK_PAIR  // whole 128-byte lines per lane: a packet's first piece waits in LDS;
 #define DMT_PSPK_PAIR 1   // C5 1 152 vs 1 278 µs per draw without (profiles/r06e)
 #endif
-#ifndef DMT_PSPK_HELPER  // a third wave per tile draws half of the producer's normals
-#define DMT_PSPK_HELPER 0
-#endif
 #ifndef DMT_PSPK_RING  // the consumer's H, F register ring (chunks of K steps; 2 = one ahead;
 #define DMT_PSPK_RING 2   // 4, three ahead, measured the same: 1 350 vs 1 341-1 343 µs, r05l)
 #endif
 template <class Mdl, class T, int K, bool SDT>
-__global__ __launch_bounds__(DMT_PSPK_HELPER ? 192 : 128, 1) void k_block_ps_pk(const BlockArgs<T> a) {
+__global__ __launch_bounds__(128, 1) void k_block_ps_pk(const BlockArgs<T> a) {
   constexpr int D = Mdl::D, M = Mdl::M, HP = D * (D + 1) / 2, PK = kPkChunkPts;  // staged piece
   constexpr int VE = 16 / (int)sizeof(T), NV = PK / VE;
   constexpr int NPB = NormPerBlock<T>::v;
@@ -1369,11 +1366,6 @@ __global__ __launch_bounds__(DMT_PSPK_HELPER ? 192 : 128, 1) void k_block_ps_pk(
   typedef T v16 __attribute__((ext_vector_type(VE)));
   __shared__ T s_dt[2][PK][64];
   __shared__ T s_dw[2][PK][M][64];
-  // DMT_PSPK_HELPER: a third wave draws the odd Philox blocks of every packet one packet ahead
-  // of the producer, which draws the even ones and reads the odd ones' normals from here
-  constexpr int NBQ = PK * M / NPB, HELP = DMT_PSPK_HELPER;
-  static_assert(!HELP || NBQ % 2 == 0, "the helper draws half of a packet's normal blocks");
-  __shared__ T s_zh[HELP ? 2 : 1][HELP ? NBQ / 2 : 1][NPB][64];
   // the one-wave fallback's X°, W° staging (DMT_PK_LDS builds; one element otherwise)
   __shared__ T stg[DMT_PK_LDS ? (Mdl::D + Mdl::M) * kPkChunkPts * 65 : 1];
   // whole-line stores (DMT_PSPK_PAIR): a layout packet is kPathPacket / PK pieces; the first
@@ -1387,7 +1379,7 @@ __global__ __launch_bounds__(DMT_PSPK_HELPER ? 192 : 128, 1) void k_block_ps_pk(
   // rows as they lie in memory, H [K][HP][64] then F [K][D][64]
   constexpr int GCH = K * HP * 64, GCF = K * D * 64;  // elements per chunk
   constexpr int NGS = DMT_PSPK_GLDS ? DMT_PSPK_GLDS_SLOTS : 1;
-  __shared__ T hfr[NGS][DMT_PSPK_GLDS ? GCH + GCF : 1];
+  [[maybe_unused]] __shared__ T hfr[NGS][DMT_PSPK_GLDS ? GCH + GCF : 1];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int64_t tile = a.tile0 + blockIdx.x / a.MB;
@@ -1428,32 +1420,6 @@ __global__ __launch_bounds__(DMT_PSPK_HELPER ? 192 : 128, 1) void k_block_ps_pk(
   auto pix = [&](int64_t i, int c, int C) -> int64_t {  // the layout's lane packets
     return plane_ix(row + i, c, C, kLanes, lane, kPathPacket);
   };
-  // the helper's draw for packet p (its odd blocks) into slot p & 1
-  auto help_draw = [&](NormalStream<T>& ns, int p) {
-#pragma unroll
-    for (int h = 0; h < NBQ / 2; ++h) {
-      const uint32_t bc = (uint32_t)((p * PK * M) / NPB + 2 * h + 1);
-      T zb[NPB];
-      normal_block(philox4x32_10(U4{bc, ns.seg, ns.iter, ns.c3}, ns.k0, ns.k1), zb);
-#pragma unroll
-      for (int e = 0; e < NPB; ++e) s_zh[p & 1][h][e][lane] = zb[e];
-    }
-  };
-  if constexpr (HELP) {
-    if (w == 2) {  // ================= helper =================
-      NormalStream<T> ns;
-      ns.init(a.seed, (uint32_t)g + a.seg_base, a.iter, a.salt);
-      help_draw(ns, 0);
-      __syncthreads();
-      for (int c = -1; c < nch; ++c) {
-        if (c + 2 < nch) help_draw(ns, c + 2);
-        __syncthreads();
-      }
-      return;
-    }
-    __syncthreads();  // packet 0's odd blocks
-  }
-
   if (w == 0) {
     // ================= producer =================
     const T rho = act ? (T)a.rho[blk] : (T)0;
@@ -1510,12 +1476,7 @@ __global__ __launch_bounds__(DMT_PSPK_HELPER ? 192 : 128, 1) void k_block_ps_pk(
 #pragma unroll
           for (int e = 0; e < NPB; ++e) zb[e] = (T)(bc & 7) * (T)0.125;
 #else
-          if (HELP && (bq & 1)) {  // the helper's block
-#pragma unroll
-            for (int e = 0; e < NPB; ++e) zb[e] = s_zh[p & 1][bq >> 1][e][lane];
-          } else {
-            normal_block(philox4x32_10(U4{bc, ns.seg, ns.iter, ns.c3}, ns.k0, ns.k1), zb);
-          }
+          normal_block(philox4x32_10(U4{bc, ns.seg, ns.iter, ns.c3}, ns.k0, ns.k1), zb);
 #endif
 #if DMT_PSPK_STUB & 16  // timing probe (results unchanged): every normal block drawn twice
           {
@@ -5555,9 +5516,9 @@ static hipError_t launch_block_t(int mapping, int mode, const void* args, int64_
         }
         if (mode == MODE_PCN && !par && !td && a.lane_split) {  // producer/consumer waves
           if (DMT_PK_SDT_TABLE && a.t_shared && a.sdt)
-            dlaunch(k_block_ps_pk<Mdl, T, kPkChunk, true>, grid, dim3(DMT_PSPK_HELPER ? 192 : 128), s, a);
+            dlaunch(k_block_ps_pk<Mdl, T, kPkChunk, true>, grid, dim3(128), s, a);
           else
-            dlaunch(k_block_ps_pk<Mdl, T, kPkChunk, false>, grid, dim3(DMT_PSPK_HELPER ? 192 : 128), s, a);
+            dlaunch(k_block_ps_pk<Mdl, T, kPkChunk, false>, grid, dim3(128), s, a);
           return hipGetLastError();
         }
         switch (mode) {
