@@ -1,6 +1,6 @@
 #!/bin/bash
 # Copy a final session pair's evidence (gpurun_out/<A>, gpurun_out/<B>: scripts/sessions/
-# r05_finalA.sh, r05_finalC.sh) into profiles/<A>, profiles/<B> and write the kstats, traffic and
+# r05_finalA.sh, r05_finalC.sh with TAG=<A>, TAG=<B>) into profiles/<A>, profiles/<B> and write the kstats, traffic and
 # issue summaries bench.py quotes (each stamped with the digest the session recorded).
 # usage: scripts/final_summaries.sh r05ia r05ib
 set -e
@@ -25,8 +25,8 @@ for c in c5 c3; do
 done
 cp $H/prof_tut/tut_kernel_stats.csv $Q/
 L2="VALU issue and dependency latency: the consumer's chain per iteration (scan, points, Girsanov trees, decision) and its wait for the producer's decision-dependent proposal; two waves per SIMD; W, F, H stay in registers/LDS across iterations (HBM traffic = the X/W proposal stores)"
-L5="the load/store path: producer (normals, u.W packets, W° packets) and consumer (H, F rows, recursion, X° packets) waves on every SIMD (1 024 waves); timing stubs: 505 µs with neither H, F loads nor X° stores, 730 with the stores, 988 with the loads (profiles/r05m)"
-L3="HBM load latency with one wave per SIMD (1 024 waves): two chunks of K = 4 steps of register prefetch in flight"
+L5="two balanced latency-bound waves per tile, one per SIMD (1 024 waves): producer (normals, u.W packets, W° whole lines) and consumer (H, F rows, recursion, X° whole lines); drawing every normal twice adds 560 µs per draw, the consumer's arithmetic twice 215 µs (profiles/r06h); loads, stores and hand-off alone 865 µs (r06g)"
+L3="HBM throughput for its 6:3 read/write fp64 row mix with one wave per SIMD: a memory-only kernel of the same pattern runs 769-898 µs whatever the prefetch depth (profiles/r06f, scripts/c3_mem_probe.hip)"
 K5='k_block_ps_pk<dmt::Lorenz<float>, float, 4'; K3='k_block<dmt::FHN<double>, double, 0'
 python scripts/kstats_summary.py --trace $P/c2_kernel_trace.csv --kernel k_mcmc_resident_pc --config c2 --skip 5 --units-per-launch 20 --tree $P/tree.txt --command "rocprofv3 --kernel-trace --stats -- python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --repeats 0 --calls-iters 0 (dispatches: 5 one-iteration warm-up calls skipped; the timed call and the two event re-runs)" --out profiles/${A}_kstats_c2.json > /dev/null
 python scripts/pmc_traffic.py --fetch $P/pmc_c2_fetch.csv --write $P/pmc_c2_write.csv --kernel k_mcmc_resident_pc --calib-fetch $P/pmc_calib_fetch.csv --calib-write $P/pmc_calib_write.csv --config c2 --units-per-launch 20 --skip 20 --tree $P/tree.txt --out profiles/${A}_traffic_c2.json > /dev/null
